@@ -1,0 +1,179 @@
+/*
+ * mx_kernels.h -- C-ABI boundary of the MI355X-native collective-reduction
+ * hot path (libmx_kernels.so, built by hipcc for gfx950).
+ *
+ * Everything here is plain C: pointers, sizes, ints.  No HIP, torch or MPI
+ * types cross this boundary (streams are passed as `void *` = hipStream_t).
+ * All entry points return MX_SUCCESS (0) or a negative MX_ERR_* code.
+ *
+ * Which reference interface each group replaces (paths relative to the
+ * reference checkout, HewlettPackard/zhpe-ompi = Open MPI 5.0.0a1):
+ *
+ *   mx_reduce2  <- ompi_op_base_handler_fn_t slots
+ *                  ompi/mca/op/op.h:258-262, instantiated by the OP_FUNC /
+ *                  FUNC_FUNC / LOC_FUNC macros of
+ *                  ompi/mca/op/base/op_base_functions.c:40-104 and tabled at
+ *                  :1485-1569 (ompi_op_base_functions[op][type]).
+ *                  Semantics: inout[i] = inout[i] OP in[i].
+ *   mx_reduce3  <- ompi_op_base_3buff_handler_fn_t slots
+ *                  ompi/mca/op/op.h:267-273; op_base_functions.c:654-775,
+ *                  table :1572-1655.  Semantics: out[i] = in1[i] OP in2[i].
+ *   mx_op_supported <- the NULL / non-NULL pattern of those tables, which
+ *                  ompi_op_base_op_select() checks
+ *                  (ompi/mca/op/base/op_base_op_select.c:185-201).
+ *   mx_is_device_ptr <- the per-call buffer probe of the accelerator
+ *                  pattern (opal/datatype/opal_datatype_cuda.c:70-90,
+ *                  opal/mca/common/cuda/common_cuda.c:1736-1857).
+ *   mx_copy     <- opal_datatype_copy_content_same_ddt for contiguous
+ *                  types (opal/datatype/opal_datatype_copy.c:99-141).
+ *   mx_ddt_* / mx_pack / mx_unpack <- the convertor pack/unpack loops
+ *                  opal_generic_simple_pack_function
+ *                  (opal/datatype/opal_datatype_pack.c:235-370) and
+ *                  opal_generic_simple_unpack_function
+ *                  (opal/datatype/opal_datatype_unpack.c:245-427), see
+ *                  mx_convertor.h.
+ *   mx_comm_* / mx_allreduce / ... <- the coll module slots
+ *                  ompi/mca/coll/coll.h:200-244 as implemented by
+ *                  ompi/mca/coll/base/coll_base_allreduce.c et al., see
+ *                  mx_coll.h.
+ *
+ * The op and type numbering is IDENTICAL to the reference's
+ * OMPI_OP_BASE_FORTRAN_* (ompi/mca/op/op.h:206-240) and
+ * OMPI_OP_BASE_TYPE_* (ompi/mca/op/op.h:104-199) enums, so an op component
+ * passes op->o_f_to_c_index and ompi_op_ddt_map[dtype->id] straight through.
+ */
+#ifndef MX_KERNELS_H
+#define MX_KERNELS_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define MX_ABI_VERSION 1
+
+/* ---- return codes ---------------------------------------------------- */
+#define MX_SUCCESS          0
+#define MX_ERR_ARG         -1  /* bad argument (NULL, misaligned, size)     */
+#define MX_ERR_UNSUPPORTED -2  /* (op,type) has no kernel: NULL table slot  */
+#define MX_ERR_HIP         -3  /* HIP runtime error                          */
+#define MX_ERR_NOMEM       -4  /* allocation failure                         */
+#define MX_ERR_TIMEOUT     -5  /* a peer never arrived (bounded spin)        */
+#define MX_ERR_RCCL        -6  /* RCCL error                                 */
+#define MX_ERR_NOT_INIT    -7  /* mx_init not called / no device             */
+#define MX_ERR_STATE       -8  /* object in the wrong state                  */
+
+/* ---- predefined reduction ops (== OMPI_OP_BASE_FORTRAN_*) ------------ */
+enum {
+    MX_OP_NULL = 0,
+    MX_OP_MAX,
+    MX_OP_MIN,
+    MX_OP_SUM,
+    MX_OP_PROD,
+    MX_OP_LAND,
+    MX_OP_BAND,
+    MX_OP_LOR,
+    MX_OP_BOR,
+    MX_OP_LXOR,
+    MX_OP_BXOR,
+    MX_OP_MAXLOC,
+    MX_OP_MINLOC,
+    MX_OP_REPLACE,
+    MX_OP_NO_OP,
+    MX_OP_COUNT
+};
+
+/* ---- reducible type slots (== OMPI_OP_BASE_TYPE_*) ------------------- */
+enum {
+    MX_TYPE_INT8_T = 0,
+    MX_TYPE_UINT8_T,
+    MX_TYPE_INT16_T,
+    MX_TYPE_UINT16_T,
+    MX_TYPE_INT32_T,
+    MX_TYPE_UINT32_T,
+    MX_TYPE_INT64_T,
+    MX_TYPE_UINT64_T,
+    MX_TYPE_INTEGER,          /* Fortran INTEGER   (4 B)                  */
+    MX_TYPE_INTEGER1,
+    MX_TYPE_INTEGER2,
+    MX_TYPE_INTEGER4,
+    MX_TYPE_INTEGER8,
+    MX_TYPE_INTEGER16,        /* never built by the reference (no kernel) */
+    MX_TYPE_SHORT_FLOAT,      /* never built by the reference (no kernel) */
+    MX_TYPE_FLOAT,
+    MX_TYPE_DOUBLE,
+    MX_TYPE_REAL,             /* Fortran REAL      (4 B)                  */
+    MX_TYPE_REAL2,            /* never built                              */
+    MX_TYPE_REAL4,
+    MX_TYPE_REAL8,
+    MX_TYPE_REAL16,           /* never built                              */
+    MX_TYPE_DOUBLE_PRECISION,
+    MX_TYPE_LONG_DOUBLE,      /* x87 80-bit in 16 B                       */
+    MX_TYPE_LOGICAL,          /* Fortran LOGICAL   (4 B)                  */
+    MX_TYPE_BOOL,
+    MX_TYPE_C_SHORT_FLOAT_COMPLEX, /* never built                         */
+    MX_TYPE_C_FLOAT_COMPLEX,
+    MX_TYPE_C_DOUBLE_COMPLEX,
+    MX_TYPE_C_LONG_DOUBLE_COMPLEX,
+    MX_TYPE_BYTE,
+    MX_TYPE_2REAL,
+    MX_TYPE_2DOUBLE_PRECISION,
+    MX_TYPE_2INTEGER,
+    MX_TYPE_FLOAT_INT,
+    MX_TYPE_DOUBLE_INT,
+    MX_TYPE_LONG_INT,
+    MX_TYPE_2INT,
+    MX_TYPE_SHORT_INT,
+    MX_TYPE_LONG_DOUBLE_INT,
+    MX_TYPE_WCHAR,            /* mapped by ompi_op_ddt_map, every kernel NULL */
+    MX_TYPE_COUNT
+};
+
+/* Table-shape variants: the reference builds its kernel tables either with
+ * or without the Fortran types (OMPI_HAVE_FORTRAN_*).  C-only = 116 pairs,
+ * with Fortran = 176 pairs. */
+#define MX_TABLE_C_ONLY      0
+#define MX_TABLE_WITH_FORTRAN 1
+
+/* ---- runtime --------------------------------------------------------- */
+
+/* Select the HIP device and allocate per-process state.  Idempotent. */
+int mx_init(int device);
+int mx_finalize(void);
+/* 1 = device (or device-mapped) memory, 0 = host memory, <0 = error. */
+int mx_is_device_ptr(const void *p);
+/* Block until all work queued on `stream` (NULL = default) completed. */
+int mx_stream_sync(void *stream);
+const char *mx_strerror(int rc);
+/* Library identification, e.g. "mx_kernels gfx950 abi 1". */
+const char *mx_version(void);
+
+/* ---- reduction kernels (K1-K4) --------------------------------------- */
+
+/* Element size in bytes of a type slot (pair types include padding:
+ * short_int 8, double_int 16, long_double_int 32 ...); 0 if none. */
+size_t mx_type_size(int type);
+/* 1 if (op,type) has a kernel in the given table variant, else 0.  The
+ * pattern equals the reference table's non-NULL pattern exactly. */
+int mx_op_supported(int op, int type, int table_variant);
+
+/* inout[i] = inout[i] OP in[i], i < count.  Asynchronous on `stream`
+ * (hipStream_t, NULL = default stream).  Both buffers must be
+ * device-accessible.  count is size_t: no INT_MAX limit. */
+int mx_reduce2(int op, int type, const void *in, void *inout,
+               size_t count, void *stream);
+/* out[i] = in1[i] OP in2[i].  out may alias neither input (restrict, as
+ * in the reference's 3-buffer functions). */
+int mx_reduce3(int op, int type, const void *in1, const void *in2,
+               void *out, size_t count, void *stream);
+
+/* Contiguous device copy (K7), asynchronous on stream. */
+int mx_copy(void *dst, const void *src, size_t bytes, void *stream);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* MX_KERNELS_H */

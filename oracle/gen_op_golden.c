@@ -1,0 +1,215 @@
+/*
+ * gen_op_golden.c -- TEST INFRASTRUCTURE ONLY.
+ *
+ * Golden-vector generator for the predefined MPI_Op kernels.  It links the
+ * reference's OWN kernels (ompi/mca/op/base/op_base_functions.c, compiled
+ * unmodified from /root/reference by oracle/Makefile into
+ * oracle/_ref/libref_op_f.so, the with-Fortran 176-entry table) and records,
+ * for every non-NULL (op, type) slot of ompi_op_base_functions /
+ * ompi_op_base_3buff_functions (op_base_functions.c:1485, :1572), seeded
+ * inputs and the reference's outputs.
+ *
+ * Output: tests/golden/op_vectors.bin (little endian):
+ *   "MXGOLD01" | u32 nrec | nrec x { u32 kind(2|3), u32 op, u32 type,
+ *     u32 elem_size, u32 n, bytes a[n*es], bytes b[n*es], bytes out[n*es] }
+ *   kind 2: a = in, b = inout (before), out = inout (after)
+ *   kind 3: a = in1, b = in2, out = out
+ * Inputs mix random values with the edge values the reference's semantics
+ * are sensitive to: NaN of both signs/payloads, +-0, +-inf, denormals,
+ * INT_MIN/INT_MAX wrap, ties for MAXLOC/MINLOC.
+ */
+#include <stdio.h>
+#include <stdlib.h>
+#include <stdint.h>
+#include <string.h>
+#include <math.h>
+#include <float.h>
+
+#include "../include/mx_kernels.h"
+
+typedef void (*fn2_t)(void *, void *, int *, void **, void *);
+typedef void (*fn3_t)(void *, void *, void *, int *, void **, void *);
+extern fn2_t ompi_op_base_functions[MX_OP_COUNT][MX_TYPE_COUNT];
+extern fn3_t ompi_op_base_3buff_functions[MX_OP_COUNT][MX_TYPE_COUNT];
+
+extern size_t mxo_type_size(int t);
+
+static uint64_t rng_state;
+static uint64_t rnd(void)
+{   /* xorshift64* */
+    rng_state ^= rng_state >> 12;
+    rng_state ^= rng_state << 25;
+    rng_state ^= rng_state >> 27;
+    return rng_state * 0x2545F4914F6CDD1DULL;
+}
+static double urand(void) { return (double)(rnd() >> 11) / 9007199254740992.0; }
+
+static float gen_float(int op)
+{
+    uint64_t r = rnd() % 100;
+    static const uint32_t specials[] = {
+        0x7fc00000u, 0xffc00000u, 0x7fa00001u, 0x7f800000u, 0xff800000u,
+        0x00000000u, 0x80000000u, 0x00000001u, 0x807fffffu, 0x00400000u,
+        0x7f7fffffu, 0xff7fffffu, 0x00800000u, 0x3f800000u, 0xbf800000u };
+    if (r < 55) {
+        if (op == MX_OP_PROD) return (float)(0.5 + 1.5 * urand()) * ((rnd() & 1) ? 1.f : -1.f);
+        return (float)(urand() * 8.0 - 4.0);
+    }
+    if (r < 75) { float f; uint32_t u = specials[rnd() % (sizeof specials / 4)]; memcpy(&f, &u, 4); return f; }
+    if (r < 85) return (float)((int)(rnd() % 7) - 3);            /* ties */
+    if (r < 95) return (float)(urand() * 1e38) * ((rnd() & 1) ? 1.f : -1.f); /* overflow */
+    { float f; uint32_t u = (uint32_t)rnd(); memcpy(&f, &u, 4); return f; }   /* raw bits */
+}
+
+static double gen_double(int op)
+{
+    uint64_t r = rnd() % 100;
+    static const uint64_t specials[] = {
+        0x7ff8000000000000ull, 0xfff8000000000000ull, 0x7ff4000000000001ull,
+        0x7ff0000000000000ull, 0xfff0000000000000ull, 0, 0x8000000000000000ull,
+        1, 0x800fffffffffffffull, 0x7fefffffffffffffull, 0x0010000000000000ull,
+        0x3ff0000000000000ull };
+    if (r < 55) {
+        if (op == MX_OP_PROD) return (0.5 + 1.5 * urand()) * ((rnd() & 1) ? 1.0 : -1.0);
+        return urand() * 8.0 - 4.0;
+    }
+    if (r < 75) { double d; uint64_t u = specials[rnd() % (sizeof specials / 8)]; memcpy(&d, &u, 8); return d; }
+    if (r < 85) return (double)((int)(rnd() % 7) - 3);
+    if (r < 95) return urand() * 1e308 * ((rnd() & 1) ? 1.0 : -1.0);
+    { double d; uint64_t u = rnd(); memcpy(&d, &u, 8); return d; }
+}
+
+static long double gen_ldouble(int op)
+{
+    long double v;
+    uint64_t r = rnd() % 100;
+    if (r < 30) v = (long double)gen_double(op);
+    else if (r < 60) v = (long double)gen_double(op) + (long double)gen_double(op) * 1e-17L;
+    else if (r < 70) v = (r & 1) ? LDBL_MAX : -LDBL_MIN;
+    else if (r < 80) v = (long double)((int)(rnd() % 7) - 3);
+    else if (r < 90) v = (long double)(urand() * 8.0 - 4.0) * 1e4000L;
+    else v = (long double)gen_double(op) / 3.0L;
+    return v;
+}
+
+static void fill_int(void *p, size_t es, size_t n, int op, int is_bool_like)
+{
+    for (size_t i = 0; i < n; i++) {
+        uint64_t r = rnd() % 100, v;
+        if (is_bool_like == 1) v = rnd() & 1;                       /* _Bool: 0/1 only (UB otherwise) */
+        else if (r < 60) v = rnd();
+        else if (r < 75) v = (uint64_t)(int64_t)((int)(rnd() % 7) - 3);
+        else {
+            static const uint64_t ext[] = { 0, 1, ~0ull, 0x7fffffffffffffffull, 0x8000000000000000ull };
+            int j = rnd() % 5;
+            v = ext[j];
+            if (j >= 3) { /* narrow extremes: INT_MAX / INT_MIN of the width */
+                int bits = (int)es * 8;
+                v = (j == 3) ? ((1ull << (bits - 1)) - 1) : (1ull << (bits - 1));
+            }
+        }
+        if (is_bool_like == 2) v = (r < 50) ? (rnd() % 3) : v;      /* Fortran LOGICAL: mostly 0/1/2 */
+        (void)op;
+        memcpy((char *)p + i * es, &v, es);
+    }
+}
+
+static void fill(int op, int t, void *p, size_t n)
+{
+    size_t es = mxo_type_size(t);
+    memset(p, 0, es * n);
+    switch (t) {
+    case MX_TYPE_FLOAT: case MX_TYPE_REAL: case MX_TYPE_REAL4:
+        for (size_t i = 0; i < n; i++) ((float *)p)[i] = gen_float(op);
+        break;
+    case MX_TYPE_DOUBLE: case MX_TYPE_REAL8: case MX_TYPE_DOUBLE_PRECISION:
+        for (size_t i = 0; i < n; i++) ((double *)p)[i] = gen_double(op);
+        break;
+    case MX_TYPE_LONG_DOUBLE:
+        for (size_t i = 0; i < n; i++) { long double v = gen_ldouble(op); memcpy((char *)p + 16 * i, &v, 10); }
+        break;
+    case MX_TYPE_C_FLOAT_COMPLEX:
+        for (size_t i = 0; i < 2 * n; i++) ((float *)p)[i] = gen_float(op);
+        break;
+    case MX_TYPE_C_DOUBLE_COMPLEX:
+        for (size_t i = 0; i < 2 * n; i++) ((double *)p)[i] = gen_double(op);
+        break;
+    case MX_TYPE_C_LONG_DOUBLE_COMPLEX:
+        for (size_t i = 0; i < 2 * n; i++) { long double v = gen_ldouble(op); memcpy((char *)p + 16 * i, &v, 10); }
+        break;
+    case MX_TYPE_BOOL:
+        fill_int(p, 1, n, op, 1);
+        break;
+    case MX_TYPE_LOGICAL:
+        fill_int(p, 4, n, op, 2);
+        break;
+    case MX_TYPE_FLOAT_INT: case MX_TYPE_DOUBLE_INT: case MX_TYPE_LONG_INT:
+    case MX_TYPE_2INT: case MX_TYPE_SHORT_INT: case MX_TYPE_LONG_DOUBLE_INT:
+    case MX_TYPE_2REAL: case MX_TYPE_2DOUBLE_PRECISION: case MX_TYPE_2INTEGER:
+        for (size_t i = 0; i < n; i++) {
+            char *e = (char *)p + i * es;
+            int small = (int)(rnd() % 4) - 1;           /* few distinct values -> ties */
+            int k = (rnd() % 4 == 0) ? (int)rnd() : (int)(rnd() % 9) - 4;
+            int nan = (rnd() % 16) == 0;
+            switch (t) {
+            case MX_TYPE_FLOAT_INT: { float v = nan ? NAN : (float)small; memcpy(e, &v, 4); memcpy(e + 4, &k, 4); } break;
+            case MX_TYPE_DOUBLE_INT: { double v = nan ? -NAN : (double)small; memcpy(e, &v, 8); memcpy(e + 8, &k, 4); } break;
+            case MX_TYPE_LONG_INT: { long v = (rnd() % 8 == 0) ? (long)rnd() : small; memcpy(e, &v, 8); memcpy(e + 8, &k, 4); } break;
+            case MX_TYPE_2INT: case MX_TYPE_2INTEGER: { int v = (rnd() % 8 == 0) ? (int)rnd() : small; memcpy(e, &v, 4); memcpy(e + 4, &k, 4); } break;
+            case MX_TYPE_SHORT_INT: { short v = (short)((rnd() % 8 == 0) ? (short)rnd() : small); memcpy(e, &v, 2); memcpy(e + 4, &k, 4); } break;
+            case MX_TYPE_LONG_DOUBLE_INT: { long double v = nan ? (long double)NAN : (long double)small; memcpy(e, &v, 10); memcpy(e + 16, &k, 4); } break;
+            case MX_TYPE_2REAL: { float v = nan ? NAN : (float)small, kk = (float)k; memcpy(e, &v, 4); memcpy(e + 4, &kk, 4); } break;
+            case MX_TYPE_2DOUBLE_PRECISION: { double v = nan ? NAN : (double)small, kk = (double)k; memcpy(e, &v, 8); memcpy(e + 8, &kk, 8); } break;
+            }
+        }
+        break;
+    default:
+        fill_int(p, es, n, op, 0);
+        break;
+    }
+}
+
+static void put32(FILE *f, uint32_t v) { fwrite(&v, 4, 1, f); }
+
+int main(int argc, char **argv)
+{
+    const char *path = argc > 1 ? argv[1] : "tests/golden/op_vectors.bin";
+    const int n = 131;   /* ragged: not a multiple of any vector width */
+    FILE *f = fopen(path, "wb");
+    uint32_t nrec = 0;
+    if (!f) { perror(path); return 1; }
+    fwrite("MXGOLD01", 8, 1, f);
+    put32(f, 0);
+    for (int kind = 2; kind <= 3; kind++) {
+        for (int op = 0; op < MX_OP_COUNT; op++) {
+            for (int t = 0; t < MX_TYPE_COUNT; t++) {
+                void *fp = (kind == 2) ? (void *)ompi_op_base_functions[op][t]
+                                       : (void *)ompi_op_base_3buff_functions[op][t];
+                size_t es = mxo_type_size(t);
+                char *a, *b, *o;
+                int cnt = n;
+                if (!fp) continue;
+                if (es == 0) { fprintf(stderr, "no size for type %d\n", t); return 1; }
+                rng_state = 0x5EEDC0DEULL ^ ((uint64_t)(op * 64 + t) << 20) ^ (uint64_t)kind;
+                a = calloc(n, es); b = calloc(n, es); o = calloc(n, es);
+                fill(op, t, a, n);
+                fill(op, t, b, n);
+                if (kind == 2) {
+                    memcpy(o, b, n * es);
+                    ((fn2_t)fp)(a, o, &cnt, NULL, NULL);
+                } else {
+                    ((fn3_t)fp)(a, b, o, &cnt, NULL, NULL);
+                }
+                put32(f, kind); put32(f, op); put32(f, t); put32(f, (uint32_t)es); put32(f, n);
+                fwrite(a, es, n, f); fwrite(b, es, n, f); fwrite(o, es, n, f);
+                free(a); free(b); free(o);
+                nrec++;
+            }
+        }
+    }
+    fseek(f, 8, SEEK_SET);
+    put32(f, nrec);
+    fclose(f);
+    printf("wrote %u records to %s\n", nrec, path);
+    return 0;
+}

@@ -1,0 +1,245 @@
+/*
+ * mx_oracle_op.c -- TEST INFRASTRUCTURE ONLY (never linked into the product).
+ *
+ * Plain-C restatement of the reference's predefined MPI_Op kernels, used as
+ * the CPU checker for the HIP kernels of libmx_kernels.so and as the "port"
+ * CPU baseline.  Only tests/, __graft_entry__.smoke() and bench.py's
+ * cpu_baseline leg may load it.
+ *
+ * Reference semantics restated here (HewlettPackard/zhpe-ompi,
+ * ompi/mca/op/base/op_base_functions.c):
+ *   OP_FUNC      :40-51   out op= in        (SUM '+=', PROD '*=')
+ *   FUNC_FUNC    :60-73   out = f(out, in)  (MAX :153 'out>in?out:in',
+ *                                            MIN :216 'out<in?out:in',
+ *                                            LAND :416 '&&', LOR :438 '||',
+ *                                            LXOR :460 '(a?1:0)^(b?1:0)',
+ *                                            BAND/BOR/BXOR :482-587)
+ *   LOC_FUNC     :88-104  in.v OP out.v -> take in; == -> k=min(k)
+ *   complex      :339-341, :408-410 (C _Complex += / *=)
+ *   3-buffer     :654-775 out = f(in1, in2); LOC_FUNC_3BUF :709-731
+ *   tables       :1485-1569 (2-buffer), :1572-1655 (3-buffer)
+ * The (op,type) availability pattern restates those tables for the C-only
+ * build (116 pairs) and the with-Fortran build (176 pairs).
+ *
+ * Parity: pinned against the reference's own compiled op_base_functions.c
+ * (oracle/_ref/libref_op*.so, built by oracle/Makefile) over the golden
+ * vectors in tests/golden/ -- see tests/test_oracle_golden.py.
+ *
+ * Integer SUM/PROD are done in the C type exactly as the reference does
+ * (promotion then truncation); signed overflow is made well-defined by
+ * compiling with -fwrapv (the reference's gcc -O2 codegen wraps too).
+ */
+#include <stdint.h>
+#include <stddef.h>
+#include <stdbool.h>
+#include <string.h>
+#include <complex.h>
+
+#include "../include/mx_kernels.h"
+
+typedef struct { float v; int k; } mxo_float_int;
+typedef struct { double v; int k; } mxo_double_int;
+typedef struct { long v; int k; } mxo_long_int;
+typedef struct { int v; int k; } mxo_2int;
+typedef struct { short v; int k; } mxo_short_int;
+typedef struct { long double v; int k; } mxo_long_double_int;
+typedef struct { float v; float k; } mxo_2real;
+typedef struct { double v; double k; } mxo_2double;
+
+/* ---------------- availability pattern (tables :1485-1655) ----------- */
+
+enum kind { K_NONE, K_SINT, K_UINT, K_FLT, K_LOGICAL, K_BOOL, K_CPLX, K_BYTE, K_LOC };
+
+static int type_kind(int t, int fortran)
+{
+    switch (t) {
+    case MX_TYPE_INT8_T: case MX_TYPE_INT16_T: case MX_TYPE_INT32_T: case MX_TYPE_INT64_T:
+        return K_SINT;
+    case MX_TYPE_UINT8_T: case MX_TYPE_UINT16_T: case MX_TYPE_UINT32_T: case MX_TYPE_UINT64_T:
+        return K_UINT;
+    case MX_TYPE_INTEGER: case MX_TYPE_INTEGER1: case MX_TYPE_INTEGER2:
+    case MX_TYPE_INTEGER4: case MX_TYPE_INTEGER8:
+        return fortran ? K_SINT : K_NONE;
+    case MX_TYPE_FLOAT: case MX_TYPE_DOUBLE: case MX_TYPE_LONG_DOUBLE:
+        return K_FLT;
+    case MX_TYPE_REAL: case MX_TYPE_REAL4: case MX_TYPE_REAL8: case MX_TYPE_DOUBLE_PRECISION:
+        return fortran ? K_FLT : K_NONE;
+    case MX_TYPE_LOGICAL:
+        return fortran ? K_LOGICAL : K_NONE;
+    case MX_TYPE_BOOL:
+        return K_BOOL;
+    case MX_TYPE_C_FLOAT_COMPLEX: case MX_TYPE_C_DOUBLE_COMPLEX: case MX_TYPE_C_LONG_DOUBLE_COMPLEX:
+        return K_CPLX;
+    case MX_TYPE_BYTE:
+        return K_BYTE;
+    case MX_TYPE_FLOAT_INT: case MX_TYPE_DOUBLE_INT: case MX_TYPE_LONG_INT:
+    case MX_TYPE_2INT: case MX_TYPE_SHORT_INT: case MX_TYPE_LONG_DOUBLE_INT:
+        return K_LOC;
+    case MX_TYPE_2REAL: case MX_TYPE_2DOUBLE_PRECISION: case MX_TYPE_2INTEGER:
+        return fortran ? K_LOC : K_NONE;
+    default:
+        return K_NONE;
+    }
+}
+
+int mxo_supported(int op, int t, int fortran)
+{
+    int k;
+    if (t < 0 || t >= MX_TYPE_COUNT) return 0;
+    k = type_kind(t, fortran);
+    if (k == K_NONE) return 0;
+    switch (op) {
+    case MX_OP_MAX: case MX_OP_MIN:
+        return k == K_SINT || k == K_UINT || k == K_FLT;
+    case MX_OP_SUM: case MX_OP_PROD:
+        return k == K_SINT || k == K_UINT || k == K_FLT || k == K_CPLX;
+    case MX_OP_LAND: case MX_OP_LOR: case MX_OP_LXOR:
+        /* C integers (not Fortran integers), LOGICAL, bool (:1520-1545) */
+        return (k == K_SINT && t <= MX_TYPE_UINT64_T) || k == K_UINT ||
+               k == K_LOGICAL || k == K_BOOL;
+    case MX_OP_BAND: case MX_OP_BOR: case MX_OP_BXOR:
+        return k == K_SINT || k == K_UINT || k == K_BYTE;
+    case MX_OP_MAXLOC: case MX_OP_MINLOC:
+        return k == K_LOC;
+    default:
+        return 0;
+    }
+}
+
+size_t mxo_type_size(int t)
+{
+    switch (t) {
+    case MX_TYPE_INT8_T: case MX_TYPE_UINT8_T: case MX_TYPE_INTEGER1:
+    case MX_TYPE_BOOL: case MX_TYPE_BYTE:
+        return 1;
+    case MX_TYPE_INT16_T: case MX_TYPE_UINT16_T: case MX_TYPE_INTEGER2:
+        return 2;
+    case MX_TYPE_INT32_T: case MX_TYPE_UINT32_T: case MX_TYPE_INTEGER: case MX_TYPE_INTEGER4:
+    case MX_TYPE_FLOAT: case MX_TYPE_REAL: case MX_TYPE_REAL4: case MX_TYPE_LOGICAL:
+        return 4;
+    case MX_TYPE_INT64_T: case MX_TYPE_UINT64_T: case MX_TYPE_INTEGER8:
+    case MX_TYPE_DOUBLE: case MX_TYPE_REAL8: case MX_TYPE_DOUBLE_PRECISION:
+    case MX_TYPE_C_FLOAT_COMPLEX: case MX_TYPE_FLOAT_INT: case MX_TYPE_2INT:
+    case MX_TYPE_SHORT_INT: case MX_TYPE_2REAL: case MX_TYPE_2INTEGER:
+        return 8;
+    case MX_TYPE_LONG_DOUBLE: case MX_TYPE_C_DOUBLE_COMPLEX: case MX_TYPE_DOUBLE_INT:
+    case MX_TYPE_LONG_INT: case MX_TYPE_2DOUBLE_PRECISION:
+        return 16;
+    case MX_TYPE_C_LONG_DOUBLE_COMPLEX: case MX_TYPE_LONG_DOUBLE_INT:
+        return 32;
+    default:
+        return 0;
+    }
+}
+
+/* ---------------- element loops ------------------------------------- */
+
+#define L2(T, EXPR)                                                        \
+    do { const T *a = (const T *)in; T *b = (T *)io;                       \
+         for (size_t i = 0; i < n; i++) { T x = b[i], y = a[i]; b[i] = (T)(EXPR); } \
+    } while (0)
+#define L3(T, EXPR)                                                        \
+    do { const T *p = (const T *)i1, *q = (const T *)i2; T *o = (T *)out;  \
+         for (size_t i = 0; i < n; i++) { T x = p[i], y = q[i]; o[i] = (T)(EXPR); } \
+    } while (0)
+
+/* x = first operand (2-buffer: out, 3-buffer: in1); y = second. */
+#define ARITH_CASES(L, T)                                                  \
+    case MX_OP_MAX:  L(T, x > y ? x : y); return 0;                        \
+    case MX_OP_MIN:  L(T, x < y ? x : y); return 0;                        \
+    case MX_OP_SUM:  L(T, x + y); return 0;                                \
+    case MX_OP_PROD: L(T, x * y); return 0;
+#define LOGIC_CASES(L, T)                                                  \
+    case MX_OP_LAND: L(T, x && y); return 0;                               \
+    case MX_OP_LOR:  L(T, x || y); return 0;                               \
+    case MX_OP_LXOR: L(T, (x ? 1 : 0) ^ (y ? 1 : 0)); return 0;
+#define BIT_CASES(L, T)                                                    \
+    case MX_OP_BAND: L(T, x & y); return 0;                                \
+    case MX_OP_BOR:  L(T, x | y); return 0;                                \
+    case MX_OP_BXOR: L(T, x ^ y); return 0;
+
+#define INT_SWITCH(L, T)                                                   \
+    switch (op) { ARITH_CASES(L, T) LOGIC_CASES(L, T) BIT_CASES(L, T) default: return -2; }
+#define FLT_SWITCH(L, T)                                                   \
+    switch (op) { ARITH_CASES(L, T) default: return -2; }
+
+/* LOC_FUNC (:88-104): 2-buffer, b = out, a = in */
+#define LOC2(T, CMP)                                                       \
+    do { const T *a = (const T *)in; T *b = (T *)io;                       \
+         for (size_t i = 0; i < n; i++) {                                  \
+             if (a[i].v CMP b[i].v) { b[i].v = a[i].v; b[i].k = a[i].k; }  \
+             else if (a[i].v == b[i].v) { b[i].k = b[i].k < a[i].k ? b[i].k : a[i].k; } \
+         } } while (0)
+/* LOC_FUNC_3BUF (:709-731) */
+#define LOC3(T, CMP)                                                       \
+    do { const T *p = (const T *)i1, *q = (const T *)i2; T *o = (T *)out;  \
+         for (size_t i = 0; i < n; i++) {                                  \
+             if (p[i].v CMP q[i].v) { o[i].v = p[i].v; o[i].k = p[i].k; }  \
+             else if (p[i].v == q[i].v) { o[i].v = p[i].v; o[i].k = q[i].k < p[i].k ? q[i].k : p[i].k; } \
+             else { o[i].v = q[i].v; o[i].k = q[i].k; }                     \
+         } } while (0)
+
+#define LOC_SWITCH(LOC, T)                                                 \
+    if (op == MX_OP_MAXLOC) { LOC(T, >); return 0; }                       \
+    if (op == MX_OP_MINLOC) { LOC(T, <); return 0; }                       \
+    return -2;
+
+#define CPLX_SWITCH(L, T)                                                  \
+    switch (op) {                                                          \
+    case MX_OP_SUM:  L(T, x + y); return 0;                                \
+    case MX_OP_PROD: L(T, x * y); return 0;                                \
+    default: return -2; }
+
+#define DISPATCH(L, LOC)                                                   \
+    switch (t) {                                                           \
+    case MX_TYPE_INT8_T: case MX_TYPE_INTEGER1: INT_SWITCH(L, int8_t)      \
+    case MX_TYPE_UINT8_T: INT_SWITCH(L, uint8_t)                           \
+    case MX_TYPE_INT16_T: case MX_TYPE_INTEGER2: INT_SWITCH(L, int16_t)    \
+    case MX_TYPE_UINT16_T: INT_SWITCH(L, uint16_t)                         \
+    case MX_TYPE_INT32_T: case MX_TYPE_INTEGER: case MX_TYPE_INTEGER4:     \
+    case MX_TYPE_LOGICAL: INT_SWITCH(L, int32_t)                           \
+    case MX_TYPE_UINT32_T: INT_SWITCH(L, uint32_t)                         \
+    case MX_TYPE_INT64_T: case MX_TYPE_INTEGER8: INT_SWITCH(L, int64_t)    \
+    case MX_TYPE_UINT64_T: INT_SWITCH(L, uint64_t)                         \
+    case MX_TYPE_BYTE: INT_SWITCH(L, char)                                 \
+    case MX_TYPE_BOOL: INT_SWITCH(L, bool)                                 \
+    case MX_TYPE_FLOAT: case MX_TYPE_REAL: case MX_TYPE_REAL4: FLT_SWITCH(L, float) \
+    case MX_TYPE_DOUBLE: case MX_TYPE_REAL8: case MX_TYPE_DOUBLE_PRECISION: FLT_SWITCH(L, double) \
+    case MX_TYPE_LONG_DOUBLE: FLT_SWITCH(L, long double)                   \
+    case MX_TYPE_C_FLOAT_COMPLEX: CPLX_SWITCH(L, float _Complex)           \
+    case MX_TYPE_C_DOUBLE_COMPLEX: CPLX_SWITCH(L, double _Complex)         \
+    case MX_TYPE_C_LONG_DOUBLE_COMPLEX: CPLX_SWITCH(L, long double _Complex) \
+    case MX_TYPE_FLOAT_INT: LOC_SWITCH(LOC, mxo_float_int)                 \
+    case MX_TYPE_DOUBLE_INT: LOC_SWITCH(LOC, mxo_double_int)               \
+    case MX_TYPE_LONG_INT: LOC_SWITCH(LOC, mxo_long_int)                   \
+    case MX_TYPE_2INT: case MX_TYPE_2INTEGER: LOC_SWITCH(LOC, mxo_2int)    \
+    case MX_TYPE_SHORT_INT: LOC_SWITCH(LOC, mxo_short_int)                 \
+    case MX_TYPE_LONG_DOUBLE_INT: LOC_SWITCH(LOC, mxo_long_double_int)     \
+    case MX_TYPE_2REAL: LOC_SWITCH(LOC, mxo_2real)                         \
+    case MX_TYPE_2DOUBLE_PRECISION: LOC_SWITCH(LOC, mxo_2double)           \
+    default: return -2;                                                    \
+    }
+
+static int reduce2_impl(int op, int t, const void *in, void *io, size_t n)
+{
+    DISPATCH(L2, LOC2)
+}
+
+static int reduce3_impl(int op, int t, const void *i1, const void *i2, void *out, size_t n)
+{
+    DISPATCH(L3, LOC3)
+}
+
+/* Returns 0, or -2 (MX_ERR_UNSUPPORTED) for a NULL table slot. */
+int mxo_reduce2(int op, int t, const void *in, void *inout, size_t n, int fortran)
+{
+    if (!mxo_supported(op, t, fortran)) return -2;
+    return reduce2_impl(op, t, in, inout, n);
+}
+
+int mxo_reduce3(int op, int t, const void *in1, const void *in2, void *out, size_t n,
+                int fortran)
+{
+    if (!mxo_supported(op, t, fortran)) return -2;
+    return reduce3_impl(op, t, in1, in2, out, n);
+}

@@ -1,0 +1,93 @@
+// mx_runtime.hip -- process-level state, error mapping and device probes of
+// libmx_kernels.so.  The buffer probe replaces the accelerator hooks the
+// reference uses to route a buffer (opal/datatype/opal_datatype_cuda.c:70-90
+// opal_cuda_check_bufs, opal/mca/common/cuda/common_cuda.c:1736-1857).
+#include <hip/hip_runtime.h>
+#include <stdio.h>
+#include <string.h>
+#include "mx_internal.h"
+
+namespace mx {
+int g_num_cus = 256;
+int g_device = -1;
+}  // namespace mx
+
+using namespace mx;
+
+int mx_hip_rc(hipError_t e) { return e == hipSuccess ? MX_SUCCESS : MX_ERR_HIP; }
+
+int mx_check_launch(void) {
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) {
+    fprintf(stderr, "mx_kernels: launch failed: %s\n", hipGetErrorString(e));
+    return MX_ERR_HIP;
+  }
+  return MX_SUCCESS;
+}
+
+extern "C" int mx_init(int device) {
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess || n <= 0) return MX_ERR_NOT_INIT;
+  if (device < 0) {
+    if (hipGetDevice(&device) != hipSuccess) return MX_ERR_HIP;
+  }
+  if (device >= n) return MX_ERR_ARG;
+  if (hipSetDevice(device) != hipSuccess) return MX_ERR_HIP;
+  hipDeviceProp_t prop;
+  if (hipGetDeviceProperties(&prop, device) != hipSuccess) return MX_ERR_HIP;
+  g_num_cus = prop.multiProcessorCount > 0 ? prop.multiProcessorCount : 256;
+  g_device = device;
+  return MX_SUCCESS;
+}
+
+int mx_ensure_init(void) {
+  if (g_device >= 0) {
+    int cur = -1;
+    if (hipGetDevice(&cur) == hipSuccess && cur == g_device) return MX_SUCCESS;
+  }
+  return mx_init(-1);
+}
+
+extern "C" int mx_finalize(void) {
+  g_device = -1;
+  return MX_SUCCESS;
+}
+
+extern "C" int mx_is_device_ptr(const void *p) {
+  if (!p) return 0;
+  hipPointerAttribute_t attr;
+  memset(&attr, 0, sizeof attr);
+  hipError_t e = hipPointerGetAttributes(&attr, p);
+  if (e != hipSuccess) {
+    (void)hipGetLastError();  // unregistered host memory: clear the sticky error
+    return 0;
+  }
+  return (attr.type == hipMemoryTypeDevice || attr.type == hipMemoryTypeManaged) ? 1 : 0;
+}
+
+extern "C" int mx_stream_sync(void *stream) {
+  return mx_hip_rc(hipStreamSynchronize((hipStream_t)stream));
+}
+
+extern "C" int mx_copy(void *dst, const void *src, size_t bytes, void *stream) {
+  if (bytes == 0) return MX_SUCCESS;
+  if (!dst || !src) return MX_ERR_ARG;
+  return mx_hip_rc(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToDevice, (hipStream_t)stream));
+}
+
+extern "C" const char *mx_strerror(int rc) {
+  switch (rc) {
+    case MX_SUCCESS: return "success";
+    case MX_ERR_ARG: return "invalid argument";
+    case MX_ERR_UNSUPPORTED: return "operation not defined for this datatype";
+    case MX_ERR_HIP: return "HIP runtime error";
+    case MX_ERR_NOMEM: return "out of memory";
+    case MX_ERR_TIMEOUT: return "timed out waiting for a peer";
+    case MX_ERR_RCCL: return "RCCL error";
+    case MX_ERR_NOT_INIT: return "not initialised / no device";
+    case MX_ERR_STATE: return "invalid state";
+    default: return "unknown error";
+  }
+}
+
+extern "C" const char *mx_version(void) { return "mx_kernels gfx950 abi 1"; }

@@ -1,0 +1,159 @@
+"""mxompi -- Python view of the MI355X collective-reduction hot path.
+
+Thin ctypes binding of the C-ABI libraries built in-tree by
+``zhpe-ompi_amd/Makefile``:
+
+* ``lib/libmx_kernels.so`` -- HIP kernels for gfx950 behind
+  ``include/mx_kernels.h`` (op kernels), ``include/mx_convertor.h``
+  (datatype pack/unpack) and ``include/mx_coll.h`` (collectives);
+* ``lib/libmx_ompi.so`` -- the host C MCA components (``op/mi355x``,
+  ``coll/mi355x``) plus the mini-host harness that mimics Open MPI's
+  selection logic.
+
+Python is used by the tests and by ``bench.py`` only (device memory comes
+from torch tensors); the product path is C/HIP.  There is no CPU fallback:
+if the HIP library is missing, :func:`lib` raises.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+PKG_ROOT = os.path.dirname(_HERE)
+REPO_ROOT = os.path.dirname(PKG_ROOT)
+LIB_DIR = os.path.join(PKG_ROOT, "lib")
+
+# ---- op / type numbering == OMPI_OP_BASE_FORTRAN_* / OMPI_OP_BASE_TYPE_* ----
+OPS = ["NULL", "MAX", "MIN", "SUM", "PROD", "LAND", "BAND", "LOR", "BOR",
+       "LXOR", "BXOR", "MAXLOC", "MINLOC", "REPLACE", "NO_OP"]
+OP = {name: i for i, name in enumerate(OPS)}
+
+TYPES = ["INT8_T", "UINT8_T", "INT16_T", "UINT16_T", "INT32_T", "UINT32_T",
+         "INT64_T", "UINT64_T", "INTEGER", "INTEGER1", "INTEGER2", "INTEGER4",
+         "INTEGER8", "INTEGER16", "SHORT_FLOAT", "FLOAT", "DOUBLE", "REAL",
+         "REAL2", "REAL4", "REAL8", "REAL16", "DOUBLE_PRECISION", "LONG_DOUBLE",
+         "LOGICAL", "BOOL", "C_SHORT_FLOAT_COMPLEX", "C_FLOAT_COMPLEX",
+         "C_DOUBLE_COMPLEX", "C_LONG_DOUBLE_COMPLEX", "BYTE", "2REAL",
+         "2DOUBLE_PRECISION", "2INTEGER", "FLOAT_INT", "DOUBLE_INT", "LONG_INT",
+         "2INT", "SHORT_INT", "LONG_DOUBLE_INT", "WCHAR"]
+TYPE = {name: i for i, name in enumerate(TYPES)}
+
+TABLE_C_ONLY = 0
+TABLE_WITH_FORTRAN = 1
+
+# MPI predefined datatype -> op type slot (restates ompi/op/op.c:131-229 with
+# the C aliases of ompi/datatype/ompi_datatype_internal.h:130-200 for LP64).
+MPI_DTYPE_SLOT = {
+    "MPI_INT8_T": "INT8_T", "MPI_UINT8_T": "UINT8_T", "MPI_INT16_T": "INT16_T",
+    "MPI_UINT16_T": "UINT16_T", "MPI_INT32_T": "INT32_T", "MPI_UINT32_T": "UINT32_T",
+    "MPI_INT64_T": "INT64_T", "MPI_UINT64_T": "UINT64_T",
+    "MPI_CHAR": "INT8_T", "MPI_SIGNED_CHAR": "INT8_T", "MPI_UNSIGNED_CHAR": "UINT8_T",
+    "MPI_BYTE": "UINT8_T", "MPI_SHORT": "INT16_T", "MPI_UNSIGNED_SHORT": "UINT16_T",
+    "MPI_INT": "INT32_T", "MPI_UNSIGNED": "UINT32_T", "MPI_LONG": "INT64_T",
+    "MPI_UNSIGNED_LONG": "UINT64_T", "MPI_LONG_LONG_INT": "INT64_T",
+    "MPI_LONG_LONG": "INT64_T", "MPI_UNSIGNED_LONG_LONG": "UINT64_T",
+    "MPI_FLOAT": "FLOAT", "MPI_DOUBLE": "DOUBLE", "MPI_LONG_DOUBLE": "LONG_DOUBLE",
+    "MPI_WCHAR": "WCHAR", "MPI_CXX_BOOL": "BOOL", "MPI_LOGICAL": "LOGICAL",
+    "MPI_CHARACTER": "UINT8_T", "MPI_INTEGER": "INTEGER", "MPI_REAL": "REAL",
+    "MPI_DOUBLE_PRECISION": "DOUBLE_PRECISION",
+    "MPI_LONG_DOUBLE_COMPLEX": "C_LONG_DOUBLE_COMPLEX",
+    "MPI_2INT": "2INT", "MPI_2INTEGER": "2INTEGER", "MPI_2REAL": "2REAL",
+    "MPI_2DOUBLE_PRECISION": "2DOUBLE_PRECISION", "MPI_FLOAT_INT": "FLOAT_INT",
+    "MPI_DOUBLE_INT": "DOUBLE_INT", "MPI_LONG_DOUBLE_INT": "LONG_DOUBLE_INT",
+    "MPI_LONG_INT": "LONG_INT", "MPI_SHORT_INT": "SHORT_INT",
+    "MPI_AINT": "INT64_T", "MPI_OFFSET": "UINT64_T", "MPI_C_BOOL": "BOOL",
+    "MPI_C_COMPLEX": "C_FLOAT_COMPLEX", "MPI_C_FLOAT_COMPLEX": "C_FLOAT_COMPLEX",
+    "MPI_C_DOUBLE_COMPLEX": "C_DOUBLE_COMPLEX",
+    "MPI_C_LONG_DOUBLE_COMPLEX": "C_LONG_DOUBLE_COMPLEX", "MPI_COUNT": "INT64_T",
+}
+
+ERRORS = {0: "MX_SUCCESS", -1: "MX_ERR_ARG", -2: "MX_ERR_UNSUPPORTED", -3: "MX_ERR_HIP",
+          -4: "MX_ERR_NOMEM", -5: "MX_ERR_TIMEOUT", -6: "MX_ERR_RCCL",
+          -7: "MX_ERR_NOT_INIT", -8: "MX_ERR_STATE"}
+
+
+class MxError(RuntimeError):
+    def __init__(self, rc: int, what: str = ""):
+        super().__init__(f"{what}: {ERRORS.get(rc, rc)} ({rc})")
+        self.rc = rc
+
+
+_libs: dict = {}
+
+
+def _load(name: str) -> ctypes.CDLL:
+    if name in _libs:
+        return _libs[name]
+    path = os.path.join(LIB_DIR, name)
+    if not os.path.exists(path):
+        raise RuntimeError(
+            f"{path} is missing: the HIP product library was not built "
+            "(run `make -C zhpe-ompi_amd` or __graft_entry__.build()); "
+            "there is no CPU fallback")
+    lib = ctypes.CDLL(path, mode=ctypes.RTLD_GLOBAL)
+    _libs[name] = lib
+    return lib
+
+
+def lib() -> ctypes.CDLL:
+    """The HIP kernel library (C-ABI of include/mx_kernels.h)."""
+    L = _load("libmx_kernels.so")
+    if not getattr(L, "_mx_typed", False):
+        vp, sz, i = ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int
+        L.mx_init.argtypes = [i]
+        L.mx_is_device_ptr.argtypes = [vp]
+        L.mx_stream_sync.argtypes = [vp]
+        L.mx_strerror.restype = ctypes.c_char_p
+        L.mx_strerror.argtypes = [i]
+        L.mx_version.restype = ctypes.c_char_p
+        L.mx_type_size.restype = sz
+        L.mx_type_size.argtypes = [i]
+        L.mx_op_supported.argtypes = [i, i, i]
+        L.mx_reduce2.argtypes = [i, i, vp, vp, sz, vp]
+        L.mx_reduce3.argtypes = [i, i, vp, vp, vp, sz, vp]
+        L.mx_copy.argtypes = [vp, vp, sz, vp]
+        L._mx_typed = True
+    return L
+
+
+def check(rc: int, what: str = "mx call") -> int:
+    if rc < 0:
+        raise MxError(rc, what)
+    return rc
+
+
+def _slot(v) -> int:
+    return TYPE[v] if isinstance(v, str) else int(v)
+
+
+def _op(v) -> int:
+    return OP[v] if isinstance(v, str) else int(v)
+
+
+def type_size(t) -> int:
+    return int(lib().mx_type_size(_slot(t)))
+
+
+def op_supported(op, t, table=TABLE_WITH_FORTRAN) -> bool:
+    return bool(lib().mx_op_supported(_op(op), _slot(t), table))
+
+
+def reduce2(op, t, in_ptr: int, inout_ptr: int, count: int, stream: int = 0) -> None:
+    """inout = inout OP in on the device (asynchronous on `stream`)."""
+    check(lib().mx_reduce2(_op(op), _slot(t), in_ptr, inout_ptr, count, stream or None),
+          f"mx_reduce2({op},{t})")
+
+
+def reduce3(op, t, in1_ptr: int, in2_ptr: int, out_ptr: int, count: int, stream: int = 0) -> None:
+    """out = in1 OP in2 on the device (asynchronous on `stream`)."""
+    check(lib().mx_reduce3(_op(op), _slot(t), in1_ptr, in2_ptr, out_ptr, count, stream or None),
+          f"mx_reduce3({op},{t})")
+
+
+def init(device: int = 0) -> None:
+    check(lib().mx_init(device), "mx_init")
+
+
+def sync(stream: int = 0) -> None:
+    check(lib().mx_stream_sync(stream or None), "mx_stream_sync")
