@@ -1,0 +1,132 @@
+/*
+ * mx_coll.h -- C-ABI of the MI355X collective data path (libmx_kernels.so).
+ *
+ * Replaces, for device-resident buffers, the host algorithms behind the coll
+ * module slots (ompi/mca/coll/coll.h:200-244):
+ *   mx_allreduce       <- ompi_coll_base_allreduce_intra_{recursivedoubling,
+ *                         ring, ring_segmented, redscat_allgather,
+ *                         basic_linear} (ompi/mca/coll/base/
+ *                         coll_base_allreduce.c:130-274, 341-536, 618-856,
+ *                         970-1243, 881-912) as chosen by
+ *                         ompi_coll_tuned_allreduce_intra_dec_fixed
+ *                         (ompi/mca/coll/tuned/coll_tuned_decision_fixed.c:44-95)
+ *   mx_reduce_scatter  <- ompi_coll_base_reduce_scatter_intra_{ring,
+ *                         basic_recursivehalving} (coll_base_reduce_scatter.c:
+ *                         456-623, 132-) + tuned rule (decision_fixed.c:466-512)
+ *   mx_allgather       <- coll_base_allgather.c (pure data movement)
+ *   mx_bcast           <- coll_base_bcast.c (pure data movement)
+ *
+ * Design (MI355X-first, not the reference's message pattern):
+ *  * data moves ALL-PEER over xGMI in one step per phase (every GPU writes
+ *    straight into the IPC-mapped staging of each of the other n-1 GPUs,
+ *    so all 7 links of an MI355X carry traffic at once) instead of the
+ *    reference's n-1 neighbour steps;
+ *  * the local reduction is ONE fused HIP kernel per output part that
+ *    reads the n contributions and evaluates, per element, exactly the
+ *    reduction tree (operand order and roles) that the selected reference
+ *    algorithm would have applied -- so results are bit-identical to
+ *    coll/tuned's for every op, including FP SUM/PROD -- and writes the
+ *    result to the local rbuf and to every peer's gather area;
+ *  * cross-GPU ordering uses generation-tagged flags in uncached device
+ *    memory written with system-scope atomics, waited on by bounded spins
+ *    (a missing peer returns MX_ERR_TIMEOUT instead of hanging the GPU).
+ *
+ * Ownership: the caller owns all buffers.  Calls are blocking with respect
+ * to `stream` semantics: work is enqueued on `stream`, and the call returns
+ * after the stream completed (MPI blocking-collective semantics); results
+ * are in rbuf on return.  One collective at a time per communicator, in the
+ * same order on every rank (MPI semantics).
+ */
+#ifndef MX_COLL_H
+#define MX_COLL_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct mx_comm mx_comm_t;
+
+/* MPI_IN_PLACE as the reference defines it (mpi.h: (void *) 1). */
+#define MX_IN_PLACE ((const void *)1)
+
+/* Maximum ranks of the custom all-peer path (one MI355X node has 8). */
+#define MX_MAX_RANKS 16
+
+/* Host bootstrap all-gather supplied by the caller: gather `bytes` from each
+ * rank into `recv` (rank-major).  In the coll component this is the host
+ * allgather of the lower-priority module saved at module enable (the
+ * coll/cuda stacking pattern, coll_cuda_module.c:120-155); in tests it is
+ * torch.distributed over gloo.  Returns 0 on success. */
+typedef int (*mx_allgather_fn)(const void *send, void *recv, size_t bytes, void *ctx);
+
+/* comm flags */
+#define MX_COMM_IPC   1   /* all-peer xGMI path over IPC-mapped staging  */
+#define MX_COMM_RCCL  2   /* also create an RCCL communicator             */
+
+/* Multi-process communicator: one rank per process (per GPU). */
+int mx_comm_create(int rank, int size, int device, size_t staging_bytes, int flags,
+                   mx_allgather_fn allgather, void *ctx, mx_comm_t **comm);
+/* `size` virtual ranks in ONE process on ONE device.  Same algorithms, same
+ * kernels, same fold order; the data path reads/writes all ranks' buffers
+ * directly (no staging, no flags).  Used by the parity tests on a single
+ * GPU and as the intra-process path. */
+int mx_comm_create_local(int size, int device, mx_comm_t **comm);
+int mx_comm_destroy(mx_comm_t *comm);
+int mx_comm_size(const mx_comm_t *comm);
+int mx_comm_rank(const mx_comm_t *comm);
+/* Bounded-spin timeout for peer waits (default 60 s). */
+int mx_comm_set_timeout(mx_comm_t *comm, double seconds);
+
+/* Allreduce algorithm ids == coll_tuned_allreduce_algorithm values
+ * (ompi/mca/coll/tuned/coll_tuned_allreduce_decision.c:37-46). */
+enum {
+    MX_ALLREDUCE_AUTO = 0,           /* tuned fixed decision                 */
+    MX_ALLREDUCE_BASIC_LINEAR = 1,
+    MX_ALLREDUCE_NONOVERLAPPING = 2, /* not provided: MX_ERR_UNSUPPORTED     */
+    MX_ALLREDUCE_RECURSIVE_DOUBLING = 3,
+    MX_ALLREDUCE_RING = 4,
+    MX_ALLREDUCE_SEGMENTED_RING = 5,
+    MX_ALLREDUCE_RABENSEIFNER = 6,
+    MX_ALLREDUCE_RCCL = 100          /* RCCL ncclAllReduce (order differs:
+                                        FP results within tolerance only)  */
+};
+/* Reduce-scatter algorithm ids (coll_tuned_reduce_scatter_decision.c). */
+enum {
+    MX_RS_AUTO = 0,
+    MX_RS_NONOVERLAPPING = 1,        /* not provided                         */
+    MX_RS_RECURSIVE_HALVING = 2,
+    MX_RS_RING = 3,
+    MX_RS_RCCL = 100
+};
+
+/* Returns the algorithm MX_ALLREDUCE_AUTO resolves to for this call shape
+ * (the tuned fixed decision), for introspection and tests. */
+int mx_allreduce_decision(int comm_size, size_t count, int type);
+int mx_reduce_scatter_decision(int comm_size, size_t total_count, int type);
+
+/* ---- multi-process (or local rank 0 of a local comm: use *_local) ------- */
+int mx_allreduce(mx_comm_t *comm, const void *sbuf, void *rbuf, size_t count,
+                 int type, int op, int alg, void *stream);
+int mx_reduce_scatter(mx_comm_t *comm, const void *sbuf, void *rbuf,
+                      const size_t *rcounts, int type, int op, int alg, void *stream);
+/* Contiguous byte allgather: rank r's `bytes` land at rbuf + r*bytes. */
+int mx_allgather(mx_comm_t *comm, const void *sbuf, void *rbuf, size_t bytes, void *stream);
+int mx_bcast(mx_comm_t *comm, void *buf, size_t bytes, int root, void *stream);
+
+/* ---- local communicator: arrays of `size` buffers, one per rank --------- */
+int mx_allreduce_local(mx_comm_t *comm, const void *const *sbufs, void *const *rbufs,
+                       size_t count, int type, int op, int alg, void *stream);
+int mx_reduce_scatter_local(mx_comm_t *comm, const void *const *sbufs, void *const *rbufs,
+                            const size_t *rcounts, int type, int op, int alg, void *stream);
+int mx_allgather_local(mx_comm_t *comm, const void *const *sbufs, void *const *rbufs,
+                       size_t bytes, void *stream);
+int mx_bcast_local(mx_comm_t *comm, void *const *bufs, size_t bytes, int root, void *stream);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* MX_COLL_H */

@@ -1,0 +1,311 @@
+"""GPU parity of the collective data path vs the reference's algorithms.
+
+The all-peer kernels evaluate, per element, the reduction tree of the
+selected coll/base algorithm; the oracle (oracle/mx_oracle_coll.c) runs the
+reference's algorithms step by step with the op oracle.  Results must be
+bit-identical -- including floating-point SUM/PROD, whose value depends on
+the order -- for every algorithm, rank count and ragged size.
+
+* local communicators (n virtual ranks, one process, one GPU);
+* multi-process communicators (n processes sharing the one GPU, IPC-mapped
+  staging, cross-process flags) through torch.distributed(gloo) bootstrap.
+"""
+import ctypes
+import os
+import socket
+
+import numpy as np
+import pytest
+
+import golden_io
+import mxompi
+import oracle_lib
+
+torch = pytest.importorskip("torch")
+pytestmark = pytest.mark.gpu
+
+vp, sz, ci = ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int
+
+
+def _oracle():
+    L = oracle_lib.oracle()
+    L.mxo_allreduce.argtypes = [ci, ci, ci, ci, sz, ctypes.POINTER(vp), ctypes.POINTER(vp)]
+    L.mxo_allreduce_segring.argtypes = [ci, ci, ci, sz, ctypes.POINTER(vp), sz]
+    L.mxo_reduce_scatter.argtypes = [ci, ci, ci, ci, ctypes.POINTER(sz), ctypes.POINTER(vp), ctypes.POINTER(vp)]
+    return L
+
+
+def gen(t, op, count, seed):
+    """Adversarial inputs: magnitudes spanning 16 decades (so FP order
+    matters), NaN/-0 for MAX/MIN, ties for MAXLOC, 0/1 for bool."""
+    rng = np.random.default_rng(seed)
+    es = mxompi.type_size(t)
+    if t in ("FLOAT", "DOUBLE"):
+        dt = np.float32 if t == "FLOAT" else np.float64
+        v = (rng.uniform(-1, 1, count) * 10.0 ** rng.uniform(-8, 8, count)).astype(dt)
+        if op in ("MAX", "MIN"):
+            k = rng.integers(0, count, max(1, count // 16))
+            v[k] = rng.choice(np.array([np.nan, -0.0, 0.0, np.inf, -np.inf], dt), len(k))
+        if op == "PROD":
+            v = rng.uniform(0.5, 2.0, count).astype(dt)
+        return v.view(np.uint8)
+    if t == "C_FLOAT_COMPLEX":
+        v = rng.uniform(0.7, 1.4, 2 * count).astype(np.float32)
+        return v.view(np.uint8)
+    if t == "LONG_DOUBLE":
+        v = (rng.uniform(-1, 1, count) * 10.0 ** rng.uniform(-8, 8, count)).astype(np.longdouble)
+        return v.view(np.uint8).copy()
+    if t == "FLOAT_INT":
+        p = np.zeros(count, dtype=[("v", "<f4"), ("k", "<i4")])
+        p["v"] = rng.integers(0, 3, count)
+        p["k"] = rng.integers(-5, 5, count)
+        return p.view(np.uint8)
+    if t == "BOOL":
+        return rng.integers(0, 2, count * es, dtype=np.uint8)
+    return rng.integers(0, 256, count * es, dtype=np.uint8)
+
+
+def _dev(a):
+    return torch.from_numpy(np.ascontiguousarray(a)).to("cuda")
+
+
+def _stream():
+    return torch.cuda.current_stream().cuda_stream
+
+
+CASES = [("SUM", "FLOAT"), ("SUM", "DOUBLE"), ("MAX", "FLOAT"), ("MIN", "DOUBLE"), ("SUM", "INT32_T"),
+         ("PROD", "INT8_T"), ("MAXLOC", "FLOAT_INT"), ("PROD", "C_FLOAT_COMPLEX"), ("SUM", "LONG_DOUBLE"),
+         ("BXOR", "UINT16_T"), ("LAND", "BOOL")]
+ALGS = ["auto", "basic_linear", "recursive_doubling", "ring", "segmented_ring", "rabenseifner"]
+ALG_ID = {"auto": 0, "basic_linear": 1, "recursive_doubling": 3, "ring": 4, "segmented_ring": 5,
+          "rabenseifner": 6}
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _init():
+    assert torch.cuda.is_available()
+    mxompi.init(0)
+
+
+def _check_allreduce_local(n, count, op, t, alg, inplace=False, seed=0):
+    L = _oracle()
+    es = mxompi.type_size(t)
+    xs = [gen(t, op, count, seed * 100 + r) for r in range(n)]
+    exp = [np.zeros(count * es, np.uint8) for _ in range(n)]
+    sp = (vp * n)(*[x.ctypes.data for x in xs])
+    rp = (vp * n)(*[e.ctypes.data for e in exp])
+    assert L.mxo_allreduce(ALG_ID[alg], mxompi.OP[op], mxompi.TYPE[t], n, count, sp, rp) == 0
+    comm = mxompi.Comm.local(n)
+    S = [_dev(x) for x in xs]
+    R = [torch.zeros(count * es, dtype=torch.uint8, device="cuda") for _ in range(n)]
+    if inplace:
+        comm.allreduce_local([mxompi.IN_PLACE] * n, [s.data_ptr() for s in S], count, t, op, alg, _stream())
+        R = S
+    else:
+        comm.allreduce_local([s.data_ptr() for s in S], [r.data_ptr() for r in R], count, t, op, alg, _stream())
+    for r in range(n):
+        golden_io.assert_op_equal(R[r].cpu().numpy(), exp[r], mxompi.OP[op], mxompi.TYPE[t],
+                                  f"allreduce {alg} n={n} count={count} {op} {t} rank {r}")
+    comm.close()
+
+
+@pytest.mark.parametrize("alg", ALGS)
+@pytest.mark.parametrize("n", [1, 2, 3, 4, 5, 7, 8])
+@pytest.mark.parametrize("op,t", CASES)
+def test_allreduce_local_bitexact(alg, n, op, t):
+    for count in (1, 3, n, 7, 100, 1001):
+        _check_allreduce_local(n, count, op, t, alg, seed=count)
+
+
+@pytest.mark.parametrize("alg", ["ring", "rabenseifner", "recursive_doubling"])
+@pytest.mark.parametrize("n", [2, 3, 8])
+def test_allreduce_local_inplace(alg, n):
+    _check_allreduce_local(n, 4099, "SUM", "FLOAT", alg, inplace=True, seed=5)
+
+
+@pytest.mark.parametrize("n", [2, 4, 8])
+def test_allreduce_auto_segmented_large(n):
+    """auto at > n * 1 MiB selects the segmented ring (tuned :72-85)."""
+    count = (n * (1 << 20)) // 4 + 12345
+    assert mxompi.allreduce_decision(n, count, "FLOAT") == 5
+    _check_allreduce_local(n, count, "SUM", "FLOAT", "auto", seed=11)
+
+
+RS_ALGS = {"auto": 0, "recursive_halving": 2, "ring": 3}
+
+
+@pytest.mark.parametrize("alg", list(RS_ALGS))
+@pytest.mark.parametrize("n", [1, 2, 3, 4, 6, 8])
+@pytest.mark.parametrize("op,t", [("SUM", "FLOAT"), ("MAX", "DOUBLE"), ("MAXLOC", "FLOAT_INT"), ("SUM", "INT64_T")])
+@pytest.mark.parametrize("inplace", [False, True])
+def test_reduce_scatter_local_bitexact(alg, n, op, t, inplace):
+    L = _oracle()
+    es = mxompi.type_size(t)
+    rng = np.random.default_rng(n * 13 + len(op))
+    for rc in ([0] * (n - 1) + [5], [int(x) for x in rng.integers(0, 300, n)], [1000] * n):
+        total = sum(rc)
+        if total == 0:
+            continue
+        xs = [gen(t, op, total, 50 + r) for r in range(n)]
+        exp = [np.zeros(max(1, c) * es, np.uint8) for c in rc]
+        assert L.mxo_reduce_scatter(RS_ALGS[alg], mxompi.OP[op], mxompi.TYPE[t], n, (sz * n)(*rc),
+                                    (vp * n)(*[x.ctypes.data for x in xs]),
+                                    (vp * n)(*[e.ctypes.data for e in exp])) == 0
+        comm = mxompi.Comm.local(n)
+        S = [_dev(x) for x in xs]
+        if inplace:
+            comm.reduce_scatter_local(None, [s.data_ptr() for s in S], rc, t, op, alg, _stream())
+            R = S
+        else:
+            R = [torch.zeros(max(1, c) * es, dtype=torch.uint8, device="cuda") for c in rc]
+            comm.reduce_scatter_local([s.data_ptr() for s in S], [r.data_ptr() for r in R], rc, t, op, alg,
+                                      _stream())
+        for r in range(n):
+            got = R[r].cpu().numpy()[: rc[r] * es]
+            golden_io.assert_op_equal(got, exp[r][: rc[r] * es], mxompi.OP[op], mxompi.TYPE[t],
+                                      f"reduce_scatter {alg} n={n} rc={rc} rank {r}")
+        comm.close()
+
+
+@pytest.mark.parametrize("n", [1, 2, 3, 8])
+@pytest.mark.parametrize("nbytes", [1, 13, 4096, 100003])
+def test_allgather_and_bcast_local(n, nbytes):
+    rng = np.random.default_rng(nbytes + n)
+    xs = [rng.integers(0, 256, nbytes, dtype=np.uint8) for _ in range(n)]
+    comm = mxompi.Comm.local(n)
+    S = [_dev(x) for x in xs]
+    R = [torch.zeros(n * nbytes, dtype=torch.uint8, device="cuda") for _ in range(n)]
+    comm.allgather_local([s.data_ptr() for s in S], [r.data_ptr() for r in R], nbytes, _stream())
+    full = np.concatenate(xs)
+    for r in range(n):
+        np.testing.assert_array_equal(R[r].cpu().numpy(), full)
+    root = n - 1
+    comm.bcast_local([s.data_ptr() for s in S], nbytes, root, _stream())
+    for r in range(n):
+        np.testing.assert_array_equal(S[r].cpu().numpy(), xs[root])
+    comm.close()
+
+
+# ---------------------------------------------------------------------------
+# multi-process: n processes on the one GPU, IPC staging + flags
+# ---------------------------------------------------------------------------
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _mp_worker(rank, n, port, staging, jobs, q):
+    import torch.distributed as dist
+    os.environ["HSA_ENABLE_IPC_MODE_LEGACY"] = "0"
+    try:
+        dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=n)
+        torch.cuda.set_device(0)
+        mxompi.init(0)
+
+        def ag(b):
+            out = [None] * n
+            dist.all_gather_object(out, b)
+            return out
+
+        comm = mxompi.Comm(rank, n, ag, device=0, staging_bytes=staging)
+        comm.set_timeout(30.0)
+        results = []
+        st = torch.cuda.current_stream().cuda_stream
+        for kind, count, op, t, alg in jobs:
+            es = mxompi.type_size(t)
+            if kind == "allreduce":
+                x = _dev(gen(t, op, count, 7000 + rank))
+                out = torch.zeros(count * es, dtype=torch.uint8, device="cuda")
+                comm.allreduce(x.data_ptr(), out.data_ptr(), count, t, op, alg, st)
+                results.append(out.cpu().numpy().tobytes())
+            elif kind == "allreduce_inplace":
+                x = _dev(gen(t, op, count, 7000 + rank))
+                comm.allreduce(mxompi.IN_PLACE, x.data_ptr(), count, t, op, alg, st)
+                results.append(x.cpu().numpy().tobytes())
+            elif kind == "reduce_scatter":
+                rc = [count + 3 * r for r in range(n)]
+                x = _dev(gen(t, op, sum(rc), 7000 + rank))
+                out = torch.zeros(rc[rank] * es + 1, dtype=torch.uint8, device="cuda")
+                comm.reduce_scatter(x.data_ptr(), out.data_ptr(), rc, t, op, alg, st)
+                results.append(out.cpu().numpy()[: rc[rank] * es].tobytes())
+            elif kind == "allgather":
+                x = _dev(gen("UINT8_T", "BAND", count, 7000 + rank))
+                out = torch.zeros(n * count, dtype=torch.uint8, device="cuda")
+                comm.allgather(x.data_ptr(), out.data_ptr(), count, st)
+                results.append(out.cpu().numpy().tobytes())
+            elif kind == "bcast":
+                x = _dev(gen("UINT8_T", "BAND", count, 7000 + rank))
+                comm.bcast(x.data_ptr(), count, n - 1, st)
+                results.append(x.cpu().numpy().tobytes())
+        comm.close()
+        dist.destroy_process_group()
+        q.put((rank, "ok", results))
+    except Exception as e:  # noqa: BLE001
+        import traceback
+        q.put((rank, "err", traceback.format_exc() + str(e)))
+
+
+def _run_mp(n, jobs, staging=1 << 20):
+    import torch.multiprocessing as mp
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_mp_worker, args=(r, n, port, staging, jobs, q)) for r in range(n)]
+    for p in procs:
+        p.start()
+    out = {}
+    for _ in range(n):
+        rank, status, payload = q.get(timeout=300)
+        assert status == "ok", payload
+        out[rank] = payload
+    for p in procs:
+        p.join(timeout=60)
+    return out
+
+
+@pytest.mark.parametrize("n", [2, 3, 4])
+def test_multiprocess_ipc_bitexact(n):
+    L = _oracle()
+    jobs = [("allreduce", 100003, "SUM", "FLOAT", "auto"),          # > staging: chunked
+            ("allreduce", 777, "MAX", "DOUBLE", "rabenseifner"),
+            ("allreduce", 5, "SUM", "FLOAT", "recursive_doubling"),
+            ("allreduce_inplace", 4099, "SUM", "DOUBLE", "ring"),
+            ("allreduce", 3001, "MAXLOC", "FLOAT_INT", "auto"),
+            ("reduce_scatter", 1000, "SUM", "FLOAT", "ring"),
+            ("reduce_scatter", 10, "SUM", "DOUBLE", "recursive_halving"),
+            ("allgather", 300001, None, None, None),
+            ("bcast", 2000003, None, None, None)]
+    jobs = [(k, c, o or "BAND", t or "UINT8_T", a or "auto") for k, c, o, t, a in jobs]
+    got = _run_mp(n, jobs)
+    for j, (kind, count, op, t, alg) in enumerate(jobs):
+        es = mxompi.type_size(t)
+        if kind.startswith("allreduce"):
+            xs = [gen(t, op, count, 7000 + r) for r in range(n)]
+            exp = [np.zeros(count * es, np.uint8) for _ in range(n)]
+            assert L.mxo_allreduce(ALG_ID[alg], mxompi.OP[op], mxompi.TYPE[t], n, count,
+                                   (vp * n)(*[x.ctypes.data for x in xs]),
+                                   (vp * n)(*[e.ctypes.data for e in exp])) == 0
+            for r in range(n):
+                golden_io.assert_op_equal(np.frombuffer(got[r][j], np.uint8), exp[r], mxompi.OP[op],
+                                          mxompi.TYPE[t], f"{kind} {alg} rank {r}")
+        elif kind == "reduce_scatter":
+            rc = [count + 3 * r for r in range(n)]
+            xs = [gen(t, op, sum(rc), 7000 + r) for r in range(n)]
+            exp = [np.zeros(c * es, np.uint8) for c in rc]
+            assert L.mxo_reduce_scatter({"ring": 3, "recursive_halving": 2}[alg], mxompi.OP[op], mxompi.TYPE[t],
+                                        n, (sz * n)(*rc), (vp * n)(*[x.ctypes.data for x in xs]),
+                                        (vp * n)(*[e.ctypes.data for e in exp])) == 0
+            for r in range(n):
+                golden_io.assert_op_equal(np.frombuffer(got[r][j], np.uint8), exp[r], mxompi.OP[op],
+                                          mxompi.TYPE[t], f"reduce_scatter {alg} rank {r}")
+        elif kind == "allgather":
+            full = np.concatenate([gen("UINT8_T", "BAND", count, 7000 + r) for r in range(n)])
+            for r in range(n):
+                np.testing.assert_array_equal(np.frombuffer(got[r][j], np.uint8), full)
+        elif kind == "bcast":
+            root = gen("UINT8_T", "BAND", count, 7000 + n - 1)
+            for r in range(n):
+                np.testing.assert_array_equal(np.frombuffer(got[r][j], np.uint8), root)

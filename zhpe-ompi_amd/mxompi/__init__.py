@@ -157,3 +157,151 @@ def init(device: int = 0) -> None:
 
 def sync(stream: int = 0) -> None:
     check(lib().mx_stream_sync(stream or None), "mx_stream_sync")
+
+
+# ---------------------------------------------------------------------------
+# collectives (include/mx_coll.h)
+# ---------------------------------------------------------------------------
+IN_PLACE = 1                       # MX_IN_PLACE
+COMM_IPC, COMM_RCCL = 1, 2
+ALLREDUCE = {"auto": 0, "basic_linear": 1, "nonoverlapping": 2, "recursive_doubling": 3,
+             "ring": 4, "segmented_ring": 5, "rabenseifner": 6, "rccl": 100}
+REDUCE_SCATTER = {"auto": 0, "nonoverlapping": 1, "recursive_halving": 2, "ring": 3, "rccl": 100}
+
+_AG_FN = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p)
+
+
+def _coll_lib():
+    L = lib()
+    if not getattr(L, "_mx_coll_typed", False):
+        vp, sz, i = ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int
+        pp = ctypes.POINTER(ctypes.c_void_p)
+        L.mx_comm_create.argtypes = [i, i, i, sz, i, _AG_FN, vp, ctypes.POINTER(vp)]
+        L.mx_comm_create_local.argtypes = [i, i, ctypes.POINTER(vp)]
+        L.mx_comm_destroy.argtypes = [vp]
+        L.mx_comm_set_timeout.argtypes = [vp, ctypes.c_double]
+        L.mx_allreduce.argtypes = [vp, vp, vp, sz, i, i, i, vp]
+        L.mx_allreduce_local.argtypes = [vp, pp, pp, sz, i, i, i, vp]
+        L.mx_reduce_scatter.argtypes = [vp, vp, vp, ctypes.POINTER(sz), i, i, i, vp]
+        L.mx_reduce_scatter_local.argtypes = [vp, pp, pp, ctypes.POINTER(sz), i, i, i, vp]
+        L.mx_allgather.argtypes = [vp, vp, vp, sz, vp]
+        L.mx_allgather_local.argtypes = [vp, pp, pp, sz, vp]
+        L.mx_bcast.argtypes = [vp, vp, sz, i, vp]
+        L.mx_bcast_local.argtypes = [vp, pp, sz, i, vp]
+        L.mx_allreduce_decision.argtypes = [i, sz, i]
+        L.mx_reduce_scatter_decision.argtypes = [i, sz, i]
+        L._mx_coll_typed = True
+    return L
+
+
+def _ptrs(seq):
+    arr = (ctypes.c_void_p * len(seq))()
+    for k, p in enumerate(seq):
+        arr[k] = p
+    return arr
+
+
+def _alg(table, a):
+    return table[a] if isinstance(a, str) else int(a)
+
+
+class Comm:
+    """A communicator of the MI355X collective path.
+
+    Comm.local(size): `size` virtual ranks in this process (one device).
+    Comm(rank, size, allgather): one rank per process; `allgather(bytes) ->
+    list[bytes]` is the host bootstrap exchange (e.g. torch.distributed)."""
+
+    def __init__(self, rank=0, size=1, allgather=None, device=0, staging_bytes=64 << 20,
+                 flags=COMM_IPC, _handle=None):
+        L = _coll_lib()
+        self.size = size
+        self.rank = rank
+        self._cb = None
+        if _handle is not None:
+            self.h = _handle
+            return
+        if allgather is None:
+            raise ValueError("a host allgather is required for a multi-process communicator")
+
+        def _ag(send, recv, nbytes, ctx):
+            try:
+                parts = allgather(ctypes.string_at(send, nbytes))
+                blob = b"".join(parts)
+                ctypes.memmove(recv, blob, len(blob))
+                return 0
+            except Exception:  # noqa: BLE001 - reported as a C error code
+                import traceback
+                traceback.print_exc()
+                return -1
+
+        self._cb = _AG_FN(_ag)
+        h = ctypes.c_void_p()
+        check(L.mx_comm_create(rank, size, device, staging_bytes, flags, self._cb, None, ctypes.byref(h)),
+              "mx_comm_create")
+        self.h = h
+
+    @classmethod
+    def local(cls, size, device=0):
+        h = ctypes.c_void_p()
+        check(_coll_lib().mx_comm_create_local(size, device, ctypes.byref(h)), "mx_comm_create_local")
+        return cls(0, size, _handle=h)
+
+    def set_timeout(self, seconds):
+        check(_coll_lib().mx_comm_set_timeout(self.h, seconds), "mx_comm_set_timeout")
+
+    def close(self):
+        if getattr(self, "h", None):
+            _coll_lib().mx_comm_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:  # noqa: BLE001
+            pass
+
+    # -- multi-process -----------------------------------------------------
+    def allreduce(self, sbuf, rbuf, count, t, op, alg="auto", stream=0):
+        check(_coll_lib().mx_allreduce(self.h, sbuf, rbuf, count, _slot(t), _op(op),
+                                       _alg(ALLREDUCE, alg), stream or None), "mx_allreduce")
+
+    def reduce_scatter(self, sbuf, rbuf, rcounts, t, op, alg="auto", stream=0):
+        rc = (ctypes.c_size_t * len(rcounts))(*rcounts)
+        check(_coll_lib().mx_reduce_scatter(self.h, sbuf, rbuf, rc, _slot(t), _op(op),
+                                            _alg(REDUCE_SCATTER, alg), stream or None), "mx_reduce_scatter")
+
+    def allgather(self, sbuf, rbuf, nbytes, stream=0):
+        check(_coll_lib().mx_allgather(self.h, sbuf, rbuf, nbytes, stream or None), "mx_allgather")
+
+    def bcast(self, buf, nbytes, root, stream=0):
+        check(_coll_lib().mx_bcast(self.h, buf, nbytes, root, stream or None), "mx_bcast")
+
+    # -- local (all ranks in this process) ---------------------------------
+    def allreduce_local(self, sbufs, rbufs, count, t, op, alg="auto", stream=0):
+        sp = _ptrs(sbufs) if sbufs is not None else None
+        check(_coll_lib().mx_allreduce_local(self.h, sp, _ptrs(rbufs), count, _slot(t), _op(op),
+                                             _alg(ALLREDUCE, alg), stream or None), "mx_allreduce_local")
+
+    def reduce_scatter_local(self, sbufs, rbufs, rcounts, t, op, alg="auto", stream=0):
+        rc = (ctypes.c_size_t * len(rcounts))(*rcounts)
+        sp = _ptrs(sbufs) if sbufs is not None else None
+        check(_coll_lib().mx_reduce_scatter_local(self.h, sp, _ptrs(rbufs), rc, _slot(t), _op(op),
+                                                  _alg(REDUCE_SCATTER, alg), stream or None),
+              "mx_reduce_scatter_local")
+
+    def allgather_local(self, sbufs, rbufs, nbytes, stream=0):
+        sp = _ptrs(sbufs) if sbufs is not None else None
+        check(_coll_lib().mx_allgather_local(self.h, sp, _ptrs(rbufs), nbytes, stream or None),
+              "mx_allgather_local")
+
+    def bcast_local(self, bufs, nbytes, root, stream=0):
+        check(_coll_lib().mx_bcast_local(self.h, _ptrs(bufs), nbytes, root, stream or None), "mx_bcast_local")
+
+
+def allreduce_decision(n, count, t):
+    return int(_coll_lib().mx_allreduce_decision(n, count, _slot(t)))
+
+
+def reduce_scatter_decision(n, total, t):
+    return int(_coll_lib().mx_reduce_scatter_decision(n, total, _slot(t)))
