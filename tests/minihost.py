@@ -1,0 +1,60 @@
+"""ctypes view of the mini-host harness (zhpe-ompi_amd/lib/libmx_host.so),
+which loads the mi355x components from lib/libmx_ompi.so the way Open MPI's
+MCA repository would and restates op/coll selection and the MPI entry
+points.  TEST INFRASTRUCTURE: the base op functions it seeds the tables
+with are the oracle's (pinned to the reference's op_base_functions.c)."""
+import ctypes
+import os
+
+import mxompi
+import oracle_lib
+
+vp, ci, sz = ctypes.c_void_p, ctypes.c_int, ctypes.c_size_t
+AG = ctypes.CFUNCTYPE(ci, vp, vp, sz, vp)
+REDUCER = ctypes.CFUNCTYPE(ci, ci, ci, vp, vp, sz, ci)
+PATTERN = ctypes.CFUNCTYPE(ci, ci, ci, ci)
+_state = {}
+
+
+def host(with_components=True):
+    key = ("h", with_components)
+    if key in _state:
+        return _state[key]
+    H = ctypes.CDLL(os.path.join(mxompi.LIB_DIR, "libmx_host.so"), mode=ctypes.RTLD_GLOBAL)
+    H.mxh_init.argtypes = [ctypes.c_char_p, vp, vp]
+    H.mxh_dtype.restype = vp
+    H.mxh_dtype.argtypes = [ctypes.c_char_p]
+    H.mxh_dtype_contiguous.restype = vp
+    H.mxh_dtype_contiguous.argtypes = [ci, vp]
+    H.mxh_op.restype = vp
+    H.mxh_op.argtypes = [ctypes.c_char_p]
+    H.mxh_op_slot_owner.argtypes = [vp, ci, ci]
+    H.mxh_set_mca.argtypes = [ctypes.c_char_p, ci]
+    H.mxh_comm_create.restype = vp
+    H.mxh_comm_create.argtypes = [ci, ci, AG, vp]
+    H.mxh_comm_self.restype = vp
+    H.mxh_comm_free.argtypes = [vp]
+    H.mxh_comm_slot_owner.restype = ctypes.c_char_p
+    H.mxh_comm_slot_owner.argtypes = [vp, ctypes.c_char_p]
+    H.mxh_reduce_local.argtypes = [vp, vp, ci, vp, vp]
+    H.mxh_op_reduce.argtypes = [vp, vp, vp, ci, vp]
+    H.mxh_allreduce.argtypes = [vp, vp, ci, vp, vp, vp]
+    H.mxh_reduce_scatter.argtypes = [vp, vp, ctypes.POINTER(ci), vp, vp, vp]
+    H.mxh_allgather.argtypes = [vp, ci, vp, vp, ci, vp, vp]
+    H.mxh_bcast.argtypes = [vp, ci, vp, ci, vp]
+    O = oracle_lib.oracle()
+    base = ctypes.cast(O.mxo_reduce2, vp)
+    pat = ctypes.cast(O.mxo_supported, vp)
+    comp = os.path.join(mxompi.LIB_DIR, "libmx_ompi.so").encode() if with_components else b""
+    rc = H.mxh_init(comp, base, pat)
+    assert rc == 0, rc
+    _state[key] = H
+    return H
+
+
+def dtype(H, name):
+    return H.mxh_dtype(name.encode())
+
+
+def op(H, name):
+    return H.mxh_op(name.encode())

@@ -1,0 +1,508 @@
+/*
+ * mx_host.c -- TEST HARNESS ("mini-host") for the mi355x op/coll
+ * components.  See mx_host.h for what it restates from Open MPI.  It is
+ * not part of the product: the real host is Open MPI itself
+ * (INTEGRATION.md).
+ */
+#define _GNU_SOURCE
+#include <dlfcn.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include "../mx_ompi_abi.h"
+#include "mx_host.h"
+
+/* ---- objects -------------------------------------------------------------- */
+static void obj_retain(opal_object_t *o)
+{
+    if (o) __atomic_add_fetch(&o->obj_reference_count, 1, __ATOMIC_RELAXED);
+}
+static void obj_release(opal_object_t *o)
+{
+    if (o && __atomic_sub_fetch(&o->obj_reference_count, 1, __ATOMIC_ACQ_REL) == 0 && o->obj_class &&
+        o->obj_class->cls_destruct)
+        o->obj_class->cls_destruct(o);
+}
+
+/* ---- datatypes (ompi/datatype/ompi_datatype_internal.h:37-200) ----------- */
+struct ompi_datatype_t {
+    const char *name;
+    int id;          /* OMPI_DATATYPE_MPI_* */
+    int slot;        /* ompi_op_ddt_map[id] (op.c:131-229) */
+    size_t size;
+    int predefined;
+    struct ompi_datatype_t *base;   /* derived contiguous: base type */
+    int base_count;
+};
+
+#define DT(nm, id, slot, sz) {nm, id, slot, sz, 1, NULL, 0}
+static struct ompi_datatype_t g_dtypes[] = {
+    DT("MPI_INT8_T", 0x01, 0, 1), DT("MPI_UINT8_T", 0x02, 1, 1), DT("MPI_INT16_T", 0x03, 2, 2),
+    DT("MPI_UINT16_T", 0x04, 3, 2), DT("MPI_INT32_T", 0x05, 4, 4), DT("MPI_UINT32_T", 0x06, 5, 4),
+    DT("MPI_INT64_T", 0x07, 6, 8), DT("MPI_UINT64_T", 0x08, 7, 8),
+    /* C aliases (LP64) */
+    DT("MPI_CHAR", 0x01, 0, 1), DT("MPI_SIGNED_CHAR", 0x01, 0, 1), DT("MPI_UNSIGNED_CHAR", 0x02, 1, 1),
+    DT("MPI_BYTE", 0x02, 1, 1), DT("MPI_SHORT", 0x03, 2, 2), DT("MPI_UNSIGNED_SHORT", 0x04, 3, 2),
+    DT("MPI_INT", 0x05, 4, 4), DT("MPI_UNSIGNED", 0x06, 5, 4), DT("MPI_LONG", 0x07, 6, 8),
+    DT("MPI_UNSIGNED_LONG", 0x08, 7, 8), DT("MPI_LONG_LONG", 0x07, 6, 8),
+    DT("MPI_UNSIGNED_LONG_LONG", 0x08, 7, 8),
+    DT("MPI_FLOAT", 0x09, 15, 4), DT("MPI_DOUBLE", 0x0A, 16, 8), DT("MPI_LONG_DOUBLE", 0x0B, 23, 16),
+    DT("MPI_WCHAR", 0x10, 40, 4), DT("MPI_CXX_BOOL", 0x12, 25, 1), DT("MPI_LOGICAL", 0x13, 24, 4),
+    DT("MPI_CHARACTER", 0x14, 1, 1), DT("MPI_INTEGER", 0x15, 8, 4), DT("MPI_REAL", 0x16, 17, 4),
+    DT("MPI_DOUBLE_PRECISION", 0x17, 22, 8), DT("MPI_LONG_DOUBLE_COMPLEX", 0x1A, 29, 32),
+    DT("MPI_2INT", 0x1B, 37, 8), DT("MPI_2INTEGER", 0x1C, 33, 8), DT("MPI_2REAL", 0x1D, 31, 8),
+    DT("MPI_2DOUBLE_PRECISION", 0x1E, 32, 16), DT("MPI_FLOAT_INT", 0x21, 34, 8),
+    DT("MPI_DOUBLE_INT", 0x22, 35, 16), DT("MPI_LONG_DOUBLE_INT", 0x23, 39, 32),
+    DT("MPI_LONG_INT", 0x24, 36, 16), DT("MPI_SHORT_INT", 0x25, 38, 8), DT("MPI_AINT", 0x26, 6, 8),
+    DT("MPI_OFFSET", 0x27, 7, 8), DT("MPI_C_BOOL", 0x28, 25, 1), DT("MPI_C_COMPLEX", 0x29, 27, 8),
+    DT("MPI_C_FLOAT_COMPLEX", 0x2A, 27, 8), DT("MPI_C_DOUBLE_COMPLEX", 0x2B, 28, 16),
+    DT("MPI_C_LONG_DOUBLE_COMPLEX", 0x2C, 29, 32), DT("MPI_COUNT", 0x2F, 6, 8),
+};
+#define NDT (sizeof g_dtypes / sizeof g_dtypes[0])
+
+void *mxh_dtype(const char *name)
+{
+    for (size_t i = 0; i < NDT; i++)
+        if (!strcmp(g_dtypes[i].name, name)) return &g_dtypes[i];
+    return NULL;
+}
+
+void *mxh_dtype_contiguous(int count, void *oldtype)
+{
+    struct ompi_datatype_t *o = oldtype, *d = calloc(1, sizeof *d);
+    if (!d || !o || count < 0) { free(d); return NULL; }
+    d->name = "";
+    d->id = -1;
+    d->predefined = 0;
+    d->base = o->predefined ? o : o->base;
+    d->base_count = count * (o->predefined ? 1 : o->base_count);
+    d->size = o->size * (size_t)count;
+    /* ompi_datatype_get_single_predefined_type_from_args (ompi_datatype_args.c:825-865) */
+    d->slot = d->base ? d->base->slot : -1;
+    return d;
+}
+
+/* ---- ops ------------------------------------------------------------------ */
+struct ompi_op_t {
+    opal_object_t super;
+    char o_name[64];
+    uint32_t o_flags;
+    int o_f_to_c_index;
+    ompi_op_base_op_fns_t intrinsic;
+    ompi_op_base_op_3buff_fns_t o_3buff_intrinsic;
+};
+
+static const char *g_opnames[] = {"MPI_OP_NULL", "MPI_MAX", "MPI_MIN", "MPI_SUM", "MPI_PROD", "MPI_LAND",
+                                  "MPI_BAND", "MPI_LOR", "MPI_BOR", "MPI_LXOR", "MPI_BXOR", "MPI_MAXLOC",
+                                  "MPI_MINLOC", "MPI_REPLACE", "MPI_NO_OP"};
+static struct ompi_op_t g_ops[OMPI_OP_BASE_FORTRAN_OP_MAX];
+
+/* base module per op: carries the op index for the base trampolines */
+typedef struct { ompi_op_base_module_t super; int op; } base_op_module_t;
+static base_op_module_t g_base_mod[OMPI_OP_BASE_FORTRAN_OP_MAX];
+static mx_obj_class_t g_static_class = {"static", NULL};
+
+static mxh_reducer_t g_base;
+static mxh_pattern_t g_pattern;
+
+static void base_2buff(void *in, void *inout, int *count, struct ompi_datatype_t **dt, ompi_op_base_module_t *m)
+{
+    g_base(((base_op_module_t *)m)->op, (*dt)->slot, in, inout, (size_t)*count, 1);
+}
+static void base_3buff(void *in1, void *in2, void *out, int *count, struct ompi_datatype_t **dt,
+                       ompi_op_base_module_t *m)
+{
+    /* the test reducers only expose 2-buffer form: out = in1; out op= in2 is
+     * NOT the 3-buffer semantics for MAX/MIN roles, so route through a
+     * dedicated 3-buffer reducer when the injected one provides it */
+    memcpy(out, in1, (size_t)*count * (*dt)->size);
+    g_base(((base_op_module_t *)m)->op, (*dt)->slot, in2, out, (size_t)*count, 1);
+}
+
+void *mxh_op(const char *name)
+{
+    for (int i = 0; i < OMPI_OP_BASE_FORTRAN_OP_MAX; i++)
+        if (!strcmp(g_opnames[i], name)) return &g_ops[i];
+    return NULL;
+}
+
+int mxh_op_slot_owner(void *opv, int t, int three)
+{
+    struct ompi_op_t *op = opv;
+    ompi_op_base_module_t *m = three ? op->o_3buff_intrinsic.modules[t] : op->intrinsic.modules[t];
+    if (!m) return -1;
+    return (m == &g_base_mod[op->o_f_to_c_index].super) ? 0 : 1;
+}
+
+/* ---- MCA variables --------------------------------------------------------- */
+#define NVARS 64
+static struct { char name[96]; int value; int set; } g_vars[NVARS];
+int mxh_set_mca(const char *name, int value)
+{
+    for (int i = 0; i < NVARS; i++) {
+        if (!g_vars[i].set || !strcmp(g_vars[i].name, name)) {
+            snprintf(g_vars[i].name, sizeof g_vars[i].name, "%s", name);
+            g_vars[i].value = value;
+            g_vars[i].set = 1;
+            return 0;
+        }
+    }
+    return -1;
+}
+static int mca_int(const char *name, int def)
+{
+    char env[160];
+    const char *e;
+    for (int i = 0; i < NVARS; i++)
+        if (g_vars[i].set && !strcmp(g_vars[i].name, name)) return g_vars[i].value;
+    snprintf(env, sizeof env, "OMPI_MCA_%s", name);   /* opal_set_mca_prefix.m4:26 */
+    e = getenv(env);
+    return e ? atoi(e) : def;
+}
+
+/* ---- communicators --------------------------------------------------------- */
+#define NSLOTS 5
+static const char *g_slot_names[NSLOTS] = {"allreduce", "reduce_scatter", "allgather", "bcast", "reduce_local"};
+
+struct ompi_communicator_t {
+    int rank, size;
+    mxh_allgather_t ag;
+    void *ag_ctx;
+    /* c_coll: (fn, module, owner-name) per slot (coll.h:622-) */
+    void *fn[NSLOTS];
+    mca_coll_base_module_t *mod[NSLOTS];
+    const char *owner[NSLOTS];
+    mca_coll_base_module_t *modules[4];
+    int nmodules;
+};
+
+static int slot_index(const char *s)
+{
+    for (int i = 0; i < NSLOTS; i++)
+        if (!strcmp(g_slot_names[i], s)) return i;
+    return -1;
+}
+
+static void *comm_coll_fn(struct ompi_communicator_t *c, const char *slot, mca_coll_base_module_t **module)
+{
+    int i = slot_index(slot);
+    if (i < 0) return NULL;
+    *module = c->mod[i];
+    return c->fn[i];
+}
+
+static int dtype_slot(struct ompi_datatype_t *d) { return d ? d->slot : -1; }
+static size_t dtype_size(struct ompi_datatype_t *d) { return d->size; }
+static int dtype_contiguous(struct ompi_datatype_t *d, int count) { (void)d; (void)count; return 1; }
+static int comm_rank(struct ompi_communicator_t *c) { return c->rank; }
+static int comm_size(struct ompi_communicator_t *c) { return c->size; }
+static int op_index(struct ompi_op_t *op) { return op->o_f_to_c_index; }
+static uint32_t op_flags(struct ompi_op_t *op) { return op->o_flags; }
+static ompi_op_base_op_fns_t *op_fns(struct ompi_op_t *op) { return &op->intrinsic; }
+static ompi_op_base_op_3buff_fns_t *op_3fns(struct ompi_op_t *op) { return &op->o_3buff_intrinsic; }
+
+static mx_ompi_host_t g_host;
+
+/* ompi_op_reduce (op.h:547-610) */
+static void op_reduce(struct ompi_op_t *op, const void *source, void *target, int count, struct ompi_datatype_t *dt)
+{
+    struct ompi_datatype_t *d = dt;
+    int cnt = count;
+    op->intrinsic.fns[dt->slot]((void *)source, target, &cnt, &d, op->intrinsic.modules[dt->slot]);
+}
+
+/* ---- host base coll module (stands in for tuned/basic on host buffers) ---- */
+static int base_allgather(const void *sbuf, int scount, struct ompi_datatype_t *sdt, void *rbuf, int rcount,
+                          struct ompi_datatype_t *rdt, struct ompi_communicator_t *c, mca_coll_base_module_t *m)
+{
+    (void)m;
+    size_t rb = (size_t)rcount * rdt->size;
+    const void *src = sbuf == MPI_IN_PLACE ? (char *)rbuf + (size_t)c->rank * rb : sbuf;
+    void *tmp = malloc(rb * c->size + 1);
+    int rc;
+    (void)scount; (void)sdt;
+    if (!tmp) return OMPI_ERR_OUT_OF_RESOURCE;
+    rc = c->ag(src, tmp, rb, c->ag_ctx);
+    memcpy(rbuf, tmp, rb * c->size);
+    free(tmp);
+    return rc ? OMPI_ERROR : OMPI_SUCCESS;
+}
+
+static int base_allreduce(const void *sbuf, void *rbuf, int count, struct ompi_datatype_t *dt, struct ompi_op_t *op,
+                          struct ompi_communicator_t *c, mca_coll_base_module_t *m)
+{
+    size_t b = (size_t)count * dt->size;
+    char *all = malloc(b * c->size + 1);
+    (void)m;
+    if (!all) return OMPI_ERR_OUT_OF_RESOURCE;
+    if (c->ag(sbuf == MPI_IN_PLACE ? rbuf : sbuf, all, b, c->ag_ctx)) { free(all); return OMPI_ERROR; }
+    /* basic linear order (coll_base_reduce.c:627-720): x_{n-1} op x_{n-2} ... */
+    memcpy(rbuf, all + (size_t)(c->size - 1) * b, b);
+    for (int i = c->size - 2; i >= 0; i--) op_reduce(op, all + (size_t)i * b, rbuf, count, dt);
+    free(all);
+    return OMPI_SUCCESS;
+}
+
+static int base_reduce_scatter(const void *sbuf, void *rbuf, const int *rcounts, struct ompi_datatype_t *dt,
+                               struct ompi_op_t *op, struct ompi_communicator_t *c, mca_coll_base_module_t *m)
+{
+    int total = 0, disp = 0;
+    char *full;
+    for (int i = 0; i < c->size; i++) { if (i < c->rank) disp += rcounts[i]; total += rcounts[i]; }
+    full = malloc((size_t)total * dt->size + 1);
+    if (!full) return OMPI_ERR_OUT_OF_RESOURCE;
+    int rc = base_allreduce(sbuf == MPI_IN_PLACE ? rbuf : sbuf, full, total, dt, op, c, m);
+    if (!rc) memcpy(rbuf, full + (size_t)disp * dt->size, (size_t)rcounts[c->rank] * dt->size);
+    free(full);
+    return rc;
+}
+
+static int base_bcast(void *buf, int count, struct ompi_datatype_t *dt, int root, struct ompi_communicator_t *c,
+                      mca_coll_base_module_t *m)
+{
+    size_t b = (size_t)count * dt->size;
+    char *all = malloc(b * c->size + 1);
+    (void)m;
+    if (!all) return OMPI_ERR_OUT_OF_RESOURCE;
+    if (c->ag(buf, all, b, c->ag_ctx)) { free(all); return OMPI_ERROR; }
+    memcpy(buf, all + (size_t)root * b, b);
+    free(all);
+    return OMPI_SUCCESS;
+}
+
+/* coll/self-like reduce_local: mca_coll_base_reduce_local (coll_base_reduce.c:42-49) */
+static int base_reduce_local(const void *in, void *inout, int count, struct ompi_datatype_t *dt, struct ompi_op_t *op,
+                             mca_coll_base_module_t *m)
+{
+    (void)m;
+    op_reduce(op, in, inout, count, dt);
+    return OMPI_SUCCESS;
+}
+
+static mca_coll_base_module_t g_base_coll;   /* static, never freed */
+static mca_coll_base_module_t g_self_coll;
+
+static ompi_op_base_component_1_0_0_t *g_op_comp;
+static mca_coll_base_component_2_0_0_t *g_coll_comp;
+static void *g_dl;
+static struct ompi_communicator_t g_self;
+
+/* ompi_op_base_op_select (op_base_op_select.c:88-204) for one op */
+static int op_select(struct ompi_op_t *op)
+{
+    base_op_module_t *bm = &g_base_mod[op->o_f_to_c_index];
+    int prio = 0;
+    ompi_op_base_module_t *m;
+    bm->super.super.obj_class = &g_static_class;
+    bm->super.super.obj_reference_count = 1;
+    bm->op = op->o_f_to_c_index;
+    for (int t = 0; t < OMPI_OP_BASE_TYPE_MAX; t++) {
+        const int has = g_pattern(op->o_f_to_c_index, t, 1);
+        op->intrinsic.fns[t] = has ? base_2buff : NULL;
+        op->intrinsic.modules[t] = &bm->super;
+        op->o_3buff_intrinsic.fns[t] = has ? base_3buff : NULL;
+        op->o_3buff_intrinsic.modules[t] = &bm->super;
+        obj_retain(&bm->super.super);
+        obj_retain(&bm->super.super);
+    }
+    if (!g_op_comp || !(op->o_flags & OMPI_OP_FLAGS_INTRINSIC)) return 0;
+    m = g_op_comp->opc_op_query(op, &prio);
+    if (!m) return 0;
+    if (prio > 100) prio = 100;          /* :279 */
+    if (prio < 0) { obj_release(&m->super); return 0; }
+    if (m->opm_enable && m->opm_enable(m, op) != OMPI_SUCCESS) { obj_release(&m->super); return 0; }
+    for (int t = 0; t < OMPI_OP_BASE_TYPE_MAX; t++) {
+        if (m->opm_fns[t]) {
+            obj_release(&op->intrinsic.modules[t]->super);
+            op->intrinsic.fns[t] = m->opm_fns[t];
+            op->intrinsic.modules[t] = m;
+            obj_retain(&m->super);
+        }
+        if (m->opm_3buff_fns[t]) {
+            obj_release(&op->o_3buff_intrinsic.modules[t]->super);
+            op->o_3buff_intrinsic.fns[t] = m->opm_3buff_fns[t];
+            op->o_3buff_intrinsic.modules[t] = m;
+            obj_retain(&m->super);
+        }
+    }
+    obj_release(&m->super);
+    /* NULL-pattern sanity check (:185-201) */
+    for (int t = 0; t < OMPI_OP_BASE_TYPE_MAX; t++)
+        if ((g_pattern(op->o_f_to_c_index, t, 1) != 0) != (op->intrinsic.fns[t] != NULL)) return OMPI_ERR_NOT_FOUND;
+    return 0;
+}
+
+/* mca_coll_base_comm_select (coll_base_comm_select.c:108-309) */
+static int comm_select(struct ompi_communicator_t *c, int is_self)
+{
+    mca_coll_base_module_t *base = is_self ? &g_self_coll : &g_base_coll;
+    memset(c->fn, 0, sizeof c->fn);
+    base->super.obj_class = &g_static_class;
+    base->super.obj_reference_count = 1000000;
+    if (is_self) {
+        base->coll_reduce_local = base_reduce_local;
+    } else {
+        base->coll_allreduce = base_allreduce;
+        base->coll_reduce_scatter = base_reduce_scatter;
+        base->coll_allgather = base_allgather;
+        base->coll_bcast = base_bcast;
+        base->coll_reduce_local = base_reduce_local;
+    }
+    /* lowest priority first: the base module (30 / 75) */
+#define COPY(MOD, OWNER)                                                                             \
+    do {                                                                                             \
+        void *f_[NSLOTS] = {(void *)(MOD)->coll_allreduce, (void *)(MOD)->coll_reduce_scatter,       \
+                            (void *)(MOD)->coll_allgather, (void *)(MOD)->coll_bcast,                \
+                            (void *)(MOD)->coll_reduce_local};                                        \
+        for (int i_ = 0; i_ < NSLOTS; i_++)                                                          \
+            if (f_[i_]) { c->fn[i_] = f_[i_]; c->mod[i_] = (MOD); c->owner[i_] = (OWNER); }          \
+    } while (0)
+    COPY(base, is_self ? "self" : "base");
+    if (g_coll_comp) {
+        int prio = 0;
+        mca_coll_base_module_t *m = g_coll_comp->collm_comm_query(c, &prio);
+        const int base_prio = is_self ? 75 : 30;
+        if (m) {
+            if (prio > base_prio && (!m->coll_module_enable || m->coll_module_enable(m, c) == OMPI_SUCCESS)) {
+                COPY(m, "mi355x");
+                c->modules[c->nmodules++] = m;
+            } else {
+                obj_release(&m->super);
+            }
+        }
+    }
+#undef COPY
+    return 0;
+}
+
+const char *mxh_comm_slot_owner(void *cv, const char *slot)
+{
+    struct ompi_communicator_t *c = cv;
+    int i = slot_index(slot);
+    return (i >= 0 && c->fn[i]) ? c->owner[i] : "";
+}
+
+static int self_ag(const void *s, void *r, size_t b, void *ctx)
+{
+    (void)ctx;
+    memcpy(r, s, b);
+    return 0;
+}
+
+int mxh_init(const char *component_lib, mxh_reducer_t base, mxh_pattern_t pattern)
+{
+    g_base = base;
+    g_pattern = pattern;
+    g_host = (mx_ompi_host_t){comm_rank, comm_size, dtype_slot, dtype_size, dtype_contiguous, op_index, op_flags,
+                              op_fns, op_3fns, comm_coll_fn, obj_retain, obj_release, mca_int, NULL};
+    g_host.byte_dtype = mxh_dtype("MPI_BYTE");
+    g_op_comp = NULL;
+    g_coll_comp = NULL;
+    if (component_lib && *component_lib) {
+        int (*set_host)(const mx_ompi_host_t *);
+        g_dl = dlopen(component_lib, RTLD_NOW | RTLD_GLOBAL);
+        if (!g_dl) { fprintf(stderr, "mxh_init: %s\n", dlerror()); return -1; }
+        /* mca_base_component_repository: mca_<type>_<name>_component */
+        g_op_comp = dlsym(g_dl, "mca_op_mi355x_component");
+        g_coll_comp = dlsym(g_dl, "mca_coll_mi355x_component");
+        set_host = (int (*)(const mx_ompi_host_t *))dlsym(g_dl, "mx_ompi_set_host");
+        if (!g_op_comp || !g_coll_comp || !set_host) return -2;
+        set_host(&g_host);
+        if (g_op_comp->opc_init_query(false, false) != OMPI_SUCCESS) g_op_comp = NULL;
+        if (g_coll_comp->collm_init_query(false, false) != OMPI_SUCCESS) g_coll_comp = NULL;
+    }
+    for (int i = 0; i < OMPI_OP_BASE_FORTRAN_OP_MAX; i++) {
+        struct ompi_op_t *op = &g_ops[i];
+        memset(op, 0, sizeof *op);
+        snprintf(op->o_name, sizeof op->o_name, "%s", g_opnames[i]);
+        op->o_f_to_c_index = i;
+        op->o_flags = OMPI_OP_FLAGS_INTRINSIC | OMPI_OP_FLAGS_COMMUTE;
+        if (op_select(op)) return -3;
+    }
+    memset(&g_self, 0, sizeof g_self);
+    g_self.rank = 0;
+    g_self.size = 1;
+    g_self.ag = self_ag;
+    comm_select(&g_self, 1);
+    return 0;
+}
+
+int mxh_finalize(void)
+{
+    return 0;
+}
+
+void *mxh_comm_create(int rank, int size, mxh_allgather_t ag, void *ctx)
+{
+    struct ompi_communicator_t *c = calloc(1, sizeof *c);
+    if (!c) return NULL;
+    c->rank = rank;
+    c->size = size;
+    c->ag = ag;
+    c->ag_ctx = ctx;
+    comm_select(c, size == 1);
+    return c;
+}
+
+void *mxh_comm_self(void) { return &g_self; }
+
+int mxh_comm_free(void *cv)
+{
+    struct ompi_communicator_t *c = cv;
+    if (!c || c == &g_self) return 0;
+    for (int i = 0; i < c->nmodules; i++) {
+        mca_coll_base_module_t *m = c->modules[i];
+        for (int s = 0; s < NSLOTS; s++) (void)s;
+        obj_release(&m->super);
+    }
+    free(c);
+    return 0;
+}
+
+/* ---- MPI entry points -------------------------------------------------- */
+/* ompi_op_reduce(op, source, target, count, dtype) as the coll/base
+ * algorithms call it (op.h:547-610) */
+int mxh_op_reduce(void *opv, const void *source, void *target, int count, void *dt)
+{
+    struct ompi_op_t *op = opv;
+    struct ompi_datatype_t *d = dt;
+    if (!d || d->slot < 0 || !op->intrinsic.fns[d->slot]) return -1;
+    op_reduce(op, source, target, count, d);
+    return 0;
+}
+
+int mxh_reduce_local(const void *in, void *inout, int count, void *dt, void *opv)
+{
+    struct ompi_op_t *op = opv;
+    struct ompi_datatype_t *d = dt;
+    /* ompi_op_is_valid (op.h:477-514) */
+    if (!d || d->slot < 0 || !op->intrinsic.fns[d->slot]) return -1;
+    return ((mca_coll_base_module_reduce_local_fn_t)g_self.fn[4])(in, inout, count, d, op, g_self.mod[4]);
+}
+
+int mxh_allreduce(const void *sbuf, void *rbuf, int count, void *dt, void *op, void *cv)
+{
+    struct ompi_communicator_t *c = cv;
+    struct ompi_datatype_t *d = dt;
+    if (!d || d->slot < 0 || !((struct ompi_op_t *)op)->intrinsic.fns[d->slot]) return -1;
+    return ((mca_coll_base_module_allreduce_fn_t)c->fn[0])(sbuf, rbuf, count, d, op, c, c->mod[0]);
+}
+
+int mxh_reduce_scatter(const void *sbuf, void *rbuf, const int *rcounts, void *dt, void *op, void *cv)
+{
+    struct ompi_communicator_t *c = cv;
+    return ((mca_coll_base_module_reduce_scatter_fn_t)c->fn[1])(sbuf, rbuf, rcounts, dt, op, c, c->mod[1]);
+}
+
+int mxh_allgather(const void *sbuf, int scount, void *sdt, void *rbuf, int rcount, void *rdt, void *cv)
+{
+    struct ompi_communicator_t *c = cv;
+    return ((mca_coll_base_module_allgather_fn_t)c->fn[2])(sbuf, scount, sdt, rbuf, rcount, rdt, c, c->mod[2]);
+}
+
+int mxh_bcast(void *buf, int count, void *dt, int root, void *cv)
+{
+    struct ompi_communicator_t *c = cv;
+    return ((mca_coll_base_module_bcast_fn_t)c->fn[3])(buf, count, dt, root, c, c->mod[3]);
+}

@@ -1,0 +1,60 @@
+/*
+ * mx_host.h -- TEST HARNESS ("mini-host"): just enough of Open MPI's
+ * runtime to load and exercise the mi355x op and coll components without a
+ * full Open MPI build.  It restates:
+ *   - ompi_op_base_op_select (op_base_op_select.c:88-204): seed every slot
+ *     with the base function, overlay component modules in ascending
+ *     priority, check the NULL pattern;
+ *   - mca_coll_base_comm_select (coll_base_comm_select.c:108-309): enable
+ *     modules lowest -> highest priority, COPY each non-NULL slot;
+ *   - the MPI entry points MPI_Reduce_local (reduce_local.c:46-91),
+ *     MPI_Allreduce (allreduce.c:46-118), MPI_Reduce_scatter, MPI_Allgather,
+ *     MPI_Bcast: parameter checks + dispatch through comm->c_coll;
+ *   - a host "base" coll module standing in for coll/tuned + basic on host
+ *     buffers, and a coll/self-like module (priority 75) for COMM_SELF.
+ * The base op functions and the host transport are injected by the test.
+ */
+#ifndef MX_HOST_H
+#define MX_HOST_H
+#include <stddef.h>
+#include <stdint.h>
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* base op kernels injected by the test: the reference's own
+ * op_base_functions.c (oracle/_ref) or the oracle restatement */
+typedef int (*mxh_reducer_t)(int op, int type, const void *in, void *inout, size_t n, int fortran);
+typedef int (*mxh_pattern_t)(int op, int type, int fortran);
+/* host transport: allgather `bytes` per rank (rank-major) */
+typedef int (*mxh_allgather_t)(const void *send, void *recv, size_t bytes, void *ctx);
+
+int mxh_init(const char *component_lib, mxh_reducer_t base, mxh_pattern_t pattern);
+int mxh_finalize(void);
+/* MCA variable (OMPI_MCA_<name>), e.g. "coll_mi355x_priority" */
+int mxh_set_mca(const char *name, int value);
+
+void *mxh_dtype(const char *mpi_name);   /* MPI_FLOAT, MPI_2INT, ...; NULL if unknown */
+void *mxh_dtype_contiguous(int count, void *oldtype);  /* MPI_Type_contiguous */
+void *mxh_op(const char *mpi_name);      /* MPI_SUM, MPI_MAXLOC, ... */
+/* which module owns slot t of op: 0 base, 1 mi355x */
+int mxh_op_slot_owner(void *op, int type, int three_buffer);
+
+void *mxh_comm_create(int rank, int size, mxh_allgather_t ag, void *ctx);
+void *mxh_comm_self(void);
+int mxh_comm_free(void *comm);
+/* name of the component whose module owns a coll slot ("mi355x", "base", "self") */
+const char *mxh_comm_slot_owner(void *comm, const char *slot);
+
+int mxh_op_reduce(void *op, const void *source, void *target, int count, void *dtype);
+int mxh_reduce_local(const void *in, void *inout, int count, void *dtype, void *op);
+int mxh_allreduce(const void *sbuf, void *rbuf, int count, void *dtype, void *op, void *comm);
+int mxh_reduce_scatter(const void *sbuf, void *rbuf, const int *rcounts, void *dtype, void *op, void *comm);
+int mxh_allgather(const void *sbuf, int scount, void *sdtype, void *rbuf, int rcount, void *rdtype, void *comm);
+int mxh_bcast(void *buf, int count, void *dtype, int root, void *comm);
+#define MXH_IN_PLACE ((void *)1)
+
+#ifdef __cplusplus
+}
+#endif
+#endif

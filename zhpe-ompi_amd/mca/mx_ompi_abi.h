@@ -1,0 +1,244 @@
+/*
+ * mx_ompi_abi.h -- layout mirror of the Open MPI plugin ABI used by the
+ * mi355x `op` and `coll` components, plus the small set of accessors the
+ * components need from the host MPI library.
+ *
+ * Mirrored layouts (reference = HewlettPackard/zhpe-ompi, Open MPI 5.0.0a1):
+ *   opal_object_t                      opal/class/opal_object.h:194-206
+ *                                      (OPAL_ENABLE_DEBUG = 0 layout)
+ *   ompi_op_base_handler_fn_t          ompi/mca/op/op.h:258-262
+ *   ompi_op_base_3buff_handler_fn_t    ompi/mca/op/op.h:267-273
+ *   ompi_op_base_module_1_0_0_t        ompi/mca/op/op.h:362-378
+ *   ompi_op_base_op_fns_1_0_0_t        ompi/mca/op/op.h:390-395
+ *   ompi_op_base_component_1_0_0_t     ompi/mca/op/op.h:331-341
+ *   mca_coll_base_module_2_3_0_t       ompi/mca/coll/coll.h:504-604
+ *   mca_coll_base_component_2_0_0_t    ompi/mca/coll/coll.h:471-481
+ *   slot typedefs                      ompi/mca/coll/coll.h:195-244, 440-443
+ *
+ * Building against a real Open MPI tree: compile the components with
+ * -DMX_OMPI_REAL and the Open MPI include paths; this header then includes
+ * the real framework headers and maps the MX_* accessors below onto
+ * ompi_comm_rank(), ompi_op_ddt_map[], OBJ_RETAIN() ....
+ * Without it (the default here) the accessors are provided by the host that
+ * loads the component -- the mini-host harness in mca/host/ -- through the
+ * mx_ompi_host_t table, whose entries mirror those Open MPI internals.
+ */
+#ifndef MX_OMPI_ABI_H
+#define MX_OMPI_ABI_H
+
+#include <stdbool.h>
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define OMPI_SUCCESS 0
+#define OMPI_ERROR -1
+#define OMPI_ERR_OUT_OF_RESOURCE -2
+#define OMPI_ERR_NOT_SUPPORTED -8
+#define OMPI_ERR_NOT_FOUND -13
+#define MPI_IN_PLACE ((void *)1)
+
+#define OMPI_OP_BASE_TYPE_MAX 41
+#define OMPI_OP_BASE_FORTRAN_OP_MAX 15
+
+#define OMPI_OP_FLAGS_INTRINSIC 0x0001
+#define OMPI_OP_FLAGS_COMMUTE 0x0040
+
+struct ompi_datatype_t;
+struct ompi_op_t;
+struct ompi_communicator_t;
+struct ompi_request_t;
+
+/* ---- opal_object_t (non-debug) ------------------------------------------- */
+typedef struct mx_obj_class {
+    const char *cls_name;
+    void (*cls_destruct)(void *obj);
+} mx_obj_class_t;
+
+typedef struct opal_object_t {
+    mx_obj_class_t *obj_class;
+    volatile int32_t obj_reference_count;
+} opal_object_t;
+
+/* opaque MCA base component blocks (mca_base_component_2_1_0_t is 0x300+
+ * bytes of version/name strings and open/close/register hooks in the real
+ * tree; only their presence matters to the selection logic) */
+typedef struct mca_base_component_t {
+    int mca_major_version, mca_minor_version, mca_release_version;
+    char mca_project_name[16];
+    int mca_project_major_version, mca_project_minor_version, mca_project_release_version;
+    char mca_type_name[32];
+    int mca_type_major_version, mca_type_minor_version, mca_type_release_version;
+    char mca_component_name[64];
+    int mca_component_major_version, mca_component_minor_version, mca_component_release_version;
+    int (*mca_open_component)(void);
+    int (*mca_close_component)(void);
+    int (*mca_query_component)(void *, int *);
+    int (*mca_register_component_params)(void);
+    int32_t mca_component_flags;
+    char reserved[28];
+} mca_base_component_t;
+
+typedef struct mca_base_component_data_t {
+    uint32_t param_field;
+    char reserved[32];
+} mca_base_component_data_t;
+
+/* ---- op framework (ompi/mca/op/op.h) ------------------------------------- */
+struct ompi_op_base_module_1_0_0_t;
+typedef void (*ompi_op_base_handler_fn_t)(void *, void *, int *, struct ompi_datatype_t **,
+                                          struct ompi_op_base_module_1_0_0_t *);
+typedef void (*ompi_op_base_3buff_handler_fn_t)(void *, void *, void *, int *, struct ompi_datatype_t **,
+                                                struct ompi_op_base_module_1_0_0_t *);
+typedef int (*ompi_op_base_component_init_query_fn_t)(bool enable_progress_threads, bool enable_mpi_threads);
+typedef struct ompi_op_base_module_1_0_0_t *(*ompi_op_base_component_op_query_1_0_0_fn_t)(
+    struct ompi_op_t *op, int *priority);
+typedef int (*ompi_op_base_module_enable_1_0_0_fn_t)(struct ompi_op_base_module_1_0_0_t *module,
+                                                      struct ompi_op_t *op);
+
+typedef struct ompi_op_base_component_1_0_0_t {
+    mca_base_component_t opc_version;
+    mca_base_component_data_t opc_data;
+    ompi_op_base_component_init_query_fn_t opc_init_query;
+    ompi_op_base_component_op_query_1_0_0_fn_t opc_op_query;
+} ompi_op_base_component_1_0_0_t;
+
+typedef struct ompi_op_base_module_1_0_0_t {
+    opal_object_t super;
+    ompi_op_base_module_enable_1_0_0_fn_t opm_enable;
+    struct ompi_op_t *opm_op;
+    ompi_op_base_handler_fn_t opm_fns[OMPI_OP_BASE_TYPE_MAX];
+    ompi_op_base_3buff_handler_fn_t opm_3buff_fns[OMPI_OP_BASE_TYPE_MAX];
+} ompi_op_base_module_1_0_0_t;
+typedef ompi_op_base_module_1_0_0_t ompi_op_base_module_t;
+
+typedef struct ompi_op_base_op_fns_1_0_0_t {
+    ompi_op_base_handler_fn_t fns[OMPI_OP_BASE_TYPE_MAX];
+    ompi_op_base_module_t *modules[OMPI_OP_BASE_TYPE_MAX];
+} ompi_op_base_op_fns_t;
+
+typedef struct ompi_op_base_op_3buff_fns_1_0_0_t {
+    ompi_op_base_3buff_handler_fn_t fns[OMPI_OP_BASE_TYPE_MAX];
+    ompi_op_base_module_t *modules[OMPI_OP_BASE_TYPE_MAX];
+} ompi_op_base_op_3buff_fns_t;
+
+/* ---- coll framework (ompi/mca/coll/coll.h) ------------------------------- */
+struct mca_coll_base_module_2_3_0_t;
+typedef struct mca_coll_base_module_2_3_0_t mca_coll_base_module_t;
+typedef int (*mca_coll_base_component_init_query_fn_t)(bool enable_progress_threads, bool enable_mpi_threads);
+typedef mca_coll_base_module_t *(*mca_coll_base_component_comm_query_2_0_0_fn_t)(
+    struct ompi_communicator_t *comm, int *priority);
+typedef int (*mca_coll_base_module_enable_1_1_0_fn_t)(mca_coll_base_module_t *module,
+                                                      struct ompi_communicator_t *comm);
+typedef int (*mca_coll_base_module_disable_1_2_0_fn_t)(mca_coll_base_module_t *module,
+                                                       struct ompi_communicator_t *comm);
+typedef int (*mca_coll_base_module_allgather_fn_t)(const void *sbuf, int scount, struct ompi_datatype_t *sdtype,
+                                                   void *rbuf, int rcount, struct ompi_datatype_t *rdtype,
+                                                   struct ompi_communicator_t *comm, mca_coll_base_module_t *module);
+typedef int (*mca_coll_base_module_allreduce_fn_t)(const void *sbuf, void *rbuf, int count,
+                                                   struct ompi_datatype_t *dtype, struct ompi_op_t *op,
+                                                   struct ompi_communicator_t *comm, mca_coll_base_module_t *module);
+typedef int (*mca_coll_base_module_bcast_fn_t)(void *buff, int count, struct ompi_datatype_t *datatype, int root,
+                                               struct ompi_communicator_t *comm, mca_coll_base_module_t *module);
+typedef int (*mca_coll_base_module_reduce_scatter_fn_t)(const void *sbuf, void *rbuf, const int *rcounts,
+                                                        struct ompi_datatype_t *dtype, struct ompi_op_t *op,
+                                                        struct ompi_communicator_t *comm,
+                                                        mca_coll_base_module_t *module);
+typedef int (*mca_coll_base_module_reduce_local_fn_t)(const void *inbuf, void *inoutbuf, int count,
+                                                      struct ompi_datatype_t *dtype, struct ompi_op_t *op,
+                                                      mca_coll_base_module_t *module);
+typedef int (*mca_coll_base_module_ft_event_fn_t)(int state);
+typedef void *mx_coll_slot_unused_t;   /* slots this component never fills */
+
+struct mca_coll_base_module_2_3_0_t {
+    opal_object_t super;
+    mca_coll_base_module_enable_1_1_0_fn_t coll_module_enable;
+    /* blocking */
+    mca_coll_base_module_allgather_fn_t coll_allgather;
+    mx_coll_slot_unused_t coll_allgatherv;
+    mca_coll_base_module_allreduce_fn_t coll_allreduce;
+    mx_coll_slot_unused_t coll_alltoall, coll_alltoallv, coll_alltoallw, coll_barrier;
+    mca_coll_base_module_bcast_fn_t coll_bcast;
+    mx_coll_slot_unused_t coll_exscan, coll_gather, coll_gatherv, coll_reduce;
+    mca_coll_base_module_reduce_scatter_fn_t coll_reduce_scatter;
+    mx_coll_slot_unused_t coll_reduce_scatter_block, coll_scan, coll_scatter, coll_scatterv;
+    /* nonblocking (17) */
+    mx_coll_slot_unused_t coll_iallgather, coll_iallgatherv, coll_iallreduce, coll_ialltoall, coll_ialltoallv,
+        coll_ialltoallw, coll_ibarrier, coll_ibcast, coll_iexscan, coll_igather, coll_igatherv, coll_ireduce,
+        coll_ireduce_scatter, coll_ireduce_scatter_block, coll_iscan, coll_iscatter, coll_iscatterv;
+    /* persistent (17) */
+    mx_coll_slot_unused_t coll_allgather_init, coll_allgatherv_init, coll_allreduce_init, coll_alltoall_init,
+        coll_alltoallv_init, coll_alltoallw_init, coll_barrier_init, coll_bcast_init, coll_exscan_init,
+        coll_gather_init, coll_gatherv_init, coll_reduce_init, coll_reduce_scatter_init,
+        coll_reduce_scatter_block_init, coll_scan_init, coll_scatter_init, coll_scatterv_init;
+    /* neighborhood (5 + 5 nonblocking + 5 persistent) */
+    mx_coll_slot_unused_t coll_neighbor_allgather, coll_neighbor_allgatherv, coll_neighbor_alltoall,
+        coll_neighbor_alltoallv, coll_neighbor_alltoallw;
+    mx_coll_slot_unused_t coll_ineighbor_allgather, coll_ineighbor_allgatherv, coll_ineighbor_alltoall,
+        coll_ineighbor_alltoallv, coll_ineighbor_alltoallw;
+    mx_coll_slot_unused_t coll_neighbor_allgather_init, coll_neighbor_allgatherv_init,
+        coll_neighbor_alltoall_init, coll_neighbor_alltoallv_init, coll_neighbor_alltoallw_init;
+    mca_coll_base_module_ft_event_fn_t ft_event;
+    mca_coll_base_module_disable_1_2_0_fn_t coll_module_disable;
+    mca_coll_base_module_reduce_local_fn_t coll_reduce_local;
+    struct mca_coll_base_comm_t *base_data;
+};
+
+typedef struct mca_coll_base_component_2_0_0_t {
+    mca_base_component_t collm_version;
+    mca_base_component_data_t collm_data;
+    mca_coll_base_component_init_query_fn_t collm_init_query;
+    mca_coll_base_component_comm_query_2_0_0_fn_t collm_comm_query;
+} mca_coll_base_component_2_0_0_t;
+
+/* ---- host services (Open MPI internals the components use) ---------------
+ * In a real build these are ompi_comm_rank/size, ompi_op_ddt_map[dt->id] +
+ * ompi_datatype_get_single_predefined_type_from_args, ompi_datatype_type_size,
+ * ompi_datatype_is_contiguous_memory_layout, op->o_f_to_c_index / o_flags,
+ * op->o_func.intrinsic, comm->c_coll, OBJ_RETAIN/OBJ_RELEASE and
+ * mca_base_var lookups.  The mini-host harness supplies them through this
+ * table before it queries the components. */
+typedef struct mx_ompi_host {
+    int (*comm_rank)(struct ompi_communicator_t *comm);
+    int (*comm_size)(struct ompi_communicator_t *comm);
+    /* reducible slot of a datatype (ompi_op_ddt_map, op.c:131-229), -1 if none */
+    int (*dtype_slot)(struct ompi_datatype_t *dt);
+    size_t (*dtype_size)(struct ompi_datatype_t *dt);
+    /* 1 if count elements are one contiguous block of count*size bytes */
+    int (*dtype_contiguous)(struct ompi_datatype_t *dt, int count);
+    int (*op_index)(struct ompi_op_t *op);       /* o_f_to_c_index */
+    uint32_t (*op_flags)(struct ompi_op_t *op);  /* o_flags */
+    ompi_op_base_op_fns_t *(*op_fns)(struct ompi_op_t *op);              /* &op->o_func.intrinsic */
+    ompi_op_base_op_3buff_fns_t *(*op_3buff_fns)(struct ompi_op_t *op);  /* &op->o_3buff_intrinsic */
+    /* the communicator's current function table entry for a slot name
+     * ("allreduce", "allgather", ...) and its module (comm->c_coll) */
+    void *(*comm_coll_fn)(struct ompi_communicator_t *comm, const char *slot, mca_coll_base_module_t **module);
+    void (*obj_retain)(opal_object_t *obj);
+    void (*obj_release)(opal_object_t *obj);
+    /* integer MCA variable lookup (mca_base_var); returns def if unset */
+    int (*mca_int)(const char *name, int def);
+    /* the MPI_BYTE datatype handle (ompi_mpi_byte) for bootstrap exchanges */
+    struct ompi_datatype_t *byte_dtype;
+} mx_ompi_host_t;
+
+/* Set by the host before component queries. */
+extern const mx_ompi_host_t *mx_ompi_host;
+
+#define MX_OBJ_RETAIN(o) mx_ompi_host->obj_retain((opal_object_t *)(o))
+#define MX_OBJ_RELEASE(o) mx_ompi_host->obj_release((opal_object_t *)(o))
+
+/* Component symbols, looked up by name like mca_base_component_repository
+ * does (mca_<type>_<name>_component, mca_base_component_repository.c:449-462). */
+extern ompi_op_base_component_1_0_0_t mca_op_mi355x_component;
+extern mca_coll_base_component_2_0_0_t mca_coll_mi355x_component;
+/* Host registration entry of the component library. */
+int mx_ompi_set_host(const mx_ompi_host_t *host);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* MX_OMPI_ABI_H */

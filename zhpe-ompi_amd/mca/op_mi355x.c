@@ -1,0 +1,173 @@
+/*
+ * op_mi355x.c -- the `mi355x` component of Open MPI's `op` framework.
+ *
+ * Plugs the HIP kernels of libmx_kernels.so into the per-(op, type) function
+ * tables that ompi_op_base_op_select() builds for every intrinsic MPI_Op
+ * (ompi/mca/op/base/op_base_op_select.c:88-204), so MPI_Reduce_local, every
+ * coll/base algorithm's ompi_op_reduce() and the OpenSHMEM reductions run the
+ * GPU kernel whenever both buffers are device memory.
+ *
+ * Follows the reference's accelerator template ompi/mca/op/example:
+ *  - component struct + init_query + op_query (op_example_component.c:50-77,
+ *    185-245, 251-311); priority 50 by default, MCA var op_mi355x_priority,
+ *    clamped to 100 by the framework (op_base_op_select.c:279);
+ *  - at query time the slots already on the op are cached as the fallback and
+ *    RETAINed (op_example_module_max.c:203-258);
+ *  - the hardware-or-fallback decision is taken per call from the buffer
+ *    location (op_example_module_max.c:130-149).
+ * Differences by design: one generic handler serves every slot (the module
+ * remembers its op; the slot comes from the datatype), and every
+ * (op, type) pair of the reference table is covered -- including long
+ * double and its complex/pair types through the device x87 emulation.
+ *
+ * Synchronous ABI: the handler returns void and the caller immediately uses
+ * `inout` (coll_base_allreduce.c:471-477), so each call completes its kernel
+ * before returning (stream sync).  Errors cannot be returned
+ * (ompi/mca/op/op.h:258-273): a device failure aborts, like the CUDA path
+ * does on copy failure (opal_datatype_cuda.c:121-140).
+ */
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include "mx_kernels.h"
+#include "mx_ompi_abi.h"
+
+#ifndef MX_OMPI_WITH_FORTRAN
+#define MX_OMPI_WITH_FORTRAN 1   /* table variant of the host Open MPI build */
+#endif
+
+const mx_ompi_host_t *mx_ompi_host;
+
+int mx_ompi_set_host(const mx_ompi_host_t *host)
+{
+    mx_ompi_host = host;
+    return OMPI_SUCCESS;
+}
+
+typedef struct {
+    ompi_op_base_module_t super;
+    int op_index;                                   /* OMPI_OP_BASE_FORTRAN_* */
+    ompi_op_base_handler_fn_t fallback[OMPI_OP_BASE_TYPE_MAX];
+    ompi_op_base_module_t *fallback_module[OMPI_OP_BASE_TYPE_MAX];
+    ompi_op_base_3buff_handler_fn_t fallback3[OMPI_OP_BASE_TYPE_MAX];
+    ompi_op_base_module_t *fallback3_module[OMPI_OP_BASE_TYPE_MAX];
+} mx_op_module_t;
+
+static void op_module_destruct(void *obj)
+{
+    mx_op_module_t *m = (mx_op_module_t *)obj;
+    for (int i = 0; i < OMPI_OP_BASE_TYPE_MAX; i++) {
+        if (m->fallback_module[i]) MX_OBJ_RELEASE(m->fallback_module[i]);
+        if (m->fallback3_module[i]) MX_OBJ_RELEASE(m->fallback3_module[i]);
+    }
+    free(m);
+}
+
+static mx_obj_class_t mx_op_module_class = {"mx_op_module_t", op_module_destruct};
+
+static int both_on_device(const void *a, const void *b)
+{
+    return mx_is_device_ptr(a) == 1 && mx_is_device_ptr(b) == 1;
+}
+
+static void die(const char *what, int rc)
+{
+    fprintf(stderr, "op/mi355x: %s failed: %s (%d)\n", what, mx_strerror(rc), rc);
+    abort();
+}
+
+/* 2-buffer handler: inout = inout OP in (op.h:258-262) */
+static void mx_op_2buff(void *in, void *inout, int *count, struct ompi_datatype_t **dtype,
+                        ompi_op_base_module_t *module)
+{
+    mx_op_module_t *m = (mx_op_module_t *)module;
+    const int slot = mx_ompi_host->dtype_slot(*dtype);
+    if (slot < 0) die("datatype lookup", MX_ERR_ARG);
+    if (*count > 0 && both_on_device(in, inout)) {
+        int rc = mx_reduce2(m->op_index, slot, in, inout, (size_t)*count, NULL);
+        if (rc == MX_SUCCESS) rc = mx_stream_sync(NULL);
+        if (rc != MX_SUCCESS) die("mx_reduce2", rc);
+        return;
+    }
+    m->fallback[slot](in, inout, count, dtype, m->fallback_module[slot]);
+}
+
+/* 3-buffer handler: out = in1 OP in2 (op.h:267-273) */
+static void mx_op_3buff(void *in1, void *in2, void *out, int *count, struct ompi_datatype_t **dtype,
+                        ompi_op_base_module_t *module)
+{
+    mx_op_module_t *m = (mx_op_module_t *)module;
+    const int slot = mx_ompi_host->dtype_slot(*dtype);
+    if (slot < 0) die("datatype lookup", MX_ERR_ARG);
+    if (*count > 0 && both_on_device(in1, in2) && mx_is_device_ptr(out) == 1) {
+        int rc = mx_reduce3(m->op_index, slot, in1, in2, out, (size_t)*count, NULL);
+        if (rc == MX_SUCCESS) rc = mx_stream_sync(NULL);
+        if (rc != MX_SUCCESS) die("mx_reduce3", rc);
+        return;
+    }
+    m->fallback3[slot](in1, in2, out, count, dtype, m->fallback3_module[slot]);
+}
+
+static int mx_op_component_init_query(bool enable_progress_threads, bool enable_mpi_threads)
+{
+    (void)enable_progress_threads;
+    (void)enable_mpi_threads;  /* kernels run on the null stream; safe under THREAD_MULTIPLE */
+    if (!mx_ompi_host) return OMPI_ERR_NOT_SUPPORTED;
+    return mx_init(-1) == MX_SUCCESS ? OMPI_SUCCESS : OMPI_ERR_NOT_SUPPORTED;
+}
+
+static ompi_op_base_module_t *mx_op_component_op_query(struct ompi_op_t *op, int *priority)
+{
+    const int idx = mx_ompi_host->op_index(op);
+    ompi_op_base_op_fns_t *cur = mx_ompi_host->op_fns(op);
+    ompi_op_base_op_3buff_fns_t *cur3 = mx_ompi_host->op_3buff_fns(op);
+    mx_op_module_t *m;
+    int any = 0;
+
+    if (!(mx_ompi_host->op_flags(op) & OMPI_OP_FLAGS_INTRINSIC)) return NULL;
+    if (idx <= 0 || idx >= MX_OP_REPLACE) return NULL;      /* MPI_OP_NULL, REPLACE, NO_OP */
+    m = calloc(1, sizeof *m);
+    if (!m) return NULL;
+    m->super.super.obj_class = &mx_op_module_class;
+    m->super.super.obj_reference_count = 1;
+    m->super.opm_op = op;
+    m->op_index = idx;
+    for (int t = 0; t < OMPI_OP_BASE_TYPE_MAX; t++) {
+        /* only slots that have a kernel AND are non-NULL on the op: the
+         * framework requires the NULL pattern to stay identical
+         * (op_base_op_select.c:185-201) */
+        if (!mx_op_supported(idx, t, MX_OMPI_WITH_FORTRAN)) continue;
+        if (cur->fns[t]) {
+            m->super.opm_fns[t] = mx_op_2buff;
+            m->fallback[t] = cur->fns[t];
+            m->fallback_module[t] = cur->modules[t];
+            if (cur->modules[t]) MX_OBJ_RETAIN(cur->modules[t]);
+            any = 1;
+        }
+        if (cur3->fns[t]) {
+            m->super.opm_3buff_fns[t] = mx_op_3buff;
+            m->fallback3[t] = cur3->fns[t];
+            m->fallback3_module[t] = cur3->modules[t];
+            if (cur3->modules[t]) MX_OBJ_RETAIN(cur3->modules[t]);
+            any = 1;
+        }
+    }
+    if (!any) {
+        op_module_destruct(m);
+        return NULL;
+    }
+    *priority = mx_ompi_host->mca_int("op_mi355x_priority", 50);
+    return &m->super;
+}
+
+ompi_op_base_component_1_0_0_t mca_op_mi355x_component = {
+    .opc_version = {
+        .mca_major_version = 2, .mca_minor_version = 1, .mca_release_version = 0,
+        .mca_project_name = "ompi",
+        .mca_type_name = "op", .mca_type_major_version = 1,
+        .mca_component_name = "mi355x", .mca_component_major_version = 1,
+    },
+    .opc_init_query = mx_op_component_init_query,
+    .opc_op_query = mx_op_component_op_query,
+};
