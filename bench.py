@@ -122,6 +122,86 @@ def bench_reduce_local(torch, mx, steps, warmup, nbytes=1 << 30):
     return wall, kms, 3.0 * n * 4
 
 
+def bench_allreduce(torch, mx, dist, rank, world, dev, steps, warmup, nbytes=256 << 20):
+    """MPI_Allreduce 256 MiB fp32 SUM per rank through the all-peer path
+    (coll/tuned's fixed decision -> segmented-ring fold order).  Returns
+    the result dict fields, or raises if the path is unavailable."""
+    count = nbytes // 4
+
+    def ag(b):
+        out = [None] * world
+        dist.all_gather_object(out, b)
+        return out
+
+    ndev = torch.cuda.device_count()
+    flags = mx.COMM_IPC | (mx.COMM_RCCL if ndev >= world else 0)
+    try:
+        comm = mx.Comm(rank, world, ag, device=dev, staging_bytes=2 * nbytes + (64 << 20), flags=flags)
+    except mx.MxError:
+        comm = mx.Comm(rank, world, ag, device=dev, staging_bytes=2 * nbytes + (64 << 20), flags=mx.COMM_IPC)
+        flags = mx.COMM_IPC
+    g = torch.Generator(device="cuda").manual_seed(0x5EED + rank)
+    x = torch.rand(count, device="cuda", generator=g) * 2 - 1
+    out = torch.empty_like(x)
+    stream = torch.cuda.current_stream()
+    sp = stream.cuda_stream
+
+    def timed(alg, k):
+        torch.cuda.synchronize()
+        dist.barrier()
+        t0 = time.perf_counter()
+        for _ in range(k):
+            comm.allreduce(x.data_ptr(), out.data_ptr(), count, "FLOAT", "SUM", alg, sp)
+        torch.cuda.synchronize()
+        dist.barrier()
+        t = torch.tensor([time.perf_counter() - t0], dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        return float(t[0])
+
+    for _ in range(warmup):
+        comm.allreduce(x.data_ptr(), out.data_ptr(), count, "FLOAT", "SUM", "auto", sp)
+    t_max = timed("auto", steps)
+    algbw = nbytes / (t_max / steps) / 1e9
+    busbw = algbw * 2 * (world - 1) / world
+    # profiled pass: per-kernel device time of the fused fold (dominant kernel)
+    comm.set_profiling(True)
+    comm.stats(reset=True)
+    for _ in range(3):
+        comm.allreduce(x.data_ptr(), out.data_ptr(), count, "FLOAT", "SUM", "auto", sp)
+    st = comm.stats(reset=True)
+    comm.set_profiling(False)
+    extra = {}
+    if flags & mx.COMM_RCCL:
+        try:
+            for _ in range(2):
+                comm.allreduce(x.data_ptr(), out.data_ptr(), count, "FLOAT", "SUM", "rccl", sp)
+            tr = timed("rccl", max(3, steps // 2))
+            extra["rccl_busbw_gbs"] = round(nbytes / (tr / max(3, steps // 2)) / 1e9 * 2 * (world - 1) / world, 2)
+        except mx.MxError as e:
+            extra["rccl_error"] = str(e)
+    comm.close()
+    fold_ms = st["fold_ms"] / max(1, st["fold_launches"])
+    fold_bytes = st["fold_bytes"] / max(1, st["fold_launches"])
+    return {
+        "value": round(busbw, 2), "unit": "GB/s", "ms_per_step": round(t_max / steps * 1e3, 4),
+        "config": {"workload": "MPI_Allreduce fp32 SUM 256 MiB per rank (coll/tuned fixed decision: "
+                               "segmented-ring fold order), all-peer xGMI",
+                   "count": count, "bytes": nbytes, "algorithm": "auto",
+                   "parallelism": f"allreduce-{world}", "algbw_gbs": round(algbw, 2),
+                   "busbw_formula": "algbw*2(n-1)/n", **extra},
+        "roofline": {"bound": "hbm", "achieved": round(fold_bytes / (fold_ms * 1e-3) / 1e9, 1) if fold_ms else None,
+                     "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": round(fold_bytes / (fold_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4) if fold_ms else None,
+                     "traffic": None, "kernel": "k_fold<float, mx::OpSum> (n reads + n writes, n-1 of them xGMI)",
+                     "algorithmic_bytes_per_launch": fold_bytes, "avg_kernel_ms": round(fold_ms, 4),
+                     "xgmi": {"busbw_gbs": round(busbw, 2), "peak_gbs_single_link": XGMI_LINK_GBS,
+                              "peak_gbs_all_links": 7 * XGMI_LINK_GBS,
+                              "frac_all_links": round(busbw / (7 * XGMI_LINK_GBS), 4)},
+                     "phase_ms_per_call": {k: round(st[k] / max(1, st["calls"]), 4)
+                                           for k in ("fold_ms", "push_ms", "gather_ms", "total_ms")}},
+    }
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -137,47 +217,53 @@ def main():
     world = _env_int("WORLD_SIZE", 1)
     rank = _env_int("RANK", 0)
     local_rank = _env_int("LOCAL_RANK", 0)
-    torch.cuda.set_device(local_rank)
-    mx.init(local_rank)
+    dev = local_rank % max(1, torch.cuda.device_count())
+    torch.cuda.set_device(dev)
+    mx.init(dev)
     dist = None
     if world > 1:
         import torch.distributed as dist
         dist.init_process_group("gloo", rank=rank, world_size=world)
 
-    def barrier():
-        torch.cuda.synchronize()
-        if dist is not None:
-            dist.barrier()
-
     result = {"metric": METRIC, "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
               "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
               "dtype": "f32", "data": "synthetic"}
 
-    barrier()
-    wall, kms, algo_bytes = bench_reduce_local(torch, mx, args.steps, args.warmup)
-    barrier()
-    t_max = wall
-    if dist is not None:
-        t = torch.tensor([wall], dtype=torch.float64)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        t_max = float(t[0])
-    ms_step = t_max / args.steps * 1e3
-    value = algo_bytes * world / (t_max / args.steps) / 1e9
-    avg_kernel_ms = sum(kms) / len(kms)
-    achieved = algo_bytes / (avg_kernel_ms * 1e-3) / 1e9
-    result.update({
-        "value": round(value, 2), "unit": "GB/s", "ms_per_step": round(ms_step, 4),
-        "config": {"workload": "MPI_Reduce_local fp32 SUM, 1 GiB device buffers"
-                               + ("" if world == 1 else f" x {world} independent replicas"),
-                   "count": algo_bytes // 12, "bytes_per_buffer": algo_bytes // 3,
-                   "parallelism": "replicas" if world > 1 else "single-gpu"},
-        "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
-                     "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
-                     "traffic": load_traffic("k_reduce2<float,OpSum>"),
-                     "kernel": "k_reduce2<float, mx::OpSum>",
-                     "algorithmic_bytes_per_launch": algo_bytes,
-                     "avg_kernel_ms": round(avg_kernel_ms, 4)},
-    })
+    done = False
+    if world > 1:
+        try:
+            result.update(bench_allreduce(torch, mx, dist, rank, world, dev, args.steps, args.warmup))
+            done = True
+        except Exception as e:  # noqa: BLE001 - reported in the JSON line
+            result["allreduce_error"] = repr(e)
+    if not done:
+        torch.cuda.synchronize()
+        if dist is not None:
+            dist.barrier()
+        wall, kms, algo_bytes = bench_reduce_local(torch, mx, args.steps, args.warmup)
+        torch.cuda.synchronize()
+        t_max = wall
+        if dist is not None:
+            dist.barrier()
+            t = torch.tensor([wall], dtype=torch.float64)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            t_max = float(t[0])
+        avg_kernel_ms = sum(kms) / len(kms)
+        achieved = algo_bytes / (avg_kernel_ms * 1e-3) / 1e9
+        result.update({
+            "value": round(algo_bytes * world / (t_max / args.steps) / 1e9, 2), "unit": "GB/s",
+            "ms_per_step": round(t_max / args.steps * 1e3, 4),
+            "config": {"workload": "MPI_Reduce_local fp32 SUM, 1 GiB device buffers"
+                                   + ("" if world == 1 else f" x {world} independent replicas"),
+                       "count": algo_bytes // 12, "bytes_per_buffer": algo_bytes // 3,
+                       "parallelism": "replicas" if world > 1 else "single-gpu"},
+            "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
+                         "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
+                         "traffic": load_traffic("k_reduce2<float,OpSum>"),
+                         "kernel": "k_reduce2<float, mx::OpSum>",
+                         "algorithmic_bytes_per_launch": algo_bytes,
+                         "avg_kernel_ms": round(avg_kernel_ms, 4)},
+        })
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         result["cpu_baseline"] = cpu_baseline_reduce_local(args.cpu_seconds)
     if rank == 0:

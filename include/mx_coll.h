@@ -80,6 +80,20 @@ int mx_comm_rank(const mx_comm_t *comm);
 /* Bounded-spin timeout for peer waits (default 60 s). */
 int mx_comm_set_timeout(mx_comm_t *comm, double seconds);
 
+/* Per-communicator kernel timing (HIP events on the collective's stream),
+ * off by default.  Times are summed over calls since the last reset. */
+typedef struct mx_coll_stats {
+    uint64_t calls;            /* collective calls                          */
+    uint64_t fold_launches;    /* fused fold kernels                        */
+    double fold_ms;            /* device time of the fold kernels           */
+    double fold_bytes;         /* algorithmic bytes: n reads + ndst writes  */
+    double push_ms;            /* scatter-push copies to peers' staging     */
+    double gather_ms;          /* gather-area -> rbuf copies                */
+    double total_ms;           /* first -> last event of each call          */
+} mx_coll_stats_t;
+int mx_comm_set_profiling(mx_comm_t *comm, int on);
+int mx_comm_get_stats(mx_comm_t *comm, mx_coll_stats_t *stats, int reset);
+
 /* Allreduce algorithm ids == coll_tuned_allreduce_algorithm values
  * (ompi/mca/coll/tuned/coll_tuned_allreduce_decision.c:37-46). */
 enum {

@@ -76,3 +76,38 @@ def assert_op_equal(out, expected, op, t, what=""):
     np.testing.assert_array_equal(no, ne, err_msg=f"{what}: NaN positions differ")
     keep = ~no
     np.testing.assert_array_equal(vo[keep], ve[keep], err_msg=what)
+
+
+def ddt_records(path=None):
+    """tests/golden/ddt_vectors.bin (oracle/gen_ddt_golden.c layout)."""
+    path = path or os.path.join(GOLDEN, "ddt_vectors.bin")
+    with open(path, "rb") as f:
+        data = f.read()
+    assert data[:8] == b"MXDDT001", "bad ddt golden magic"
+    nrec, nbasic = struct.unpack_from("<II", data, 8)
+    off = 16
+    basic = np.frombuffer(data, np.uint64, nbasic, off).copy()
+    off += 8 * nbasic
+    recs = []
+    for _ in range(nrec):
+        name = data[off: off + 48].split(b"\0")[0].decode()
+        off += 48
+        count, nelem = struct.unpack_from("<II", data, off)
+        off += 8
+        size, lb, ub, tlb, tub, span = struct.unpack_from("<6q", data, off)
+        off += 48
+
+        def take(nb):
+            nonlocal off
+            a = np.frombuffer(data, np.uint8, nb, off).copy()
+            off += nb
+            return a
+        desc = take(32 * nelem)
+        user = take(span)
+        packed = take(size * count)
+        prefill = take(span)
+        unpacked = take(span)
+        recs.append(dict(name=name, count=count, nrec=nelem, size=size, lb=lb, ub=ub, true_lb=tlb,
+                         true_ub=tub, span=span, desc=desc, user=user, packed=packed, prefill=prefill,
+                         unpacked=unpacked))
+    return basic, recs

@@ -279,6 +279,13 @@ struct mx_comm {
   double timeout_s;
   uint64_t timeout_ticks;
   ncclComm_t nccl;
+  // profiling: event pairs recorded around kernels of the current call
+  int prof;
+  hipEvent_t ev[64];
+  int nev;
+  int ev_kind[32];   // 0 fold, 1 push, 2 gather
+  double ev_bytes[32];
+  mx_coll_stats_t st;
 };
 
 static uint64_t ticks_for(double seconds) {
@@ -286,6 +293,55 @@ static uint64_t ticks_for(double seconds) {
   if (hipDeviceGetAttribute(&rate_khz, hipDeviceAttributeWallClockRate, 0) != hipSuccess || rate_khz <= 0)
     rate_khz = 100000;
   return (uint64_t)(seconds * rate_khz * 1000.0);
+}
+
+extern "C" int mx_comm_set_profiling(mx_comm_t *c, int on) {
+  if (!c) return MX_ERR_ARG;
+  if (on && !c->prof) {
+    for (int i = 0; i < 64; i++)
+      if (hipEventCreate(&c->ev[i]) != hipSuccess) return MX_ERR_HIP;
+  }
+  c->prof = on ? 1 : 0;
+  c->nev = 0;
+  return MX_SUCCESS;
+}
+
+extern "C" int mx_comm_get_stats(mx_comm_t *c, mx_coll_stats_t *st, int reset) {
+  if (!c || !st) return MX_ERR_ARG;
+  *st = c->st;
+  if (reset) memset(&c->st, 0, sizeof c->st);
+  return MX_SUCCESS;
+}
+
+// bracket a kernel with an event pair (no-op unless profiling)
+static inline void prof_begin(mx_comm *c, hipStream_t s) {
+  if (c && c->prof && c->nev + 2 <= 64) (void)hipEventRecord(c->ev[c->nev], s);
+}
+static inline void prof_end(mx_comm *c, hipStream_t s, int kind, double bytes) {
+  if (c && c->prof && c->nev + 2 <= 64) {
+    (void)hipEventRecord(c->ev[c->nev + 1], s);
+    c->ev_kind[c->nev / 2] = kind;
+    c->ev_bytes[c->nev / 2] = bytes;
+    c->nev += 2;
+  }
+}
+static void prof_collect(mx_comm *c) {
+  if (!c || !c->prof) return;
+  c->st.calls++;
+  for (int i = 0; i < c->nev; i += 2) {
+    float ms = 0;
+    (void)hipEventElapsedTime(&ms, c->ev[i], c->ev[i + 1]);
+    const int k = c->ev_kind[i / 2];
+    if (k == 0) { c->st.fold_ms += ms; c->st.fold_launches++; c->st.fold_bytes += c->ev_bytes[i / 2]; }
+    else if (k == 1) c->st.push_ms += ms;
+    else c->st.gather_ms += ms;
+  }
+  if (c->nev >= 2) {
+    float ms = 0;
+    (void)hipEventElapsedTime(&ms, c->ev[0], c->ev[c->nev - 1]);
+    c->st.total_ms += ms;
+  }
+  c->nev = 0;
 }
 
 extern "C" int mx_comm_set_timeout(mx_comm_t *c, double seconds) {
@@ -413,6 +469,8 @@ extern "C" int mx_comm_destroy(mx_comm_t *c) {
   if (c->flagmem) (void)hipFree(c->flagmem);
   if (c->err_host) (void)hipHostFree(c->err_host);
   if (c->nccl) ncclCommDestroy(c->nccl);
+  if (c->prof)
+    for (int i = 0; i < 64; i++) (void)hipEventDestroy(c->ev[i]);
   free(c);
   return MX_SUCCESS;
 }
@@ -569,6 +627,7 @@ static int reduce_scatter_segments(int alg, int n, const size_t *rcounts, size_t
 
 static int finish(mx_comm *c, hipStream_t s) {
   if (hipStreamSynchronize(s) != hipSuccess) return MX_ERR_HIP;
+  prof_collect(c);
   if (c->err_host && *(volatile int *)c->err_host) {
     int e = *(volatile int *)c->err_host;
     *c->err_host = 0;
@@ -577,7 +636,7 @@ static int finish(mx_comm *c, hipStream_t s) {
   return MX_SUCCESS;
 }
 
-static int run_fold(fold_launch_fn fl, const Seg &sg, size_t part_lo, const char *const *src_base,
+static int run_fold(mx_comm *c, fold_launch_fn fl, const Seg &sg, size_t part_lo, const char *const *src_base,
                     int nsrc, char *const *dst_base, int ndst, size_t es, hipStream_t s) {
   // src_base / dst_base point at element part_lo of each operand/destination
   FoldArgs a;
@@ -588,7 +647,10 @@ static int run_fold(fold_launch_fn fl, const Seg &sg, size_t part_lo, const char
   a.ndst = ndst;
   a.n = sg.hi - sg.lo;
   a.p = sg.p;
-  return fl(a, s);
+  prof_begin(c, s);
+  const int rc = fl(a, s);
+  prof_end(c, s, 0, (double)(nsrc + ndst) * (double)a.n * (double)es);
+  return rc;
 }
 
 }  // namespace
@@ -656,7 +718,7 @@ extern "C" int mx_allreduce_local(mx_comm_t *c, const void *const *sbufs, void *
     char *dp[MAXR];
     for (int j = 0; j < n; j++) { sp[j] = src[j] + off[p] * es; dp[j] = dst[j] + off[p] * es; }
     for (const Seg &sg : segs) {
-      rc = run_fold(fl, sg, off[p], sp, n, dp, n, es, s);
+      rc = run_fold(c, fl, sg, off[p], sp, n, dp, n, es, s);
       if (rc) return rc;
     }
   }
@@ -702,7 +764,7 @@ extern "C" int mx_reduce_scatter_local(mx_comm_t *c, const void *const *sbufs, v
     for (int j = 0; j < n; j++) sp[j] = src[j] + disp[p] * es;
     char *dp[1] = {tmp ? tmp + disp[p] * es : (char *)rbufs[p]};
     for (const Seg &sg : segs)
-      if ((rc = run_fold(fl, sg, disp[p], sp, n, dp, 1, es, s))) return rc;
+      if ((rc = run_fold(c, fl, sg, disp[p], sp, n, dp, 1, es, s))) return rc;
   }
   if (tmp) {
     CopyArgs ca;
@@ -876,7 +938,9 @@ extern "C" int mx_allreduce(mx_comm_t *c, const void *sbuf, void *rbuf, size_t c
       const size_t e0 = c0 + off[p];
       ca.j[ca.n++] = CopyJob{sb + e0 * es, c->peer_staging[p] + (size_t)r * L.slot + ((e0 * es) & 15), len[p] * es};
     }
+    prof_begin(c, s);
     if ((rc = copy_launch(ca, s))) return rc;
+    prof_end(c, s, 1, 0);
     if ((rc = signal_all(c, FLAG_READY, g, s))) return rc;
     if ((rc = wait_all(c, FLAG_READY, g, s))) return rc;
     // (c) fold my part, store to my rbuf and every peer's gather area
@@ -893,7 +957,7 @@ extern "C" int mx_allreduce(mx_comm_t *c, const void *sbuf, void *rbuf, size_t c
       std::vector<Seg> segs;
       if ((rc = allreduce_segments(alg, n, count, es, e0, e0 + len[r], segs))) return rc;
       for (const Seg &sg : segs)
-        if ((rc = run_fold(fl, sg, e0, sp, n, dp, nd, es, s))) return rc;
+        if ((rc = run_fold(c, fl, sg, e0, sp, n, dp, nd, es, s))) return rc;
     }
     if ((rc = signal_all(c, FLAG_PUSHED, g, s))) return rc;
     if ((rc = wait_all(c, FLAG_PUSHED, g, s))) return rc;
@@ -904,7 +968,9 @@ extern "C" int mx_allreduce(mx_comm_t *c, const void *sbuf, void *rbuf, size_t c
       ca.j[ca.n++] = CopyJob{c->staging + L.gather_off + ((c0 * es) & 15) + off[p] * es, rb + (c0 + off[p]) * es,
                              len[p] * es};
     }
+    prof_begin(c, s);
     if ((rc = copy_launch(ca, s))) return rc;
+    prof_end(c, s, 2, 0);
     if ((rc = signal_all(c, FLAG_DONE, g, s))) return rc;
   }
   return finish(c, s);
@@ -965,7 +1031,7 @@ extern "C" int mx_reduce_scatter(mx_comm_t *c, const void *sbuf, void *rbuf, con
     if (overlap && n * slot + mis + rcounts[r] * es > c->staging_bytes) return MX_ERR_NOMEM;
     char *dp[1] = {dst};
     for (const Seg &sg : segs)
-      if ((rc = run_fold(fl, sg, disp[r], sp, n, dp, 1, es, s))) return rc;
+      if ((rc = run_fold(c, fl, sg, disp[r], sp, n, dp, 1, es, s))) return rc;
     if (overlap) {
       memset(&ca, 0, sizeof ca);
       ca.j[ca.n++] = CopyJob{dst, (char *)rbuf, rcounts[r] * es};

@@ -151,6 +151,10 @@ struct OpCprod {
 // ---- MAXLOC / MINLOC pairs (value, index), host struct layout ----------
 template <class V, class K> struct pair_t { V v; K k; };
 
+// Value-field assignment of a pair; overloaded for x87 so that only the 10
+// value bytes move (the host's `b->v = a->v` is an fldt/fstpt pair).
+template <class V> __device__ __forceinline__ void loc_assign(V &a, const V &b) { a = b; }
+
 // 2-buffer LOC_FUNC (:88-104): x = out, y = in.
 //   if (in.v OP out.v) out = in; else if (in.v == out.v) out.k = min(out.k, in.k)
 // Only the v and k fields are written, so padding keeps the out bytes.
@@ -158,7 +162,7 @@ template <bool IS_MAX>
 struct OpLoc2 {
   template <class P> __device__ __forceinline__ P operator()(P x, P y) const {
     const bool take = IS_MAX ? (y.v > x.v) : (y.v < x.v);
-    if (take) { x.v = y.v; x.k = y.k; }
+    if (take) { loc_assign(x.v, y.v); x.k = y.k; }
     else if (y.v == x.v) { x.k = x.k < y.k ? x.k : y.k; }
     return x;
   }

@@ -38,6 +38,8 @@ struct alignas(16) x87_pair { x87 v; int k; int pad[3]; };
 
 typedef unsigned __int128 u128;
 
+__device__ __forceinline__ void loc_assign(x87 &a, const x87 &b) { a.m = b.m; a.se = b.se; }
+
 __device__ __forceinline__ int x87_exp(const x87 &a) { return a.se & 0x7fff; }
 __device__ __forceinline__ int x87_sign(const x87 &a) { return a.se >> 15; }
 __device__ __forceinline__ bool x87_isnan(const x87 &a) {

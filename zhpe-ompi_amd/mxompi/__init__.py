@@ -168,6 +168,12 @@ ALLREDUCE = {"auto": 0, "basic_linear": 1, "nonoverlapping": 2, "recursive_doubl
              "ring": 4, "segmented_ring": 5, "rabenseifner": 6, "rccl": 100}
 REDUCE_SCATTER = {"auto": 0, "nonoverlapping": 1, "recursive_halving": 2, "ring": 3, "rccl": 100}
 
+class CollStats(ctypes.Structure):
+    _fields_ = [("calls", ctypes.c_uint64), ("fold_launches", ctypes.c_uint64), ("fold_ms", ctypes.c_double),
+                ("fold_bytes", ctypes.c_double), ("push_ms", ctypes.c_double), ("gather_ms", ctypes.c_double),
+                ("total_ms", ctypes.c_double)]
+
+
 _AG_FN = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p)
 
 
@@ -189,6 +195,8 @@ def _coll_lib():
         L.mx_bcast.argtypes = [vp, vp, sz, i, vp]
         L.mx_bcast_local.argtypes = [vp, pp, sz, i, vp]
         L.mx_allreduce_decision.argtypes = [i, sz, i]
+        L.mx_comm_set_profiling.argtypes = [vp, i]
+        L.mx_comm_get_stats.argtypes = [vp, ctypes.POINTER(CollStats), i]
         L.mx_reduce_scatter_decision.argtypes = [i, sz, i]
         L._mx_coll_typed = True
     return L
@@ -246,6 +254,14 @@ class Comm:
         h = ctypes.c_void_p()
         check(_coll_lib().mx_comm_create_local(size, device, ctypes.byref(h)), "mx_comm_create_local")
         return cls(0, size, _handle=h)
+
+    def set_profiling(self, on=True):
+        check(_coll_lib().mx_comm_set_profiling(self.h, 1 if on else 0), "mx_comm_set_profiling")
+
+    def stats(self, reset=False):
+        st = CollStats()
+        check(_coll_lib().mx_comm_get_stats(self.h, ctypes.byref(st), 1 if reset else 0), "mx_comm_get_stats")
+        return {k: getattr(st, k) for k, _ in CollStats._fields_}
 
     def set_timeout(self, seconds):
         check(_coll_lib().mx_comm_set_timeout(self.h, seconds), "mx_comm_set_timeout")
@@ -305,3 +321,69 @@ def allreduce_decision(n, count, t):
 
 def reduce_scatter_decision(n, total, t):
     return int(_coll_lib().mx_reduce_scatter_decision(n, total, _slot(t)))
+
+
+# ---------------------------------------------------------------------------
+# device convertor (include/mx_convertor.h)
+# ---------------------------------------------------------------------------
+def _ddt_lib():
+    L = lib()
+    if not getattr(L, "_mx_ddt_typed", False):
+        vp, sz = ctypes.c_void_p, ctypes.c_size_t
+        L.mx_ddt_create.argtypes = [vp, sz, vp, sz, ctypes.c_int64, ctypes.c_int64, ctypes.POINTER(vp)]
+        L.mx_ddt_destroy.argtypes = [vp]
+        L.mx_ddt_size.restype = sz
+        L.mx_ddt_size.argtypes = [vp]
+        L.mx_ddt_extent.restype = ctypes.c_int64
+        L.mx_ddt_extent.argtypes = [vp]
+        L.mx_ddt_runs.restype = sz
+        L.mx_ddt_runs.argtypes = [vp]
+        L.mx_pack.argtypes = [vp, sz, vp, vp, sz, sz, vp]
+        L.mx_unpack.argtypes = [vp, sz, vp, vp, sz, sz, vp]
+        L._mx_ddt_typed = True
+    return L
+
+
+class Datatype:
+    """A committed derived datatype on the device, built from the
+    reference's committed description records (opt_desc)."""
+
+    def __init__(self, desc: bytes, nrec: int, size: int, lb: int, ub: int, basic_sizes=None):
+        L = _ddt_lib()
+        h = ctypes.c_void_p()
+        self._desc = ctypes.create_string_buffer(bytes(desc), len(desc))
+        bs = None
+        if basic_sizes is not None:
+            self._bs = (ctypes.c_uint64 * len(basic_sizes))(*[int(x) for x in basic_sizes])
+            bs = ctypes.cast(self._bs, ctypes.c_void_p)
+        check(L.mx_ddt_create(ctypes.cast(self._desc, ctypes.c_void_p), nrec, bs, size, lb, ub, ctypes.byref(h)),
+              "mx_ddt_create")
+        self.h = h
+        self.size, self.lb, self.ub = size, lb, ub
+
+    @property
+    def extent(self):
+        return self.ub - self.lb
+
+    @property
+    def runs(self):
+        return int(_ddt_lib().mx_ddt_runs(self.h))
+
+    def pack(self, count, user, packed, offset=0, length=None, stream=0):
+        length = self.size * count - offset if length is None else length
+        check(_ddt_lib().mx_pack(self.h, count, user, packed, offset, length, stream or None), "mx_pack")
+
+    def unpack(self, count, user, packed, offset=0, length=None, stream=0):
+        length = self.size * count - offset if length is None else length
+        check(_ddt_lib().mx_unpack(self.h, count, user, packed, offset, length, stream or None), "mx_unpack")
+
+    def close(self):
+        if getattr(self, "h", None):
+            _ddt_lib().mx_ddt_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:  # noqa: BLE001
+            pass
