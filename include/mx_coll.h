@@ -130,6 +130,25 @@ int mx_reduce_scatter(mx_comm_t *comm, const void *sbuf, void *rbuf,
 int mx_allgather(mx_comm_t *comm, const void *sbuf, void *rbuf, size_t bytes, void *stream);
 int mx_bcast(mx_comm_t *comm, void *buf, size_t bytes, int root, void *stream);
 
+/* ---- OpenSHMEM reductions (shmem_<type>_<op>_to_all) --------------------
+ * The OSHMEM op/type numbering (oshmem/op/op.h: OSHMEM_OP_AND..PROD,
+ * OSHMEM_OP_TYPE_SHORT..FREAL16).  mx_shmem_to_mpi restates scoll/mpi's
+ * mapping onto an MPI op + datatype (oshmem/mca/scoll/mpi/
+ * scoll_mpi_dtypes.h: shmem_dtype_to_ompi_dtype / shmem_op_to_ompi_op;
+ * integer types map by dt_size: 8/16/32/64 bits), which then runs as a
+ * coll allreduce (scoll_mpi_ops.c:212-275). */
+enum { MX_SHMEM_AND, MX_SHMEM_OR, MX_SHMEM_XOR, MX_SHMEM_MAX, MX_SHMEM_MIN, MX_SHMEM_SUM, MX_SHMEM_PROD };
+enum { MX_SHMEM_SHORT, MX_SHMEM_INT, MX_SHMEM_LONG, MX_SHMEM_LLONG, MX_SHMEM_INT16, MX_SHMEM_INT32,
+       MX_SHMEM_INT64, MX_SHMEM_FLOAT, MX_SHMEM_DOUBLE, MX_SHMEM_LDOUBLE, MX_SHMEM_FCOMPLEX,
+       MX_SHMEM_DCOMPLEX, MX_SHMEM_FINT2, MX_SHMEM_FINT4, MX_SHMEM_FINT8, MX_SHMEM_FREAL4,
+       MX_SHMEM_FREAL8, MX_SHMEM_FREAL16 };
+int mx_shmem_to_mpi(int shmem_op, int shmem_type, size_t dt_size, int *mx_op, int *mx_type);
+/* target[i] = reduction over the active set of source[i], i < nreduce
+ * (target may equal source).  Runs mx_allreduce with the tuned decision,
+ * exactly what scoll/mpi asks of coll/tuned. */
+int mx_shmem_reduce(mx_comm_t *comm, int shmem_op, int shmem_type, size_t dt_size, void *target,
+                    const void *source, size_t nreduce, void *stream);
+
 /* ---- local communicator: arrays of `size` buffers, one per rank --------- */
 int mx_allreduce_local(mx_comm_t *comm, const void *const *sbufs, void *const *rbufs,
                        size_t count, int type, int op, int alg, void *stream);

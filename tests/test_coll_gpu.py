@@ -236,6 +236,12 @@ def _mp_worker(rank, n, port, staging, jobs, q):
                 out = torch.zeros(n * count, dtype=torch.uint8, device="cuda")
                 comm.allgather(x.data_ptr(), out.data_ptr(), count, st)
                 results.append(out.cpu().numpy().tobytes())
+            elif kind == "shmem":
+                # shmem_float_max_to_all (examples/oshmem_max_reduction.c:46) -> MPI_MAX / MPI_FLOAT
+                x = _dev(gen("FLOAT", "MAX", count, 7000 + rank))
+                out = torch.zeros(count * 4, dtype=torch.uint8, device="cuda")
+                comm.shmem_reduce("MAX", "FLOAT", 4, out.data_ptr(), x.data_ptr(), count, st)
+                results.append(out.cpu().numpy().tobytes())
             elif kind == "bcast":
                 x = _dev(gen("UINT8_T", "BAND", count, 7000 + rank))
                 comm.bcast(x.data_ptr(), count, n - 1, st)
@@ -277,12 +283,13 @@ def test_multiprocess_ipc_bitexact(n):
             ("reduce_scatter", 1000, "SUM", "FLOAT", "ring"),
             ("reduce_scatter", 10, "SUM", "DOUBLE", "recursive_halving"),
             ("allgather", 300001, None, None, None),
+            ("shmem", 5003, "MAX", "FLOAT", "auto"),
             ("bcast", 2000003, None, None, None)]
     jobs = [(k, c, o or "BAND", t or "UINT8_T", a or "auto") for k, c, o, t, a in jobs]
     got = _run_mp(n, jobs)
     for j, (kind, count, op, t, alg) in enumerate(jobs):
         es = mxompi.type_size(t)
-        if kind.startswith("allreduce"):
+        if kind.startswith("allreduce") or kind == "shmem":
             xs = [gen(t, op, count, 7000 + r) for r in range(n)]
             exp = [np.zeros(count * es, np.uint8) for _ in range(n)]
             assert L.mxo_allreduce(ALG_ID[alg], mxompi.OP[op], mxompi.TYPE[t], n, count,

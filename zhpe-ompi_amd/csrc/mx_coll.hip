@@ -1122,3 +1122,52 @@ extern "C" int mx_bcast(mx_comm_t *c, void *buf, size_t bytes, int root, void *s
   }
   return finish(c, s);
 }
+
+// ---------------------------------------------------------------------------
+// OpenSHMEM reductions through the allreduce (scoll/mpi, scoll_mpi_ops.c:212-275)
+// ---------------------------------------------------------------------------
+extern "C" int mx_shmem_to_mpi(int sop, int st, size_t dt_size, int *mx_op, int *mx_type) {
+  if (!mx_op || !mx_type) return MX_ERR_ARG;
+  switch (sop) {  // shmem_op_to_ompi_op
+    case MX_SHMEM_AND: *mx_op = MX_OP_BAND; break;
+    case MX_SHMEM_OR: *mx_op = MX_OP_BOR; break;
+    case MX_SHMEM_XOR: *mx_op = MX_OP_BXOR; break;
+    case MX_SHMEM_MAX: *mx_op = MX_OP_MAX; break;
+    case MX_SHMEM_MIN: *mx_op = MX_OP_MIN; break;
+    case MX_SHMEM_SUM: *mx_op = MX_OP_SUM; break;
+    case MX_SHMEM_PROD: *mx_op = MX_OP_PROD; break;
+    default: return MX_ERR_ARG;
+  }
+  switch (st) {  // shmem_dtype_to_ompi_dtype
+    case MX_SHMEM_FLOAT: *mx_type = MX_TYPE_FLOAT; break;
+    case MX_SHMEM_DOUBLE: *mx_type = MX_TYPE_DOUBLE; break;
+    case MX_SHMEM_LDOUBLE: *mx_type = MX_TYPE_LONG_DOUBLE; break;
+    case MX_SHMEM_FCOMPLEX: *mx_type = MX_TYPE_C_FLOAT_COMPLEX; break;
+    case MX_SHMEM_DCOMPLEX: *mx_type = MX_TYPE_C_DOUBLE_COMPLEX; break;
+    case MX_SHMEM_FINT4: *mx_type = MX_TYPE_INTEGER4; break;
+    case MX_SHMEM_FINT8: *mx_type = MX_TYPE_INTEGER8; break;
+    case MX_SHMEM_FREAL4: *mx_type = MX_TYPE_REAL4; break;
+    case MX_SHMEM_FREAL8: *mx_type = MX_TYPE_REAL8; break;
+    case MX_SHMEM_FREAL16: *mx_type = MX_TYPE_REAL16; break;   // no kernel (as in the reference)
+    default:
+      switch (dt_size * 8) {
+        case 64: *mx_type = MX_TYPE_INT64_T; break;
+        case 32: *mx_type = MX_TYPE_INT32_T; break;
+        case 16: *mx_type = MX_TYPE_INT16_T; break;
+        case 8: *mx_type = MX_TYPE_INT8_T; break;
+        default: return MX_ERR_ARG;   // ompi_mpi_datatype_null
+      }
+  }
+  return MX_SUCCESS;
+}
+
+extern "C" int mx_shmem_reduce(mx_comm_t *c, int sop, int st, size_t dt_size, void *target, const void *source,
+                               size_t nreduce, void *stream) {
+  int op, type;
+  int rc = mx_shmem_to_mpi(sop, st, dt_size, &op, &type);
+  if (rc) return rc;
+  if (!mx_op_supported(op, type, MX_TABLE_WITH_FORTRAN)) return MX_ERR_UNSUPPORTED;
+  if (nreduce == 0) return MX_SUCCESS;
+  return mx_allreduce(c, source == target ? MX_IN_PLACE : source, target, nreduce, type, op, MX_ALLREDUCE_AUTO,
+                      stream);
+}

@@ -113,6 +113,7 @@ def lib() -> ctypes.CDLL:
         L.mx_reduce2.argtypes = [i, i, vp, vp, sz, vp]
         L.mx_reduce3.argtypes = [i, i, vp, vp, vp, sz, vp]
         L.mx_copy.argtypes = [vp, vp, sz, vp]
+        L.mx_shmem_to_mpi.argtypes = [i, i, sz, ctypes.POINTER(i), ctypes.POINTER(i)]
         L._mx_typed = True
     return L
 
@@ -196,6 +197,7 @@ def _coll_lib():
         L.mx_bcast_local.argtypes = [vp, pp, sz, i, vp]
         L.mx_allreduce_decision.argtypes = [i, sz, i]
         L.mx_comm_set_profiling.argtypes = [vp, i]
+        L.mx_shmem_reduce.argtypes = [vp, i, i, sz, vp, vp, sz, vp]
         L.mx_comm_get_stats.argtypes = [vp, ctypes.POINTER(CollStats), i]
         L.mx_reduce_scatter_decision.argtypes = [i, sz, i]
         L._mx_coll_typed = True
@@ -289,6 +291,14 @@ class Comm:
 
     def allgather(self, sbuf, rbuf, nbytes, stream=0):
         check(_coll_lib().mx_allgather(self.h, sbuf, rbuf, nbytes, stream or None), "mx_allgather")
+
+    def shmem_reduce(self, op, t, dt_size, target, source, nreduce, stream=0):
+        """shmem_<t>_<op>_to_all over this communicator's ranks (scoll/mpi path)."""
+        sops = ["AND", "OR", "XOR", "MAX", "MIN", "SUM", "PROD"]
+        sts = ["SHORT", "INT", "LONG", "LLONG", "INT16", "INT32", "INT64", "FLOAT", "DOUBLE", "LDOUBLE",
+               "FCOMPLEX", "DCOMPLEX", "FINT2", "FINT4", "FINT8", "FREAL4", "FREAL8", "FREAL16"]
+        check(_coll_lib().mx_shmem_reduce(self.h, sops.index(op), sts.index(t), dt_size, target, source, nreduce,
+                                          stream or None), "mx_shmem_reduce")
 
     def bcast(self, buf, nbytes, root, stream=0):
         check(_coll_lib().mx_bcast(self.h, buf, nbytes, root, stream or None), "mx_bcast")
