@@ -95,7 +95,27 @@ def cpu_baseline_reduce_local(seconds=10.0):
     gbs = 3.0 * n * 4 * iters / el / 1e9
     return {"value": round(gbs, 3), "unit": "GB/s", "cores": 1, "kind": kind,
             "sample": f"fp32 SUM 2-buffer, 2 x 256 MiB host buffers, {iters} calls in {el:.1f} s "
-                      f"(1 pinned host thread; algorithmic 3*N*4 B per call)"}
+                      f"(1 host thread; algorithmic 3*N*4 B per call)"}
+
+
+def cpu_baseline_allreduce(ranks=8, nbytes=256 << 20, iters=10):
+    """The host MPI_Allreduce the reference runs with coll/tuned + vader,
+    restated as `ranks` pinned processes over shared memory (ring,
+    single-copy; oracle/cpu_coll_proxy.c, BASELINE.md 2 "Fallback": no Open
+    MPI on the box), fp32 SUM through the reference's own compiled loop."""
+    import subprocess
+    exe = os.path.join(ROOT, "oracle", "build", "cpu_coll_proxy")
+    ref = os.path.join(ROOT, "oracle", "_ref", "libref_op.so")
+    if not os.path.exists(exe):
+        return {"error": "oracle/build/cpu_coll_proxy not built"}
+    cmd = [exe, str(ranks), str(nbytes), str(iters)] + ([ref] if os.path.exists(ref) else [])
+    try:
+        p = subprocess.run(cmd, capture_output=True, text=True, timeout=300)
+        d = json.loads(p.stdout.strip().splitlines()[-1])
+        d["kind"] = d["kind"] + "-proxy"
+        return d
+    except Exception as e:  # noqa: BLE001 - reported in the JSON line
+        return {"error": repr(e)}
 
 
 def bench_reduce_local(torch, mx, steps, warmup, nbytes=1 << 30):
@@ -170,6 +190,7 @@ def bench_allreduce(torch, mx, dist, rank, world, dev, steps, warmup, nbytes=256
         comm.allreduce(x.data_ptr(), out.data_ptr(), count, "FLOAT", "SUM", "auto", sp)
     st = comm.stats(reset=True)
     comm.set_profiling(False)
+    sweep = allreduce_sweep(torch, mx, dist, comm, world, x, out, sp, flags)
     extra = {}
     if flags & mx.COMM_RCCL:
         try:
@@ -199,7 +220,51 @@ def bench_allreduce(torch, mx, dist, rank, world, dev, steps, warmup, nbytes=256
                               "frac_all_links": round(busbw / (7 * XGMI_LINK_GBS), 4)},
                      "phase_ms_per_call": {k: round(st[k] / max(1, st["calls"]), 4)
                                            for k in ("fold_ms", "push_ms", "gather_ms", "total_ms")}},
+        "sweep": sweep,
     }
+
+
+def allreduce_sweep(torch, mx, dist, comm, world, x, out, sp, flags, budget_s=20.0):
+    """Compact CFG-D sweep (BASELINE configs[3]): busBW / latency of
+    MPI_Allreduce for a few sizes and fold orders (fp32 SUM, uint16 BAND),
+    max over ranks.  Bounded to ~budget_s seconds in total."""
+    rows = []
+    algs = ["auto", "ring", "rabenseifner"] + (["rccl"] if flags & mx.COMM_RCCL else [])
+    t_start = time.perf_counter()
+    for nbytes in (8, 1 << 10, 64 << 10, 1 << 20, 16 << 20, 256 << 20):
+        for t, op in (("FLOAT", "SUM"), ("UINT16_T", "BAND")):
+            if t == "UINT16_T" and nbytes not in (64 << 10, 16 << 20):
+                continue
+            count = max(1, nbytes // (4 if t == "FLOAT" else 2))
+            iters = 50 if nbytes <= (64 << 10) else (20 if nbytes <= (1 << 20) else (10 if nbytes <= (16 << 20) else 5))
+            for alg in algs:
+                if alg == "rccl" and t == "UINT16_T":
+                    continue
+                ok = torch.tensor([1.0])
+                try:
+                    for _ in range(2):
+                        comm.allreduce(x.data_ptr(), out.data_ptr(), count, t, op, alg, sp)
+                    torch.cuda.synchronize()
+                except mx.MxError:
+                    ok[0] = 0.0
+                dist.all_reduce(ok, op=dist.ReduceOp.MIN)
+                if ok[0] == 0.0:
+                    rows.append({"bytes": nbytes, "type": t, "op": op, "alg": alg, "error": "unsupported"})
+                    continue
+                dist.barrier()
+                t0 = time.perf_counter()
+                for _ in range(iters):
+                    comm.allreduce(x.data_ptr(), out.data_ptr(), count, t, op, alg, sp)
+                torch.cuda.synchronize()
+                el = torch.tensor([time.perf_counter() - t0], dtype=torch.float64)
+                dist.all_reduce(el, op=dist.ReduceOp.MAX)
+                per = float(el[0]) / iters
+                algbw = count * (4 if t == "FLOAT" else 2) / per / 1e9
+                rows.append({"bytes": nbytes, "type": t, "op": op, "alg": alg, "us": round(per * 1e6, 2),
+                             "algbw_gbs": round(algbw, 2), "busbw_gbs": round(algbw * 2 * (world - 1) / world, 2)})
+            if time.perf_counter() - t_start > budget_s:
+                return rows
+    return rows
 
 
 def main():
@@ -266,6 +331,7 @@ def main():
         })
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         result["cpu_baseline"] = cpu_baseline_reduce_local(args.cpu_seconds)
+        result["cpu_baseline_allreduce"] = cpu_baseline_allreduce()
     if rank == 0:
         print(json.dumps(result), flush=True)
     if dist is not None:

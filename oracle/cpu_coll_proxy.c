@@ -1,0 +1,185 @@
+/*
+ * cpu_coll_proxy.c -- TEST INFRASTRUCTURE ONLY (CPU baseline, BASELINE.md 2
+ * "Fallback"): the host MPI_Allreduce the reference would run with
+ * coll/tuned + the vader (sm) BTL, restated as N forked processes over one
+ * shared-memory segment, because no Open MPI install exists on the GPU box.
+ *
+ * Algorithm: ompi_coll_base_allreduce_intra_ring (coll_base_allreduce.c:
+ * 341-536): rbuf = sbuf (copy_content_same_ddt, :408); reduce-scatter in
+ * n-1 steps, step k receiving block (r-k) mod n from the left neighbour and
+ * computing rbuf[b] = inbuf OP rbuf[b] (:470-477, :488-496); allgather in
+ * n-1 steps, step k receiving block (r-k) mod n (:500-530).  Blocks follow
+ * COLL_BASE_COMPUTE_BLOCKCOUNT (coll_base_functions.h:428-435).  Transport
+ * is modelled as vader's single-copy path (CMA): the receiver copies the
+ * block straight out of the sender's buffer; one process-shared barrier per
+ * step stands in for the send/recv completion.  (Tuned selects the 1 MiB
+ * segmented ring at 256 MiB; it moves the same bytes in smaller messages.)
+ * The local reduction is the reference's own compiled
+ * ompi_op_base_2buff_sum_float (oracle/_ref/libref_op.so) when present
+ * ("reference"), else a plain C loop ("port").
+ *
+ * usage: cpu_coll_proxy RANKS BYTES ITERS [libref_op.so]
+ * prints one JSON object: busBW GB/s = S/t * 2(n-1)/n, t = median.
+ */
+#define _GNU_SOURCE
+#include <dlfcn.h>
+#include <pthread.h>
+#include <sched.h>
+#include <stdint.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+#include <sys/mman.h>
+#include <sys/wait.h>
+#include <time.h>
+#include <unistd.h>
+
+typedef void (*ref_fn)(void *in, void *inout, int *count, void *dtype, void *module);
+
+static ref_fn g_ref;
+
+static void reduce_sum_float(const float *in, float *inout, size_t n)
+{
+    if (g_ref) {
+        /* the reference takes an int count; feed it in <= 2^30 pieces */
+        while (n) {
+            int c = n > (1u << 30) ? (1 << 30) : (int)n;
+            g_ref((void *)in, inout, &c, NULL, NULL);
+            in += c; inout += c; n -= (size_t)c;
+        }
+        return;
+    }
+    for (size_t i = 0; i < n; i++) inout[i] += in[i];   /* op_base_functions.c:312 */
+}
+
+static double now(void)
+{
+    struct timespec ts;
+    clock_gettime(CLOCK_MONOTONIC, &ts);
+    return ts.tv_sec + ts.tv_nsec * 1e-9;
+}
+
+struct shared {
+    pthread_barrier_t bar;
+    double times[64];
+    int mismatch;
+};
+
+static void blockcount(size_t count, int n, int b, size_t *off, size_t *len)
+{
+    const size_t late = count / n, split = count % n, early = late + (split ? 1 : 0);
+    *off = (size_t)b < split ? b * early : b * late + split;
+    *len = (size_t)b < split ? early : late;
+}
+
+static int cmp_double(const void *a, const void *b)
+{
+    double x = *(const double *)a, y = *(const double *)b;
+    return x < y ? -1 : x > y;
+}
+
+int main(int argc, char **argv)
+{
+    if (argc < 4) {
+        fprintf(stderr, "usage: %s RANKS BYTES ITERS [libref_op.so]\n", argv[0]);
+        return 2;
+    }
+    const int n = atoi(argv[1]);
+    const size_t bytes = strtoull(argv[2], NULL, 0);
+    const int iters = atoi(argv[3]);
+    const char *kind = "port";
+    if (argc > 4) {
+        void *h = dlopen(argv[4], RTLD_NOW);
+        if (h) {
+            void **tab = (void **)dlsym(h, "ompi_op_base_functions");
+            if (tab) {
+                g_ref = (ref_fn)tab[3 * 41 + 15];   /* [MPI_SUM][OMPI_OP_BASE_TYPE_FLOAT] */
+                kind = "reference";
+            }
+        }
+    }
+    if (n < 2 || n > 64 || iters < 1) return 2;
+    const size_t count = bytes / 4;
+    size_t off, maxblk;
+    blockcount(count, n, 0, &off, &maxblk);
+    const size_t per_rank = 2 * count * 4 + maxblk * 4 + 4096;
+    struct shared *sh = mmap(NULL, sizeof *sh, PROT_READ | PROT_WRITE, MAP_SHARED | MAP_ANONYMOUS, -1, 0);
+    char *mem = mmap(NULL, per_rank * n, PROT_READ | PROT_WRITE, MAP_SHARED | MAP_ANONYMOUS | MAP_NORESERVE, -1, 0);
+    if (sh == MAP_FAILED || mem == MAP_FAILED) { perror("mmap"); return 1; }
+    pthread_barrierattr_t ba;
+    pthread_barrierattr_init(&ba);
+    pthread_barrierattr_setpshared(&ba, PTHREAD_PROCESS_SHARED);
+    pthread_barrier_init(&sh->bar, &ba, n);
+    cpu_set_t allowed;
+    CPU_ZERO(&allowed);
+    sched_getaffinity(0, sizeof allowed, &allowed);
+    int cpus[1024], ncpu = 0;
+    for (int i = 0; i < CPU_SETSIZE && ncpu < 1024; i++) if (CPU_ISSET(i, &allowed)) cpus[ncpu++] = i;
+
+    for (int r = 0; r < n; r++) {
+        pid_t pid = fork();
+        if (pid < 0) { perror("fork"); return 1; }
+        if (pid > 0) continue;
+        if (ncpu) {   /* --bind-to core */
+            cpu_set_t one;
+            CPU_ZERO(&one);
+            CPU_SET(cpus[r % ncpu], &one);
+            sched_setaffinity(0, sizeof one, &one);
+        }
+        float *sbuf = (float *)(mem + per_rank * r);
+        float *rbuf = sbuf + count;
+        float *inbuf = rbuf + count;
+        uint64_t x = 0x5EED + (uint64_t)r;
+        for (size_t i = 0; i < count; i++) {   /* xorshift64*, uniform [-1, 1) */
+            x ^= x >> 12; x ^= x << 25; x ^= x >> 27;
+            sbuf[i] = (float)((double)((x * 0x2545F4914F6CDD1DULL) >> 11) * 0x1.0p-52 - 1.0);
+        }
+        const int left = (r + n - 1) % n;
+        const float *lrbuf = (const float *)(mem + per_rank * left) + count;
+        double *ts = malloc(sizeof(double) * (iters + 2));
+        for (int it = 0; it < iters + 2; it++) {   /* 2 warmup iterations */
+            pthread_barrier_wait(&sh->bar);
+            const double t0 = now();
+            memcpy(rbuf, sbuf, count * 4);
+            for (int k = 1; k < n; k++) {          /* reduce-scatter */
+                const int b = (r - k + 2 * n) % n;
+                size_t bo, bl;
+                blockcount(count, n, b, &bo, &bl);
+                pthread_barrier_wait(&sh->bar);
+                memcpy(inbuf, lrbuf + bo, bl * 4);
+                reduce_sum_float(inbuf, rbuf + bo, bl);
+            }
+            for (int k = 0; k < n - 1; k++) {      /* allgather */
+                const int b = (r - k + 2 * n) % n;
+                size_t bo, bl;
+                blockcount(count, n, b, &bo, &bl);
+                pthread_barrier_wait(&sh->bar);
+                memcpy(rbuf + bo, lrbuf + bo, bl * 4);
+            }
+            pthread_barrier_wait(&sh->bar);
+            ts[it] = now() - t0;
+        }
+        /* all ranks hold the same vector */
+        if (r > 0 && memcmp(rbuf, (const float *)mem + count, count * 4) != 0) sh->mismatch = 1;
+        if (r == 0) {
+            qsort(ts + 2, iters, sizeof(double), cmp_double);
+            sh->times[0] = ts[2 + iters / 2];
+        }
+        _exit(0);
+    }
+    int bad = 0;
+    for (int r = 0; r < n; r++) {
+        int st;
+        wait(&st);
+        if (!WIFEXITED(st) || WEXITSTATUS(st)) bad = 1;
+    }
+    if (bad || sh->mismatch) { fprintf(stderr, "cpu_coll_proxy: rank failure or mismatch\n"); return 1; }
+    const double t = sh->times[0];
+    const double algbw = (double)count * 4 / t / 1e9;
+    printf("{\"value\": %.3f, \"unit\": \"GB/s\", \"cores\": %d, \"kind\": \"%s\", "
+           "\"algbw_gbs\": %.3f, \"ms_per_call\": %.3f, \"sample\": \"MPI_Allreduce fp32 SUM %zu B, %d ranks "
+           "(processes pinned one per core), ring (coll_base_allreduce.c:341-536) over shared memory with "
+           "single-copy transfers, median of %d calls; busBW = S/t*2(n-1)/n\"}\n",
+           algbw * 2.0 * (n - 1) / n, n, kind, algbw, t * 1e3, count * 4, n, iters);
+    return 0;
+}

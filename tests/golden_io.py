@@ -59,6 +59,36 @@ def _components(buf, t):
     return None
 
 
+# Bytes of an element that carry MPI data, for types whose storage has
+# other bytes: struct gaps of the pair datatypes (size < extent -- the
+# convertor never moves them) and the 6 pad bytes of an x87 long double.
+# Collective results are compared on these bytes only.
+_DATA_BYTES = {
+    38: (8, [0, 1, 4, 5, 6, 7]),                       # SHORT_INT
+    35: (16, list(range(12))),                          # DOUBLE_INT
+    36: (16, list(range(12))),                          # LONG_INT
+    39: (32, list(range(10)) + [16, 17, 18, 19]),       # LONG_DOUBLE_INT
+    23: (16, list(range(10))),                          # LONG_DOUBLE
+    29: (32, list(range(10)) + list(range(16, 26))),    # C_LONG_DOUBLE_COMPLEX
+}
+
+
+def data_bytes(buf, t):
+    """Drop the non-data bytes of slot-t elements (no-op for other types)."""
+    buf = np.ascontiguousarray(buf).view(np.uint8).ravel()
+    if t not in _DATA_BYTES:
+        return buf
+    es, keep = _DATA_BYTES[t]
+    return buf.reshape(-1, es)[:, keep].ravel()
+
+
+def assert_coll_equal(out, expected, op, t, what=""):
+    """assert_op_equal on the data bytes only (collective results)."""
+    if t in _DATA_BYTES and not (op in (SUM, PROD) and t in (23, 29)):
+        out, expected = data_bytes(out, t), data_bytes(expected, t)
+    assert_op_equal(out, expected, op, t, what)
+
+
 def assert_op_equal(out, expected, op, t, what=""):
     """Bit-exact comparison, except that for floating-point SUM/PROD a NaN
     result only has to be a NaN: which NaN payload/sign survives a

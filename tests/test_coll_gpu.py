@@ -75,7 +75,8 @@ def _stream():
 
 CASES = [("SUM", "FLOAT"), ("SUM", "DOUBLE"), ("MAX", "FLOAT"), ("MIN", "DOUBLE"), ("SUM", "INT32_T"),
          ("PROD", "INT8_T"), ("MAXLOC", "FLOAT_INT"), ("PROD", "C_FLOAT_COMPLEX"), ("SUM", "LONG_DOUBLE"),
-         ("BXOR", "UINT16_T"), ("LAND", "BOOL")]
+         ("BXOR", "UINT16_T"), ("LAND", "BOOL"), ("MAXLOC", "DOUBLE_INT"), ("MINLOC", "SHORT_INT"),
+         ("MAXLOC", "LONG_DOUBLE_INT")]
 ALGS = ["auto", "basic_linear", "recursive_doubling", "ring", "segmented_ring", "rabenseifner"]
 ALG_ID = {"auto": 0, "basic_linear": 1, "recursive_doubling": 3, "ring": 4, "segmented_ring": 5,
           "rabenseifner": 6}
@@ -104,7 +105,7 @@ def _check_allreduce_local(n, count, op, t, alg, inplace=False, seed=0):
     else:
         comm.allreduce_local([s.data_ptr() for s in S], [r.data_ptr() for r in R], count, t, op, alg, _stream())
     for r in range(n):
-        golden_io.assert_op_equal(R[r].cpu().numpy(), exp[r], mxompi.OP[op], mxompi.TYPE[t],
+        golden_io.assert_coll_equal(R[r].cpu().numpy(), exp[r], mxompi.OP[op], mxompi.TYPE[t],
                                   f"allreduce {alg} n={n} count={count} {op} {t} rank {r}")
     comm.close()
 
@@ -162,7 +163,7 @@ def test_reduce_scatter_local_bitexact(alg, n, op, t, inplace):
                                       _stream())
         for r in range(n):
             got = R[r].cpu().numpy()[: rc[r] * es]
-            golden_io.assert_op_equal(got, exp[r][: rc[r] * es], mxompi.OP[op], mxompi.TYPE[t],
+            golden_io.assert_coll_equal(got, exp[r][: rc[r] * es], mxompi.OP[op], mxompi.TYPE[t],
                                       f"reduce_scatter {alg} n={n} rc={rc} rank {r}")
         comm.close()
 
@@ -284,7 +285,17 @@ def test_multiprocess_ipc_bitexact(n):
             ("reduce_scatter", 10, "SUM", "DOUBLE", "recursive_halving"),
             ("allgather", 300001, None, None, None),
             ("shmem", 5003, "MAX", "FLOAT", "auto"),
-            ("bcast", 2000003, None, None, None)]
+            ("bcast", 2000003, None, None, None),
+            # back-to-back one-shot calls (both staging parities, every fold shape)
+            ("allreduce", 1000, "SUM", "FLOAT", "auto"),
+            ("allreduce", 3000, "SUM", "FLOAT", "ring"),
+            ("allreduce_inplace", 333, "PROD", "LONG_DOUBLE", "auto"),
+            ("allreduce", 1999, "MAXLOC", "DOUBLE_INT", "rabenseifner"),
+            ("allreduce", 1, "MIN", "INT64_T", "auto"),
+            ("allreduce", 17, "SUM", "DOUBLE", "basic_linear"),
+            ("allreduce", 200003, "SUM", "FLOAT", "segmented_ring"),   # chunked path in between
+            ("allreduce", 2500, "BXOR", "UINT16_T", "auto"),
+            ("allreduce_inplace", 4000, "SUM", "FLOAT", "auto")]
     jobs = [(k, c, o or "BAND", t or "UINT8_T", a or "auto") for k, c, o, t, a in jobs]
     got = _run_mp(n, jobs)
     for j, (kind, count, op, t, alg) in enumerate(jobs):
@@ -296,7 +307,7 @@ def test_multiprocess_ipc_bitexact(n):
                                    (vp * n)(*[x.ctypes.data for x in xs]),
                                    (vp * n)(*[e.ctypes.data for e in exp])) == 0
             for r in range(n):
-                golden_io.assert_op_equal(np.frombuffer(got[r][j], np.uint8), exp[r], mxompi.OP[op],
+                golden_io.assert_coll_equal(np.frombuffer(got[r][j], np.uint8), exp[r], mxompi.OP[op],
                                           mxompi.TYPE[t], f"{kind} {alg} rank {r}")
         elif kind == "reduce_scatter":
             rc = [count + 3 * r for r in range(n)]
@@ -306,7 +317,7 @@ def test_multiprocess_ipc_bitexact(n):
                                         n, (sz * n)(*rc), (vp * n)(*[x.ctypes.data for x in xs]),
                                         (vp * n)(*[e.ctypes.data for e in exp])) == 0
             for r in range(n):
-                golden_io.assert_op_equal(np.frombuffer(got[r][j], np.uint8), exp[r], mxompi.OP[op],
+                golden_io.assert_coll_equal(np.frombuffer(got[r][j], np.uint8), exp[r], mxompi.OP[op],
                                           mxompi.TYPE[t], f"reduce_scatter {alg} rank {r}")
         elif kind == "allgather":
             full = np.concatenate([gen("UINT8_T", "BAND", count, 7000 + r) for r in range(n)])

@@ -109,15 +109,18 @@ def test_device_pack_unpack_match_reference(rec):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("shift", [0, 3])
 @pytest.mark.parametrize("name", ["vector_f32_b1_s2", "vector_f32_b4_s8", "vector_f32_b16_s32",
-                                  "vector_f32_b64_s128", "indexed_f32_random", "struct_char_d3_int_resized48"])
-def test_device_pack_large_cfg_c(name):
-    """CFG-C sizes: the golden type description with a large instance count,
-    checked against the oracle restatement."""
+                                  "vector_f32_b64_s128", "indexed_f32_random", "struct_char_d3_int_resized48",
+                                  "ref_lower_matrix_47", "ref_strange", "ref_blacs_indexed"])
+def test_device_pack_large_cfg_c(name, shift):
+    """CFG-C sizes: the golden type description with a large instance count
+    (many tiles), user buffer aligned or shifted by 3 bytes, checked against
+    the oracle restatement."""
     mxompi.init(0)
     rec = next(r for r in RECS if r["name"] == name)
     dt = _dt(rec)
-    count = max(1, (64 << 20) // rec["size"])
+    count = max(1, (64 << 20) // rec["size"]) + 7
     ext = rec["ub"] - rec["lb"]
     span = ext * (count - 1) + rec["true_ub"] - rec["true_lb"]
     rng = np.random.default_rng(5)
@@ -126,16 +129,34 @@ def test_device_pack_large_cfg_c(name):
     O = _oracle()
     O.mxo_ddt_convert(rec["desc"].ctypes.data, rec["nrec"], np.ascontiguousarray(BASIC).ctypes.data, rec["lb"],
                       rec["ub"], count, user.ctypes.data - rec["true_lb"], exp.ctypes.data, 0)
-    U = torch.from_numpy(user).cuda()
+    Ubuf = torch.zeros(span + 16, dtype=torch.uint8, device="cuda")
+    Ubuf[shift:shift + span] = torch.from_numpy(user).cuda()
     P = torch.zeros(exp.size, dtype=torch.uint8, device="cuda")
-    dt.pack(count, U.data_ptr() - rec["true_lb"], P.data_ptr(), stream=torch.cuda.current_stream().cuda_stream)
+    st = torch.cuda.current_stream().cuda_stream
+    dt.pack(count, Ubuf.data_ptr() + shift - rec["true_lb"], P.data_ptr(), stream=st)
     torch.cuda.synchronize()
     np.testing.assert_array_equal(P.cpu().numpy(), exp)
-    # and back
-    D = torch.zeros(span, dtype=torch.uint8, device="cuda")
-    dt.unpack(count, D.data_ptr() - rec["true_lb"], P.data_ptr(), stream=torch.cuda.current_stream().cuda_stream)
+    # fragments that straddle tiles, at odd offsets
+    P2 = torch.zeros(exp.size + 16, dtype=torch.uint8, device="cuda")
+    off = 0
+    while off < exp.size:
+        ln = min(100003, exp.size - off)
+        dt.pack(count, Ubuf.data_ptr() + shift - rec["true_lb"], P2.data_ptr() + off, offset=off, length=ln, stream=st)
+        off += ln
     torch.cuda.synchronize()
-    got = D.cpu().numpy()
+    np.testing.assert_array_equal(P2.cpu().numpy()[:exp.size], exp)
+    # and back (whole, then fragmented into a second buffer)
+    Dbuf = torch.zeros(span + 16, dtype=torch.uint8, device="cuda")
+    dt.unpack(count, Dbuf.data_ptr() + shift - rec["true_lb"], P.data_ptr(), stream=st)
+    D2 = torch.zeros(span + 16, dtype=torch.uint8, device="cuda")
+    off = 0
+    while off < exp.size:
+        ln = min(77777, exp.size - off)
+        dt.unpack(count, D2.data_ptr() + shift - rec["true_lb"], P.data_ptr() + off, offset=off, length=ln, stream=st)
+        off += ln
+    torch.cuda.synchronize()
+    got = Dbuf.cpu().numpy()[shift:shift + span]
+    np.testing.assert_array_equal(D2.cpu().numpy()[shift:shift + span], got)
     exp_u = np.zeros(span, np.uint8)
     O.mxo_ddt_convert(rec["desc"].ctypes.data, rec["nrec"], np.ascontiguousarray(BASIC).ctypes.data, rec["lb"],
                       rec["ub"], count, exp_u.ctypes.data - rec["true_lb"], exp.ctypes.data, 1)

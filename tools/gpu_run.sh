@@ -26,6 +26,7 @@ for s in $STAGES; do
                python3 bench.py --no-cpu-baseline --steps 5 --warmup 1 || exit 1
            run pmc_write 400 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $O/${T}_pmc_write -o run -- \
                python3 bench.py --no-cpu-baseline --steps 5 --warmup 1 || exit 1 ;;
+    sweep) run sweep 900 python tools/sweep.py --out $O/${T}_sweep.json ${SWEEP_ARGS:-} || exit 1 ;;
     extra) run extra 900 bash -c "${EXTRA_CMD}" || exit 1 ;;
   esac
 done

@@ -124,11 +124,6 @@ __device__ __forceinline__ V eval_prog(const FoldProg &p, L LD) {
   return R[0];
 }
 
-template <class T> struct has_padding { static constexpr bool value = false; };
-template <> struct has_padding<pair_t<short, int>> { static constexpr bool value = true; };
-template <> struct has_padding<pair_t<double, int>> { static constexpr bool value = true; };
-template <> struct has_padding<pair_t<long, int>> { static constexpr bool value = true; };
-
 template <class T, class OP>
 __global__ void __launch_bounds__(kFB) k_fold(FoldArgs a) {
   using V = fvec<T>;
@@ -151,7 +146,7 @@ __global__ void __launch_bounds__(kFB) k_fold(FoldArgs a) {
     const T r = eval_prog<OP, T>(a.p, [&](int j) { return *reinterpret_cast<const T *>(a.src[j] + off); });
 #pragma unroll
     for (int d = 0; d < MAXR; d++)
-      if (d < a.ndst) *reinterpret_cast<T *>(a.dst[d] + off) = r;
+      if (d < a.ndst) store_fields(reinterpret_cast<T *>(a.dst[d] + off), r);
   }
 }
 
@@ -160,7 +155,7 @@ typedef int (*fold_launch_fn)(FoldArgs &, hipStream_t);
 template <class T, class OP>
 static int fold_launch(FoldArgs &a, hipStream_t s) {
   constexpr size_t N = (sizeof(T) <= 16 && 16 % sizeof(T) == 0) ? 16 / sizeof(T) : 0;
-  bool vec = N > 0;
+  bool vec = N > 0 && !has_pad<T>::value;   // padded types: field stores, element path
   uintptr_t m = (uintptr_t)a.src[0] & 15;
   for (int j = 0; j < MAXR; j++)
     if (a.src[j] && ((uintptr_t)a.src[j] & 15) != m) vec = false;
@@ -171,7 +166,7 @@ static int fold_launch(FoldArgs &a, hipStream_t s) {
     size_t head = m ? (16 - m) / sizeof(T) : 0;
     if (head > a.n) head = a.n;
     a.head = head;
-    a.nvec = (a.n - head) / N;
+    a.nvec = (a.n - head) / (N ? N : 1);
   } else {
     a.head = a.n;  // everything scalar (element per lane)
     a.nvec = 0;
@@ -233,6 +228,15 @@ static int copy_launch(CopyArgs &a, hipStream_t s) {
 // ---------------------------------------------------------------------------
 enum { FLAG_READY = 0, FLAG_PUSHED = 1, FLAG_DONE = 2, NFLAGS = 3 };
 
+// one-shot small-message allreduce: per (source rank, workgroup) READY flags
+// after the NFLAGS x MAXR block, then one local completion counter.
+constexpr int OSWG = 16;
+constexpr size_t OS_FLAG_BASE = NFLAGS * MAXR;
+constexpr size_t OS_COUNTER = OS_FLAG_BASE + (size_t)MAXR * OSWG;
+constexpr size_t FLAG_WORDS = OS_COUNTER + 8;
+constexpr size_t kOneShotMax = 64 << 10;   // bytes per rank
+constexpr int OS_MAXSEG = 16;
+
 struct SignalArgs { uint64_t *peer_flag[MAXR]; int n; uint64_t value; };
 
 __global__ void k_signal(SignalArgs a) {
@@ -259,6 +263,112 @@ __global__ void k_wait(const uint64_t *flags, uint32_t mask, uint64_t value, uin
   __atomic_thread_fence(__ATOMIC_ACQUIRE);
 }
 
+// ---------------------------------------------------------------------------
+// one-shot allreduce for small messages: ONE launch per call.  Workgroup w
+// owns element slice w: it pushes that slice of my contribution into every
+// peer's one-shot slot (double-buffered by generation parity), raises READY
+// (source=me, slice=w) at each peer, waits for every peer's READY for slice
+// w, and folds the slice for the WHOLE vector from the n copies (every rank
+// evaluates the same fold program per element, so all ranks agree bit for
+// bit).  Reuse of a parity buffer needs the peer to have finished gen-2,
+// i.e. DONE >= gen-2; the last workgroup to finish raises DONE(gen).
+// ---------------------------------------------------------------------------
+struct OsSeg { size_t lo, hi; FoldProg p; };
+struct OneShotArgs {
+  const char *sb;
+  char *rb;
+  char *peer_slot[MAXR];        // peer p's buffer (this parity) at my slot; null for me
+  const char *src[MAXR];        // operand j: my buffer (this parity) slot j; src[rank] = sb
+  uint64_t *peer_ready[MAXR];   // peer p's OS READY row for source = me
+  uint64_t *peer_done[MAXR];    // peer p's DONE flag for source = me
+  const uint64_t *my_ready;     // my OS READY rows [src][wg]
+  const uint64_t *my_done;      // my DONE flags [src]
+  uint64_t *counter;
+  uint64_t counter_last, gen, timeout_ticks;
+  int *err;
+  int n, rank, nseg;
+  size_t count, es, slice;
+  OsSeg seg[OS_MAXSEG];
+};
+
+constexpr int kOSB = 256;
+
+__device__ __forceinline__ void os_spin(const uint64_t *f, uint64_t v, uint64_t ticks, int *err) {
+  const uint64_t t0 = wall_clock64();
+  while (__hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) < v) {
+    __builtin_amdgcn_s_sleep(1);
+    if (wall_clock64() - t0 > ticks) {
+      __hip_atomic_store(err, MX_ERR_TIMEOUT, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      break;
+    }
+  }
+}
+
+template <class T, class OP>
+__global__ void __launch_bounds__(kOSB) k_oneshot(OneShotArgs a) {
+  const int w = blockIdx.x, t = threadIdx.x;
+  const size_t lo = (size_t)w * a.slice, hi = lo + a.slice < a.count ? lo + a.slice : a.count;
+  // (1) every peer is past gen-2: its reads of this parity buffer are over
+  if (t < a.n && t != a.rank && a.gen > 2) os_spin(a.my_done + t, a.gen - 2, a.timeout_ticks, a.err);
+  __syncthreads();
+  // (2) push my slice (bytes [lo*es, hi*es)) to every peer
+  if (lo < hi) {
+    const size_t b0 = lo * a.es, b1 = hi * a.es;
+    const bool vec = (((uintptr_t)a.sb | b0 | b1) & 15) == 0;
+    for (int p = 0; p < a.n; p++) {
+      if (p == a.rank) continue;
+      char *d = a.peer_slot[p];
+      if (vec) {
+        for (size_t i = b0 / 16 + t; i < b1 / 16; i += kOSB)
+          reinterpret_cast<uint4 *>(d)[i] = reinterpret_cast<const uint4 *>(a.sb)[i];
+      } else {
+        for (size_t i = b0 + t; i < b1; i += kOSB) d[i] = a.sb[i];
+      }
+    }
+  }
+  __threadfence_system();
+  __syncthreads();
+  // (3) READY(me, w) at every peer; (4) wait READY(p, w) from every peer
+  if (t < a.n && t != a.rank) {
+    __hip_atomic_store(a.peer_ready[t] + w, a.gen, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+    os_spin(a.my_ready + (size_t)t * OSWG + w, a.gen, a.timeout_ticks, a.err);
+  }
+  __syncthreads();
+  __atomic_thread_fence(__ATOMIC_ACQUIRE);
+  // (5) fold the slice
+  int sidx = 0;
+  for (size_t e = lo + t; e < hi; e += kOSB) {
+    while (sidx + 1 < a.nseg && e >= a.seg[sidx].hi) sidx++;
+    const size_t off = e * sizeof(T);
+    const T r = eval_prog<OP, T>(a.seg[sidx].p, [&](int j) { return *reinterpret_cast<const T *>(a.src[j] + off); });
+    store_fields(reinterpret_cast<T *>(a.rb + off), r);
+  }
+  // (6) the last workgroup out raises DONE(gen) at every peer
+  __syncthreads();
+  if (t == 0) {
+    __threadfence();
+    const uint64_t old = __hip_atomic_fetch_add(a.counter, (uint64_t)1, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+    if (old == a.counter_last) {
+      __threadfence_system();
+      for (int p = 0; p < a.n; p++)
+        if (p != a.rank) __hip_atomic_store(a.peer_done[p], a.gen, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+  }
+}
+
+typedef int (*oneshot_launch_fn)(OneShotArgs &, int nwg, hipStream_t);
+
+template <class T, class OP>
+static int oneshot_launch(OneShotArgs &a, int nwg, hipStream_t s) {
+  hipLaunchKernelGGL((k_oneshot<T, OP>), dim3(nwg), dim3(kOSB), 0, s, a);
+  return mx_check_launch();
+}
+
+struct OneShotVisitor {
+  template <class T, class OP2, class OP3> oneshot_launch_fn go() { return &oneshot_launch<T, OP2>; }
+  oneshot_launch_fn none() { return nullptr; }
+};
+
 }  // namespace mx
 
 using namespace mx;
@@ -270,6 +380,9 @@ struct mx_comm {
   int rank, size, device, local;
   int flags;
   size_t staging_bytes;
+  size_t main_bytes;           // staging for the chunked paths: [0, main_bytes)
+  size_t os_max, os_slot;      // one-shot: max bytes per rank, slot stride
+  uint64_t os_count;           // one-shot workgroup completions so far
   char *staging;               // mine (uncached, IPC-exported)
   char *peer_staging[MAXR];    // mapped views (peer_staging[rank] = staging)
   uint64_t *flagmem;           // mine: [NFLAGS][MAXR]
@@ -396,10 +509,15 @@ extern "C" int mx_comm_create(int rank, int size, int device, size_t staging_byt
     ipc_info mine, *all = (ipc_info *)calloc(size, sizeof(ipc_info));
     if (!all) goto fail;
     c->staging_bytes = staging_bytes ? staging_bytes : ((size_t)64 << 20);
+    // one-shot region at the top of staging: 2 parities x n slots
+    c->os_max = std::min<size_t>(kOneShotMax, c->staging_bytes / (8 * (size_t)size)) & ~(size_t)255;
+    if (c->os_max < 1024) c->os_max = 0;
+    c->os_slot = c->os_max ? c->os_max + 256 : 0;
+    c->main_bytes = (c->staging_bytes - 2 * (size_t)size * c->os_slot) & ~(size_t)255;
     if (hipExtMallocWithFlags((void **)&c->staging, c->staging_bytes, hipDeviceMallocUncached) != hipSuccess ||
-        hipExtMallocWithFlags((void **)&c->flagmem, NFLAGS * MAXR * sizeof(uint64_t), hipDeviceMallocUncached) !=
+        hipExtMallocWithFlags((void **)&c->flagmem, FLAG_WORDS * sizeof(uint64_t), hipDeviceMallocUncached) !=
             hipSuccess ||
-        hipMemset(c->flagmem, 0, NFLAGS * MAXR * sizeof(uint64_t)) != hipSuccess ||
+        hipMemset(c->flagmem, 0, FLAG_WORDS * sizeof(uint64_t)) != hipSuccess ||
         hipDeviceSynchronize() != hipSuccess) {
       free(all);
       goto fail;
@@ -855,12 +973,57 @@ static size_t chunk_elems(const mx_comm *c, size_t count, size_t es) {
   size_t ce = count;
   while (ce > 1) {
     Layout L = layout_for(n, ce, es);
-    if (L.gather_off + ce * es + 16 <= c->staging_bytes) break;
-    const size_t fit = (c->staging_bytes > (size_t)(n + 2) * 512)
-                           ? (c->staging_bytes - (size_t)(n + 2) * 512) / (2 * es) : 1;
+    if (L.gather_off + ce * es + 16 <= c->main_bytes) break;
+    const size_t fit = (c->main_bytes > (size_t)(n + 2) * 512)
+                           ? (c->main_bytes - (size_t)(n + 2) * 512) / (2 * es) : 1;
     ce = std::min(ce - 1, std::max<size_t>(fit, 1));
   }
   return ce;
+}
+
+// one-shot allreduce (small messages): one kernel, see k_oneshot
+static int allreduce_oneshot(mx_comm *c, oneshot_launch_fn ol, const std::vector<Seg> &segs, const char *sb,
+                             char *rb, size_t count, size_t es, hipStream_t s) {
+  const int n = c->size, r = c->rank;
+  const uint64_t g = ++c->gen;
+  char *const region = c->staging + c->main_bytes + (g & 1) * (size_t)n * c->os_slot;
+  OneShotArgs a;
+  memset(&a, 0, sizeof a);
+  a.sb = sb;
+  a.rb = rb;
+  for (int p = 0; p < n; p++) {
+    const size_t peer_region = c->main_bytes + (g & 1) * (size_t)n * c->os_slot;
+    a.peer_slot[p] = p == r ? nullptr : c->peer_staging[p] + peer_region + (size_t)r * c->os_slot;
+    a.src[p] = p == r ? sb : region + (size_t)p * c->os_slot;
+    a.peer_ready[p] = p == r ? nullptr : c->peer_flags[p] + OS_FLAG_BASE + (size_t)r * OSWG;
+    a.peer_done[p] = p == r ? nullptr : c->peer_flags[p] + FLAG_DONE * MAXR + r;
+  }
+  a.my_ready = c->flagmem + OS_FLAG_BASE;
+  a.my_done = c->flagmem + FLAG_DONE * MAXR;
+  a.counter = c->flagmem + OS_COUNTER;
+  a.gen = g;
+  a.timeout_ticks = c->timeout_ticks;
+  a.err = c->err_dev;
+  a.n = n;
+  a.rank = r;
+  a.count = count;
+  a.es = es;
+  // slices of ~4 KiB, 16-byte aligned when the element size allows
+  const size_t bytes = count * es;
+  size_t nwg = std::min<size_t>(OSWG, std::max<size_t>(1, (bytes + 4095) / 4096));
+  size_t slice = (count + nwg - 1) / nwg;
+  if (16 % es == 0) slice = rup(slice, 16 / es);
+  nwg = (count + slice - 1) / slice;
+  a.slice = slice;
+  a.counter_last = c->os_count + nwg - 1;
+  c->os_count += nwg;
+  a.nseg = (int)segs.size();
+  for (size_t i = 0; i < segs.size(); i++) a.seg[i] = OsSeg{segs[i].lo, segs[i].hi, segs[i].p};
+  prof_begin(c, s);
+  int rc = ol(a, (int)nwg, s);
+  prof_end(c, s, 0, (double)(n + 1) * (double)bytes);
+  if (rc) return rc;
+  return finish(c, s);
 }
 
 }  // namespace
@@ -915,6 +1078,14 @@ extern "C" int mx_allreduce(mx_comm_t *c, const void *sbuf, void *rbuf, size_t c
     return finish(c, s);
   }
   if (!(c->flags & MX_COMM_IPC)) return MX_ERR_STATE;
+  if (c->os_max && count * es <= c->os_max) {
+    std::vector<Seg> segs;
+    int rc = allreduce_segments(alg, n, count, es, 0, count, segs);
+    if (rc) return rc;
+    OneShotVisitor ov;
+    oneshot_launch_fn ol = dispatch(op, type, ov);
+    if (ol && segs.size() <= (size_t)OS_MAXSEG) return allreduce_oneshot(c, ol, segs, sb, rb, count, es, s);
+  }
   {  // validate the algorithm once for the whole vector
     std::vector<Seg> probe;
     int rc = allreduce_segments(alg, n, count, es, 0, 0, probe);
@@ -1061,7 +1232,7 @@ extern "C" int mx_allgather(mx_comm_t *c, const void *sbuf, void *rbuf, size_t b
   }
   if (!(c->flags & MX_COMM_IPC)) return MX_ERR_STATE;
   // n slots of `slot` bytes; each round moves up to `cb` bytes per rank
-  const size_t slot = (c->staging_bytes / n) & ~(size_t)255;
+  const size_t slot = (c->main_bytes / n) & ~(size_t)255;
   if (slot < 512) return MX_ERR_NOMEM;
   const size_t cb = slot - 256;
   for (size_t o = 0; o < bytes; o += cb) {
@@ -1098,7 +1269,7 @@ extern "C" int mx_bcast(mx_comm_t *c, void *buf, size_t bytes, int root, void *s
   const int n = c->size, r = c->rank;
   if (!bytes || n == 1) return MX_SUCCESS;
   if (!(c->flags & MX_COMM_IPC)) return MX_ERR_STATE;
-  const size_t cb = (c->staging_bytes - 256) & ~(size_t)255;
+  const size_t cb = (c->main_bytes - 256) & ~(size_t)255;
   for (size_t o = 0; o < bytes; o += cb) {
     const size_t l = std::min(cb, bytes - o);
     const uint64_t g = ++c->gen;

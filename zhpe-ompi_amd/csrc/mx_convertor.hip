@@ -28,6 +28,16 @@
 
 namespace mx {
 
+// Division by a run-time constant without a 64-bit divide: for numerators
+// n < 2^48, floor(n / d) = floor(n * m / 2^k) with k = 48 + ceil(log2 d),
+// m = ceil(2^k / d) (Granlund & Montgomery, PLDI'94, thm 4.2).
+struct Magic { uint64_t m; uint32_t k; uint32_t pad; };
+constexpr int kMagicBits = 48;
+
+__host__ __device__ __forceinline__ uint64_t udiv(uint64_t n, const Magic &M) {
+  return (uint64_t)(((unsigned __int128)n * M.m) >> M.k);
+}
+
 struct DRun {
   int64_t disp;
   uint64_t blen;     // bytes per block
@@ -37,14 +47,27 @@ struct DRun {
   int64_t stride2;
   uint64_t poff;     // packed offset of the run within one instance
   uint64_t bytes;    // blen * cnt1 * cnt2
+  Magic mblen, mcnt1;
 };
 
 constexpr int kCB = 256;
-constexpr int kLdsRuns = 1024;   // 64 KiB of LDS
+constexpr int kLdsRuns = 512;    // run tables up to 48 KiB are staged in LDS
 
 struct Pos {
-  uint64_t inst, b, o;
+  uint64_t inst, l2, l1, o;
   int r;
+};
+
+struct ConvArgs {
+  const DRun *runs;
+  int nruns;
+  uint64_t S;        // packed bytes per instance
+  Magic mS;
+  int64_t ext;       // instance extent
+  char *user;
+  char *packed;      // receives / holds stream bytes [offset, offset + len)
+  uint64_t offset, len;
+  int pk_vec;        // packed is 16-byte aligned
 };
 
 __device__ __forceinline__ int find_run(const DRun *runs, int n, uint64_t q) {
@@ -56,6 +79,45 @@ __device__ __forceinline__ int find_run(const DRun *runs, int n, uint64_t q) {
   return lo;
 }
 
+// stream position p -> (instance, run, outer block, inner block, byte)
+__device__ __forceinline__ Pos map_pos(const DRun *runs, int nruns, uint64_t S, const Magic &mS, uint64_t p) {
+  Pos P;
+  P.inst = udiv(p, mS);
+  const uint64_t q = p - P.inst * S;
+  P.r = find_run(runs, nruns, q);
+  const DRun &R = runs[P.r];
+  const uint64_t w = q - R.poff;
+  const uint64_t b = udiv(w, R.mblen);
+  P.o = w - b * R.blen;
+  P.l2 = udiv(b, R.mcnt1);
+  P.l1 = b - P.l2 * R.cnt1;
+  return P;
+}
+
+__device__ __forceinline__ int64_t block_addr(const Pos &P, const DRun &R, int64_t ext) {
+  return (int64_t)P.inst * ext + R.disp + (int64_t)P.l2 * R.stride2 + (int64_t)P.l1 * R.stride1;
+}
+
+// advance to the next block after finishing one
+__device__ __forceinline__ void next_block(Pos &P, const DRun *runs, int nruns, DRun &R) {
+  P.o = 0;
+  if (++P.l1 == R.cnt1) {
+    P.l1 = 0;
+    if (++P.l2 == R.cnt2) {
+      P.l2 = 0;
+      if (++P.r == nruns) { P.r = 0; P.inst++; }
+      R = runs[P.r];
+    }
+  }
+}
+
+__device__ __forceinline__ const DRun *stage_runs(const ConvArgs &a, DRun *sruns) {
+  if (a.nruns > kLdsRuns) return a.runs;
+  for (int i = threadIdx.x; i < a.nruns; i += kCB) sruns[i] = a.runs[i];
+  __syncthreads();
+  return sruns;
+}
+
 template <int UNIT> struct unit_t;
 template <> struct unit_t<16> { using T = uint4; };
 template <> struct unit_t<8> { using T = uint64_t; };
@@ -63,79 +125,205 @@ template <> struct unit_t<4> { using T = uint32_t; };
 template <> struct unit_t<2> { using T = uint16_t; };
 template <> struct unit_t<1> { using T = uint8_t; };
 
-// One lane = one 16-byte granule of the packed buffer: granule g covers
-// packed[g*16, g*16+16) = stream bytes [offset + g*16, ...).  The granule is
-// staged in 16/UNIT registers (compile-time indexed, no scratch): PACK
-// gathers UNIT-sized pieces from the user layout and stores the granule
-// with one 16-byte access; UNPACK loads it with one access and scatters.
+// ---------------------------------------------------------------------------
+// GRANULE kernel: one lane = one 16-byte granule of the packed buffer
+// (granule g = stream bytes [offset + 16g, +16)), staged in 16/UNIT
+// registers (compile-time indexed, no scratch).  PACK gathers UNIT-sized
+// pieces from the user layout and stores the granule with one 16-byte
+// access; UNPACK loads it with one access and scatters.  Used when every
+// piece is 16-byte aligned (UNIT = 16: whole-vector moves, no staging) and
+// as the per-tile fallback of the TILE kernels.
+// ---------------------------------------------------------------------------
 template <int UNIT, bool PACK>
-__global__ void __launch_bounds__(kCB)
-k_convert(const DRun *__restrict__ gruns, int nruns, uint64_t S, int64_t extent, char *user, char *packed,
-          uint64_t offset, uint64_t len, int pk_vec) {
+__device__ __forceinline__ void convert_granule(const ConvArgs &a, const DRun *runs, uint64_t g) {
   using U = typename unit_t<UNIT>::T;
   constexpr int K = 16 / UNIT;
-  __shared__ DRun sruns[kLdsRuns];
-  const DRun *runs = gruns;
-  if (nruns <= kLdsRuns) {
-    for (int i = threadIdx.x; i < nruns; i += kCB) sruns[i] = gruns[i];
-    __syncthreads();
-    runs = sruns;
-  }
-  const uint64_t g = (uint64_t)blockIdx.x * kCB + threadIdx.x;
   const uint64_t rel0 = g * 16;
-  if (rel0 >= len) return;
-  const uint64_t n = (len - rel0) < 16 ? (len - rel0) : 16;
-  const bool full = (n == 16) && pk_vec;
-  const uint64_t p = offset + rel0;
-  uint64_t inst = p / S;
-  const uint64_t q = p - inst * S;
-  int r = find_run(runs, nruns, q);
-  DRun R = runs[r];
-  const uint64_t w = q - R.poff;
-  const uint64_t b = w / R.blen;
-  uint64_t o = w - b * R.blen;
-  uint64_t l2 = b / R.cnt1, l1 = b - l2 * R.cnt1;
+  if (rel0 >= a.len) return;
+  const uint64_t n = (a.len - rel0) < 16 ? (a.len - rel0) : 16;
+  const bool full = (n == 16) && a.pk_vec;
+  Pos P = map_pos(runs, a.nruns, a.S, a.mS, a.offset + rel0);
+  DRun R = runs[P.r];
   U regs[K];
   if (!PACK) {
     if (full) {
-      const uint4 v = *reinterpret_cast<const uint4 *>(packed + rel0);
+      const uint4 v = *reinterpret_cast<const uint4 *>(a.packed + rel0);
       memcpy(regs, &v, 16);
     } else {
 #pragma unroll
       for (int k = 0; k < K; k++)
-        if ((uint64_t)k * UNIT < n) regs[k] = *reinterpret_cast<const U *>(packed + rel0 + k * UNIT);
+        if ((uint64_t)k * UNIT < n) regs[k] = *reinterpret_cast<const U *>(a.packed + rel0 + k * UNIT);
     }
   }
 #pragma unroll
   for (int k = 0; k < K; k++) {
     if ((uint64_t)k * UNIT < n) {
-      char *a = user + (int64_t)inst * extent + R.disp + (int64_t)l2 * R.stride2 + (int64_t)l1 * R.stride1 + o;
-      if (PACK) regs[k] = *reinterpret_cast<const U *>(a);
-      else *reinterpret_cast<U *>(a) = regs[k];
-      o += UNIT;
-      if (o == R.blen) {
-        o = 0;
-        if (++l1 == R.cnt1) {
-          l1 = 0;
-          if (++l2 == R.cnt2) {
-            l2 = 0;
-            if (++r == nruns) { r = 0; inst++; }
-            R = runs[r];
-          }
-        }
-      }
+      char *p = a.user + block_addr(P, R, a.ext) + P.o;
+      if (PACK) regs[k] = *reinterpret_cast<const U *>(p);
+      else *reinterpret_cast<U *>(p) = regs[k];
+      P.o += UNIT;
+      if (P.o == R.blen) next_block(P, runs, a.nruns, R);
     }
   }
   if (PACK) {
     if (full) {
       uint4 v;
       memcpy(&v, regs, 16);
-      *reinterpret_cast<uint4 *>(packed + rel0) = v;
+      *reinterpret_cast<uint4 *>(a.packed + rel0) = v;
     } else {
 #pragma unroll
       for (int k = 0; k < K; k++)
-        if ((uint64_t)k * UNIT < n) *reinterpret_cast<U *>(packed + rel0 + k * UNIT) = regs[k];
+        if ((uint64_t)k * UNIT < n) *reinterpret_cast<U *>(a.packed + rel0 + k * UNIT) = regs[k];
     }
+  }
+}
+
+template <int UNIT, bool PACK>
+__global__ void __launch_bounds__(kCB) k_convert(ConvArgs a) {
+  extern __shared__ DRun sruns[];
+  const DRun *runs = stage_runs(a, sruns);
+  convert_granule<UNIT, PACK>(a, runs, (uint64_t)blockIdx.x * kCB + threadIdx.x);
+}
+
+// ---------------------------------------------------------------------------
+// TILE kernels (pieces narrower than 16 bytes): a workgroup owns kTP bytes
+// of the stream.  PACK loads the user span the tile reads (monotonic
+// layouts: [addr(first byte), addr(last byte)]) into LDS with 16-byte
+// coalesced loads, every lane walks the pieces of its kChunk-byte stretch
+// copying LDS -> LDS (4-byte words, v_alignbyte for misaligned pieces), and
+// the packed tile leaves with 16-byte coalesced stores.  UNPACK stages the
+// packed tile in LDS the same way and stores each piece straight to user
+// memory with the widest aligned accesses (gap bytes are never written).
+// One mapping (three multiply-shift divisions) per lane instead of one per
+// byte; HBM sees only wide accesses.
+// ---------------------------------------------------------------------------
+constexpr int kTP = 8192;                  // stream bytes per tile
+constexpr int kChunk = kTP / kCB;          // 32 bytes per lane
+constexpr int kSpanCap = 3 * kTP;          // user bytes a PACK tile may stage
+
+__device__ __forceinline__ uint32_t lds_word(const char *s) {  // 4 bytes at any alignment
+  const uintptr_t u = (uintptr_t)s;
+  const uint32_t *w = reinterpret_cast<const uint32_t *>(u & ~(uintptr_t)3);
+  const int sh = (int)(u & 3);
+  return sh ? __builtin_amdgcn_alignbyte(w[1], w[0], sh) : w[0];
+}
+
+__device__ __forceinline__ void lds_copy(char *d, const char *s, uint64_t n) {
+  while (n && ((uintptr_t)d & 3)) { *d++ = *s++; n--; }
+  for (; n >= 4; n -= 4, d += 4, s += 4) *reinterpret_cast<uint32_t *>(d) = lds_word(s);
+  while (n--) *d++ = *s++;
+}
+
+__device__ __forceinline__ void lds_to_global(char *g, const char *s, uint64_t n) {
+  while (n && ((uintptr_t)g & 3)) { *g++ = *s++; n--; }
+  while (n >= 4 && ((uintptr_t)g & 15)) {
+    *reinterpret_cast<uint32_t *>(g) = lds_word(s);
+    g += 4; s += 4; n -= 4;
+  }
+  for (; n >= 16; n -= 16, g += 16, s += 16)
+    *reinterpret_cast<uint4 *>(g) = make_uint4(lds_word(s), lds_word(s + 4), lds_word(s + 8), lds_word(s + 12));
+  for (; n >= 4; n -= 4, g += 4, s += 4) *reinterpret_cast<uint32_t *>(g) = lds_word(s);
+  while (n--) *g++ = *s++;
+}
+
+// stream bytes [t0, t1) between global and LDS (16-byte accesses when aligned)
+template <bool TO_LDS>
+__device__ __forceinline__ void tile_move(char *lds, char *glob, uint64_t nbytes, int vec) {
+  if (vec) {
+    const uint64_t nv = nbytes / 16;
+    for (uint64_t i = threadIdx.x; i < nv; i += kCB) {
+      if (TO_LDS) reinterpret_cast<uint4 *>(lds)[i] = reinterpret_cast<const uint4 *>(glob)[i];
+      else reinterpret_cast<uint4 *>(glob)[i] = reinterpret_cast<const uint4 *>(lds)[i];
+    }
+    for (uint64_t i = nv * 16 + threadIdx.x; i < nbytes; i += kCB) {
+      if (TO_LDS) lds[i] = glob[i]; else glob[i] = lds[i];
+    }
+  } else {
+    for (uint64_t i = threadIdx.x; i < nbytes; i += kCB) {
+      if (TO_LDS) lds[i] = glob[i]; else glob[i] = lds[i];
+    }
+  }
+}
+
+template <bool PACK>
+__global__ void __launch_bounds__(kCB) k_convert_tile(ConvArgs a, int nruns_lds, int wordpar) {
+  extern __shared__ __align__(16) char smem[];
+  char *pk = smem;                                   // kTP (+16 slack)
+  char *span = smem + kTP + 16;                      // kSpanCap (+32 slack), PACK only
+  DRun *sruns = reinterpret_cast<DRun *>(smem + kTP + 16 + (PACK ? kSpanCap + 32 : 0));
+  __shared__ int64_t s_first, s_last;
+  const DRun *runs = a.runs;
+  if (nruns_lds) {
+    for (int i = threadIdx.x; i < a.nruns; i += kCB) sruns[i] = a.runs[i];
+    runs = sruns;
+  }
+  const uint64_t r0 = (uint64_t)blockIdx.x * kTP;                 // relative to offset
+  const uint64_t r1 = r0 + kTP < a.len ? r0 + kTP : a.len;
+  const int vec = a.pk_vec;
+  uintptr_t lo = 0;
+  bool staged = true;
+  if (PACK) {
+    __syncthreads();
+    if (threadIdx.x < 2) {
+      const uint64_t p = a.offset + (threadIdx.x ? r1 - 1 : r0);
+      const Pos P = map_pos(runs, a.nruns, a.S, a.mS, p);
+      const int64_t ad = block_addr(P, runs[P.r], a.ext) + (int64_t)P.o;
+      if (threadIdx.x) s_last = ad; else s_first = ad;
+    }
+    __syncthreads();
+    lo = ((uintptr_t)a.user + s_first) & ~(uintptr_t)15;
+    const uintptr_t hi = ((uintptr_t)a.user + s_last + 16) & ~(uintptr_t)15;
+    staged = s_last >= s_first && hi - lo <= (uintptr_t)kSpanCap;
+    if (staged) tile_move<true>(span, reinterpret_cast<char *>(lo), hi - lo, 1);
+  } else {
+    tile_move<true>(pk, a.packed + r0, r1 - r0, vec);
+  }
+  __syncthreads();
+  if (PACK && !staged) {   // span too wide for LDS: per-granule gather
+    const uint64_t g0 = r0 / 16, g1 = (r1 + 15) / 16;
+    for (uint64_t g = g0 + threadIdx.x; g < g1; g += kCB) convert_granule<1, true>(a, runs, g);
+    return;
+  }
+  if (!PACK && wordpar) {
+    // word-parallel stores: consecutive lanes write consecutive stream
+    // words, so a wave's stores land on neighbouring user blocks
+    const uint64_t nb = r1 - r0;
+    for (uint64_t w = threadIdx.x; w * 4 < nb; w += kCB) {
+      const uint64_t nbytes = nb - w * 4 < 4 ? nb - w * 4 : 4;
+      Pos P = map_pos(runs, a.nruns, a.S, a.mS, a.offset + r0 + w * 4);
+      DRun R = runs[P.r];
+      char *ua = a.user + block_addr(P, R, a.ext) + (int64_t)P.o;
+      if (nbytes == 4 && P.o + 4 <= R.blen && ((uintptr_t)ua & 3) == 0) {
+        *reinterpret_cast<uint32_t *>(ua) = *reinterpret_cast<const uint32_t *>(pk + w * 4);
+      } else {
+        for (uint64_t i = 0; i < nbytes; i++) {
+          a.user[block_addr(P, R, a.ext) + (int64_t)P.o] = pk[w * 4 + i];
+          if (++P.o == R.blen) next_block(P, runs, a.nruns, R);
+        }
+      }
+    }
+    return;
+  }
+  const uint64_t c0 = r0 + (uint64_t)threadIdx.x * kChunk;
+  const uint64_t c1 = c0 + kChunk < r1 ? c0 + kChunk : r1;
+  if (c0 < c1) {
+    Pos P = map_pos(runs, a.nruns, a.S, a.mS, a.offset + c0);
+    DRun R = runs[P.r];
+    uint64_t pos = c0;
+    while (pos < c1) {
+      const uint64_t avail = R.blen - P.o, want = c1 - pos;
+      const uint64_t n = avail < want ? avail : want;
+      const int64_t ua = block_addr(P, R, a.ext) + (int64_t)P.o;
+      if (PACK) lds_copy(pk + (pos - r0), span + ((uintptr_t)a.user + ua - lo), n);
+      else lds_to_global(a.user + ua, pk + (pos - r0), n);
+      pos += n;
+      P.o += n;
+      if (P.o == R.blen) next_block(P, runs, a.nruns, R);
+    }
+  }
+  if (PACK) {
+    __syncthreads();
+    tile_move<false>(pk, a.packed + r0, r1 - r0, vec);
   }
 }
 
@@ -149,6 +337,8 @@ struct mx_ddt {
   size_t size;
   int64_t lb, ub;
   uint64_t gcd_all;  // gcd of every disp/stride/blen/extent (access unit)
+  Magic mS;          // divide by size
+  bool monotonic;    // user addresses strictly increase along the stream
 };
 
 namespace {
@@ -242,6 +432,33 @@ static int flatten(const uint8_t *recs, size_t lo, size_t hi, int64_t base, cons
   return MX_SUCCESS;
 }
 
+static Magic make_magic(uint64_t d) {
+  Magic M;
+  int l = 0;
+  while (l < 64 && (((unsigned __int128)1) << l) < d) l++;
+  M.k = (uint32_t)(kMagicBits + l);
+  const unsigned __int128 two_k = ((unsigned __int128)1) << M.k;
+  M.m = (uint64_t)((two_k + d - 1) / d);
+  M.pad = 0;
+  return M;
+}
+
+// Every byte of the stream lies at a higher user address than the one
+// before it (runs, blocks and instances in address order, no overlap):
+// then a tile's bytes all lie in [addr(first), addr(last)].
+static bool is_monotonic(const std::vector<DRun> &runs, int64_t ext) {
+  if (runs.empty()) return false;
+  int64_t prev_end = INT64_MIN;   // one past the last byte so far
+  for (const DRun &r : runs) {
+    if (r.cnt1 > 1 && r.stride1 < (int64_t)r.blen) return false;
+    const int64_t inner = (int64_t)(r.cnt1 - 1) * r.stride1 + (int64_t)r.blen;
+    if (r.cnt2 > 1 && r.stride2 < inner) return false;
+    if (r.disp < prev_end) return false;
+    prev_end = r.disp + (int64_t)(r.cnt2 - 1) * r.stride2 + inner;
+  }
+  return prev_end <= ext + runs[0].disp;   // next instance starts after
+}
+
 static uint64_t gcd64(uint64_t a, uint64_t b) {
   while (b) { uint64_t t = a % b; a = b; b = t; }
   return a;
@@ -268,10 +485,16 @@ extern "C" int mx_ddt_create(const void *desc, size_t nrec, const uint64_t *basi
     if (r.cnt2 > 1) g = gcd64(g, absg(r.stride2));
   }
   if (poff != size) { delete d; return MX_ERR_ARG; }   // description / size mismatch
+  for (DRun &r : d->host) {
+    r.mblen = make_magic(r.blen);
+    r.mcnt1 = make_magic(r.cnt1);
+  }
   d->size = size;
   d->lb = lb;
   d->ub = ub;
   d->gcd_all = gcd64(g, absg(ub - lb));
+  d->mS = make_magic(size ? size : 1);
+  d->monotonic = is_monotonic(d->host, ub - lb);
   d->dev = nullptr;
   if (!d->host.empty()) {
     if ((rc = mx_ensure_init())) { delete d; return rc; }
@@ -303,26 +526,52 @@ static int convert(const mx_ddt_t *d, size_t count, char *user, char *packed, si
   if (!d || !user || !packed) return MX_ERR_ARG;
   if (len == 0) return MX_SUCCESS;
   if (d->size == 0 || offset + len > d->size * count) return MX_ERR_ARG;
+  if ((offset + len) >> kMagicBits) return MX_ERR_UNSUPPORTED;   // > 256 TiB streams
   int rc = mx_ensure_init();
   if (rc) return rc;
+  ConvArgs a;
+  a.runs = d->dev;
+  a.nruns = (int)d->host.size();
+  a.S = d->size;
+  a.mS = d->mS;
+  a.ext = d->ub - d->lb;
+  a.user = user;
+  a.packed = packed;
+  a.offset = offset;
+  a.len = len;
+  a.pk_vec = ((uintptr_t)packed & 15) == 0;
+  hipStream_t s = (hipStream_t)stream;
   // widest unit that every piece of every granule respects: layout gcd,
   // alignment of the user origin, and the stream offset of granule 0
   uint64_t u = gcd64(d->gcd_all, ((uintptr_t)user) & 15 ? ((uintptr_t)user & 15) : 16);
   u = gcd64(u, offset & 15 ? (offset & 15) : 16);
   u = gcd64(u, len & 15 ? (len & 15) : 16);
-  if (((uintptr_t)packed & 15) != 0) u = gcd64(u, (uintptr_t)packed & 15);
-  const int pk_vec = ((uintptr_t)packed & 15) == 0;
-  const int nr = (int)d->host.size();
-  const uint64_t g = (len + 15) / 16;
-  const dim3 grid((unsigned)((g + kCB - 1) / kCB)), block(kCB);
-  hipStream_t s = (hipStream_t)stream;
-  const int64_t ext = d->ub - d->lb;
+  if (!a.pk_vec) u = gcd64(u, (uintptr_t)packed & 15);
+  const size_t run_lds = a.nruns <= kLdsRuns ? (size_t)a.nruns * sizeof(DRun) : 0;
+  if (u == 16) {
+    const uint64_t g = (len + 15) / 16;
+    hipLaunchKernelGGL((k_convert<16, PACK>), dim3((unsigned)((g + kCB - 1) / kCB)), dim3(kCB), run_lds, s, a);
+    return mx_check_launch();
+  }
+  // narrow pieces: tile kernels (PACK needs a monotonic layout so that a
+  // tile's user bytes form one span)
+  if (!PACK || d->monotonic) {
+    const int nlds = a.nruns <= 64 ? 1 : 0;
+    const size_t lds = kTP + 16 + (PACK ? kSpanCap + 32 : 0) + (nlds ? (size_t)a.nruns * sizeof(DRun) : 0);
+    const uint64_t tiles = (len + kTP - 1) / kTP;
+    // narrow 4-byte-aligned blocks: word-parallel stores (see the kernel)
+    uint64_t maxblen = 0;
+    for (const DRun &r : d->host) maxblen = std::max<uint64_t>(maxblen, r.blen);
+    const int wordpar = !PACK && (u % 4) == 0 && maxblen <= 32;
+    hipLaunchKernelGGL((k_convert_tile<PACK>), dim3((unsigned)tiles), dim3(kCB), lds, s, a, nlds, wordpar);
+    return mx_check_launch();
+  }
+  const dim3 grid((unsigned)(((len + 15) / 16 + kCB - 1) / kCB)), block(kCB);
   switch (u) {
-    case 16: hipLaunchKernelGGL((k_convert<16, PACK>), grid, block, 0, s, d->dev, nr, d->size, ext, user, packed, offset, len, pk_vec); break;
-    case 8: hipLaunchKernelGGL((k_convert<8, PACK>), grid, block, 0, s, d->dev, nr, d->size, ext, user, packed, offset, len, pk_vec); break;
-    case 4: hipLaunchKernelGGL((k_convert<4, PACK>), grid, block, 0, s, d->dev, nr, d->size, ext, user, packed, offset, len, pk_vec); break;
-    case 2: hipLaunchKernelGGL((k_convert<2, PACK>), grid, block, 0, s, d->dev, nr, d->size, ext, user, packed, offset, len, pk_vec); break;
-    default: hipLaunchKernelGGL((k_convert<1, PACK>), grid, block, 0, s, d->dev, nr, d->size, ext, user, packed, offset, len, pk_vec); break;
+    case 8: hipLaunchKernelGGL((k_convert<8, PACK>), grid, block, run_lds, s, a); break;
+    case 4: hipLaunchKernelGGL((k_convert<4, PACK>), grid, block, run_lds, s, a); break;
+    case 2: hipLaunchKernelGGL((k_convert<2, PACK>), grid, block, run_lds, s, a); break;
+    default: hipLaunchKernelGGL((k_convert<1, PACK>), grid, block, run_lds, s, a); break;
   }
   return mx_check_launch();
 }

@@ -28,6 +28,35 @@ using p_short_int = pair_t<short, int>;
 using p_2real = pair_t<float, float>;
 using p_2double = pair_t<double, double>;
 
+// Types whose storage has bytes outside the value fields: the struct pair
+// types (gaps that MPI never transfers -- their datatypes have size <
+// extent) and x87 long double (10 value bytes in 16).  Results are stored
+// field by field so those bytes keep the destination's content, as the
+// reference's field assignments (LOC_FUNC, op_base_functions.c:88-104) and
+// gap-skipping copies (opal_datatype_copy.h) leave them.
+template <class T> struct has_pad { static constexpr bool value = false; };
+template <> struct has_pad<pair_t<short, int>> { static constexpr bool value = true; };
+template <> struct has_pad<pair_t<double, int>> { static constexpr bool value = true; };
+template <> struct has_pad<pair_t<long, int>> { static constexpr bool value = true; };
+template <> struct has_pad<x87> { static constexpr bool value = true; };
+template <> struct has_pad<x87c> { static constexpr bool value = true; };
+template <> struct has_pad<x87_pair> { static constexpr bool value = true; };
+
+template <class T> __device__ __forceinline__ void store_fields(T *p, const T &r) { *p = r; }
+template <class V, class K> __device__ __forceinline__ void store_fields(pair_t<V, K> *p, const pair_t<V, K> &r) {
+  p->v = r.v;
+  p->k = r.k;
+}
+__device__ __forceinline__ void store_fields(x87 *p, const x87 &r) { p->m = r.m; p->se = r.se; }
+__device__ __forceinline__ void store_fields(x87c *p, const x87c &r) {
+  store_fields(&p->re, r.re);
+  store_fields(&p->im, r.im);
+}
+__device__ __forceinline__ void store_fields(x87_pair *p, const x87_pair &r) {
+  store_fields(&p->v, r.v);
+  p->k = r.k;
+}
+
 static_assert(sizeof(p_float_int) == 8 && sizeof(p_double_int) == 16 && sizeof(p_long_int) == 16 &&
               sizeof(p_2int) == 8 && sizeof(p_short_int) == 8 && sizeof(p_2real) == 8 &&
               sizeof(p_2double) == 16 && sizeof(x87_pair) == 32 && sizeof(f32c) == 8 &&

@@ -98,29 +98,6 @@ k_reduce3(const T *__restrict__ a1, const T *__restrict__ a2, T *__restrict__ o,
 // padding (pairs, x87): the reference's LOC_FUNC_3BUF / `*(b) = a1 op a2`
 // write only the value fields, so the padding bytes of `out` must keep
 // whatever they held.
-template <class T> struct has_pad { static constexpr bool value = false; };
-template <> struct has_pad<pair_t<short, int>> { static constexpr bool value = true; };
-template <> struct has_pad<pair_t<double, int>> { static constexpr bool value = true; };
-template <> struct has_pad<pair_t<long, int>> { static constexpr bool value = true; };
-template <> struct has_pad<x87> { static constexpr bool value = true; };
-template <> struct has_pad<x87c> { static constexpr bool value = true; };
-template <> struct has_pad<x87_pair> { static constexpr bool value = true; };
-
-template <class T> __device__ __forceinline__ void store_fields(T *p, const T &r) { *p = r; }
-template <class V, class K> __device__ __forceinline__ void store_fields(pair_t<V, K> *p, const pair_t<V, K> &r) {
-  p->v = r.v;
-  p->k = r.k;
-}
-__device__ __forceinline__ void store_fields(x87 *p, const x87 &r) { p->m = r.m; p->se = r.se; }
-__device__ __forceinline__ void store_fields(x87c *p, const x87c &r) {
-  store_fields(&p->re, r.re);
-  store_fields(&p->im, r.im);
-}
-__device__ __forceinline__ void store_fields(x87_pair *p, const x87_pair &r) {
-  store_fields(&p->v, r.v);
-  p->k = r.k;
-}
-
 template <class T, class OP>
 __global__ void __launch_bounds__(kBlock)
 k_reduce3_elem(const T *__restrict__ a1, const T *__restrict__ a2, T *__restrict__ o, size_t n) {

@@ -42,11 +42,18 @@ __device__ __forceinline__ void loc_assign(x87 &a, const x87 &b) { a.m = b.m; a.
 
 __device__ __forceinline__ int x87_exp(const x87 &a) { return a.se & 0x7fff; }
 __device__ __forceinline__ int x87_sign(const x87 &a) { return a.se >> 15; }
+// Unsupported encodings (a nonzero exponent with the explicit integer bit
+// clear: unnormals, pseudo-NaNs, pseudo-infinities) are invalid operands
+// since the 387: arithmetic returns the indefinite QNaN whatever the other
+// operand, comparisons are unordered -- so for every test they are NaNs.
+__device__ __forceinline__ bool x87_unsupported(const x87 &a) {
+  return x87_exp(a) != 0 && (a.m >> 63) == 0;
+}
 __device__ __forceinline__ bool x87_isnan(const x87 &a) {
-  return x87_exp(a) == 0x7fff && (a.m << 1) != 0;
+  return (x87_exp(a) == 0x7fff && (a.m << 1) != 0) || x87_unsupported(a);
 }
 __device__ __forceinline__ bool x87_isinf(const x87 &a) {
-  return x87_exp(a) == 0x7fff && (a.m << 1) == 0;
+  return x87_exp(a) == 0x7fff && a.m == (1ull << 63);
 }
 __device__ __forceinline__ bool x87_iszero(const x87 &a) { return x87_exp(a) == 0 && a.m == 0; }
 
@@ -146,6 +153,7 @@ __device__ __forceinline__ void x87_unpack(const x87 &a, uint64_t &m, int &E) {
 }
 
 __device__ __noinline__ x87 x87_add(const x87 &like, const x87 &a, const x87 &b) {
+  if (x87_unsupported(a) || x87_unsupported(b)) return x87_indefinite(like);
   if (x87_isnan(a) || x87_isnan(b)) return x87_nan_result(like, a, b);
   const int sa = x87_sign(a), sb = x87_sign(b);
   if (x87_isinf(a) || x87_isinf(b)) {
@@ -189,11 +197,14 @@ __device__ __forceinline__ x87 x87_neg(const x87 &a) {
   r.se ^= 0x8000;
   return r;
 }
+// fsub does not negate a NaN operand: NaNs propagate with their own sign
 __device__ __forceinline__ x87 x87_sub(const x87 &like, const x87 &a, const x87 &b) {
+  if (x87_isnan(b)) return x87_add(like, a, b);
   return x87_add(like, a, x87_neg(b));
 }
 
 __device__ __noinline__ x87 x87_mul(const x87 &like, const x87 &a, const x87 &b) {
+  if (x87_unsupported(a) || x87_unsupported(b)) return x87_indefinite(like);
   if (x87_isnan(a) || x87_isnan(b)) return x87_nan_result(like, a, b);
   const int s = x87_sign(a) ^ x87_sign(b);
   const bool ia = x87_isinf(a), ib = x87_isinf(b), za = x87_iszero(a), zb = x87_iszero(b);
