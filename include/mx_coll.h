@@ -116,10 +116,31 @@ enum {
     MX_RS_RCCL = 100
 };
 
+/* Rooted reduce algorithm ids == coll_tuned_reduce_algorithm values
+ * (ompi/mca/coll/tuned/coll_tuned_reduce_decision.c:36-45). */
+enum {
+    MX_REDUCE_AUTO = 0,              /* tuned fixed decision (decision_fixed.c:354-429) */
+    MX_REDUCE_LINEAR = 1,
+    MX_REDUCE_CHAIN = 2,             /* fanout MX_REDUCE_CHAIN_FANOUT (tuned default 4,
+                                        coll_tuned_component.c:56) */
+    MX_REDUCE_PIPELINE = 3,
+    MX_REDUCE_BINARY = 4,
+    MX_REDUCE_BINOMIAL = 5,
+    MX_REDUCE_IN_ORDER_BINARY = 6,
+    MX_REDUCE_RABENSEIFNER = 7       /* not provided: MX_ERR_UNSUPPORTED      */
+};
+#define MX_REDUCE_CHAIN_FANOUT 4
+/* Scan / exscan algorithm ids == coll_tuned_{scan,exscan}_algorithm
+ * (coll_tuned_scan_decision.c:29-33).  AUTO = linear: coll/tuned leaves
+ * the scan slots empty (coll_tuned_module.c:106,112), so coll/basic's
+ * linear scan / exscan run (coll_basic_scan.c:43-50, coll_basic_exscan.c:45-52). */
+enum { MX_SCAN_AUTO = 0, MX_SCAN_LINEAR = 1, MX_SCAN_RECURSIVE_DOUBLING = 2 };
+
 /* Returns the algorithm MX_ALLREDUCE_AUTO resolves to for this call shape
  * (the tuned fixed decision), for introspection and tests. */
 int mx_allreduce_decision(int comm_size, size_t count, int type);
 int mx_reduce_scatter_decision(int comm_size, size_t total_count, int type);
+int mx_reduce_decision(int comm_size, size_t count, int type);
 
 /* ---- multi-process (or local rank 0 of a local comm: use *_local) ------- */
 int mx_allreduce(mx_comm_t *comm, const void *sbuf, void *rbuf, size_t count,
@@ -129,6 +150,24 @@ int mx_reduce_scatter(mx_comm_t *comm, const void *sbuf, void *rbuf,
 /* Contiguous byte allgather: rank r's `bytes` land at rbuf + r*bytes. */
 int mx_allgather(mx_comm_t *comm, const void *sbuf, void *rbuf, size_t bytes, void *stream);
 int mx_bcast(mx_comm_t *comm, void *buf, size_t bytes, int root, void *stream);
+
+/* Rooted reduce (coll slot `reduce`, coll.h:239-241): the result lands in
+ * rbuf on `root` only (rbuf may be NULL elsewhere); sbuf MPI_IN_PLACE on
+ * the root.  Bit-identical to the reference algorithm `alg` (the tree of
+ * coll_base_topo.c, the operand roles of coll_base_reduce.c:143-240). */
+int mx_reduce(mx_comm_t *comm, const void *sbuf, void *rbuf, size_t count, int type, int op,
+              int root, int alg, void *stream);
+/* Inclusive / exclusive prefix reductions (slots `scan`, `exscan`,
+ * coll.h:228-230, 248-250).  exscan leaves rank 0's rbuf untouched. */
+int mx_scan(mx_comm_t *comm, const void *sbuf, void *rbuf, size_t count, int type, int op,
+            int alg, void *stream);
+int mx_exscan(mx_comm_t *comm, const void *sbuf, void *rbuf, size_t count, int type, int op,
+              int alg, void *stream);
+/* MPI_Reduce_scatter_block (slot coll.h:245-247): rank r receives block r
+ * (rcount elements) of the reduction, folded as coll/tuned's basic_linear
+ * does it (reduce to rank 0 with the reduce algorithm `alg`, then scatter). */
+int mx_reduce_scatter_block(mx_comm_t *comm, const void *sbuf, void *rbuf, size_t rcount,
+                            int type, int op, int alg, void *stream);
 
 /* ---- OpenSHMEM reductions (shmem_<type>_<op>_to_all) --------------------
  * The OSHMEM op/type numbering (oshmem/op/op.h: OSHMEM_OP_AND..PROD,
@@ -157,6 +196,14 @@ int mx_reduce_scatter_local(mx_comm_t *comm, const void *const *sbufs, void *con
 int mx_allgather_local(mx_comm_t *comm, const void *const *sbufs, void *const *rbufs,
                        size_t bytes, void *stream);
 int mx_bcast_local(mx_comm_t *comm, void *const *bufs, size_t bytes, int root, void *stream);
+int mx_reduce_local(mx_comm_t *comm, const void *const *sbufs, void *const *rbufs, size_t count,
+                    int type, int op, int root, int alg, void *stream);
+int mx_scan_local(mx_comm_t *comm, const void *const *sbufs, void *const *rbufs, size_t count,
+                  int type, int op, int alg, void *stream);
+int mx_exscan_local(mx_comm_t *comm, const void *const *sbufs, void *const *rbufs, size_t count,
+                    int type, int op, int alg, void *stream);
+int mx_reduce_scatter_block_local(mx_comm_t *comm, const void *const *sbufs, void *const *rbufs,
+                                  size_t rcount, int type, int op, int alg, void *stream);
 
 #ifdef __cplusplus
 }

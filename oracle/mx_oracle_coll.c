@@ -584,3 +584,369 @@ int mxo_reduce_scatter(int alg, int op, int type, int n, const size_t *rcounts, 
     for (int r = 0; r < n; r++) free(work[r]);
     return 0;
 }
+
+/* ======================================================================
+ * Rooted reduce, scan, exscan, reduce_scatter_block (TEST INFRASTRUCTURE)
+ * ====================================================================== */
+
+/* ---- topology (coll_base_topo.c), restated ------------------------------ */
+typedef struct { int nnext; int next[MAXN]; } otree_t;
+
+static int o_pown(int fanout, int num)                    /* :34-46 */
+{
+    int p = 1;
+    if (num < 0) return 0;
+    if (num == 1) return fanout;
+    if (fanout == 2) return p << num;
+    for (int j = 0; j < num; j++) p *= fanout;
+    return p;
+}
+static int o_level(int fanout, int rank)                  /* :48-56 */
+{
+    int level, num;
+    if (rank < 0) return -1;
+    for (level = 0, num = 0; num <= rank; level++) num += o_pown(fanout, level);
+    return level - 1;
+}
+static void o_tree(int fanout, int size, int root, int rank, otree_t *t)   /* build_tree :78-175 */
+{
+    int shiftedrank, level, delta;
+    t->nnext = 0;
+    if (size < 2) return;
+    shiftedrank = rank - root;
+    if (shiftedrank < 0) shiftedrank += size;
+    level = o_level(fanout, shiftedrank);
+    delta = o_pown(fanout, level);
+    for (int i = 0; i < fanout; i++) {
+        int schild = shiftedrank + delta * (i + 1);
+        if (schild < size) t->next[t->nnext++] = (schild + root) % size;
+        else break;
+    }
+}
+static void o_in_order_bmtree(int size, int root, int rank, otree_t *t)   /* :403-458 */
+{
+    int vrank = (rank - root + size) % size, mask = 1;
+    t->nnext = 0;
+    while (mask < size) {
+        int remote = vrank ^ mask;
+        if (remote < vrank) break;
+        else if (remote < size) t->next[t->nnext++] = (remote + root) % size;
+        mask <<= 1;
+    }
+}
+static void o_chain(int fanout, int size, int root, int rank, otree_t *t)  /* build_chain :531-673 */
+{
+    int maxchainlen, mark, head, len, srank;
+    if (fanout < 1) fanout = 1;
+    if (fanout > 32) fanout = 32;
+    t->nnext = 0;
+    if ((size - 1) < fanout) fanout = size - 1;
+    srank = rank - root;
+    if (srank < 0) srank += size;
+    if (fanout == 1) {
+        if (srank + 1 < size) t->next[t->nnext++] = (srank + 1 + root) % size;
+        return;
+    }
+    if (size == 1 || fanout < 1) return;
+    maxchainlen = (size - 1) / fanout;
+    if ((size - 1) % fanout != 0) { maxchainlen++; mark = (size - 1) % fanout; }
+    else mark = fanout + 1;
+    if (srank != 0) {
+        if (srank - 1 < mark * maxchainlen) {
+            int column = (srank - 1) / maxchainlen;
+            head = 1 + column * maxchainlen;
+            len = maxchainlen;
+        } else {
+            int column = mark + (srank - 1 - mark * maxchainlen) / (maxchainlen - 1);
+            head = mark * maxchainlen + 1 + (column - mark) * (maxchainlen - 1);
+            len = maxchainlen - 1;
+        }
+        if (srank != head + len - 1 && srank + 1 < size) t->next[t->nnext++] = (srank + 1 + root) % size;
+    } else {
+        t->next[0] = (root + 1) % size;
+        for (int i = 1; i < fanout; i++) {
+            t->next[i] = t->next[i - 1] + maxchainlen;
+            if (i > mark) t->next[i]--;
+            t->next[i] %= size;
+        }
+        t->nnext = fanout;
+    }
+}
+static void o_in_order_bintree(int size, int rank, otree_t *t)            /* :192-295 */
+{
+    int myrank = rank, parent = size - 1, delta = 0, rightsize, lchild, rchild;
+    int n0 = -1, n1 = -1;
+    while (1) {
+        rightsize = size >> 1;
+        lchild = -1;
+        rchild = -1;
+        if (size - 1 > 0) {
+            lchild = parent - 1;
+            if (lchild > 0) rchild = rightsize - 1;
+        }
+        if (myrank == parent) {
+            if (lchild >= 0) n0 = lchild + delta;
+            if (rchild >= 0) n1 = rchild + delta;
+            break;
+        }
+        if (myrank > rchild) {
+            size = size - rightsize - 1;
+            delta = delta + rightsize;
+            myrank = myrank - rightsize;
+            parent = size - 1;
+        } else {
+            size = rightsize;
+            parent = rchild;
+        }
+    }
+    t->nnext = 0;
+    if (n0 >= 0) t->next[t->nnext++] = n0;
+    if (n1 >= 0) t->next[t->nnext++] = n1;
+}
+
+/* tuned fixed reduce decision (coll_tuned_decision_fixed.c:354-429) ->
+ * algorithm id and segment size */
+int mxo_reduce_decision(int n, size_t count, size_t es, int *segsize)
+{
+    const double a1 = 0.6016 / 1024.0, b1 = 1.3496, a2 = 0.0410 / 1024.0, b2 = 9.7128;
+    const double a3 = 0.0422 / 1024.0, b3 = 1.1614, a4 = 0.0033 / 1024.0, b4 = 1.6761;
+    const size_t message_size = es * count;
+    int seg = 0, alg;
+    if (n < 8 && message_size < 512) alg = 1;
+    else if ((n < 8 && message_size < 20480) || message_size < 2048 || count <= 1) { alg = 5; seg = 0; }
+    else if (n > a1 * (double)message_size + b1) { alg = 5; seg = 1024; }
+    else if (n > a2 * (double)message_size + b2) { alg = 3; seg = 1024; }
+    else if (n > a3 * (double)message_size + b3) { alg = 4; seg = 32 * 1024; }
+    else { alg = 3; seg = (n > a4 * (double)message_size + b4) ? 32 * 1024 : 64 * 1024; }
+    if (segsize) *segsize = seg;
+    return alg;
+}
+
+/* ompi_coll_base_reduce_generic (coll_base_reduce.c:62-370), commutative
+ * op, over the tree of `kind`.  Ranks are processed children-first; a
+ * "message" from a child for segment s is the child's accumulator (or, for a
+ * leaf, its sendbuf) for that segment after the child finished it. */
+static int g_tree_kind, g_tree_fanout;
+static void o_tree_of(int n, int root, int rank, otree_t *t)
+{
+    switch (g_tree_kind) {
+    case 2: o_chain(g_tree_fanout, n, root, rank, t); break;
+    case 3: o_chain(1, n, root, rank, t); break;
+    case 4: o_tree(2, n, root, rank, t); break;
+    case 5: o_in_order_bmtree(n, root, rank, t); break;
+    case 6: o_in_order_bintree(n, rank, t); break;
+    default: t->nnext = 0;
+    }
+}
+
+static char *rg_out[MAXN];     /* what rank r sends to its parent */
+static char *rg_free[MAXN];
+
+static void rg_rank(int r, int n, int root, size_t count, size_t segcount, char *const *sendbuf, char *recvbuf,
+                    int inplace_root)
+{
+    otree_t t;
+    o_tree_of(n, root, r, &t);
+    for (int i = 0; i < t.nnext; i++) rg_rank(t.next[i], n, root, count, segcount, sendbuf, recvbuf, inplace_root);
+    if (t.nnext == 0) { rg_out[r] = sendbuf[r]; return; }     /* leaf: sends sendbuf segments */
+    char *accum = (r == root && recvbuf) ? recvbuf : (rg_free[r] = malloc(count * g_es + 1));
+    char *sendtmp = (r == root && inplace_root) ? recvbuf : sendbuf[r];
+    const int role_inplace = (r == root && inplace_root);
+    const size_t nseg = (count + segcount - 1) / segcount;
+    for (size_t s = 0; s < nseg; s++) {
+        const size_t o = s * segcount, cnt = (s == nseg - 1) ? count - o : segcount;
+        if (!role_inplace) {
+            cp(AT(accum, o), AT(rg_out[t.next[0]], o), cnt);          /* irecv child 0 into accumbuf */
+            red(AT(sendtmp, o), AT(accum, o), cnt);                     /* own data onto it (:196-215) */
+            for (int i = 1; i < t.nnext; i++) red(AT(rg_out[t.next[i]], o), AT(accum, o), cnt);
+        } else {                                                        /* accumbuf = recvbuf = own data */
+            for (int i = 0; i < t.nnext; i++) red(AT(rg_out[t.next[i]], o), AT(accum, o), cnt);
+        }
+    }
+    rg_out[r] = accum;
+}
+
+/* reduce_intra_basic_linear (:626-735) */
+static void reduce_linear(int n, size_t count, char *const *sendbuf, char *rbuf)
+{
+    cp(rbuf, sendbuf[n - 1], count);                                   /* from rank size-1 */
+    for (int i = n - 2; i >= 0; --i) red(sendbuf[i], rbuf, count);
+}
+
+/* MPI_Reduce of `count` elements on n simulated ranks.  sbufs[r] may be NULL
+ * only for r == root (MPI_IN_PLACE: the root's data is in rbuf).  alg ids:
+ * 0 tuned decision, 1 linear, 2 chain (fanout 4), 3 pipeline, 4 binary,
+ * 5 binomial, 6 in-order binary. */
+int mxo_reduce(int alg, int op, int type, int n, size_t count, int root, const void *const *sbufs, void *rbuf)
+{
+    char *sb[MAXN];
+    int segsize = 0, inplace;
+    if (n < 1 || n > MAXN || root < 0 || root >= n || !rbuf) return -1;
+    g_op = op; g_type = type; g_es = mxo_type_size(type);
+    if (!g_es) return -1;
+    inplace = !sbufs[root];
+    for (int r = 0; r < n; r++) sb[r] = (char *)(sbufs[r] ? sbufs[r] : rbuf);
+    if (count == 0) return 0;
+    if (n == 1) { if (!inplace) cp(rbuf, sb[0], count); return 0; }
+    if (alg == 0) alg = mxo_reduce_decision(n, count, g_es, &segsize);
+    else segsize = 0;
+    size_t segcount = count;
+    if ((size_t)segsize >= g_es && (size_t)segsize < g_es * segcount) {   /* COMPUTED_SEGCOUNT */
+        segcount = segsize / g_es;
+        if (segsize - segcount * g_es > (g_es >> 1)) segcount++;
+    }
+    if (alg == 1) {
+        if (inplace) {                                                  /* rbuf = temp, copied back */
+            char *tmp = malloc(count * g_es + 1);
+            reduce_linear(n, count, sb, tmp);
+            cp(rbuf, tmp, count);
+            free(tmp);
+        } else {
+            reduce_linear(n, count, sb, rbuf);
+        }
+        return 0;
+    }
+    if (alg < 2 || alg > 6) return -2;
+    g_tree_kind = alg;
+    g_tree_fanout = 4;                                                  /* ompi_coll_tuned_init_chain_fanout */
+    memset(rg_free, 0, sizeof rg_free);
+    if (alg == 6) {
+        /* in-order binary (:509-605): generic rooted at io_root = n-1 */
+        const int io_root = n - 1;
+        char *tmp_send = NULL, *tmp_recv = NULL, *io_recv = (char *)rbuf;
+        int io_inplace = inplace;
+        if (io_root != root) {
+            if (inplace) {                                              /* root: copy rbuf to a temp sendbuf */
+                tmp_send = malloc(count * g_es + 1);
+                cp(tmp_send, rbuf, count);
+                sb[root] = tmp_send;
+                io_inplace = 0;
+            }
+            tmp_recv = malloc(count * g_es + 1);                        /* io_root's temporary recvbuf */
+            io_recv = tmp_recv;
+        }
+        rg_rank(io_root, n, io_root, count, segcount, sb, io_recv, io_inplace);
+        if (io_root != root) cp(rbuf, io_recv, count);                  /* io_root sends the result to root */
+        free(tmp_send);
+        free(tmp_recv);
+    } else {
+        rg_rank(root, n, root, count, segcount, sb, (char *)rbuf, inplace);
+    }
+    for (int r = 0; r < n; r++) free(rg_free[r]);
+    return 0;
+}
+
+/* scan / exscan (coll_base_scan.c, coll_base_exscan.c), alg 0/1 linear,
+ * 2 recursive doubling.  sbufs NULL = MPI_IN_PLACE everywhere. */
+static int scan_common(int alg, int op, int type, int n, size_t count, const void *const *sbufs, void *const *rbufs,
+                       int exclusive)
+{
+    char *sb[MAXN];
+    if (n < 1 || n > MAXN) return -1;
+    g_op = op; g_type = type; g_es = mxo_type_size(type);
+    if (!g_es) return -1;
+    for (int r = 0; r < n; r++) sb[r] = (char *)((sbufs && sbufs[r]) ? sbufs[r] : rbufs[r]);
+    if (count == 0) return 0;
+    if (alg == 0 || alg == 1) {
+        if (!exclusive) {
+            /* rank 0 copies; rank r copies sbuf into rbuf, receives rank r-1's
+             * rbuf and reduces it in (target = own rbuf) (:51-109) */
+            for (int r = 0; r < n; r++) {
+                if (sb[r] != (char *)rbufs[r]) cp(rbufs[r], sb[r], count);
+                if (r > 0) red(rbufs[r - 1], rbufs[r], count);
+            }
+        } else {
+            /* rank r receives rank r-1's reduce_buffer into rbuf; sends
+             * reduce_buffer = sbuf op rbuf (target = own copy) (:57-100) */
+            char *rb_prev = malloc(count * g_es + 1), *rbuf_tmp = malloc(count * g_es + 1);
+            cp(rb_prev, sb[0], count);                                  /* rank 0 sends its sbuf */
+            for (int r = 1; r < n; r++) {
+                cp(rbuf_tmp, rb_prev, count);                           /* what rank r receives */
+                if (r < n - 1) {
+                    char *reduce_buffer = malloc(count * g_es + 1);
+                    cp(reduce_buffer, sb[r], count);
+                    red(rbuf_tmp, reduce_buffer, count);
+                    cp(rb_prev, reduce_buffer, count);
+                    free(reduce_buffer);
+                }
+                cp(rbufs[r], rbuf_tmp, count);
+            }
+            free(rb_prev);
+            free(rbuf_tmp);
+        }
+        return 0;
+    }
+    if (alg != 2) return -2;
+    {
+        char *psend[MAXN], *precv[MAXN], *rb[MAXN];
+        int first[MAXN];
+        for (int r = 0; r < n; r++) {
+            psend[r] = malloc(count * g_es + 1);
+            precv[r] = malloc(count * g_es + 1);
+            rb[r] = malloc(count * g_es + 1);
+            cp(psend[r], sb[r], count);                                 /* exscan :169-175 / scan :173-191 */
+            cp(rb[r], sb[r], count);
+            first[r] = 1;
+        }
+        for (int mask = 1; mask < n; mask <<= 1) {
+            for (int r = 0; r < n; r++) {                               /* sendrecv: snapshot */
+                int remote = r ^ mask;
+                if (remote < n) cp(precv[r], psend[remote], count);
+            }
+            for (int r = 0; r < n; r++) {
+                int remote = r ^ mask;
+                if (remote >= n) continue;
+                if (r > remote) {
+                    if (exclusive && first[r]) { cp(rb[r], precv[r], count); first[r] = 0; }
+                    else red(precv[r], rb[r], count);                   /* recvbuf = precv op recvbuf */
+                    red(precv[r], psend[r], count);
+                } else {
+                    red(precv[r], psend[r], count);                     /* commutative branch */
+                }
+            }
+        }
+        for (int r = exclusive ? 1 : 0; r < n; r++) cp(rbufs[r], rb[r], count);
+        for (int r = 0; r < n; r++) { free(psend[r]); free(precv[r]); free(rb[r]); }
+    }
+    return 0;
+}
+
+int mxo_scan(int alg, int op, int type, int n, size_t count, const void *const *sbufs, void *const *rbufs)
+{
+    return scan_common(alg, op, type, n, count, sbufs, rbufs, 0);
+}
+
+int mxo_exscan(int alg, int op, int type, int n, size_t count, const void *const *sbufs, void *const *rbufs)
+{
+    return scan_common(alg, op, type, n, count, sbufs, rbufs, 1);
+}
+
+/* reduce_scatter_block basic_linear (coll_base_reduce_scatter_block.c:55-110):
+ * coll_reduce to rank 0 (tuned reduce decision on rcount*n; `alg` forces the
+ * reduce algorithm) then a linear scatter.  sbufs NULL = MPI_IN_PLACE. */
+int mxo_reduce_scatter_block(int alg, int op, int type, int n, size_t rcount, const void *const *sbufs,
+                             void *const *rbufs)
+{
+    const void *sb[MAXN];
+    size_t es = mxo_type_size(type);
+    if (n < 1 || n > MAXN || !es) return -1;
+    if (rcount == 0) return 0;
+    for (int r = 0; r < n; r++) sb[r] = (sbufs && sbufs[r]) ? sbufs[r] : rbufs[r];
+    char *full = malloc(rcount * n * es + 1);
+    int rc = mxo_reduce(alg, op, type, n, rcount * n, 0, sb, full);
+    if (rc == 0)
+        for (int r = 0; r < n; r++) memcpy(rbufs[r], full + (size_t)r * rcount * es, rcount * es);
+    free(full);
+    return rc;
+}
+
+/* children of `rank` in the tree of a reduce algorithm (tests print trees) */
+int mxo_reduce_tree(int kind, int n, int root, int rank, int *children)
+{
+    otree_t t;
+    g_tree_kind = kind;
+    g_tree_fanout = 4;
+    o_tree_of(n, root, rank, &t);
+    for (int i = 0; i < t.nnext; i++) children[i] = t.next[i];
+    return t.nnext;
+}

@@ -65,6 +65,11 @@ def gen(t, op, count, seed):
     return rng.integers(0, 256, count * es, dtype=np.uint8)
 
 
+def _tree_oracle():
+    from test_coll_tree import _oracle as tree_oracle
+    return tree_oracle()
+
+
 def _dev(a):
     return torch.from_numpy(np.ascontiguousarray(a)).to("cuda")
 
@@ -247,6 +252,25 @@ def _mp_worker(rank, n, port, staging, jobs, q):
                 x = _dev(gen("UINT8_T", "BAND", count, 7000 + rank))
                 comm.bcast(x.data_ptr(), count, n - 1, st)
                 results.append(x.cpu().numpy().tobytes())
+            elif kind in ("reduce", "reduce_inplace"):
+                root = n - 1 if kind == "reduce" else 0
+                x = _dev(gen(t, op, count, 7000 + rank))
+                out = torch.zeros(count * es, dtype=torch.uint8, device="cuda")
+                if kind == "reduce_inplace" and rank == root:
+                    comm.reduce(mxompi.IN_PLACE, x.data_ptr(), count, t, op, root, alg, st)
+                    out = x
+                else:
+                    comm.reduce(x.data_ptr(), out.data_ptr() if rank == root else 0, count, t, op, root, alg, st)
+                results.append(out.cpu().numpy().tobytes() if rank == root else b"")
+            elif kind in ("scan", "exscan"):
+                x = _dev(gen(t, op, count, 7000 + rank))
+                out = torch.zeros(count * es, dtype=torch.uint8, device="cuda")
+                getattr(comm, kind)(x.data_ptr(), out.data_ptr(), count, t, op, alg, st)
+                results.append(out.cpu().numpy().tobytes())
+            elif kind == "reduce_scatter_block":
+                x = _dev(gen(t, op, count * n, 7000 + rank))
+                comm.reduce_scatter_block(mxompi.IN_PLACE, x.data_ptr(), count, t, op, alg, st)
+                results.append(x.cpu().numpy()[: count * es].tobytes())
         comm.close()
         dist.destroy_process_group()
         q.put((rank, "ok", results))
@@ -295,7 +319,17 @@ def test_multiprocess_ipc_bitexact(n):
             ("allreduce", 17, "SUM", "DOUBLE", "basic_linear"),
             ("allreduce", 200003, "SUM", "FLOAT", "segmented_ring"),   # chunked path in between
             ("allreduce", 2500, "BXOR", "UINT16_T", "auto"),
-            ("allreduce_inplace", 4000, "SUM", "FLOAT", "auto")]
+            ("allreduce_inplace", 4000, "SUM", "FLOAT", "auto"),
+            # rooted reduce / scan / exscan / reduce_scatter_block (VM fold)
+            ("reduce", 100003, "SUM", "FLOAT", "auto"),                 # chunked
+            ("reduce", 3001, "MAX", "DOUBLE", "binary"),
+            ("reduce_inplace", 5000, "MAX", "FLOAT", "binomial"),       # root's IN_PLACE variant
+            ("reduce_inplace", 777, "MAXLOC", "FLOAT_INT", "pipeline"),
+            ("reduce", 999, "SUM", "DOUBLE", "in_order_binary"),
+            ("scan", 20001, "SUM", "FLOAT", "auto"),
+            ("exscan", 4097, "SUM", "DOUBLE", "recursive_doubling"),
+            ("scan", 333, "MIN", "FLOAT", "recursive_doubling"),
+            ("reduce_scatter_block", 3000, "SUM", "FLOAT", "auto")]
     jobs = [(k, c, o or "BAND", t or "UINT8_T", a or "auto") for k, c, o, t, a in jobs]
     got = _run_mp(n, jobs)
     for j, (kind, count, op, t, alg) in enumerate(jobs):
@@ -319,6 +353,39 @@ def test_multiprocess_ipc_bitexact(n):
             for r in range(n):
                 golden_io.assert_coll_equal(np.frombuffer(got[r][j], np.uint8), exp[r], mxompi.OP[op],
                                           mxompi.TYPE[t], f"reduce_scatter {alg} rank {r}")
+        elif kind in ("reduce", "reduce_inplace"):
+            root = n - 1 if kind == "reduce" else 0
+            xs = [gen(t, op, count, 7000 + r) for r in range(n)]
+            exp = np.zeros(count * es, np.uint8)
+            sp = [x.ctypes.data for x in xs]
+            if kind == "reduce_inplace":
+                exp[:] = xs[root]
+                sp[root] = None
+            T = _tree_oracle()
+            assert T.mxo_reduce({"auto": 0, "binary": 4, "binomial": 5, "pipeline": 3, "in_order_binary": 6}[alg],
+                                mxompi.OP[op], mxompi.TYPE[t], n, count, root, (vp * n)(*sp), exp.ctypes.data) == 0
+            golden_io.assert_coll_equal(np.frombuffer(got[root][j], np.uint8), exp, mxompi.OP[op], mxompi.TYPE[t],
+                                        f"{kind} {alg} root {root}")
+        elif kind in ("scan", "exscan"):
+            xs = [gen(t, op, count, 7000 + r) for r in range(n)]
+            exp = [np.zeros(count * es, np.uint8) for _ in range(n)]
+            T = _tree_oracle()
+            fn = T.mxo_scan if kind == "scan" else T.mxo_exscan
+            assert fn(mxompi.SCAN[alg], mxompi.OP[op], mxompi.TYPE[t], n, count,
+                      (vp * n)(*[x.ctypes.data for x in xs]), (vp * n)(*[e.ctypes.data for e in exp])) == 0
+            for r in range(1 if kind == "exscan" else 0, n):
+                golden_io.assert_coll_equal(np.frombuffer(got[r][j], np.uint8), exp[r], mxompi.OP[op],
+                                            mxompi.TYPE[t], f"{kind} {alg} rank {r}")
+        elif kind == "reduce_scatter_block":
+            xs = [gen(t, op, count * n, 7000 + r) for r in range(n)]
+            exp = [np.zeros(count * es, np.uint8) for _ in range(n)]
+            T = _tree_oracle()
+            assert T.mxo_reduce_scatter_block(0, mxompi.OP[op], mxompi.TYPE[t], n, count,
+                                              (vp * n)(*[x.ctypes.data for x in xs]),
+                                              (vp * n)(*[e.ctypes.data for e in exp])) == 0
+            for r in range(n):
+                golden_io.assert_coll_equal(np.frombuffer(got[r][j], np.uint8), exp[r], mxompi.OP[op],
+                                            mxompi.TYPE[t], f"reduce_scatter_block rank {r}")
         elif kind == "allgather":
             full = np.concatenate([gen("UINT8_T", "BAND", count, 7000 + r) for r in range(n)])
             for r in range(n):

@@ -38,150 +38,12 @@
 #include <string.h>
 #include <vector>
 #include <algorithm>
+#include <map>
 
-#include "mx_dispatch.hpp"
-#include "mx_internal.h"
-#include "../../include/mx_coll.h"
+#include "mx_fold.hpp"
 
 namespace mx {
 
-constexpr int MAXR = MX_MAX_RANKS;
-constexpr int kFB = 256;  // fold / copy block size
-
-// ---------------------------------------------------------------------------
-// fold programs
-// ---------------------------------------------------------------------------
-enum { PROG_CHAIN = 0, PROG_BFLY = 1 };
-
-struct FoldProg {
-  int kind;
-  int n;           // chain: number of operands; butterfly: p' leaves
-  int D;           // butterfly depth (p' = 1 << D)
-  int acc_first;   // chain: accumulator is the target (first operand)
-  uint32_t pref;   // butterfly: bit s set -> upper half is the target at level s
-  int8_t ord[MAXR];  // chain: source index per step
-  int8_t la[MAXR];   // butterfly leaf slot i: first operand source
-  int8_t lb[MAXR];   //   second operand source, -1 = plain leaf
-};
-
-struct FoldArgs {
-  const char *src[MAXR];
-  char *dst[MAXR];
-  int ndst;
-  size_t n, head, nvec;  // elements; scalar head; 16-B vectors after head
-  FoldProg p;
-};
-
-template <class T> struct alignas(16) fvec {
-  static constexpr int N = 16 / sizeof(T);
-  T e[N];
-};
-
-template <class OP, class T>
-__device__ __forceinline__ T comb(const T &x, const T &y) { return OP()(x, y); }
-template <class OP, class T>
-__device__ __forceinline__ fvec<T> comb(const fvec<T> &x, const fvec<T> &y) {
-  fvec<T> r;
-#pragma unroll
-  for (int j = 0; j < fvec<T>::N; j++) r.e[j] = OP()(x.e[j], y.e[j]);
-  return r;
-}
-
-// Evaluates the program; LD(j) returns operand j at this lane's position.
-template <class OP, class V, class L>
-__device__ __forceinline__ V eval_prog(const FoldProg &p, L LD) {
-  if (p.kind == PROG_CHAIN) {
-    V acc = LD(p.ord[0]);
-#pragma unroll
-    for (int j = 1; j < MAXR; j++) {
-      if (j < p.n) {
-        const V v = LD(p.ord[j]);
-        acc = p.acc_first ? comb<OP>(acc, v) : comb<OP>(v, acc);
-      }
-    }
-    return acc;
-  }
-  V R[MAXR];
-#pragma unroll
-  for (int i = 0; i < MAXR; i++) {
-    if (i < p.n) {
-      V a = LD(p.la[i]);
-      if (p.lb[i] >= 0) a = comb<OP>(a, LD(p.lb[i]));
-      R[i] = a;
-    }
-  }
-#pragma unroll
-  for (int s = 0; s < 4; s++) {
-    if (s < p.D) {
-      const int h = 1 << s;
-      const bool hi_first = (p.pref >> s) & 1;
-#pragma unroll
-      for (int u = 0; u < MAXR; u += 2 << s) {
-        if (u < p.n) R[u] = hi_first ? comb<OP>(R[u + h], R[u]) : comb<OP>(R[u], R[u + h]);
-      }
-    }
-  }
-  return R[0];
-}
-
-template <class T, class OP>
-__global__ void __launch_bounds__(kFB) k_fold(FoldArgs a) {
-  using V = fvec<T>;
-  constexpr int N = V::N;
-  const size_t tid = (size_t)blockIdx.x * kFB + threadIdx.x;
-  if (N > 0 && tid < a.nvec) {
-    const size_t off = a.head * sizeof(T) + tid * 16;
-    const V r = eval_prog<OP, V>(a.p, [&](int j) { return *reinterpret_cast<const V *>(a.src[j] + off); });
-#pragma unroll
-    for (int d = 0; d < MAXR; d++)
-      if (d < a.ndst) *reinterpret_cast<V *>(a.dst[d] + off) = r;
-  }
-  // scalar elements: the head, the tail, or everything (element path)
-  const size_t tail0 = a.head + a.nvec * N;
-  size_t e = (size_t)-1;
-  if (tid < a.head) e = tid;
-  else if (tid - a.head < a.n - tail0 && tid >= a.head) e = tail0 + (tid - a.head);
-  if (e < a.n) {
-    const size_t off = e * sizeof(T);
-    const T r = eval_prog<OP, T>(a.p, [&](int j) { return *reinterpret_cast<const T *>(a.src[j] + off); });
-#pragma unroll
-    for (int d = 0; d < MAXR; d++)
-      if (d < a.ndst) store_fields(reinterpret_cast<T *>(a.dst[d] + off), r);
-  }
-}
-
-typedef int (*fold_launch_fn)(FoldArgs &, hipStream_t);
-
-template <class T, class OP>
-static int fold_launch(FoldArgs &a, hipStream_t s) {
-  constexpr size_t N = (sizeof(T) <= 16 && 16 % sizeof(T) == 0) ? 16 / sizeof(T) : 0;
-  bool vec = N > 0 && !has_pad<T>::value;   // padded types: field stores, element path
-  uintptr_t m = (uintptr_t)a.src[0] & 15;
-  for (int j = 0; j < MAXR; j++)
-    if (a.src[j] && ((uintptr_t)a.src[j] & 15) != m) vec = false;
-  for (int d = 0; d < a.ndst; d++)
-    if (((uintptr_t)a.dst[d] & 15) != m) vec = false;
-  if (vec && (m % sizeof(T)) != 0) vec = false;
-  if (vec) {
-    size_t head = m ? (16 - m) / sizeof(T) : 0;
-    if (head > a.n) head = a.n;
-    a.head = head;
-    a.nvec = (a.n - head) / (N ? N : 1);
-  } else {
-    a.head = a.n;  // everything scalar (element per lane)
-    a.nvec = 0;
-  }
-  size_t work = a.nvec + a.head + (N ? N : 1);
-  if (!vec) work = a.n;
-  const size_t g = (work + kFB - 1) / kFB;
-  hipLaunchKernelGGL((k_fold<T, OP>), dim3((unsigned)(g ? g : 1)), dim3(kFB), 0, s, a);
-  return mx_check_launch();
-}
-
-struct FoldVisitor {
-  template <class T, class OP2, class OP3> fold_launch_fn go() { return &fold_launch<T, OP2>; }
-  fold_launch_fn none() { return nullptr; }
-};
 
 // ---------------------------------------------------------------------------
 // multi-job byte copy (scatter push, gather, allgather, bcast)
@@ -189,6 +51,7 @@ struct FoldVisitor {
 struct CopyJob { const char *src; char *dst; size_t bytes; };
 struct CopyArgs { CopyJob j[MAXR]; int n; };
 
+template <bool NT>
 __global__ void __launch_bounds__(kFB) k_copy(CopyArgs a) {
   const CopyJob jb = a.j[blockIdx.y];
   const size_t tid = (size_t)blockIdx.x * kFB + threadIdx.x;
@@ -198,7 +61,11 @@ __global__ void __launch_bounds__(kFB) k_copy(CopyArgs a) {
     if (head > jb.bytes) head = jb.bytes;
     const size_t nvec = (jb.bytes - head) / 16;
     if (tid < nvec)
-      reinterpret_cast<uint4 *>(jb.dst + head)[tid] = reinterpret_cast<const uint4 *>(jb.src + head)[tid];
+    {
+      uint4 v;
+      ld16<NT>(v, reinterpret_cast<const uint4 *>(jb.src + head) + tid);
+      st16<NT>(reinterpret_cast<uint4 *>(jb.dst + head) + tid, v);
+    }
     const size_t tail0 = head + nvec * 16;
     if (tid < head) jb.dst[tid] = jb.src[tid];
     if (tid < jb.bytes - tail0) jb.dst[tail0 + tid] = jb.src[tail0 + tid];
@@ -208,34 +75,50 @@ __global__ void __launch_bounds__(kFB) k_copy(CopyArgs a) {
 }
 
 static int copy_launch(CopyArgs &a, hipStream_t s) {
-  size_t maxw = 1;
+  size_t maxw = 1, total = 0;
   int k = 0;
   for (int i = 0; i < a.n; i++) {
     if (a.j[i].bytes == 0) continue;
     a.j[k++] = a.j[i];
     size_t w = a.j[i].bytes / 16 + 32;
     if (w > maxw) maxw = w;
+    total += a.j[i].bytes;
   }
   a.n = k;
   if (k == 0) return MX_SUCCESS;
   const size_t g = (maxw + kFB - 1) / kFB;
-  hipLaunchKernelGGL(k_copy, dim3((unsigned)g, (unsigned)k), dim3(kFB), 0, s, a);
+  if (mx_nt_for(2 * total))
+    hipLaunchKernelGGL(k_copy<true>, dim3((unsigned)g, (unsigned)k), dim3(kFB), 0, s, a);
+  else
+    hipLaunchKernelGGL(k_copy<false>, dim3((unsigned)g, (unsigned)k), dim3(kFB), 0, s, a);
   return mx_check_launch();
+}
+
+// Device-to-device copy on `s` (K7, opal_datatype_copy_content_same_ddt for a
+// contiguous type, opal_datatype_copy.c:99-141): the 16-byte copy kernel when
+// both ends share their misalignment mod 16, else the runtime's copy.
+int copy_async(void *dst, const void *src, size_t bytes, hipStream_t s) {
+  if (!bytes || dst == src) return MX_SUCCESS;
+  if ((((uintptr_t)dst ^ (uintptr_t)src) & 15) == 0) {
+    CopyArgs a;
+    memset(&a, 0, sizeof a);
+    a.j[0] = CopyJob{(const char *)src, (char *)dst, bytes};
+    a.n = 1;
+    return copy_launch(a, s);
+  }
+  return mx_hip_rc(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToDevice, s));
 }
 
 // ---------------------------------------------------------------------------
 // cross-GPU flags: generation-tagged, system scope, bounded spin
 // ---------------------------------------------------------------------------
-enum { FLAG_READY = 0, FLAG_PUSHED = 1, FLAG_DONE = 2, NFLAGS = 3 };
 
 // one-shot small-message allreduce: per (source rank, workgroup) READY flags
 // after the NFLAGS x MAXR block, then one local completion counter.
-constexpr int OSWG = 16;
 constexpr size_t OS_FLAG_BASE = NFLAGS * MAXR;
 constexpr size_t OS_COUNTER = OS_FLAG_BASE + (size_t)MAXR * OSWG;
 constexpr size_t FLAG_WORDS = OS_COUNTER + 8;
 constexpr size_t kOneShotMax = 64 << 10;   // bytes per rank
-constexpr int OS_MAXSEG = 16;
 
 struct SignalArgs { uint64_t *peer_flag[MAXR]; int n; uint64_t value; };
 
@@ -262,112 +145,6 @@ __global__ void k_wait(const uint64_t *flags, uint32_t mask, uint64_t value, uin
   __syncthreads();
   __atomic_thread_fence(__ATOMIC_ACQUIRE);
 }
-
-// ---------------------------------------------------------------------------
-// one-shot allreduce for small messages: ONE launch per call.  Workgroup w
-// owns element slice w: it pushes that slice of my contribution into every
-// peer's one-shot slot (double-buffered by generation parity), raises READY
-// (source=me, slice=w) at each peer, waits for every peer's READY for slice
-// w, and folds the slice for the WHOLE vector from the n copies (every rank
-// evaluates the same fold program per element, so all ranks agree bit for
-// bit).  Reuse of a parity buffer needs the peer to have finished gen-2,
-// i.e. DONE >= gen-2; the last workgroup to finish raises DONE(gen).
-// ---------------------------------------------------------------------------
-struct OsSeg { size_t lo, hi; FoldProg p; };
-struct OneShotArgs {
-  const char *sb;
-  char *rb;
-  char *peer_slot[MAXR];        // peer p's buffer (this parity) at my slot; null for me
-  const char *src[MAXR];        // operand j: my buffer (this parity) slot j; src[rank] = sb
-  uint64_t *peer_ready[MAXR];   // peer p's OS READY row for source = me
-  uint64_t *peer_done[MAXR];    // peer p's DONE flag for source = me
-  const uint64_t *my_ready;     // my OS READY rows [src][wg]
-  const uint64_t *my_done;      // my DONE flags [src]
-  uint64_t *counter;
-  uint64_t counter_last, gen, timeout_ticks;
-  int *err;
-  int n, rank, nseg;
-  size_t count, es, slice;
-  OsSeg seg[OS_MAXSEG];
-};
-
-constexpr int kOSB = 256;
-
-__device__ __forceinline__ void os_spin(const uint64_t *f, uint64_t v, uint64_t ticks, int *err) {
-  const uint64_t t0 = wall_clock64();
-  while (__hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) < v) {
-    __builtin_amdgcn_s_sleep(1);
-    if (wall_clock64() - t0 > ticks) {
-      __hip_atomic_store(err, MX_ERR_TIMEOUT, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-      break;
-    }
-  }
-}
-
-template <class T, class OP>
-__global__ void __launch_bounds__(kOSB) k_oneshot(OneShotArgs a) {
-  const int w = blockIdx.x, t = threadIdx.x;
-  const size_t lo = (size_t)w * a.slice, hi = lo + a.slice < a.count ? lo + a.slice : a.count;
-  // (1) every peer is past gen-2: its reads of this parity buffer are over
-  if (t < a.n && t != a.rank && a.gen > 2) os_spin(a.my_done + t, a.gen - 2, a.timeout_ticks, a.err);
-  __syncthreads();
-  // (2) push my slice (bytes [lo*es, hi*es)) to every peer
-  if (lo < hi) {
-    const size_t b0 = lo * a.es, b1 = hi * a.es;
-    const bool vec = (((uintptr_t)a.sb | b0 | b1) & 15) == 0;
-    for (int p = 0; p < a.n; p++) {
-      if (p == a.rank) continue;
-      char *d = a.peer_slot[p];
-      if (vec) {
-        for (size_t i = b0 / 16 + t; i < b1 / 16; i += kOSB)
-          reinterpret_cast<uint4 *>(d)[i] = reinterpret_cast<const uint4 *>(a.sb)[i];
-      } else {
-        for (size_t i = b0 + t; i < b1; i += kOSB) d[i] = a.sb[i];
-      }
-    }
-  }
-  __threadfence_system();
-  __syncthreads();
-  // (3) READY(me, w) at every peer; (4) wait READY(p, w) from every peer
-  if (t < a.n && t != a.rank) {
-    __hip_atomic_store(a.peer_ready[t] + w, a.gen, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
-    os_spin(a.my_ready + (size_t)t * OSWG + w, a.gen, a.timeout_ticks, a.err);
-  }
-  __syncthreads();
-  __atomic_thread_fence(__ATOMIC_ACQUIRE);
-  // (5) fold the slice
-  int sidx = 0;
-  for (size_t e = lo + t; e < hi; e += kOSB) {
-    while (sidx + 1 < a.nseg && e >= a.seg[sidx].hi) sidx++;
-    const size_t off = e * sizeof(T);
-    const T r = eval_prog<OP, T>(a.seg[sidx].p, [&](int j) { return *reinterpret_cast<const T *>(a.src[j] + off); });
-    store_fields(reinterpret_cast<T *>(a.rb + off), r);
-  }
-  // (6) the last workgroup out raises DONE(gen) at every peer
-  __syncthreads();
-  if (t == 0) {
-    __threadfence();
-    const uint64_t old = __hip_atomic_fetch_add(a.counter, (uint64_t)1, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
-    if (old == a.counter_last) {
-      __threadfence_system();
-      for (int p = 0; p < a.n; p++)
-        if (p != a.rank) __hip_atomic_store(a.peer_done[p], a.gen, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
-    }
-  }
-}
-
-typedef int (*oneshot_launch_fn)(OneShotArgs &, int nwg, hipStream_t);
-
-template <class T, class OP>
-static int oneshot_launch(OneShotArgs &a, int nwg, hipStream_t s) {
-  hipLaunchKernelGGL((k_oneshot<T, OP>), dim3(nwg), dim3(kOSB), 0, s, a);
-  return mx_check_launch();
-}
-
-struct OneShotVisitor {
-  template <class T, class OP2, class OP3> oneshot_launch_fn go() { return &oneshot_launch<T, OP2>; }
-  oneshot_launch_fn none() { return nullptr; }
-};
 
 }  // namespace mx
 
@@ -807,8 +584,7 @@ extern "C" int mx_reduce_scatter_decision(int n, size_t total_count, int type) {
 extern "C" int mx_allreduce_local(mx_comm_t *c, const void *const *sbufs, void *const *rbufs, size_t count,
                                   int type, int op, int alg, void *stream) {
   if (!c || !c->local || !rbufs) return MX_ERR_ARG;
-  FoldVisitor fv;
-  fold_launch_fn fl = dispatch(op, type, fv);
+  fold_launch_fn fl = fold_fns(op, type).fold;
   if (!fl) return MX_ERR_UNSUPPORTED;
   const size_t es = mx_type_size(type);
   const int n = c->size;
@@ -822,8 +598,7 @@ extern "C" int mx_allreduce_local(mx_comm_t *c, const void *const *sbufs, void *
     dst[j] = (char *)rbufs[j];
   }
   if (n == 1) {
-    if (src[0] != dst[0] && hipMemcpyAsync(dst[0], src[0], count * es, hipMemcpyDeviceToDevice, s) != hipSuccess)
-      return MX_ERR_HIP;
+    if (int rc = copy_async(dst[0], src[0], count * es, s)) return rc;
     return finish(c, s);
   }
   size_t off[MAXR], len[MAXR];
@@ -846,8 +621,7 @@ extern "C" int mx_allreduce_local(mx_comm_t *c, const void *const *sbufs, void *
 extern "C" int mx_reduce_scatter_local(mx_comm_t *c, const void *const *sbufs, void *const *rbufs,
                                        const size_t *rcounts, int type, int op, int alg, void *stream) {
   if (!c || !c->local || !rbufs || !rcounts) return MX_ERR_ARG;
-  FoldVisitor fv;
-  fold_launch_fn fl = dispatch(op, type, fv);
+  fold_launch_fn fl = fold_fns(op, type).fold;
   if (!fl) return MX_ERR_UNSUPPORTED;
   const size_t es = mx_type_size(type);
   const int n = c->size;
@@ -860,9 +634,7 @@ extern "C" int mx_reduce_scatter_local(mx_comm_t *c, const void *const *sbufs, v
     src[j] = (const char *)sb;
   }
   if (n == 1) {
-    if (src[0] != rbufs[0] && total &&
-        hipMemcpyAsync(rbufs[0], src[0], total * es, hipMemcpyDeviceToDevice, s) != hipSuccess)
-      return MX_ERR_HIP;
+    if (int rc = copy_async(rbufs[0], src[0], total * es, s)) return rc;
     return finish(c, s);
   }
   // IN_PLACE (or rbuf aliasing sbuf): rank p's result lands at rbufs[p][0..)
@@ -1069,12 +841,10 @@ extern "C" int mx_allreduce(mx_comm_t *c, const void *sbuf, void *rbuf, size_t c
     if (ncclAllReduce(sb, rb, count, dt, ro, c->nccl, s) != ncclSuccess) return MX_ERR_RCCL;
     return finish(c, s);
   }
-  FoldVisitor fv;
-  fold_launch_fn fl = dispatch(op, type, fv);
+  fold_launch_fn fl = fold_fns(op, type).fold;
   if (!fl) return MX_ERR_UNSUPPORTED;
   if (n == 1) {
-    if (sb != rb && hipMemcpyAsync(rb, sb, count * es, hipMemcpyDeviceToDevice, s) != hipSuccess)
-      return MX_ERR_HIP;
+    if (int rc = copy_async(rb, sb, count * es, s)) return rc;
     return finish(c, s);
   }
   if (!(c->flags & MX_COMM_IPC)) return MX_ERR_STATE;
@@ -1082,8 +852,7 @@ extern "C" int mx_allreduce(mx_comm_t *c, const void *sbuf, void *rbuf, size_t c
     std::vector<Seg> segs;
     int rc = allreduce_segments(alg, n, count, es, 0, count, segs);
     if (rc) return rc;
-    OneShotVisitor ov;
-    oneshot_launch_fn ol = dispatch(op, type, ov);
+    oneshot_launch_fn ol = fold_fns(op, type).oneshot;
     if (ol && segs.size() <= (size_t)OS_MAXSEG) return allreduce_oneshot(c, ol, segs, sb, rb, count, es, s);
   }
   {  // validate the algorithm once for the whole vector
@@ -1112,8 +881,8 @@ extern "C" int mx_allreduce(mx_comm_t *c, const void *sbuf, void *rbuf, size_t c
     prof_begin(c, s);
     if ((rc = copy_launch(ca, s))) return rc;
     prof_end(c, s, 1, 0);
-    if ((rc = signal_all(c, FLAG_READY, g, s))) return rc;
-    if ((rc = wait_all(c, FLAG_READY, g, s))) return rc;
+    if ((rc = signal_all(c, FLAG_READY, g << 1, s))) return rc;
+    if ((rc = wait_all(c, FLAG_READY, g << 1, s))) return rc;
     // (c) fold my part, store to my rbuf and every peer's gather area
     if (len[r]) {
       const size_t e0 = c0 + off[r];
@@ -1164,12 +933,10 @@ extern "C" int mx_reduce_scatter(mx_comm_t *c, const void *sbuf, void *rbuf, con
   size_t disp[MAXR], total = 0, maxc = 0;
   for (int j = 0; j < n; j++) { disp[j] = total; total += rcounts[j]; maxc = std::max(maxc, rcounts[j]); }
   if (total == 0) return MX_SUCCESS;
-  FoldVisitor fv;
-  fold_launch_fn fl = dispatch(op, type, fv);
+  fold_launch_fn fl = fold_fns(op, type).fold;
   if (!fl) return MX_ERR_UNSUPPORTED;
   if (n == 1) {
-    if (sb != rbuf && hipMemcpyAsync(rbuf, sb, total * es, hipMemcpyDeviceToDevice, s) != hipSuccess)
-      return MX_ERR_HIP;
+    if (int rc = copy_async(rbuf, sb, total * es, s)) return rc;
     return finish(c, s);
   }
   if (!(c->flags & MX_COMM_IPC)) return MX_ERR_STATE;
@@ -1188,8 +955,8 @@ extern "C" int mx_reduce_scatter(mx_comm_t *c, const void *sbuf, void *rbuf, con
                            rcounts[p] * es};
   }
   if ((rc = copy_launch(ca, s))) return rc;
-  if ((rc = signal_all(c, FLAG_READY, g, s))) return rc;
-  if ((rc = wait_all(c, FLAG_READY, g, s))) return rc;
+  if ((rc = signal_all(c, FLAG_READY, g << 1, s))) return rc;
+  if ((rc = wait_all(c, FLAG_READY, g << 1, s))) return rc;
   if (rcounts[r]) {
     const size_t mis = (disp[r] * es) & 15;
     const char *sp[MAXR];
@@ -1227,7 +994,7 @@ extern "C" int mx_allgather(mx_comm_t *c, const void *sbuf, void *rbuf, size_t b
   const char *sb = (sbuf == MX_IN_PLACE || !sbuf) ? rb + (size_t)r * bytes : (const char *)sbuf;
   if (!bytes) return MX_SUCCESS;
   if (n == 1) {
-    if (sb != rb && hipMemcpyAsync(rb, sb, bytes, hipMemcpyDeviceToDevice, s) != hipSuccess) return MX_ERR_HIP;
+    if (int rc = copy_async(rb, sb, bytes, s)) return rc;
     return finish(c, s);
   }
   if (!(c->flags & MX_COMM_IPC)) return MX_ERR_STATE;
@@ -1246,8 +1013,8 @@ extern "C" int mx_allgather(mx_comm_t *c, const void *sbuf, void *rbuf, size_t b
       if (p != r) ca.j[ca.n++] = CopyJob{sb + o, c->peer_staging[p] + (size_t)r * slot + ((r * bytes + o) & 15), l};
     if (sb != rb + (size_t)r * bytes) ca.j[ca.n++] = CopyJob{sb + o, rb + (size_t)r * bytes + o, l};
     if ((rc = copy_launch(ca, s))) return rc;
-    if ((rc = signal_all(c, FLAG_READY, g, s))) return rc;
-    if ((rc = wait_all(c, FLAG_READY, g, s))) return rc;
+    if ((rc = signal_all(c, FLAG_READY, g << 1, s))) return rc;
+    if ((rc = wait_all(c, FLAG_READY, g << 1, s))) return rc;
     memset(&ca, 0, sizeof ca);
     for (int p = 0; p < n; p++)
       if (p != r)
@@ -1281,15 +1048,710 @@ extern "C" int mx_bcast(mx_comm_t *c, void *buf, size_t bytes, int root, void *s
       for (int p = 0; p < n; p++)
         if (p != r) ca.j[ca.n++] = CopyJob{(const char *)buf + o, c->peer_staging[p] + (o & 15), l};
       if ((rc = copy_launch(ca, s))) return rc;
-      if ((rc = signal_all(c, FLAG_READY, g, s))) return rc;
+      if ((rc = signal_all(c, FLAG_READY, g << 1, s))) return rc;
     } else {
-      if ((rc = wait_mask(c, FLAG_READY, 1u << root, g, s))) return rc;
+      if ((rc = wait_mask(c, FLAG_READY, 1u << root, g << 1, s))) return rc;
       CopyArgs ca;
       memset(&ca, 0, sizeof ca);
       ca.j[ca.n++] = CopyJob{c->staging + (o & 15), (char *)buf + o, l};
       if ((rc = copy_launch(ca, s))) return rc;
     }
     if ((rc = signal_all(c, FLAG_DONE, g, s))) return rc;
+  }
+  return finish(c, s);
+}
+
+// ---------------------------------------------------------------------------
+// rooted reduce, scan, exscan, reduce_scatter_block.
+//
+// The reference runs these as trees / chains of point-to-point steps
+// (coll_base_reduce.c, coll_base_scan.c, coll_base_exscan.c,
+// coll_base_reduce_scatter_block.c).  Here the per-element reduction order
+// of the selected algorithm is derived on the host as an expression DAG over
+// the n contributions -- restating the reference's topology builders
+// (coll_base_topo.c) and operand roles -- compiled to a VM program
+// (mx_fold.hpp k_vm), and evaluated by the owner of each element part after
+// an all-peer exchange, exactly like the allreduce.  Expression nodes are
+// COMB(target, source) = ompi_op_reduce(op, source, target).
+// ---------------------------------------------------------------------------
+namespace {
+
+// output: expression -> destination rank (-1 = the part's owner), guard 0
+// always / VM_IF_SET / VM_IF_CLEAR (the root's MPI_IN_PLACE variant)
+struct DagOut { int e, dst, guard; };
+struct Dag {
+  int n;
+  std::vector<std::pair<int, int>> node;     // node id n + i = COMB(first, second)
+  std::map<std::pair<int, int>, int> memo;   // structural sharing
+  std::vector<DagOut> out;
+  explicit Dag(int n_) : n(n_) {}
+  void emit(int e, int dst, int guard = 0) { out.push_back(DagOut{e, dst, guard}); }
+  int comb(int target, int source) {
+    const auto k = std::make_pair(target, source);
+    const auto it = memo.find(k);
+    if (it != memo.end()) return it->second;
+    const int id = n + (int)node.size();
+    node.push_back(k);
+    memo[k] = id;
+    return id;
+  }
+};
+
+// Program: EMITs of bare contributions first, then each needed node in
+// creation order (children precede parents) followed by its EMITs.
+// Registers: contribution j starts in r_j; a register is released after its
+// last use and reused by the next definition.
+static int dag_compile(const Dag &g, int owner, VmProg &p) {
+  const int n = g.n, m = (int)g.node.size(), tot = n + m;
+  // need[i]: bit 0 = needed when the info bit is set, bit 1 = when clear
+  std::vector<int> need(tot, 0);
+  for (const auto &o : g.out) need[o.e] |= o.guard == VM_IF_SET ? 1 : o.guard == VM_IF_CLEAR ? 2 : 3;
+  for (int i = tot - 1; i >= n; i--)
+    if (need[i]) {
+      need[g.node[i - n].first] |= need[i];
+      need[g.node[i - n].second] |= need[i];
+    }
+  auto guard_of = [](int nd) { return nd == 1 ? (int)VM_IF_SET : nd == 2 ? (int)VM_IF_CLEAR : 0; };
+  struct Ins { int op, d, a, b, guard; };
+  std::vector<Ins> seq;
+  for (const auto &o : g.out)
+    if (o.e < n) seq.push_back({VM_EMIT, o.dst < 0 ? owner : o.dst, o.e, -1, o.guard});
+  for (int i = n; i < tot; i++) {
+    if (!need[i]) continue;
+    seq.push_back({VM_COMB, i, g.node[i - n].first, g.node[i - n].second, guard_of(need[i])});
+    for (const auto &o : g.out)
+      if (o.e == i) seq.push_back({VM_EMIT, o.dst < 0 ? owner : o.dst, i, -1, o.guard});
+  }
+  if ((int)seq.size() > VM_MAXI) return MX_ERR_UNSUPPORTED;
+  std::vector<int> last(tot, -1);
+  for (int k = 0; k < (int)seq.size(); k++) {
+    last[seq[k].a] = k;
+    if (seq[k].op == VM_COMB) last[seq[k].b] = k;
+  }
+  // registers: contribution j starts in r_j; a register is released after
+  // its last use (in program order -- guarded-out instructions only skip
+  // values nothing live depends on) and reused by the next definition
+  std::vector<int> reg(tot, -1), free_regs;
+  int nregs = n;
+  for (int j = 0; j < n; j++) reg[j] = j;
+  memset(&p, 0, sizeof p);
+  p.nsrc = n;
+  for (int k = 0; k < (int)seq.size(); k++) {
+    const Ins &q = seq[k];
+    VmIns &o = p.ins[p.nins++];
+    o.op = (int8_t)(q.op | q.guard);
+    o.a = (int8_t)reg[q.a];
+    if (q.op == VM_EMIT) {
+      o.d = (int8_t)q.d;
+      o.b = 0;
+      if (last[q.a] == k) free_regs.push_back(reg[q.a]);
+      continue;
+    }
+    o.b = (int8_t)reg[q.b];
+    if (last[q.a] == k) free_regs.push_back(reg[q.a]);   // operands are read before the result is written
+    if (last[q.b] == k && q.b != q.a) free_regs.push_back(reg[q.b]);
+    int r;
+    if (!free_regs.empty()) {
+      r = free_regs.back();
+      free_regs.pop_back();
+    } else {
+      r = nregs++;
+    }
+    reg[q.d] = r;
+    o.d = (int8_t)r;
+  }
+  p.nregs = nregs;
+  return nregs > VM_MAXREG ? MX_ERR_UNSUPPORTED : MX_SUCCESS;
+}
+
+// ---- topology builders (ompi/mca/coll/base/coll_base_topo.c) -------------
+static int t_pown(int fanout, int num) {           // pown (:34-46)
+  if (num < 0) return 0;
+  if (num == 1) return fanout;
+  int p = 1;
+  for (int j = 0; j < num; j++) p *= fanout;
+  return p;
+}
+static int t_level(int fanout, int rank) {         // calculate_level (:48-56)
+  int level, num;
+  if (rank < 0) return -1;
+  for (level = 0, num = 0; num <= rank; level++) num += t_pown(fanout, level);
+  return level - 1;
+}
+// ompi_coll_base_topo_build_tree (:78-175): children of `rank`, in order
+static std::vector<int> topo_tree(int fanout, int n, int root, int rank) {
+  std::vector<int> ch;
+  if (n < 2) return ch;
+  int sr = rank - root;
+  if (sr < 0) sr += n;
+  const int level = t_level(fanout, sr), delta = t_pown(fanout, level);
+  for (int i = 0; i < fanout; i++) {
+    const int sc = sr + delta * (i + 1);
+    if (sc < n) ch.push_back((sc + root) % n);
+    else break;
+  }
+  return ch;
+}
+// ompi_coll_base_topo_build_in_order_bmtree (:403-458)
+static std::vector<int> topo_in_order_bmtree(int n, int root, int rank) {
+  std::vector<int> ch;
+  const int vrank = (rank - root + n) % n;
+  for (int mask = 1; mask < n; mask <<= 1) {
+    const int remote = vrank ^ mask;
+    if (remote < vrank) break;
+    if (remote < n) ch.push_back((remote + root) % n);
+  }
+  return ch;
+}
+// ompi_coll_base_topo_build_chain (:531-673)
+static std::vector<int> topo_chain(int fanout, int n, int root, int rank) {
+  std::vector<int> ch;
+  if (fanout < 1) fanout = 1;
+  if (fanout > 32) fanout = 32;                    // MAXTREEFANOUT
+  if (n - 1 < fanout) fanout = n - 1;
+  const int srank = (rank - root + n) % n;
+  if (fanout == 1) {
+    if (srank + 1 < n) ch.push_back((srank + 1 + root) % n);
+    return ch;
+  }
+  if (n == 1 || fanout < 1) return ch;
+  int maxchainlen = (n - 1) / fanout, mark;
+  if ((n - 1) % fanout != 0) {
+    maxchainlen++;
+    mark = (n - 1) % fanout;
+  } else {
+    mark = fanout + 1;
+  }
+  if (srank != 0) {
+    int head, len;
+    if (srank - 1 < mark * maxchainlen) {
+      const int column = (srank - 1) / maxchainlen;
+      head = 1 + column * maxchainlen;
+      len = maxchainlen;
+    } else {
+      const int column = mark + (srank - 1 - mark * maxchainlen) / (maxchainlen - 1);
+      head = mark * maxchainlen + 1 + (column - mark) * (maxchainlen - 1);
+      len = maxchainlen - 1;
+    }
+    if (srank != head + len - 1 && srank + 1 < n) ch.push_back((srank + 1 + root) % n);
+  } else {
+    int prev = (root + 1) % n;
+    ch.push_back(prev);
+    for (int i = 1; i < fanout; i++) {
+      int nx = prev + maxchainlen;
+      if (i > mark) nx--;
+      nx %= n;
+      ch.push_back(nx);
+      prev = nx;
+    }
+  }
+  return ch;
+}
+// ompi_coll_base_topo_build_in_order_bintree (:192-295); root is n - 1
+static std::vector<int> topo_in_order_bintree(int n, int rank) {
+  int size = n, myrank = rank, parent = n - 1, delta = 0, next0 = -1, next1 = -1;
+  while (true) {
+    const int rightsize = size >> 1;
+    int lchild = -1, rchild = -1;
+    if (size - 1 > 0) {
+      lchild = parent - 1;
+      if (lchild > 0) rchild = rightsize - 1;
+    }
+    if (myrank == parent) {
+      if (lchild >= 0) next0 = lchild + delta;
+      if (rchild >= 0) next1 = rchild + delta;
+      break;
+    }
+    if (myrank > rchild) {
+      size = size - rightsize - 1;
+      delta = delta + rightsize;
+      myrank = myrank - rightsize;
+      parent = size - 1;
+    } else {
+      size = rightsize;
+      parent = rchild;
+    }
+  }
+  std::vector<int> ch;
+  if (next0 >= 0) ch.push_back(next0);
+  if (next1 >= 0) ch.push_back(next1);
+  return ch;
+}
+
+// ompi_coll_base_reduce_generic (coll_base_reduce.c:143-240), commutative
+// op: a node folds its first child's partial result with its own data
+// (child = target, :159-172 + :196-205), then every further child onto that
+// accumulator; the root with MPI_IN_PLACE keeps its own data as the target.
+template <class CH>
+static int reduce_generic_expr(Dag &g, int v, int root, bool root_inplace, const CH &children, int depth) {
+  if (depth > g.n) return -1;   // malformed tree
+  const std::vector<int> ch = children(v);
+  if (ch.empty()) return v;
+  int acc;
+  size_t i0;
+  if (v == root && root_inplace) { acc = v; i0 = 0; }
+  else {
+    const int c0 = reduce_generic_expr(g, ch[0], root, root_inplace, children, depth + 1);
+    if (c0 < 0) return -1;
+    acc = g.comb(c0, v);
+    i0 = 1;
+  }
+  for (size_t i = i0; i < ch.size(); i++) {
+    const int ci = reduce_generic_expr(g, ch[i], root, root_inplace, children, depth + 1);
+    if (ci < 0) return -1;
+    acc = g.comb(acc, ci);
+  }
+  return acc;
+}
+
+// The fold expression of MPI_Reduce(root) under algorithm `alg`
+// (coll_tuned_reduce_decision.c:36-45 numbering).
+static int reduce_expr(Dag &g, int alg, int root, bool root_inplace) {
+  const int n = g.n;
+  switch (alg) {
+    case MX_REDUCE_LINEAR: {           // basic_linear (:699-722): rbuf = x_{n-1}; rbuf op= x_i
+      int acc = n - 1;
+      for (int i = n - 2; i >= 0; i--) acc = g.comb(acc, i);
+      return acc;
+    }
+    case MX_REDUCE_CHAIN:
+      return reduce_generic_expr(g, root, root, root_inplace,
+                                 [&](int v) { return topo_chain(MX_REDUCE_CHAIN_FANOUT, n, root, v); }, 0);
+    case MX_REDUCE_PIPELINE:
+      return reduce_generic_expr(g, root, root, root_inplace, [&](int v) { return topo_chain(1, n, root, v); }, 0);
+    case MX_REDUCE_BINARY:
+      return reduce_generic_expr(g, root, root, root_inplace, [&](int v) { return topo_tree(2, n, root, v); }, 0);
+    case MX_REDUCE_BINOMIAL:
+      return reduce_generic_expr(g, root, root, root_inplace,
+                                 [&](int v) { return topo_in_order_bmtree(n, root, v); }, 0);
+    case MX_REDUCE_IN_ORDER_BINARY: {
+      // reduce_intra_in_order_binary (:509-605): generic over the in-order
+      // binary tree rooted at n-1; the real root's MPI_IN_PLACE data is
+      // copied to a temporary unless n-1 is the root
+      const int io_root = n - 1;
+      return reduce_generic_expr(g, io_root, io_root, root_inplace && io_root == root,
+                                 [&](int v) { return topo_in_order_bintree(n, v); }, 0);
+    }
+    default:
+      return -2;
+  }
+}
+
+// root_inplace: 0 no, 1 yes, 2 unknown here (multi-process part owners):
+// both variants, guarded by the root's info bit, sharing every subtree
+static int reduce_dag(Dag &g, int alg, size_t count, size_t es, int root, int root_inplace) {
+  if (alg == MX_REDUCE_AUTO) alg = mx_reduce_decision(g.n, count, -(int)es);
+  if (g.n == 1) {
+    g.emit(0, root);
+    return MX_SUCCESS;
+  }
+  const int e1 = root_inplace != 0 ? reduce_expr(g, alg, root, true) : -3;
+  const int e0 = root_inplace != 1 ? reduce_expr(g, alg, root, false) : -3;
+  if (e1 == -2 || e0 == -2) return MX_ERR_UNSUPPORTED;
+  if (e1 == -1 || e0 == -1) return MX_ERR_ARG;
+  if (root_inplace == 1) g.emit(e1, root);
+  else if (root_inplace == 0 || e0 == e1) g.emit(e0, root);
+  else {
+    g.emit(e1, root, VM_IF_SET);
+    g.emit(e0, root, VM_IF_CLEAR);
+  }
+  return MX_SUCCESS;
+}
+
+// MPI_Scan: linear (coll_base_scan.c:35-122; coll/basic's scan) and
+// recursive doubling (:157-230, commutative branch).
+static int scan_dag(Dag &g, int alg, bool exclusive) {
+  const int n = g.n;
+  if (alg == MX_SCAN_AUTO) alg = MX_SCAN_LINEAR;   // tuned has no fixed scan/exscan: coll/basic (linear)
+  if (alg == MX_SCAN_LINEAR) {
+    if (!exclusive) {                 // rbuf_r = x_r; rbuf_r op= rbuf_{r-1} (target = own data)
+      int acc = 0;
+      g.emit(0, 0);
+      for (int r = 1; r < n; r++) {
+        acc = g.comb(r, acc);
+        g.emit(acc, r);
+      }
+    } else if (n > 1) {               // exscan linear (coll_base_exscan.c:35-107)
+      int acc = 0;                    // rank 1 receives x_0
+      g.emit(0, 1);
+      for (int r = 2; r < n; r++) {   // rank r-1 sends reduce_buffer = x_{r-1} op rbuf_{r-1}
+        acc = g.comb(r - 1, acc);
+        g.emit(acc, r);
+      }
+    }
+    return MX_SUCCESS;
+  }
+  if (alg != MX_SCAN_RECURSIVE_DOUBLING) return MX_ERR_UNSUPPORTED;
+  std::vector<int> rbuf(n), psend(n), prev(n);
+  std::vector<char> first(n, 1);
+  for (int r = 0; r < n; r++) rbuf[r] = psend[r] = r;
+  for (int mask = 1; mask < n; mask <<= 1) {
+    prev = psend;                     // sendrecv: every rank sends its psend before reducing
+    for (int r = 0; r < n; r++) {
+      const int remote = r ^ mask;
+      if (remote >= n) continue;
+      const int precv = prev[remote];
+      if (r > remote) {
+        if (exclusive && first[r]) { rbuf[r] = precv; first[r] = 0; }   // exscan :191-195
+        else rbuf[r] = g.comb(rbuf[r], precv);                          // recvbuf = precv op recvbuf
+      }
+      psend[r] = g.comb(psend[r], precv);                               // psend = precv op psend
+    }
+  }
+  for (int r = exclusive ? 1 : 0; r < n; r++) g.emit(rbuf[r], r);
+  return MX_SUCCESS;
+}
+
+}  // namespace
+
+extern "C" int mx_reduce_decision(int n, size_t count, int type) {
+  // ompi_coll_tuned_reduce_intra_dec_fixed (coll_tuned_decision_fixed.c:354-429),
+  // commutative ops (every predefined MPI_Op)
+  const size_t es = type < 0 ? (size_t)(-type) : mx_type_size(type);
+  const double a1 = 0.6016 / 1024.0, b1 = 1.3496, a2 = 0.0410 / 1024.0, b2 = 9.7128;
+  const double a3 = 0.0422 / 1024.0, b3 = 1.1614;
+  const size_t message_size = es * count;
+  const double ms = (double)message_size, cs = (double)n;
+  if (n < 8 && message_size < 512) return MX_REDUCE_LINEAR;
+  if ((n < 8 && message_size < 20480) || message_size < 2048 || count <= 1) return MX_REDUCE_BINOMIAL;
+  if (cs > a1 * ms + b1) return MX_REDUCE_BINOMIAL;
+  if (cs > a2 * ms + b2) return MX_REDUCE_PIPELINE;
+  if (cs > a3 * ms + b3) return MX_REDUCE_BINARY;
+  return MX_REDUCE_PIPELINE;
+}
+
+namespace {
+
+// local communicators: one VM launch over elements [lo, hi)
+static int vm_run_local(vm_launch_fn vl, const VmProg &p, const char *const *src, char *const *dst, size_t lo,
+                        size_t hi, size_t es, hipStream_t s) {
+  if (hi <= lo) return MX_SUCCESS;
+  VmArgs a;
+  memset(&a, 0, sizeof a);
+  for (int j = 0; j < p.nsrc; j++) a.src[j] = src[j] + lo * es;
+  for (int d = 0; d < MAXR; d++) a.dst[d] = dst[d];
+  a.n = hi - lo;
+  a.p = p;
+  return vl(a, s);
+}
+
+// multi-process: all-peer exchange of the element parts, VM fold of my part
+// by every destination's program, results to the destinations' gather areas
+// (or my rbuf), destinations copy the other parts in (the allreduce scheme
+// of mx_allreduce with per-output destinations).
+// info_rank >= 0: that rank's READY word carries the info bit of the
+// guarded instructions (info_bit is this rank's own bit, sent if it is
+// info_rank).
+static int vm_partitioned(mx_comm *c, vm_launch_fn vl, const VmProg &p, const char *sb, char *rb, size_t count,
+                          size_t es, uint32_t dest_mask, int info_rank, int info_bit, hipStream_t s) {
+  const int n = c->size, r = c->rank;
+  const bool me_dest = (dest_mask >> r) & 1;
+  const size_t ce = chunk_elems(c, count, es);
+  for (size_t c0 = 0; c0 < count; c0 += ce) {
+    const size_t cl = std::min(ce, count - c0);
+    const Layout L = layout_for(n, ce, es);
+    size_t off[MAXR], len[MAXR];
+    blockcount(cl, n, off, len);
+    const uint64_t g = ++c->gen;
+    int rc;
+    if ((rc = wait_all(c, FLAG_DONE, g - 1, s))) return rc;
+    CopyArgs ca;
+    memset(&ca, 0, sizeof ca);
+    for (int q = 0; q < n; q++) {
+      if (q == r || !len[q]) continue;
+      const size_t e0 = c0 + off[q];
+      ca.j[ca.n++] = CopyJob{sb + e0 * es, c->peer_staging[q] + (size_t)r * L.slot + ((e0 * es) & 15), len[q] * es};
+    }
+    prof_begin(c, s);
+    if ((rc = copy_launch(ca, s))) return rc;
+    prof_end(c, s, 1, 0);
+    if ((rc = signal_all(c, FLAG_READY, (g << 1) | (uint64_t)(r == info_rank ? info_bit : 0), s))) return rc;
+    if ((rc = wait_all(c, FLAG_READY, g << 1, s))) return rc;
+    if (len[r]) {
+      const size_t e0 = c0 + off[r];
+      const size_t mis = (e0 * es) & 15;
+      VmArgs a;
+      memset(&a, 0, sizeof a);
+      if (info_rank >= 0 && info_rank != r) a.info = c->flagmem + FLAG_READY * MAXR + info_rank;
+      a.info_host = info_bit;
+      for (int j = 0; j < n; j++) a.src[j] = (j == r) ? sb + e0 * es : c->staging + (size_t)j * L.slot + mis;
+      for (int d = 0; d < n; d++) {
+        if (!((dest_mask >> d) & 1)) continue;
+        a.dst[d] = (d == r) ? rb + e0 * es : c->peer_staging[d] + L.gather_off + ((c0 * es) & 15) + off[r] * es;
+      }
+      a.n = len[r];
+      a.p = p;
+      int nemit = 0;
+      for (int i = 0; i < p.nins; i++) nemit += (p.ins[i].op & 3) == VM_EMIT;
+      prof_begin(c, s);
+      if ((rc = vl(a, s))) return rc;
+      prof_end(c, s, 0, (double)(n + nemit) * (double)len[r] * (double)es);
+    }
+    if ((rc = signal_all(c, FLAG_PUSHED, g, s))) return rc;
+    if (me_dest) {
+      if ((rc = wait_all(c, FLAG_PUSHED, g, s))) return rc;
+      memset(&ca, 0, sizeof ca);
+      for (int q = 0; q < n; q++) {
+        if (q == r || !len[q]) continue;
+        ca.j[ca.n++] = CopyJob{c->staging + L.gather_off + ((c0 * es) & 15) + off[q] * es,
+                               rb + (c0 + off[q]) * es, len[q] * es};
+      }
+      prof_begin(c, s);
+      if ((rc = copy_launch(ca, s))) return rc;
+      prof_end(c, s, 2, 0);
+    }
+    if ((rc = signal_all(c, FLAG_DONE, g, s))) return rc;
+  }
+  return finish(c, s);
+}
+
+static int vm_setup(int op, int type, vm_launch_fn *vl, size_t *es) {
+  *vl = fold_fns(op, type).vm;
+  if (!*vl) return MX_ERR_UNSUPPORTED;
+  *es = mx_type_size(type);
+  return *es ? MX_SUCCESS : MX_ERR_ARG;
+}
+
+static uint32_t dest_mask_of(const Dag &g, int owner_rank) {
+  uint32_t m = 0;
+  for (const auto &o : g.out) m |= 1u << (o.dst < 0 ? owner_rank : o.dst);
+  return m;
+}
+
+}  // namespace
+
+// ---- rooted reduce ------------------------------------------------------
+extern "C" int mx_reduce_local(mx_comm_t *c, const void *const *sbufs, void *const *rbufs, size_t count, int type,
+                               int op, int root, int alg, void *stream) {
+  if (!c || !c->local || !rbufs || root < 0 || root >= c->size) return MX_ERR_ARG;
+  vm_launch_fn vl;
+  size_t es;
+  int rc = vm_setup(op, type, &vl, &es);
+  if (rc) return rc;
+  const int n = c->size;
+  if (count == 0) return MX_SUCCESS;
+  const bool inplace = !sbufs || sbufs[root] == MX_IN_PLACE;
+  const char *src[MAXR];
+  char *dst[MAXR] = {};
+  for (int j = 0; j < n; j++) {
+    const void *sb = (sbufs && sbufs[j] != MX_IN_PLACE) ? sbufs[j] : rbufs[j];
+    if (!sb) return MX_ERR_ARG;
+    src[j] = (const char *)sb;
+  }
+  dst[root] = (char *)rbufs[root];
+  if (!dst[root]) return MX_ERR_ARG;
+  Dag g(n);
+  if ((rc = reduce_dag(g, alg, count, es, root, inplace ? 1 : 0))) return rc;
+  VmProg p;
+  if ((rc = dag_compile(g, root, p))) return rc;
+  if ((rc = vm_run_local(vl, p, src, dst, 0, count, es, (hipStream_t)stream))) return rc;
+  return finish(c, (hipStream_t)stream);
+}
+
+extern "C" int mx_reduce(mx_comm_t *c, const void *sbuf, void *rbuf, size_t count, int type, int op, int root,
+                         int alg, void *stream) {
+  if (!c || root < 0 || root >= c->size) return MX_ERR_ARG;
+  const int r = c->rank;
+  if (r == root && !rbuf) return MX_ERR_ARG;
+  if (c->local) {
+    if (c->size != 1) return MX_ERR_STATE;
+    const void *sb[1] = {sbuf};
+    void *rb[1] = {rbuf};
+    return mx_reduce_local(c, sb, rb, count, type, op, root, alg, stream);
+  }
+  vm_launch_fn vl;
+  size_t es;
+  int rc = vm_setup(op, type, &vl, &es);
+  if (rc) return rc;
+  hipStream_t s = (hipStream_t)stream;
+  if (count == 0) return MX_SUCCESS;
+  const bool inplace = (r == root) && (sbuf == MX_IN_PLACE || !sbuf);
+  const char *sb = (sbuf == MX_IN_PLACE || !sbuf) ? (const char *)rbuf : (const char *)sbuf;
+  if (!sb) return MX_ERR_ARG;
+  if (c->size == 1) {
+    if ((rc = copy_async(rbuf, sb, count * es, s))) return rc;
+    return finish(c, s);
+  }
+  if (!(c->flags & MX_COMM_IPC)) return MX_ERR_STATE;
+  // Part owners fold for the root, whose MPI_IN_PLACE choice sets the
+  // operand roles of its own combination: the program carries both
+  // variants, and the root's READY word tells the owners which one.
+  Dag g(c->size);
+  if ((rc = reduce_dag(g, alg, count, es, root, 2))) return rc;
+  VmProg p;
+  if ((rc = dag_compile(g, root, p))) return rc;
+  return vm_partitioned(c, vl, p, sb, (char *)rbuf, count, es, 1u << root, root, inplace ? 1 : 0, s);
+}
+
+// ---- scan / exscan ------------------------------------------------------
+static int scan_local_impl(mx_comm_t *c, const void *const *sbufs, void *const *rbufs, size_t count, int type,
+                           int op, int alg, bool exclusive, void *stream) {
+  if (!c || !c->local || !rbufs) return MX_ERR_ARG;
+  vm_launch_fn vl;
+  size_t es;
+  int rc = vm_setup(op, type, &vl, &es);
+  if (rc) return rc;
+  const int n = c->size;
+  if (count == 0) return MX_SUCCESS;
+  const char *src[MAXR];
+  char *dst[MAXR] = {};
+  for (int j = 0; j < n; j++) {
+    const void *sb = (sbufs && sbufs[j] != MX_IN_PLACE) ? sbufs[j] : rbufs[j];
+    if (!sb) return MX_ERR_ARG;
+    src[j] = (const char *)sb;
+    dst[j] = (char *)rbufs[j];
+  }
+  Dag g(n);
+  if ((rc = scan_dag(g, alg, exclusive))) return rc;
+  if (g.out.empty()) return finish(c, (hipStream_t)stream);
+  VmProg p;
+  if ((rc = dag_compile(g, 0, p))) return rc;
+  if ((rc = vm_run_local(vl, p, src, dst, 0, count, es, (hipStream_t)stream))) return rc;
+  return finish(c, (hipStream_t)stream);
+}
+
+static int scan_impl(mx_comm_t *c, const void *sbuf, void *rbuf, size_t count, int type, int op, int alg,
+                     bool exclusive, void *stream) {
+  if (!c || !rbuf) return MX_ERR_ARG;
+  if (c->local) {
+    if (c->size != 1) return MX_ERR_STATE;
+    const void *sb[1] = {sbuf};
+    void *rb[1] = {rbuf};
+    return scan_local_impl(c, sb, rb, count, type, op, alg, exclusive, stream);
+  }
+  vm_launch_fn vl;
+  size_t es;
+  int rc = vm_setup(op, type, &vl, &es);
+  if (rc) return rc;
+  hipStream_t s = (hipStream_t)stream;
+  if (count == 0) return MX_SUCCESS;
+  const char *sb = (sbuf == MX_IN_PLACE || !sbuf) ? (const char *)rbuf : (const char *)sbuf;
+  if (c->size == 1) {   // scan: a copy; exscan: rank 0's rbuf is undefined (left untouched)
+    if (!exclusive && (rc = copy_async(rbuf, sb, count * es, s))) return rc;
+    return finish(c, s);
+  }
+  if (!(c->flags & MX_COMM_IPC)) return MX_ERR_STATE;
+  Dag g(c->size);
+  if ((rc = scan_dag(g, alg, exclusive))) return rc;
+  VmProg p;
+  if ((rc = dag_compile(g, c->rank, p))) return rc;
+  return vm_partitioned(c, vl, p, sb, (char *)rbuf, count, es, dest_mask_of(g, c->rank), -1, 0, s);
+}
+
+extern "C" int mx_scan_local(mx_comm_t *c, const void *const *sbufs, void *const *rbufs, size_t count, int type,
+                             int op, int alg, void *stream) {
+  return scan_local_impl(c, sbufs, rbufs, count, type, op, alg, false, stream);
+}
+extern "C" int mx_exscan_local(mx_comm_t *c, const void *const *sbufs, void *const *rbufs, size_t count, int type,
+                               int op, int alg, void *stream) {
+  return scan_local_impl(c, sbufs, rbufs, count, type, op, alg, true, stream);
+}
+extern "C" int mx_scan(mx_comm_t *c, const void *sbuf, void *rbuf, size_t count, int type, int op, int alg,
+                       void *stream) {
+  return scan_impl(c, sbuf, rbuf, count, type, op, alg, false, stream);
+}
+extern "C" int mx_exscan(mx_comm_t *c, const void *sbuf, void *rbuf, size_t count, int type, int op, int alg,
+                         void *stream) {
+  return scan_impl(c, sbuf, rbuf, count, type, op, alg, true, stream);
+}
+
+// ---- reduce_scatter_block -------------------------------------------------
+// coll/tuned's fixed rule is basic_linear (coll_tuned_decision_fixed.c:522-532):
+// coll_reduce to root 0 of rcount*n elements (the tuned reduce decision on
+// that size; sbuf = rbuf for MPI_IN_PLACE, so never an IN_PLACE root) and
+// a scatter (coll_base_reduce_scatter_block.c:55-110).  Rank p's block is
+// folded by rank p itself.
+extern "C" int mx_reduce_scatter_block_local(mx_comm_t *c, const void *const *sbufs, void *const *rbufs,
+                                             size_t rcount, int type, int op, int alg, void *stream) {
+  if (!c || !c->local || !rbufs) return MX_ERR_ARG;
+  vm_launch_fn vl;
+  size_t es;
+  int rc = vm_setup(op, type, &vl, &es);
+  if (rc) return rc;
+  const int n = c->size;
+  if (rcount == 0) return MX_SUCCESS;
+  const char *src[MAXR];
+  for (int j = 0; j < n; j++) {
+    const void *sb = (sbufs && sbufs[j] != MX_IN_PLACE) ? sbufs[j] : rbufs[j];
+    if (!sb || !rbufs[j]) return MX_ERR_ARG;
+    src[j] = (const char *)sb;
+  }
+  Dag g(n);
+  if ((rc = reduce_dag(g, alg, rcount * n, es, 0, 0))) return rc;
+  g.out.back().dst = -1;   // the block's owner
+  // block p, in order 0..n-1: with MPI_IN_PLACE rank p's result overwrites
+  // its own block 0, which block 0's launch consumed first
+  for (int q = 0; q < n; q++) {
+    VmProg p;
+    if ((rc = dag_compile(g, q, p))) return rc;
+    char *dst[MAXR] = {};
+    dst[q] = (char *)rbufs[q];
+    if ((rc = vm_run_local(vl, p, src, dst, (size_t)q * rcount, (size_t)(q + 1) * rcount, es, (hipStream_t)stream)))
+      return rc;
+    // vm_run_local offsets the sources by the block start; the destination is rbufs[q][0..rcount)
+  }
+  return finish(c, (hipStream_t)stream);
+}
+
+extern "C" int mx_reduce_scatter_block(mx_comm_t *c, const void *sbuf, void *rbuf, size_t rcount, int type, int op,
+                                       int alg, void *stream) {
+  if (!c || !rbuf) return MX_ERR_ARG;
+  if (c->local) {
+    if (c->size != 1) return MX_ERR_STATE;
+    const void *sb[1] = {sbuf};
+    void *rb[1] = {rbuf};
+    return mx_reduce_scatter_block_local(c, sb, rb, rcount, type, op, alg, stream);
+  }
+  vm_launch_fn vl;
+  size_t es;
+  int rc = vm_setup(op, type, &vl, &es);
+  if (rc) return rc;
+  hipStream_t s = (hipStream_t)stream;
+  const int n = c->size, r = c->rank;
+  if (rcount == 0) return MX_SUCCESS;
+  const char *sb = (sbuf == MX_IN_PLACE || !sbuf) ? (const char *)rbuf : (const char *)sbuf;
+  if (n == 1) {
+    if ((rc = copy_async(rbuf, sb, rcount * es, s))) return rc;
+    return finish(c, s);
+  }
+  if (!(c->flags & MX_COMM_IPC)) return MX_ERR_STATE;
+  Dag g(n);
+  if ((rc = reduce_dag(g, alg, rcount * n, es, 0, 0))) return rc;
+  g.out.back().dst = -1;
+  VmProg p;
+  if ((rc = dag_compile(g, r, p))) return rc;
+  // chunks of each block: slot j holds rank j's piece of my block
+  size_t kc = rcount;
+  while (kc > 1 && (size_t)n * rup(kc * es + 16, 256) > c->main_bytes) kc = (kc + 1) / 2;
+  const size_t slot = rup(kc * es + 16, 256);
+  for (size_t k0 = 0; k0 < rcount; k0 += kc) {
+    const size_t kl = std::min(kc, rcount - k0);
+    const uint64_t gen = ++c->gen;
+    if ((rc = wait_all(c, FLAG_DONE, gen - 1, s))) return rc;
+    CopyArgs ca;
+    memset(&ca, 0, sizeof ca);
+    for (int q = 0; q < n; q++) {
+      if (q == r) continue;
+      const size_t e0 = (size_t)q * rcount + k0;
+      ca.j[ca.n++] = CopyJob{sb + e0 * es, c->peer_staging[q] + (size_t)r * slot + ((e0 * es) & 15), kl * es};
+    }
+    prof_begin(c, s);
+    if ((rc = copy_launch(ca, s))) return rc;
+    prof_end(c, s, 1, 0);
+    if ((rc = signal_all(c, FLAG_READY, gen << 1, s))) return rc;
+    if ((rc = wait_all(c, FLAG_READY, gen << 1, s))) return rc;
+    const size_t e0 = (size_t)r * rcount + k0;
+    const size_t mis = (e0 * es) & 15;
+    VmArgs a;
+    memset(&a, 0, sizeof a);
+    for (int j = 0; j < n; j++) a.src[j] = (j == r) ? sb + e0 * es : c->staging + (size_t)j * slot + mis;
+    a.dst[r] = (char *)rbuf + k0 * es;
+    a.n = kl;
+    a.p = p;
+    prof_begin(c, s);
+    if ((rc = vl(a, s))) return rc;
+    prof_end(c, s, 0, (double)(n + 1) * (double)kl * (double)es);
+    if ((rc = signal_all(c, FLAG_DONE, gen, s))) return rc;
   }
   return finish(c, s);
 }

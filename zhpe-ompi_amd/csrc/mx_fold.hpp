@@ -1,0 +1,444 @@
+// mx_fold.hpp -- device side of the collective fold: the kernels that read
+// the n contributions of a range of elements and evaluate, per element, the
+// reduction tree of a reference algorithm (see mx_coll.hip for the host
+// side).  Three evaluators:
+//   k_fold     CHAIN / BUTTERFLY programs in registers (allreduce and
+//              reduce_scatter: the ring / recursive-doubling / Rabenseifner /
+//              recursive-halving trees);
+//   k_oneshot  the same programs fused with the all-peer exchange for small
+//              allreduce messages;
+//   k_vm       an LDS-register VM for arbitrary trees and multi-output DAGs:
+//              rooted reduce (binomial / binary / pipeline / chain /
+//              in-order binary trees of coll_base_topo.c), scan / exscan
+//              (linear and recursive doubling) and reduce_scatter_block.
+// The per-type instantiations are split over mx_fold_f*.hip by element-type
+// family (build time); fold_fns() finds the launchers of an (op, type) pair.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <string.h>
+
+#include "mx_dispatch.hpp"
+#include "mx_internal.h"
+#include "mx_mem.hpp"
+#include "../../include/mx_coll.h"
+
+namespace mx {
+
+constexpr int MAXR = MX_MAX_RANKS;
+constexpr int kFB = 256;  // fold / copy block size
+
+// one-shot small-message allreduce: flag layout shared with mx_coll.hip
+// READY carries (generation << 1) | info bit: the info bit is the root's
+// MPI_IN_PLACE choice in a rooted reduce (the operand roles of the root's
+// own combination depend on it, and the element parts are folded by other
+// ranks); PUSHED and DONE carry the plain generation.
+enum { FLAG_READY = 0, FLAG_PUSHED = 1, FLAG_DONE = 2, NFLAGS = 3 };
+constexpr int OSWG = 16;
+constexpr int OS_MAXSEG = 16;
+
+// ---------------------------------------------------------------------------
+// fold programs
+// ---------------------------------------------------------------------------
+enum { PROG_CHAIN = 0, PROG_BFLY = 1 };
+
+struct FoldProg {
+  int kind;
+  int n;           // chain: number of operands; butterfly: p' leaves
+  int D;           // butterfly depth (p' = 1 << D)
+  int acc_first;   // chain: accumulator is the target (first operand)
+  uint32_t pref;   // butterfly: bit s set -> upper half is the target at level s
+  int8_t ord[MAXR];  // chain: source index per step
+  int8_t la[MAXR];   // butterfly leaf slot i: first operand source
+  int8_t lb[MAXR];   //   second operand source, -1 = plain leaf
+};
+
+struct FoldArgs {
+  const char *src[MAXR];
+  char *dst[MAXR];
+  int ndst;
+  size_t n, head, nvec;  // elements; scalar head; 16-B vectors after head
+  FoldProg p;
+};
+
+template <class T> struct alignas(16) fvec {
+  static constexpr int N = 16 / sizeof(T);
+  T e[N];
+};
+
+template <class OP, class T>
+__device__ __forceinline__ T comb(const T &x, const T &y) { return OP()(x, y); }
+template <class OP, class T>
+__device__ __forceinline__ fvec<T> comb(const fvec<T> &x, const fvec<T> &y) {
+  fvec<T> r;
+#pragma unroll
+  for (int j = 0; j < fvec<T>::N; j++) r.e[j] = OP()(x.e[j], y.e[j]);
+  return r;
+}
+
+// Evaluates the program; LD(j) returns operand j at this lane's position.
+template <class OP, class V, class L>
+__device__ __forceinline__ V eval_prog(const FoldProg &p, L LD) {
+  if (p.kind == PROG_CHAIN) {
+    V acc = LD(p.ord[0]);
+#pragma unroll
+    for (int j = 1; j < MAXR; j++) {
+      if (j < p.n) {
+        const V v = LD(p.ord[j]);
+        acc = p.acc_first ? comb<OP>(acc, v) : comb<OP>(v, acc);
+      }
+    }
+    return acc;
+  }
+  V R[MAXR];
+#pragma unroll
+  for (int i = 0; i < MAXR; i++) {
+    if (i < p.n) {
+      V a = LD(p.la[i]);
+      if (p.lb[i] >= 0) a = comb<OP>(a, LD(p.lb[i]));
+      R[i] = a;
+    }
+  }
+#pragma unroll
+  for (int s = 0; s < 4; s++) {
+    if (s < p.D) {
+      const int h = 1 << s;
+      const bool hi_first = (p.pref >> s) & 1;
+#pragma unroll
+      for (int u = 0; u < MAXR; u += 2 << s) {
+        if (u < p.n) R[u] = hi_first ? comb<OP>(R[u + h], R[u]) : comb<OP>(R[u], R[u + h]);
+      }
+    }
+  }
+  return R[0];
+}
+
+template <class T, class OP, bool NT>
+__global__ void __launch_bounds__(kFB) k_fold(FoldArgs a) {
+  using V = fvec<T>;
+  constexpr int N = V::N;
+  const size_t tid = (size_t)blockIdx.x * kFB + threadIdx.x;
+  if (N > 0 && tid < a.nvec) {
+    const size_t off = a.head * sizeof(T) + tid * 16;
+    const V r = eval_prog<OP, V>(a.p, [&](int j) {
+      V v;
+      ld16<NT>(v, reinterpret_cast<const V *>(a.src[j] + off));
+      return v;
+    });
+#pragma unroll
+    for (int d = 0; d < MAXR; d++)
+      if (d < a.ndst) st16<NT>(reinterpret_cast<V *>(a.dst[d] + off), r);
+  }
+  // scalar elements: the head, the tail, or everything (element path)
+  const size_t tail0 = a.head + a.nvec * N;
+  size_t e = (size_t)-1;
+  if (tid < a.head) e = tid;
+  else if (tid - a.head < a.n - tail0 && tid >= a.head) e = tail0 + (tid - a.head);
+  if (e < a.n) {
+    const size_t off = e * sizeof(T);
+    const T r = eval_prog<OP, T>(a.p, [&](int j) { return *reinterpret_cast<const T *>(a.src[j] + off); });
+#pragma unroll
+    for (int d = 0; d < MAXR; d++)
+      if (d < a.ndst) store_fields(reinterpret_cast<T *>(a.dst[d] + off), r);
+  }
+}
+
+typedef int (*fold_launch_fn)(FoldArgs &, hipStream_t);
+
+template <class T, class OP>
+int fold_launch(FoldArgs &a, hipStream_t s) {
+  constexpr size_t N = (sizeof(T) <= 16 && 16 % sizeof(T) == 0) ? 16 / sizeof(T) : 0;
+  bool vec = N > 0 && !has_pad<T>::value;   // padded types: field stores, element path
+  uintptr_t m = (uintptr_t)a.src[0] & 15;
+  for (int j = 0; j < MAXR; j++)
+    if (a.src[j] && ((uintptr_t)a.src[j] & 15) != m) vec = false;
+  for (int d = 0; d < a.ndst; d++)
+    if (((uintptr_t)a.dst[d] & 15) != m) vec = false;
+  if (vec && (m % sizeof(T)) != 0) vec = false;
+  if (vec) {
+    size_t head = m ? (16 - m) / sizeof(T) : 0;
+    if (head > a.n) head = a.n;
+    a.head = head;
+    a.nvec = (a.n - head) / (N ? N : 1);
+  } else {
+    a.head = a.n;  // everything scalar (element per lane)
+    a.nvec = 0;
+  }
+  size_t work = a.nvec + a.head + (N ? N : 1);
+  if (!vec) work = a.n;
+  const size_t g = (work + kFB - 1) / kFB;
+  int nsrc = 0;
+  for (int j = 0; j < MAXR; j++) nsrc += a.src[j] != nullptr;
+  if (vec && mx_nt_for((size_t)(nsrc + a.ndst) * a.n * sizeof(T)))
+    hipLaunchKernelGGL((k_fold<T, OP, true>), dim3((unsigned)(g ? g : 1)), dim3(kFB), 0, s, a);
+  else
+    hipLaunchKernelGGL((k_fold<T, OP, false>), dim3((unsigned)(g ? g : 1)), dim3(kFB), 0, s, a);
+  return mx_check_launch();
+}
+
+
+
+// ---------------------------------------------------------------------------
+// one-shot allreduce for small messages: ONE launch per call.  Workgroup w
+// owns element slice w: it pushes that slice of my contribution into every
+// peer's one-shot slot (double-buffered by generation parity), raises READY
+// (source=me, slice=w) at each peer, waits for every peer's READY for slice
+// w, and folds the slice for the WHOLE vector from the n copies (every rank
+// evaluates the same fold program per element, so all ranks agree bit for
+// bit).  Reuse of a parity buffer needs the peer to have finished gen-2,
+// i.e. DONE >= gen-2; the last workgroup to finish raises DONE(gen).
+// ---------------------------------------------------------------------------
+struct OsSeg { size_t lo, hi; FoldProg p; };
+struct OneShotArgs {
+  const char *sb;
+  char *rb;
+  char *peer_slot[MAXR];        // peer p's buffer (this parity) at my slot; null for me
+  const char *src[MAXR];        // operand j: my buffer (this parity) slot j; src[rank] = sb
+  uint64_t *peer_ready[MAXR];   // peer p's OS READY row for source = me
+  uint64_t *peer_done[MAXR];    // peer p's DONE flag for source = me
+  const uint64_t *my_ready;     // my OS READY rows [src][wg]
+  const uint64_t *my_done;      // my DONE flags [src]
+  uint64_t *counter;
+  uint64_t counter_last, gen, timeout_ticks;
+  int *err;
+  int n, rank, nseg;
+  size_t count, es, slice;
+  OsSeg seg[OS_MAXSEG];
+};
+
+constexpr int kOSB = 256;
+
+__device__ __forceinline__ void os_spin(const uint64_t *f, uint64_t v, uint64_t ticks, int *err) {
+  const uint64_t t0 = wall_clock64();
+  while (__hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) < v) {
+    __builtin_amdgcn_s_sleep(1);
+    if (wall_clock64() - t0 > ticks) {
+      __hip_atomic_store(err, MX_ERR_TIMEOUT, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      break;
+    }
+  }
+}
+
+template <class T, class OP>
+__global__ void __launch_bounds__(kOSB) k_oneshot(OneShotArgs a) {
+  const int w = blockIdx.x, t = threadIdx.x;
+  const size_t lo = (size_t)w * a.slice, hi = lo + a.slice < a.count ? lo + a.slice : a.count;
+  // (1) every peer is past gen-2: its reads of this parity buffer are over
+  if (t < a.n && t != a.rank && a.gen > 2) os_spin(a.my_done + t, a.gen - 2, a.timeout_ticks, a.err);
+  __syncthreads();
+  // (2) push my slice (bytes [lo*es, hi*es)) to every peer
+  if (lo < hi) {
+    const size_t b0 = lo * a.es, b1 = hi * a.es;
+    const bool vec = (((uintptr_t)a.sb | b0 | b1) & 15) == 0;
+    for (int p = 0; p < a.n; p++) {
+      if (p == a.rank) continue;
+      char *d = a.peer_slot[p];
+      if (vec) {
+        for (size_t i = b0 / 16 + t; i < b1 / 16; i += kOSB)
+          reinterpret_cast<uint4 *>(d)[i] = reinterpret_cast<const uint4 *>(a.sb)[i];
+      } else {
+        for (size_t i = b0 + t; i < b1; i += kOSB) d[i] = a.sb[i];
+      }
+    }
+  }
+  __threadfence_system();
+  __syncthreads();
+  // (3) READY(me, w) at every peer; (4) wait READY(p, w) from every peer
+  if (t < a.n && t != a.rank) {
+    __hip_atomic_store(a.peer_ready[t] + w, a.gen, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+    os_spin(a.my_ready + (size_t)t * OSWG + w, a.gen, a.timeout_ticks, a.err);
+  }
+  __syncthreads();
+  __atomic_thread_fence(__ATOMIC_ACQUIRE);
+  // (5) fold the slice
+  int sidx = 0;
+  for (size_t e = lo + t; e < hi; e += kOSB) {
+    while (sidx + 1 < a.nseg && e >= a.seg[sidx].hi) sidx++;
+    const size_t off = e * sizeof(T);
+    const T r = eval_prog<OP, T>(a.seg[sidx].p, [&](int j) { return *reinterpret_cast<const T *>(a.src[j] + off); });
+    store_fields(reinterpret_cast<T *>(a.rb + off), r);
+  }
+  // (6) the last workgroup out raises DONE(gen) at every peer
+  __syncthreads();
+  if (t == 0) {
+    __threadfence();
+    const uint64_t old = __hip_atomic_fetch_add(a.counter, (uint64_t)1, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+    if (old == a.counter_last) {
+      __threadfence_system();
+      for (int p = 0; p < a.n; p++)
+        if (p != a.rank) __hip_atomic_store(a.peer_done[p], a.gen, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+  }
+}
+
+typedef int (*oneshot_launch_fn)(OneShotArgs &, int nwg, hipStream_t);
+
+template <class T, class OP>
+int oneshot_launch(OneShotArgs &a, int nwg, hipStream_t s) {
+  hipLaunchKernelGGL((k_oneshot<T, OP>), dim3(nwg), dim3(kOSB), 0, s, a);
+  return mx_check_launch();
+}
+
+
+
+// ---------------------------------------------------------------------------
+// fold VM: arbitrary reduction trees / DAGs with LDS-resident registers.
+// Registers 0..nsrc-1 hold the n contributions of this lane's element(s);
+// COMB r[d] = OP(r[a], r[b]) (a = target/first operand, b = source); EMIT
+// stores r[a] to destination d.  Register j of lane t lives at LDS
+// (j * kVB + t) * SLOT, so each lane only touches its own column (no
+// barriers) and the uniform register index costs one address add -- where a
+// VGPR array indexed by a run-time register number would be spilled to
+// scratch or expanded into selects.
+// ---------------------------------------------------------------------------
+constexpr int kVB = 128;         // VM block size
+constexpr int VM_MAXI = 192;     // instructions per program
+constexpr int VM_MAXREG = 40;    // registers (contributions + temporaries)
+// op: VM_COMB / VM_EMIT, optionally guarded by the call's info bit (the
+// root's MPI_IN_PLACE in a rooted reduce): executed only if set / clear
+enum { VM_COMB = 0, VM_EMIT = 1, VM_IF_SET = 4, VM_IF_CLEAR = 8 };
+struct VmIns { int8_t op, d, a, b; };
+struct VmProg {
+  int nsrc, nregs, nins;
+  VmIns ins[VM_MAXI];
+};
+struct VmArgs {
+  const char *src[MAXR];
+  char *dst[MAXR];
+  size_t n, head, nvec;
+  const uint64_t *info;   // READY word carrying the info bit (bit 0), or null
+  int info_host;          // info bit when `info` is null
+  VmProg p;
+};
+
+template <class T> constexpr int vm_slot() { return sizeof(T) > 16 ? (int)sizeof(T) : 16; }
+
+template <class OP, bool NT, bool VEC, class E, int SLOT>
+__device__ __forceinline__ void vm_run(const VmArgs &a, char *my, size_t off, int info) {
+  auto R = [&](int j) { return reinterpret_cast<E *>(my + (size_t)j * kVB * SLOT); };
+  for (int j = 0; j < a.p.nsrc; j++) {
+    E v;
+    if constexpr (VEC) ld16<NT>(v, reinterpret_cast<const E *>(a.src[j] + off));
+    else v = *reinterpret_cast<const E *>(a.src[j] + off);
+    *R(j) = v;
+  }
+  const int skip = info ? VM_IF_CLEAR : VM_IF_SET;
+  for (int i = 0; i < a.p.nins; i++) {
+    const VmIns in = a.p.ins[i];
+    if (in.op & skip) continue;
+    if ((in.op & 3) == VM_COMB) {
+      const E x = *R(in.a), y = *R(in.b);
+      *R(in.d) = comb<OP>(x, y);
+    } else {
+      const E v = *R(in.a);
+      if constexpr (VEC) st16<NT>(reinterpret_cast<E *>(a.dst[in.d] + off), v);
+      else store_fields(reinterpret_cast<E *>(a.dst[in.d] + off), v);
+    }
+  }
+}
+
+template <class T, class OP, bool NT>
+__global__ void __launch_bounds__(kVB) k_vm(VmArgs a) {
+  using V = fvec<T>;
+  constexpr int N = V::N;
+  constexpr int SLOT = vm_slot<T>();
+  extern __shared__ __align__(16) char vm_lds[];
+  char *const my = vm_lds + (size_t)threadIdx.x * SLOT;
+  const size_t tid = (size_t)blockIdx.x * kVB + threadIdx.x;
+  const int info = a.info ? (int)(__hip_atomic_load(a.info, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) & 1)
+                          : a.info_host;
+  if constexpr (N > 0) {
+    if (tid < a.nvec) vm_run<OP, NT, true, V, SLOT>(a, my, a.head * sizeof(T) + tid * 16, info);
+  }
+  const size_t tail0 = a.head + a.nvec * N;
+  size_t e = (size_t)-1;
+  if (tid < a.head) e = tid;
+  else if (tid >= a.head && tid - a.head < a.n - tail0) e = tail0 + (tid - a.head);
+  if (e < a.n) vm_run<OP, false, false, T, SLOT>(a, my, e * sizeof(T), info);
+}
+
+typedef int (*vm_launch_fn)(VmArgs &, hipStream_t);
+
+template <class T, class OP>
+int vm_launch(VmArgs &a, hipStream_t s) {
+  constexpr size_t N = (sizeof(T) <= 16 && 16 % sizeof(T) == 0) ? 16 / sizeof(T) : 0;
+  const size_t lds = (size_t)a.p.nregs * kVB * vm_slot<T>();
+  if (lds > 64 * 1024 || a.p.nregs > VM_MAXREG || a.p.nins > VM_MAXI) return MX_ERR_UNSUPPORTED;
+  bool vec = N > 0 && !has_pad<T>::value;
+  const uintptr_t m = (uintptr_t)a.src[0] & 15;
+  for (int j = 0; j < a.p.nsrc; j++)
+    if (((uintptr_t)a.src[j] & 15) != m) vec = false;
+  for (int i = 0; i < a.p.nins; i++)
+    if ((a.p.ins[i].op & 3) == VM_EMIT && ((uintptr_t)a.dst[a.p.ins[i].d] & 15) != m) vec = false;
+  if (vec && (m % sizeof(T)) != 0) vec = false;
+  if (vec) {
+    size_t head = m ? (16 - m) / sizeof(T) : 0;
+    if (head > a.n) head = a.n;
+    a.head = head;
+    a.nvec = (a.n - head) / (N ? N : 1);
+  } else {
+    a.head = a.n;
+    a.nvec = 0;
+  }
+  const size_t work = vec ? a.nvec + a.head + N : a.n;
+  const size_t g = (work + kVB - 1) / kVB;
+  int nemit = 0;
+  for (int i = 0; i < a.p.nins; i++) nemit += (a.p.ins[i].op & 3) == VM_EMIT;
+  if (vec && mx_nt_for((size_t)(a.p.nsrc + nemit) * a.n * sizeof(T)))
+    hipLaunchKernelGGL((k_vm<T, OP, true>), dim3((unsigned)(g ? g : 1)), dim3(kVB), lds, s, a);
+  else
+    hipLaunchKernelGGL((k_vm<T, OP, false>), dim3((unsigned)(g ? g : 1)), dim3(kVB), lds, s, a);
+  return mx_check_launch();
+}
+
+// ---------------------------------------------------------------------------
+// per-(op, type) launchers, instantiated by element-type family
+// ---------------------------------------------------------------------------
+struct FoldFns {
+  fold_launch_fn fold;
+  oneshot_launch_fn oneshot;
+  vm_launch_fn vm;
+};
+
+// family of an element type: 0 8/16-bit integers, 1 32/64-bit integers,
+// 2 float / double / complex, 3 x87 long double (+ complex), 4 pair types
+template <class T> struct fam { static constexpr int value = sizeof(T) <= 2 ? 0 : 1; };
+template <> struct fam<float> { static constexpr int value = 2; };
+template <> struct fam<double> { static constexpr int value = 2; };
+template <> struct fam<cplx<float>> { static constexpr int value = 2; };
+template <> struct fam<cplx<double>> { static constexpr int value = 2; };
+template <> struct fam<x87> { static constexpr int value = 3; };
+template <> struct fam<x87c> { static constexpr int value = 3; };
+template <class V, class K> struct fam<pair_t<V, K>> { static constexpr int value = 4; };
+template <> struct fam<x87_pair> { static constexpr int value = 4; };
+constexpr int NFAM = 5;
+
+template <int F>
+struct FamVisitor {
+  template <class T, class OP2, class OP3> FoldFns go() {
+    if constexpr (fam<T>::value == F)
+      return FoldFns{&fold_launch<T, OP2>, &oneshot_launch<T, OP2>, &vm_launch<T, OP2>};
+    else
+      return FoldFns{nullptr, nullptr, nullptr};
+  }
+  FoldFns none() { return FoldFns{nullptr, nullptr, nullptr}; }
+};
+
+// defined in mx_fold_f<F>.hip
+FoldFns fold_fns_fam0(int op, int type);
+FoldFns fold_fns_fam1(int op, int type);
+FoldFns fold_fns_fam2(int op, int type);
+FoldFns fold_fns_fam3(int op, int type);
+FoldFns fold_fns_fam4(int op, int type);
+
+inline FoldFns fold_fns(int op, int type) {
+  FoldFns (*const f[NFAM])(int, int) = {fold_fns_fam0, fold_fns_fam1, fold_fns_fam2, fold_fns_fam3,
+                                         fold_fns_fam4};
+  for (int i = 0; i < NFAM; i++) {
+    const FoldFns r = f[i](op, type);
+    if (r.fold) return r;
+  }
+  return FoldFns{nullptr, nullptr, nullptr};
+}
+
+}  // namespace mx

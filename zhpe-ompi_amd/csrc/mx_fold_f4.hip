@@ -1,0 +1,11 @@
+// mx_fold_f4.hip -- instantiates the fold kernels (mx_fold.hpp) for
+// element-type family 4 only; the families are split over translation units
+// so the kernel library builds in parallel.
+#include "mx_fold.hpp"
+
+namespace mx {
+FoldFns fold_fns_fam4(int op, int type) {
+  FamVisitor<4> v;
+  return dispatch(op, type, v);
+}
+}  // namespace mx

@@ -6,6 +6,8 @@
 namespace mx {
 extern int g_num_cus;      // CUs of the current device (256 on MI355X)
 extern int g_device;       // device selected by mx_init
+// 16-byte streaming device copy (mx_coll.hip), falls back to the runtime copy
+int copy_async(void *dst, const void *src, size_t bytes, hipStream_t s);
 }  // namespace mx
 
 // Lazily performs mx_init(current device) if the caller did not.

@@ -10,7 +10,9 @@
 //    the first lanes of the grid (ragged counts, unaligned sub-blocks of a
 //    ring step);
 //  * buffers whose misalignment differs mod 16 fall back to an
-//    element-per-lane kernel (still coalesced).
+//    element-per-lane kernel (still coalesced);
+//  * large launches use non-temporal loads AND stores (mx_mem.hpp): 1 GiB
+//    fp32 SUM 5.65-5.86 -> 6.30-6.46 TB/s on MI355X (bw_probe3).
 // Algorithmic bytes per launch: 2-buffer 3*n*size (read in, read inout,
 // write inout), 3-buffer 3*n*size.
 #include <hip/hip_runtime.h>
@@ -19,6 +21,7 @@
 
 #include "mx_dispatch.hpp"
 #include "mx_internal.h"
+#include "mx_mem.hpp"
 
 namespace mx {
 
@@ -31,9 +34,12 @@ struct alignas(16) vec16 {
 };
 
 // Scalar per-element application, inout-form (x = b, y = a) or 3-buffer.
+// Results are stored field by field (store_fields): bytes of the target
+// outside the value fields (pair-type padding, x87 pad) keep their content,
+// as the reference's member assignments leave them (LOC_FUNC :88-104).
 template <class T, class OP>
 __device__ __forceinline__ void red2_elem(const T *__restrict__ a, T *__restrict__ b, size_t i) {
-  b[i] = OP()(b[i], a[i]);
+  store_fields(&b[i], OP()(b[i], a[i]));
 }
 
 // 2-buffer, vector body: elements [head, head + nvec*N) as 16-B vectors,
@@ -41,7 +47,7 @@ __device__ __forceinline__ void red2_elem(const T *__restrict__ a, T *__restrict
 // loop): measured on MI355X at 1 GiB this dense block->address mapping
 // streams at ~5.9 TB/s vs 4.3-5.6 TB/s for grid-stride variants
 // (tools/bw_probe*.hip).
-template <class T, class OP>
+template <class T, class OP, bool NT>
 __global__ void __launch_bounds__(kBlock)
 k_reduce2(const T *__restrict__ a, T *__restrict__ b, size_t n, size_t head, size_t nvec) {
   using V = vec16<T>;
@@ -51,11 +57,12 @@ k_reduce2(const T *__restrict__ a, T *__restrict__ b, size_t n, size_t head, siz
   if (tid < nvec) {
     const V *__restrict__ av = reinterpret_cast<const V *>(a + head);
     V *__restrict__ bv = reinterpret_cast<V *>(b + head);
-    V x = bv[tid];
-    const V y = av[tid];
+    V x, y;
+    ld16<NT>(x, bv + tid);
+    ld16<NT>(y, av + tid);
 #pragma unroll
-    for (int j = 0; j < N; j++) x.e[j] = op(x.e[j], y.e[j]);
-    bv[tid] = x;
+    for (int j = 0; j < N; j++) store_fields(&x.e[j], op(x.e[j], y.e[j]));
+    st16<NT>(bv + tid, x);
   }
   // ragged head and tail
   const size_t tail0 = head + nvec * N;
@@ -71,7 +78,7 @@ k_reduce2_elem(const T *__restrict__ a, T *__restrict__ b, size_t n) {
   if (i < n) red2_elem<T, OP>(a, b, i);
 }
 
-template <class T, class OP>
+template <class T, class OP, bool NT>
 __global__ void __launch_bounds__(kBlock)
 k_reduce3(const T *__restrict__ a1, const T *__restrict__ a2, T *__restrict__ o, size_t n,
           size_t head, size_t nvec) {
@@ -83,11 +90,12 @@ k_reduce3(const T *__restrict__ a1, const T *__restrict__ a2, T *__restrict__ o,
     const V *__restrict__ p = reinterpret_cast<const V *>(a1 + head);
     const V *__restrict__ q = reinterpret_cast<const V *>(a2 + head);
     V *__restrict__ ov = reinterpret_cast<V *>(o + head);
-    V x = p[tid];
-    const V y = q[tid];
+    V x, y;
+    ld16<NT>(x, p + tid);
+    ld16<NT>(y, q + tid);
 #pragma unroll
     for (int j = 0; j < N; j++) x.e[j] = op(x.e[j], y.e[j]);
-    ov[tid] = x;
+    st16<NT>(ov + tid, x);
   }
   const size_t tail0 = head + nvec * N;
   if (tid < head) o[tid] = op(a1[tid], a2[tid]);
@@ -130,7 +138,10 @@ static int launch2(const void *in, void *inout, size_t n, hipStream_t s) {
   const size_t nvec = N ? (n - head) / N : 0;
   size_t work = nvec;
   if (work < head + N) work = head + N;  // enough lanes for head + tail
-  hipLaunchKernelGGL((k_reduce2<T, OP>), dim3(grid_for(work)), dim3(kBlock), 0, s, a, b, n, head, nvec);
+  if (mx_nt_for(2 * n * sizeof(T)))
+    hipLaunchKernelGGL((k_reduce2<T, OP, true>), dim3(grid_for(work)), dim3(kBlock), 0, s, a, b, n, head, nvec);
+  else
+    hipLaunchKernelGGL((k_reduce2<T, OP, false>), dim3(grid_for(work)), dim3(kBlock), 0, s, a, b, n, head, nvec);
   return mx_check_launch();
 }
 
@@ -151,7 +162,10 @@ static int launch3(const void *in1, const void *in2, void *out, size_t n, hipStr
   const size_t nvec = N ? (n - head) / N : 0;
   size_t work = nvec;
   if (work < head + N) work = head + N;
-  hipLaunchKernelGGL((k_reduce3<T, OP>), dim3(grid_for(work)), dim3(kBlock), 0, s, a1, a2, o, n, head, nvec);
+  if (mx_nt_for(3 * n * sizeof(T)))
+    hipLaunchKernelGGL((k_reduce3<T, OP, true>), dim3(grid_for(work)), dim3(kBlock), 0, s, a1, a2, o, n, head, nvec);
+  else
+    hipLaunchKernelGGL((k_reduce3<T, OP, false>), dim3(grid_for(work)), dim3(kBlock), 0, s, a1, a2, o, n, head, nvec);
   return mx_check_launch();
 }
 

@@ -4,12 +4,32 @@
 // opal_cuda_check_bufs, opal/mca/common/cuda/common_cuda.c:1736-1857).
 #include <hip/hip_runtime.h>
 #include <stdio.h>
+#include <stdlib.h>
 #include <string.h>
 #include "mx_internal.h"
+#include "mx_mem.hpp"
 
 namespace mx {
 int g_num_cus = 256;
 int g_device = -1;
+
+// Launches whose streams together touch at least this many bytes use
+// non-temporal 16-byte accesses (mx_mem.hpp); MX_NT_MIN_BYTES overrides
+// (0 = always, -1 = never).  384 MiB: above the 256 MiB Infinity Cache a
+// re-used working set no longer stays on-die (measured crossover between
+// 2 x 128 MiB, where default accesses win 7.36 vs 6.42 TB/s, and 2 x 512 MiB,
+// where nt wins 6.32 vs 5.86 TB/s; profiles/r01/nt_policy_sizes.txt).
+static long long nt_min_bytes() {
+  static long long v = [] {
+    const char *e = getenv("MX_NT_MIN_BYTES");
+    return e ? atoll(e) : (384LL << 20);
+  }();
+  return v;
+}
+bool mx_nt_for(size_t bytes) {
+  const long long t = nt_min_bytes();
+  return t >= 0 && (long long)bytes >= t;
+}
 }  // namespace mx
 
 using namespace mx;
@@ -72,7 +92,9 @@ extern "C" int mx_stream_sync(void *stream) {
 extern "C" int mx_copy(void *dst, const void *src, size_t bytes, void *stream) {
   if (bytes == 0) return MX_SUCCESS;
   if (!dst || !src) return MX_ERR_ARG;
-  return mx_hip_rc(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToDevice, (hipStream_t)stream));
+  int rc = mx_ensure_init();
+  if (rc) return rc;
+  return copy_async(dst, src, bytes, (hipStream_t)stream);
 }
 
 extern "C" const char *mx_strerror(int rc) {

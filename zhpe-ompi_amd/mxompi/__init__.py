@@ -168,6 +168,9 @@ COMM_IPC, COMM_RCCL = 1, 2
 ALLREDUCE = {"auto": 0, "basic_linear": 1, "nonoverlapping": 2, "recursive_doubling": 3,
              "ring": 4, "segmented_ring": 5, "rabenseifner": 6, "rccl": 100}
 REDUCE_SCATTER = {"auto": 0, "nonoverlapping": 1, "recursive_halving": 2, "ring": 3, "rccl": 100}
+REDUCE = {"auto": 0, "linear": 1, "chain": 2, "pipeline": 3, "binary": 4, "binomial": 5,
+          "in_order_binary": 6, "rabenseifner": 7}
+SCAN = {"auto": 0, "linear": 1, "recursive_doubling": 2}
 
 class CollStats(ctypes.Structure):
     _fields_ = [("calls", ctypes.c_uint64), ("fold_launches", ctypes.c_uint64), ("fold_ms", ctypes.c_double),
@@ -200,6 +203,12 @@ def _coll_lib():
         L.mx_shmem_reduce.argtypes = [vp, i, i, sz, vp, vp, sz, vp]
         L.mx_comm_get_stats.argtypes = [vp, ctypes.POINTER(CollStats), i]
         L.mx_reduce_scatter_decision.argtypes = [i, sz, i]
+        L.mx_reduce_decision.argtypes = [i, sz, i]
+        L.mx_reduce.argtypes = [vp, vp, vp, sz, i, i, i, i, vp]
+        L.mx_reduce_local.argtypes = [vp, pp, pp, sz, i, i, i, i, vp]
+        for name in ("mx_scan", "mx_exscan", "mx_reduce_scatter_block"):
+            getattr(L, name).argtypes = [vp, vp, vp, sz, i, i, i, vp]
+            getattr(L, name + "_local").argtypes = [vp, pp, pp, sz, i, i, i, vp]
         L._mx_coll_typed = True
     return L
 
@@ -303,6 +312,22 @@ class Comm:
     def bcast(self, buf, nbytes, root, stream=0):
         check(_coll_lib().mx_bcast(self.h, buf, nbytes, root, stream or None), "mx_bcast")
 
+    def reduce(self, sbuf, rbuf, count, t, op, root, alg="auto", stream=0):
+        check(_coll_lib().mx_reduce(self.h, sbuf, rbuf or None, count, _slot(t), _op(op), root,
+                                    _alg(REDUCE, alg), stream or None), "mx_reduce")
+
+    def scan(self, sbuf, rbuf, count, t, op, alg="auto", stream=0):
+        check(_coll_lib().mx_scan(self.h, sbuf, rbuf, count, _slot(t), _op(op), _alg(SCAN, alg),
+                                  stream or None), "mx_scan")
+
+    def exscan(self, sbuf, rbuf, count, t, op, alg="auto", stream=0):
+        check(_coll_lib().mx_exscan(self.h, sbuf, rbuf, count, _slot(t), _op(op), _alg(SCAN, alg),
+                                    stream or None), "mx_exscan")
+
+    def reduce_scatter_block(self, sbuf, rbuf, rcount, t, op, alg="auto", stream=0):
+        check(_coll_lib().mx_reduce_scatter_block(self.h, sbuf, rbuf, rcount, _slot(t), _op(op),
+                                                  _alg(REDUCE, alg), stream or None), "mx_reduce_scatter_block")
+
     # -- local (all ranks in this process) ---------------------------------
     def allreduce_local(self, sbufs, rbufs, count, t, op, alg="auto", stream=0):
         sp = _ptrs(sbufs) if sbufs is not None else None
@@ -324,6 +349,25 @@ class Comm:
     def bcast_local(self, bufs, nbytes, root, stream=0):
         check(_coll_lib().mx_bcast_local(self.h, _ptrs(bufs), nbytes, root, stream or None), "mx_bcast_local")
 
+    def reduce_local(self, sbufs, rbufs, count, t, op, root, alg="auto", stream=0):
+        sp = _ptrs(sbufs) if sbufs is not None else None
+        check(_coll_lib().mx_reduce_local(self.h, sp, _ptrs(rbufs), count, _slot(t), _op(op), root,
+                                          _alg(REDUCE, alg), stream or None), "mx_reduce_local")
+
+    def _local3(self, name, table, sbufs, rbufs, count, t, op, alg, stream):
+        sp = _ptrs(sbufs) if sbufs is not None else None
+        check(getattr(_coll_lib(), name)(self.h, sp, _ptrs(rbufs), count, _slot(t), _op(op), _alg(table, alg),
+                                         stream or None), name)
+
+    def scan_local(self, sbufs, rbufs, count, t, op, alg="auto", stream=0):
+        self._local3("mx_scan_local", SCAN, sbufs, rbufs, count, t, op, alg, stream)
+
+    def exscan_local(self, sbufs, rbufs, count, t, op, alg="auto", stream=0):
+        self._local3("mx_exscan_local", SCAN, sbufs, rbufs, count, t, op, alg, stream)
+
+    def reduce_scatter_block_local(self, sbufs, rbufs, rcount, t, op, alg="auto", stream=0):
+        self._local3("mx_reduce_scatter_block_local", REDUCE, sbufs, rbufs, rcount, t, op, alg, stream)
+
 
 def allreduce_decision(n, count, t):
     return int(_coll_lib().mx_allreduce_decision(n, count, _slot(t)))
@@ -331,6 +375,10 @@ def allreduce_decision(n, count, t):
 
 def reduce_scatter_decision(n, total, t):
     return int(_coll_lib().mx_reduce_scatter_decision(n, total, _slot(t)))
+
+
+def reduce_decision(n, count, t):
+    return int(_coll_lib().mx_reduce_decision(n, count, _slot(t)))
 
 
 # ---------------------------------------------------------------------------
