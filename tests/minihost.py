@@ -42,6 +42,10 @@ def host(with_components=True):
     H.mxh_reduce_scatter.argtypes = [vp, vp, ctypes.POINTER(ci), vp, vp, vp]
     H.mxh_allgather.argtypes = [vp, ci, vp, vp, ci, vp, vp]
     H.mxh_bcast.argtypes = [vp, ci, vp, ci, vp]
+    H.mxh_reduce.argtypes = [vp, vp, ci, vp, vp, ci, vp]
+    H.mxh_reduce_scatter_block.argtypes = [vp, vp, ci, vp, vp, vp]
+    H.mxh_scan.argtypes = [vp, vp, ci, vp, vp, vp]
+    H.mxh_exscan.argtypes = [vp, vp, ci, vp, vp, vp]
     O = oracle_lib.oracle()
     base = ctypes.cast(O.mxo_reduce2, vp)
     pat = ctypes.cast(O.mxo_supported, vp)

@@ -1,8 +1,9 @@
 /*
  * coll_mi355x.c -- the `mi355x` component of Open MPI's `coll` framework.
  *
- * Takes the allreduce / reduce_scatter / allgather / bcast (and, above
- * coll/self's priority, reduce_local) slots of a communicator and runs them
+ * Takes the allreduce / reduce_scatter / allgather / bcast slots (plus
+ * reduce / reduce_scatter_block / scan / exscan and, above coll/self's
+ * priority, reduce_local) of a communicator and runs them
  * on the MI355X all-peer path of libmx_kernels.so (include/mx_coll.h) when
  * the buffers are device memory; everything else is handed to the module
  * that owned the slot before us.
@@ -48,6 +49,14 @@ typedef struct {
     mca_coll_base_module_t *prev_bcast_module;
     mca_coll_base_module_reduce_local_fn_t prev_reduce_local;
     mca_coll_base_module_t *prev_reduce_local_module;
+    mca_coll_base_module_reduce_fn_t prev_reduce;
+    mca_coll_base_module_t *prev_reduce_module;
+    mca_coll_base_module_reduce_scatter_block_fn_t prev_reduce_scatter_block;
+    mca_coll_base_module_t *prev_reduce_scatter_block_module;
+    mca_coll_base_module_scan_fn_t prev_scan;
+    mca_coll_base_module_t *prev_scan_module;
+    mca_coll_base_module_exscan_fn_t prev_exscan;
+    mca_coll_base_module_t *prev_exscan_module;
 } mx_coll_module_t;
 
 static int map_rc(int rc)
@@ -69,6 +78,10 @@ static void coll_module_destruct(void *obj)
     if (m->prev_allgather_module) MX_OBJ_RELEASE(m->prev_allgather_module);
     if (m->prev_bcast_module) MX_OBJ_RELEASE(m->prev_bcast_module);
     if (m->prev_reduce_local_module) MX_OBJ_RELEASE(m->prev_reduce_local_module);
+    if (m->prev_reduce_module) MX_OBJ_RELEASE(m->prev_reduce_module);
+    if (m->prev_reduce_scatter_block_module) MX_OBJ_RELEASE(m->prev_reduce_scatter_block_module);
+    if (m->prev_scan_module) MX_OBJ_RELEASE(m->prev_scan_module);
+    if (m->prev_exscan_module) MX_OBJ_RELEASE(m->prev_exscan_module);
     free(m);
 }
 
@@ -173,6 +186,90 @@ static int mx_coll_reduce_local(const void *inbuf, void *inoutbuf, int count, st
     return m->prev_reduce_local(inbuf, inoutbuf, count, dtype, op, m->prev_reduce_local_module);
 }
 
+/* Reduction slots beyond the four of the north star:
+ * MPI_Reduce (coll.h:239-241), MPI_Reduce_scatter_block (:245-247),
+ * MPI_Scan / MPI_Exscan (:248-250, :228-230).  Same device / host split
+ * and delegation; algorithms follow coll/tuned's fixed decisions (reduce:
+ * coll_tuned_decision_fixed.c:354-429; reduce_scatter_block: basic_linear,
+ * :522-532) and coll/basic's linear scan / exscan (tuned leaves those slots
+ * empty, coll_tuned_module.c:106,112), or the forced algorithm of the MCA
+ * vars coll_mi355x_{reduce,scan,exscan}_algorithm (tuned's numbering). */
+static int reducible(mx_coll_module_t *m, struct ompi_datatype_t *dtype, struct ompi_op_t *op, int count, int *slot,
+                     int *opi)
+{
+    *slot = mx_ompi_host->dtype_slot(dtype);
+    *opi = mx_ompi_host->op_index(op);
+    return m->mx && count > 0 && *slot >= 0 && (mx_ompi_host->op_flags(op) & OMPI_OP_FLAGS_INTRINSIC) &&
+           mx_op_supported(*opi, *slot, MX_TABLE_WITH_FORTRAN) && mx_ompi_host->dtype_contiguous(dtype, count);
+}
+
+static int mx_coll_reduce(const void *sbuf, void *rbuf, int count, struct ompi_datatype_t *dtype,
+                          struct ompi_op_t *op, int root, struct ompi_communicator_t *comm,
+                          mca_coll_base_module_t *module)
+{
+    mx_coll_module_t *m = (mx_coll_module_t *)module;
+    const int rank = mx_ompi_host->comm_rank(comm);
+    int slot, opi;
+    /* rbuf matters on the root only (MPI-3.1 5.9.1) */
+    if (reducible(m, dtype, op, count, &slot, &opi) && (sbuf == MPI_IN_PLACE ? rank == root : on_device(sbuf)) &&
+        (rank != root || on_device(rbuf))) {
+        const int alg = mx_ompi_host->mca_int("coll_mi355x_reduce_algorithm", MX_REDUCE_AUTO);
+        int rc = mx_reduce(m->mx, sbuf == MPI_IN_PLACE ? MX_IN_PLACE : sbuf, rank == root ? rbuf : NULL,
+                           (size_t)count, slot, opi, root, alg, NULL);
+        if (rc != MX_ERR_UNSUPPORTED) return map_rc(rc);
+    }
+    return m->prev_reduce(sbuf, rbuf, count, dtype, op, root, comm, m->prev_reduce_module);
+}
+
+static int mx_coll_reduce_scatter_block(const void *sbuf, void *rbuf, int rcount, struct ompi_datatype_t *dtype,
+                                        struct ompi_op_t *op, struct ompi_communicator_t *comm,
+                                        mca_coll_base_module_t *module)
+{
+    mx_coll_module_t *m = (mx_coll_module_t *)module;
+    const int n = mx_ompi_host->comm_size(comm);
+    int slot, opi;
+    if (reducible(m, dtype, op, rcount * n, &slot, &opi) && (sbuf == MPI_IN_PLACE || on_device(sbuf)) &&
+        on_device(rbuf)) {
+        const int alg = mx_ompi_host->mca_int("coll_mi355x_reduce_algorithm", MX_REDUCE_AUTO);
+        int rc = mx_reduce_scatter_block(m->mx, sbuf == MPI_IN_PLACE ? MX_IN_PLACE : sbuf, rbuf, (size_t)rcount,
+                                         slot, opi, alg, NULL);
+        if (rc != MX_ERR_UNSUPPORTED) return map_rc(rc);
+    }
+    return m->prev_reduce_scatter_block(sbuf, rbuf, rcount, dtype, op, comm, m->prev_reduce_scatter_block_module);
+}
+
+static int scan_common(mx_coll_module_t *m, const void *sbuf, void *rbuf, int count, struct ompi_datatype_t *dtype,
+                       struct ompi_op_t *op, int exclusive)
+{
+    int slot, opi;
+    if (reducible(m, dtype, op, count, &slot, &opi) && (sbuf == MPI_IN_PLACE || on_device(sbuf)) &&
+        on_device(rbuf)) {
+        const int alg = mx_ompi_host->mca_int(exclusive ? "coll_mi355x_exscan_algorithm"
+                                                        : "coll_mi355x_scan_algorithm", MX_SCAN_AUTO);
+        const void *sb = sbuf == MPI_IN_PLACE ? MX_IN_PLACE : sbuf;
+        int rc = exclusive ? mx_exscan(m->mx, sb, rbuf, (size_t)count, slot, opi, alg, NULL)
+                           : mx_scan(m->mx, sb, rbuf, (size_t)count, slot, opi, alg, NULL);
+        if (rc != MX_ERR_UNSUPPORTED) return map_rc(rc);
+    }
+    return 1;   /* delegate */
+}
+
+static int mx_coll_scan(const void *sbuf, void *rbuf, int count, struct ompi_datatype_t *dtype,
+                        struct ompi_op_t *op, struct ompi_communicator_t *comm, mca_coll_base_module_t *module)
+{
+    mx_coll_module_t *m = (mx_coll_module_t *)module;
+    int rc = scan_common(m, sbuf, rbuf, count, dtype, op, 0);
+    return rc != 1 ? rc : m->prev_scan(sbuf, rbuf, count, dtype, op, comm, m->prev_scan_module);
+}
+
+static int mx_coll_exscan(const void *sbuf, void *rbuf, int count, struct ompi_datatype_t *dtype,
+                          struct ompi_op_t *op, struct ompi_communicator_t *comm, mca_coll_base_module_t *module)
+{
+    mx_coll_module_t *m = (mx_coll_module_t *)module;
+    int rc = scan_common(m, sbuf, rbuf, count, dtype, op, 1);
+    return rc != 1 ? rc : m->prev_exscan(sbuf, rbuf, count, dtype, op, comm, m->prev_exscan_module);
+}
+
 /* ---- module enable / component query ------------------------------------ */
 
 #define SAVE_PREV(m, comm, name, type)                                                              \
@@ -194,6 +291,10 @@ static int mx_coll_module_enable(mca_coll_base_module_t *module, struct ompi_com
         SAVE_PREV(m, comm, reduce_scatter, mca_coll_base_module_reduce_scatter_fn_t);
         SAVE_PREV(m, comm, allgather, mca_coll_base_module_allgather_fn_t);
         SAVE_PREV(m, comm, bcast, mca_coll_base_module_bcast_fn_t);
+        SAVE_PREV(m, comm, reduce, mca_coll_base_module_reduce_fn_t);
+        SAVE_PREV(m, comm, reduce_scatter_block, mca_coll_base_module_reduce_scatter_block_fn_t);
+        SAVE_PREV(m, comm, scan, mca_coll_base_module_scan_fn_t);
+        SAVE_PREV(m, comm, exscan, mca_coll_base_module_exscan_fn_t);
     }
     if (m->super.coll_reduce_local) SAVE_PREV(m, comm, reduce_local, mca_coll_base_module_reduce_local_fn_t);
     if (m->super.coll_allreduce && n > 1 && n <= MX_MAX_RANKS) {
@@ -230,6 +331,10 @@ static mca_coll_base_module_t *mx_coll_component_comm_query(struct ompi_communic
         m->super.coll_reduce_scatter = mx_coll_reduce_scatter;
         m->super.coll_allgather = mx_coll_allgather;
         m->super.coll_bcast = mx_coll_bcast;
+        m->super.coll_reduce = mx_coll_reduce;
+        m->super.coll_reduce_scatter_block = mx_coll_reduce_scatter_block;
+        m->super.coll_scan = mx_coll_scan;
+        m->super.coll_exscan = mx_coll_exscan;
     } else {
         /* size-1 comms (MPI_COMM_SELF): MPI_Reduce_local lands here when
          * our priority beats coll/self's 75 (coll_self_module.c:60,84) */

@@ -162,8 +162,9 @@ static int mca_int(const char *name, int def)
 }
 
 /* ---- communicators --------------------------------------------------------- */
-#define NSLOTS 5
-static const char *g_slot_names[NSLOTS] = {"allreduce", "reduce_scatter", "allgather", "bcast", "reduce_local"};
+#define NSLOTS 9
+static const char *g_slot_names[NSLOTS] = {"allreduce", "reduce_scatter", "allgather", "bcast", "reduce_local",
+                                           "reduce", "reduce_scatter_block", "scan", "exscan"};
 
 struct ompi_communicator_t {
     int rank, size;
@@ -271,6 +272,65 @@ static int base_bcast(void *buf, int count, struct ompi_datatype_t *dt, int root
     return OMPI_SUCCESS;
 }
 
+/* rooted reduce, basic linear order (coll_base_reduce.c:626-735) */
+static int base_reduce(const void *sbuf, void *rbuf, int count, struct ompi_datatype_t *dt, struct ompi_op_t *op,
+                       int root, struct ompi_communicator_t *c, mca_coll_base_module_t *m)
+{
+    size_t b = (size_t)count * dt->size;
+    char *all = malloc(b * c->size + 1);
+    (void)m;
+    if (!all) return OMPI_ERR_OUT_OF_RESOURCE;
+    if (c->ag(sbuf == MPI_IN_PLACE ? rbuf : sbuf, all, b, c->ag_ctx)) { free(all); return OMPI_ERROR; }
+    if (c->rank == root) {
+        memcpy(rbuf, all + (size_t)(c->size - 1) * b, b);
+        for (int i = c->size - 2; i >= 0; i--) op_reduce(op, all + (size_t)i * b, rbuf, count, dt);
+    }
+    free(all);
+    return OMPI_SUCCESS;
+}
+
+static int base_reduce_scatter_block(const void *sbuf, void *rbuf, int rcount, struct ompi_datatype_t *dt,
+                                     struct ompi_op_t *op, struct ompi_communicator_t *c, mca_coll_base_module_t *m)
+{
+    int rcounts[256];
+    if (c->size > 256) return OMPI_ERR_NOT_SUPPORTED;
+    for (int i = 0; i < c->size; i++) rcounts[i] = rcount;
+    return base_reduce_scatter(sbuf, rbuf, rcounts, dt, op, c, m);
+}
+
+/* linear scan / exscan (coll_base_scan.c:35-122, coll_base_exscan.c:35-107) */
+static int base_scan_common(const void *sbuf, void *rbuf, int count, struct ompi_datatype_t *dt, struct ompi_op_t *op,
+                            struct ompi_communicator_t *c, int exclusive)
+{
+    size_t b = (size_t)count * dt->size;
+    char *all = malloc(b * c->size + 1), *acc = malloc(b + 1), *tmp = malloc(b + 1);
+    int rc = OMPI_SUCCESS;
+    if (!all || !acc || !tmp) { rc = OMPI_ERR_OUT_OF_RESOURCE; goto out; }
+    if (c->ag(sbuf == MPI_IN_PLACE ? rbuf : sbuf, all, b, c->ag_ctx)) { rc = OMPI_ERROR; goto out; }
+    memcpy(acc, all, b);
+    for (int r = 1; r <= (exclusive ? c->rank - 1 : c->rank); r++) {
+        memcpy(tmp, all + (size_t)r * b, b);                 /* own data is the target */
+        op_reduce(op, acc, tmp, count, dt);
+        memcpy(acc, tmp, b);
+    }
+    if (!exclusive || c->rank > 0) memcpy(rbuf, acc, b);
+out:
+    free(all); free(acc); free(tmp);
+    return rc;
+}
+static int base_scan(const void *sbuf, void *rbuf, int count, struct ompi_datatype_t *dt, struct ompi_op_t *op,
+                     struct ompi_communicator_t *c, mca_coll_base_module_t *m)
+{
+    (void)m;
+    return base_scan_common(sbuf, rbuf, count, dt, op, c, 0);
+}
+static int base_exscan(const void *sbuf, void *rbuf, int count, struct ompi_datatype_t *dt, struct ompi_op_t *op,
+                       struct ompi_communicator_t *c, mca_coll_base_module_t *m)
+{
+    (void)m;
+    return base_scan_common(sbuf, rbuf, count, dt, op, c, 1);
+}
+
 /* coll/self-like reduce_local: mca_coll_base_reduce_local (coll_base_reduce.c:42-49) */
 static int base_reduce_local(const void *in, void *inout, int count, struct ompi_datatype_t *dt, struct ompi_op_t *op,
                              mca_coll_base_module_t *m)
@@ -348,13 +408,19 @@ static int comm_select(struct ompi_communicator_t *c, int is_self)
         base->coll_allgather = base_allgather;
         base->coll_bcast = base_bcast;
         base->coll_reduce_local = base_reduce_local;
+        base->coll_reduce = base_reduce;
+        base->coll_reduce_scatter_block = base_reduce_scatter_block;
+        base->coll_scan = base_scan;
+        base->coll_exscan = base_exscan;
     }
     /* lowest priority first: the base module (30 / 75) */
 #define COPY(MOD, OWNER)                                                                             \
     do {                                                                                             \
         void *f_[NSLOTS] = {(void *)(MOD)->coll_allreduce, (void *)(MOD)->coll_reduce_scatter,       \
                             (void *)(MOD)->coll_allgather, (void *)(MOD)->coll_bcast,                \
-                            (void *)(MOD)->coll_reduce_local};                                        \
+                            (void *)(MOD)->coll_reduce_local, (void *)(MOD)->coll_reduce,            \
+                            (void *)(MOD)->coll_reduce_scatter_block, (void *)(MOD)->coll_scan,      \
+                            (void *)(MOD)->coll_exscan};                                             \
         for (int i_ = 0; i_ < NSLOTS; i_++)                                                          \
             if (f_[i_]) { c->fn[i_] = f_[i_]; c->mod[i_] = (MOD); c->owner[i_] = (OWNER); }          \
     } while (0)
@@ -505,4 +571,31 @@ int mxh_bcast(void *buf, int count, void *dt, int root, void *cv)
 {
     struct ompi_communicator_t *c = cv;
     return ((mca_coll_base_module_bcast_fn_t)c->fn[3])(buf, count, dt, root, c, c->mod[3]);
+}
+
+int mxh_reduce(const void *sbuf, void *rbuf, int count, void *dt, void *op, int root, void *cv)
+{
+    struct ompi_communicator_t *c = cv;
+    struct ompi_datatype_t *d = dt;
+    if (!d || d->slot < 0 || !((struct ompi_op_t *)op)->intrinsic.fns[d->slot]) return -1;
+    if (root < 0 || root >= c->size) return -1;
+    return ((mca_coll_base_module_reduce_fn_t)c->fn[5])(sbuf, rbuf, count, d, op, root, c, c->mod[5]);
+}
+
+int mxh_reduce_scatter_block(const void *sbuf, void *rbuf, int rcount, void *dt, void *op, void *cv)
+{
+    struct ompi_communicator_t *c = cv;
+    return ((mca_coll_base_module_reduce_scatter_block_fn_t)c->fn[6])(sbuf, rbuf, rcount, dt, op, c, c->mod[6]);
+}
+
+int mxh_scan(const void *sbuf, void *rbuf, int count, void *dt, void *op, void *cv)
+{
+    struct ompi_communicator_t *c = cv;
+    return ((mca_coll_base_module_scan_fn_t)c->fn[7])(sbuf, rbuf, count, dt, op, c, c->mod[7]);
+}
+
+int mxh_exscan(const void *sbuf, void *rbuf, int count, void *dt, void *op, void *cv)
+{
+    struct ompi_communicator_t *c = cv;
+    return ((mca_coll_base_module_exscan_fn_t)c->fn[8])(sbuf, rbuf, count, dt, op, c, c->mod[8]);
 }

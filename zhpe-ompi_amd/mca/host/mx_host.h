@@ -9,7 +9,8 @@
  *     modules lowest -> highest priority, COPY each non-NULL slot;
  *   - the MPI entry points MPI_Reduce_local (reduce_local.c:46-91),
  *     MPI_Allreduce (allreduce.c:46-118), MPI_Reduce_scatter, MPI_Allgather,
- *     MPI_Bcast: parameter checks + dispatch through comm->c_coll;
+ *     MPI_Bcast, MPI_Reduce, MPI_Reduce_scatter_block, MPI_Scan, MPI_Exscan:
+ *     parameter checks + dispatch through comm->c_coll;
  *   - a host "base" coll module standing in for coll/tuned + basic on host
  *     buffers, and a coll/self-like module (priority 75) for COMM_SELF.
  * The base op functions and the host transport are injected by the test.
@@ -52,6 +53,10 @@ int mxh_allreduce(const void *sbuf, void *rbuf, int count, void *dtype, void *op
 int mxh_reduce_scatter(const void *sbuf, void *rbuf, const int *rcounts, void *dtype, void *op, void *comm);
 int mxh_allgather(const void *sbuf, int scount, void *sdtype, void *rbuf, int rcount, void *rdtype, void *comm);
 int mxh_bcast(void *buf, int count, void *dtype, int root, void *comm);
+int mxh_reduce(const void *sbuf, void *rbuf, int count, void *dtype, void *op, int root, void *comm);
+int mxh_reduce_scatter_block(const void *sbuf, void *rbuf, int rcount, void *dtype, void *op, void *comm);
+int mxh_scan(const void *sbuf, void *rbuf, int count, void *dtype, void *op, void *comm);
+int mxh_exscan(const void *sbuf, void *rbuf, int count, void *dtype, void *op, void *comm);
 #define MXH_IN_PLACE ((void *)1)
 
 #ifdef __cplusplus

@@ -13,7 +13,7 @@
  *   ompi_op_base_component_1_0_0_t     ompi/mca/op/op.h:331-341
  *   mca_coll_base_module_2_3_0_t       ompi/mca/coll/coll.h:504-604
  *   mca_coll_base_component_2_0_0_t    ompi/mca/coll/coll.h:471-481
- *   slot typedefs                      ompi/mca/coll/coll.h:195-244, 440-443
+ *   slot typedefs                      ompi/mca/coll/coll.h:195-250, 440-443
  *
  * Building against a real Open MPI tree: compile the components with
  * -DMX_OMPI_REAL and the Open MPI include paths; this header then includes
@@ -150,6 +150,17 @@ typedef int (*mca_coll_base_module_reduce_scatter_fn_t)(const void *sbuf, void *
 typedef int (*mca_coll_base_module_reduce_local_fn_t)(const void *inbuf, void *inoutbuf, int count,
                                                       struct ompi_datatype_t *dtype, struct ompi_op_t *op,
                                                       mca_coll_base_module_t *module);
+typedef int (*mca_coll_base_module_reduce_fn_t)(const void *sbuf, void *rbuf, int count,
+                                                struct ompi_datatype_t *dtype, struct ompi_op_t *op, int root,
+                                                struct ompi_communicator_t *comm, mca_coll_base_module_t *module);
+typedef int (*mca_coll_base_module_reduce_scatter_block_fn_t)(const void *sbuf, void *rbuf, int rcount,
+                                                              struct ompi_datatype_t *dtype, struct ompi_op_t *op,
+                                                              struct ompi_communicator_t *comm,
+                                                              mca_coll_base_module_t *module);
+typedef int (*mca_coll_base_module_scan_fn_t)(const void *sbuf, void *rbuf, int count, struct ompi_datatype_t *dtype,
+                                              struct ompi_op_t *op, struct ompi_communicator_t *comm,
+                                              mca_coll_base_module_t *module);
+typedef mca_coll_base_module_scan_fn_t mca_coll_base_module_exscan_fn_t;
 typedef int (*mca_coll_base_module_ft_event_fn_t)(int state);
 typedef void *mx_coll_slot_unused_t;   /* slots this component never fills */
 
@@ -162,9 +173,13 @@ struct mca_coll_base_module_2_3_0_t {
     mca_coll_base_module_allreduce_fn_t coll_allreduce;
     mx_coll_slot_unused_t coll_alltoall, coll_alltoallv, coll_alltoallw, coll_barrier;
     mca_coll_base_module_bcast_fn_t coll_bcast;
-    mx_coll_slot_unused_t coll_exscan, coll_gather, coll_gatherv, coll_reduce;
+    mca_coll_base_module_exscan_fn_t coll_exscan;
+    mx_coll_slot_unused_t coll_gather, coll_gatherv;
+    mca_coll_base_module_reduce_fn_t coll_reduce;
     mca_coll_base_module_reduce_scatter_fn_t coll_reduce_scatter;
-    mx_coll_slot_unused_t coll_reduce_scatter_block, coll_scan, coll_scatter, coll_scatterv;
+    mca_coll_base_module_reduce_scatter_block_fn_t coll_reduce_scatter_block;
+    mca_coll_base_module_scan_fn_t coll_scan;
+    mx_coll_slot_unused_t coll_scatter, coll_scatterv;
     /* nonblocking (17) */
     mx_coll_slot_unused_t coll_iallgather, coll_iallgatherv, coll_iallreduce, coll_ialltoall, coll_ialltoallv,
         coll_ialltoallw, coll_ibarrier, coll_ibcast, coll_iexscan, coll_igather, coll_igatherv, coll_ireduce,
