@@ -156,9 +156,11 @@ def bench_allreduce(torch, mx, dist, rank, world, dev, steps, warmup, nbytes=256
     ndev = torch.cuda.device_count()
     flags = mx.COMM_IPC | (mx.COMM_RCCL if ndev >= world else 0)
     try:
-        comm = mx.Comm(rank, world, ag, device=dev, staging_bytes=2 * nbytes + (64 << 20), flags=flags)
+        comm = mx.Comm(rank, world, ag, device=dev, staging_bytes=2 * nbytes + (64 << 20), flags=flags,
+                       heap_bytes=2 * nbytes + (4 << 20))
     except mx.MxError:
-        comm = mx.Comm(rank, world, ag, device=dev, staging_bytes=2 * nbytes + (64 << 20), flags=mx.COMM_IPC)
+        comm = mx.Comm(rank, world, ag, device=dev, staging_bytes=2 * nbytes + (64 << 20), flags=mx.COMM_IPC,
+                       heap_bytes=2 * nbytes + (4 << 20))
         flags = mx.COMM_IPC
     g = torch.Generator(device="cuda").manual_seed(0x5EED + rank)
     x = torch.rand(count, device="cuda", generator=g) * 2 - 1
@@ -191,6 +193,7 @@ def bench_allreduce(torch, mx, dist, rank, world, dev, steps, warmup, nbytes=256
     st = comm.stats(reset=True)
     comm.set_profiling(False)
     sweep = allreduce_sweep(torch, mx, dist, comm, world, x, out, sp, flags)
+    cfge = cfg_e(torch, mx, dist, comm, world, rank, sp)
     extra = {}
     if flags & mx.COMM_RCCL:
         try:
@@ -221,29 +224,46 @@ def bench_allreduce(torch, mx, dist, rank, world, dev, steps, warmup, nbytes=256
                      "phase_ms_per_call": {k: round(st[k] / max(1, st["calls"]), 4)
                                            for k in ("fold_ms", "push_ms", "gather_ms", "total_ms")}},
         "sweep": sweep,
+        "cfg_e": cfge,
     }
 
 
-def allreduce_sweep(torch, mx, dist, comm, world, x, out, sp, flags, budget_s=20.0):
-    """Compact CFG-D sweep (BASELINE configs[3]): busBW / latency of
-    MPI_Allreduce for a few sizes and fold orders (fp32 SUM, uint16 BAND),
-    max over ranks.  Bounded to ~budget_s seconds in total."""
+def allreduce_sweep(torch, mx, dist, comm, world, x, out, sp, flags, budget_s=45.0):
+    """CFG-D sweep (BASELINE configs[3]): MPI_Allreduce busBW / latency from
+    8 B to 4 GiB per rank (x4 steps) for fp32 SUM under the tuned decision,
+    the forced ring and Rabenseifner fold orders and RCCL, plus uint16 BAND
+    (bf16-as-uint16); max over ranks, bounded to ~budget_s seconds."""
     rows = []
     algs = ["auto", "ring", "rabenseifner"] + (["rccl"] if flags & mx.COMM_RCCL else [])
     t_start = time.perf_counter()
-    for nbytes in (8, 1 << 10, 64 << 10, 1 << 20, 16 << 20, 256 << 20):
+    big = None
+    sizes = [8 << (2 * k) for k in range(15)] + [4 << 30]       # 8 B, 32 B, ..., 2 GiB, 4 GiB
+    for nbytes in sizes:
+        if nbytes > x.numel() * 4:
+            if big is None:   # one pair of buffers for every size above the headline's, sized for the largest
+                try:
+                    big = (torch.empty(sizes[-1] // 4, device="cuda").uniform_(-1, 1),
+                           torch.empty(sizes[-1] // 4, device="cuda"))
+                except RuntimeError:
+                    rows.append({"bytes": nbytes, "error": "out of device memory"})
+                    break
+            bx, bo = big
+        else:
+            bx, bo = x, out
+        assert bx.numel() * 4 >= nbytes and bo.numel() * 4 >= nbytes, "sweep buffer smaller than the message"
         for t, op in (("FLOAT", "SUM"), ("UINT16_T", "BAND")):
-            if t == "UINT16_T" and nbytes not in (64 << 10, 16 << 20):
+            if t == "UINT16_T" and nbytes not in (8, 64 << 10, 16 << 20, 256 << 20, 4 << 30):
                 continue
             count = max(1, nbytes // (4 if t == "FLOAT" else 2))
-            iters = 50 if nbytes <= (64 << 10) else (20 if nbytes <= (1 << 20) else (10 if nbytes <= (16 << 20) else 5))
+            iters = 50 if nbytes <= (64 << 10) else (20 if nbytes <= (4 << 20) else (8 if nbytes <= (64 << 20)
+                                                                                      else 3))
             for alg in algs:
                 if alg == "rccl" and t == "UINT16_T":
                     continue
                 ok = torch.tensor([1.0])
                 try:
                     for _ in range(2):
-                        comm.allreduce(x.data_ptr(), out.data_ptr(), count, t, op, alg, sp)
+                        comm.allreduce(bx.data_ptr(), bo.data_ptr(), count, t, op, alg, sp)
                     torch.cuda.synchronize()
                 except mx.MxError:
                     ok[0] = 0.0
@@ -254,7 +274,7 @@ def allreduce_sweep(torch, mx, dist, comm, world, x, out, sp, flags, budget_s=20
                 dist.barrier()
                 t0 = time.perf_counter()
                 for _ in range(iters):
-                    comm.allreduce(x.data_ptr(), out.data_ptr(), count, t, op, alg, sp)
+                    comm.allreduce(bx.data_ptr(), bo.data_ptr(), count, t, op, alg, sp)
                 torch.cuda.synchronize()
                 el = torch.tensor([time.perf_counter() - t0], dtype=torch.float64)
                 dist.all_reduce(el, op=dist.ReduceOp.MAX)
@@ -262,9 +282,80 @@ def allreduce_sweep(torch, mx, dist, comm, world, x, out, sp, flags, budget_s=20
                 algbw = count * (4 if t == "FLOAT" else 2) / per / 1e9
                 rows.append({"bytes": nbytes, "type": t, "op": op, "alg": alg, "us": round(per * 1e6, 2),
                              "algbw_gbs": round(algbw, 2), "busbw_gbs": round(algbw * 2 * (world - 1) / world, 2)})
-            if time.perf_counter() - t_start > budget_s:
-                return rows
+        done = torch.tensor([1.0 if time.perf_counter() - t_start > budget_s else 0.0])
+        dist.all_reduce(done, op=dist.ReduceOp.MAX)
+        if done[0] > 0:
+            rows.append({"note": f"sweep stopped after {nbytes} B (time budget {budget_s} s)"})
+            break
+    del big
+    torch.cuda.empty_cache()
     return rows
+
+
+def cfg_e(torch, mx, dist, comm, world, rank, sp, nbytes=256 << 20, iters=5):
+    """CFG-E (BASELINE configs[4]) at 256 MiB: MPI_Reduce_scatter and
+    MPI_Allgather (busBW = algBW*(n-1)/n, algBW over the full vector),
+    MAXLOC float_int allreduce, OpenSHMEM float max_to_all and the other
+    reduction slots (rooted reduce, reduce_scatter_block, scan), each with the
+    coll/tuned (or coll/basic) fold order; max over ranks."""
+    res = {}
+    count = nbytes // 4
+    g = torch.Generator(device="cuda").manual_seed(0x5EED + 101 * rank)
+    x = torch.rand(count, device="cuda", generator=g)
+    y = torch.empty_like(x)
+
+    def timed(name, fn, algbw_bytes, factor):
+        try:
+            fn()
+            torch.cuda.synchronize()
+            dist.barrier()
+            t0 = time.perf_counter()
+            for _ in range(iters):
+                fn()
+            torch.cuda.synchronize()
+            el = torch.tensor([time.perf_counter() - t0], dtype=torch.float64)
+            dist.all_reduce(el, op=dist.ReduceOp.MAX)
+            per = float(el[0]) / iters
+            res[name] = {"ms": round(per * 1e3, 4), "algbw_gbs": round(algbw_bytes / per / 1e9, 2),
+                         "busbw_gbs": round(algbw_bytes / per / 1e9 * factor, 2)}
+        except mx.MxError as e:
+            res[name] = {"error": str(e)}
+
+    f_ring = (world - 1) / world
+    rc = [count // world] * world
+    timed("reduce_scatter_fp32_sum", lambda: comm.reduce_scatter(x.data_ptr(), y.data_ptr(), rc, "FLOAT", "SUM",
+                                                                "auto", sp), nbytes, f_ring)
+    per_rank = nbytes // world
+    timed("allgather", lambda: comm.allgather(x.data_ptr(), y.data_ptr(), per_rank, sp), nbytes, f_ring)
+    timed("bcast", lambda: comm.bcast(x.data_ptr(), nbytes, 0, sp), nbytes, 1.0)
+    # MPI_FLOAT_INT pairs: 8 B per element, value ties and random indices
+    timed("allreduce_maxloc_float_int", lambda: comm.allreduce(x.data_ptr(), y.data_ptr(), count // 2, "FLOAT_INT",
+                                                               "MAXLOC", "auto", sp), nbytes, 2 * f_ring)
+    timed("shmem_float_max_to_all", lambda: comm.shmem_reduce("MAX", "FLOAT", 4, y.data_ptr(), x.data_ptr(), count,
+                                                              sp), nbytes, 2 * f_ring)
+    timed("reduce_fp32_sum_root0", lambda: comm.reduce(x.data_ptr(), y.data_ptr(), count, "FLOAT", "SUM", 0,
+                                                       "auto", sp), nbytes, 1.0)
+    timed("reduce_scatter_block_fp32_sum", lambda: comm.reduce_scatter_block(x.data_ptr(), y.data_ptr(),
+                                                                             count // world, "FLOAT", "SUM",
+                                                                             "auto", sp), nbytes, f_ring)
+    timed("scan_fp32_sum", lambda: comm.scan(x.data_ptr(), y.data_ptr(), count, "FLOAT", "SUM", "auto", sp),
+          nbytes, 1.0)
+    # OpenSHMEM max_to_all on the device symmetric heap: every PE folds its
+    # part straight from all sources into all targets (no staging copies)
+    try:
+        heap = mx.Heap(comm, 2 * nbytes + (1 << 20))
+        src, tgt = heap.alloc(nbytes), heap.alloc(nbytes)
+        mx.lib().mx_copy(src, x.data_ptr(), nbytes, None)
+        mx.sync()
+        heap.barrier_all()
+        timed("shmem_float_max_to_all_symheap", lambda: heap.reduce("MAX", "FLOAT", 4, tgt, src, count, stream=sp),
+              nbytes, 2 * f_ring)
+        heap.close()
+    except mx.MxError as e:
+        res["shmem_float_max_to_all_symheap"] = {"error": str(e)}
+    del x, y
+    torch.cuda.empty_cache()
+    return res
 
 
 def main():

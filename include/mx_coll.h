@@ -69,6 +69,11 @@ typedef int (*mx_allgather_fn)(const void *send, void *recv, size_t bytes, void 
 /* Multi-process communicator: one rank per process (per GPU). */
 int mx_comm_create(int rank, int size, int device, size_t staging_bytes, int flags,
                    mx_allgather_fn allgather, void *ctx, mx_comm_t **comm);
+/* As mx_comm_create, plus a symmetric-heap region of heap_bytes per rank,
+ * exported and mapped (and verified) with the staging; mx_heap_create
+ * carves heaps from it (see "device symmetric heap" below). */
+int mx_comm_create_ex(int rank, int size, int device, size_t staging_bytes, size_t heap_bytes, int flags,
+                      mx_allgather_fn allgather, void *ctx, mx_comm_t **comm);
 /* `size` virtual ranks in ONE process on ONE device.  Same algorithms, same
  * kernels, same fold order; the data path reads/writes all ranks' buffers
  * directly (no staging, no flags).  Used by the parity tests on a single
@@ -187,6 +192,35 @@ int mx_shmem_to_mpi(int shmem_op, int shmem_type, size_t dt_size, int *mx_op, in
  * exactly what scoll/mpi asks of coll/tuned. */
 int mx_shmem_reduce(mx_comm_t *comm, int shmem_op, int shmem_type, size_t dt_size, void *target,
                     const void *source, size_t nreduce, void *stream);
+
+/* ---- device symmetric heap (OpenSHMEM on device memory) ------------------
+ * Replaces, for GPU-resident symmetric data, the host-only symmetric heap of
+ * oshmem/mca/sshmem + oshmem/mca/memheap (device addresses fail
+ * RUNTIME_CHECK_ADDR today, oshmem/runtime/runtime.h:205-210).  Collective
+ * over `comm` (same `bytes` on every PE): each PE allocates its heap in
+ * device memory and maps every peer's.  mx_shmalloc / mx_shfree are
+ * collective too (same call sequence on every PE -> same offsets). */
+typedef struct mx_heap mx_heap_t;
+int mx_heap_create(mx_comm_t *comm, size_t bytes, mx_heap_t **heap);
+int mx_heap_destroy(mx_heap_t *heap);
+void *mx_heap_base(const mx_heap_t *heap);
+void *mx_shmalloc(mx_heap_t *heap, size_t bytes);
+int mx_shfree(mx_heap_t *heap, void *ptr);
+/* shmem_ptr (oshmem/shmem/c/shmem_ptr.c:32-70): `addr` as PE `pe`'s array,
+ * directly loadable/storable by kernels on this GPU; NULL if not symmetric. */
+void *mx_shmem_ptr(const mx_heap_t *heap, const void *addr, int pe);
+/* shmem_putmem / shmem_getmem (blocking; device copies over xGMI). */
+int mx_shmem_putmem(mx_heap_t *heap, void *dest, const void *src, size_t bytes, int pe, void *stream);
+int mx_shmem_getmem(mx_heap_t *heap, void *dest, const void *src, size_t bytes, int pe, void *stream);
+int mx_shmem_barrier_all(mx_heap_t *heap, void *stream);
+/* shmem_<type>_<op>_to_all (shmem_reduce.c:29-65) on symmetric target and
+ * source over the active set (PE_start, logPE_stride, PE_size): every member
+ * folds its element part straight from all members' sources into all
+ * members' targets (no staging), in the order coll/tuned gives scoll/mpi's
+ * allreduce on the active set, i.e. bit-identical to mx_shmem_reduce. */
+int mx_shmem_reduce_heap(mx_heap_t *heap, int shmem_op, int shmem_type, size_t dt_size, void *target,
+                         const void *source, size_t nreduce, int pe_start, int log_pe_stride,
+                         int pe_size, void *stream);
 
 /* ---- local communicator: arrays of `size` buffers, one per rank --------- */
 int mx_allreduce_local(mx_comm_t *comm, const void *const *sbufs, void *const *rbufs,

@@ -216,7 +216,7 @@ def _mp_worker(rank, n, port, staging, jobs, q):
             dist.all_gather_object(out, b)
             return out
 
-        comm = mxompi.Comm(rank, n, ag, device=0, staging_bytes=staging)
+        comm = mxompi.Comm(rank, n, ag, device=0, staging_bytes=staging, heap_bytes=160 << 20)
         comm.set_timeout(30.0)
         results = []
         st = torch.cuda.current_stream().cuda_stream
@@ -267,6 +267,43 @@ def _mp_worker(rank, n, port, staging, jobs, q):
                 out = torch.zeros(count * es, dtype=torch.uint8, device="cuda")
                 getattr(comm, kind)(x.data_ptr(), out.data_ptr(), count, t, op, alg, st)
                 results.append(out.cpu().numpy().tobytes())
+            elif kind == "symheap":
+                # device symmetric heap: put / get / barrier / shmem_<t>_<op>_to_all
+                heap = mxompi.Heap(comm, 64 << 20)
+                nb = count * es
+                src = heap.alloc(nb)
+                tgt = heap.alloc(nb)
+                scratch = heap.alloc(nb)
+                x = _dev(gen(t, op, count, 7000 + rank))
+                ctypes.memmove  # noqa: B018 (keeps the import used)
+                torch.cuda.synchronize()
+                mxompi.lib().mx_copy(src, x.data_ptr(), nb, None)
+                mxompi.sync()
+                heap.barrier_all()
+                heap.put(scratch, src, nb, (rank + 1) % n)       # my source -> right neighbour's scratch
+                heap.barrier_all()
+                got_put = torch.empty(nb, dtype=torch.uint8, device="cuda")
+                mxompi.lib().mx_copy(got_put.data_ptr(), scratch, nb, None)
+                got_get = torch.empty(nb, dtype=torch.uint8, device="cuda")
+                heap.get(got_get.data_ptr(), src, nb, (rank + n - 1) % n)   # left neighbour's source
+                sops = {"SUM": "SUM", "MAX": "MAX", "MIN": "MIN", "PROD": "PROD", "BAND": "AND", "BXOR": "XOR"}
+                sts = {"FLOAT": "FLOAT", "DOUBLE": "DOUBLE", "INT32_T": "INT32", "INT64_T": "INT64"}
+                heap.reduce(sops[op], sts[t], es, tgt, src, count)                      # all PEs
+                red_all = torch.empty(nb, dtype=torch.uint8, device="cuda")
+                mxompi.lib().mx_copy(red_all.data_ptr(), tgt, nb, None)
+                mxompi.sync()
+                if n >= 3 and rank >= 1:                                             # active set 1..n-1
+                    heap.reduce(sops[op], sts[t], es, src, src, count, 1, 0, n - 1)      # in place
+                red_sub = torch.empty(nb, dtype=torch.uint8, device="cuda")
+                mxompi.lib().mx_copy(red_sub.data_ptr(), src, nb, None)
+                mxompi.sync()
+                heap.barrier_all()
+                results.append((got_put.cpu().numpy().tobytes(), got_get.cpu().numpy().tobytes(),
+                                red_all.cpu().numpy().tobytes(), red_sub.cpu().numpy().tobytes()))
+                heap.free(scratch)
+                heap.free(tgt)
+                heap.free(src)
+                heap.close()
             elif kind == "reduce_scatter_block":
                 x = _dev(gen(t, op, count * n, 7000 + rank))
                 comm.reduce_scatter_block(mxompi.IN_PLACE, x.data_ptr(), count, t, op, alg, st)
@@ -329,7 +366,9 @@ def test_multiprocess_ipc_bitexact(n):
             ("scan", 20001, "SUM", "FLOAT", "auto"),
             ("exscan", 4097, "SUM", "DOUBLE", "recursive_doubling"),
             ("scan", 333, "MIN", "FLOAT", "recursive_doubling"),
-            ("reduce_scatter_block", 3000, "SUM", "FLOAT", "auto")]
+            ("reduce_scatter_block", 3000, "SUM", "FLOAT", "auto"),
+            ("symheap", 30001, "SUM", "FLOAT", "auto"),
+            ("symheap", 777, "MAX", "DOUBLE", "auto")]
     jobs = [(k, c, o or "BAND", t or "UINT8_T", a or "auto") for k, c, o, t, a in jobs]
     got = _run_mp(n, jobs)
     for j, (kind, count, op, t, alg) in enumerate(jobs):
@@ -376,6 +415,28 @@ def test_multiprocess_ipc_bitexact(n):
             for r in range(1 if kind == "exscan" else 0, n):
                 golden_io.assert_coll_equal(np.frombuffer(got[r][j], np.uint8), exp[r], mxompi.OP[op],
                                             mxompi.TYPE[t], f"{kind} {alg} rank {r}")
+        elif kind == "symheap":
+            xs = [gen(t, op, count, 7000 + r) for r in range(n)]
+            exp = [np.zeros(count * es, np.uint8) for _ in range(n)]
+            assert L.mxo_allreduce(0, mxompi.OP[op], mxompi.TYPE[t], n, count, (vp * n)(*[x.ctypes.data for x in xs]),
+                                   (vp * n)(*[e.ctypes.data for e in exp])) == 0
+            sub = None
+            if n >= 3:
+                sub = [np.zeros(count * es, np.uint8) for _ in range(n - 1)]
+                assert L.mxo_allreduce(0, mxompi.OP[op], mxompi.TYPE[t], n - 1, count,
+                                       (vp * (n - 1))(*[x.ctypes.data for x in xs[1:]]),
+                                       (vp * (n - 1))(*[e.ctypes.data for e in sub])) == 0
+            for r in range(n):
+                put_b, get_b, all_b, sub_b = got[r][j]
+                np.testing.assert_array_equal(np.frombuffer(put_b, np.uint8), xs[(r + n - 1) % n])
+                np.testing.assert_array_equal(np.frombuffer(get_b, np.uint8), xs[(r + n - 1) % n])
+                golden_io.assert_coll_equal(np.frombuffer(all_b, np.uint8), exp[r], mxompi.OP[op], mxompi.TYPE[t],
+                                            f"symheap reduce rank {r}")
+                if sub is not None and r >= 1:
+                    golden_io.assert_coll_equal(np.frombuffer(sub_b, np.uint8), sub[r - 1], mxompi.OP[op],
+                                                mxompi.TYPE[t], f"symheap active-set reduce rank {r}")
+                elif sub is not None:
+                    np.testing.assert_array_equal(np.frombuffer(sub_b, np.uint8), xs[0])   # PE 0 not in the set
         elif kind == "reduce_scatter_block":
             xs = [gen(t, op, count * n, 7000 + r) for r in range(n)]
             exp = [np.zeros(count * es, np.uint8) for _ in range(n)]

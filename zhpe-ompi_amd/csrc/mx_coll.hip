@@ -169,6 +169,15 @@ struct mx_comm {
   double timeout_s;
   uint64_t timeout_ticks;
   ncclComm_t nccl;
+  // the host bootstrap exchange, kept for later collective setups
+  // (symmetric heaps); ctx must outlive the communicator
+  mx_allgather_fn ag;
+  void *ag_ctx;
+  // symmetric-heap region exported with the staging at creation
+  // (mx_comm_create_ex heap_bytes): heaps are carved from it
+  char *hregion;
+  char *peer_hregion[MAXR];
+  size_t hregion_bytes, hregion_used;
   // profiling: event pairs recorded around kernels of the current call
   int prof;
   hipEvent_t ev[64];
@@ -260,13 +269,18 @@ extern "C" int mx_comm_create_local(int size, int device, mx_comm_t **out) {
 }
 
 struct ipc_info {
-  hipIpcMemHandle_t staging, flags;
+  hipIpcMemHandle_t staging, flags, hregion;
   int rank, device;
-  uint64_t staging_bytes;
+  uint64_t staging_bytes, hregion_bytes;
 };
 
 extern "C" int mx_comm_create(int rank, int size, int device, size_t staging_bytes, int flags,
                               mx_allgather_fn ag, void *ctx, mx_comm_t **out) {
+  return mx_comm_create_ex(rank, size, device, staging_bytes, 0, flags, ag, ctx, out);
+}
+
+extern "C" int mx_comm_create_ex(int rank, int size, int device, size_t staging_bytes, size_t heap_bytes, int flags,
+                                 mx_allgather_fn ag, void *ctx, mx_comm_t **out) {
   if (!out || !ag || size < 1 || rank < 0 || rank >= size) return MX_ERR_ARG;
   if ((flags & MX_COMM_IPC) && size > MAXR) return MX_ERR_ARG;
   int rc = mx_init(device);
@@ -277,6 +291,8 @@ extern "C" int mx_comm_create(int rank, int size, int device, size_t staging_byt
   c->size = size;
   c->device = g_device;
   c->flags = flags;
+  c->ag = ag;
+  c->ag_ctx = ctx;
   mx_comm_set_timeout(c, 60.0);
   if (hipHostMalloc((void **)&c->err_host, sizeof(int), hipHostMallocMapped) != hipSuccess) goto fail;
   *c->err_host = 0;
@@ -291,9 +307,12 @@ extern "C" int mx_comm_create(int rank, int size, int device, size_t staging_byt
     if (c->os_max < 1024) c->os_max = 0;
     c->os_slot = c->os_max ? c->os_max + 256 : 0;
     c->main_bytes = (c->staging_bytes - 2 * (size_t)size * c->os_slot) & ~(size_t)255;
+    c->hregion_bytes = heap_bytes ? ((heap_bytes + 4095) & ~(size_t)4095) : 0;
     if (hipExtMallocWithFlags((void **)&c->staging, c->staging_bytes, hipDeviceMallocUncached) != hipSuccess ||
-        hipExtMallocWithFlags((void **)&c->flagmem, FLAG_WORDS * sizeof(uint64_t), hipDeviceMallocUncached) !=
+        hipExtMallocWithFlags((void **)&c->flagmem, (FLAG_WORDS + 8) * sizeof(uint64_t), hipDeviceMallocUncached) !=
             hipSuccess ||
+        (c->hregion_bytes &&
+         hipExtMallocWithFlags((void **)&c->hregion, c->hregion_bytes, hipDeviceMallocUncached) != hipSuccess) ||
         hipMemset(c->flagmem, 0, FLAG_WORDS * sizeof(uint64_t)) != hipSuccess ||
         hipDeviceSynchronize() != hipSuccess) {
       free(all);
@@ -301,35 +320,70 @@ extern "C" int mx_comm_create(int rank, int size, int device, size_t staging_byt
     }
     memset(&mine, 0, sizeof mine);
     if (hipIpcGetMemHandle(&mine.staging, c->staging) != hipSuccess ||
-        hipIpcGetMemHandle(&mine.flags, c->flagmem) != hipSuccess) {
+        hipIpcGetMemHandle(&mine.flags, c->flagmem) != hipSuccess ||
+        (c->hregion && hipIpcGetMemHandle(&mine.hregion, c->hregion) != hipSuccess)) {
       free(all);
       goto fail;
     }
     mine.rank = rank;
     mine.device = c->device;
     mine.staging_bytes = c->staging_bytes;
+    mine.hregion_bytes = c->hregion_bytes;
+    // signature words, read back through every mapping below
+    {
+      const uint64_t sig[2] = {0x5EED0000ull + (uint64_t)rank, 0x5EED1000ull + (uint64_t)rank};
+      if (hipMemcpy(c->flagmem + FLAG_WORDS, sig, sizeof sig, hipMemcpyHostToDevice) != hipSuccess ||
+          (c->hregion && hipMemcpy(c->hregion, sig + 1, 8, hipMemcpyHostToDevice) != hipSuccess) ||
+          hipDeviceSynchronize() != hipSuccess) {
+        free(all);
+        goto fail;
+      }
+    }
     if (ag(&mine, all, sizeof(ipc_info), ctx) != 0) { free(all); goto fail; }
     for (int p = 0; p < size; p++) {
-      if (all[p].staging_bytes != c->staging_bytes) { free(all); goto fail; }
+      if (all[p].staging_bytes != c->staging_bytes || all[p].hregion_bytes != c->hregion_bytes) {
+        free(all);
+        goto fail;
+      }
       if (p == rank) {
         c->peer_staging[p] = c->staging;
         c->peer_flags[p] = c->flagmem;
+        c->peer_hregion[p] = c->hregion;
         continue;
       }
       if (hipIpcOpenMemHandle((void **)&c->peer_staging[p], all[p].staging, hipIpcMemLazyEnablePeerAccess) !=
               hipSuccess ||
           hipIpcOpenMemHandle((void **)&c->peer_flags[p], all[p].flags, hipIpcMemLazyEnablePeerAccess) !=
-              hipSuccess) {
+              hipSuccess ||
+          (c->hregion &&
+           hipIpcOpenMemHandle((void **)&c->peer_hregion[p], all[p].hregion, hipIpcMemLazyEnablePeerAccess) !=
+               hipSuccess)) {
         fprintf(stderr, "mx_comm_create: rank %d cannot map rank %d's staging\n", rank, p);
         free(all);
         goto fail;
       }
     }
     free(all);
-    // every rank mapped every peer before anyone signals
-    int dummy = 0, *dummies = (int *)calloc(size, sizeof(int));
-    int arc = dummies ? ag(&dummy, dummies, sizeof(int), ctx) : -1;
-    free(dummies);
+    // every mapping shows its owner's signature (a wrong IPC mapping fails
+    // creation here instead of corrupting data later); the exchange of the
+    // verdicts doubles as the "every rank mapped every peer" barrier
+    int ok = 1;
+    for (int p = 0; p < size; p++) {
+      uint64_t v[2] = {0, 0};
+      if (hipMemcpy(v, c->peer_flags[p] + FLAG_WORDS, 8, hipMemcpyDeviceToHost) != hipSuccess ||
+          v[0] != 0x5EED0000ull + (uint64_t)p ||
+          (c->hregion && (hipMemcpy(v + 1, c->peer_hregion[p], 8, hipMemcpyDeviceToHost) != hipSuccess ||
+                          v[1] != 0x5EED1000ull + (uint64_t)p))) {
+        fprintf(stderr, "mx_comm_create: rank %d: mapping of rank %d shows 0x%llx/0x%llx\n", rank, p,
+                (unsigned long long)v[0], (unsigned long long)v[1]);
+        ok = 0;
+      }
+    }
+    int *oks = (int *)calloc(size, sizeof(int));
+    int arc = oks ? ag(&ok, oks, sizeof(int), ctx) : -1;
+    for (int p = 0; p < size && !arc; p++)
+      if (!oks[p]) arc = -1;
+    free(oks);
     if (arc) goto fail;
   }
   if (flags & MX_COMM_RCCL) {
@@ -359,8 +413,10 @@ extern "C" int mx_comm_destroy(mx_comm_t *c) {
     if (p == c->rank) continue;
     if (c->peer_staging[p]) (void)hipIpcCloseMemHandle(c->peer_staging[p]);
     if (c->peer_flags[p]) (void)hipIpcCloseMemHandle(c->peer_flags[p]);
+    if (c->peer_hregion[p]) (void)hipIpcCloseMemHandle(c->peer_hregion[p]);
   }
   if (c->staging) (void)hipFree(c->staging);
+  if (c->hregion) (void)hipFree(c->hregion);
   if (c->flagmem) (void)hipFree(c->flagmem);
   if (c->err_host) (void)hipHostFree(c->err_host);
   if (c->nccl) ncclCommDestroy(c->nccl);
@@ -742,15 +798,16 @@ static Layout layout_for(int n, size_t ce, size_t es) {
 }
 static size_t chunk_elems(const mx_comm *c, size_t count, size_t es) {
   const int n = c->size;
-  size_t ce = count;
-  while (ce > 1) {
-    Layout L = layout_for(n, ce, es);
-    if (L.gather_off + ce * es + 16 <= c->main_bytes) break;
-    const size_t fit = (c->main_bytes > (size_t)(n + 2) * 512)
-                           ? (c->main_bytes - (size_t)(n + 2) * 512) / (2 * es) : 1;
-    ce = std::min(ce - 1, std::max<size_t>(fit, 1));
-  }
-  return ce;
+  auto fits = [&](size_t ce) {
+    const Layout L = layout_for(n, ce, es);
+    return L.gather_off + ce * es + 16 <= c->main_bytes;
+  };
+  if (fits(count)) return count;
+  // n slots of ce/n elements + a gather area of ce elements, plus padding
+  size_t ce = c->main_bytes > (size_t)(n + 2) * 512 ? (c->main_bytes - (size_t)(n + 2) * 512) / (2 * es) : 1;
+  if (ce >= count) ce = count - 1;
+  while (ce > 1 && !fits(ce)) ce -= std::max<size_t>(1, ce / 64);
+  return ce ? ce : 1;
 }
 
 // one-shot allreduce (small messages): one kernel, see k_oneshot
@@ -944,7 +1001,7 @@ extern "C" int mx_reduce_scatter(mx_comm_t *c, const void *sbuf, void *rbuf, con
   int rc = reduce_scatter_segments(alg, n, rcounts, es, r, segs);
   if (rc) return rc;
   const size_t slot = rup(maxc * es + 16, 256);
-  if (slot * n > c->staging_bytes) return MX_ERR_NOMEM;  // TODO: chunk very large blocks
+  if (slot * n > c->main_bytes) return MX_ERR_NOMEM;  // caller delegates (coll component)
   const uint64_t g = ++c->gen;
   if ((rc = wait_all(c, FLAG_DONE, g - 1, s))) return rc;
   CopyArgs ca;
@@ -966,7 +1023,7 @@ extern "C" int mx_reduce_scatter(mx_comm_t *c, const void *sbuf, void *rbuf, con
     // first, then copy.
     const bool overlap = (sb == (const char *)rbuf) && disp[r] != 0;
     char *dst = overlap ? c->staging + n * slot + mis : (char *)rbuf;
-    if (overlap && n * slot + mis + rcounts[r] * es > c->staging_bytes) return MX_ERR_NOMEM;
+    if (overlap && n * slot + mis + rcounts[r] * es > c->main_bytes) return MX_ERR_NOMEM;
     char *dp[1] = {dst};
     for (const Seg &sg : segs)
       if ((rc = run_fold(c, fl, sg, disp[r], sp, n, dp, 1, es, s))) return rc;
@@ -1803,4 +1860,380 @@ extern "C" int mx_shmem_reduce(mx_comm_t *c, int sop, int st, size_t dt_size, vo
   if (nreduce == 0) return MX_SUCCESS;
   return mx_allreduce(c, source == target ? MX_IN_PLACE : source, target, nreduce, type, op, MX_ALLREDUCE_AUTO,
                       stream);
+}
+
+// ---------------------------------------------------------------------------
+// Device symmetric heap for OpenSHMEM.
+//
+// The reference's symmetric heap is host memory (sshmem segment + memheap
+// allocator); RUNTIME_CHECK_ADDR rejects anything else
+// (oshmem/runtime/runtime.h:205-210), so device arrays cannot take part in
+// shmem_*_to_all today.  Here every PE allocates its heap in device memory
+// (uncached, IPC-exported -- the role of sshmem_<x>_segment_create/attach),
+// maps every peer's heap (shmem_ptr, oshmem/shmem/c/shmem_ptr.c:32-70: the
+// local-node shared-memory case), and the collective allocator hands out
+// the same offsets on every PE (memheap's symmetric allocation).  Because
+// every PE can load and store every other PE's symmetric arrays directly,
+// the reduction needs no staging: each PE folds its element part reading
+// all sources over xGMI and writes the result into every target.
+// Synchronisation uses per-pair sequence numbers (both sides of a pair see
+// the same order of collectives involving both -- the pSync discipline), so
+// collectives over different active sets never desynchronise.
+// ---------------------------------------------------------------------------
+namespace mx {
+
+struct SeqSignalArgs { uint64_t *flag[MAXR]; uint64_t value[MAXR]; };
+struct SeqWaitArgs { const uint64_t *flag[MAXR]; uint64_t value[MAXR]; uint64_t timeout_ticks; int *err; };
+
+__global__ void k_seq_signal(SeqSignalArgs a) {
+  const int j = threadIdx.x;
+  __threadfence_system();
+  if (j < MAXR && a.flag[j]) __hip_atomic_store(a.flag[j], a.value[j], __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+__global__ void k_seq_wait(SeqWaitArgs a) {
+  const int j = threadIdx.x;
+  if (j < MAXR && a.flag[j]) {
+    const uint64_t t0 = wall_clock64();
+    while (__hip_atomic_load(a.flag[j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) < a.value[j]) {
+      __builtin_amdgcn_s_sleep(2);
+      if (wall_clock64() - t0 > a.timeout_ticks) {
+        __hip_atomic_store(a.err, MX_ERR_TIMEOUT, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        break;
+      }
+    }
+  }
+  __syncthreads();
+  __atomic_thread_fence(__ATOMIC_ACQUIRE);
+}
+
+}  // namespace mx
+
+constexpr size_t kHeapFlagBytes = 4096;   // flag page at the start of each heap allocation
+
+struct mx_heap {
+  mx_comm *c;
+  size_t bytes;                 // usable symmetric bytes
+  int carved;                   // 1: a slice of the communicator's heap region (no own IPC export)
+  size_t region_off;            // offset of the slice in the region
+  char *mem;                    // my allocation: flag page + heap
+  char *base;                   // my heap
+  char *peer[MAXR];             // every PE's heap, mapped here
+  uint64_t *flags;              // my flag page: word p = sequence number signalled by PE p
+  uint64_t *peer_flags[MAXR];
+  uint64_t seq[MAXR];           // syncs done with PE p
+  size_t brk;                   // symmetric allocator: bump pointer + first-fit free list
+  std::map<size_t, size_t> live, freed;
+};
+
+namespace {
+struct heap_info { hipIpcMemHandle_t h; uint64_t bytes; };
+
+// one synchronisation step among the PEs in `mask` (this PE included)
+static int heap_sync(mx_heap *h, uint32_t mask, hipStream_t s) {
+  mx_comm *c = h->c;
+  SeqSignalArgs sa;
+  SeqWaitArgs wa;
+  memset(&sa, 0, sizeof sa);
+  memset(&wa, 0, sizeof wa);
+  for (int p = 0; p < c->size; p++) {
+    if (p == c->rank || !((mask >> p) & 1)) continue;
+    const uint64_t v = ++h->seq[p];
+    sa.flag[p] = h->peer_flags[p] + c->rank;
+    sa.value[p] = v;
+    wa.flag[p] = h->flags + p;
+    wa.value[p] = v;
+  }
+  wa.timeout_ticks = c->timeout_ticks;
+  wa.err = c->err_dev;
+  hipLaunchKernelGGL(k_seq_signal, dim3(1), dim3(64), 0, s, sa);
+  int rc = mx_check_launch();
+  if (rc) return rc;
+  hipLaunchKernelGGL(k_seq_wait, dim3(1), dim3(64), 0, s, wa);
+  return mx_check_launch();
+}
+
+static bool heap_has(const mx_heap *h, const void *p, size_t bytes) {
+  const uintptr_t q = (uintptr_t)p, b = (uintptr_t)h->base;
+  return q >= b && bytes <= h->bytes && q - b <= h->bytes - bytes;
+}
+}  // namespace
+
+namespace {
+// every PE contributes `ok`; true iff all PEs are ok (and the exchange worked)
+static bool heap_agree(mx_comm *c, int ok) {
+  std::vector<int> all(c->size, 0);
+  if (c->ag(&ok, all.data(), sizeof(int), c->ag_ctx) != 0) return false;
+  for (int v : all)
+    if (!v) return false;
+  return true;
+}
+
+static void heap_unmap(mx_heap *h) {
+  for (int p = 0; p < h->c->size && p < MAXR; p++) {
+    if (p != h->c->rank && h->peer_flags[p]) (void)hipIpcCloseMemHandle((void *)h->peer_flags[p]);
+    if (p != h->c->rank) { h->peer_flags[p] = nullptr; h->peer[p] = nullptr; }
+  }
+}
+
+// One collective attempt at exporting my heap allocation and mapping every
+// peer's.  Every PE makes the same sequence of exchanges whatever fails
+// locally, so a failure on one PE never strands the others in an exchange.
+// The mappings are verified by reading each PE's signature word through
+// them: on this image an IPC import has been seen (intermittently, 4
+// processes on one GPU) to return a mapping of another PE's buffer, which
+// would otherwise surface as a hang or wrong data much later.
+static bool heap_map_attempt(mx_heap *h) {
+  mx_comm *c = h->c;
+  const int dbg = getenv("MX_DEBUG_IPC") != nullptr;
+  heap_info mine;
+  memset(&mine, 0, sizeof mine);
+  int ok = hipIpcGetMemHandle(&mine.h, h->mem) == hipSuccess;
+  mine.bytes = ok ? h->bytes : 0;
+  std::vector<heap_info> all(c->size);
+  if (c->ag(&mine, all.data(), sizeof mine, c->ag_ctx) != 0) return false;
+  for (int p = 0; p < c->size; p++) {
+    if (p == c->rank || !ok) continue;
+    char *m = nullptr;
+    if (all[p].bytes != h->bytes) ok = 0;   // shmem heaps are the same size everywhere
+    else if (hipIpcOpenMemHandle((void **)&m, all[p].h, hipIpcMemLazyEnablePeerAccess) != hipSuccess) {
+      fprintf(stderr, "mx_heap_create: rank %d cannot map PE %d's heap\n", c->rank, p);
+      ok = 0;
+    } else {
+      h->peer[p] = m + kHeapFlagBytes;
+      h->peer_flags[p] = (uint64_t *)m;
+    }
+  }
+  const uint64_t sig = 0x5EED0000ull + (uint64_t)c->rank;
+  if (ok && (hipMemcpy(h->flags + 256, &sig, sizeof sig, hipMemcpyHostToDevice) != hipSuccess ||
+             hipDeviceSynchronize() != hipSuccess))
+    ok = 0;
+  if (!heap_agree(c, ok)) return false;   // every PE mapped and signed before anyone checks
+  for (int p = 0; p < c->size; p++) {
+    uint64_t v = 0;
+    const hipError_t e = hipMemcpy(&v, h->peer_flags[p] + 256, sizeof v, hipMemcpyDeviceToHost);
+    if (dbg) fprintf(stderr, "[mx ipc] rank %d: PE %d mapped at %p reads 0x%llx\n", c->rank, p,
+                     (void *)h->peer_flags[p], (unsigned long long)v);
+    if (e != hipSuccess || v != 0x5EED0000ull + (uint64_t)p) {
+      fprintf(stderr, "mx_heap_create: rank %d reads 0x%llx through its mapping of PE %d's heap; remapping\n",
+              c->rank, (unsigned long long)v, p);
+      ok = 0;
+    }
+  }
+  return heap_agree(c, ok);               // nobody uses the heap before every PE checked its mappings
+}
+}  // namespace
+
+extern "C" int mx_heap_create(mx_comm_t *c, size_t bytes, mx_heap_t **out) {
+  if (!c || !out || !bytes) return MX_ERR_ARG;
+  if (c->local && c->size != 1) return MX_ERR_STATE;
+  if (!c->local && (!(c->flags & MX_COMM_IPC) || !c->ag)) return MX_ERR_STATE;
+  int rc = mx_ensure_init();
+  if (rc) return rc;
+  mx_heap *h = new (std::nothrow) mx_heap();
+  if (!h) return MX_ERR_NOMEM;
+  h->c = c;
+  h->bytes = (bytes + 255) & ~(size_t)255;
+  // preferred: a slice of the heap region mapped (and verified) at
+  // communicator creation -- the same sequence on every PE gives the same
+  // offset, and no new IPC export is needed
+  if (c->hregion && c->hregion_used + kHeapFlagBytes + h->bytes <= c->hregion_bytes) {
+    h->carved = 1;
+    h->region_off = c->hregion_used;
+    c->hregion_used += kHeapFlagBytes + h->bytes;
+    for (int p = 0; p < c->size; p++) {
+      h->peer_flags[p] = (uint64_t *)(c->peer_hregion[p] + h->region_off);
+      h->peer[p] = c->peer_hregion[p] + h->region_off + kHeapFlagBytes;
+    }
+    h->mem = c->hregion + h->region_off;
+    h->flags = (uint64_t *)h->mem;
+    h->base = h->mem + kHeapFlagBytes;
+    // flag words start at 0 on every PE before anyone signals
+    int ok = hipMemset(h->mem, 0, kHeapFlagBytes) == hipSuccess && hipDeviceSynchronize() == hipSuccess;
+    if (!heap_agree(c, ok)) {
+      c->hregion_used = h->region_off;
+      delete h;
+      return MX_ERR_HIP;
+    }
+    *out = h;
+    return MX_SUCCESS;
+  }
+  std::vector<char *> discarded;   // failed attempts' buffers stay allocated until we succeed (fresh VAs)
+  bool mapped = false;
+  for (int attempt = 0; attempt < 3 && !mapped; attempt++) {
+    int ok = hipExtMallocWithFlags((void **)&h->mem, kHeapFlagBytes + h->bytes, hipDeviceMallocUncached) ==
+             hipSuccess;
+    if (ok && (hipMemset(h->mem, 0, kHeapFlagBytes) != hipSuccess || hipDeviceSynchronize() != hipSuccess)) ok = 0;
+    if (!ok) h->mem = nullptr;
+    if (c->local) {
+      mapped = ok;
+      if (!ok) break;
+    } else if (!heap_agree(c, ok)) {
+      if (h->mem) discarded.push_back(h->mem);
+      h->mem = nullptr;
+      break;                       // an allocation failed somewhere: give up together
+    }
+    h->base = h->mem + kHeapFlagBytes;
+    h->flags = (uint64_t *)h->mem;
+    h->peer[c->rank] = h->base;
+    h->peer_flags[c->rank] = h->flags;
+    if (c->local) break;
+    mapped = heap_map_attempt(h);
+    if (!mapped) {
+      heap_unmap(h);
+      discarded.push_back(h->mem);
+      h->mem = nullptr;
+    }
+  }
+  for (char *m : discarded) (void)hipFree(m);
+  if (!mapped) {
+    if (h->mem) (void)hipFree(h->mem);
+    delete h;
+    return MX_ERR_HIP;
+  }
+  *out = h;
+  return MX_SUCCESS;
+}
+
+extern "C" int mx_heap_destroy(mx_heap_t *h) {
+  if (!h) return MX_SUCCESS;
+  (void)hipDeviceSynchronize();
+  if (h->carved) {   // give the slice back if it is the last one (heaps are destroyed in LIFO order)
+    if (h->region_off + kHeapFlagBytes + h->bytes == h->c->hregion_used) h->c->hregion_used = h->region_off;
+    delete h;
+    return MX_SUCCESS;
+  }
+  heap_unmap(h);
+  if (h->mem) (void)hipFree(h->mem);
+  delete h;
+  return MX_SUCCESS;
+}
+
+extern "C" void *mx_heap_base(const mx_heap_t *h) { return h ? h->base : nullptr; }
+
+// Symmetric allocation: every PE makes the same calls in the same order
+// (shmem_malloc is collective), so first-fit over the same free list gives
+// the same offset everywhere.
+extern "C" void *mx_shmalloc(mx_heap_t *h, size_t bytes) {
+  if (!h || !bytes) return nullptr;
+  const size_t need = (bytes + 255) & ~(size_t)255;
+  for (auto it = h->freed.begin(); it != h->freed.end(); ++it) {
+    if (it->second >= need) {
+      const size_t off = it->first, rest = it->second - need;
+      h->freed.erase(it);
+      if (rest) h->freed[off + need] = rest;
+      h->live[off] = need;
+      return h->base + off;
+    }
+  }
+  if (h->brk + need > h->bytes) return nullptr;
+  const size_t off = h->brk;
+  h->brk += need;
+  h->live[off] = need;
+  return h->base + off;
+}
+
+extern "C" int mx_shfree(mx_heap_t *h, void *p) {
+  if (!h || !p) return MX_ERR_ARG;
+  const size_t off = (size_t)((char *)p - h->base);
+  auto it = h->live.find(off);
+  if (it == h->live.end()) return MX_ERR_ARG;
+  size_t start = off, len = it->second;
+  h->live.erase(it);
+  auto nx = h->freed.lower_bound(start);              // coalesce with neighbours
+  if (nx != h->freed.end() && nx->first == start + len) { len += nx->second; h->freed.erase(nx); }
+  auto pv = h->freed.lower_bound(start);
+  if (pv != h->freed.begin()) {
+    --pv;
+    if (pv->first + pv->second == start) { start = pv->first; len += pv->second; h->freed.erase(pv); }
+  }
+  if (start + len == h->brk) h->brk = start;           // give the tail back to the bump pointer
+  else h->freed[start] = len;
+  return MX_SUCCESS;
+}
+
+extern "C" void *mx_shmem_ptr(const mx_heap_t *h, const void *addr, int pe) {
+  if (!h || pe < 0 || pe >= h->c->size || !heap_has(h, addr, 1)) return nullptr;
+  return h->peer[pe] + ((const char *)addr - h->base);
+}
+
+extern "C" int mx_shmem_putmem(mx_heap_t *h, void *dest, const void *src, size_t bytes, int pe, void *stream) {
+  if (!h || !dest || !src || !heap_has(h, dest, bytes)) return MX_ERR_ARG;
+  void *remote = mx_shmem_ptr(h, dest, pe);
+  if (!remote) return MX_ERR_ARG;
+  int rc = copy_async(remote, src, bytes, (hipStream_t)stream);
+  return rc ? rc : finish(h->c, (hipStream_t)stream);
+}
+
+extern "C" int mx_shmem_getmem(mx_heap_t *h, void *dest, const void *src, size_t bytes, int pe, void *stream) {
+  if (!h || !dest || !src || !heap_has(h, src, bytes)) return MX_ERR_ARG;
+  const void *remote = mx_shmem_ptr(h, src, pe);
+  if (!remote) return MX_ERR_ARG;
+  int rc = copy_async(dest, remote, bytes, (hipStream_t)stream);
+  return rc ? rc : finish(h->c, (hipStream_t)stream);
+}
+
+extern "C" int mx_shmem_barrier_all(mx_heap_t *h, void *stream) {
+  if (!h) return MX_ERR_ARG;
+  const uint32_t all = h->c->size >= 32 ? 0xffffffffu : ((1u << h->c->size) - 1);
+  int rc = heap_sync(h, all, (hipStream_t)stream);
+  return rc ? rc : finish(h->c, (hipStream_t)stream);
+}
+
+// shmem_<type>_<op>_to_all over the active set (PE_start, logPE_stride,
+// PE_size) with symmetric target/source (oshmem/shmem/c/shmem_reduce.c:29-65).
+// The fold order is the one scoll/mpi would get from coll/tuned on a
+// communicator of the active set (mx_allreduce_decision over PE_size ranks,
+// virtual rank = position in the active set), so results equal
+// mx_shmem_reduce's bit for bit.
+extern "C" int mx_shmem_reduce_heap(mx_heap_t *h, int sop, int st, size_t dt_size, void *target,
+                                    const void *source, size_t nreduce, int pe_start, int log_pe_stride,
+                                    int pe_size, void *stream) {
+  if (!h || !target || !source) return MX_ERR_ARG;
+  mx_comm *c = h->c;
+  int op, type;
+  int rc = mx_shmem_to_mpi(sop, st, dt_size, &op, &type);
+  if (rc) return rc;
+  fold_launch_fn fl = fold_fns(op, type).fold;
+  if (!fl || !mx_op_supported(op, type, MX_TABLE_WITH_FORTRAN)) return MX_ERR_UNSUPPORTED;
+  const size_t es = mx_type_size(type);
+  if (pe_size < 1 || pe_size > MAXR || pe_start < 0 || log_pe_stride < 0 || log_pe_stride > 5) return MX_ERR_ARG;
+  int members[MAXR], me = -1;
+  uint32_t mask = 0;
+  for (int i = 0; i < pe_size; i++) {
+    members[i] = pe_start + (i << log_pe_stride);
+    if (members[i] >= c->size) return MX_ERR_ARG;
+    mask |= 1u << members[i];
+    if (members[i] == c->rank) me = i;
+  }
+  if (me < 0) return MX_ERR_ARG;   // only the active set calls (RUNTIME_CHECK_PE semantics)
+  if (!heap_has(h, target, nreduce * es) || !heap_has(h, source, nreduce * es)) return MX_ERR_ARG;
+  hipStream_t s = (hipStream_t)stream;
+  if (nreduce == 0) return MX_SUCCESS;
+  const int n = pe_size;
+  if (n == 1) {
+    if ((rc = copy_async(target, source, nreduce * es, s))) return rc;
+    return finish(c, s);
+  }
+  // (1) every member's source is final; (2) each member folds its part from
+  // all sources into all targets; (3) every target is complete
+  if ((rc = heap_sync(h, mask, s))) return rc;
+  size_t off[MAXR], len[MAXR];
+  blockcount(nreduce, n, off, len);
+  if (len[me]) {
+    std::vector<Seg> segs;
+    if ((rc = allreduce_segments(MX_ALLREDUCE_AUTO, n, nreduce, es, off[me], off[me] + len[me], segs))) return rc;
+    const char *sp[MAXR];
+    char *dp[MAXR];
+    const size_t so = (size_t)((const char *)source - h->base) + off[me] * es;
+    const size_t to = (size_t)((char *)target - h->base) + off[me] * es;
+    for (int j = 0; j < n; j++) {
+      sp[j] = h->peer[members[j]] + so;
+      dp[j] = h->peer[members[j]] + to;
+    }
+    for (const Seg &sg : segs)
+      if ((rc = run_fold(c, fl, sg, off[me], sp, n, dp, n, es, s))) return rc;
+  }
+  if ((rc = heap_sync(h, mask, s))) return rc;
+  return finish(c, s);
 }

@@ -187,6 +187,7 @@ def _coll_lib():
         vp, sz, i = ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int
         pp = ctypes.POINTER(ctypes.c_void_p)
         L.mx_comm_create.argtypes = [i, i, i, sz, i, _AG_FN, vp, ctypes.POINTER(vp)]
+        L.mx_comm_create_ex.argtypes = [i, i, i, sz, sz, i, _AG_FN, vp, ctypes.POINTER(vp)]
         L.mx_comm_create_local.argtypes = [i, i, ctypes.POINTER(vp)]
         L.mx_comm_destroy.argtypes = [vp]
         L.mx_comm_set_timeout.argtypes = [vp, ctypes.c_double]
@@ -232,7 +233,7 @@ class Comm:
     list[bytes]` is the host bootstrap exchange (e.g. torch.distributed)."""
 
     def __init__(self, rank=0, size=1, allgather=None, device=0, staging_bytes=64 << 20,
-                 flags=COMM_IPC, _handle=None):
+                 flags=COMM_IPC, heap_bytes=0, _handle=None):
         L = _coll_lib()
         self.size = size
         self.rank = rank
@@ -256,8 +257,8 @@ class Comm:
 
         self._cb = _AG_FN(_ag)
         h = ctypes.c_void_p()
-        check(L.mx_comm_create(rank, size, device, staging_bytes, flags, self._cb, None, ctypes.byref(h)),
-              "mx_comm_create")
+        check(L.mx_comm_create_ex(rank, size, device, staging_bytes, heap_bytes, flags, self._cb, None,
+                                  ctypes.byref(h)), "mx_comm_create")
         self.h = h
 
     @classmethod
@@ -367,6 +368,76 @@ class Comm:
 
     def reduce_scatter_block_local(self, sbufs, rbufs, rcount, t, op, alg="auto", stream=0):
         self._local3("mx_reduce_scatter_block_local", REDUCE, sbufs, rbufs, rcount, t, op, alg, stream)
+
+
+SHMEM_OPS = ["AND", "OR", "XOR", "MAX", "MIN", "SUM", "PROD"]
+SHMEM_TYPES = ["SHORT", "INT", "LONG", "LLONG", "INT16", "INT32", "INT64", "FLOAT", "DOUBLE", "LDOUBLE",
+               "FCOMPLEX", "DCOMPLEX", "FINT2", "FINT4", "FINT8", "FREAL4", "FREAL8", "FREAL16"]
+
+
+def _heap_lib():
+    L = _coll_lib()
+    if not getattr(L, "_mx_heap_typed", False):
+        vp, sz, i = ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int
+        L.mx_heap_create.argtypes = [vp, sz, ctypes.POINTER(vp)]
+        L.mx_heap_destroy.argtypes = [vp]
+        L.mx_heap_base.restype = vp
+        L.mx_heap_base.argtypes = [vp]
+        L.mx_shmalloc.restype = vp
+        L.mx_shmalloc.argtypes = [vp, sz]
+        L.mx_shfree.argtypes = [vp, vp]
+        L.mx_shmem_ptr.restype = vp
+        L.mx_shmem_ptr.argtypes = [vp, vp, i]
+        L.mx_shmem_putmem.argtypes = [vp, vp, vp, sz, i, vp]
+        L.mx_shmem_getmem.argtypes = [vp, vp, vp, sz, i, vp]
+        L.mx_shmem_barrier_all.argtypes = [vp, vp]
+        L.mx_shmem_reduce_heap.argtypes = [vp, i, i, sz, vp, vp, sz, i, i, i, vp]
+        L._mx_heap_typed = True
+    return L
+
+
+class Heap:
+    """Device symmetric heap over a multi-process Comm (collective calls)."""
+
+    def __init__(self, comm, nbytes):
+        L = _heap_lib()
+        h = ctypes.c_void_p()
+        check(L.mx_heap_create(comm.h, nbytes, ctypes.byref(h)), "mx_heap_create")
+        self.h, self.comm = h, comm
+
+    def alloc(self, nbytes):
+        p = _heap_lib().mx_shmalloc(self.h, nbytes)
+        if not p:
+            raise MxError(-4, "mx_shmalloc")
+        return p
+
+    def free(self, p):
+        check(_heap_lib().mx_shfree(self.h, p), "mx_shfree")
+
+    def ptr(self, addr, pe):
+        return _heap_lib().mx_shmem_ptr(self.h, addr, pe)
+
+    def put(self, dest, src, nbytes, pe, stream=0):
+        check(_heap_lib().mx_shmem_putmem(self.h, dest, src, nbytes, pe, stream or None), "mx_shmem_putmem")
+
+    def get(self, dest, src, nbytes, pe, stream=0):
+        check(_heap_lib().mx_shmem_getmem(self.h, dest, src, nbytes, pe, stream or None), "mx_shmem_getmem")
+
+    def barrier_all(self, stream=0):
+        check(_heap_lib().mx_shmem_barrier_all(self.h, stream or None), "mx_shmem_barrier_all")
+
+    def reduce(self, op, t, dt_size, target, source, nreduce, pe_start=0, log_pe_stride=0, pe_size=None,
+               stream=0):
+        """shmem_<t>_<op>_to_all on symmetric arrays (active set defaults to all PEs)."""
+        pe_size = self.comm.size if pe_size is None else pe_size
+        check(_heap_lib().mx_shmem_reduce_heap(self.h, SHMEM_OPS.index(op), SHMEM_TYPES.index(t), dt_size, target,
+                                               source, nreduce, pe_start, log_pe_stride, pe_size, stream or None),
+              "mx_shmem_reduce_heap")
+
+    def close(self):
+        if getattr(self, "h", None):
+            _heap_lib().mx_heap_destroy(self.h)
+            self.h = None
 
 
 def allreduce_decision(n, count, t):
