@@ -416,7 +416,7 @@ def main():
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
                          "traffic": load_traffic("k_reduce2<float,OpSum>"),
-                         "kernel": "k_reduce2<float, mx::OpSum>",
+                         "kernel": "k_reduce2<float, mx::OpSum, true> (non-temporal instance at >= 384 MiB footprint)",
                          "algorithmic_bytes_per_launch": algo_bytes,
                          "avg_kernel_ms": round(avg_kernel_ms, 4)},
         })
