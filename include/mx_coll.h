@@ -34,8 +34,9 @@
  * Ownership: the caller owns all buffers.  Calls are blocking with respect
  * to `stream` semantics: work is enqueued on `stream`, and the call returns
  * after the stream completed (MPI blocking-collective semantics); results
- * are in rbuf on return.  One collective at a time per communicator, in the
- * same order on every rank (MPI semantics).
+ * are in rbuf on return.  Collectives are issued in the same order on every
+ * rank (MPI semantics); the non-blocking / persistent forms below return
+ * before completion.
  */
 #ifndef MX_COLL_H
 #define MX_COLL_H
@@ -173,6 +174,84 @@ int mx_exscan(mx_comm_t *comm, const void *sbuf, void *rbuf, size_t count, int t
  * does it (reduce to rank 0 with the reduce algorithm `alg`, then scatter). */
 int mx_reduce_scatter_block(mx_comm_t *comm, const void *sbuf, void *rbuf, size_t rcount,
                             int type, int op, int alg, void *stream);
+
+/* ---- non-blocking and persistent collectives ----------------------------
+ * Replace, for device buffers, coll/libnbc's slots (coll.h:261-338 i<coll>,
+ * :339-420 <coll>_init; ompi/mca/coll/libnbc/nbc_i*.c).  The collective is
+ * enqueued on `stream` exactly like the blocking call but the call returns
+ * at once: the GPU progresses every step itself (device-side flag waits),
+ * nothing needs host progress calls.  A request completes when its last
+ * kernel has run.  Collectives of one communicator execute in issue order
+ * even across streams (MPI ordering); buffers must not be touched until
+ * completion.  Reduction orders are libnbc's (its algorithm numbering and
+ * default rule below), so results are bit-identical to MPI_I<coll> on the
+ * reference.  Persistent requests (*_init, MPI-4) are created inactive and
+ * run on every mx_start. */
+typedef struct mx_request mx_request_t;
+/* coll_libnbc_iallreduce_algorithm (coll_libnbc_component.c:58-64) */
+enum {
+    MX_IALLREDUCE_AUTO = 0,          /* libnbc rule (nbc_iallreduce.c:113-121)  */
+    MX_IALLREDUCE_RING = 1,
+    MX_IALLREDUCE_BINOMIAL = 2,
+    MX_IALLREDUCE_RABENSEIFNER = 3,
+    MX_IALLREDUCE_RECURSIVE_DOUBLING = 4
+};
+/* coll_libnbc_ireduce_algorithm (coll_libnbc_component.c:87-92) */
+enum {
+    MX_IREDUCE_AUTO = 0,             /* libnbc rule (nbc_ireduce.c:107-116)     */
+    MX_IREDUCE_CHAIN = 1,
+    MX_IREDUCE_BINOMIAL = 2,
+    MX_IREDUCE_RABENSEIFNER = 3
+};
+/* iscan / iexscan: MX_SCAN_* (== coll_libnbc_i{scan,exscan}_algorithm:
+ * 1 linear, 2 recursive doubling; AUTO = linear). */
+int mx_iallreduce_decision(int comm_size, size_t count, int type, int inplace);
+int mx_ireduce_decision(int comm_size, size_t count, int type);
+
+int mx_iallreduce(mx_comm_t *comm, const void *sbuf, void *rbuf, size_t count, int type, int op,
+                  int alg, void *stream, mx_request_t **req);
+int mx_ireduce(mx_comm_t *comm, const void *sbuf, void *rbuf, size_t count, int type, int op,
+               int root, int alg, void *stream, mx_request_t **req);
+int mx_ireduce_scatter(mx_comm_t *comm, const void *sbuf, void *rbuf, const size_t *rcounts,
+                       int type, int op, void *stream, mx_request_t **req);
+int mx_ireduce_scatter_block(mx_comm_t *comm, const void *sbuf, void *rbuf, size_t rcount,
+                             int type, int op, void *stream, mx_request_t **req);
+int mx_iscan(mx_comm_t *comm, const void *sbuf, void *rbuf, size_t count, int type, int op,
+             int alg, void *stream, mx_request_t **req);
+int mx_iexscan(mx_comm_t *comm, const void *sbuf, void *rbuf, size_t count, int type, int op,
+               int alg, void *stream, mx_request_t **req);
+int mx_iallgather(mx_comm_t *comm, const void *sbuf, void *rbuf, size_t bytes, void *stream,
+                  mx_request_t **req);
+int mx_ibcast(mx_comm_t *comm, void *buf, size_t bytes, int root, void *stream, mx_request_t **req);
+
+int mx_allreduce_init(mx_comm_t *comm, const void *sbuf, void *rbuf, size_t count, int type, int op,
+                      int alg, void *stream, mx_request_t **req);
+int mx_reduce_init(mx_comm_t *comm, const void *sbuf, void *rbuf, size_t count, int type, int op,
+                   int root, int alg, void *stream, mx_request_t **req);
+int mx_reduce_scatter_init(mx_comm_t *comm, const void *sbuf, void *rbuf, const size_t *rcounts,
+                           int type, int op, void *stream, mx_request_t **req);
+int mx_reduce_scatter_block_init(mx_comm_t *comm, const void *sbuf, void *rbuf, size_t rcount,
+                                 int type, int op, void *stream, mx_request_t **req);
+int mx_scan_init(mx_comm_t *comm, const void *sbuf, void *rbuf, size_t count, int type, int op,
+                 int alg, void *stream, mx_request_t **req);
+int mx_exscan_init(mx_comm_t *comm, const void *sbuf, void *rbuf, size_t count, int type, int op,
+                   int alg, void *stream, mx_request_t **req);
+int mx_allgather_init(mx_comm_t *comm, const void *sbuf, void *rbuf, size_t bytes, void *stream,
+                      mx_request_t **req);
+int mx_bcast_init(mx_comm_t *comm, void *buf, size_t bytes, int root, void *stream, mx_request_t **req);
+
+/* MPI_Start / MPI_Startall (persistent requests only). */
+int mx_start(mx_request_t *req);
+int mx_startall(size_t n, mx_request_t *const *reqs);
+/* MPI_Test / MPI_Wait: flag = 1 once complete (also for an inactive
+ * persistent request); the return value is the operation's status. */
+int mx_test(mx_request_t *req, int *flag);
+int mx_wait(mx_request_t *req);
+/* Make `stream` wait for the request on the device, without a host wait. */
+int mx_request_stream_wait(mx_request_t *req, void *stream);
+int mx_request_is_active(const mx_request_t *req);
+/* MPI_Request_free: an active request is completed first. */
+int mx_request_free(mx_request_t *req);
 
 /* ---- OpenSHMEM reductions (shmem_<type>_<op>_to_all) --------------------
  * The OSHMEM op/type numbering (oshmem/op/op.h: OSHMEM_OP_AND..PROD,

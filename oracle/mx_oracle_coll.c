@@ -950,3 +950,235 @@ int mxo_reduce_tree(int kind, int n, int root, int rank, int *children)
     for (int i = 0; i < t.nnext; i++) children[i] = t.next[i];
     return t.nnext;
 }
+
+/* ========================================================================
+ * coll/libnbc schedules -- what MPI_I<coll> and MPI_<Coll>_init compute
+ * (ompi/mca/coll/libnbc).  Same lockstep model; every NBC_Sched_op(buf1,
+ * buf2) executes ompi_op_reduce(op, buf1, buf2) (nbc.c:523): buf2 is the
+ * target.
+ * ======================================================================== */
+#include <math.h>
+#define NBC_LOG2 0.69314718055994530941     /* nbc_internal.h:54 */
+
+static int nbc_maxr(int p) { return (int)ceil(log((double)p) / NBC_LOG2); }
+/* RANK2VRANK / VRANK2RANK (nbc_iallreduce.c:353-364): 0 <-> root */
+static int nbc_swap(int v, int root) { return v == 0 ? root : (v == root ? 0 : v); }
+static int nbc_pof2(int p) { int q = 1; while (q * 2 <= p) q *= 2; return q; }   /* opal_next_poweroftwo(p) >> 1 */
+
+/* Reduction half of allred_sched_diss (nbc_iallreduce.c:365-424),
+ * red_sched_binomial (nbc_ireduce.c:356-445) and ireduce_scatter(_block)
+ * (nbc_ireduce_scatter.c:103-150): in round r a vrank with v % 2^r == 0
+ * receives the partner's current buffer into rbuf and computes
+ * rbuf = own OP rbuf (NBC_Sched_op(sendbuf|lbuf, rbuf)), then swaps lbuf and
+ * rbuf; the other vranks send their current buffer and leave.  `x` is
+ * indexed by real rank; the result is vrank 0's buffer. */
+static void nbc_binomial(int n, int vroot, size_t count, char *const *x, char *out)
+{
+    char *cur[MAXN], *msg[MAXN];
+    int left[MAXN];
+    const int maxr = nbc_maxr(n);
+    for (int v = 0; v < n; v++) {
+        cur[v] = malloc(count * g_es + 1);
+        msg[v] = malloc(count * g_es + 1);
+        cp(cur[v], x[nbc_swap(v, vroot)], count);
+        left[v] = 0;
+    }
+    for (int r = 1; r <= maxr; r++) {
+        for (int v = 0; v < n; v++)                       /* this round's senders */
+            if (!left[v] && v % (1 << r) != 0) { cp(msg[v], cur[v], count); left[v] = 1; }
+        for (int v = 0; v < n; v++) {
+            if (left[v] || v % (1 << r) != 0) continue;
+            const int vp = v + (1 << (r - 1));
+            if (nbc_swap(vp, vroot) >= n) continue;        /* peer < p (:393) */
+            char *rb = msg[vp];
+            red(cur[v], rb, count);                         /* rbuf = own OP rbuf */
+            msg[vp] = cur[v];                               /* swap left and right buffers */
+            cur[v] = rb;
+        }
+    }
+    cp(out, cur[0], count);
+    for (int v = 0; v < n; v++) { free(cur[v]); free(msg[v]); }
+}
+
+/* allred_sched_ring (nbc_iallreduce.c:629-860).  segsize = ceil(count/p);
+ * rounds 0..p-2: rank r sends segment (r+1-round) (round 0 from sendbuf,
+ * then from recvbuf) to r+1, receives segment (r-round) from r-1 into
+ * recvbuf and reduces recvbuf = sendbuf OP recvbuf; rounds p-1..2p-3 pass
+ * the finished segments on. */
+static void nbc_ring(int p, size_t count, char *const *sbuf, void *const *rbuf)
+{
+    size_t segsize = (count + p - 1) / p, segsizes[MAXN], segoffsets[MAXN];
+    char *msg[MAXN];
+    long mycount = (long)count;
+    segoffsets[0] = 0;
+    for (int i = 0; i < p; i++) {
+        mycount -= (long)segsize;
+        segsizes[i] = segsize;
+        if (mycount < 0) { segsizes[i] = (size_t)((long)segsize + mycount); mycount = 0; }
+        if (i) segoffsets[i] = segoffsets[i - 1] + segsizes[i - 1];
+    }
+    for (int r = 0; r < p; r++) msg[r] = malloc(segsize * g_es + 1);
+    for (int round = 0; round < 2 * p - 2; round++) {
+        for (int r = 0; r < p; r++) {
+            const int se = (r + 1 - round + 2 * p) % p;
+            const char *from = round == 0 ? sbuf[r] : (const char *)rbuf[r];
+            cp(msg[r], AT(from, segoffsets[se]), segsizes[se]);
+        }
+        for (int r = 0; r < p; r++) {
+            const int re = (r - round + 2 * p) % p, from = (r - 1 + p) % p;
+            cp(AT(rbuf[r], segoffsets[re]), msg[from], segsizes[re]);
+            if (round < p - 1) red(AT(sbuf[r], segoffsets[re]), AT(rbuf[r], segoffsets[re]), segsizes[re]);
+        }
+    }
+    for (int r = 0; r < p; r++) free(msg[r]);
+}
+
+/* libnbc default iallreduce rule (nbc_iallreduce.c:113-121), commutative ops */
+int mxo_iallreduce_decision(int n, size_t count, size_t es, int inplace)
+{
+    if (n < 4 || es * count < 65536 || inplace) return 2;
+    if (count >= (size_t)nbc_pof2(n)) return 3;
+    return 1;
+}
+
+/* MPI_Iallreduce on n simulated ranks; sbufs NULL = MPI_IN_PLACE.  alg:
+ * 0 libnbc rule, 1 ring, 2 binomial, 3 Rabenseifner, 4 recursive doubling.
+ * allred_sched_redscat_allgather (:976-1180) and
+ * allred_sched_recursivedoubling (:512-625) are step for step coll/base's
+ * (coll_base_allreduce.c:970-1243, :130-274), simulated above.  libnbc's
+ * ring is not in-place safe (round 0 receives over the input when
+ * sendbuf == recvbuf); here in-place ring reads the input from a copy. */
+int mxo_iallreduce(int alg, int op, int type, int n, size_t count, const void *const *sbufs, void *const *rbufs)
+{
+    void *rb[MAXN];
+    char *sb[MAXN], *tmp[MAXN] = {0};
+    const int inplace = !sbufs;
+    if (n < 1 || n > MAXN) return -1;
+    g_op = op; g_type = type; g_es = mxo_type_size(type);
+    if (!g_es) return -1;
+    for (int r = 0; r < n; r++) rb[r] = rbufs[r];
+    if (count == 0) return 0;
+    if (n == 1) { if (!inplace) cp(rb[0], sbufs[0], count); return 0; }
+    if (alg == 0) alg = mxo_iallreduce_decision(n, count, g_es, inplace);
+    if (alg == 3 && count < (size_t)nbc_pof2(n)) alg = 1;             /* :121-124 */
+    if (alg < 1 || alg > 4) alg = 1;
+    for (int r = 0; r < n; r++) {
+        if (inplace) { tmp[r] = malloc(count * g_es + 1); cp(tmp[r], rb[r], count); sb[r] = tmp[r]; }
+        else sb[r] = (char *)sbufs[r];
+    }
+    switch (alg) {
+    case 1: nbc_ring(n, count, sb, rb); break;
+    case 2: {
+        char *out = malloc(count * g_es + 1);
+        nbc_binomial(n, 0, count, sb, out);
+        for (int r = 0; r < n; r++) cp(rb[r], out, count);             /* bcast half (:426-455) */
+        free(out);
+        break;
+    }
+    case 3:
+        for (int r = 0; r < n; r++) cp(rb[r], sb[r], count);           /* NBC_Sched_copy(sbuf, rbuf) */
+        ar_rabenseifner(n, count, rb);
+        break;
+    case 4:
+        for (int r = 0; r < n; r++) cp(rb[r], sb[r], count);
+        ar_recursive_doubling(n, count, rb);
+        break;
+    }
+    for (int r = 0; r < n; r++) free(tmp[r]);
+    return 0;
+}
+
+/* libnbc default ireduce rule (nbc_ireduce.c:107-116), commutative ops */
+int mxo_ireduce_decision(int n, size_t count, size_t es)
+{
+    if (n > 2 && count >= (size_t)nbc_pof2(n)) return 3;
+    if (n > 4 || es * count < 65536) return 2;
+    return 1;
+}
+
+/* red_sched_chain (nbc_ireduce.c:461-536): vrank p-1 sends its sendbuf to
+ * p-2; every vrank receives the partial result into tmp and computes
+ * tmp = sendbuf OP tmp; the root (vrank 0) computes recvbuf = sendbuf OP
+ * recvbuf, or -- MPI_IN_PLACE, sendbuf == recvbuf -- recvbuf = tmp OP recvbuf.
+ * Fragmentation (:474-485) splits elements, not the per-element order. */
+static void nbc_chain(int n, int root, size_t count, char *const *x, char *rbuf, int inplace)
+{
+    char *acc = malloc(count * g_es + 1), *tmp = malloc(count * g_es + 1);
+    cp(acc, x[nbc_swap(n - 1, root)], count);
+    for (int v = n - 2; v >= 1; v--) {
+        cp(tmp, acc, count);                                         /* recv into tmp */
+        red(x[nbc_swap(v, root)], tmp, count);
+        cp(acc, tmp, count);
+    }
+    if (inplace) {
+        red(acc, rbuf, count);                                       /* recvbuf = tmp OP recvbuf */
+    } else {
+        cp(rbuf, acc, count);
+        red(x[root], rbuf, count);                                   /* recvbuf = sendbuf OP recvbuf */
+    }
+    free(acc);
+    free(tmp);
+}
+
+/* MPI_Ireduce: sbufs[root] NULL = MPI_IN_PLACE on the root.  alg: 0 libnbc
+ * rule, 1 chain, 2 binomial, 3 Rabenseifner (red_sched_redscat_gather
+ * :649-: steps 1-2 are the allreduce's reduce-scatter, then a gather). */
+int mxo_ireduce(int alg, int op, int type, int n, size_t count, int root, const void *const *sbufs, void *rbuf)
+{
+    char *sb[MAXN];
+    if (n < 1 || n > MAXN || root < 0 || root >= n || !rbuf) return -1;
+    g_op = op; g_type = type; g_es = mxo_type_size(type);
+    if (!g_es) return -1;
+    const int inplace = !sbufs[root];
+    for (int r = 0; r < n; r++) sb[r] = (char *)(sbufs[r] ? sbufs[r] : rbuf);
+    if (count == 0) return 0;
+    if (n == 1) { if (!inplace) cp(rbuf, sb[0], count); return 0; }
+    if (alg == 0) alg = mxo_ireduce_decision(n, count, g_es);
+    else if (alg == 3 && !(n > 2 && count >= (size_t)nbc_pof2(n))) alg = 1;   /* :121-125 */
+    else if (alg != 2 && alg != 3) alg = 1;
+    if (alg == 1) {
+        if (inplace) nbc_chain(n, root, count, sb, rbuf, 1);
+        else nbc_chain(n, root, count, sb, rbuf, 0);
+        return 0;
+    }
+    if (alg == 2) {
+        char *in_copy = NULL;
+        if (inplace) { in_copy = malloc(count * g_es + 1); cp(in_copy, rbuf, count); sb[root] = in_copy; }
+        nbc_binomial(n, root, count, sb, rbuf);
+        free(in_copy);
+        return 0;
+    }
+    {
+        void *rb[MAXN];
+        char *all = malloc((size_t)n * count * g_es + 1);
+        for (int r = 0; r < n; r++) { rb[r] = all + (size_t)r * count * g_es; cp(rb[r], sb[r], count); }
+        ar_rabenseifner(n, count, rb);
+        cp(rbuf, rb[root], count);
+        free(all);
+    }
+    return 0;
+}
+
+/* MPI_Ireduce_scatter (nbc_ireduce_scatter.c:103-186) and
+ * MPI_Ireduce_scatter_block: binomial reduction to rank 0, then rank 0
+ * scatters the blocks.  sbufs NULL = MPI_IN_PLACE. */
+int mxo_ireduce_scatter(int op, int type, int n, const size_t *rcounts, const void *const *sbufs, void *const *rbufs)
+{
+    char *sb[MAXN];
+    size_t total = 0;
+    if (n < 1 || n > MAXN) return -1;
+    g_op = op; g_type = type; g_es = mxo_type_size(type);
+    if (!g_es) return -1;
+    for (int r = 0; r < n; r++) total += rcounts[r];
+    if (total == 0) return 0;
+    char *full = malloc(total * g_es + 1), *copies = malloc((size_t)n * total * g_es + 1);
+    for (int r = 0; r < n; r++) {
+        sb[r] = copies + (size_t)r * total * g_es;
+        cp(sb[r], (sbufs && sbufs[r]) ? sbufs[r] : rbufs[r], total);
+    }
+    nbc_binomial(n, 0, total, sb, full);
+    for (int r = 0, off = 0; r < n; off += (int)rcounts[r], r++) cp(rbufs[r], AT(full, off), rcounts[r]);
+    free(full);
+    free(copies);
+    return 0;
+}

@@ -39,6 +39,7 @@
 #include <vector>
 #include <algorithm>
 #include <map>
+#include <new>
 
 #include "mx_fold.hpp"
 
@@ -185,6 +186,16 @@ struct mx_comm {
   int ev_kind[32];   // 0 fold, 1 push, 2 gather
   double ev_bytes[32];
   mx_coll_stats_t st;
+  // non-blocking / persistent requests: while `defer`
+  // is set, finish() leaves the stream running; `tail` is an event after the
+  // last deferred collective, which a collective enqueued on another stream
+  // waits for (collectives of a communicator stay in issue order across
+  // streams, as MPI orders them); `pending` counts active requests.
+  int defer;
+  int tail_valid;
+  hipEvent_t tail;
+  hipStream_t tail_stream;
+  int pending;
 };
 
 static uint64_t ticks_for(double seconds) {
@@ -422,6 +433,7 @@ extern "C" int mx_comm_destroy(mx_comm_t *c) {
   if (c->nccl) ncclCommDestroy(c->nccl);
   if (c->prof)
     for (int i = 0; i < 64; i++) (void)hipEventDestroy(c->ev[i]);
+  if (c->tail) (void)hipEventDestroy(c->tail);
   free(c);
   return MX_SUCCESS;
 }
@@ -492,9 +504,25 @@ static void push_clip(std::vector<Seg> &out, size_t lo, size_t hi, size_t rlo, s
   if (a < b) out.push_back(Seg{a, b, p});
 }
 
+// Internal allreduce algorithm id: libnbc's ring (allred_sched_ring,
+// nbc_iallreduce.c:629-860), reached through mx_iallreduce.
+constexpr int kArNbcRing = 1001;
+
 // Allreduce fold segments restricted to [rlo, rhi).
 static int allreduce_segments(int alg, int n, size_t count, size_t es, size_t rlo, size_t rhi,
                               std::vector<Seg> &out) {
+  if (alg == kArNbcRing) {
+    // segments of ceil(count/p) elements (the last ones short or empty,
+    // :648-661); segment b is first sent by rank b-1 from its sendbuf
+    // (round 0: element r+1 goes to r+1), then every rank reduces
+    // recvbuf = own OP recvbuf (:796-799) -> acc is the target
+    const size_t seg = (count + n - 1) / n;
+    for (int b = 0; b < n; b++) {
+      const size_t lo = std::min(count, (size_t)b * seg), hi = std::min(count, lo + seg);
+      push_clip(out, lo, hi, rlo, rhi, chain(n, b - 1, +1, true));
+    }
+    return MX_SUCCESS;
+  }
   if (alg == MX_ALLREDUCE_AUTO) alg = mx_allreduce_decision(n, count, -(int)es);
   if (alg == MX_ALLREDUCE_RING || alg == MX_ALLREDUCE_SEGMENTED_RING) {
     if (count < (size_t)n) alg = MX_ALLREDUCE_RECURSIVE_DOUBLING;  // :371-377 (segmented -> ring -> RD)
@@ -577,13 +605,22 @@ static int reduce_scatter_segments(int alg, int n, const size_t *rcounts, size_t
 }
 
 static int finish(mx_comm *c, hipStream_t s) {
+  if (c->defer) return MX_SUCCESS;   // request path: completion through the request's event
   if (hipStreamSynchronize(s) != hipSuccess) return MX_ERR_HIP;
-  prof_collect(c);
+  c->tail_valid = 0;                 // everything enqueued before is done
+  if (!c->pending) prof_collect(c);
   if (c->err_host && *(volatile int *)c->err_host) {
     int e = *(volatile int *)c->err_host;
     *c->err_host = 0;
     return e;
   }
+  return MX_SUCCESS;
+}
+
+// A collective about to be enqueued on `s` waits for the previous deferred
+// collective of the communicator when that one went to another stream.
+static int order(mx_comm *c, hipStream_t s) {
+  if (c->tail_valid && c->tail_stream != s && hipStreamWaitEvent(s, c->tail, 0) != hipSuccess) return MX_ERR_HIP;
   return MX_SUCCESS;
 }
 
@@ -645,6 +682,7 @@ extern "C" int mx_allreduce_local(mx_comm_t *c, const void *const *sbufs, void *
   const size_t es = mx_type_size(type);
   const int n = c->size;
   hipStream_t s = (hipStream_t)stream;
+  if (int orc = order(c, s)) return orc;
   if (count == 0) return MX_SUCCESS;
   const char *src[MAXR];
   char *dst[MAXR];
@@ -682,6 +720,7 @@ extern "C" int mx_reduce_scatter_local(mx_comm_t *c, const void *const *sbufs, v
   const size_t es = mx_type_size(type);
   const int n = c->size;
   hipStream_t s = (hipStream_t)stream;
+  if (int orc = order(c, s)) return orc;
   size_t disp[MAXR], total = 0;
   for (int j = 0; j < n; j++) { disp[j] = total; total += rcounts[j]; }
   const char *src[MAXR];
@@ -729,6 +768,7 @@ extern "C" int mx_allgather_local(mx_comm_t *c, const void *const *sbufs, void *
   if (!c || !c->local || !rbufs) return MX_ERR_ARG;
   const int n = c->size;
   hipStream_t s = (hipStream_t)stream;
+  if (int orc = order(c, s)) return orc;
   if (!bytes) return MX_SUCCESS;
   // all-peer: rank j's block goes to every rank in one launch per source
   for (int j = 0; j < n; j++) {
@@ -750,6 +790,7 @@ extern "C" int mx_allgather_local(mx_comm_t *c, const void *const *sbufs, void *
 extern "C" int mx_bcast_local(mx_comm_t *c, void *const *bufs, size_t bytes, int root, void *stream) {
   if (!c || !c->local || !bufs || root < 0 || root >= c->size) return MX_ERR_ARG;
   hipStream_t s = (hipStream_t)stream;
+  if (int orc = order(c, s)) return orc;
   if (!bytes) return MX_SUCCESS;
   CopyArgs a;
   memset(&a, 0, sizeof a);
@@ -867,6 +908,7 @@ extern "C" int mx_allreduce(mx_comm_t *c, const void *sbuf, void *rbuf, size_t c
     return mx_allreduce_local(c, sb, rb, count, type, op, alg, stream);
   }
   hipStream_t s = (hipStream_t)stream;
+  if (int orc = order(c, s)) return orc;
   const size_t es = mx_type_size(type);
   if (!es) return MX_ERR_ARG;
   const int n = c->size, r = c->rank;
@@ -983,6 +1025,7 @@ extern "C" int mx_reduce_scatter(mx_comm_t *c, const void *sbuf, void *rbuf, con
     return mx_reduce_scatter_local(c, sb, rb, rcounts, type, op, alg, stream);
   }
   hipStream_t s = (hipStream_t)stream;
+  if (int orc = order(c, s)) return orc;
   const size_t es = mx_type_size(type);
   if (!es) return MX_ERR_ARG;
   const int n = c->size, r = c->rank;
@@ -1046,6 +1089,7 @@ extern "C" int mx_allgather(mx_comm_t *c, const void *sbuf, void *rbuf, size_t b
     return mx_allgather_local(c, sb, rb, bytes, stream);
   }
   hipStream_t s = (hipStream_t)stream;
+  if (int orc = order(c, s)) return orc;
   const int n = c->size, r = c->rank;
   char *rb = (char *)rbuf;
   const char *sb = (sbuf == MX_IN_PLACE || !sbuf) ? rb + (size_t)r * bytes : (const char *)sbuf;
@@ -1090,6 +1134,7 @@ extern "C" int mx_bcast(mx_comm_t *c, void *buf, size_t bytes, int root, void *s
     return mx_bcast_local(c, b, bytes, root, stream);
   }
   hipStream_t s = (hipStream_t)stream;
+  if (int orc = order(c, s)) return orc;
   const int n = c->size, r = c->rank;
   if (!bytes || n == 1) return MX_SUCCESS;
   if (!(c->flags & MX_COMM_IPC)) return MX_ERR_STATE;
@@ -1499,8 +1544,10 @@ static int vm_run_local(vm_launch_fn vl, const VmProg &p, const char *const *src
 // info_rank >= 0: that rank's READY word carries the info bit of the
 // guarded instructions (info_bit is this rank's own bit, sent if it is
 // info_rank).
-static int vm_partitioned(mx_comm *c, vm_launch_fn vl, const VmProg &p, const char *sb, char *rb, size_t count,
-                          size_t es, uint32_t dest_mask, int info_rank, int info_bit, hipStream_t s) {
+struct VmSeg { size_t lo, hi; VmProg p; };   // program for elements [lo, hi)
+
+static int vm_partitioned(mx_comm *c, vm_launch_fn vl, const std::vector<VmSeg> &segs, const char *sb, char *rb,
+                          size_t count, size_t es, uint32_t dest_mask, int info_rank, int info_bit, hipStream_t s) {
   const int n = c->size, r = c->rank;
   const bool me_dest = (dest_mask >> r) & 1;
   const size_t ce = chunk_elems(c, count, es);
@@ -1524,25 +1571,28 @@ static int vm_partitioned(mx_comm *c, vm_launch_fn vl, const VmProg &p, const ch
     prof_end(c, s, 1, 0);
     if ((rc = signal_all(c, FLAG_READY, (g << 1) | (uint64_t)(r == info_rank ? info_bit : 0), s))) return rc;
     if ((rc = wait_all(c, FLAG_READY, g << 1, s))) return rc;
-    if (len[r]) {
-      const size_t e0 = c0 + off[r];
-      const size_t mis = (e0 * es) & 15;
+    // my part [e0, e1) of this chunk, one launch per program segment in it
+    const size_t e0 = c0 + off[r], e1 = e0 + len[r];
+    for (const VmSeg &sg : segs) {
+      const size_t lo = std::max(e0, sg.lo), hi = std::min(e1, sg.hi);
+      if (lo >= hi) continue;
+      const size_t mis = (e0 * es) & 15, sh = (lo - e0) * es;
       VmArgs a;
       memset(&a, 0, sizeof a);
       if (info_rank >= 0 && info_rank != r) a.info = c->flagmem + FLAG_READY * MAXR + info_rank;
       a.info_host = info_bit;
-      for (int j = 0; j < n; j++) a.src[j] = (j == r) ? sb + e0 * es : c->staging + (size_t)j * L.slot + mis;
+      for (int j = 0; j < n; j++) a.src[j] = ((j == r) ? sb + e0 * es : c->staging + (size_t)j * L.slot + mis) + sh;
       for (int d = 0; d < n; d++) {
         if (!((dest_mask >> d) & 1)) continue;
-        a.dst[d] = (d == r) ? rb + e0 * es : c->peer_staging[d] + L.gather_off + ((c0 * es) & 15) + off[r] * es;
+        a.dst[d] = ((d == r) ? rb + e0 * es : c->peer_staging[d] + L.gather_off + ((c0 * es) & 15) + off[r] * es) + sh;
       }
-      a.n = len[r];
-      a.p = p;
+      a.n = hi - lo;
+      a.p = sg.p;
       int nemit = 0;
-      for (int i = 0; i < p.nins; i++) nemit += (p.ins[i].op & 3) == VM_EMIT;
+      for (int i = 0; i < sg.p.nins; i++) nemit += (sg.p.ins[i].op & 3) == VM_EMIT;
       prof_begin(c, s);
       if ((rc = vl(a, s))) return rc;
-      prof_end(c, s, 0, (double)(n + nemit) * (double)len[r] * (double)es);
+      prof_end(c, s, 0, (double)(n + nemit) * (double)a.n * (double)es);
     }
     if ((rc = signal_all(c, FLAG_PUSHED, g, s))) return rc;
     if (me_dest) {
@@ -1558,6 +1608,64 @@ static int vm_partitioned(mx_comm *c, vm_launch_fn vl, const VmProg &p, const ch
       prof_end(c, s, 2, 0);
     }
     if ((rc = signal_all(c, FLAG_DONE, g, s))) return rc;
+  }
+  return finish(c, s);
+}
+static int vm_partitioned(mx_comm *c, vm_launch_fn vl, const VmProg &p, const char *sb, char *rb, size_t count,
+                          size_t es, uint32_t dest_mask, int info_rank, int info_bit, hipStream_t s) {
+  return vm_partitioned(c, vl, std::vector<VmSeg>{VmSeg{0, count, p}}, sb, rb, count, es, dest_mask, info_rank,
+                        info_bit, s);
+}
+
+// Each rank folds its own block (MPI_Reduce_scatter / _block shapes): the
+// pieces of block q go to rank q's slots, q evaluates `p` for its block into
+// its rbuf.  Chunked over the largest block.
+static int vm_scatter_blocks(mx_comm *c, vm_launch_fn vl, const VmProg &p, const char *sb, char *rb,
+                             const size_t *rcounts, size_t es, hipStream_t s) {
+  const int n = c->size, r = c->rank;
+  size_t disp[MAXR], total = 0, maxc = 0;
+  for (int j = 0; j < n; j++) { disp[j] = total; total += rcounts[j]; maxc = std::max(maxc, rcounts[j]); }
+  if (!maxc) return finish(c, s);
+  // IN_PLACE with my block starting inside the range my result overwrites:
+  // fold into a spare slot after the n slots, then copy
+  const bool overlap = sb == rb && disp[r] != 0 && disp[r] < rcounts[r];
+  const size_t nslots = (size_t)n + (overlap ? 1 : 0);
+  size_t kc = maxc;
+  while (kc > 1 && nslots * rup(kc * es + 16, 256) > c->main_bytes) kc = (kc + 1) / 2;
+  const size_t slot = rup(kc * es + 16, 256);
+  if (nslots * slot > c->main_bytes) return MX_ERR_NOMEM;
+  for (size_t k0 = 0; k0 < maxc; k0 += kc) {
+    const uint64_t gen = ++c->gen;
+    int rc;
+    if ((rc = wait_all(c, FLAG_DONE, gen - 1, s))) return rc;
+    CopyArgs ca;
+    memset(&ca, 0, sizeof ca);
+    for (int q = 0; q < n; q++) {
+      if (q == r || k0 >= rcounts[q]) continue;
+      const size_t e0 = disp[q] + k0;
+      ca.j[ca.n++] = CopyJob{sb + e0 * es, c->peer_staging[q] + (size_t)r * slot + ((e0 * es) & 15),
+                             std::min(kc, rcounts[q] - k0) * es};
+    }
+    prof_begin(c, s);
+    if ((rc = copy_launch(ca, s))) return rc;
+    prof_end(c, s, 1, 0);
+    if ((rc = signal_all(c, FLAG_READY, gen << 1, s))) return rc;
+    if ((rc = wait_all(c, FLAG_READY, gen << 1, s))) return rc;
+    if (k0 < rcounts[r]) {
+      const size_t kl = std::min(kc, rcounts[r] - k0), e0 = disp[r] + k0, mis = (e0 * es) & 15;
+      VmArgs a;
+      memset(&a, 0, sizeof a);
+      for (int j = 0; j < n; j++) a.src[j] = (j == r) ? sb + e0 * es : c->staging + (size_t)j * slot + mis;
+      char *dst = overlap ? c->staging + (size_t)n * slot + mis : rb + k0 * es;
+      a.dst[r] = dst;
+      a.n = kl;
+      a.p = p;
+      prof_begin(c, s);
+      if ((rc = vl(a, s))) return rc;
+      prof_end(c, s, 0, (double)(n + 1) * (double)kl * (double)es);
+      if (overlap && (rc = copy_async(rb + k0 * es, dst, kl * es, s))) return rc;
+    }
+    if ((rc = signal_all(c, FLAG_DONE, gen, s))) return rc;
   }
   return finish(c, s);
 }
@@ -1597,6 +1705,7 @@ extern "C" int mx_reduce_local(mx_comm_t *c, const void *const *sbufs, void *con
   }
   dst[root] = (char *)rbufs[root];
   if (!dst[root]) return MX_ERR_ARG;
+  if ((rc = order(c, (hipStream_t)stream))) return rc;
   Dag g(n);
   if ((rc = reduce_dag(g, alg, count, es, root, inplace ? 1 : 0))) return rc;
   VmProg p;
@@ -1621,6 +1730,7 @@ extern "C" int mx_reduce(mx_comm_t *c, const void *sbuf, void *rbuf, size_t coun
   int rc = vm_setup(op, type, &vl, &es);
   if (rc) return rc;
   hipStream_t s = (hipStream_t)stream;
+  if (int orc = order(c, s)) return orc;
   if (count == 0) return MX_SUCCESS;
   const bool inplace = (r == root) && (sbuf == MX_IN_PLACE || !sbuf);
   const char *sb = (sbuf == MX_IN_PLACE || !sbuf) ? (const char *)rbuf : (const char *)sbuf;
@@ -1658,6 +1768,7 @@ static int scan_local_impl(mx_comm_t *c, const void *const *sbufs, void *const *
     src[j] = (const char *)sb;
     dst[j] = (char *)rbufs[j];
   }
+  if ((rc = order(c, (hipStream_t)stream))) return rc;
   Dag g(n);
   if ((rc = scan_dag(g, alg, exclusive))) return rc;
   if (g.out.empty()) return finish(c, (hipStream_t)stream);
@@ -1681,6 +1792,7 @@ static int scan_impl(mx_comm_t *c, const void *sbuf, void *rbuf, size_t count, i
   int rc = vm_setup(op, type, &vl, &es);
   if (rc) return rc;
   hipStream_t s = (hipStream_t)stream;
+  if (int orc = order(c, s)) return orc;
   if (count == 0) return MX_SUCCESS;
   const char *sb = (sbuf == MX_IN_PLACE || !sbuf) ? (const char *)rbuf : (const char *)sbuf;
   if (c->size == 1) {   // scan: a copy; exscan: rank 0's rbuf is undefined (left untouched)
@@ -1733,6 +1845,7 @@ extern "C" int mx_reduce_scatter_block_local(mx_comm_t *c, const void *const *sb
     if (!sb || !rbufs[j]) return MX_ERR_ARG;
     src[j] = (const char *)sb;
   }
+  if ((rc = order(c, (hipStream_t)stream))) return rc;
   Dag g(n);
   if ((rc = reduce_dag(g, alg, rcount * n, es, 0, 0))) return rc;
   g.out.back().dst = -1;   // the block's owner
@@ -1764,6 +1877,7 @@ extern "C" int mx_reduce_scatter_block(mx_comm_t *c, const void *sbuf, void *rbu
   int rc = vm_setup(op, type, &vl, &es);
   if (rc) return rc;
   hipStream_t s = (hipStream_t)stream;
+  if (int orc = order(c, s)) return orc;
   const int n = c->size, r = c->rank;
   if (rcount == 0) return MX_SUCCESS;
   const char *sb = (sbuf == MX_IN_PLACE || !sbuf) ? (const char *)rbuf : (const char *)sbuf;
@@ -1777,40 +1891,477 @@ extern "C" int mx_reduce_scatter_block(mx_comm_t *c, const void *sbuf, void *rbu
   g.out.back().dst = -1;
   VmProg p;
   if ((rc = dag_compile(g, r, p))) return rc;
-  // chunks of each block: slot j holds rank j's piece of my block
-  size_t kc = rcount;
-  while (kc > 1 && (size_t)n * rup(kc * es + 16, 256) > c->main_bytes) kc = (kc + 1) / 2;
-  const size_t slot = rup(kc * es + 16, 256);
-  for (size_t k0 = 0; k0 < rcount; k0 += kc) {
-    const size_t kl = std::min(kc, rcount - k0);
-    const uint64_t gen = ++c->gen;
-    if ((rc = wait_all(c, FLAG_DONE, gen - 1, s))) return rc;
-    CopyArgs ca;
-    memset(&ca, 0, sizeof ca);
-    for (int q = 0; q < n; q++) {
-      if (q == r) continue;
-      const size_t e0 = (size_t)q * rcount + k0;
-      ca.j[ca.n++] = CopyJob{sb + e0 * es, c->peer_staging[q] + (size_t)r * slot + ((e0 * es) & 15), kl * es};
+  size_t rcounts[MAXR];
+  for (int q = 0; q < n; q++) rcounts[q] = rcount;
+  return vm_scatter_blocks(c, vl, p, sb, (char *)rbuf, rcounts, es, s);
+}
+
+// ---------------------------------------------------------------------------
+// Non-blocking and persistent collectives.
+//
+// The reference runs MPI_I<coll> / MPI_<Coll>_init in coll/libnbc: a
+// schedule of sends, receives and local ompi_op_reduce calls (nbc.c:523)
+// that the host must progress (ompi_coll_libnbc_progress,
+// coll_libnbc_component.c:426-482).  Here every collective already runs as a
+// chain of kernels with device-side flag waits, so a non-blocking collective
+// is the same enqueue without the final stream synchronisation: the GPU
+// progresses it on its own, and the request is an event after the last
+// kernel.  Reduction orders follow libnbc's schedules (its algorithm
+// selection and its operand roles), not coll/tuned's, so MPI_Iallreduce
+// results are bit-identical to what libnbc computes:
+//   iallreduce  binomial (allred_sched_diss :365-455, root 0, then bcast),
+//               ring (allred_sched_ring :629-860), Rabenseifner
+//               (allred_sched_redscat_allgather :976-1180 == coll/base's),
+//               recursive doubling (allred_sched_recursivedoubling
+//               :512-625 == coll/base's)
+//   ireduce     binomial (red_sched_binomial nbc_ireduce.c:356-458), chain
+//               (red_sched_chain :461-536), Rabenseifner reduce
+//               (red_sched_redscat_gather :649-: steps 1-2 == allreduce's)
+//   ireduce_scatter(_block)  binomial reduce to 0 + scatter
+//               (nbc_ireduce_scatter.c:103-186, nbc_ireduce_scatter_block.c)
+//   iscan/iexscan  linear / recursive doubling (== coll/base's,
+//               nbc_iscan.c:183-320, nbc_iexscan.c:213-350)
+//   iallgather/ibcast  data movement only
+// ---------------------------------------------------------------------------
+namespace {
+
+// libnbc's binomial reduction in virtual ranks (0 <-> vroot swapped,
+// RANK2VRANK nbc_iallreduce.c:353-364): round r = 1..ceil(log2 p), v with
+// v % 2^r == 0 receives the partial result of v + 2^(r-1) and computes
+// recv = own OP recv (NBC_Sched_op(sendbuf|lbuf, rbuf), :401-409).
+static int nbc_binomial_expr(Dag &g, int vroot) {
+  const int n = g.n;
+  auto real = [&](int v) { return v == 0 ? vroot : v == vroot ? 0 : v; };
+  std::vector<int> acc(n);
+  for (int v = 0; v < n; v++) acc[v] = real(v);
+  int maxr = 0;
+  while ((1 << maxr) < n) maxr++;
+  for (int r = 1; r <= maxr; r++)
+    for (int v = 0; v < n; v += 1 << r) {
+      const int vp = v + (1 << (r - 1));
+      if (vp < n) acc[v] = g.comb(acc[vp], acc[v]);
     }
-    prof_begin(c, s);
-    if ((rc = copy_launch(ca, s))) return rc;
-    prof_end(c, s, 1, 0);
-    if ((rc = signal_all(c, FLAG_READY, gen << 1, s))) return rc;
-    if ((rc = wait_all(c, FLAG_READY, gen << 1, s))) return rc;
-    const size_t e0 = (size_t)r * rcount + k0;
-    const size_t mis = (e0 * es) & 15;
-    VmArgs a;
-    memset(&a, 0, sizeof a);
-    for (int j = 0; j < n; j++) a.src[j] = (j == r) ? sb + e0 * es : c->staging + (size_t)j * slot + mis;
-    a.dst[r] = (char *)rbuf + k0 * es;
-    a.n = kl;
-    a.p = p;
-    prof_begin(c, s);
-    if ((rc = vl(a, s))) return rc;
-    prof_end(c, s, 0, (double)(n + 1) * (double)kl * (double)es);
-    if ((rc = signal_all(c, FLAG_DONE, gen, s))) return rc;
+  return acc[0];
+}
+
+// red_sched_chain (nbc_ireduce.c:461-536): virtual ranks (0 <-> root); v = p-1
+// sends its data down the chain, every v computes acc = own OP acc (:500-503);
+// the root with MPI_IN_PLACE reduces recvbuf = acc OP own (:497-499).
+static int nbc_chain_expr(Dag &g, int root, bool root_inplace) {
+  const int n = g.n;
+  auto real = [&](int v) { return v == 0 ? root : v == root ? 0 : v; };
+  int acc = real(n - 1);
+  for (int v = n - 2; v >= 1; v--) acc = g.comb(acc, real(v));
+  return root_inplace ? g.comb(root, acc) : g.comb(acc, root);
+}
+
+// The expression a fold program evaluates (eval_prog, mx_fold.hpp).
+static int fold_expr(Dag &g, const FoldProg &p) {
+  if (p.kind == PROG_CHAIN) {
+    int acc = p.ord[0];
+    for (int j = 1; j < p.n; j++) acc = p.acc_first ? g.comb(acc, p.ord[j]) : g.comb(p.ord[j], acc);
+    return acc;
   }
-  return finish(c, s);
+  std::vector<int> R(p.n);
+  for (int i = 0; i < p.n; i++) R[i] = p.lb[i] >= 0 ? g.comb(p.la[i], p.lb[i]) : p.la[i];
+  for (int s = 0; s < p.D; s++) {
+    const int h = 1 << s;
+    const bool hi_first = (p.pref >> s) & 1;
+    for (int u = 0; u < p.n; u += 2 << s) R[u] = hi_first ? g.comb(R[u + h], R[u]) : g.comb(R[u], R[u + h]);
+  }
+  return R[0];
+}
+
+static int pof2_le(int n) { return 1 << ilog2(n); }
+
+static int nbc_allreduce(mx_comm *c, const void *sbuf, void *rbuf, size_t count, int type, int op, int alg,
+                         hipStream_t s) {
+  const size_t es = mx_type_size(type);
+  if (!es) return MX_ERR_ARG;
+  const int n = c->size;
+  const bool inplace = sbuf == MX_IN_PLACE || !sbuf || sbuf == rbuf;
+  if (alg == MX_IALLREDUCE_AUTO) alg = mx_iallreduce_decision(n, count, type, inplace ? 1 : 0);
+  if (n == 1 || c->local || count == 0) return mx_allreduce(c, sbuf, rbuf, count, type, op, MX_ALLREDUCE_RING, s);
+  switch (alg) {
+    case MX_IALLREDUCE_BINOMIAL: {
+      vm_launch_fn vl;
+      size_t es2;
+      int rc = vm_setup(op, type, &vl, &es2);
+      if (rc) return rc;
+      if (!(c->flags & MX_COMM_IPC)) return MX_ERR_STATE;
+      if ((rc = order(c, s))) return rc;
+      Dag g(n);
+      const int e = nbc_binomial_expr(g, 0);
+      for (int d = 0; d < n; d++) g.emit(e, d);
+      VmProg p;
+      if ((rc = dag_compile(g, c->rank, p))) return rc;
+      const char *sb = inplace ? (const char *)rbuf : (const char *)sbuf;
+      const uint32_t all = (n >= 32) ? 0xffffffffu : ((1u << n) - 1);
+      return vm_partitioned(c, vl, p, sb, (char *)rbuf, count, es, all, -1, 0, s);
+    }
+    case MX_IALLREDUCE_RECURSIVE_DOUBLING:
+      return mx_allreduce(c, sbuf, rbuf, count, type, op, MX_ALLREDUCE_RECURSIVE_DOUBLING, s);
+    case MX_IALLREDUCE_RABENSEIFNER:
+      if (count >= (size_t)pof2_le(n))   // :121-124; otherwise ring
+        return mx_allreduce(c, sbuf, rbuf, count, type, op, MX_ALLREDUCE_RABENSEIFNER, s);
+      return mx_allreduce(c, sbuf, rbuf, count, type, op, kArNbcRing, s);
+    default:   // 1 and anything unknown: ring (:125-127)
+      return mx_allreduce(c, sbuf, rbuf, count, type, op, kArNbcRing, s);
+  }
+}
+
+static int nbc_reduce(mx_comm *c, const void *sbuf, void *rbuf, size_t count, int type, int op, int root, int alg,
+                      hipStream_t s) {
+  if (root < 0 || root >= c->size) return MX_ERR_ARG;
+  const int n = c->size, r = c->rank;
+  if (n == 1 || c->local || count == 0) return mx_reduce(c, sbuf, rbuf, count, type, op, root, MX_REDUCE_LINEAR, s);
+  vm_launch_fn vl;
+  size_t es;
+  int rc = vm_setup(op, type, &vl, &es);
+  if (rc) return rc;
+  if (r == root && !rbuf) return MX_ERR_ARG;
+  if (!(c->flags & MX_COMM_IPC)) return MX_ERR_STATE;
+  if ((rc = order(c, s))) return rc;
+  const bool inplace = (r == root) && (sbuf == MX_IN_PLACE || !sbuf || sbuf == rbuf);
+  const char *sb = (sbuf == MX_IN_PLACE || !sbuf) ? (const char *)rbuf : (const char *)sbuf;
+  if (!sb) return MX_ERR_ARG;
+  if (alg == MX_IREDUCE_AUTO) alg = mx_ireduce_decision(n, count, type);
+  else if (alg == MX_IREDUCE_RABENSEIFNER && !(n > 2 && count >= (size_t)pof2_le(n))) alg = MX_IREDUCE_CHAIN;
+  else if (alg != MX_IREDUCE_BINOMIAL && alg != MX_IREDUCE_RABENSEIFNER) alg = MX_IREDUCE_CHAIN;   // :117-125
+  std::vector<VmSeg> segs;
+  if (alg == MX_IREDUCE_RABENSEIFNER) {
+    // steps 1-2 are the allreduce's reduce-scatter: same per-element trees
+    std::vector<Seg> fs;
+    if ((rc = allreduce_segments(MX_ALLREDUCE_RABENSEIFNER, n, count, es, 0, count, fs))) return rc;
+    for (const Seg &f : fs) {
+      Dag g(n);
+      g.emit(fold_expr(g, f.p), root);
+      VmSeg v{f.lo, f.hi, {}};
+      if ((rc = dag_compile(g, r, v.p))) return rc;
+      segs.push_back(v);
+    }
+    return vm_partitioned(c, vl, segs, sb, (char *)rbuf, count, es, 1u << root, -1, 0, s);
+  }
+  Dag g(n);
+  if (alg == MX_IREDUCE_BINOMIAL) {
+    g.emit(nbc_binomial_expr(g, root), root);   // commutative ops: vroot = root (:369-373)
+  } else {
+    const int e1 = nbc_chain_expr(g, root, true), e0 = nbc_chain_expr(g, root, false);
+    g.emit(e1, root, VM_IF_SET);
+    g.emit(e0, root, VM_IF_CLEAR);
+  }
+  VmProg p;
+  if ((rc = dag_compile(g, r, p))) return rc;
+  return vm_partitioned(c, vl, p, sb, (char *)rbuf, count, es, 1u << root, root, inplace ? 1 : 0, s);
+}
+
+static int nbc_reduce_scatter(mx_comm *c, const void *sbuf, void *rbuf, const size_t *rcounts, int type, int op,
+                              hipStream_t s) {
+  const int n = c->size;
+  if (n == 1 || c->local) return mx_reduce_scatter(c, sbuf, rbuf, rcounts, type, op, MX_RS_RING, s);
+  vm_launch_fn vl;
+  size_t es;
+  int rc = vm_setup(op, type, &vl, &es);
+  if (rc) return rc;
+  if (!(c->flags & MX_COMM_IPC)) return MX_ERR_STATE;
+  if ((rc = order(c, s))) return rc;
+  const char *sb = (sbuf == MX_IN_PLACE || !sbuf) ? (const char *)rbuf : (const char *)sbuf;
+  Dag g(n);
+  g.emit(nbc_binomial_expr(g, 0), -1);   // reduce to rank 0, scatter (:103-186)
+  VmProg p;
+  if ((rc = dag_compile(g, c->rank, p))) return rc;
+  return vm_scatter_blocks(c, vl, p, sb, (char *)rbuf, rcounts, es, s);
+}
+
+}  // namespace
+
+extern "C" int mx_iallreduce_decision(int n, size_t count, int type, int inplace) {
+  // nbc_allreduce_init (nbc_iallreduce.c:113-121), commutative ops
+  const size_t es = type < 0 ? (size_t)(-type) : mx_type_size(type);
+  if (n < 4 || es * count < 65536 || inplace) return MX_IALLREDUCE_BINOMIAL;
+  if (count >= (size_t)pof2_le(n)) return MX_IALLREDUCE_RABENSEIFNER;
+  return MX_IALLREDUCE_RING;
+}
+
+extern "C" int mx_ireduce_decision(int n, size_t count, int type) {
+  // nbc_reduce_init (nbc_ireduce.c:107-116), commutative ops
+  const size_t es = type < 0 ? (size_t)(-type) : mx_type_size(type);
+  if (n > 2 && count >= (size_t)pof2_le(n)) return MX_IREDUCE_RABENSEIFNER;
+  if (n > 4 || es * count < 65536) return MX_IREDUCE_BINOMIAL;
+  return MX_IREDUCE_CHAIN;
+}
+
+enum { RQ_ALLREDUCE, RQ_REDUCE, RQ_REDUCE_SCATTER, RQ_REDUCE_SCATTER_BLOCK, RQ_SCAN, RQ_EXSCAN, RQ_ALLGATHER, RQ_BCAST };
+
+struct mx_request {
+  mx_comm *c;
+  int kind, persistent, active;
+  hipStream_t s;
+  hipEvent_t done;
+  const void *sbuf;
+  void *rbuf;
+  size_t count;   // elements (bytes for allgather / bcast)
+  int type, op, alg, root;
+  std::vector<size_t> rcounts;
+};
+
+namespace {
+
+static int req_dispatch(mx_request *q) {
+  mx_comm *c = q->c;
+  switch (q->kind) {
+    case RQ_ALLREDUCE: return nbc_allreduce(c, q->sbuf, q->rbuf, q->count, q->type, q->op, q->alg, q->s);
+    case RQ_REDUCE: return nbc_reduce(c, q->sbuf, q->rbuf, q->count, q->type, q->op, q->root, q->alg, q->s);
+    case RQ_REDUCE_SCATTER:
+    case RQ_REDUCE_SCATTER_BLOCK:
+      return nbc_reduce_scatter(c, q->sbuf, q->rbuf, q->rcounts.data(), q->type, q->op, q->s);
+    case RQ_SCAN:
+    case RQ_EXSCAN: {
+      // nbc_iscan.c:75-84 / nbc_iexscan.c:75-84: 2 = recursive doubling, else linear
+      const int alg = q->alg == MX_SCAN_RECURSIVE_DOUBLING ? MX_SCAN_RECURSIVE_DOUBLING : MX_SCAN_LINEAR;
+      return scan_impl(c, q->sbuf, q->rbuf, q->count, q->type, q->op, alg, q->kind == RQ_EXSCAN, q->s);
+    }
+    case RQ_ALLGATHER: return mx_allgather(c, q->sbuf, q->rbuf, q->count, q->s);
+    case RQ_BCAST: return mx_bcast(c, q->rbuf, q->count, q->root, q->s);
+  }
+  return MX_ERR_ARG;
+}
+
+static int req_start(mx_request *q) {
+  mx_comm *c = q->c;
+  if (q->active) return MX_ERR_STATE;
+  if (!c->tail && hipEventCreateWithFlags(&c->tail, hipEventDisableTiming) != hipSuccess) return MX_ERR_HIP;
+  c->defer = 1;
+  const int rc = req_dispatch(q);
+  c->defer = 0;
+  // whatever this call enqueued orders the communicator's next collective
+  if (hipEventRecord(c->tail, q->s) != hipSuccess) return MX_ERR_HIP;
+  c->tail_valid = 1;
+  c->tail_stream = q->s;
+  if (rc) return rc;
+  if (hipEventRecord(q->done, q->s) != hipSuccess) return MX_ERR_HIP;
+  q->active = 1;
+  c->pending++;
+  return MX_SUCCESS;
+}
+
+static int req_complete(mx_request *q) {
+  mx_comm *c = q->c;
+  q->active = 0;
+  if (--c->pending == 0) prof_collect(c);
+  if (c->err_host && *(volatile int *)c->err_host) {
+    const int e = *(volatile int *)c->err_host;
+    *c->err_host = 0;
+    return e;
+  }
+  return MX_SUCCESS;
+}
+
+static int req_new(mx_comm *c, int kind, int persistent, void *stream, mx_request_t **out, mx_request **q) {
+  if (!c || !out) return MX_ERR_ARG;
+  *out = nullptr;
+  mx_request *r = new (std::nothrow) mx_request();
+  if (!r) return MX_ERR_NOMEM;
+  if (hipEventCreateWithFlags(&r->done, hipEventDisableTiming) != hipSuccess) {
+    delete r;
+    return MX_ERR_HIP;
+  }
+  r->c = c;
+  r->kind = kind;
+  r->persistent = persistent;
+  r->s = (hipStream_t)stream;
+  *q = r;
+  return MX_SUCCESS;
+}
+
+// non-blocking: start now; persistent: hand back an inactive request
+static int req_post(mx_request *q, mx_request_t **out) {
+  if (!q->persistent) {
+    const int rc = req_start(q);
+    if (rc) {
+      (void)hipEventDestroy(q->done);
+      delete q;
+      return rc;
+    }
+  }
+  *out = q;
+  return MX_SUCCESS;
+}
+
+static int req_reduction(mx_comm_t *c, int kind, int persistent, const void *sbuf, void *rbuf, size_t count,
+                         int type, int op, int root, int alg, void *stream, mx_request_t **req) {
+  mx_request *q;
+  int rc = req_new(c, kind, persistent, stream, req, &q);
+  if (rc) return rc;
+  if (!mx_type_size(type) || (kind != RQ_REDUCE && !rbuf)) rc = MX_ERR_ARG;
+  else if (!fold_fns(op, type).vm) rc = MX_ERR_UNSUPPORTED;
+  if (rc) {
+    (void)hipEventDestroy(q->done);
+    delete q;
+    return rc;
+  }
+  q->sbuf = sbuf;
+  q->rbuf = rbuf;
+  q->count = count;
+  q->type = type;
+  q->op = op;
+  q->root = root;
+  q->alg = alg;
+  return req_post(q, req);
+}
+
+}  // namespace
+
+extern "C" int mx_iallreduce(mx_comm_t *c, const void *sbuf, void *rbuf, size_t count, int type, int op, int alg,
+                             void *stream, mx_request_t **req) {
+  return req_reduction(c, RQ_ALLREDUCE, 0, sbuf, rbuf, count, type, op, 0, alg, stream, req);
+}
+extern "C" int mx_allreduce_init(mx_comm_t *c, const void *sbuf, void *rbuf, size_t count, int type, int op,
+                                 int alg, void *stream, mx_request_t **req) {
+  return req_reduction(c, RQ_ALLREDUCE, 1, sbuf, rbuf, count, type, op, 0, alg, stream, req);
+}
+extern "C" int mx_ireduce(mx_comm_t *c, const void *sbuf, void *rbuf, size_t count, int type, int op, int root,
+                          int alg, void *stream, mx_request_t **req) {
+  if (c && (root < 0 || root >= c->size)) return MX_ERR_ARG;
+  return req_reduction(c, RQ_REDUCE, 0, sbuf, rbuf, count, type, op, root, alg, stream, req);
+}
+extern "C" int mx_reduce_init(mx_comm_t *c, const void *sbuf, void *rbuf, size_t count, int type, int op, int root,
+                              int alg, void *stream, mx_request_t **req) {
+  if (c && (root < 0 || root >= c->size)) return MX_ERR_ARG;
+  return req_reduction(c, RQ_REDUCE, 1, sbuf, rbuf, count, type, op, root, alg, stream, req);
+}
+extern "C" int mx_iscan(mx_comm_t *c, const void *sbuf, void *rbuf, size_t count, int type, int op, int alg,
+                        void *stream, mx_request_t **req) {
+  return req_reduction(c, RQ_SCAN, 0, sbuf, rbuf, count, type, op, 0, alg, stream, req);
+}
+extern "C" int mx_scan_init(mx_comm_t *c, const void *sbuf, void *rbuf, size_t count, int type, int op, int alg,
+                            void *stream, mx_request_t **req) {
+  return req_reduction(c, RQ_SCAN, 1, sbuf, rbuf, count, type, op, 0, alg, stream, req);
+}
+extern "C" int mx_iexscan(mx_comm_t *c, const void *sbuf, void *rbuf, size_t count, int type, int op, int alg,
+                          void *stream, mx_request_t **req) {
+  return req_reduction(c, RQ_EXSCAN, 0, sbuf, rbuf, count, type, op, 0, alg, stream, req);
+}
+extern "C" int mx_exscan_init(mx_comm_t *c, const void *sbuf, void *rbuf, size_t count, int type, int op, int alg,
+                              void *stream, mx_request_t **req) {
+  return req_reduction(c, RQ_EXSCAN, 1, sbuf, rbuf, count, type, op, 0, alg, stream, req);
+}
+
+static int req_reduce_scatter(mx_comm_t *c, int kind, int persistent, const void *sbuf, void *rbuf,
+                              const size_t *rcounts, size_t rcount, int type, int op, void *stream,
+                              mx_request_t **req) {
+  if (!c || (kind == RQ_REDUCE_SCATTER && !rcounts)) return MX_ERR_ARG;
+  mx_request *q;
+  int rc = req_new(c, kind, persistent, stream, req, &q);
+  if (rc) return rc;
+  if (!mx_type_size(type) || !rbuf) rc = MX_ERR_ARG;
+  else if (!fold_fns(op, type).vm) rc = MX_ERR_UNSUPPORTED;
+  if (rc) {
+    (void)hipEventDestroy(q->done);
+    delete q;
+    return rc;
+  }
+  q->sbuf = sbuf;
+  q->rbuf = rbuf;
+  q->type = type;
+  q->op = op;
+  q->rcounts.resize(c->size);
+  for (int i = 0; i < c->size; i++) q->rcounts[i] = kind == RQ_REDUCE_SCATTER ? rcounts[i] : rcount;
+  return req_post(q, req);
+}
+
+extern "C" int mx_ireduce_scatter(mx_comm_t *c, const void *sbuf, void *rbuf, const size_t *rcounts, int type,
+                                  int op, void *stream, mx_request_t **req) {
+  return req_reduce_scatter(c, RQ_REDUCE_SCATTER, 0, sbuf, rbuf, rcounts, 0, type, op, stream, req);
+}
+extern "C" int mx_reduce_scatter_init(mx_comm_t *c, const void *sbuf, void *rbuf, const size_t *rcounts, int type,
+                                      int op, void *stream, mx_request_t **req) {
+  return req_reduce_scatter(c, RQ_REDUCE_SCATTER, 1, sbuf, rbuf, rcounts, 0, type, op, stream, req);
+}
+extern "C" int mx_ireduce_scatter_block(mx_comm_t *c, const void *sbuf, void *rbuf, size_t rcount, int type,
+                                        int op, void *stream, mx_request_t **req) {
+  return req_reduce_scatter(c, RQ_REDUCE_SCATTER_BLOCK, 0, sbuf, rbuf, nullptr, rcount, type, op, stream, req);
+}
+extern "C" int mx_reduce_scatter_block_init(mx_comm_t *c, const void *sbuf, void *rbuf, size_t rcount, int type,
+                                            int op, void *stream, mx_request_t **req) {
+  return req_reduce_scatter(c, RQ_REDUCE_SCATTER_BLOCK, 1, sbuf, rbuf, nullptr, rcount, type, op, stream, req);
+}
+
+static int req_move(mx_comm_t *c, int kind, int persistent, const void *sbuf, void *buf, size_t bytes, int root,
+                    void *stream, mx_request_t **req) {
+  if (!c || !buf || (kind == RQ_BCAST && (root < 0 || root >= c->size))) return MX_ERR_ARG;
+  mx_request *q;
+  int rc = req_new(c, kind, persistent, stream, req, &q);
+  if (rc) return rc;
+  q->sbuf = sbuf;
+  q->rbuf = buf;
+  q->count = bytes;
+  q->root = root;
+  return req_post(q, req);
+}
+extern "C" int mx_iallgather(mx_comm_t *c, const void *sbuf, void *rbuf, size_t bytes, void *stream,
+                             mx_request_t **req) {
+  return req_move(c, RQ_ALLGATHER, 0, sbuf, rbuf, bytes, 0, stream, req);
+}
+extern "C" int mx_allgather_init(mx_comm_t *c, const void *sbuf, void *rbuf, size_t bytes, void *stream,
+                                 mx_request_t **req) {
+  return req_move(c, RQ_ALLGATHER, 1, sbuf, rbuf, bytes, 0, stream, req);
+}
+extern "C" int mx_ibcast(mx_comm_t *c, void *buf, size_t bytes, int root, void *stream, mx_request_t **req) {
+  return req_move(c, RQ_BCAST, 0, nullptr, buf, bytes, root, stream, req);
+}
+extern "C" int mx_bcast_init(mx_comm_t *c, void *buf, size_t bytes, int root, void *stream, mx_request_t **req) {
+  return req_move(c, RQ_BCAST, 1, nullptr, buf, bytes, root, stream, req);
+}
+
+extern "C" int mx_start(mx_request_t *q) {
+  if (!q) return MX_ERR_ARG;
+  if (!q->persistent) return MX_ERR_STATE;
+  return req_start(q);
+}
+
+extern "C" int mx_startall(size_t n, mx_request_t *const *reqs) {
+  if (n && !reqs) return MX_ERR_ARG;
+  for (size_t i = 0; i < n; i++)
+    if (int rc = mx_start(reqs[i])) return rc;
+  return MX_SUCCESS;
+}
+
+extern "C" int mx_test(mx_request_t *q, int *flag) {
+  if (!q || !flag) return MX_ERR_ARG;
+  *flag = 1;
+  if (!q->active) return MX_SUCCESS;   // completed or inactive persistent: MPI_Test gives true
+  const hipError_t e = hipEventQuery(q->done);
+  if (e == hipErrorNotReady) {
+    *flag = 0;
+    return MX_SUCCESS;
+  }
+  if (e != hipSuccess) return MX_ERR_HIP;
+  return req_complete(q);
+}
+
+extern "C" int mx_wait(mx_request_t *q) {
+  if (!q) return MX_ERR_ARG;
+  if (!q->active) return MX_SUCCESS;
+  if (hipEventSynchronize(q->done) != hipSuccess) return MX_ERR_HIP;
+  return req_complete(q);
+}
+
+extern "C" int mx_request_stream_wait(mx_request_t *q, void *stream) {
+  if (!q) return MX_ERR_ARG;
+  if (!q->active) return MX_SUCCESS;
+  return hipStreamWaitEvent((hipStream_t)stream, q->done, 0) == hipSuccess ? MX_SUCCESS : MX_ERR_HIP;
+}
+
+extern "C" int mx_request_is_active(const mx_request_t *q) { return q ? q->active : MX_ERR_ARG; }
+
+extern "C" int mx_request_free(mx_request_t *q) {
+  if (!q) return MX_SUCCESS;
+  int rc = MX_SUCCESS;
+  if (q->active) rc = mx_wait(q);   // MPI_Request_free lets an active operation finish
+  (void)hipEventDestroy(q->done);
+  delete q;
+  return rc;
 }
 
 // ---------------------------------------------------------------------------

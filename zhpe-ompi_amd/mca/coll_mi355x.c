@@ -19,6 +19,14 @@
  *  - the device/host decision is taken per call from the buffers
  *    (coll_cuda_allreduce.c:39-56) -- but instead of staging through host
  *    memory the device path runs the collective on the GPUs.
+ * The nonblocking and persistent slots (iallreduce, ireduce, ireduce_scatter,
+ * ireduce_scatter_block, iscan, iexscan, iallgather, ibcast and their
+ * *_init forms) replace coll/libnbc's for device buffers: the collective is
+ * enqueued on the GPU and the request completes through a progress
+ * callback that polls its event (libnbc's ompi_coll_libnbc_progress,
+ * coll_libnbc_component.c:426-482, progresses the schedule on the host
+ * instead); reduction orders are libnbc's, algorithm selection follows the
+ * coll_libnbc_<coll>_algorithm vars (coll_mi355x_<coll>_algorithm wins).
  * The algorithm is chosen with coll/tuned's fixed decision
  * (coll_tuned_decision_fixed.c:44-95, :466-512) unless forced with the MCA
  * vars coll_mi355x_allreduce_algorithm / coll_mi355x_reduce_scatter_algorithm
@@ -57,7 +65,32 @@ typedef struct {
     mca_coll_base_module_t *prev_scan_module;
     mca_coll_base_module_exscan_fn_t prev_exscan;
     mca_coll_base_module_t *prev_exscan_module;
+    /* nonblocking / persistent delegation targets (coll/libnbc); a slot the
+     * lower modules do not provide is left to them (not installed) */
+#define MX_PREV_SLOT(T, name) T prev_##name; mca_coll_base_module_t *prev_##name##_module;
+    MX_PREV_SLOT(mca_coll_base_module_iallreduce_fn_t, iallreduce)
+    MX_PREV_SLOT(mca_coll_base_module_ireduce_fn_t, ireduce)
+    MX_PREV_SLOT(mca_coll_base_module_ireduce_scatter_fn_t, ireduce_scatter)
+    MX_PREV_SLOT(mca_coll_base_module_ireduce_scatter_block_fn_t, ireduce_scatter_block)
+    MX_PREV_SLOT(mca_coll_base_module_iscan_fn_t, iscan)
+    MX_PREV_SLOT(mca_coll_base_module_iexscan_fn_t, iexscan)
+    MX_PREV_SLOT(mca_coll_base_module_iallgather_fn_t, iallgather)
+    MX_PREV_SLOT(mca_coll_base_module_ibcast_fn_t, ibcast)
+    MX_PREV_SLOT(mca_coll_base_module_allreduce_init_fn_t, allreduce_init)
+    MX_PREV_SLOT(mca_coll_base_module_reduce_init_fn_t, reduce_init)
+    MX_PREV_SLOT(mca_coll_base_module_reduce_scatter_init_fn_t, reduce_scatter_init)
+    MX_PREV_SLOT(mca_coll_base_module_reduce_scatter_block_init_fn_t, reduce_scatter_block_init)
+    MX_PREV_SLOT(mca_coll_base_module_scan_init_fn_t, scan_init)
+    MX_PREV_SLOT(mca_coll_base_module_exscan_init_fn_t, exscan_init)
+    MX_PREV_SLOT(mca_coll_base_module_allgather_init_fn_t, allgather_init)
+    MX_PREV_SLOT(mca_coll_base_module_bcast_init_fn_t, bcast_init)
+#undef MX_PREV_SLOT
 } mx_coll_module_t;
+
+#define MX_NB_SLOTS(X)                                                                                    \
+    X(iallreduce) X(ireduce) X(ireduce_scatter) X(ireduce_scatter_block) X(iscan) X(iexscan) X(iallgather) \
+    X(ibcast) X(allreduce_init) X(reduce_init) X(reduce_scatter_init) X(reduce_scatter_block_init)        \
+    X(scan_init) X(exscan_init) X(allgather_init) X(bcast_init)
 
 static int map_rc(int rc)
 {
@@ -82,6 +115,9 @@ static void coll_module_destruct(void *obj)
     if (m->prev_reduce_scatter_block_module) MX_OBJ_RELEASE(m->prev_reduce_scatter_block_module);
     if (m->prev_scan_module) MX_OBJ_RELEASE(m->prev_scan_module);
     if (m->prev_exscan_module) MX_OBJ_RELEASE(m->prev_exscan_module);
+#define MX_RELEASE_PREV(name) if (m->prev_##name##_module) MX_OBJ_RELEASE(m->prev_##name##_module);
+    MX_NB_SLOTS(MX_RELEASE_PREV)
+#undef MX_RELEASE_PREV
     free(m);
 }
 
@@ -270,6 +306,383 @@ static int mx_coll_exscan(const void *sbuf, void *rbuf, int count, struct ompi_d
     return rc != 1 ? rc : m->prev_exscan(sbuf, rbuf, count, dtype, op, comm, m->prev_exscan_module);
 }
 
+/* ---- nonblocking and persistent slots ------------------
+ * A device-path request is an mx_request_t (include/mx_coll.h) wrapped in a
+ * host ompi_request_t; active ones sit on a list that the progress callback
+ * (registered once, like libnbc's) polls with mx_test and completes.  The
+ * GPU needs no host progress: polling only reports completion. */
+typedef struct mx_coll_req {
+    struct ompi_request_t *req;
+    mx_request_t *mx;
+    struct mx_coll_req *next;
+    int active;
+} mx_coll_req_t;
+
+static mx_coll_req_t *g_active;
+static int g_progress_registered;
+
+static int mx_coll_progress(void)
+{
+    int completed = 0;
+    mx_coll_req_t **pp = &g_active;
+    while (*pp) {
+        mx_coll_req_t *r = *pp;
+        int flag = 0;
+        const int rc = mx_test(r->mx, &flag);
+        if (flag || rc != MX_SUCCESS) {
+            *pp = r->next;
+            r->active = 0;
+            mx_ompi_host->request_complete(r->req, map_rc(rc));
+            completed++;
+        } else {
+            pp = &r->next;
+        }
+    }
+    return completed;
+}
+
+static void activate(mx_coll_req_t *r)
+{
+    r->active = 1;
+    r->next = g_active;
+    g_active = r;
+}
+
+static void deactivate(mx_coll_req_t *r)
+{
+    for (mx_coll_req_t **pp = &g_active; *pp; pp = &(*pp)->next)
+        if (*pp == r) { *pp = r->next; break; }
+    r->active = 0;
+}
+
+static int req_start_cb(struct ompi_request_t *req)     /* MPI_Start */
+{
+    mx_coll_req_t *r = (mx_coll_req_t *)mx_ompi_host->request_ctx(req);
+    const int rc = mx_start(r->mx);
+    if (rc != MX_SUCCESS) return map_rc(rc);
+    mx_ompi_host->request_activate(req);
+    activate(r);
+    return OMPI_SUCCESS;
+}
+
+static int req_free_cb(struct ompi_request_t *req)      /* MPI_Request_free */
+{
+    mx_coll_req_t *r = (mx_coll_req_t *)mx_ompi_host->request_ctx(req);
+    if (r->active) deactivate(r);
+    const int rc = mx_request_free(r->mx);   /* lets an active operation finish */
+    free(r);
+    return map_rc(rc);
+}
+
+/* wrap an mx request (rc from its creation) into *request; returns 1 when
+ * the call should be delegated instead */
+static int post(int rc, mx_request_t *mxr, int persistent, struct ompi_request_t **request, int *ret)
+{
+    if (rc == MX_ERR_UNSUPPORTED || rc == MX_ERR_NOMEM) return 1;
+    if (rc != MX_SUCCESS) { *ret = map_rc(rc); return 0; }
+    mx_coll_req_t *r = calloc(1, sizeof *r);
+    if (r) r->req = mx_ompi_host->request_create(persistent, req_start_cb, req_free_cb, r);
+    if (!r || !r->req) {
+        mx_request_free(mxr);
+        free(r);
+        *ret = OMPI_ERR_OUT_OF_RESOURCE;
+        return 0;
+    }
+    r->mx = mxr;
+    if (!g_progress_registered) {
+        mx_ompi_host->progress_register(mx_coll_progress);
+        g_progress_registered = 1;
+    }
+    if (!persistent) activate(r);
+    *request = r->req;
+    *ret = OMPI_SUCCESS;
+    return 0;
+}
+
+/* coll_mi355x_<name>_algorithm, defaulting to coll_libnbc_<name>_algorithm */
+static int nbc_alg(const char *name)
+{
+    char a[96], b[96];
+    snprintf(a, sizeof a, "coll_mi355x_%s_algorithm", name);
+    snprintf(b, sizeof b, "coll_libnbc_%s_algorithm", name);
+    return mx_ompi_host->mca_int(a, mx_ompi_host->mca_int(b, 0));
+}
+
+static int allreduce_like(mx_coll_module_t *m, const void *sbuf, void *rbuf, int count, struct ompi_datatype_t *dtype,
+                          struct ompi_op_t *op, int persistent, struct ompi_request_t **request, int *ret)
+{
+    int slot, opi;
+    mx_request_t *q = NULL;
+    if (!reducible(m, dtype, op, count, &slot, &opi) || !(sbuf == MPI_IN_PLACE || on_device(sbuf)) ||
+        !on_device(rbuf))
+        return 1;
+    const void *sb = sbuf == MPI_IN_PLACE ? MX_IN_PLACE : sbuf;
+    const int alg = nbc_alg("iallreduce");
+    const int rc = persistent ? mx_allreduce_init(m->mx, sb, rbuf, (size_t)count, slot, opi, alg, NULL, &q)
+                              : mx_iallreduce(m->mx, sb, rbuf, (size_t)count, slot, opi, alg, NULL, &q);
+    return post(rc, q, persistent, request, ret);
+}
+
+static int mx_coll_iallreduce(const void *sbuf, void *rbuf, int count, struct ompi_datatype_t *dtype,
+                              struct ompi_op_t *op, struct ompi_communicator_t *comm, struct ompi_request_t **request,
+                              mca_coll_base_module_t *module)
+{
+    mx_coll_module_t *m = (mx_coll_module_t *)module;
+    int ret;
+    if (!allreduce_like(m, sbuf, rbuf, count, dtype, op, 0, request, &ret)) return ret;
+    return m->prev_iallreduce(sbuf, rbuf, count, dtype, op, comm, request, m->prev_iallreduce_module);
+}
+
+static int mx_coll_allreduce_init(const void *sbuf, void *rbuf, int count, struct ompi_datatype_t *dtype,
+                                  struct ompi_op_t *op, struct ompi_communicator_t *comm, struct ompi_info_t *info,
+                                  struct ompi_request_t **request, mca_coll_base_module_t *module)
+{
+    mx_coll_module_t *m = (mx_coll_module_t *)module;
+    int ret;
+    if (!allreduce_like(m, sbuf, rbuf, count, dtype, op, 1, request, &ret)) return ret;
+    return m->prev_allreduce_init(sbuf, rbuf, count, dtype, op, comm, info, request,
+                                  m->prev_allreduce_init_module);
+}
+
+static int reduce_like(mx_coll_module_t *m, const void *sbuf, void *rbuf, int count, struct ompi_datatype_t *dtype,
+                       struct ompi_op_t *op, int root, struct ompi_communicator_t *comm, int persistent,
+                       struct ompi_request_t **request, int *ret)
+{
+    const int rank = mx_ompi_host->comm_rank(comm);
+    int slot, opi;
+    mx_request_t *q = NULL;
+    if (!reducible(m, dtype, op, count, &slot, &opi) || !(sbuf == MPI_IN_PLACE ? rank == root : on_device(sbuf)) ||
+        (rank == root && !on_device(rbuf)))
+        return 1;
+    const void *sb = sbuf == MPI_IN_PLACE ? MX_IN_PLACE : sbuf;
+    void *rb = rank == root ? rbuf : NULL;
+    const int alg = nbc_alg("ireduce");
+    const int rc = persistent ? mx_reduce_init(m->mx, sb, rb, (size_t)count, slot, opi, root, alg, NULL, &q)
+                              : mx_ireduce(m->mx, sb, rb, (size_t)count, slot, opi, root, alg, NULL, &q);
+    return post(rc, q, persistent, request, ret);
+}
+
+static int mx_coll_ireduce(const void *sbuf, void *rbuf, int count, struct ompi_datatype_t *dtype, struct ompi_op_t *op,
+                           int root, struct ompi_communicator_t *comm, struct ompi_request_t **request,
+                           mca_coll_base_module_t *module)
+{
+    mx_coll_module_t *m = (mx_coll_module_t *)module;
+    int ret;
+    if (!reduce_like(m, sbuf, rbuf, count, dtype, op, root, comm, 0, request, &ret)) return ret;
+    return m->prev_ireduce(sbuf, rbuf, count, dtype, op, root, comm, request, m->prev_ireduce_module);
+}
+
+static int mx_coll_reduce_init(const void *sbuf, void *rbuf, int count, struct ompi_datatype_t *dtype,
+                               struct ompi_op_t *op, int root, struct ompi_communicator_t *comm,
+                               struct ompi_info_t *info, struct ompi_request_t **request,
+                               mca_coll_base_module_t *module)
+{
+    mx_coll_module_t *m = (mx_coll_module_t *)module;
+    int ret;
+    if (!reduce_like(m, sbuf, rbuf, count, dtype, op, root, comm, 1, request, &ret)) return ret;
+    return m->prev_reduce_init(sbuf, rbuf, count, dtype, op, root, comm, info, request, m->prev_reduce_init_module);
+}
+
+/* rcounts == NULL: the _block form with `rcount` per rank */
+static int rs_like(mx_coll_module_t *m, const void *sbuf, void *rbuf, const int *rcounts, int rcount,
+                   struct ompi_datatype_t *dtype, struct ompi_op_t *op, struct ompi_communicator_t *comm,
+                   int persistent, struct ompi_request_t **request, int *ret)
+{
+    const int n = mx_ompi_host->comm_size(comm);
+    size_t rc64[MX_MAX_RANKS];
+    int total = 0, slot, opi;
+    mx_request_t *q = NULL;
+    if (n > MX_MAX_RANKS) return 1;
+    for (int i = 0; i < n; i++) { rc64[i] = (size_t)(rcounts ? rcounts[i] : rcount); total += (int)rc64[i]; }
+    if (!reducible(m, dtype, op, total, &slot, &opi) || !(sbuf == MPI_IN_PLACE || on_device(sbuf)) ||
+        !on_device(rbuf))
+        return 1;
+    const void *sb = sbuf == MPI_IN_PLACE ? MX_IN_PLACE : sbuf;
+    int rc;
+    if (rcounts)
+        rc = persistent ? mx_reduce_scatter_init(m->mx, sb, rbuf, rc64, slot, opi, NULL, &q)
+                        : mx_ireduce_scatter(m->mx, sb, rbuf, rc64, slot, opi, NULL, &q);
+    else
+        rc = persistent ? mx_reduce_scatter_block_init(m->mx, sb, rbuf, (size_t)rcount, slot, opi, NULL, &q)
+                        : mx_ireduce_scatter_block(m->mx, sb, rbuf, (size_t)rcount, slot, opi, NULL, &q);
+    return post(rc, q, persistent, request, ret);
+}
+
+static int mx_coll_ireduce_scatter(const void *sbuf, void *rbuf, const int *rcounts, struct ompi_datatype_t *dtype,
+                                   struct ompi_op_t *op, struct ompi_communicator_t *comm,
+                                   struct ompi_request_t **request, mca_coll_base_module_t *module)
+{
+    mx_coll_module_t *m = (mx_coll_module_t *)module;
+    int ret;
+    if (!rs_like(m, sbuf, rbuf, rcounts, 0, dtype, op, comm, 0, request, &ret)) return ret;
+    return m->prev_ireduce_scatter(sbuf, rbuf, rcounts, dtype, op, comm, request, m->prev_ireduce_scatter_module);
+}
+
+static int mx_coll_reduce_scatter_init(const void *sbuf, void *rbuf, const int *rcounts,
+                                       struct ompi_datatype_t *dtype, struct ompi_op_t *op,
+                                       struct ompi_communicator_t *comm, struct ompi_info_t *info,
+                                       struct ompi_request_t **request, mca_coll_base_module_t *module)
+{
+    mx_coll_module_t *m = (mx_coll_module_t *)module;
+    int ret;
+    if (!rs_like(m, sbuf, rbuf, rcounts, 0, dtype, op, comm, 1, request, &ret)) return ret;
+    return m->prev_reduce_scatter_init(sbuf, rbuf, rcounts, dtype, op, comm, info, request,
+                                       m->prev_reduce_scatter_init_module);
+}
+
+static int mx_coll_ireduce_scatter_block(const void *sbuf, void *rbuf, int rcount, struct ompi_datatype_t *dtype,
+                                         struct ompi_op_t *op, struct ompi_communicator_t *comm,
+                                         struct ompi_request_t **request, mca_coll_base_module_t *module)
+{
+    mx_coll_module_t *m = (mx_coll_module_t *)module;
+    int ret;
+    if (!rs_like(m, sbuf, rbuf, NULL, rcount, dtype, op, comm, 0, request, &ret)) return ret;
+    return m->prev_ireduce_scatter_block(sbuf, rbuf, rcount, dtype, op, comm, request,
+                                         m->prev_ireduce_scatter_block_module);
+}
+
+static int mx_coll_reduce_scatter_block_init(const void *sbuf, void *rbuf, int rcount, struct ompi_datatype_t *dtype,
+                                             struct ompi_op_t *op, struct ompi_communicator_t *comm,
+                                             struct ompi_info_t *info, struct ompi_request_t **request,
+                                             mca_coll_base_module_t *module)
+{
+    mx_coll_module_t *m = (mx_coll_module_t *)module;
+    int ret;
+    if (!rs_like(m, sbuf, rbuf, NULL, rcount, dtype, op, comm, 1, request, &ret)) return ret;
+    return m->prev_reduce_scatter_block_init(sbuf, rbuf, rcount, dtype, op, comm, info, request,
+                                             m->prev_reduce_scatter_block_init_module);
+}
+
+static int scan_like(mx_coll_module_t *m, const void *sbuf, void *rbuf, int count, struct ompi_datatype_t *dtype,
+                     struct ompi_op_t *op, int exclusive, int persistent, struct ompi_request_t **request, int *ret)
+{
+    int slot, opi, rc;
+    mx_request_t *q = NULL;
+    if (!reducible(m, dtype, op, count, &slot, &opi) || !(sbuf == MPI_IN_PLACE || on_device(sbuf)) ||
+        !on_device(rbuf))
+        return 1;
+    const void *sb = sbuf == MPI_IN_PLACE ? MX_IN_PLACE : sbuf;
+    const int alg = nbc_alg(exclusive ? "iexscan" : "iscan");
+    if (exclusive)
+        rc = persistent ? mx_exscan_init(m->mx, sb, rbuf, (size_t)count, slot, opi, alg, NULL, &q)
+                        : mx_iexscan(m->mx, sb, rbuf, (size_t)count, slot, opi, alg, NULL, &q);
+    else
+        rc = persistent ? mx_scan_init(m->mx, sb, rbuf, (size_t)count, slot, opi, alg, NULL, &q)
+                        : mx_iscan(m->mx, sb, rbuf, (size_t)count, slot, opi, alg, NULL, &q);
+    return post(rc, q, persistent, request, ret);
+}
+
+static int mx_coll_iscan(const void *sbuf, void *rbuf, int count, struct ompi_datatype_t *dtype, struct ompi_op_t *op,
+                         struct ompi_communicator_t *comm, struct ompi_request_t **request,
+                         mca_coll_base_module_t *module)
+{
+    mx_coll_module_t *m = (mx_coll_module_t *)module;
+    int ret;
+    if (!scan_like(m, sbuf, rbuf, count, dtype, op, 0, 0, request, &ret)) return ret;
+    return m->prev_iscan(sbuf, rbuf, count, dtype, op, comm, request, m->prev_iscan_module);
+}
+
+static int mx_coll_iexscan(const void *sbuf, void *rbuf, int count, struct ompi_datatype_t *dtype,
+                           struct ompi_op_t *op, struct ompi_communicator_t *comm, struct ompi_request_t **request,
+                           mca_coll_base_module_t *module)
+{
+    mx_coll_module_t *m = (mx_coll_module_t *)module;
+    int ret;
+    if (!scan_like(m, sbuf, rbuf, count, dtype, op, 1, 0, request, &ret)) return ret;
+    return m->prev_iexscan(sbuf, rbuf, count, dtype, op, comm, request, m->prev_iexscan_module);
+}
+
+static int mx_coll_scan_init(const void *sbuf, void *rbuf, int count, struct ompi_datatype_t *dtype,
+                             struct ompi_op_t *op, struct ompi_communicator_t *comm, struct ompi_info_t *info,
+                             struct ompi_request_t **request, mca_coll_base_module_t *module)
+{
+    mx_coll_module_t *m = (mx_coll_module_t *)module;
+    int ret;
+    if (!scan_like(m, sbuf, rbuf, count, dtype, op, 0, 1, request, &ret)) return ret;
+    return m->prev_scan_init(sbuf, rbuf, count, dtype, op, comm, info, request, m->prev_scan_init_module);
+}
+
+static int mx_coll_exscan_init(const void *sbuf, void *rbuf, int count, struct ompi_datatype_t *dtype,
+                               struct ompi_op_t *op, struct ompi_communicator_t *comm, struct ompi_info_t *info,
+                               struct ompi_request_t **request, mca_coll_base_module_t *module)
+{
+    mx_coll_module_t *m = (mx_coll_module_t *)module;
+    int ret;
+    if (!scan_like(m, sbuf, rbuf, count, dtype, op, 1, 1, request, &ret)) return ret;
+    return m->prev_exscan_init(sbuf, rbuf, count, dtype, op, comm, info, request, m->prev_exscan_init_module);
+}
+
+static int allgather_like(mx_coll_module_t *m, const void *sbuf, int scount, struct ompi_datatype_t *sdtype,
+                          void *rbuf, int rcount, struct ompi_datatype_t *rdtype, struct ompi_communicator_t *comm,
+                          int persistent, struct ompi_request_t **request, int *ret)
+{
+    const size_t rbytes = (size_t)rcount * mx_ompi_host->dtype_size(rdtype);
+    const int n = mx_ompi_host->comm_size(comm);
+    mx_request_t *q = NULL;
+    if (!m->mx || !rbytes || !on_device(rbuf) || !mx_ompi_host->dtype_contiguous(rdtype, rcount * n) ||
+        !(sbuf == MPI_IN_PLACE ||
+          (on_device(sbuf) && mx_ompi_host->dtype_contiguous(sdtype, scount) &&
+           (size_t)scount * mx_ompi_host->dtype_size(sdtype) == rbytes)))
+        return 1;
+    const void *sb = sbuf == MPI_IN_PLACE ? MX_IN_PLACE : sbuf;
+    const int rc = persistent ? mx_allgather_init(m->mx, sb, rbuf, rbytes, NULL, &q)
+                              : mx_iallgather(m->mx, sb, rbuf, rbytes, NULL, &q);
+    return post(rc, q, persistent, request, ret);
+}
+
+static int mx_coll_iallgather(const void *sbuf, int scount, struct ompi_datatype_t *sdtype, void *rbuf, int rcount,
+                              struct ompi_datatype_t *rdtype, struct ompi_communicator_t *comm,
+                              struct ompi_request_t **request, mca_coll_base_module_t *module)
+{
+    mx_coll_module_t *m = (mx_coll_module_t *)module;
+    int ret;
+    if (!allgather_like(m, sbuf, scount, sdtype, rbuf, rcount, rdtype, comm, 0, request, &ret)) return ret;
+    return m->prev_iallgather(sbuf, scount, sdtype, rbuf, rcount, rdtype, comm, request, m->prev_iallgather_module);
+}
+
+static int mx_coll_allgather_init(const void *sbuf, int scount, struct ompi_datatype_t *sdtype, void *rbuf,
+                                  int rcount, struct ompi_datatype_t *rdtype, struct ompi_communicator_t *comm,
+                                  struct ompi_info_t *info, struct ompi_request_t **request,
+                                  mca_coll_base_module_t *module)
+{
+    mx_coll_module_t *m = (mx_coll_module_t *)module;
+    int ret;
+    if (!allgather_like(m, sbuf, scount, sdtype, rbuf, rcount, rdtype, comm, 1, request, &ret)) return ret;
+    return m->prev_allgather_init(sbuf, scount, sdtype, rbuf, rcount, rdtype, comm, info, request,
+                                  m->prev_allgather_init_module);
+}
+
+static int bcast_like(mx_coll_module_t *m, void *buf, int count, struct ompi_datatype_t *dtype, int root,
+                      int persistent, struct ompi_request_t **request, int *ret)
+{
+    const size_t bytes = (size_t)count * mx_ompi_host->dtype_size(dtype);
+    mx_request_t *q = NULL;
+    if (!m->mx || !bytes || !on_device(buf) || !mx_ompi_host->dtype_contiguous(dtype, count)) return 1;
+    const int rc = persistent ? mx_bcast_init(m->mx, buf, bytes, root, NULL, &q)
+                              : mx_ibcast(m->mx, buf, bytes, root, NULL, &q);
+    return post(rc, q, persistent, request, ret);
+}
+
+static int mx_coll_ibcast(void *buf, int count, struct ompi_datatype_t *dtype, int root,
+                          struct ompi_communicator_t *comm, struct ompi_request_t **request,
+                          mca_coll_base_module_t *module)
+{
+    mx_coll_module_t *m = (mx_coll_module_t *)module;
+    int ret;
+    if (!bcast_like(m, buf, count, dtype, root, 0, request, &ret)) return ret;
+    return m->prev_ibcast(buf, count, dtype, root, comm, request, m->prev_ibcast_module);
+}
+
+static int mx_coll_bcast_init(void *buf, int count, struct ompi_datatype_t *dtype, int root,
+                              struct ompi_communicator_t *comm, struct ompi_info_t *info,
+                              struct ompi_request_t **request, mca_coll_base_module_t *module)
+{
+    mx_coll_module_t *m = (mx_coll_module_t *)module;
+    int ret;
+    if (!bcast_like(m, buf, count, dtype, root, 1, request, &ret)) return ret;
+    return m->prev_bcast_init(buf, count, dtype, root, comm, info, request, m->prev_bcast_init_module);
+}
+
 /* ---- module enable / component query ------------------------------------ */
 
 #define SAVE_PREV(m, comm, name, type)                                                              \
@@ -297,6 +710,19 @@ static int mx_coll_module_enable(mca_coll_base_module_t *module, struct ompi_com
         SAVE_PREV(m, comm, exscan, mca_coll_base_module_exscan_fn_t);
     }
     if (m->super.coll_reduce_local) SAVE_PREV(m, comm, reduce_local, mca_coll_base_module_reduce_local_fn_t);
+    /* nonblocking / persistent: take a slot only where a lower module
+     * (coll/libnbc) provides it for delegation; mca_coll_base_comm_select
+     * copies the slots after enable, so a cleared one stays theirs */
+#define SAVE_PREV_OPT(name)                                                                         \
+    if (m->super.coll_##name) {                                                                     \
+        mca_coll_base_module_t *pm_ = NULL;                                                         \
+        m->prev_##name = (__typeof__(m->prev_##name))mx_ompi_host->comm_coll_fn(comm, #name, &pm_); \
+        m->prev_##name##_module = pm_;                                                              \
+        if (m->prev_##name && pm_) MX_OBJ_RETAIN(pm_);                                              \
+        else { m->prev_##name = NULL; m->prev_##name##_module = NULL; m->super.coll_##name = NULL; } \
+    }
+    MX_NB_SLOTS(SAVE_PREV_OPT)
+#undef SAVE_PREV_OPT
     if (m->super.coll_allreduce && n > 1 && n <= MX_MAX_RANKS) {
         const size_t staging = (size_t)mx_ompi_host->mca_int("coll_mi355x_staging_mb", 1024) << 20;
         int flags = MX_COMM_IPC;
@@ -335,6 +761,9 @@ static mca_coll_base_module_t *mx_coll_component_comm_query(struct ompi_communic
         m->super.coll_reduce_scatter_block = mx_coll_reduce_scatter_block;
         m->super.coll_scan = mx_coll_scan;
         m->super.coll_exscan = mx_coll_exscan;
+#define SET_NB(name) m->super.coll_##name = mx_coll_##name;
+        MX_NB_SLOTS(SET_NB)
+#undef SET_NB
     } else {
         /* size-1 comms (MPI_COMM_SELF): MPI_Reduce_local lands here when
          * our priority beats coll/self's 75 (coll_self_module.c:60,84) */

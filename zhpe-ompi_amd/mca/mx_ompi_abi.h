@@ -13,7 +13,8 @@
  *   ompi_op_base_component_1_0_0_t     ompi/mca/op/op.h:331-341
  *   mca_coll_base_module_2_3_0_t       ompi/mca/coll/coll.h:504-604
  *   mca_coll_base_component_2_0_0_t    ompi/mca/coll/coll.h:471-481
- *   slot typedefs                      ompi/mca/coll/coll.h:195-250, 440-443
+ *   slot typedefs                      ompi/mca/coll/coll.h:195-250, 261-420, 440-443
+ *   request services                   ompi/request/request.h:125-139, 436-
  *
  * Building against a real Open MPI tree: compile the components with
  * -DMX_OMPI_REAL and the Open MPI include paths; this header then includes
@@ -51,6 +52,7 @@ struct ompi_datatype_t;
 struct ompi_op_t;
 struct ompi_communicator_t;
 struct ompi_request_t;
+struct ompi_info_t;
 
 /* ---- opal_object_t (non-debug) ------------------------------------------- */
 typedef struct mx_obj_class {
@@ -161,6 +163,49 @@ typedef int (*mca_coll_base_module_scan_fn_t)(const void *sbuf, void *rbuf, int 
                                               struct ompi_op_t *op, struct ompi_communicator_t *comm,
                                               mca_coll_base_module_t *module);
 typedef mca_coll_base_module_scan_fn_t mca_coll_base_module_exscan_fn_t;
+/* nonblocking (coll.h:261-338) and persistent (:339-420: + MPI_Info) */
+#define MX_NB_ARGS struct ompi_communicator_t *comm, struct ompi_request_t **request, mca_coll_base_module_t *module
+#define MX_PI_ARGS struct ompi_communicator_t *comm, struct ompi_info_t *info, struct ompi_request_t **request, \
+                   mca_coll_base_module_t *module
+typedef int (*mca_coll_base_module_iallgather_fn_t)(const void *sbuf, int scount, struct ompi_datatype_t *sdtype,
+                                                    void *rbuf, int rcount, struct ompi_datatype_t *rdtype,
+                                                    MX_NB_ARGS);
+typedef int (*mca_coll_base_module_iallreduce_fn_t)(const void *sbuf, void *rbuf, int count,
+                                                    struct ompi_datatype_t *dtype, struct ompi_op_t *op, MX_NB_ARGS);
+typedef int (*mca_coll_base_module_ibcast_fn_t)(void *buff, int count, struct ompi_datatype_t *datatype, int root,
+                                                MX_NB_ARGS);
+typedef int (*mca_coll_base_module_ireduce_fn_t)(const void *sbuf, void *rbuf, int count,
+                                                 struct ompi_datatype_t *dtype, struct ompi_op_t *op, int root,
+                                                 MX_NB_ARGS);
+typedef int (*mca_coll_base_module_ireduce_scatter_fn_t)(const void *sbuf, void *rbuf, const int *rcounts,
+                                                         struct ompi_datatype_t *dtype, struct ompi_op_t *op,
+                                                         MX_NB_ARGS);
+typedef int (*mca_coll_base_module_ireduce_scatter_block_fn_t)(const void *sbuf, void *rbuf, int rcount,
+                                                               struct ompi_datatype_t *dtype, struct ompi_op_t *op,
+                                                               MX_NB_ARGS);
+typedef int (*mca_coll_base_module_iscan_fn_t)(const void *sbuf, void *rbuf, int count, struct ompi_datatype_t *dtype,
+                                               struct ompi_op_t *op, MX_NB_ARGS);
+typedef mca_coll_base_module_iscan_fn_t mca_coll_base_module_iexscan_fn_t;
+typedef int (*mca_coll_base_module_allgather_init_fn_t)(const void *sbuf, int scount,
+                                                        struct ompi_datatype_t *sdtype, void *rbuf, int rcount,
+                                                        struct ompi_datatype_t *rdtype, MX_PI_ARGS);
+typedef int (*mca_coll_base_module_allreduce_init_fn_t)(const void *sbuf, void *rbuf, int count,
+                                                        struct ompi_datatype_t *dtype, struct ompi_op_t *op,
+                                                        MX_PI_ARGS);
+typedef int (*mca_coll_base_module_bcast_init_fn_t)(void *buff, int count, struct ompi_datatype_t *datatype,
+                                                    int root, MX_PI_ARGS);
+typedef int (*mca_coll_base_module_reduce_init_fn_t)(const void *sbuf, void *rbuf, int count,
+                                                     struct ompi_datatype_t *dtype, struct ompi_op_t *op, int root,
+                                                     MX_PI_ARGS);
+typedef int (*mca_coll_base_module_reduce_scatter_init_fn_t)(const void *sbuf, void *rbuf, const int *rcounts,
+                                                             struct ompi_datatype_t *dtype, struct ompi_op_t *op,
+                                                             MX_PI_ARGS);
+typedef int (*mca_coll_base_module_reduce_scatter_block_init_fn_t)(const void *sbuf, void *rbuf, int rcount,
+                                                                   struct ompi_datatype_t *dtype,
+                                                                   struct ompi_op_t *op, MX_PI_ARGS);
+typedef int (*mca_coll_base_module_scan_init_fn_t)(const void *sbuf, void *rbuf, int count,
+                                                   struct ompi_datatype_t *dtype, struct ompi_op_t *op, MX_PI_ARGS);
+typedef mca_coll_base_module_scan_init_fn_t mca_coll_base_module_exscan_init_fn_t;
 typedef int (*mca_coll_base_module_ft_event_fn_t)(int state);
 typedef void *mx_coll_slot_unused_t;   /* slots this component never fills */
 
@@ -181,14 +226,31 @@ struct mca_coll_base_module_2_3_0_t {
     mca_coll_base_module_scan_fn_t coll_scan;
     mx_coll_slot_unused_t coll_scatter, coll_scatterv;
     /* nonblocking (17) */
-    mx_coll_slot_unused_t coll_iallgather, coll_iallgatherv, coll_iallreduce, coll_ialltoall, coll_ialltoallv,
-        coll_ialltoallw, coll_ibarrier, coll_ibcast, coll_iexscan, coll_igather, coll_igatherv, coll_ireduce,
-        coll_ireduce_scatter, coll_ireduce_scatter_block, coll_iscan, coll_iscatter, coll_iscatterv;
+    mca_coll_base_module_iallgather_fn_t coll_iallgather;
+    mx_coll_slot_unused_t coll_iallgatherv;
+    mca_coll_base_module_iallreduce_fn_t coll_iallreduce;
+    mx_coll_slot_unused_t coll_ialltoall, coll_ialltoallv, coll_ialltoallw, coll_ibarrier;
+    mca_coll_base_module_ibcast_fn_t coll_ibcast;
+    mca_coll_base_module_iexscan_fn_t coll_iexscan;
+    mx_coll_slot_unused_t coll_igather, coll_igatherv;
+    mca_coll_base_module_ireduce_fn_t coll_ireduce;
+    mca_coll_base_module_ireduce_scatter_fn_t coll_ireduce_scatter;
+    mca_coll_base_module_ireduce_scatter_block_fn_t coll_ireduce_scatter_block;
+    mca_coll_base_module_iscan_fn_t coll_iscan;
+    mx_coll_slot_unused_t coll_iscatter, coll_iscatterv;
     /* persistent (17) */
-    mx_coll_slot_unused_t coll_allgather_init, coll_allgatherv_init, coll_allreduce_init, coll_alltoall_init,
-        coll_alltoallv_init, coll_alltoallw_init, coll_barrier_init, coll_bcast_init, coll_exscan_init,
-        coll_gather_init, coll_gatherv_init, coll_reduce_init, coll_reduce_scatter_init,
-        coll_reduce_scatter_block_init, coll_scan_init, coll_scatter_init, coll_scatterv_init;
+    mca_coll_base_module_allgather_init_fn_t coll_allgather_init;
+    mx_coll_slot_unused_t coll_allgatherv_init;
+    mca_coll_base_module_allreduce_init_fn_t coll_allreduce_init;
+    mx_coll_slot_unused_t coll_alltoall_init, coll_alltoallv_init, coll_alltoallw_init, coll_barrier_init;
+    mca_coll_base_module_bcast_init_fn_t coll_bcast_init;
+    mca_coll_base_module_exscan_init_fn_t coll_exscan_init;
+    mx_coll_slot_unused_t coll_gather_init, coll_gatherv_init;
+    mca_coll_base_module_reduce_init_fn_t coll_reduce_init;
+    mca_coll_base_module_reduce_scatter_init_fn_t coll_reduce_scatter_init;
+    mca_coll_base_module_reduce_scatter_block_init_fn_t coll_reduce_scatter_block_init;
+    mca_coll_base_module_scan_init_fn_t coll_scan_init;
+    mx_coll_slot_unused_t coll_scatter_init, coll_scatterv_init;
     /* neighborhood (5 + 5 nonblocking + 5 persistent) */
     mx_coll_slot_unused_t coll_neighbor_allgather, coll_neighbor_allgatherv, coll_neighbor_alltoall,
         coll_neighbor_alltoallv, coll_neighbor_alltoallw;
@@ -237,6 +299,25 @@ typedef struct mx_ompi_host {
     int (*mca_int)(const char *name, int def);
     /* the MPI_BYTE datatype handle (ompi_mpi_byte) for bootstrap exchanges */
     struct ompi_datatype_t *byte_dtype;
+    /* ---- requests of the nonblocking / persistent slots ----
+     * request_create: OBJ_NEW of the component's ompi_request_t subclass +
+     *   OMPI_REQUEST_INIT(req, persistent) with req_type OMPI_REQUEST_COLL,
+     *   req_start / req_free set to the given callbacks and `ctx` stored in
+     *   the subclass (coll_libnbc_component.c:570-583 does the same);
+     *   persistent requests start inactive (OMPI_REQUEST_INACTIVE), others
+     *   active (OMPI_REQUEST_ACTIVE, REQUEST_PENDING);
+     * request_ctx: the subclass field;
+     * request_activate: MPI_Start's part of req_start -- req_state = ACTIVE,
+     *   req_complete = REQUEST_PENDING;
+     * request_complete: req_status.MPI_ERROR = status;
+     *   ompi_request_complete(req, true) (request.h:436-);
+     * progress_register: opal_progress_register (opal/runtime/opal_progress.h). */
+    struct ompi_request_t *(*request_create)(int persistent, int (*start)(struct ompi_request_t *req),
+                                             int (*free_fn)(struct ompi_request_t *req), void *ctx);
+    void *(*request_ctx)(struct ompi_request_t *req);
+    void (*request_activate)(struct ompi_request_t *req);
+    void (*request_complete)(struct ompi_request_t *req, int status);
+    int (*progress_register)(int (*fn)(void));
 } mx_ompi_host_t;
 
 /* Set by the host before component queries. */

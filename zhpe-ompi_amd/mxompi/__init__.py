@@ -171,6 +171,9 @@ REDUCE_SCATTER = {"auto": 0, "nonoverlapping": 1, "recursive_halving": 2, "ring"
 REDUCE = {"auto": 0, "linear": 1, "chain": 2, "pipeline": 3, "binary": 4, "binomial": 5,
           "in_order_binary": 6, "rabenseifner": 7}
 SCAN = {"auto": 0, "linear": 1, "recursive_doubling": 2}
+# libnbc numbering (coll_libnbc_component.c:58-92)
+IALLREDUCE = {"auto": 0, "ring": 1, "binomial": 2, "rabenseifner": 3, "recursive_doubling": 4}
+IREDUCE = {"auto": 0, "chain": 1, "binomial": 2, "rabenseifner": 3}
 
 class CollStats(ctypes.Structure):
     _fields_ = [("calls", ctypes.c_uint64), ("fold_launches", ctypes.c_uint64), ("fold_ms", ctypes.c_double),
@@ -210,6 +213,30 @@ def _coll_lib():
         for name in ("mx_scan", "mx_exscan", "mx_reduce_scatter_block"):
             getattr(L, name).argtypes = [vp, vp, vp, sz, i, i, i, vp]
             getattr(L, name + "_local").argtypes = [vp, pp, pp, sz, i, i, i, vp]
+        # non-blocking / persistent
+        rq = ctypes.POINTER(vp)
+        for name in ("mx_iallreduce", "mx_allreduce_init", "mx_iscan", "mx_scan_init", "mx_iexscan",
+                     "mx_exscan_init"):
+            getattr(L, name).argtypes = [vp, vp, vp, sz, i, i, i, vp, rq]
+        for name in ("mx_ireduce", "mx_reduce_init"):
+            getattr(L, name).argtypes = [vp, vp, vp, sz, i, i, i, i, vp, rq]
+        for name in ("mx_ireduce_scatter", "mx_reduce_scatter_init"):
+            getattr(L, name).argtypes = [vp, vp, vp, ctypes.POINTER(sz), i, i, vp, rq]
+        for name in ("mx_ireduce_scatter_block", "mx_reduce_scatter_block_init"):
+            getattr(L, name).argtypes = [vp, vp, vp, sz, i, i, vp, rq]
+        for name in ("mx_iallgather", "mx_allgather_init"):
+            getattr(L, name).argtypes = [vp, vp, vp, sz, vp, rq]
+        for name in ("mx_ibcast", "mx_bcast_init"):
+            getattr(L, name).argtypes = [vp, vp, sz, i, vp, rq]
+        L.mx_start.argtypes = [vp]
+        L.mx_startall.argtypes = [sz, pp]
+        L.mx_test.argtypes = [vp, ctypes.POINTER(i)]
+        L.mx_wait.argtypes = [vp]
+        L.mx_request_stream_wait.argtypes = [vp, vp]
+        L.mx_request_is_active.argtypes = [vp]
+        L.mx_request_free.argtypes = [vp]
+        L.mx_iallreduce_decision.argtypes = [i, sz, i, i]
+        L.mx_ireduce_decision.argtypes = [i, sz, i]
         L._mx_coll_typed = True
     return L
 
@@ -223,6 +250,58 @@ def _ptrs(seq):
 
 def _alg(table, a):
     return table[a] if isinstance(a, str) else int(a)
+
+
+class Request:
+    """A non-blocking or persistent collective (include/mx_coll.h requests):
+    MPI_Test / MPI_Wait / MPI_Start / MPI_Request_free."""
+
+    def __init__(self, handle, persistent, keep=()):
+        self.h = handle
+        self.persistent = persistent
+        self._keep = keep          # ctypes arrays the request reads at start
+
+    def start(self):
+        check(_coll_lib().mx_start(self.h), "mx_start")
+
+    def test(self) -> bool:
+        flag = ctypes.c_int(0)
+        check(_coll_lib().mx_test(self.h, ctypes.byref(flag)), "mx_test")
+        return bool(flag.value)
+
+    def wait(self):
+        check(_coll_lib().mx_wait(self.h), "mx_wait")
+
+    def stream_wait(self, stream=0):
+        check(_coll_lib().mx_request_stream_wait(self.h, stream or None), "mx_request_stream_wait")
+
+    @property
+    def active(self) -> bool:
+        return bool(_coll_lib().mx_request_is_active(self.h))
+
+    def free(self):
+        if getattr(self, "h", None):
+            h, self.h = self.h, None
+            check(_coll_lib().mx_request_free(h), "mx_request_free")
+
+    def __del__(self):
+        try:
+            self.free()
+        except Exception:  # noqa: BLE001
+            pass
+
+
+def startall(reqs):
+    arr = _ptrs([r.h for r in reqs])
+    check(_coll_lib().mx_startall(len(reqs), arr), "mx_startall")
+
+
+def iallreduce_decision(n, count, t, inplace=False):
+    return _coll_lib().mx_iallreduce_decision(n, count, _slot(t), 1 if inplace else 0)
+
+
+def ireduce_decision(n, count, t):
+    return _coll_lib().mx_ireduce_decision(n, count, _slot(t))
 
 
 class Comm:
@@ -328,6 +407,45 @@ class Comm:
     def reduce_scatter_block(self, sbuf, rbuf, rcount, t, op, alg="auto", stream=0):
         check(_coll_lib().mx_reduce_scatter_block(self.h, sbuf, rbuf, rcount, _slot(t), _op(op),
                                                   _alg(REDUCE, alg), stream or None), "mx_reduce_scatter_block")
+
+    # -- non-blocking (persistent=True: MPI-4 *_init, started with .start()) --
+    def _req(self, name, persistent, *args, keep=()):
+        h = ctypes.c_void_p()
+        check(getattr(_coll_lib(), name)(self.h, *args, ctypes.byref(h)), name)
+        return Request(h, persistent, keep)
+
+    def iallreduce(self, sbuf, rbuf, count, t, op, alg="auto", stream=0, persistent=False):
+        return self._req("mx_allreduce_init" if persistent else "mx_iallreduce", persistent, sbuf, rbuf, count,
+                         _slot(t), _op(op), _alg(IALLREDUCE, alg), stream or None)
+
+    def ireduce(self, sbuf, rbuf, count, t, op, root, alg="auto", stream=0, persistent=False):
+        return self._req("mx_reduce_init" if persistent else "mx_ireduce", persistent, sbuf, rbuf or None, count,
+                         _slot(t), _op(op), root, _alg(IREDUCE, alg), stream or None)
+
+    def iscan(self, sbuf, rbuf, count, t, op, alg="auto", stream=0, persistent=False):
+        return self._req("mx_scan_init" if persistent else "mx_iscan", persistent, sbuf, rbuf, count, _slot(t),
+                         _op(op), _alg(SCAN, alg), stream or None)
+
+    def iexscan(self, sbuf, rbuf, count, t, op, alg="auto", stream=0, persistent=False):
+        return self._req("mx_exscan_init" if persistent else "mx_iexscan", persistent, sbuf, rbuf, count,
+                         _slot(t), _op(op), _alg(SCAN, alg), stream or None)
+
+    def ireduce_scatter(self, sbuf, rbuf, rcounts, t, op, stream=0, persistent=False):
+        rc = (ctypes.c_size_t * len(rcounts))(*rcounts)
+        return self._req("mx_reduce_scatter_init" if persistent else "mx_ireduce_scatter", persistent, sbuf, rbuf,
+                         rc, _slot(t), _op(op), stream or None, keep=(rc,))
+
+    def ireduce_scatter_block(self, sbuf, rbuf, rcount, t, op, stream=0, persistent=False):
+        return self._req("mx_reduce_scatter_block_init" if persistent else "mx_ireduce_scatter_block", persistent,
+                         sbuf, rbuf, rcount, _slot(t), _op(op), stream or None)
+
+    def iallgather(self, sbuf, rbuf, nbytes, stream=0, persistent=False):
+        return self._req("mx_allgather_init" if persistent else "mx_iallgather", persistent, sbuf, rbuf, nbytes,
+                         stream or None)
+
+    def ibcast(self, buf, nbytes, root, stream=0, persistent=False):
+        return self._req("mx_bcast_init" if persistent else "mx_ibcast", persistent, buf, nbytes, root,
+                         stream or None)
 
     # -- local (all ranks in this process) ---------------------------------
     def allreduce_local(self, sbufs, rbufs, count, t, op, alg="auto", stream=0):
