@@ -46,6 +46,19 @@ def host(with_components=True):
     H.mxh_reduce_scatter_block.argtypes = [vp, vp, ci, vp, vp, vp]
     H.mxh_scan.argtypes = [vp, vp, ci, vp, vp, vp]
     H.mxh_exscan.argtypes = [vp, vp, ci, vp, vp, vp]
+    rq = ctypes.POINTER(vp)
+    for name in ("mxh_iallreduce", "mxh_allreduce_init", "mxh_iscan", "mxh_iexscan"):
+        getattr(H, name).argtypes = [vp, vp, ci, vp, vp, vp, rq]
+    H.mxh_ireduce.argtypes = [vp, vp, ci, vp, vp, ci, vp, rq]
+    H.mxh_reduce_init.argtypes = [vp, vp, ci, vp, vp, ci, vp, rq]
+    H.mxh_ireduce_scatter.argtypes = [vp, vp, ctypes.POINTER(ci), vp, vp, vp, rq]
+    H.mxh_ireduce_scatter_block.argtypes = [vp, vp, ci, vp, vp, vp, rq]
+    H.mxh_iallgather.argtypes = [vp, ci, vp, vp, ci, vp, vp, rq]
+    H.mxh_ibcast.argtypes = [vp, ci, vp, ci, vp, rq]
+    H.mxh_start.argtypes = [vp]
+    H.mxh_test.argtypes = [rq, ctypes.POINTER(ci)]
+    H.mxh_wait.argtypes = [rq]
+    H.mxh_request_free.argtypes = [rq]
     O = oracle_lib.oracle()
     base = ctypes.cast(O.mxo_reduce2, vp)
     pat = ctypes.cast(O.mxo_supported, vp)

@@ -10,6 +10,11 @@
 * GPU (n processes sharing the one GPU): device buffers go through
   coll/mi355x -> mx_* all-peer path and must be bit-identical to the
   coll/tuned algorithm the oracle restates.
+* Nonblocking and persistent forms (MPI_Iallreduce, MPI_Ireduce, MPI_Iscan,
+  MPI_Iexscan, MPI_Ireduce_scatter_block posted together, then MPI_Test /
+  MPI_Wait; MPI_Allreduce_init + MPI_Start twice): host buffers stay with
+  the host base module (libnbc's role), device buffers go through
+  coll/mi355x's requests and must match coll/libnbc's orders.
 """
 import ctypes
 import os
@@ -61,7 +66,8 @@ def _worker(rank, n, port, use_gpu, q):
         comm = H.mxh_comm_create(rank, n, ag, None)
         owners = {s: H.mxh_comm_slot_owner(comm, s.encode()).decode()
                   for s in ("allreduce", "reduce", "scan", "exscan", "reduce_scatter_block", "reduce_scatter",
-                            "allgather", "bcast")}
+                            "allgather", "bcast", "iallreduce", "ireduce", "iscan", "iexscan",
+                            "ireduce_scatter_block", "allreduce_init")}
         f32, i32 = minihost.dtype(H, "MPI_FLOAT"), minihost.dtype(H, "MPI_INT")
         SUM, MAX = minihost.op(H, "MPI_SUM"), minihost.op(H, "MPI_MAX")
         res = {"owners": owners}
@@ -97,6 +103,44 @@ def _worker(rank, n, port, use_gpu, q):
             R = out_like(xb, 300)
             assert H.mxh_reduce_scatter_block(XB.data_ptr(), R.data_ptr(), 300, dt, op, comm) == 0
             res[("rsb", kind, op == MAX)] = R.cpu().numpy().tobytes()
+            # nonblocking: post five, then complete them (one by MPI_Test polling)
+            outs, reqs = {}, []
+            for what in ("allreduce", "reduce", "scan", "exscan", "rsb"):
+                R = out_like(xb, 300) if what == "rsb" else out_like(x)
+                r = vp()
+                if what == "allreduce":
+                    rc = H.mxh_iallreduce(X.data_ptr(), R.data_ptr(), count, dt, op, comm, ctypes.byref(r))
+                elif what == "reduce":
+                    rc = H.mxh_ireduce(X.data_ptr(), R.data_ptr(), count, dt, op, n - 1, comm, ctypes.byref(r))
+                elif what == "rsb":
+                    rc = H.mxh_ireduce_scatter_block(XB.data_ptr(), R.data_ptr(), 300, dt, op, comm, ctypes.byref(r))
+                else:
+                    fn = H.mxh_iscan if what == "scan" else H.mxh_iexscan
+                    rc = fn(X.data_ptr(), R.data_ptr(), count, dt, op, comm, ctypes.byref(r))
+                assert rc == 0, (what, rc)
+                outs[what] = R
+                reqs.append(r)
+            flag = ci(0)
+            while not flag.value:
+                assert H.mxh_test(ctypes.byref(reqs[0]), ctypes.byref(flag)) == 0
+            assert reqs[0].value is None                      # MPI_REQUEST_NULL after completion
+            for r in reqs[1:]:
+                assert H.mxh_wait(ctypes.byref(r)) == 0
+                assert r.value is None
+            for what, R in outs.items():
+                res[("i" + what, kind, op == MAX)] = R.cpu().numpy().tobytes()
+            # persistent: MPI_Allreduce_init, started twice
+            P, R = vp(), out_like(x)
+            assert H.mxh_allreduce_init(X.data_ptr(), R.data_ptr(), count, dt, op, comm, ctypes.byref(P)) == 0
+            flag = ci(0)
+            assert H.mxh_test(ctypes.byref(P), ctypes.byref(flag)) == 0 and flag.value   # inactive
+            for _ in range(2):
+                R.zero_()
+                assert H.mxh_start(P) == 0
+                assert H.mxh_wait(ctypes.byref(P)) == 0
+                assert P.value is not None                    # persistent requests survive MPI_Wait
+            res[("pallreduce", kind, op == MAX)] = R.cpu().numpy().tobytes()
+            assert H.mxh_request_free(ctypes.byref(P)) == 0
         if use_gpu:
             torch.cuda.synchronize()
         H.mxh_comm_free(comm)
@@ -157,6 +201,51 @@ def _expected(n, kind, is_max, what, alg_of):
     return exp
 
 
+def _expected_nbc(n, kind, is_max, what):
+    """coll/libnbc's orders (oracle restatement) for the nonblocking forms."""
+    import mxompi
+    import test_nbc_oracle
+    L = test_nbc_oracle._L()
+    t = "INT32_T" if kind == "int" else "FLOAT"
+    op = mxompi.OP["MAX" if is_max else "SUM"]
+    ty = mxompi.TYPE[t]
+    count = 5003 if what != "rsb" else 300 * n
+    xs = [_gen(kind, count, r) for r in range(n)]
+    sp = (vp * n)(*[x.ctypes.data for x in xs])
+    if what == "allreduce":
+        exp = [np.zeros_like(xs[0]) for _ in range(n)]
+        assert L.mxo_iallreduce(0, op, ty, n, count, sp, (vp * n)(*[e.ctypes.data for e in exp])) == 0
+        return exp
+    if what == "reduce":
+        e = np.zeros_like(xs[0])
+        assert L.mxo_ireduce(0, op, ty, n, count, n - 1, sp, e.ctypes.data) == 0
+        return {n - 1: e}
+    if what == "rsb":
+        exp = [np.zeros(300, xs[0].dtype) for _ in range(n)]
+        assert L.mxo_ireduce_scatter(op, ty, n, (sz * n)(*([300] * n)), sp,
+                                     (vp * n)(*[e.ctypes.data for e in exp])) == 0
+        return exp
+    return _expected(n, kind, is_max, what, lambda w: 1)     # libnbc scan / exscan: linear == coll/basic
+
+
+def _check_nb(n, got, gpu):
+    import golden_io
+    import mxompi
+    for kind in ("int", "flt"):
+        for is_max in ((False,) if kind == "int" else (False, True)):
+            for what in ("allreduce", "reduce", "scan", "exscan", "rsb", "pallreduce"):
+                base = "allreduce" if what == "pallreduce" else what
+                exp = _expected_nbc(n, kind, is_max, base) if gpu else _expected(n, kind, is_max, base, lambda w: 1)
+                key = (what if what == "pallreduce" else "i" + what, kind, is_max)
+                items = exp.items() if isinstance(exp, dict) else enumerate(exp)
+                for r, e in items:
+                    g = np.frombuffer(got[r][key], e.dtype)
+                    golden_io.assert_coll_equal(g.view(np.uint8), e.view(np.uint8),
+                                                mxompi.OP["MAX" if is_max else "SUM"],
+                                                mxompi.TYPE["INT32_T" if kind == "int" else "FLOAT"],
+                                                f"{key} rank {r}")
+
+
 def _check(n, got, alg_of, bitexact_fp):
     import golden_io
     import mxompi
@@ -187,6 +276,7 @@ def test_multirank_host_buffers_gloo_cpu(n):
     # linear (rbuf = x_{n-1}; op= x_i), linear scan / exscan, RSB = linear
     # reduce + scatter: bit-identical to the oracle's linear algorithms
     _check(n, got, lambda w: 1, bitexact_fp=True)
+    _check_nb(n, got, gpu=False)
 
 
 @pytest.mark.gpu
@@ -203,3 +293,4 @@ def test_multirank_device_buffers_through_components(n):
     def alg_of(what):
         return 0       # coll/tuned fixed decisions (the oracle's alg 0)
     _check(n, got, alg_of, bitexact_fp=True)
+    _check_nb(n, got, gpu=True)

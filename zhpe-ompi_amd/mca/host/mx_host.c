@@ -162,9 +162,16 @@ static int mca_int(const char *name, int def)
 }
 
 /* ---- communicators --------------------------------------------------------- */
-#define NSLOTS 9
-static const char *g_slot_names[NSLOTS] = {"allreduce", "reduce_scatter", "allgather", "bcast", "reduce_local",
-                                           "reduce", "reduce_scatter_block", "scan", "exscan"};
+#define NSLOTS 25
+static const char *g_slot_names[NSLOTS] = {
+    "allreduce", "reduce_scatter", "allgather", "bcast", "reduce_local", "reduce", "reduce_scatter_block", "scan",
+    "exscan",
+    /* nonblocking (coll.h:534-550) and persistent (:553-569) */
+    "iallreduce", "ireduce", "ireduce_scatter", "ireduce_scatter_block", "iscan", "iexscan", "iallgather", "ibcast",
+    "allreduce_init", "reduce_init", "reduce_scatter_init", "reduce_scatter_block_init", "scan_init", "exscan_init",
+    "allgather_init", "bcast_init"};
+enum { S_IALLREDUCE = 9, S_IREDUCE, S_IREDUCE_SCATTER, S_IREDUCE_SCATTER_BLOCK, S_ISCAN, S_IEXSCAN, S_IALLGATHER,
+       S_IBCAST, S_PERSISTENT0 };
 
 struct ompi_communicator_t {
     int rank, size;
@@ -204,6 +211,47 @@ static ompi_op_base_op_fns_t *op_fns(struct ompi_op_t *op) { return &op->intrins
 static ompi_op_base_op_3buff_fns_t *op_3fns(struct ompi_op_t *op) { return &op->o_3buff_intrinsic; }
 
 static mx_ompi_host_t g_host;
+
+/* ---- requests (ompi/request/request.h:125-139) and progress -------------- */
+struct ompi_request_t {
+    int persistent, active, complete, status;
+    int (*start)(struct ompi_request_t *req);
+    int (*free_fn)(struct ompi_request_t *req);
+    void *ctx;
+};
+
+static struct ompi_request_t *request_create(int persistent, int (*start)(struct ompi_request_t *),
+                                             int (*free_fn)(struct ompi_request_t *), void *ctx)
+{
+    struct ompi_request_t *r = calloc(1, sizeof *r);
+    if (!r) return NULL;
+    r->persistent = persistent;
+    r->active = !persistent;          /* OMPI_REQUEST_INACTIVE until MPI_Start */
+    r->complete = persistent;         /* an inactive request tests complete */
+    r->start = start;
+    r->free_fn = free_fn;
+    r->ctx = ctx;
+    return r;
+}
+static void *request_ctx(struct ompi_request_t *r) { return r->ctx; }
+static void request_activate(struct ompi_request_t *r) { r->active = 1; r->complete = 0; r->status = 0; }
+static void request_complete(struct ompi_request_t *r, int status) { r->status = status; r->complete = 1; }
+
+#define MAXPROGRESS 8
+static int (*g_progress[MAXPROGRESS])(void);
+static int g_nprogress;
+static int progress_register(int (*fn)(void))        /* opal_progress_register */
+{
+    for (int i = 0; i < g_nprogress; i++)
+        if (g_progress[i] == fn) return 0;
+    if (g_nprogress == MAXPROGRESS) return -1;
+    g_progress[g_nprogress++] = fn;
+    return 0;
+}
+static void opal_progress(void)
+{
+    for (int i = 0; i < g_nprogress; i++) g_progress[i]();
+}
 
 /* ompi_op_reduce (op.h:547-610) */
 static void op_reduce(struct ompi_op_t *op, const void *source, void *target, int count, struct ompi_datatype_t *dt)
@@ -340,6 +388,179 @@ static int base_reduce_local(const void *in, void *inout, int count, struct ompi
     return OMPI_SUCCESS;
 }
 
+/* nonblocking / persistent stand-ins for coll/libnbc on host buffers: the
+ * blocking base algorithm runs at post (or MPI_Start) time and the request
+ * is complete at once */
+typedef struct {
+    int slot;
+    const void *sbuf;
+    void *rbuf;
+    int count, scount, root;
+    int *rcounts;
+    struct ompi_datatype_t *dt, *rdt;
+    struct ompi_op_t *op;
+    struct ompi_communicator_t *c;
+} base_nb_t;
+
+static int base_nb_run(const base_nb_t *a)
+{
+    switch (a->slot) {
+    case S_IALLREDUCE: return base_allreduce(a->sbuf, a->rbuf, a->count, a->dt, a->op, a->c, NULL);
+    case S_IREDUCE: return base_reduce(a->sbuf, a->rbuf, a->count, a->dt, a->op, a->root, a->c, NULL);
+    case S_IREDUCE_SCATTER: return base_reduce_scatter(a->sbuf, a->rbuf, a->rcounts, a->dt, a->op, a->c, NULL);
+    case S_IREDUCE_SCATTER_BLOCK: return base_reduce_scatter_block(a->sbuf, a->rbuf, a->count, a->dt, a->op, a->c, NULL);
+    case S_ISCAN: return base_scan(a->sbuf, a->rbuf, a->count, a->dt, a->op, a->c, NULL);
+    case S_IEXSCAN: return base_exscan(a->sbuf, a->rbuf, a->count, a->dt, a->op, a->c, NULL);
+    case S_IALLGATHER: return base_allgather(a->sbuf, a->scount, a->dt, a->rbuf, a->count, a->rdt, a->c, NULL);
+    case S_IBCAST: return base_bcast(a->rbuf, a->count, a->dt, a->root, a->c, NULL);
+    }
+    return OMPI_ERROR;
+}
+static int base_nb_start(struct ompi_request_t *r)
+{
+    request_activate(r);
+    request_complete(r, base_nb_run(r->ctx));
+    return OMPI_SUCCESS;
+}
+static int base_nb_free(struct ompi_request_t *r)
+{
+    base_nb_t *a = r->ctx;
+    free(a->rcounts);
+    free(a);
+    return OMPI_SUCCESS;
+}
+static int base_nb_post(const base_nb_t *a, int persistent, struct ompi_request_t **request)
+{
+    base_nb_t *h = malloc(sizeof *h);
+    if (!h) return OMPI_ERR_OUT_OF_RESOURCE;
+    *h = *a;
+    if (a->rcounts) {
+        h->rcounts = malloc(sizeof(int) * (size_t)a->c->size);
+        if (!h->rcounts) { free(h); return OMPI_ERR_OUT_OF_RESOURCE; }
+        memcpy(h->rcounts, a->rcounts, sizeof(int) * (size_t)a->c->size);
+    }
+    *request = request_create(persistent, base_nb_start, base_nb_free, h);
+    if (!*request) { free(h->rcounts); free(h); return OMPI_ERR_OUT_OF_RESOURCE; }
+    if (!persistent) request_complete(*request, base_nb_run(h));
+    return OMPI_SUCCESS;
+}
+#define NB(...) base_nb_t a_ = {__VA_ARGS__}
+static int base_iallreduce(const void *sbuf, void *rbuf, int count, struct ompi_datatype_t *dt, struct ompi_op_t *op,
+                           struct ompi_communicator_t *c, struct ompi_request_t **req, mca_coll_base_module_t *m)
+{
+    (void)m;
+    NB(.slot = S_IALLREDUCE, .sbuf = sbuf, .rbuf = rbuf, .count = count, .dt = dt, .op = op, .c = c);
+    return base_nb_post(&a_, 0, req);
+}
+static int base_allreduce_init(const void *sbuf, void *rbuf, int count, struct ompi_datatype_t *dt,
+                               struct ompi_op_t *op, struct ompi_communicator_t *c, struct ompi_info_t *info,
+                               struct ompi_request_t **req, mca_coll_base_module_t *m)
+{
+    (void)m; (void)info;
+    NB(.slot = S_IALLREDUCE, .sbuf = sbuf, .rbuf = rbuf, .count = count, .dt = dt, .op = op, .c = c);
+    return base_nb_post(&a_, 1, req);
+}
+static int base_ireduce(const void *sbuf, void *rbuf, int count, struct ompi_datatype_t *dt, struct ompi_op_t *op,
+                        int root, struct ompi_communicator_t *c, struct ompi_request_t **req, mca_coll_base_module_t *m)
+{
+    (void)m;
+    NB(.slot = S_IREDUCE, .sbuf = sbuf, .rbuf = rbuf, .count = count, .dt = dt, .op = op, .root = root, .c = c);
+    return base_nb_post(&a_, 0, req);
+}
+static int base_reduce_init(const void *sbuf, void *rbuf, int count, struct ompi_datatype_t *dt, struct ompi_op_t *op,
+                            int root, struct ompi_communicator_t *c, struct ompi_info_t *info,
+                            struct ompi_request_t **req, mca_coll_base_module_t *m)
+{
+    (void)m; (void)info;
+    NB(.slot = S_IREDUCE, .sbuf = sbuf, .rbuf = rbuf, .count = count, .dt = dt, .op = op, .root = root, .c = c);
+    return base_nb_post(&a_, 1, req);
+}
+static int base_ireduce_scatter(const void *sbuf, void *rbuf, const int *rcounts, struct ompi_datatype_t *dt,
+                                struct ompi_op_t *op, struct ompi_communicator_t *c, struct ompi_request_t **req,
+                                mca_coll_base_module_t *m)
+{
+    (void)m;
+    NB(.slot = S_IREDUCE_SCATTER, .sbuf = sbuf, .rbuf = rbuf, .rcounts = (int *)rcounts, .dt = dt, .op = op, .c = c);
+    return base_nb_post(&a_, 0, req);
+}
+static int base_reduce_scatter_init(const void *sbuf, void *rbuf, const int *rcounts, struct ompi_datatype_t *dt,
+                                    struct ompi_op_t *op, struct ompi_communicator_t *c, struct ompi_info_t *info,
+                                    struct ompi_request_t **req, mca_coll_base_module_t *m)
+{
+    (void)m; (void)info;
+    NB(.slot = S_IREDUCE_SCATTER, .sbuf = sbuf, .rbuf = rbuf, .rcounts = (int *)rcounts, .dt = dt, .op = op, .c = c);
+    return base_nb_post(&a_, 1, req);
+}
+static int base_ireduce_scatter_block(const void *sbuf, void *rbuf, int rcount, struct ompi_datatype_t *dt,
+                                      struct ompi_op_t *op, struct ompi_communicator_t *c, struct ompi_request_t **req,
+                                      mca_coll_base_module_t *m)
+{
+    (void)m;
+    NB(.slot = S_IREDUCE_SCATTER_BLOCK, .sbuf = sbuf, .rbuf = rbuf, .count = rcount, .dt = dt, .op = op, .c = c);
+    return base_nb_post(&a_, 0, req);
+}
+static int base_reduce_scatter_block_init(const void *sbuf, void *rbuf, int rcount, struct ompi_datatype_t *dt,
+                                          struct ompi_op_t *op, struct ompi_communicator_t *c,
+                                          struct ompi_info_t *info, struct ompi_request_t **req,
+                                          mca_coll_base_module_t *m)
+{
+    (void)m; (void)info;
+    NB(.slot = S_IREDUCE_SCATTER_BLOCK, .sbuf = sbuf, .rbuf = rbuf, .count = rcount, .dt = dt, .op = op, .c = c);
+    return base_nb_post(&a_, 1, req);
+}
+#define BASE_SCAN_NB(fname, SLOT)                                                                               \
+    static int base_i##fname(const void *sbuf, void *rbuf, int count, struct ompi_datatype_t *dt,               \
+                             struct ompi_op_t *op, struct ompi_communicator_t *c, struct ompi_request_t **req,  \
+                             mca_coll_base_module_t *m)                                                        \
+    {                                                                                                           \
+        (void)m;                                                                                                \
+        NB(.slot = SLOT, .sbuf = sbuf, .rbuf = rbuf, .count = count, .dt = dt, .op = op, .c = c);             \
+        return base_nb_post(&a_, 0, req);                                                                       \
+    }                                                                                                           \
+    static int base_##fname##_init(const void *sbuf, void *rbuf, int count, struct ompi_datatype_t *dt,         \
+                                   struct ompi_op_t *op, struct ompi_communicator_t *c, struct ompi_info_t *info, \
+                                   struct ompi_request_t **req, mca_coll_base_module_t *m)                     \
+    {                                                                                                           \
+        (void)m; (void)info;                                                                                    \
+        NB(.slot = SLOT, .sbuf = sbuf, .rbuf = rbuf, .count = count, .dt = dt, .op = op, .c = c);             \
+        return base_nb_post(&a_, 1, req);                                                                       \
+    }
+BASE_SCAN_NB(scan, S_ISCAN)
+BASE_SCAN_NB(exscan, S_IEXSCAN)
+static int base_iallgather(const void *sbuf, int scount, struct ompi_datatype_t *sdt, void *rbuf, int rcount,
+                           struct ompi_datatype_t *rdt, struct ompi_communicator_t *c, struct ompi_request_t **req,
+                           mca_coll_base_module_t *m)
+{
+    (void)m;
+    NB(.slot = S_IALLGATHER, .sbuf = sbuf, .scount = scount, .dt = sdt, .rbuf = rbuf, .count = rcount, .rdt = rdt,
+       .c = c);
+    return base_nb_post(&a_, 0, req);
+}
+static int base_allgather_init(const void *sbuf, int scount, struct ompi_datatype_t *sdt, void *rbuf, int rcount,
+                               struct ompi_datatype_t *rdt, struct ompi_communicator_t *c, struct ompi_info_t *info,
+                               struct ompi_request_t **req, mca_coll_base_module_t *m)
+{
+    (void)m; (void)info;
+    NB(.slot = S_IALLGATHER, .sbuf = sbuf, .scount = scount, .dt = sdt, .rbuf = rbuf, .count = rcount, .rdt = rdt,
+       .c = c);
+    return base_nb_post(&a_, 1, req);
+}
+static int base_ibcast(void *buf, int count, struct ompi_datatype_t *dt, int root, struct ompi_communicator_t *c,
+                       struct ompi_request_t **req, mca_coll_base_module_t *m)
+{
+    (void)m;
+    NB(.slot = S_IBCAST, .rbuf = buf, .count = count, .dt = dt, .root = root, .c = c);
+    return base_nb_post(&a_, 0, req);
+}
+static int base_bcast_init(void *buf, int count, struct ompi_datatype_t *dt, int root, struct ompi_communicator_t *c,
+                           struct ompi_info_t *info, struct ompi_request_t **req, mca_coll_base_module_t *m)
+{
+    (void)m; (void)info;
+    NB(.slot = S_IBCAST, .rbuf = buf, .count = count, .dt = dt, .root = root, .c = c);
+    return base_nb_post(&a_, 1, req);
+}
+#undef NB
+
 static mca_coll_base_module_t g_base_coll;   /* static, never freed */
 static mca_coll_base_module_t g_self_coll;
 
@@ -412,6 +633,13 @@ static int comm_select(struct ompi_communicator_t *c, int is_self)
         base->coll_reduce_scatter_block = base_reduce_scatter_block;
         base->coll_scan = base_scan;
         base->coll_exscan = base_exscan;
+#define SET_BASE_NB(name) base->coll_##name = base_##name;
+        SET_BASE_NB(iallreduce) SET_BASE_NB(ireduce) SET_BASE_NB(ireduce_scatter) SET_BASE_NB(ireduce_scatter_block)
+        SET_BASE_NB(iscan) SET_BASE_NB(iexscan) SET_BASE_NB(iallgather) SET_BASE_NB(ibcast)
+        SET_BASE_NB(allreduce_init) SET_BASE_NB(reduce_init) SET_BASE_NB(reduce_scatter_init)
+        SET_BASE_NB(reduce_scatter_block_init) SET_BASE_NB(scan_init) SET_BASE_NB(exscan_init)
+        SET_BASE_NB(allgather_init) SET_BASE_NB(bcast_init)
+#undef SET_BASE_NB
     }
     /* lowest priority first: the base module (30 / 75) */
 #define COPY(MOD, OWNER)                                                                             \
@@ -420,7 +648,15 @@ static int comm_select(struct ompi_communicator_t *c, int is_self)
                             (void *)(MOD)->coll_allgather, (void *)(MOD)->coll_bcast,                \
                             (void *)(MOD)->coll_reduce_local, (void *)(MOD)->coll_reduce,            \
                             (void *)(MOD)->coll_reduce_scatter_block, (void *)(MOD)->coll_scan,      \
-                            (void *)(MOD)->coll_exscan};                                             \
+                            (void *)(MOD)->coll_exscan, (void *)(MOD)->coll_iallreduce,              \
+                            (void *)(MOD)->coll_ireduce, (void *)(MOD)->coll_ireduce_scatter,        \
+                            (void *)(MOD)->coll_ireduce_scatter_block, (void *)(MOD)->coll_iscan,    \
+                            (void *)(MOD)->coll_iexscan, (void *)(MOD)->coll_iallgather,             \
+                            (void *)(MOD)->coll_ibcast, (void *)(MOD)->coll_allreduce_init,          \
+                            (void *)(MOD)->coll_reduce_init, (void *)(MOD)->coll_reduce_scatter_init, \
+                            (void *)(MOD)->coll_reduce_scatter_block_init,                           \
+                            (void *)(MOD)->coll_scan_init, (void *)(MOD)->coll_exscan_init,          \
+                            (void *)(MOD)->coll_allgather_init, (void *)(MOD)->coll_bcast_init};     \
         for (int i_ = 0; i_ < NSLOTS; i_++)                                                          \
             if (f_[i_]) { c->fn[i_] = f_[i_]; c->mod[i_] = (MOD); c->owner[i_] = (OWNER); }          \
     } while (0)
@@ -463,6 +699,12 @@ int mxh_init(const char *component_lib, mxh_reducer_t base, mxh_pattern_t patter
     g_host = (mx_ompi_host_t){comm_rank, comm_size, dtype_slot, dtype_size, dtype_contiguous, op_index, op_flags,
                               op_fns, op_3fns, comm_coll_fn, obj_retain, obj_release, mca_int, NULL};
     g_host.byte_dtype = mxh_dtype("MPI_BYTE");
+    g_host.request_create = request_create;
+    g_host.request_ctx = request_ctx;
+    g_host.request_activate = request_activate;
+    g_host.request_complete = request_complete;
+    g_host.progress_register = progress_register;
+    g_nprogress = 0;
     g_op_comp = NULL;
     g_coll_comp = NULL;
     if (component_lib && *component_lib) {
@@ -598,4 +840,125 @@ int mxh_exscan(const void *sbuf, void *rbuf, int count, void *dt, void *op, void
 {
     struct ompi_communicator_t *c = cv;
     return ((mca_coll_base_module_exscan_fn_t)c->fn[8])(sbuf, rbuf, count, dt, op, c, c->mod[8]);
+}
+
+/* ---- nonblocking / persistent entry points and request completion ------ */
+int mxh_iallreduce(const void *sbuf, void *rbuf, int count, void *dt, void *op, void *cv, void **req)
+{
+    struct ompi_communicator_t *c = cv;
+    struct ompi_datatype_t *d = dt;
+    if (!d || d->slot < 0 || !((struct ompi_op_t *)op)->intrinsic.fns[d->slot]) return -1;
+    return ((mca_coll_base_module_iallreduce_fn_t)c->fn[S_IALLREDUCE])(sbuf, rbuf, count, d, op, c,
+                                                                        (struct ompi_request_t **)req,
+                                                                        c->mod[S_IALLREDUCE]);
+}
+int mxh_allreduce_init(const void *sbuf, void *rbuf, int count, void *dt, void *op, void *cv, void **req)
+{
+    struct ompi_communicator_t *c = cv;
+    const int k = slot_index("allreduce_init");
+    return ((mca_coll_base_module_allreduce_init_fn_t)c->fn[k])(sbuf, rbuf, count, dt, op, c, NULL,
+                                                                 (struct ompi_request_t **)req, c->mod[k]);
+}
+int mxh_ireduce(const void *sbuf, void *rbuf, int count, void *dt, void *op, int root, void *cv, void **req)
+{
+    struct ompi_communicator_t *c = cv;
+    if (root < 0 || root >= c->size) return -1;
+    return ((mca_coll_base_module_ireduce_fn_t)c->fn[S_IREDUCE])(sbuf, rbuf, count, dt, op, root, c,
+                                                                  (struct ompi_request_t **)req, c->mod[S_IREDUCE]);
+}
+int mxh_reduce_init(const void *sbuf, void *rbuf, int count, void *dt, void *op, int root, void *cv, void **req)
+{
+    struct ompi_communicator_t *c = cv;
+    const int k = slot_index("reduce_init");
+    if (root < 0 || root >= c->size) return -1;
+    return ((mca_coll_base_module_reduce_init_fn_t)c->fn[k])(sbuf, rbuf, count, dt, op, root, c, NULL,
+                                                              (struct ompi_request_t **)req, c->mod[k]);
+}
+int mxh_ireduce_scatter(const void *sbuf, void *rbuf, const int *rcounts, void *dt, void *op, void *cv, void **req)
+{
+    struct ompi_communicator_t *c = cv;
+    return ((mca_coll_base_module_ireduce_scatter_fn_t)c->fn[S_IREDUCE_SCATTER])(
+        sbuf, rbuf, rcounts, dt, op, c, (struct ompi_request_t **)req, c->mod[S_IREDUCE_SCATTER]);
+}
+int mxh_ireduce_scatter_block(const void *sbuf, void *rbuf, int rcount, void *dt, void *op, void *cv, void **req)
+{
+    struct ompi_communicator_t *c = cv;
+    return ((mca_coll_base_module_ireduce_scatter_block_fn_t)c->fn[S_IREDUCE_SCATTER_BLOCK])(
+        sbuf, rbuf, rcount, dt, op, c, (struct ompi_request_t **)req, c->mod[S_IREDUCE_SCATTER_BLOCK]);
+}
+int mxh_iscan(const void *sbuf, void *rbuf, int count, void *dt, void *op, void *cv, void **req)
+{
+    struct ompi_communicator_t *c = cv;
+    return ((mca_coll_base_module_iscan_fn_t)c->fn[S_ISCAN])(sbuf, rbuf, count, dt, op, c,
+                                                              (struct ompi_request_t **)req, c->mod[S_ISCAN]);
+}
+int mxh_iexscan(const void *sbuf, void *rbuf, int count, void *dt, void *op, void *cv, void **req)
+{
+    struct ompi_communicator_t *c = cv;
+    return ((mca_coll_base_module_iexscan_fn_t)c->fn[S_IEXSCAN])(sbuf, rbuf, count, dt, op, c,
+                                                                  (struct ompi_request_t **)req, c->mod[S_IEXSCAN]);
+}
+int mxh_iallgather(const void *sbuf, int scount, void *sdt, void *rbuf, int rcount, void *rdt, void *cv, void **req)
+{
+    struct ompi_communicator_t *c = cv;
+    return ((mca_coll_base_module_iallgather_fn_t)c->fn[S_IALLGATHER])(
+        sbuf, scount, sdt, rbuf, rcount, rdt, c, (struct ompi_request_t **)req, c->mod[S_IALLGATHER]);
+}
+int mxh_ibcast(void *buf, int count, void *dt, int root, void *cv, void **req)
+{
+    struct ompi_communicator_t *c = cv;
+    return ((mca_coll_base_module_ibcast_fn_t)c->fn[S_IBCAST])(buf, count, dt, root, c,
+                                                                (struct ompi_request_t **)req, c->mod[S_IBCAST]);
+}
+
+/* MPI_Start (ompi/mpi/c/start.c: req->req_start) */
+int mxh_start(void *rv)
+{
+    struct ompi_request_t *r = rv;
+    if (!r || !r->persistent || r->active) return -1;
+    return r->start(r);
+}
+
+/* MPI_Test / MPI_Wait (ompi_request_default_test / _wait): drive
+ * opal_progress until complete; a completed nonblocking request is freed
+ * (set to MPI_REQUEST_NULL), a persistent one becomes inactive. */
+static int finish_request(void **rp)
+{
+    struct ompi_request_t *r = *rp;
+    const int st = r->status;
+    if (r->persistent) {
+        r->active = 0;
+    } else {
+        const int frc = r->free_fn(r);
+        free(r);
+        *rp = NULL;
+        if (st == OMPI_SUCCESS && frc != OMPI_SUCCESS) return frc;
+    }
+    return st;
+}
+int mxh_test(void **rp, int *flag)
+{
+    struct ompi_request_t *r = *rp;
+    *flag = 1;
+    if (!r || (r->persistent && !r->active)) return 0;
+    if (!r->complete) opal_progress();
+    if (!r->complete) { *flag = 0; return 0; }
+    return finish_request(rp);
+}
+int mxh_wait(void **rp)
+{
+    struct ompi_request_t *r = *rp;
+    if (!r || (r->persistent && !r->active)) return 0;
+    while (!r->complete) opal_progress();
+    return finish_request(rp);
+}
+/* MPI_Request_free (ompi/mpi/c/request_free.c -> req_free) */
+int mxh_request_free(void **rp)
+{
+    struct ompi_request_t *r = *rp;
+    if (!r) return 0;
+    const int rc = r->free_fn(r);
+    free(r);
+    *rp = NULL;
+    return rc;
 }

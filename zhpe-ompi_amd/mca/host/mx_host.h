@@ -9,8 +9,11 @@
  *     modules lowest -> highest priority, COPY each non-NULL slot;
  *   - the MPI entry points MPI_Reduce_local (reduce_local.c:46-91),
  *     MPI_Allreduce (allreduce.c:46-118), MPI_Reduce_scatter, MPI_Allgather,
- *     MPI_Bcast, MPI_Reduce, MPI_Reduce_scatter_block, MPI_Scan, MPI_Exscan:
- *     parameter checks + dispatch through comm->c_coll;
+ *     MPI_Bcast, MPI_Reduce, MPI_Reduce_scatter_block, MPI_Scan, MPI_Exscan
+ *     and their nonblocking / persistent forms: parameter checks + dispatch
+ *     through comm->c_coll;
+ *   - requests (ompi/request/request.h:125-139), opal_progress_register and
+ *     MPI_Start / MPI_Test / MPI_Wait / MPI_Request_free;
  *   - a host "base" coll module standing in for coll/tuned + basic on host
  *     buffers, and a coll/self-like module (priority 75) for COMM_SELF.
  * The base op functions and the host transport are injected by the test.
@@ -57,6 +60,25 @@ int mxh_reduce(const void *sbuf, void *rbuf, int count, void *dtype, void *op, i
 int mxh_reduce_scatter_block(const void *sbuf, void *rbuf, int rcount, void *dtype, void *op, void *comm);
 int mxh_scan(const void *sbuf, void *rbuf, int count, void *dtype, void *op, void *comm);
 int mxh_exscan(const void *sbuf, void *rbuf, int count, void *dtype, void *op, void *comm);
+/* nonblocking / persistent (MPI_I<coll>, MPI_<Coll>_init): *req receives
+ * the request; MPI_Start / MPI_Test / MPI_Wait / MPI_Request_free */
+int mxh_iallreduce(const void *sbuf, void *rbuf, int count, void *dtype, void *op, void *comm, void **req);
+int mxh_allreduce_init(const void *sbuf, void *rbuf, int count, void *dtype, void *op, void *comm, void **req);
+int mxh_ireduce(const void *sbuf, void *rbuf, int count, void *dtype, void *op, int root, void *comm, void **req);
+int mxh_reduce_init(const void *sbuf, void *rbuf, int count, void *dtype, void *op, int root, void *comm, void **req);
+int mxh_ireduce_scatter(const void *sbuf, void *rbuf, const int *rcounts, void *dtype, void *op, void *comm,
+                        void **req);
+int mxh_ireduce_scatter_block(const void *sbuf, void *rbuf, int rcount, void *dtype, void *op, void *comm,
+                              void **req);
+int mxh_iscan(const void *sbuf, void *rbuf, int count, void *dtype, void *op, void *comm, void **req);
+int mxh_iexscan(const void *sbuf, void *rbuf, int count, void *dtype, void *op, void *comm, void **req);
+int mxh_iallgather(const void *sbuf, int scount, void *sdtype, void *rbuf, int rcount, void *rdtype, void *comm,
+                   void **req);
+int mxh_ibcast(void *buf, int count, void *dtype, int root, void *comm, void **req);
+int mxh_start(void *req);
+int mxh_test(void **req, int *flag);
+int mxh_wait(void **req);
+int mxh_request_free(void **req);
 #define MXH_IN_PLACE ((void *)1)
 
 #ifdef __cplusplus
