@@ -301,6 +301,32 @@ int mx_shmem_reduce_heap(mx_heap_t *heap, int shmem_op, int shmem_type, size_t d
                          const void *source, size_t nreduce, int pe_start, int log_pe_stride,
                          int pe_size, void *stream);
 
+/* ---- one-sided accumulate on the symmetric heap ---------------------------
+ * MPI_Accumulate / MPI_Get_accumulate / MPI_Fetch_and_op /
+ * MPI_Compare_and_swap (osc/rdma: osc_rdma_accumulate.c:121-251, 770-1100;
+ * ompi_osc_base_sndrcv_op, osc_base_obj_convert.c:160-253) with the target
+ * at the symmetric address `target` of PE `pe`: target = origin OP target
+ * element-wise (ompi_op_reduce(op, origin, target)), op MX_OP_REPLACE /
+ * MX_OP_NO_OP included.  Accumulates to one PE are serialised by an
+ * exclusive device lock in that PE's heap (MPI's per-element atomicity);
+ * get_accumulate / fetch_and_op return the value before the update in
+ * `result` (local device memory).  Calls complete before returning. */
+int mx_accumulate(mx_heap_t *heap, const void *origin, size_t count, int type, int op, int pe, void *target,
+                  void *stream);
+int mx_get_accumulate(mx_heap_t *heap, const void *origin, void *result, size_t count, int type, int op, int pe,
+                      void *target, void *stream);
+int mx_fetch_and_op(mx_heap_t *heap, const void *origin, void *result, int type, int op, int pe, void *target,
+                    void *stream);
+int mx_compare_and_swap(mx_heap_t *heap, const void *origin, const void *compare, void *result, int type, int pe,
+                        void *target, void *stream);
+/* Derived datatypes (mx_convertor.h) on either side, NULL = contiguous
+ * elements of `type`; both sides hold the same number of `type` elements,
+ * matched in type-map order. */
+struct mx_ddt;
+int mx_accumulate_ddt(mx_heap_t *heap, const void *origin, size_t origin_count, const struct mx_ddt *origin_ddt,
+                      int type, int op, int pe, void *target, size_t target_count, const struct mx_ddt *target_ddt,
+                      void *stream);
+
 /* ---- local communicator: arrays of `size` buffers, one per rank --------- */
 int mx_allreduce_local(mx_comm_t *comm, const void *const *sbufs, void *const *rbufs,
                        size_t count, int type, int op, int alg, void *stream);

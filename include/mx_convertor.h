@@ -50,6 +50,9 @@ int mx_ddt_destroy(mx_ddt_t *ddt);
 size_t mx_ddt_size(const mx_ddt_t *ddt);            /* packed bytes per instance */
 int64_t mx_ddt_extent(const mx_ddt_t *ddt);         /* ub - lb                   */
 size_t mx_ddt_runs(const mx_ddt_t *ddt);            /* flattened strided runs    */
+/* [*lo, *hi): bytes relative to the user pointer that `count` instances
+ * touch (true lb .. true ub of the whole message). */
+int mx_ddt_span(const mx_ddt_t *ddt, size_t count, int64_t *lo, int64_t *hi);
 
 /* Pack bytes [offset, offset+len) of the packed stream of `count`
  * instances starting at `user` into `packed` (which receives exactly len

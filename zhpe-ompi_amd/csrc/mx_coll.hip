@@ -42,6 +42,7 @@
 #include <new>
 
 #include "mx_fold.hpp"
+#include "../../include/mx_convertor.h"
 
 namespace mx {
 
@@ -2787,4 +2788,195 @@ extern "C" int mx_shmem_reduce_heap(mx_heap_t *h, int sop, int st, size_t dt_siz
   }
   if ((rc = heap_sync(h, mask, s))) return rc;
   return finish(c, s);
+}
+
+// ---------------------------------------------------------------------------
+// One-sided accumulate on symmetric device memory.
+//
+// MPI_Accumulate / MPI_Get_accumulate / MPI_Fetch_and_op /
+// MPI_Compare_and_swap with a target in another GPU's symmetric heap.  The
+// reference's osc/rdma, without network atomics, takes the target's
+// accumulate lock, reads the target region, applies ompi_op_reduce(op,
+// origin, tmp) and writes it back (ompi_osc_rdma_gacc_contig,
+// osc_rdma_accumulate.c:188-251; the same process for a local target:
+// ompi_osc_rdma_gacc_local :121-168 -> ompi_osc_base_sndrcv_op,
+// osc_base_obj_convert.c:160-253).  Here the target region is directly
+// addressable over xGMI, so the op kernel itself (k_reduce2, in = origin,
+// inout = the mapped target) is the read-modify-write; an exclusive lock
+// word in the target heap's flag page (system-scope CAS from a one-thread
+// kernel, released after a system fence) serialises it against every other
+// accumulate on that PE, which is the MPI per-element atomicity guarantee.
+// Non-contiguous datatypes go through the convertor kernels: origin packed
+// once, target region gathered, combined element for element in type-map
+// order (what ompi_osc_base_sndrcv_op's paired iovec walk does), scattered
+// back -- all under the lock.  Every call completes before it returns (the
+// flush of osc/rdma folded into the call).
+// ---------------------------------------------------------------------------
+namespace mx {
+
+constexpr size_t kAccLockWord = 384;   // heap flag page: words 0..15 pair sequences, 256 signature
+
+__global__ void k_acc_lock(uint64_t *lock, uint64_t tag, uint64_t timeout_ticks, int *err) {
+  if (threadIdx.x == 0) {
+    const uint64_t t0 = wall_clock64();
+    uint64_t expect = 0;
+    while (!__hip_atomic_compare_exchange_strong(lock, &expect, tag, __ATOMIC_ACQUIRE, __ATOMIC_RELAXED,
+                                                 __HIP_MEMORY_SCOPE_SYSTEM)) {
+      expect = 0;
+      __builtin_amdgcn_s_sleep(4);
+      if (wall_clock64() - t0 > timeout_ticks) {
+        __hip_atomic_store(err, MX_ERR_TIMEOUT, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        break;
+      }
+    }
+  }
+  __atomic_thread_fence(__ATOMIC_ACQUIRE);
+}
+
+__global__ void k_acc_unlock(uint64_t *lock) {
+  if (threadIdx.x == 0) {
+    __threadfence_system();   // the target update is visible before the lock is free
+    __hip_atomic_store(lock, 0, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
+}
+
+// compare-and-swap of one element (osc_rdma_accumulate.c:170-186 semantics):
+// result = target; if (target == compare, bytewise) target = origin
+__global__ void k_cas_bytes(char *target, const char *compare, const char *origin, char *result, int es) {
+  if (threadIdx.x == 0) {
+    bool eq = true;
+    for (int i = 0; i < es; i++) {
+      const char t = target[i];
+      result[i] = t;
+      eq = eq && t == compare[i];
+    }
+    if (eq)
+      for (int i = 0; i < es; i++) target[i] = origin[i];
+  }
+}
+
+}  // namespace mx
+
+namespace {
+
+static uint64_t *acc_lock_word(mx_heap *h, int pe) {
+  return (pe == h->c->rank ? h->flags : h->peer_flags[pe]) + kAccLockWord;
+}
+
+static int acc_lock(mx_heap *h, int pe, hipStream_t s) {
+  hipLaunchKernelGGL(k_acc_lock, dim3(1), dim3(64), 0, s, acc_lock_word(h, pe), (uint64_t)h->c->rank + 1,
+                     h->c->timeout_ticks, h->c->err_dev);
+  return mx_check_launch();
+}
+
+static int acc_unlock(mx_heap *h, int pe, hipStream_t s) {
+  hipLaunchKernelGGL(k_acc_unlock, dim3(1), dim3(64), 0, s, acc_lock_word(h, pe));
+  return mx_check_launch();
+}
+
+static bool acc_op_ok(int op, int type) {
+  if (!mx_type_size(type)) return false;
+  return op == MX_OP_REPLACE || op == MX_OP_NO_OP || mx_op_supported(op, type, MX_TABLE_WITH_FORTRAN);
+}
+
+// target op= origin on `count` elements at `remote` (lock held)
+static int acc_apply(int op, int type, const void *origin, void *remote, size_t count, hipStream_t s) {
+  if (op == MX_OP_NO_OP || !count) return MX_SUCCESS;
+  if (op == MX_OP_REPLACE) return copy_async(remote, origin, count * mx_type_size(type), s);
+  return mx_reduce2(op, type, origin, remote, count, s);
+}
+
+static int acc_common(mx_heap *h, const void *origin, void *result, size_t count, int type, int op, int pe,
+                      void *target, void *stream) {
+  if (!h || pe < 0 || pe >= h->c->size || !target) return MX_ERR_ARG;
+  if (!acc_op_ok(op, type)) return MX_ERR_UNSUPPORTED;
+  const size_t es = mx_type_size(type);
+  if (!heap_has(h, target, count * es) || (!origin && op != MX_OP_NO_OP && count)) return MX_ERR_ARG;
+  void *remote = mx_shmem_ptr(h, target, pe);
+  if (!remote) return MX_ERR_ARG;
+  hipStream_t s = (hipStream_t)stream;
+  if (!count) return MX_SUCCESS;
+  int rc;
+  if ((rc = acc_lock(h, pe, s))) return rc;
+  if (result && (rc = copy_async(result, remote, count * es, s))) return rc;   // fetch the old value
+  if ((rc = acc_apply(op, type, origin, remote, count, s))) return rc;
+  if ((rc = acc_unlock(h, pe, s))) return rc;
+  return finish(h->c, s);
+}
+
+}  // namespace
+
+extern "C" int mx_accumulate(mx_heap_t *h, const void *origin, size_t count, int type, int op, int pe, void *target,
+                             void *stream) {
+  return acc_common(h, origin, nullptr, count, type, op, pe, target, stream);
+}
+
+extern "C" int mx_get_accumulate(mx_heap_t *h, const void *origin, void *result, size_t count, int type, int op,
+                                 int pe, void *target, void *stream) {
+  if (!result) return MX_ERR_ARG;
+  return acc_common(h, origin, result, count, type, op, pe, target, stream);
+}
+
+extern "C" int mx_fetch_and_op(mx_heap_t *h, const void *origin, void *result, int type, int op, int pe,
+                               void *target, void *stream) {
+  if (!result) return MX_ERR_ARG;
+  return acc_common(h, origin, result, 1, type, op, pe, target, stream);
+}
+
+extern "C" int mx_compare_and_swap(mx_heap_t *h, const void *origin, const void *compare, void *result, int type,
+                                   int pe, void *target, void *stream) {
+  if (!h || !origin || !compare || !result || pe < 0 || pe >= h->c->size) return MX_ERR_ARG;
+  const size_t es = mx_type_size(type);
+  if (!es || !heap_has(h, target, es)) return MX_ERR_ARG;
+  void *remote = mx_shmem_ptr(h, target, pe);
+  hipStream_t s = (hipStream_t)stream;
+  int rc;
+  if ((rc = acc_lock(h, pe, s))) return rc;
+  hipLaunchKernelGGL(k_cas_bytes, dim3(1), dim3(64), 0, s, (char *)remote, (const char *)compare,
+                     (const char *)origin, (char *)result, (int)es);
+  if ((rc = mx_check_launch())) return rc;
+  if ((rc = acc_unlock(h, pe, s))) return rc;
+  return finish(h->c, s);
+}
+
+// Derived datatypes on either side (NULL = `count` contiguous elements of
+// `type`); both sides carry the same number of `type` elements.
+extern "C" int mx_accumulate_ddt(mx_heap_t *h, const void *origin, size_t origin_count, const mx_ddt_t *origin_ddt,
+                                 int type, int op, int pe, void *target, size_t target_count,
+                                 const mx_ddt_t *target_ddt, void *stream) {
+  if (!h || pe < 0 || pe >= h->c->size || !target || (!origin && op != MX_OP_NO_OP)) return MX_ERR_ARG;
+  if (!acc_op_ok(op, type)) return MX_ERR_UNSUPPORTED;
+  const size_t es = mx_type_size(type);
+  const size_t obytes = origin_ddt ? origin_count * mx_ddt_size(origin_ddt) : origin_count * es;
+  const size_t tbytes = target_ddt ? target_count * mx_ddt_size(target_ddt) : target_count * es;
+  if (obytes != tbytes || obytes % es) return MX_ERR_ARG;
+  if (!obytes) return MX_SUCCESS;
+  int64_t lo = 0, hi = (int64_t)tbytes;
+  if (target_ddt && mx_ddt_span(target_ddt, target_count, &lo, &hi)) return MX_ERR_ARG;
+  if (!heap_has(h, (const char *)target + lo, (size_t)(hi - lo))) return MX_ERR_ARG;
+  char *remote = (char *)mx_shmem_ptr(h, (const char *)target + lo, pe) - lo;
+  hipStream_t s = (hipStream_t)stream;
+  char *po = nullptr, *pt = nullptr;
+  int rc = MX_SUCCESS;
+  const size_t nel = obytes / es;
+  if (origin_ddt && hipMallocAsync((void **)&po, obytes, s) != hipSuccess) return MX_ERR_NOMEM;
+  if (target_ddt && hipMallocAsync((void **)&pt, tbytes, s) != hipSuccess) rc = MX_ERR_NOMEM;
+  if (!rc && po) rc = mx_pack(origin_ddt, origin_count, origin, po, 0, obytes, s);
+  const void *osrc = po ? (const void *)po : origin;
+  if (!rc) rc = acc_lock(h, pe, s);
+  if (!rc) {
+    if (!pt) {
+      rc = acc_apply(op, type, osrc, remote, nel, s);
+    } else {
+      // gather the target region, combine in type-map order, scatter back
+      if (op != MX_OP_REPLACE) rc = mx_pack(target_ddt, target_count, remote, pt, 0, tbytes, s);
+      if (!rc) rc = acc_apply(op == MX_OP_REPLACE ? MX_OP_REPLACE : op, type, osrc, pt, nel, s);
+      if (!rc && op != MX_OP_NO_OP) rc = mx_unpack(target_ddt, target_count, remote, pt, 0, tbytes, s);
+    }
+    const int urc = acc_unlock(h, pe, s);
+    if (!rc) rc = urc;
+  }
+  if (po) (void)hipFreeAsync(po, s);
+  if (pt) (void)hipFreeAsync(pt, s);
+  return rc ? rc : finish(h->c, s);
 }

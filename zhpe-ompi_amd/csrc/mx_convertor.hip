@@ -21,6 +21,7 @@
 #include <stdlib.h>
 #include <string.h>
 #include <vector>
+#include <climits>
 #include <algorithm>
 
 #include "mx_internal.h"
@@ -519,6 +520,28 @@ extern "C" int mx_ddt_destroy(mx_ddt_t *d) {
 extern "C" size_t mx_ddt_size(const mx_ddt_t *d) { return d ? d->size : 0; }
 extern "C" int64_t mx_ddt_extent(const mx_ddt_t *d) { return d ? d->ub - d->lb : 0; }
 extern "C" size_t mx_ddt_runs(const mx_ddt_t *d) { return d ? d->host.size() : 0; }
+
+// Byte range [*lo, *hi) relative to `user` that `count` instances touch
+// (the true extent; instance i is displaced by i * extent).
+extern "C" int mx_ddt_span(const mx_ddt_t *d, size_t count, int64_t *lo, int64_t *hi) {
+  if (!d || !lo || !hi) return MX_ERR_ARG;
+  *lo = *hi = 0;
+  if (!count || d->host.empty()) return MX_SUCCESS;
+  int64_t a = INT64_MAX, b = INT64_MIN;
+  for (const DRun &r : d->host) {
+    if (!r.bytes) continue;
+    const int64_t s1 = (int64_t)(r.cnt1 - 1) * r.stride1, s2 = (int64_t)(r.cnt2 - 1) * r.stride2;
+    const int64_t first = r.disp + std::min<int64_t>(0, s1) + std::min<int64_t>(0, s2);
+    const int64_t last = r.disp + std::max<int64_t>(0, s1) + std::max<int64_t>(0, s2) + (int64_t)r.blen;
+    a = std::min(a, first);
+    b = std::max(b, last);
+  }
+  if (a > b) return MX_SUCCESS;
+  const int64_t ext = d->ub - d->lb, tail = (int64_t)(count - 1) * ext;
+  *lo = a + std::min<int64_t>(0, tail);
+  *hi = b + std::max<int64_t>(0, tail);
+  return MX_SUCCESS;
+}
 
 template <bool PACK>
 static int convert(const mx_ddt_t *d, size_t count, char *user, char *packed, size_t offset, size_t len,

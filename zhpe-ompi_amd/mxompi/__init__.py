@@ -510,6 +510,11 @@ def _heap_lib():
         L.mx_shmem_getmem.argtypes = [vp, vp, vp, sz, i, vp]
         L.mx_shmem_barrier_all.argtypes = [vp, vp]
         L.mx_shmem_reduce_heap.argtypes = [vp, i, i, sz, vp, vp, sz, i, i, i, vp]
+        L.mx_accumulate.argtypes = [vp, vp, sz, i, i, i, vp, vp]
+        L.mx_get_accumulate.argtypes = [vp, vp, vp, sz, i, i, i, vp, vp]
+        L.mx_fetch_and_op.argtypes = [vp, vp, vp, i, i, i, vp, vp]
+        L.mx_compare_and_swap.argtypes = [vp, vp, vp, vp, i, i, vp, vp]
+        L.mx_accumulate_ddt.argtypes = [vp, vp, sz, vp, i, i, i, vp, sz, vp, vp]
         L._mx_heap_typed = True
     return L
 
@@ -551,6 +556,31 @@ class Heap:
         check(_heap_lib().mx_shmem_reduce_heap(self.h, SHMEM_OPS.index(op), SHMEM_TYPES.index(t), dt_size, target,
                                                source, nreduce, pe_start, log_pe_stride, pe_size, stream or None),
               "mx_shmem_reduce_heap")
+
+    # -- one-sided accumulate (MPI_Accumulate & co. on symmetric memory) ----
+    def accumulate(self, origin, count, t, op, pe, target, stream=0):
+        check(_heap_lib().mx_accumulate(self.h, origin or None, count, _slot(t), _op(op), pe, target,
+                                        stream or None), "mx_accumulate")
+
+    def get_accumulate(self, origin, result, count, t, op, pe, target, stream=0):
+        check(_heap_lib().mx_get_accumulate(self.h, origin or None, result, count, _slot(t), _op(op), pe, target,
+                                            stream or None), "mx_get_accumulate")
+
+    def fetch_and_op(self, origin, result, t, op, pe, target, stream=0):
+        check(_heap_lib().mx_fetch_and_op(self.h, origin or None, result, _slot(t), _op(op), pe, target,
+                                          stream or None), "mx_fetch_and_op")
+
+    def compare_and_swap(self, origin, compare, result, t, pe, target, stream=0):
+        check(_heap_lib().mx_compare_and_swap(self.h, origin, compare, result, _slot(t), pe, target,
+                                              stream or None), "mx_compare_and_swap")
+
+    def accumulate_ddt(self, origin, origin_count, origin_dt, t, op, pe, target, target_count, target_dt,
+                       stream=0):
+        """origin_dt / target_dt: Datatype or None (contiguous elements of t)."""
+        check(_heap_lib().mx_accumulate_ddt(self.h, origin, origin_count, origin_dt.h if origin_dt else None,
+                                            _slot(t), _op(op), pe, target, target_count,
+                                            target_dt.h if target_dt else None, stream or None),
+              "mx_accumulate_ddt")
 
     def close(self):
         if getattr(self, "h", None):
