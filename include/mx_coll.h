@@ -49,6 +49,7 @@ extern "C" {
 #endif
 
 typedef struct mx_comm mx_comm_t;
+struct mx_ddt;   /* mx_convertor.h */
 
 /* MPI_IN_PLACE as the reference defines it (mpi.h: (void *) 1). */
 #define MX_IN_PLACE ((const void *)1)
@@ -253,6 +254,39 @@ int mx_request_is_active(const mx_request_t *req);
 /* MPI_Request_free: an active request is completed first. */
 int mx_request_free(mx_request_t *req);
 
+/* ---- point-to-point on device buffers ------------------------------------
+ * MPI_Send / MPI_Recv / MPI_Isend / MPI_Irecv / MPI_Sendrecv /
+ * MPI_Send_init / MPI_Recv_init between ranks of a multi-process
+ * communicator (the role btl/smcuda + common/cuda play for CUDA buffers:
+ * opal/mca/btl/smcuda, common_cuda.c:1008-1180; non-contiguous layouts via
+ * the device convertor, as the convertor CUDA hooks do,
+ * opal_datatype_cuda.c:44-140).  Each message streams through a mailbox the
+ * receiver owns (mapped at communicator creation) under device-side flow
+ * control; no host progress, no per-message IPC.  Work starts after what
+ * `stream` had queued; completion is through the request (blocking forms
+ * return complete).  Matching is in order per (source, destination) pair;
+ * the envelope tag is checked (MX_ERR_TAG on a mismatch, tag < 0 = any);
+ * a longer message than the receive buffer delivers what fits and
+ * completes with MX_ERR_TRUNCATE.  `received` / mx_request_status: bytes
+ * delivered and the envelope tag. */
+int mx_send(mx_comm_t *comm, const void *buf, size_t bytes, int dst, int tag, void *stream);
+int mx_recv(mx_comm_t *comm, void *buf, size_t bytes, int src, int tag, void *stream, size_t *received);
+int mx_isend(mx_comm_t *comm, const void *buf, size_t bytes, int dst, int tag, void *stream,
+             mx_request_t **req);
+int mx_irecv(mx_comm_t *comm, void *buf, size_t bytes, int src, int tag, void *stream, mx_request_t **req);
+int mx_send_init(mx_comm_t *comm, const void *buf, size_t bytes, int dst, int tag, void *stream,
+                 mx_request_t **req);
+int mx_recv_init(mx_comm_t *comm, void *buf, size_t bytes, int src, int tag, void *stream,
+                 mx_request_t **req);
+int mx_sendrecv(mx_comm_t *comm, const void *sbuf, size_t sbytes, int dst, int stag, void *rbuf,
+                size_t rbytes, int src, int rtag, void *stream, size_t *received);
+/* `count` instances of a derived datatype (mx_convertor.h) at `buf`. */
+int mx_isend_ddt(mx_comm_t *comm, const void *buf, size_t count, const struct mx_ddt *ddt, int dst,
+                 int tag, void *stream, mx_request_t **req);
+int mx_irecv_ddt(mx_comm_t *comm, void *buf, size_t count, const struct mx_ddt *ddt, int src,
+                 int tag, void *stream, mx_request_t **req);
+int mx_request_status(const mx_request_t *req, size_t *bytes, int *tag);
+
 /* ---- OpenSHMEM reductions (shmem_<type>_<op>_to_all) --------------------
  * The OSHMEM op/type numbering (oshmem/op/op.h: OSHMEM_OP_AND..PROD,
  * OSHMEM_OP_TYPE_SHORT..FREAL16).  mx_shmem_to_mpi restates scoll/mpi's
@@ -322,7 +356,6 @@ int mx_compare_and_swap(mx_heap_t *heap, const void *origin, const void *compare
 /* Derived datatypes (mx_convertor.h) on either side, NULL = contiguous
  * elements of `type`; both sides hold the same number of `type` elements,
  * matched in type-map order. */
-struct mx_ddt;
 int mx_accumulate_ddt(mx_heap_t *heap, const void *origin, size_t origin_count, const struct mx_ddt *origin_ddt,
                       int type, int op, int pe, void *target, size_t target_count, const struct mx_ddt *target_ddt,
                       void *stream);

@@ -64,6 +64,8 @@ extern "C" {
 #define MX_ERR_RCCL        -6  /* RCCL error                                 */
 #define MX_ERR_NOT_INIT    -7  /* mx_init not called / no device             */
 #define MX_ERR_STATE       -8  /* object in the wrong state                  */
+#define MX_ERR_TRUNCATE    -9  /* message longer than the receive buffer     */
+#define MX_ERR_TAG        -10  /* in-order channel: envelope tag differs     */
 
 /* ---- predefined reduction ops (== OMPI_OP_BASE_FORTRAN_*) ------------ */
 enum {

@@ -1,0 +1,218 @@
+"""GPU: point-to-point transfers of device buffers (SURVEY 8(f) row 1:
+MPI_Send / MPI_Recv / MPI_Isend / MPI_Irecv / MPI_Sendrecv / persistent
+MPI_Send_init / MPI_Recv_init, derived datatypes through the device
+convertor).
+
+n processes share the one GPU.  Payload bytes must arrive unchanged for
+every size (0 bytes, sub-vector tails, several times the mailbox), every
+alignment (user pointers offset by 1..15 bytes), many messages in flight
+per pair (more than the envelope ring), a ring shift, an all-to-all, and
+sends to self; truncation and tag mismatches complete with MPI's errors and
+leave the channel usable; derived datatypes on either side match the
+reference convertor's packed stream (golden vectors).
+"""
+import os
+
+import numpy as np
+import pytest
+
+import golden_io
+import mxompi
+from test_coll_gpu import _dev, _free_port
+
+torch = pytest.importorskip("torch")
+pytestmark = pytest.mark.gpu
+
+BASIC, RECS = golden_io.ddt_records()
+REC = {r["name"]: r for r in RECS}
+SIZES = [0, 1, 15, 16, 17, 4097, 65536, 3 * (1 << 20) + 7]
+SHIFT = 10 * (1 << 20) + 13
+
+
+def _data(seed, nbytes):
+    return np.random.default_rng(seed).integers(0, 256, nbytes, dtype=np.uint8)
+
+
+def _p2p_worker(rank, n, port, q):
+    import torch.distributed as dist
+    os.environ["HSA_ENABLE_IPC_MODE_LEGACY"] = "0"
+    try:
+        dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=n)
+        torch.cuda.set_device(0)
+        mxompi.init(0)
+
+        def ag(b):
+            out = [None] * n
+            dist.all_gather_object(out, b)
+            return out
+
+        comm = mxompi.Comm(rank, n, ag, device=0, staging_bytes=1 << 20)
+        comm.set_timeout(30.0)
+        res = {}
+        right, left = (rank + 1) % n, (rank - 1) % n
+
+        # (1) ring shift with MPI_Sendrecv, 5x the mailbox
+        x = _dev(_data(rank, SHIFT))
+        y = torch.zeros(SHIFT, dtype=torch.uint8, device="cuda")
+        got = comm.sendrecv(x.data_ptr(), SHIFT, right, y.data_ptr(), SHIFT, left, 7, 7)
+        res["shift"] = (got, y.cpu().numpy().tobytes())
+
+        # (2) sizes x misalignment, 0 -> 1 (blocking on both sides)
+        if rank == 0:
+            for k, nb in enumerate(SIZES):
+                src = _dev(_data(100 + k, nb + 32))
+                comm.send(src.data_ptr() + (k * 3) % 16, nb, 1, tag=k)
+        elif rank == 1:
+            outs = []
+            for k, nb in enumerate(SIZES):
+                dst = torch.zeros(nb + 64, dtype=torch.uint8, device="cuda")
+                off = (k * 5) % 16
+                got = comm.recv(dst.data_ptr() + off, nb + 16, 0, tag=k)
+                outs.append((got, dst.cpu().numpy()[off: off + nb].tobytes()))
+            res["sizes"] = outs
+
+        # (3) many in flight on one pair: 20 x 300 KB, posted before any wait
+        M, MB = 20, 300 * 1024 + 3
+        if rank == 0:
+            bufs = [_dev(_data(200 + k, MB)) for k in range(M)]
+            reqs = [comm.isend(b.data_ptr(), MB, 1, tag=k) for k, b in enumerate(bufs)]
+            for r in reqs:
+                r.wait()
+                r.free()
+        elif rank == 1:
+            bufs = [torch.zeros(MB, dtype=torch.uint8, device="cuda") for _ in range(M)]
+            reqs = [comm.irecv(b.data_ptr(), MB, 0, tag=k) for k, b in enumerate(bufs)]
+            st = []
+            for r in reqs:
+                r.wait()
+                st.append(r.status())
+                r.free()
+            res["inflight"] = (st, [b.cpu().numpy().tobytes() for b in bufs])
+
+        # (4) truncation and tag mismatch complete with MPI's errors; the
+        # channel stays in step
+        if rank == 0:
+            a = _dev(_data(300, 1000))
+            comm.send(a.data_ptr(), 1000, 1, tag=5)
+            comm.send(a.data_ptr(), 1000, 1, tag=5)
+            comm.send(a.data_ptr(), 1000, 1, tag=9)
+        elif rank == 1:
+            d = torch.zeros(1000, dtype=torch.uint8, device="cuda")
+            errs = []
+            try:
+                comm.recv(d.data_ptr(), 600, 0, tag=5)
+            except mxompi.MxError as e:
+                errs.append(e.rc)
+            res["trunc"] = d.cpu().numpy()[:600].tobytes()
+            try:
+                comm.recv(d.data_ptr(), 1000, 0, tag=6)
+            except mxompi.MxError as e:
+                errs.append(e.rc)
+            r = comm.irecv(d.data_ptr(), 1000, 0, tag=-1)
+            r.wait()
+            errs.append(r.status())
+            r.free()
+            res["errs"] = errs
+
+        # (5) persistent pair started three times on fresh data
+        P = 1 << 20
+        pb = torch.zeros(P, dtype=torch.uint8, device="cuda")
+        if rank == 0:
+            req = comm.isend(pb.data_ptr(), P, 1, tag=1, persistent=True)
+        elif rank == 1:
+            req = comm.irecv(pb.data_ptr(), P, 0, tag=1, persistent=True)
+        reps = []
+        for it in range(3):
+            if rank == 0:
+                pb.copy_(_dev(_data(400 + it, P)))
+                torch.cuda.synchronize()
+            if rank in (0, 1):
+                req.start()
+                req.wait()
+                if rank == 1:
+                    reps.append(pb.cpu().numpy().tobytes())
+        if rank in (0, 1):
+            req.free()
+        res["persistent"] = reps
+
+        # (6) derived datatypes on either side (golden reference types)
+        tv = REC["vector_f64_b3_s5"]
+        dt = mxompi.Datatype(tv["desc"].tobytes(), tv["nrec"], tv["size"], tv["lb"], tv["ub"])
+        nbp = tv["size"] * tv["count"]
+        if rank == 0:
+            user = _dev(tv["user"])
+            r1 = comm.isend_ddt(user.data_ptr() - tv["true_lb"], tv["count"], dt, 1, tag=2)
+            pk = _dev(tv["packed"])
+            r2 = comm.isend(pk.data_ptr(), nbp, 1, tag=3)
+            r1.wait(); r2.wait(); r1.free(); r2.free()
+        elif rank == 1:
+            got = torch.zeros(nbp, dtype=torch.uint8, device="cuda")
+            r1 = comm.irecv(got.data_ptr(), nbp, 0, tag=2)
+            ub = _dev(tv["prefill"])
+            r2 = comm.irecv_ddt(ub.data_ptr() - tv["true_lb"], tv["count"], dt, 0, tag=3)
+            r1.wait(); r2.wait(); r1.free(); r2.free()
+            res["ddt"] = (got.cpu().numpy().tobytes(), ub.cpu().numpy().tobytes())
+        dt.close()
+
+        # (7) all-to-all of isend / irecv, sends to self included
+        A = 77777
+        sb = [_dev(_data(1000 * rank + p, A)) for p in range(n)]
+        rb = [torch.zeros(A, dtype=torch.uint8, device="cuda") for _ in range(n)]
+        reqs = [comm.irecv(rb[p].data_ptr(), A, p, tag=11) for p in range(n)]
+        reqs += [comm.isend(sb[p].data_ptr(), A, p, tag=11) for p in range(n)]
+        for r in reqs:
+            r.wait()
+            r.free()
+        res["a2a"] = [b.cpu().numpy().tobytes() for b in rb]
+
+        comm.close()
+        dist.destroy_process_group()
+        q.put((rank, "ok", res))
+    except Exception as e:  # noqa: BLE001
+        import traceback
+        q.put((rank, "err", traceback.format_exc() + str(e)))
+
+
+def _run(n):
+    import torch.multiprocessing as mp
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_p2p_worker, args=(r, n, port, q)) for r in range(n)]
+    for p in procs:
+        p.start()
+    out = {}
+    for _ in range(n):
+        rank, status, payload = q.get(timeout=300)
+        assert status == "ok", payload
+        out[rank] = payload
+    for p in procs:
+        p.join(timeout=60)
+    return out
+
+
+@pytest.mark.parametrize("n", [2, 3, 4])
+def test_point_to_point(n):
+    got = _run(n)
+    for r in range(n):
+        nb, data = got[r]["shift"]
+        assert nb == SHIFT
+        assert data == _data((r - 1) % n, SHIFT).tobytes(), f"shift rank {r}"
+    for k, (nb, data) in enumerate(got[1]["sizes"]):
+        exp = _data(100 + k, SIZES[k] + 32)[(k * 3) % 16: (k * 3) % 16 + SIZES[k]]
+        assert nb == SIZES[k] and data == exp.tobytes(), f"size {SIZES[k]}"
+    st, bufs = got[1]["inflight"]
+    assert st == [(300 * 1024 + 3, k) for k in range(20)]
+    for k, b in enumerate(bufs):
+        assert b == _data(200 + k, 300 * 1024 + 3).tobytes(), f"in-flight message {k}"
+    assert got[1]["trunc"] == _data(300, 1000)[:600].tobytes()
+    assert got[1]["errs"] == [-9, -10, (1000, 9)], got[1]["errs"]    # MX_ERR_TRUNCATE, MX_ERR_TAG, any-tag status
+    for it, b in enumerate(got[1]["persistent"]):
+        assert b == _data(400 + it, 1 << 20).tobytes(), f"persistent start {it}"
+    tv = REC["vector_f64_b3_s5"]
+    packed, unpacked = got[1]["ddt"]
+    np.testing.assert_array_equal(np.frombuffer(packed, np.uint8), tv["packed"])
+    np.testing.assert_array_equal(np.frombuffer(unpacked, np.uint8), tv["unpacked"])
+    for r in range(n):
+        for p in range(n):
+            assert got[r]["a2a"][p] == _data(1000 * p + r, 77777).tobytes(), f"a2a {p} -> {r}"

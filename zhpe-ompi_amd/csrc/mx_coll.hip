@@ -41,7 +41,7 @@
 #include <map>
 #include <new>
 
-#include "mx_fold.hpp"
+#include "mx_comm.hpp"
 #include "../../include/mx_convertor.h"
 
 namespace mx {
@@ -115,11 +115,6 @@ int copy_async(void *dst, const void *src, size_t bytes, hipStream_t s) {
 // cross-GPU flags: generation-tagged, system scope, bounded spin
 // ---------------------------------------------------------------------------
 
-// one-shot small-message allreduce: per (source rank, workgroup) READY flags
-// after the NFLAGS x MAXR block, then one local completion counter.
-constexpr size_t OS_FLAG_BASE = NFLAGS * MAXR;
-constexpr size_t OS_COUNTER = OS_FLAG_BASE + (size_t)MAXR * OSWG;
-constexpr size_t FLAG_WORDS = OS_COUNTER + 8;
 constexpr size_t kOneShotMax = 64 << 10;   // bytes per rank
 
 struct SignalArgs { uint64_t *peer_flag[MAXR]; int n; uint64_t value; };
@@ -151,53 +146,6 @@ __global__ void k_wait(const uint64_t *flags, uint32_t mask, uint64_t value, uin
 }  // namespace mx
 
 using namespace mx;
-
-// ---------------------------------------------------------------------------
-// communicator
-// ---------------------------------------------------------------------------
-struct mx_comm {
-  int rank, size, device, local;
-  int flags;
-  size_t staging_bytes;
-  size_t main_bytes;           // staging for the chunked paths: [0, main_bytes)
-  size_t os_max, os_slot;      // one-shot: max bytes per rank, slot stride
-  uint64_t os_count;           // one-shot workgroup completions so far
-  char *staging;               // mine (uncached, IPC-exported)
-  char *peer_staging[MAXR];    // mapped views (peer_staging[rank] = staging)
-  uint64_t *flagmem;           // mine: [NFLAGS][MAXR]
-  uint64_t *peer_flags[MAXR];  // mapped views
-  int *err_host, *err_dev;
-  uint64_t gen;
-  double timeout_s;
-  uint64_t timeout_ticks;
-  ncclComm_t nccl;
-  // the host bootstrap exchange, kept for later collective setups
-  // (symmetric heaps); ctx must outlive the communicator
-  mx_allgather_fn ag;
-  void *ag_ctx;
-  // symmetric-heap region exported with the staging at creation
-  // (mx_comm_create_ex heap_bytes): heaps are carved from it
-  char *hregion;
-  char *peer_hregion[MAXR];
-  size_t hregion_bytes, hregion_used;
-  // profiling: event pairs recorded around kernels of the current call
-  int prof;
-  hipEvent_t ev[64];
-  int nev;
-  int ev_kind[32];   // 0 fold, 1 push, 2 gather
-  double ev_bytes[32];
-  mx_coll_stats_t st;
-  // non-blocking / persistent requests: while `defer`
-  // is set, finish() leaves the stream running; `tail` is an event after the
-  // last deferred collective, which a collective enqueued on another stream
-  // waits for (collectives of a communicator stay in issue order across
-  // streams, as MPI orders them); `pending` counts active requests.
-  int defer;
-  int tail_valid;
-  hipEvent_t tail;
-  hipStream_t tail_stream;
-  int pending;
-};
 
 static uint64_t ticks_for(double seconds) {
   int rate_khz = 0;
@@ -320,12 +268,15 @@ extern "C" int mx_comm_create_ex(int rank, int size, int device, size_t staging_
     c->os_slot = c->os_max ? c->os_max + 256 : 0;
     c->main_bytes = (c->staging_bytes - 2 * (size_t)size * c->os_slot) & ~(size_t)255;
     c->hregion_bytes = heap_bytes ? ((heap_bytes + 4095) & ~(size_t)4095) : 0;
-    if (hipExtMallocWithFlags((void **)&c->staging, c->staging_bytes, hipDeviceMallocUncached) != hipSuccess ||
-        hipExtMallocWithFlags((void **)&c->flagmem, (FLAG_WORDS + 8) * sizeof(uint64_t), hipDeviceMallocUncached) !=
+    // point-to-point mailboxes (one per source rank) follow the staging
+    c->p2p_off = (c->staging_bytes + 4095) & ~(size_t)4095;
+    if (hipExtMallocWithFlags((void **)&c->staging, c->p2p_off + (size_t)size * P2P_BOX, hipDeviceMallocUncached) !=
+            hipSuccess ||
+        hipExtMallocWithFlags((void **)&c->flagmem, ALL_FLAG_WORDS * sizeof(uint64_t), hipDeviceMallocUncached) !=
             hipSuccess ||
         (c->hregion_bytes &&
          hipExtMallocWithFlags((void **)&c->hregion, c->hregion_bytes, hipDeviceMallocUncached) != hipSuccess) ||
-        hipMemset(c->flagmem, 0, FLAG_WORDS * sizeof(uint64_t)) != hipSuccess ||
+        hipMemset(c->flagmem, 0, ALL_FLAG_WORDS * sizeof(uint64_t)) != hipSuccess ||
         hipDeviceSynchronize() != hipSuccess) {
       free(all);
       goto fail;
@@ -435,6 +386,7 @@ extern "C" int mx_comm_destroy(mx_comm_t *c) {
   if (c->prof)
     for (int i = 0; i < 64; i++) (void)hipEventDestroy(c->ev[i]);
   if (c->tail) (void)hipEventDestroy(c->tail);
+  p2p_release(c);
   free(c);
   return MX_SUCCESS;
 }
@@ -2092,25 +2044,16 @@ extern "C" int mx_ireduce_decision(int n, size_t count, int type) {
   return MX_IREDUCE_CHAIN;
 }
 
-enum { RQ_ALLREDUCE, RQ_REDUCE, RQ_REDUCE_SCATTER, RQ_REDUCE_SCATTER_BLOCK, RQ_SCAN, RQ_EXSCAN, RQ_ALLGATHER, RQ_BCAST };
 
-struct mx_request {
-  mx_comm *c;
-  int kind, persistent, active;
-  hipStream_t s;
-  hipEvent_t done;
-  const void *sbuf;
-  void *rbuf;
-  size_t count;   // elements (bytes for allgather / bcast)
-  int type, op, alg, root;
-  std::vector<size_t> rcounts;
-};
 
 namespace {
 
-static int req_dispatch(mx_request *q) {
+static int req_dispatch(mx_request *q, hipStream_t *done_stream) {
   mx_comm *c = q->c;
+  *done_stream = q->s;
   switch (q->kind) {
+    case RQ_SEND:
+    case RQ_RECV: return p2p_enqueue(q, done_stream);
     case RQ_ALLREDUCE: return nbc_allreduce(c, q->sbuf, q->rbuf, q->count, q->type, q->op, q->alg, q->s);
     case RQ_REDUCE: return nbc_reduce(c, q->sbuf, q->rbuf, q->count, q->type, q->op, q->root, q->alg, q->s);
     case RQ_REDUCE_SCATTER:
@@ -2132,15 +2075,18 @@ static int req_start(mx_request *q) {
   mx_comm *c = q->c;
   if (q->active) return MX_ERR_STATE;
   if (!c->tail && hipEventCreateWithFlags(&c->tail, hipEventDisableTiming) != hipSuccess) return MX_ERR_HIP;
+  hipStream_t ds;
   c->defer = 1;
-  const int rc = req_dispatch(q);
+  const int rc = req_dispatch(q, &ds);
   c->defer = 0;
-  // whatever this call enqueued orders the communicator's next collective
-  if (hipEventRecord(c->tail, q->s) != hipSuccess) return MX_ERR_HIP;
-  c->tail_valid = 1;
-  c->tail_stream = q->s;
+  if (q->kind != RQ_SEND && q->kind != RQ_RECV) {
+    // whatever this call enqueued orders the communicator's next collective
+    if (hipEventRecord(c->tail, q->s) != hipSuccess) return MX_ERR_HIP;
+    c->tail_valid = 1;
+    c->tail_stream = q->s;
+  }
   if (rc) return rc;
-  if (hipEventRecord(q->done, q->s) != hipSuccess) return MX_ERR_HIP;
+  if (hipEventRecord(q->done, ds) != hipSuccess) return MX_ERR_HIP;
   q->active = 1;
   c->pending++;
   return MX_SUCCESS;
@@ -2155,6 +2101,7 @@ static int req_complete(mx_request *q) {
     *c->err_host = 0;
     return e;
   }
+  if (q->kind == RQ_RECV && q->status && q->status[2]) return (int)q->status[2];   // truncation / tag
   return MX_SUCCESS;
 }
 
@@ -2181,6 +2128,7 @@ static int req_post(mx_request *q, mx_request_t **out) {
     const int rc = req_start(q);
     if (rc) {
       (void)hipEventDestroy(q->done);
+      if (q->status) (void)hipHostFree(q->status);
       delete q;
       return rc;
     }
@@ -2212,6 +2160,19 @@ static int req_reduction(mx_comm_t *c, int kind, int persistent, const void *sbu
 }
 
 }  // namespace
+
+namespace mx {
+int req_create(mx_comm *c, int kind, int persistent, void *stream, mx_request **q) {
+  mx_request_t *dummy;
+  return req_new(c, kind, persistent, stream, &dummy, q);
+}
+int req_submit(mx_request *q, mx_request_t **out) { return req_post(q, out); }
+void req_discard(mx_request *q) {
+  (void)hipEventDestroy(q->done);
+  if (q->status) (void)hipHostFree(q->status);
+  delete q;
+}
+}  // namespace mx
 
 extern "C" int mx_iallreduce(mx_comm_t *c, const void *sbuf, void *rbuf, size_t count, int type, int op, int alg,
                              void *stream, mx_request_t **req) {
@@ -2361,6 +2322,7 @@ extern "C" int mx_request_free(mx_request_t *q) {
   int rc = MX_SUCCESS;
   if (q->active) rc = mx_wait(q);   // MPI_Request_free lets an active operation finish
   (void)hipEventDestroy(q->done);
+  if (q->status) (void)hipHostFree(q->status);
   delete q;
   return rc;
 }

@@ -1,0 +1,378 @@
+// mx_p2p.hip -- point-to-point transfers of device buffers between the
+// ranks of a communicator.
+//
+// The reference moves intra-node CUDA buffers with btl/smcuda: the sender's
+// buffer is registered and its IPC handle sent in the rendezvous, the
+// receiver opens it and issues cuMemcpy from the peer buffer, completion by
+// CUDA events polled from opal_progress (mca_common_cuda_memcpy,
+// opal/mca/common/cuda/common_cuda.c:1008-1180); non-contiguous layouts go
+// through the convertor's CUDA hooks, one copy per block
+// (opal_datatype_cuda.c:44-140).
+//
+// MI355X design: no per-message IPC export (an export costs far more than a
+// copy, and late exports are the operation this image has been seen to get
+// wrong, see mx_coll.hip).  Instead every rank owns, next to its collective
+// staging, one mailbox per source rank, mapped by every peer at
+// communicator creation.  A message is a device-driven stream through that
+// mailbox: the send kernel (one workgroup per lane) writes the envelope
+// (bytes, tag) into the mailbox's header ring and each lane streams its
+// stripe of the payload in P2P_C chunks through P2P_S slots, directly into
+// the receiver's memory over xGMI; the receive kernel copies the chunks out
+// as they land and hands the slots back.  Flow control is cumulative
+// counters in the ranks' uncached flag arrays (system-scope atomics), so a
+// message of any size streams with no host involvement, and with P2P_L
+// lanes in flight per pair.  Sends and receives run on two internal
+// streams, after the work the caller's stream had queued, so a send never
+// waits behind a receive of its own process.
+//
+// Matching: messages of one (source, destination) pair match in order --
+// the i-th receive from a source gets the i-th send to it (the envelope's
+// tag is checked: a mismatch completes the receive with MX_ERR_TAG, tag < 0
+// is MPI_ANY_TAG).  A message longer than the receive buffer delivers what
+// fits and completes with MX_ERR_TRUNCATE (MPI_ERR_TRUNCATE); the status
+// holds the delivered byte count.  Non-contiguous layouts are packed /
+// unpacked by the device convertor (mx_convertor.h) around the stream.
+#include <hip/hip_runtime.h>
+#include <string.h>
+
+#include <algorithm>
+
+#include "mx_comm.hpp"
+#include "../../include/mx_convertor.h"
+
+namespace mx {
+
+constexpr int kP2PThreads = 256;
+
+__device__ __forceinline__ bool p2p_wait_ge(const uint64_t *f, uint64_t v, uint64_t t0, uint64_t tmo, int *err) {
+  while (__hip_atomic_load(f, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) < v) {
+    __builtin_amdgcn_s_sleep(2);
+    if (wall_clock64() - t0 > tmo) {
+      __hip_atomic_store(err, MX_ERR_TIMEOUT, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      return false;
+    }
+  }
+  return true;
+}
+
+// len bytes: 16-byte vectors when both ends are aligned, 4-byte words when
+// they are word aligned, bytes otherwise
+__device__ __forceinline__ void p2p_copy(char *dst, const char *src, uint64_t len) {
+  const int t = threadIdx.x;
+  if ((((uintptr_t)dst | (uintptr_t)src) & 15) == 0) {
+    const uint64_t nv = len / 16;
+    for (uint64_t i = t; i < nv; i += kP2PThreads)
+      reinterpret_cast<uint4 *>(dst)[i] = reinterpret_cast<const uint4 *>(src)[i];
+    for (uint64_t i = nv * 16 + t; i < len; i += kP2PThreads) dst[i] = src[i];
+  } else if ((((uintptr_t)dst | (uintptr_t)src) & 3) == 0) {
+    const uint64_t nw = len / 4;
+    for (uint64_t i = t; i < nw; i += kP2PThreads)
+      reinterpret_cast<uint32_t *>(dst)[i] = reinterpret_cast<const uint32_t *>(src)[i];
+    for (uint64_t i = nw * 4 + t; i < len; i += kP2PThreads) dst[i] = src[i];
+  } else {
+    for (uint64_t i = t; i < len; i += kP2PThreads) dst[i] = src[i];
+  }
+}
+
+// stripe of lane l: 16-byte multiples, the last lanes short or empty
+__device__ __forceinline__ void p2p_lane(uint64_t bytes, int l, uint64_t *lo, uint64_t *hi) {
+  const uint64_t stripe = ((bytes + P2P_L - 1) / P2P_L + 15) & ~(uint64_t)15;
+  *lo = std::min<uint64_t>(bytes, (uint64_t)l * stripe);
+  *hi = std::min<uint64_t>(bytes, *lo + stripe);
+}
+
+struct P2PSendArgs {
+  const char *buf;
+  uint64_t bytes;
+  int64_t tag;
+  char *box;                 // the receiver's mailbox for me
+  uint64_t *posted;          // receiver's flags: posted[me]
+  uint64_t *filled;          // receiver's flags: filled[me][lane]
+  const uint64_t *seen;      // my flags: seen[dst][lane]
+  const uint64_t *drained;   // my flags: drained[dst][lane]
+  P2PSendState *st;
+  uint64_t timeout_ticks;
+  int *err;
+};
+
+__global__ void __launch_bounds__(kP2PThreads) k_p2p_send(P2PSendArgs a) {
+  const int l = blockIdx.x;
+  const uint64_t t0 = wall_clock64();
+  __shared__ int ok;
+  if (l == 0 && threadIdx.x == 0) {
+    // envelope: the header slot is free once every lane of the receiver has
+    // read the envelope P2P_H messages back
+    const uint64_t m = a.st->msgs;
+    bool good = true;
+    for (int i = 0; i < P2P_L && good; i++)
+      good = p2p_wait_ge(a.seen + i, m + 1 > P2P_H ? m + 1 - P2P_H : 0, t0, a.timeout_ticks, a.err);
+    if (good) {
+      volatile uint64_t *h = reinterpret_cast<volatile uint64_t *>(a.box + (m % P2P_H) * P2P_HDR);
+      h[0] = a.bytes;
+      h[1] = (uint64_t)a.tag;
+      __threadfence_system();
+      __hip_atomic_store(a.posted, m + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+      a.st->msgs = m + 1;
+    }
+  }
+  uint64_t lo, hi;
+  p2p_lane(a.bytes, l, &lo, &hi);
+  uint64_t k = a.st->lane_chunks[l];   // this lane's counter: read and written by this workgroup only
+  for (uint64_t pos = lo; pos < hi; pos += P2P_C) {
+    const uint64_t len = std::min<uint64_t>(P2P_C, hi - pos);
+    k++;
+    if (threadIdx.x == 0) ok = p2p_wait_ge(a.drained + l, k > P2P_S ? k - P2P_S : 0, t0, a.timeout_ticks, a.err);
+    __syncthreads();
+    if (!ok) return;
+    char *slot = a.box + 4096 + ((size_t)l * P2P_S + (size_t)((k - 1) % P2P_S)) * P2P_C;
+    p2p_copy(slot, a.buf + pos, len);
+    __threadfence_system();   // my stores reach the peer before the counter moves
+    __syncthreads();
+    if (threadIdx.x == 0) __hip_atomic_store(a.filled + l, k, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
+  if (threadIdx.x == 0) a.st->lane_chunks[l] = k;
+}
+
+struct P2PRecvArgs {
+  char *buf;
+  uint64_t cap;
+  int64_t tag;               // < 0: any
+  const char *box;           // my mailbox for src
+  const uint64_t *posted;    // my flags: posted[src]
+  const uint64_t *filled;    // my flags: filled[src][lane]
+  uint64_t *seen;            // sender's flags: seen[me][lane]
+  uint64_t *drained;         // sender's flags: drained[me][lane]
+  P2PRecvState *st;
+  int64_t *status;           // mapped host: delivered bytes, tag, error
+  uint64_t timeout_ticks;
+  int *err;
+};
+
+__global__ void __launch_bounds__(kP2PThreads) k_p2p_recv(P2PRecvArgs a) {
+  const int l = blockIdx.x;
+  const uint64_t t0 = wall_clock64();
+  __shared__ int ok;
+  __shared__ uint64_t s_bytes;
+  __shared__ int64_t s_tag;
+  if (threadIdx.x == 0) {
+    const uint64_t m = a.st->lane_msgs[l];
+    ok = p2p_wait_ge(a.posted, m + 1, t0, a.timeout_ticks, a.err);
+    if (ok) {
+      const volatile uint64_t *h = reinterpret_cast<const volatile uint64_t *>(a.box + (m % P2P_H) * P2P_HDR);
+      s_bytes = h[0];
+      s_tag = (int64_t)h[1];
+      __hip_atomic_store(a.seen + l, m + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+      a.st->lane_msgs[l] = m + 1;
+    }
+  }
+  __syncthreads();
+  if (!ok) return;
+  const uint64_t bytes = s_bytes;
+  uint64_t lo, hi;
+  p2p_lane(bytes, l, &lo, &hi);
+  uint64_t k = a.st->lane_chunks[l];
+  for (uint64_t pos = lo; pos < hi; pos += P2P_C) {
+    const uint64_t len = std::min<uint64_t>(P2P_C, hi - pos);
+    k++;
+    if (threadIdx.x == 0) ok = p2p_wait_ge(a.filled + l, k, t0, a.timeout_ticks, a.err);
+    __syncthreads();
+    if (!ok) return;
+    const char *slot = a.box + 4096 + ((size_t)l * P2P_S + (size_t)((k - 1) % P2P_S)) * P2P_C;
+    if (pos < a.cap) p2p_copy(a.buf + pos, slot, std::min<uint64_t>(len, a.cap - pos));
+    __syncthreads();          // every load of the slot has returned
+    if (threadIdx.x == 0) __hip_atomic_store(a.drained + l, k, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
+  if (threadIdx.x == 0) {
+    a.st->lane_chunks[l] = k;
+    if (l == 0) {
+      a.status[0] = (int64_t)std::min<uint64_t>(bytes, a.cap);
+      a.status[1] = s_tag;
+      a.status[2] = bytes > a.cap ? MX_ERR_TRUNCATE : (a.tag >= 0 && s_tag != a.tag) ? MX_ERR_TAG : 0;
+      __threadfence_system();
+    }
+  }
+}
+
+int p2p_setup(mx_comm *c) {
+  if (c->p2p_send) return MX_SUCCESS;
+  const size_t sb = sizeof(P2PSendState) * c->size, rb = sizeof(P2PRecvState) * c->size;
+  if (hipMalloc((void **)&c->p2p_send, sb) != hipSuccess) return MX_ERR_NOMEM;
+  if (hipMalloc((void **)&c->p2p_recv, rb) != hipSuccess) {
+    (void)hipFree(c->p2p_send);
+    c->p2p_send = nullptr;
+    return MX_ERR_NOMEM;
+  }
+  if (hipMemset(c->p2p_send, 0, sb) != hipSuccess || hipMemset(c->p2p_recv, 0, rb) != hipSuccess ||
+      hipStreamCreateWithFlags(&c->p2p_stream[0], hipStreamNonBlocking) != hipSuccess ||
+      hipStreamCreateWithFlags(&c->p2p_stream[1], hipStreamNonBlocking) != hipSuccess ||
+      hipEventCreateWithFlags(&c->p2p_ev, hipEventDisableTiming) != hipSuccess ||
+      hipDeviceSynchronize() != hipSuccess) {
+    p2p_release(c);
+    return MX_ERR_HIP;
+  }
+  return MX_SUCCESS;
+}
+
+void p2p_release(mx_comm *c) {
+  if (c->p2p_stream[0]) (void)hipStreamDestroy(c->p2p_stream[0]);
+  if (c->p2p_stream[1]) (void)hipStreamDestroy(c->p2p_stream[1]);
+  if (c->p2p_ev) (void)hipEventDestroy(c->p2p_ev);
+  if (c->p2p_send) (void)hipFree(c->p2p_send);
+  if (c->p2p_recv) (void)hipFree(c->p2p_recv);
+  c->p2p_stream[0] = c->p2p_stream[1] = nullptr;
+  c->p2p_ev = nullptr;
+  c->p2p_send = nullptr;
+  c->p2p_recv = nullptr;
+}
+
+// Enqueue request q (RQ_SEND / RQ_RECV) on the internal stream, after the
+// caller's stream; *done_stream receives the stream completion is on.
+int p2p_enqueue(mx_request *q, hipStream_t *done_stream) {
+  mx_comm *c = q->c;
+  if (c->local || !(c->flags & MX_COMM_IPC)) return MX_ERR_STATE;
+  int rc = p2p_setup(c);
+  if (rc) return rc;
+  const bool send = q->kind == RQ_SEND;
+  hipStream_t s = c->p2p_stream[send ? 0 : 1];
+  if (hipEventRecord(c->p2p_ev, q->s) != hipSuccess || hipStreamWaitEvent(s, c->p2p_ev, 0) != hipSuccess)
+    return MX_ERR_HIP;
+  *done_stream = s;
+  const int me = c->rank, p = q->peer;
+  const size_t bytes = q->ddt ? q->count * mx_ddt_size(q->ddt) : q->count;
+  char *tmp = nullptr;
+  if (q->ddt && bytes && hipMallocAsync((void **)&tmp, bytes, s) != hipSuccess) return MX_ERR_NOMEM;
+  if (send) {
+    if (tmp && (rc = mx_pack(q->ddt, q->count, q->sbuf, tmp, 0, bytes, s))) return rc;
+    P2PSendArgs a;
+    memset(&a, 0, sizeof a);
+    a.buf = tmp ? tmp : (const char *)q->sbuf;
+    a.bytes = bytes;
+    a.tag = q->tag;
+    a.box = c->peer_staging[p] + c->p2p_off + (size_t)me * P2P_BOX;
+    a.posted = c->peer_flags[p] + P2P_POSTED + me;
+    a.filled = c->peer_flags[p] + P2P_FILLED + (size_t)me * P2P_L;
+    a.seen = c->flagmem + P2P_SEEN + (size_t)p * P2P_L;
+    a.drained = c->flagmem + P2P_DRAINED + (size_t)p * P2P_L;
+    a.st = c->p2p_send + p;
+    a.timeout_ticks = c->timeout_ticks;
+    a.err = c->err_dev;
+    hipLaunchKernelGGL(k_p2p_send, dim3(P2P_L), dim3(kP2PThreads), 0, s, a);
+    if ((rc = mx_check_launch())) return rc;
+  } else {
+    if (!q->status && hipHostMalloc((void **)&q->status, 4 * sizeof(int64_t), hipHostMallocMapped) != hipSuccess)
+      return MX_ERR_NOMEM;
+    memset(q->status, 0, 4 * sizeof(int64_t));
+    int64_t *st_dev = nullptr;
+    if (hipHostGetDevicePointer((void **)&st_dev, q->status, 0) != hipSuccess) return MX_ERR_HIP;
+    P2PRecvArgs a;
+    memset(&a, 0, sizeof a);
+    a.buf = tmp ? tmp : (char *)q->rbuf;
+    a.cap = bytes;
+    a.tag = q->tag;
+    a.box = c->staging + c->p2p_off + (size_t)p * P2P_BOX;
+    a.posted = c->flagmem + P2P_POSTED + p;
+    a.filled = c->flagmem + P2P_FILLED + (size_t)p * P2P_L;
+    a.seen = c->peer_flags[p] + P2P_SEEN + (size_t)me * P2P_L;
+    a.drained = c->peer_flags[p] + P2P_DRAINED + (size_t)me * P2P_L;
+    a.st = c->p2p_recv + p;
+    a.status = st_dev;
+    a.timeout_ticks = c->timeout_ticks;
+    a.err = c->err_dev;
+    hipLaunchKernelGGL(k_p2p_recv, dim3(P2P_L), dim3(kP2PThreads), 0, s, a);
+    if ((rc = mx_check_launch())) return rc;
+    if (tmp && (rc = mx_unpack(q->ddt, q->count, q->rbuf, tmp, 0, bytes, s))) return rc;
+  }
+  if (tmp) (void)hipFreeAsync(tmp, s);
+  return MX_SUCCESS;
+}
+
+}  // namespace mx
+
+using namespace mx;
+
+namespace {
+
+static int p2p_request(mx_comm_t *c, int kind, int persistent, const void *sbuf, void *rbuf, size_t count,
+                       const mx_ddt_t *ddt, int peer, int tag, void *stream, mx_request_t **req) {
+  if (!c || !req || peer < 0 || peer >= c->size) return MX_ERR_ARG;
+  if (count && (kind == RQ_SEND ? !sbuf : !rbuf)) return MX_ERR_ARG;
+  mx_request *q;
+  int rc = req_create(c, kind, persistent, stream, &q);
+  if (rc) return rc;
+  q->sbuf = sbuf;
+  q->rbuf = rbuf;
+  q->count = count;
+  q->ddt = ddt;
+  q->peer = peer;
+  q->tag = tag;
+  return req_submit(q, req);
+}
+
+static int p2p_blocking(mx_comm_t *c, int kind, const void *sbuf, void *rbuf, size_t count, const mx_ddt_t *ddt,
+                        int peer, int tag, void *stream, size_t *received) {
+  mx_request_t *q = nullptr;
+  int rc = p2p_request(c, kind, 0, sbuf, rbuf, count, ddt, peer, tag, stream, &q);
+  if (rc) return rc;
+  rc = mx_wait(q);
+  if (received) *received = (kind == RQ_RECV && q->status) ? (size_t)q->status[0] : 0;
+  const int frc = mx_request_free(q);
+  return rc ? rc : frc;
+}
+
+}  // namespace
+
+extern "C" int mx_isend(mx_comm_t *c, const void *buf, size_t bytes, int dst, int tag, void *stream,
+                        mx_request_t **req) {
+  return p2p_request(c, RQ_SEND, 0, buf, nullptr, bytes, nullptr, dst, tag, stream, req);
+}
+extern "C" int mx_irecv(mx_comm_t *c, void *buf, size_t bytes, int src, int tag, void *stream, mx_request_t **req) {
+  return p2p_request(c, RQ_RECV, 0, nullptr, buf, bytes, nullptr, src, tag, stream, req);
+}
+extern "C" int mx_send_init(mx_comm_t *c, const void *buf, size_t bytes, int dst, int tag, void *stream,
+                            mx_request_t **req) {
+  return p2p_request(c, RQ_SEND, 1, buf, nullptr, bytes, nullptr, dst, tag, stream, req);
+}
+extern "C" int mx_recv_init(mx_comm_t *c, void *buf, size_t bytes, int src, int tag, void *stream,
+                            mx_request_t **req) {
+  return p2p_request(c, RQ_RECV, 1, nullptr, buf, bytes, nullptr, src, tag, stream, req);
+}
+extern "C" int mx_send(mx_comm_t *c, const void *buf, size_t bytes, int dst, int tag, void *stream) {
+  return p2p_blocking(c, RQ_SEND, buf, nullptr, bytes, nullptr, dst, tag, stream, nullptr);
+}
+extern "C" int mx_recv(mx_comm_t *c, void *buf, size_t bytes, int src, int tag, void *stream, size_t *received) {
+  return p2p_blocking(c, RQ_RECV, nullptr, buf, bytes, nullptr, src, tag, stream, received);
+}
+extern "C" int mx_isend_ddt(mx_comm_t *c, const void *buf, size_t count, const mx_ddt_t *ddt, int dst, int tag,
+                            void *stream, mx_request_t **req) {
+  if (!ddt) return MX_ERR_ARG;
+  return p2p_request(c, RQ_SEND, 0, buf, nullptr, count, ddt, dst, tag, stream, req);
+}
+extern "C" int mx_irecv_ddt(mx_comm_t *c, void *buf, size_t count, const mx_ddt_t *ddt, int src, int tag,
+                            void *stream, mx_request_t **req) {
+  if (!ddt) return MX_ERR_ARG;
+  return p2p_request(c, RQ_RECV, 0, nullptr, buf, count, ddt, src, tag, stream, req);
+}
+
+// MPI_Sendrecv: both directions in flight at once (send and receive streams)
+extern "C" int mx_sendrecv(mx_comm_t *c, const void *sbuf, size_t sbytes, int dst, int stag, void *rbuf,
+                           size_t rbytes, int src, int rtag, void *stream, size_t *received) {
+  mx_request_t *rq = nullptr, *sq = nullptr;
+  int rc = p2p_request(c, RQ_RECV, 0, nullptr, rbuf, rbytes, nullptr, src, rtag, stream, &rq);
+  if (rc) return rc;
+  rc = p2p_request(c, RQ_SEND, 0, sbuf, nullptr, sbytes, nullptr, dst, stag, stream, &sq);
+  const int wrc = sq ? mx_wait(sq) : MX_SUCCESS;
+  const int rrc = mx_wait(rq);
+  if (received) *received = rq->status ? (size_t)rq->status[0] : 0;
+  if (sq) mx_request_free(sq);
+  mx_request_free(rq);
+  return rc ? rc : wrc ? wrc : rrc;
+}
+
+// status of a completed receive request (MPI_Get_count / MPI_TAG)
+extern "C" int mx_request_status(const mx_request_t *q, size_t *bytes, int *tag) {
+  if (!q || q->kind != RQ_RECV || !q->status) return MX_ERR_ARG;
+  if (q->active) return MX_ERR_STATE;
+  if (bytes) *bytes = (size_t)q->status[0];
+  if (tag) *tag = (int)q->status[1];
+  return MX_SUCCESS;
+}

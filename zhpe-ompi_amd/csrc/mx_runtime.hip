@@ -108,6 +108,8 @@ extern "C" const char *mx_strerror(int rc) {
     case MX_ERR_RCCL: return "RCCL error";
     case MX_ERR_NOT_INIT: return "not initialised / no device";
     case MX_ERR_STATE: return "invalid state";
+    case MX_ERR_TRUNCATE: return "message truncated (longer than the receive buffer)";
+    case MX_ERR_TAG: return "envelope tag differs from the receive's (channels match in order)";
     default: return "unknown error";
   }
 }

@@ -70,7 +70,7 @@ MPI_DTYPE_SLOT = {
 
 ERRORS = {0: "MX_SUCCESS", -1: "MX_ERR_ARG", -2: "MX_ERR_UNSUPPORTED", -3: "MX_ERR_HIP",
           -4: "MX_ERR_NOMEM", -5: "MX_ERR_TIMEOUT", -6: "MX_ERR_RCCL",
-          -7: "MX_ERR_NOT_INIT", -8: "MX_ERR_STATE"}
+          -7: "MX_ERR_NOT_INIT", -8: "MX_ERR_STATE", -9: "MX_ERR_TRUNCATE", -10: "MX_ERR_TAG"}
 
 
 class MxError(RuntimeError):
@@ -236,6 +236,15 @@ def _coll_lib():
         L.mx_request_is_active.argtypes = [vp]
         L.mx_request_free.argtypes = [vp]
         L.mx_iallreduce_decision.argtypes = [i, sz, i, i]
+        # point-to-point
+        L.mx_send.argtypes = [vp, vp, sz, i, i, vp]
+        L.mx_recv.argtypes = [vp, vp, sz, i, i, vp, ctypes.POINTER(sz)]
+        for name in ("mx_isend", "mx_irecv", "mx_send_init", "mx_recv_init"):
+            getattr(L, name).argtypes = [vp, vp, sz, i, i, vp, rq]
+        for name in ("mx_isend_ddt", "mx_irecv_ddt"):
+            getattr(L, name).argtypes = [vp, vp, sz, vp, i, i, vp, rq]
+        L.mx_sendrecv.argtypes = [vp, vp, sz, i, i, vp, sz, i, i, vp, ctypes.POINTER(sz)]
+        L.mx_request_status.argtypes = [vp, ctypes.POINTER(sz), ctypes.POINTER(i)]
         L.mx_ireduce_decision.argtypes = [i, sz, i]
         L._mx_coll_typed = True
     return L
@@ -278,6 +287,12 @@ class Request:
     @property
     def active(self) -> bool:
         return bool(_coll_lib().mx_request_is_active(self.h))
+
+    def status(self):
+        """(bytes delivered, envelope tag) of a completed receive."""
+        nb, tag = ctypes.c_size_t(), ctypes.c_int()
+        check(_coll_lib().mx_request_status(self.h, ctypes.byref(nb), ctypes.byref(tag)), "mx_request_status")
+        return nb.value, tag.value
 
     def free(self):
         if getattr(self, "h", None):
@@ -446,6 +461,35 @@ class Comm:
     def ibcast(self, buf, nbytes, root, stream=0, persistent=False):
         return self._req("mx_bcast_init" if persistent else "mx_ibcast", persistent, buf, nbytes, root,
                          stream or None)
+
+    # -- point-to-point on device buffers -------------------------------------
+    def send(self, buf, nbytes, dst, tag=0, stream=0):
+        check(_coll_lib().mx_send(self.h, buf, nbytes, dst, tag, stream or None), "mx_send")
+
+    def recv(self, buf, nbytes, src, tag=-1, stream=0):
+        got = ctypes.c_size_t()
+        check(_coll_lib().mx_recv(self.h, buf, nbytes, src, tag, stream or None, ctypes.byref(got)), "mx_recv")
+        return got.value
+
+    def sendrecv(self, sbuf, sbytes, dst, rbuf, rbytes, src, stag=0, rtag=-1, stream=0):
+        got = ctypes.c_size_t()
+        check(_coll_lib().mx_sendrecv(self.h, sbuf, sbytes, dst, stag, rbuf, rbytes, src, rtag, stream or None,
+                                      ctypes.byref(got)), "mx_sendrecv")
+        return got.value
+
+    def isend(self, buf, nbytes, dst, tag=0, stream=0, persistent=False):
+        return self._req("mx_send_init" if persistent else "mx_isend", persistent, buf, nbytes, dst, tag,
+                         stream or None)
+
+    def irecv(self, buf, nbytes, src, tag=-1, stream=0, persistent=False):
+        return self._req("mx_recv_init" if persistent else "mx_irecv", persistent, buf, nbytes, src, tag,
+                         stream or None)
+
+    def isend_ddt(self, buf, count, dt, dst, tag=0, stream=0):
+        return self._req("mx_isend_ddt", False, buf, count, dt.h, dst, tag, stream or None, keep=(dt,))
+
+    def irecv_ddt(self, buf, count, dt, src, tag=-1, stream=0):
+        return self._req("mx_irecv_ddt", False, buf, count, dt.h, src, tag, stream or None, keep=(dt,))
 
     # -- local (all ranks in this process) ---------------------------------
     def allreduce_local(self, sbufs, rbufs, count, t, op, alg="auto", stream=0):
