@@ -297,7 +297,9 @@ def cfg_e(torch, mx, dist, comm, world, rank, sp, nbytes=256 << 20, iters=5):
     MPI_Allgather (busBW = algBW*(n-1)/n, algBW over the full vector),
     MAXLOC float_int allreduce, OpenSHMEM float max_to_all and the other
     reduction slots (rooted reduce, reduce_scatter_block, scan), each with the
-    coll/tuned (or coll/basic) fold order; max over ranks."""
+    coll/tuned (or coll/basic) fold order; then MPI_Accumulate on the symmetric
+    heap, MPI_Iallreduce (libnbc orders) and an MPI_Sendrecv ring shift; max
+    over ranks."""
     res = {}
     count = nbytes // 4
     g = torch.Generator(device="cuda").manual_seed(0x5EED + 101 * rank)
@@ -350,9 +352,29 @@ def cfg_e(torch, mx, dist, comm, world, rank, sp, nbytes=256 << 20, iters=5):
         heap.barrier_all()
         timed("shmem_float_max_to_all_symheap", lambda: heap.reduce("MAX", "FLOAT", 4, tgt, src, count, stream=sp),
               nbytes, 2 * f_ring)
+        # MPI_Accumulate(SUM) of a quarter of the buffer into the right
+        # neighbour's window (lock, op kernel over xGMI, unlock); GB/s per rank
+        acc = count // 4
+        timed("accumulate_fp32_sum_to_right", lambda: heap.accumulate(src, acc, "FLOAT", "SUM", (rank + 1) % world,
+                                                                      tgt, stream=sp), acc * 4, 1.0)
         heap.close()
     except mx.MxError as e:
         res["shmem_float_max_to_all_symheap"] = {"error": str(e)}
+    # MPI_Iallreduce: eight slices posted back to back, then waited (libnbc's
+    # orders); busBW over the whole vector
+    k = 8
+
+    def iar():
+        sl = count // k
+        reqs = [comm.iallreduce(x.data_ptr() + i * sl * 4, y.data_ptr() + i * sl * 4, sl, "FLOAT", "SUM", "auto", sp)
+                for i in range(k)]
+        for r in reqs:
+            r.wait()
+            r.free()
+    timed("iallreduce_fp32_sum_8x", iar, (count // k) * k * 4, 2 * f_ring)
+    # MPI_Sendrecv ring shift of the whole buffer (GB/s per rank per direction)
+    timed("sendrecv_ring_shift", lambda: comm.sendrecv(x.data_ptr(), nbytes, (rank + 1) % world, y.data_ptr(),
+                                                       nbytes, (rank - 1) % world, 0, 0, sp), nbytes, 1.0)
     del x, y
     torch.cuda.empty_cache()
     return res

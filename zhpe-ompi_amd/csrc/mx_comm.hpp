@@ -28,9 +28,9 @@ constexpr size_t FLAG_WORDS = OS_COUNTER + 8;
 //   filled[src][lane]    my flags: chunks src has written into my lane
 //   seen[dst][lane]      my flags (written by dst): envelopes dst has read
 //   drained[dst][lane]   my flags (written by dst): chunks dst has consumed
-constexpr int P2P_L = 16;
+constexpr int P2P_L = 64;
 constexpr int P2P_S = 4;
-constexpr size_t P2P_C = 32 << 10;
+constexpr size_t P2P_C = 64 << 10;
 constexpr int P2P_H = 8;
 constexpr size_t P2P_HDR = 64;
 constexpr size_t P2P_BOX = 4096 + (size_t)P2P_L * P2P_S * P2P_C;
