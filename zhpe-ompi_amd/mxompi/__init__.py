@@ -125,11 +125,17 @@ def check(rc: int, what: str = "mx call") -> int:
 
 
 def _slot(v) -> int:
-    return TYPE[v] if isinstance(v, str) else int(v)
+    """Type slot from a slot name ("FLOAT"), an MPI datatype name ("MPI_FLOAT") or an int."""
+    if isinstance(v, str):
+        return TYPE[MPI_DTYPE_SLOT[v]] if v.startswith("MPI_") else TYPE[v]
+    return int(v)
 
 
 def _op(v) -> int:
-    return OP[v] if isinstance(v, str) else int(v)
+    """Op index from "SUM", "MPI_SUM" or an int."""
+    if isinstance(v, str):
+        return OP[v[4:] if v.startswith("MPI_") else v]
+    return int(v)
 
 
 def type_size(t) -> int:
