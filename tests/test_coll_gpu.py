@@ -237,6 +237,11 @@ def _mp_worker(rank, n, port, staging, jobs, q):
                 out = torch.zeros(rc[rank] * es + 1, dtype=torch.uint8, device="cuda")
                 comm.reduce_scatter(x.data_ptr(), out.data_ptr(), rc, t, op, alg, st)
                 results.append(out.cpu().numpy()[: rc[rank] * es].tobytes())
+            elif kind == "reduce_scatter_inplace":
+                rc = [count + 3 * r for r in range(n)]
+                x = _dev(gen(t, op, sum(rc), 7000 + rank))
+                comm.reduce_scatter(mxompi.IN_PLACE, x.data_ptr(), rc, t, op, alg, st)
+                results.append(x.cpu().numpy()[: rc[rank] * es].tobytes())
             elif kind == "allgather":
                 x = _dev(gen("UINT8_T", "BAND", count, 7000 + rank))
                 out = torch.zeros(n * count, dtype=torch.uint8, device="cuda")
@@ -325,12 +330,17 @@ def _run_mp(n, jobs, staging=1 << 20):
     for p in procs:
         p.start()
     out = {}
-    for _ in range(n):
-        rank, status, payload = q.get(timeout=300)
-        assert status == "ok", payload
-        out[rank] = payload
-    for p in procs:
-        p.join(timeout=60)
+    try:
+        for _ in range(n):
+            rank, status, payload = q.get(timeout=300)
+            assert status == "ok", payload
+            out[rank] = payload
+    finally:
+        for p in procs:
+            p.join(timeout=60 if len(out) == n else 5)
+            if p.is_alive():      # a failed rank leaves its peers waiting: end them
+                p.terminate()
+                p.join(timeout=10)
     return out
 
 
@@ -344,6 +354,8 @@ def test_multiprocess_ipc_bitexact(n):
             ("allreduce", 3001, "MAXLOC", "FLOAT_INT", "auto"),
             ("reduce_scatter", 1000, "SUM", "FLOAT", "ring"),
             ("reduce_scatter", 10, "SUM", "DOUBLE", "recursive_halving"),
+            ("reduce_scatter", 300001, "SUM", "FLOAT", "ring"),              # blocks > staging: chunked
+            ("reduce_scatter_inplace", 200003, "SUM", "DOUBLE", "recursive_halving"),
             ("allgather", 300001, None, None, None),
             ("shmem", 5003, "MAX", "FLOAT", "auto"),
             ("bcast", 2000003, None, None, None),
@@ -382,7 +394,7 @@ def test_multiprocess_ipc_bitexact(n):
             for r in range(n):
                 golden_io.assert_coll_equal(np.frombuffer(got[r][j], np.uint8), exp[r], mxompi.OP[op],
                                           mxompi.TYPE[t], f"{kind} {alg} rank {r}")
-        elif kind == "reduce_scatter":
+        elif kind in ("reduce_scatter", "reduce_scatter_inplace"):
             rc = [count + 3 * r for r in range(n)]
             xs = [gen(t, op, sum(rc), 7000 + r) for r in range(n)]
             exp = [np.zeros(c * es, np.uint8) for c in rc]

@@ -53,6 +53,7 @@ JOBS = [
     ("ireduce", 999, "MIN", "FLOAT", "binomial", "root_inplace"),
     ("ireduce", 5000, "SUM", "FLOAT", "rabenseifner", "root_last"),
     ("ireduce_scatter", 1000, "SUM", "FLOAT", "auto", False),
+    ("ireduce_scatter", 70001, "SUM", "DOUBLE", "auto", True),       # in place, blocks > staging
     ("ireduce_scatter_block", 3000, "SUM", "DOUBLE", "auto", True),
     ("iscan", 20001, "SUM", "FLOAT", "auto", False),
     ("iexscan", 4097, "SUM", "DOUBLE", "recursive_doubling", False),
@@ -114,8 +115,11 @@ def _nb_worker(rank, n, port, q):
             elif kind == "ireduce_scatter":
                 rc = [count + 3 * p for p in range(n)]
                 x = _dev(gen(t, op, sum(rc), _seed(j, rank)))
-                out = torch.zeros(rc[rank] * es, dtype=torch.uint8, device="cuda")
-                posted.append((j, comm.ireduce_scatter(x.data_ptr(), out.data_ptr(), rc, t, op, st), out, x))
+                if extra:
+                    posted.append((j, comm.ireduce_scatter(mxompi.IN_PLACE, x.data_ptr(), rc, t, op, st), x, None))
+                else:
+                    out = torch.zeros(rc[rank] * es, dtype=torch.uint8, device="cuda")
+                    posted.append((j, comm.ireduce_scatter(x.data_ptr(), out.data_ptr(), rc, t, op, st), out, x))
             elif kind == "ireduce_scatter_block":
                 x = _dev(gen(t, op, count * n, _seed(j, rank)))
                 r = comm.ireduce_scatter_block(mxompi.IN_PLACE, x.data_ptr(), count, t, op, st)
@@ -190,12 +194,17 @@ def _run(n):
     for p in procs:
         p.start()
     out = {}
-    for _ in range(n):
-        rank, status, payload = q.get(timeout=300)
-        assert status == "ok", payload
-        out[rank] = payload
-    for p in procs:
-        p.join(timeout=60)
+    try:
+        for _ in range(n):
+            rank, status, payload = q.get(timeout=300)
+            assert status == "ok", payload
+            out[rank] = payload
+    finally:
+        for p in procs:
+            p.join(timeout=60 if len(out) == n else 5)
+            if p.is_alive():      # a failed rank leaves its peers waiting: end them
+                p.terminate()
+                p.join(timeout=10)
     return out
 
 

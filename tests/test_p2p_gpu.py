@@ -182,12 +182,17 @@ def _run(n):
     for p in procs:
         p.start()
     out = {}
-    for _ in range(n):
-        rank, status, payload = q.get(timeout=300)
-        assert status == "ok", payload
-        out[rank] = payload
-    for p in procs:
-        p.join(timeout=60)
+    try:
+        for _ in range(n):
+            rank, status, payload = q.get(timeout=300)
+            assert status == "ok", payload
+            out[rank] = payload
+    finally:
+        for p in procs:
+            p.join(timeout=60 if len(out) == n else 5)
+            if p.is_alive():      # a failed rank leaves its peers waiting: end them
+                p.terminate()
+                p.join(timeout=10)
     return out
 
 

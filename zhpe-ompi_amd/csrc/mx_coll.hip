@@ -996,40 +996,49 @@ extern "C" int mx_reduce_scatter(mx_comm_t *c, const void *sbuf, void *rbuf, con
   std::vector<Seg> segs;
   int rc = reduce_scatter_segments(alg, n, rcounts, es, r, segs);
   if (rc) return rc;
-  const size_t slot = rup(maxc * es + 16, 256);
-  if (slot * n > c->main_bytes) return MX_ERR_NOMEM;  // caller delegates (coll component)
-  const uint64_t g = ++c->gen;
-  if ((rc = wait_all(c, FLAG_DONE, g - 1, s))) return rc;
-  CopyArgs ca;
-  memset(&ca, 0, sizeof ca);
-  for (int p = 0; p < n; p++) {
-    if (p == r || !rcounts[p]) continue;
-    ca.j[ca.n++] = CopyJob{sb + disp[p] * es, c->peer_staging[p] + (size_t)r * slot + ((disp[p] * es) & 15),
-                           rcounts[p] * es};
-  }
-  if ((rc = copy_launch(ca, s))) return rc;
-  if ((rc = signal_all(c, FLAG_READY, g << 1, s))) return rc;
-  if ((rc = wait_all(c, FLAG_READY, g << 1, s))) return rc;
-  if (rcounts[r]) {
-    const size_t mis = (disp[r] * es) & 15;
-    const char *sp[MAXR];
-    for (int j = 0; j < n; j++) sp[j] = (j == r) ? sb + disp[r] * es : c->staging + (size_t)j * slot + mis;
-    // IN_PLACE with disp[r] != 0: the result goes to rbuf[0..] which may
-    // overlap my own input still being read -> fold into the gather area
-    // first, then copy.
-    const bool overlap = (sb == (const char *)rbuf) && disp[r] != 0;
-    char *dst = overlap ? c->staging + n * slot + mis : (char *)rbuf;
-    if (overlap && n * slot + mis + rcounts[r] * es > c->main_bytes) return MX_ERR_NOMEM;
-    char *dp[1] = {dst};
-    for (const Seg &sg : segs)
-      if ((rc = run_fold(c, fl, sg, disp[r], sp, n, dp, 1, es, s))) return rc;
-    if (overlap) {
-      memset(&ca, 0, sizeof ca);
-      ca.j[ca.n++] = CopyJob{dst, (char *)rbuf, rcounts[r] * es};
-      if ((rc = copy_launch(ca, s))) return rc;
+  // IN_PLACE with my block not first: my result would overwrite input still
+  // to be read -> fold into a spare slot after the n slots, then copy
+  // (the slot geometry must be the same on every rank: it depends only on
+  // the collective IN_PLACE choice, not on this rank's block)
+  const bool inplace = sb == (const char *)rbuf;
+  const bool overlap = inplace && disp[r] != 0;
+  const size_t nslots = (size_t)n + (inplace ? 1 : 0);
+  // chunks of every block (piece k0 of block q goes to rank q's slot r):
+  // blocks of any size run through the staging
+  size_t kc = maxc;
+  while (kc > 1 && nslots * rup(kc * es + 16, 256) > c->main_bytes) kc = (kc + 1) / 2;
+  const size_t slot = rup(kc * es + 16, 256);
+  if (nslots * slot > c->main_bytes) return MX_ERR_NOMEM;
+  for (size_t k0 = 0; k0 < maxc; k0 += kc) {
+    const uint64_t g = ++c->gen;
+    if ((rc = wait_all(c, FLAG_DONE, g - 1, s))) return rc;
+    CopyArgs ca;
+    memset(&ca, 0, sizeof ca);
+    for (int p = 0; p < n; p++) {
+      if (p == r || k0 >= rcounts[p]) continue;
+      const size_t e0 = disp[p] + k0;
+      ca.j[ca.n++] = CopyJob{sb + e0 * es, c->peer_staging[p] + (size_t)r * slot + ((e0 * es) & 15),
+                             std::min(kc, rcounts[p] - k0) * es};
     }
+    prof_begin(c, s);
+    if ((rc = copy_launch(ca, s))) return rc;
+    prof_end(c, s, 1, 0);
+    if ((rc = signal_all(c, FLAG_READY, g << 1, s))) return rc;
+    if ((rc = wait_all(c, FLAG_READY, g << 1, s))) return rc;
+    if (k0 < rcounts[r]) {
+      const size_t kl = std::min(kc, rcounts[r] - k0), e0 = disp[r] + k0, mis = (e0 * es) & 15;
+      const char *sp[MAXR];
+      for (int j = 0; j < n; j++) sp[j] = (j == r) ? sb + e0 * es : c->staging + (size_t)j * slot + mis;
+      char *dst = overlap ? c->staging + (size_t)n * slot + mis : (char *)rbuf + k0 * es;
+      char *dp[1] = {dst};
+      for (const Seg &sg : segs) {
+        const Seg piece{std::max(sg.lo, e0), std::min(sg.hi, e0 + kl), sg.p};
+        if (piece.lo < piece.hi && (rc = run_fold(c, fl, piece, e0, sp, n, dp, 1, es, s))) return rc;
+      }
+      if (overlap && (rc = copy_async((char *)rbuf + k0 * es, dst, kl * es, s))) return rc;
+    }
+    if ((rc = signal_all(c, FLAG_DONE, g, s))) return rc;
   }
-  if ((rc = signal_all(c, FLAG_DONE, g, s))) return rc;
   return finish(c, s);
 }
 
@@ -1582,7 +1591,7 @@ static int vm_scatter_blocks(mx_comm *c, vm_launch_fn vl, const VmProg &p, const
   // IN_PLACE with my block starting inside the range my result overwrites:
   // fold into a spare slot after the n slots, then copy
   const bool overlap = sb == rb && disp[r] != 0 && disp[r] < rcounts[r];
-  const size_t nslots = (size_t)n + (overlap ? 1 : 0);
+  const size_t nslots = (size_t)n + (sb == rb ? 1 : 0);   // same geometry on every rank
   size_t kc = maxc;
   while (kc > 1 && nslots * rup(kc * es + 16, 256) > c->main_bytes) kc = (kc + 1) / 2;
   const size_t slot = rup(kc * es + 16, 256);
