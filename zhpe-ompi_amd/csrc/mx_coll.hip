@@ -115,7 +115,14 @@ int copy_async(void *dst, const void *src, size_t bytes, hipStream_t s) {
 // cross-GPU flags: generation-tagged, system scope, bounded spin
 // ---------------------------------------------------------------------------
 
-constexpr size_t kOneShotMax = 64 << 10;   // bytes per rank
+constexpr size_t kOneShotMax = 256 << 10;  // bytes per rank (default; MX_ONESHOT_MAX overrides)
+
+static size_t oneshot_max() {
+  const char *e = getenv("MX_ONESHOT_MAX");
+  if (!e || !*e) return kOneShotMax;
+  const long long v = atoll(e);
+  return v > 0 ? (size_t)v : 0;
+}
 
 struct SignalArgs { uint64_t *peer_flag[MAXR]; int n; uint64_t value; };
 
@@ -263,7 +270,7 @@ extern "C" int mx_comm_create_ex(int rank, int size, int device, size_t staging_
     if (!all) goto fail;
     c->staging_bytes = staging_bytes ? staging_bytes : ((size_t)64 << 20);
     // one-shot region at the top of staging: 2 parities x n slots
-    c->os_max = std::min<size_t>(kOneShotMax, c->staging_bytes / (8 * (size_t)size)) & ~(size_t)255;
+    c->os_max = std::min<size_t>(oneshot_max(), c->staging_bytes / (8 * (size_t)size)) & ~(size_t)255;
     if (c->os_max < 1024) c->os_max = 0;
     c->os_slot = c->os_max ? c->os_max + 256 : 0;
     c->main_bytes = (c->staging_bytes - 2 * (size_t)size * c->os_slot) & ~(size_t)255;

@@ -34,7 +34,7 @@ constexpr int kFB = 256;  // fold / copy block size
 // own combination depend on it, and the element parts are folded by other
 // ranks); PUSHED and DONE carry the plain generation.
 enum { FLAG_READY = 0, FLAG_PUSHED = 1, FLAG_DONE = 2, NFLAGS = 3 };
-constexpr int OSWG = 16;
+constexpr int OSWG = 64;
 constexpr int OS_MAXSEG = 16;
 
 // ---------------------------------------------------------------------------
