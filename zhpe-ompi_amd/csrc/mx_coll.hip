@@ -51,12 +51,15 @@ namespace mx {
 // multi-job byte copy (scatter push, gather, allgather, bcast)
 // ---------------------------------------------------------------------------
 struct CopyJob { const char *src; char *dst; size_t bytes; };
-struct CopyArgs { CopyJob j[MAXR]; int n; };
+struct CopyArgs { CopyJob j[MAXR]; int n; unsigned bpj; };
 
+// Jobs are interleaved block by block (job = blockIdx.x % n): a push to
+// n-1 peers keeps every xGMI link busy from the first wave on, instead of
+// draining the peers one after another in dispatch order.
 template <bool NT>
 __global__ void __launch_bounds__(kFB) k_copy(CopyArgs a) {
-  const CopyJob jb = a.j[blockIdx.y];
-  const size_t tid = (size_t)blockIdx.x * kFB + threadIdx.x;
+  const CopyJob jb = a.j[blockIdx.x % (unsigned)a.n];
+  const size_t tid = (size_t)(blockIdx.x / (unsigned)a.n) * kFB + threadIdx.x;
   const uintptr_t ms = (uintptr_t)jb.src & 15, md = (uintptr_t)jb.dst & 15;
   if (ms == md) {
     size_t head = ms ? 16 - ms : 0;
@@ -72,7 +75,7 @@ __global__ void __launch_bounds__(kFB) k_copy(CopyArgs a) {
     if (tid < head) jb.dst[tid] = jb.src[tid];
     if (tid < jb.bytes - tail0) jb.dst[tail0 + tid] = jb.src[tail0 + tid];
   } else {
-    for (size_t i = tid; i < jb.bytes; i += (size_t)gridDim.x * kFB) jb.dst[i] = jb.src[i];
+    for (size_t i = tid; i < jb.bytes; i += (size_t)a.bpj * kFB) jb.dst[i] = jb.src[i];
   }
 }
 
@@ -89,10 +92,12 @@ static int copy_launch(CopyArgs &a, hipStream_t s) {
   a.n = k;
   if (k == 0) return MX_SUCCESS;
   const size_t g = (maxw + kFB - 1) / kFB;
+  if (g * (size_t)k * kFB > 0xffffffffu) return MX_ERR_UNSUPPORTED;   // HIP: grid threads < 2^32
+  a.bpj = (unsigned)g;
   if (mx_nt_for(2 * total))
-    hipLaunchKernelGGL(k_copy<true>, dim3((unsigned)g, (unsigned)k), dim3(kFB), 0, s, a);
+    hipLaunchKernelGGL(k_copy<true>, dim3((unsigned)(g * k)), dim3(kFB), 0, s, a);
   else
-    hipLaunchKernelGGL(k_copy<false>, dim3((unsigned)g, (unsigned)k), dim3(kFB), 0, s, a);
+    hipLaunchKernelGGL(k_copy<false>, dim3((unsigned)(g * k)), dim3(kFB), 0, s, a);
   return mx_check_launch();
 }
 
