@@ -109,7 +109,7 @@ def test_device_pack_unpack_match_reference(rec):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("shift", [0, 3])
+@pytest.mark.parametrize("shift", [0, 3, 4, 8])
 @pytest.mark.parametrize("name", ["vector_f32_b1_s2", "vector_f32_b4_s8", "vector_f32_b16_s32",
                                   "vector_f32_b64_s128", "indexed_f32_random", "struct_char_d3_int_resized48",
                                   "ref_lower_matrix_47", "ref_strange", "ref_blacs_indexed"])

@@ -120,7 +120,7 @@ def sweep_sizes(torch, mx, max_bytes, iters):
     return rows
 
 
-PACK_TYPES = ["vector_f32_b1_s2", "vector_f32_b4_s8", "vector_f32_b16_s32", "vector_f32_b64_s128",
+PACK_TYPES = ["vector_f32_b1_s2", "vector_f64_b3_s5", "vector_f32_b4_s8", "vector_f32_b16_s32", "vector_f32_b64_s128",
               "indexed_f32_random", "struct_char_d3_int_resized48"]
 
 

@@ -187,6 +187,66 @@ __global__ void __launch_bounds__(kCB) k_convert(ConvArgs a) {
 }
 
 // ---------------------------------------------------------------------------
+// VEC kernel: the layout is ONE strided 1-level run (what MPI_Type_vector /
+// hvector and resized contiguous types flatten to): block l of instance i
+// lives at  i*ext + disp + l*stride1, blen bytes, cnt1 blocks per instance,
+// and every piece is a whole number of aligned W-byte words (W = 4 or 8).
+// Consecutive lanes own consecutive W-byte words of a workgroup's stretch
+// of the stream, so the packed side is one coalesced access per wave
+// instruction and the user side touches only the lines holding data.  The
+// stretch start is mapped once (two multiply-shift divisions); each word is
+// mapped from it in 32-bit arithmetic (float-reciprocal quotient by blen,
+// made exact by the remainder correction), with no LDS phase and no barrier.
+// kVIt words per lane are loaded before any is stored.
+// ---------------------------------------------------------------------------
+constexpr int kVIt = 8;
+constexpr uint64_t kVecMaxBlen = (uint64_t)1 << 22;   // keeps t / blen exact in fp32 + 1 correction
+
+template <int W, bool PACK>
+__global__ void __launch_bounds__(kCB) k_convert_vec(ConvArgs a, DRun R, float rblen) {
+  using U = typename unit_t<W>::T;
+  const uint64_t nw = a.len / W;
+  const uint64_t wbase = (uint64_t)blockIdx.x * (kCB * kVIt);
+  const uint64_t p0 = a.offset + wbase * W;   // stream byte where this stretch starts
+  const uint64_t B0 = udiv(p0, R.mblen);      // global block index (S = cnt1 * blen)
+  const uint32_t o0 = (uint32_t)(p0 - B0 * R.blen);
+  const uint64_t i0 = udiv(B0, R.mcnt1);
+  const uint64_t l0 = B0 - i0 * R.cnt1;
+  const uint32_t blen = (uint32_t)R.blen;
+  U v[kVIt];
+  U *ua[kVIt];
+#pragma unroll
+  for (int k = 0; k < kVIt; k++) {
+    const uint32_t rel = (uint32_t)(k * kCB + threadIdx.x);
+    if (wbase + rel < nw) {
+      const uint32_t t = o0 + rel * W;
+      uint32_t q = (uint32_t)((float)t * rblen);
+      int32_t r = (int32_t)(t - q * blen);
+      if (r < 0) { q--; r += (int32_t)blen; }
+      if (r < 0) { q--; r += (int32_t)blen; }
+      if (r >= (int32_t)blen) { q++; r -= (int32_t)blen; }
+      if (r >= (int32_t)blen) { q++; r -= (int32_t)blen; }
+      uint64_t l1 = l0 + q, inst = i0;
+      if (l1 >= R.cnt1) {
+        const uint64_t d = udiv(l1, R.mcnt1);
+        inst += d;
+        l1 -= d * R.cnt1;
+      }
+      ua[k] = reinterpret_cast<U *>(a.user + (int64_t)inst * a.ext + R.disp + (int64_t)l1 * R.stride1 + r);
+      v[k] = PACK ? *ua[k] : reinterpret_cast<const U *>(a.packed)[wbase + rel];
+    }
+  }
+#pragma unroll
+  for (int k = 0; k < kVIt; k++) {
+    const uint32_t rel = (uint32_t)(k * kCB + threadIdx.x);
+    if (wbase + rel < nw) {
+      if (PACK) reinterpret_cast<U *>(a.packed)[wbase + rel] = v[k];
+      else *ua[k] = v[k];
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
 // TILE kernels (pieces narrower than 16 bytes): a workgroup owns kTP bytes
 // of the stream.  PACK loads the user span the tile reads (monotonic
 // layouts: [addr(first byte), addr(last byte)]) into LDS with 16-byte
@@ -543,6 +603,16 @@ extern "C" int mx_ddt_span(const mx_ddt_t *d, size_t count, int64_t *lo, int64_t
   return MX_SUCCESS;
 }
 
+// MX_CONV_VEC=0 sends single-run layouts to the general kernels instead
+// (A/B measurement switch; results are identical).
+static bool conv_vec_enabled() {
+  static const int on = [] {
+    const char *e = getenv("MX_CONV_VEC");
+    return (e && *e == '0') ? 0 : 1;
+  }();
+  return on != 0;
+}
+
 template <bool PACK>
 static int convert(const mx_ddt_t *d, size_t count, char *user, char *packed, size_t offset, size_t len,
                    void *stream) {
@@ -571,6 +641,21 @@ static int convert(const mx_ddt_t *d, size_t count, char *user, char *packed, si
   u = gcd64(u, len & 15 ? (len & 15) : 16);
   if (!a.pk_vec) u = gcd64(u, (uintptr_t)packed & 15);
   const size_t run_lds = a.nruns <= kLdsRuns ? (size_t)a.nruns * sizeof(DRun) : 0;
+  // one strided 1-level run of whole aligned 4/8-byte words: the VEC kernel
+  // (16-byte-granular layouts stay on k_convert<16>: measured 3.9 vs 2.8 TB/s
+  // for 16-byte blocks at 1 GiB, while 4-byte blocks go 2.1 -> 3.5 TB/s here;
+  // profiles/r01/convertor_vec_ab.txt)
+  if (a.nruns == 1 && d->host[0].cnt2 == 1 && u % 4 == 0 && u != 16 && d->host[0].blen <= kVecMaxBlen &&
+      conv_vec_enabled()) {
+    const DRun &R = d->host[0];
+    const uint64_t W = (u % 8 == 0) ? 8 : 4;
+    const uint64_t nw = len / W;
+    const dim3 grid((unsigned)((nw + kCB * kVIt - 1) / (kCB * kVIt))), block(kCB);
+    const float rblen = 1.0f / (float)R.blen;
+    if (W == 8) hipLaunchKernelGGL((k_convert_vec<8, PACK>), grid, block, 0, s, a, R, rblen);
+    else hipLaunchKernelGGL((k_convert_vec<4, PACK>), grid, block, 0, s, a, R, rblen);
+    return mx_check_launch();
+  }
   if (u == 16) {
     const uint64_t g = (len + 15) / 16;
     hipLaunchKernelGGL((k_convert<16, PACK>), dim3((unsigned)((g + kCB - 1) / kCB)), dim3(kCB), run_lds, s, a);
