@@ -124,12 +124,12 @@ PACK_TYPES = ["vector_f32_b1_s2", "vector_f64_b3_s5", "vector_f32_b4_s8", "vecto
               "indexed_f32_random", "struct_char_d3_int_resized48"]
 
 
-def sweep_pack(torch, mx, max_packed, iters):
+def sweep_pack(torch, mx, max_packed, iters, types=None, min_packed=8):
     import golden_io
     _, recs = golden_io.ddt_records()
     sp = torch.cuda.current_stream().cuda_stream
     rows = []
-    for name in PACK_TYPES:
+    for name in (types or PACK_TYPES):
         rec = next(r for r in recs if r["name"] == name)
         dt = mx.Datatype(rec["desc"].tobytes(), rec["nrec"], rec["size"], rec["lb"], rec["ub"])
         ext = rec["ub"] - rec["lb"]
@@ -139,6 +139,8 @@ def sweep_pack(torch, mx, max_packed, iters):
         P = torch.empty(top * rec["size"], dtype=torch.uint8, device="cuda")
         ubase = U.data_ptr() - rec["true_lb"]
         packed = 8
+        while packed < min_packed:
+            packed *= 8 if packed < (1 << 29) else 2
         while packed <= max_packed:
             count = packed // rec["size"]
             if count >= 1:
@@ -170,6 +172,8 @@ def main():
     ap.add_argument("--iters", type=int, default=5)
     ap.add_argument("--pair-bytes", type=int, default=1 << 30)
     ap.add_argument("--max-bytes", type=int, default=4 << 30)
+    ap.add_argument("--min-bytes", type=int, default=8)
+    ap.add_argument("--types", default="", help="comma-separated golden type names for the pack sweep")
     args = ap.parse_args()
     import torch
     import mxompi as mx
@@ -184,7 +188,8 @@ def main():
         doc["sizes"] = sweep_sizes(torch, mx, args.max_bytes, args.iters)
         torch.cuda.empty_cache()
     if "pack" in what:
-        doc["pack"] = sweep_pack(torch, mx, args.max_bytes, args.iters)
+        doc["pack"] = sweep_pack(torch, mx, args.max_bytes, args.iters,
+                                 [t for t in args.types.split(",") if t] or None, args.min_bytes)
     os.makedirs(os.path.dirname(os.path.abspath(args.out)), exist_ok=True)
     with open(args.out, "w") as f:
         json.dump(doc, f, indent=1)

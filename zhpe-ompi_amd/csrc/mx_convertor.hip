@@ -258,9 +258,17 @@ __global__ void __launch_bounds__(kCB) k_convert_vec(ConvArgs a, DRun R, float r
 // One mapping (three multiply-shift divisions) per lane instead of one per
 // byte; HBM sees only wide accesses.
 // ---------------------------------------------------------------------------
-constexpr int kTP = 8192;                  // stream bytes per tile
-constexpr int kChunk = kTP / kCB;          // 32 bytes per lane
-constexpr int kSpanCap = 3 * kTP;          // user bytes a PACK tile may stage
+// TP = stream bytes per tile (TP / kCB per lane); a PACK tile may stage up
+// to 3 * TP user bytes.  Each piece's user address is advanced in place
+// (next block: + stride1; next outer block / run / instance: from the
+// instance base) instead of being recomputed with 64-bit multiplies.
+template <int TP> struct TileGeom {
+  static constexpr int kChunk = TP / kCB;
+  static constexpr int kSpanCap = 3 * TP;
+  static constexpr size_t lds(bool pack, size_t run_bytes) {
+    return TP + 16 + (pack ? kSpanCap + 32 : 0) + run_bytes;
+  }
+};
 
 __device__ __forceinline__ uint32_t lds_word(const char *s) {  // 4 bytes at any alignment
   const uintptr_t u = (uintptr_t)s;
@@ -306,8 +314,9 @@ __device__ __forceinline__ void tile_move(char *lds, char *glob, uint64_t nbytes
   }
 }
 
-template <bool PACK>
+template <bool PACK, int TP>
 __global__ void __launch_bounds__(kCB) k_convert_tile(ConvArgs a, int nruns_lds, int wordpar) {
+  constexpr int kTP = TP, kChunk = TileGeom<TP>::kChunk, kSpanCap = TileGeom<TP>::kSpanCap;
   extern __shared__ __align__(16) char smem[];
   char *pk = smem;                                   // kTP (+16 slack)
   char *span = smem + kTP + 16;                      // kSpanCap (+32 slack), PACK only
@@ -369,17 +378,37 @@ __global__ void __launch_bounds__(kCB) k_convert_tile(ConvArgs a, int nruns_lds,
   const uint64_t c1 = c0 + kChunk < r1 ? c0 + kChunk : r1;
   if (c0 < c1) {
     Pos P = map_pos(runs, a.nruns, a.S, a.mS, a.offset + c0);
-    DRun R = runs[P.r];
+    const DRun *R = &runs[P.r];
+    int64_t ibase = (int64_t)P.inst * a.ext;                       // instance origin
+    int64_t obase = ibase + R->disp + (int64_t)P.l2 * R->stride2;  // outer block origin
+    int64_t ua = obase + (int64_t)P.l1 * R->stride1 + (int64_t)P.o;
     uint64_t pos = c0;
     while (pos < c1) {
-      const uint64_t avail = R.blen - P.o, want = c1 - pos;
+      const uint64_t blen = R->blen;
+      const uint64_t avail = blen - P.o, want = c1 - pos;
       const uint64_t n = avail < want ? avail : want;
-      const int64_t ua = block_addr(P, R, a.ext) + (int64_t)P.o;
       if (PACK) lds_copy(pk + (pos - r0), span + ((uintptr_t)a.user + ua - lo), n);
       else lds_to_global(a.user + ua, pk + (pos - r0), n);
       pos += n;
       P.o += n;
-      if (P.o == R.blen) next_block(P, runs, a.nruns, R);
+      ua += (int64_t)n;
+      if (P.o == blen) {
+        P.o = 0;
+        if (++P.l1 < R->cnt1) {
+          ua += R->stride1 - (int64_t)blen;
+        } else {
+          P.l1 = 0;
+          if (++P.l2 < R->cnt2) {
+            obase += R->stride2;
+          } else {
+            P.l2 = 0;
+            if (++P.r == a.nruns) { P.r = 0; ibase += a.ext; }
+            R = &runs[P.r];
+            obase = ibase + R->disp;
+          }
+          ua = obase;
+        }
+      }
     }
   }
   if (PACK) {
@@ -613,6 +642,17 @@ static bool conv_vec_enabled() {
   return on != 0;
 }
 
+// Tile size of the TILE kernels (MX_CONV_TP = 2048 / 4096 / 8192 for
+// measurement; results are identical).
+static int conv_tile_bytes() {
+  static const int tp = [] {
+    const char *e = getenv("MX_CONV_TP");
+    const int v = e ? atoi(e) : 0;
+    return (v == 2048 || v == 4096 || v == 8192) ? v : 8192;
+  }();
+  return tp;
+}
+
 template <bool PACK>
 static int convert(const mx_ddt_t *d, size_t count, char *user, char *packed, size_t offset, size_t len,
                    void *stream) {
@@ -665,13 +705,19 @@ static int convert(const mx_ddt_t *d, size_t count, char *user, char *packed, si
   // tile's user bytes form one span)
   if (!PACK || d->monotonic) {
     const int nlds = a.nruns <= 64 ? 1 : 0;
-    const size_t lds = kTP + 16 + (PACK ? kSpanCap + 32 : 0) + (nlds ? (size_t)a.nruns * sizeof(DRun) : 0);
-    const uint64_t tiles = (len + kTP - 1) / kTP;
+    const size_t rb = nlds ? (size_t)a.nruns * sizeof(DRun) : 0;
+    const int tp = conv_tile_bytes();
     // narrow 4-byte-aligned blocks: word-parallel stores (see the kernel)
     uint64_t maxblen = 0;
     for (const DRun &r : d->host) maxblen = std::max<uint64_t>(maxblen, r.blen);
     const int wordpar = !PACK && (u % 4) == 0 && maxblen <= 32;
-    hipLaunchKernelGGL((k_convert_tile<PACK>), dim3((unsigned)tiles), dim3(kCB), lds, s, a, nlds, wordpar);
+#define MX_TILE_LAUNCH(TPV)                                                                          \
+  hipLaunchKernelGGL((k_convert_tile<PACK, TPV>), dim3((unsigned)((len + TPV - 1) / TPV)), dim3(kCB),     \
+                     TileGeom<TPV>::lds(PACK, rb), s, a, nlds, wordpar)
+    if (tp == 2048) MX_TILE_LAUNCH(2048);
+    else if (tp == 4096) MX_TILE_LAUNCH(4096);
+    else MX_TILE_LAUNCH(8192);
+#undef MX_TILE_LAUNCH
     return mx_check_launch();
   }
   const dim3 grid((unsigned)(((len + 15) / 16 + kCB - 1) / kCB)), block(kCB);
