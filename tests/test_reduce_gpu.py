@@ -123,6 +123,24 @@ def test_full_size_fp32_sum_1gib():
     np.testing.assert_array_equal(got.view(np.uint32), b.view(np.uint32))
 
 
+@pytest.mark.parametrize("shift", [0, 1, 3])
+def test_streaming_instance_ragged(shift):
+    """The non-temporal, XCD-mapped K1 instance (>= 384 MiB footprint) on a
+    count that leaves a partial grid tail and, shifted, a ragged head."""
+    O = oracle_lib.oracle()
+    n = 34_000_001
+    rng = np.random.default_rng(11 + shift)
+    a = rng.uniform(-1, 1, n + shift).astype(np.float32)
+    b = rng.uniform(-1, 1, n + shift).astype(np.float32)
+    A = _dev(a); B = _dev(b)
+    mxompi.reduce2("SUM", "FLOAT", A.data_ptr() + 4 * shift, B.data_ptr() + 4 * shift, n, _stream())
+    torch.cuda.synchronize()
+    got = B.cpu().numpy()
+    exp = b.copy()
+    assert O.mxo_reduce2(3, 15, a[shift:].ctypes.data, exp[shift:].ctypes.data, n, 1) == 0
+    np.testing.assert_array_equal(got.view(np.uint32), exp.view(np.uint32))
+
+
 def test_count_zero_is_noop():
     B = torch.ones(16, device="cuda")
     mxompi.reduce2("SUM", "FLOAT", B.data_ptr(), B.data_ptr(), 0, _stream())
