@@ -268,7 +268,11 @@ int mx_request_free(mx_request_t *req);
  * the envelope tag is checked (MX_ERR_TAG on a mismatch, tag < 0 = any);
  * a longer message than the receive buffer delivers what fits and
  * completes with MX_ERR_TRUNCATE.  `received` / mx_request_status: bytes
- * delivered and the envelope tag. */
+ * delivered and the envelope tag.  A receive may name MX_ANY_SOURCE
+ * (MPI_ANY_SOURCE): it matches the next unconsumed message of whichever
+ * source has one (per-pair order is kept); mx_request_source gives the
+ * matched source (MPI_SOURCE). */
+#define MX_ANY_SOURCE (-1)
 int mx_send(mx_comm_t *comm, const void *buf, size_t bytes, int dst, int tag, void *stream);
 int mx_recv(mx_comm_t *comm, void *buf, size_t bytes, int src, int tag, void *stream, size_t *received);
 int mx_isend(mx_comm_t *comm, const void *buf, size_t bytes, int dst, int tag, void *stream,
@@ -286,6 +290,7 @@ int mx_isend_ddt(mx_comm_t *comm, const void *buf, size_t count, const struct mx
 int mx_irecv_ddt(mx_comm_t *comm, void *buf, size_t count, const struct mx_ddt *ddt, int src,
                  int tag, void *stream, mx_request_t **req);
 int mx_request_status(const mx_request_t *req, size_t *bytes, int *tag);
+int mx_request_source(const mx_request_t *req, int *source);
 
 /* ---- OpenSHMEM reductions (shmem_<type>_<op>_to_all) --------------------
  * The OSHMEM op/type numbering (oshmem/op/op.h: OSHMEM_OP_AND..PROD,

@@ -165,6 +165,35 @@ def _p2p_worker(rank, n, port, q):
             r.free()
         res["a2a"] = [b.cpu().numpy().tobytes() for b in rb]
 
+        # (8) MPI_ANY_SOURCE: every other rank sends two messages to rank 0,
+        # which takes all but one with non-blocking ANY_SOURCE receives
+        # posted at once and the last with a blocking one; after a barrier a
+        # specific-source receive still finds the next message of its pair
+        B = 50001
+        if rank == 0:
+            M = 2 * (n - 1)
+            rbs = [torch.zeros(B, dtype=torch.uint8, device="cuda") for _ in range(M)]
+            reqs = [comm.irecv(b.data_ptr(), B, mxompi.ANY_SOURCE, tag=-1) for b in rbs[:M - 1]]
+            got = []
+            for r, b in zip(reqs, rbs):
+                r.wait()
+                got.append((r.source(), r.status(), b.cpu().numpy().tobytes()))
+                r.free()
+            nb = comm.recv(rbs[M - 1].data_ptr(), B, mxompi.ANY_SOURCE, tag=-1)
+            res["any"] = (got, nb, rbs[M - 1].cpu().numpy().tobytes())
+        else:
+            for k in range(2):
+                m = _dev(_data(5000 + 10 * rank + k, B))
+                comm.send(m.data_ptr(), B, 0, tag=20 + k)
+        dist.barrier()
+        if rank == n - 1:
+            m = _dev(_data(6000, B))
+            comm.send(m.data_ptr(), B, 0, tag=22)
+        elif rank == 0:
+            d = torch.zeros(B, dtype=torch.uint8, device="cuda")
+            comm.recv(d.data_ptr(), B, n - 1, tag=22)
+            res["any_specific"] = d.cpu().numpy().tobytes()
+
         comm.close()
         dist.destroy_process_group()
         q.put((rank, "ok", res))
@@ -221,3 +250,17 @@ def test_point_to_point(n):
     for r in range(n):
         for p in range(n):
             assert got[r]["a2a"][p] == _data(1000 * p + r, 77777).tobytes(), f"a2a {p} -> {r}"
+    got0, nb_last, last = got[0]["any"]
+    expect = {(p, k): _data(5000 + 10 * p + k, 50001).tobytes() for p in range(1, n) for k in range(2)}
+    seen = {p: 0 for p in range(1, n)}
+    payloads = []
+    for src, (nb, tag), data in got0:
+        assert 1 <= src < n, src
+        k = seen[src]                                   # per-pair order holds under ANY_SOURCE
+        assert (nb, tag) == (50001, 20 + k) and data == expect[(src, k)], f"ANY_SOURCE message {k} of {src}"
+        seen[src] += 1
+        payloads.append(data)
+    assert nb_last == 50001
+    payloads.append(last)
+    assert sorted(payloads) == sorted(expect.values())
+    assert got[0]["any_specific"] == _data(6000, 50001).tobytes()

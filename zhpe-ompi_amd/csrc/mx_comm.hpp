@@ -99,6 +99,7 @@ struct mx_comm {
   mx::P2PRecvState *p2p_recv;   // [size]
   hipStream_t p2p_stream[2];
   hipEvent_t p2p_ev;
+  unsigned p2p_any_rr;   // MPI_ANY_SOURCE: source the next pick scans first
 };
 
 

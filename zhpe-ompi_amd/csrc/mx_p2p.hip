@@ -28,7 +28,14 @@
 // Matching: messages of one (source, destination) pair match in order --
 // the i-th receive from a source gets the i-th send to it (the envelope's
 // tag is checked: a mismatch completes the receive with MX_ERR_TAG, tag < 0
-// is MPI_ANY_TAG).  A message longer than the receive buffer delivers what
+// is MPI_ANY_TAG).  A receive from MX_ANY_SOURCE is preceded on the receive
+// stream by a one-thread pick kernel that waits until some source has a
+// posted envelope this process has not consumed yet (scanning from a
+// rotating start, so no source starves) and records it in the request's
+// status; the receive kernel then takes its mailbox and flags from that
+// slot.  Receives run in issue order on one stream, so an ANY_SOURCE
+// receive consumes exactly one message and later receives -- specific or
+// not -- see the channel advanced (MPI only orders messages per pair).  A message longer than the receive buffer delivers what
 // fits and completes with MX_ERR_TRUNCATE (MPI_ERR_TRUNCATE); the status
 // holds the delivered byte count.  Non-contiguous layouts are packed /
 // unpacked by the device convertor (mx_convertor.h) around the stream.
@@ -143,10 +150,42 @@ struct P2PRecvArgs {
   uint64_t *seen;            // sender's flags: seen[me][lane]
   uint64_t *drained;         // sender's flags: drained[me][lane]
   P2PRecvState *st;
-  int64_t *status;           // mapped host: delivered bytes, tag, error
+  int64_t *status;           // mapped host: delivered bytes, tag, error, source
   uint64_t timeout_ticks;
   int *err;
+  // MX_ANY_SOURCE: the fields above are taken for the source the pick
+  // kernel stored in status[3], from these per-source bases
+  int any, me;
+  const char *box0;
+  const uint64_t *flag0;     // my flag array
+  uint64_t *peer_flags[MAXR];
+  P2PRecvState *st0;
 };
+
+// MX_ANY_SOURCE: wait until some source p has posted an envelope beyond what
+// this process consumed from it (lane 0's message count), store p in
+// status[3] (-1 after a timeout).
+__global__ void k_p2p_pick(const uint64_t *flag0, const P2PRecvState *st0, int n, int start, int64_t *status,
+                           uint64_t timeout_ticks, int *err) {
+  if (threadIdx.x != 0) return;
+  const uint64_t t0 = wall_clock64();
+  for (;;) {
+    for (int i = 0; i < n; i++) {
+      const int p = (start + i) % n;
+      if (__hip_atomic_load(flag0 + P2P_POSTED + p, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) >
+          st0[p].lane_msgs[0]) {
+        __hip_atomic_store(&status[3], (int64_t)p, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+        return;
+      }
+    }
+    __builtin_amdgcn_s_sleep(2);
+    if (wall_clock64() - t0 > timeout_ticks) {
+      __hip_atomic_store(&status[3], (int64_t)-1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+      __hip_atomic_store(err, MX_ERR_TIMEOUT, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      return;
+    }
+  }
+}
 
 __global__ void __launch_bounds__(kP2PThreads) k_p2p_recv(P2PRecvArgs a) {
   const int l = blockIdx.x;
@@ -154,15 +193,29 @@ __global__ void __launch_bounds__(kP2PThreads) k_p2p_recv(P2PRecvArgs a) {
   __shared__ int ok;
   __shared__ uint64_t s_bytes;
   __shared__ int64_t s_tag;
+  const char *box = a.box;
+  const uint64_t *posted = a.posted, *filled = a.filled;
+  uint64_t *seen = a.seen, *drained = a.drained;
+  P2PRecvState *st = a.st;
+  if (a.any) {
+    const int p = (int)__hip_atomic_load(&a.status[3], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM);
+    if (p < 0) return;   // the pick timed out (error already raised)
+    box = a.box0 + (size_t)p * P2P_BOX;
+    posted = a.flag0 + P2P_POSTED + p;
+    filled = a.flag0 + P2P_FILLED + (size_t)p * P2P_L;
+    seen = a.peer_flags[p] + P2P_SEEN + (size_t)a.me * P2P_L;
+    drained = a.peer_flags[p] + P2P_DRAINED + (size_t)a.me * P2P_L;
+    st = a.st0 + p;
+  }
   if (threadIdx.x == 0) {
-    const uint64_t m = a.st->lane_msgs[l];
-    ok = p2p_wait_ge(a.posted, m + 1, t0, a.timeout_ticks, a.err);
+    const uint64_t m = st->lane_msgs[l];
+    ok = p2p_wait_ge(posted, m + 1, t0, a.timeout_ticks, a.err);
     if (ok) {
-      const volatile uint64_t *h = reinterpret_cast<const volatile uint64_t *>(a.box + (m % P2P_H) * P2P_HDR);
+      const volatile uint64_t *h = reinterpret_cast<const volatile uint64_t *>(box + (m % P2P_H) * P2P_HDR);
       s_bytes = h[0];
       s_tag = (int64_t)h[1];
-      __hip_atomic_store(a.seen + l, m + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
-      a.st->lane_msgs[l] = m + 1;
+      __hip_atomic_store(seen + l, m + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+      st->lane_msgs[l] = m + 1;
     }
   }
   __syncthreads();
@@ -170,20 +223,20 @@ __global__ void __launch_bounds__(kP2PThreads) k_p2p_recv(P2PRecvArgs a) {
   const uint64_t bytes = s_bytes;
   uint64_t lo, hi;
   p2p_lane(bytes, l, &lo, &hi);
-  uint64_t k = a.st->lane_chunks[l];
+  uint64_t k = st->lane_chunks[l];
   for (uint64_t pos = lo; pos < hi; pos += P2P_C) {
     const uint64_t len = std::min<uint64_t>(P2P_C, hi - pos);
     k++;
-    if (threadIdx.x == 0) ok = p2p_wait_ge(a.filled + l, k, t0, a.timeout_ticks, a.err);
+    if (threadIdx.x == 0) ok = p2p_wait_ge(filled + l, k, t0, a.timeout_ticks, a.err);
     __syncthreads();
     if (!ok) return;
-    const char *slot = a.box + 4096 + ((size_t)l * P2P_S + (size_t)((k - 1) % P2P_S)) * P2P_C;
+    const char *slot = box + 4096 + ((size_t)l * P2P_S + (size_t)((k - 1) % P2P_S)) * P2P_C;
     if (pos < a.cap) p2p_copy(a.buf + pos, slot, std::min<uint64_t>(len, a.cap - pos));
     __syncthreads();          // every load of the slot has returned
-    if (threadIdx.x == 0) __hip_atomic_store(a.drained + l, k, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+    if (threadIdx.x == 0) __hip_atomic_store(drained + l, k, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
   }
   if (threadIdx.x == 0) {
-    a.st->lane_chunks[l] = k;
+    st->lane_chunks[l] = k;
     if (l == 0) {
       a.status[0] = (int64_t)std::min<uint64_t>(bytes, a.cap);
       a.status[1] = s_tag;
@@ -262,6 +315,7 @@ int p2p_enqueue(mx_request *q, hipStream_t *done_stream) {
     if (!q->status && hipHostMalloc((void **)&q->status, 4 * sizeof(int64_t), hipHostMallocMapped) != hipSuccess)
       return MX_ERR_NOMEM;
     memset(q->status, 0, 4 * sizeof(int64_t));
+    q->status[3] = p;
     int64_t *st_dev = nullptr;
     if (hipHostGetDevicePointer((void **)&st_dev, q->status, 0) != hipSuccess) return MX_ERR_HIP;
     P2PRecvArgs a;
@@ -269,12 +323,25 @@ int p2p_enqueue(mx_request *q, hipStream_t *done_stream) {
     a.buf = tmp ? tmp : (char *)q->rbuf;
     a.cap = bytes;
     a.tag = q->tag;
-    a.box = c->staging + c->p2p_off + (size_t)p * P2P_BOX;
-    a.posted = c->flagmem + P2P_POSTED + p;
-    a.filled = c->flagmem + P2P_FILLED + (size_t)p * P2P_L;
-    a.seen = c->peer_flags[p] + P2P_SEEN + (size_t)me * P2P_L;
-    a.drained = c->peer_flags[p] + P2P_DRAINED + (size_t)me * P2P_L;
-    a.st = c->p2p_recv + p;
+    if (p >= 0) {
+      a.box = c->staging + c->p2p_off + (size_t)p * P2P_BOX;
+      a.posted = c->flagmem + P2P_POSTED + p;
+      a.filled = c->flagmem + P2P_FILLED + (size_t)p * P2P_L;
+      a.seen = c->peer_flags[p] + P2P_SEEN + (size_t)me * P2P_L;
+      a.drained = c->peer_flags[p] + P2P_DRAINED + (size_t)me * P2P_L;
+      a.st = c->p2p_recv + p;
+    } else {   // MX_ANY_SOURCE
+      a.any = 1;
+      a.me = me;
+      a.box0 = c->staging + c->p2p_off;
+      a.flag0 = c->flagmem;
+      for (int j = 0; j < c->size; j++) a.peer_flags[j] = c->peer_flags[j];
+      a.st0 = c->p2p_recv;
+      const int start = (int)(c->p2p_any_rr++ % (unsigned)c->size);
+      hipLaunchKernelGGL(k_p2p_pick, dim3(1), dim3(64), 0, s, (const uint64_t *)c->flagmem,
+                         (const P2PRecvState *)c->p2p_recv, c->size, start, st_dev, c->timeout_ticks, c->err_dev);
+      if ((rc = mx_check_launch())) return rc;
+    }
     a.status = st_dev;
     a.timeout_ticks = c->timeout_ticks;
     a.err = c->err_dev;
@@ -294,7 +361,8 @@ namespace {
 
 static int p2p_request(mx_comm_t *c, int kind, int persistent, const void *sbuf, void *rbuf, size_t count,
                        const mx_ddt_t *ddt, int peer, int tag, void *stream, mx_request_t **req) {
-  if (!c || !req || peer < 0 || peer >= c->size) return MX_ERR_ARG;
+  if (!c || !req || peer >= c->size) return MX_ERR_ARG;
+  if (peer < 0 && !(kind == RQ_RECV && peer == MX_ANY_SOURCE)) return MX_ERR_ARG;
   if (count && (kind == RQ_SEND ? !sbuf : !rbuf)) return MX_ERR_ARG;
   mx_request *q;
   int rc = req_create(c, kind, persistent, stream, &q);
@@ -366,6 +434,15 @@ extern "C" int mx_sendrecv(mx_comm_t *c, const void *sbuf, size_t sbytes, int ds
   if (sq) mx_request_free(sq);
   mx_request_free(rq);
   return rc ? rc : wrc ? wrc : rrc;
+}
+
+// MPI_SOURCE of a completed receive request (the matched source for
+// MX_ANY_SOURCE)
+extern "C" int mx_request_source(const mx_request_t *q, int *source) {
+  if (!q || q->kind != RQ_RECV || !q->status || !source) return MX_ERR_ARG;
+  if (q->active) return MX_ERR_STATE;
+  *source = (int)q->status[3];
+  return MX_SUCCESS;
 }
 
 // status of a completed receive request (MPI_Get_count / MPI_TAG)

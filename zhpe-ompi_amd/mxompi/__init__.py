@@ -170,6 +170,7 @@ def sync(stream: int = 0) -> None:
 # collectives (include/mx_coll.h)
 # ---------------------------------------------------------------------------
 IN_PLACE = 1                       # MX_IN_PLACE
+ANY_SOURCE = -1                    # MX_ANY_SOURCE (MPI_ANY_SOURCE)
 COMM_IPC, COMM_RCCL = 1, 2
 ALLREDUCE = {"auto": 0, "basic_linear": 1, "nonoverlapping": 2, "recursive_doubling": 3,
              "ring": 4, "segmented_ring": 5, "rabenseifner": 6, "rccl": 100}
@@ -251,6 +252,7 @@ def _coll_lib():
             getattr(L, name).argtypes = [vp, vp, sz, vp, i, i, vp, rq]
         L.mx_sendrecv.argtypes = [vp, vp, sz, i, i, vp, sz, i, i, vp, ctypes.POINTER(sz)]
         L.mx_request_status.argtypes = [vp, ctypes.POINTER(sz), ctypes.POINTER(i)]
+        L.mx_request_source.argtypes = [vp, ctypes.POINTER(i)]
         L.mx_ireduce_decision.argtypes = [i, sz, i]
         L._mx_coll_typed = True
     return L
@@ -299,6 +301,12 @@ class Request:
         nb, tag = ctypes.c_size_t(), ctypes.c_int()
         check(_coll_lib().mx_request_status(self.h, ctypes.byref(nb), ctypes.byref(tag)), "mx_request_status")
         return nb.value, tag.value
+
+    def source(self):
+        """MPI_SOURCE of a completed receive (the matched rank for ANY_SOURCE)."""
+        src = ctypes.c_int()
+        check(_coll_lib().mx_request_source(self.h, ctypes.byref(src)), "mx_request_source")
+        return src.value
 
     def free(self):
         if getattr(self, "h", None):
