@@ -120,7 +120,12 @@ int copy_async(void *dst, const void *src, size_t bytes, hipStream_t s) {
 // cross-GPU flags: generation-tagged, system scope, bounded spin
 // ---------------------------------------------------------------------------
 
-constexpr size_t kOneShotMax = 256 << 10;  // bytes per rank (default; MX_ONESHOT_MAX overrides)
+// bytes per rank (default; MX_ONESHOT_MAX overrides).  Measured crossover on
+// ranks sharing one GPU: 256 KiB - 1 MiB (tools/lat_probe.py); there every
+// rank's n-1 pushes land in one HBM, over xGMI they spread over n-1 links
+// while the staged path still pays its nine dependent launches, so the
+// one-shot range is set at the top of that bracket.
+constexpr size_t kOneShotMax = 1 << 20;
 
 static size_t oneshot_max() {
   const char *e = getenv("MX_ONESHOT_MAX");
