@@ -1,0 +1,69 @@
+"""MPI_Send/MPI_Recv ping-pong latency between 2 processes sharing the GPU
+(diagnostic): half round trip per size, blocking and Isend/Irecv forms.
+usage: python tools/p2p_lat.py"""
+import os
+import sys
+import time
+
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "zhpe-ompi_amd"))
+
+
+def worker(rank, n, port, q):
+    import torch
+    import torch.distributed as dist
+    import mxompi
+    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=n)
+    torch.cuda.set_device(0)
+    mxompi.init(0)
+
+    def ag(b):
+        out = [None] * n
+        dist.all_gather_object(out, b)
+        return out
+    comm = mxompi.Comm(rank, n, ag, device=0, staging_bytes=64 << 20)
+    x = torch.zeros(4 << 20, dtype=torch.uint8, device="cuda")
+    peer = 1 - rank
+    rows = []
+    for nb in [8, 4096, 65536, 1 << 20]:
+        for form in ("blocking", "nonblocking"):
+            def one():
+                if form == "blocking":
+                    if rank == 0:
+                        comm.send(x.data_ptr(), nb, peer, tag=1)
+                        comm.recv(x.data_ptr(), nb, peer, tag=1)
+                    else:
+                        comm.recv(x.data_ptr(), nb, peer, tag=1)
+                        comm.send(x.data_ptr(), nb, peer, tag=1)
+                else:
+                    if rank == 0:
+                        s = comm.isend(x.data_ptr(), nb, peer, tag=1); s.wait(); s.free()
+                        r = comm.irecv(x.data_ptr(), nb, peer, tag=1); r.wait(); r.free()
+                    else:
+                        r = comm.irecv(x.data_ptr(), nb, peer, tag=1); r.wait(); r.free()
+                        s = comm.isend(x.data_ptr(), nb, peer, tag=1); s.wait(); s.free()
+            for _ in range(10):
+                one()
+            dist.barrier()
+            it = 100
+            t0 = time.perf_counter()
+            for _ in range(it):
+                one()
+            rows.append((nb, form, round((time.perf_counter() - t0) / it / 2 * 1e6, 1)))
+    comm.close()
+    dist.destroy_process_group()
+    q.put((rank, rows))
+
+
+if __name__ == "__main__":
+    import socket
+    import torch.multiprocessing as mp
+    s = socket.socket(); s.bind(("127.0.0.1", 0)); port = s.getsockname()[1]; s.close()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    ps = [ctx.Process(target=worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in ps:
+        p.start()
+    res = dict(q.get(timeout=300) for _ in range(2))
+    for p in ps:
+        p.join(timeout=60)
+    print("p2p half-round-trip us (bytes, form, us):", res[0], flush=True)

@@ -38,6 +38,7 @@
 #include <string.h>
 #include <vector>
 #include <algorithm>
+#include <chrono>
 #include <map>
 #include <new>
 
@@ -2154,7 +2155,7 @@ static int req_post(mx_request *q, mx_request_t **out) {
     const int rc = req_start(q);
     if (rc) {
       (void)hipEventDestroy(q->done);
-      if (q->status) (void)hipHostFree(q->status);
+      mx::p2p_status_put(q->status);
       delete q;
       return rc;
     }
@@ -2195,7 +2196,7 @@ int req_create(mx_comm *c, int kind, int persistent, void *stream, mx_request **
 int req_submit(mx_request *q, mx_request_t **out) { return req_post(q, out); }
 void req_discard(mx_request *q) {
   (void)hipEventDestroy(q->done);
-  if (q->status) (void)hipHostFree(q->status);
+  mx::p2p_status_put(q->status);
   delete q;
 }
 }  // namespace mx
@@ -2328,9 +2329,22 @@ extern "C" int mx_test(mx_request_t *q, int *flag) {
   return req_complete(q);
 }
 
+// MPI_Wait: poll the completion event for up to kWaitSpinUs (a blocking
+// hipEventSynchronize wakes tens of microseconds late, which is most of a
+// small message's latency), then block.
+constexpr double kWaitSpinUs = 2000.0;
+
 extern "C" int mx_wait(mx_request_t *q) {
   if (!q) return MX_ERR_ARG;
   if (!q->active) return MX_SUCCESS;
+  const auto t0 = std::chrono::steady_clock::now();
+  for (;;) {
+    const hipError_t e = hipEventQuery(q->done);
+    if (e == hipSuccess) return req_complete(q);
+    if (e != hipErrorNotReady) return MX_ERR_HIP;
+    if (std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0).count() > kWaitSpinUs)
+      break;
+  }
   if (hipEventSynchronize(q->done) != hipSuccess) return MX_ERR_HIP;
   return req_complete(q);
 }
@@ -2348,7 +2362,7 @@ extern "C" int mx_request_free(mx_request_t *q) {
   int rc = MX_SUCCESS;
   if (q->active) rc = mx_wait(q);   // MPI_Request_free lets an active operation finish
   (void)hipEventDestroy(q->done);
-  if (q->status) (void)hipHostFree(q->status);
+  mx::p2p_status_put(q->status);
   delete q;
   return rc;
 }

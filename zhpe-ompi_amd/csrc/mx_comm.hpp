@@ -134,4 +134,9 @@ int req_submit(mx_request *q, mx_request_t **out);
 void req_discard(mx_request *q);
 int p2p_setup(mx_comm *c);
 void p2p_release(mx_comm *c);
+// receive status blocks (4 x int64, mapped host memory): from a process-wide
+// pool allocated once (never released, so a request may outlive its
+// communicator), else one hipHostMalloc each
+int64_t *p2p_status_get();
+void p2p_status_put(int64_t *st);
 }  // namespace mx

@@ -43,6 +43,7 @@
 #include <string.h>
 
 #include <algorithm>
+#include <mutex>
 
 #include "mx_comm.hpp"
 #include "../../include/mx_convertor.h"
@@ -278,6 +279,46 @@ void p2p_release(mx_comm *c) {
   c->p2p_recv = nullptr;
 }
 
+namespace {
+constexpr int kStatusPool = 4096;
+std::mutex g_status_mu;
+int64_t *g_status_pool;          // kStatusPool blocks of 4 x int64
+int g_status_free[kStatusPool];
+int g_status_nfree = -1;         // -1: not allocated yet
+}  // namespace
+
+int64_t *p2p_status_get() {
+  {
+    std::lock_guard<std::mutex> lk(g_status_mu);
+    if (g_status_nfree < 0) {
+      g_status_nfree = 0;
+      if (hipHostMalloc((void **)&g_status_pool, (size_t)kStatusPool * 4 * sizeof(int64_t), hipHostMallocMapped) ==
+          hipSuccess) {
+        for (int i = 0; i < kStatusPool; i++) g_status_free[i] = kStatusPool - 1 - i;
+        g_status_nfree = kStatusPool;
+      } else {
+        g_status_pool = nullptr;
+      }
+    }
+    if (g_status_nfree > 0) return g_status_pool + (size_t)g_status_free[--g_status_nfree] * 4;
+  }
+  int64_t *st = nullptr;
+  if (hipHostMalloc((void **)&st, 4 * sizeof(int64_t), hipHostMallocMapped) != hipSuccess) return nullptr;
+  return st;
+}
+
+void p2p_status_put(int64_t *st) {
+  if (!st) return;
+  {
+    std::lock_guard<std::mutex> lk(g_status_mu);
+    if (g_status_pool && st >= g_status_pool && st < g_status_pool + (size_t)kStatusPool * 4) {
+      g_status_free[g_status_nfree++] = (int)((st - g_status_pool) / 4);
+      return;
+    }
+  }
+  (void)hipHostFree(st);
+}
+
 // Enqueue request q (RQ_SEND / RQ_RECV) on the internal stream, after the
 // caller's stream; *done_stream receives the stream completion is on.
 int p2p_enqueue(mx_request *q, hipStream_t *done_stream) {
@@ -312,8 +353,7 @@ int p2p_enqueue(mx_request *q, hipStream_t *done_stream) {
     hipLaunchKernelGGL(k_p2p_send, dim3(P2P_L), dim3(kP2PThreads), 0, s, a);
     if ((rc = mx_check_launch())) return rc;
   } else {
-    if (!q->status && hipHostMalloc((void **)&q->status, 4 * sizeof(int64_t), hipHostMallocMapped) != hipSuccess)
-      return MX_ERR_NOMEM;
+    if (!q->status && !(q->status = p2p_status_get())) return MX_ERR_NOMEM;
     memset(q->status, 0, 4 * sizeof(int64_t));
     q->status[3] = p;
     int64_t *st_dev = nullptr;
