@@ -253,9 +253,9 @@ def _mp_worker(rank, n, port, staging, jobs, q):
                 out = torch.zeros(count * 4, dtype=torch.uint8, device="cuda")
                 comm.shmem_reduce("MAX", "FLOAT", 4, out.data_ptr(), x.data_ptr(), count, st)
                 results.append(out.cpu().numpy().tobytes())
-            elif kind == "bcast":
+            elif kind in ("bcast", "bcast_root0"):
                 x = _dev(gen("UINT8_T", "BAND", count, 7000 + rank))
-                comm.bcast(x.data_ptr(), count, n - 1, st)
+                comm.bcast(x.data_ptr(), count, n - 1 if kind == "bcast" else 0, st)
                 results.append(x.cpu().numpy().tobytes())
             elif kind in ("reduce", "reduce_inplace"):
                 root = n - 1 if kind == "reduce" else 0
@@ -359,6 +359,8 @@ def test_multiprocess_ipc_bitexact(n):
             ("allgather", 300001, None, None, None),
             ("shmem", 5003, "MAX", "FLOAT", "auto"),
             ("bcast", 2000003, None, None, None),
+            ("bcast_root0", 5, None, None, None),        # fewer bytes than non-roots: empty parts
+            ("bcast_root0", 1000001, None, None, None),
             # back-to-back one-shot calls (both staging parities, every fold shape)
             ("allreduce", 1000, "SUM", "FLOAT", "auto"),
             ("allreduce", 3000, "SUM", "FLOAT", "ring"),
@@ -463,7 +465,7 @@ def test_multiprocess_ipc_bitexact(n):
             full = np.concatenate([gen("UINT8_T", "BAND", count, 7000 + r) for r in range(n)])
             for r in range(n):
                 np.testing.assert_array_equal(np.frombuffer(got[r][j], np.uint8), full)
-        elif kind == "bcast":
-            root = gen("UINT8_T", "BAND", count, 7000 + n - 1)
+        elif kind in ("bcast", "bcast_root0"):
+            root = gen("UINT8_T", "BAND", count, 7000 + (n - 1 if kind == "bcast" else 0))
             for r in range(n):
                 np.testing.assert_array_equal(np.frombuffer(got[r][j], np.uint8), root)

@@ -1106,6 +1106,19 @@ extern "C" int mx_allgather(mx_comm_t *c, const void *sbuf, void *rbuf, size_t b
   return finish(c, s);
 }
 
+// MPI_Bcast, all-peer scatter + allgather (the reference's large-message
+// bcast pipelines segments down a tree, coll_base_bcast.c:38-300; over
+// point-to-point xGMI a push of the whole buffer from the root loads each
+// of its links with all S bytes).  Per round of l bytes: the root pushes
+// part q (blockcount split over the n-1 non-roots) into non-root q's slot q
+// (S/(n-1) per root link); every non-root forwards its part into the same
+// slot of every other non-root (S/(n-1) per link again) and copies it into
+// its buffer; after PUSHED from the other non-roots each copies their parts
+// out.  Messages up to kBcastDirectMax (and n = 2) take one step: the root
+// pushes the whole round to every peer.  Pure data movement: results are the
+// root's bytes.
+constexpr size_t kBcastDirectMax = 512 << 10;
+
 extern "C" int mx_bcast(mx_comm_t *c, void *buf, size_t bytes, int root, void *stream) {
   if (!c || !buf || root < 0 || root >= c->size) return MX_ERR_ARG;
   if (c->local) {
@@ -1115,27 +1128,59 @@ extern "C" int mx_bcast(mx_comm_t *c, void *buf, size_t bytes, int root, void *s
   }
   hipStream_t s = (hipStream_t)stream;
   if (int orc = order(c, s)) return orc;
-  const int n = c->size, r = c->rank;
+  const int n = c->size, r = c->rank, m = n - 1;
   if (!bytes || n == 1) return MX_SUCCESS;
   if (!(c->flags & MX_COMM_IPC)) return MX_ERR_STATE;
-  const size_t cb = (c->main_bytes - 256) & ~(size_t)255;
+  char *ub = (char *)buf;
+  // n slots (indexed by rank; the root's stays unused), each a part + alignment pad
+  const size_t slot = (c->main_bytes / n) & ~(size_t)255;
+  if (slot < 512) return MX_ERR_NOMEM;
+  const size_t cb = (slot - 32) * (size_t)m;
+  const uint32_t all = (n >= 32) ? 0xffffffffu : ((1u << n) - 1);
+  auto part_of = [&](int rank) { return rank < root ? rank : rank - 1; };   // non-root -> part index
+  const bool direct = bytes <= kBcastDirectMax || m == 1;
   for (size_t o = 0; o < bytes; o += cb) {
     const size_t l = std::min(cb, bytes - o);
+    size_t off[MAXR], len[MAXR];
+    blockcount(l, m, off, len);
     const uint64_t g = ++c->gen;
     int rc;
     if ((rc = wait_all(c, FLAG_DONE, g - 1, s))) return rc;
-    if (r == root) {
-      CopyArgs ca;
-      memset(&ca, 0, sizeof ca);
-      for (int p = 0; p < n; p++)
-        if (p != r) ca.j[ca.n++] = CopyJob{(const char *)buf + o, c->peer_staging[p] + (o & 15), l};
+    auto slot_ptr = [&](char *base, int q) {   // non-root q's part in a staging area
+      const size_t e = o + off[part_of(q)];
+      return base + (size_t)q * slot + (e & 15);
+    };
+    CopyArgs ca;
+    memset(&ca, 0, sizeof ca);
+    if (direct) {   // small message: the root pushes it whole, one dependent step fewer
+      if (r == root) {
+        for (int q = 0; q < n; q++)
+          if (q != root) ca.j[ca.n++] = CopyJob{ub + o, c->peer_staging[q] + (o & 15), l};
+        if ((rc = copy_launch(ca, s))) return rc;
+        if ((rc = signal_all(c, FLAG_READY, g << 1, s))) return rc;
+      } else {
+        if ((rc = wait_mask(c, FLAG_READY, 1u << root, g << 1, s))) return rc;
+        ca.j[ca.n++] = CopyJob{c->staging + (o & 15), ub + o, l};
+        if ((rc = copy_launch(ca, s))) return rc;
+      }
+    } else if (r == root) {
+      for (int q = 0; q < n; q++)
+        if (q != root) ca.j[ca.n++] = CopyJob{ub + o + off[part_of(q)], slot_ptr(c->peer_staging[q], q), len[part_of(q)]};
       if ((rc = copy_launch(ca, s))) return rc;
       if ((rc = signal_all(c, FLAG_READY, g << 1, s))) return rc;
     } else {
+      const int pr = part_of(r);
       if ((rc = wait_mask(c, FLAG_READY, 1u << root, g << 1, s))) return rc;
-      CopyArgs ca;
+      const char *mine = slot_ptr(c->staging, r);
+      for (int q = 0; q < n; q++)
+        if (q != root && q != r) ca.j[ca.n++] = CopyJob{mine, slot_ptr(c->peer_staging[q], r), len[pr]};
+      ca.j[ca.n++] = CopyJob{mine, ub + o + off[pr], len[pr]};
+      if ((rc = copy_launch(ca, s))) return rc;
+      if ((rc = signal_all(c, FLAG_PUSHED, g, s))) return rc;
+      if ((rc = wait_mask(c, FLAG_PUSHED, all & ~(1u << root) & ~(1u << r), g, s))) return rc;
       memset(&ca, 0, sizeof ca);
-      ca.j[ca.n++] = CopyJob{c->staging + (o & 15), (char *)buf + o, l};
+      for (int q = 0; q < n; q++)
+        if (q != root && q != r) ca.j[ca.n++] = CopyJob{slot_ptr(c->staging, q), ub + o + off[part_of(q)], len[part_of(q)]};
       if ((rc = copy_launch(ca, s))) return rc;
     }
     if ((rc = signal_all(c, FLAG_DONE, g, s))) return rc;
