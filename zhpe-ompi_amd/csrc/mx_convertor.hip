@@ -314,9 +314,55 @@ __device__ __forceinline__ void tile_move(char *lds, char *glob, uint64_t nbytes
   }
 }
 
+// One lane's kChunk-byte stretch of tile [r0, r1): PACK copies pieces from
+// the staged user span (LDS, origin `lo`) into the packed tile (LDS),
+// UNPACK stores pieces from the packed tile straight to user memory.
+template <bool PACK, int TP>
+__device__ __forceinline__ void walk_chunk(const ConvArgs &a, const DRun *runs, char *pk, const char *span,
+                                           uintptr_t lo, uint64_t r0, uint64_t r1) {
+  constexpr int kChunk = TileGeom<TP>::kChunk;
+  const uint64_t c0 = r0 + (uint64_t)threadIdx.x * kChunk;
+  const uint64_t c1 = c0 + kChunk < r1 ? c0 + kChunk : r1;
+  if (c0 < c1) {
+    Pos P = map_pos(runs, a.nruns, a.S, a.mS, a.offset + c0);
+    const DRun *R = &runs[P.r];
+    int64_t ibase = (int64_t)P.inst * a.ext;                       // instance origin
+    int64_t obase = ibase + R->disp + (int64_t)P.l2 * R->stride2;  // outer block origin
+    int64_t ua = obase + (int64_t)P.l1 * R->stride1 + (int64_t)P.o;
+    uint64_t pos = c0;
+    while (pos < c1) {
+      const uint64_t blen = R->blen;
+      const uint64_t avail = blen - P.o, want = c1 - pos;
+      const uint64_t n = avail < want ? avail : want;
+      if (PACK) lds_copy(pk + (pos - r0), span + ((uintptr_t)a.user + ua - lo), n);
+      else lds_to_global(a.user + ua, pk + (pos - r0), n);
+      pos += n;
+      P.o += n;
+      ua += (int64_t)n;
+      if (P.o == blen) {
+        P.o = 0;
+        if (++P.l1 < R->cnt1) {
+          ua += R->stride1 - (int64_t)blen;
+        } else {
+          P.l1 = 0;
+          if (++P.l2 < R->cnt2) {
+            obase += R->stride2;
+          } else {
+            P.l2 = 0;
+            if (++P.r == a.nruns) { P.r = 0; ibase += a.ext; }
+            R = &runs[P.r];
+            obase = ibase + R->disp;
+          }
+          ua = obase;
+        }
+      }
+    }
+  }
+}
+
 template <bool PACK, int TP>
 __global__ void __launch_bounds__(kCB) k_convert_tile(ConvArgs a, int nruns_lds, int wordpar) {
-  constexpr int kTP = TP, kChunk = TileGeom<TP>::kChunk, kSpanCap = TileGeom<TP>::kSpanCap;
+  constexpr int kTP = TP, kSpanCap = TileGeom<TP>::kSpanCap;
   extern __shared__ __align__(16) char smem[];
   char *pk = smem;                                   // kTP (+16 slack)
   char *span = smem + kTP + 16;                      // kSpanCap (+32 slack), PACK only
@@ -374,46 +420,97 @@ __global__ void __launch_bounds__(kCB) k_convert_tile(ConvArgs a, int nruns_lds,
     }
     return;
   }
-  const uint64_t c0 = r0 + (uint64_t)threadIdx.x * kChunk;
-  const uint64_t c1 = c0 + kChunk < r1 ? c0 + kChunk : r1;
-  if (c0 < c1) {
-    Pos P = map_pos(runs, a.nruns, a.S, a.mS, a.offset + c0);
-    const DRun *R = &runs[P.r];
-    int64_t ibase = (int64_t)P.inst * a.ext;                       // instance origin
-    int64_t obase = ibase + R->disp + (int64_t)P.l2 * R->stride2;  // outer block origin
-    int64_t ua = obase + (int64_t)P.l1 * R->stride1 + (int64_t)P.o;
-    uint64_t pos = c0;
-    while (pos < c1) {
-      const uint64_t blen = R->blen;
-      const uint64_t avail = blen - P.o, want = c1 - pos;
-      const uint64_t n = avail < want ? avail : want;
-      if (PACK) lds_copy(pk + (pos - r0), span + ((uintptr_t)a.user + ua - lo), n);
-      else lds_to_global(a.user + ua, pk + (pos - r0), n);
-      pos += n;
-      P.o += n;
-      ua += (int64_t)n;
-      if (P.o == blen) {
-        P.o = 0;
-        if (++P.l1 < R->cnt1) {
-          ua += R->stride1 - (int64_t)blen;
-        } else {
-          P.l1 = 0;
-          if (++P.l2 < R->cnt2) {
-            obase += R->stride2;
-          } else {
-            P.l2 = 0;
-            if (++P.r == a.nruns) { P.r = 0; ibase += a.ext; }
-            R = &runs[P.r];
-            obase = ibase + R->disp;
-          }
-          ua = obase;
-        }
-      }
-    }
-  }
+  walk_chunk<PACK, TP>(a, runs, pk, span, lo, r0, r1);
   if (PACK) {
     __syncthreads();
     tile_move<false>(pk, a.packed + r0, r1 - r0, vec);
+  }
+}
+
+// PACK, pipelined: persistent workgroups walk tiles t, t + grid, ...; while
+// the lanes copy tile t's pieces out of LDS, the next tile's user span is
+// already in flight into registers (<= kSpanCap / 16 / kCB uint4 per lane),
+// and lands in LDS after the tile's packed bytes have left.  The one-tile
+// kernel above idles the memory pipe during every LDS phase (SQ counters on
+// the struct type: ~730 VALU instructions per 22.6k-cycle wave, i.e. waves
+// mostly wait on the span load).
+template <int TP>
+__global__ void __launch_bounds__(kCB) k_pack_tile_pipe(ConvArgs a, int nruns_lds, uint64_t ntiles) {
+  constexpr int kTP = TP, kSpanCap = TileGeom<TP>::kSpanCap;
+  constexpr int kPre = kSpanCap / 16 / kCB;   // uint4 per lane for a full span
+  static_assert(kSpanCap % (16 * kCB) == 0, "span staging is whole vectors per lane");
+  extern __shared__ __align__(16) char smem[];
+  char *pk = smem;
+  char *span = smem + kTP + 16;
+  DRun *sruns = reinterpret_cast<DRun *>(smem + kTP + 16 + kSpanCap + 32);
+  __shared__ uintptr_t s_lo[2];
+  __shared__ uint64_t s_nb[2];
+  __shared__ int s_ok[2];
+  const DRun *runs = a.runs;
+  if (nruns_lds) {
+    for (int i = threadIdx.x; i < a.nruns; i += kCB) sruns[i] = a.runs[i];
+    runs = sruns;
+  }
+  auto bounds = [&](uint64_t t, int slot) {   // one thread: user span of tile t
+    const uint64_t r0 = t * kTP, r1 = r0 + kTP < a.len ? r0 + kTP : a.len;
+    const Pos P0 = map_pos(runs, a.nruns, a.S, a.mS, a.offset + r0);
+    const Pos P1 = map_pos(runs, a.nruns, a.S, a.mS, a.offset + r1 - 1);
+    const int64_t f = block_addr(P0, runs[P0.r], a.ext) + (int64_t)P0.o;
+    const int64_t l = block_addr(P1, runs[P1.r], a.ext) + (int64_t)P1.o;
+    const uintptr_t lo = ((uintptr_t)a.user + f) & ~(uintptr_t)15;
+    const uintptr_t hi = ((uintptr_t)a.user + l + 16) & ~(uintptr_t)15;
+    s_lo[slot] = lo;
+    s_nb[slot] = hi - lo;
+    s_ok[slot] = l >= f && hi - lo <= (uintptr_t)kSpanCap;
+  };
+  uint64_t t = blockIdx.x;
+  if (t >= ntiles) return;
+  __syncthreads();                                   // runs staged
+  if (threadIdx.x == 0) bounds(t, 0);
+  __syncthreads();
+  if (s_ok[0]) tile_move<true>(span, reinterpret_cast<char *>(s_lo[0]), s_nb[0], 1);
+  int cur = 0;
+  for (;;) {
+    const uint64_t tn = t + gridDim.x;
+    const bool has_next = tn < ntiles;
+    if (has_next && threadIdx.x == 0) bounds(tn, cur ^ 1);
+    __syncthreads();                                 // span of t in LDS; bounds of tn visible
+    static_assert(kPre == 6, "prefetch registers below are spelled out for a 24 KiB span");
+    uint4 p0 = {}, p1 = {}, p2 = {}, p3 = {}, p4 = {}, p5 = {};
+    const bool pre_ok = has_next && s_ok[cur ^ 1];
+    const uint32_t nvn = pre_ok ? (uint32_t)(s_nb[cur ^ 1] / 16) : 0;
+    const uint32_t tx = threadIdx.x;
+    {
+      const uint4 *g = reinterpret_cast<const uint4 *>(s_lo[cur ^ 1]);
+      if (tx < nvn) p0 = g[tx];
+      if (tx + kCB < nvn) p1 = g[tx + kCB];
+      if (tx + 2 * kCB < nvn) p2 = g[tx + 2 * kCB];
+      if (tx + 3 * kCB < nvn) p3 = g[tx + 3 * kCB];
+      if (tx + 4 * kCB < nvn) p4 = g[tx + 4 * kCB];
+      if (tx + 5 * kCB < nvn) p5 = g[tx + 5 * kCB];
+    }
+    const uint64_t r0 = t * kTP, r1 = r0 + kTP < a.len ? r0 + kTP : a.len;
+    if (s_ok[cur]) {
+      walk_chunk<true, TP>(a, runs, pk, span, s_lo[cur], r0, r1);
+      __syncthreads();
+      tile_move<false>(pk, a.packed + r0, r1 - r0, a.pk_vec);
+    } else {                                         // span too wide for LDS: per-granule gather
+      const uint64_t g0 = r0 / 16, g1 = (r1 + 15) / 16;
+      for (uint64_t g = g0 + threadIdx.x; g < g1; g += kCB) convert_granule<1, true>(a, runs, g);
+    }
+    if (!has_next) break;
+    __syncthreads();                                 // span and pk of t are free
+    {
+      uint4 *d = reinterpret_cast<uint4 *>(span);
+      if (tx < nvn) d[tx] = p0;
+      if (tx + kCB < nvn) d[tx + kCB] = p1;
+      if (tx + 2 * kCB < nvn) d[tx + 2 * kCB] = p2;
+      if (tx + 3 * kCB < nvn) d[tx + 3 * kCB] = p3;
+      if (tx + 4 * kCB < nvn) d[tx + 4 * kCB] = p4;
+      if (tx + 5 * kCB < nvn) d[tx + 5 * kCB] = p5;
+    }
+    t = tn;
+    cur ^= 1;
   }
 }
 
@@ -642,6 +739,16 @@ static bool conv_vec_enabled() {
   return on != 0;
 }
 
+// MX_CONV_PIPE=0 sends PACK to the one-tile-per-workgroup kernel instead
+// of the pipelined one (A/B switch; results are identical).
+static bool conv_pipe_enabled() {
+  static const int on = [] {
+    const char *e = getenv("MX_CONV_PIPE");
+    return (e && *e == '0') ? 0 : 1;
+  }();
+  return on != 0;
+}
+
 // Tile size of the TILE kernels (MX_CONV_TP = 2048 / 4096 / 8192 for
 // measurement; results are identical).
 static int conv_tile_bytes() {
@@ -706,6 +813,13 @@ static int convert(const mx_ddt_t *d, size_t count, char *user, char *packed, si
   if (!PACK || d->monotonic) {
     const int nlds = a.nruns <= 64 ? 1 : 0;
     const size_t rb = nlds ? (size_t)a.nruns * sizeof(DRun) : 0;
+    if (PACK && conv_pipe_enabled()) {
+      const uint64_t tiles = (len + 8191) / 8192;
+      const uint64_t grid = std::min<uint64_t>(tiles, (uint64_t)g_num_cus * 4);
+      hipLaunchKernelGGL((k_pack_tile_pipe<8192>), dim3((unsigned)grid), dim3(kCB), TileGeom<8192>::lds(true, rb), s,
+                         a, nlds, tiles);
+      return mx_check_launch();
+    }
     const int tp = conv_tile_bytes();
     // narrow 4-byte-aligned blocks: word-parallel stores (see the kernel)
     uint64_t maxblen = 0;
