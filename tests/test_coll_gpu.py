@@ -344,47 +344,47 @@ def _run_mp(n, jobs, staging=1 << 20):
     return out
 
 
-@pytest.mark.parametrize("n", [2, 3, 4])
-def test_multiprocess_ipc_bitexact(n):
+_JOBS = [("allreduce", 100003, "SUM", "FLOAT", "auto"),          # > staging: chunked
+        ("allreduce", 777, "MAX", "DOUBLE", "rabenseifner"),
+        ("allreduce", 5, "SUM", "FLOAT", "recursive_doubling"),
+        ("allreduce_inplace", 4099, "SUM", "DOUBLE", "ring"),
+        ("allreduce", 3001, "MAXLOC", "FLOAT_INT", "auto"),
+        ("reduce_scatter", 1000, "SUM", "FLOAT", "ring"),
+        ("reduce_scatter", 10, "SUM", "DOUBLE", "recursive_halving"),
+        ("reduce_scatter", 300001, "SUM", "FLOAT", "ring"),              # blocks > staging: chunked
+        ("reduce_scatter_inplace", 200003, "SUM", "DOUBLE", "recursive_halving"),
+        ("allgather", 300001, None, None, None),
+        ("shmem", 5003, "MAX", "FLOAT", "auto"),
+        ("bcast", 2000003, None, None, None),
+        ("bcast_root0", 5, None, None, None),        # fewer bytes than non-roots: empty parts
+        ("bcast_root0", 1000001, None, None, None),
+        # back-to-back one-shot calls (both staging parities, every fold shape)
+        ("allreduce", 1000, "SUM", "FLOAT", "auto"),
+        ("allreduce", 3000, "SUM", "FLOAT", "ring"),
+        ("allreduce_inplace", 333, "PROD", "LONG_DOUBLE", "auto"),
+        ("allreduce", 1999, "MAXLOC", "DOUBLE_INT", "rabenseifner"),
+        ("allreduce", 1, "MIN", "INT64_T", "auto"),
+        ("allreduce", 17, "SUM", "DOUBLE", "basic_linear"),
+        ("allreduce", 200003, "SUM", "FLOAT", "segmented_ring"),   # chunked path in between
+        ("allreduce", 2500, "BXOR", "UINT16_T", "auto"),
+        ("allreduce_inplace", 4000, "SUM", "FLOAT", "auto"),
+        # rooted reduce / scan / exscan / reduce_scatter_block (VM fold)
+        ("reduce", 100003, "SUM", "FLOAT", "auto"),                 # chunked
+        ("reduce", 3001, "MAX", "DOUBLE", "binary"),
+        ("reduce_inplace", 5000, "MAX", "FLOAT", "binomial"),       # root's IN_PLACE variant
+        ("reduce_inplace", 777, "MAXLOC", "FLOAT_INT", "pipeline"),
+        ("reduce", 999, "SUM", "DOUBLE", "in_order_binary"),
+        ("scan", 20001, "SUM", "FLOAT", "auto"),
+        ("exscan", 4097, "SUM", "DOUBLE", "recursive_doubling"),
+        ("scan", 333, "MIN", "FLOAT", "recursive_doubling"),
+        ("reduce_scatter_block", 3000, "SUM", "FLOAT", "auto"),
+        ("symheap", 30001, "SUM", "FLOAT", "auto"),
+        ("symheap", 777, "MAX", "DOUBLE", "auto")]
+_JOBS = [(k, c, o or "BAND", t or "UINT8_T", a or "auto") for k, c, o, t, a in _JOBS]
+
+
+def _check_jobs(n, jobs, got):
     L = _oracle()
-    jobs = [("allreduce", 100003, "SUM", "FLOAT", "auto"),          # > staging: chunked
-            ("allreduce", 777, "MAX", "DOUBLE", "rabenseifner"),
-            ("allreduce", 5, "SUM", "FLOAT", "recursive_doubling"),
-            ("allreduce_inplace", 4099, "SUM", "DOUBLE", "ring"),
-            ("allreduce", 3001, "MAXLOC", "FLOAT_INT", "auto"),
-            ("reduce_scatter", 1000, "SUM", "FLOAT", "ring"),
-            ("reduce_scatter", 10, "SUM", "DOUBLE", "recursive_halving"),
-            ("reduce_scatter", 300001, "SUM", "FLOAT", "ring"),              # blocks > staging: chunked
-            ("reduce_scatter_inplace", 200003, "SUM", "DOUBLE", "recursive_halving"),
-            ("allgather", 300001, None, None, None),
-            ("shmem", 5003, "MAX", "FLOAT", "auto"),
-            ("bcast", 2000003, None, None, None),
-            ("bcast_root0", 5, None, None, None),        # fewer bytes than non-roots: empty parts
-            ("bcast_root0", 1000001, None, None, None),
-            # back-to-back one-shot calls (both staging parities, every fold shape)
-            ("allreduce", 1000, "SUM", "FLOAT", "auto"),
-            ("allreduce", 3000, "SUM", "FLOAT", "ring"),
-            ("allreduce_inplace", 333, "PROD", "LONG_DOUBLE", "auto"),
-            ("allreduce", 1999, "MAXLOC", "DOUBLE_INT", "rabenseifner"),
-            ("allreduce", 1, "MIN", "INT64_T", "auto"),
-            ("allreduce", 17, "SUM", "DOUBLE", "basic_linear"),
-            ("allreduce", 200003, "SUM", "FLOAT", "segmented_ring"),   # chunked path in between
-            ("allreduce", 2500, "BXOR", "UINT16_T", "auto"),
-            ("allreduce_inplace", 4000, "SUM", "FLOAT", "auto"),
-            # rooted reduce / scan / exscan / reduce_scatter_block (VM fold)
-            ("reduce", 100003, "SUM", "FLOAT", "auto"),                 # chunked
-            ("reduce", 3001, "MAX", "DOUBLE", "binary"),
-            ("reduce_inplace", 5000, "MAX", "FLOAT", "binomial"),       # root's IN_PLACE variant
-            ("reduce_inplace", 777, "MAXLOC", "FLOAT_INT", "pipeline"),
-            ("reduce", 999, "SUM", "DOUBLE", "in_order_binary"),
-            ("scan", 20001, "SUM", "FLOAT", "auto"),
-            ("exscan", 4097, "SUM", "DOUBLE", "recursive_doubling"),
-            ("scan", 333, "MIN", "FLOAT", "recursive_doubling"),
-            ("reduce_scatter_block", 3000, "SUM", "FLOAT", "auto"),
-            ("symheap", 30001, "SUM", "FLOAT", "auto"),
-            ("symheap", 777, "MAX", "DOUBLE", "auto")]
-    jobs = [(k, c, o or "BAND", t or "UINT8_T", a or "auto") for k, c, o, t, a in jobs]
-    got = _run_mp(n, jobs)
     for j, (kind, count, op, t, alg) in enumerate(jobs):
         es = mxompi.type_size(t)
         if kind.startswith("allreduce") or kind == "shmem":
@@ -469,3 +469,22 @@ def test_multiprocess_ipc_bitexact(n):
             root = gen("UINT8_T", "BAND", count, 7000 + (n - 1 if kind == "bcast" else 0))
             for r in range(n):
                 np.testing.assert_array_equal(np.frombuffer(got[r][j], np.uint8), root)
+
+
+@pytest.mark.parametrize("n", [2, 3, 4])
+def test_multiprocess_ipc_bitexact(n):
+    _check_jobs(n, _JOBS, _run_mp(n, _JOBS))
+
+
+# the driver's 8-GPU run reaches these at n = 8: every slot's 8-rank masks,
+# one-shot and chunked allreduce, scatter + allgather bcast from two roots
+_JOBS8 = [j for j in _JOBS if (j[0], j[1]) in {
+    ("allreduce", 100003), ("allreduce", 777), ("allreduce", 1000), ("reduce_scatter", 300001),
+    ("allgather", 300001), ("bcast", 2000003), ("bcast_root0", 5), ("bcast_root0", 1000001),
+    ("reduce", 100003), ("scan", 20001), ("shmem", 5003), ("allreduce", 3001)}]
+
+
+def test_multiprocess_ipc_bitexact_8_ranks():
+    assert len(_JOBS8) >= 10
+    _check_jobs(8, _JOBS8, _run_mp(8, _JOBS8))
+
