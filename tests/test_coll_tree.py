@@ -162,8 +162,6 @@ def _gen(t, op, count, seed):
 @pytest.mark.parametrize("op,t", CASES)
 def test_reduce_local_bitexact(alg, n, op, t):
     torch = _gpu()
-    if n == 16 and t in ("LONG_DOUBLE", "MAXLOC") or (n == 16 and "LONG_DOUBLE" in t):
-        pytest.skip("x87 types at 16 ranks exceed the VM's LDS register budget (delegated)")
     L = _oracle()
     es = mxompi.type_size(t)
     comm = mxompi.Comm.local(n)
@@ -204,8 +202,6 @@ def test_reduce_local_bitexact(alg, n, op, t):
 @pytest.mark.parametrize("op,t", CASES)
 def test_scan_local_bitexact(kind, alg, n, op, t):
     torch = _gpu()
-    if n == 16 and "LONG_DOUBLE" in t:
-        pytest.skip("x87 types at 16 ranks exceed the VM's LDS register budget (delegated)")
     L = _oracle()
     es = mxompi.type_size(t)
     comm = mxompi.Comm.local(n)

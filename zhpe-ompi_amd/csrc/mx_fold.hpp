@@ -294,6 +294,7 @@ int oneshot_launch(OneShotArgs &a, int nwg, hipStream_t s) {
 constexpr int kVB = 128;         // VM block size
 constexpr int VM_MAXI = 192;     // instructions per program
 constexpr int VM_MAXREG = 40;    // registers (contributions + temporaries)
+constexpr size_t kVmLdsMax = 160 * 1024;   // LDS per CU, all of it available to one workgroup
 // op: VM_COMB / VM_EMIT, optionally guarded by the call's info bit (the
 // root's MPI_IN_PLACE in a rooted reduce): executed only if set / clear
 enum { VM_COMB = 0, VM_EMIT = 1, VM_IF_SET = 4, VM_IF_CLEAR = 8 };
@@ -362,8 +363,20 @@ typedef int (*vm_launch_fn)(VmArgs &, hipStream_t);
 template <class T, class OP>
 int vm_launch(VmArgs &a, hipStream_t s) {
   constexpr size_t N = (sizeof(T) <= 16 && 16 % sizeof(T) == 0) ? 16 / sizeof(T) : 0;
+  // a gfx950 workgroup may take the whole 160 KiB of its CU's LDS; above the
+  // 64 KiB default the kernel has to opt in (x87 pair types at 16 ranks:
+  // ~20 registers x 128 lanes x 32 B)
   const size_t lds = (size_t)a.p.nregs * kVB * vm_slot<T>();
-  if (lds > 64 * 1024 || a.p.nregs > VM_MAXREG || a.p.nins > VM_MAXI) return MX_ERR_UNSUPPORTED;
+  if (lds > kVmLdsMax || a.p.nregs > VM_MAXREG || a.p.nins > VM_MAXI) return MX_ERR_UNSUPPORTED;
+  if (lds > 64 * 1024) {
+    static const bool opted = [] {
+      return hipFuncSetAttribute(reinterpret_cast<const void *>(&k_vm<T, OP, true>),
+                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)kVmLdsMax) == hipSuccess &&
+             hipFuncSetAttribute(reinterpret_cast<const void *>(&k_vm<T, OP, false>),
+                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)kVmLdsMax) == hipSuccess;
+    }();
+    if (!opted) return MX_ERR_UNSUPPORTED;
+  }
   bool vec = N > 0 && !has_pad<T>::value;
   const uintptr_t m = (uintptr_t)a.src[0] & 15;
   for (int j = 0; j < a.p.nsrc; j++)
