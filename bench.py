@@ -18,9 +18,8 @@ Metric (BASELINE.json): "MPI_Allreduce busBW GB/s (256 MiB fp32 SUM,
 
 The JSON line also carries `roofline` (the dominant kernel's achieved
 bytes/launch / its HIP-event-timed average duration vs the 8 TB/s HBM
-peak) and `cpu_baseline` (the reference's own op_base_functions.c compiled
-from source -- oracle/_ref -- or our C restatement, timed on the host on a
-bounded sample).
+peak) and `cpu_baseline` (the CPU oracle's restatement of the reference's
+fp32 SUM loop, timed on one host core on a bounded sample).
 """
 from __future__ import annotations
 
@@ -61,29 +60,19 @@ def load_traffic(kernel_key):
 
 
 def cpu_baseline_reduce_local(seconds=10.0):
-    """Time the reference's own 2-buffer fp32 SUM (op_base_functions.c:312,
-    compiled from source into oracle/_ref/libref_op.so) on one host core,
-    on a bounded sample: 2 x 256 MiB host buffers, repeated ~`seconds`."""
+    """Time the 2-buffer fp32 SUM of the CPU oracle -- oracle/mx_oracle_op.c,
+    the restatement of op_base_functions.c:40-51 (OP_FUNC, instantiated for
+    float at :312), compiled -O2 for the x86-64 baseline like the reference's
+    own loop -- on one host core, on a bounded sample: 2 x 256 MiB host
+    buffers, repeated ~`seconds`."""
     import numpy as np
-    ref = os.path.join(ROOT, "oracle", "_ref", "libref_op.so")
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import oracle_lib
     n = 1 << 26
     a = np.random.default_rng(1).uniform(-1, 1, n).astype(np.float32)
     b = np.random.default_rng(2).uniform(-1, 1, n).astype(np.float32)
-    if os.path.exists(ref):
-        L = ctypes.CDLL(ref)
-        tab = (ctypes.c_void_p * (15 * 41)).in_dll(L, "ompi_op_base_functions")
-        FN = ctypes.CFUNCTYPE(None, ctypes.c_void_p, ctypes.c_void_p,
-                              ctypes.POINTER(ctypes.c_int), ctypes.c_void_p, ctypes.c_void_p)
-        fn = FN(tab[3 * 41 + 15])          # [MPI_SUM][OMPI_OP_BASE_TYPE_FLOAT]
-        cnt = ctypes.c_int(n)
-        call = lambda: fn(a.ctypes.data, b.ctypes.data, ctypes.byref(cnt), None, None)
-        kind = "reference"
-    else:
-        sys.path.insert(0, os.path.join(ROOT, "tests"))
-        import oracle_lib
-        O = oracle_lib.oracle()
-        call = lambda: O.mxo_reduce2(3, 15, a.ctypes.data, b.ctypes.data, n, 1)
-        kind = "port"
+    O = oracle_lib.oracle()
+    call = lambda: O.mxo_reduce2(3, 15, a.ctypes.data, b.ctypes.data, n, 1)   # [MPI_SUM][FLOAT]
     call()
     iters, t0 = 0, time.perf_counter()
     while True:
@@ -93,7 +82,7 @@ def cpu_baseline_reduce_local(seconds=10.0):
         if el >= seconds:
             break
     gbs = 3.0 * n * 4 * iters / el / 1e9
-    return {"value": round(gbs, 3), "unit": "GB/s", "cores": 1, "kind": kind,
+    return {"value": round(gbs, 3), "unit": "GB/s", "cores": 1, "kind": "port",
             "sample": f"fp32 SUM 2-buffer, 2 x 256 MiB host buffers, {iters} calls in {el:.1f} s "
                       f"(1 host thread; algorithmic 3*N*4 B per call)"}
 
@@ -105,10 +94,9 @@ def cpu_baseline_allreduce(ranks=8, nbytes=256 << 20, iters=10):
     MPI on the box), fp32 SUM through the reference's own compiled loop."""
     import subprocess
     exe = os.path.join(ROOT, "oracle", "build", "cpu_coll_proxy")
-    ref = os.path.join(ROOT, "oracle", "_ref", "libref_op.so")
     if not os.path.exists(exe):
         return {"error": "oracle/build/cpu_coll_proxy not built"}
-    cmd = [exe, str(ranks), str(nbytes), str(iters)] + ([ref] if os.path.exists(ref) else [])
+    cmd = [exe, str(ranks), str(nbytes), str(iters)]
     try:
         p = subprocess.run(cmd, capture_output=True, text=True, timeout=300)
         d = json.loads(p.stdout.strip().splitlines()[-1])
@@ -154,14 +142,15 @@ def bench_allreduce(torch, mx, dist, rank, world, dev, steps, warmup, nbytes=256
         return out
 
     ndev = torch.cuda.device_count()
-    flags = mx.COMM_IPC | (mx.COMM_RCCL if ndev >= world else 0)
+    flags = mx.COMM_IPC | mx.COMM_P2P | (mx.COMM_RCCL if ndev >= world else 0)
     try:
         comm = mx.Comm(rank, world, ag, device=dev, staging_bytes=2 * nbytes + (64 << 20), flags=flags,
                        heap_bytes=2 * nbytes + (4 << 20))
     except mx.MxError:
-        comm = mx.Comm(rank, world, ag, device=dev, staging_bytes=2 * nbytes + (64 << 20), flags=mx.COMM_IPC,
+        comm = mx.Comm(rank, world, ag, device=dev, staging_bytes=2 * nbytes + (64 << 20),
+                       flags=mx.COMM_IPC | mx.COMM_P2P,
                        heap_bytes=2 * nbytes + (4 << 20))
-        flags = mx.COMM_IPC
+        flags = mx.COMM_IPC | mx.COMM_P2P
     g = torch.Generator(device="cuda").manual_seed(0x5EED + rank)
     x = torch.rand(count, device="cuda", generator=g) * 2 - 1
     out = torch.empty_like(x)

@@ -28,8 +28,8 @@
  *    coll/tuned's for every op, including FP SUM/PROD -- and writes the
  *    result to the local rbuf and to every peer's gather area;
  *  * cross-GPU ordering uses generation-tagged flags in uncached device
- *    memory written with system-scope atomics, waited on by bounded spins
- *    (a missing peer returns MX_ERR_TIMEOUT instead of hanging the GPU).
+ *    memory written with system-scope atomics, waited on by device spins
+ *    (optionally bounded: mx_comm_set_timeout).
  *
  * Ownership: the caller owns all buffers.  Calls are blocking with respect
  * to `stream` semantics: work is enqueued on `stream`, and the call returns
@@ -67,6 +67,8 @@ typedef int (*mx_allgather_fn)(const void *send, void *recv, size_t bytes, void 
 /* comm flags */
 #define MX_COMM_IPC   1   /* all-peer xGMI path over IPC-mapped staging  */
 #define MX_COMM_RCCL  2   /* also create an RCCL communicator             */
+#define MX_COMM_P2P   4   /* point-to-point mailboxes (size x 16 MiB of
+                             device memory per rank; needs MX_COMM_IPC)   */
 
 /* Multi-process communicator: one rank per process (per GPU). */
 int mx_comm_create(int rank, int size, int device, size_t staging_bytes, int flags,
@@ -84,7 +86,13 @@ int mx_comm_create_local(int size, int device, mx_comm_t **comm);
 int mx_comm_destroy(mx_comm_t *comm);
 int mx_comm_size(const mx_comm_t *comm);
 int mx_comm_rank(const mx_comm_t *comm);
-/* Bounded-spin timeout for peer waits (default 60 s). */
+/* Timeout of the device-side peer waits (default 60 s; 0 = wait forever,
+ * what an MPI communicator needs: a peer may legally arrive arbitrarily
+ * late).  When a wait does time out the communicator is POISONED: every
+ * copy / fold / signal kernel already queued behind the wait does nothing
+ * (no peer is handed stale data, no staging a late peer still reads is
+ * overwritten), the call returns MX_ERR_TIMEOUT, and every later call on
+ * the communicator fails with it. */
 int mx_comm_set_timeout(mx_comm_t *comm, double seconds);
 
 /* Per-communicator kernel timing (HIP events on the collective's stream),

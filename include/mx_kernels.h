@@ -144,10 +144,31 @@ enum {
 /* Select the HIP device and allocate per-process state.  Idempotent. */
 int mx_init(int device);
 int mx_finalize(void);
-/* 1 = device (or device-mapped) memory, 0 = host memory, <0 = error. */
+/* 1 = device (or device-mapped) memory, 0 = host memory, <0 = error.
+ * Device allocations are cached as address ranges (64 entries, LRU), so the
+ * per-call probe of the accelerator pattern (common_cuda.c:1736-1857) costs
+ * no runtime call for a known buffer. */
 int mx_is_device_ptr(const void *p);
+/* Drop cached ranges overlapping [p, p+bytes) (a caller freeing device
+ * memory it did not get from mx_alloc). */
+int mx_ptr_cache_forget(const void *p, size_t bytes);
 /* Block until all work queued on `stream` (NULL = default) completed. */
 int mx_stream_sync(void *stream);
+
+/* ---- memory and streams for the host components ----------------------
+ * The coll component stages host buffers through device scratch (every
+ * rank of a communicator takes the same path whatever memory its buffers
+ * are in) and runs its kernels on streams it owns. */
+int mx_alloc(size_t bytes, void **p);      /* device memory                */
+int mx_free(void *p);
+/* Any direction (host pageable / pinned / device), ordered on `stream`. */
+int mx_memcpy(void *dst, const void *src, size_t bytes, void *stream);
+/* A non-blocking stream (does not synchronise with the legacy default one). */
+int mx_stream_create(void **stream);
+int mx_stream_destroy(void *stream);
+/* `stream` waits on the device for the work queued on `after` so far
+ * (NULL = the legacy default stream). */
+int mx_stream_order(void *stream, void *after);
 const char *mx_strerror(int rc);
 /* Library identification, e.g. "mx_kernels gfx950 abi 1". */
 const char *mx_version(void);

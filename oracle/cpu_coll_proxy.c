@@ -14,11 +14,11 @@
  * block straight out of the sender's buffer; one process-shared barrier per
  * step stands in for the send/recv completion.  (Tuned selects the 1 MiB
  * segmented ring at 256 MiB; it moves the same bytes in smaller messages.)
- * The local reduction is the reference's own compiled
- * ompi_op_base_2buff_sum_float (oracle/_ref/libref_op.so) when present
- * ("reference"), else a plain C loop ("port").
+ * The local reduction is a plain C loop of the OP_FUNC shape
+ * (op_base_functions.c:40-51) ("port"); an optional shared library
+ * exporting the reference's table may be named instead (not built here).
  *
- * usage: cpu_coll_proxy RANKS BYTES ITERS [libref_op.so]
+ * usage: cpu_coll_proxy RANKS BYTES ITERS [lib exporting ompi_op_base_functions]
  * prints one JSON object: busBW GB/s = S/t * 2(n-1)/n, t = median.
  */
 #define _GNU_SOURCE

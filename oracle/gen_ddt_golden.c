@@ -1,5 +1,12 @@
 /*
- * gen_ddt_golden.c -- TEST INFRASTRUCTURE ONLY.
+ * gen_ddt_golden.c -- TEST INFRASTRUCTURE ONLY.  RETIRED: kept as the record
+ * of how the committed tests/golden/ddt_vectors.bin was made in round 1; it
+ * is no longer built.  It linked the reference's datatype engine compiled
+ * through configuration stand-ins (oracle/shim_ddt, removed), a build that
+ * pins nothing under the rules: the fixture's descriptions and
+ * streams are checked against our own restatement (oracle/mx_oracle_ddt.c)
+ * and, where the reference's own datatype tests state expected values,
+ * against those (tests/test_convertor_pins.py).
  *
  * Golden vectors for the convertor (derived-datatype pack/unpack).  Links
  * the reference's OWN datatype engine (opal/datatype/*.c compiled unmodified

@@ -26,6 +26,8 @@ def host(with_components=True):
     H.mxh_dtype.argtypes = [ctypes.c_char_p]
     H.mxh_dtype_contiguous.restype = vp
     H.mxh_dtype_contiguous.argtypes = [ci, vp]
+    H.mxh_dtype_vector.restype = vp
+    H.mxh_dtype_vector.argtypes = [ci, ci, ci, vp]
     H.mxh_op.restype = vp
     H.mxh_op.argtypes = [ctypes.c_char_p]
     H.mxh_op_slot_owner.argtypes = [vp, ci, ci]

@@ -1,0 +1,152 @@
+"""The drop-in boundary, checked against the reference's own headers.
+
+The components are compiled against a layout mirror of the plugin ABI
+(zhpe-ompi_amd/mca/mx_ompi_abi.h).  Here every mirrored struct is compared
+member by member with the reference:
+
+* opal_object_t, mca_base_component_2_1_0_t / _data_t
+  (opal/mca/mca.h:285-342), ompi_op_base_component_1_0_0_t and
+  ompi_op_base_module_1_0_0_t (ompi/mca/op/op.h:331-378): a probe program
+  that includes the reference's real headers reports offsetof / sizeof;
+* mca_coll_base_module_2_3_0_t (ompi/mca/coll/coll.h:504-604) and
+  mca_coll_base_component_2_0_0_t (:471-481): coll.h needs the generated
+  mpi.h, so its member list is read from the header text -- every member
+  after `opal_object_t super` is one pointer, so a member's offset is
+  sizeof(opal_object_t) + 8 x its position;
+* the op component itself is compiled with -DMX_OMPI_REAL against the
+  reference's ompi/mca/op/op.h (to an object file, the stage this tree
+  allows: libopen-pal / libmpi are not built here).
+
+The config header tests/abi/opal_config.h is test infrastructure: it stands
+for the configure output of an x86-64 gcc build so the reference headers can
+be included; nothing of the reference is built or linked.
+"""
+import json
+import os
+import re
+import subprocess
+
+import pytest
+
+REF = "/root/reference"
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+ABI = os.path.join(ROOT, "zhpe-ompi_amd", "mca")
+pytestmark = pytest.mark.skipif(not os.path.isdir(os.path.join(REF, "ompi")),
+                                reason="needs the reference headers (/root/reference)")
+
+
+def struct_members(path, tag):
+    """Member names of `struct tag { ... };` in a C header, in order."""
+    text = open(path).read()
+    m = re.search(r"struct\s+" + re.escape(tag) + r"\s*\{", text)
+    assert m, (path, tag)
+    depth, i = 1, m.end()
+    while depth:
+        depth += {"{": 1, "}": -1}.get(text[i], 0)
+        i += 1
+    body = text[m.end():i - 1]
+    body = re.sub(r"/\*.*?\*/", "", body, flags=re.S)
+    body = re.sub(r"//[^\n]*", "", body)
+    body = "\n".join(ln for ln in body.splitlines() if not ln.strip().startswith("#"))
+    names = []
+    for decl in body.split(";"):
+        decl = decl.strip()
+        if not decl:
+            continue
+        decl = re.sub(r"\[[^\]]*\]", "", decl)
+        names.append(re.findall(r"[A-Za-z_]\w*", decl)[-1])
+    return names
+
+
+def compile_run(tmp_path, name, src, incs, defs=()):
+    c = tmp_path / f"{name}.c"
+    exe = tmp_path / name
+    c.write_text(src)
+    cmd = ["gcc", "-std=gnu11", "-w", *[f"-D{d}" for d in defs], *[f"-I{i}" for i in incs], str(c), "-o", str(exe)]
+    r = subprocess.run(cmd, capture_output=True, text=True)
+    assert r.returncode == 0, r.stderr[-3000:]
+    out = subprocess.run([str(exe)], capture_output=True, text=True, check=True).stdout
+    return json.loads(out)
+
+
+def probe_src(includes, items):
+    """items: (key, struct type, member or None)"""
+    lines = ["#include <stddef.h>", "#include <stdio.h>", *[f'#include "{h}"' for h in includes],
+             "int main(void) {", '  printf("{");']
+    for k, (key, typ, mem) in enumerate(items):
+        expr = f"sizeof({typ})" if mem is None else f"offsetof({typ}, {mem})"
+        sep = "" if k == 0 else ","
+        lines.append(f'  printf("{sep}\\"{key}\\": %zu", (size_t)({expr}));')
+    lines += ['  printf("}\\n");', "  return 0;", "}"]
+    return "\n".join(lines)
+
+
+REAL_INCS = [os.path.join(ROOT, "tests", "abi"), REF, os.path.join(REF, "opal", "include"),
+             os.path.join(REF, "ompi", "include")]
+
+OP_H = os.path.join(REF, "ompi", "mca", "op", "op.h")
+MCA_H = os.path.join(REF, "opal", "mca", "mca.h")
+COLL_H = os.path.join(REF, "ompi", "mca", "coll", "coll.h")
+
+
+def _items():
+    items = [("sizeof opal_object_t", "opal_object_t", None),
+             ("sizeof mca_base_component_t", "mca_base_component_t", None),
+             ("sizeof mca_base_component_data_t", "mca_base_component_data_t", None)]
+    for typ, tag in (("mca_base_component_t", "mca_base_component_2_1_0_t"),):
+        for mem in struct_members(MCA_H, tag):
+            items.append((f"{typ}.{mem}", typ, mem))
+    for typ, tag in (("ompi_op_base_component_1_0_0_t", "ompi_op_base_component_1_0_0_t"),
+                     ("ompi_op_base_module_1_0_0_t", "ompi_op_base_module_1_0_0_t")):
+        for mem in struct_members(OP_H, tag):
+            items.append((f"{typ}.{mem}", typ, mem))
+        items.append((f"sizeof {typ}", typ, None))
+    return items
+
+
+def test_op_framework_and_mca_base_layouts_match_reference(tmp_path):
+    items = _items()
+    real = compile_run(tmp_path, "real", probe_src(["opal/mca/mca.h", "ompi/mca/op/op.h"], items), REAL_INCS)
+    mirror = compile_run(tmp_path, "mirror", probe_src(["mx_ompi_abi.h"], items), [ABI, os.path.join(ROOT, "include")])
+    assert real["sizeof opal_object_t"] == 16, real     # OPAL_ENABLE_DEBUG = 0 layout
+    diff = {k: (real[k], mirror[k]) for k in real if real[k] != mirror[k]}
+    assert not diff, f"mirror differs from the reference headers (reference, mirror): {diff}"
+
+
+def test_coll_module_and_component_layouts_match_reference(tmp_path):
+    mods = struct_members(COLL_H, "mca_coll_base_module_2_3_0_t")
+    comps = struct_members(COLL_H, "mca_coll_base_component_2_0_0_t")
+    assert mods[0] == "super" and mods[1] == "coll_module_enable" and mods[-1] == "base_data"
+    assert len(mods) == 1 + 1 + 3 * 17 + 3 * 5 + 3 + 1, len(mods)      # coll.h:504-604
+    assert comps == ["collm_version", "collm_data", "collm_init_query", "collm_comm_query"]
+    items = [(f"m.{x}", "mca_coll_base_module_t", x) for x in mods] + \
+            [(f"c.{x}", "mca_coll_base_component_2_0_0_t", x) for x in comps] + \
+            [("sizeof m", "mca_coll_base_module_t", None)]
+    mirror = compile_run(tmp_path, "mirror_coll", probe_src(["mx_ompi_abi.h"], items),
+                         [ABI, os.path.join(ROOT, "include")])
+    real = compile_run(tmp_path, "real_base", probe_src(["opal/class/opal_object.h", "opal/mca/mca.h"], [
+        ("obj", "opal_object_t", None), ("comp", "mca_base_component_t", None),
+        ("data", "mca_base_component_data_t", None)]), REAL_INCS)
+    for i, x in enumerate(mods):
+        exp = 0 if i == 0 else real["obj"] + 8 * (i - 1)
+        assert mirror[f"m.{x}"] == exp, (x, mirror[f"m.{x}"], exp)
+    assert mirror["sizeof m"] == real["obj"] + 8 * (len(mods) - 1)
+    data_off = real["comp"]
+    fn_off = (data_off + real["data"] + 7) // 8 * 8
+    assert [mirror[f"c.{x}"] for x in comps] == [0, data_off, fn_off, fn_off + 8]
+
+
+def test_op_component_compiles_against_reference_op_h(tmp_path):
+    """-DMX_OMPI_REAL: the real ompi/mca/op/op.h replaces the mirror; module
+    objects become OPAL classes derived from ompi_op_base_module_t."""
+    obj = tmp_path / "op_mi355x_real.o"
+    cmd = ["gcc", "-std=gnu11", "-Wall", "-Werror", "-c", "-DMX_OMPI_REAL", "-DMX_OMPI_REAL_NO_COLL",
+           *[f"-I{i}" for i in REAL_INCS], f"-I{os.path.join(ROOT, 'include')}", f"-I{ABI}",
+           os.path.join(ABI, "op_mi355x.c"), "-o", str(obj)]
+    r = subprocess.run(cmd, capture_output=True, text=True)
+    assert r.returncode == 0, r.stderr[-4000:]
+    syms = subprocess.run(["nm", str(obj)], capture_output=True, text=True, check=True).stdout
+    assert re.search(r" D mca_op_mi355x_component$", syms, re.M)
+    assert re.search(r" D mx_op_module_t_class$", syms, re.M)            # OBJ_CLASS_INSTANCE
+    assert re.search(r" U ompi_op_base_module_t_class$", syms, re.M)     # parent class from libmpi
+    assert re.search(r" U mx_ompi_host_real_register$", syms, re.M)      # the real host table (open fn)

@@ -488,3 +488,83 @@ def test_multiprocess_ipc_bitexact_8_ranks():
     assert len(_JOBS8) >= 10
     _check_jobs(8, _JOBS8, _run_mp(8, _JOBS8))
 
+
+
+# ---------------------------------------------------------------------------
+# a peer later than the wait timeout: poisoned communicator, no stale data
+# ---------------------------------------------------------------------------
+def _late_worker(rank, n, port, q):
+    import time
+    import torch.distributed as dist
+    os.environ["HSA_ENABLE_IPC_MODE_LEGACY"] = "0"
+    try:
+        dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=n)
+        torch.cuda.set_device(0)
+        mxompi.init(0)
+
+        def ag(b):
+            out = [None] * n
+            dist.all_gather_object(out, b)
+            return out
+
+        comm = mxompi.Comm(rank, n, ag, device=0, staging_bytes=4 << 20)
+        comm.set_timeout(2.0)
+        st = torch.cuda.current_stream().cuda_stream
+        count = 400_003                                   # staged path (> one-shot range)
+        x = _dev(gen("FLOAT", "SUM", count, 7000 + rank))
+        out = torch.zeros(count * 4, dtype=torch.uint8, device="cuda")
+        comm.allreduce(x.data_ptr(), out.data_ptr(), count, "FLOAT", "SUM", "auto", st)   # both on time
+        first = out.cpu().numpy().tobytes()
+        dist.barrier()
+        if rank == 1:
+            time.sleep(5.0)                               # arrives after rank 0's wait gave up
+        rcs = []
+        for _ in range(2):
+            t0 = time.time()
+            try:
+                comm.allreduce(x.data_ptr(), out.data_ptr(), count, "FLOAT", "SUM", "auto", st)
+                rcs.append((0, time.time() - t0))
+            except mxompi.MxError as e:
+                rcs.append((e.rc, time.time() - t0))
+        dist.barrier()
+        comm.close()
+        dist.destroy_process_group()
+        q.put((rank, "ok", {"first": first, "rcs": rcs}))
+    except Exception as e:  # noqa: BLE001
+        import traceback
+        q.put((rank, "err", traceback.format_exc() + str(e)))
+
+
+def test_late_peer_poisons_instead_of_corrupting():
+    """Rank 1 enters the second allreduce 5 s late with a 2 s wait timeout.
+    Rank 0's wait for rank 1's contribution times out: the copy / fold /
+    signal kernels queued behind it do nothing, it returns MX_ERR_TIMEOUT,
+    and its next call fails at once.  Rank 1 then finds rank 0's PUSHED
+    signal never raised (rank 0 folded nothing) and times out too, instead
+    of copying stale gather data and returning success."""
+    import torch.multiprocessing as mp
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_late_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    out = {}
+    try:
+        for _ in range(2):
+            rank, status, payload = q.get(timeout=120)
+            assert status == "ok", payload
+            out[rank] = payload
+    finally:
+        for p in procs:
+            p.join(timeout=30 if len(out) == 2 else 5)
+            if p.is_alive():
+                p.terminate()
+                p.join(timeout=10)
+    TIMEOUT = -5
+    assert out[0]["first"] == out[1]["first"]
+    (rc0a, _), (rc0b, t0b) = out[0]["rcs"]
+    (rc1a, _), (rc1b, t1b) = out[1]["rcs"]
+    assert rc0a == TIMEOUT and rc1a == TIMEOUT, out
+    assert rc0b == TIMEOUT and rc1b == TIMEOUT, out          # poisoned: every later call fails
+    assert t0b < 1.0 and t1b < 1.0, (t0b, t1b)               # ... without waiting again

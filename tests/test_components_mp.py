@@ -299,3 +299,336 @@ def test_multirank_device_buffers_through_components(n):
         return 0       # coll/tuned fixed decisions (the oracle's alg 0)
     _check(n, got, alg_of, bitexact_fp=True)
     _check_nb(n, got, gpu=True)
+
+
+# ---------------------------------------------------------------------------
+# every rank takes the same protocol whatever memory its buffers are in
+# ---------------------------------------------------------------------------
+def _mixed_worker(rank, n, port, q):
+    """Rank 0 passes HOST buffers (and, for allgather / bcast, a
+    non-contiguous MPI_Type_vector layout of the same type signature); the
+    other ranks pass contiguous device buffers.  MPI allows both, so the
+    component must not let rank 0 delegate to the host module while the
+    others run the device protocol (that would deadlock): all ranks run the
+    device path, rank 0 staged through device scratch."""
+    try:
+        import torch
+        import torch.distributed as dist
+        import minihost
+        import mxompi
+        os.environ["OMPI_MCA_coll_mi355x_wait_timeout"] = "60"
+        dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=n)
+
+        @minihost.AG
+        def ag(send, recv, nbytes, ctx):
+            out = [None] * n
+            dist.all_gather_object(out, ctypes.string_at(send, nbytes))
+            blob = b"".join(out)
+            ctypes.memmove(recv, blob, len(blob))
+            return 0
+
+        torch.cuda.set_device(0)
+        mxompi.init(0)
+        H = minihost.host(with_components=True)
+        comm = H.mxh_comm_create(rank, n, ag, None)
+        f32, i32 = minihost.dtype(H, "MPI_FLOAT"), minihost.dtype(H, "MPI_INT")
+        SUM = minihost.op(H, "MPI_SUM")
+        host = rank == 0
+        res = {}
+
+        def buf(a):
+            t = torch.from_numpy(np.ascontiguousarray(a).copy())
+            return t if host else t.cuda()
+
+        count = 5003
+        x = _gen("flt", count, rank)
+        X, R = buf(x), buf(np.zeros(count, np.float32))
+        assert H.mxh_allreduce(X.data_ptr(), R.data_ptr(), count, f32, SUM, comm) == 0
+        res["allreduce"] = R.cpu().numpy().tobytes()
+        R = buf(x)
+        assert H.mxh_allreduce(1, R.data_ptr(), count, f32, SUM, comm) == 0     # MPI_IN_PLACE
+        res["allreduce_inplace"] = R.cpu().numpy().tobytes()
+        R = buf(np.zeros(count, np.float32))
+        assert H.mxh_reduce(X.data_ptr(), R.data_ptr(), count, f32, SUM, n - 1, comm) == 0
+        res["reduce"] = R.cpu().numpy().tobytes()
+        R = buf(np.zeros(count, np.float32))
+        assert H.mxh_scan(X.data_ptr(), R.data_ptr(), count, f32, SUM, comm) == 0
+        res["scan"] = R.cpu().numpy().tobytes()
+        xb = _gen("int", 300 * n, rank)
+        XB, RB = buf(xb), buf(np.zeros(300, np.int32))
+        assert H.mxh_reduce_scatter_block(XB.data_ptr(), RB.data_ptr(), 300, i32, SUM, comm) == 0
+        res["rsb"] = RB.cpu().numpy().tobytes()
+        rc = (ctypes.c_int * n)(*[100 + 7 * r for r in range(n)])
+        XR, RR = buf(_gen("int", sum(rc), rank)), buf(np.zeros(rc[rank], np.int32))
+        assert H.mxh_reduce_scatter(XR.data_ptr(), RR.data_ptr(), rc, i32, SUM, comm) == 0
+        res["reduce_scatter"] = RR.cpu().numpy().tobytes()
+        # nonblocking + persistent with host buffers on rank 0
+        R = buf(np.zeros(count, np.float32))
+        r = vp()
+        assert H.mxh_iallreduce(X.data_ptr(), R.data_ptr(), count, f32, SUM, comm, ctypes.byref(r)) == 0
+        assert H.mxh_wait(ctypes.byref(r)) == 0
+        res["iallreduce"] = R.cpu().numpy().tobytes()
+        P, R = vp(), buf(np.zeros(count, np.float32))
+        assert H.mxh_allreduce_init(X.data_ptr(), R.data_ptr(), count, f32, SUM, comm, ctypes.byref(P)) == 0
+        for _ in range(2):
+            R.zero_()
+            assert H.mxh_start(P) == 0
+            assert H.mxh_wait(ctypes.byref(P)) == 0
+        assert H.mxh_request_free(ctypes.byref(P)) == 0
+        res["pallreduce"] = R.cpu().numpy().tobytes()
+        # allgather / bcast: rank 0 uses vector(4 blocks of 3 ints, stride 5)
+        # x 10 elements, the others 120 contiguous ints: same signature
+        vec = H.mxh_dtype_vector(4, 3, 5, i32)
+        assert vec
+        mine = np.arange(120, dtype=np.int32) + 1000 * rank
+        # MPI_Type_vector(4, 3, 5): extent 18 ints, element i at 18 i
+        pos = (np.arange(10)[:, None, None] * 18 + np.arange(4)[None, :, None] * 5
+               + np.arange(3)[None, None, :]).reshape(-1)
+        if host:
+            lay = np.full(180, -1, np.int32)
+            lay[pos] = mine
+            S = buf(lay)
+            sdt, scnt = vec, 10
+        else:
+            S, sdt, scnt = buf(mine), i32, 120
+        G = buf(np.full(120 * n, -7, np.int32))
+        assert H.mxh_allgather(S.data_ptr(), scnt, sdt, G.data_ptr(), 120, i32, comm) == 0
+        res["allgather"] = G.cpu().numpy().tobytes()
+        if host:
+            lay = np.full(180, -1, np.int32)
+            lay[pos] = mine
+            B = buf(lay)
+            assert H.mxh_bcast(B.data_ptr(), 10, vec, n - 1, comm) == 0
+            got = B.cpu().numpy()
+            res["bcast"] = got[pos].tobytes()
+            gaps = np.ones(180, bool)
+            gaps[pos] = False
+            res["bcast_gaps"] = bool(np.all(got[gaps] == -1))
+        else:
+            B = buf(mine)
+            assert H.mxh_bcast(B.data_ptr(), 120, i32, n - 1, comm) == 0
+            res["bcast"] = B.cpu().numpy().tobytes()
+        owners = {s: H.mxh_comm_slot_owner(comm, s.encode()).decode() for s in ("allreduce", "allgather", "bcast")}
+        res["owners"] = owners
+        torch.cuda.synchronize()
+        H.mxh_comm_free(comm)
+        dist.destroy_process_group()
+        q.put((rank, "ok", res))
+    except Exception:  # noqa: BLE001
+        import traceback
+        q.put((rank, "err", traceback.format_exc()))
+
+
+def _run_fn(fn, n):
+    import torch.multiprocessing as mp
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=fn, args=(r, n, port, q)) for r in range(n)]
+    for p in procs:
+        p.start()
+    out = {}
+    try:
+        for _ in range(n):
+            rank, status, payload = q.get(timeout=300)
+            assert status == "ok", payload
+            out[rank] = payload
+    finally:
+        for p in procs:
+            p.join(timeout=60 if len(out) == n else 5)
+            if p.is_alive():
+                p.terminate()
+                p.join(timeout=10)
+    return out
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("n", [2, 3])
+def test_mixed_host_and_device_buffers_take_one_protocol(n):
+    import torch
+    if not torch.cuda.is_available():
+        pytest.skip("needs a GPU")
+    os.environ["HSA_ENABLE_IPC_MODE_LEGACY"] = "0"
+    got = _run_fn(_mixed_worker, n)
+    assert got[0]["owners"] == {"allreduce": "mi355x", "allgather": "mi355x", "bcast": "mi355x"}
+    import golden_io
+    import mxompi
+    FLT, INT, SUM = mxompi.TYPE["FLOAT"], mxompi.TYPE["INT32_T"], mxompi.OP["SUM"]
+    # device-path orders: coll/tuned fixed decisions / libnbc for the i-forms
+    ar = _expected(n, "flt", False, "allreduce", lambda w: 0)
+    nb = _expected_nbc(n, "flt", False, "allreduce")
+    red = _expected(n, "flt", False, "reduce", lambda w: 0)
+    scan = _expected(n, "flt", False, "scan", lambda w: 1)
+    rsb = _expected(n, "int", False, "rsb", lambda w: 0)
+    for r in range(n):
+        for key, exp in (("allreduce", ar[r]), ("allreduce_inplace", ar[r]), ("scan", scan[r]),
+                         ("iallreduce", nb[r]), ("pallreduce", nb[r])):
+            golden_io.assert_coll_equal(np.frombuffer(got[r][key], np.uint8), exp.view(np.uint8), SUM, FLT,
+                                        f"{key} rank {r} (rank 0 host buffers)")
+        np.testing.assert_array_equal(np.frombuffer(got[r]["rsb"], np.int32), rsb[r])
+    golden_io.assert_coll_equal(np.frombuffer(got[n - 1]["reduce"], np.uint8), red[n - 1].view(np.uint8), SUM, FLT,
+                                "reduce root")
+    rc = [100 + 7 * r for r in range(n)]
+    xs = [_gen("int", sum(rc), r).astype(np.int64) for r in range(n)]
+    tot = np.sum(xs, axis=0).astype(np.int32)
+    for r in range(n):
+        lo = sum(rc[:r])
+        np.testing.assert_array_equal(np.frombuffer(got[r]["reduce_scatter"], np.int32), tot[lo:lo + rc[r]])
+    full = np.concatenate([np.arange(120, dtype=np.int32) + 1000 * p for p in range(n)])
+    for r in range(n):
+        np.testing.assert_array_equal(np.frombuffer(got[r]["allgather"], np.int32), full)
+        np.testing.assert_array_equal(np.frombuffer(got[r]["bcast"], np.int32),
+                                      np.arange(120, dtype=np.int32) + 1000 * (n - 1))
+    assert got[0]["bcast_gaps"], "bcast into a vector layout wrote into its gaps"
+
+
+def _overlap_worker(rank, n, port, q):
+    """MPI-legal ordering that a collective spinning on the legacy default
+    stream would deadlock: rank 0 posts MPI_Iallreduce and then needs a
+    device copy on the default stream (what a PML's device-buffer transfer
+    does) before the host handshake that lets rank 1 post its MPI_Iallreduce.
+    The component's requests run on its own non-blocking stream, so the copy
+    completes while the collective waits for rank 1."""
+    try:
+        import time
+        import torch
+        import torch.distributed as dist
+        import minihost
+        import mxompi
+        os.environ["OMPI_MCA_coll_mi355x_wait_timeout"] = "20"
+        dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=n)
+
+        @minihost.AG
+        def ag(send, recv, nbytes, ctx):
+            out = [None] * n
+            dist.all_gather_object(out, ctypes.string_at(send, nbytes))
+            blob = b"".join(out)
+            ctypes.memmove(recv, blob, len(blob))
+            return 0
+
+        torch.cuda.set_device(0)
+        mxompi.init(0)
+        H = minihost.host(with_components=True)
+        comm = H.mxh_comm_create(rank, n, ag, None)
+        f32, SUM = minihost.dtype(H, "MPI_FLOAT"), minihost.op(H, "MPI_SUM")
+        count = 100003
+        x = _gen("flt", count, rank)
+        X, R = torch.from_numpy(x.copy()).cuda(), torch.zeros(count, device="cuda")
+        # warm up: the device communicator is created at the first eligible call
+        assert H.mxh_allreduce(X.data_ptr(), R.data_ptr(), count, f32, SUM, comm) == 0
+        Y = torch.arange(1 << 20, dtype=torch.float32, device="cuda")
+        t0 = time.time()
+        r = vp()
+        if rank == 0:
+            assert H.mxh_iallreduce(X.data_ptr(), R.data_ptr(), count, f32, SUM, comm, ctypes.byref(r)) == 0
+            y = Y.cpu()                      # default-stream device copy while rank 1 is not in the collective
+            assert float(y[-1]) == float((1 << 20) - 1)
+            dist.barrier()
+        else:
+            dist.barrier()
+            assert H.mxh_iallreduce(X.data_ptr(), R.data_ptr(), count, f32, SUM, comm, ctypes.byref(r)) == 0
+        rc = H.mxh_wait(ctypes.byref(r))
+        el = time.time() - t0
+        torch.cuda.synchronize()
+        H.mxh_comm_free(comm)
+        dist.destroy_process_group()
+        q.put((rank, "ok", {"rc": rc, "seconds": el, "out": R.cpu().numpy().tobytes()}))
+    except Exception:  # noqa: BLE001
+        import traceback
+        q.put((rank, "err", traceback.format_exc()))
+
+
+@pytest.mark.gpu
+def test_iallreduce_does_not_block_the_default_stream():
+    import torch
+    if not torch.cuda.is_available():
+        pytest.skip("needs a GPU")
+    os.environ["HSA_ENABLE_IPC_MODE_LEGACY"] = "0"
+    got = _run_fn(_overlap_worker, 2)
+    for r in range(2):
+        assert got[r]["rc"] == 0, got[r]
+        assert got[r]["seconds"] < 10.0, got[r]["seconds"]
+    import golden_io
+    import mxompi
+    import test_nbc_oracle
+    L = test_nbc_oracle._L()
+    xs = [_gen("flt", 100003, r) for r in range(2)]
+    exp = [np.zeros(100003, np.float32) for _ in range(2)]
+    assert L.mxo_iallreduce(0, mxompi.OP["SUM"], mxompi.TYPE["FLOAT"], 2, 100003,
+                            (vp * 2)(*[x.ctypes.data for x in xs]), (vp * 2)(*[e.ctypes.data for e in exp])) == 0
+    for r in range(2):
+        golden_io.assert_coll_equal(np.frombuffer(got[r]["out"], np.uint8), exp[r].view(np.uint8),
+                                    mxompi.OP["SUM"], mxompi.TYPE["FLOAT"], f"iallreduce rank {r}")
+
+
+def _dup_worker(rank, n, port, q):
+    """8 communicators over the same ranks (MPI_Comm_dup x 8): the device
+    communicator is created at each one's first eligible collective, so idle
+    duplicates cost no device memory, and a used one costs its staging
+    (coll_mi355x_staging_mb, default 256 MiB) plus ~1 KiB of flags -- no
+    point-to-point mailboxes (the coll component never uses them)."""
+    try:
+        import torch
+        import torch.distributed as dist
+        import minihost
+        import mxompi
+        os.environ["OMPI_MCA_coll_mi355x_wait_timeout"] = "60"
+        os.environ["OMPI_MCA_coll_mi355x_staging_mb"] = "64"
+        dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=n)
+
+        @minihost.AG
+        def ag(send, recv, nbytes, ctx):
+            out = [None] * n
+            dist.all_gather_object(out, ctypes.string_at(send, nbytes))
+            blob = b"".join(out)
+            ctypes.memmove(recv, blob, len(blob))
+            return 0
+
+        torch.cuda.set_device(0)
+        mxompi.init(0)
+        H = minihost.host(with_components=True)
+        f32, SUM = minihost.dtype(H, "MPI_FLOAT"), minihost.op(H, "MPI_SUM")
+        X = torch.ones(1000, device="cuda")
+        R = torch.zeros(1000, device="cuda")
+        torch.cuda.synchronize()
+        dist.barrier()     # the GPU is shared: measure while no rank allocates
+        free0 = torch.cuda.mem_get_info()[0]
+        dist.barrier()
+        comms = [H.mxh_comm_create(rank, n, ag, None) for _ in range(8)]
+        torch.cuda.synchronize()
+        dist.barrier()
+        free1 = torch.cuda.mem_get_info()[0]
+        dist.barrier()
+        sums = []
+        for c in comms:
+            R.zero_()
+            assert H.mxh_allreduce(X.data_ptr(), R.data_ptr(), 1000, f32, SUM, c) == 0
+            sums.append(float(R[0]))
+        torch.cuda.synchronize()
+        dist.barrier()
+        free2 = torch.cuda.mem_get_info()[0]
+        dist.barrier()
+        for c in comms:
+            H.mxh_comm_free(c)
+        dist.destroy_process_group()
+        q.put((rank, "ok", {"idle_bytes": free0 - free1, "used_bytes": free1 - free2, "sums": sums}))
+    except Exception:  # noqa: BLE001
+        import traceback
+        q.put((rank, "err", traceback.format_exc()))
+
+
+@pytest.mark.gpu
+def test_dup_communicators_bounded_device_memory():
+    import torch
+    if not torch.cuda.is_available():
+        pytest.skip("needs a GPU")
+    os.environ["HSA_ENABLE_IPC_MODE_LEGACY"] = "0"
+    n = 2
+    got = _run_fn(_dup_worker, n)
+    MiB = 1 << 20
+    for r in range(n):
+        g = got[r]
+        assert g["sums"] == [float(n)] * 8
+        # mem_get_info is device-wide (both ranks share the GPU): budgets are per process x n
+        assert g["idle_bytes"] < n * 8 * MiB, g
+        assert g["used_bytes"] < n * 8 * (64 + 8) * MiB, g

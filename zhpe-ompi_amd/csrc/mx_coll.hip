@@ -52,13 +52,14 @@ namespace mx {
 // multi-job byte copy (scatter push, gather, allgather, bcast)
 // ---------------------------------------------------------------------------
 struct CopyJob { const char *src; char *dst; size_t bytes; };
-struct CopyArgs { CopyJob j[MAXR]; int n; unsigned bpj; };
+struct CopyArgs { CopyJob j[MAXR]; int n; unsigned bpj; const int *poison; };
 
 // Jobs are interleaved block by block (job = blockIdx.x % n): a push to
 // n-1 peers keeps every xGMI link busy from the first wave on, instead of
 // draining the peers one after another in dispatch order.
 template <bool NT>
 __global__ void __launch_bounds__(kFB) k_copy(CopyArgs a) {
+  if (poisoned(a.poison)) return;
   const CopyJob jb = a.j[blockIdx.x % (unsigned)a.n];
   const size_t tid = (size_t)(blockIdx.x / (unsigned)a.n) * kFB + threadIdx.x;
   const uintptr_t ms = (uintptr_t)jb.src & 15, md = (uintptr_t)jb.dst & 15;
@@ -117,6 +118,12 @@ int copy_async(void *dst, const void *src, size_t bytes, hipStream_t s) {
   return mx_hip_rc(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToDevice, s));
 }
 
+// a communicator's copy: skipped on the device once the communicator is poisoned
+static int copy_launch(const mx_comm *c, CopyArgs &a, hipStream_t s) {
+  a.poison = c ? c->poison : nullptr;
+  return copy_launch(a, s);
+}
+
 // ---------------------------------------------------------------------------
 // cross-GPU flags: generation-tagged, system scope, bounded spin
 // ---------------------------------------------------------------------------
@@ -135,24 +142,27 @@ static size_t oneshot_max() {
   return v > 0 ? (size_t)v : 0;
 }
 
-struct SignalArgs { uint64_t *peer_flag[MAXR]; int n; uint64_t value; };
+struct SignalArgs { uint64_t *peer_flag[MAXR]; int n; uint64_t value; const int *poison; };
 
 __global__ void k_signal(SignalArgs a) {
   const int j = threadIdx.x;
+  if (poisoned(a.poison)) return;   // a wait before this one timed out: tell no peer anything
   __threadfence_system();  // everything this stream wrote is visible first
   if (j < a.n && a.peer_flag[j])
     __hip_atomic_store(a.peer_flag[j], a.value, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
-// Waits until flags[j] >= value for every j in `mask`.
-__global__ void k_wait(const uint64_t *flags, uint32_t mask, uint64_t value, uint64_t timeout_ticks, int *err) {
+// Waits until flags[j] >= value for every j in `mask`; a timeout raises the
+// host error and poisons the communicator (timeout_ticks = ~0: wait forever).
+__global__ void k_wait(const uint64_t *flags, uint32_t mask, uint64_t value, uint64_t timeout_ticks, int *err,
+                       int *poison) {
   const int j = threadIdx.x;
-  if (j < MAXR && ((mask >> j) & 1)) {
+  if (j < MAXR && ((mask >> j) & 1) && !poisoned(poison)) {
     const uint64_t t0 = wall_clock64();
     while (__hip_atomic_load(&flags[j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) < value) {
       __builtin_amdgcn_s_sleep(2);
       if (wall_clock64() - t0 > timeout_ticks) {
-        __hip_atomic_store(err, MX_ERR_TIMEOUT, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        raise_timeout(err, poison);
         break;
       }
     }
@@ -222,9 +232,9 @@ static void prof_collect(mx_comm *c) {
 }
 
 extern "C" int mx_comm_set_timeout(mx_comm_t *c, double seconds) {
-  if (!c || seconds <= 0) return MX_ERR_ARG;
+  if (!c || seconds < 0) return MX_ERR_ARG;
   c->timeout_s = seconds;
-  c->timeout_ticks = ticks_for(seconds);
+  c->timeout_ticks = seconds == 0 ? ~(uint64_t)0 : ticks_for(seconds);
   return MX_SUCCESS;
 }
 
@@ -248,7 +258,7 @@ extern "C" int mx_comm_create_local(int size, int device, mx_comm_t **out) {
 
 struct ipc_info {
   hipIpcMemHandle_t staging, flags, hregion;
-  int rank, device;
+  int rank, device, ok;
   uint64_t staging_bytes, hregion_bytes;
 };
 
@@ -257,75 +267,87 @@ extern "C" int mx_comm_create(int rank, int size, int device, size_t staging_byt
   return mx_comm_create_ex(rank, size, device, staging_bytes, 0, flags, ag, ctx, out);
 }
 
+// Every bootstrap exchange runs on every rank whatever happened locally:
+// each carries this rank's verdict so far, and the communicator exists only
+// if every rank says yes -- so either all ranks get one or none does (a rank
+// failing alone would otherwise leave its peers blocked in the exchange, or
+// give ranks different protocols to run).
+static int agree(mx_allgather_fn ag, void *ctx, int size, int ok) {
+  int *oks = (int *)calloc(size, sizeof(int));
+  if (!oks) return -1;   // cannot even take part: the exchange itself fails
+  int all = ag(&ok, oks, sizeof(int), ctx) == 0 ? 1 : -1;
+  for (int p = 0; p < size && all == 1; p++)
+    if (!oks[p]) all = 0;
+  free(oks);
+  return all;
+}
+
 extern "C" int mx_comm_create_ex(int rank, int size, int device, size_t staging_bytes, size_t heap_bytes, int flags,
                                  mx_allgather_fn ag, void *ctx, mx_comm_t **out) {
   if (!out || !ag || size < 1 || rank < 0 || rank >= size) return MX_ERR_ARG;
   if ((flags & MX_COMM_IPC) && size > MAXR) return MX_ERR_ARG;
-  int rc = mx_init(device);
-  if (rc) return rc;
+  int ok = mx_init(device) == MX_SUCCESS;
   mx_comm *c = (mx_comm *)calloc(1, sizeof(mx_comm));
-  if (!c) return MX_ERR_NOMEM;
-  c->rank = rank;
-  c->size = size;
-  c->device = g_device;
-  c->flags = flags;
-  c->ag = ag;
-  c->ag_ctx = ctx;
-  mx_comm_set_timeout(c, 60.0);
-  if (hipHostMalloc((void **)&c->err_host, sizeof(int), hipHostMallocMapped) != hipSuccess) goto fail;
-  *c->err_host = 0;
-  if (hipHostGetDevicePointer((void **)&c->err_dev, c->err_host, 0) != hipSuccess) goto fail;
+  ok = ok && c;
+  int rc = MX_ERR_HIP;
+  if (c) {
+    c->rank = rank;
+    c->size = size;
+    c->device = g_device;
+    c->flags = flags;
+    c->ag = ag;
+    c->ag_ctx = ctx;
+    mx_comm_set_timeout(c, 60.0);
+  }
+  ok = ok && hipHostMalloc((void **)&c->err_host, sizeof(int), hipHostMallocMapped) == hipSuccess;
+  if (ok) *c->err_host = 0;
+  ok = ok && hipHostGetDevicePointer((void **)&c->err_dev, c->err_host, 0) == hipSuccess;
+  ok = ok && hipMalloc((void **)&c->poison, sizeof(int)) == hipSuccess &&
+       hipMemset(c->poison, 0, sizeof(int)) == hipSuccess;
 
   if (flags & MX_COMM_IPC) {
-    ipc_info mine, *all = (ipc_info *)calloc(size, sizeof(ipc_info));
-    if (!all) goto fail;
-    c->staging_bytes = staging_bytes ? staging_bytes : ((size_t)64 << 20);
-    // one-shot region at the top of staging: 2 parities x n slots
-    c->os_max = std::min<size_t>(oneshot_max(), c->staging_bytes / (8 * (size_t)size)) & ~(size_t)255;
-    if (c->os_max < 1024) c->os_max = 0;
-    c->os_slot = c->os_max ? c->os_max + 256 : 0;
-    c->main_bytes = (c->staging_bytes - 2 * (size_t)size * c->os_slot) & ~(size_t)255;
-    c->hregion_bytes = heap_bytes ? ((heap_bytes + 4095) & ~(size_t)4095) : 0;
-    // point-to-point mailboxes (one per source rank) follow the staging
-    c->p2p_off = (c->staging_bytes + 4095) & ~(size_t)4095;
-    if (hipExtMallocWithFlags((void **)&c->staging, c->p2p_off + (size_t)size * P2P_BOX, hipDeviceMallocUncached) !=
-            hipSuccess ||
-        hipExtMallocWithFlags((void **)&c->flagmem, ALL_FLAG_WORDS * sizeof(uint64_t), hipDeviceMallocUncached) !=
-            hipSuccess ||
-        (c->hregion_bytes &&
-         hipExtMallocWithFlags((void **)&c->hregion, c->hregion_bytes, hipDeviceMallocUncached) != hipSuccess) ||
-        hipMemset(c->flagmem, 0, ALL_FLAG_WORDS * sizeof(uint64_t)) != hipSuccess ||
-        hipDeviceSynchronize() != hipSuccess) {
-      free(all);
-      goto fail;
-    }
+    ipc_info mine, all[MAXR];
     memset(&mine, 0, sizeof mine);
-    if (hipIpcGetMemHandle(&mine.staging, c->staging) != hipSuccess ||
-        hipIpcGetMemHandle(&mine.flags, c->flagmem) != hipSuccess ||
-        (c->hregion && hipIpcGetMemHandle(&mine.hregion, c->hregion) != hipSuccess)) {
-      free(all);
-      goto fail;
+    memset(all, 0, sizeof all);
+    if (ok) {
+      c->staging_bytes = staging_bytes ? staging_bytes : ((size_t)64 << 20);
+      // one-shot region at the top of staging: 2 parities x n slots
+      c->os_max = std::min<size_t>(oneshot_max(), c->staging_bytes / (8 * (size_t)size)) & ~(size_t)255;
+      if (c->os_max < 1024) c->os_max = 0;
+      c->os_slot = c->os_max ? c->os_max + 256 : 0;
+      c->main_bytes = (c->staging_bytes - 2 * (size_t)size * c->os_slot) & ~(size_t)255;
+      c->hregion_bytes = heap_bytes ? ((heap_bytes + 4095) & ~(size_t)4095) : 0;
+      // point-to-point mailboxes (one per source rank) follow the staging
+      c->p2p_off = (c->staging_bytes + 4095) & ~(size_t)4095;
+      const uint64_t sig[2] = {0x5EED0000ull + (uint64_t)rank, 0x5EED1000ull + (uint64_t)rank};
+      const size_t boxes = (flags & MX_COMM_P2P) ? (size_t)size * P2P_BOX : 0;
+      ok = hipExtMallocWithFlags((void **)&c->staging, c->p2p_off + boxes, hipDeviceMallocUncached) == hipSuccess &&
+           hipExtMallocWithFlags((void **)&c->flagmem, ALL_FLAG_WORDS * sizeof(uint64_t), hipDeviceMallocUncached) ==
+               hipSuccess &&
+           (!c->hregion_bytes ||
+            hipExtMallocWithFlags((void **)&c->hregion, c->hregion_bytes, hipDeviceMallocUncached) == hipSuccess) &&
+           hipMemset(c->flagmem, 0, ALL_FLAG_WORDS * sizeof(uint64_t)) == hipSuccess &&
+           hipDeviceSynchronize() == hipSuccess &&
+           hipIpcGetMemHandle(&mine.staging, c->staging) == hipSuccess &&
+           hipIpcGetMemHandle(&mine.flags, c->flagmem) == hipSuccess &&
+           (!c->hregion || hipIpcGetMemHandle(&mine.hregion, c->hregion) == hipSuccess) &&
+           // signature words, read back through every mapping below
+           hipMemcpy(c->flagmem + FLAG_WORDS, sig, sizeof sig, hipMemcpyHostToDevice) == hipSuccess &&
+           (!c->hregion || hipMemcpy(c->hregion, sig + 1, 8, hipMemcpyHostToDevice) == hipSuccess) &&
+           hipDeviceSynchronize() == hipSuccess;
+      mine.staging_bytes = c->staging_bytes;
+      mine.hregion_bytes = c->hregion_bytes;
+    } else {
+      ok = 0;
     }
     mine.rank = rank;
-    mine.device = c->device;
-    mine.staging_bytes = c->staging_bytes;
-    mine.hregion_bytes = c->hregion_bytes;
-    // signature words, read back through every mapping below
-    {
-      const uint64_t sig[2] = {0x5EED0000ull + (uint64_t)rank, 0x5EED1000ull + (uint64_t)rank};
-      if (hipMemcpy(c->flagmem + FLAG_WORDS, sig, sizeof sig, hipMemcpyHostToDevice) != hipSuccess ||
-          (c->hregion && hipMemcpy(c->hregion, sig + 1, 8, hipMemcpyHostToDevice) != hipSuccess) ||
-          hipDeviceSynchronize() != hipSuccess) {
-        free(all);
-        goto fail;
-      }
-    }
-    if (ag(&mine, all, sizeof(ipc_info), ctx) != 0) { free(all); goto fail; }
-    for (int p = 0; p < size; p++) {
-      if (all[p].staging_bytes != c->staging_bytes || all[p].hregion_bytes != c->hregion_bytes) {
-        free(all);
-        goto fail;
-      }
+    mine.device = c ? c->device : -1;
+    mine.ok = ok;
+    // exchange 1: handles + verdicts (taken part in even after a local failure)
+    if (ag(&mine, all, sizeof(ipc_info), ctx) != 0) ok = 0;
+    for (int p = 0; ok && p < size; p++)
+      if (!all[p].ok || all[p].staging_bytes != c->staging_bytes || all[p].hregion_bytes != c->hregion_bytes) ok = 0;
+    for (int p = 0; ok && p < size; p++) {
       if (p == rank) {
         c->peer_staging[p] = c->staging;
         c->peer_flags[p] = c->flagmem;
@@ -340,16 +362,13 @@ extern "C" int mx_comm_create_ex(int rank, int size, int device, size_t staging_
            hipIpcOpenMemHandle((void **)&c->peer_hregion[p], all[p].hregion, hipIpcMemLazyEnablePeerAccess) !=
                hipSuccess)) {
         fprintf(stderr, "mx_comm_create: rank %d cannot map rank %d's staging\n", rank, p);
-        free(all);
-        goto fail;
+        (void)hipGetLastError();
+        ok = 0;
       }
     }
-    free(all);
     // every mapping shows its owner's signature (a wrong IPC mapping fails
-    // creation here instead of corrupting data later); the exchange of the
-    // verdicts doubles as the "every rank mapped every peer" barrier
-    int ok = 1;
-    for (int p = 0; p < size; p++) {
+    // creation here instead of corrupting data later)
+    for (int p = 0; ok && p < size; p++) {
       uint64_t v[2] = {0, 0};
       if (hipMemcpy(v, c->peer_flags[p] + FLAG_WORDS, 8, hipMemcpyDeviceToHost) != hipSuccess ||
           v[0] != 0x5EED0000ull + (uint64_t)p ||
@@ -360,31 +379,43 @@ extern "C" int mx_comm_create_ex(int rank, int size, int device, size_t staging_
         ok = 0;
       }
     }
-    int *oks = (int *)calloc(size, sizeof(int));
-    int arc = oks ? ag(&ok, oks, sizeof(int), ctx) : -1;
-    for (int p = 0; p < size && !arc; p++)
-      if (!oks[p]) arc = -1;
-    free(oks);
-    if (arc) goto fail;
+    // exchange 2: every rank mapped every peer (doubles as the barrier)
+    const int all_ok = agree(ag, ctx, size, ok);
+    if (all_ok != 1) {
+      mx_comm_destroy(c);
+      return all_ok < 0 ? MX_ERR_HIP : MX_ERR_STATE;
+    }
+  } else {
+    const int all_ok = agree(ag, ctx, size, ok);
+    if (all_ok != 1) {
+      mx_comm_destroy(c);
+      return all_ok < 0 ? MX_ERR_HIP : MX_ERR_STATE;
+    }
   }
   if (flags & MX_COMM_RCCL) {
+    // every rank reached here (the verdicts above agreed), so the RCCL
+    // bootstrap is entered by all of them
     ncclUniqueId id, *ids = (ncclUniqueId *)calloc(size, sizeof(ncclUniqueId));
-    if (!ids) goto fail;
     memset(&id, 0, sizeof id);
-    if (rank == 0 && ncclGetUniqueId(&id) != ncclSuccess) { free(ids); goto fail; }
-    if (ag(&id, ids, sizeof(id), ctx) != 0) { free(ids); goto fail; }
-    id = ids[0];
+    ok = ids != nullptr && (rank != 0 || ncclGetUniqueId(&id) == ncclSuccess);
+    ncclUniqueId dummy[1];
+    if (ag(&id, ids ? ids : dummy, ids ? sizeof(id) : 0, ctx) != 0) ok = 0;
+    if (ok) {
+      id = ids[0];
+      if (ncclCommInitRank(&c->nccl, size, id, rank) != ncclSuccess) {
+        c->nccl = nullptr;
+        ok = 0;
+      }
+    }
     free(ids);
-    if (ncclCommInitRank(&c->nccl, size, id, rank) != ncclSuccess) {
-      c->nccl = nullptr;
-      goto fail;
+    rc = agree(ag, ctx, size, ok);
+    if (rc != 1) {
+      mx_comm_destroy(c);
+      return rc < 0 ? MX_ERR_HIP : MX_ERR_RCCL;
     }
   }
   *out = c;
   return MX_SUCCESS;
-fail:
-  mx_comm_destroy(c);
-  return MX_ERR_HIP;
 }
 
 extern "C" int mx_comm_destroy(mx_comm_t *c) {
@@ -400,6 +431,7 @@ extern "C" int mx_comm_destroy(mx_comm_t *c) {
   if (c->hregion) (void)hipFree(c->hregion);
   if (c->flagmem) (void)hipFree(c->flagmem);
   if (c->err_host) (void)hipHostFree(c->err_host);
+  if (c->poison) (void)hipFree(c->poison);
   if (c->nccl) ncclCommDestroy(c->nccl);
   if (c->prof)
     for (int i = 0; i < 64; i++) (void)hipEventDestroy(c->ev[i]);
@@ -583,6 +615,7 @@ static int finish(mx_comm *c, hipStream_t s) {
   if (c->err_host && *(volatile int *)c->err_host) {
     int e = *(volatile int *)c->err_host;
     *c->err_host = 0;
+    if (e == MX_ERR_TIMEOUT) c->poisoned = e;   // sticky: the device side is poisoned too
     return e;
   }
   return MX_SUCCESS;
@@ -591,6 +624,7 @@ static int finish(mx_comm *c, hipStream_t s) {
 // A collective about to be enqueued on `s` waits for the previous deferred
 // collective of the communicator when that one went to another stream.
 static int order(mx_comm *c, hipStream_t s) {
+  if (c->poisoned) return c->poisoned;   // a peer wait timed out earlier: nothing more on this communicator
   if (c->tail_valid && c->tail_stream != s && hipStreamWaitEvent(s, c->tail, 0) != hipSuccess) return MX_ERR_HIP;
   return MX_SUCCESS;
 }
@@ -606,6 +640,7 @@ static int run_fold(mx_comm *c, fold_launch_fn fl, const Seg &sg, size_t part_lo
   a.ndst = ndst;
   a.n = sg.hi - sg.lo;
   a.p = sg.p;
+  a.poison = c ? c->poison : nullptr;
   prof_begin(c, s);
   const int rc = fl(a, s);
   prof_end(c, s, 0, (double)(nsrc + ndst) * (double)a.n * (double)es);
@@ -727,7 +762,7 @@ extern "C" int mx_reduce_scatter_local(mx_comm_t *c, const void *const *sbufs, v
     memset(&ca, 0, sizeof ca);
     for (int p = 0; p < n; p++)
       if (rcounts[p]) ca.j[ca.n++] = CopyJob{tmp + disp[p] * es, (char *)rbufs[p], rcounts[p] * es};
-    int rc = copy_launch(ca, s);
+    int rc = copy_launch(c, ca, s);
     (void)hipFreeAsync(tmp, s);
     if (rc) return rc;
   }
@@ -752,7 +787,7 @@ extern "C" int mx_allgather_local(mx_comm_t *c, const void *const *sbufs, void *
       if (d == sb) continue;
       a.j[a.n++] = CopyJob{sb, d, bytes};
     }
-    int rc = copy_launch(a, s);
+    int rc = copy_launch(c, a, s);
     if (rc) return rc;
   }
   return finish(c, s);
@@ -767,7 +802,7 @@ extern "C" int mx_bcast_local(mx_comm_t *c, void *const *bufs, size_t bytes, int
   memset(&a, 0, sizeof a);
   for (int r = 0; r < c->size; r++)
     if (r != root) a.j[a.n++] = CopyJob{(const char *)bufs[root], (char *)bufs[r], bytes};
-  int rc = copy_launch(a, s);
+  int rc = copy_launch(c, a, s);
   if (rc) return rc;
   return finish(c, s);
 }
@@ -782,6 +817,7 @@ static int signal_all(mx_comm *c, int kind, uint64_t value, hipStream_t s) {
   memset(&a, 0, sizeof a);
   a.n = c->size;
   a.value = value;
+  a.poison = c->poison;
   for (int p = 0; p < c->size; p++)
     a.peer_flag[p] = (p == c->rank) ? nullptr : c->peer_flags[p] + kind * MAXR + c->rank;
   hipLaunchKernelGGL(k_signal, dim3(1), dim3(64), 0, s, a);
@@ -790,7 +826,7 @@ static int signal_all(mx_comm *c, int kind, uint64_t value, hipStream_t s) {
 
 static int wait_mask(mx_comm *c, int kind, uint32_t mask, uint64_t value, hipStream_t s) {
   hipLaunchKernelGGL(k_wait, dim3(1), dim3(64), 0, s, (const uint64_t *)(c->flagmem + kind * MAXR), mask, value,
-                     c->timeout_ticks, c->err_dev);
+                     c->timeout_ticks, c->err_dev, c->poison);
   return mx_check_launch();
 }
 static int wait_all(mx_comm *c, int kind, uint64_t value, hipStream_t s) {
@@ -845,6 +881,7 @@ static int allreduce_oneshot(mx_comm *c, oneshot_launch_fn ol, const std::vector
   a.gen = g;
   a.timeout_ticks = c->timeout_ticks;
   a.err = c->err_dev;
+  a.poison = c->poison;
   a.n = n;
   a.rank = r;
   a.count = count;
@@ -949,7 +986,7 @@ extern "C" int mx_allreduce(mx_comm_t *c, const void *sbuf, void *rbuf, size_t c
       ca.j[ca.n++] = CopyJob{sb + e0 * es, c->peer_staging[p] + (size_t)r * L.slot + ((e0 * es) & 15), len[p] * es};
     }
     prof_begin(c, s);
-    if ((rc = copy_launch(ca, s))) return rc;
+    if ((rc = copy_launch(c, ca, s))) return rc;
     prof_end(c, s, 1, 0);
     if ((rc = signal_all(c, FLAG_READY, g << 1, s))) return rc;
     if ((rc = wait_all(c, FLAG_READY, g << 1, s))) return rc;
@@ -979,7 +1016,7 @@ extern "C" int mx_allreduce(mx_comm_t *c, const void *sbuf, void *rbuf, size_t c
                              len[p] * es};
     }
     prof_begin(c, s);
-    if ((rc = copy_launch(ca, s))) return rc;
+    if ((rc = copy_launch(c, ca, s))) return rc;
     prof_end(c, s, 2, 0);
     if ((rc = signal_all(c, FLAG_DONE, g, s))) return rc;
   }
@@ -1039,7 +1076,7 @@ extern "C" int mx_reduce_scatter(mx_comm_t *c, const void *sbuf, void *rbuf, con
                              std::min(kc, rcounts[p] - k0) * es};
     }
     prof_begin(c, s);
-    if ((rc = copy_launch(ca, s))) return rc;
+    if ((rc = copy_launch(c, ca, s))) return rc;
     prof_end(c, s, 1, 0);
     if ((rc = signal_all(c, FLAG_READY, g << 1, s))) return rc;
     if ((rc = wait_all(c, FLAG_READY, g << 1, s))) return rc;
@@ -1093,14 +1130,14 @@ extern "C" int mx_allgather(mx_comm_t *c, const void *sbuf, void *rbuf, size_t b
     for (int p = 0; p < n; p++)
       if (p != r) ca.j[ca.n++] = CopyJob{sb + o, c->peer_staging[p] + (size_t)r * slot + ((r * bytes + o) & 15), l};
     if (sb != rb + (size_t)r * bytes) ca.j[ca.n++] = CopyJob{sb + o, rb + (size_t)r * bytes + o, l};
-    if ((rc = copy_launch(ca, s))) return rc;
+    if ((rc = copy_launch(c, ca, s))) return rc;
     if ((rc = signal_all(c, FLAG_READY, g << 1, s))) return rc;
     if ((rc = wait_all(c, FLAG_READY, g << 1, s))) return rc;
     memset(&ca, 0, sizeof ca);
     for (int p = 0; p < n; p++)
       if (p != r)
         ca.j[ca.n++] = CopyJob{c->staging + (size_t)p * slot + ((p * bytes + o) & 15), rb + (size_t)p * bytes + o, l};
-    if ((rc = copy_launch(ca, s))) return rc;
+    if ((rc = copy_launch(c, ca, s))) return rc;
     if ((rc = signal_all(c, FLAG_DONE, g, s))) return rc;
   }
   return finish(c, s);
@@ -1156,17 +1193,17 @@ extern "C" int mx_bcast(mx_comm_t *c, void *buf, size_t bytes, int root, void *s
       if (r == root) {
         for (int q = 0; q < n; q++)
           if (q != root) ca.j[ca.n++] = CopyJob{ub + o, c->peer_staging[q] + (o & 15), l};
-        if ((rc = copy_launch(ca, s))) return rc;
+        if ((rc = copy_launch(c, ca, s))) return rc;
         if ((rc = signal_all(c, FLAG_READY, g << 1, s))) return rc;
       } else {
         if ((rc = wait_mask(c, FLAG_READY, 1u << root, g << 1, s))) return rc;
         ca.j[ca.n++] = CopyJob{c->staging + (o & 15), ub + o, l};
-        if ((rc = copy_launch(ca, s))) return rc;
+        if ((rc = copy_launch(c, ca, s))) return rc;
       }
     } else if (r == root) {
       for (int q = 0; q < n; q++)
         if (q != root) ca.j[ca.n++] = CopyJob{ub + o + off[part_of(q)], slot_ptr(c->peer_staging[q], q), len[part_of(q)]};
-      if ((rc = copy_launch(ca, s))) return rc;
+      if ((rc = copy_launch(c, ca, s))) return rc;
       if ((rc = signal_all(c, FLAG_READY, g << 1, s))) return rc;
     } else {
       const int pr = part_of(r);
@@ -1175,13 +1212,13 @@ extern "C" int mx_bcast(mx_comm_t *c, void *buf, size_t bytes, int root, void *s
       for (int q = 0; q < n; q++)
         if (q != root && q != r) ca.j[ca.n++] = CopyJob{mine, slot_ptr(c->peer_staging[q], r), len[pr]};
       ca.j[ca.n++] = CopyJob{mine, ub + o + off[pr], len[pr]};
-      if ((rc = copy_launch(ca, s))) return rc;
+      if ((rc = copy_launch(c, ca, s))) return rc;
       if ((rc = signal_all(c, FLAG_PUSHED, g, s))) return rc;
       if ((rc = wait_mask(c, FLAG_PUSHED, all & ~(1u << root) & ~(1u << r), g, s))) return rc;
       memset(&ca, 0, sizeof ca);
       for (int q = 0; q < n; q++)
         if (q != root && q != r) ca.j[ca.n++] = CopyJob{slot_ptr(c->staging, q), ub + o + off[part_of(q)], len[part_of(q)]};
-      if ((rc = copy_launch(ca, s))) return rc;
+      if ((rc = copy_launch(c, ca, s))) return rc;
     }
     if ((rc = signal_all(c, FLAG_DONE, g, s))) return rc;
   }
@@ -1592,7 +1629,7 @@ static int vm_partitioned(mx_comm *c, vm_launch_fn vl, const std::vector<VmSeg> 
       ca.j[ca.n++] = CopyJob{sb + e0 * es, c->peer_staging[q] + (size_t)r * L.slot + ((e0 * es) & 15), len[q] * es};
     }
     prof_begin(c, s);
-    if ((rc = copy_launch(ca, s))) return rc;
+    if ((rc = copy_launch(c, ca, s))) return rc;
     prof_end(c, s, 1, 0);
     if ((rc = signal_all(c, FLAG_READY, (g << 1) | (uint64_t)(r == info_rank ? info_bit : 0), s))) return rc;
     if ((rc = wait_all(c, FLAG_READY, g << 1, s))) return rc;
@@ -1604,6 +1641,7 @@ static int vm_partitioned(mx_comm *c, vm_launch_fn vl, const std::vector<VmSeg> 
       const size_t mis = (e0 * es) & 15, sh = (lo - e0) * es;
       VmArgs a;
       memset(&a, 0, sizeof a);
+      a.poison = c->poison;
       if (info_rank >= 0 && info_rank != r) a.info = c->flagmem + FLAG_READY * MAXR + info_rank;
       a.info_host = info_bit;
       for (int j = 0; j < n; j++) a.src[j] = ((j == r) ? sb + e0 * es : c->staging + (size_t)j * L.slot + mis) + sh;
@@ -1629,7 +1667,7 @@ static int vm_partitioned(mx_comm *c, vm_launch_fn vl, const std::vector<VmSeg> 
                                rb + (c0 + off[q]) * es, len[q] * es};
       }
       prof_begin(c, s);
-      if ((rc = copy_launch(ca, s))) return rc;
+      if ((rc = copy_launch(c, ca, s))) return rc;
       prof_end(c, s, 2, 0);
     }
     if ((rc = signal_all(c, FLAG_DONE, g, s))) return rc;
@@ -1672,7 +1710,7 @@ static int vm_scatter_blocks(mx_comm *c, vm_launch_fn vl, const VmProg &p, const
                              std::min(kc, rcounts[q] - k0) * es};
     }
     prof_begin(c, s);
-    if ((rc = copy_launch(ca, s))) return rc;
+    if ((rc = copy_launch(c, ca, s))) return rc;
     prof_end(c, s, 1, 0);
     if ((rc = signal_all(c, FLAG_READY, gen << 1, s))) return rc;
     if ((rc = wait_all(c, FLAG_READY, gen << 1, s))) return rc;
@@ -1680,6 +1718,7 @@ static int vm_scatter_blocks(mx_comm *c, vm_launch_fn vl, const VmProg &p, const
       const size_t kl = std::min(kc, rcounts[r] - k0), e0 = disp[r] + k0, mis = (e0 * es) & 15;
       VmArgs a;
       memset(&a, 0, sizeof a);
+      a.poison = c->poison;
       for (int j = 0; j < n; j++) a.src[j] = (j == r) ? sb + e0 * es : c->staging + (size_t)j * slot + mis;
       char *dst = overlap ? c->staging + (size_t)n * slot + mis : rb + k0 * es;
       a.dst[r] = dst;
@@ -2171,6 +2210,7 @@ static int req_complete(mx_request *q) {
   if (c->err_host && *(volatile int *)c->err_host) {
     const int e = *(volatile int *)c->err_host;
     *c->err_host = 0;
+    if (e == MX_ERR_TIMEOUT) c->poisoned = e;
     return e;
   }
   if (q->kind == RQ_RECV && q->status && q->status[2]) return (int)q->status[2];   // truncation / tag
@@ -2481,23 +2521,30 @@ extern "C" int mx_shmem_reduce(mx_comm_t *c, int sop, int st, size_t dt_size, vo
 // ---------------------------------------------------------------------------
 namespace mx {
 
-struct SeqSignalArgs { uint64_t *flag[MAXR]; uint64_t value[MAXR]; };
-struct SeqWaitArgs { const uint64_t *flag[MAXR]; uint64_t value[MAXR]; uint64_t timeout_ticks; int *err; };
+struct SeqSignalArgs { uint64_t *flag[MAXR]; uint64_t value[MAXR]; const int *poison; };
+struct SeqWaitArgs {
+  const uint64_t *flag[MAXR];
+  uint64_t value[MAXR];
+  uint64_t timeout_ticks;
+  int *err;
+  int *poison;
+};
 
 __global__ void k_seq_signal(SeqSignalArgs a) {
   const int j = threadIdx.x;
+  if (poisoned(a.poison)) return;
   __threadfence_system();
   if (j < MAXR && a.flag[j]) __hip_atomic_store(a.flag[j], a.value[j], __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
 __global__ void k_seq_wait(SeqWaitArgs a) {
   const int j = threadIdx.x;
-  if (j < MAXR && a.flag[j]) {
+  if (j < MAXR && a.flag[j] && !poisoned(a.poison)) {
     const uint64_t t0 = wall_clock64();
     while (__hip_atomic_load(a.flag[j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) < a.value[j]) {
       __builtin_amdgcn_s_sleep(2);
       if (wall_clock64() - t0 > a.timeout_ticks) {
-        __hip_atomic_store(a.err, MX_ERR_TIMEOUT, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        raise_timeout(a.err, a.poison);
         break;
       }
     }
@@ -2531,6 +2578,7 @@ struct heap_info { hipIpcMemHandle_t h; uint64_t bytes; };
 // one synchronisation step among the PEs in `mask` (this PE included)
 static int heap_sync(mx_heap *h, uint32_t mask, hipStream_t s) {
   mx_comm *c = h->c;
+  if (c->poisoned) return c->poisoned;
   SeqSignalArgs sa;
   SeqWaitArgs wa;
   memset(&sa, 0, sizeof sa);
@@ -2545,6 +2593,8 @@ static int heap_sync(mx_heap *h, uint32_t mask, hipStream_t s) {
   }
   wa.timeout_ticks = c->timeout_ticks;
   wa.err = c->err_dev;
+  wa.poison = c->poison;
+  sa.poison = c->poison;
   hipLaunchKernelGGL(k_seq_signal, dim3(1), dim3(64), 0, s, sa);
   int rc = mx_check_launch();
   if (rc) return rc;
@@ -2863,8 +2913,8 @@ namespace mx {
 
 constexpr size_t kAccLockWord = 384;   // heap flag page: words 0..15 pair sequences, 256 signature
 
-__global__ void k_acc_lock(uint64_t *lock, uint64_t tag, uint64_t timeout_ticks, int *err) {
-  if (threadIdx.x == 0) {
+__global__ void k_acc_lock(uint64_t *lock, uint64_t tag, uint64_t timeout_ticks, int *err, int *poison) {
+  if (threadIdx.x == 0 && !poisoned(poison)) {
     const uint64_t t0 = wall_clock64();
     uint64_t expect = 0;
     while (!__hip_atomic_compare_exchange_strong(lock, &expect, tag, __ATOMIC_ACQUIRE, __ATOMIC_RELAXED,
@@ -2872,7 +2922,7 @@ __global__ void k_acc_lock(uint64_t *lock, uint64_t tag, uint64_t timeout_ticks,
       expect = 0;
       __builtin_amdgcn_s_sleep(4);
       if (wall_clock64() - t0 > timeout_ticks) {
-        __hip_atomic_store(err, MX_ERR_TIMEOUT, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        raise_timeout(err, poison);
         break;
       }
     }
@@ -2912,8 +2962,15 @@ static uint64_t *acc_lock_word(mx_heap *h, int pe) {
 
 static int acc_lock(mx_heap *h, int pe, hipStream_t s) {
   hipLaunchKernelGGL(k_acc_lock, dim3(1), dim3(64), 0, s, acc_lock_word(h, pe), (uint64_t)h->c->rank + 1,
-                     h->c->timeout_ticks, h->c->err_dev);
-  return mx_check_launch();
+                     h->c->timeout_ticks, h->c->err_dev, h->c->poison);
+  int rc = mx_check_launch();
+  // with a bounded wait the lock may not have been taken: find out before
+  // the read-modify-write runs (the element kernels take no poison word)
+  if (!rc && h->c->timeout_ticks != ~(uint64_t)0) {
+    if (hipStreamSynchronize(s) != hipSuccess) return MX_ERR_HIP;
+    if (*(volatile int *)h->c->err_host) rc = finish(h->c, s);
+  }
+  return rc;
 }
 
 static int acc_unlock(mx_heap *h, int pe, hipStream_t s) {

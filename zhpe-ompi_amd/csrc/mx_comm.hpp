@@ -61,6 +61,13 @@ struct mx_comm {
   uint64_t *flagmem;           // mine: [NFLAGS][mx::MAXR]
   uint64_t *peer_flags[mx::MAXR];  // mapped views
   int *err_host, *err_dev;
+  // poison word (device memory): set by the kernel whose peer wait timed
+  // out; every later copy / fold / signal kernel of the communicator sees
+  // it and does nothing, so no peer is handed stale staging data and no
+  // staging a late peer still reads is overwritten.  `poisoned` is the
+  // host's sticky copy: every later call fails with it.
+  int *poison;
+  int poisoned;
   uint64_t gen;
   double timeout_s;
   uint64_t timeout_ticks;

@@ -37,6 +37,17 @@ enum { FLAG_READY = 0, FLAG_PUSHED = 1, FLAG_DONE = 2, NFLAGS = 3 };
 constexpr int OSWG = 64;
 constexpr int OS_MAXSEG = 16;
 
+// Poisoned communicator (mx_comm::poison): a peer wait of an earlier kernel
+// timed out.  The word is device memory written at agent scope; kernels of
+// the same stream that run later see it (kernel boundaries order it).
+__device__ __forceinline__ bool poisoned(const int *poison) {
+  return poison && __hip_atomic_load(poison, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0;
+}
+__device__ __forceinline__ void raise_timeout(int *err, int *poison) {
+  __hip_atomic_store(err, MX_ERR_TIMEOUT, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  if (poison) __hip_atomic_store(poison, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
 // ---------------------------------------------------------------------------
 // fold programs
 // ---------------------------------------------------------------------------
@@ -58,6 +69,7 @@ struct FoldArgs {
   char *dst[MAXR];
   int ndst;
   size_t n, head, nvec;  // elements; scalar head; 16-B vectors after head
+  const int *poison;     // communicator poison word (null: local)
   FoldProg p;
 };
 
@@ -115,6 +127,7 @@ __device__ __forceinline__ V eval_prog(const FoldProg &p, L LD) {
 
 template <class T, class OP, bool NT>
 __global__ void __launch_bounds__(kFB) k_fold(FoldArgs a) {
+  if (poisoned(a.poison)) return;
   using V = fvec<T>;
   constexpr int N = V::N;
   const size_t tid = (size_t)blockIdx.x * kFB + threadIdx.x;
@@ -201,6 +214,7 @@ struct OneShotArgs {
   uint64_t *counter;
   uint64_t counter_last, gen, timeout_ticks;
   int *err;
+  int *poison;
   int n, rank, nseg;
   size_t count, es, slice;
   OsSeg seg[OS_MAXSEG];
@@ -208,12 +222,12 @@ struct OneShotArgs {
 
 constexpr int kOSB = 256;
 
-__device__ __forceinline__ void os_spin(const uint64_t *f, uint64_t v, uint64_t ticks, int *err) {
+__device__ __forceinline__ void os_spin(const uint64_t *f, uint64_t v, uint64_t ticks, int *err, int *poison) {
   const uint64_t t0 = wall_clock64();
   while (__hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) < v) {
     __builtin_amdgcn_s_sleep(1);
     if (wall_clock64() - t0 > ticks) {
-      __hip_atomic_store(err, MX_ERR_TIMEOUT, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      raise_timeout(err, poison);
       break;
     }
   }
@@ -223,9 +237,18 @@ template <class T, class OP>
 __global__ void __launch_bounds__(kOSB) k_oneshot(OneShotArgs a) {
   const int w = blockIdx.x, t = threadIdx.x;
   const size_t lo = (size_t)w * a.slice, hi = lo + a.slice < a.count ? lo + a.slice : a.count;
-  // (1) every peer is past gen-2: its reads of this parity buffer are over
-  if (t < a.n && t != a.rank && a.gen > 2) os_spin(a.my_done + t, a.gen - 2, a.timeout_ticks, a.err);
+  // poison checks are taken by thread 0 and shared, so the whole workgroup
+  // leaves together (no thread may skip a barrier the others reach)
+  __shared__ int s_bad;
+  if (t == 0) s_bad = poisoned(a.poison);
   __syncthreads();
+  if (s_bad) return;
+  // (1) every peer is past gen-2: its reads of this parity buffer are over
+  if (t < a.n && t != a.rank && a.gen > 2) os_spin(a.my_done + t, a.gen - 2, a.timeout_ticks, a.err, a.poison);
+  __syncthreads();
+  if (t == 0) s_bad = poisoned(a.poison);
+  __syncthreads();
+  if (s_bad) return;   // a peer never freed its buffer: push nothing
   // (2) push my slice (bytes [lo*es, hi*es)) to every peer
   if (lo < hi) {
     const size_t b0 = lo * a.es, b1 = hi * a.es;
@@ -246,10 +269,13 @@ __global__ void __launch_bounds__(kOSB) k_oneshot(OneShotArgs a) {
   // (3) READY(me, w) at every peer; (4) wait READY(p, w) from every peer
   if (t < a.n && t != a.rank) {
     __hip_atomic_store(a.peer_ready[t] + w, a.gen, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
-    os_spin(a.my_ready + (size_t)t * OSWG + w, a.gen, a.timeout_ticks, a.err);
+    os_spin(a.my_ready + (size_t)t * OSWG + w, a.gen, a.timeout_ticks, a.err, a.poison);
   }
   __syncthreads();
+  if (t == 0) s_bad = poisoned(a.poison);
+  __syncthreads();
   __atomic_thread_fence(__ATOMIC_ACQUIRE);
+  if (s_bad) return;   // stale slots: no fold, and DONE is never raised
   // (5) fold the slice
   int sidx = 0;
   for (size_t e = lo + t; e < hi; e += kOSB) {
@@ -307,6 +333,7 @@ struct VmArgs {
   const char *src[MAXR];
   char *dst[MAXR];
   size_t n, head, nvec;
+  const int *poison;      // communicator poison word (null: local)
   const uint64_t *info;   // READY word carrying the info bit (bit 0), or null
   int info_host;          // info bit when `info` is null
   VmProg p;
@@ -344,6 +371,7 @@ __global__ void __launch_bounds__(kVB) k_vm(VmArgs a) {
   constexpr int N = V::N;
   constexpr int SLOT = vm_slot<T>();
   extern __shared__ __align__(16) char vm_lds[];
+  if (poisoned(a.poison)) return;
   char *const my = vm_lds + (size_t)threadIdx.x * SLOT;
   const size_t tid = (size_t)blockIdx.x * kVB + threadIdx.x;
   const int info = a.info ? (int)(__hip_atomic_load(a.info, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) & 1)

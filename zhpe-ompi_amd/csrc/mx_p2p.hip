@@ -323,7 +323,8 @@ void p2p_status_put(int64_t *st) {
 // caller's stream; *done_stream receives the stream completion is on.
 int p2p_enqueue(mx_request *q, hipStream_t *done_stream) {
   mx_comm *c = q->c;
-  if (c->local || !(c->flags & MX_COMM_IPC)) return MX_ERR_STATE;
+  if (c->local || !(c->flags & MX_COMM_IPC) || !(c->flags & MX_COMM_P2P)) return MX_ERR_STATE;
+  if (c->poisoned) return c->poisoned;
   int rc = p2p_setup(c);
   if (rc) return rc;
   const bool send = q->kind == RQ_SEND;

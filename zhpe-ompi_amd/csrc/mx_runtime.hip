@@ -6,6 +6,7 @@
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
+#include <pthread.h>
 #include "mx_internal.h"
 #include "mx_mem.hpp"
 
@@ -73,16 +74,135 @@ extern "C" int mx_finalize(void) {
   return MX_SUCCESS;
 }
 
+// Buffer classification is on every op-handler and coll-slot call (the
+// framework's function tables are fixed at init), so device
+// allocations are remembered as address ranges: a pointer inside a known
+// range answers without a HIP call.  A miss asks the runtime once
+// (hipPointerGetAttributes, then hipMemGetAddressRange for the allocation's
+// extent) and replaces the least recently used entry.  Host pointers are not
+// cached (a host page never turns into device memory; a freed device range
+// can only come back as another device allocation from the same aperture).
+namespace {
+constexpr int kPtrCache = 64;
+struct PtrRange { uintptr_t lo, hi; uint64_t used; };
+PtrRange g_ranges[kPtrCache];
+uint64_t g_ptr_clock;
+pthread_mutex_t g_ptr_mu = PTHREAD_MUTEX_INITIALIZER;
+}  // namespace
+
+// MX_PTR_CACHE=0 disables the cache (the before/after measurement of
+// profiles/r02/op_call_cost.txt)
+static bool ptr_cache_on() {
+  static const bool on = [] {
+    const char *e = getenv("MX_PTR_CACHE");
+    return !(e && e[0] == '0');
+  }();
+  return on;
+}
+
 extern "C" int mx_is_device_ptr(const void *p) {
   if (!p) return 0;
+  const uintptr_t a = (uintptr_t)p;
+  if (!ptr_cache_on()) {
+    hipPointerAttribute_t attr;
+    memset(&attr, 0, sizeof attr);
+    if (hipPointerGetAttributes(&attr, p) != hipSuccess) {
+      (void)hipGetLastError();
+      return 0;
+    }
+    return (attr.type == hipMemoryTypeDevice || attr.type == hipMemoryTypeManaged) ? 1 : 0;
+  }
+  pthread_mutex_lock(&g_ptr_mu);
+  for (int i = 0; i < kPtrCache; i++)
+    if (a >= g_ranges[i].lo && a < g_ranges[i].hi) {
+      g_ranges[i].used = ++g_ptr_clock;
+      pthread_mutex_unlock(&g_ptr_mu);
+      return 1;
+    }
+  pthread_mutex_unlock(&g_ptr_mu);
   hipPointerAttribute_t attr;
   memset(&attr, 0, sizeof attr);
-  hipError_t e = hipPointerGetAttributes(&attr, p);
-  if (e != hipSuccess) {
-    (void)hipGetLastError();  // unregistered host memory: clear the sticky error
+  if (hipPointerGetAttributes(&attr, p) != hipSuccess) {
+    // unregistered host memory: the runtime reports it as an error; take
+    // back exactly that error so a later launch check does not see it
+    (void)hipGetLastError();
     return 0;
   }
-  return (attr.type == hipMemoryTypeDevice || attr.type == hipMemoryTypeManaged) ? 1 : 0;
+  if (attr.type != hipMemoryTypeDevice && attr.type != hipMemoryTypeManaged) return 0;
+  void *base = nullptr;
+  size_t bytes = 0;
+  if (hipMemGetAddressRange(&base, &bytes, (void *)p) == hipSuccess && base && bytes) {
+    pthread_mutex_lock(&g_ptr_mu);
+    int victim = 0;
+    for (int i = 1; i < kPtrCache; i++)
+      if (g_ranges[i].used < g_ranges[victim].used) victim = i;
+    g_ranges[victim] = PtrRange{(uintptr_t)base, (uintptr_t)base + bytes, ++g_ptr_clock};
+    pthread_mutex_unlock(&g_ptr_mu);
+  } else {
+    (void)hipGetLastError();
+  }
+  return 1;
+}
+
+// Forget cached device ranges overlapping [p, p + bytes) (the allocation is
+// being freed by a caller that knows it; mx_free does this itself).
+extern "C" int mx_ptr_cache_forget(const void *p, size_t bytes) {
+  const uintptr_t lo = (uintptr_t)p, hi = lo + (bytes ? bytes : 1);
+  pthread_mutex_lock(&g_ptr_mu);
+  for (int i = 0; i < kPtrCache; i++)
+    if (g_ranges[i].lo < hi && lo < g_ranges[i].hi) g_ranges[i] = PtrRange{0, 0, 0};
+  pthread_mutex_unlock(&g_ptr_mu);
+  return MX_SUCCESS;
+}
+
+extern "C" int mx_alloc(size_t bytes, void **p) {
+  if (!p) return MX_ERR_ARG;
+  *p = nullptr;
+  if (!bytes) return MX_SUCCESS;
+  if (int rc = mx_ensure_init()) return rc;
+  return hipMalloc(p, bytes) == hipSuccess ? MX_SUCCESS : MX_ERR_NOMEM;
+}
+
+extern "C" int mx_free(void *p) {
+  if (!p) return MX_SUCCESS;
+  void *base = nullptr;
+  size_t bytes = 0;
+  if (hipMemGetAddressRange(&base, &bytes, p) == hipSuccess) mx_ptr_cache_forget(base, bytes);
+  else (void)hipGetLastError();
+  return mx_hip_rc(hipFree(p));
+}
+
+extern "C" int mx_memcpy(void *dst, const void *src, size_t bytes, void *stream) {
+  if (!bytes) return MX_SUCCESS;
+  if (!dst || !src) return MX_ERR_ARG;
+  return mx_hip_rc(hipMemcpyAsync(dst, src, bytes, hipMemcpyDefault, (hipStream_t)stream));
+}
+
+extern "C" int mx_stream_create(void **stream) {
+  if (!stream) return MX_ERR_ARG;
+  if (int rc = mx_ensure_init()) return rc;
+  hipStream_t s = nullptr;
+  if (hipStreamCreateWithFlags(&s, hipStreamNonBlocking) != hipSuccess) return MX_ERR_HIP;
+  *stream = s;
+  return MX_SUCCESS;
+}
+
+extern "C" int mx_stream_destroy(void *stream) {
+  return stream ? mx_hip_rc(hipStreamDestroy((hipStream_t)stream)) : MX_SUCCESS;
+}
+
+// `stream` waits (on the device) for everything queued on `after` so far.
+// A thread-local event per calling thread: the record and the wait are the
+// only host work.
+extern "C" int mx_stream_order(void *stream, void *after) {
+  if (stream == after) return MX_SUCCESS;
+  static thread_local hipEvent_t ev = nullptr;
+  if (!ev && hipEventCreateWithFlags(&ev, hipEventDisableTiming) != hipSuccess) {
+    ev = nullptr;
+    return MX_ERR_HIP;
+  }
+  if (hipEventRecord(ev, (hipStream_t)after) != hipSuccess) return MX_ERR_HIP;
+  return mx_hip_rc(hipStreamWaitEvent((hipStream_t)stream, ev, 0));
 }
 
 extern "C" int mx_stream_sync(void *stream) {

@@ -2,38 +2,52 @@
  * coll_mi355x.c -- the `mi355x` component of Open MPI's `coll` framework.
  *
  * Takes the allreduce / reduce_scatter / allgather / bcast slots (plus
- * reduce / reduce_scatter_block / scan / exscan and, above coll/self's
- * priority, reduce_local) of a communicator and runs them
- * on the MI355X all-peer path of libmx_kernels.so (include/mx_coll.h) when
- * the buffers are device memory; everything else is handed to the module
- * that owned the slot before us.
+ * reduce / reduce_scatter_block / scan / exscan, their nonblocking and
+ * persistent forms and, above coll/self's priority, reduce_local) of a
+ * communicator and runs them on the MI355X all-peer path of
+ * libmx_kernels.so (include/mx_coll.h).
  *
  * Follows the reference's stacking accelerator component, coll/cuda:
  *  - comm_query returns a module with only the slots we implement
  *    (coll_cuda_module.c:79-117); priority 80 by default (above tuned's 30
- *    and coll/cuda's 78, below coll/self's 75 only for reduce_local unless
- *    raised), MCA var coll_mi355x_priority;
+ *    and coll/cuda's 78, and above coll/self's 75 for reduce_local), MCA var
+ *    coll_mi355x_priority;
  *  - module_enable saves and RETAINs the previous c_coll slot + module for
  *    delegation (CHECK_AND_RETAIN, coll_cuda_module.c:120-155) and fails with
- *    OMPI_ERR_NOT_FOUND if a needed lower slot is missing;
- *  - the device/host decision is taken per call from the buffers
- *    (coll_cuda_allreduce.c:39-56) -- but instead of staging through host
- *    memory the device path runs the collective on the GPUs.
+ *    OMPI_ERR_NOT_FOUND if a needed lower slot is missing.
+ *
+ * Every rank of a communicator must run the same protocol, so whether a call
+ * takes the device path depends only on what MPI requires to match across
+ * ranks -- the op, the type signature, the counts, the root -- and on state
+ * all ranks agreed on (the device communicator, created collectively at the
+ * first eligible call).  Where the buffers live does NOT enter the decision:
+ * coll/cuda makes the same point the other way round (every rank stages its
+ * device buffers through the host and calls the same lower collective,
+ * coll_cuda_allreduce.c:30-73).  Here a rank whose buffer is host memory (or
+ * a non-contiguous layout) stages it through device scratch; device buffers
+ * are used in place.
+ *
+ * The device work runs on a stream the module owns (non-blocking: a wait
+ * for a late peer never stalls the process's legacy default stream, e.g. a
+ * PML copy), ordered after the work already queued on the default stream.
+ * Peer waits are unbounded by default (a peer may legally arrive arbitrarily
+ * late); coll_mi355x_wait_timeout bounds them, and a timeout poisons the
+ * communicator (include/mx_coll.h).
+ *
  * The nonblocking and persistent slots (iallreduce, ireduce, ireduce_scatter,
  * ireduce_scatter_block, iscan, iexscan, iallgather, ibcast and their
- * *_init forms) replace coll/libnbc's for device buffers: the collective is
- * enqueued on the GPU and the request completes through a progress
- * callback that polls its event (libnbc's ompi_coll_libnbc_progress,
- * coll_libnbc_component.c:426-482, progresses the schedule on the host
- * instead); reduction orders are libnbc's, algorithm selection follows the
- * coll_libnbc_<coll>_algorithm vars (coll_mi355x_<coll>_algorithm wins).
- * The algorithm is chosen with coll/tuned's fixed decision
- * (coll_tuned_decision_fixed.c:44-95, :466-512) unless forced with the MCA
- * vars coll_mi355x_allreduce_algorithm / coll_mi355x_reduce_scatter_algorithm
- * (same numbering as coll_tuned_*_algorithm), so results match coll/tuned
- * bit for bit.  The mx communicator is created at enable time with the
- * saved host allgather as the bootstrap exchange.
+ * *_init forms) replace coll/libnbc's: the collective is enqueued on the GPU
+ * and the request completes through a progress callback that polls its event
+ * (libnbc's ompi_coll_libnbc_progress, coll_libnbc_component.c:426-482,
+ * progresses the schedule on the host instead); reduction orders are
+ * libnbc's, algorithm selection follows the coll_libnbc_<coll>_algorithm vars
+ * (coll_mi355x_<coll>_algorithm wins).  The blocking algorithm is chosen with
+ * coll/tuned's fixed decision (coll_tuned_decision_fixed.c:44-95, :466-512)
+ * unless forced with coll_mi355x_allreduce_algorithm /
+ * coll_mi355x_reduce_scatter_algorithm (coll_tuned_*_algorithm numbering), so
+ * results match coll/tuned bit for bit.
  */
+#include <limits.h>
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
@@ -42,10 +56,17 @@
 #include "mx_kernels.h"
 #include "mx_ompi_abi.h"
 
+/* device scratch a staged buffer lives in (grown on demand, kept) */
+typedef struct { void *p; size_t bytes; } mx_scratch_t;
+enum { SCR_IN, SCR_OUT, SCR_N };
+
 typedef struct {
     mca_coll_base_module_t super;
     struct ompi_communicator_t *comm;
     mx_comm_t *mx;
+    int mx_state;         /* 0 not created yet, 1 ready, -1 unavailable (agreed by all ranks) */
+    void *stream;         /* module-owned non-blocking stream */
+    mx_scratch_t scratch[SCR_N];
     /* delegation targets (the slots we replaced) */
     mca_coll_base_module_allreduce_fn_t prev_allreduce;
     mca_coll_base_module_t *prev_allreduce_module;
@@ -102,10 +123,12 @@ static int map_rc(int rc)
     }
 }
 
-static void coll_module_destruct(void *obj)
+/* releases what the module holds; the object itself is freed by OBJ_RELEASE */
+static void coll_module_destruct(mx_coll_module_t *m)
 {
-    mx_coll_module_t *m = (mx_coll_module_t *)obj;
     if (m->mx) mx_comm_destroy(m->mx);
+    for (int k = 0; k < SCR_N; k++) mx_free(m->scratch[k].p);
+    if (m->stream) mx_stream_destroy(m->stream);
     if (m->prev_allreduce_module) MX_OBJ_RELEASE(m->prev_allreduce_module);
     if (m->prev_reduce_scatter_module) MX_OBJ_RELEASE(m->prev_reduce_scatter_module);
     if (m->prev_allgather_module) MX_OBJ_RELEASE(m->prev_allgather_module);
@@ -118,38 +141,174 @@ static void coll_module_destruct(void *obj)
 #define MX_RELEASE_PREV(name) if (m->prev_##name##_module) MX_OBJ_RELEASE(m->prev_##name##_module);
     MX_NB_SLOTS(MX_RELEASE_PREV)
 #undef MX_RELEASE_PREV
-    free(m);
 }
 
-static mx_obj_class_t mx_coll_module_class = {"mx_coll_module_t", coll_module_destruct};
-
-static int on_device(const void *p) { return p != MPI_IN_PLACE && mx_is_device_ptr(p) == 1; }
+MX_MODULE_CLASS(mx_coll_module_t, mca_coll_base_module_t, coll_module_destruct);
 
 /* Bootstrap exchange for mx_comm_create: the saved host allgather on
  * MPI_BYTE buffers (host memory, so it never recurses into us). */
 static int bootstrap_allgather(const void *send, void *recv, size_t bytes, void *ctx)
 {
     mx_coll_module_t *m = (mx_coll_module_t *)ctx;
+    if (bytes > INT_MAX) return -1;
     return m->prev_allgather(send, (int)bytes, mx_ompi_host->byte_dtype, recv, (int)bytes,
                              mx_ompi_host->byte_dtype, m->comm, m->prev_allgather_module);
 }
 
-/* ---- slots -------------------------------------------------------------- */
+/* The device communicator, created at the first call every rank found
+ * eligible (eligibility only uses arguments MPI requires to match, so all
+ * ranks get here in the same call).  mx_comm_create is itself collective and
+ * either succeeds on every rank or on none, so mx_state agrees everywhere. */
+static int comm_ready(mx_coll_module_t *m)
+{
+    if (m->mx_state) return m->mx_state > 0;
+    const int n = mx_ompi_host->comm_size(m->comm), rank = mx_ompi_host->comm_rank(m->comm);
+    const size_t staging = (size_t)mx_ompi_host->mca_int("coll_mi355x_staging_mb", 256) << 20;
+    int flags = MX_COMM_IPC;
+    if (mx_ompi_host->mca_int("coll_mi355x_rccl", 0)) flags |= MX_COMM_RCCL;
+    int rc = mx_comm_create(rank, n, -1, staging, flags, bootstrap_allgather, m, &m->mx);
+    if (rc == MX_SUCCESS) {
+        const int t = mx_ompi_host->mca_int("coll_mi355x_wait_timeout", 0);
+        rc = mx_comm_set_timeout(m->mx, t > 0 ? (double)t : 0.0);
+    }
+    /* the stream is process-local: a failure here is reported by the calls,
+     * never turned into a different protocol on this rank */
+    if (rc == MX_SUCCESS && !m->stream && mx_stream_create(&m->stream) != MX_SUCCESS) m->stream = NULL;
+    if (rc != MX_SUCCESS) {
+        if (m->mx) mx_comm_destroy(m->mx);
+        m->mx = NULL;
+        m->mx_state = -1;
+        return 0;
+    }
+    m->mx_state = 1;
+    return 1;
+}
+
+/* ---- staging of host / non-contiguous buffers ---------------------------- */
+
+static int scratch(mx_coll_module_t *m, int k, size_t bytes, void **p)
+{
+    mx_scratch_t *s = &m->scratch[k];
+    if (s->bytes < bytes) {
+        mx_free(s->p);
+        s->p = NULL;
+        s->bytes = 0;
+        const size_t want = bytes < ((size_t)1 << 20) ? ((size_t)1 << 20) : bytes;
+        if (mx_alloc(want, &s->p) != MX_SUCCESS) return MX_ERR_NOMEM;
+        s->bytes = want;
+    }
+    *p = s->p;
+    return MX_SUCCESS;
+}
+
+/* A caller buffer as the device path sees it (`count` elements of `dt`):
+ *  dev      what to hand to mx_* (the buffer itself if it is contiguous
+ *           device memory, else scratch k);
+ *  user     the caller's buffer, for the copy back (NULL: nothing to copy). */
+typedef struct {
+    void *dev, *user;
+    size_t bytes;
+    struct ompi_datatype_t *dt;
+    int count, contiguous;
+} xbuf_t;
+
+/* contiguous bytes [0, bytes) of a non-contiguous layout <-> packed */
+static int xfer_packed(mx_coll_module_t *m, const xbuf_t *x, void *packed_dev, int to_device)
+{
+    ptrdiff_t lo = 0, hi = 0;
+    if (!mx_ompi_host->dtype_pack || !mx_ompi_host->dtype_unpack || !mx_ompi_host->dtype_span ||
+        mx_ompi_host->dtype_span(x->dt, x->count, &lo, &hi) != OMPI_SUCCESS || hi < lo)
+        return MX_ERR_UNSUPPORTED;
+    const int on_dev = mx_is_device_ptr(x->user) == 1;
+    char *span = NULL, *packed = malloc(x->bytes ? x->bytes : 1);
+    char *user = (char *)x->user;
+    int rc = packed ? MX_SUCCESS : MX_ERR_NOMEM;
+    if (!rc && on_dev) {   /* the convertor walks host memory: bring the span over */
+        span = malloc((size_t)(hi - lo) ? (size_t)(hi - lo) : 1);
+        if (!span) rc = MX_ERR_NOMEM;
+        else if (!(rc = mx_memcpy(span, user + lo, (size_t)(hi - lo), m->stream))) rc = mx_stream_sync(m->stream);
+        user = span - lo;
+    }
+    if (!rc && to_device) {
+        if (mx_ompi_host->dtype_pack(x->dt, x->count, user, packed) != OMPI_SUCCESS) rc = MX_ERR_ARG;
+        if (!rc) rc = mx_memcpy(packed_dev, packed, x->bytes, m->stream);
+        if (!rc) rc = mx_stream_sync(m->stream);
+    } else if (!rc) {
+        if (!(rc = mx_memcpy(packed, packed_dev, x->bytes, m->stream))) rc = mx_stream_sync(m->stream);
+        if (!rc && mx_ompi_host->dtype_unpack(x->dt, x->count, packed, user) != OMPI_SUCCESS) rc = MX_ERR_ARG;
+        if (!rc && on_dev && !(rc = mx_memcpy((char *)x->user + lo, span, (size_t)(hi - lo), m->stream)))
+            rc = mx_stream_sync(m->stream);
+    }
+    free(span);
+    free(packed);
+    return rc;
+}
+
+/* stage `count` x `dt` at `user`; copy_in: the call reads it */
+static int xin(mx_coll_module_t *m, int k, const void *user, struct ompi_datatype_t *dt, size_t count, int copy_in,
+               xbuf_t *x)
+{
+    memset(x, 0, sizeof *x);
+    x->bytes = count * mx_ompi_host->dtype_size(dt);
+    x->dt = dt;
+    x->count = count > INT_MAX ? INT_MAX : (int)count;
+    x->contiguous = mx_ompi_host->dtype_contiguous(dt, x->count);
+    if (x->contiguous && (!x->bytes || mx_is_device_ptr(user) == 1)) {
+        x->dev = (void *)user;   /* in place: nothing to copy back */
+        return MX_SUCCESS;
+    }
+    int rc = scratch(m, k, x->bytes, &x->dev);
+    if (rc) return rc;
+    x->user = (void *)user;
+    if (!copy_in) return MX_SUCCESS;
+    if (!x->contiguous) return xfer_packed(m, x, x->dev, 1);
+    return mx_memcpy(x->dev, user, x->bytes, m->stream);
+}
+
+/* copy the first `bytes` of a staged result back to the caller */
+static int xout(mx_coll_module_t *m, xbuf_t *x, size_t bytes)
+{
+    if (!x->user || !bytes) return MX_SUCCESS;
+    if (!x->contiguous) return xfer_packed(m, x, x->dev, 0);
+    int rc = mx_memcpy(x->user, x->dev, bytes, m->stream);
+    return rc ? rc : mx_stream_sync(m->stream);
+}
+
+/* the device work of a call starts after what the legacy default stream
+ * already holds (the caller's kernels filling the buffers) */
+static int begin(mx_coll_module_t *m)
+{
+    return m->stream ? mx_stream_order(m->stream, NULL) : MX_SUCCESS;
+}
+
+/* reduction eligibility: intrinsic op with a kernel for the (predefined)
+ * type -- identical on every rank for a correct MPI program */
+static int reducible(struct ompi_datatype_t *dtype, struct ompi_op_t *op, size_t count, int n, int *slot, int *opi)
+{
+    *slot = mx_ompi_host->dtype_slot(dtype);
+    *opi = mx_ompi_host->op_index(op);
+    return count > 0 && n <= MX_MAX_RANKS && *slot >= 0 && (mx_ompi_host->op_flags(op) & OMPI_OP_FLAGS_INTRINSIC) &&
+           mx_op_supported(*opi, *slot, MX_TABLE_WITH_FORTRAN);
+}
+
+/* ---- blocking slots -------------------------------------------------------- */
 
 static int mx_coll_allreduce(const void *sbuf, void *rbuf, int count, struct ompi_datatype_t *dtype,
                              struct ompi_op_t *op, struct ompi_communicator_t *comm, mca_coll_base_module_t *module)
 {
     mx_coll_module_t *m = (mx_coll_module_t *)module;
-    const int slot = mx_ompi_host->dtype_slot(dtype);
-    const int opi = mx_ompi_host->op_index(op);
-    const int sb_dev = (sbuf == MPI_IN_PLACE) ? 1 : on_device(sbuf);
-    if (m->mx && count > 0 && slot >= 0 && (mx_ompi_host->op_flags(op) & OMPI_OP_FLAGS_INTRINSIC) &&
-        mx_op_supported(opi, slot, MX_TABLE_WITH_FORTRAN) && mx_ompi_host->dtype_contiguous(dtype, count) &&
-        sb_dev && on_device(rbuf)) {
+    const int n = mx_ompi_host->comm_size(comm);
+    int slot, opi;
+    if (reducible(dtype, op, (size_t)count, n, &slot, &opi) && comm_ready(m)) {
         const int alg = mx_ompi_host->mca_int("coll_mi355x_allreduce_algorithm", MX_ALLREDUCE_AUTO);
-        int rc = mx_allreduce(m->mx, sbuf == MPI_IN_PLACE ? MX_IN_PLACE : sbuf, rbuf, (size_t)count, slot, opi,
-                              alg, NULL);
-        if (rc != MX_ERR_UNSUPPORTED) return map_rc(rc);
+        const int inplace = sbuf == MPI_IN_PLACE;
+        xbuf_t s, r;
+        int rc = begin(m);
+        if (!rc && !inplace) rc = xin(m, SCR_IN, sbuf, dtype, (size_t)count, 1, &s);
+        if (!rc) rc = xin(m, SCR_OUT, rbuf, dtype, (size_t)count, inplace, &r);
+        if (!rc) rc = mx_allreduce(m->mx, inplace ? MX_IN_PLACE : s.dev, r.dev, (size_t)count, slot, opi, alg, m->stream);
+        if (!rc) rc = xout(m, &r, r.bytes);
+        return map_rc(rc);
     }
     return m->prev_allreduce(sbuf, rbuf, count, dtype, op, comm, m->prev_allreduce_module);
 }
@@ -159,21 +318,24 @@ static int mx_coll_reduce_scatter(const void *sbuf, void *rbuf, const int *rcoun
                                   mca_coll_base_module_t *module)
 {
     mx_coll_module_t *m = (mx_coll_module_t *)module;
-    const int slot = mx_ompi_host->dtype_slot(dtype);
-    const int opi = mx_ompi_host->op_index(op);
-    const int n = mx_ompi_host->comm_size(comm);
-    if (m->mx && slot >= 0 && (mx_ompi_host->op_flags(op) & OMPI_OP_FLAGS_INTRINSIC) &&
-        mx_op_supported(opi, slot, MX_TABLE_WITH_FORTRAN) && n <= MX_MAX_RANKS &&
-        (sbuf == MPI_IN_PLACE || on_device(sbuf)) && on_device(rbuf)) {
-        size_t rc64[MX_MAX_RANKS];
-        int total = 0;
-        for (int i = 0; i < n; i++) { rc64[i] = (size_t)rcounts[i]; total += rcounts[i]; }
-        if (mx_ompi_host->dtype_contiguous(dtype, total)) {
-            const int alg = mx_ompi_host->mca_int("coll_mi355x_reduce_scatter_algorithm", MX_RS_AUTO);
-            int rc = mx_reduce_scatter(m->mx, sbuf == MPI_IN_PLACE ? MX_IN_PLACE : sbuf, rbuf, rc64, slot, opi,
-                                       alg, NULL);
-            if (rc != MX_ERR_UNSUPPORTED && rc != MX_ERR_NOMEM) return map_rc(rc);
+    const int n = mx_ompi_host->comm_size(comm), rank = mx_ompi_host->comm_rank(comm);
+    size_t rc64[MX_MAX_RANKS], total = 0;
+    int slot, opi;
+    for (int i = 0; i < n && i < MX_MAX_RANKS; i++) { rc64[i] = (size_t)rcounts[i]; total += rc64[i]; }
+    if (reducible(dtype, op, total, n, &slot, &opi) && comm_ready(m)) {
+        const int alg = mx_ompi_host->mca_int("coll_mi355x_reduce_scatter_algorithm", MX_RS_AUTO);
+        const int inplace = sbuf == MPI_IN_PLACE;
+        xbuf_t s, r;
+        int rc = begin(m);
+        if (!rc && !inplace) rc = xin(m, SCR_IN, sbuf, dtype, total, 1, &s);
+        /* MPI_IN_PLACE: rbuf holds the whole input vector */
+        if (!rc) rc = xin(m, SCR_OUT, rbuf, dtype, inplace ? total : rc64[rank], inplace, &r);
+        if (!rc) rc = mx_reduce_scatter(m->mx, inplace ? MX_IN_PLACE : s.dev, r.dev, rc64, slot, opi, alg, m->stream);
+        if (!rc) {
+            r.count = rcounts[rank];
+            rc = xout(m, &r, rc64[rank] * mx_ompi_host->dtype_size(dtype));
         }
+        return map_rc(rc);
     }
     return m->prev_reduce_scatter(sbuf, rbuf, rcounts, dtype, op, comm, m->prev_reduce_scatter_module);
 }
@@ -184,13 +346,20 @@ static int mx_coll_allgather(const void *sbuf, int scount, struct ompi_datatype_
 {
     mx_coll_module_t *m = (mx_coll_module_t *)module;
     const size_t rbytes = (size_t)rcount * mx_ompi_host->dtype_size(rdtype);
-    const int n = mx_ompi_host->comm_size(comm);
-    if (m->mx && rbytes && on_device(rbuf) && mx_ompi_host->dtype_contiguous(rdtype, rcount * n) &&
-        (sbuf == MPI_IN_PLACE ||
-         (on_device(sbuf) && mx_ompi_host->dtype_contiguous(sdtype, scount) &&
-          (size_t)scount * mx_ompi_host->dtype_size(sdtype) == rbytes))) {
-        int rc = mx_allgather(m->mx, sbuf == MPI_IN_PLACE ? MX_IN_PLACE : sbuf, rbuf, rbytes, NULL);
-        if (rc != MX_ERR_UNSUPPORTED) return map_rc(rc);
+    const int n = mx_ompi_host->comm_size(comm), rank = mx_ompi_host->comm_rank(comm);
+    /* (rcount, rdtype) is significant, and its signature equal, on every rank */
+    if (rbytes && n <= MX_MAX_RANKS && comm_ready(m)) {
+        const int inplace = sbuf == MPI_IN_PLACE;
+        xbuf_t s, r;
+        int rc = begin(m);
+        if (!rc && !inplace) rc = xin(m, SCR_IN, sbuf, sdtype, (size_t)scount, 1, &s);
+        if (!rc && !inplace && s.bytes != rbytes) rc = MX_ERR_ARG;   /* type signatures differ */
+        if (!rc) rc = xin(m, SCR_OUT, rbuf, rdtype, (size_t)rcount * n, inplace, &r);
+        if (!rc)
+            rc = mx_allgather(m->mx, inplace ? MX_IN_PLACE : s.dev, r.dev, rbytes, m->stream);
+        if (!rc) rc = xout(m, &r, r.bytes);
+        (void)rank;
+        return map_rc(rc);
     }
     return m->prev_allgather(sbuf, scount, sdtype, rbuf, rcount, rdtype, comm, m->prev_allgather_module);
 }
@@ -200,23 +369,30 @@ static int mx_coll_bcast(void *buf, int count, struct ompi_datatype_t *dtype, in
 {
     mx_coll_module_t *m = (mx_coll_module_t *)module;
     const size_t bytes = (size_t)count * mx_ompi_host->dtype_size(dtype);
-    if (m->mx && bytes && on_device(buf) && mx_ompi_host->dtype_contiguous(dtype, count)) {
-        int rc = mx_bcast(m->mx, buf, bytes, root, NULL);
-        if (rc != MX_ERR_UNSUPPORTED) return map_rc(rc);
+    const int n = mx_ompi_host->comm_size(comm), rank = mx_ompi_host->comm_rank(comm);
+    if (bytes && n <= MX_MAX_RANKS && comm_ready(m)) {
+        xbuf_t b;
+        int rc = begin(m);
+        if (!rc) rc = xin(m, SCR_OUT, buf, dtype, (size_t)count, rank == root, &b);
+        if (!rc) rc = mx_bcast(m->mx, b.dev, bytes, root, m->stream);
+        if (!rc && rank != root) rc = xout(m, &b, bytes);
+        return map_rc(rc);
     }
     return m->prev_bcast(buf, count, dtype, root, comm, m->prev_bcast_module);
 }
 
+/* MPI_Reduce_local has no peers: the per-call buffer check is all it needs */
 static int mx_coll_reduce_local(const void *inbuf, void *inoutbuf, int count, struct ompi_datatype_t *dtype,
                                 struct ompi_op_t *op, mca_coll_base_module_t *module)
 {
     mx_coll_module_t *m = (mx_coll_module_t *)module;
-    const int slot = mx_ompi_host->dtype_slot(dtype);
-    const int opi = mx_ompi_host->op_index(op);
-    if (count > 0 && slot >= 0 && (mx_ompi_host->op_flags(op) & OMPI_OP_FLAGS_INTRINSIC) &&
-        mx_op_supported(opi, slot, MX_TABLE_WITH_FORTRAN) && on_device(inbuf) && on_device(inoutbuf)) {
-        int rc = mx_reduce2(opi, slot, inbuf, inoutbuf, (size_t)count, NULL);
-        if (rc == MX_SUCCESS) rc = mx_stream_sync(NULL);
+    int slot, opi;
+    if (reducible(dtype, op, (size_t)count, 1, &slot, &opi) && mx_is_device_ptr(inbuf) == 1 &&
+        mx_is_device_ptr(inoutbuf) == 1) {
+        if (!m->stream && mx_stream_create(&m->stream) != MX_SUCCESS) m->stream = NULL;
+        int rc = begin(m);
+        if (!rc) rc = mx_reduce2(opi, slot, inbuf, inoutbuf, (size_t)count, m->stream);
+        if (!rc) rc = mx_stream_sync(m->stream);
         return map_rc(rc);
     }
     return m->prev_reduce_local(inbuf, inoutbuf, count, dtype, op, m->prev_reduce_local_module);
@@ -224,35 +400,31 @@ static int mx_coll_reduce_local(const void *inbuf, void *inoutbuf, int count, st
 
 /* Reduction slots beyond the four of the north star:
  * MPI_Reduce (coll.h:239-241), MPI_Reduce_scatter_block (:245-247),
- * MPI_Scan / MPI_Exscan (:248-250, :228-230).  Same device / host split
- * and delegation; algorithms follow coll/tuned's fixed decisions (reduce:
- * coll_tuned_decision_fixed.c:354-429; reduce_scatter_block: basic_linear,
- * :522-532) and coll/basic's linear scan / exscan (tuned leaves those slots
- * empty, coll_tuned_module.c:106,112), or the forced algorithm of the MCA
- * vars coll_mi355x_{reduce,scan,exscan}_algorithm (tuned's numbering). */
-static int reducible(mx_coll_module_t *m, struct ompi_datatype_t *dtype, struct ompi_op_t *op, int count, int *slot,
-                     int *opi)
-{
-    *slot = mx_ompi_host->dtype_slot(dtype);
-    *opi = mx_ompi_host->op_index(op);
-    return m->mx && count > 0 && *slot >= 0 && (mx_ompi_host->op_flags(op) & OMPI_OP_FLAGS_INTRINSIC) &&
-           mx_op_supported(*opi, *slot, MX_TABLE_WITH_FORTRAN) && mx_ompi_host->dtype_contiguous(dtype, count);
-}
-
+ * MPI_Scan / MPI_Exscan (:248-250, :228-230).  Algorithms follow coll/tuned's
+ * fixed decisions (reduce: coll_tuned_decision_fixed.c:354-429;
+ * reduce_scatter_block: basic_linear, :522-532) and coll/basic's linear scan /
+ * exscan (tuned leaves those slots empty, coll_tuned_module.c:106,112), or
+ * the forced algorithm of coll_mi355x_{reduce,scan,exscan}_algorithm. */
 static int mx_coll_reduce(const void *sbuf, void *rbuf, int count, struct ompi_datatype_t *dtype,
                           struct ompi_op_t *op, int root, struct ompi_communicator_t *comm,
                           mca_coll_base_module_t *module)
 {
     mx_coll_module_t *m = (mx_coll_module_t *)module;
-    const int rank = mx_ompi_host->comm_rank(comm);
+    const int n = mx_ompi_host->comm_size(comm), rank = mx_ompi_host->comm_rank(comm);
     int slot, opi;
-    /* rbuf matters on the root only (MPI-3.1 5.9.1) */
-    if (reducible(m, dtype, op, count, &slot, &opi) && (sbuf == MPI_IN_PLACE ? rank == root : on_device(sbuf)) &&
-        (rank != root || on_device(rbuf))) {
+    if (reducible(dtype, op, (size_t)count, n, &slot, &opi) && comm_ready(m)) {
         const int alg = mx_ompi_host->mca_int("coll_mi355x_reduce_algorithm", MX_REDUCE_AUTO);
-        int rc = mx_reduce(m->mx, sbuf == MPI_IN_PLACE ? MX_IN_PLACE : sbuf, rank == root ? rbuf : NULL,
-                           (size_t)count, slot, opi, root, alg, NULL);
-        if (rc != MX_ERR_UNSUPPORTED) return map_rc(rc);
+        const int inplace = sbuf == MPI_IN_PLACE && rank == root;   /* rbuf matters on the root only */
+        xbuf_t s, r;
+        memset(&r, 0, sizeof r);
+        int rc = begin(m);
+        if (!rc && !inplace) rc = xin(m, SCR_IN, sbuf, dtype, (size_t)count, 1, &s);
+        if (!rc && rank == root) rc = xin(m, SCR_OUT, rbuf, dtype, (size_t)count, inplace, &r);
+        if (!rc)
+            rc = mx_reduce(m->mx, inplace ? MX_IN_PLACE : s.dev, rank == root ? r.dev : NULL, (size_t)count, slot, opi,
+                           root, alg, m->stream);
+        if (!rc && rank == root) rc = xout(m, &r, r.bytes);
+        return map_rc(rc);
     }
     return m->prev_reduce(sbuf, rbuf, count, dtype, op, root, comm, m->prev_reduce_module);
 }
@@ -263,63 +435,132 @@ static int mx_coll_reduce_scatter_block(const void *sbuf, void *rbuf, int rcount
 {
     mx_coll_module_t *m = (mx_coll_module_t *)module;
     const int n = mx_ompi_host->comm_size(comm);
+    const size_t total = (size_t)rcount * (size_t)n;
     int slot, opi;
-    if (reducible(m, dtype, op, rcount * n, &slot, &opi) && (sbuf == MPI_IN_PLACE || on_device(sbuf)) &&
-        on_device(rbuf)) {
+    if (reducible(dtype, op, total, n, &slot, &opi) && comm_ready(m)) {
         const int alg = mx_ompi_host->mca_int("coll_mi355x_reduce_algorithm", MX_REDUCE_AUTO);
-        int rc = mx_reduce_scatter_block(m->mx, sbuf == MPI_IN_PLACE ? MX_IN_PLACE : sbuf, rbuf, (size_t)rcount,
-                                         slot, opi, alg, NULL);
-        if (rc != MX_ERR_UNSUPPORTED) return map_rc(rc);
+        const int inplace = sbuf == MPI_IN_PLACE;
+        xbuf_t s, r;
+        int rc = begin(m);
+        if (!rc && !inplace) rc = xin(m, SCR_IN, sbuf, dtype, total, 1, &s);
+        if (!rc) rc = xin(m, SCR_OUT, rbuf, dtype, inplace ? total : (size_t)rcount, inplace, &r);
+        if (!rc)
+            rc = mx_reduce_scatter_block(m->mx, inplace ? MX_IN_PLACE : s.dev, r.dev, (size_t)rcount, slot, opi, alg,
+                                         m->stream);
+        if (!rc) {
+            r.count = rcount;
+            rc = xout(m, &r, (size_t)rcount * mx_ompi_host->dtype_size(dtype));
+        }
+        return map_rc(rc);
     }
     return m->prev_reduce_scatter_block(sbuf, rbuf, rcount, dtype, op, comm, m->prev_reduce_scatter_block_module);
 }
 
+/* returns 1 when the call should be delegated */
 static int scan_common(mx_coll_module_t *m, const void *sbuf, void *rbuf, int count, struct ompi_datatype_t *dtype,
-                       struct ompi_op_t *op, int exclusive)
+                       struct ompi_op_t *op, int exclusive, int *ret)
 {
+    const int n = mx_ompi_host->comm_size(m->comm);
     int slot, opi;
-    if (reducible(m, dtype, op, count, &slot, &opi) && (sbuf == MPI_IN_PLACE || on_device(sbuf)) &&
-        on_device(rbuf)) {
-        const int alg = mx_ompi_host->mca_int(exclusive ? "coll_mi355x_exscan_algorithm"
-                                                        : "coll_mi355x_scan_algorithm", MX_SCAN_AUTO);
-        const void *sb = sbuf == MPI_IN_PLACE ? MX_IN_PLACE : sbuf;
-        int rc = exclusive ? mx_exscan(m->mx, sb, rbuf, (size_t)count, slot, opi, alg, NULL)
-                           : mx_scan(m->mx, sb, rbuf, (size_t)count, slot, opi, alg, NULL);
-        if (rc != MX_ERR_UNSUPPORTED) return map_rc(rc);
-    }
-    return 1;   /* delegate */
+    if (!reducible(dtype, op, (size_t)count, n, &slot, &opi) || !comm_ready(m)) return 1;
+    const int alg = mx_ompi_host->mca_int(exclusive ? "coll_mi355x_exscan_algorithm" : "coll_mi355x_scan_algorithm",
+                                          MX_SCAN_AUTO);
+    const int inplace = sbuf == MPI_IN_PLACE;
+    xbuf_t s, r;
+    int rc = begin(m);
+    if (!rc && !inplace) rc = xin(m, SCR_IN, sbuf, dtype, (size_t)count, 1, &s);
+    /* exscan leaves rank 0's rbuf untouched: stage it in so the copy back is a no-op */
+    if (!rc) rc = xin(m, SCR_OUT, rbuf, dtype, (size_t)count, inplace || exclusive, &r);
+    const void *sb = inplace ? MX_IN_PLACE : s.dev;
+    if (!rc)
+        rc = exclusive ? mx_exscan(m->mx, sb, r.dev, (size_t)count, slot, opi, alg, m->stream)
+                       : mx_scan(m->mx, sb, r.dev, (size_t)count, slot, opi, alg, m->stream);
+    if (!rc) rc = xout(m, &r, r.bytes);
+    *ret = map_rc(rc);
+    return 0;
 }
 
 static int mx_coll_scan(const void *sbuf, void *rbuf, int count, struct ompi_datatype_t *dtype,
                         struct ompi_op_t *op, struct ompi_communicator_t *comm, mca_coll_base_module_t *module)
 {
     mx_coll_module_t *m = (mx_coll_module_t *)module;
-    int rc = scan_common(m, sbuf, rbuf, count, dtype, op, 0);
-    return rc != 1 ? rc : m->prev_scan(sbuf, rbuf, count, dtype, op, comm, m->prev_scan_module);
+    int ret;
+    if (!scan_common(m, sbuf, rbuf, count, dtype, op, 0, &ret)) return ret;
+    return m->prev_scan(sbuf, rbuf, count, dtype, op, comm, m->prev_scan_module);
 }
 
 static int mx_coll_exscan(const void *sbuf, void *rbuf, int count, struct ompi_datatype_t *dtype,
                           struct ompi_op_t *op, struct ompi_communicator_t *comm, mca_coll_base_module_t *module)
 {
     mx_coll_module_t *m = (mx_coll_module_t *)module;
-    int rc = scan_common(m, sbuf, rbuf, count, dtype, op, 1);
-    return rc != 1 ? rc : m->prev_exscan(sbuf, rbuf, count, dtype, op, comm, m->prev_exscan_module);
+    int ret;
+    if (!scan_common(m, sbuf, rbuf, count, dtype, op, 1, &ret)) return ret;
+    return m->prev_exscan(sbuf, rbuf, count, dtype, op, comm, m->prev_exscan_module);
 }
 
 /* ---- nonblocking and persistent slots ------------------
  * A device-path request is an mx_request_t (include/mx_coll.h) wrapped in a
  * host ompi_request_t; active ones sit on a list that the progress callback
  * (registered once, like libnbc's) polls with mx_test and completes.  The
- * GPU needs no host progress: polling only reports completion. */
+ * GPU needs no host progress: polling only reports completion.  A staged
+ * buffer belongs to its request (requests overlap): it is filled when the
+ * operation starts and copied back when the progress callback sees the
+ * device part complete. */
 typedef struct mx_coll_req {
     struct ompi_request_t *req;
     mx_request_t *mx;
+    mx_coll_module_t *m;
     struct mx_coll_req *next;
     int active;
+    /* staged buffers: s (input, copied in at every start) and r (output,
+     * copied in too when the operation reads it; copied back at completion) */
+    xbuf_t s, r;
+    int s_in, r_in;
+    size_t r_back;   /* bytes of r copied back */
 } mx_coll_req_t;
 
 static mx_coll_req_t *g_active;
 static int g_progress_registered;
+
+static void req_release_staging(mx_coll_req_t *r)
+{
+    if (r->s.user) mx_free(r->s.dev);
+    if (r->r.user) mx_free(r->r.dev);
+    r->s.user = r->r.user = NULL;
+}
+
+/* a request's own staging (not the module's scratch: requests overlap) */
+static int req_stage(mx_coll_req_t *q, const void *user, struct ompi_datatype_t *dt, size_t count, int copy_in,
+                     xbuf_t *x)
+{
+    memset(x, 0, sizeof *x);
+    x->bytes = count * mx_ompi_host->dtype_size(dt);
+    x->dt = dt;
+    x->count = count > INT_MAX ? INT_MAX : (int)count;
+    x->contiguous = mx_ompi_host->dtype_contiguous(dt, x->count);
+    if (x->contiguous && (!x->bytes || mx_is_device_ptr(user) == 1)) {
+        x->dev = (void *)user;
+        return MX_SUCCESS;
+    }
+    if (mx_alloc(x->bytes, &x->dev) != MX_SUCCESS) return MX_ERR_NOMEM;
+    x->user = (void *)user;
+    (void)copy_in;   /* filled by req_fill at each start */
+    return MX_SUCCESS;
+}
+
+static int req_fill(mx_coll_req_t *q)
+{
+    mx_coll_module_t *m = q->m;
+    int rc = begin(m);
+    const xbuf_t *xs[2] = {&q->s, &q->r};
+    const int in[2] = {q->s_in, q->r_in};
+    for (int i = 0; i < 2 && !rc; i++) {
+        const xbuf_t *x = xs[i];
+        if (!x->user || !in[i]) continue;
+        rc = x->contiguous ? mx_memcpy(x->dev, x->user, x->bytes, m->stream) : xfer_packed(m, x, x->dev, 1);
+    }
+    return rc;
+}
 
 static int mx_coll_progress(void)
 {
@@ -328,10 +569,11 @@ static int mx_coll_progress(void)
     while (*pp) {
         mx_coll_req_t *r = *pp;
         int flag = 0;
-        const int rc = mx_test(r->mx, &flag);
+        int rc = mx_test(r->mx, &flag);
         if (flag || rc != MX_SUCCESS) {
             *pp = r->next;
             r->active = 0;
+            if (rc == MX_SUCCESS && r->r.user) rc = xout(r->m, &r->r, r->r_back);
             mx_ompi_host->request_complete(r->req, map_rc(rc));
             completed++;
         } else {
@@ -358,7 +600,8 @@ static void deactivate(mx_coll_req_t *r)
 static int req_start_cb(struct ompi_request_t *req)     /* MPI_Start */
 {
     mx_coll_req_t *r = (mx_coll_req_t *)mx_ompi_host->request_ctx(req);
-    const int rc = mx_start(r->mx);
+    int rc = req_fill(r);
+    if (!rc) rc = mx_start(r->mx);
     if (rc != MX_SUCCESS) return map_rc(rc);
     mx_ompi_host->request_activate(req);
     activate(r);
@@ -370,23 +613,33 @@ static int req_free_cb(struct ompi_request_t *req)      /* MPI_Request_free */
     mx_coll_req_t *r = (mx_coll_req_t *)mx_ompi_host->request_ctx(req);
     if (r->active) deactivate(r);
     const int rc = mx_request_free(r->mx);   /* lets an active operation finish */
+    req_release_staging(r);
     free(r);
     return map_rc(rc);
 }
 
-/* wrap an mx request (rc from its creation) into *request; returns 1 when
- * the call should be delegated instead */
-static int post(int rc, mx_request_t *mxr, int persistent, struct ompi_request_t **request, int *ret)
+/* a request wrapper with its staged buffers (NULL on failure) */
+static mx_coll_req_t *req_new(mx_coll_module_t *m)
 {
-    if (rc == MX_ERR_UNSUPPORTED || rc == MX_ERR_NOMEM) return 1;
-    if (rc != MX_SUCCESS) { *ret = map_rc(rc); return 0; }
     mx_coll_req_t *r = calloc(1, sizeof *r);
-    if (r) r->req = mx_ompi_host->request_create(persistent, req_start_cb, req_free_cb, r);
-    if (!r || !r->req) {
-        mx_request_free(mxr);
+    if (r) r->m = m;
+    return r;
+}
+
+/* wrap the mx request created with rc into *request */
+static int post(mx_coll_req_t *r, int rc, mx_request_t *mxr, int persistent, struct ompi_request_t **request)
+{
+    if (rc != MX_SUCCESS) {
+        req_release_staging(r);
         free(r);
-        *ret = OMPI_ERR_OUT_OF_RESOURCE;
-        return 0;
+        return map_rc(rc);
+    }
+    r->req = mx_ompi_host->request_create(persistent, req_start_cb, req_free_cb, r);
+    if (!r->req) {
+        mx_request_free(mxr);
+        req_release_staging(r);
+        free(r);
+        return OMPI_ERR_OUT_OF_RESOURCE;
     }
     r->mx = mxr;
     if (!g_progress_registered) {
@@ -395,8 +648,7 @@ static int post(int rc, mx_request_t *mxr, int persistent, struct ompi_request_t
     }
     if (!persistent) activate(r);
     *request = r->req;
-    *ret = OMPI_SUCCESS;
-    return 0;
+    return OMPI_SUCCESS;
 }
 
 /* coll_mi355x_<name>_algorithm, defaulting to coll_libnbc_<name>_algorithm */
@@ -408,19 +660,55 @@ static int nbc_alg(const char *name)
     return mx_ompi_host->mca_int(a, mx_ompi_host->mca_int(b, 0));
 }
 
+/* Common set-up of a device-path request: staging of sbuf (count_s
+ * elements, read) and rbuf (count_r elements, read when r_in, copied back
+ * r_back bytes); a nonblocking request is filled here, a persistent one at
+ * each start.  Returns the request or NULL (error in *ret). */
+static mx_coll_req_t *req_setup(mx_coll_module_t *m, const void *sbuf, size_t count_s, struct ompi_datatype_t *sdt,
+                                void *rbuf, size_t count_r, struct ompi_datatype_t *rdt, int r_in, size_t r_back,
+                                int persistent, int *ret)
+{
+    mx_coll_req_t *r = req_new(m);
+    int rc = r ? MX_SUCCESS : MX_ERR_NOMEM;
+    if (!rc && sbuf && sbuf != MPI_IN_PLACE) {
+        rc = req_stage(r, sbuf, sdt, count_s, 1, &r->s);
+        r->s_in = 1;
+    } else if (r) {
+        r->s.dev = (void *)sbuf;
+    }
+    if (!rc && rbuf) {
+        rc = req_stage(r, rbuf, rdt, count_r, r_in, &r->r);
+        r->r_in = r_in;
+        r->r_back = r_back;
+        r->r.count = rdt && mx_ompi_host->dtype_size(rdt) ? (int)(r_back / mx_ompi_host->dtype_size(rdt)) : 0;
+    }
+    if (!rc && !persistent) rc = req_fill(r);
+    if (rc) {
+        if (r) { req_release_staging(r); free(r); }
+        *ret = map_rc(rc);
+        return NULL;
+    }
+    return r;
+}
+#define SB(r) ((r)->s.dev == MPI_IN_PLACE ? MX_IN_PLACE : (r)->s.dev)
+
+/* returns 1 when the call should be delegated */
 static int allreduce_like(mx_coll_module_t *m, const void *sbuf, void *rbuf, int count, struct ompi_datatype_t *dtype,
                           struct ompi_op_t *op, int persistent, struct ompi_request_t **request, int *ret)
 {
+    const int n = mx_ompi_host->comm_size(m->comm);
     int slot, opi;
     mx_request_t *q = NULL;
-    if (!reducible(m, dtype, op, count, &slot, &opi) || !(sbuf == MPI_IN_PLACE || on_device(sbuf)) ||
-        !on_device(rbuf))
-        return 1;
-    const void *sb = sbuf == MPI_IN_PLACE ? MX_IN_PLACE : sbuf;
+    if (!reducible(dtype, op, (size_t)count, n, &slot, &opi) || !comm_ready(m)) return 1;
+    const size_t bytes = (size_t)count * mx_ompi_host->dtype_size(dtype);
+    mx_coll_req_t *r = req_setup(m, sbuf, (size_t)count, dtype, rbuf, (size_t)count, dtype, sbuf == MPI_IN_PLACE,
+                                 bytes, persistent, ret);
+    if (!r) return 0;
     const int alg = nbc_alg("iallreduce");
-    const int rc = persistent ? mx_allreduce_init(m->mx, sb, rbuf, (size_t)count, slot, opi, alg, NULL, &q)
-                              : mx_iallreduce(m->mx, sb, rbuf, (size_t)count, slot, opi, alg, NULL, &q);
-    return post(rc, q, persistent, request, ret);
+    const int rc = persistent ? mx_allreduce_init(m->mx, SB(r), r->r.dev, (size_t)count, slot, opi, alg, m->stream, &q)
+                              : mx_iallreduce(m->mx, SB(r), r->r.dev, (size_t)count, slot, opi, alg, m->stream, &q);
+    *ret = post(r, rc, q, persistent, request);
+    return 0;
 }
 
 static int mx_coll_iallreduce(const void *sbuf, void *rbuf, int count, struct ompi_datatype_t *dtype,
@@ -448,18 +736,21 @@ static int reduce_like(mx_coll_module_t *m, const void *sbuf, void *rbuf, int co
                        struct ompi_op_t *op, int root, struct ompi_communicator_t *comm, int persistent,
                        struct ompi_request_t **request, int *ret)
 {
-    const int rank = mx_ompi_host->comm_rank(comm);
+    const int n = mx_ompi_host->comm_size(comm), rank = mx_ompi_host->comm_rank(comm);
     int slot, opi;
     mx_request_t *q = NULL;
-    if (!reducible(m, dtype, op, count, &slot, &opi) || !(sbuf == MPI_IN_PLACE ? rank == root : on_device(sbuf)) ||
-        (rank == root && !on_device(rbuf)))
-        return 1;
-    const void *sb = sbuf == MPI_IN_PLACE ? MX_IN_PLACE : sbuf;
-    void *rb = rank == root ? rbuf : NULL;
+    if (!reducible(dtype, op, (size_t)count, n, &slot, &opi) || !comm_ready(m)) return 1;
+    const int inplace = sbuf == MPI_IN_PLACE && rank == root;
+    const size_t bytes = (size_t)count * mx_ompi_host->dtype_size(dtype);
+    mx_coll_req_t *r = req_setup(m, inplace ? MPI_IN_PLACE : sbuf, (size_t)count, dtype, rank == root ? rbuf : NULL,
+                                 (size_t)count, dtype, inplace, bytes, persistent, ret);
+    if (!r) return 0;
+    void *rb = rank == root ? r->r.dev : NULL;
     const int alg = nbc_alg("ireduce");
-    const int rc = persistent ? mx_reduce_init(m->mx, sb, rb, (size_t)count, slot, opi, root, alg, NULL, &q)
-                              : mx_ireduce(m->mx, sb, rb, (size_t)count, slot, opi, root, alg, NULL, &q);
-    return post(rc, q, persistent, request, ret);
+    const int rc = persistent ? mx_reduce_init(m->mx, SB(r), rb, (size_t)count, slot, opi, root, alg, m->stream, &q)
+                              : mx_ireduce(m->mx, SB(r), rb, (size_t)count, slot, opi, root, alg, m->stream, &q);
+    *ret = post(r, rc, q, persistent, request);
+    return 0;
 }
 
 static int mx_coll_ireduce(const void *sbuf, void *rbuf, int count, struct ompi_datatype_t *dtype, struct ompi_op_t *op,
@@ -488,24 +779,27 @@ static int rs_like(mx_coll_module_t *m, const void *sbuf, void *rbuf, const int 
                    struct ompi_datatype_t *dtype, struct ompi_op_t *op, struct ompi_communicator_t *comm,
                    int persistent, struct ompi_request_t **request, int *ret)
 {
-    const int n = mx_ompi_host->comm_size(comm);
-    size_t rc64[MX_MAX_RANKS];
-    int total = 0, slot, opi;
+    const int n = mx_ompi_host->comm_size(comm), rank = mx_ompi_host->comm_rank(comm);
+    size_t rc64[MX_MAX_RANKS], total = 0;
+    int slot, opi;
     mx_request_t *q = NULL;
     if (n > MX_MAX_RANKS) return 1;
-    for (int i = 0; i < n; i++) { rc64[i] = (size_t)(rcounts ? rcounts[i] : rcount); total += (int)rc64[i]; }
-    if (!reducible(m, dtype, op, total, &slot, &opi) || !(sbuf == MPI_IN_PLACE || on_device(sbuf)) ||
-        !on_device(rbuf))
-        return 1;
-    const void *sb = sbuf == MPI_IN_PLACE ? MX_IN_PLACE : sbuf;
+    for (int i = 0; i < n; i++) { rc64[i] = (size_t)(rcounts ? rcounts[i] : rcount); total += rc64[i]; }
+    if (!reducible(dtype, op, total, n, &slot, &opi) || !comm_ready(m)) return 1;
+    const int inplace = sbuf == MPI_IN_PLACE;
+    const size_t es = mx_ompi_host->dtype_size(dtype);
+    mx_coll_req_t *r = req_setup(m, sbuf, total, dtype, rbuf, inplace ? total : rc64[rank], dtype, inplace,
+                                 rc64[rank] * es, persistent, ret);
+    if (!r) return 0;
     int rc;
     if (rcounts)
-        rc = persistent ? mx_reduce_scatter_init(m->mx, sb, rbuf, rc64, slot, opi, NULL, &q)
-                        : mx_ireduce_scatter(m->mx, sb, rbuf, rc64, slot, opi, NULL, &q);
+        rc = persistent ? mx_reduce_scatter_init(m->mx, SB(r), r->r.dev, rc64, slot, opi, m->stream, &q)
+                        : mx_ireduce_scatter(m->mx, SB(r), r->r.dev, rc64, slot, opi, m->stream, &q);
     else
-        rc = persistent ? mx_reduce_scatter_block_init(m->mx, sb, rbuf, (size_t)rcount, slot, opi, NULL, &q)
-                        : mx_ireduce_scatter_block(m->mx, sb, rbuf, (size_t)rcount, slot, opi, NULL, &q);
-    return post(rc, q, persistent, request, ret);
+        rc = persistent ? mx_reduce_scatter_block_init(m->mx, SB(r), r->r.dev, (size_t)rcount, slot, opi, m->stream, &q)
+                        : mx_ireduce_scatter_block(m->mx, SB(r), r->r.dev, (size_t)rcount, slot, opi, m->stream, &q);
+    *ret = post(r, rc, q, persistent, request);
+    return 0;
 }
 
 static int mx_coll_ireduce_scatter(const void *sbuf, void *rbuf, const int *rcounts, struct ompi_datatype_t *dtype,
@@ -556,20 +850,23 @@ static int mx_coll_reduce_scatter_block_init(const void *sbuf, void *rbuf, int r
 static int scan_like(mx_coll_module_t *m, const void *sbuf, void *rbuf, int count, struct ompi_datatype_t *dtype,
                      struct ompi_op_t *op, int exclusive, int persistent, struct ompi_request_t **request, int *ret)
 {
+    const int n = mx_ompi_host->comm_size(m->comm);
     int slot, opi, rc;
     mx_request_t *q = NULL;
-    if (!reducible(m, dtype, op, count, &slot, &opi) || !(sbuf == MPI_IN_PLACE || on_device(sbuf)) ||
-        !on_device(rbuf))
-        return 1;
-    const void *sb = sbuf == MPI_IN_PLACE ? MX_IN_PLACE : sbuf;
+    if (!reducible(dtype, op, (size_t)count, n, &slot, &opi) || !comm_ready(m)) return 1;
+    const size_t bytes = (size_t)count * mx_ompi_host->dtype_size(dtype);
+    mx_coll_req_t *r = req_setup(m, sbuf, (size_t)count, dtype, rbuf, (size_t)count, dtype,
+                                 sbuf == MPI_IN_PLACE || exclusive, bytes, persistent, ret);
+    if (!r) return 0;
     const int alg = nbc_alg(exclusive ? "iexscan" : "iscan");
     if (exclusive)
-        rc = persistent ? mx_exscan_init(m->mx, sb, rbuf, (size_t)count, slot, opi, alg, NULL, &q)
-                        : mx_iexscan(m->mx, sb, rbuf, (size_t)count, slot, opi, alg, NULL, &q);
+        rc = persistent ? mx_exscan_init(m->mx, SB(r), r->r.dev, (size_t)count, slot, opi, alg, m->stream, &q)
+                        : mx_iexscan(m->mx, SB(r), r->r.dev, (size_t)count, slot, opi, alg, m->stream, &q);
     else
-        rc = persistent ? mx_scan_init(m->mx, sb, rbuf, (size_t)count, slot, opi, alg, NULL, &q)
-                        : mx_iscan(m->mx, sb, rbuf, (size_t)count, slot, opi, alg, NULL, &q);
-    return post(rc, q, persistent, request, ret);
+        rc = persistent ? mx_scan_init(m->mx, SB(r), r->r.dev, (size_t)count, slot, opi, alg, m->stream, &q)
+                        : mx_iscan(m->mx, SB(r), r->r.dev, (size_t)count, slot, opi, alg, m->stream, &q);
+    *ret = post(r, rc, q, persistent, request);
+    return 0;
 }
 
 static int mx_coll_iscan(const void *sbuf, void *rbuf, int count, struct ompi_datatype_t *dtype, struct ompi_op_t *op,
@@ -619,15 +916,18 @@ static int allgather_like(mx_coll_module_t *m, const void *sbuf, int scount, str
     const size_t rbytes = (size_t)rcount * mx_ompi_host->dtype_size(rdtype);
     const int n = mx_ompi_host->comm_size(comm);
     mx_request_t *q = NULL;
-    if (!m->mx || !rbytes || !on_device(rbuf) || !mx_ompi_host->dtype_contiguous(rdtype, rcount * n) ||
-        !(sbuf == MPI_IN_PLACE ||
-          (on_device(sbuf) && mx_ompi_host->dtype_contiguous(sdtype, scount) &&
-           (size_t)scount * mx_ompi_host->dtype_size(sdtype) == rbytes)))
-        return 1;
-    const void *sb = sbuf == MPI_IN_PLACE ? MX_IN_PLACE : sbuf;
-    const int rc = persistent ? mx_allgather_init(m->mx, sb, rbuf, rbytes, NULL, &q)
-                              : mx_iallgather(m->mx, sb, rbuf, rbytes, NULL, &q);
-    return post(rc, q, persistent, request, ret);
+    if (!rbytes || n > MX_MAX_RANKS || !comm_ready(m)) return 1;
+    if (sbuf != MPI_IN_PLACE && (size_t)scount * mx_ompi_host->dtype_size(sdtype) != rbytes) {
+        *ret = OMPI_ERROR;   /* type signatures differ: erroneous program */
+        return 0;
+    }
+    mx_coll_req_t *r = req_setup(m, sbuf, (size_t)scount, sdtype, rbuf, (size_t)rcount * n, rdtype,
+                                 sbuf == MPI_IN_PLACE, rbytes * n, persistent, ret);
+    if (!r) return 0;
+    const int rc = persistent ? mx_allgather_init(m->mx, SB(r), r->r.dev, rbytes, m->stream, &q)
+                              : mx_iallgather(m->mx, SB(r), r->r.dev, rbytes, m->stream, &q);
+    *ret = post(r, rc, q, persistent, request);
+    return 0;
 }
 
 static int mx_coll_iallgather(const void *sbuf, int scount, struct ompi_datatype_t *sdtype, void *rbuf, int rcount,
@@ -656,11 +956,16 @@ static int bcast_like(mx_coll_module_t *m, void *buf, int count, struct ompi_dat
                       int persistent, struct ompi_request_t **request, int *ret)
 {
     const size_t bytes = (size_t)count * mx_ompi_host->dtype_size(dtype);
+    const int n = mx_ompi_host->comm_size(m->comm), rank = mx_ompi_host->comm_rank(m->comm);
     mx_request_t *q = NULL;
-    if (!m->mx || !bytes || !on_device(buf) || !mx_ompi_host->dtype_contiguous(dtype, count)) return 1;
-    const int rc = persistent ? mx_bcast_init(m->mx, buf, bytes, root, NULL, &q)
-                              : mx_ibcast(m->mx, buf, bytes, root, NULL, &q);
-    return post(rc, q, persistent, request, ret);
+    if (!bytes || n > MX_MAX_RANKS || !comm_ready(m)) return 1;
+    mx_coll_req_t *r = req_setup(m, NULL, 0, NULL, buf, (size_t)count, dtype, rank == root,
+                                 rank == root ? 0 : bytes, persistent, ret);
+    if (!r) return 0;
+    const int rc = persistent ? mx_bcast_init(m->mx, r->r.dev, bytes, root, m->stream, &q)
+                              : mx_ibcast(m->mx, r->r.dev, bytes, root, m->stream, &q);
+    *ret = post(r, rc, q, persistent, request);
+    return 0;
 }
 
 static int mx_coll_ibcast(void *buf, int count, struct ompi_datatype_t *dtype, int root,
@@ -697,7 +1002,7 @@ static int mx_coll_bcast_init(void *buf, int count, struct ompi_datatype_t *dtyp
 static int mx_coll_module_enable(mca_coll_base_module_t *module, struct ompi_communicator_t *comm)
 {
     mx_coll_module_t *m = (mx_coll_module_t *)module;
-    const int n = mx_ompi_host->comm_size(comm), rank = mx_ompi_host->comm_rank(comm);
+    const int n = mx_ompi_host->comm_size(comm);
     m->comm = comm;
     if (m->super.coll_allreduce) {
         SAVE_PREV(m, comm, allreduce, mca_coll_base_module_allreduce_fn_t);
@@ -723,13 +1028,11 @@ static int mx_coll_module_enable(mca_coll_base_module_t *module, struct ompi_com
     }
     MX_NB_SLOTS(SAVE_PREV_OPT)
 #undef SAVE_PREV_OPT
-    if (m->super.coll_allreduce && n > 1 && n <= MX_MAX_RANKS) {
-        const size_t staging = (size_t)mx_ompi_host->mca_int("coll_mi355x_staging_mb", 1024) << 20;
-        int flags = MX_COMM_IPC;
-        if (mx_ompi_host->mca_int("coll_mi355x_rccl", 0)) flags |= MX_COMM_RCCL;
-        int rc = mx_comm_create(rank, n, -1, staging, flags, bootstrap_allgather, m, &m->mx);
-        if (rc != MX_SUCCESS) m->mx = NULL;   /* every call delegates */
-    }
+    /* the device communicator (IPC staging, flags) is created at the first
+     * eligible collective, so a communicator that never runs one on the
+     * device -- an MPI_Comm_dup kept for a library, say -- costs no device
+     * memory; communicators above the all-peer path's rank limit delegate */
+    m->mx_state = (n > 1 && n <= MX_MAX_RANKS) ? 0 : -1;
     return OMPI_SUCCESS;
 }
 
@@ -747,10 +1050,8 @@ static mca_coll_base_module_t *mx_coll_component_comm_query(struct ompi_communic
     const int n = mx_ompi_host->comm_size(comm);
     *priority = mx_ompi_host->mca_int("coll_mi355x_priority", 80);
     if (*priority < 0) return NULL;
-    m = calloc(1, sizeof *m);
+    m = MX_MODULE_NEW(mx_coll_module_t, super);
     if (!m) return NULL;
-    m->super.super.obj_class = &mx_coll_module_class;
-    m->super.super.obj_reference_count = 1;
     m->super.coll_module_enable = mx_coll_module_enable;
     if (n > 1) {
         m->super.coll_allreduce = mx_coll_allreduce;
@@ -771,11 +1072,16 @@ static mca_coll_base_module_t *mx_coll_component_comm_query(struct ompi_communic
     }
     if (*priority > 75) m->super.coll_reduce_local = mx_coll_reduce_local;
     if (n == 1 && !m->super.coll_reduce_local) {
-        free(m);
+        MX_OBJ_RELEASE(m);
         return NULL;
     }
     return &m->super;
 }
+
+#ifdef MX_OMPI_REAL
+int mx_ompi_host_real_register(void);
+static int mx_coll_component_open(void) { return mx_ompi_host_real_register(); }
+#endif
 
 mca_coll_base_component_2_0_0_t mca_coll_mi355x_component = {
     .collm_version = {
@@ -783,6 +1089,9 @@ mca_coll_base_component_2_0_0_t mca_coll_mi355x_component = {
         .mca_project_name = "ompi",
         .mca_type_name = "coll", .mca_type_major_version = 2,
         .mca_component_name = "mi355x", .mca_component_major_version = 1,
+#ifdef MX_OMPI_REAL
+        .mca_open_component = mx_coll_component_open,
+#endif
     },
     .collm_init_query = mx_coll_component_init_query,
     .collm_comm_query = mx_coll_component_comm_query,

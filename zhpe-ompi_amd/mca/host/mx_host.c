@@ -9,6 +9,7 @@
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
+#include <time.h>
 
 #include "../mx_ompi_abi.h"
 #include "mx_host.h"
@@ -18,11 +19,15 @@ static void obj_retain(opal_object_t *o)
 {
     if (o) __atomic_add_fetch(&o->obj_reference_count, 1, __ATOMIC_RELAXED);
 }
+/* OBJ_RELEASE: at zero the class destructor runs and the object is freed
+ * (objects of classes without a destructor are the harness's static ones) */
 static void obj_release(opal_object_t *o)
 {
     if (o && __atomic_sub_fetch(&o->obj_reference_count, 1, __ATOMIC_ACQ_REL) == 0 && o->obj_class &&
-        o->obj_class->cls_destruct)
+        o->obj_class->cls_destruct) {
         o->obj_class->cls_destruct(o);
+        free(o);
+    }
 }
 
 /* ---- datatypes (ompi/datatype/ompi_datatype_internal.h:37-200) ----------- */
@@ -32,11 +37,14 @@ struct ompi_datatype_t {
     int slot;        /* ompi_op_ddt_map[id] (op.c:131-229) */
     size_t size;
     int predefined;
-    struct ompi_datatype_t *base;   /* derived contiguous: base type */
+    struct ompi_datatype_t *base;   /* derived: base type */
     int base_count;
+    /* MPI_Type_vector of the base type (vcount blocks of vblen, stride
+     * vstride elements); vcount == 0: contiguous */
+    int vcount, vblen, vstride;
 };
 
-#define DT(nm, id, slot, sz) {nm, id, slot, sz, 1, NULL, 0}
+#define DT(nm, id, slot, sz) {nm, id, slot, sz, 1, NULL, 0, 0, 0, 0}
 static struct ompi_datatype_t g_dtypes[] = {
     DT("MPI_INT8_T", 0x01, 0, 1), DT("MPI_UINT8_T", 0x02, 1, 1), DT("MPI_INT16_T", 0x03, 2, 2),
     DT("MPI_UINT16_T", 0x04, 3, 2), DT("MPI_INT32_T", 0x05, 4, 4), DT("MPI_UINT32_T", 0x06, 5, 4),
@@ -71,7 +79,7 @@ void *mxh_dtype(const char *name)
 void *mxh_dtype_contiguous(int count, void *oldtype)
 {
     struct ompi_datatype_t *o = oldtype, *d = calloc(1, sizeof *d);
-    if (!d || !o || count < 0) { free(d); return NULL; }
+    if (!d || !o || count < 0 || o->vcount) { free(d); return NULL; }   /* contiguous of predefined / contiguous */
     d->name = "";
     d->id = -1;
     d->predefined = 0;
@@ -81,6 +89,32 @@ void *mxh_dtype_contiguous(int count, void *oldtype)
     /* ompi_datatype_get_single_predefined_type_from_args (ompi_datatype_args.c:825-865) */
     d->slot = d->base ? d->base->slot : -1;
     return d;
+}
+
+/* MPI_Type_vector(count, blocklen, stride, oldtype) over a predefined type:
+ * the non-contiguous layouts of the allgather / bcast tests */
+void *mxh_dtype_vector(int count, int blocklen, int stride, void *oldtype)
+{
+    struct ompi_datatype_t *o = oldtype, *d;
+    if (!o || !o->predefined || count < 1 || blocklen < 1 || stride < blocklen) return NULL;
+    d = calloc(1, sizeof *d);
+    if (!d) return NULL;
+    d->name = "";
+    d->id = -1;
+    d->base = o;
+    d->base_count = count * blocklen;
+    d->size = o->size * (size_t)count * (size_t)blocklen;
+    d->slot = -1;                 /* no reductions on derived types (ompi_op_is_valid) */
+    d->vcount = count;
+    d->vblen = blocklen;
+    d->vstride = stride;
+    return d;
+}
+
+static size_t dtype_extent(const struct ompi_datatype_t *d)
+{
+    if (!d->vcount) return d->size;
+    return ((size_t)(d->vcount - 1) * (size_t)d->vstride + (size_t)d->vblen) * d->base->size;
 }
 
 /* ---- ops ------------------------------------------------------------------ */
@@ -202,7 +236,42 @@ static void *comm_coll_fn(struct ompi_communicator_t *c, const char *slot, mca_c
 
 static int dtype_slot(struct ompi_datatype_t *d) { return d ? d->slot : -1; }
 static size_t dtype_size(struct ompi_datatype_t *d) { return d->size; }
-static int dtype_contiguous(struct ompi_datatype_t *d, int count) { (void)d; (void)count; return 1; }
+static int dtype_contiguous(struct ompi_datatype_t *d, int count)
+{
+    (void)count;
+    return !d->vcount || d->vblen == d->vstride || (d->vcount == 1);
+}
+/* opal_convertor_pack / _unpack over host memory (opal_convertor.c:218-325) */
+static void vec_copy(struct ompi_datatype_t *d, int count, char *user, char *packed, int pack)
+{
+    const size_t bs = d->base->size, blk = (size_t)d->vblen * bs, ext = dtype_extent(d);
+    for (int i = 0; i < count; i++)
+        for (int b = 0; b < d->vcount; b++) {
+            char *u = user + (size_t)i * ext + (size_t)b * (size_t)d->vstride * bs;
+            if (pack) memcpy(packed, u, blk);
+            else memcpy(u, packed, blk);
+            packed += blk;
+        }
+}
+static int dtype_pack(struct ompi_datatype_t *d, int count, const void *user, void *packed)
+{
+    if (!d->vcount) memcpy(packed, user, (size_t)count * d->size);
+    else vec_copy(d, count, (char *)user, packed, 1);
+    return OMPI_SUCCESS;
+}
+static int dtype_unpack(struct ompi_datatype_t *d, int count, const void *packed, void *user)
+{
+    if (!d->vcount) memcpy(user, packed, (size_t)count * d->size);
+    else vec_copy(d, count, user, (char *)packed, 0);
+    return OMPI_SUCCESS;
+}
+/* opal_datatype_span (opal_datatype.h:329-340), true lb = 0 here */
+static int dtype_span(struct ompi_datatype_t *d, int count, ptrdiff_t *lo, ptrdiff_t *hi)
+{
+    *lo = 0;
+    *hi = count > 0 ? (ptrdiff_t)((size_t)count * dtype_extent(d)) : 0;
+    return OMPI_SUCCESS;
+}
 static int comm_rank(struct ompi_communicator_t *c) { return c->rank; }
 static int comm_size(struct ompi_communicator_t *c) { return c->size; }
 static int op_index(struct ompi_op_t *op) { return op->o_f_to_c_index; }
@@ -262,19 +331,23 @@ static void op_reduce(struct ompi_op_t *op, const void *source, void *target, in
 }
 
 /* ---- host base coll module (stands in for tuned/basic on host buffers) ---- */
+static int dtype_pack(struct ompi_datatype_t *d, int count, const void *user, void *packed);
+static int dtype_unpack(struct ompi_datatype_t *d, int count, const void *packed, void *user);
+
 static int base_allgather(const void *sbuf, int scount, struct ompi_datatype_t *sdt, void *rbuf, int rcount,
                           struct ompi_datatype_t *rdt, struct ompi_communicator_t *c, mca_coll_base_module_t *m)
 {
     (void)m;
-    size_t rb = (size_t)rcount * rdt->size;
-    const void *src = sbuf == MPI_IN_PLACE ? (char *)rbuf + (size_t)c->rank * rb : sbuf;
-    void *tmp = malloc(rb * c->size + 1);
+    const size_t rb = (size_t)rcount * rdt->size, rext = (size_t)rcount * dtype_extent(rdt);
+    char *tmp = malloc(rb * c->size + 1), *mine = malloc(rb + 1);
     int rc;
-    (void)scount; (void)sdt;
-    if (!tmp) return OMPI_ERR_OUT_OF_RESOURCE;
-    rc = c->ag(src, tmp, rb, c->ag_ctx);
-    memcpy(rbuf, tmp, rb * c->size);
+    if (!tmp || !mine) { free(tmp); free(mine); return OMPI_ERR_OUT_OF_RESOURCE; }
+    if (sbuf == MPI_IN_PLACE) dtype_pack(rdt, rcount, (char *)rbuf + (size_t)c->rank * rext, mine);
+    else dtype_pack(sdt, scount, sbuf, mine);
+    rc = c->ag(mine, tmp, rb, c->ag_ctx);
+    for (int p = 0; p < c->size && !rc; p++) dtype_unpack(rdt, rcount, tmp + (size_t)p * rb, (char *)rbuf + p * rext);
     free(tmp);
+    free(mine);
     return rc ? OMPI_ERROR : OMPI_SUCCESS;
 }
 
@@ -311,12 +384,14 @@ static int base_bcast(void *buf, int count, struct ompi_datatype_t *dt, int root
                       mca_coll_base_module_t *m)
 {
     size_t b = (size_t)count * dt->size;
-    char *all = malloc(b * c->size + 1);
+    char *all = malloc(b * c->size + 1), *mine = malloc(b + 1);
     (void)m;
-    if (!all) return OMPI_ERR_OUT_OF_RESOURCE;
-    if (c->ag(buf, all, b, c->ag_ctx)) { free(all); return OMPI_ERROR; }
-    memcpy(buf, all + (size_t)root * b, b);
+    if (!all || !mine) { free(all); free(mine); return OMPI_ERR_OUT_OF_RESOURCE; }
+    dtype_pack(dt, count, buf, mine);
+    if (c->ag(mine, all, b, c->ag_ctx)) { free(all); free(mine); return OMPI_ERROR; }
+    dtype_unpack(dt, count, all + (size_t)root * b, buf);
     free(all);
+    free(mine);
     return OMPI_SUCCESS;
 }
 
@@ -704,6 +779,9 @@ int mxh_init(const char *component_lib, mxh_reducer_t base, mxh_pattern_t patter
     g_host.request_activate = request_activate;
     g_host.request_complete = request_complete;
     g_host.progress_register = progress_register;
+    g_host.dtype_pack = dtype_pack;
+    g_host.dtype_unpack = dtype_unpack;
+    g_host.dtype_span = dtype_span;
     g_nprogress = 0;
     g_op_comp = NULL;
     g_coll_comp = NULL;
@@ -778,6 +856,22 @@ int mxh_op_reduce(void *opv, const void *source, void *target, int count, void *
     if (!d || d->slot < 0 || !op->intrinsic.fns[d->slot]) return -1;
     op_reduce(op, source, target, count, d);
     return 0;
+}
+
+/* Cost of one ompi_op_reduce through the op table (the segmented ring's
+ * per-segment call, coll_base_allreduce.c:782): average ns over `iters`
+ * back-to-back calls, after one warm-up call. */
+double mxh_time_op_reduce(void *opv, const void *source, void *target, int count, void *dt, int iters)
+{
+    struct ompi_op_t *op = opv;
+    struct ompi_datatype_t *d = dt;
+    struct timespec t0, t1;
+    if (!d || d->slot < 0 || !op->intrinsic.fns[d->slot] || iters < 1) return -1.0;
+    op_reduce(op, source, target, count, d);
+    clock_gettime(CLOCK_MONOTONIC, &t0);
+    for (int i = 0; i < iters; i++) op_reduce(op, source, target, count, d);
+    clock_gettime(CLOCK_MONOTONIC, &t1);
+    return ((double)(t1.tv_sec - t0.tv_sec) * 1e9 + (double)(t1.tv_nsec - t0.tv_nsec)) / iters;
 }
 
 int mxh_reduce_local(const void *in, void *inout, int count, void *dt, void *opv)

@@ -40,6 +40,7 @@ int mxh_set_mca(const char *name, int value);
 
 void *mxh_dtype(const char *mpi_name);   /* MPI_FLOAT, MPI_2INT, ...; NULL if unknown */
 void *mxh_dtype_contiguous(int count, void *oldtype);  /* MPI_Type_contiguous */
+void *mxh_dtype_vector(int count, int blocklen, int stride, void *oldtype);  /* MPI_Type_vector */
 void *mxh_op(const char *mpi_name);      /* MPI_SUM, MPI_MAXLOC, ... */
 /* which module owns slot t of op: 0 base, 1 mi355x */
 int mxh_op_slot_owner(void *op, int type, int three_buffer);
@@ -51,6 +52,8 @@ int mxh_comm_free(void *comm);
 const char *mxh_comm_slot_owner(void *comm, const char *slot);
 
 int mxh_op_reduce(void *op, const void *source, void *target, int count, void *dtype);
+/* average ns of one ompi_op_reduce through the op table over `iters` calls */
+double mxh_time_op_reduce(void *op, const void *source, void *target, int count, void *dtype, int iters);
 int mxh_reduce_local(const void *in, void *inout, int count, void *dtype, void *op);
 int mxh_allreduce(const void *sbuf, void *rbuf, int count, void *dtype, void *op, void *comm);
 int mxh_reduce_scatter(const void *sbuf, void *rbuf, const int *rcounts, void *dtype, void *op, void *comm);

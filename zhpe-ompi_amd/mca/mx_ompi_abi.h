@@ -17,12 +17,18 @@
  *   request services                   ompi/request/request.h:125-139, 436-
  *
  * Building against a real Open MPI tree: compile the components with
- * -DMX_OMPI_REAL and the Open MPI include paths; this header then includes
- * the real framework headers and maps the MX_* accessors below onto
- * ompi_comm_rank(), ompi_op_ddt_map[], OBJ_RETAIN() ....
- * Without it (the default here) the accessors are provided by the host that
- * loads the component -- the mini-host harness in mca/host/ -- through the
- * mx_ompi_host_t table, whose entries mirror those Open MPI internals.
+ * -DMX_OMPI_REAL and the Open MPI include paths.  This header then includes
+ * the real framework headers (ompi/mca/op/op.h, ompi/mca/coll/coll.h,
+ * ompi/request/request.h) instead of the mirrors below, and module objects
+ * are real OPAL classes (OBJ_CLASS_INSTANCE / OBJ_NEW).  The host services
+ * stay behind the mx_ompi_host_t table, filled from the real internals by
+ * mca/mx_ompi_host_real.c.  -DMX_OMPI_REAL_NO_COLL leaves
+ * out the coll headers (the op component needs only op.h).
+ * Without MX_OMPI_REAL (the default here) the mirrors are used and the
+ * table is filled by the host that loads the component -- the mini-host
+ * harness in mca/host/.  tests/test_abi_layout.py checks every mirrored
+ * offset against the reference's own headers and compiles op_mi355x.c in
+ * the real mode against them.
  */
 #ifndef MX_OMPI_ABI_H
 #define MX_OMPI_ABI_H
@@ -34,6 +40,33 @@
 #ifdef __cplusplus
 extern "C" {
 #endif
+
+#ifdef MX_OMPI_REAL
+/* ---- real Open MPI headers -------------------------------------------- */
+#include "ompi_config.h"
+#include "ompi/constants.h"
+#include "opal/class/opal_object.h"
+#include "ompi/mca/op/op.h"
+#ifndef MX_OMPI_REAL_NO_COLL
+#include "mpi.h"
+#include "ompi/mca/coll/coll.h"
+#include "ompi/request/request.h"
+#endif
+#ifndef OMPI_OP_FLAGS_INTRINSIC          /* ompi/op/op.h:99-117 */
+#define OMPI_OP_FLAGS_INTRINSIC 0x0001
+#define OMPI_OP_FLAGS_COMMUTE 0x0040
+#endif
+struct mca_coll_base_module_2_3_0_t;
+/* module classes: real OPAL classes derived from the framework's module
+ * class; the destructor runs before OBJ_RELEASE frees the object */
+#define MX_MODULE_CLASS(T, PARENT, DTOR) OBJ_CLASS_INSTANCE(T, PARENT, NULL, DTOR)
+#define MX_MODULE_NEW(T, SUPER_FIELD)                                                          \
+    ({                                                                                          \
+        T *o_ = OBJ_NEW(T);                                                                     \
+        if (o_) memset((char *)o_ + sizeof(o_->SUPER_FIELD), 0, sizeof(T) - sizeof(o_->SUPER_FIELD)); \
+        o_;                                                                                     \
+    })
+#else /* !MX_OMPI_REAL */
 
 #define OMPI_SUCCESS 0
 #define OMPI_ERROR -1
@@ -271,6 +304,22 @@ typedef struct mca_coll_base_component_2_0_0_t {
     mca_coll_base_component_comm_query_2_0_0_fn_t collm_comm_query;
 } mca_coll_base_component_2_0_0_t;
 
+/* module classes (mirror): the destructor runs, then the host frees the
+ * object -- the OPAL OBJ_RELEASE semantics */
+#define MX_MODULE_CLASS(T, PARENT, DTOR) static mx_obj_class_t T##_class = {#T, (void (*)(void *))(DTOR)}
+#define MX_MODULE_NEW(T, SUPER_FIELD) ((T *)mx_obj_new(sizeof(T), &T##_class))
+#include <stdlib.h>
+static inline void *mx_obj_new(size_t bytes, mx_obj_class_t *cls)
+{
+    opal_object_t *o = (opal_object_t *)calloc(1, bytes);
+    if (o) {
+        o->obj_class = cls;
+        o->obj_reference_count = 1;
+    }
+    return o;
+}
+#endif /* MX_OMPI_REAL */
+
 /* ---- host services (Open MPI internals the components use) ---------------
  * In a real build these are ompi_comm_rank/size, ompi_op_ddt_map[dt->id] +
  * ompi_datatype_get_single_predefined_type_from_args, ompi_datatype_type_size,
@@ -292,7 +341,8 @@ typedef struct mx_ompi_host {
     ompi_op_base_op_3buff_fns_t *(*op_3buff_fns)(struct ompi_op_t *op);  /* &op->o_3buff_intrinsic */
     /* the communicator's current function table entry for a slot name
      * ("allreduce", "allgather", ...) and its module (comm->c_coll) */
-    void *(*comm_coll_fn)(struct ompi_communicator_t *comm, const char *slot, mca_coll_base_module_t **module);
+    void *(*comm_coll_fn)(struct ompi_communicator_t *comm, const char *slot,
+                          struct mca_coll_base_module_2_3_0_t **module);
     void (*obj_retain)(opal_object_t *obj);
     void (*obj_release)(opal_object_t *obj);
     /* integer MCA variable lookup (mca_base_var); returns def if unset */
@@ -318,6 +368,19 @@ typedef struct mx_ompi_host {
     void (*request_activate)(struct ompi_request_t *req);
     void (*request_complete)(struct ompi_request_t *req, int status);
     int (*progress_register)(int (*fn)(void));
+    /* ---- non-contiguous layouts (allgather / bcast may use any datatype;
+     * the reductions only predefined ones, ompi_op_is_valid, op.h:477-514).
+     * The layout of a datatype may differ between ranks as long as the type
+     * signatures match, so the device-or-delegate choice cannot depend on
+     * it: a non-contiguous buffer is packed into a contiguous one and back.
+     * In a real build: opal_convertor_pack / _unpack over host memory
+     * (opal_convertor.c:218-325) and opal_datatype_span (opal_datatype.h:
+     * 329-340).  Host memory only; the component copies a device span to
+     * the host first. */
+    int (*dtype_pack)(struct ompi_datatype_t *dt, int count, const void *user, void *packed);
+    int (*dtype_unpack)(struct ompi_datatype_t *dt, int count, const void *packed, void *user);
+    /* bytes [*lo, *hi) relative to the buffer that count elements touch */
+    int (*dtype_span)(struct ompi_datatype_t *dt, int count, ptrdiff_t *lo, ptrdiff_t *hi);
 } mx_ompi_host_t;
 
 /* Set by the host before component queries. */
@@ -329,7 +392,9 @@ extern const mx_ompi_host_t *mx_ompi_host;
 /* Component symbols, looked up by name like mca_base_component_repository
  * does (mca_<type>_<name>_component, mca_base_component_repository.c:449-462). */
 extern ompi_op_base_component_1_0_0_t mca_op_mi355x_component;
+#if !defined(MX_OMPI_REAL) || !defined(MX_OMPI_REAL_NO_COLL)
 extern mca_coll_base_component_2_0_0_t mca_coll_mi355x_component;
+#endif
 /* Host registration entry of the component library. */
 int mx_ompi_set_host(const mx_ompi_host_t *host);
 

@@ -22,7 +22,7 @@
  *
  * Synchronous ABI: the handler returns void and the caller immediately uses
  * `inout` (coll_base_allreduce.c:471-477), so each call completes its kernel
- * before returning (stream sync).  Errors cannot be returned
+ * before returning (sync of the calling thread's stream).  Errors cannot be returned
  * (ompi/mca/op/op.h:258-273): a device failure aborts, like the CUDA path
  * does on copy failure (opal_datatype_cuda.c:121-140).
  */
@@ -37,6 +37,9 @@
 #define MX_OMPI_WITH_FORTRAN 1   /* table variant of the host Open MPI build */
 #endif
 
+#ifndef MX_OMPI_REAL
+/* one library holds both components here; in an Open MPI tree each
+ * component DSO gets its own copy from mx_ompi_host_real.c */
 const mx_ompi_host_t *mx_ompi_host;
 
 int mx_ompi_set_host(const mx_ompi_host_t *host)
@@ -44,6 +47,10 @@ int mx_ompi_set_host(const mx_ompi_host_t *host)
     mx_ompi_host = host;
     return OMPI_SUCCESS;
 }
+#else
+int mx_ompi_host_real_register(void);
+static int mx_op_component_open(void) { return mx_ompi_host_real_register(); }
+#endif
 
 typedef struct {
     ompi_op_base_module_t super;
@@ -54,21 +61,47 @@ typedef struct {
     ompi_op_base_module_t *fallback3_module[OMPI_OP_BASE_TYPE_MAX];
 } mx_op_module_t;
 
-static void op_module_destruct(void *obj)
+/* releases the cached fallbacks; the object itself is freed by OBJ_RELEASE */
+static void op_module_destruct(mx_op_module_t *m)
 {
-    mx_op_module_t *m = (mx_op_module_t *)obj;
     for (int i = 0; i < OMPI_OP_BASE_TYPE_MAX; i++) {
         if (m->fallback_module[i]) MX_OBJ_RELEASE(m->fallback_module[i]);
         if (m->fallback3_module[i]) MX_OBJ_RELEASE(m->fallback3_module[i]);
     }
-    free(m);
 }
 
-static mx_obj_class_t mx_op_module_class = {"mx_op_module_t", op_module_destruct};
+MX_MODULE_CLASS(mx_op_module_t, ompi_op_base_module_t, op_module_destruct);
 
 static int both_on_device(const void *a, const void *b)
 {
-    return mx_is_device_ptr(a) == 1 && mx_is_device_ptr(b) == 1;
+    return mx_is_device_ptr(a) == 1 && mx_is_device_ptr(b) == 1;   /* range-cached: no runtime call */
+}
+
+/* The kernels run on a stream of the calling thread (non-blocking, so a
+ * handler call never waits for unrelated work of other streams the way a
+ * legacy-default-stream synchronise does; one per thread, so concurrent
+ * callers under MPI_THREAD_MULTIPLE do not share one), ordered after what
+ * the legacy default stream holds -- the kernels that produced the operands.
+ * op_mi355x_stream = 0 selects the legacy default stream instead. */
+static _Thread_local void *t_stream;
+static _Thread_local int t_stream_tried;
+static int g_use_stream = -1;   /* op_mi355x_stream, read once */
+
+static void *op_stream(void)
+{
+    if (g_use_stream < 0) g_use_stream = mx_ompi_host->mca_int("op_mi355x_stream", 1) != 0;
+    if (!g_use_stream) return NULL;
+    if (!t_stream_tried) {
+        t_stream_tried = 1;
+        if (mx_stream_create(&t_stream) != MX_SUCCESS) t_stream = NULL;
+    }
+    return t_stream;
+}
+
+static int run_sync(void *s, int rc)
+{
+    if (rc == MX_SUCCESS) rc = mx_stream_sync(s);
+    return rc;
 }
 
 static void die(const char *what, int rc)
@@ -85,8 +118,10 @@ static void mx_op_2buff(void *in, void *inout, int *count, struct ompi_datatype_
     const int slot = mx_ompi_host->dtype_slot(*dtype);
     if (slot < 0) die("datatype lookup", MX_ERR_ARG);
     if (*count > 0 && both_on_device(in, inout)) {
-        int rc = mx_reduce2(m->op_index, slot, in, inout, (size_t)*count, NULL);
-        if (rc == MX_SUCCESS) rc = mx_stream_sync(NULL);
+        void *s = op_stream();
+        int rc = s ? mx_stream_order(s, NULL) : MX_SUCCESS;
+        if (rc == MX_SUCCESS) rc = mx_reduce2(m->op_index, slot, in, inout, (size_t)*count, s);
+        rc = run_sync(s, rc);
         if (rc != MX_SUCCESS) die("mx_reduce2", rc);
         return;
     }
@@ -101,8 +136,10 @@ static void mx_op_3buff(void *in1, void *in2, void *out, int *count, struct ompi
     const int slot = mx_ompi_host->dtype_slot(*dtype);
     if (slot < 0) die("datatype lookup", MX_ERR_ARG);
     if (*count > 0 && both_on_device(in1, in2) && mx_is_device_ptr(out) == 1) {
-        int rc = mx_reduce3(m->op_index, slot, in1, in2, out, (size_t)*count, NULL);
-        if (rc == MX_SUCCESS) rc = mx_stream_sync(NULL);
+        void *s = op_stream();
+        int rc = s ? mx_stream_order(s, NULL) : MX_SUCCESS;
+        if (rc == MX_SUCCESS) rc = mx_reduce3(m->op_index, slot, in1, in2, out, (size_t)*count, s);
+        rc = run_sync(s, rc);
         if (rc != MX_SUCCESS) die("mx_reduce3", rc);
         return;
     }
@@ -112,7 +149,7 @@ static void mx_op_3buff(void *in1, void *in2, void *out, int *count, struct ompi
 static int mx_op_component_init_query(bool enable_progress_threads, bool enable_mpi_threads)
 {
     (void)enable_progress_threads;
-    (void)enable_mpi_threads;  /* kernels run on the null stream; safe under THREAD_MULTIPLE */
+    (void)enable_mpi_threads;  /* one stream per calling thread: safe under THREAD_MULTIPLE */
     if (!mx_ompi_host) return OMPI_ERR_NOT_SUPPORTED;
     return mx_init(-1) == MX_SUCCESS ? OMPI_SUCCESS : OMPI_ERR_NOT_SUPPORTED;
 }
@@ -127,10 +164,8 @@ static ompi_op_base_module_t *mx_op_component_op_query(struct ompi_op_t *op, int
 
     if (!(mx_ompi_host->op_flags(op) & OMPI_OP_FLAGS_INTRINSIC)) return NULL;
     if (idx <= 0 || idx >= MX_OP_REPLACE) return NULL;      /* MPI_OP_NULL, REPLACE, NO_OP */
-    m = calloc(1, sizeof *m);
+    m = MX_MODULE_NEW(mx_op_module_t, super);
     if (!m) return NULL;
-    m->super.super.obj_class = &mx_op_module_class;
-    m->super.super.obj_reference_count = 1;
     m->super.opm_op = op;
     m->op_index = idx;
     for (int t = 0; t < OMPI_OP_BASE_TYPE_MAX; t++) {
@@ -154,7 +189,7 @@ static ompi_op_base_module_t *mx_op_component_op_query(struct ompi_op_t *op, int
         }
     }
     if (!any) {
-        op_module_destruct(m);
+        MX_OBJ_RELEASE(m);
         return NULL;
     }
     *priority = mx_ompi_host->mca_int("op_mi355x_priority", 50);
@@ -167,6 +202,9 @@ ompi_op_base_component_1_0_0_t mca_op_mi355x_component = {
         .mca_project_name = "ompi",
         .mca_type_name = "op", .mca_type_major_version = 1,
         .mca_component_name = "mi355x", .mca_component_major_version = 1,
+#ifdef MX_OMPI_REAL
+        .mca_open_component = mx_op_component_open,
+#endif
     },
     .opc_init_query = mx_op_component_init_query,
     .opc_op_query = mx_op_component_op_query,

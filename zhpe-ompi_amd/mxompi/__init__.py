@@ -171,7 +171,7 @@ def sync(stream: int = 0) -> None:
 # ---------------------------------------------------------------------------
 IN_PLACE = 1                       # MX_IN_PLACE
 ANY_SOURCE = -1                    # MX_ANY_SOURCE (MPI_ANY_SOURCE)
-COMM_IPC, COMM_RCCL = 1, 2
+COMM_IPC, COMM_RCCL, COMM_P2P = 1, 2, 4
 ALLREDUCE = {"auto": 0, "basic_linear": 1, "nonoverlapping": 2, "recursive_doubling": 3,
              "ring": 4, "segmented_ring": 5, "rabenseifner": 6, "rccl": 100}
 REDUCE_SCATTER = {"auto": 0, "nonoverlapping": 1, "recursive_halving": 2, "ring": 3, "rccl": 100}
@@ -341,7 +341,7 @@ class Comm:
     list[bytes]` is the host bootstrap exchange (e.g. torch.distributed)."""
 
     def __init__(self, rank=0, size=1, allgather=None, device=0, staging_bytes=64 << 20,
-                 flags=COMM_IPC, heap_bytes=0, _handle=None):
+                 flags=COMM_IPC | COMM_P2P, heap_bytes=0, _handle=None):
         L = _coll_lib()
         self.size = size
         self.rank = rank
