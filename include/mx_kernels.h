@@ -165,6 +165,9 @@ int mx_free(void *p);
 int mx_memcpy(void *dst, const void *src, size_t bytes, void *stream);
 /* A non-blocking stream (does not synchronise with the legacy default one). */
 int mx_stream_create(void **stream);
+/* A blocking stream: ordered with the legacy default stream implicitly (no
+ * per-call event; same host cost as the default stream). */
+int mx_stream_create_ordered(void **stream);
 int mx_stream_destroy(void *stream);
 /* `stream` waits on the device for the work queued on `after` so far
  * (NULL = the legacy default stream). */

@@ -429,16 +429,32 @@ __global__ void __launch_bounds__(kCB) k_convert_tile(ConvArgs a, int nruns_lds,
 
 // PACK, pipelined: persistent workgroups walk tiles t, t + grid, ...; while
 // the lanes copy tile t's pieces out of LDS, the next tile's user span is
-// already in flight into registers (<= kSpanCap / 16 / kCB uint4 per lane),
-// and lands in LDS after the tile's packed bytes have left.  The one-tile
+// already in flight into registers (SPAN / 16 / kCB uint4 per lane), and
+// lands in LDS after the tile's packed bytes have left.  The one-tile
 // kernel above idles the memory pipe during every LDS phase (SQ counters on
 // the struct type: ~730 VALU instructions per 22.6k-cycle wave, i.e. waves
 // mostly wait on the span load).
-template <int TP>
+// Geometry (TP stream bytes per tile, SPAN bytes of user span staged): each
+// lane owns TP / kCB consecutive stream bytes, so at every step of the walk
+// the 64 lanes of a wave write the packed tile at a stride of TP / kCB
+// bytes.  With 32-byte stretches (TP 8192) lane starts fall on only 8 of
+// the 64 LDS banks (8-way conflicts, SQ_LDS_BANK_CONFLICT 2.7 cycles per LDS
+// instruction on the struct type); 36-byte stretches (TP 9216, 9 dwords,
+// coprime to 64) start every lane of a wave on its own bank.  A smaller span
+// cap (16 KiB: the struct type reads 48/29 x TP) lets 6 instead of 4
+// workgroups share a CU.
+template <int TP, int SPAN>
+struct PipeGeom {
+  static constexpr int kSpanCap = SPAN;
+  static constexpr int kPre = SPAN / 16 / kCB;   // uint4 per lane for a full span
+  static constexpr size_t lds(size_t run_bytes) { return TP + 16 + SPAN + 32 + run_bytes; }
+};
+
+template <int TP, int SPAN>
 __global__ void __launch_bounds__(kCB) k_pack_tile_pipe(ConvArgs a, int nruns_lds, uint64_t ntiles) {
-  constexpr int kTP = TP, kSpanCap = TileGeom<TP>::kSpanCap;
-  constexpr int kPre = kSpanCap / 16 / kCB;   // uint4 per lane for a full span
+  constexpr int kTP = TP, kSpanCap = SPAN, kPre = PipeGeom<TP, SPAN>::kPre;
   static_assert(kSpanCap % (16 * kCB) == 0, "span staging is whole vectors per lane");
+  static_assert(kTP % (16 * 4) == 0 && kTP / kCB >= 16, "tiles are whole 16-byte vectors");
   extern __shared__ __align__(16) char smem[];
   char *pk = smem;
   char *span = smem + kTP + 16;
@@ -475,19 +491,15 @@ __global__ void __launch_bounds__(kCB) k_pack_tile_pipe(ConvArgs a, int nruns_ld
     const bool has_next = tn < ntiles;
     if (has_next && threadIdx.x == 0) bounds(tn, cur ^ 1);
     __syncthreads();                                 // span of t in LDS; bounds of tn visible
-    static_assert(kPre == 6, "prefetch registers below are spelled out for a 24 KiB span");
-    uint4 p0 = {}, p1 = {}, p2 = {}, p3 = {}, p4 = {}, p5 = {};
+    uint4 pre[kPre];
     const bool pre_ok = has_next && s_ok[cur ^ 1];
     const uint32_t nvn = pre_ok ? (uint32_t)(s_nb[cur ^ 1] / 16) : 0;
     const uint32_t tx = threadIdx.x;
     {
       const uint4 *g = reinterpret_cast<const uint4 *>(s_lo[cur ^ 1]);
-      if (tx < nvn) p0 = g[tx];
-      if (tx + kCB < nvn) p1 = g[tx + kCB];
-      if (tx + 2 * kCB < nvn) p2 = g[tx + 2 * kCB];
-      if (tx + 3 * kCB < nvn) p3 = g[tx + 3 * kCB];
-      if (tx + 4 * kCB < nvn) p4 = g[tx + 4 * kCB];
-      if (tx + 5 * kCB < nvn) p5 = g[tx + 5 * kCB];
+#pragma unroll
+      for (int k = 0; k < kPre; k++)
+        if (tx + k * kCB < nvn) pre[k] = g[tx + k * kCB];
     }
     const uint64_t r0 = t * kTP, r1 = r0 + kTP < a.len ? r0 + kTP : a.len;
     if (s_ok[cur]) {
@@ -502,12 +514,9 @@ __global__ void __launch_bounds__(kCB) k_pack_tile_pipe(ConvArgs a, int nruns_ld
     __syncthreads();                                 // span and pk of t are free
     {
       uint4 *d = reinterpret_cast<uint4 *>(span);
-      if (tx < nvn) d[tx] = p0;
-      if (tx + kCB < nvn) d[tx + kCB] = p1;
-      if (tx + 2 * kCB < nvn) d[tx + 2 * kCB] = p2;
-      if (tx + 3 * kCB < nvn) d[tx + 3 * kCB] = p3;
-      if (tx + 4 * kCB < nvn) d[tx + 4 * kCB] = p4;
-      if (tx + 5 * kCB < nvn) d[tx + 5 * kCB] = p5;
+#pragma unroll
+      for (int k = 0; k < kPre; k++)
+        if (tx + k * kCB < nvn) d[tx + k * kCB] = pre[k];
     }
     t = tn;
     cur ^= 1;
@@ -749,6 +758,15 @@ static bool conv_pipe_enabled() {
   return on != 0;
 }
 
+static int conv_pipe_geom() {
+  static const int g = [] {
+    const char *e = getenv("MX_CONV_PIPE_GEOM");
+    const int v = e ? atoi(e) : 1;
+    return (v >= 0 && v <= 3) ? v : 1;
+  }();
+  return g;
+}
+
 // Tile size of the TILE kernels (MX_CONV_TP = 2048 / 4096 / 8192 for
 // measurement; results are identical).
 static int conv_tile_bytes() {
@@ -814,10 +832,22 @@ static int convert(const mx_ddt_t *d, size_t count, char *user, char *packed, si
     const int nlds = a.nruns <= 64 ? 1 : 0;
     const size_t rb = nlds ? (size_t)a.nruns * sizeof(DRun) : 0;
     if (PACK && conv_pipe_enabled()) {
-      const uint64_t tiles = (len + 8191) / 8192;
-      const uint64_t grid = std::min<uint64_t>(tiles, (uint64_t)g_num_cus * 4);
-      hipLaunchKernelGGL((k_pack_tile_pipe<8192>), dim3((unsigned)grid), dim3(kCB), TileGeom<8192>::lds(true, rb), s,
-                         a, nlds, tiles);
+      // MX_CONV_PIPE_GEOM selects the tile geometry (A/B measurement; results
+      // are identical): 0 = 8192 x 24 KiB span (round 1), 1 = 9216 x 16 KiB,
+      // 2 = 9216 x 28 KiB, 3 = 8192 x 16 KiB
+      const int geom = conv_pipe_geom();
+#define MX_PIPE_LAUNCH(TPV, SPV, WGS)                                                                        \
+  do {                                                                                                        \
+    const uint64_t tiles = (len + TPV - 1) / TPV;                                                             \
+    const uint64_t grid = std::min<uint64_t>(tiles, (uint64_t)g_num_cus * (WGS));                             \
+    hipLaunchKernelGGL((k_pack_tile_pipe<TPV, SPV>), dim3((unsigned)grid), dim3(kCB),                          \
+                       (PipeGeom<TPV, SPV>::lds(rb)), s, a, nlds, tiles);                                        \
+  } while (0)
+      if (geom == 0) MX_PIPE_LAUNCH(8192, 24576, 4);
+      else if (geom == 2) MX_PIPE_LAUNCH(9216, 28672, 3);
+      else if (geom == 3) MX_PIPE_LAUNCH(8192, 16384, 6);
+      else MX_PIPE_LAUNCH(9216, 16384, 6);
+#undef MX_PIPE_LAUNCH
       return mx_check_launch();
     }
     const int tp = conv_tile_bytes();

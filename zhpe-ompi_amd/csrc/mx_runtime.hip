@@ -187,6 +187,20 @@ extern "C" int mx_stream_create(void **stream) {
   return MX_SUCCESS;
 }
 
+// A blocking stream: implicitly after the legacy default stream's earlier
+// work (and before its later work) with no event per call -- the same host
+// cost as the default stream itself (profiles/r02/stream_probe.txt: 11.6 us
+// per synchronous call vs 22.9 us for a non-blocking stream + explicit
+// event order).
+extern "C" int mx_stream_create_ordered(void **stream) {
+  if (!stream) return MX_ERR_ARG;
+  if (int rc = mx_ensure_init()) return rc;
+  hipStream_t s = nullptr;
+  if (hipStreamCreateWithFlags(&s, hipStreamDefault) != hipSuccess) return MX_ERR_HIP;
+  *stream = s;
+  return MX_SUCCESS;
+}
+
 extern "C" int mx_stream_destroy(void *stream) {
   return stream ? mx_hip_rc(hipStreamDestroy((hipStream_t)stream)) : MX_SUCCESS;
 }

@@ -65,7 +65,8 @@ typedef struct {
     struct ompi_communicator_t *comm;
     mx_comm_t *mx;
     int mx_state;         /* 0 not created yet, 1 ready, -1 unavailable (agreed by all ranks) */
-    void *stream;         /* module-owned non-blocking stream */
+    void *stream;         /* blocking collectives: module-owned stream ordered with the default one */
+    void *nb_stream;      /* nonblocking / persistent requests: non-blocking stream */
     mx_scratch_t scratch[SCR_N];
     /* delegation targets (the slots we replaced) */
     mca_coll_base_module_allreduce_fn_t prev_allreduce;
@@ -129,6 +130,7 @@ static void coll_module_destruct(mx_coll_module_t *m)
     if (m->mx) mx_comm_destroy(m->mx);
     for (int k = 0; k < SCR_N; k++) mx_free(m->scratch[k].p);
     if (m->stream) mx_stream_destroy(m->stream);
+    if (m->nb_stream) mx_stream_destroy(m->nb_stream);
     if (m->prev_allreduce_module) MX_OBJ_RELEASE(m->prev_allreduce_module);
     if (m->prev_reduce_scatter_module) MX_OBJ_RELEASE(m->prev_reduce_scatter_module);
     if (m->prev_allgather_module) MX_OBJ_RELEASE(m->prev_allgather_module);
@@ -171,9 +173,11 @@ static int comm_ready(mx_coll_module_t *m)
         const int t = mx_ompi_host->mca_int("coll_mi355x_wait_timeout", 0);
         rc = mx_comm_set_timeout(m->mx, t > 0 ? (double)t : 0.0);
     }
-    /* the stream is process-local: a failure here is reported by the calls,
-     * never turned into a different protocol on this rank */
-    if (rc == MX_SUCCESS && !m->stream && mx_stream_create(&m->stream) != MX_SUCCESS) m->stream = NULL;
+    /* the streams are process-local: a failure here is reported by the calls
+     * (or falls back to the default stream), never turned into a different
+     * protocol on this rank */
+    if (rc == MX_SUCCESS && !m->stream && mx_stream_create_ordered(&m->stream) != MX_SUCCESS) m->stream = NULL;
+    if (rc == MX_SUCCESS && !m->nb_stream && mx_stream_create(&m->nb_stream) != MX_SUCCESS) m->nb_stream = NULL;
     if (rc != MX_SUCCESS) {
         if (m->mx) mx_comm_destroy(m->mx);
         m->mx = NULL;
@@ -274,11 +278,21 @@ static int xout(mx_coll_module_t *m, xbuf_t *x, size_t bytes)
     return rc ? rc : mx_stream_sync(m->stream);
 }
 
-/* the device work of a call starts after what the legacy default stream
- * already holds (the caller's kernels filling the buffers) */
+/* The device work of a call starts after what the legacy default stream
+ * already holds (the caller's kernels filling the buffers).  Blocking
+ * collectives run on a blocking stream, which is ordered with the default
+ * one implicitly; requests run on a non-blocking stream (a collective waiting
+ * for a late peer must not hold up the default stream -- a PML's device copy,
+ * say -- while the request is outstanding) and take an explicit event order
+ * (~11 us of host time per post, profiles/r02/stream_probe.txt). */
 static int begin(mx_coll_module_t *m)
 {
-    return m->stream ? mx_stream_order(m->stream, NULL) : MX_SUCCESS;
+    (void)m;
+    return MX_SUCCESS;
+}
+static int begin_nb(mx_coll_module_t *m)
+{
+    return m->nb_stream ? mx_stream_order(m->nb_stream, NULL) : MX_SUCCESS;
 }
 
 /* reduction eligibility: intrinsic op with a kernel for the (predefined)
@@ -389,7 +403,7 @@ static int mx_coll_reduce_local(const void *inbuf, void *inoutbuf, int count, st
     int slot, opi;
     if (reducible(dtype, op, (size_t)count, 1, &slot, &opi) && mx_is_device_ptr(inbuf) == 1 &&
         mx_is_device_ptr(inoutbuf) == 1) {
-        if (!m->stream && mx_stream_create(&m->stream) != MX_SUCCESS) m->stream = NULL;
+        if (!m->stream && mx_stream_create_ordered(&m->stream) != MX_SUCCESS) m->stream = NULL;
         int rc = begin(m);
         if (!rc) rc = mx_reduce2(opi, slot, inbuf, inoutbuf, (size_t)count, m->stream);
         if (!rc) rc = mx_stream_sync(m->stream);
@@ -551,13 +565,13 @@ static int req_stage(mx_coll_req_t *q, const void *user, struct ompi_datatype_t 
 static int req_fill(mx_coll_req_t *q)
 {
     mx_coll_module_t *m = q->m;
-    int rc = begin(m);
+    int rc = begin_nb(m);
     const xbuf_t *xs[2] = {&q->s, &q->r};
     const int in[2] = {q->s_in, q->r_in};
     for (int i = 0; i < 2 && !rc; i++) {
         const xbuf_t *x = xs[i];
         if (!x->user || !in[i]) continue;
-        rc = x->contiguous ? mx_memcpy(x->dev, x->user, x->bytes, m->stream) : xfer_packed(m, x, x->dev, 1);
+        rc = x->contiguous ? mx_memcpy(x->dev, x->user, x->bytes, m->nb_stream) : xfer_packed(m, x, x->dev, 1);
     }
     return rc;
 }
@@ -705,8 +719,8 @@ static int allreduce_like(mx_coll_module_t *m, const void *sbuf, void *rbuf, int
                                  bytes, persistent, ret);
     if (!r) return 0;
     const int alg = nbc_alg("iallreduce");
-    const int rc = persistent ? mx_allreduce_init(m->mx, SB(r), r->r.dev, (size_t)count, slot, opi, alg, m->stream, &q)
-                              : mx_iallreduce(m->mx, SB(r), r->r.dev, (size_t)count, slot, opi, alg, m->stream, &q);
+    const int rc = persistent ? mx_allreduce_init(m->mx, SB(r), r->r.dev, (size_t)count, slot, opi, alg, m->nb_stream, &q)
+                              : mx_iallreduce(m->mx, SB(r), r->r.dev, (size_t)count, slot, opi, alg, m->nb_stream, &q);
     *ret = post(r, rc, q, persistent, request);
     return 0;
 }
@@ -747,8 +761,8 @@ static int reduce_like(mx_coll_module_t *m, const void *sbuf, void *rbuf, int co
     if (!r) return 0;
     void *rb = rank == root ? r->r.dev : NULL;
     const int alg = nbc_alg("ireduce");
-    const int rc = persistent ? mx_reduce_init(m->mx, SB(r), rb, (size_t)count, slot, opi, root, alg, m->stream, &q)
-                              : mx_ireduce(m->mx, SB(r), rb, (size_t)count, slot, opi, root, alg, m->stream, &q);
+    const int rc = persistent ? mx_reduce_init(m->mx, SB(r), rb, (size_t)count, slot, opi, root, alg, m->nb_stream, &q)
+                              : mx_ireduce(m->mx, SB(r), rb, (size_t)count, slot, opi, root, alg, m->nb_stream, &q);
     *ret = post(r, rc, q, persistent, request);
     return 0;
 }
@@ -793,11 +807,11 @@ static int rs_like(mx_coll_module_t *m, const void *sbuf, void *rbuf, const int 
     if (!r) return 0;
     int rc;
     if (rcounts)
-        rc = persistent ? mx_reduce_scatter_init(m->mx, SB(r), r->r.dev, rc64, slot, opi, m->stream, &q)
-                        : mx_ireduce_scatter(m->mx, SB(r), r->r.dev, rc64, slot, opi, m->stream, &q);
+        rc = persistent ? mx_reduce_scatter_init(m->mx, SB(r), r->r.dev, rc64, slot, opi, m->nb_stream, &q)
+                        : mx_ireduce_scatter(m->mx, SB(r), r->r.dev, rc64, slot, opi, m->nb_stream, &q);
     else
-        rc = persistent ? mx_reduce_scatter_block_init(m->mx, SB(r), r->r.dev, (size_t)rcount, slot, opi, m->stream, &q)
-                        : mx_ireduce_scatter_block(m->mx, SB(r), r->r.dev, (size_t)rcount, slot, opi, m->stream, &q);
+        rc = persistent ? mx_reduce_scatter_block_init(m->mx, SB(r), r->r.dev, (size_t)rcount, slot, opi, m->nb_stream, &q)
+                        : mx_ireduce_scatter_block(m->mx, SB(r), r->r.dev, (size_t)rcount, slot, opi, m->nb_stream, &q);
     *ret = post(r, rc, q, persistent, request);
     return 0;
 }
@@ -860,11 +874,11 @@ static int scan_like(mx_coll_module_t *m, const void *sbuf, void *rbuf, int coun
     if (!r) return 0;
     const int alg = nbc_alg(exclusive ? "iexscan" : "iscan");
     if (exclusive)
-        rc = persistent ? mx_exscan_init(m->mx, SB(r), r->r.dev, (size_t)count, slot, opi, alg, m->stream, &q)
-                        : mx_iexscan(m->mx, SB(r), r->r.dev, (size_t)count, slot, opi, alg, m->stream, &q);
+        rc = persistent ? mx_exscan_init(m->mx, SB(r), r->r.dev, (size_t)count, slot, opi, alg, m->nb_stream, &q)
+                        : mx_iexscan(m->mx, SB(r), r->r.dev, (size_t)count, slot, opi, alg, m->nb_stream, &q);
     else
-        rc = persistent ? mx_scan_init(m->mx, SB(r), r->r.dev, (size_t)count, slot, opi, alg, m->stream, &q)
-                        : mx_iscan(m->mx, SB(r), r->r.dev, (size_t)count, slot, opi, alg, m->stream, &q);
+        rc = persistent ? mx_scan_init(m->mx, SB(r), r->r.dev, (size_t)count, slot, opi, alg, m->nb_stream, &q)
+                        : mx_iscan(m->mx, SB(r), r->r.dev, (size_t)count, slot, opi, alg, m->nb_stream, &q);
     *ret = post(r, rc, q, persistent, request);
     return 0;
 }
@@ -924,8 +938,8 @@ static int allgather_like(mx_coll_module_t *m, const void *sbuf, int scount, str
     mx_coll_req_t *r = req_setup(m, sbuf, (size_t)scount, sdtype, rbuf, (size_t)rcount * n, rdtype,
                                  sbuf == MPI_IN_PLACE, rbytes * n, persistent, ret);
     if (!r) return 0;
-    const int rc = persistent ? mx_allgather_init(m->mx, SB(r), r->r.dev, rbytes, m->stream, &q)
-                              : mx_iallgather(m->mx, SB(r), r->r.dev, rbytes, m->stream, &q);
+    const int rc = persistent ? mx_allgather_init(m->mx, SB(r), r->r.dev, rbytes, m->nb_stream, &q)
+                              : mx_iallgather(m->mx, SB(r), r->r.dev, rbytes, m->nb_stream, &q);
     *ret = post(r, rc, q, persistent, request);
     return 0;
 }
@@ -962,8 +976,8 @@ static int bcast_like(mx_coll_module_t *m, void *buf, int count, struct ompi_dat
     mx_coll_req_t *r = req_setup(m, NULL, 0, NULL, buf, (size_t)count, dtype, rank == root,
                                  rank == root ? 0 : bytes, persistent, ret);
     if (!r) return 0;
-    const int rc = persistent ? mx_bcast_init(m->mx, r->r.dev, bytes, root, m->stream, &q)
-                              : mx_ibcast(m->mx, r->r.dev, bytes, root, m->stream, &q);
+    const int rc = persistent ? mx_bcast_init(m->mx, r->r.dev, bytes, root, m->nb_stream, &q)
+                              : mx_ibcast(m->mx, r->r.dev, bytes, root, m->nb_stream, &q);
     *ret = post(r, rc, q, persistent, request);
     return 0;
 }

@@ -77,11 +77,13 @@ static int both_on_device(const void *a, const void *b)
     return mx_is_device_ptr(a) == 1 && mx_is_device_ptr(b) == 1;   /* range-cached: no runtime call */
 }
 
-/* The kernels run on a stream of the calling thread (non-blocking, so a
- * handler call never waits for unrelated work of other streams the way a
- * legacy-default-stream synchronise does; one per thread, so concurrent
- * callers under MPI_THREAD_MULTIPLE do not share one), ordered after what
- * the legacy default stream holds -- the kernels that produced the operands.
+/* The kernels run on a stream of the calling thread: one per thread, so
+ * concurrent callers under MPI_THREAD_MULTIPLE neither share a stream nor
+ * synchronise each other's work; a blocking stream, so it is implicitly
+ * ordered after what the legacy default stream holds (the kernels that
+ * produced the operands) at no per-call cost.  Measured per handler call
+ * (profiles/r02/op_call_cost.txt, stream_probe.txt): a non-blocking stream
+ * plus an explicit event order costs ~11 us more than this.
  * op_mi355x_stream = 0 selects the legacy default stream instead. */
 static _Thread_local void *t_stream;
 static _Thread_local int t_stream_tried;
@@ -93,7 +95,7 @@ static void *op_stream(void)
     if (!g_use_stream) return NULL;
     if (!t_stream_tried) {
         t_stream_tried = 1;
-        if (mx_stream_create(&t_stream) != MX_SUCCESS) t_stream = NULL;
+        if (mx_stream_create_ordered(&t_stream) != MX_SUCCESS) t_stream = NULL;
     }
     return t_stream;
 }
@@ -119,8 +121,7 @@ static void mx_op_2buff(void *in, void *inout, int *count, struct ompi_datatype_
     if (slot < 0) die("datatype lookup", MX_ERR_ARG);
     if (*count > 0 && both_on_device(in, inout)) {
         void *s = op_stream();
-        int rc = s ? mx_stream_order(s, NULL) : MX_SUCCESS;
-        if (rc == MX_SUCCESS) rc = mx_reduce2(m->op_index, slot, in, inout, (size_t)*count, s);
+        int rc = mx_reduce2(m->op_index, slot, in, inout, (size_t)*count, s);
         rc = run_sync(s, rc);
         if (rc != MX_SUCCESS) die("mx_reduce2", rc);
         return;
@@ -137,8 +138,7 @@ static void mx_op_3buff(void *in1, void *in2, void *out, int *count, struct ompi
     if (slot < 0) die("datatype lookup", MX_ERR_ARG);
     if (*count > 0 && both_on_device(in1, in2) && mx_is_device_ptr(out) == 1) {
         void *s = op_stream();
-        int rc = s ? mx_stream_order(s, NULL) : MX_SUCCESS;
-        if (rc == MX_SUCCESS) rc = mx_reduce3(m->op_index, slot, in1, in2, out, (size_t)*count, s);
+        int rc = mx_reduce3(m->op_index, slot, in1, in2, out, (size_t)*count, s);
         rc = run_sync(s, rc);
         if (rc != MX_SUCCESS) die("mx_reduce3", rc);
         return;
