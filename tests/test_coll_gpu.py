@@ -368,6 +368,16 @@ _JOBS = [("allreduce", 100003, "SUM", "FLOAT", "auto"),          # > staging: ch
         ("allreduce", 200003, "SUM", "FLOAT", "segmented_ring"),   # chunked path in between
         ("allreduce", 2500, "BXOR", "UINT16_T", "auto"),
         ("allreduce_inplace", 4000, "SUM", "FLOAT", "auto"),
+        # two-shot (above the one-shot range, one staging round): every fold
+        # shape, element path (x87, pair types) and 16-byte path, in place
+        ("allreduce", 30001, "SUM", "FLOAT", "auto"),
+        ("allreduce", 20011, "MAX", "DOUBLE", "rabenseifner"),
+        ("allreduce_inplace", 40000, "SUM", "FLOAT", "ring"),
+        ("allreduce", 9001, "MAXLOC", "FLOAT_INT", "segmented_ring"),
+        ("allreduce", 50001, "BAND", "UINT16_T", "auto"),
+        ("allreduce", 5001, "SUM", "LONG_DOUBLE", "recursive_doubling"),
+        ("allreduce", 12345, "PROD", "C_FLOAT_COMPLEX", "basic_linear"),
+        ("allreduce", 30001, "SUM", "FLOAT", "auto"),                  # back to back
         # rooted reduce / scan / exscan / reduce_scatter_block (VM fold)
         ("reduce", 100003, "SUM", "FLOAT", "auto"),                 # chunked
         ("reduce", 3001, "MAX", "DOUBLE", "binary"),
@@ -481,7 +491,8 @@ def test_multiprocess_ipc_bitexact(n):
 _JOBS8 = [j for j in _JOBS if (j[0], j[1]) in {
     ("allreduce", 100003), ("allreduce", 777), ("allreduce", 1000), ("reduce_scatter", 300001),
     ("allgather", 300001), ("bcast", 2000003), ("bcast_root0", 5), ("bcast_root0", 1000001),
-    ("reduce", 100003), ("scan", 20001), ("shmem", 5003), ("allreduce", 3001)}]
+    ("reduce", 100003), ("scan", 20001), ("shmem", 5003), ("allreduce", 3001), ("allreduce", 30001),
+    ("allreduce", 20011)}]
 
 
 def test_multiprocess_ipc_bitexact_8_ranks():

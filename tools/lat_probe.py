@@ -1,5 +1,5 @@
 """Allreduce latency per size on n processes sharing the GPU (diagnostic).
-usage: python tools/lat_probe.py N  (MX_ONESHOT_MAX in the environment)"""
+usage: python tools/lat_probe.py N  (MX_ONESHOT_MAX / MX_TWOSHOT_MAX in the environment)"""
 import os
 import sys
 import time
@@ -21,11 +21,12 @@ def worker(rank, n, port, q):
         dist.all_gather_object(out, b)
         return out
     comm = mxompi.Comm(rank, n, ag, device=0, staging_bytes=256 << 20)
-    x = torch.rand(4 << 20, device="cuda")
+    x = torch.rand(16 << 20, device="cuda")
     y = torch.empty_like(x)
     st = torch.cuda.current_stream().cuda_stream
     rows = []
-    for nb in [4 << 10, 16 << 10, 64 << 10, 128 << 10, 256 << 10, 512 << 10, 1 << 20, 2 << 20, 4 << 20, 8 << 20]:
+    for nb in [4 << 10, 16 << 10, 64 << 10, 128 << 10, 256 << 10, 512 << 10, 1 << 20, 2 << 20, 4 << 20, 8 << 20,
+               16 << 20, 32 << 20, 64 << 20]:
         cnt = nb // 4
         for _ in range(5):
             comm.allreduce(x.data_ptr(), y.data_ptr(), cnt, "FLOAT", "SUM", "auto", st)
@@ -57,4 +58,5 @@ if __name__ == "__main__":
     res = dict(q.get(timeout=300) for _ in range(n))
     for p in ps:
         p.join(timeout=60)
-    print(f"n={n} oneshot_max={os.environ.get('MX_ONESHOT_MAX', 'default')}:", res[0], flush=True)
+    print(f"n={n} oneshot_max={os.environ.get('MX_ONESHOT_MAX', 'default')} "
+          f"twoshot_max={os.environ.get('MX_TWOSHOT_MAX', 'default')}:", res[0], flush=True)

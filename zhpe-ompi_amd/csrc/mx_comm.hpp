@@ -38,7 +38,11 @@ constexpr size_t P2P_POSTED = FLAG_WORDS + 8;
 constexpr size_t P2P_FILLED = P2P_POSTED + MAXR;
 constexpr size_t P2P_SEEN = P2P_FILLED + (size_t)MAXR * P2P_L;
 constexpr size_t P2P_DRAINED = P2P_SEEN + (size_t)MAXR * P2P_L;
-constexpr size_t ALL_FLAG_WORDS = P2P_DRAINED + (size_t)MAXR * P2P_L;
+// two-shot mid-size allreduce (k_twoshot): per (source rank, workgroup)
+// READY and PUSHED flags
+constexpr size_t TS_READY = P2P_DRAINED + (size_t)MAXR * P2P_L;
+constexpr size_t TS_PUSHED = TS_READY + (size_t)MAXR * TSWG;
+constexpr size_t ALL_FLAG_WORDS = TS_PUSHED + (size_t)MAXR * TSWG;
 
 // device-local sequence state of the channels (not shared)
 struct P2PSendState { uint64_t msgs; uint64_t lane_chunks[P2P_L]; };
@@ -106,6 +110,8 @@ struct mx_comm {
   mx::P2PRecvState *p2p_recv;   // [size]
   hipStream_t p2p_stream[2];
   hipEvent_t p2p_ev;
+  uint64_t *p2p_lanes;     // device: finished-lane counters of the two streams
+  uint64_t p2p_kseq[2];    // transfer kernels enqueued per stream
   unsigned p2p_any_rr;   // MPI_ANY_SOURCE: source the next pick scans first
 };
 
@@ -126,7 +132,8 @@ struct mx_request {
   // point-to-point: peer, tag, and the status the receiving kernel writes
   // (mapped host memory: received bytes, envelope tag, error)
   int peer, tag;
-  int64_t *status;
+  int64_t *status;   // [0] bytes [1] tag [2] error [3] source [4] done (P2P_STATUS_WORDS)
+  int fast;          // completion by status[4] (no unpack kernel after the transfer)
   const struct mx_ddt *ddt;   // non-contiguous user layout (count instances), or null
 };
 
@@ -141,9 +148,10 @@ int req_submit(mx_request *q, mx_request_t **out);
 void req_discard(mx_request *q);
 int p2p_setup(mx_comm *c);
 void p2p_release(mx_comm *c);
-// receive status blocks (4 x int64, mapped host memory): from a process-wide
+// status blocks (P2P_STATUS_WORDS x int64, mapped host memory): from a process-wide
 // pool allocated once (never released, so a request may outlive its
 // communicator), else one hipHostMalloc each
+constexpr int P2P_STATUS_WORDS = 8;
 int64_t *p2p_status_get();
 void p2p_status_put(int64_t *st);
 }  // namespace mx

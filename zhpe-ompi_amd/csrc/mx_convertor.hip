@@ -23,6 +23,7 @@
 #include <vector>
 #include <climits>
 #include <algorithm>
+#include <mutex>
 
 #include "mx_internal.h"
 #include "../../include/mx_convertor.h"
@@ -523,6 +524,235 @@ __global__ void __launch_bounds__(kCB) k_pack_tile_pipe(ConvArgs a, int nruns_ld
   }
 }
 
+// ---------------------------------------------------------------------------
+// BYTE-MAP / PIECE kernels (instances of at most kBmapMaxS packed bytes,
+// i.e. the struct-like types whose pieces are narrow and irregular).
+//
+// The run walk above serialises each lane on its own stretch of pieces (the
+// struct type: ~3 divergent byte / word loops per lane per tile), so the
+// tile kernels are instruction-bound, and their unpack stores leave a user
+// line partially written for long enough that L2 writes it back more than
+// once (WRITE_SIZE 3.1 x the span on the struct type,
+// profiles/r02/convertor_r2.txt).  Here the instance layout is tabled once
+// per type and every lane runs the same straight-line code:
+//   PACK (byte map): bmap[b] = user offset of packed byte b of an instance.
+//     A workgroup stages the user span of a tile of stream bytes in LDS
+//     (16-byte coalesced loads), each lane assembles 16 packed bytes with 16
+//     LDS byte reads through the map and leaves with one 16-byte store.
+//   UNPACK (pieces): the instance is cut into naturally aligned pieces of
+//     1/2/4/8/16 user bytes (per user-pointer alignment), in stream order.
+//     A workgroup stages the packed bytes of a tile of pieces in LDS; lane l
+//     takes piece l, reads its bytes with five dword LDS reads + byte
+//     alignment and writes them with ONE store of the piece's width, so a
+//     wave writes 64 consecutive pieces at once and every user line is
+//     complete within a few instructions.  Gap bytes are never written.
+// ---------------------------------------------------------------------------
+constexpr uint32_t kBmapMaxS = 65535;      // packed bytes per instance (piece soff is 16-bit)
+constexpr size_t kBmapLds = 20480;         // PACK: map bytes staged in LDS
+constexpr int kBmapSpan = 24576;           // PACK: user span staged per tile
+constexpr int kPieceStage = 16384;         // UNPACK: packed bytes staged per tile
+
+struct DPiece {
+  int32_t uoff;       // user offset from the instance origin
+  uint16_t soff;      // stream offset within the instance
+  uint8_t lg;         // width = 1 << lg bytes (user address aligned to it)
+  uint8_t pad;
+};
+
+struct BmapArgs {
+  const void *map;         // M[S]: user offset of packed byte b minus umin
+  uint32_t S;
+  Magic mS;
+  int64_t ext;
+  int64_t umin, uspan;     // an instance touches user [umin, umin + uspan)
+  int mono;                // monotonic layout: a tile's span is [addr(first), addr(last)]
+  const char *user;
+  char *packed;            // (packed - offset) is 16-byte aligned
+  uint64_t offset, len;
+  uint64_t g0;             // first absolute granule (offset / 16)
+  uint64_t T;              // stream bytes per tile (multiple of 16)
+  uint64_t ntiles;
+  uint32_t adv_b;          // kCB * 4 stream bytes = adv_io / ext instances + adv_b bytes
+  int64_t adv_io;
+};
+
+// M = uint16_t when the instance's user span is below 64 KiB, else uint32_t
+template <int SPAN, class M, bool DW>
+__global__ void __launch_bounds__(kCB) k_pack_bmap(BmapArgs a) {
+  extern __shared__ __align__(16) char smem[];
+  char *span = smem;                                         // SPAN + 32
+  M *bmap = reinterpret_cast<M *>(smem + SPAN + 32);
+  __shared__ uintptr_t s_lo, s_hi;
+  for (uint32_t i = threadIdx.x; i < a.S; i += kCB) bmap[i] = reinterpret_cast<const M *>(a.map)[i];
+  const uint64_t wend = a.offset + a.len;
+  for (uint64_t t = blockIdx.x; t < a.ntiles; t += gridDim.x) {
+    const uint64_t s0 = a.g0 * 16 + t * a.T;                 // absolute stream bytes [s0, s1)
+    const uint64_t sa = s0 < a.offset ? a.offset : s0;
+    const uint64_t s1 = s0 + a.T < wend ? s0 + a.T : wend;
+    const uint64_t ia = udiv(sa, a.mS), ib = udiv(s1 - 1, a.mS);
+    const uintptr_t ubase = (uintptr_t)a.user + (int64_t)ia * a.ext + a.umin;   // instance ia, + umin
+    __syncthreads();                                          // map staged; previous tile done with span
+    if (threadIdx.x == 0) {
+      uintptr_t lo = ubase, hi = ubase + (int64_t)(ib - ia) * a.ext + a.uspan;
+      if (a.mono) {
+        lo = ubase + bmap[sa - ia * a.S];
+        hi = ubase + (int64_t)(ib - ia) * a.ext + bmap[s1 - 1 - ib * a.S] + 1;
+      }
+      s_lo = lo & ~(uintptr_t)15;
+      s_hi = (hi + 15) & ~(uintptr_t)15;
+    }
+    __syncthreads();
+    const uintptr_t lo = s_lo;
+    {
+      const uint4 *g = reinterpret_cast<const uint4 *>(lo);
+      uint4 *d = reinterpret_cast<uint4 *>(span);
+      const uint32_t nv = (uint32_t)((s_hi - lo) / 16);
+      for (uint32_t i = threadIdx.x; i < nv; i += kCB) d[i] = g[i];
+    }
+    __syncthreads();
+    const int64_t d0 = (int64_t)(ubase - lo);
+    if (DW) {
+      // lane = one packed dword per step, consecutive lanes consecutive
+      // dwords: the map reads of a wave are 8 bytes apart (2-way bank
+      // conflicts; 16-byte lanes read it 32 bytes apart, 8-way) and each
+      // store instruction writes 256 contiguous bytes
+      const uint64_t q0 = s0 / 4 + threadIdx.x;
+      uint64_t inst = udiv(q0 * 4, a.mS);
+      uint32_t b = (uint32_t)(q0 * 4 - inst * a.S);
+      int64_t io = (int64_t)(inst - ia) * a.ext + d0;
+      for (uint64_t q = q0; q * 4 < s1; q += kCB) {
+        const uint64_t p = q * 4;
+        if (p >= a.offset && p + 4 <= wend) {
+          uint32_t v = 0;
+          uint32_t bb = b;
+          int64_t ii = io;
+#pragma unroll
+          for (int i = 0; i < 4; i++) {
+            v |= (uint32_t)(uint8_t)span[ii + bmap[bb]] << (8 * i);
+            if (++bb == a.S) { bb = 0; ii += a.ext; }
+          }
+          *reinterpret_cast<uint32_t *>(a.packed + (p - a.offset)) = v;
+        } else {                                              // window edge: the bytes inside only
+          for (uint64_t x = p < a.offset ? a.offset : p; x < p + 4 && x < wend; x++) {
+            const uint64_t i = udiv(x, a.mS);
+            a.packed[x - a.offset] = span[(int64_t)(i - ia) * a.ext + d0 + bmap[x - i * a.S]];
+          }
+        }
+        b += a.adv_b;                                         // next: kCB dwords further
+        io += a.adv_io;
+        if (b >= a.S) { b -= a.S; io += a.ext; }
+      }
+      continue;
+    }
+    for (uint64_t g = s0 / 16 + threadIdx.x; g * 16 < s1; g += kCB) {
+      const uint64_t p = g * 16;
+      if (p < a.offset || p + 16 > wend) {                    // window edge: the bytes inside only
+        for (uint64_t q = p < a.offset ? a.offset : p; q < p + 16 && q < wend; q++) {
+          const uint64_t i = udiv(q, a.mS);
+          a.packed[q - a.offset] = span[(int64_t)(i - ia) * a.ext + d0 + bmap[q - i * a.S]];
+        }
+        continue;
+      }
+      uint64_t inst = udiv(p, a.mS);
+      uint32_t b = (uint32_t)(p - inst * a.S);
+      int64_t io = (int64_t)(inst - ia) * a.ext + d0;       // LDS offset of the instance origin (+ umin)
+      uint32_t w[4];
+#pragma unroll
+      for (int k = 0; k < 4; k++) {
+        uint32_t v = 0;
+#pragma unroll
+        for (int i = 0; i < 4; i++) {
+          v |= (uint32_t)(uint8_t)span[io + bmap[b]] << (8 * i);
+          if (++b == a.S) { b = 0; io += a.ext; }
+        }
+        w[k] = v;
+      }
+      *reinterpret_cast<uint4 *>(a.packed + (p - a.offset)) = make_uint4(w[0], w[1], w[2], w[3]);
+    }
+  }
+}
+
+struct PieceArgs {
+  const DPiece *pieces;
+  uint32_t npi;
+  Magic mnpi;
+  uint64_t S;
+  int64_t ext;
+  char *user;
+  const char *packed;
+  uint64_t offset, len;
+  uint64_t P0, P1;         // pieces overlapping [offset, offset + len)
+  uint32_t K;              // pieces per tile (multiple of kCB)
+  uint32_t dinst, dj;      // kCB pieces = dinst instances + dj pieces
+  uint64_t ntiles;
+  int tbl_lds;             // table staged in LDS
+};
+
+__device__ __forceinline__ void piece_store(char *u, int lg, uint32_t v0, uint32_t v1, uint32_t v2, uint32_t v3) {
+  switch (lg) {
+    case 0: *reinterpret_cast<uint8_t *>(u) = (uint8_t)v0; break;
+    case 1: *reinterpret_cast<uint16_t *>(u) = (uint16_t)v0; break;
+    case 2: *reinterpret_cast<uint32_t *>(u) = v0; break;
+    case 3: *reinterpret_cast<uint2 *>(u) = make_uint2(v0, v1); break;
+    default: *reinterpret_cast<uint4 *>(u) = make_uint4(v0, v1, v2, v3); break;
+  }
+}
+
+__global__ void __launch_bounds__(kCB) k_unpack_piece(PieceArgs a) {
+  extern __shared__ __align__(16) char smem[];
+  char *stage = smem;                                        // kPieceStage + 48
+  DPiece *stbl = reinterpret_cast<DPiece *>(smem + kPieceStage + 48);
+  const DPiece *tbl = a.pieces;
+  if (a.tbl_lds) {
+    for (uint32_t i = threadIdx.x; i < a.npi; i += kCB) stbl[i] = a.pieces[i];
+    tbl = stbl;
+  }
+  const uint64_t wend = a.offset + a.len;
+  for (uint64_t t = blockIdx.x; t < a.ntiles; t += gridDim.x) {
+    const uint64_t Pa = a.P0 + t * a.K;
+    const uint64_t Pb = Pa + a.K < a.P1 ? Pa + a.K : a.P1;
+    __syncthreads();                                          // table staged / previous tile consumed
+    // stream range of the tile: first byte of piece Pa .. last byte of Pb - 1
+    const uint64_t ia = udiv(Pa, a.mnpi), ib = udiv(Pb - 1, a.mnpi);
+    const DPiece fa = tbl[Pa - ia * a.npi], fb = tbl[Pb - 1 - ib * a.npi];
+    uint64_t sa = ia * a.S + fa.soff, sb = ib * a.S + fb.soff + (1u << fb.lg);
+    sa = sa < a.offset ? a.offset : sa;
+    sb = sb < wend ? sb : wend;
+    const uintptr_t lo = (uintptr_t)(a.packed + (sa - a.offset)) & ~(uintptr_t)15;
+    const uintptr_t hi = ((uintptr_t)(a.packed + (sb - a.offset)) + 15) & ~(uintptr_t)15;
+    {
+      const uint4 *g = reinterpret_cast<const uint4 *>(lo);
+      uint4 *d = reinterpret_cast<uint4 *>(stage);
+      const uint32_t nv = (uint32_t)((hi - lo) / 16);
+      for (uint32_t i = threadIdx.x; i < nv; i += kCB) d[i] = g[i];
+    }
+    __syncthreads();
+    uint64_t P = Pa + threadIdx.x;
+    uint64_t inst = udiv(P, a.mnpi);
+    uint32_t j = (uint32_t)(P - inst * a.npi);
+    for (; P < Pb; P += kCB) {
+      const DPiece pc = tbl[j];
+      const uint64_t sp = inst * a.S + pc.soff;
+      const uint32_t n = 1u << pc.lg;
+      char *u = a.user + (int64_t)inst * a.ext + pc.uoff;
+      const int64_t li = (int64_t)((uintptr_t)(a.packed + (sp - a.offset)) - lo);
+      if (sp >= a.offset && sp + n <= wend) {
+        const uint32_t *w = reinterpret_cast<const uint32_t *>(stage + (li & ~(int64_t)3));
+        const int sh = (int)(li & 3);
+        const uint32_t w0 = w[0], w1 = w[1], w2 = w[2], w3 = w[3], w4 = w[4];
+        piece_store(u, pc.lg, __builtin_amdgcn_alignbyte(w1, w0, sh), __builtin_amdgcn_alignbyte(w2, w1, sh),
+                    __builtin_amdgcn_alignbyte(w3, w2, sh), __builtin_amdgcn_alignbyte(w4, w3, sh));
+      } else {                                                // piece cut by the window
+        for (uint32_t i = 0; i < n; i++)
+          if (sp + i >= a.offset && sp + i < wend) u[i] = stage[li + i];
+      }
+      j += a.dj;
+      inst += a.dinst;
+      if (j >= a.npi) { j -= a.npi; inst++; }
+    }
+  }
+}
+
 }  // namespace mx
 
 using namespace mx;
@@ -535,6 +765,23 @@ struct mx_ddt {
   uint64_t gcd_all;  // gcd of every disp/stride/blen/extent (access unit)
   Magic mS;          // divide by size
   bool monotonic;    // user addresses strictly increase along the stream
+  // byte map of one instance (size <= kBmapMaxS): bmap[b] = user offset of
+  // packed byte b.  PACK kernel k_pack_bmap stages (bmap - umin) as 16-bit
+  // (user span < 64 KiB) or 32-bit words when they fit kBmapLds.
+  std::vector<int32_t> bmap;
+  void *map_dev = nullptr;
+  int map16 = 0;
+  int64_t umin = 0, uspan = 0;
+  uint64_t bmap_T = 0;             // stream bytes per PACK tile (0: no PACK kernel)
+  // piece tables per user-origin alignment (address mod 16), built on first
+  // use: UNPACK kernel k_unpack_piece
+  struct PieceTab {
+    std::vector<DPiece> host;
+    DPiece *dev = nullptr;
+    uint32_t K = 0;                // pieces per tile
+    int built = 0;                 // 1 ok, -1 not applicable
+  } ptab[16];
+  std::mutex mu;
 };
 
 namespace {
@@ -661,6 +908,117 @@ static uint64_t gcd64(uint64_t a, uint64_t b) {
 }
 static uint64_t absg(int64_t v) { return v < 0 ? (uint64_t)(-v) : (uint64_t)v; }
 
+// Byte map of one instance: bmap[b] = user offset of packed byte b.  Also
+// fixes the PACK tile: the largest multiple of 256 stream bytes (<= 16 KiB)
+// whose user span, rounded out to 16 bytes, always fits kBmapSpan -- whole
+// instances for a non-monotonic layout, [addr(first), addr(last)] for a
+// monotonic one.
+static void build_bmap(mx_ddt *d) {
+  const int64_t ext = d->ub - d->lb;
+  const uint64_t S = d->size;
+  if (S == 0 || S > kBmapMaxS || ext <= 0) return;
+  std::vector<int32_t> m;
+  m.reserve(S);
+  int64_t lo = INT64_MAX, hi = INT64_MIN;
+  for (const DRun &r : d->host)
+    for (uint64_t l2 = 0; l2 < r.cnt2; l2++)
+      for (uint64_t l1 = 0; l1 < r.cnt1; l1++)
+        for (uint64_t o = 0; o < r.blen; o++) {
+          const int64_t u = r.disp + (int64_t)l2 * r.stride2 + (int64_t)l1 * r.stride1 + (int64_t)o;
+          if (u < INT32_MIN || u > INT32_MAX) return;
+          m.push_back((int32_t)u);
+          lo = std::min(lo, u);
+          hi = std::max(hi, u + 1);
+        }
+  if (m.size() != S) return;
+  d->bmap.swap(m);
+  d->umin = lo;
+  d->uspan = hi - lo;
+  d->map16 = d->uspan <= 65536;
+  // PACK stages whole user spans: only for dense layouts (<= 4 user bytes
+  // per packed byte; a sparse one reads mostly gaps -- ref_matrix_borders at
+  // 23: 0.83 -> 0.42 TB/s) and maps small enough for >= 3 workgroups per CU
+  // (ref_upper_matrix_60's 29 KiB map: 1.32 -> 1.25 TB/s)
+  if (S * (d->map16 ? 2 : 4) > kBmapLds || ext > 4 * (int64_t)S || d->uspan > 4 * (int64_t)S) return;
+  // user bytes a tile of T stream bytes starting at instance byte b touches
+  auto U = [&](uint64_t x) { return (int64_t)(x / S) * ext + d->bmap[x % S]; };
+  auto worst = [&](uint64_t T) {
+    if (!d->monotonic) return (int64_t)(((T - 1) / S + 1) * (uint64_t)ext) + d->uspan;
+    int64_t w = 0;
+    for (uint64_t b = 0; b < S; b++) w = std::max<int64_t>(w, U(b + T - 1) - U(b) + 1);
+    return w;
+  };
+  uint64_t T = 16384;
+  while (T >= 256 && worst(T) + 32 > kBmapSpan) T -= 256;
+  d->bmap_T = T >= 256 ? T : 0;
+}
+
+// Pieces of one instance for a user origin at address `al` mod 16: maximal
+// contiguous user runs in stream order, cut into naturally aligned
+// 1/2/4/8/16-byte pieces (aligned for every instance: the width also
+// divides the extent).  Caller holds d->mu.
+static mx_ddt::PieceTab *piece_tab(mx_ddt *d, int al) {
+  mx_ddt::PieceTab &P = d->ptab[al];
+  if (P.built) return P.built > 0 ? &P : nullptr;
+  P.built = -1;
+  const uint64_t A = gcd64(16, absg(d->ub - d->lb));
+  const size_t S = d->bmap.size();
+  std::vector<DPiece> v;
+  for (size_t b = 0; b < S;) {
+    size_t L = 1;
+    while (b + L < S && d->bmap[b + L] == d->bmap[b] + (int32_t)L) L++;
+    for (size_t pos = 0; pos < L;) {
+      const int64_t x = (int64_t)d->bmap[b] + (int64_t)pos;
+      const uint64_t addr = (uint64_t)(((al + x) % 16 + 16) % 16);
+      uint64_t w = 16;
+      while (w > 1 && (addr % w || w > L - pos || A % w)) w >>= 1;
+      DPiece pc;
+      pc.uoff = (int32_t)x;
+      pc.soff = (uint16_t)(b + pos);
+      pc.lg = (uint8_t)__builtin_ctzll(w);
+      pc.pad = 0;
+      v.push_back(pc);
+      pos += w;
+    }
+    b += L;
+  }
+  const uint32_t npi = (uint32_t)v.size();
+  // pieces per tile: ~8 KiB of stream, staged bytes (+ alignment slop) <= kPieceStage
+  auto window = [&](uint32_t K) {
+    uint64_t mx = 0;
+    for (uint32_t j = 0; j < npi; j++) {
+      const uint64_t e = (uint64_t)j + K - 1;
+      const DPiece &pe = v[e % npi];
+      const uint64_t end = (e / npi) * S + pe.soff + (1u << pe.lg);
+      mx = std::max<uint64_t>(mx, end - v[j].soff);
+    }
+    return mx;
+  };
+  uint64_t K = std::max<uint64_t>(kCB, std::min<uint64_t>(4096, (8192ull * npi / S) / kCB * kCB));
+  while (K > kCB && window((uint32_t)K) + 32 > (uint64_t)kPieceStage) K -= kCB;
+  if (window((uint32_t)K) + 32 > (uint64_t)kPieceStage) return nullptr;
+  if (hipMalloc((void **)&P.dev, npi * sizeof(DPiece)) != hipSuccess) { P.dev = nullptr; return nullptr; }
+  if (hipMemcpy(P.dev, v.data(), npi * sizeof(DPiece), hipMemcpyHostToDevice) != hipSuccess) {
+    (void)hipFree(P.dev);
+    P.dev = nullptr;
+    return nullptr;
+  }
+  P.host.swap(v);
+  P.K = (uint32_t)K;
+  P.built = 1;
+  return &P;
+}
+
+// index of the piece holding packed byte b of an instance
+static uint32_t piece_of(const std::vector<DPiece> &v, uint64_t b) {
+  uint32_t lo = 0, hi = (uint32_t)v.size() - 1;
+  while (lo < hi) {
+    const uint32_t mid = (lo + hi + 1) / 2;
+    if (v[mid].soff <= b) lo = mid; else hi = mid - 1;
+  }
+  return lo;
+}
+
 }  // namespace
 
 extern "C" int mx_ddt_create(const void *desc, size_t nrec, const uint64_t *basic_sizes, size_t size, int64_t lb,
@@ -701,6 +1059,23 @@ extern "C" int mx_ddt_create(const void *desc, size_t nrec, const uint64_t *basi
       return MX_ERR_HIP;
     }
   }
+  build_bmap(d);
+  if (d->bmap_T) {
+    std::vector<uint16_t> m16;
+    std::vector<uint32_t> m32;
+    for (int32_t u : d->bmap) {
+      if (d->map16) m16.push_back((uint16_t)(u - d->umin));
+      else m32.push_back((uint32_t)(u - d->umin));
+    }
+    const size_t nb = d->map16 ? m16.size() * 2 : m32.size() * 4;
+    const void *src = d->map16 ? (const void *)m16.data() : (const void *)m32.data();
+    if (hipMalloc(&d->map_dev, nb) != hipSuccess || hipMemcpy(d->map_dev, src, nb, hipMemcpyHostToDevice) != hipSuccess) {
+      if (d->map_dev) (void)hipFree(d->map_dev);
+      if (d->dev) (void)hipFree(d->dev);
+      delete d;
+      return MX_ERR_HIP;
+    }
+  }
   *out = d;
   return MX_SUCCESS;
 }
@@ -708,6 +1083,9 @@ extern "C" int mx_ddt_create(const void *desc, size_t nrec, const uint64_t *basi
 extern "C" int mx_ddt_destroy(mx_ddt_t *d) {
   if (!d) return MX_SUCCESS;
   if (d->dev) (void)hipFree(d->dev);
+  if (d->map_dev) (void)hipFree(d->map_dev);
+  for (auto &P : d->ptab)
+    if (P.dev) (void)hipFree(P.dev);
   delete d;
   return MX_SUCCESS;
 }
@@ -758,11 +1136,31 @@ static bool conv_pipe_enabled() {
   return on != 0;
 }
 
+// MX_CONV_BMAP=0 keeps small irregular instances on the run-walking tile
+// kernels (A/B switch; results are identical).
+static bool conv_bmap_enabled() {
+  static const int on = [] {
+    const char *e = getenv("MX_CONV_BMAP");
+    return (e && *e == '0') ? 0 : 1;
+  }();
+  return on != 0;
+}
+
+// MX_CONV_BMAP_DW=0 gives each lane of the byte-map PACK kernel 16 packed
+// bytes (one 16-byte store) instead of one dword per step (A/B switch).
+static bool conv_bmap_dw() {
+  static const int on = [] {
+    const char *e = getenv("MX_CONV_BMAP_DW");
+    return (e && *e == '0') ? 0 : 1;
+  }();
+  return on != 0;
+}
+
 static int conv_pipe_geom() {
   static const int g = [] {
     const char *e = getenv("MX_CONV_PIPE_GEOM");
-    const int v = e ? atoi(e) : 1;
-    return (v >= 0 && v <= 3) ? v : 1;
+    const int v = e ? atoi(e) : 0;
+    return (v >= 0 && v <= 3) ? v : 0;
   }();
   return g;
 }
@@ -826,6 +1224,72 @@ static int convert(const mx_ddt_t *d, size_t count, char *user, char *packed, si
     hipLaunchKernelGGL((k_convert<16, PACK>), dim3((unsigned)((g + kCB - 1) / kCB)), dim3(kCB), run_lds, s, a);
     return mx_check_launch();
   }
+  // small irregular instances: byte-map PACK / piece UNPACK (see the kernels)
+  if (!d->bmap.empty() && conv_bmap_enabled()) {
+    if (PACK && d->bmap_T && (((uintptr_t)packed - offset) & 15) == 0) {
+      BmapArgs b;
+      b.map = d->map_dev;
+      b.mono = d->monotonic;
+      b.S = (uint32_t)d->size;
+      b.mS = d->mS;
+      b.ext = d->ub - d->lb;
+      b.umin = d->umin;
+      b.uspan = d->uspan;
+      b.user = user;
+      b.packed = packed;
+      b.offset = offset;
+      b.len = len;
+      b.g0 = offset / 16;
+      b.T = d->bmap_T;
+      b.ntiles = ((offset + len + 15) / 16 * 16 - b.g0 * 16 + b.T - 1) / b.T;
+      const size_t lds = kBmapSpan + 32 + d->size * (d->map16 ? 2 : 4);
+      const uint64_t per_cu = std::max<uint64_t>(1, std::min<uint64_t>(8, (160 * 1024) / lds));
+      const uint64_t grid = std::min<uint64_t>(b.ntiles, (uint64_t)g_num_cus * per_cu);
+      b.adv_b = (uint32_t)((kCB * 4) % d->size);
+      b.adv_io = (int64_t)((kCB * 4) / d->size) * b.ext;
+      const bool dw = conv_bmap_dw();
+#define MX_BMAP_LAUNCH(M, DW) \
+  hipLaunchKernelGGL((k_pack_bmap<kBmapSpan, M, DW>), dim3((unsigned)grid), dim3(kCB), lds, s, b)
+      if (d->map16) { if (dw) MX_BMAP_LAUNCH(uint16_t, true); else MX_BMAP_LAUNCH(uint16_t, false); }
+      else { if (dw) MX_BMAP_LAUNCH(uint32_t, true); else MX_BMAP_LAUNCH(uint32_t, false); }
+#undef MX_BMAP_LAUNCH
+      return mx_check_launch();
+    }
+    if (!PACK) {
+      mx_ddt *dm = const_cast<mx_ddt *>(d);
+      mx_ddt::PieceTab *pt;
+      {
+        std::lock_guard<std::mutex> g(dm->mu);
+        pt = piece_tab(dm, (int)((uintptr_t)user & 15));
+      }
+      if (pt) {
+        PieceArgs p;
+        const uint32_t npi = (uint32_t)pt->host.size();
+        p.pieces = pt->dev;
+        p.npi = npi;
+        p.mnpi = make_magic(npi);
+        p.S = d->size;
+        p.ext = d->ub - d->lb;
+        p.user = user;
+        p.packed = packed;
+        p.offset = offset;
+        p.len = len;
+        const uint64_t i0 = offset / d->size, i1 = (offset + len - 1) / d->size;
+        p.P0 = i0 * npi + piece_of(pt->host, offset - i0 * d->size);
+        p.P1 = i1 * npi + piece_of(pt->host, offset + len - 1 - i1 * d->size) + 1;
+        p.K = pt->K;
+        p.dinst = (uint32_t)(kCB / npi);
+        p.dj = (uint32_t)(kCB % npi);
+        p.ntiles = (p.P1 - p.P0 + p.K - 1) / p.K;
+        p.tbl_lds = npi * sizeof(DPiece) <= 16384;
+        const size_t lds = kPieceStage + 48 + (p.tbl_lds ? npi * sizeof(DPiece) : 0);
+        const uint64_t per_cu = std::max<uint64_t>(1, std::min<uint64_t>(8, (160 * 1024) / lds));
+        const uint64_t grid = std::min<uint64_t>(p.ntiles, (uint64_t)g_num_cus * per_cu);
+        hipLaunchKernelGGL(k_unpack_piece, dim3((unsigned)grid), dim3(kCB), lds, s, p);
+        return mx_check_launch();
+      }
+    }
+  }
   // narrow pieces: tile kernels (PACK needs a monotonic layout so that a
   // tile's user bytes form one span)
   if (!PACK || d->monotonic) {
@@ -833,8 +1297,11 @@ static int convert(const mx_ddt_t *d, size_t count, char *user, char *packed, si
     const size_t rb = nlds ? (size_t)a.nruns * sizeof(DRun) : 0;
     if (PACK && conv_pipe_enabled()) {
       // MX_CONV_PIPE_GEOM selects the tile geometry (A/B measurement; results
-      // are identical): 0 = 8192 x 24 KiB span (round 1), 1 = 9216 x 16 KiB,
-      // 2 = 9216 x 28 KiB, 3 = 8192 x 16 KiB
+      // are identical): 0 = 8192 x 24 KiB span, 1 = 9216 x 16 KiB,
+      // 2 = 9216 x 28 KiB, 3 = 8192 x 16 KiB.  0 is fastest on every type
+      // measured (profiles/r02/convertor_r2.txt): the bank-conflict-free
+      // 36-byte stretches of 1 / 2 lose more to the tile / occupancy change
+      // than the conflicts cost (20k of ~4M cycles per wave).
       const int geom = conv_pipe_geom();
 #define MX_PIPE_LAUNCH(TPV, SPV, WGS)                                                                        \
   do {                                                                                                        \
@@ -843,10 +1310,10 @@ static int convert(const mx_ddt_t *d, size_t count, char *user, char *packed, si
     hipLaunchKernelGGL((k_pack_tile_pipe<TPV, SPV>), dim3((unsigned)grid), dim3(kCB),                          \
                        (PipeGeom<TPV, SPV>::lds(rb)), s, a, nlds, tiles);                                        \
   } while (0)
-      if (geom == 0) MX_PIPE_LAUNCH(8192, 24576, 4);
-      else if (geom == 2) MX_PIPE_LAUNCH(9216, 28672, 3);
+      if (geom == 2) MX_PIPE_LAUNCH(9216, 28672, 3);
       else if (geom == 3) MX_PIPE_LAUNCH(8192, 16384, 6);
-      else MX_PIPE_LAUNCH(9216, 16384, 6);
+      else if (geom == 1) MX_PIPE_LAUNCH(9216, 16384, 6);
+      else MX_PIPE_LAUNCH(8192, 24576, 4);
 #undef MX_PIPE_LAUNCH
       return mx_check_launch();
     }

@@ -89,6 +89,34 @@ __device__ __forceinline__ void p2p_lane(uint64_t bytes, int l, uint64_t *lo, ui
   *hi = std::min<uint64_t>(bytes, *lo + stripe);
 }
 
+// Host-visible completion of a transfer kernel: every lane workgroup counts
+// itself out on a device counter (kernels of one internal stream run one
+// after another, so the counter reaches `target` exactly when this kernel's
+// last lane is done, whatever path the lanes took), and that last lane
+// raises `done` in the request's mapped status block.  mx_wait polls the
+// word in host memory instead of querying a HIP event, which wakes tens of
+// microseconds late.
+struct P2PDone {
+  uint64_t *lanes;       // device counter of finished lanes (per stream)
+  uint64_t target;
+  int64_t *done;         // mapped host word, or null
+};
+
+__device__ __forceinline__ void lane_finished(const P2PDone &f) {
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    __threadfence_system();
+    const uint64_t old = __hip_atomic_fetch_add(f.lanes, (uint64_t)1, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+    if (old + 1 == f.target && f.done) {
+      __threadfence_system();
+      __hip_atomic_store(f.done, (int64_t)1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+  }
+}
+
+struct P2PSendArgs;
+__device__ __forceinline__ void send_body(const P2PSendArgs &a);
+
 struct P2PSendArgs {
   const char *buf;
   uint64_t bytes;
@@ -101,9 +129,15 @@ struct P2PSendArgs {
   P2PSendState *st;
   uint64_t timeout_ticks;
   int *err;
+  P2PDone fin;
 };
 
 __global__ void __launch_bounds__(kP2PThreads) k_p2p_send(P2PSendArgs a) {
+  send_body(a);
+  lane_finished(a.fin);
+}
+
+__device__ __forceinline__ void send_body(const P2PSendArgs &a) {
   const int l = blockIdx.x;
   const uint64_t t0 = wall_clock64();
   __shared__ int ok;
@@ -161,6 +195,7 @@ struct P2PRecvArgs {
   const uint64_t *flag0;     // my flag array
   uint64_t *peer_flags[MAXR];
   P2PRecvState *st0;
+  P2PDone fin;
 };
 
 // MX_ANY_SOURCE: wait until some source p has posted an envelope beyond what
@@ -188,7 +223,14 @@ __global__ void k_p2p_pick(const uint64_t *flag0, const P2PRecvState *st0, int n
   }
 }
 
+__device__ __forceinline__ void recv_body(const P2PRecvArgs &a);
+
 __global__ void __launch_bounds__(kP2PThreads) k_p2p_recv(P2PRecvArgs a) {
+  recv_body(a);
+  lane_finished(a.fin);
+}
+
+__device__ __forceinline__ void recv_body(const P2PRecvArgs &a) {
   const int l = blockIdx.x;
   const uint64_t t0 = wall_clock64();
   __shared__ int ok;
@@ -256,7 +298,14 @@ int p2p_setup(mx_comm *c) {
     c->p2p_send = nullptr;
     return MX_ERR_NOMEM;
   }
+  if (hipMalloc((void **)&c->p2p_lanes, 2 * sizeof(uint64_t)) != hipSuccess) {
+    c->p2p_lanes = nullptr;
+    p2p_release(c);
+    return MX_ERR_NOMEM;
+  }
+  c->p2p_kseq[0] = c->p2p_kseq[1] = 0;
   if (hipMemset(c->p2p_send, 0, sb) != hipSuccess || hipMemset(c->p2p_recv, 0, rb) != hipSuccess ||
+      hipMemset(c->p2p_lanes, 0, 2 * sizeof(uint64_t)) != hipSuccess ||
       hipStreamCreateWithFlags(&c->p2p_stream[0], hipStreamNonBlocking) != hipSuccess ||
       hipStreamCreateWithFlags(&c->p2p_stream[1], hipStreamNonBlocking) != hipSuccess ||
       hipEventCreateWithFlags(&c->p2p_ev, hipEventDisableTiming) != hipSuccess ||
@@ -273,6 +322,8 @@ void p2p_release(mx_comm *c) {
   if (c->p2p_ev) (void)hipEventDestroy(c->p2p_ev);
   if (c->p2p_send) (void)hipFree(c->p2p_send);
   if (c->p2p_recv) (void)hipFree(c->p2p_recv);
+  if (c->p2p_lanes) (void)hipFree(c->p2p_lanes);
+  c->p2p_lanes = nullptr;
   c->p2p_stream[0] = c->p2p_stream[1] = nullptr;
   c->p2p_ev = nullptr;
   c->p2p_send = nullptr;
@@ -282,7 +333,7 @@ void p2p_release(mx_comm *c) {
 namespace {
 constexpr int kStatusPool = 4096;
 std::mutex g_status_mu;
-int64_t *g_status_pool;          // kStatusPool blocks of 4 x int64
+int64_t *g_status_pool;          // kStatusPool blocks of P2P_STATUS_WORDS x int64
 int g_status_free[kStatusPool];
 int g_status_nfree = -1;         // -1: not allocated yet
 }  // namespace
@@ -292,7 +343,8 @@ int64_t *p2p_status_get() {
     std::lock_guard<std::mutex> lk(g_status_mu);
     if (g_status_nfree < 0) {
       g_status_nfree = 0;
-      if (hipHostMalloc((void **)&g_status_pool, (size_t)kStatusPool * 4 * sizeof(int64_t), hipHostMallocMapped) ==
+      if (hipHostMalloc((void **)&g_status_pool, (size_t)kStatusPool * P2P_STATUS_WORDS * sizeof(int64_t),
+                        hipHostMallocMapped) ==
           hipSuccess) {
         for (int i = 0; i < kStatusPool; i++) g_status_free[i] = kStatusPool - 1 - i;
         g_status_nfree = kStatusPool;
@@ -300,10 +352,11 @@ int64_t *p2p_status_get() {
         g_status_pool = nullptr;
       }
     }
-    if (g_status_nfree > 0) return g_status_pool + (size_t)g_status_free[--g_status_nfree] * 4;
+    if (g_status_nfree > 0) return g_status_pool + (size_t)g_status_free[--g_status_nfree] * P2P_STATUS_WORDS;
   }
   int64_t *st = nullptr;
-  if (hipHostMalloc((void **)&st, 4 * sizeof(int64_t), hipHostMallocMapped) != hipSuccess) return nullptr;
+  if (hipHostMalloc((void **)&st, P2P_STATUS_WORDS * sizeof(int64_t), hipHostMallocMapped) != hipSuccess)
+    return nullptr;
   return st;
 }
 
@@ -311,8 +364,8 @@ void p2p_status_put(int64_t *st) {
   if (!st) return;
   {
     std::lock_guard<std::mutex> lk(g_status_mu);
-    if (g_status_pool && st >= g_status_pool && st < g_status_pool + (size_t)kStatusPool * 4) {
-      g_status_free[g_status_nfree++] = (int)((st - g_status_pool) / 4);
+    if (g_status_pool && st >= g_status_pool && st < g_status_pool + (size_t)kStatusPool * P2P_STATUS_WORDS) {
+      g_status_free[g_status_nfree++] = (int)((st - g_status_pool) / P2P_STATUS_WORDS);
       return;
     }
   }
@@ -328,10 +381,28 @@ int p2p_enqueue(mx_request *q, hipStream_t *done_stream) {
   int rc = p2p_setup(c);
   if (rc) return rc;
   const bool send = q->kind == RQ_SEND;
-  hipStream_t s = c->p2p_stream[send ? 0 : 1];
-  if (hipEventRecord(c->p2p_ev, q->s) != hipSuccess || hipStreamWaitEvent(s, c->p2p_ev, 0) != hipSuccess)
-    return MX_ERR_HIP;
+  const int dir = send ? 0 : 1;
+  hipStream_t s = c->p2p_stream[dir];
+  // after the work the caller's stream has queued -- none when it is idle
+  // (the event pair costs as much as the transfer of a small message)
+  const hipError_t qe = hipStreamQuery(q->s);
+  if (qe != hipSuccess) {
+    if (qe != hipErrorNotReady) return MX_ERR_HIP;
+    if (hipEventRecord(c->p2p_ev, q->s) != hipSuccess || hipStreamWaitEvent(s, c->p2p_ev, 0) != hipSuccess)
+      return MX_ERR_HIP;
+  }
   *done_stream = s;
+  if (!q->status && !(q->status = p2p_status_get())) return MX_ERR_NOMEM;
+  memset(q->status, 0, P2P_STATUS_WORDS * sizeof(int64_t));
+  int64_t *st_dev = nullptr;
+  if (hipHostGetDevicePointer((void **)&st_dev, q->status, 0) != hipSuccess) return MX_ERR_HIP;
+  // completion through status[4] when the transfer kernel is the last one
+  P2PDone fin;
+  q->fast = !q->ddt;
+  fin.lanes = c->p2p_lanes + dir;
+  fin.target = (c->p2p_kseq[dir] + 1) * P2P_L;
+  fin.done = q->fast ? st_dev + 4 : nullptr;
+  c->p2p_kseq[dir]++;   // every transfer kernel counts its lanes, flagged or not
   const int me = c->rank, p = q->peer;
   const size_t bytes = q->ddt ? q->count * mx_ddt_size(q->ddt) : q->count;
   char *tmp = nullptr;
@@ -351,14 +422,11 @@ int p2p_enqueue(mx_request *q, hipStream_t *done_stream) {
     a.st = c->p2p_send + p;
     a.timeout_ticks = c->timeout_ticks;
     a.err = c->err_dev;
+    a.fin = fin;
     hipLaunchKernelGGL(k_p2p_send, dim3(P2P_L), dim3(kP2PThreads), 0, s, a);
     if ((rc = mx_check_launch())) return rc;
   } else {
-    if (!q->status && !(q->status = p2p_status_get())) return MX_ERR_NOMEM;
-    memset(q->status, 0, 4 * sizeof(int64_t));
     q->status[3] = p;
-    int64_t *st_dev = nullptr;
-    if (hipHostGetDevicePointer((void **)&st_dev, q->status, 0) != hipSuccess) return MX_ERR_HIP;
     P2PRecvArgs a;
     memset(&a, 0, sizeof a);
     a.buf = tmp ? tmp : (char *)q->rbuf;
@@ -386,6 +454,7 @@ int p2p_enqueue(mx_request *q, hipStream_t *done_stream) {
     a.status = st_dev;
     a.timeout_ticks = c->timeout_ticks;
     a.err = c->err_dev;
+    a.fin = fin;
     hipLaunchKernelGGL(k_p2p_recv, dim3(P2P_L), dim3(kP2PThreads), 0, s, a);
     if ((rc = mx_check_launch())) return rc;
     if (tmp && (rc = mx_unpack(q->ddt, q->count, q->rbuf, tmp, 0, bytes, s))) return rc;
