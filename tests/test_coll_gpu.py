@@ -368,7 +368,7 @@ _JOBS = [("allreduce", 100003, "SUM", "FLOAT", "auto"),          # > staging: ch
         ("allreduce", 200003, "SUM", "FLOAT", "segmented_ring"),   # chunked path in between
         ("allreduce", 2500, "BXOR", "UINT16_T", "auto"),
         ("allreduce_inplace", 4000, "SUM", "FLOAT", "auto"),
-        # two-shot (above the one-shot range, one staging round): every fold
+        # above the one-shot range within one staging round: every fold
         # shape, element path (x87, pair types) and 16-byte path, in place
         ("allreduce", 30001, "SUM", "FLOAT", "auto"),
         ("allreduce", 20011, "MAX", "DOUBLE", "rabenseifner"),

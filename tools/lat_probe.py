@@ -1,5 +1,5 @@
 """Allreduce latency per size on n processes sharing the GPU (diagnostic).
-usage: python tools/lat_probe.py N  (MX_ONESHOT_MAX / MX_TWOSHOT_MAX in the environment)"""
+usage: python tools/lat_probe.py N  (MX_ONESHOT_MAX in the environment)"""
 import os
 import sys
 import time
@@ -58,5 +58,4 @@ if __name__ == "__main__":
     res = dict(q.get(timeout=300) for _ in range(n))
     for p in ps:
         p.join(timeout=60)
-    print(f"n={n} oneshot_max={os.environ.get('MX_ONESHOT_MAX', 'default')} "
-          f"twoshot_max={os.environ.get('MX_TWOSHOT_MAX', 'default')}:", res[0], flush=True)
+    print(f"n={n} oneshot_max={os.environ.get('MX_ONESHOT_MAX', 'default')}:", res[0], flush=True)

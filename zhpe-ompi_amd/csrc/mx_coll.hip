@@ -40,6 +40,7 @@
 #include <algorithm>
 #include <chrono>
 #include <map>
+#include <mutex>
 #include <new>
 
 #include "mx_comm.hpp"
@@ -835,10 +836,7 @@ static int wait_all(mx_comm *c, int kind, uint64_t value, hipStream_t s) {
 }
 
 static inline size_t rup(size_t v, size_t a) { return (v + a - 1) / a * a; }
-static inline size_t gcd_sz(size_t a, size_t b) {
-  while (b) { const size_t t = a % b; a = b; b = t; }
-  return a;
-}
+
 
 // staging layout for a chunk of `ce` elements of size es
 struct Layout { size_t slot, gather_off; };
@@ -908,97 +906,6 @@ static int allreduce_oneshot(mx_comm *c, oneshot_launch_fn ol, const std::vector
   return finish(c, s);
 }
 
-// Two-shot allreduce (mid-size messages): the staged path in one kernel,
-// see k_twoshot.  Eligible when the whole vector fits one staging round and
-// every part's fold has at most OS_MAXSEG segments; the decision depends only
-// on (n, count, type, alg, staging), so every rank takes the same path.
-// Bytes per rank up to MX_TWOSHOT_MAX (default 64 MiB; 0 disables).
-static size_t twoshot_max() {
-  static const size_t v = [] {
-    const char *e = getenv("MX_TWOSHOT_MAX");
-    if (!e || !*e) return (size_t)64 << 20;
-    const long long x = atoll(e);
-    return x > 0 ? (size_t)x : (size_t)0;
-  }();
-  return v;
-}
-
-// 1 = not eligible (caller takes the chunked path), else an MX_* code
-static int allreduce_twoshot(mx_comm *c, twoshot_launch_fn tl, int alg, const char *sb, char *rb, size_t count,
-                             size_t es, hipStream_t s) {
-  const int n = c->size, r = c->rank;
-  if (!tl || count * es > twoshot_max() || count < (size_t)n) return 1;
-  const Layout L = layout_for(n, count, es);
-  if (L.gather_off + count * es + 16 > c->main_bytes) return 1;
-  size_t off[MAXR], len[MAXR];
-  blockcount(count, n, off, len);
-  std::vector<Seg> mine;
-  for (int p = 0; p < n; p++) {
-    std::vector<Seg> segs;
-    if (int rc = allreduce_segments(alg, n, count, es, off[p], off[p] + len[p], segs)) return rc;
-    if (segs.size() > (size_t)OS_MAXSEG) return 1;
-    if (p == r) mine.swap(segs);
-  }
-  // slices: >= 4 KiB (one 16-byte vector per lane: the memory parallelism
-  // comes from the number of workgroups -- 16 KiB slices, 4 dependent
-  // round trips per lane, ran 2.5x slower than the chunked path), at most
-  // TSWG workgroups and 1024 / n per rank (n ranks sharing one GPU stay
-  // co-resident), whole 16-byte vectors
-  const size_t part_bytes = len[0] * es;
-  static const size_t wg_env = [] {
-    const char *e = getenv("MX_TWOSHOT_WG");
-    return (size_t)(e && *e ? atoll(e) : 0);
-  }();
-  size_t cap = std::max<size_t>(1, std::min<size_t>(TSWG, 1024 / (size_t)n));
-  if (wg_env) cap = std::min(cap, wg_env);
-  const size_t unit = 16 / gcd_sz(es, 16);
-  size_t slice = std::max<size_t>((size_t)4 << 10, (part_bytes + cap - 1) / cap);
-  slice = (slice + es - 1) / es;
-  slice = (slice + unit - 1) / unit * unit;
-  const size_t nwg = (len[0] + slice - 1) / slice;
-  if (nwg > cap) return 1;
-  TwoShotArgs a;
-  memset(&a, 0, sizeof a);
-  const uint64_t g = ++c->gen;
-  a.sb = sb;
-  a.rb = rb;
-  a.slice = slice;
-  a.ndst = 0;
-  a.dst[a.ndst++] = rb + off[r] * es;
-  for (int p = 0; p < n; p++) {
-    a.off[p] = off[p];
-    a.len[p] = len[p];
-    a.src[p] = p == r ? sb + off[r] * es : c->staging + (size_t)p * L.slot + ((off[r] * es) & 15);
-    if (p == r) continue;
-    a.push_dst[p] = c->peer_staging[p] + (size_t)r * L.slot + ((off[p] * es) & 15);
-    a.dst[a.ndst++] = c->peer_staging[p] + L.gather_off + off[r] * es;
-    a.gath[p] = c->staging + L.gather_off + off[p] * es;
-    a.peer_ready[p] = c->peer_flags[p] + TS_READY + (size_t)r * TSWG;
-    a.peer_pushed[p] = c->peer_flags[p] + TS_PUSHED + (size_t)r * TSWG;
-    a.peer_done[p] = c->peer_flags[p] + FLAG_DONE * MAXR + r;
-  }
-  a.my_ready = c->flagmem + TS_READY;
-  a.my_pushed = c->flagmem + TS_PUSHED;
-  a.my_done = c->flagmem + FLAG_DONE * MAXR;
-  a.counter = c->flagmem + OS_COUNTER;
-  a.counter_last = c->os_count + nwg - 1;
-  c->os_count += nwg;
-  a.gen = g;
-  a.timeout_ticks = c->timeout_ticks;
-  a.err = c->err_dev;
-  a.poison = c->poison;
-  a.n = n;
-  a.rank = r;
-  a.es = es;
-  a.nseg = (int)mine.size();
-  for (size_t i = 0; i < mine.size(); i++) a.seg[i] = OsSeg{mine[i].lo, mine[i].hi, mine[i].p};
-  prof_begin(c, s);
-  int rc = tl(a, (int)nwg, s);
-  prof_end(c, s, 0, (double)(2 * n + 2) * (double)(count * es) / (double)n);
-  if (rc) return rc;
-  return finish(c, s);
-}
-
 }  // namespace
 
 extern "C" int mx_allreduce(mx_comm_t *c, const void *sbuf, void *rbuf, size_t count, int type, int op, int alg,
@@ -1056,10 +963,6 @@ extern "C" int mx_allreduce(mx_comm_t *c, const void *sbuf, void *rbuf, size_t c
     if (rc) return rc;
     oneshot_launch_fn ol = fold_fns(op, type).oneshot;
     if (ol && segs.size() <= (size_t)OS_MAXSEG) return allreduce_oneshot(c, ol, segs, sb, rb, count, es, s);
-  }
-  {
-    const int rc = allreduce_twoshot(c, fold_fns(op, type).twoshot, alg, sb, rb, count, es, s);
-    if (rc != 1) return rc;
   }
   {  // validate the algorithm once for the whole vector
     std::vector<Seg> probe;
@@ -2316,12 +2219,37 @@ static int req_complete(mx_request *q) {
   return MX_SUCCESS;
 }
 
+// Completion events of requests come from a process-wide free list: a
+// hipEventCreate + hipEventDestroy pair per request is a large part of a
+// small message's host cost.
+static std::mutex g_ev_mu;
+static std::vector<hipEvent_t> g_ev_free;
+
+static int req_event_get(hipEvent_t *e) {
+  {
+    std::lock_guard<std::mutex> lk(g_ev_mu);
+    if (!g_ev_free.empty()) {
+      *e = g_ev_free.back();
+      g_ev_free.pop_back();
+      return MX_SUCCESS;
+    }
+  }
+  return hipEventCreateWithFlags(e, hipEventDisableTiming) == hipSuccess ? MX_SUCCESS : MX_ERR_HIP;
+}
+
+static void req_event_put(hipEvent_t e) {
+  if (!e) return;
+  std::lock_guard<std::mutex> lk(g_ev_mu);
+  if (g_ev_free.size() < 1024) g_ev_free.push_back(e);
+  else (void)hipEventDestroy(e);
+}
+
 static int req_new(mx_comm *c, int kind, int persistent, void *stream, mx_request_t **out, mx_request **q) {
   if (!c || !out) return MX_ERR_ARG;
   *out = nullptr;
   mx_request *r = new (std::nothrow) mx_request();
   if (!r) return MX_ERR_NOMEM;
-  if (hipEventCreateWithFlags(&r->done, hipEventDisableTiming) != hipSuccess) {
+  if (req_event_get(&r->done) != MX_SUCCESS) {
     delete r;
     return MX_ERR_HIP;
   }
@@ -2338,7 +2266,7 @@ static int req_post(mx_request *q, mx_request_t **out) {
   if (!q->persistent) {
     const int rc = req_start(q);
     if (rc) {
-      (void)hipEventDestroy(q->done);
+      req_event_put(q->done);
       mx::p2p_status_put(q->status);
       delete q;
       return rc;
@@ -2356,7 +2284,7 @@ static int req_reduction(mx_comm_t *c, int kind, int persistent, const void *sbu
   if (!mx_type_size(type) || (kind != RQ_REDUCE && !rbuf)) rc = MX_ERR_ARG;
   else if (!fold_fns(op, type).vm) rc = MX_ERR_UNSUPPORTED;
   if (rc) {
-    (void)hipEventDestroy(q->done);
+    req_event_put(q->done);
     delete q;
     return rc;
   }
@@ -2379,7 +2307,7 @@ int req_create(mx_comm *c, int kind, int persistent, void *stream, mx_request **
 }
 int req_submit(mx_request *q, mx_request_t **out) { return req_post(q, out); }
 void req_discard(mx_request *q) {
-  (void)hipEventDestroy(q->done);
+  req_event_put(q->done);
   mx::p2p_status_put(q->status);
   delete q;
 }
@@ -2430,7 +2358,7 @@ static int req_reduce_scatter(mx_comm_t *c, int kind, int persistent, const void
   if (!mx_type_size(type) || !rbuf) rc = MX_ERR_ARG;
   else if (!fold_fns(op, type).vm) rc = MX_ERR_UNSUPPORTED;
   if (rc) {
-    (void)hipEventDestroy(q->done);
+    req_event_put(q->done);
     delete q;
     return rc;
   }
@@ -2559,7 +2487,7 @@ extern "C" int mx_request_free(mx_request_t *q) {
   if (!q) return MX_SUCCESS;
   int rc = MX_SUCCESS;
   if (q->active) rc = mx_wait(q);   // MPI_Request_free lets an active operation finish
-  (void)hipEventDestroy(q->done);
+  req_event_put(q->done);
   mx::p2p_status_put(q->status);
   delete q;
   return rc;

@@ -38,11 +38,7 @@ constexpr size_t P2P_POSTED = FLAG_WORDS + 8;
 constexpr size_t P2P_FILLED = P2P_POSTED + MAXR;
 constexpr size_t P2P_SEEN = P2P_FILLED + (size_t)MAXR * P2P_L;
 constexpr size_t P2P_DRAINED = P2P_SEEN + (size_t)MAXR * P2P_L;
-// two-shot mid-size allreduce (k_twoshot): per (source rank, workgroup)
-// READY and PUSHED flags
-constexpr size_t TS_READY = P2P_DRAINED + (size_t)MAXR * P2P_L;
-constexpr size_t TS_PUSHED = TS_READY + (size_t)MAXR * TSWG;
-constexpr size_t ALL_FLAG_WORDS = TS_PUSHED + (size_t)MAXR * TSWG;
+constexpr size_t ALL_FLAG_WORDS = P2P_DRAINED + (size_t)MAXR * P2P_L;
 
 // device-local sequence state of the channels (not shared)
 struct P2PSendState { uint64_t msgs; uint64_t lane_chunks[P2P_L]; };

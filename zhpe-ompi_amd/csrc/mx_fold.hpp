@@ -1,14 +1,12 @@
 // mx_fold.hpp -- device side of the collective fold: the kernels that read
 // the n contributions of a range of elements and evaluate, per element, the
 // reduction tree of a reference algorithm (see mx_coll.hip for the host
-// side).  Four evaluators:
+// side).  Three evaluators:
 //   k_fold     CHAIN / BUTTERFLY programs in registers (allreduce and
 //              reduce_scatter: the ring / recursive-doubling / Rabenseifner /
 //              recursive-halving trees);
 //   k_oneshot  the same programs fused with the all-peer exchange for small
 //              allreduce messages;
-//   k_twoshot  the staged reduce-scatter + allgather of mid-size allreduce
-//              messages in one launch;
 //   k_vm       an LDS-register VM for arbitrary trees and multi-output DAGs:
 //              rooted reduce (binomial / binary / pipeline / chain /
 //              in-order binary trees of coll_base_topo.c), scan / exscan
@@ -308,196 +306,6 @@ int oneshot_launch(OneShotArgs &a, int nwg, hipStream_t s) {
 }
 
 // ---------------------------------------------------------------------------
-// two-shot allreduce for mid-size messages: the staged reduce-scatter +
-// allgather of the chunked path (push parts -> fold own part -> push result
-// -> collect) in ONE launch.  The vector is cut into n parts
-// (COMPUTE_BLOCKCOUNT) and every part into slices; workgroup w owns slice w
-// of every part and synchronises with workgroup w of each peer only, through
-// per-(source, workgroup) READY / PUSHED flags -- so the phases of different
-// slices overlap and no launch boundary separates them (the chunked path
-// pays nine dependent launches).  Every rank folds its own part with the
-// same program as the chunked path (bit-identical results).  Staging reuse
-// needs every peer past gen-1 (DONE flags, as in the chunked path); the last
-// workgroup out raises DONE(gen).
-// ---------------------------------------------------------------------------
-constexpr int TSWG = 512;   // workgroups (slices per part) at most
-
-struct TwoShotArgs {
-  const char *sb;
-  char *rb;
-  size_t off[MAXR], len[MAXR];   // parts, elements
-  size_t slice;                  // elements per slice
-  char *push_dst[MAXR];          // peer p's slot for source = me at element off[p] (null for me)
-  const char *src[MAXR];         // operand j of my part, at element off[rank]
-  char *dst[MAXR];               // my part's result: my rbuf, then every peer's gather area
-  int ndst;
-  const char *gath[MAXR];        // my gather area at element off[p]
-  uint64_t *peer_ready[MAXR];    // peer p's TS READY row for source = me
-  uint64_t *peer_pushed[MAXR];   // peer p's TS PUSHED row for source = me
-  uint64_t *peer_done[MAXR];     // peer p's DONE flag for source = me
-  const uint64_t *my_ready;      // my TS READY rows [src][TSWG]
-  const uint64_t *my_pushed;     // my TS PUSHED rows [src][TSWG]
-  const uint64_t *my_done;       // my DONE flags [src]
-  uint64_t *counter;
-  uint64_t counter_last, gen, timeout_ticks;
-  int *err;
-  int *poison;
-  int n, rank, nseg, vec;
-  size_t es;
-  OsSeg seg[OS_MAXSEG];          // fold programs over my part (absolute elements)
-};
-
-// bytes [0, nb) from s to d by the workgroup: 16-byte moves when both sides
-// share their alignment
-__device__ __forceinline__ void ts_copy(char *d, const char *s, size_t nb) {
-  const int t = threadIdx.x;
-  const size_t ph = (uintptr_t)s & 15;
-  if ((((uintptr_t)d ^ (uintptr_t)s) & 15) == 0 && nb >= 32) {
-    const size_t head = ph ? 16 - ph : 0, nv = (nb - head) / 16, tail0 = head + nv * 16;
-    if ((size_t)t < head) d[t] = s[t];
-    const uint4 *sv = reinterpret_cast<const uint4 *>(s + head);
-    uint4 *dv = reinterpret_cast<uint4 *>(d + head);
-    constexpr int U = 4;                       // loads in flight per lane before any store
-    for (size_t i = t; i < nv; i += U * kOSB) {
-      uint4 v[U];
-#pragma unroll
-      for (int k = 0; k < U; k++)
-        if (i + (size_t)k * kOSB < nv) v[k] = sv[i + (size_t)k * kOSB];
-#pragma unroll
-      for (int k = 0; k < U; k++)
-        if (i + (size_t)k * kOSB < nv) dv[i + (size_t)k * kOSB] = v[k];
-    }
-    for (size_t i = tail0 + t; i < nb; i += kOSB) d[i] = s[i];
-  } else {
-    for (size_t i = t; i < nb; i += kOSB) d[i] = s[i];
-  }
-}
-
-// fold elements [e0, e1) of my part (relative to its first element) with
-// program p; every operand / destination shares one alignment when a.vec
-template <class T, class OP>
-__device__ __forceinline__ void ts_fold(const TwoShotArgs &a, const FoldProg &p, size_t e0, size_t e1) {
-  using V = fvec<T>;
-  constexpr int N = V::N;
-  const int t = threadIdx.x;
-  auto scalar = [&](size_t e) {
-    const size_t off = e * sizeof(T);
-    const T r = eval_prog<OP, T>(p, [&](int j) { return *reinterpret_cast<const T *>(a.src[j] + off); });
-#pragma unroll
-    for (int d = 0; d < MAXR; d++)
-      if (d < a.ndst) store_fields(reinterpret_cast<T *>(a.dst[d] + off), r);
-  };
-  size_t head = e1 - e0, nvec = 0;
-  if (N > 0 && a.vec) {
-    const size_t ph = ((uintptr_t)a.src[0] + e0 * sizeof(T)) & 15;
-    head = ph ? (16 - ph) / sizeof(T) : 0;
-    if (head > e1 - e0) head = e1 - e0;
-    nvec = (e1 - e0 - head) / (N ? N : 1);
-  }
-  for (size_t i = t; i < head; i += kOSB) scalar(e0 + i);
-  if constexpr (N > 0) {
-    const size_t vb = (e0 + head) * sizeof(T);
-    for (size_t i = t; i < nvec; i += kOSB) {
-      const size_t off = vb + i * 16;
-      const V r = eval_prog<OP, V>(p, [&](int j) { return *reinterpret_cast<const V *>(a.src[j] + off); });
-#pragma unroll
-      for (int d = 0; d < MAXR; d++)
-        if (d < a.ndst) *reinterpret_cast<V *>(a.dst[d] + off) = r;
-    }
-  }
-  for (size_t i = e0 + head + nvec * (N ? N : 1) + t; i < e1; i += kOSB) scalar(i);
-}
-
-template <class T, class OP>
-__global__ void __launch_bounds__(kOSB) k_twoshot(TwoShotArgs a) {
-  const int w = blockIdx.x, t = threadIdx.x, r = a.rank;
-  __shared__ int s_bad;
-  auto bad = [&]() {
-    __syncthreads();
-    if (t == 0) s_bad = poisoned(a.poison);
-    __syncthreads();
-    return s_bad != 0;
-  };
-  if (bad()) return;
-  // (1) every peer finished gen-1: its staging (my slot there) is free
-  if (t < a.n && t != r && a.gen > 1) os_spin(a.my_done + t, a.gen - 1, a.timeout_ticks, a.err, a.poison);
-  if (bad()) return;
-  // (2) slice w of every peer's part -> that peer's slot for me
-  for (int p = 0; p < a.n; p++) {
-    if (p == r) continue;
-    const size_t lo = (size_t)w * a.slice;
-    if (lo >= a.len[p]) continue;
-    const size_t ne = (lo + a.slice < a.len[p] ? lo + a.slice : a.len[p]) - lo;
-    ts_copy(a.push_dst[p] + lo * a.es, a.sb + (a.off[p] + lo) * a.es, ne * a.es);
-  }
-  __threadfence_system();
-  __syncthreads();
-  // (3) READY(me, w) at every peer; wait READY(p, w) from every peer
-  if (t < a.n && t != r) {
-    __hip_atomic_store(a.peer_ready[t] + w, a.gen, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
-    os_spin(a.my_ready + (size_t)t * TSWG + w, a.gen, a.timeout_ticks, a.err, a.poison);
-  }
-  if (bad()) return;
-  __atomic_thread_fence(__ATOMIC_ACQUIRE);
-  // (4) fold slice w of my part into my rbuf and every peer's gather area
-  {
-    const size_t lo = (size_t)w * a.slice;
-    const size_t hi = lo + a.slice < a.len[r] ? lo + a.slice : a.len[r];
-    for (int k = 0; k < a.nseg && lo < hi; k++) {
-      const size_t s0 = a.seg[k].lo - a.off[r], s1 = a.seg[k].hi - a.off[r];
-      const size_t e0 = s0 > lo ? s0 : lo, e1 = s1 < hi ? s1 : hi;
-      if (e0 < e1) ts_fold<T, OP>(a, a.seg[k].p, e0, e1);
-    }
-  }
-  __threadfence_system();
-  __syncthreads();
-  // (5) PUSHED(me, w) at every peer; wait PUSHED(p, w); collect slice w of part p
-  if (t < a.n && t != r) {
-    __hip_atomic_store(a.peer_pushed[t] + w, a.gen, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
-    os_spin(a.my_pushed + (size_t)t * TSWG + w, a.gen, a.timeout_ticks, a.err, a.poison);
-  }
-  if (bad()) return;
-  __atomic_thread_fence(__ATOMIC_ACQUIRE);
-  for (int p = 0; p < a.n; p++) {
-    if (p == r) continue;
-    const size_t lo = (size_t)w * a.slice;
-    if (lo >= a.len[p]) continue;
-    const size_t ne = (lo + a.slice < a.len[p] ? lo + a.slice : a.len[p]) - lo;
-    ts_copy(a.rb + (a.off[p] + lo) * a.es, a.gath[p] + lo * a.es, ne * a.es);
-  }
-  // (6) the last workgroup out raises DONE(gen) at every peer
-  __syncthreads();
-  if (t == 0) {
-    __threadfence();
-    const uint64_t old = __hip_atomic_fetch_add(a.counter, (uint64_t)1, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
-    if (old == a.counter_last) {
-      __threadfence_system();
-      for (int p = 0; p < a.n; p++)
-        if (p != r) __hip_atomic_store(a.peer_done[p], a.gen, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
-    }
-  }
-}
-
-typedef int (*twoshot_launch_fn)(TwoShotArgs &, int nwg, hipStream_t);
-
-template <class T, class OP>
-int twoshot_launch(TwoShotArgs &a, int nwg, hipStream_t s) {
-  constexpr size_t N = (sizeof(T) <= 16 && 16 % sizeof(T) == 0) ? 16 / sizeof(T) : 0;
-  bool vec = N > 0 && !has_pad<T>::value;
-  const uintptr_t m = (uintptr_t)a.src[a.rank] & 15;
-  for (int j = 0; j < a.n; j++)
-    if (((uintptr_t)a.src[j] & 15) != m) vec = false;
-  for (int d = 0; d < a.ndst; d++)
-    if (((uintptr_t)a.dst[d] & 15) != m) vec = false;
-  if (m % sizeof(T)) vec = false;
-  a.vec = vec;
-  hipLaunchKernelGGL((k_twoshot<T, OP>), dim3(nwg), dim3(kOSB), 0, s, a);
-  return mx_check_launch();
-}
-
-
-
-// ---------------------------------------------------------------------------
 // fold VM: arbitrary reduction trees / DAGs with LDS-resident registers.
 // Registers 0..nsrc-1 hold the n contributions of this lane's element(s);
 // COMB r[d] = OP(r[a], r[b]) (a = target/first operand, b = source); EMIT
@@ -629,7 +437,6 @@ struct FoldFns {
   fold_launch_fn fold;
   oneshot_launch_fn oneshot;
   vm_launch_fn vm;
-  twoshot_launch_fn twoshot;
 };
 
 // family of an element type: 0 8/16-bit integers, 1 32/64-bit integers,
@@ -649,11 +456,11 @@ template <int F>
 struct FamVisitor {
   template <class T, class OP2, class OP3> FoldFns go() {
     if constexpr (fam<T>::value == F)
-      return FoldFns{&fold_launch<T, OP2>, &oneshot_launch<T, OP2>, &vm_launch<T, OP2>, &twoshot_launch<T, OP2>};
+      return FoldFns{&fold_launch<T, OP2>, &oneshot_launch<T, OP2>, &vm_launch<T, OP2>};
     else
-      return FoldFns{nullptr, nullptr, nullptr, nullptr};
+      return FoldFns{nullptr, nullptr, nullptr};
   }
-  FoldFns none() { return FoldFns{nullptr, nullptr, nullptr, nullptr}; }
+  FoldFns none() { return FoldFns{nullptr, nullptr, nullptr}; }
 };
 
 // defined in mx_fold_f<F>.hip
@@ -670,7 +477,7 @@ inline FoldFns fold_fns(int op, int type) {
     const FoldFns r = f[i](op, type);
     if (r.fold) return r;
   }
-  return FoldFns{nullptr, nullptr, nullptr, nullptr};
+  return FoldFns{nullptr, nullptr, nullptr};
 }
 
 }  // namespace mx

@@ -141,14 +141,20 @@ __device__ __forceinline__ void send_body(const P2PSendArgs &a) {
   const int l = blockIdx.x;
   const uint64_t t0 = wall_clock64();
   __shared__ int ok;
-  if (l == 0 && threadIdx.x == 0) {
+  __shared__ int s_seen_bad;
+  if (l == 0) {
     // envelope: the header slot is free once every lane of the receiver has
-    // read the envelope P2P_H messages back
+    // read the envelope P2P_H messages back -- one thread per lane counter
+    // (a serial scan of 64 uncached words by one thread cost most of a
+    // small message's latency)
     const uint64_t m = a.st->msgs;
-    bool good = true;
-    for (int i = 0; i < P2P_L && good; i++)
-      good = p2p_wait_ge(a.seen + i, m + 1 > P2P_H ? m + 1 - P2P_H : 0, t0, a.timeout_ticks, a.err);
-    if (good) {
+    if (threadIdx.x == 0) s_seen_bad = 0;
+    __syncthreads();
+    if (threadIdx.x < P2P_L &&
+        !p2p_wait_ge(a.seen + threadIdx.x, m + 1 > P2P_H ? m + 1 - P2P_H : 0, t0, a.timeout_ticks, a.err))
+      s_seen_bad = 1;
+    __syncthreads();
+    if (threadIdx.x == 0 && !s_seen_bad) {
       volatile uint64_t *h = reinterpret_cast<volatile uint64_t *>(a.box + (m % P2P_H) * P2P_HDR);
       h[0] = a.bytes;
       h[1] = (uint64_t)a.tag;
@@ -334,6 +340,7 @@ namespace {
 constexpr int kStatusPool = 4096;
 std::mutex g_status_mu;
 int64_t *g_status_pool;          // kStatusPool blocks of P2P_STATUS_WORDS x int64
+int64_t *g_status_pool_dev;      // its device address
 int g_status_free[kStatusPool];
 int g_status_nfree = -1;         // -1: not allocated yet
 }  // namespace
@@ -348,6 +355,8 @@ int64_t *p2p_status_get() {
           hipSuccess) {
         for (int i = 0; i < kStatusPool; i++) g_status_free[i] = kStatusPool - 1 - i;
         g_status_nfree = kStatusPool;
+        if (hipHostGetDevicePointer((void **)&g_status_pool_dev, g_status_pool, 0) != hipSuccess)
+          g_status_pool_dev = nullptr;
       } else {
         g_status_pool = nullptr;
       }
@@ -358,6 +367,18 @@ int64_t *p2p_status_get() {
   if (hipHostMalloc((void **)&st, P2P_STATUS_WORDS * sizeof(int64_t), hipHostMallocMapped) != hipSuccess)
     return nullptr;
   return st;
+}
+
+// device address of a status block (pool blocks: no runtime call)
+int64_t *p2p_status_dev(int64_t *st) {
+  {
+    std::lock_guard<std::mutex> lk(g_status_mu);
+    if (g_status_pool && g_status_pool_dev && st >= g_status_pool &&
+        st < g_status_pool + (size_t)kStatusPool * P2P_STATUS_WORDS)
+      return g_status_pool_dev + (st - g_status_pool);
+  }
+  int64_t *d = nullptr;
+  return hipHostGetDevicePointer((void **)&d, st, 0) == hipSuccess ? d : nullptr;
 }
 
 void p2p_status_put(int64_t *st) {
@@ -394,8 +415,8 @@ int p2p_enqueue(mx_request *q, hipStream_t *done_stream) {
   *done_stream = s;
   if (!q->status && !(q->status = p2p_status_get())) return MX_ERR_NOMEM;
   memset(q->status, 0, P2P_STATUS_WORDS * sizeof(int64_t));
-  int64_t *st_dev = nullptr;
-  if (hipHostGetDevicePointer((void **)&st_dev, q->status, 0) != hipSuccess) return MX_ERR_HIP;
+  int64_t *st_dev = p2p_status_dev(q->status);
+  if (!st_dev) return MX_ERR_HIP;
   // completion through status[4] when the transfer kernel is the last one
   P2PDone fin;
   q->fast = !q->ddt;
