@@ -7,6 +7,10 @@
 //   nb+evsync launch(s) + hipEventRecord(done, s) + hipEventSynchronize(done)
 //   blocking  launch on a hipStreamDefault stream (implicitly ordered with 0) + sync(s)
 //   nb+query  launch(s) + poll hipStreamQuery(s) until done
+// and the host cost of single calls on an idle device (no wait):
+//   query0    hipStreamQuery(0)        queryNB  hipStreamQuery(nb)
+//   record    hipEventRecord(ev, nb)   launch64 a 64-workgroup kernel on nb
+//   devptr    hipHostGetDevicePointer of a mapped host block
 #include <hip/hip_runtime.h>
 #include <chrono>
 #include <cstdio>
@@ -58,6 +62,26 @@ int main() {
     while (hipStreamQuery(0) == hipErrorNotReady) {
     }
   });
+  hipDeviceSynchronize();
+  auto cost = [&](const char *name, auto body) {
+    for (int i = 0; i < 100; i++) body();
+    hipDeviceSynchronize();
+    double tot = 0;
+    for (int i = 0; i < iters; i++) {
+      const auto t0 = std::chrono::steady_clock::now();
+      body();
+      tot += std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0).count();
+      if ((i & 63) == 63) hipDeviceSynchronize();
+    }
+    printf("%-10s %7.2f us per call (host)\n", name, tot / iters);
+  };
+  int64_t *hb = nullptr, *db = nullptr;
+  hipHostMalloc((void **)&hb, 64, hipHostMallocMapped);
+  cost("query0", [&] { (void)hipStreamQuery(0); });
+  cost("queryNB", [&] { (void)hipStreamQuery(nb); });
+  cost("record", [&] { hipEventRecord(done, nb); });
+  cost("launch64", [&] { hipLaunchKernelGGL(k_add, dim3(64), dim3(256), 0, nb, a, b, n); });
+  cost("devptr", [&] { hipHostGetDevicePointer((void **)&db, hb, 0); });
   hipDeviceSynchronize();
   return 0;
 }

@@ -148,9 +148,9 @@ struct SignalArgs { uint64_t *peer_flag[MAXR]; int n; uint64_t value; const int 
 __global__ void k_signal(SignalArgs a) {
   const int j = threadIdx.x;
   if (poisoned(a.poison)) return;   // a wait before this one timed out: tell no peer anything
-  __threadfence_system();  // everything this stream wrote is visible first
+  __threadfence_system();  // everything this stream wrote is visible first (the fence is the release)
   if (j < a.n && a.peer_flag[j])
-    __hip_atomic_store(a.peer_flag[j], a.value, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+    __hip_atomic_store(a.peer_flag[j], a.value, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
 // Waits until flags[j] >= value for every j in `mask`; a timeout raises the

@@ -267,8 +267,8 @@ __global__ void __launch_bounds__(kOSB) k_oneshot(OneShotArgs a) {
   __threadfence_system();
   __syncthreads();
   // (3) READY(me, w) at every peer; (4) wait READY(p, w) from every peer
-  if (t < a.n && t != a.rank) {
-    __hip_atomic_store(a.peer_ready[t] + w, a.gen, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+  if (t < a.n && t != a.rank) {   // (the system fence above is the release)
+    __hip_atomic_store(a.peer_ready[t] + w, a.gen, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     os_spin(a.my_ready + (size_t)t * OSWG + w, a.gen, a.timeout_ticks, a.err, a.poison);
   }
   __syncthreads();
@@ -292,7 +292,7 @@ __global__ void __launch_bounds__(kOSB) k_oneshot(OneShotArgs a) {
     if (old == a.counter_last) {
       __threadfence_system();
       for (int p = 0; p < a.n; p++)
-        if (p != a.rank) __hip_atomic_store(a.peer_done[p], a.gen, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+        if (p != a.rank) __hip_atomic_store(a.peer_done[p], a.gen, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     }
   }
 }

@@ -52,14 +52,20 @@ namespace mx {
 
 constexpr int kP2PThreads = 256;
 
+// Memory ordering of the channel: a counter moves with a relaxed
+// system-scope store after the data it covers was fenced (one system fence
+// per chunk or envelope), and a wait spins with relaxed loads and takes one
+// acquire fence when it succeeds.  Release / acquire atomics in the loops
+// themselves cost an L2 write-back / invalidate per access on gfx950.
 __device__ __forceinline__ bool p2p_wait_ge(const uint64_t *f, uint64_t v, uint64_t t0, uint64_t tmo, int *err) {
-  while (__hip_atomic_load(f, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) < v) {
+  while (__hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) < v) {
     __builtin_amdgcn_s_sleep(2);
     if (wall_clock64() - t0 > tmo) {
       __hip_atomic_store(err, MX_ERR_TIMEOUT, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
       return false;
     }
   }
+  __atomic_thread_fence(__ATOMIC_ACQUIRE);
   return true;
 }
 
@@ -82,9 +88,14 @@ __device__ __forceinline__ void p2p_copy(char *dst, const char *src, uint64_t le
   }
 }
 
-// stripe of lane l: 16-byte multiples, the last lanes short or empty
+// stripe of lane l: 16-byte multiples of at least kMinStripe, the last
+// lanes short or empty -- a small message moves in one or a few lanes (each
+// lane with data pays a drained / filled handshake per chunk; 4 KiB spread
+// over all 64 lanes cost 9 us more per hop than 8 B in one)
+constexpr uint64_t kMinStripe = 16 << 10;
 __device__ __forceinline__ void p2p_lane(uint64_t bytes, int l, uint64_t *lo, uint64_t *hi) {
-  const uint64_t stripe = ((bytes + P2P_L - 1) / P2P_L + 15) & ~(uint64_t)15;
+  uint64_t stripe = ((bytes + P2P_L - 1) / P2P_L + 15) & ~(uint64_t)15;
+  if (stripe < kMinStripe) stripe = kMinStripe;
   *lo = std::min<uint64_t>(bytes, (uint64_t)l * stripe);
   *hi = std::min<uint64_t>(bytes, *lo + stripe);
 }
@@ -102,15 +113,16 @@ struct P2PDone {
   int64_t *done;         // mapped host word, or null
 };
 
-__device__ __forceinline__ void lane_finished(const P2PDone &f) {
+// `wrote`: this lane stored user data without a fence after it (a receive
+// lane with data): make it visible device-wide before counting out -- work
+// the host launches once `done` is seen may run on any XCD.  Send lanes
+// fenced every chunk already; lanes without data have nothing to publish.
+__device__ __forceinline__ void lane_finished(const P2PDone &f, bool wrote) {
   __syncthreads();
   if (threadIdx.x == 0) {
-    __threadfence_system();
+    if (wrote) __threadfence();
     const uint64_t old = __hip_atomic_fetch_add(f.lanes, (uint64_t)1, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
-    if (old + 1 == f.target && f.done) {
-      __threadfence_system();
-      __hip_atomic_store(f.done, (int64_t)1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
-    }
+    if (old + 1 == f.target && f.done) __hip_atomic_store(f.done, (int64_t)1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
   }
 }
 
@@ -134,7 +146,7 @@ struct P2PSendArgs {
 
 __global__ void __launch_bounds__(kP2PThreads) k_p2p_send(P2PSendArgs a) {
   send_body(a);
-  lane_finished(a.fin);
+  lane_finished(a.fin, false);
 }
 
 __device__ __forceinline__ void send_body(const P2PSendArgs &a) {
@@ -159,7 +171,7 @@ __device__ __forceinline__ void send_body(const P2PSendArgs &a) {
       h[0] = a.bytes;
       h[1] = (uint64_t)a.tag;
       __threadfence_system();
-      __hip_atomic_store(a.posted, m + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+      __hip_atomic_store(a.posted, m + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
       a.st->msgs = m + 1;
     }
   }
@@ -176,7 +188,7 @@ __device__ __forceinline__ void send_body(const P2PSendArgs &a) {
     p2p_copy(slot, a.buf + pos, len);
     __threadfence_system();   // my stores reach the peer before the counter moves
     __syncthreads();
-    if (threadIdx.x == 0) __hip_atomic_store(a.filled + l, k, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+    if (threadIdx.x == 0) __hip_atomic_store(a.filled + l, k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
   }
   if (threadIdx.x == 0) a.st->lane_chunks[l] = k;
 }
@@ -229,14 +241,15 @@ __global__ void k_p2p_pick(const uint64_t *flag0, const P2PRecvState *st0, int n
   }
 }
 
-__device__ __forceinline__ void recv_body(const P2PRecvArgs &a);
+__device__ __forceinline__ bool recv_body(const P2PRecvArgs &a);
 
 __global__ void __launch_bounds__(kP2PThreads) k_p2p_recv(P2PRecvArgs a) {
-  recv_body(a);
-  lane_finished(a.fin);
+  const bool wrote = recv_body(a);
+  lane_finished(a.fin, wrote);
 }
 
-__device__ __forceinline__ void recv_body(const P2PRecvArgs &a) {
+// returns whether this lane stored user data
+__device__ __forceinline__ bool recv_body(const P2PRecvArgs &a) {
   const int l = blockIdx.x;
   const uint64_t t0 = wall_clock64();
   __shared__ int ok;
@@ -248,7 +261,7 @@ __device__ __forceinline__ void recv_body(const P2PRecvArgs &a) {
   P2PRecvState *st = a.st;
   if (a.any) {
     const int p = (int)__hip_atomic_load(&a.status[3], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM);
-    if (p < 0) return;   // the pick timed out (error already raised)
+    if (p < 0) return false;   // the pick timed out (error already raised)
     box = a.box0 + (size_t)p * P2P_BOX;
     posted = a.flag0 + P2P_POSTED + p;
     filled = a.flag0 + P2P_FILLED + (size_t)p * P2P_L;
@@ -263,12 +276,12 @@ __device__ __forceinline__ void recv_body(const P2PRecvArgs &a) {
       const volatile uint64_t *h = reinterpret_cast<const volatile uint64_t *>(box + (m % P2P_H) * P2P_HDR);
       s_bytes = h[0];
       s_tag = (int64_t)h[1];
-      __hip_atomic_store(seen + l, m + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+      __hip_atomic_store(seen + l, m + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
       st->lane_msgs[l] = m + 1;
     }
   }
   __syncthreads();
-  if (!ok) return;
+  if (!ok) return false;
   const uint64_t bytes = s_bytes;
   uint64_t lo, hi;
   p2p_lane(bytes, l, &lo, &hi);
@@ -278,11 +291,11 @@ __device__ __forceinline__ void recv_body(const P2PRecvArgs &a) {
     k++;
     if (threadIdx.x == 0) ok = p2p_wait_ge(filled + l, k, t0, a.timeout_ticks, a.err);
     __syncthreads();
-    if (!ok) return;
+    if (!ok) return pos > lo;
     const char *slot = box + 4096 + ((size_t)l * P2P_S + (size_t)((k - 1) % P2P_S)) * P2P_C;
     if (pos < a.cap) p2p_copy(a.buf + pos, slot, std::min<uint64_t>(len, a.cap - pos));
     __syncthreads();          // every load of the slot has returned
-    if (threadIdx.x == 0) __hip_atomic_store(drained + l, k, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+    if (threadIdx.x == 0) __hip_atomic_store(drained + l, k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
   }
   if (threadIdx.x == 0) {
     st->lane_chunks[l] = k;
@@ -293,6 +306,7 @@ __device__ __forceinline__ void recv_body(const P2PRecvArgs &a) {
       __threadfence_system();
     }
   }
+  return lo < hi && lo < a.cap;
 }
 
 int p2p_setup(mx_comm *c) {
