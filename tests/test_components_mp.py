@@ -482,6 +482,97 @@ def test_mixed_host_and_device_buffers_take_one_protocol(n):
     assert got[0]["bcast_gaps"], "bcast into a vector layout wrote into its gaps"
 
 
+# ---------------------------------------------------------------------------
+# non-contiguous DEVICE buffers: the device convertor, not a host round trip
+# ---------------------------------------------------------------------------
+def _vec_positions(nelem):
+    """element positions (in ints) of MPI_Type_vector(4, 3, 5, MPI_INT) x nelem"""
+    return (np.arange(nelem)[:, None, None] * 18 + np.arange(4)[None, :, None] * 5
+            + np.arange(3)[None, None, :]).reshape(-1)
+
+
+def _noncontig_worker(rank, n, port, q):
+    """Every rank passes DEVICE buffers laid out as MPI_Type_vector(4, 3, 5,
+    MPI_INT) for allgather (send and receive side) and bcast.  coll/mi355x
+    packs / unpacks them with the device convertor built from the datatype's
+    committed description (host table dtype_desc) -- or, with
+    MXH_NO_DTYPE_DESC set, through the host convertor: both must give the
+    same bytes and leave the gaps alone."""
+    try:
+        import torch
+        import torch.distributed as dist
+        import minihost
+        import mxompi
+        dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=n)
+
+        @minihost.AG
+        def ag(send, recv, nbytes, ctx):
+            out = [None] * n
+            dist.all_gather_object(out, ctypes.string_at(send, nbytes))
+            blob = b"".join(out)
+            ctypes.memmove(recv, blob, len(blob))
+            return 0
+
+        torch.cuda.set_device(0)
+        mxompi.init(0)
+        H = minihost.host(with_components=True)
+        comm = H.mxh_comm_create(rank, n, ag, None)
+        i32 = minihost.dtype(H, "MPI_INT")
+        vec = H.mxh_dtype_vector(4, 3, 5, i32)
+        assert vec
+        res = {}
+        pos = _vec_positions(10)
+        mine = np.arange(120, dtype=np.int32) + 1000 * rank
+        lay = np.full(180, -1, np.int32)
+        lay[pos] = mine
+        S = torch.from_numpy(lay).cuda()
+        G = torch.full((180 * n,), -7, dtype=torch.int32, device="cuda")
+        assert H.mxh_allgather(S.data_ptr(), 10, vec, G.data_ptr(), 10, vec, comm) == 0
+        res["allgather"] = G.cpu().numpy().tobytes()
+        B = torch.from_numpy(lay).cuda() if rank == n - 1 else torch.full((180,), -1, dtype=torch.int32,
+                                                                            device="cuda")
+        assert H.mxh_bcast(B.data_ptr(), 10, vec, n - 1, comm) == 0
+        res["bcast"] = B.cpu().numpy().tobytes()
+        res["owners"] = {s: H.mxh_comm_slot_owner(comm, s.encode()).decode() for s in ("allgather", "bcast")}
+        torch.cuda.synchronize()
+        H.mxh_comm_free(comm)
+        dist.destroy_process_group()
+        q.put((rank, "ok", res))
+    except Exception:  # noqa: BLE001
+        import traceback
+        q.put((rank, "err", traceback.format_exc()))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("desc", [True, False], ids=["device_convertor", "host_convertor"])
+def test_noncontiguous_device_buffers(desc):
+    import torch
+    if not torch.cuda.is_available():
+        pytest.skip("needs a GPU")
+    os.environ["HSA_ENABLE_IPC_MODE_LEGACY"] = "0"
+    if desc:
+        os.environ.pop("MXH_NO_DTYPE_DESC", None)
+    else:
+        os.environ["MXH_NO_DTYPE_DESC"] = "1"
+    try:
+        n = 2
+        got = _run_fn(_noncontig_worker, n)
+    finally:
+        os.environ.pop("MXH_NO_DTYPE_DESC", None)
+    pos = _vec_positions(10)
+    for r in range(n):
+        assert got[r]["owners"] == {"allgather": "mi355x", "bcast": "mi355x"}
+        g = np.frombuffer(got[r]["allgather"], np.int32)
+        exp = np.full(180 * n, -7, np.int32)
+        for p in range(n):
+            exp[180 * p + pos] = np.arange(120, dtype=np.int32) + 1000 * p
+        np.testing.assert_array_equal(g, exp)              # data in place, gaps untouched
+        b = np.frombuffer(got[r]["bcast"], np.int32)
+        expb = np.full(180, -1, np.int32)
+        expb[pos] = np.arange(120, dtype=np.int32) + 1000 * (n - 1)
+        np.testing.assert_array_equal(b, expb)
+
+
 def _overlap_worker(rank, n, port, q):
     """MPI-legal ordering that a collective spinning on the legacy default
     stream would deadlock: rank 0 posts MPI_Iallreduce and then needs a

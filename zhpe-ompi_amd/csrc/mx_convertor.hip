@@ -679,7 +679,7 @@ struct PieceArgs {
   uint64_t S;
   int64_t ext;
   char *user;
-  const char *packed;
+  char *packed;            // UNPACK reads it, PACK writes it
   uint64_t offset, len;
   uint64_t P0, P1;         // pieces overlapping [offset, offset + len)
   uint32_t K;              // pieces per tile (multiple of kCB)
@@ -749,6 +749,91 @@ __global__ void __launch_bounds__(kCB) k_unpack_piece(PieceArgs a) {
       j += a.dj;
       inst += a.dinst;
       if (j >= a.npi) { j -= a.npi; inst++; }
+    }
+  }
+}
+
+// PACK, pieces: the mirror of k_unpack_piece for layouts the byte map does
+// not take (instances whose map exceeds the LDS budget, sparse layouts that
+// would stage mostly gaps).  Lane l loads piece l straight from user memory
+// with one aligned load of the piece's width -- a wave reads 64 consecutive
+// pieces, so only lines holding data are fetched -- and drops its bytes into
+// the tile's packed image in LDS (whole words when the stream offset allows,
+// bytes otherwise); the image leaves with 16-byte stores, the two edge
+// granules a neighbouring tile shares byte by byte.
+__device__ __forceinline__ void piece_load(const char *u, int lg, uint32_t &v0, uint32_t &v1, uint32_t &v2,
+                                           uint32_t &v3) {
+  v1 = v2 = v3 = 0;
+  switch (lg) {
+    case 0: v0 = *reinterpret_cast<const uint8_t *>(u); break;
+    case 1: v0 = *reinterpret_cast<const uint16_t *>(u); break;
+    case 2: v0 = *reinterpret_cast<const uint32_t *>(u); break;
+    case 3: { const uint2 t = *reinterpret_cast<const uint2 *>(u); v0 = t.x; v1 = t.y; break; }
+    default: { const uint4 t = *reinterpret_cast<const uint4 *>(u); v0 = t.x; v1 = t.y; v2 = t.z; v3 = t.w; break; }
+  }
+}
+
+__global__ void __launch_bounds__(kCB) k_pack_piece(PieceArgs a) {
+  extern __shared__ __align__(16) char smem[];
+  char *stage = smem;                                        // kPieceStage + 48
+  DPiece *stbl = reinterpret_cast<DPiece *>(smem + kPieceStage + 48);
+  const DPiece *tbl = a.pieces;
+  if (a.tbl_lds) {
+    for (uint32_t i = threadIdx.x; i < a.npi; i += kCB) stbl[i] = a.pieces[i];
+    tbl = stbl;
+  }
+  const uint64_t wend = a.offset + a.len;
+  for (uint64_t t = blockIdx.x; t < a.ntiles; t += gridDim.x) {
+    const uint64_t Pa = a.P0 + t * a.K;
+    const uint64_t Pb = Pa + a.K < a.P1 ? Pa + a.K : a.P1;
+    __syncthreads();                                          // table staged / previous tile stored
+    const uint64_t ia = udiv(Pa, a.mnpi), ib = udiv(Pb - 1, a.mnpi);
+    const DPiece fa = tbl[Pa - ia * a.npi], fb = tbl[Pb - 1 - ib * a.npi];
+    uint64_t sa = ia * a.S + fa.soff, sb = ib * a.S + fb.soff + (1u << fb.lg);
+    sa = sa < a.offset ? a.offset : sa;
+    sb = sb < wend ? sb : wend;
+    const uintptr_t gA = (uintptr_t)(a.packed + (sa - a.offset)), gB = (uintptr_t)(a.packed + (sb - a.offset));
+    const uintptr_t lo = gA & ~(uintptr_t)15;
+    uint64_t P = Pa + threadIdx.x;
+    uint64_t inst = udiv(P, a.mnpi);
+    uint32_t j = (uint32_t)(P - inst * a.npi);
+    for (; P < Pb; P += kCB) {
+      const DPiece pc = tbl[j];
+      const uint64_t sp = inst * a.S + pc.soff;
+      const uint32_t n = 1u << pc.lg;
+      const char *u = a.user + (int64_t)inst * a.ext + pc.uoff;
+      const int64_t li = (int64_t)((uintptr_t)(a.packed + (sp - a.offset)) - lo);
+      if (sp >= a.offset && sp + n <= wend) {
+        uint32_t v[4];
+        piece_load(u, pc.lg, v[0], v[1], v[2], v[3]);
+        if (n >= 4 && (li & 3) == 0) {
+          uint32_t *w = reinterpret_cast<uint32_t *>(stage + li);
+#pragma unroll
+          for (int k = 0; k < 4; k++)
+            if ((uint32_t)k * 4 < n) w[k] = v[k];
+        } else {
+#pragma unroll
+          for (int i = 0; i < 16; i++)
+            if ((uint32_t)i < n) stage[li + i] = (char)(v[i >> 2] >> (8 * (i & 3)));
+        }
+      } else {                                                // piece cut by the window
+        for (uint32_t i = 0; i < n; i++)
+          if (sp + i >= a.offset && sp + i < wend) stage[li + i] = u[i];
+      }
+      j += a.dj;
+      inst += a.dinst;
+      if (j >= a.npi) { j -= a.npi; inst++; }
+    }
+    __syncthreads();
+    const uint32_t ng = (uint32_t)((((gB + 15) & ~(uintptr_t)15) - lo) / 16);
+    for (uint32_t g = threadIdx.x; g < ng; g += kCB) {
+      const uintptr_t ga = lo + (uintptr_t)g * 16;
+      if (ga >= gA && ga + 16 <= gB) {
+        *reinterpret_cast<uint4 *>(ga) = reinterpret_cast<const uint4 *>(stage)[g];
+      } else {
+        for (int i = 0; i < 16; i++)
+          if (ga + i >= gA && ga + i < gB) reinterpret_cast<char *>(ga)[i] = stage[g * 16 + i];
+      }
     }
   }
 }
@@ -1146,6 +1231,26 @@ static bool conv_bmap_enabled() {
   return on != 0;
 }
 
+// MX_CONV_BMAP_PACK=0 sends PACK of small dense instances to the piece
+// kernel instead of the byte-map kernel (A/B switch).
+static bool conv_bmap_pack_enabled() {
+  static const int on = [] {
+    const char *e = getenv("MX_CONV_BMAP_PACK");
+    return (e && *e == '0') ? 0 : 1;
+  }();
+  return on != 0;
+}
+
+// MX_CONV_PPACK=0 keeps PACK of layouts the byte map does not take on the
+// run-walking kernels instead of the piece kernel (A/B switch).
+static bool conv_ppack_enabled() {
+  static const int on = [] {
+    const char *e = getenv("MX_CONV_PPACK");
+    return (e && *e == '0') ? 0 : 1;
+  }();
+  return on != 0;
+}
+
 // MX_CONV_BMAP_DW=0 gives each lane of the byte-map PACK kernel 16 packed
 // bytes (one 16-byte store) instead of one dword per step (A/B switch).
 static bool conv_bmap_dw() {
@@ -1226,7 +1331,7 @@ static int convert(const mx_ddt_t *d, size_t count, char *user, char *packed, si
   }
   // small irregular instances: byte-map PACK / piece UNPACK (see the kernels)
   if (!d->bmap.empty() && conv_bmap_enabled()) {
-    if (PACK && d->bmap_T && (((uintptr_t)packed - offset) & 15) == 0) {
+    if (PACK && d->bmap_T && (((uintptr_t)packed - offset) & 15) == 0 && conv_bmap_pack_enabled()) {
       BmapArgs b;
       b.map = d->map_dev;
       b.mono = d->monotonic;
@@ -1255,7 +1360,7 @@ static int convert(const mx_ddt_t *d, size_t count, char *user, char *packed, si
 #undef MX_BMAP_LAUNCH
       return mx_check_launch();
     }
-    if (!PACK) {
+    if (!PACK || conv_ppack_enabled()) {
       mx_ddt *dm = const_cast<mx_ddt *>(d);
       mx_ddt::PieceTab *pt;
       {
@@ -1285,7 +1390,8 @@ static int convert(const mx_ddt_t *d, size_t count, char *user, char *packed, si
         const size_t lds = kPieceStage + 48 + (p.tbl_lds ? npi * sizeof(DPiece) : 0);
         const uint64_t per_cu = std::max<uint64_t>(1, std::min<uint64_t>(8, (160 * 1024) / lds));
         const uint64_t grid = std::min<uint64_t>(p.ntiles, (uint64_t)g_num_cus * per_cu);
-        hipLaunchKernelGGL(k_unpack_piece, dim3((unsigned)grid), dim3(kCB), lds, s, p);
+        if (PACK) hipLaunchKernelGGL(k_pack_piece, dim3((unsigned)grid), dim3(kCB), lds, s, p);
+        else hipLaunchKernelGGL(k_unpack_piece, dim3((unsigned)grid), dim3(kCB), lds, s, p);
         return mx_check_launch();
       }
     }

@@ -53,12 +53,26 @@
 #include <string.h>
 
 #include "mx_coll.h"
+#include "mx_convertor.h"
 #include "mx_kernels.h"
 #include "mx_ompi_abi.h"
 
 /* device scratch a staged buffer lives in (grown on demand, kept) */
 typedef struct { void *p; size_t bytes; } mx_scratch_t;
 enum { SCR_IN, SCR_OUT, SCR_N };
+
+/* device convertor handles of the datatypes this communicator moved, keyed
+ * by the datatype AND a copy of its committed records (a freed datatype's
+ * address may come back as another type) */
+typedef struct {
+    struct ompi_datatype_t *dt;
+    void *recs;
+    size_t nrec, size;
+    ptrdiff_t lb, ub;
+    mx_ddt_t *h;
+    unsigned long used;
+} mx_ddt_slot_t;
+#define MX_DDT_CACHE 4
 
 typedef struct {
     mca_coll_base_module_t super;
@@ -68,6 +82,8 @@ typedef struct {
     void *stream;         /* blocking collectives: module-owned stream ordered with the default one */
     void *nb_stream;      /* nonblocking / persistent requests: non-blocking stream */
     mx_scratch_t scratch[SCR_N];
+    mx_ddt_slot_t ddt[MX_DDT_CACHE];
+    unsigned long ddt_clock;
     /* delegation targets (the slots we replaced) */
     mca_coll_base_module_allreduce_fn_t prev_allreduce;
     mca_coll_base_module_t *prev_allreduce_module;
@@ -129,6 +145,10 @@ static void coll_module_destruct(mx_coll_module_t *m)
 {
     if (m->mx) mx_comm_destroy(m->mx);
     for (int k = 0; k < SCR_N; k++) mx_free(m->scratch[k].p);
+    for (int k = 0; k < MX_DDT_CACHE; k++) {
+        if (m->ddt[k].h) mx_ddt_destroy(m->ddt[k].h);
+        free(m->ddt[k].recs);
+    }
     if (m->stream) mx_stream_destroy(m->stream);
     if (m->nb_stream) mx_stream_destroy(m->nb_stream);
     if (m->prev_allreduce_module) MX_OBJ_RELEASE(m->prev_allreduce_module);
@@ -216,14 +236,65 @@ typedef struct {
     int count, contiguous;
 } xbuf_t;
 
-/* contiguous bytes [0, bytes) of a non-contiguous layout <-> packed */
+/* the device convertor for dt (mx_ddt_create from the committed records),
+ * or NULL when the host cannot describe it */
+static mx_ddt_t *ddt_for(mx_coll_module_t *m, struct ompi_datatype_t *dt)
+{
+    const void *recs;
+    size_t nrec, size;
+    ptrdiff_t lb, ub;
+    if (!mx_ompi_host->dtype_desc || mx_ompi_host->dtype_desc(dt, &recs, &nrec, &size, &lb, &ub) != OMPI_SUCCESS ||
+        !nrec)
+        return NULL;
+    int victim = 0;
+    for (int k = 0; k < MX_DDT_CACHE; k++) {
+        mx_ddt_slot_t *e = &m->ddt[k];
+        if (e->h && e->dt == dt && e->nrec == nrec && e->size == size && e->lb == lb && e->ub == ub &&
+            !memcmp(e->recs, recs, nrec * 32)) {
+            e->used = ++m->ddt_clock;
+            return e->h;
+        }
+        if (e->used < m->ddt[victim].used) victim = k;
+    }
+    mx_ddt_slot_t *e = &m->ddt[victim];
+    if (e->h) mx_ddt_destroy(e->h);
+    free(e->recs);
+    memset(e, 0, sizeof *e);
+    if (!(e->recs = malloc(nrec * 32))) return NULL;
+    memcpy(e->recs, recs, nrec * 32);
+    if (mx_ddt_create(recs, nrec, NULL, size, (int64_t)lb, (int64_t)ub, &e->h) != MX_SUCCESS) {
+        free(e->recs);
+        memset(e, 0, sizeof *e);
+        return NULL;
+    }
+    e->dt = dt;
+    e->nrec = nrec;
+    e->size = size;
+    e->lb = lb;
+    e->ub = ub;
+    e->used = ++m->ddt_clock;
+    return e->h;
+}
+
+/* contiguous bytes [0, bytes) of a non-contiguous layout <-> packed: on the
+ * device for a device buffer whose datatype the host describes (the reference
+ * would walk it with one cuMemcpy per block, opal_datatype_cuda.c:121-140),
+ * else through the host convertor */
 static int xfer_packed(mx_coll_module_t *m, const xbuf_t *x, void *packed_dev, int to_device)
 {
     ptrdiff_t lo = 0, hi = 0;
+    const int on_dev = mx_is_device_ptr(x->user) == 1;
+    if (on_dev) {
+        mx_ddt_t *h = ddt_for(m, x->dt);
+        if (h) {
+            int rc = to_device ? mx_pack(h, (size_t)x->count, x->user, packed_dev, 0, x->bytes, m->stream)
+                               : mx_unpack(h, (size_t)x->count, x->user, packed_dev, 0, x->bytes, m->stream);
+            return rc ? rc : mx_stream_sync(m->stream);
+        }
+    }
     if (!mx_ompi_host->dtype_pack || !mx_ompi_host->dtype_unpack || !mx_ompi_host->dtype_span ||
         mx_ompi_host->dtype_span(x->dt, x->count, &lo, &hi) != OMPI_SUCCESS || hi < lo)
         return MX_ERR_UNSUPPORTED;
-    const int on_dev = mx_is_device_ptr(x->user) == 1;
     char *span = NULL, *packed = malloc(x->bytes ? x->bytes : 1);
     char *user = (char *)x->user;
     int rc = packed ? MX_SUCCESS : MX_ERR_NOMEM;

@@ -42,9 +42,10 @@ struct ompi_datatype_t {
     /* MPI_Type_vector of the base type (vcount blocks of vblen, stride
      * vstride elements); vcount == 0: contiguous */
     int vcount, vblen, vstride;
+    void *desc;      /* committed description records, built on first use */
 };
 
-#define DT(nm, id, slot, sz) {nm, id, slot, sz, 1, NULL, 0, 0, 0, 0}
+#define DT(nm, id, slot, sz) {nm, id, slot, sz, 1, NULL, 0, 0, 0, 0, NULL}
 static struct ompi_datatype_t g_dtypes[] = {
     DT("MPI_INT8_T", 0x01, 0, 1), DT("MPI_UINT8_T", 0x02, 1, 1), DT("MPI_INT16_T", 0x03, 2, 2),
     DT("MPI_UINT16_T", 0x04, 3, 2), DT("MPI_INT32_T", 0x05, 4, 4), DT("MPI_UINT32_T", 0x06, 5, 4),
@@ -270,6 +271,38 @@ static int dtype_span(struct ompi_datatype_t *d, int count, ptrdiff_t *lo, ptrdi
 {
     *lo = 0;
     *hi = count > 0 ? (ptrdiff_t)((size_t)count * dtype_extent(d)) : 0;
+    return OMPI_SUCCESS;
+}
+/* committed description of a mini-host datatype, in the reference's record
+ * format (opal_datatype_internal.h:146-196): one ELEM of the raw bytes
+ * (OPAL_UINT1 -- pack / unpack on a homogeneous node only move bytes) and
+ * the closing END_LOOP.  Records live with the datatype. */
+#define MXH_OPAL_UINT1 9
+#define MXH_OPAL_END_LOOP 1
+#define MXH_DT_DATA 0x0100
+struct mxh_rec { uint16_t flags, type; uint32_t count; uint64_t blocklen; int64_t extent; int64_t disp; };
+static int dtype_desc(struct ompi_datatype_t *d, const void **recs, size_t *nrec, size_t *size, ptrdiff_t *lb,
+                      ptrdiff_t *ub)
+{
+    if (!d->desc) {
+        struct mxh_rec *r = calloc(2, sizeof *r);
+        if (!r) return OMPI_ERROR;
+        const size_t bs = d->vcount ? d->base->size : d->size;
+        r[0].flags = MXH_DT_DATA;
+        r[0].type = MXH_OPAL_UINT1;
+        r[0].count = d->vcount ? (uint32_t)d->vcount : 1;
+        r[0].blocklen = d->vcount ? (uint64_t)d->vblen * bs : d->size;
+        r[0].extent = d->vcount ? (int64_t)d->vstride * (int64_t)bs : (int64_t)d->size;
+        r[1].type = MXH_OPAL_END_LOOP;
+        r[1].count = 1;
+        r[1].extent = (int64_t)d->size;
+        d->desc = r;
+    }
+    *recs = d->desc;
+    *nrec = 2;
+    *size = d->size;
+    *lb = 0;
+    *ub = (ptrdiff_t)dtype_extent(d);
     return OMPI_SUCCESS;
 }
 static int comm_rank(struct ompi_communicator_t *c) { return c->rank; }
@@ -782,6 +815,7 @@ int mxh_init(const char *component_lib, mxh_reducer_t base, mxh_pattern_t patter
     g_host.dtype_pack = dtype_pack;
     g_host.dtype_unpack = dtype_unpack;
     g_host.dtype_span = dtype_span;
+    g_host.dtype_desc = getenv("MXH_NO_DTYPE_DESC") ? NULL : dtype_desc;
     g_nprogress = 0;
     g_op_comp = NULL;
     g_coll_comp = NULL;

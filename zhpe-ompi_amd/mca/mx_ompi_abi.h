@@ -381,6 +381,14 @@ typedef struct mx_ompi_host {
     int (*dtype_unpack)(struct ompi_datatype_t *dt, int count, const void *packed, void *user);
     /* bytes [*lo, *hi) relative to the buffer that count elements touch */
     int (*dtype_span)(struct ompi_datatype_t *dt, int count, ptrdiff_t *lo, ptrdiff_t *hi);
+    /* the committed description of dt: the 32-byte dt_elem_desc records the
+     * convertor walks (opal_datatype_t opt_desc.desc, used + 1 records with
+     * the closing END_LOOP, opal_datatype.h:126 / opal_datatype_internal.h:
+     * 146-196) with size, lb and ub -- the input of mx_ddt_create, so a
+     * non-contiguous DEVICE buffer is packed / unpacked on the device.  NULL
+     * (or an error return): device spans go through the host as above. */
+    int (*dtype_desc)(struct ompi_datatype_t *dt, const void **recs, size_t *nrec, size_t *size, ptrdiff_t *lb,
+                      ptrdiff_t *ub);
 } mx_ompi_host_t;
 
 /* Set by the host before component queries. */

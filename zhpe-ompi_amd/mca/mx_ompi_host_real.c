@@ -14,6 +14,8 @@
  *                                ompi_datatype_is_contiguous_memory_layout
  *   dtype_pack / _unpack / _span opal_convertor_pack / _unpack on host memory
  *                                (opal_convertor.c:218-325), opal_datatype_span
+ *   dtype_desc                   dt->super.opt_desc (or desc): the committed
+ *                                records the device convertor is built from
  *   op_index / op_flags / fns    op->o_f_to_c_index, op->o_flags,
  *                                op->o_func.intrinsic, op->o_3buff_intrinsic
  *   comm_coll_fn                 comm->c_coll->coll_<slot> and its module
@@ -98,6 +100,22 @@ static int h_span(struct ompi_datatype_t *dt, int count, ptrdiff_t *lo, ptrdiff_
     const ptrdiff_t span = opal_datatype_span(&dt->super, count, &gap);
     *lo = gap;
     *hi = gap + span;
+    return OMPI_SUCCESS;
+}
+
+/* the committed description (opal_datatype.h:126): the optimized records
+ * when the datatype has them, else the plain ones, plus the closing END_LOOP */
+static int h_desc(struct ompi_datatype_t *dt, const void **recs, size_t *nrec, size_t *size, ptrdiff_t *lb,
+                  ptrdiff_t *ub)
+{
+    const opal_datatype_t *d = &dt->super;
+    const dt_type_desc_t *td = d->opt_desc.used ? &d->opt_desc : &d->desc;
+    if (!td->desc || !td->used) return OMPI_ERROR;
+    *recs = td->desc;
+    *nrec = (size_t)td->used + 1;
+    *size = d->size;
+    *lb = d->lb;
+    *ub = d->ub;
     return OMPI_SUCCESS;
 }
 
@@ -231,5 +249,6 @@ int mx_ompi_host_real_register(void)
     real_host.dtype_pack = h_pack;
     real_host.dtype_unpack = h_unpack;
     real_host.dtype_span = h_span;
+    real_host.dtype_desc = h_desc;
     return mx_ompi_set_host(&real_host);
 }
