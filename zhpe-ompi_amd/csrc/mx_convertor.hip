@@ -858,6 +858,7 @@ struct mx_ddt {
   int map16 = 0;
   int64_t umin = 0, uspan = 0;
   uint64_t bmap_T = 0;             // stream bytes per PACK tile (0: no PACK kernel)
+  bool piece_pack = false;         // PACK takes the piece kernel (wide word-aligned pieces, build_bmap)
   // piece tables per user-origin alignment (address mod 16), built on first
   // use: UNPACK kernel k_unpack_piece
   struct PieceTab {
@@ -993,6 +994,33 @@ static uint64_t gcd64(uint64_t a, uint64_t b) {
 }
 static uint64_t absg(int64_t v) { return v < 0 ? (uint64_t)(-v) : (uint64_t)v; }
 
+// Pieces of one instance for a user origin at address `al` mod 16: maximal
+// contiguous user runs in stream order, cut into naturally aligned
+// 1/2/4/8/16-byte pieces (aligned for every instance: the width also
+// divides the extent).
+static void cut_pieces(const mx_ddt *d, int al, std::vector<DPiece> &v) {
+  const uint64_t A = gcd64(16, absg(d->ub - d->lb));
+  const size_t S = d->bmap.size();
+  for (size_t b = 0; b < S;) {
+    size_t L = 1;
+    while (b + L < S && d->bmap[b + L] == d->bmap[b] + (int32_t)L) L++;
+    for (size_t pos = 0; pos < L;) {
+      const int64_t x = (int64_t)d->bmap[b] + (int64_t)pos;
+      const uint64_t addr = (uint64_t)(((al + x) % 16 + 16) % 16);
+      uint64_t w = 16;
+      while (w > 1 && (addr % w || w > L - pos || A % w)) w >>= 1;
+      DPiece pc;
+      pc.uoff = (int32_t)x;
+      pc.soff = (uint16_t)(b + pos);
+      pc.lg = (uint8_t)__builtin_ctzll(w);
+      pc.pad = 0;
+      v.push_back(pc);
+      pos += w;
+    }
+    b += L;
+  }
+}
+
 // Byte map of one instance: bmap[b] = user offset of packed byte b.  Also
 // fixes the PACK tile: the largest multiple of 256 stream bytes (<= 16 KiB)
 // whose user span, rounded out to 16 bytes, always fits kBmapSpan -- whole
@@ -1020,9 +1048,23 @@ static void build_bmap(mx_ddt *d) {
   d->umin = lo;
   d->uspan = hi - lo;
   d->map16 = d->uspan <= 65536;
-  // PACK stages whole user spans: only for dense layouts (<= 4 user bytes
-  // per packed byte; a sparse one reads mostly gaps -- ref_matrix_borders at
-  // 23: 0.83 -> 0.42 TB/s) and maps small enough for >= 3 workgroups per CU
+  // PACK kernel choice: pieces of >= 8 bytes on average that all land on
+  // whole packed words move with few wide accesses through the piece kernel;
+  // narrow or misaligned pieces go through the byte map, whose cost per
+  // byte is flat.  Measured at 1 GiB (profiles/r02/convertor_r2.txt): lower
+  // triangle (8-byte pieces) piece 3.58 vs byte map 2.28 TB/s; indexed /
+  // BLACS (4-byte) 2.66 / 2.85 vs 3.40 / 3.05; struct (misaligned) 2.46 vs
+  // 3.41; 8-byte struct types equal within 2 %.
+  {
+    std::vector<DPiece> v;
+    cut_pieces(d, 0, v);
+    bool words = true;
+    for (const DPiece &p : v) words = words && p.lg >= 2 && (p.soff & 3) == 0;
+    d->piece_pack = words && !v.empty() && S >= 8 * v.size();
+  }
+  // The byte map is staged only for dense layouts (<= 4 user bytes per
+  // packed byte; a sparse one reads mostly gaps -- ref_matrix_borders at 23:
+  // 0.83 -> 0.42 TB/s) and maps small enough for >= 3 workgroups per CU
   // (ref_upper_matrix_60's 29 KiB map: 1.32 -> 1.25 TB/s)
   if (S * (d->map16 ? 2 : 4) > kBmapLds || ext > 4 * (int64_t)S || d->uspan > 4 * (int64_t)S) return;
   // user bytes a tile of T stream bytes starting at instance byte b touches
@@ -1038,35 +1080,15 @@ static void build_bmap(mx_ddt *d) {
   d->bmap_T = T >= 256 ? T : 0;
 }
 
-// Pieces of one instance for a user origin at address `al` mod 16: maximal
-// contiguous user runs in stream order, cut into naturally aligned
-// 1/2/4/8/16-byte pieces (aligned for every instance: the width also
-// divides the extent).  Caller holds d->mu.
+// The piece table for a user origin at address `al` mod 16 (cut_pieces),
+// uploaded, with its tile size.  Caller holds d->mu.
 static mx_ddt::PieceTab *piece_tab(mx_ddt *d, int al) {
   mx_ddt::PieceTab &P = d->ptab[al];
   if (P.built) return P.built > 0 ? &P : nullptr;
   P.built = -1;
-  const uint64_t A = gcd64(16, absg(d->ub - d->lb));
   const size_t S = d->bmap.size();
   std::vector<DPiece> v;
-  for (size_t b = 0; b < S;) {
-    size_t L = 1;
-    while (b + L < S && d->bmap[b + L] == d->bmap[b] + (int32_t)L) L++;
-    for (size_t pos = 0; pos < L;) {
-      const int64_t x = (int64_t)d->bmap[b] + (int64_t)pos;
-      const uint64_t addr = (uint64_t)(((al + x) % 16 + 16) % 16);
-      uint64_t w = 16;
-      while (w > 1 && (addr % w || w > L - pos || A % w)) w >>= 1;
-      DPiece pc;
-      pc.uoff = (int32_t)x;
-      pc.soff = (uint16_t)(b + pos);
-      pc.lg = (uint8_t)__builtin_ctzll(w);
-      pc.pad = 0;
-      v.push_back(pc);
-      pos += w;
-    }
-    b += L;
-  }
+  cut_pieces(d, al, v);
   const uint32_t npi = (uint32_t)v.size();
   // pieces per tile: ~8 KiB of stream, staged bytes (+ alignment slop) <= kPieceStage
   auto window = [&](uint32_t K) {
@@ -1302,6 +1324,14 @@ static int convert(const mx_ddt_t *d, size_t count, char *user, char *packed, si
   a.len = len;
   a.pk_vec = ((uintptr_t)packed & 15) == 0;
   hipStream_t s = (hipStream_t)stream;
+  // a contiguous type (one block, extent = size): the stream is the user
+  // bytes themselves -- one copy (ref_contiguous_int2_77 unpack 2.27 TB/s
+  // through the piece kernel)
+  if (a.nruns == 1 && d->host[0].cnt1 == 1 && d->host[0].cnt2 == 1 && d->host[0].blen == d->size &&
+      a.ext == (int64_t)d->size) {
+    char *u = user + d->host[0].disp + offset;
+    return PACK ? copy_async(packed, u, len, s) : copy_async(u, packed, len, s);
+  }
   // widest unit that every piece of every granule respects: layout gcd,
   // alignment of the user origin, and the stream offset of granule 0
   uint64_t u = gcd64(d->gcd_all, ((uintptr_t)user) & 15 ? ((uintptr_t)user & 15) : 16);
@@ -1331,7 +1361,8 @@ static int convert(const mx_ddt_t *d, size_t count, char *user, char *packed, si
   }
   // small irregular instances: byte-map PACK / piece UNPACK (see the kernels)
   if (!d->bmap.empty() && conv_bmap_enabled()) {
-    if (PACK && d->bmap_T && (((uintptr_t)packed - offset) & 15) == 0 && conv_bmap_pack_enabled()) {
+    if (PACK && d->bmap_T && !d->piece_pack && (((uintptr_t)packed - offset) & 15) == 0 &&
+        conv_bmap_pack_enabled()) {
       BmapArgs b;
       b.map = d->map_dev;
       b.mono = d->monotonic;
