@@ -7,8 +7,9 @@ n processes share the one GPU.  Payload bytes must arrive unchanged for
 every size (0 bytes, sub-vector tails, several times the mailbox), every
 alignment (user pointers offset by 1..15 bytes), many messages in flight
 per pair (more than the envelope ring), a ring shift, an all-to-all, and
-sends to self; truncation and tag mismatches complete with MPI's errors and
-leave the channel usable; derived datatypes on either side match the
+sends to self; truncation completes with MPI's error and leaves the channel
+usable; tags match out of order within a pair (unexpected messages stashed
+on the device); derived datatypes on either side match the
 reference convertor's packed stream (golden vectors).
 """
 import os
@@ -89,30 +90,45 @@ def _p2p_worker(rank, n, port, q):
                 r.free()
             res["inflight"] = (st, [b.cpu().numpy().tobytes() for b in bufs])
 
-        # (4) truncation and tag mismatch complete with MPI's errors; the
-        # channel stays in step
+        # (4) truncation completes with MPI_ERR_TRUNCATE; tags match out of
+        # order within the pair (pml/ob1's matching): a receive whose tag is
+        # not the next message's stashes that message on the device and a
+        # later receive takes it, oldest first
         if rank == 0:
-            a = _dev(_data(300, 1000))
-            comm.send(a.data_ptr(), 1000, 1, tag=5)
-            comm.send(a.data_ptr(), 1000, 1, tag=5)
-            comm.send(a.data_ptr(), 1000, 1, tag=9)
+            comm.send(_dev(_data(300, 1000)).data_ptr(), 1000, 1, tag=5)
+            comm.send(_dev(_data(301, 1000)).data_ptr(), 1000, 1, tag=9)
+            comm.send(_dev(_data(302, 1000)).data_ptr(), 1000, 1, tag=5)
+            comm.send(_dev(_data(303, 2000)).data_ptr(), 2000, 1, tag=7)
+            comm.send(_dev(_data(304, 700)).data_ptr(), 700, 1, tag=8)
+            comm.send(_dev(_data(305, 300 << 10)).data_ptr(), 300 << 10, 1, tag=3)   # too big to stash
+            comm.send(_dev(_data(306, 64)).data_ptr(), 64, 1, tag=4)
         elif rank == 1:
-            d = torch.zeros(1000, dtype=torch.uint8, device="cuda")
-            errs = []
+            d = torch.zeros(2000, dtype=torch.uint8, device="cuda")
+            errs, data = [], []
             try:
                 comm.recv(d.data_ptr(), 600, 0, tag=5)
             except mxompi.MxError as e:
                 errs.append(e.rc)
-            res["trunc"] = d.cpu().numpy()[:600].tobytes()
-            try:
-                comm.recv(d.data_ptr(), 1000, 0, tag=6)
+            data.append(d.cpu().numpy()[:600].tobytes())
+            for tag in (7, 5, -1, 8):          # 7 stashes the 9 and the second 5
+                r = comm.irecv(d.data_ptr(), 2000, 0, tag=tag)
+                r.wait()
+                st = r.status()
+                r.free()
+                errs.append(st)
+                data.append(d.cpu().numpy()[:st[0]].tobytes())
+            big = torch.zeros(300 << 10, dtype=torch.uint8, device="cuda")
+            try:                               # the 300 KiB tag-3 message cannot be stashed
+                comm.recv(big.data_ptr(), 300 << 10, 0, tag=4)
             except mxompi.MxError as e:
                 errs.append(e.rc)
-            r = comm.irecv(d.data_ptr(), 1000, 0, tag=-1)
+            r = comm.irecv(d.data_ptr(), 64, 0, tag=4)
             r.wait()
             errs.append(r.status())
+            data.append(d.cpu().numpy()[:64].tobytes())
             r.free()
             res["errs"] = errs
+            res["tagdata"] = data
 
         # (5) persistent pair started three times on fresh data
         P = 1 << 20
@@ -239,8 +255,13 @@ def test_point_to_point(n):
     assert st == [(300 * 1024 + 3, k) for k in range(20)]
     for k, b in enumerate(bufs):
         assert b == _data(200 + k, 300 * 1024 + 3).tobytes(), f"in-flight message {k}"
-    assert got[1]["trunc"] == _data(300, 1000)[:600].tobytes()
-    assert got[1]["errs"] == [-9, -10, (1000, 9)], got[1]["errs"]    # MX_ERR_TRUNCATE, MX_ERR_TAG, any-tag status
+    # MX_ERR_TRUNCATE; then tag 7 (stashing 9 and 5), the stashed 5, the
+    # stashed 9 for MPI_ANY_TAG (oldest), 8; a mismatch too large to stash
+    # completes with MX_ERR_TAG and the channel goes on
+    assert got[1]["errs"] == [-9, (2000, 7), (1000, 5), (1000, 9), (700, 8), -10, (64, 4)], got[1]["errs"]
+    want = [_data(300, 1000)[:600], _data(303, 2000), _data(302, 1000), _data(301, 1000), _data(304, 700),
+            _data(306, 64)]
+    assert got[1]["tagdata"] == [w.tobytes() for w in want]
     for it, b in enumerate(got[1]["persistent"]):
         assert b == _data(400 + it, 1 << 20).tobytes(), f"persistent start {it}"
     tv = REC["vector_f64_b3_s5"]

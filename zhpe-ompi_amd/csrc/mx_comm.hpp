@@ -40,9 +40,22 @@ constexpr size_t P2P_SEEN = P2P_FILLED + (size_t)MAXR * P2P_L;
 constexpr size_t P2P_DRAINED = P2P_SEEN + (size_t)MAXR * P2P_L;
 constexpr size_t ALL_FLAG_WORDS = P2P_DRAINED + (size_t)MAXR * P2P_L;
 
+// Unexpected messages: a receive whose tag does not match the pair's next
+// envelope drains that message into a stash slot (up to P2P_STASH_N
+// messages of at most P2P_STASH_C bytes per source) and goes on to the next
+// envelope; later receives match the stash first, oldest first (MPI's
+// per-pair order among the messages a receive could match).
+constexpr int P2P_STASH_N = 8;
+constexpr size_t P2P_STASH_C = 256 << 10;
+struct P2PStashEntry { uint64_t valid; int64_t tag; uint64_t bytes; uint64_t seq; };
+
 // device-local sequence state of the channels (not shared)
 struct P2PSendState { uint64_t msgs; uint64_t lane_chunks[P2P_L]; };
-struct P2PRecvState { uint64_t lane_msgs[P2P_L]; uint64_t lane_chunks[P2P_L]; };
+struct P2PRecvState {
+  uint64_t lane_msgs[P2P_L];
+  uint64_t lane_chunks[P2P_L];
+  P2PStashEntry stash[P2P_STASH_N];   // written only by the last lane of a receive kernel
+};
 
 }  // namespace mx
 
@@ -104,6 +117,7 @@ struct mx_comm {
   size_t p2p_off;
   mx::P2PSendState *p2p_send;   // [size]
   mx::P2PRecvState *p2p_recv;   // [size]
+  char *p2p_stash;              // [size][P2P_STASH_N][P2P_STASH_C] unexpected-message payloads
   hipStream_t p2p_stream[2];
   hipEvent_t p2p_ev;
   uint64_t *p2p_lanes;     // device: finished-lane counters of the two streams

@@ -197,92 +197,85 @@ struct P2PRecvArgs {
   char *buf;
   uint64_t cap;
   int64_t tag;               // < 0: any
-  const char *box;           // my mailbox for src
-  const uint64_t *posted;    // my flags: posted[src]
-  const uint64_t *filled;    // my flags: filled[src][lane]
-  uint64_t *seen;            // sender's flags: seen[me][lane]
-  uint64_t *drained;         // sender's flags: drained[me][lane]
-  P2PRecvState *st;
   int64_t *status;           // mapped host: delivered bytes, tag, error, source
   uint64_t timeout_ticks;
   int *err;
-  // MX_ANY_SOURCE: the fields above are taken for the source the pick
-  // kernel stored in status[3], from these per-source bases
-  int any, me;
-  const char *box0;
+  // the source's mailbox, flags and state, from these per-source bases; with
+  // `any` (MX_ANY_SOURCE) the source is the one the pick kernel stored in
+  // status[3]
+  int src, any, me;
+  const char *box0;          // my mailbox for source 0 (source p at + p * P2P_BOX)
   const uint64_t *flag0;     // my flag array
   uint64_t *peer_flags[MAXR];
   P2PRecvState *st0;
+  char *stash0;              // stash payloads of source 0 (source p at + p * N * C)
   P2PDone fin;
 };
 
-// MX_ANY_SOURCE: wait until some source p has posted an envelope beyond what
-// this process consumed from it (lane 0's message count), store p in
+// oldest stashed message of `st` a receive with `tag` (< 0: any) matches, or -1
+__device__ __forceinline__ int stash_match(const P2PRecvState *st, int64_t tag) {
+  int hit = -1;
+  uint64_t best = ~(uint64_t)0;
+  for (int k = 0; k < P2P_STASH_N; k++) {
+    const P2PStashEntry &e = st->stash[k];
+    if (e.valid && (tag < 0 || e.tag == tag) && e.seq < best) {
+      best = e.seq;
+      hit = k;
+    }
+  }
+  return hit;
+}
+
+// MX_ANY_SOURCE: wait until some source p has a message this receive can
+// take -- a matching stashed one, or a posted envelope beyond what this
+// process consumed from it (lane 0's message count) -- and store p in
 // status[3] (-1 after a timeout).
-__global__ void k_p2p_pick(const uint64_t *flag0, const P2PRecvState *st0, int n, int start, int64_t *status,
-                           uint64_t timeout_ticks, int *err) {
+__global__ void k_p2p_pick(const uint64_t *flag0, const P2PRecvState *st0, int n, int start, int64_t tag,
+                           int64_t *status, uint64_t timeout_ticks, int *err) {
   if (threadIdx.x != 0) return;
   const uint64_t t0 = wall_clock64();
+  for (int i = 0; i < n; i++) {
+    const int p = (start + i) % n;
+    if (stash_match(st0 + p, tag) >= 0) {
+      __hip_atomic_store(&status[3], (int64_t)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      return;
+    }
+  }
   for (;;) {
     for (int i = 0; i < n; i++) {
       const int p = (start + i) % n;
-      if (__hip_atomic_load(flag0 + P2P_POSTED + p, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) >
+      if (__hip_atomic_load(flag0 + P2P_POSTED + p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) >
           st0[p].lane_msgs[0]) {
-        __hip_atomic_store(&status[3], (int64_t)p, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+        __hip_atomic_store(&status[3], (int64_t)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
         return;
       }
     }
     __builtin_amdgcn_s_sleep(2);
     if (wall_clock64() - t0 > timeout_ticks) {
-      __hip_atomic_store(&status[3], (int64_t)-1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+      __hip_atomic_store(&status[3], (int64_t)-1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
       __hip_atomic_store(err, MX_ERR_TIMEOUT, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
       return;
     }
   }
 }
 
-__device__ __forceinline__ bool recv_body(const P2PRecvArgs &a);
+// What a receive kernel decided, identically in every lane (each lane sees
+// the same stash table -- it changes only at a kernel's end -- and the same
+// envelope sequence): the stash slot it took, and the messages it stashed.
+struct StashPlan {
+  int hit;                         // stash slot delivered, or -1
+  int n;                           // messages stashed by this kernel
+  int slot[P2P_STASH_N];
+  int64_t tag[P2P_STASH_N];
+  uint64_t bytes[P2P_STASH_N], seq[P2P_STASH_N];
+};
 
-__global__ void __launch_bounds__(kP2PThreads) k_p2p_recv(P2PRecvArgs a) {
-  const bool wrote = recv_body(a);
-  lane_finished(a.fin, wrote);
-}
-
-// returns whether this lane stored user data
-__device__ __forceinline__ bool recv_body(const P2PRecvArgs &a) {
-  const int l = blockIdx.x;
-  const uint64_t t0 = wall_clock64();
+// Copy one message of `bytes` through this lane's stripe: from the mailbox
+// (chunk handshake) into dst (dst_cap bytes kept; the rest drained).
+__device__ __forceinline__ bool recv_stream(int l, uint64_t bytes, char *dst, uint64_t dst_cap, const char *box,
+                                            const uint64_t *filled, uint64_t *drained, P2PRecvState *st, uint64_t t0,
+                                            const P2PRecvArgs &a, bool *wrote) {
   __shared__ int ok;
-  __shared__ uint64_t s_bytes;
-  __shared__ int64_t s_tag;
-  const char *box = a.box;
-  const uint64_t *posted = a.posted, *filled = a.filled;
-  uint64_t *seen = a.seen, *drained = a.drained;
-  P2PRecvState *st = a.st;
-  if (a.any) {
-    const int p = (int)__hip_atomic_load(&a.status[3], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM);
-    if (p < 0) return false;   // the pick timed out (error already raised)
-    box = a.box0 + (size_t)p * P2P_BOX;
-    posted = a.flag0 + P2P_POSTED + p;
-    filled = a.flag0 + P2P_FILLED + (size_t)p * P2P_L;
-    seen = a.peer_flags[p] + P2P_SEEN + (size_t)a.me * P2P_L;
-    drained = a.peer_flags[p] + P2P_DRAINED + (size_t)a.me * P2P_L;
-    st = a.st0 + p;
-  }
-  if (threadIdx.x == 0) {
-    const uint64_t m = st->lane_msgs[l];
-    ok = p2p_wait_ge(posted, m + 1, t0, a.timeout_ticks, a.err);
-    if (ok) {
-      const volatile uint64_t *h = reinterpret_cast<const volatile uint64_t *>(box + (m % P2P_H) * P2P_HDR);
-      s_bytes = h[0];
-      s_tag = (int64_t)h[1];
-      __hip_atomic_store(seen + l, m + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-      st->lane_msgs[l] = m + 1;
-    }
-  }
-  __syncthreads();
-  if (!ok) return false;
-  const uint64_t bytes = s_bytes;
   uint64_t lo, hi;
   p2p_lane(bytes, l, &lo, &hi);
   uint64_t k = st->lane_chunks[l];
@@ -291,22 +284,138 @@ __device__ __forceinline__ bool recv_body(const P2PRecvArgs &a) {
     k++;
     if (threadIdx.x == 0) ok = p2p_wait_ge(filled + l, k, t0, a.timeout_ticks, a.err);
     __syncthreads();
-    if (!ok) return pos > lo;
+    if (!ok) return false;
     const char *slot = box + 4096 + ((size_t)l * P2P_S + (size_t)((k - 1) % P2P_S)) * P2P_C;
-    if (pos < a.cap) p2p_copy(a.buf + pos, slot, std::min<uint64_t>(len, a.cap - pos));
+    if (pos < dst_cap) {
+      p2p_copy(dst + pos, slot, std::min<uint64_t>(len, dst_cap - pos));
+      *wrote = true;
+    }
     __syncthreads();          // every load of the slot has returned
-    if (threadIdx.x == 0) __hip_atomic_store(drained + l, k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-  }
-  if (threadIdx.x == 0) {
-    st->lane_chunks[l] = k;
-    if (l == 0) {
-      a.status[0] = (int64_t)std::min<uint64_t>(bytes, a.cap);
-      a.status[1] = s_tag;
-      a.status[2] = bytes > a.cap ? MX_ERR_TRUNCATE : (a.tag >= 0 && s_tag != a.tag) ? MX_ERR_TAG : 0;
-      __threadfence_system();
+    if (threadIdx.x == 0) {
+      __hip_atomic_store(drained + l, k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      st->lane_chunks[l] = k;
     }
   }
-  return lo < hi && lo < a.cap;
+  return true;
+}
+
+// one lane of a receive; returns whether this lane stored user data
+__device__ __forceinline__ bool recv_body(const P2PRecvArgs &a, StashPlan &plan, P2PRecvState **stp) {
+  const int l = blockIdx.x;
+  const uint64_t t0 = wall_clock64();
+  __shared__ int ok;
+  __shared__ uint64_t s_bytes;
+  __shared__ int64_t s_tag;
+  __shared__ uint64_t s_seq;
+  int p = a.src;
+  if (a.any) {
+    p = (int)__hip_atomic_load(&a.status[3], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    if (p < 0) return false;   // the pick timed out (error already raised)
+  }
+  const char *box = a.box0 + (size_t)p * P2P_BOX;
+  const uint64_t *posted = a.flag0 + P2P_POSTED + p, *filled = a.flag0 + P2P_FILLED + (size_t)p * P2P_L;
+  uint64_t *seen = a.peer_flags[p] + P2P_SEEN + (size_t)a.me * P2P_L;
+  uint64_t *drained = a.peer_flags[p] + P2P_DRAINED + (size_t)a.me * P2P_L;
+  P2PRecvState *st = a.st0 + p;
+  char *stash = a.stash0 + (size_t)p * P2P_STASH_N * P2P_STASH_C;
+  *stp = st;
+  bool wrote = false;
+  // (1) a stashed message this receive matches: deliver it, consume no envelope
+  plan.hit = stash_match(st, a.tag);
+  if (plan.hit >= 0) {
+    const P2PStashEntry e = st->stash[plan.hit];
+    uint64_t lo, hi;
+    p2p_lane(e.bytes, l, &lo, &hi);
+    if (lo < hi && lo < a.cap) {
+      p2p_copy(a.buf + lo, stash + (size_t)plan.hit * P2P_STASH_C + lo, std::min(hi, a.cap) - lo);
+      wrote = true;
+    }
+    if (l == 0 && threadIdx.x == 0) {
+      a.status[0] = (int64_t)std::min<uint64_t>(e.bytes, a.cap);
+      a.status[1] = e.tag;
+      a.status[2] = e.bytes > a.cap ? MX_ERR_TRUNCATE : 0;
+      __threadfence_system();
+    }
+    return wrote;
+  }
+  // (2) envelopes in order: a mismatch goes to a free stash slot
+  for (;;) {
+    if (threadIdx.x == 0) {
+      const uint64_t m = st->lane_msgs[l];
+      ok = p2p_wait_ge(posted, m + 1, t0, a.timeout_ticks, a.err);
+      if (ok) {
+        const volatile uint64_t *h = reinterpret_cast<const volatile uint64_t *>(box + (m % P2P_H) * P2P_HDR);
+        s_bytes = h[0];
+        s_tag = (int64_t)h[1];
+        s_seq = m;
+        __hip_atomic_store(seen + l, m + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        st->lane_msgs[l] = m + 1;
+      }
+    }
+    __syncthreads();
+    if (!ok) return wrote;
+    const uint64_t bytes = s_bytes;
+    const int64_t tag = s_tag;
+    const uint64_t seq = s_seq;
+    __syncthreads();          // every thread has read the envelope before the next one
+    int slot = -1;
+    if (a.tag >= 0 && tag != a.tag && bytes <= P2P_STASH_C) {
+      for (int k = 0; k < P2P_STASH_N && slot < 0; k++) {
+        bool taken = st->stash[k].valid != 0;
+        for (int j = 0; j < plan.n; j++) taken = taken || plan.slot[j] == k;
+        if (!taken) slot = k;
+      }
+    }
+    if (slot >= 0) {          // unexpected: keep it for a later receive
+      if (!recv_stream(l, bytes, stash + (size_t)slot * P2P_STASH_C, bytes, box, filled, drained, st, t0, a, &wrote))
+        return wrote;
+      wrote = false;          // stash bytes are not the user's
+      plan.slot[plan.n] = slot;
+      plan.tag[plan.n] = tag;
+      plan.bytes[plan.n] = bytes;
+      plan.seq[plan.n] = seq;
+      plan.n++;
+      continue;
+    }
+    // this receive's message (or one that cannot be stashed: MX_ERR_TAG)
+    if (!recv_stream(l, bytes, a.buf, a.cap, box, filled, drained, st, t0, a, &wrote)) return wrote;
+    if (l == 0 && threadIdx.x == 0) {
+      a.status[0] = (int64_t)std::min<uint64_t>(bytes, a.cap);
+      a.status[1] = tag;
+      a.status[2] = bytes > a.cap ? MX_ERR_TRUNCATE : (a.tag >= 0 && tag != a.tag) ? MX_ERR_TAG : 0;
+      __threadfence_system();
+    }
+    return wrote;
+  }
+}
+
+__global__ void __launch_bounds__(kP2PThreads) k_p2p_recv(P2PRecvArgs a) {
+  StashPlan plan;
+  plan.hit = -1;
+  plan.n = 0;
+  P2PRecvState *st = nullptr;
+  const bool wrote = recv_body(a, plan, &st);
+  // the last lane out commits the stash changes (the table is read by every
+  // lane during the kernel, so it only changes between kernels)
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    if (wrote) __threadfence();
+    const uint64_t old = __hip_atomic_fetch_add(a.fin.lanes, (uint64_t)1, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+    if (old + 1 == a.fin.target) {
+      if (st) {
+        if (plan.hit >= 0) st->stash[plan.hit].valid = 0;
+        for (int j = 0; j < plan.n; j++) {
+          P2PStashEntry &e = st->stash[plan.slot[j]];
+          e.tag = plan.tag[j];
+          e.bytes = plan.bytes[j];
+          e.seq = plan.seq[j];
+          e.valid = 1;
+        }
+        __threadfence();
+      }
+      if (a.fin.done) __hip_atomic_store(a.fin.done, (int64_t)1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+  }
 }
 
 int p2p_setup(mx_comm *c) {
@@ -320,6 +429,11 @@ int p2p_setup(mx_comm *c) {
   }
   if (hipMalloc((void **)&c->p2p_lanes, 2 * sizeof(uint64_t)) != hipSuccess) {
     c->p2p_lanes = nullptr;
+    p2p_release(c);
+    return MX_ERR_NOMEM;
+  }
+  if (hipMalloc((void **)&c->p2p_stash, (size_t)c->size * P2P_STASH_N * P2P_STASH_C) != hipSuccess) {
+    c->p2p_stash = nullptr;
     p2p_release(c);
     return MX_ERR_NOMEM;
   }
@@ -343,7 +457,9 @@ void p2p_release(mx_comm *c) {
   if (c->p2p_send) (void)hipFree(c->p2p_send);
   if (c->p2p_recv) (void)hipFree(c->p2p_recv);
   if (c->p2p_lanes) (void)hipFree(c->p2p_lanes);
+  if (c->p2p_stash) (void)hipFree(c->p2p_stash);
   c->p2p_lanes = nullptr;
+  c->p2p_stash = nullptr;
   c->p2p_stream[0] = c->p2p_stream[1] = nullptr;
   c->p2p_ev = nullptr;
   c->p2p_send = nullptr;
@@ -467,23 +583,19 @@ int p2p_enqueue(mx_request *q, hipStream_t *done_stream) {
     a.buf = tmp ? tmp : (char *)q->rbuf;
     a.cap = bytes;
     a.tag = q->tag;
-    if (p >= 0) {
-      a.box = c->staging + c->p2p_off + (size_t)p * P2P_BOX;
-      a.posted = c->flagmem + P2P_POSTED + p;
-      a.filled = c->flagmem + P2P_FILLED + (size_t)p * P2P_L;
-      a.seen = c->peer_flags[p] + P2P_SEEN + (size_t)me * P2P_L;
-      a.drained = c->peer_flags[p] + P2P_DRAINED + (size_t)me * P2P_L;
-      a.st = c->p2p_recv + p;
-    } else {   // MX_ANY_SOURCE
+    a.src = p;
+    a.me = me;
+    a.box0 = c->staging + c->p2p_off;
+    a.flag0 = c->flagmem;
+    for (int j = 0; j < c->size; j++) a.peer_flags[j] = c->peer_flags[j];
+    a.st0 = c->p2p_recv;
+    a.stash0 = c->p2p_stash;
+    if (p < 0) {   // MX_ANY_SOURCE
       a.any = 1;
-      a.me = me;
-      a.box0 = c->staging + c->p2p_off;
-      a.flag0 = c->flagmem;
-      for (int j = 0; j < c->size; j++) a.peer_flags[j] = c->peer_flags[j];
-      a.st0 = c->p2p_recv;
       const int start = (int)(c->p2p_any_rr++ % (unsigned)c->size);
       hipLaunchKernelGGL(k_p2p_pick, dim3(1), dim3(64), 0, s, (const uint64_t *)c->flagmem,
-                         (const P2PRecvState *)c->p2p_recv, c->size, start, st_dev, c->timeout_ticks, c->err_dev);
+                         (const P2PRecvState *)c->p2p_recv, c->size, start, (int64_t)q->tag, st_dev,
+                         c->timeout_ticks, c->err_dev);
       if ((rc = mx_check_launch())) return rc;
     }
     a.status = st_dev;
