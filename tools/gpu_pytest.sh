@@ -1,4 +1,4 @@
-# Round-2 GPU session script. usage on the box: bash tools/gpu_r2.sh TAG 'pytest args' [more pytest arg sets...]
+# GPU pytest runner. usage on the box: bash tools/gpu_pytest.sh TAG 'pytest args' [more pytest arg sets...]
 # Each argument set runs as one pytest process under its own time limit;
 # the first failure ends the script (nothing more runs on the GPU after it).
 set -o pipefail
