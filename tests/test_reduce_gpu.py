@@ -123,6 +123,54 @@ def test_full_size_fp32_sum_1gib():
     np.testing.assert_array_equal(got.view(np.uint32), b.view(np.uint32))
 
 
+# CFG-B at full size beyond fp32 SUM: one pair per kernel family / operator
+# class, 1 GiB per buffer (the non-temporal instance), checked against the
+# restatement element for element.  Inputs: full-range bytes for integer and
+# bitwise ops, ties-heavy pairs for the LOC ops, [0.5, 2) for FP PROD.
+_FULL = [("BAND", "UINT16_T"), ("PROD", "INT64_T"), ("MAX", "DOUBLE"), ("MAXLOC", "FLOAT_INT"),
+         ("MINLOC", "DOUBLE_INT"), ("PROD", "C_FLOAT_COMPLEX"), ("LXOR", "INT8_T"), ("SUM", "LONG_DOUBLE")]
+
+
+@pytest.mark.parametrize("op,t", _FULL, ids=[f"{o}-{t}" for o, t in _FULL])
+def test_full_size_1gib_pairs(op, t):
+    O = oracle_lib.oracle()
+    es = mxompi.type_size(t)
+    n = (1 << 30) // es
+    rng = np.random.default_rng(0x5EEDC0DE + mxompi.TYPE[t])
+    if t == "FLOAT_INT":
+        v = np.zeros((2, n), dtype=[("v", "<f4"), ("k", "<i4")])
+        v["v"] = rng.integers(0, 16, (2, n))
+        v["k"] = rng.integers(-1000, 1000, (2, n))
+        raw = [v[0].view(np.uint8), v[1].view(np.uint8)]
+    elif t == "DOUBLE_INT":
+        v = np.zeros((2, n), dtype=[("v", "<f8"), ("k", "<i4"), ("pad", "<i4")])
+        v["v"] = rng.integers(0, 16, (2, n))
+        v["k"] = rng.integers(-1000, 1000, (2, n))
+        v["pad"] = rng.integers(-1 << 31, 1 << 31, (2, n))
+        raw = [v[0].view(np.uint8), v[1].view(np.uint8)]
+    elif t == "C_FLOAT_COMPLEX":
+        raw = [rng.uniform(0.5, 2.0, 2 * n).astype(np.float32).view(np.uint8) for _ in range(2)]
+    elif t == "DOUBLE":
+        raw = [rng.uniform(-1e6, 1e6, n).view(np.uint8) for _ in range(2)]
+    elif t == "LONG_DOUBLE":
+        raw = []
+        for _ in range(2):
+            r = rng.integers(0, 256, n * 16, dtype=np.uint8)
+            r.reshape(-1, 16)[:] = rng.uniform(-4, 4, n).astype(np.longdouble).view(np.uint8).reshape(-1, 16)
+            raw.append(r)
+    else:
+        raw = [rng.integers(0, 256, n * es, dtype=np.uint8) for _ in range(2)]
+    A, B = _dev(raw[0]), _dev(raw[1])
+    mxompi.reduce2(op, t, A.data_ptr(), B.data_ptr(), n, _stream())
+    torch.cuda.synchronize()
+    got = B.cpu().numpy()
+    del A, B
+    torch.cuda.empty_cache()
+    exp = raw[1].copy()
+    assert O.mxo_reduce2(mxompi.OP[op], mxompi.TYPE[t], raw[0].ctypes.data, exp.ctypes.data, n, 1) == 0
+    golden_io.assert_op_equal(got, exp, mxompi.OP[op], mxompi.TYPE[t])
+
+
 @pytest.mark.parametrize("shift", [0, 1, 3])
 def test_streaming_instance_ragged(shift):
     """The non-temporal, XCD-mapped K1 instance (>= 384 MiB footprint) on a
