@@ -73,13 +73,15 @@ def time_launches(torch, fn, iters, reps):
     return out[len(out) // 2]
 
 
-def sweep_pairs(torch, mx, nbytes, iters):
+def sweep_pairs(torch, mx, nbytes, iters, only=None):
     sp = torch.cuda.current_stream().cuda_stream
     gen = torch.Generator(device="cuda").manual_seed(0x5EEDC0DE)
     a = torch.empty(nbytes, dtype=torch.uint8, device="cuda")
     b = torch.empty(nbytes, dtype=torch.uint8, device="cuda")
     rows = []
     for t, tname in enumerate(mx.TYPES):
+        if only and tname not in only:
+            continue
         ops = [o for o in range(1, 13) if mx.op_supported(o, t)]
         if not ops:
             continue
@@ -174,6 +176,7 @@ def main():
     ap.add_argument("--max-bytes", type=int, default=4 << 30)
     ap.add_argument("--min-bytes", type=int, default=8)
     ap.add_argument("--types", default="", help="comma-separated golden type names for the pack sweep")
+    ap.add_argument("--pair-types", default="", help="comma-separated MPI type names for the pairs sweep")
     args = ap.parse_args()
     import torch
     import mxompi as mx
@@ -182,7 +185,8 @@ def main():
            "timing": "HIP events on the launch stream, median of batches", "when": time.strftime("%F %T")}
     what = args.what.split(",")
     if "pairs" in what:
-        doc["pairs"] = sweep_pairs(torch, mx, args.pair_bytes, args.iters)
+        doc["pairs"] = sweep_pairs(torch, mx, args.pair_bytes, args.iters,
+                                   {t for t in args.pair_types.split(",") if t} or None)
         torch.cuda.empty_cache()
     if "sizes" in what:
         doc["sizes"] = sweep_sizes(torch, mx, args.max_bytes, args.iters)

@@ -113,13 +113,13 @@ __device__ __noinline__ x87 x87_nan_result(const x87 &like, const x87 &a, const 
   return x87_make(like, x87_sign(w), 0x7fff, w.m | q);
 }
 
-// value = S * 2^X, S != 0: normalise, round to nearest even at 64 bits,
-// handle gradual underflow and overflow.
-__device__ __noinline__ x87 x87_round_pack(const x87 &like, int s, u128 S, int X) {
-  const int p = 127 - clz128(S);
-  S <<= (127 - p);
-  int e = X + p - 63 + 16446;  // biased: value = m * 2^(e - 16446)
-  if (e < 1) {
+// value = S * 2^X with S normalised (bit 127 set): round to nearest even at
+// 64 bits, handle gradual underflow and overflow.  The arithmetic fast paths
+// are inlined (a call per element spills the 128-bit temporaries to
+// scratch); only the NaN / complex-recovery paths stay out of line.
+__device__ __forceinline__ x87 x87_round_norm(const x87 &like, int s, u128 S, int X) {
+  int e = X + 64 + 16446;  // biased: value = m * 2^(e - 16446)
+  if (__builtin_expect(e < 1, 0)) {
     const int sh = 1 - e;
     if (sh >= 128) {
       S = 1;  // pure sticky
@@ -142,6 +142,12 @@ __device__ __noinline__ x87 x87_round_pack(const x87 &like, int s, u128 S, int X
   return x87_make(like, s, e, m);
 }
 
+// value = S * 2^X, S != 0, any normalisation
+__device__ __forceinline__ x87 x87_round_pack(const x87 &like, int s, u128 S, int X) {
+  const int z = clz128(S);
+  return x87_round_norm(like, s, S << z, X - z);
+}
+
 // unpack finite nonzero to normalised (m with bit 63 set, value m*2^E)
 __device__ __forceinline__ void x87_unpack(const x87 &a, uint64_t &m, int &E) {
   int e = x87_exp(a);
@@ -152,7 +158,7 @@ __device__ __forceinline__ void x87_unpack(const x87 &a, uint64_t &m, int &E) {
   E -= lz;
 }
 
-__device__ __noinline__ x87 x87_add(const x87 &like, const x87 &a, const x87 &b) {
+__device__ __forceinline__ x87 x87_add(const x87 &like, const x87 &a, const x87 &b) {
   if (x87_unsupported(a) || x87_unsupported(b)) return x87_indefinite(like);
   if (x87_isnan(a) || x87_isnan(b)) return x87_nan_result(like, a, b);
   const int sa = x87_sign(a), sb = x87_sign(b);
@@ -187,6 +193,8 @@ __device__ __noinline__ x87 x87_add(const x87 &like, const x87 &a, const x87 &b)
     B >>= d;
     if (lost) B |= 1;
   }
+  // one path for effective addition and subtraction: a branch on the signs
+  // would diverge on mixed-sign data
   const u128 S = (sa == sb) ? A + B : A - B;
   if (S == 0) return x87_make(like, 0, 0, 0);  // exact cancellation: +0 under RNE
   return x87_round_pack(like, s, S, Ea - 62);
@@ -203,7 +211,7 @@ __device__ __forceinline__ x87 x87_sub(const x87 &like, const x87 &a, const x87 
   return x87_add(like, a, x87_neg(b));
 }
 
-__device__ __noinline__ x87 x87_mul(const x87 &like, const x87 &a, const x87 &b) {
+__device__ __forceinline__ x87 x87_mul(const x87 &like, const x87 &a, const x87 &b) {
   if (x87_unsupported(a) || x87_unsupported(b)) return x87_indefinite(like);
   if (x87_isnan(a) || x87_isnan(b)) return x87_nan_result(like, a, b);
   const int s = x87_sign(a) ^ x87_sign(b);
@@ -217,8 +225,10 @@ __device__ __noinline__ x87 x87_mul(const x87 &like, const x87 &a, const x87 &b)
   int Ea, Eb;
   x87_unpack(a, ma, Ea);
   x87_unpack(b, mb, Eb);
-  const u128 P = (u128)ma * (u128)mb;
-  return x87_round_pack(like, s, P, Ea + Eb);
+  u128 P = (u128)ma * (u128)mb;  // normalised inputs: bit 127 or 126 set
+  int X = Ea + Eb;
+  if (!(uint64_t)(P >> 127)) { P <<= 1; X--; }
+  return x87_round_norm(like, s, P, X);
 }
 
 // ---- operator functors (x = first operand, y = second) -----------------
@@ -243,12 +253,13 @@ __device__ __forceinline__ x87 x87_copysign01(const x87 &like, bool one, const x
   return one ? x87_make(like, x87_sign(sign_of), 16383, 1ull << 63) : x87_make(like, x87_sign(sign_of), 0, 0);
 }
 
-__device__ __noinline__ x87c x87c_mul(const x87c &p, const x87c &q) {
+// Annex-G recovery of an x87 complex product whose both parts came out NaN
+// (rare: out of line)
+__device__ __noinline__ x87c x87c_mul_recover(const x87c &p, const x87c &q, x87 x, x87 y, const x87 &ac,
+                                             const x87 &bd, const x87 &ad, const x87 &bc) {
   x87 a = p.re, b = p.im, c = q.re, d = q.im;
   const x87 &L = p.re;
-  const x87 ac = x87_mul(L, a, c), bd = x87_mul(L, b, d), ad = x87_mul(L, a, d), bc = x87_mul(L, b, c);
-  x87 x = x87_sub(p.re, ac, bd), y = x87_add(p.im, ad, bc);
-  if (x87_isnan(x) && x87_isnan(y)) {
+  {
     bool recalc = false;
     if (x87_isinf(a) || x87_isinf(b)) {
       a = x87_copysign01(L, x87_isinf(a), a);
@@ -277,6 +288,15 @@ __device__ __noinline__ x87c x87c_mul(const x87c &p, const x87c &q) {
       y = x87_mul(p.im, inf, x87_add(L, x87_mul(L, a, d), x87_mul(L, b, c)));
     }
   }
+  return x87c{x, y};
+}
+
+__device__ __forceinline__ x87c x87c_mul(const x87c &p, const x87c &q) {
+  const x87 &a = p.re, &b = p.im, &c = q.re, &d = q.im;
+  const x87 &L = p.re;
+  const x87 ac = x87_mul(L, a, c), bd = x87_mul(L, b, d), ad = x87_mul(L, a, d), bc = x87_mul(L, b, c);
+  const x87 x = x87_sub(p.re, ac, bd), y = x87_add(p.im, ad, bc);
+  if (x87_isnan(x) && x87_isnan(y)) return x87c_mul_recover(p, q, x, y, ac, bd, ad, bc);
   return x87c{x, y};
 }
 
