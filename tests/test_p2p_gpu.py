@@ -8,8 +8,9 @@ every size (0 bytes, sub-vector tails, several times the mailbox), every
 alignment (user pointers offset by 1..15 bytes), many messages in flight
 per pair (more than the envelope ring), a ring shift, an all-to-all, and
 sends to self; truncation completes with MPI's error and leaves the channel
-usable; tags match out of order within a pair (unexpected messages stashed
-on the device); derived datatypes on either side match the
+usable; tags match out of order within a pair (unexpected eager messages
+stashed on the device, unexpected rendezvous messages deferred with their
+data left at the sender until a receive clears them); derived datatypes on either side match the
 reference convertor's packed stream (golden vectors).
 """
 import os
@@ -100,8 +101,11 @@ def _p2p_worker(rank, n, port, q):
             comm.send(_dev(_data(302, 1000)).data_ptr(), 1000, 1, tag=5)
             comm.send(_dev(_data(303, 2000)).data_ptr(), 2000, 1, tag=7)
             comm.send(_dev(_data(304, 700)).data_ptr(), 700, 1, tag=8)
-            comm.send(_dev(_data(305, 300 << 10)).data_ptr(), 300 << 10, 1, tag=3)   # too big to stash
+            big = _dev(_data(305, 300 << 10))      # rendezvous: moves once a receive clears it
+            rb = comm.isend(big.data_ptr(), 300 << 10, 1, tag=3)
             comm.send(_dev(_data(306, 64)).data_ptr(), 64, 1, tag=4)
+            rb.wait()
+            rb.free()
         elif rank == 1:
             d = torch.zeros(2000, dtype=torch.uint8, device="cuda")
             errs, data = [], []
@@ -117,15 +121,19 @@ def _p2p_worker(rank, n, port, q):
                 r.free()
                 errs.append(st)
                 data.append(d.cpu().numpy()[:st[0]].tobytes())
-            big = torch.zeros(300 << 10, dtype=torch.uint8, device="cuda")
-            try:                               # the 300 KiB tag-3 message cannot be stashed
-                comm.recv(big.data_ptr(), 300 << 10, 0, tag=4)
-            except mxompi.MxError as e:
-                errs.append(e.rc)
+            # tag 4 defers the 300 KiB tag-3 rendezvous envelope (its data
+            # stays with the sender) and takes the 64 B behind it; tag 3 then
+            # clears the deferred message
             r = comm.irecv(d.data_ptr(), 64, 0, tag=4)
             r.wait()
             errs.append(r.status())
             data.append(d.cpu().numpy()[:64].tobytes())
+            r.free()
+            big = torch.zeros(300 << 10, dtype=torch.uint8, device="cuda")
+            r = comm.irecv(big.data_ptr(), 300 << 10, 0, tag=3)
+            r.wait()
+            errs.append(r.status())
+            data.append(big.cpu().numpy().tobytes())
             r.free()
             res["errs"] = errs
             res["tagdata"] = data
@@ -180,6 +188,55 @@ def _p2p_worker(rank, n, port, q):
             r.wait()
             r.free()
         res["a2a"] = [b.cpu().numpy().tobytes() for b in rb]
+
+        # (7b) the same with rendezvous-sized messages: every rank's pick
+        # kernels serve the CTS of several destinations in whatever order
+        # they arrive (receives posted in descending source order)
+        A2 = 300001
+        sb = [_dev(_data(2000 * rank + p, A2)) for p in range(n)]
+        rb = [torch.zeros(A2, dtype=torch.uint8, device="cuda") for _ in range(n)]
+        reqs = [comm.isend(sb[p].data_ptr(), A2, p, tag=12) for p in range(n)]
+        reqs += [comm.irecv(rb[p].data_ptr(), A2, p, tag=12) for p in reversed(range(n))]
+        for r in reqs:
+            r.wait()
+            r.free()
+        res["a2a_rndv"] = [b.cpu().numpy().tobytes() for b in rb]
+
+        # (7c) rendezvous messages matched out of order within a pair: 0 -> 1
+        # sends R1 (tag 31), R2 (tag 32), an eager E (tag 33), R3 (tag 31);
+        # 1 takes 33 (deferring R1 and R2), 32, ANY_TAG (the oldest held:
+        # R1), then 31 (R3, from the envelope ring) into a short buffer
+        sizes = {31: (1 << 20) + 5, 32: 600 << 10, 33: 5000}
+        if rank == 0:
+            msgs = [(31, 401, sizes[31]), (32, 402, sizes[32]), (33, 403, sizes[33]), (31, 404, 2 << 20)]
+            bufs = [_dev(_data(seed, nb)) for _, seed, nb in msgs]
+            reqs = [comm.isend(b.data_ptr(), nb, 1, tag=t) for b, (t, _, nb) in zip(bufs, msgs)]
+            for r in reqs:
+                r.wait()
+                r.free()
+        elif rank == 1:
+            out = []
+            for tag, cap in ((33, 8000), (32, 700 << 10), (-1, 2 << 20), (31, (1 << 20) + 3)):
+                b = torch.zeros(cap, dtype=torch.uint8, device="cuda")
+                r = comm.irecv(b.data_ptr(), cap, 0, tag=tag)
+                try:
+                    r.wait()
+                    st = r.status()
+                except mxompi.MxError as e:
+                    st = (e.rc, r.status())
+                r.free()
+                nb = st[0] if isinstance(st[0], int) and st[0] >= 0 else st[1][0]
+                out.append((st, b.cpu().numpy()[:nb].tobytes()))
+            res["rndv_order"] = out
+
+        # (7d) rendezvous to self, receive posted after the send
+        S = (1 << 20) + 17
+        x = _dev(_data(7000 + rank, S))
+        y = torch.zeros(S, dtype=torch.uint8, device="cuda")
+        rs = comm.isend(x.data_ptr(), S, rank, tag=41)
+        rr = comm.irecv(y.data_ptr(), S, rank, tag=41)
+        rr.wait(); rs.wait(); rr.free(); rs.free()
+        res["self_rndv"] = y.cpu().numpy().tobytes()
 
         # (8) MPI_ANY_SOURCE: every other rank sends two messages to rank 0,
         # which takes all but one with non-blocking ANY_SOURCE receives
@@ -256,12 +313,24 @@ def test_point_to_point(n):
     for k, b in enumerate(bufs):
         assert b == _data(200 + k, 300 * 1024 + 3).tobytes(), f"in-flight message {k}"
     # MX_ERR_TRUNCATE; then tag 7 (stashing 9 and 5), the stashed 5, the
-    # stashed 9 for MPI_ANY_TAG (oldest), 8; a mismatch too large to stash
-    # completes with MX_ERR_TAG and the channel goes on
-    assert got[1]["errs"] == [-9, (2000, 7), (1000, 5), (1000, 9), (700, 8), -10, (64, 4)], got[1]["errs"]
+    # stashed 9 for MPI_ANY_TAG (oldest), 8; tag 4 past the deferred 300 KiB
+    # rendezvous message, which tag 3 then takes
+    assert got[1]["errs"] == [-9, (2000, 7), (1000, 5), (1000, 9), (700, 8), (64, 4), (300 << 10, 3)], \
+        got[1]["errs"]
     want = [_data(300, 1000)[:600], _data(303, 2000), _data(302, 1000), _data(301, 1000), _data(304, 700),
-            _data(306, 64)]
+            _data(306, 64), _data(305, 300 << 10)]
     assert got[1]["tagdata"] == [w.tobytes() for w in want]
+    for r in range(n):
+        for p in range(n):
+            assert got[r]["a2a_rndv"][p] == _data(2000 * p + r, 300001).tobytes(), f"rendezvous a2a {p} -> {r}"
+        assert got[r]["self_rndv"] == _data(7000 + r, (1 << 20) + 17).tobytes(), f"rendezvous to self {r}"
+    order = got[1]["rndv_order"]
+    assert [o[0] for o in order] == [(5000, 33), (600 << 10, 32), ((1 << 20) + 5, 31),
+                                     (-9, ((1 << 20) + 3, 31))], [o[0] for o in order]
+    assert order[0][1] == _data(403, 5000).tobytes()
+    assert order[1][1] == _data(402, 600 << 10).tobytes()
+    assert order[2][1] == _data(401, (1 << 20) + 5).tobytes()
+    assert order[3][1] == _data(404, 2 << 20)[:(1 << 20) + 3].tobytes()
     for it, b in enumerate(got[1]["persistent"]):
         assert b == _data(400 + it, 1 << 20).tobytes(), f"persistent start {it}"
     tv = REC["vector_f64_b3_s5"]

@@ -21,10 +21,10 @@ def worker(rank, n, port, q):
         dist.all_gather_object(out, b)
         return out
     comm = mxompi.Comm(rank, n, ag, device=0, staging_bytes=64 << 20)
-    x = torch.zeros(4 << 20, dtype=torch.uint8, device="cuda")
+    x = torch.zeros(64 << 20, dtype=torch.uint8, device="cuda")
     peer = 1 - rank
     rows = []
-    for nb in [8, 4096, 65536, 1 << 20]:
+    for nb in [8, 4096, 65536, 256 << 10, (256 << 10) + 16, 1 << 20, 16 << 20, 64 << 20]:
         for form in ("blocking", "nonblocking"):
             def one():
                 if form == "blocking":
@@ -44,11 +44,12 @@ def worker(rank, n, port, q):
             for _ in range(10):
                 one()
             dist.barrier()
-            it = 100
+            it = 100 if nb <= (1 << 20) else 20
             t0 = time.perf_counter()
             for _ in range(it):
                 one()
-            rows.append((nb, form, round((time.perf_counter() - t0) / it / 2 * 1e6, 1)))
+            us = (time.perf_counter() - t0) / it / 2 * 1e6
+            rows.append((nb, form, round(us, 1), round(nb / us / 1e3, 2)))
     comm.close()
     dist.destroy_process_group()
     q.put((rank, rows))
@@ -66,4 +67,4 @@ if __name__ == "__main__":
     res = dict(q.get(timeout=300) for _ in range(2))
     for p in ps:
         p.join(timeout=60)
-    print("p2p half-round-trip us (bytes, form, us):", res[0], flush=True)
+    print("p2p half-round-trip (bytes, form, us, GB/s):", res[0], flush=True)

@@ -31,6 +31,7 @@
 // partition (which tree an element gets) always follows the reference
 // algorithm over the full count, so chunking never changes results.
 #include <hip/hip_runtime.h>
+#include <thread>
 #include <rccl/rccl.h>
 #include <stdint.h>
 #include <stdio.h>
@@ -2208,6 +2209,7 @@ static int req_start(mx_request *q) {
 static int req_complete(mx_request *q) {
   mx_comm *c = q->c;
   q->active = 0;
+  if (q->kind == RQ_SEND || q->kind == RQ_RECV) mx::p2p_finish(q);
   if (--c->pending == 0) prof_collect(c);
   if (c->err_host && *(volatile int *)c->err_host) {
     const int e = *(volatile int *)c->err_host;
@@ -2439,6 +2441,10 @@ extern "C" int mx_test(mx_request_t *q, int *flag) {
   *flag = 1;
   if (!q->active) return MX_SUCCESS;   // completed or inactive persistent: MPI_Test gives true
   if (fast_done(q)) return req_complete(q);
+  if (q->fast == 2) {                  // a rendezvous send: only its status word tells
+    *flag = 0;
+    return MX_SUCCESS;
+  }
   const hipError_t e = hipEventQuery(q->done);
   if (e == hipErrorNotReady) {
     *flag = 0;
@@ -2460,8 +2466,10 @@ extern "C" int mx_wait(mx_request_t *q) {
   if (q->fast && q->status) {
     for (;;) {
       if (fast_done(q)) return req_complete(q);
-      if (std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0).count() > kWaitSpinUs)
-        break;
+      if (std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0).count() > kWaitSpinUs) {
+        if (q->fast != 2) break;
+        std::this_thread::sleep_for(std::chrono::microseconds(20));   // a rendezvous send: no event to block on
+      }
     }
   }
   for (;;) {
@@ -2478,6 +2486,10 @@ extern "C" int mx_wait(mx_request_t *q) {
 extern "C" int mx_request_stream_wait(mx_request_t *q, void *stream) {
   if (!q) return MX_ERR_ARG;
   if (!q->active) return MX_SUCCESS;
+  if (q->fast == 2) {   // a rendezvous send has no event: the host waits for its status word
+    while (!fast_done(q)) std::this_thread::sleep_for(std::chrono::microseconds(20));
+    return MX_SUCCESS;
+  }
   return hipStreamWaitEvent((hipStream_t)stream, q->done, 0) == hipSuccess ? MX_SUCCESS : MX_ERR_HIP;
 }
 

@@ -23,12 +23,19 @@ constexpr size_t FLAG_WORDS = OS_COUNTER + 8;
 // ---- point-to-point channels (mx_p2p.hip) --------------------------------
 // Every rank owns one mailbox per source rank after the collective staging:
 // a header ring of P2P_H message envelopes and P2P_L lanes of P2P_S chunk
-// slots of P2P_C bytes.  Counters (cumulative, per pair):
+// slots of P2P_C bytes.  Lanes [0, P2P_LE) carry eager messages (at most
+// P2P_STASH_C bytes, pushed as soon as they are sent); lanes [P2P_LE, P2P_L)
+// carry rendezvous messages (larger ones), whose data moves only after the
+// matching receive has cleared it (CTS), so a large message no receive wants
+// yet never blocks the pair's later messages.  Counters (cumulative, per pair):
 //   posted[src]          my flags: envelopes src has written into my mailbox
 //   filled[src][lane]    my flags: chunks src has written into my lane
 //   seen[dst][lane]      my flags (written by dst): envelopes dst has read
 //   drained[dst][lane]   my flags (written by dst): chunks dst has consumed
-constexpr int P2P_L = 64;
+//   cts[dst]             my flags (written by dst): {seq, ticket} of the
+//                        rendezvous message dst has cleared last
+constexpr int P2P_LE = 8;
+constexpr int P2P_L = P2P_LE + 64;
 constexpr int P2P_S = 4;
 constexpr size_t P2P_C = 64 << 10;
 constexpr int P2P_H = 8;
@@ -38,23 +45,57 @@ constexpr size_t P2P_POSTED = FLAG_WORDS + 8;
 constexpr size_t P2P_FILLED = P2P_POSTED + MAXR;
 constexpr size_t P2P_SEEN = P2P_FILLED + (size_t)MAXR * P2P_L;
 constexpr size_t P2P_DRAINED = P2P_SEEN + (size_t)MAXR * P2P_L;
-constexpr size_t ALL_FLAG_WORDS = P2P_DRAINED + (size_t)MAXR * P2P_L;
+constexpr size_t P2P_CTS = P2P_DRAINED + (size_t)MAXR * P2P_L;
+constexpr size_t ALL_FLAG_WORDS = P2P_CTS + 2 * (size_t)MAXR;
 
 // Unexpected messages: a receive whose tag does not match the pair's next
-// envelope drains that message into a stash slot (up to P2P_STASH_N
-// messages of at most P2P_STASH_C bytes per source) and goes on to the next
-// envelope; later receives match the stash first, oldest first (MPI's
-// per-pair order among the messages a receive could match).
+// envelope sets that message aside and goes on to the next envelope; later
+// receives match what was set aside first, oldest first (MPI's per-pair
+// order among the messages a receive could match).  An eager message is
+// drained into a stash slot (P2P_STASH_N per source, P2P_STASH_C bytes
+// each); a rendezvous message only has its envelope recorded (P2P_DEFER_N
+// per source) -- its data stays with the sender until a receive clears it.
 constexpr int P2P_STASH_N = 8;
 constexpr size_t P2P_STASH_C = 256 << 10;
+constexpr int P2P_DEFER_N = 32;
 struct P2PStashEntry { uint64_t valid; int64_t tag; uint64_t bytes; uint64_t seq; };
 
 // device-local sequence state of the channels (not shared)
-struct P2PSendState { uint64_t msgs; uint64_t lane_chunks[P2P_L]; };
+struct P2PSendState {
+  uint64_t msgs;
+  uint64_t lane_chunks[P2P_L];
+  uint64_t cts_served;                 // CTS tickets of this destination taken
+};
 struct P2PRecvState {
   uint64_t lane_msgs[P2P_L];
   uint64_t lane_chunks[P2P_L];
-  P2PStashEntry stash[P2P_STASH_N];   // written only by the last lane of a receive kernel
+  uint64_t cts_sent;                   // CTS tickets issued to this source
+  uint64_t held;                       // valid entries in stash + defer (0: skip the scan)
+  P2PStashEntry stash[P2P_STASH_N];    // written only by the last lane of a receive kernel
+  P2PStashEntry defer[P2P_DEFER_N];    // likewise
+};
+
+// Rendezvous sends waiting for their CTS (mapped host memory, written by the
+// host when the send is posted, read by the rendezvous pick kernel)
+constexpr int P2P_RNDV_Q = 256;
+struct P2PRndvEntry {
+  const char *buf;
+  uint64_t bytes, seq;
+  int64_t *done;       // device address of the request's status[4]
+  int32_t dst, valid;
+};
+struct P2PRndvTable {
+  P2PRndvEntry e[P2P_RNDV_Q];
+  int32_t abort;       // communicator teardown: pending picks give up
+};
+// the message the running rendezvous kernel's workgroup 0 picked (device
+// memory, read by its other workgroups once `gen` moves)
+struct P2PRndvCur {
+  const char *buf;
+  uint64_t bytes;
+  int64_t *done;
+  int32_t dst, ok;
+  uint64_t gen;        // rendezvous kernels that have published a pick
 };
 
 }  // namespace mx
@@ -118,10 +159,20 @@ struct mx_comm {
   mx::P2PSendState *p2p_send;   // [size]
   mx::P2PRecvState *p2p_recv;   // [size]
   char *p2p_stash;              // [size][P2P_STASH_N][P2P_STASH_C] unexpected-message payloads
-  hipStream_t p2p_stream[2];
+  // streams: [0] sends (envelopes, eager data), [1] receives, [2] rendezvous
+  // data; all three spin on the device, so they are created at the highest
+  // priority, whose hardware queues the process's ordinary streams do not
+  // share
+  hipStream_t p2p_stream[3];
   hipEvent_t p2p_ev;
-  uint64_t *p2p_lanes;     // device: finished-lane counters of the two streams
-  uint64_t p2p_kseq[2];    // transfer kernels enqueued per stream
+  uint64_t *p2p_lanes;     // device: finished-lane counters of the three streams
+  uint64_t p2p_ltot[3];    // lanes (workgroups) of the transfer kernels enqueued per stream
+  uint64_t p2p_host_msgs[mx::MAXR];   // envelopes enqueued per destination (the device's msgs)
+  mx::P2PRndvTable *p2p_rndv;        // mapped host: pending rendezvous sends
+  mx::P2PRndvTable *p2p_rndv_dev;    // its device address
+  mx::P2PRndvCur *p2p_rndv_cur;      // device
+  uint64_t p2p_rndv_gen;             // rendezvous kernels enqueued
+  std::vector<int> *p2p_rndv_free;   // free table slots
   unsigned p2p_any_rr;   // MPI_ANY_SOURCE: source the next pick scans first
 };
 
@@ -143,7 +194,10 @@ struct mx_request {
   // (mapped host memory: received bytes, envelope tag, error)
   int peer, tag;
   int64_t *status;   // [0] bytes [1] tag [2] error [3] source [4] done (P2P_STATUS_WORDS)
-  int fast;          // completion by status[4] (no unpack kernel after the transfer)
+  int fast;          // completion by status[4]: 1 also by the event, 2 only by status[4]
+                     // (a rendezvous send: its data moves on whichever kernel takes its CTS)
+  int rndv;          // rendezvous send: table slot + 1, else 0
+  void *tmp;         // packed staging freed at completion (a rendezvous send of a datatype)
   const struct mx_ddt *ddt;   // non-contiguous user layout (count instances), or null
 };
 
@@ -158,6 +212,8 @@ int req_submit(mx_request *q, mx_request_t **out);
 void req_discard(mx_request *q);
 int p2p_setup(mx_comm *c);
 void p2p_release(mx_comm *c);
+// a point-to-point request completed: release its rendezvous slot / staging
+void p2p_finish(mx_request *q);
 // status blocks (P2P_STATUS_WORDS x int64, mapped host memory): from a process-wide
 // pool allocated once (never released, so a request may outlive its
 // communicator), else one hipHostMalloc each

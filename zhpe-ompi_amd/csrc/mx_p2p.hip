@@ -40,6 +40,7 @@
 // holds the delivered byte count.  Non-contiguous layouts are packed /
 // unpacked by the device convertor (mx_convertor.h) around the stream.
 #include <hip/hip_runtime.h>
+#include <stdlib.h>
 #include <string.h>
 
 #include <algorithm>
@@ -88,17 +89,24 @@ __device__ __forceinline__ void p2p_copy(char *dst, const char *src, uint64_t le
   }
 }
 
-// stripe of lane l: 16-byte multiples of at least kMinStripe, the last
-// lanes short or empty -- a small message moves in one or a few lanes (each
-// lane with data pays a drained / filled handshake per chunk; 4 KiB spread
-// over all 64 lanes cost 9 us more per hop than 8 B in one)
+// stripe of lane l among the nl lanes from `first` (eager: [0, P2P_LE), at
+// most 32 KiB each; rendezvous: [P2P_LE, P2P_L)): 16-byte multiples of at least kMinStripe,
+// the last lanes short or empty -- a small message moves in one or a few
+// lanes (each lane with data pays a drained / filled handshake per chunk;
+// 4 KiB spread over all 64 lanes cost 9 us more per hop than 8 B in one)
 constexpr uint64_t kMinStripe = 16 << 10;
-__device__ __forceinline__ void p2p_lane(uint64_t bytes, int l, uint64_t *lo, uint64_t *hi) {
-  uint64_t stripe = ((bytes + P2P_L - 1) / P2P_L + 15) & ~(uint64_t)15;
+__device__ __forceinline__ void p2p_lane(uint64_t bytes, int l, int first, int nl, uint64_t *lo, uint64_t *hi) {
+  const int j = l - first;
+  if (j < 0 || j >= nl) {
+    *lo = *hi = 0;
+    return;
+  }
+  uint64_t stripe = ((bytes + nl - 1) / nl + 15) & ~(uint64_t)15;
   if (stripe < kMinStripe) stripe = kMinStripe;
-  *lo = std::min<uint64_t>(bytes, (uint64_t)l * stripe);
+  *lo = std::min<uint64_t>(bytes, (uint64_t)j * stripe);
   *hi = std::min<uint64_t>(bytes, *lo + stripe);
 }
+constexpr int P2P_LR = P2P_L - P2P_LE;   // rendezvous lanes
 
 // Host-visible completion of a transfer kernel: every lane workgroup counts
 // itself out on a device counter (kernels of one internal stream run one
@@ -117,22 +125,46 @@ struct P2PDone {
 // lane with data): make it visible device-wide before counting out -- work
 // the host launches once `done` is seen may run on any XCD.  Send lanes
 // fenced every chunk already; lanes without data have nothing to publish.
-__device__ __forceinline__ void lane_finished(const P2PDone &f, bool wrote) {
+// Returns whether this was the kernel's last lane.
+__device__ __forceinline__ bool lane_finished(const P2PDone &f, bool wrote) {
   __syncthreads();
+  bool last = false;
   if (threadIdx.x == 0) {
     if (wrote) __threadfence();
     const uint64_t old = __hip_atomic_fetch_add(f.lanes, (uint64_t)1, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
-    if (old + 1 == f.target && f.done) __hip_atomic_store(f.done, (int64_t)1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    last = old + 1 == f.target;
+    if (last && f.done) __hip_atomic_store(f.done, (int64_t)1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
   }
+  return last;
 }
 
-struct P2PSendArgs;
-__device__ __forceinline__ void send_body(const P2PSendArgs &a);
+// Push [lo, hi) of `src` through lane l's chunk slots of mailbox `box`.
+__device__ __forceinline__ bool send_stream(int l, uint64_t lo, uint64_t hi, const char *src, char *box,
+                                            uint64_t *filled, const uint64_t *drained, P2PSendState *st,
+                                            uint64_t t0, uint64_t tmo, int *err) {
+  __shared__ int ok;
+  uint64_t k = st->lane_chunks[l];   // this lane's counter: read and written by this workgroup only
+  for (uint64_t pos = lo; pos < hi; pos += P2P_C) {
+    const uint64_t len = std::min<uint64_t>(P2P_C, hi - pos);
+    k++;
+    if (threadIdx.x == 0) ok = p2p_wait_ge(drained + l, k > P2P_S ? k - P2P_S : 0, t0, tmo, err);
+    __syncthreads();
+    if (!ok) return false;
+    char *slot = box + 4096 + ((size_t)l * P2P_S + (size_t)((k - 1) % P2P_S)) * P2P_C;
+    p2p_copy(slot, src + pos, len);
+    __threadfence_system();   // my stores reach the peer before the counter moves
+    __syncthreads();
+    if (threadIdx.x == 0) __hip_atomic_store(filled + l, k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
+  if (threadIdx.x == 0) st->lane_chunks[l] = k;
+  return true;
+}
 
 struct P2PSendArgs {
   const char *buf;
   uint64_t bytes;
   int64_t tag;
+  int rndv;                  // rendezvous: the envelope only (the data follows its CTS)
   char *box;                 // the receiver's mailbox for me
   uint64_t *posted;          // receiver's flags: posted[me]
   uint64_t *filled;          // receiver's flags: filled[me][lane]
@@ -144,15 +176,10 @@ struct P2PSendArgs {
   P2PDone fin;
 };
 
+// one workgroup per eager lane; lane 0 also writes the envelope
 __global__ void __launch_bounds__(kP2PThreads) k_p2p_send(P2PSendArgs a) {
-  send_body(a);
-  lane_finished(a.fin, false);
-}
-
-__device__ __forceinline__ void send_body(const P2PSendArgs &a) {
   const int l = blockIdx.x;
   const uint64_t t0 = wall_clock64();
-  __shared__ int ok;
   __shared__ int s_seen_bad;
   if (l == 0) {
     // envelope: the header slot is free once every lane of the receiver has
@@ -170,29 +197,133 @@ __device__ __forceinline__ void send_body(const P2PSendArgs &a) {
       volatile uint64_t *h = reinterpret_cast<volatile uint64_t *>(a.box + (m % P2P_H) * P2P_HDR);
       h[0] = a.bytes;
       h[1] = (uint64_t)a.tag;
+      h[2] = (uint64_t)a.rndv;
       __threadfence_system();
       __hip_atomic_store(a.posted, m + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
       a.st->msgs = m + 1;
     }
   }
-  uint64_t lo, hi;
-  p2p_lane(a.bytes, l, &lo, &hi);
-  uint64_t k = a.st->lane_chunks[l];   // this lane's counter: read and written by this workgroup only
-  for (uint64_t pos = lo; pos < hi; pos += P2P_C) {
-    const uint64_t len = std::min<uint64_t>(P2P_C, hi - pos);
-    k++;
-    if (threadIdx.x == 0) ok = p2p_wait_ge(a.drained + l, k > P2P_S ? k - P2P_S : 0, t0, a.timeout_ticks, a.err);
-    __syncthreads();
-    if (!ok) return;
-    char *slot = a.box + 4096 + ((size_t)l * P2P_S + (size_t)((k - 1) % P2P_S)) * P2P_C;
-    p2p_copy(slot, a.buf + pos, len);
-    __threadfence_system();   // my stores reach the peer before the counter moves
-    __syncthreads();
-    if (threadIdx.x == 0) __hip_atomic_store(a.filled + l, k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  if (!a.rndv) {
+    uint64_t lo, hi;
+    p2p_lane(a.bytes, l, 0, P2P_LE, &lo, &hi);
+    send_stream(l, lo, hi, a.buf, a.box, a.filled, a.drained, a.st, t0, a.timeout_ticks, a.err);
   }
-  if (threadIdx.x == 0) a.st->lane_chunks[l] = k;
+  lane_finished(a.fin, false);
 }
 
+// ---- rendezvous sends ------------------------------------------------------
+// Each rendezvous send enqueues one rendezvous kernel on the rendezvous
+// stream.  Its workgroup 0 waits until some destination has cleared a
+// message of this process (its CTS ticket moved past what was served) and
+// publishes that message; every workgroup then streams its lane's stripe of
+// it -- whichever message it is: receivers clear messages in their own
+// matching order and the kernels are interchangeable, so no message waits
+// behind another.  (Workgroup 0 is dispatched first, so the waiting
+// workgroups never hold back the one they wait for.)
+struct P2PRndvArgs {
+  P2PRndvCur *cur;
+  uint64_t gen;              // this kernel's publication number
+  const uint64_t *cts0;      // my flags: cts[0]
+  int n;
+  const P2PRndvTable *tab;   // device address of the mapped table
+  char *box[MAXR];           // box[d]: d's mailbox for me
+  uint64_t *filled[MAXR];    // filled[d]: d's flags, filled[me][lane]
+  const uint64_t *drained0;  // my flags: drained[0][lane]
+  P2PSendState *st0;
+  uint64_t timeout_ticks;
+  int *err;
+  P2PDone fin;
+};
+
+__device__ __forceinline__ void rndv_pick(const P2PRndvArgs &a) {
+  __shared__ int s_dst, s_hit;
+  __shared__ uint64_t s_seq;
+  const uint64_t t0 = wall_clock64();
+  if (threadIdx.x == 0) {
+    s_dst = -1;
+    for (;;) {
+      for (int d = 0; d < a.n && s_dst < 0; d++) {
+        const uint64_t t = __hip_atomic_load(a.cts0 + 2 * d + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        if (t > a.st0[d].cts_served) {
+          __atomic_thread_fence(__ATOMIC_ACQUIRE);
+          s_seq = __hip_atomic_load(a.cts0 + 2 * d, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+          a.st0[d].cts_served = t;
+          s_dst = d;
+        }
+      }
+      if (s_dst >= 0) break;
+      if (__hip_atomic_load(&a.tab->abort, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM)) {
+        s_dst = -2;
+        break;
+      }
+      __builtin_amdgcn_s_sleep(2);
+      if (wall_clock64() - t0 > a.timeout_ticks) {
+        __hip_atomic_store(a.err, MX_ERR_TIMEOUT, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        s_dst = -3;
+        break;
+      }
+    }
+    s_hit = -1;
+  }
+  __syncthreads();
+  const int d = s_dst;
+  if (d == -3) {   // timed out: release every pending send (they complete with the error)
+    for (int i = threadIdx.x; i < P2P_RNDV_Q; i += blockDim.x)
+      if (a.tab->e[i].valid)
+        __hip_atomic_store(a.tab->e[i].done, (int64_t)1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
+  if (d >= 0) {    // the table is in host memory: scan it with every thread
+    for (int i = threadIdx.x; i < P2P_RNDV_Q; i += blockDim.x) {
+      const P2PRndvEntry &e = a.tab->e[i];
+      if (e.valid && e.dst == d && e.seq == s_seq) s_hit = i;
+    }
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    P2PRndvCur &c = *a.cur;
+    c.ok = 0;
+    if (d >= 0 && s_hit >= 0) {
+      const P2PRndvEntry &e = a.tab->e[s_hit];
+      c.buf = e.buf;
+      c.bytes = e.bytes;
+      c.done = e.done;
+      c.dst = d;
+      c.ok = 1;
+    } else if (d >= 0) {   // a CTS for no pending send: the channel is corrupt
+      __hip_atomic_store(a.err, MX_ERR_STATE, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+    __threadfence();
+    __hip_atomic_store(&c.gen, a.gen, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  __syncthreads();   // the rest of this workgroup reads the pick too
+}
+
+// one workgroup per rendezvous lane (workgroup 0 also picks); the last lane
+// out raises the send request's status word
+__global__ void __launch_bounds__(kP2PThreads) k_p2p_rndv(P2PRndvArgs a) {
+  const int l = P2P_LE + blockIdx.x;
+  if (blockIdx.x == 0) {
+    rndv_pick(a);
+  } else {
+    if (threadIdx.x == 0) {
+      while (__hip_atomic_load(&a.cur->gen, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < a.gen)
+        __builtin_amdgcn_s_sleep(4);
+      __atomic_thread_fence(__ATOMIC_ACQUIRE);
+    }
+    __syncthreads();
+  }
+  const P2PRndvCur c = *a.cur;   // after the acquire fence (or written by this workgroup)
+  if (c.ok) {
+    uint64_t lo, hi;
+    p2p_lane(c.bytes, l, P2P_LE, P2P_LR, &lo, &hi);
+    send_stream(l, lo, hi, c.buf, a.box[c.dst], a.filled[c.dst], a.drained0 + (size_t)c.dst * P2P_L,
+                a.st0 + c.dst, wall_clock64(), a.timeout_ticks, a.err);
+  }
+  if (lane_finished(a.fin, false) && c.ok)
+    __hip_atomic_store(c.done, (int64_t)1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+// ---- receives --------------------------------------------------------------
 struct P2PRecvArgs {
   char *buf;
   uint64_t cap;
@@ -212,22 +343,32 @@ struct P2PRecvArgs {
   P2PDone fin;
 };
 
-// oldest stashed message of `st` a receive with `tag` (< 0: any) matches, or -1
-__device__ __forceinline__ int stash_match(const P2PRecvState *st, int64_t tag) {
-  int hit = -1;
+// oldest message set aside in `st` (stashed eager payload or deferred
+// rendezvous envelope) that a receive with `tag` (< 0: any) matches:
+// {kind 0 stash / 1 defer, slot}, or {-1, -1}
+__device__ __forceinline__ int2 held_match(const P2PRecvState *st, int64_t tag) {
+  int2 hit{-1, -1};
+  if (!st->held) return hit;
   uint64_t best = ~(uint64_t)0;
   for (int k = 0; k < P2P_STASH_N; k++) {
     const P2PStashEntry &e = st->stash[k];
     if (e.valid && (tag < 0 || e.tag == tag) && e.seq < best) {
       best = e.seq;
-      hit = k;
+      hit = int2{0, k};
+    }
+  }
+  for (int k = 0; k < P2P_DEFER_N; k++) {
+    const P2PStashEntry &e = st->defer[k];
+    if (e.valid && (tag < 0 || e.tag == tag) && e.seq < best) {
+      best = e.seq;
+      hit = int2{1, k};
     }
   }
   return hit;
 }
 
 // MX_ANY_SOURCE: wait until some source p has a message this receive can
-// take -- a matching stashed one, or a posted envelope beyond what this
+// take -- a matching held one, or a posted envelope beyond what this
 // process consumed from it (lane 0's message count) -- and store p in
 // status[3] (-1 after a timeout).
 __global__ void k_p2p_pick(const uint64_t *flag0, const P2PRecvState *st0, int n, int start, int64_t tag,
@@ -236,7 +377,7 @@ __global__ void k_p2p_pick(const uint64_t *flag0, const P2PRecvState *st0, int n
   const uint64_t t0 = wall_clock64();
   for (int i = 0; i < n; i++) {
     const int p = (start + i) % n;
-    if (stash_match(st0 + p, tag) >= 0) {
+    if (held_match(st0 + p, tag).x >= 0) {
       __hip_atomic_store(&status[3], (int64_t)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
       return;
     }
@@ -260,24 +401,27 @@ __global__ void k_p2p_pick(const uint64_t *flag0, const P2PRecvState *st0, int n
 }
 
 // What a receive kernel decided, identically in every lane (each lane sees
-// the same stash table -- it changes only at a kernel's end -- and the same
-// envelope sequence): the stash slot it took, and the messages it stashed.
-struct StashPlan {
-  int hit;                         // stash slot delivered, or -1
-  int n;                           // messages stashed by this kernel
-  int slot[P2P_STASH_N];
-  int64_t tag[P2P_STASH_N];
-  uint64_t bytes[P2P_STASH_N], seq[P2P_STASH_N];
+// the same held tables -- they change only at a kernel's end -- and the same
+// envelope sequence): the held message it took, and the messages it set
+// aside.  In LDS, written by thread 0.
+struct HoldPlan {
+  int kind, hit;                   // held message delivered: kind 0 stash / 1 defer, or -1
+  int n;                           // entries set aside by this kernel
+  int defer[P2P_STASH_N + P2P_DEFER_N];
+  int slot[P2P_STASH_N + P2P_DEFER_N];
+  int64_t tag[P2P_STASH_N + P2P_DEFER_N];
+  uint64_t bytes[P2P_STASH_N + P2P_DEFER_N], seq[P2P_STASH_N + P2P_DEFER_N];
 };
 
-// Copy one message of `bytes` through this lane's stripe: from the mailbox
-// (chunk handshake) into dst (dst_cap bytes kept; the rest drained).
-__device__ __forceinline__ bool recv_stream(int l, uint64_t bytes, char *dst, uint64_t dst_cap, const char *box,
-                                            const uint64_t *filled, uint64_t *drained, P2PRecvState *st, uint64_t t0,
-                                            const P2PRecvArgs &a, bool *wrote) {
+// Copy one message of `bytes` through this lane's stripe (lanes [first,
+// first + nl)): from the mailbox (chunk handshake) into dst (dst_cap bytes
+// kept; the rest drained).
+__device__ __forceinline__ bool recv_stream(int l, int first, int nl, uint64_t bytes, char *dst, uint64_t dst_cap,
+                                            const char *box, const uint64_t *filled, uint64_t *drained,
+                                            P2PRecvState *st, uint64_t t0, const P2PRecvArgs &a, bool *wrote) {
   __shared__ int ok;
   uint64_t lo, hi;
-  p2p_lane(bytes, l, &lo, &hi);
+  p2p_lane(bytes, l, first, nl, &lo, &hi);
   uint64_t k = st->lane_chunks[l];
   for (uint64_t pos = lo; pos < hi; pos += P2P_C) {
     const uint64_t len = std::min<uint64_t>(P2P_C, hi - pos);
@@ -299,14 +443,25 @@ __device__ __forceinline__ bool recv_stream(int l, uint64_t bytes, char *dst, ui
   return true;
 }
 
+// first free slot of a held table (valid entries and this kernel's new ones taken), or -1
+__device__ __forceinline__ int held_free(const P2PStashEntry *tab, int n, const HoldPlan &plan, int defer) {
+  for (int k = 0; k < n; k++) {
+    bool taken = tab[k].valid != 0;
+    for (int j = 0; j < plan.n; j++) taken = taken || (plan.defer[j] == defer && plan.slot[j] == k);
+    if (!taken) return k;
+  }
+  return -1;
+}
+
 // one lane of a receive; returns whether this lane stored user data
-__device__ __forceinline__ bool recv_body(const P2PRecvArgs &a, StashPlan &plan, P2PRecvState **stp) {
+__device__ __forceinline__ bool recv_body(const P2PRecvArgs &a, HoldPlan &plan, P2PRecvState **stp) {
   const int l = blockIdx.x;
   const uint64_t t0 = wall_clock64();
   __shared__ int ok;
   __shared__ uint64_t s_bytes;
   __shared__ int64_t s_tag;
   __shared__ uint64_t s_seq;
+  __shared__ int s_rndv;
   int p = a.src;
   if (a.any) {
     p = (int)__hip_atomic_load(&a.status[3], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
@@ -316,37 +471,63 @@ __device__ __forceinline__ bool recv_body(const P2PRecvArgs &a, StashPlan &plan,
   const uint64_t *posted = a.flag0 + P2P_POSTED + p, *filled = a.flag0 + P2P_FILLED + (size_t)p * P2P_L;
   uint64_t *seen = a.peer_flags[p] + P2P_SEEN + (size_t)a.me * P2P_L;
   uint64_t *drained = a.peer_flags[p] + P2P_DRAINED + (size_t)a.me * P2P_L;
+  uint64_t *cts = a.peer_flags[p] + P2P_CTS + 2 * (size_t)a.me;
   P2PRecvState *st = a.st0 + p;
   char *stash = a.stash0 + (size_t)p * P2P_STASH_N * P2P_STASH_C;
   *stp = st;
   bool wrote = false;
-  // (1) a stashed message this receive matches: deliver it, consume no envelope
-  plan.hit = stash_match(st, a.tag);
-  if (plan.hit >= 0) {
-    const P2PStashEntry e = st->stash[plan.hit];
-    uint64_t lo, hi;
-    p2p_lane(e.bytes, l, &lo, &hi);
-    if (lo < hi && lo < a.cap) {
-      p2p_copy(a.buf + lo, stash + (size_t)plan.hit * P2P_STASH_C + lo, std::min(hi, a.cap) - lo);
-      wrote = true;
-    }
+  // clear rendezvous message `seq` with the sender, then take its data
+  // through the rendezvous lanes
+  auto rndv_take = [&](uint64_t seq, uint64_t bytes) -> bool {
     if (l == 0 && threadIdx.x == 0) {
-      a.status[0] = (int64_t)std::min<uint64_t>(e.bytes, a.cap);
-      a.status[1] = e.tag;
-      a.status[2] = e.bytes > a.cap ? MX_ERR_TRUNCATE : 0;
+      const uint64_t t = st->cts_sent + 1;
+      __hip_atomic_store(cts, seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      __threadfence_system();
+      __hip_atomic_store(cts + 1, t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      st->cts_sent = t;
+    }
+    return recv_stream(l, P2P_LE, P2P_LR, bytes, a.buf, a.cap, box, filled, drained, st, t0, a, &wrote);
+  };
+  auto deliver_status = [&](uint64_t bytes, int64_t tag, int err) {
+    if (l == 0 && threadIdx.x == 0) {
+      a.status[0] = (int64_t)std::min<uint64_t>(bytes, a.cap);
+      a.status[1] = tag;
+      a.status[2] = err ? err : bytes > a.cap ? MX_ERR_TRUNCATE : 0;
       __threadfence_system();
     }
+  };
+  // (1) a held message this receive matches: deliver it, consume no envelope
+  const int2 h = held_match(st, a.tag);
+  if (h.x >= 0) {
+    if (threadIdx.x == 0) {
+      plan.kind = h.x;
+      plan.hit = h.y;
+    }
+    const P2PStashEntry e = h.x == 0 ? st->stash[h.y] : st->defer[h.y];
+    if (h.x == 0) {
+      uint64_t lo, hi;
+      p2p_lane(e.bytes, l, 0, P2P_LE, &lo, &hi);
+      if (lo < hi && lo < a.cap) {
+        p2p_copy(a.buf + lo, stash + (size_t)h.y * P2P_STASH_C + lo, std::min(hi, a.cap) - lo);
+        wrote = true;
+      }
+    } else if (!rndv_take(e.seq, e.bytes)) {
+      return wrote;
+    }
+    deliver_status(e.bytes, e.tag, 0);
     return wrote;
   }
-  // (2) envelopes in order: a mismatch goes to a free stash slot
+  // (2) envelopes in order: a mismatch is set aside (eager payload stashed,
+  // rendezvous envelope deferred) while a slot is free
   for (;;) {
     if (threadIdx.x == 0) {
       const uint64_t m = st->lane_msgs[l];
       ok = p2p_wait_ge(posted, m + 1, t0, a.timeout_ticks, a.err);
       if (ok) {
-        const volatile uint64_t *h = reinterpret_cast<const volatile uint64_t *>(box + (m % P2P_H) * P2P_HDR);
-        s_bytes = h[0];
-        s_tag = (int64_t)h[1];
+        const volatile uint64_t *hd = reinterpret_cast<const volatile uint64_t *>(box + (m % P2P_H) * P2P_HDR);
+        s_bytes = hd[0];
+        s_tag = (int64_t)hd[1];
+        s_rndv = (int)hd[2];
         s_seq = m;
         __hip_atomic_store(seen + l, m + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
         st->lane_msgs[l] = m + 1;
@@ -357,55 +538,63 @@ __device__ __forceinline__ bool recv_body(const P2PRecvArgs &a, StashPlan &plan,
     const uint64_t bytes = s_bytes;
     const int64_t tag = s_tag;
     const uint64_t seq = s_seq;
+    const int rndv = s_rndv;
     __syncthreads();          // every thread has read the envelope before the next one
     int slot = -1;
-    if (a.tag >= 0 && tag != a.tag && bytes <= P2P_STASH_C) {
-      for (int k = 0; k < P2P_STASH_N && slot < 0; k++) {
-        bool taken = st->stash[k].valid != 0;
-        for (int j = 0; j < plan.n; j++) taken = taken || plan.slot[j] == k;
-        if (!taken) slot = k;
-      }
+    if (a.tag >= 0 && tag != a.tag) {
+      slot = rndv ? held_free(st->defer, P2P_DEFER_N, plan, 1)
+                  : bytes <= P2P_STASH_C ? held_free(st->stash, P2P_STASH_N, plan, 0) : -1;
     }
     if (slot >= 0) {          // unexpected: keep it for a later receive
-      if (!recv_stream(l, bytes, stash + (size_t)slot * P2P_STASH_C, bytes, box, filled, drained, st, t0, a, &wrote))
-        return wrote;
-      wrote = false;          // stash bytes are not the user's
-      plan.slot[plan.n] = slot;
-      plan.tag[plan.n] = tag;
-      plan.bytes[plan.n] = bytes;
-      plan.seq[plan.n] = seq;
-      plan.n++;
+      if (!rndv) {
+        bool stashed = false;
+        if (!recv_stream(l, 0, P2P_LE, bytes, stash + (size_t)slot * P2P_STASH_C, bytes, box, filled, drained, st,
+                         t0, a, &stashed))
+          return wrote;
+      }
+      if (threadIdx.x == 0) {
+        plan.defer[plan.n] = rndv;
+        plan.slot[plan.n] = slot;
+        plan.tag[plan.n] = tag;
+        plan.bytes[plan.n] = bytes;
+        plan.seq[plan.n] = seq;
+        plan.n++;
+      }
+      __syncthreads();
       continue;
     }
-    // this receive's message (or one that cannot be stashed: MX_ERR_TAG)
-    if (!recv_stream(l, bytes, a.buf, a.cap, box, filled, drained, st, t0, a, &wrote)) return wrote;
-    if (l == 0 && threadIdx.x == 0) {
-      a.status[0] = (int64_t)std::min<uint64_t>(bytes, a.cap);
-      a.status[1] = tag;
-      a.status[2] = bytes > a.cap ? MX_ERR_TRUNCATE : (a.tag >= 0 && tag != a.tag) ? MX_ERR_TAG : 0;
-      __threadfence_system();
+    // this receive's message (or one that cannot be set aside: MX_ERR_TAG)
+    if (rndv) {
+      if (!rndv_take(seq, bytes)) return wrote;
+    } else if (!recv_stream(l, 0, P2P_LE, bytes, a.buf, a.cap, box, filled, drained, st, t0, a, &wrote)) {
+      return wrote;
     }
+    deliver_status(bytes, tag, (a.tag >= 0 && tag != a.tag) ? MX_ERR_TAG : 0);
     return wrote;
   }
 }
 
 __global__ void __launch_bounds__(kP2PThreads) k_p2p_recv(P2PRecvArgs a) {
-  StashPlan plan;
-  plan.hit = -1;
-  plan.n = 0;
+  __shared__ HoldPlan plan;
+  if (threadIdx.x == 0) {
+    plan.kind = plan.hit = -1;
+    plan.n = 0;
+  }
+  __syncthreads();
   P2PRecvState *st = nullptr;
   const bool wrote = recv_body(a, plan, &st);
-  // the last lane out commits the stash changes (the table is read by every
-  // lane during the kernel, so it only changes between kernels)
+  // the last lane out commits the held-table changes (the tables are read by
+  // every lane during the kernel, so they only change between kernels)
   __syncthreads();
   if (threadIdx.x == 0) {
     if (wrote) __threadfence();
     const uint64_t old = __hip_atomic_fetch_add(a.fin.lanes, (uint64_t)1, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
     if (old + 1 == a.fin.target) {
       if (st) {
-        if (plan.hit >= 0) st->stash[plan.hit].valid = 0;
+        st->held += (uint64_t)plan.n - (plan.hit >= 0 ? 1 : 0);
+        if (plan.hit >= 0) (plan.kind ? st->defer : st->stash)[plan.hit].valid = 0;
         for (int j = 0; j < plan.n; j++) {
-          P2PStashEntry &e = st->stash[plan.slot[j]];
+          P2PStashEntry &e = (plan.defer[j] ? st->defer : st->stash)[plan.slot[j]];
           e.tag = plan.tag[j];
           e.bytes = plan.bytes[j];
           e.seq = plan.seq[j];
@@ -418,30 +607,51 @@ __global__ void __launch_bounds__(kP2PThreads) k_p2p_recv(P2PRecvArgs a) {
   }
 }
 
+// The internal streams spin on the device (a receive waits for its message,
+// a rendezvous pick for a CTS).  HIP multiplexes a process's streams onto
+// GPU_MAX_HW_QUEUES hardware queues per priority, and a kernel spinning on
+// a queue holds back every kernel queued behind it there, whatever its
+// stream (tools/queue_probe.hip, profiles/r02/queue_probe.txt): created at
+// the highest priority, the channel streams get queues the process's
+// ordinary streams do not share.
+// (MX_P2P_PRIORITY=0: ordinary priority, for measurements)
+static hipError_t p2p_stream_create(hipStream_t *s) {
+  int least = 0, greatest = 0;
+  if (hipDeviceGetStreamPriorityRange(&least, &greatest) != hipSuccess) greatest = 0;
+  const char *e = getenv("MX_P2P_PRIORITY");
+  if (e && atoi(e) == 0) return hipStreamCreateWithFlags(s, hipStreamNonBlocking);
+  return hipStreamCreateWithPriority(s, hipStreamNonBlocking, greatest);
+}
+
 int p2p_setup(mx_comm *c) {
   if (c->p2p_send) return MX_SUCCESS;
   const size_t sb = sizeof(P2PSendState) * c->size, rb = sizeof(P2PRecvState) * c->size;
-  if (hipMalloc((void **)&c->p2p_send, sb) != hipSuccess) return MX_ERR_NOMEM;
-  if (hipMalloc((void **)&c->p2p_recv, rb) != hipSuccess) {
-    (void)hipFree(c->p2p_send);
+  if (hipMalloc((void **)&c->p2p_send, sb) != hipSuccess) {
     c->p2p_send = nullptr;
     return MX_ERR_NOMEM;
   }
-  if (hipMalloc((void **)&c->p2p_lanes, 2 * sizeof(uint64_t)) != hipSuccess) {
-    c->p2p_lanes = nullptr;
+  const bool ok =
+      hipMalloc((void **)&c->p2p_recv, rb) == hipSuccess &&
+      hipMalloc((void **)&c->p2p_lanes, 3 * sizeof(uint64_t)) == hipSuccess &&
+      hipMalloc((void **)&c->p2p_stash, (size_t)c->size * P2P_STASH_N * P2P_STASH_C) == hipSuccess &&
+      hipMalloc((void **)&c->p2p_rndv_cur, sizeof(P2PRndvCur)) == hipSuccess &&
+      hipHostMalloc((void **)&c->p2p_rndv, sizeof(P2PRndvTable), hipHostMallocMapped) == hipSuccess &&
+      hipHostGetDevicePointer((void **)&c->p2p_rndv_dev, c->p2p_rndv, 0) == hipSuccess;
+  if (!ok) {
     p2p_release(c);
     return MX_ERR_NOMEM;
   }
-  if (hipMalloc((void **)&c->p2p_stash, (size_t)c->size * P2P_STASH_N * P2P_STASH_C) != hipSuccess) {
-    c->p2p_stash = nullptr;
-    p2p_release(c);
-    return MX_ERR_NOMEM;
-  }
-  c->p2p_kseq[0] = c->p2p_kseq[1] = 0;
+  memset(c->p2p_rndv, 0, sizeof(P2PRndvTable));
+  c->p2p_rndv_gen = 0;
+  c->p2p_rndv_free = new std::vector<int>();
+  for (int i = P2P_RNDV_Q - 1; i >= 0; i--) c->p2p_rndv_free->push_back(i);
+  c->p2p_ltot[0] = c->p2p_ltot[1] = c->p2p_ltot[2] = 0;
+  for (int j = 0; j < MAXR; j++) c->p2p_host_msgs[j] = 0;
   if (hipMemset(c->p2p_send, 0, sb) != hipSuccess || hipMemset(c->p2p_recv, 0, rb) != hipSuccess ||
-      hipMemset(c->p2p_lanes, 0, 2 * sizeof(uint64_t)) != hipSuccess ||
-      hipStreamCreateWithFlags(&c->p2p_stream[0], hipStreamNonBlocking) != hipSuccess ||
-      hipStreamCreateWithFlags(&c->p2p_stream[1], hipStreamNonBlocking) != hipSuccess ||
+      hipMemset(c->p2p_lanes, 0, 3 * sizeof(uint64_t)) != hipSuccess ||
+      hipMemset(c->p2p_rndv_cur, 0, sizeof(P2PRndvCur)) != hipSuccess ||
+      p2p_stream_create(&c->p2p_stream[0]) != hipSuccess || p2p_stream_create(&c->p2p_stream[1]) != hipSuccess ||
+      p2p_stream_create(&c->p2p_stream[2]) != hipSuccess ||
       hipEventCreateWithFlags(&c->p2p_ev, hipEventDisableTiming) != hipSuccess ||
       hipDeviceSynchronize() != hipSuccess) {
     p2p_release(c);
@@ -451,19 +661,39 @@ int p2p_setup(mx_comm *c) {
 }
 
 void p2p_release(mx_comm *c) {
-  if (c->p2p_stream[0]) (void)hipStreamDestroy(c->p2p_stream[0]);
-  if (c->p2p_stream[1]) (void)hipStreamDestroy(c->p2p_stream[1]);
+  // rendezvous sends no receive ever cleared: their picks give up
+  if (c->p2p_rndv) __atomic_store_n(&c->p2p_rndv->abort, 1, __ATOMIC_RELEASE);
+  if (c->p2p_stream[2]) (void)hipStreamSynchronize(c->p2p_stream[2]);
+  for (int i = 0; i < 3; i++)
+    if (c->p2p_stream[i]) (void)hipStreamDestroy(c->p2p_stream[i]);
   if (c->p2p_ev) (void)hipEventDestroy(c->p2p_ev);
   if (c->p2p_send) (void)hipFree(c->p2p_send);
   if (c->p2p_recv) (void)hipFree(c->p2p_recv);
   if (c->p2p_lanes) (void)hipFree(c->p2p_lanes);
   if (c->p2p_stash) (void)hipFree(c->p2p_stash);
+  if (c->p2p_rndv_cur) (void)hipFree(c->p2p_rndv_cur);
+  if (c->p2p_rndv) (void)hipHostFree(c->p2p_rndv);
+  delete c->p2p_rndv_free;
+  c->p2p_rndv_free = nullptr;
+  c->p2p_rndv = c->p2p_rndv_dev = nullptr;
+  c->p2p_rndv_cur = nullptr;
   c->p2p_lanes = nullptr;
   c->p2p_stash = nullptr;
-  c->p2p_stream[0] = c->p2p_stream[1] = nullptr;
+  c->p2p_stream[0] = c->p2p_stream[1] = c->p2p_stream[2] = nullptr;
   c->p2p_ev = nullptr;
   c->p2p_send = nullptr;
   c->p2p_recv = nullptr;
+}
+
+void p2p_finish(mx_request *q) {
+  mx_comm *c = q->c;
+  if (q->rndv && c->p2p_rndv) {
+    c->p2p_rndv->e[q->rndv - 1].valid = 0;
+    c->p2p_rndv_free->push_back(q->rndv - 1);
+  }
+  q->rndv = 0;
+  if (q->tmp) (void)hipFreeAsync(q->tmp, c->p2p_stream[2] ? c->p2p_stream[2] : nullptr);
+  q->tmp = nullptr;
 }
 
 namespace {
@@ -547,24 +777,46 @@ int p2p_enqueue(mx_request *q, hipStream_t *done_stream) {
   memset(q->status, 0, P2P_STATUS_WORDS * sizeof(int64_t));
   int64_t *st_dev = p2p_status_dev(q->status);
   if (!st_dev) return MX_ERR_HIP;
-  // completion through status[4] when the transfer kernel is the last one
-  P2PDone fin;
-  q->fast = !q->ddt;
-  fin.lanes = c->p2p_lanes + dir;
-  fin.target = (c->p2p_kseq[dir] + 1) * P2P_L;
-  fin.done = q->fast ? st_dev + 4 : nullptr;
-  c->p2p_kseq[dir]++;   // every transfer kernel counts its lanes, flagged or not
   const int me = c->rank, p = q->peer;
   const size_t bytes = q->ddt ? q->count * mx_ddt_size(q->ddt) : q->count;
+  const bool rndv = send && bytes > P2P_STASH_C;
+  if (rndv && c->p2p_rndv_free->empty()) return MX_ERR_NOMEM;   // P2P_RNDV_Q rendezvous sends pending
+  // completion through status[4] when the transfer kernel is the last one
+  // (a send's pack runs before it on the same stream; a receive's unpack
+  // after it); a rendezvous send completes only through status[4], raised
+  // by whichever rendezvous kernel takes its CTS
+  q->fast = rndv ? 2 : (send || !q->ddt) ? 1 : 0;
+  const int nl = send ? P2P_LE : P2P_L;
+  P2PDone fin;
+  fin.lanes = c->p2p_lanes + dir;
+  fin.target = c->p2p_ltot[dir] + nl;
+  fin.done = q->fast == 1 ? st_dev + 4 : nullptr;
+  c->p2p_ltot[dir] += nl;   // every transfer kernel counts its lanes, flagged or not
   char *tmp = nullptr;
   if (q->ddt && bytes && hipMallocAsync((void **)&tmp, bytes, s) != hipSuccess) return MX_ERR_NOMEM;
   if (send) {
     if (tmp && (rc = mx_pack(q->ddt, q->count, q->sbuf, tmp, 0, bytes, s))) return rc;
+    const char *src = tmp ? tmp : (const char *)q->sbuf;
+    if (rndv) {
+      const int slot = c->p2p_rndv_free->back();
+      c->p2p_rndv_free->pop_back();
+      P2PRndvEntry &e = c->p2p_rndv->e[slot];
+      e.buf = src;
+      e.bytes = bytes;
+      e.seq = c->p2p_host_msgs[p];
+      e.done = st_dev + 4;
+      e.dst = p;
+      __atomic_store_n(&e.valid, 1, __ATOMIC_RELEASE);
+      q->rndv = slot + 1;
+      q->tmp = tmp;
+    }
+    c->p2p_host_msgs[p]++;
     P2PSendArgs a;
     memset(&a, 0, sizeof a);
-    a.buf = tmp ? tmp : (const char *)q->sbuf;
+    a.buf = src;
     a.bytes = bytes;
     a.tag = q->tag;
+    a.rndv = rndv;
     a.box = c->peer_staging[p] + c->p2p_off + (size_t)me * P2P_BOX;
     a.posted = c->peer_flags[p] + P2P_POSTED + me;
     a.filled = c->peer_flags[p] + P2P_FILLED + (size_t)me * P2P_L;
@@ -574,8 +826,34 @@ int p2p_enqueue(mx_request *q, hipStream_t *done_stream) {
     a.timeout_ticks = c->timeout_ticks;
     a.err = c->err_dev;
     a.fin = fin;
-    hipLaunchKernelGGL(k_p2p_send, dim3(P2P_L), dim3(kP2PThreads), 0, s, a);
+    hipLaunchKernelGGL(k_p2p_send, dim3(P2P_LE), dim3(kP2PThreads), 0, s, a);
     if ((rc = mx_check_launch())) return rc;
+    if (rndv) {
+      // the rendezvous kernel needs no event: the CTS it waits for follows
+      // the envelope, which follows the caller's stream and the pack
+      P2PRndvArgs ra;
+      memset(&ra, 0, sizeof ra);
+      ra.cur = c->p2p_rndv_cur;
+      ra.gen = ++c->p2p_rndv_gen;
+      ra.cts0 = c->flagmem + P2P_CTS;
+      ra.n = c->size;
+      ra.tab = c->p2p_rndv_dev;
+      for (int j = 0; j < c->size; j++) {
+        ra.box[j] = c->peer_staging[j] + c->p2p_off + (size_t)me * P2P_BOX;
+        ra.filled[j] = c->peer_flags[j] + P2P_FILLED + (size_t)me * P2P_L;
+      }
+      ra.drained0 = c->flagmem + P2P_DRAINED;
+      ra.st0 = c->p2p_send;
+      ra.timeout_ticks = c->timeout_ticks;
+      ra.err = c->err_dev;
+      ra.fin.lanes = c->p2p_lanes + 2;
+      ra.fin.target = c->p2p_ltot[2] + P2P_LR;
+      ra.fin.done = nullptr;
+      c->p2p_ltot[2] += P2P_LR;
+      hipLaunchKernelGGL(k_p2p_rndv, dim3(P2P_LR), dim3(kP2PThreads), 0, c->p2p_stream[2], ra);
+      if ((rc = mx_check_launch())) return rc;
+      return MX_SUCCESS;   // tmp is freed when the request completes (p2p_finish)
+    }
   } else {
     q->status[3] = p;
     P2PRecvArgs a;
