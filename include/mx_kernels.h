@@ -163,7 +163,9 @@ int mx_alloc(size_t bytes, void **p);      /* device memory                */
 int mx_free(void *p);
 /* Any direction (host pageable / pinned / device), ordered on `stream`. */
 int mx_memcpy(void *dst, const void *src, size_t bytes, void *stream);
-/* A non-blocking stream (does not synchronise with the legacy default one). */
+/* A non-blocking stream (does not synchronise with the legacy default one),
+ * at the highest stream priority so the kernels that spin on it (request
+ * collectives) never share a hardware queue with ordinary streams. */
 int mx_stream_create(void **stream);
 /* A blocking stream: ordered with the legacy default stream implicitly (no
  * per-call event; same host cost as the default stream). */

@@ -608,12 +608,26 @@ def _overlap_worker(rank, n, port, q):
         # warm up: the device communicator is created at the first eligible call
         assert H.mxh_allreduce(X.data_ptr(), R.data_ptr(), count, f32, SUM, comm) == 0
         Y = torch.arange(1 << 20, dtype=torch.float32, device="cuda")
+        # ordinary streams in use (MX_TEST_BUSY_STREAMS): more than there are
+        # hardware queues, so every ordinary queue is shared -- a kernel on
+        # any of them would wait behind a collective spinning on that queue
+        busy = [torch.cuda.Stream() for _ in range(int(os.environ.get("MX_TEST_BUSY_STREAMS", "0")))]
+        Z = [torch.zeros(1024, device="cuda") for _ in busy]
+        for s_, z in zip(busy, Z):
+            with torch.cuda.stream(s_):
+                z.add_(1.0)
+        torch.cuda.synchronize()
         t0 = time.time()
         r = vp()
         if rank == 0:
             assert H.mxh_iallreduce(X.data_ptr(), R.data_ptr(), count, f32, SUM, comm, ctypes.byref(r)) == 0
             y = Y.cpu()                      # default-stream device copy while rank 1 is not in the collective
             assert float(y[-1]) == float((1 << 20) - 1)
+            for s_, z in zip(busy, Z):       # and work on every ordinary stream
+                with torch.cuda.stream(s_):
+                    z.add_(1.0)
+                s_.synchronize()
+                assert float(z[0]) == 2.0
             dist.barrier()
         else:
             dist.barrier()
@@ -630,11 +644,13 @@ def _overlap_worker(rank, n, port, q):
 
 
 @pytest.mark.gpu
-def test_iallreduce_does_not_block_the_default_stream():
+@pytest.mark.parametrize("busy_streams", [0, 8])
+def test_iallreduce_does_not_block_the_default_stream(busy_streams, monkeypatch):
     import torch
     if not torch.cuda.is_available():
         pytest.skip("needs a GPU")
     os.environ["HSA_ENABLE_IPC_MODE_LEGACY"] = "0"
+    monkeypatch.setenv("MX_TEST_BUSY_STREAMS", str(busy_streams))
     got = _run_fn(_overlap_worker, 2)
     for r in range(2):
         assert got[r]["rc"] == 0, got[r]

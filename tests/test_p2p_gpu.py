@@ -354,3 +354,78 @@ def test_point_to_point(n):
     payloads.append(last)
     assert sorted(payloads) == sorted(expect.values())
     assert got[0]["any_specific"] == _data(6000, 50001).tobytes()
+
+
+def _busy_worker(rank, n, port, q):
+    """A receive posted first spins on the device until its message comes;
+    the peer only sends after work on each of 8 ordinary streams of its own
+    (more than there are hardware queues, so they share every ordinary
+    queue) has finished.  The channel streams run at the highest priority,
+    on queues no ordinary stream shares, so that work is never queued behind
+    the spinning receive."""
+    import time
+    import torch.distributed as dist
+    os.environ["HSA_ENABLE_IPC_MODE_LEGACY"] = "0"
+    try:
+        dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=n)
+        torch.cuda.set_device(0)
+        mxompi.init(0)
+
+        def ag(b):
+            out = [None] * n
+            dist.all_gather_object(out, b)
+            return out
+
+        comm = mxompi.Comm(rank, n, ag, device=0, staging_bytes=1 << 20)
+        comm.set_timeout(20.0)
+        busy = [torch.cuda.Stream() for _ in range(8)]
+        Z = [torch.zeros(1024, device="cuda") for _ in busy]
+        peer = 1 - rank
+        t0 = time.time()
+        out = {}
+        for nb in (4096, 3 << 20):            # eager, rendezvous
+            x = _dev(_data(900 + rank, nb))
+            y = torch.zeros(nb, dtype=torch.uint8, device="cuda")
+            r = comm.irecv(y.data_ptr(), nb, peer, tag=nb & 0xffff)
+            dist.barrier()                    # both receives are spinning now
+            for s_, z in zip(busy, Z):
+                with torch.cuda.stream(s_):
+                    z.add_(1.0)
+                s_.synchronize()
+            s = comm.isend(x.data_ptr(), nb, peer, tag=nb & 0xffff)
+            r.wait(); s.wait(); r.free(); s.free()
+            out[nb] = y.cpu().numpy().tobytes()
+        res = {"seconds": time.time() - t0, "out": out, "z": [float(z[0]) for z in Z]}
+        comm.close()
+        dist.destroy_process_group()
+        q.put((rank, "ok", res))
+    except Exception as e:  # noqa: BLE001
+        import traceback
+        q.put((rank, "err", traceback.format_exc() + str(e)))
+
+
+def test_channel_streams_do_not_block_ordinary_streams():
+    import torch.multiprocessing as mp
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_busy_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    got = {}
+    try:
+        for _ in range(2):
+            rank, status, payload = q.get(timeout=120)
+            assert status == "ok", payload
+            got[rank] = payload
+    finally:
+        for p in procs:
+            p.join(timeout=30 if len(got) == 2 else 5)
+            if p.is_alive():
+                p.terminate()
+                p.join(timeout=10)
+    for r in range(2):
+        assert got[r]["seconds"] < 10.0, got[r]["seconds"]
+        assert got[r]["z"] == [2.0] * 8
+        for nb in (4096, 3 << 20):
+            assert got[r]["out"][nb] == _data(900 + (1 - r), nb).tobytes(), (r, nb)

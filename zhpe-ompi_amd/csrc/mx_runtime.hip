@@ -178,11 +178,18 @@ extern "C" int mx_memcpy(void *dst, const void *src, size_t bytes, void *stream)
   return mx_hip_rc(hipMemcpyAsync(dst, src, bytes, hipMemcpyDefault, (hipStream_t)stream));
 }
 
+// A non-blocking stream at the highest priority: the collectives queued on
+// it spin on their peers, and a spinning kernel holds back every kernel
+// behind it on its hardware queue, whatever the stream; the highest
+// priority's queues are not shared with the process's ordinary streams
+// (profiles/r02/queue_probe.txt).
 extern "C" int mx_stream_create(void **stream) {
   if (!stream) return MX_ERR_ARG;
   if (int rc = mx_ensure_init()) return rc;
   hipStream_t s = nullptr;
-  if (hipStreamCreateWithFlags(&s, hipStreamNonBlocking) != hipSuccess) return MX_ERR_HIP;
+  int least = 0, greatest = 0;
+  if (hipDeviceGetStreamPriorityRange(&least, &greatest) != hipSuccess) greatest = 0;
+  if (hipStreamCreateWithPriority(&s, hipStreamNonBlocking, greatest) != hipSuccess) return MX_ERR_HIP;
   *stream = s;
   return MX_SUCCESS;
 }
