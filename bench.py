@@ -181,6 +181,28 @@ def bench_allreduce(torch, mx, dist, rank, world, dev, steps, warmup, nbytes=256
         comm.allreduce(x.data_ptr(), out.data_ptr(), count, "FLOAT", "SUM", "auto", sp)
     st = comm.stats(reset=True)
     comm.set_profiling(False)
+    # data-movement A/B at the headline size (results are identical under
+    # all three): zero-copy between registered user buffers (the default above
+    # 4 MiB per rank), and the staged path under PUSH and PULL (the staged
+    # default: PULL when the ranks sit on different GPUs, PUSH on one GPU)
+    proto_default = comm.protocol()
+    proto_ab = {"staged_protocol": proto_default,
+                "timed_path": "zero_copy" if st["zero_copy_calls"] else "staged"}
+    for name, reg, proto in (("staged_push", 0, "push"), ("staged_pull", 0, "pull"), ("zero_copy", 4 << 20, None)):
+        try:
+            comm.set_reg_min(reg)
+        except mx.MxError:
+            if reg:
+                proto_ab[name] = {"error": "registration unavailable"}
+                continue
+        comm.set_protocol(proto or proto_default)
+        for _ in range(2):
+            comm.allreduce(x.data_ptr(), out.data_ptr(), count, "FLOAT", "SUM", "auto", sp)
+        k = max(3, steps // 2)
+        tp = timed("auto", k)
+        proto_ab[name] = {"busbw_gbs": round(nbytes / (tp / k) / 1e9 * 2 * (world - 1) / world, 2),
+                          "ms": round(tp / k * 1e3, 4)}
+    comm.set_protocol(proto_default)
     sweep = allreduce_sweep(torch, mx, dist, comm, world, x, out, sp, flags)
     cfge = cfg_e(torch, mx, dist, comm, world, rank, sp)
     extra = {}
@@ -201,6 +223,7 @@ def bench_allreduce(torch, mx, dist, rank, world, dev, steps, warmup, nbytes=256
                                "segmented-ring fold order), all-peer xGMI",
                    "count": count, "bytes": nbytes, "algorithm": "auto",
                    "parallelism": f"allreduce-{world}", "algbw_gbs": round(algbw, 2),
+                   "data_path_ab": proto_ab,
                    "busbw_formula": "algbw*2(n-1)/n", **extra},
         "roofline": {"bound": "hbm", "achieved": round(fold_bytes / (fold_ms * 1e-3) / 1e9, 1) if fold_ms else None,
                      "peak": HBM_PEAK_GBS, "unit": "GB/s",

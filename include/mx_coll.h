@@ -95,6 +95,37 @@ int mx_comm_rank(const mx_comm_t *comm);
  * the communicator fails with it. */
 int mx_comm_set_timeout(mx_comm_t *comm, double seconds);
 
+/* Data movement of the staged (above the one-shot range) allreduce.  Results
+ * are identical under every protocol (same fold programs); only the traffic
+ * pattern differs:
+ *   PUSH  each rank writes part p of its input into rank p's staging, then
+ *         rank p folds locally and writes the result to every peer (each
+ *         phase loads the links in one direction);
+ *   PULL  each rank copies its input into its own staging (local HBM), then
+ *         rank p's fold reads part p of every peer's staging over xGMI while
+ *         it writes the result to every peer (both directions at once).
+ * AUTO (the default) is PULL when some peer runs on another GPU and PUSH when
+ * every rank shares one device; env MX_ALLREDUCE_PROTO=push|pull overrides
+ * it at creation.  Every rank of a communicator must use the same protocol:
+ * set it on all ranks between collectives.  Returns the protocol in force
+ * (MX_PROTO_PUSH / MX_PROTO_PULL) or an error. */
+enum { MX_PROTO_AUTO = 0, MX_PROTO_PUSH = 1, MX_PROTO_PULL = 2 };
+int mx_comm_set_protocol(mx_comm_t *comm, int proto);
+int mx_comm_get_protocol(const mx_comm_t *comm);
+
+/* Zero-copy allreduce between user buffers (the device-buffer registration
+ * of btl/smcuda + rcache/gpusm, done per call): a blocking mx_allreduce of at
+ * least `min_bytes` per rank publishes the IPC handles of its sbuf / rbuf
+ * allocations in a host shared-memory page of the communicator; every peer
+ * maps them (cached, LRU) and rank p folds part p straight from every
+ * rank's sbuf into every rank's rbuf -- no staging copies.  A call falls back
+ * to the staged path on every rank when any rank's buffers cannot be
+ * exported or mapped, or their misalignments mod 16 differ.  Default
+ * 4 MiB (env MX_REG_MIN at creation; 0 = off).  Same value on every rank.
+ * Returns MX_ERR_UNSUPPORTED when the communicator has no registration page
+ * (single rank, local communicator, or /dev/shm unavailable on some rank). */
+int mx_comm_set_reg_min(mx_comm_t *comm, size_t min_bytes);
+
 /* Per-communicator kernel timing (HIP events on the collective's stream),
  * off by default.  Times are summed over calls since the last reset. */
 typedef struct mx_coll_stats {
@@ -105,6 +136,10 @@ typedef struct mx_coll_stats {
     double push_ms;            /* scatter-push copies to peers' staging     */
     double gather_ms;          /* gather-area -> rbuf copies                */
     double total_ms;           /* first -> last event of each call          */
+    /* counted whether or not profiling is on: */
+    uint64_t zero_copy_calls;  /* allreduces folded between registered user
+                                  buffers (no staging copies)               */
+    uint64_t staged_calls;     /* allreduces through the staging chunks     */
 } mx_coll_stats_t;
 int mx_comm_set_profiling(mx_comm_t *comm, int on);
 int mx_comm_get_stats(mx_comm_t *comm, mx_coll_stats_t *stats, int reset);

@@ -203,9 +203,10 @@ def _free_port():
     return p
 
 
-def _mp_worker(rank, n, port, staging, jobs, q):
+def _mp_worker(rank, n, port, staging, jobs, q, env=None):
     import torch.distributed as dist
     os.environ["HSA_ENABLE_IPC_MODE_LEGACY"] = "0"
+    os.environ.update(env or {})
     try:
         dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=n)
         torch.cuda.set_device(0)
@@ -231,6 +232,19 @@ def _mp_worker(rank, n, port, staging, jobs, q):
                 x = _dev(gen(t, op, count, 7000 + rank))
                 comm.allreduce(mxompi.IN_PLACE, x.data_ptr(), count, t, op, alg, st)
                 results.append(x.cpu().numpy().tobytes())
+            elif kind == "allreduce_mis":
+                # this rank's buffers at a rank-dependent misalignment mod 16:
+                # the registered path must decline on every rank together
+                x = _dev(gen(t, op, count, 7000 + rank))
+                sh = (rank % 4) * es if 16 % es == 0 else 0
+                xs = torch.zeros(count * es + 16, dtype=torch.uint8, device="cuda")
+                xs[sh:sh + count * es].copy_(x)
+                out = torch.zeros(count * es + 16, dtype=torch.uint8, device="cuda")
+                comm.allreduce(xs.data_ptr() + sh, out.data_ptr() + sh, count, t, op, alg, st)
+                results.append(out[sh:sh + count * es].cpu().numpy().tobytes())
+            elif kind == "stats":
+                sts = comm.stats()
+                results.append((sts["zero_copy_calls"], sts["staged_calls"]))
             elif kind == "reduce_scatter":
                 rc = [count + 3 * r for r in range(n)]
                 x = _dev(gen(t, op, sum(rc), 7000 + rank))
@@ -321,12 +335,12 @@ def _mp_worker(rank, n, port, staging, jobs, q):
         q.put((rank, "err", traceback.format_exc() + str(e)))
 
 
-def _run_mp(n, jobs, staging=1 << 20):
+def _run_mp(n, jobs, staging=1 << 20, env=None):
     import torch.multiprocessing as mp
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_mp_worker, args=(r, n, port, staging, jobs, q)) for r in range(n)]
+    procs = [ctx.Process(target=_mp_worker, args=(r, n, port, staging, jobs, q, env)) for r in range(n)]
     for p in procs:
         p.start()
     out = {}
@@ -397,6 +411,8 @@ def _check_jobs(n, jobs, got):
     L = _oracle()
     for j, (kind, count, op, t, alg) in enumerate(jobs):
         es = mxompi.type_size(t)
+        if kind == "stats":
+            continue
         if kind.startswith("allreduce") or kind == "shmem":
             xs = [gen(t, op, count, 7000 + r) for r in range(n)]
             exp = [np.zeros(count * es, np.uint8) for _ in range(n)]
@@ -498,6 +514,59 @@ _JOBS8 = [j for j in _JOBS if (j[0], j[1]) in {
 def test_multiprocess_ipc_bitexact_8_ranks():
     assert len(_JOBS8) >= 10
     _check_jobs(8, _JOBS8, _run_mp(8, _JOBS8))
+
+
+# the PULL protocol (mx_comm_set_protocol; the default when ranks sit on
+# different GPUs, so the driver's 8-GPU run takes it): same fold programs,
+# peers' parts read over IPC from their own staging.  Every staged allreduce
+# shape of _JOBS (chunked, in place, element / 16-byte paths, every algorithm)
+# plus a rooted reduce between them (same staging, other layout)
+_JOBS_PULL = [j for j in _JOBS if j[0].startswith("allreduce")] + [("reduce", 100003, "SUM", "FLOAT", "auto"),
+                                                                   ("allreduce", 100003, "SUM", "FLOAT", "auto")]
+
+
+# zero-copy allreduce between registered user buffers (mx_comm_set_reg_min):
+# every staged shape of _JOBS folded straight between the ranks' own buffers,
+# in place, chunk-sized counts, and a call whose ranks disagree on alignment
+# (every rank falls back to the staged path together)
+_JOBS_ZC = [j for j in _JOBS if j[0].startswith(("allreduce", "reduce_scatter", "allgather"))
+            and j[0] != "reduce_scatter_block"] + [
+    ("allreduce_mis", 30001, "SUM", "FLOAT", "auto"),
+    ("allreduce_mis", 20011, "MAX", "DOUBLE", "ring"),
+    ("allreduce", 100003, "SUM", "FLOAT", "auto"),
+    ("allgather", 65536, "BAND", "UINT8_T", "auto"),
+    ("stats", 0, "SUM", "FLOAT", "auto")]
+
+
+@pytest.mark.parametrize("n", [2, 3, 8])
+def test_multiprocess_allreduce_zero_copy(n):
+    env = {"MX_REG_MIN": "1", "MX_ONESHOT_MAX": "0"}
+    got = _run_mp(n, _JOBS_ZC, env=env)
+    _check_jobs(n, _JOBS_ZC, got)
+    zc, staged = got[0][-1]
+
+    def eligible(kind, count, t):
+        # registered path: every rank's blocks at one misalignment mod 16
+        # (IN_PLACE reduce_scatter stays staged; neither counts it)
+        if kind in ("allreduce", "allreduce_inplace"):
+            return True
+        if kind == "reduce_scatter":
+            rc, es = [count + 3 * r for r in range(n)], mxompi.type_size(t)
+            return all(sum(rc[:r]) * es % 16 == 0 for r in range(n))
+        if kind == "allgather":
+            return count % 16 == 0
+        return False
+    n_mis = sum(1 for j in _JOBS_ZC if j[0] == "allreduce_mis")
+    n_zc = sum(1 for j in _JOBS_ZC if eligible(j[0], j[1], j[3]))
+    assert staged == n_mis and zc == n_zc, (zc, staged, n_zc)
+    for r in range(n):
+        assert got[r][-1] == got[0][-1]
+
+
+@pytest.mark.parametrize("n", [2, 3, 8])
+def test_multiprocess_allreduce_pull_protocol(n):
+    env = {"MX_ALLREDUCE_PROTO": "pull", "MX_ONESHOT_MAX": "0", "MX_REG_MIN": "0"}   # every call staged
+    _check_jobs(n, _JOBS_PULL, _run_mp(n, _JOBS_PULL, env=env))
 
 
 

@@ -81,9 +81,10 @@ def _rcounts(count, n):
     return [count + 3 * r for r in range(n)]
 
 
-def _worker(rank, n, port, staging, jobs, q):
+def _worker(rank, n, port, staging, jobs, q, env=None):
     import torch.distributed as dist
     os.environ["HSA_ENABLE_IPC_MODE_LEGACY"] = "0"
+    os.environ.update(env or {})
     try:
         dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=n)
         torch.cuda.set_device(0)
@@ -128,12 +129,12 @@ def _worker(rank, n, port, staging, jobs, q):
         q.put((rank, "err", traceback.format_exc() + str(e)))
 
 
-def _run(jobs, staging, n=N):
+def _run(jobs, staging, n=N, env=None):
     import torch.multiprocessing as mp
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, n, port, staging, jobs, q)) for r in range(n)]
+    procs = [ctx.Process(target=_worker, args=(r, n, port, staging, jobs, q, env)) for r in range(n)]
     for p in procs:
         p.start()
     out = {}
@@ -206,7 +207,9 @@ STAGING_CHUNKED = 48 * MiB
 
 def test_allreduce_fp32_sum_256mib_8_ranks():
     """The metric's allreduce at its own size: tuned decision (segmented ring,
-    32 phases of 1 MiB at n = 8), forced ring and forced Rabenseifner."""
+    32 phases of 1 MiB at n = 8), forced ring and forced Rabenseifner.  By
+    default these run zero-copy between the ranks' registered buffers; the
+    chunked test below takes the staged path under both protocols."""
     assert mxompi.allreduce_decision(N, C256, "FLOAT") == 5
     jobs = [("allreduce", C256, "SUM", "FLOAT", "auto"),
             ("allreduce", C256, "SUM", "FLOAT", "ring"),
@@ -234,12 +237,14 @@ def test_reduce_scatter_allgather_maxloc_64mib_8_ranks():
     _check(jobs, _run(jobs, STAGING_ONE_CHUNK))
 
 
-def test_allreduce_256mib_chunked_8_ranks():
-    """The same headline allreduces through a 48 MiB staging area: the
-    message runs in ~12 chunks, each with its own work partition but the fold
-    partition of the full count, so results must not change."""
+@pytest.mark.parametrize("proto", ["push", "pull"])
+def test_allreduce_256mib_chunked_8_ranks(proto):
+    """The same headline allreduces through a 48 MiB staging area (no
+    registration): the message runs in ~12 chunks, each with its own work
+    partition but the fold partition of the full count, so results must not
+    change -- under both staged data movements."""
     jobs = [("allreduce", C256, "SUM", "FLOAT", "auto"),
             ("allreduce", C256 - 12345, "SUM", "FLOAT", "rabenseifner"),
             ("allreduce", 100_000_007, "BAND", "UINT16_T", "ring"),
             ("reduce_scatter", (64 * MiB) // 4 // N + 7, "SUM", "FLOAT", "ring")]
-    _check(jobs, _run(jobs, STAGING_CHUNKED))
+    _check(jobs, _run(jobs, STAGING_CHUNKED, env={"MX_REG_MIN": "0", "MX_ALLREDUCE_PROTO": proto}))

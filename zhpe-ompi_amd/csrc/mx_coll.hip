@@ -43,6 +43,11 @@
 #include <map>
 #include <mutex>
 #include <new>
+#include <atomic>
+#include <fcntl.h>
+#include <sched.h>
+#include <sys/mman.h>
+#include <unistd.h>
 
 #include "mx_comm.hpp"
 #include "../../include/mx_convertor.h"
@@ -262,7 +267,103 @@ struct ipc_info {
   hipIpcMemHandle_t staging, flags, hregion;
   int rank, device, ok;
   uint64_t staging_bytes, hregion_bytes;
+  char pci[32];   // PCI bus id of the rank's GPU (hipDeviceGetPCIBusId)
+  char shm[48];   // rank 0: name of the registration page ("" = none)
 };
+
+// ---------------------------------------------------------------------------
+// user-buffer registration exchange (zero-copy allreduce).  One
+// record per rank in a POSIX shared-memory page (the ranks of an IPC
+// communicator share a node).  Per call k every rank publishes the IPC
+// handles of its buffers (seq = k, written last), reads every peer's, maps
+// them (cached), then publishes whether that worked (vseq = k); all ranks
+// see the same records and verdicts, so all take the same path.  A record
+// is rewritten only at call k+1, which no rank reaches before every peer
+// has read record k (call k needs every rank's device participation).
+// ---------------------------------------------------------------------------
+struct RegRec {
+  std::atomic<uint64_t> seq, vseq;
+  hipIpcMemHandle_t sh, rh;     // allocations holding sbuf / rbuf
+  uint64_t soff, roff;          // the buffers' offsets in them
+  int32_t ok, mis, verdict, pad_;
+  char pad[256 - 2 * 8 - 2 * sizeof(hipIpcMemHandle_t) - 2 * 8 - 4 * 4];
+};
+static_assert(sizeof(RegRec) == 256, "RegRec layout");
+static_assert(std::atomic<uint64_t>::is_always_lock_free, "shared-memory atomics");
+
+constexpr size_t kRegMinDefault = (size_t)4 << 20;   // bytes per rank (MX_REG_MIN overrides; 0 = off)
+constexpr size_t kRegCachePerPeer = 8;
+
+static size_t reg_min() {
+  const char *e = getenv("MX_REG_MIN");
+  if (!e || !*e) return kRegMinDefault;
+  const long long v = atoll(e);
+  return v > 0 ? (size_t)v : 0;
+}
+
+static void reg_release(mx_comm *c) {
+  if (c->reg_imp) {
+    for (const mx_reg_import &m : *c->reg_imp) (void)hipIpcCloseMemHandle(m.ptr);
+    delete c->reg_imp;
+    c->reg_imp = nullptr;
+  }
+  if (c->reg_shm) munmap(c->reg_shm, c->reg_shm_bytes);
+  c->reg_shm = nullptr;
+}
+
+// rank 0 creates the page before the first exchange; the others open it
+// after it; rank 0 unlinks it once every rank has agreed (nothing is left in
+// /dev/shm whatever happens later)
+static void reg_create(mx_comm *c, char *name, size_t cap) {
+  static std::atomic<unsigned> ctr{0};
+  name[0] = 0;
+  if (c->size < 2 || !reg_min()) return;
+  snprintf(name, cap, "/mx_reg_%d_%u", (int)getpid(), ctr.fetch_add(1));
+  const size_t bytes = (size_t)c->size * sizeof(RegRec);
+  const int fd = shm_open(name, O_CREAT | O_EXCL | O_RDWR, 0600);
+  if (fd < 0) { name[0] = 0; return; }
+  void *p = MAP_FAILED;
+  if (ftruncate(fd, (off_t)bytes) == 0) p = mmap(nullptr, bytes, PROT_READ | PROT_WRITE, MAP_SHARED, fd, 0);
+  close(fd);
+  if (p == MAP_FAILED) { shm_unlink(name); name[0] = 0; return; }
+  memset(p, 0, bytes);
+  c->reg_shm = p;
+  c->reg_shm_bytes = bytes;
+}
+
+static void reg_open(mx_comm *c, const char *name) {
+  if (c->reg_shm || !name[0]) return;
+  const size_t bytes = (size_t)c->size * sizeof(RegRec);
+  const int fd = shm_open(name, O_RDWR, 0600);
+  if (fd < 0) return;
+  void *p = mmap(nullptr, bytes, PROT_READ | PROT_WRITE, MAP_SHARED, fd, 0);
+  close(fd);
+  if (p == MAP_FAILED) return;
+  c->reg_shm = p;
+  c->reg_shm_bytes = bytes;
+}
+
+static int proto_default(const mx_comm *c) {
+  const char *e = getenv("MX_ALLREDUCE_PROTO");
+  if (e && !strcmp(e, "push")) return MX_PROTO_PUSH;
+  if (e && !strcmp(e, "pull")) return MX_PROTO_PULL;
+  return c->xdev ? MX_PROTO_PULL : MX_PROTO_PUSH;
+}
+
+extern "C" int mx_comm_set_protocol(mx_comm_t *c, int proto) {
+  if (!c || proto < MX_PROTO_AUTO || proto > MX_PROTO_PULL) return MX_ERR_ARG;
+  c->proto = proto == MX_PROTO_AUTO ? proto_default(c) : proto;
+  return c->proto;
+}
+
+extern "C" int mx_comm_get_protocol(const mx_comm_t *c) { return c ? c->proto : MX_ERR_ARG; }
+
+extern "C" int mx_comm_set_reg_min(mx_comm_t *c, size_t min_bytes) {
+  if (!c) return MX_ERR_ARG;
+  if (!c->reg_shm) return min_bytes ? MX_ERR_UNSUPPORTED : MX_SUCCESS;
+  c->reg_min = min_bytes;
+  return MX_SUCCESS;
+}
 
 extern "C" int mx_comm_create(int rank, int size, int device, size_t staging_bytes, int flags,
                               mx_allgather_fn ag, void *ctx, mx_comm_t **out) {
@@ -344,11 +445,22 @@ extern "C" int mx_comm_create_ex(int rank, int size, int device, size_t staging_
     }
     mine.rank = rank;
     mine.device = c ? c->device : -1;
+    if (c && hipDeviceGetPCIBusId(mine.pci, (int)sizeof mine.pci - 1, c->device) != hipSuccess) {
+      (void)hipGetLastError();
+      snprintf(mine.pci, sizeof mine.pci, "dev%d", c->device);
+    }
+    if (ok && rank == 0) reg_create(c, mine.shm, sizeof mine.shm);
     mine.ok = ok;
     // exchange 1: handles + verdicts (taken part in even after a local failure)
     if (ag(&mine, all, sizeof(ipc_info), ctx) != 0) ok = 0;
+    if (ok && rank != 0) reg_open(c, all[0].shm);
     for (int p = 0; ok && p < size; p++)
       if (!all[p].ok || all[p].staging_bytes != c->staging_bytes || all[p].hregion_bytes != c->hregion_bytes) ok = 0;
+    if (ok) {
+      for (int p = 0; p < size; p++)
+        if (strncmp(all[p].pci, mine.pci, sizeof mine.pci)) c->xdev = 1;
+      c->proto = proto_default(c);   // the same on every rank: xdev is symmetric, the env is job-wide
+    }
     for (int p = 0; ok && p < size; p++) {
       if (p == rank) {
         c->peer_staging[p] = c->staging;
@@ -384,9 +496,18 @@ extern "C" int mx_comm_create_ex(int rank, int size, int device, size_t staging_
     // exchange 2: every rank mapped every peer (doubles as the barrier)
     const int all_ok = agree(ag, ctx, size, ok);
     if (all_ok != 1) {
+      if (rank == 0 && mine.shm[0]) shm_unlink(mine.shm);
       mx_comm_destroy(c);
       return all_ok < 0 ? MX_ERR_HIP : MX_ERR_STATE;
     }
+    // registration: available only if every rank mapped the page
+    const int reg_all = agree(ag, ctx, size, c->reg_shm != nullptr);
+    if (rank == 0 && mine.shm[0]) shm_unlink(mine.shm);
+    if (reg_all == 1) {
+      c->reg_min = reg_min();
+      c->reg_imp = new (std::nothrow) std::vector<mx_reg_import>();
+    }
+    if (reg_all != 1 || !c->reg_imp) reg_release(c);
   } else {
     const int all_ok = agree(ag, ctx, size, ok);
     if (all_ok != 1) {
@@ -438,6 +559,7 @@ extern "C" int mx_comm_destroy(mx_comm_t *c) {
   if (c->prof)
     for (int i = 0; i < 64; i++) (void)hipEventDestroy(c->ev[i]);
   if (c->tail) (void)hipEventDestroy(c->tail);
+  reg_release(c);
   p2p_release(c);
   free(c);
   return MX_SUCCESS;
@@ -841,21 +963,24 @@ static inline size_t rup(size_t v, size_t a) { return (v + a - 1) / a * a; }
 
 // staging layout for a chunk of `ce` elements of size es
 struct Layout { size_t slot, gather_off; };
-static Layout layout_for(int n, size_t ce, size_t es) {
+// gather_only: the contributions are read where they are (registered user
+// buffers), so the staging holds only the gather area
+static Layout layout_for(int n, size_t ce, size_t es, bool gather_only = false) {
   Layout L;
-  L.slot = rup((ce + n - 1) / n * es + 16, 256);
+  L.slot = gather_only ? 0 : rup((ce + n - 1) / n * es + 16, 256);
   L.gather_off = rup(L.slot * n, 256);
   return L;
 }
-static size_t chunk_elems(const mx_comm *c, size_t count, size_t es) {
+static size_t chunk_elems(const mx_comm *c, size_t count, size_t es, bool gather_only = false) {
   const int n = c->size;
   auto fits = [&](size_t ce) {
-    const Layout L = layout_for(n, ce, es);
+    const Layout L = layout_for(n, ce, es, gather_only);
     return L.gather_off + ce * es + 16 <= c->main_bytes;
   };
   if (fits(count)) return count;
   // n slots of ce/n elements + a gather area of ce elements, plus padding
-  size_t ce = c->main_bytes > (size_t)(n + 2) * 512 ? (c->main_bytes - (size_t)(n + 2) * 512) / (2 * es) : 1;
+  size_t ce = c->main_bytes > (size_t)(n + 2) * 512 ? (c->main_bytes - (size_t)(n + 2) * 512) / ((gather_only ? 1 : 2) * es)
+                                                    : 1;
   if (ce >= count) ce = count - 1;
   while (ce > 1 && !fits(ce)) ce -= std::max<size_t>(1, ce / 64);
   return ce ? ce : 1;
@@ -905,6 +1030,112 @@ static int allreduce_oneshot(mx_comm *c, oneshot_launch_fn ol, const std::vector
   prof_end(c, s, 0, (double)(n + 1) * (double)bytes);
   if (rc) return rc;
   return finish(c, s);
+}
+
+// the allocation holding [p, p+bytes): IPC handle + offset of p in it
+static bool reg_export(const void *p, size_t bytes, hipIpcMemHandle_t *h, uint64_t *off) {
+  void *base = nullptr;
+  size_t size = 0;
+  if (hipMemGetAddressRange(&base, &size, const_cast<void *>(p)) != hipSuccess || !base ||
+      (const char *)p + bytes > (const char *)base + size || hipIpcGetMemHandle(h, base) != hipSuccess) {
+    (void)hipGetLastError();   // clear only the error this call raised
+    return false;
+  }
+  *off = (uint64_t)((const char *)p - (const char *)base);
+  return true;
+}
+
+// peer p's allocation `h`, mapped once and kept (LRU, kRegCachePerPeer per
+// peer; an evicted mapping is closed -- no kernel of this communicator is in
+// flight between blocking calls)
+static char *reg_import(mx_comm *c, int p, const hipIpcMemHandle_t &h, char *const *own, int nown) {
+  std::vector<mx_reg_import> &v = *c->reg_imp;
+  for (mx_reg_import &m : v)
+    if (m.peer == p && !memcmp(&m.h, &h, sizeof h)) {
+      m.used = ++c->reg_tick;
+      return m.ptr;
+    }
+  size_t held = 0, lru = (size_t)-1;
+  for (size_t i = 0; i < v.size(); i++)
+    if (v[i].peer == p) {
+      held++;
+      if (lru == (size_t)-1 || v[i].used < v[lru].used) lru = i;
+    }
+  if (held >= kRegCachePerPeer) {
+    (void)hipIpcCloseMemHandle(v[lru].ptr);
+    v.erase(v.begin() + (long)lru);
+  }
+  char *ptr = nullptr;
+  if (hipIpcOpenMemHandle((void **)&ptr, h, hipIpcMemLazyEnablePeerAccess) != hipSuccess || !ptr) {
+    (void)hipGetLastError();
+    return nullptr;
+  }
+  // a mapping must never be one of this rank's own buffers (the round-1 IPC
+  // aliasing symptom): refuse it, the call takes the staged path
+  for (int i = 0; i < nown; i++)
+    if (ptr == own[i]) {
+      (void)hipIpcCloseMemHandle(ptr);
+      return nullptr;
+    }
+  v.push_back(mx_reg_import{p, h, ptr, ++c->reg_tick});
+  return ptr;
+}
+
+// host wait until every rank's record field reaches k (the communicator's
+// wait timeout bounds it; 0 = forever)
+static int reg_wait(mx_comm *c, bool verdict, uint64_t k) {
+  RegRec *R = (RegRec *)c->reg_shm;
+  const auto t0 = std::chrono::steady_clock::now();
+  for (int p = 0; p < c->size; p++) {
+    unsigned spins = 0;
+    while ((verdict ? R[p].vseq : R[p].seq).load(std::memory_order_acquire) < k) {
+      if (++spins > 256) {
+        sched_yield();
+        if (c->timeout_s > 0 &&
+            std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count() > c->timeout_s) {
+          c->poisoned = MX_ERR_TIMEOUT;
+          return MX_ERR_TIMEOUT;
+        }
+      }
+    }
+  }
+  return MX_SUCCESS;
+}
+
+// Registration exchange of one call: 1 = every rank's buffers are mapped by
+// every peer (ps / pr filled: peer j's sbuf / rbuf in this process), 0 = the
+// call takes the staged path (on every rank), < 0 = error.  `mis` must be
+// equal on every rank and `local_ok` true on every rank (the caller's
+// conditions for the 16-byte vector path and for its data flow).
+static int reg_exchange(mx_comm *c, const char *sb, size_t sbytes, char *rb, size_t rbytes, int mis, bool local_ok,
+                        const char **ps, char **pr) {
+  RegRec *R = (RegRec *)c->reg_shm;
+  const int n = c->size, r = c->rank;
+  const uint64_t k = ++c->reg_seq;
+  RegRec &me = R[r];
+  int ok = local_ok && reg_export(sb, sbytes, &me.sh, &me.soff) && reg_export(rb, rbytes, &me.rh, &me.roff);
+  me.mis = mis;
+  me.ok = ok;
+  me.seq.store(k, std::memory_order_release);
+  if (int rc = reg_wait(c, false, k)) return rc;
+  int verdict = 1;
+  for (int p = 0; p < n; p++)
+    if (!R[p].ok || R[p].mis != me.mis) verdict = 0;
+  char *own[2] = {(char *)sb, rb};
+  for (int p = 0; verdict && p < n; p++) {
+    if (p == r) { ps[p] = sb; pr[p] = rb; continue; }
+    char *s0 = reg_import(c, p, R[p].sh, own, 2);
+    char *r0 = s0 && !memcmp(&R[p].sh, &R[p].rh, sizeof(hipIpcMemHandle_t)) ? s0 : reg_import(c, p, R[p].rh, own, 2);
+    if (!s0 || !r0) { verdict = 0; break; }
+    ps[p] = s0 + R[p].soff;
+    pr[p] = r0 + R[p].roff;
+  }
+  me.verdict = verdict;
+  me.vseq.store(k, std::memory_order_release);
+  if (int rc = reg_wait(c, true, k)) return rc;
+  for (int p = 0; p < n; p++)
+    if (!R[p].verdict) return 0;
+  return 1;
 }
 
 }  // namespace
@@ -970,23 +1201,50 @@ extern "C" int mx_allreduce(mx_comm_t *c, const void *sbuf, void *rbuf, size_t c
     int rc = allreduce_segments(alg, n, count, es, 0, 0, probe);
     if (rc) return rc;
   }
-  const size_t ce = chunk_elems(c, count, es);
+  // Zero-copy input: with every rank's sbuf registered, the fold reads the
+  // peers' parts straight from their sbufs over xGMI (the PULL fold without
+  // its input copy).  Results still travel through the peers' uncached
+  // gather areas: every remote WRITE of this library lands in uncached
+  // memory, so no GPU's L2 can hold a stale copy of it.
+  const char *ps[MAXR];
+  char *pr[MAXR];
+  int zc = 0;
+  if (c->reg_shm && !c->defer && c->reg_min && count * es >= c->reg_min) {
+    zc = reg_exchange(c, sb, count * es, rb, count * es, (int)((uintptr_t)sb & 15), true, ps, pr);
+    if (zc < 0) return zc;
+  }
+  const size_t ce = chunk_elems(c, count, es, zc);
+  if (zc) c->st.zero_copy_calls++;
+  else c->st.staged_calls++;
   for (size_t c0 = 0; c0 < count; c0 += ce) {
     const size_t cl = std::min(ce, count - c0);
-    const Layout L = layout_for(n, ce, es);
+    const Layout L = layout_for(n, ce, es, zc);
     size_t off[MAXR], len[MAXR];
     blockcount(cl, n, off, len);
     const uint64_t g = ++c->gen;
     int rc;
     // (a) peers finished the previous round with their staging
     if ((rc = wait_all(c, FLAG_DONE, g - 1, s))) return rc;
-    // (b) push my contribution for part p into rank p's slot `r`
+    const bool pull = c->proto == MX_PROTO_PULL;
+    const size_t mis0 = (c0 * es) & 15;
     CopyArgs ca;
     memset(&ca, 0, sizeof ca);
-    for (int p = 0; p < n; p++) {
-      if (p == r || !len[p]) continue;
-      const size_t e0 = c0 + off[p];
-      ca.j[ca.n++] = CopyJob{sb + e0 * es, c->peer_staging[p] + (size_t)r * L.slot + ((e0 * es) & 15), len[p] * es};
+    if (zc) {
+      // (b) nothing to move: the peers read my sbuf where it is
+    } else if (pull) {
+      // (b) copy the parts the peers fold (all but mine) into my own
+      // staging, laid out as the chunk at its own misalignment mod 16
+      const size_t lo = off[r], hi = off[r] + len[r];
+      if (lo) ca.j[ca.n++] = CopyJob{sb + c0 * es, c->staging + mis0, lo * es};
+      if (hi < cl) ca.j[ca.n++] = CopyJob{sb + (c0 + hi) * es, c->staging + mis0 + hi * es, (cl - hi) * es};
+    } else {
+      // (b) push my contribution for part p into rank p's slot `r`
+      for (int p = 0; p < n; p++) {
+        if (p == r || !len[p]) continue;
+        const size_t e0 = c0 + off[p];
+        ca.j[ca.n++] =
+            CopyJob{sb + e0 * es, c->peer_staging[p] + (size_t)r * L.slot + ((e0 * es) & 15), len[p] * es};
+      }
     }
     prof_begin(c, s);
     if ((rc = copy_launch(c, ca, s))) return rc;
@@ -994,13 +1252,18 @@ extern "C" int mx_allreduce(mx_comm_t *c, const void *sbuf, void *rbuf, size_t c
     if ((rc = signal_all(c, FLAG_READY, g << 1, s))) return rc;
     if ((rc = wait_all(c, FLAG_READY, g << 1, s))) return rc;
     // (c) fold my part, store to my rbuf and every peer's gather area
+    // (PULL: the peers' contributions are read from their staging over xGMI)
     if (len[r]) {
       const size_t e0 = c0 + off[r];
       const size_t mis = (e0 * es) & 15;
       const char *sp[MAXR];
       char *dp[MAXR];
       int nd = 0;
-      for (int j = 0; j < n; j++) sp[j] = (j == r) ? sb + e0 * es : c->staging + (size_t)j * L.slot + mis;
+      for (int j = 0; j < n; j++)
+        sp[j] = (j == r) ? sb + e0 * es
+                : zc     ? ps[j] + e0 * es
+                : pull   ? c->peer_staging[j] + mis0 + off[r] * es
+                         : c->staging + (size_t)j * L.slot + mis;
       dp[nd++] = rb + e0 * es;
       for (int p = 0; p < n; p++)
         if (p != r) dp[nd++] = c->peer_staging[p] + L.gather_off + ((c0 * es) & 15) + off[r] * es;
@@ -1059,6 +1322,34 @@ extern "C" int mx_reduce_scatter(mx_comm_t *c, const void *sbuf, void *rbuf, con
   // (the slot geometry must be the same on every rank: it depends only on
   // the collective IN_PLACE choice, not on this rank's block)
   const bool inplace = sb == (const char *)rbuf;
+  if (c->reg_shm && !c->defer && c->reg_min && total * es >= c->reg_min && !inplace) {
+    // zero-copy: rank r folds block r straight from every rank's registered
+    // sbuf into its own rbuf (IN_PLACE stays staged: block 0 of a rank's
+    // input is its output area, which rank 0 would still be reading)
+    const char *ps[MAXR];
+    char *pr[MAXR];
+    const bool lok = (((uintptr_t)rbuf - ((uintptr_t)sb + disp[r] * es)) & 15) == 0;
+    const int zc = reg_exchange(c, sb, total * es, (char *)rbuf, rcounts[r] * es, (int)((uintptr_t)sb & 15), lok,
+                                ps, pr);
+    if (zc < 0) return zc;
+    if (zc) {
+      const uint64_t g = ++c->gen;
+      c->st.zero_copy_calls++;
+      if ((rc = signal_all(c, FLAG_READY, g << 1, s))) return rc;
+      if ((rc = wait_all(c, FLAG_READY, g << 1, s))) return rc;
+      if (rcounts[r]) {
+        const char *sp[MAXR];
+        for (int j = 0; j < n; j++) sp[j] = ps[j] + disp[r] * es;
+        char *dp[1] = {(char *)rbuf};
+        for (const Seg &sg : segs)
+          if ((rc = run_fold(c, fl, sg, disp[r], sp, n, dp, 1, es, s))) return rc;
+      }
+      if ((rc = signal_all(c, FLAG_PUSHED, g, s))) return rc;     // every peer is done with my sbuf
+      if ((rc = wait_all(c, FLAG_PUSHED, g, s))) return rc;
+      if ((rc = signal_all(c, FLAG_DONE, g, s))) return rc;
+      return finish(c, s);
+    }
+  }
   const bool overlap = inplace && disp[r] != 0;
   const size_t nslots = (size_t)n + (inplace ? 1 : 0);
   // chunks of every block (piece k0 of block q goes to rank q's slot r):
@@ -1119,6 +1410,32 @@ extern "C" int mx_allgather(mx_comm_t *c, const void *sbuf, void *rbuf, size_t b
     return finish(c, s);
   }
   if (!(c->flags & MX_COMM_IPC)) return MX_ERR_STATE;
+  if (c->reg_shm && !c->defer && c->reg_min && (size_t)n * bytes >= c->reg_min) {
+    // zero-copy: every rank reads the peers' blocks straight from their
+    // registered sbufs into its own rbuf (remote reads, local writes only)
+    const char *ps[MAXR];
+    char *pr[MAXR];
+    const bool lok = ((uintptr_t)sb & 15) == (((uintptr_t)rb + (size_t)r * bytes) & 15);
+    const int zc = reg_exchange(c, sb, bytes, rb, (size_t)n * bytes, (int)((uintptr_t)rb & 15), lok, ps, pr);
+    if (zc < 0) return zc;
+    if (zc) {
+      const uint64_t g = ++c->gen;
+      int rc;
+      c->st.zero_copy_calls++;
+      if ((rc = signal_all(c, FLAG_READY, g << 1, s))) return rc;   // every sbuf holds its block
+      if ((rc = wait_all(c, FLAG_READY, g << 1, s))) return rc;
+      CopyArgs ca;
+      memset(&ca, 0, sizeof ca);
+      for (int p = 0; p < n; p++)
+        if (p != r) ca.j[ca.n++] = CopyJob{ps[p], rb + (size_t)p * bytes, bytes};
+      if (sb != rb + (size_t)r * bytes) ca.j[ca.n++] = CopyJob{sb, rb + (size_t)r * bytes, bytes};
+      if ((rc = copy_launch(c, ca, s))) return rc;
+      if ((rc = signal_all(c, FLAG_PUSHED, g, s))) return rc;     // done reading the peers' sbufs
+      if ((rc = wait_all(c, FLAG_PUSHED, g, s))) return rc;
+      if ((rc = signal_all(c, FLAG_DONE, g, s))) return rc;
+      return finish(c, s);
+    }
+  }
   // n slots of `slot` bytes; each round moves up to `cb` bytes per rank
   const size_t slot = (c->main_bytes / n) & ~(size_t)255;
   if (slot < 512) return MX_ERR_NOMEM;

@@ -100,6 +100,16 @@ struct P2PRndvCur {
 
 }  // namespace mx
 
+// a peer allocation mapped for zero-copy collectives (key: peer + handle;
+// the handle carries a per-allocation id, so a reallocation at the same
+// address is a new entry)
+struct mx_reg_import {
+  int peer;
+  hipIpcMemHandle_t h;
+  char *ptr;
+  uint64_t used;
+};
+
 // ---------------------------------------------------------------------------
 // communicator
 // ---------------------------------------------------------------------------
@@ -123,6 +133,21 @@ struct mx_comm {
   int *poison;
   int poisoned;
   uint64_t gen;
+  // staged allreduce data movement (MX_PROTO_*): PUSH writes each part to
+  // its owner before the fold (every link busy in one direction per phase);
+  // PULL copies the input into the rank's own staging and the owner's fold
+  // reads the parts over xGMI while it writes results to the peers (both
+  // directions of every link in one phase).  `xdev`: some peer runs on
+  // another GPU (PCI bus ids differ), which makes PULL the default.
+  int proto, xdev;
+  // user-buffer registration (zero-copy allreduce): a host
+  // shared-memory page per communicator where every rank publishes the IPC
+  // handles of its call's buffers; peers' allocations stay mapped in an LRU
+  // cache.  reg_shm null: registration unavailable (every rank agrees).
+  void *reg_shm;
+  size_t reg_shm_bytes, reg_min;
+  uint64_t reg_seq, reg_tick;
+  std::vector<struct mx_reg_import> *reg_imp;
   double timeout_s;
   uint64_t timeout_ticks;
   ncclComm_t nccl;

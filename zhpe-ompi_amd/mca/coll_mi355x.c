@@ -193,6 +193,16 @@ static int comm_ready(mx_coll_module_t *m)
         const int t = mx_ompi_host->mca_int("coll_mi355x_wait_timeout", 0);
         rc = mx_comm_set_timeout(m->mx, t > 0 ? (double)t : 0.0);
     }
+    if (rc == MX_SUCCESS) {
+        /* MCA vars are job-wide, so every rank sets the same data path:
+         * zero-copy from coll_mi355x_reg_min_kb per rank (0 = off; the
+         * communicator declines it collectively when /dev/shm is missing),
+         * staged protocol 0 auto / 1 push / 2 pull */
+        const int kb = mx_ompi_host->mca_int("coll_mi355x_reg_min_kb", 4096);
+        (void)mx_comm_set_reg_min(m->mx, kb > 0 ? (size_t)kb << 10 : 0);
+        const int proto = mx_ompi_host->mca_int("coll_mi355x_protocol", MX_PROTO_AUTO);
+        if (mx_comm_set_protocol(m->mx, proto) < 0) rc = MX_ERR_ARG;
+    }
     /* the streams are process-local: a failure here is reported by the calls
      * (or falls back to the default stream), never turned into a different
      * protocol on this rank */

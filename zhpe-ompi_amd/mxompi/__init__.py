@@ -185,7 +185,8 @@ IREDUCE = {"auto": 0, "chain": 1, "binomial": 2, "rabenseifner": 3}
 class CollStats(ctypes.Structure):
     _fields_ = [("calls", ctypes.c_uint64), ("fold_launches", ctypes.c_uint64), ("fold_ms", ctypes.c_double),
                 ("fold_bytes", ctypes.c_double), ("push_ms", ctypes.c_double), ("gather_ms", ctypes.c_double),
-                ("total_ms", ctypes.c_double)]
+                ("total_ms", ctypes.c_double), ("zero_copy_calls", ctypes.c_uint64),
+                ("staged_calls", ctypes.c_uint64)]
 
 
 _AG_FN = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p)
@@ -201,6 +202,9 @@ def _coll_lib():
         L.mx_comm_create_local.argtypes = [i, i, ctypes.POINTER(vp)]
         L.mx_comm_destroy.argtypes = [vp]
         L.mx_comm_set_timeout.argtypes = [vp, ctypes.c_double]
+        L.mx_comm_set_protocol.argtypes = [vp, i]
+        L.mx_comm_get_protocol.argtypes = [vp]
+        L.mx_comm_set_reg_min.argtypes = [vp, sz]
         L.mx_allreduce.argtypes = [vp, vp, vp, sz, i, i, i, vp]
         L.mx_allreduce_local.argtypes = [vp, pp, pp, sz, i, i, i, vp]
         L.mx_reduce_scatter.argtypes = [vp, vp, vp, ctypes.POINTER(sz), i, i, i, vp]
@@ -385,6 +389,23 @@ class Comm:
 
     def set_timeout(self, seconds):
         check(_coll_lib().mx_comm_set_timeout(self.h, seconds), "mx_comm_set_timeout")
+
+    PROTO = {"auto": 0, "push": 1, "pull": 2}
+
+    def set_protocol(self, proto):
+        """Staged allreduce data movement ("auto" | "push" | "pull", mx_comm_set_protocol);
+        every rank must set the same one.  Returns the protocol in force."""
+        rc = _coll_lib().mx_comm_set_protocol(self.h, self.PROTO[proto])
+        check(min(rc, 0), "mx_comm_set_protocol")
+        return {1: "push", 2: "pull"}[rc]
+
+    def protocol(self):
+        return {1: "push", 2: "pull"}.get(_coll_lib().mx_comm_get_protocol(self.h), "none")
+
+    def set_reg_min(self, min_bytes):
+        """Zero-copy (registered user buffers) allreduce from min_bytes per rank; 0 = off
+        (mx_comm_set_reg_min).  Every rank must set the same value."""
+        check(_coll_lib().mx_comm_set_reg_min(self.h, min_bytes), "mx_comm_set_reg_min")
 
     def close(self):
         if getattr(self, "h", None):
