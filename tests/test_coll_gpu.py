@@ -236,7 +236,7 @@ def _mp_worker(rank, n, port, staging, jobs, q, env=None):
                 # this rank's buffers at a rank-dependent misalignment mod 16:
                 # the registered path must decline on every rank together
                 x = _dev(gen(t, op, count, 7000 + rank))
-                sh = (rank % 4) * es if 16 % es == 0 else 0
+                sh = (rank % (16 // es)) * es if 16 % es == 0 else 0   # < 16: inside the padding
                 xs = torch.zeros(count * es + 16, dtype=torch.uint8, device="cuda")
                 xs[sh:sh + count * es].copy_(x)
                 out = torch.zeros(count * es + 16, dtype=torch.uint8, device="cuda")
@@ -529,7 +529,7 @@ _JOBS_PULL = [j for j in _JOBS if j[0].startswith("allreduce")] + [("reduce", 10
 # every staged shape of _JOBS folded straight between the ranks' own buffers,
 # in place, chunk-sized counts, and a call whose ranks disagree on alignment
 # (every rank falls back to the staged path together)
-_JOBS_ZC = [j for j in _JOBS if j[0].startswith(("allreduce", "reduce_scatter", "allgather"))
+_JOBS_ZC = [j for j in _JOBS if j[0].startswith(("allreduce", "reduce_scatter", "allgather", "bcast"))
             and j[0] != "reduce_scatter_block"] + [
     ("allreduce_mis", 30001, "SUM", "FLOAT", "auto"),
     ("allreduce_mis", 20011, "MAX", "DOUBLE", "ring"),
@@ -548,7 +548,7 @@ def test_multiprocess_allreduce_zero_copy(n):
     def eligible(kind, count, t):
         # registered path: every rank's blocks at one misalignment mod 16
         # (IN_PLACE reduce_scatter stays staged; neither counts it)
-        if kind in ("allreduce", "allreduce_inplace"):
+        if kind in ("allreduce", "allreduce_inplace", "bcast", "bcast_root0"):
             return True
         if kind == "reduce_scatter":
             rc, es = [count + 3 * r for r in range(n)], mxompi.type_size(t)

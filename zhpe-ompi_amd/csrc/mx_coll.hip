@@ -281,12 +281,16 @@ struct ipc_info {
 // is rewritten only at call k+1, which no rank reaches before every peer
 // has read record k (call k needs every rank's device participation).
 // ---------------------------------------------------------------------------
+struct RegBuf {
+  hipIpcMemHandle_t h;          // the allocation holding the buffer
+  uint64_t base, size, id;      // its base address, size and runtime buffer id (exporter side)
+  uint64_t off;                 // the buffer's offset in it
+};
 struct RegRec {
   std::atomic<uint64_t> seq, vseq;
-  hipIpcMemHandle_t sh, rh;     // allocations holding sbuf / rbuf
-  uint64_t soff, roff;          // the buffers' offsets in them
+  RegBuf sb, rb;
   int32_t ok, mis, verdict, pad_;
-  char pad[256 - 2 * 8 - 2 * sizeof(hipIpcMemHandle_t) - 2 * 8 - 4 * 4];
+  char pad[256 - 2 * 8 - 2 * sizeof(RegBuf) - 4 * 4];
 };
 static_assert(sizeof(RegRec) == 256, "RegRec layout");
 static_assert(std::atomic<uint64_t>::is_always_lock_free, "shared-memory atomics");
@@ -754,7 +758,7 @@ static int order(mx_comm *c, hipStream_t s) {
 }
 
 static int run_fold(mx_comm *c, fold_launch_fn fl, const Seg &sg, size_t part_lo, const char *const *src_base,
-                    int nsrc, char *const *dst_base, int ndst, size_t es, hipStream_t s) {
+                    int nsrc, char *const *dst_base, int ndst, size_t es, hipStream_t s, bool nt_force = false) {
   // src_base / dst_base point at element part_lo of each operand/destination
   FoldArgs a;
   memset(&a, 0, sizeof a);
@@ -765,6 +769,7 @@ static int run_fold(mx_comm *c, fold_launch_fn fl, const Seg &sg, size_t part_lo
   a.n = sg.hi - sg.lo;
   a.p = sg.p;
   a.poison = c ? c->poison : nullptr;
+  a.nt_force = nt_force;
   prof_begin(c, s);
   const int rc = fl(a, s);
   prof_end(c, s, 0, (double)(nsrc + ndst) * (double)a.n * (double)es);
@@ -1032,41 +1037,57 @@ static int allreduce_oneshot(mx_comm *c, oneshot_launch_fn ol, const std::vector
   return finish(c, s);
 }
 
-// the allocation holding [p, p+bytes): IPC handle + offset of p in it
-static bool reg_export(const void *p, size_t bytes, hipIpcMemHandle_t *h, uint64_t *off) {
+// the allocation holding [p, p+bytes): IPC handle, identity, offset of p
+static bool reg_export(const void *p, size_t bytes, RegBuf *b) {
   void *base = nullptr;
   size_t size = 0;
+  unsigned long long id = 0;
   if (hipMemGetAddressRange(&base, &size, const_cast<void *>(p)) != hipSuccess || !base ||
-      (const char *)p + bytes > (const char *)base + size || hipIpcGetMemHandle(h, base) != hipSuccess) {
+      (const char *)p + bytes > (const char *)base + size ||
+      hipPointerGetAttribute(&id, HIP_POINTER_ATTRIBUTE_BUFFER_ID, (hipDeviceptr_t)base) != hipSuccess ||
+      hipIpcGetMemHandle(&b->h, base) != hipSuccess) {
     (void)hipGetLastError();   // clear only the error this call raised
     return false;
   }
-  *off = (uint64_t)((const char *)p - (const char *)base);
+  b->base = (uint64_t)(uintptr_t)base;
+  b->size = size;
+  b->id = id;
+  b->off = (uint64_t)((const char *)p - (const char *)base);
   return true;
 }
 
-// peer p's allocation `h`, mapped once and kept (LRU, kRegCachePerPeer per
-// peer; an evicted mapping is closed -- no kernel of this communicator is in
-// flight between blocking calls)
-static char *reg_import(mx_comm *c, int p, const hipIpcMemHandle_t &h, char *const *own, int nown) {
+// peer p's allocation, mapped once and kept (LRU, kRegCachePerPeer per
+// peer).  A cached mapping of an allocation the peer has since freed (same
+// peer range, other buffer id) is closed BEFORE the new handle is opened, so
+// the runtime can never hand back the stale import.  Closing is safe: no
+// kernel of this communicator is in flight between blocking calls.
+static char *reg_import(mx_comm *c, int p, const RegBuf &b, char *const *own, int nown) {
   std::vector<mx_reg_import> &v = *c->reg_imp;
   for (mx_reg_import &m : v)
-    if (m.peer == p && !memcmp(&m.h, &h, sizeof h)) {
+    if (m.peer == p && m.base == b.base && m.size == b.size && m.id == b.id) {
       m.used = ++c->reg_tick;
       return m.ptr;
     }
-  size_t held = 0, lru = (size_t)-1;
-  for (size_t i = 0; i < v.size(); i++)
-    if (v[i].peer == p) {
-      held++;
-      if (lru == (size_t)-1 || v[i].used < v[lru].used) lru = i;
+  size_t held = 0;
+  for (size_t i = 0; i < v.size();) {
+    const mx_reg_import &m = v[i];
+    if (m.peer == p && m.base < b.base + b.size && b.base < m.base + m.size) {   // overlaps: stale
+      (void)hipIpcCloseMemHandle(m.ptr);
+      v.erase(v.begin() + (long)i);
+      continue;
     }
+    held += m.peer == p;
+    i++;
+  }
   if (held >= kRegCachePerPeer) {
+    size_t lru = (size_t)-1;
+    for (size_t i = 0; i < v.size(); i++)
+      if (v[i].peer == p && (lru == (size_t)-1 || v[i].used < v[lru].used)) lru = i;
     (void)hipIpcCloseMemHandle(v[lru].ptr);
     v.erase(v.begin() + (long)lru);
   }
   char *ptr = nullptr;
-  if (hipIpcOpenMemHandle((void **)&ptr, h, hipIpcMemLazyEnablePeerAccess) != hipSuccess || !ptr) {
+  if (hipIpcOpenMemHandle((void **)&ptr, b.h, hipIpcMemLazyEnablePeerAccess) != hipSuccess || !ptr) {
     (void)hipGetLastError();
     return nullptr;
   }
@@ -1077,7 +1098,7 @@ static char *reg_import(mx_comm *c, int p, const hipIpcMemHandle_t &h, char *con
       (void)hipIpcCloseMemHandle(ptr);
       return nullptr;
     }
-  v.push_back(mx_reg_import{p, h, ptr, ++c->reg_tick});
+  v.push_back(mx_reg_import{p, b.base, b.size, b.id, ptr, ++c->reg_tick});
   return ptr;
 }
 
@@ -1113,7 +1134,7 @@ static int reg_exchange(mx_comm *c, const char *sb, size_t sbytes, char *rb, siz
   const int n = c->size, r = c->rank;
   const uint64_t k = ++c->reg_seq;
   RegRec &me = R[r];
-  int ok = local_ok && reg_export(sb, sbytes, &me.sh, &me.soff) && reg_export(rb, rbytes, &me.rh, &me.roff);
+  int ok = local_ok && reg_export(sb, sbytes, &me.sb) && reg_export(rb, rbytes, &me.rb);
   me.mis = mis;
   me.ok = ok;
   me.seq.store(k, std::memory_order_release);
@@ -1124,11 +1145,12 @@ static int reg_exchange(mx_comm *c, const char *sb, size_t sbytes, char *rb, siz
   char *own[2] = {(char *)sb, rb};
   for (int p = 0; verdict && p < n; p++) {
     if (p == r) { ps[p] = sb; pr[p] = rb; continue; }
-    char *s0 = reg_import(c, p, R[p].sh, own, 2);
-    char *r0 = s0 && !memcmp(&R[p].sh, &R[p].rh, sizeof(hipIpcMemHandle_t)) ? s0 : reg_import(c, p, R[p].rh, own, 2);
+    const RegBuf &bs = R[p].sb, &br = R[p].rb;
+    char *s0 = reg_import(c, p, bs, own, 2);
+    char *r0 = s0 && br.base == bs.base && br.id == bs.id ? s0 : reg_import(c, p, br, own, 2);
     if (!s0 || !r0) { verdict = 0; break; }
-    ps[p] = s0 + R[p].soff;
-    pr[p] = r0 + R[p].roff;
+    ps[p] = s0 + bs.off;
+    pr[p] = r0 + br.off;
   }
   me.verdict = verdict;
   me.vseq.store(k, std::memory_order_release);
@@ -1270,7 +1292,7 @@ extern "C" int mx_allreduce(mx_comm_t *c, const void *sbuf, void *rbuf, size_t c
       std::vector<Seg> segs;
       if ((rc = allreduce_segments(alg, n, count, es, e0, e0 + len[r], segs))) return rc;
       for (const Seg &sg : segs)
-        if ((rc = run_fold(c, fl, sg, e0, sp, n, dp, nd, es, s))) return rc;
+        if ((rc = run_fold(c, fl, sg, e0, sp, n, dp, nd, es, s, zc))) return rc;
     }
     if ((rc = signal_all(c, FLAG_PUSHED, g, s))) return rc;
     if ((rc = wait_all(c, FLAG_PUSHED, g, s))) return rc;
@@ -1342,7 +1364,7 @@ extern "C" int mx_reduce_scatter(mx_comm_t *c, const void *sbuf, void *rbuf, con
         for (int j = 0; j < n; j++) sp[j] = ps[j] + disp[r] * es;
         char *dp[1] = {(char *)rbuf};
         for (const Seg &sg : segs)
-          if ((rc = run_fold(c, fl, sg, disp[r], sp, n, dp, 1, es, s))) return rc;
+          if ((rc = run_fold(c, fl, sg, disp[r], sp, n, dp, 1, es, s, true))) return rc;
       }
       if ((rc = signal_all(c, FLAG_PUSHED, g, s))) return rc;     // every peer is done with my sbuf
       if ((rc = wait_all(c, FLAG_PUSHED, g, s))) return rc;
@@ -1495,6 +1517,42 @@ extern "C" int mx_bcast(mx_comm_t *c, void *buf, size_t bytes, int root, void *s
   const size_t cb = (slot - 32) * (size_t)m;
   const uint32_t all = (n >= 32) ? 0xffffffffu : ((1u << n) - 1);
   auto part_of = [&](int rank) { return rank < root ? rank : rank - 1; };   // non-root -> part index
+  if (c->reg_shm && !c->defer && c->reg_min && bytes >= c->reg_min) {
+    // zero-copy scatter + allgather: non-root q reads its part from the
+    // root's registered buffer, then the other parts from their owners'
+    // buffers (remote reads, local writes only)
+    const char *ps[MAXR];
+    char *pr[MAXR];
+    const int zc = reg_exchange(c, ub, bytes, ub, bytes, (int)((uintptr_t)ub & 15), true, ps, pr);
+    if (zc < 0) return zc;
+    if (zc) {
+      size_t off[MAXR], len[MAXR];
+      blockcount(bytes, m, off, len);
+      const uint64_t g = ++c->gen;
+      const uint32_t nonroot = all & ~(1u << root);
+      int rc;
+      c->st.zero_copy_calls++;
+      if ((rc = signal_all(c, FLAG_READY, g << 1, s))) return rc;
+      if (r != root) {
+        const int p0 = part_of(r);
+        if ((rc = wait_mask(c, FLAG_READY, 1u << root, g << 1, s))) return rc;
+        CopyArgs ca;
+        memset(&ca, 0, sizeof ca);
+        ca.j[ca.n++] = CopyJob{ps[root] + off[p0], ub + off[p0], len[p0]};
+        if ((rc = copy_launch(c, ca, s))) return rc;
+        if ((rc = signal_all(c, FLAG_PUSHED, g, s))) return rc;   // my part is in my buffer
+        if ((rc = wait_mask(c, FLAG_PUSHED, nonroot & ~(1u << r), g, s))) return rc;
+        memset(&ca, 0, sizeof ca);
+        for (int q = 0; q < n; q++)
+          if (q != root && q != r) ca.j[ca.n++] = CopyJob{ps[q] + off[part_of(q)], ub + off[part_of(q)], len[part_of(q)]};
+        if ((rc = copy_launch(c, ca, s))) return rc;
+      }
+      // nobody reads my buffer any more once every non-root is done
+      if ((rc = signal_all(c, FLAG_DONE, g, s))) return rc;
+      if ((rc = wait_mask(c, FLAG_DONE, nonroot & ~(1u << r), g, s))) return rc;
+      return finish(c, s);
+    }
+  }
   const bool direct = bytes <= kBcastDirectMax || m == 1;
   for (size_t o = 0; o < bytes; o += cb) {
     const size_t l = std::min(cb, bytes - o);

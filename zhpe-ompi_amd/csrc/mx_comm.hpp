@@ -100,12 +100,14 @@ struct P2PRndvCur {
 
 }  // namespace mx
 
-// a peer allocation mapped for zero-copy collectives (key: peer + handle;
-// the handle carries a per-allocation id, so a reallocation at the same
-// address is a new entry)
+// a peer allocation mapped for zero-copy collectives.  Key: peer + the
+// exporter's allocation base + its runtime buffer id (HIP_POINTER_ATTRIBUTE_
+// BUFFER_ID): an allocation freed and re-made at the same address -- what a
+// caching allocator does after empty_cache() -- can carry byte-identical IPC
+// handles, so the handle alone does not tell a stale mapping from a live one.
 struct mx_reg_import {
   int peer;
-  hipIpcMemHandle_t h;
+  uint64_t base, size, id;
   char *ptr;
   uint64_t used;
 };

@@ -70,6 +70,7 @@ struct FoldArgs {
   int ndst;
   size_t n, head, nvec;  // elements; scalar head; 16-B vectors after head
   const int *poison;     // communicator poison word (null: local)
+  int nt_force;          // non-temporal accesses whatever the footprint (operands read once over xGMI)
   FoldProg p;
 };
 
@@ -182,7 +183,7 @@ int fold_launch(FoldArgs &a, hipStream_t s) {
   const size_t g = (work + kFB - 1) / kFB;
   int nsrc = 0;
   for (int j = 0; j < MAXR; j++) nsrc += a.src[j] != nullptr;
-  if (vec && mx_nt_for((size_t)(nsrc + a.ndst) * a.n * sizeof(T)))
+  if (vec && (a.nt_force || mx_nt_for((size_t)(nsrc + a.ndst) * a.n * sizeof(T))))
     hipLaunchKernelGGL((k_fold<T, OP, true>), dim3((unsigned)(g ? g : 1)), dim3(kFB), 0, s, a);
   else
     hipLaunchKernelGGL((k_fold<T, OP, false>), dim3((unsigned)(g ? g : 1)), dim3(kFB), 0, s, a);
