@@ -1037,17 +1037,40 @@ static int allreduce_oneshot(mx_comm *c, oneshot_launch_fn ol, const std::vector
   return finish(c, s);
 }
 
-// the allocation holding [p, p+bytes): IPC handle, identity, offset of p
+// the allocation holding [p, p+bytes): IPC handle, identity, offset of p.
+// Handles of recent allocations are kept per process (the runtime buffer id
+// tells a live allocation from one re-made at the same address).
 static bool reg_export(const void *p, size_t bytes, RegBuf *b) {
+  struct Exp { uint64_t base, size, id; hipIpcMemHandle_t h; };
+  static std::mutex mu;
+  static std::vector<Exp> recent;   // most recent last, at most 16
   void *base = nullptr;
   size_t size = 0;
   unsigned long long id = 0;
   if (hipMemGetAddressRange(&base, &size, const_cast<void *>(p)) != hipSuccess || !base ||
       (const char *)p + bytes > (const char *)base + size ||
-      hipPointerGetAttribute(&id, HIP_POINTER_ATTRIBUTE_BUFFER_ID, (hipDeviceptr_t)base) != hipSuccess ||
-      hipIpcGetMemHandle(&b->h, base) != hipSuccess) {
+      hipPointerGetAttribute(&id, HIP_POINTER_ATTRIBUTE_BUFFER_ID, (hipDeviceptr_t)base) != hipSuccess) {
     (void)hipGetLastError();   // clear only the error this call raised
     return false;
+  }
+  bool hit = false;
+  {
+    std::lock_guard<std::mutex> lk(mu);
+    for (const Exp &e : recent)
+      if (e.base == (uint64_t)(uintptr_t)base && e.size == size && e.id == id) {
+        b->h = e.h;
+        hit = true;
+        break;
+      }
+  }
+  if (!hit) {
+    if (hipIpcGetMemHandle(&b->h, base) != hipSuccess) {
+      (void)hipGetLastError();
+      return false;
+    }
+    std::lock_guard<std::mutex> lk(mu);
+    if (recent.size() >= 16) recent.erase(recent.begin());
+    recent.push_back(Exp{(uint64_t)(uintptr_t)base, size, id, b->h});
   }
   b->base = (uint64_t)(uintptr_t)base;
   b->size = size;
