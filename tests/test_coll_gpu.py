@@ -540,8 +540,11 @@ _JOBS_ZC = [j for j in _JOBS if j[0].startswith(("allreduce", "reduce_scatter", 
 
 @pytest.mark.parametrize("n", [2, 3, 8])
 def test_multiprocess_allreduce_zero_copy(n):
+    import glob
+    before = set(glob.glob("/dev/shm/mx_reg_*"))
     env = {"MX_REG_MIN": "1", "MX_ONESHOT_MAX": "0"}
     got = _run_mp(n, _JOBS_ZC, env=env)
+    assert set(glob.glob("/dev/shm/mx_reg_*")) <= before, "registration page left in /dev/shm"
     _check_jobs(n, _JOBS_ZC, got)
     zc, staged = got[0][-1]
 
