@@ -97,13 +97,13 @@ int mx_comm_set_timeout(mx_comm_t *comm, double seconds);
 
 /* Data movement of the staged (above the one-shot range) allreduce.  Results
  * are identical under every protocol (same fold programs); only the traffic
- * pattern differs:
+ * pattern differs (the link bytes are the same):
  *   PUSH  each rank writes part p of its input into rank p's staging, then
- *         rank p folds locally and writes the result to every peer (each
- *         phase loads the links in one direction);
+ *         rank p folds locally and writes the result to every peer (two
+ *         xGMI phases with a flag round trip between them);
  *   PULL  each rank copies its input into its own staging (local HBM), then
  *         rank p's fold reads part p of every peer's staging over xGMI while
- *         it writes the result to every peer (both directions at once).
+ *         it writes the result to every peer (one xGMI phase, remote reads).
  * AUTO (the default) is PULL when some peer runs on another GPU and PUSH when
  * every rank shares one device; env MX_ALLREDUCE_PROTO=push|pull overrides
  * it at creation.  Every rank of a communicator must use the same protocol:
