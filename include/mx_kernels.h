@@ -154,6 +154,10 @@ int mx_is_device_ptr(const void *p);
 int mx_ptr_cache_forget(const void *p, size_t bytes);
 /* Block until all work queued on `stream` (NULL = default) completed. */
 int mx_stream_sync(void *stream);
+/* As mx_stream_sync, through a completion word in mapped host memory that a
+ * marker kernel raises last on the stream (the host sees it without the
+ * runtime's wake-up latency); falls back to mx_stream_sync after ~2 ms. */
+int mx_stream_sync_fast(void *stream);
 
 /* ---- memory and streams for the host components ----------------------
  * The coll component stages host buffers through device scratch (every

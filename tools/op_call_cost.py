@@ -8,7 +8,8 @@ is read once per process):
   round1   MX_PTR_CACHE=0, op_mi355x_stream=0: hipPointerGetAttributes x2 per
            call, launch + synchronise on the legacy default stream
   cache    pointer-range cache, legacy default stream
-  stream   pointer-range cache, the calling thread's own stream (default)
+  stream   pointer-range cache, the calling thread's own stream, hipStreamSynchronize
+  fastsync as stream, completion through the marker kernel's mapped word (default)
 
 Prints one JSON line per configuration and size: avg us per call and the
 kernel-only time (HIP events around 200 mx_reduce2 launches) for reference.
@@ -21,7 +22,8 @@ import sys
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 CONFIGS = {"round1": {"MX_PTR_CACHE": "0", "OMPI_MCA_op_mi355x_stream": "0"},
            "cache": {"MX_PTR_CACHE": "1", "OMPI_MCA_op_mi355x_stream": "0"},
-           "stream": {"MX_PTR_CACHE": "1", "OMPI_MCA_op_mi355x_stream": "1"}}
+           "stream": {"MX_PTR_CACHE": "1", "OMPI_MCA_op_mi355x_stream": "1", "OMPI_MCA_op_mi355x_fast_sync": "0"},
+           "fastsync": {"MX_PTR_CACHE": "1", "OMPI_MCA_op_mi355x_stream": "1", "OMPI_MCA_op_mi355x_fast_sync": "1"}}
 SIZES = [4 << 10, 64 << 10, 1 << 20]
 
 

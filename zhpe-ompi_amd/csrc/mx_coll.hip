@@ -735,9 +735,19 @@ static int reduce_scatter_segments(int alg, int n, const size_t *rcounts, size_t
   return MX_ERR_UNSUPPORTED;
 }
 
+// blocking completion: the mapped completion word (mx_stream_sync_fast)
+// unless MX_FAST_SYNC=0 selects hipStreamSynchronize
+static bool fast_sync() {
+  static const bool v = [] {
+    const char *e = getenv("MX_FAST_SYNC");
+    return !(e && *e == '0');
+  }();
+  return v;
+}
+
 static int finish(mx_comm *c, hipStream_t s) {
   if (c->defer) return MX_SUCCESS;   // request path: completion through the request's event
-  if (hipStreamSynchronize(s) != hipSuccess) return MX_ERR_HIP;
+  if (fast_sync() ? mx_stream_sync_fast(s) != MX_SUCCESS : hipStreamSynchronize(s) != hipSuccess) return MX_ERR_HIP;
   c->tail_valid = 0;                 // everything enqueued before is done
   if (!c->pending) prof_collect(c);
   if (c->err_host && *(volatile int *)c->err_host) {

@@ -230,6 +230,55 @@ extern "C" int mx_stream_sync(void *stream) {
   return mx_hip_rc(hipStreamSynchronize((hipStream_t)stream));
 }
 
+namespace {
+// one thread's completion word: the marker kernel, last on the stream,
+// raises it to the call's sequence number (system-scope store into mapped
+// host memory after a system fence), the host polls it
+__global__ void k_mark(uint64_t *w, uint64_t v) {
+  if (threadIdx.x == 0) {
+    __threadfence_system();
+    __hip_atomic_store(w, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
+}
+struct MarkWord {
+  uint64_t *host = nullptr, *dev = nullptr;
+  uint64_t seq = 0;
+  bool failed = false;
+  ~MarkWord() { if (host) (void)hipHostFree(host); }
+};
+thread_local MarkWord t_mark;
+}  // namespace
+
+// hipStreamSynchronize wakes the host several microseconds after the GPU is
+// done; a word in mapped host memory is seen as soon as the marker kernel
+// writes it (the p2p completion path).  After ~2 ms without the
+// word (a long kernel, or a fault) the call falls back to the runtime's wait,
+// which also reports errors.
+extern "C" int mx_stream_sync_fast(void *stream) {
+  MarkWord &m = t_mark;
+  if (!m.host && !m.failed) {
+    if (hipHostMalloc((void **)&m.host, 64, hipHostMallocMapped) != hipSuccess ||
+        hipHostGetDevicePointer((void **)&m.dev, m.host, 0) != hipSuccess) {
+      (void)hipGetLastError();
+      if (m.host) (void)hipHostFree(m.host);
+      m.host = nullptr;
+      m.failed = true;
+    } else {
+      *(volatile uint64_t *)m.host = 0;
+    }
+  }
+  hipStream_t s = (hipStream_t)stream;
+  if (!m.host) return mx_hip_rc(hipStreamSynchronize(s));
+  const uint64_t v = ++m.seq;
+  hipLaunchKernelGGL(k_mark, dim3(1), dim3(64), 0, s, m.dev, v);
+  if (int rc = mx_check_launch()) return rc;
+  for (long i = 0; i < (1L << 16); i++) {   // ~2 ms of polling
+    if (__atomic_load_n(m.host, __ATOMIC_ACQUIRE) >= v) return MX_SUCCESS;
+    __builtin_ia32_pause();
+  }
+  return mx_hip_rc(hipStreamSynchronize(s));
+}
+
 extern "C" int mx_copy(void *dst, const void *src, size_t bytes, void *stream) {
   if (bytes == 0) return MX_SUCCESS;
   if (!dst || !src) return MX_ERR_ARG;

@@ -100,9 +100,14 @@ static void *op_stream(void)
     return t_stream;
 }
 
+/* op_mi355x_fast_sync (default 1): wait through the marker kernel's mapped
+ * completion word instead of hipStreamSynchronize (profiles/r02/op_call_cost.txt) */
+static int g_fast_sync = -1;
+
 static int run_sync(void *s, int rc)
 {
-    if (rc == MX_SUCCESS) rc = mx_stream_sync(s);
+    if (g_fast_sync < 0) g_fast_sync = mx_ompi_host->mca_int("op_mi355x_fast_sync", 1) != 0;
+    if (rc == MX_SUCCESS) rc = g_fast_sync ? mx_stream_sync_fast(s) : mx_stream_sync(s);
     return rc;
 }
 
