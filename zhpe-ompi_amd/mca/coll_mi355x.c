@@ -218,6 +218,15 @@ static int comm_ready(mx_coll_module_t *m)
     return 1;
 }
 
+/* Blocking waits of the component (staging copies, reduce_local): through the
+ * marker kernel's mapped completion word unless coll_mi355x_fast_sync = 0 */
+static int g_fast_sync = -1;
+static int stream_wait(void *s)
+{
+    if (g_fast_sync < 0) g_fast_sync = mx_ompi_host->mca_int("coll_mi355x_fast_sync", 1) != 0;
+    return g_fast_sync ? mx_stream_sync_fast(s) : mx_stream_sync(s);
+}
+
 /* ---- staging of host / non-contiguous buffers ---------------------------- */
 
 static int scratch(mx_coll_module_t *m, int k, size_t bytes, void **p)
@@ -299,7 +308,7 @@ static int xfer_packed(mx_coll_module_t *m, const xbuf_t *x, void *packed_dev, i
         if (h) {
             int rc = to_device ? mx_pack(h, (size_t)x->count, x->user, packed_dev, 0, x->bytes, m->stream)
                                : mx_unpack(h, (size_t)x->count, x->user, packed_dev, 0, x->bytes, m->stream);
-            return rc ? rc : mx_stream_sync(m->stream);
+            return rc ? rc : stream_wait(m->stream);
         }
     }
     if (!mx_ompi_host->dtype_pack || !mx_ompi_host->dtype_unpack || !mx_ompi_host->dtype_span ||
@@ -311,18 +320,18 @@ static int xfer_packed(mx_coll_module_t *m, const xbuf_t *x, void *packed_dev, i
     if (!rc && on_dev) {   /* the convertor walks host memory: bring the span over */
         span = malloc((size_t)(hi - lo) ? (size_t)(hi - lo) : 1);
         if (!span) rc = MX_ERR_NOMEM;
-        else if (!(rc = mx_memcpy(span, user + lo, (size_t)(hi - lo), m->stream))) rc = mx_stream_sync(m->stream);
+        else if (!(rc = mx_memcpy(span, user + lo, (size_t)(hi - lo), m->stream))) rc = stream_wait(m->stream);
         user = span - lo;
     }
     if (!rc && to_device) {
         if (mx_ompi_host->dtype_pack(x->dt, x->count, user, packed) != OMPI_SUCCESS) rc = MX_ERR_ARG;
         if (!rc) rc = mx_memcpy(packed_dev, packed, x->bytes, m->stream);
-        if (!rc) rc = mx_stream_sync(m->stream);
+        if (!rc) rc = stream_wait(m->stream);
     } else if (!rc) {
-        if (!(rc = mx_memcpy(packed, packed_dev, x->bytes, m->stream))) rc = mx_stream_sync(m->stream);
+        if (!(rc = mx_memcpy(packed, packed_dev, x->bytes, m->stream))) rc = stream_wait(m->stream);
         if (!rc && mx_ompi_host->dtype_unpack(x->dt, x->count, packed, user) != OMPI_SUCCESS) rc = MX_ERR_ARG;
         if (!rc && on_dev && !(rc = mx_memcpy((char *)x->user + lo, span, (size_t)(hi - lo), m->stream)))
-            rc = mx_stream_sync(m->stream);
+            rc = stream_wait(m->stream);
     }
     free(span);
     free(packed);
@@ -356,7 +365,7 @@ static int xout(mx_coll_module_t *m, xbuf_t *x, size_t bytes)
     if (!x->user || !bytes) return MX_SUCCESS;
     if (!x->contiguous) return xfer_packed(m, x, x->dev, 0);
     int rc = mx_memcpy(x->user, x->dev, bytes, m->stream);
-    return rc ? rc : mx_stream_sync(m->stream);
+    return rc ? rc : stream_wait(m->stream);
 }
 
 /* The device work of a call starts after what the legacy default stream
@@ -487,7 +496,7 @@ static int mx_coll_reduce_local(const void *inbuf, void *inoutbuf, int count, st
         if (!m->stream && mx_stream_create_ordered(&m->stream) != MX_SUCCESS) m->stream = NULL;
         int rc = begin(m);
         if (!rc) rc = mx_reduce2(opi, slot, inbuf, inoutbuf, (size_t)count, m->stream);
-        if (!rc) rc = mx_stream_sync(m->stream);
+        if (!rc) rc = stream_wait(m->stream);
         return map_rc(rc);
     }
     return m->prev_reduce_local(inbuf, inoutbuf, count, dtype, op, m->prev_reduce_local_module);
