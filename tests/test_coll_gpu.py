@@ -529,7 +529,8 @@ _JOBS_PULL = [j for j in _JOBS if j[0].startswith("allreduce")] + [("reduce", 10
 # every staged shape of _JOBS folded straight between the ranks' own buffers,
 # in place, chunk-sized counts, and a call whose ranks disagree on alignment
 # (every rank falls back to the staged path together)
-_JOBS_ZC = [j for j in _JOBS if j[0].startswith(("allreduce", "reduce_scatter", "allgather", "bcast"))
+_JOBS_ZC = [j for j in _JOBS if j[0].startswith(("allreduce", "reduce_scatter", "allgather", "bcast", "reduce",
+                                                  "scan", "exscan"))
             and j[0] != "reduce_scatter_block"] + [
     ("allreduce_mis", 30001, "SUM", "FLOAT", "auto"),
     ("allreduce_mis", 20011, "MAX", "DOUBLE", "ring"),
@@ -551,7 +552,8 @@ def test_multiprocess_allreduce_zero_copy(n):
     def eligible(kind, count, t):
         # registered path: every rank's blocks at one misalignment mod 16
         # (IN_PLACE reduce_scatter stays staged; neither counts it)
-        if kind in ("allreduce", "allreduce_inplace", "bcast", "bcast_root0"):
+        if kind in ("allreduce", "allreduce_inplace", "bcast", "bcast_root0", "reduce", "reduce_inplace", "scan",
+                    "exscan"):
             return True
         if kind == "reduce_scatter":
             rc, es = [count + 3 * r for r in range(n)], mxompi.type_size(t)

@@ -2023,10 +2023,24 @@ static int vm_partitioned(mx_comm *c, vm_launch_fn vl, const std::vector<VmSeg> 
                           size_t count, size_t es, uint32_t dest_mask, int info_rank, int info_bit, hipStream_t s) {
   const int n = c->size, r = c->rank;
   const bool me_dest = (dest_mask >> r) & 1;
-  const size_t ce = chunk_elems(c, count, es);
+  // zero-copy input (as mx_allreduce): part owners read the contributions
+  // straight from the registered sbufs; outputs still go through the
+  // destinations' uncached gather areas
+  const char *ps[MAXR];
+  char *pr[MAXR];
+  int zc = 0;
+  if (c->reg_shm && !c->defer && c->reg_min && count * es >= c->reg_min) {
+    // a rank without an output (reduce: non-root, whose rbuf MPI ignores) exports only its input
+    const bool out = me_dest && rb;
+    zc = reg_exchange(c, sb, count * es, out ? rb : (char *)sb, out ? count * es : 0, (int)((uintptr_t)sb & 15),
+                      true, ps, pr);
+    if (zc < 0) return zc;
+  }
+  if (zc) c->st.zero_copy_calls++;
+  const size_t ce = chunk_elems(c, count, es, zc);
   for (size_t c0 = 0; c0 < count; c0 += ce) {
     const size_t cl = std::min(ce, count - c0);
-    const Layout L = layout_for(n, ce, es);
+    const Layout L = layout_for(n, ce, es, zc);
     size_t off[MAXR], len[MAXR];
     blockcount(cl, n, off, len);
     const uint64_t g = ++c->gen;
@@ -2034,7 +2048,7 @@ static int vm_partitioned(mx_comm *c, vm_launch_fn vl, const std::vector<VmSeg> 
     if ((rc = wait_all(c, FLAG_DONE, g - 1, s))) return rc;
     CopyArgs ca;
     memset(&ca, 0, sizeof ca);
-    for (int q = 0; q < n; q++) {
+    for (int q = 0; q < n && !zc; q++) {
       if (q == r || !len[q]) continue;
       const size_t e0 = c0 + off[q];
       ca.j[ca.n++] = CopyJob{sb + e0 * es, c->peer_staging[q] + (size_t)r * L.slot + ((e0 * es) & 15), len[q] * es};
@@ -2055,7 +2069,8 @@ static int vm_partitioned(mx_comm *c, vm_launch_fn vl, const std::vector<VmSeg> 
       a.poison = c->poison;
       if (info_rank >= 0 && info_rank != r) a.info = c->flagmem + FLAG_READY * MAXR + info_rank;
       a.info_host = info_bit;
-      for (int j = 0; j < n; j++) a.src[j] = ((j == r) ? sb + e0 * es : c->staging + (size_t)j * L.slot + mis) + sh;
+      for (int j = 0; j < n; j++)
+        a.src[j] = ((j == r) ? sb + e0 * es : zc ? ps[j] + e0 * es : c->staging + (size_t)j * L.slot + mis) + sh;
       for (int d = 0; d < n; d++) {
         if (!((dest_mask >> d) & 1)) continue;
         a.dst[d] = ((d == r) ? rb + e0 * es : c->peer_staging[d] + L.gather_off + ((c0 * es) & 15) + off[r] * es) + sh;
@@ -2069,8 +2084,11 @@ static int vm_partitioned(mx_comm *c, vm_launch_fn vl, const std::vector<VmSeg> 
       prof_end(c, s, 0, (double)(n + nemit) * (double)a.n * (double)es);
     }
     if ((rc = signal_all(c, FLAG_PUSHED, g, s))) return rc;
-    if (me_dest) {
+    // zero-copy: every rank waits -- its sbuf is read by the peers' folds
+    if (me_dest || zc) {
       if ((rc = wait_all(c, FLAG_PUSHED, g, s))) return rc;
+    }
+    if (me_dest) {
       memset(&ca, 0, sizeof ca);
       for (int q = 0; q < n; q++) {
         if (q == r || !len[q]) continue;
