@@ -327,6 +327,11 @@ def _mp_worker(rank, n, port, staging, jobs, q, env=None):
                 x = _dev(gen(t, op, count * n, 7000 + rank))
                 comm.reduce_scatter_block(mxompi.IN_PLACE, x.data_ptr(), count, t, op, alg, st)
                 results.append(x.cpu().numpy()[: count * es].tobytes())
+            elif kind == "reduce_scatter_block_oop":
+                x = _dev(gen(t, op, count * n, 7000 + rank))
+                out = torch.zeros(count * es, dtype=torch.uint8, device="cuda")
+                comm.reduce_scatter_block(x.data_ptr(), out.data_ptr(), count, t, op, alg, st)
+                results.append(out.cpu().numpy().tobytes())
         comm.close()
         dist.destroy_process_group()
         q.put((rank, "ok", results))
@@ -477,7 +482,7 @@ def _check_jobs(n, jobs, got):
                                                 mxompi.TYPE[t], f"symheap active-set reduce rank {r}")
                 elif sub is not None:
                     np.testing.assert_array_equal(np.frombuffer(sub_b, np.uint8), xs[0])   # PE 0 not in the set
-        elif kind == "reduce_scatter_block":
+        elif kind in ("reduce_scatter_block", "reduce_scatter_block_oop"):
             xs = [gen(t, op, count * n, 7000 + r) for r in range(n)]
             exp = [np.zeros(count * es, np.uint8) for _ in range(n)]
             T = _tree_oracle()
@@ -536,6 +541,8 @@ _JOBS_ZC = [j for j in _JOBS if j[0].startswith(("allreduce", "reduce_scatter", 
     ("allreduce_mis", 20011, "MAX", "DOUBLE", "ring"),
     ("allreduce", 100003, "SUM", "FLOAT", "auto"),
     ("allgather", 65536, "BAND", "UINT8_T", "auto"),
+    ("reduce_scatter_block_oop", 4096, "SUM", "FLOAT", "auto"),
+    ("reduce_scatter_block", 3000, "SUM", "FLOAT", "auto"),      # IN_PLACE: staged
     ("stats", 0, "SUM", "FLOAT", "auto")]
 
 
@@ -560,6 +567,8 @@ def test_multiprocess_allreduce_zero_copy(n):
             return all(sum(rc[:r]) * es % 16 == 0 for r in range(n))
         if kind == "allgather":
             return count % 16 == 0
+        if kind == "reduce_scatter_block_oop":
+            return count * mxompi.type_size(t) % 16 == 0
         return False
     n_mis = sum(1 for j in _JOBS_ZC if j[0] == "allreduce_mis")
     n_zc = sum(1 for j in _JOBS_ZC if eligible(j[0], j[1], j[3]))

@@ -2118,6 +2118,38 @@ static int vm_scatter_blocks(mx_comm *c, vm_launch_fn vl, const VmProg &p, const
   size_t disp[MAXR], total = 0, maxc = 0;
   for (int j = 0; j < n; j++) { disp[j] = total; total += rcounts[j]; maxc = std::max(maxc, rcounts[j]); }
   if (!maxc) return finish(c, s);
+  if (c->reg_shm && !c->defer && c->reg_min && total * es >= c->reg_min && sb != rb) {
+    // zero-copy (as mx_reduce_scatter): block r folded from every rank's
+    // registered sbuf into my rbuf; IN_PLACE stays staged
+    const char *ps[MAXR];
+    char *pr[MAXR];
+    const bool lok = (((uintptr_t)rb - ((uintptr_t)sb + disp[r] * es)) & 15) == 0;
+    const int zc = reg_exchange(c, sb, total * es, rb, rcounts[r] * es, (int)((uintptr_t)sb & 15), lok, ps, pr);
+    if (zc < 0) return zc;
+    if (zc) {
+      const uint64_t gen = ++c->gen;
+      int rc;
+      c->st.zero_copy_calls++;
+      if ((rc = signal_all(c, FLAG_READY, gen << 1, s))) return rc;
+      if ((rc = wait_all(c, FLAG_READY, gen << 1, s))) return rc;
+      if (rcounts[r]) {
+        VmArgs a;
+        memset(&a, 0, sizeof a);
+        a.poison = c->poison;
+        for (int j = 0; j < n; j++) a.src[j] = ps[j] + disp[r] * es;
+        a.dst[r] = rb;
+        a.n = rcounts[r];
+        a.p = p;
+        prof_begin(c, s);
+        if ((rc = vl(a, s))) return rc;
+        prof_end(c, s, 0, (double)(n + 1) * (double)rcounts[r] * (double)es);
+      }
+      if ((rc = signal_all(c, FLAG_PUSHED, gen, s))) return rc;   // done reading the peers' sbufs
+      if ((rc = wait_all(c, FLAG_PUSHED, gen, s))) return rc;
+      if ((rc = signal_all(c, FLAG_DONE, gen, s))) return rc;
+      return finish(c, s);
+    }
+  }
   // IN_PLACE with my block starting inside the range my result overwrites:
   // fold into a spare slot after the n slots, then copy
   const bool overlap = sb == rb && disp[r] != 0 && disp[r] < rcounts[r];
