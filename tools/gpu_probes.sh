@@ -6,7 +6,7 @@ cd "$GRAFT_REPO_ROOT"
 export TMPDIR=/tmp HSA_ENABLE_IPC_MODE_LEGACY=0
 O=gpurun_out
 mkdir -p $O
-STAGES=${STAGES:-"convertor sector latency p2p ipc stream opcost"}
+STAGES=${STAGES:-"convertor sector latency p2p ipc stream opcost datapath"}
 TYPES=$(python -c "
 import sys; sys.path.insert(0, 'tests'); import golden_io
 print(' '.join(r['name'] for r in golden_io.ddt_records()[1]))")
@@ -29,9 +29,15 @@ for s in $STAGES; do
       done ;;
     p2p)         # send/recv ping-pong half round trip
       timeout -k 10 300 python -u tools/p2p_lat.py 2>&1 | grep half >> $O/probe_p2p.txt || exit 1 ;;
-    ipc)         # IPC handle contents and same-VA imports, 2-3 processes
+    ipc)         # IPC handle contents, same-VA imports (2-3 processes), imports across a re-allocation
       timeout -k 10 60 ./tools/ipc_handle_probe > $O/probe_ipc_handle.txt 2>&1 || exit 1
-      timeout -k 10 60 ./tools/ipc_alias_probe > $O/probe_ipc_alias.txt 2>&1 || exit 1 ;;
+      timeout -k 10 60 ./tools/ipc_alias_probe > $O/probe_ipc_alias.txt 2>&1 || exit 1
+      hipcc --offload-arch=gfx950 -O2 -o /tmp/ipc_realloc_probe tools/ipc_realloc_probe.cpp || exit 1
+      timeout -k 10 60 /tmp/ipc_realloc_probe > $O/probe_ipc_realloc.txt 2>&1 || exit 1 ;;
+    datapath)    # allreduce latency per size and data movement (zero-copy / push / pull), 2 and 4 processes
+      for n in 2 4; do
+        timeout -k 10 300 python -u tools/lat_probe.py $n zc,push,pull 2>&1 | grep "^n=. {" >> $O/probe_datapath.txt || exit 1
+      done ;;
     stream)      # host cost of launch / sync disciplines
       timeout -k 10 60 ./tools/stream_probe > $O/probe_stream.txt 2>&1 || exit 1 ;;
     opcost)      # ompi_op_reduce through op/mi355x
