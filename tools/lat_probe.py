@@ -36,7 +36,10 @@ def worker(rank, n, port, q, modes):
         cnt = nb // 4
         row = {"bytes": nb}
         for mode in modes:
-            if mode == "zc":
+            if mode == "default":          # the library defaults: zero-copy from 4 MiB, auto protocol
+                comm.set_reg_min(4 << 20)
+                comm.set_protocol("auto")
+            elif mode == "zc":
                 comm.set_reg_min(1)
             elif mode in ("push", "pull"):
                 comm.set_reg_min(0)

@@ -178,6 +178,31 @@ __global__ void k_wait(const uint64_t *flags, uint32_t mask, uint64_t value, uin
   __atomic_thread_fence(__ATOMIC_ACQUIRE);
 }
 
+// k_signal then k_wait in one launch (one kernel and one inter-kernel gap
+// less per phase): thread j raises my flag at peer j, then spins on flag j
+// of mine.  Poisoned: neither.
+__global__ void k_signal_wait(SignalArgs a, const uint64_t *flags, uint32_t mask, uint64_t value,
+                              uint64_t timeout_ticks, int *err, int *poison) {
+  const int j = threadIdx.x;
+  if (!poisoned(a.poison)) {
+    __threadfence_system();
+    if (j < a.n && a.peer_flag[j])
+      __hip_atomic_store(a.peer_flag[j], a.value, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    if (j < MAXR && ((mask >> j) & 1)) {
+      const uint64_t t0 = wall_clock64();
+      while (__hip_atomic_load(&flags[j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) < value) {
+        __builtin_amdgcn_s_sleep(2);
+        if (wall_clock64() - t0 > timeout_ticks) {
+          raise_timeout(err, poison);
+          break;
+        }
+      }
+    }
+  }
+  __syncthreads();
+  __atomic_thread_fence(__ATOMIC_ACQUIRE);
+}
+
 }  // namespace mx
 
 using namespace mx;
@@ -963,6 +988,21 @@ static int signal_all(mx_comm *c, int kind, uint64_t value, hipStream_t s) {
   return mx_check_launch();
 }
 
+// signal_all(kind, svalue) + wait_all(kind, wvalue) as one launch
+static int signal_wait_all(mx_comm *c, int kind, uint64_t svalue, uint64_t wvalue, hipStream_t s) {
+  SignalArgs a;
+  memset(&a, 0, sizeof a);
+  a.n = c->size;
+  a.value = svalue;
+  a.poison = c->poison;
+  for (int p = 0; p < c->size; p++)
+    a.peer_flag[p] = (p == c->rank) ? nullptr : c->peer_flags[p] + kind * MAXR + c->rank;
+  const uint32_t all = (c->size >= 32) ? 0xffffffffu : ((1u << c->size) - 1);
+  hipLaunchKernelGGL(k_signal_wait, dim3(1), dim3(64), 0, s, a, (const uint64_t *)(c->flagmem + kind * MAXR),
+                     all & ~(1u << c->rank), wvalue, c->timeout_ticks, c->err_dev, c->poison);
+  return mx_check_launch();
+}
+
 static int wait_mask(mx_comm *c, int kind, uint32_t mask, uint64_t value, hipStream_t s) {
   hipLaunchKernelGGL(k_wait, dim3(1), dim3(64), 0, s, (const uint64_t *)(c->flagmem + kind * MAXR), mask, value,
                      c->timeout_ticks, c->err_dev, c->poison);
@@ -1278,9 +1318,12 @@ extern "C" int mx_allreduce(mx_comm_t *c, const void *sbuf, void *rbuf, size_t c
     blockcount(cl, n, off, len);
     const uint64_t g = ++c->gen;
     int rc;
-    // (a) peers finished the previous round with their staging
-    if ((rc = wait_all(c, FLAG_DONE, g - 1, s))) return rc;
     const bool pull = c->proto == MX_PROTO_PULL;
+    // (a) peers finished the previous round with their staging.  Only PUSH
+    // writes into peers' staging before the READY exchange; otherwise a peer's
+    // READY(g) -- raised on its stream after everything it did in round g-1 --
+    // already implies it (DONE(g-1) comes earlier on the same stream).
+    if (!zc && !pull && (rc = wait_all(c, FLAG_DONE, g - 1, s))) return rc;
     const size_t mis0 = (c0 * es) & 15;
     CopyArgs ca;
     memset(&ca, 0, sizeof ca);
@@ -1304,8 +1347,7 @@ extern "C" int mx_allreduce(mx_comm_t *c, const void *sbuf, void *rbuf, size_t c
     prof_begin(c, s);
     if ((rc = copy_launch(c, ca, s))) return rc;
     prof_end(c, s, 1, 0);
-    if ((rc = signal_all(c, FLAG_READY, g << 1, s))) return rc;
-    if ((rc = wait_all(c, FLAG_READY, g << 1, s))) return rc;
+    if ((rc = signal_wait_all(c, FLAG_READY, g << 1, g << 1, s))) return rc;
     // (c) fold my part, store to my rbuf and every peer's gather area
     // (PULL: the peers' contributions are read from their staging over xGMI)
     if (len[r]) {
@@ -1327,8 +1369,7 @@ extern "C" int mx_allreduce(mx_comm_t *c, const void *sbuf, void *rbuf, size_t c
       for (const Seg &sg : segs)
         if ((rc = run_fold(c, fl, sg, e0, sp, n, dp, nd, es, s, zc))) return rc;
     }
-    if ((rc = signal_all(c, FLAG_PUSHED, g, s))) return rc;
-    if ((rc = wait_all(c, FLAG_PUSHED, g, s))) return rc;
+    if ((rc = signal_wait_all(c, FLAG_PUSHED, g, g, s))) return rc;
     // (d) copy the other parts from my gather area into rbuf
     memset(&ca, 0, sizeof ca);
     for (int p = 0; p < n; p++) {
@@ -1390,8 +1431,7 @@ extern "C" int mx_reduce_scatter(mx_comm_t *c, const void *sbuf, void *rbuf, con
     if (zc) {
       const uint64_t g = ++c->gen;
       c->st.zero_copy_calls++;
-      if ((rc = signal_all(c, FLAG_READY, g << 1, s))) return rc;
-      if ((rc = wait_all(c, FLAG_READY, g << 1, s))) return rc;
+      if ((rc = signal_wait_all(c, FLAG_READY, g << 1, g << 1, s))) return rc;
       if (rcounts[r]) {
         const char *sp[MAXR];
         for (int j = 0; j < n; j++) sp[j] = ps[j] + disp[r] * es;
@@ -1399,8 +1439,7 @@ extern "C" int mx_reduce_scatter(mx_comm_t *c, const void *sbuf, void *rbuf, con
         for (const Seg &sg : segs)
           if ((rc = run_fold(c, fl, sg, disp[r], sp, n, dp, 1, es, s, true))) return rc;
       }
-      if ((rc = signal_all(c, FLAG_PUSHED, g, s))) return rc;     // every peer is done with my sbuf
-      if ((rc = wait_all(c, FLAG_PUSHED, g, s))) return rc;
+      if ((rc = signal_wait_all(c, FLAG_PUSHED, g, g, s))) return rc;     // every peer is done with my sbuf
       if ((rc = signal_all(c, FLAG_DONE, g, s))) return rc;
       return finish(c, s);
     }
@@ -1427,8 +1466,7 @@ extern "C" int mx_reduce_scatter(mx_comm_t *c, const void *sbuf, void *rbuf, con
     prof_begin(c, s);
     if ((rc = copy_launch(c, ca, s))) return rc;
     prof_end(c, s, 1, 0);
-    if ((rc = signal_all(c, FLAG_READY, g << 1, s))) return rc;
-    if ((rc = wait_all(c, FLAG_READY, g << 1, s))) return rc;
+    if ((rc = signal_wait_all(c, FLAG_READY, g << 1, g << 1, s))) return rc;
     if (k0 < rcounts[r]) {
       const size_t kl = std::min(kc, rcounts[r] - k0), e0 = disp[r] + k0, mis = (e0 * es) & 15;
       const char *sp[MAXR];
@@ -1477,16 +1515,14 @@ extern "C" int mx_allgather(mx_comm_t *c, const void *sbuf, void *rbuf, size_t b
       const uint64_t g = ++c->gen;
       int rc;
       c->st.zero_copy_calls++;
-      if ((rc = signal_all(c, FLAG_READY, g << 1, s))) return rc;   // every sbuf holds its block
-      if ((rc = wait_all(c, FLAG_READY, g << 1, s))) return rc;
+      if ((rc = signal_wait_all(c, FLAG_READY, g << 1, g << 1, s))) return rc;   // every sbuf holds its block
       CopyArgs ca;
       memset(&ca, 0, sizeof ca);
       for (int p = 0; p < n; p++)
         if (p != r) ca.j[ca.n++] = CopyJob{ps[p], rb + (size_t)p * bytes, bytes};
       if (sb != rb + (size_t)r * bytes) ca.j[ca.n++] = CopyJob{sb, rb + (size_t)r * bytes, bytes};
       if ((rc = copy_launch(c, ca, s))) return rc;
-      if ((rc = signal_all(c, FLAG_PUSHED, g, s))) return rc;     // done reading the peers' sbufs
-      if ((rc = wait_all(c, FLAG_PUSHED, g, s))) return rc;
+      if ((rc = signal_wait_all(c, FLAG_PUSHED, g, g, s))) return rc;     // done reading the peers' sbufs
       if ((rc = signal_all(c, FLAG_DONE, g, s))) return rc;
       return finish(c, s);
     }
@@ -1506,8 +1542,7 @@ extern "C" int mx_allgather(mx_comm_t *c, const void *sbuf, void *rbuf, size_t b
       if (p != r) ca.j[ca.n++] = CopyJob{sb + o, c->peer_staging[p] + (size_t)r * slot + ((r * bytes + o) & 15), l};
     if (sb != rb + (size_t)r * bytes) ca.j[ca.n++] = CopyJob{sb + o, rb + (size_t)r * bytes + o, l};
     if ((rc = copy_launch(c, ca, s))) return rc;
-    if ((rc = signal_all(c, FLAG_READY, g << 1, s))) return rc;
-    if ((rc = wait_all(c, FLAG_READY, g << 1, s))) return rc;
+    if ((rc = signal_wait_all(c, FLAG_READY, g << 1, g << 1, s))) return rc;
     memset(&ca, 0, sizeof ca);
     for (int p = 0; p < n; p++)
       if (p != r)
@@ -2045,7 +2080,8 @@ static int vm_partitioned(mx_comm *c, vm_launch_fn vl, const std::vector<VmSeg> 
     blockcount(cl, n, off, len);
     const uint64_t g = ++c->gen;
     int rc;
-    if ((rc = wait_all(c, FLAG_DONE, g - 1, s))) return rc;
+    // zero-copy writes nothing of a peer's before READY(g), which implies DONE(g-1) (mx_allreduce)
+    if (!zc && (rc = wait_all(c, FLAG_DONE, g - 1, s))) return rc;
     CopyArgs ca;
     memset(&ca, 0, sizeof ca);
     for (int q = 0; q < n && !zc; q++) {
@@ -2056,8 +2092,8 @@ static int vm_partitioned(mx_comm *c, vm_launch_fn vl, const std::vector<VmSeg> 
     prof_begin(c, s);
     if ((rc = copy_launch(c, ca, s))) return rc;
     prof_end(c, s, 1, 0);
-    if ((rc = signal_all(c, FLAG_READY, (g << 1) | (uint64_t)(r == info_rank ? info_bit : 0), s))) return rc;
-    if ((rc = wait_all(c, FLAG_READY, g << 1, s))) return rc;
+    if ((rc = signal_wait_all(c, FLAG_READY, (g << 1) | (uint64_t)(r == info_rank ? info_bit : 0), g << 1, s)))
+      return rc;
     // my part [e0, e1) of this chunk, one launch per program segment in it
     const size_t e0 = c0 + off[r], e1 = e0 + len[r];
     for (const VmSeg &sg : segs) {
@@ -2130,8 +2166,7 @@ static int vm_scatter_blocks(mx_comm *c, vm_launch_fn vl, const VmProg &p, const
       const uint64_t gen = ++c->gen;
       int rc;
       c->st.zero_copy_calls++;
-      if ((rc = signal_all(c, FLAG_READY, gen << 1, s))) return rc;
-      if ((rc = wait_all(c, FLAG_READY, gen << 1, s))) return rc;
+      if ((rc = signal_wait_all(c, FLAG_READY, gen << 1, gen << 1, s))) return rc;
       if (rcounts[r]) {
         VmArgs a;
         memset(&a, 0, sizeof a);
@@ -2144,8 +2179,7 @@ static int vm_scatter_blocks(mx_comm *c, vm_launch_fn vl, const VmProg &p, const
         if ((rc = vl(a, s))) return rc;
         prof_end(c, s, 0, (double)(n + 1) * (double)rcounts[r] * (double)es);
       }
-      if ((rc = signal_all(c, FLAG_PUSHED, gen, s))) return rc;   // done reading the peers' sbufs
-      if ((rc = wait_all(c, FLAG_PUSHED, gen, s))) return rc;
+      if ((rc = signal_wait_all(c, FLAG_PUSHED, gen, gen, s))) return rc;   // done reading the peers' sbufs
       if ((rc = signal_all(c, FLAG_DONE, gen, s))) return rc;
       return finish(c, s);
     }
@@ -2173,8 +2207,7 @@ static int vm_scatter_blocks(mx_comm *c, vm_launch_fn vl, const VmProg &p, const
     prof_begin(c, s);
     if ((rc = copy_launch(c, ca, s))) return rc;
     prof_end(c, s, 1, 0);
-    if ((rc = signal_all(c, FLAG_READY, gen << 1, s))) return rc;
-    if ((rc = wait_all(c, FLAG_READY, gen << 1, s))) return rc;
+    if ((rc = signal_wait_all(c, FLAG_READY, gen << 1, gen << 1, s))) return rc;
     if (k0 < rcounts[r]) {
       const size_t kl = std::min(kc, rcounts[r] - k0), e0 = disp[r] + k0, mis = (e0 * es) & 15;
       VmArgs a;
