@@ -104,9 +104,8 @@ int mx_comm_set_timeout(mx_comm_t *comm, double seconds);
  *   PULL  each rank copies its input into its own staging (local HBM), then
  *         rank p's fold reads part p of every peer's staging over xGMI while
  *         it writes the result to every peer (one xGMI phase, remote reads).
- * AUTO (the default) is PULL when some peer runs on another GPU and PUSH when
- * every rank shares one device; env MX_ALLREDUCE_PROTO=push|pull overrides
- * it at creation.  Every rank of a communicator must use the same protocol:
+ * AUTO (the default) is PULL (measured ahead of PUSH on one GPU at every size
+ * from 2 MiB); env MX_ALLREDUCE_PROTO=push|pull overrides it at creation.  Every rank of a communicator must use the same protocol:
  * set it on all ranks between collectives.  Returns the protocol in force
  * (MX_PROTO_PUSH / MX_PROTO_PULL) or an error. */
 enum { MX_PROTO_AUTO = 0, MX_PROTO_PUSH = 1, MX_PROTO_PULL = 2 };

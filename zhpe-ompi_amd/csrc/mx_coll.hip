@@ -376,7 +376,10 @@ static int proto_default(const mx_comm *c) {
   const char *e = getenv("MX_ALLREDUCE_PROTO");
   if (e && !strcmp(e, "push")) return MX_PROTO_PUSH;
   if (e && !strcmp(e, "pull")) return MX_PROTO_PULL;
-  return c->xdev ? MX_PROTO_PULL : MX_PROTO_PUSH;
+  // PULL: one xGMI phase and no DONE(g-1) wait; measured ahead of PUSH on one
+  // GPU too, so it no longer depends on c->xdev
+  (void)c;
+  return MX_PROTO_PULL;
 }
 
 extern "C" int mx_comm_set_protocol(mx_comm_t *c, int proto) {

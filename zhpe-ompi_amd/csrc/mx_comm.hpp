@@ -138,9 +138,8 @@ struct mx_comm {
   // staged allreduce data movement (MX_PROTO_*): PUSH writes each part to
   // its owner before the fold (two xGMI phases); PULL copies the input into
   // the rank's own staging and the owner's fold reads the parts over xGMI
-  // while it writes results to the peers (one xGMI phase).  `xdev`: some
-  // peer runs on another GPU (PCI bus ids differ), which makes PULL the
-  // default.
+  // while it writes results to the peers (one xGMI phase; the default).
+  // `xdev`: some peer runs on another GPU (PCI bus ids differ).
   int proto, xdev;
   // user-buffer registration (zero-copy allreduce): a host
   // shared-memory page per communicator where every rank publishes the IPC
