@@ -183,12 +183,12 @@ def bench_allreduce(torch, mx, dist, rank, world, dev, steps, warmup, nbytes=256
     comm.set_profiling(False)
     # data-movement A/B at the headline size (results are identical under
     # all three): zero-copy between registered user buffers (the default above
-    # 4 MiB per rank), and the staged path under PUSH and PULL (the staged
-    # default: PULL when the ranks sit on different GPUs, PUSH on one GPU)
+    # 256 KiB per rank), and the staged path under PUSH and PULL (the staged
+    # default: PULL)
     proto_default = comm.protocol()
     proto_ab = {"staged_protocol": proto_default,
                 "timed_path": "zero_copy" if st["zero_copy_calls"] else "staged"}
-    for name, reg, proto in (("staged_push", 0, "push"), ("staged_pull", 0, "pull"), ("zero_copy", 4 << 20, None)):
+    for name, reg, proto in (("staged_push", 0, "push"), ("staged_pull", 0, "pull"), ("zero_copy", 256 << 10, None)):
         try:
             comm.set_reg_min(reg)
         except mx.MxError:

@@ -120,7 +120,7 @@ int mx_comm_get_protocol(const mx_comm_t *comm);
  * rank's sbuf into every rank's rbuf -- no staging copies.  A call falls back
  * to the staged path on every rank when any rank's buffers cannot be
  * exported or mapped, or their misalignments mod 16 differ.  Default
- * 4 MiB (env MX_REG_MIN at creation; 0 = off).  Same value on every rank.
+ * 256 KiB (env MX_REG_MIN at creation; 0 = off).  Same value on every rank.
  * Returns MX_ERR_UNSUPPORTED when the communicator has no registration page
  * (single rank, local communicator, or /dev/shm unavailable on some rank). */
 int mx_comm_set_reg_min(mx_comm_t *comm, size_t min_bytes);

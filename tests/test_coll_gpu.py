@@ -521,9 +521,9 @@ def test_multiprocess_ipc_bitexact_8_ranks():
     _check_jobs(8, _JOBS8, _run_mp(8, _JOBS8))
 
 
-# the PULL protocol (mx_comm_set_protocol; the default when ranks sit on
-# different GPUs, so the driver's 8-GPU run takes it): same fold programs,
-# peers' parts read over IPC from their own staging.  Every staged allreduce
+# the staged protocols (mx_comm_set_protocol; PULL is the default): same fold
+# programs, PULL reads the peers' parts over IPC from their own staging, PUSH
+# writes them into the owner's staging first.  Every staged allreduce
 # shape of _JOBS (chunked, in place, element / 16-byte paths, every algorithm)
 # plus a rooted reduce between them (same staging, other layout)
 _JOBS_PULL = [j for j in _JOBS if j[0].startswith("allreduce")] + [("reduce", 100003, "SUM", "FLOAT", "auto"),
@@ -577,9 +577,12 @@ def test_multiprocess_allreduce_zero_copy(n):
         assert got[r][-1] == got[0][-1]
 
 
+@pytest.mark.parametrize("proto", ["push", "pull"])
 @pytest.mark.parametrize("n", [2, 3, 8])
-def test_multiprocess_allreduce_pull_protocol(n):
-    env = {"MX_ALLREDUCE_PROTO": "pull", "MX_ONESHOT_MAX": "0", "MX_REG_MIN": "0"}   # every call staged
+def test_multiprocess_allreduce_staged_protocols(n, proto):
+    """Both staged data movements with registration off (the default path
+    takes zero-copy above 256 KiB)."""
+    env = {"MX_ALLREDUCE_PROTO": proto, "MX_ONESHOT_MAX": "0", "MX_REG_MIN": "0"}   # every call staged
     _check_jobs(n, _JOBS_PULL, _run_mp(n, _JOBS_PULL, env=env))
 
 

@@ -36,8 +36,8 @@ def worker(rank, n, port, q, modes):
         cnt = nb // 4
         row = {"bytes": nb}
         for mode in modes:
-            if mode == "default":          # the library defaults: zero-copy from 4 MiB, auto protocol
-                comm.set_reg_min(4 << 20)
+            if mode == "default":          # the library defaults: zero-copy from 256 KiB, auto protocol
+                comm.set_reg_min(256 << 10)
                 comm.set_protocol("auto")
             elif mode == "zc":
                 comm.set_reg_min(1)

@@ -135,12 +135,13 @@ static int copy_launch(const mx_comm *c, CopyArgs &a, hipStream_t s) {
 // cross-GPU flags: generation-tagged, system scope, bounded spin
 // ---------------------------------------------------------------------------
 
-// bytes per rank (default; MX_ONESHOT_MAX overrides).  Measured crossover on
-// ranks sharing one GPU: 256 KiB - 1 MiB (tools/lat_probe.py); there every
-// rank's n-1 pushes land in one HBM, over xGMI they spread over n-1 links
-// while the staged path still pays its nine dependent launches, so the
-// one-shot range is set at the top of that bracket.
-constexpr size_t kOneShotMax = 1 << 20;
+// bytes per rank (default; MX_ONESHOT_MAX overrides).  Round 1 put the
+// crossover with the nine-launch staged path at 256 KiB - 1 MiB; since the
+// staged / zero-copy rounds take six launches and the completion word, they
+// win from 256 KiB (2 ranks on one GPU: 256 KiB 27 vs 31 us, 1 MiB 26 vs
+// 51 us; profiles/r02/allreduce_oneshot_crossover.txt), so one-shot keeps
+// the messages up to 128 KiB (24.7 vs 26.3 us there).
+constexpr size_t kOneShotMax = 128 << 10;
 
 static size_t oneshot_max() {
   const char *e = getenv("MX_ONESHOT_MAX");
@@ -320,7 +321,9 @@ struct RegRec {
 static_assert(sizeof(RegRec) == 256, "RegRec layout");
 static_assert(std::atomic<uint64_t>::is_always_lock_free, "shared-memory atomics");
 
-constexpr size_t kRegMinDefault = (size_t)4 << 20;   // bytes per rank (MX_REG_MIN overrides; 0 = off)
+// bytes per rank (MX_REG_MIN overrides; 0 = off): zero-copy is ahead of the
+// staged path at every size measured above the one-shot range
+constexpr size_t kRegMinDefault = (size_t)256 << 10;
 constexpr size_t kRegCachePerPeer = 8;
 
 static size_t reg_min() {

@@ -198,7 +198,7 @@ static int comm_ready(mx_coll_module_t *m)
          * zero-copy from coll_mi355x_reg_min_kb per rank (0 = off; the
          * communicator declines it collectively when /dev/shm is missing),
          * staged protocol 0 auto / 1 push / 2 pull */
-        const int kb = mx_ompi_host->mca_int("coll_mi355x_reg_min_kb", 4096);
+        const int kb = mx_ompi_host->mca_int("coll_mi355x_reg_min_kb", 256);
         (void)mx_comm_set_reg_min(m->mx, kb > 0 ? (size_t)kb << 10 : 0);
         const int proto = mx_ompi_host->mca_int("coll_mi355x_protocol", MX_PROTO_AUTO);
         if (mx_comm_set_protocol(m->mx, proto) < 0) rc = MX_ERR_ARG;
