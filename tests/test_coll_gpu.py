@@ -577,6 +577,15 @@ def test_multiprocess_allreduce_zero_copy(n):
         assert got[r][-1] == got[0][-1]
 
 
+@pytest.mark.parametrize("env", [{"MX_FAST_SYNC_SPINS": "0"}, {"MX_FAST_SYNC": "0"}], ids=["fallback", "runtime"])
+def test_multiprocess_blocking_completion_paths(env):
+    """Blocking calls complete through the marker kernel's mapped word; with no
+    polling budget every call takes the fallback (the runtime's wait), and
+    MX_FAST_SYNC=0 uses the runtime's wait only: same results either way."""
+    jobs = [j for j in _JOBS_ZC if j[0] != "stats"]
+    _check_jobs(2, jobs, _run_mp(2, jobs, env=dict(env, MX_REG_MIN="1")))
+
+
 @pytest.mark.parametrize("proto", ["push", "pull"])
 @pytest.mark.parametrize("n", [2, 3, 8])
 def test_multiprocess_allreduce_staged_protocols(n, proto):

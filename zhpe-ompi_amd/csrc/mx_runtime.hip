@@ -272,7 +272,11 @@ extern "C" int mx_stream_sync_fast(void *stream) {
   const uint64_t v = ++m.seq;
   hipLaunchKernelGGL(k_mark, dim3(1), dim3(64), 0, s, m.dev, v);
   if (int rc = mx_check_launch()) return rc;
-  for (long i = 0; i < (1L << 16); i++) {   // ~2 ms of polling
+  static const long spins = [] {            // ~2 ms of polling; MX_FAST_SYNC_SPINS overrides (tests)
+    const char *e = getenv("MX_FAST_SYNC_SPINS");
+    return e && *e ? atol(e) : (1L << 16);
+  }();
+  for (long i = 0; i < spins; i++) {
     if (__atomic_load_n(m.host, __ATOMIC_ACQUIRE) >= v) return MX_SUCCESS;
     __builtin_ia32_pause();
   }
