@@ -267,6 +267,34 @@ def _p2p_worker(rank, n, port, q):
             comm.recv(d.data_ptr(), B, n - 1, tag=22)
             res["any_specific"] = d.cpu().numpy().tobytes()
 
+        # (9) MPI_ANY_SOURCE with a specific tag: rank 1's message (tag 50)
+        # is already in rank 0's mailbox when rank 0 posts ANY_SOURCE / tag 51,
+        # which only rank 2 sends, later -- the receive must take rank 2's
+        # message, and the next ANY_SOURCE / tag 50 receive rank 1's
+        if n >= 3:
+            C = 3001
+            if rank == 1:
+                m = _dev(_data(8100, C))
+                comm.send(m.data_ptr(), C, 0, tag=50)
+            dist.barrier()
+            if rank == 0:
+                b51 = torch.zeros(C, dtype=torch.uint8, device="cuda")
+                r51 = comm.irecv(b51.data_ptr(), C, mxompi.ANY_SOURCE, tag=51)
+            dist.barrier()
+            if rank == 2:
+                m = _dev(_data(8200, C))
+                comm.send(m.data_ptr(), C, 0, tag=51)
+            if rank == 0:
+                r51.wait()
+                first = (r51.source(), r51.status(), b51.cpu().numpy().tobytes())
+                r51.free()
+                b50 = torch.zeros(C, dtype=torch.uint8, device="cuda")
+                r50 = comm.irecv(b50.data_ptr(), C, mxompi.ANY_SOURCE, tag=50)
+                r50.wait()
+                res["any_tag"] = [first, (r50.source(), r50.status(), b50.cpu().numpy().tobytes())]
+                r50.free()
+            dist.barrier()
+
         comm.close()
         dist.destroy_process_group()
         q.put((rank, "ok", res))
@@ -340,6 +368,10 @@ def test_point_to_point(n):
     for r in range(n):
         for p in range(n):
             assert got[r]["a2a"][p] == _data(1000 * p + r, 77777).tobytes(), f"a2a {p} -> {r}"
+    if n >= 3:
+        (s51, st51, d51), (s50, st50, d50) = got[0]["any_tag"]
+        assert (s51, tuple(st51)[:2]) == (2, (3001, 51)) and d51 == _data(8200, 3001).tobytes(), (s51, st51)
+        assert (s50, tuple(st50)[:2]) == (1, (3001, 50)) and d50 == _data(8100, 3001).tobytes(), (s50, st50)
     got0, nb_last, last = got[0]["any"]
     expect = {(p, k): _data(5000 + 10 * p + k, 50001).tobytes() for p in range(1, n) for k in range(2)}
     seen = {p: 0 for p in range(1, n)}

@@ -368,11 +368,16 @@ __device__ __forceinline__ int2 held_match(const P2PRecvState *st, int64_t tag) 
 }
 
 // MX_ANY_SOURCE: wait until some source p has a message this receive can
-// take -- a matching held one, or a posted envelope beyond what this
-// process consumed from it (lane 0's message count) -- and store p in
-// status[3] (-1 after a timeout).
-__global__ void k_p2p_pick(const uint64_t *flag0, const P2PRecvState *st0, int n, int start, int64_t tag,
-                           int64_t *status, uint64_t timeout_ticks, int *err) {
+// take -- a matching held one, or, among the envelopes p has posted beyond
+// what this process consumed from it (lane 0's message count), one whose tag
+// matches (any, for MPI_ANY_TAG) -- and store p in status[3] (-1 after a
+// timeout).  A source whose pending messages all carry other tags is not
+// chosen: its messages stay in its mailbox for the receives that match them
+// (pml/ob1 matches an ANY_SOURCE receive against every peer's queue).  The
+// envelope ring slots read here cannot be rewritten meanwhile: a sender
+// reuses slot m % P2P_H only after this process has consumed message m.
+__global__ void k_p2p_pick(const uint64_t *flag0, const P2PRecvState *st0, const char *box0, int n, int start,
+                           int64_t tag, int64_t *status, uint64_t timeout_ticks, int *err) {
   if (threadIdx.x != 0) return;
   const uint64_t t0 = wall_clock64();
   for (int i = 0; i < n; i++) {
@@ -385,8 +390,17 @@ __global__ void k_p2p_pick(const uint64_t *flag0, const P2PRecvState *st0, int n
   for (;;) {
     for (int i = 0; i < n; i++) {
       const int p = (start + i) % n;
-      if (__hip_atomic_load(flag0 + P2P_POSTED + p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) >
-          st0[p].lane_msgs[0]) {
+      const uint64_t posted = __hip_atomic_load(flag0 + P2P_POSTED + p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      const uint64_t m0 = st0[p].lane_msgs[0];
+      if (posted <= m0) continue;
+      bool hit = tag < 0;
+      if (!hit) {
+        __atomic_thread_fence(__ATOMIC_ACQUIRE);   // the envelopes before their `posted` count
+        const char *box = box0 + (size_t)p * P2P_BOX;
+        for (uint64_t m = m0; !hit && m < posted && m < m0 + P2P_H; m++)
+          hit = (int64_t)reinterpret_cast<const volatile uint64_t *>(box + (m % P2P_H) * P2P_HDR)[1] == tag;
+      }
+      if (hit) {
         __hip_atomic_store(&status[3], (int64_t)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
         return;
       }
@@ -872,8 +886,8 @@ int p2p_enqueue(mx_request *q, hipStream_t *done_stream) {
       a.any = 1;
       const int start = (int)(c->p2p_any_rr++ % (unsigned)c->size);
       hipLaunchKernelGGL(k_p2p_pick, dim3(1), dim3(64), 0, s, (const uint64_t *)c->flagmem,
-                         (const P2PRecvState *)c->p2p_recv, c->size, start, (int64_t)q->tag, st_dev,
-                         c->timeout_ticks, c->err_dev);
+                         (const P2PRecvState *)c->p2p_recv, (const char *)(c->staging + c->p2p_off), c->size,
+                         start, (int64_t)q->tag, st_dev, c->timeout_ticks, c->err_dev);
       if ((rc = mx_check_launch())) return rc;
     }
     a.status = st_dev;
