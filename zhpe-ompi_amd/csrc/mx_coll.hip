@@ -1140,7 +1140,7 @@ static bool reg_export(const void *p, size_t bytes, RegBuf *b) {
 // peer range, other buffer id) is closed BEFORE the new handle is opened, so
 // the runtime can never hand back the stale import.  Closing is safe: no
 // kernel of this communicator is in flight between blocking calls.
-static char *reg_import(mx_comm *c, int p, const RegBuf &b, char *const *own, int nown) {
+static char *reg_import(mx_comm *c, int p, const RegBuf &b, const RegBuf *own, int nown) {
   std::vector<mx_reg_import> &v = *c->reg_imp;
   for (mx_reg_import &m : v)
     if (m.peer == p && m.base == b.base && m.size == b.size && m.id == b.id) {
@@ -1170,10 +1170,11 @@ static char *reg_import(mx_comm *c, int p, const RegBuf &b, char *const *own, in
     (void)hipGetLastError();
     return nullptr;
   }
-  // a mapping must never be one of this rank's own buffers (the round-1 IPC
-  // aliasing symptom): refuse it, the call takes the staged path
+  // a mapping must never overlap one of this rank's own allocations (the
+  // round-1 IPC aliasing symptom): refuse it, the call takes the
+  // staged path
   for (int i = 0; i < nown; i++)
-    if (ptr == own[i]) {
+    if ((uint64_t)(uintptr_t)ptr < own[i].base + own[i].size && own[i].base < (uint64_t)(uintptr_t)ptr + b.size) {
       (void)hipIpcCloseMemHandle(ptr);
       return nullptr;
     }
@@ -1221,7 +1222,7 @@ static int reg_exchange(mx_comm *c, const char *sb, size_t sbytes, char *rb, siz
   int verdict = 1;
   for (int p = 0; p < n; p++)
     if (!R[p].ok || R[p].mis != me.mis) verdict = 0;
-  char *own[2] = {(char *)sb, rb};
+  const RegBuf own[2] = {me.sb, me.rb};   // this rank's allocations (valid: the verdict needs ok)
   for (int p = 0; verdict && p < n; p++) {
     if (p == r) { ps[p] = sb; pr[p] = rb; continue; }
     const RegBuf &bs = R[p].sb, &br = R[p].rb;
