@@ -285,12 +285,18 @@ def test_multirank_host_buffers_gloo_cpu(n):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("path", ["default", "zero_copy"])
 @pytest.mark.parametrize("n", [2, 3])
-def test_multirank_device_buffers_through_components(n):
+def test_multirank_device_buffers_through_components(n, path, monkeypatch):
+    """Every slot through coll/mi355x on device buffers; `zero_copy` lowers
+    coll_mi355x_reg_min_kb to 1 KiB so the blocking reductions, allgather and
+    bcast of this job run between the ranks' registered buffers."""
     import torch
     if not torch.cuda.is_available():
         pytest.skip("needs a GPU")
     os.environ["HSA_ENABLE_IPC_MODE_LEGACY"] = "0"
+    if path == "zero_copy":
+        monkeypatch.setenv("OMPI_MCA_coll_mi355x_reg_min_kb", "1")
     got = _run(n, use_gpu=True)
     assert all(v == "mi355x" for v in got[0]["owners"].values()), got[0]["owners"]
     import mxompi
