@@ -186,8 +186,12 @@ def bench_allreduce(torch, mx, dist, rank, world, dev, steps, warmup, nbytes=256
     # 256 KiB per rank), and the staged path under PUSH and PULL (the staged
     # default: PULL)
     proto_default = comm.protocol()
-    proto_ab = {"staged_protocol": proto_default,
-                "timed_path": "zero_copy" if st["zero_copy_calls"] else "staged"}
+    proto_ab = {"staged_protocol": proto_default, "autotuned": comm.tuning(nbytes),
+                "timed_path_last_calls": "zero_copy" if st["zero_copy_calls"] else "staged"}
+    try:
+        comm.set_autotune(False)   # the A/B below forces each path
+    except mx.MxError:
+        pass
     for name, reg, proto in (("staged_push", 0, "push"), ("staged_pull", 0, "pull"), ("zero_copy", 256 << 10, None)):
         try:
             comm.set_reg_min(reg)
@@ -199,9 +203,10 @@ def bench_allreduce(torch, mx, dist, rank, world, dev, steps, warmup, nbytes=256
         for _ in range(2):
             comm.allreduce(x.data_ptr(), out.data_ptr(), count, "FLOAT", "SUM", "auto", sp)
         k = max(3, steps // 2)
+        zc0 = comm.stats()["zero_copy_calls"]
         tp = timed("auto", k)
         proto_ab[name] = {"busbw_gbs": round(nbytes / (tp / k) / 1e9 * 2 * (world - 1) / world, 2),
-                          "ms": round(tp / k * 1e3, 4)}
+                          "ms": round(tp / k * 1e3, 4), "zero_copy_calls": comm.stats()["zero_copy_calls"] - zc0}
     comm.set_protocol(proto_default)
     sweep = allreduce_sweep(torch, mx, dist, comm, world, x, out, sp, flags)
     cfge = cfg_e(torch, mx, dist, comm, world, rank, sp)

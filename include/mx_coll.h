@@ -125,6 +125,18 @@ int mx_comm_get_protocol(const mx_comm_t *comm);
  * (single rank, local communicator, or /dev/shm unavailable on some rank). */
 int mx_comm_set_reg_min(mx_comm_t *comm, size_t min_bytes);
 
+/* Autotuning of the data movement (default on when the registration page
+ * exists and neither MX_ALLREDUCE_PROTO nor MX_REG_MIN forces a path;
+ * MX_AUTOTUNE=0 switches it off): per power-of-two size class of blocking
+ * allreduces >= 4 MiB per rank, the first call runs the defaults, the next
+ * three run zero-copy, staged PULL and staged PUSH, each timed on the host
+ * and the maximum over ranks exchanged through the registration page; the
+ * fastest is kept for that class.  Results are identical on every path.
+ * mx_comm_get_tuning returns the choice for a message size (0 zero-copy,
+ * 1 PULL, 2 PUSH) or -1 while untuned.  Same setting on every rank. */
+int mx_comm_set_autotune(mx_comm_t *comm, int on);
+int mx_comm_get_tuning(const mx_comm_t *comm, size_t bytes);
+
 /* Per-communicator kernel timing (HIP events on the collective's stream),
  * off by default.  Times are summed over calls since the last reset. */
 typedef struct mx_coll_stats {

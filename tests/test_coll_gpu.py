@@ -245,6 +245,8 @@ def _mp_worker(rank, n, port, staging, jobs, q, env=None):
             elif kind == "stats":
                 sts = comm.stats()
                 results.append((sts["zero_copy_calls"], sts["staged_calls"]))
+            elif kind == "tuning":
+                results.append(comm.tuning(count * es))
             elif kind == "reduce_scatter":
                 rc = [count + 3 * r for r in range(n)]
                 x = _dev(gen(t, op, sum(rc), 7000 + rank))
@@ -416,7 +418,7 @@ def _check_jobs(n, jobs, got):
     L = _oracle()
     for j, (kind, count, op, t, alg) in enumerate(jobs):
         es = mxompi.type_size(t)
-        if kind == "stats":
+        if kind in ("stats", "tuning"):
             continue
         if kind.startswith("allreduce") or kind == "shmem":
             xs = [gen(t, op, count, 7000 + r) for r in range(n)]
@@ -575,6 +577,28 @@ def test_multiprocess_allreduce_zero_copy(n):
     assert staged == n_mis and zc == n_zc, (zc, staged, n_zc)
     for r in range(n):
         assert got[r][-1] == got[0][-1]
+
+
+# autotuning (mx_comm_set_autotune, on by default): five allreduces of one
+# size class -- warm-up, zero-copy, PULL and PUSH trials, then the kept choice
+# -- all bit-exact, every rank keeping the same choice
+_JOBS_TUNE = [("allreduce", 1_500_001, "SUM", "FLOAT", "auto"),
+              ("allreduce_inplace", 1_500_001, "SUM", "FLOAT", "auto"),
+              ("allreduce", 1_500_001, "MAX", "FLOAT", "rabenseifner"),
+              ("allreduce", 1_500_001, "SUM", "FLOAT", "ring"),
+              ("allreduce", 1_500_001, "BAND", "UINT16_T", "auto"),      # another size class: untuned
+              ("tuning", 1_500_001, "SUM", "FLOAT", "auto"),
+              ("allreduce", 1_500_001, "SUM", "FLOAT", "auto"),
+              ("tuning", 1_500_001, "SUM", "FLOAT", "auto")]
+
+
+@pytest.mark.parametrize("n", [2, 8])
+def test_multiprocess_allreduce_autotune(n):
+    got = _run_mp(n, _JOBS_TUNE, staging=64 << 20)
+    _check_jobs(n, _JOBS_TUNE, got)
+    for r in range(n):
+        assert got[r][5] in ("zero_copy", "pull", "push"), got[r][5]   # the fp32 size class: 4 calls done
+        assert got[r][5] == got[0][5] and got[r][-1] == got[0][5]
 
 
 @pytest.mark.parametrize("env", [{"MX_FAST_SYNC_SPINS": "0"}, {"MX_FAST_SYNC": "0"}], ids=["fallback", "runtime"])

@@ -316,7 +316,9 @@ struct RegRec {
   std::atomic<uint64_t> seq, vseq;
   RegBuf sb, rb;
   int32_t ok, mis, verdict, pad_;
-  char pad[256 - 2 * 8 - 2 * sizeof(RegBuf) - 4 * 4];
+  std::atomic<uint64_t> tseq;   // autotuning: the call's elapsed time, published with tseq
+  double t;
+  char pad[256 - 2 * 8 - 2 * sizeof(RegBuf) - 4 * 4 - 2 * 8];
 };
 static_assert(sizeof(RegRec) == 256, "RegRec layout");
 static_assert(std::atomic<uint64_t>::is_always_lock_free, "shared-memory atomics");
@@ -325,6 +327,7 @@ static_assert(std::atomic<uint64_t>::is_always_lock_free, "shared-memory atomics
 // staged path at every size measured above the one-shot range
 constexpr size_t kRegMinDefault = (size_t)256 << 10;
 constexpr size_t kRegCachePerPeer = 8;
+constexpr size_t kTuneMin = (size_t)4 << 20;   // autotuned allreduces: bytes per rank
 
 static size_t reg_min() {
   const char *e = getenv("MX_REG_MIN");
@@ -392,6 +395,19 @@ extern "C" int mx_comm_set_protocol(mx_comm_t *c, int proto) {
 }
 
 extern "C" int mx_comm_get_protocol(const mx_comm_t *c) { return c ? c->proto : MX_ERR_ARG; }
+
+extern "C" int mx_comm_set_autotune(mx_comm_t *c, int on) {
+  if (!c) return MX_ERR_ARG;
+  if (on && !c->reg_shm) return MX_ERR_UNSUPPORTED;   // the timings travel through the registration page
+  c->tune_on = on ? 1 : 0;
+  return MX_SUCCESS;
+}
+
+extern "C" int mx_comm_get_tuning(const mx_comm_t *c, size_t bytes) {
+  if (!c || !bytes) return MX_ERR_ARG;
+  const int b = 63 - __builtin_clzll((unsigned long long)bytes);
+  return c->tune_best[b] ? c->tune_best[b] - 1 : -1;
+}
 
 extern "C" int mx_comm_set_reg_min(mx_comm_t *c, size_t min_bytes) {
   if (!c) return MX_ERR_ARG;
@@ -541,6 +557,9 @@ extern "C" int mx_comm_create_ex(int rank, int size, int device, size_t staging_
     if (reg_all == 1) {
       c->reg_min = reg_min();
       c->reg_imp = new (std::nothrow) std::vector<mx_reg_import>();
+      // autotuning unless switched off, or a data path is forced through the environment
+      const char *at = getenv("MX_AUTOTUNE");
+      c->tune_on = !(at && *at == '0') && !getenv("MX_ALLREDUCE_PROTO") && !getenv("MX_REG_MIN");
     }
     if (reg_all != 1 || !c->reg_imp) reg_release(c);
   } else {
@@ -1093,6 +1112,34 @@ static int allreduce_oneshot(mx_comm *c, oneshot_launch_fn ol, const std::vector
   return finish(c, s);
 }
 
+// Autotuning: publish this rank's elapsed time of a trial call, return the
+// maximum over the ranks (the same on every rank, so every rank keeps the same
+// choice).  Bounded by the communicator's wait timeout like reg_wait.
+static int tune_exchange(mx_comm *c, double el, double *tmax) {
+  RegRec *R = (RegRec *)c->reg_shm;
+  const uint64_t k = ++c->tune_seq;
+  R[c->rank].t = el;
+  R[c->rank].tseq.store(k, std::memory_order_release);
+  const auto t0 = std::chrono::steady_clock::now();
+  double m = 0;
+  for (int p = 0; p < c->size; p++) {
+    unsigned spins = 0;
+    while (R[p].tseq.load(std::memory_order_acquire) < k) {
+      if (++spins > 256) {
+        sched_yield();
+        if (c->timeout_s > 0 &&
+            std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count() > c->timeout_s) {
+          c->poisoned = MX_ERR_TIMEOUT;
+          return MX_ERR_TIMEOUT;
+        }
+      }
+    }
+    m = std::max(m, R[p].t);
+  }
+  *tmax = m;
+  return MX_SUCCESS;
+}
+
 // the allocation holding [p, p+bytes): IPC handle, identity, offset of p.
 // Handles of recent allocations are kept per process (the runtime buffer id
 // tells a live allocation from one re-made at the same address).
@@ -1242,67 +1289,10 @@ static int reg_exchange(mx_comm *c, const char *sb, size_t sbytes, char *rb, siz
 
 }  // namespace
 
-extern "C" int mx_allreduce(mx_comm_t *c, const void *sbuf, void *rbuf, size_t count, int type, int op, int alg,
-                            void *stream) {
-  if (!c || !rbuf) return MX_ERR_ARG;
-  if (c->local) {
-    const void *sb[1] = {sbuf};
-    void *rb[1] = {rbuf};
-    if (c->size != 1) return MX_ERR_STATE;
-    return mx_allreduce_local(c, sb, rb, count, type, op, alg, stream);
-  }
-  hipStream_t s = (hipStream_t)stream;
-  if (int orc = order(c, s)) return orc;
-  const size_t es = mx_type_size(type);
-  if (!es) return MX_ERR_ARG;
+// The staged / zero-copy allreduce above the one-shot range (mx_allreduce)
+static int allreduce_staged(mx_comm *c, fold_launch_fn fl, int alg, const char *sb, char *rb, size_t count,
+                            size_t es, bool allow_zc, hipStream_t s) {
   const int n = c->size, r = c->rank;
-  const char *sb = (sbuf == MX_IN_PLACE || !sbuf) ? (const char *)rbuf : (const char *)sbuf;
-  char *rb = (char *)rbuf;
-  if (count == 0) return MX_SUCCESS;
-  if (alg == MX_ALLREDUCE_RCCL) {
-    if (!c->nccl) return MX_ERR_STATE;
-    ncclDataType_t dt;
-    ncclRedOp_t ro;
-    switch (type) {
-      case MX_TYPE_INT8_T: case MX_TYPE_INTEGER1: dt = ncclInt8; break;
-      case MX_TYPE_UINT8_T: dt = ncclUint8; break;
-      case MX_TYPE_INT32_T: case MX_TYPE_INTEGER: case MX_TYPE_INTEGER4: dt = ncclInt32; break;
-      case MX_TYPE_UINT32_T: dt = ncclUint32; break;
-      case MX_TYPE_INT64_T: case MX_TYPE_INTEGER8: dt = ncclInt64; break;
-      case MX_TYPE_UINT64_T: dt = ncclUint64; break;
-      case MX_TYPE_FLOAT: case MX_TYPE_REAL: case MX_TYPE_REAL4: dt = ncclFloat32; break;
-      case MX_TYPE_DOUBLE: case MX_TYPE_REAL8: case MX_TYPE_DOUBLE_PRECISION: dt = ncclFloat64; break;
-      default: return MX_ERR_UNSUPPORTED;
-    }
-    switch (op) {
-      case MX_OP_SUM: ro = ncclSum; break;
-      case MX_OP_PROD: ro = ncclProd; break;
-      case MX_OP_MAX: ro = ncclMax; break;
-      case MX_OP_MIN: ro = ncclMin; break;
-      default: return MX_ERR_UNSUPPORTED;
-    }
-    if (ncclAllReduce(sb, rb, count, dt, ro, c->nccl, s) != ncclSuccess) return MX_ERR_RCCL;
-    return finish(c, s);
-  }
-  fold_launch_fn fl = fold_fns(op, type).fold;
-  if (!fl) return MX_ERR_UNSUPPORTED;
-  if (n == 1) {
-    if (int rc = copy_async(rb, sb, count * es, s)) return rc;
-    return finish(c, s);
-  }
-  if (!(c->flags & MX_COMM_IPC)) return MX_ERR_STATE;
-  if (c->os_max && count * es <= c->os_max) {
-    std::vector<Seg> segs;
-    int rc = allreduce_segments(alg, n, count, es, 0, count, segs);
-    if (rc) return rc;
-    oneshot_launch_fn ol = fold_fns(op, type).oneshot;
-    if (ol && segs.size() <= (size_t)OS_MAXSEG) return allreduce_oneshot(c, ol, segs, sb, rb, count, es, s);
-  }
-  {  // validate the algorithm once for the whole vector
-    std::vector<Seg> probe;
-    int rc = allreduce_segments(alg, n, count, es, 0, 0, probe);
-    if (rc) return rc;
-  }
   // Zero-copy input: with every rank's sbuf registered, the fold reads the
   // peers' parts straight from their sbufs over xGMI (the PULL fold without
   // its input copy).  Results still travel through the peers' uncached
@@ -1311,7 +1301,7 @@ extern "C" int mx_allreduce(mx_comm_t *c, const void *sbuf, void *rbuf, size_t c
   const char *ps[MAXR];
   char *pr[MAXR];
   int zc = 0;
-  if (c->reg_shm && !c->defer && c->reg_min && count * es >= c->reg_min) {
+  if (allow_zc && c->reg_shm && !c->defer && c->reg_min && count * es >= c->reg_min) {
     zc = reg_exchange(c, sb, count * es, rb, count * es, (int)((uintptr_t)sb & 15), true, ps, pr);
     if (zc < 0) return zc;
   }
@@ -1390,6 +1380,97 @@ extern "C" int mx_allreduce(mx_comm_t *c, const void *sbuf, void *rbuf, size_t c
     if ((rc = signal_all(c, FLAG_DONE, g, s))) return rc;
   }
   return finish(c, s);
+}
+
+extern "C" int mx_allreduce(mx_comm_t *c, const void *sbuf, void *rbuf, size_t count, int type, int op, int alg,
+                            void *stream) {
+  if (!c || !rbuf) return MX_ERR_ARG;
+  if (c->local) {
+    const void *sb[1] = {sbuf};
+    void *rb[1] = {rbuf};
+    if (c->size != 1) return MX_ERR_STATE;
+    return mx_allreduce_local(c, sb, rb, count, type, op, alg, stream);
+  }
+  hipStream_t s = (hipStream_t)stream;
+  if (int orc = order(c, s)) return orc;
+  const size_t es = mx_type_size(type);
+  if (!es) return MX_ERR_ARG;
+  const int n = c->size;
+  const char *sb = (sbuf == MX_IN_PLACE || !sbuf) ? (const char *)rbuf : (const char *)sbuf;
+  char *rb = (char *)rbuf;
+  if (count == 0) return MX_SUCCESS;
+  if (alg == MX_ALLREDUCE_RCCL) {
+    if (!c->nccl) return MX_ERR_STATE;
+    ncclDataType_t dt;
+    ncclRedOp_t ro;
+    switch (type) {
+      case MX_TYPE_INT8_T: case MX_TYPE_INTEGER1: dt = ncclInt8; break;
+      case MX_TYPE_UINT8_T: dt = ncclUint8; break;
+      case MX_TYPE_INT32_T: case MX_TYPE_INTEGER: case MX_TYPE_INTEGER4: dt = ncclInt32; break;
+      case MX_TYPE_UINT32_T: dt = ncclUint32; break;
+      case MX_TYPE_INT64_T: case MX_TYPE_INTEGER8: dt = ncclInt64; break;
+      case MX_TYPE_UINT64_T: dt = ncclUint64; break;
+      case MX_TYPE_FLOAT: case MX_TYPE_REAL: case MX_TYPE_REAL4: dt = ncclFloat32; break;
+      case MX_TYPE_DOUBLE: case MX_TYPE_REAL8: case MX_TYPE_DOUBLE_PRECISION: dt = ncclFloat64; break;
+      default: return MX_ERR_UNSUPPORTED;
+    }
+    switch (op) {
+      case MX_OP_SUM: ro = ncclSum; break;
+      case MX_OP_PROD: ro = ncclProd; break;
+      case MX_OP_MAX: ro = ncclMax; break;
+      case MX_OP_MIN: ro = ncclMin; break;
+      default: return MX_ERR_UNSUPPORTED;
+    }
+    if (ncclAllReduce(sb, rb, count, dt, ro, c->nccl, s) != ncclSuccess) return MX_ERR_RCCL;
+    return finish(c, s);
+  }
+  fold_launch_fn fl = fold_fns(op, type).fold;
+  if (!fl) return MX_ERR_UNSUPPORTED;
+  if (n == 1) {
+    if (int rc = copy_async(rb, sb, count * es, s)) return rc;
+    return finish(c, s);
+  }
+  if (!(c->flags & MX_COMM_IPC)) return MX_ERR_STATE;
+  if (c->os_max && count * es <= c->os_max) {
+    std::vector<Seg> segs;
+    int rc = allreduce_segments(alg, n, count, es, 0, count, segs);
+    if (rc) return rc;
+    oneshot_launch_fn ol = fold_fns(op, type).oneshot;
+    if (ol && segs.size() <= (size_t)OS_MAXSEG) return allreduce_oneshot(c, ol, segs, sb, rb, count, es, s);
+  }
+  {  // validate the algorithm once for the whole vector
+    std::vector<Seg> probe;
+    int rc = allreduce_segments(alg, n, count, es, 0, 0, probe);
+    if (rc) return rc;
+  }
+  // autotuning: which data movement this call takes
+  const size_t bytes = count * es;
+  int cand = -1, bucket = -1;   // cand: 0 zero-copy, 1 staged PULL, 2 staged PUSH; -1 the defaults
+  if (c->tune_on && c->reg_shm && !c->defer && bytes >= kTuneMin) {
+    bucket = 63 - __builtin_clzll((unsigned long long)bytes);
+    const int k = c->tune_calls[bucket];
+    cand = c->tune_best[bucket] ? c->tune_best[bucket] - 1 : (k == 0 ? 0 : k - 1);   // call 0 warms up
+  }
+  const int proto0 = c->proto;
+  if (cand == 1) c->proto = MX_PROTO_PULL;
+  if (cand == 2) c->proto = MX_PROTO_PUSH;
+  const auto t0 = std::chrono::steady_clock::now();
+  int rc = allreduce_staged(c, fl, alg, sb, rb, count, es, cand <= 0, s);
+  c->proto = proto0;
+  if (rc || cand < 0 || c->tune_best[bucket]) return rc;
+  const double el = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+  const int k = c->tune_calls[bucket]++;
+  if (k == 0) return MX_SUCCESS;
+  double tmax = 0;
+  if ((rc = tune_exchange(c, el, &tmax))) return rc;
+  c->tune_t[bucket][cand] = tmax;
+  if (k == 3) {
+    int best = 0;
+    for (int i = 1; i < 3; i++)
+      if (c->tune_t[bucket][i] < c->tune_t[bucket][best]) best = i;
+    c->tune_best[bucket] = (int8_t)(best + 1);
+  }
+  return MX_SUCCESS;
 }
 
 extern "C" int mx_reduce_scatter(mx_comm_t *c, const void *sbuf, void *rbuf, const size_t *rcounts, int type,

@@ -149,6 +149,15 @@ struct mx_comm {
   size_t reg_shm_bytes, reg_min;
   uint64_t reg_seq, reg_tick;
   std::vector<struct mx_reg_import> *reg_imp;
+  // data-movement autotuning of blocking allreduces >= 4 MiB: per
+  // power-of-two size class, the first call warms up, the next three time
+  // zero-copy / PULL / PUSH (max over ranks, exchanged in the registration
+  // page) and the fastest is kept.  tune_best: choice + 1, 0 = not yet.
+  int tune_on;
+  uint8_t tune_calls[64];
+  int8_t tune_best[64];
+  double tune_t[64][3];
+  uint64_t tune_seq;
   double timeout_s;
   uint64_t timeout_ticks;
   ncclComm_t nccl;

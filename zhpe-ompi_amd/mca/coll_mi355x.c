@@ -202,6 +202,8 @@ static int comm_ready(mx_coll_module_t *m)
         (void)mx_comm_set_reg_min(m->mx, kb > 0 ? (size_t)kb << 10 : 0);
         const int proto = mx_ompi_host->mca_int("coll_mi355x_protocol", MX_PROTO_AUTO);
         if (mx_comm_set_protocol(m->mx, proto) < 0) rc = MX_ERR_ARG;
+        /* data-movement autotuning of large allreduces (on by default) */
+        if (!mx_ompi_host->mca_int("coll_mi355x_autotune", 1)) (void)mx_comm_set_autotune(m->mx, 0);
     }
     /* the streams are process-local: a failure here is reported by the calls
      * (or falls back to the default stream), never turned into a different

@@ -205,6 +205,8 @@ def _coll_lib():
         L.mx_comm_set_protocol.argtypes = [vp, i]
         L.mx_comm_get_protocol.argtypes = [vp]
         L.mx_comm_set_reg_min.argtypes = [vp, sz]
+        L.mx_comm_set_autotune.argtypes = [vp, i]
+        L.mx_comm_get_tuning.argtypes = [vp, sz]
         L.mx_allreduce.argtypes = [vp, vp, vp, sz, i, i, i, vp]
         L.mx_allreduce_local.argtypes = [vp, pp, pp, sz, i, i, i, vp]
         L.mx_reduce_scatter.argtypes = [vp, vp, vp, ctypes.POINTER(sz), i, i, i, vp]
@@ -401,6 +403,14 @@ class Comm:
 
     def protocol(self):
         return {1: "push", 2: "pull"}.get(_coll_lib().mx_comm_get_protocol(self.h), "none")
+
+    def set_autotune(self, on):
+        """Data-movement autotuning of large blocking allreduces (mx_comm_set_autotune)."""
+        check(_coll_lib().mx_comm_set_autotune(self.h, 1 if on else 0), "mx_comm_set_autotune")
+
+    def tuning(self, nbytes):
+        """The data movement autotuning kept for allreduces of nbytes per rank, or None."""
+        return {0: "zero_copy", 1: "pull", 2: "push"}.get(_coll_lib().mx_comm_get_tuning(self.h, nbytes))
 
     def set_reg_min(self, min_bytes):
         """Zero-copy (registered user buffers) allreduce from min_bytes per rank; 0 = off
