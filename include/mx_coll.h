@@ -129,7 +129,8 @@ int mx_comm_set_reg_min(mx_comm_t *comm, size_t min_bytes);
  * exists and neither MX_ALLREDUCE_PROTO nor MX_REG_MIN forces a path;
  * MX_AUTOTUNE=0 switches it off): per power-of-two size class of blocking
  * allreduces >= 4 MiB per rank, the first call runs the defaults, the next
- * three run zero-copy, staged PULL and staged PUSH, each timed on the host
+ * three run zero-copy, staged PULL and staged PUSH (reduce_scatter and
+ * allgather: zero-copy and staged), each timed on the host
  * and the maximum over ranks exchanged through the registration page; the
  * fastest is kept for that class.  Results are identical on every path.
  * mx_comm_get_tuning returns the choice for a message size (0 zero-copy,

@@ -589,7 +589,10 @@ _JOBS_TUNE = [("allreduce", 1_500_001, "SUM", "FLOAT", "auto"),
               ("allreduce", 1_500_001, "BAND", "UINT16_T", "auto"),      # another size class: untuned
               ("tuning", 1_500_001, "SUM", "FLOAT", "auto"),
               ("allreduce", 1_500_001, "SUM", "FLOAT", "auto"),
-              ("tuning", 1_500_001, "SUM", "FLOAT", "auto")]
+              ("tuning", 1_500_001, "SUM", "FLOAT", "auto"),
+              # reduce_scatter and allgather: warm-up, zero-copy and staged trials, kept choice
+              *[("reduce_scatter", 600_000, "SUM", "FLOAT", "ring")] * 4,
+              *[("allgather", 2_500_000, "BAND", "UINT8_T", "auto")] * 4]
 
 
 @pytest.mark.parametrize("n", [2, 8])
@@ -598,7 +601,7 @@ def test_multiprocess_allreduce_autotune(n):
     _check_jobs(n, _JOBS_TUNE, got)
     for r in range(n):
         assert got[r][5] in ("zero_copy", "pull", "push"), got[r][5]   # the fp32 size class: 4 calls done
-        assert got[r][5] == got[0][5] and got[r][-1] == got[0][5]
+        assert got[r][5] == got[0][5] and got[r][7] == got[0][5]
 
 
 @pytest.mark.parametrize("env", [{"MX_FAST_SYNC_SPINS": "0"}, {"MX_FAST_SYNC": "0"}], ids=["fallback", "runtime"])

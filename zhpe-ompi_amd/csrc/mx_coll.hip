@@ -406,7 +406,7 @@ extern "C" int mx_comm_set_autotune(mx_comm_t *c, int on) {
 extern "C" int mx_comm_get_tuning(const mx_comm_t *c, size_t bytes) {
   if (!c || !bytes) return MX_ERR_ARG;
   const int b = 63 - __builtin_clzll((unsigned long long)bytes);
-  return c->tune_best[b] ? c->tune_best[b] - 1 : -1;
+  return c->tune_best[0][b] ? c->tune_best[0][b] - 1 : -1;   // TUNE_ALLREDUCE
 }
 
 extern "C" int mx_comm_set_reg_min(mx_comm_t *c, size_t min_bytes) {
@@ -1140,6 +1140,39 @@ static int tune_exchange(mx_comm *c, double el, double *tmax) {
   return MX_SUCCESS;
 }
 
+// Autotuning bookkeeping shared by the tuned collectives.  tune_pick: the
+// candidate this call runs (-1: the defaults, untuned), *bucket its size
+// class.  tune_done: after a successful call, record its time (trial calls
+// exchange the max over ranks) and keep the fastest once every candidate ran.
+enum { TUNE_ALLREDUCE = 0, TUNE_REDUCE_SCATTER = 1, TUNE_ALLGATHER = 2 };
+static int tune_pick(const mx_comm *c, int kind, size_t bytes, int *bucket) {
+  *bucket = -1;
+  if (!c->tune_on || !c->reg_shm || c->defer || bytes < kTuneMin) return -1;
+  const int b = 63 - __builtin_clzll((unsigned long long)bytes);
+  *bucket = b;
+  if (c->tune_best[kind][b]) return c->tune_best[kind][b] - 1;
+  const int k = c->tune_calls[kind][b];
+  return k == 0 ? 0 : k - 1;   // call 0 warms up (and maps the peers' buffers) on candidate 0
+}
+static int tune_done(mx_comm *c, int kind, int bucket, int cand, int ncand, double el) {
+  if (cand < 0 || c->tune_best[kind][bucket]) return MX_SUCCESS;
+  const int k = c->tune_calls[kind][bucket]++;
+  if (k == 0) return MX_SUCCESS;
+  double tmax = 0;
+  if (int rc = tune_exchange(c, el, &tmax)) return rc;
+  c->tune_t[kind][bucket][cand] = tmax;
+  if (k == ncand) {
+    int best = 0;
+    for (int i = 1; i < ncand; i++)
+      if (c->tune_t[kind][bucket][i] < c->tune_t[kind][bucket][best]) best = i;
+    c->tune_best[kind][bucket] = (int8_t)(best + 1);
+  }
+  return MX_SUCCESS;
+}
+static double secs_since(std::chrono::steady_clock::time_point t0) {
+  return std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+}
+
 // the allocation holding [p, p+bytes): IPC handle, identity, offset of p.
 // Handles of recent allocations are kept per process (the runtime buffer id
 // tells a live allocation from one re-made at the same address).
@@ -1443,38 +1476,20 @@ extern "C" int mx_allreduce(mx_comm_t *c, const void *sbuf, void *rbuf, size_t c
     int rc = allreduce_segments(alg, n, count, es, 0, 0, probe);
     if (rc) return rc;
   }
-  // autotuning: which data movement this call takes
-  const size_t bytes = count * es;
-  int cand = -1, bucket = -1;   // cand: 0 zero-copy, 1 staged PULL, 2 staged PUSH; -1 the defaults
-  if (c->tune_on && c->reg_shm && !c->defer && bytes >= kTuneMin) {
-    bucket = 63 - __builtin_clzll((unsigned long long)bytes);
-    const int k = c->tune_calls[bucket];
-    cand = c->tune_best[bucket] ? c->tune_best[bucket] - 1 : (k == 0 ? 0 : k - 1);   // call 0 warms up
-  }
+  // autotuning: cand 0 zero-copy, 1 staged PULL, 2 staged PUSH; -1 the defaults
+  int bucket;
+  const int cand = tune_pick(c, TUNE_ALLREDUCE, count * es, &bucket);
   const int proto0 = c->proto;
   if (cand == 1) c->proto = MX_PROTO_PULL;
   if (cand == 2) c->proto = MX_PROTO_PUSH;
   const auto t0 = std::chrono::steady_clock::now();
-  int rc = allreduce_staged(c, fl, alg, sb, rb, count, es, cand <= 0, s);
+  const int rc = allreduce_staged(c, fl, alg, sb, rb, count, es, cand <= 0, s);
   c->proto = proto0;
-  if (rc || cand < 0 || c->tune_best[bucket]) return rc;
-  const double el = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
-  const int k = c->tune_calls[bucket]++;
-  if (k == 0) return MX_SUCCESS;
-  double tmax = 0;
-  if ((rc = tune_exchange(c, el, &tmax))) return rc;
-  c->tune_t[bucket][cand] = tmax;
-  if (k == 3) {
-    int best = 0;
-    for (int i = 1; i < 3; i++)
-      if (c->tune_t[bucket][i] < c->tune_t[bucket][best]) best = i;
-    c->tune_best[bucket] = (int8_t)(best + 1);
-  }
-  return MX_SUCCESS;
+  return rc ? rc : tune_done(c, TUNE_ALLREDUCE, bucket, cand, 3, secs_since(t0));
 }
 
-extern "C" int mx_reduce_scatter(mx_comm_t *c, const void *sbuf, void *rbuf, const size_t *rcounts, int type,
-                                 int op, int alg, void *stream) {
+static int reduce_scatter_impl(mx_comm_t *c, const void *sbuf, void *rbuf, const size_t *rcounts, int type, int op,
+                               int alg, void *stream, bool allow_zc) {
   if (!c || !rbuf || !rcounts) return MX_ERR_ARG;
   if (c->local) {
     if (c->size != 1) return MX_ERR_STATE;
@@ -1506,7 +1521,7 @@ extern "C" int mx_reduce_scatter(mx_comm_t *c, const void *sbuf, void *rbuf, con
   // (the slot geometry must be the same on every rank: it depends only on
   // the collective IN_PLACE choice, not on this rank's block)
   const bool inplace = sb == (const char *)rbuf;
-  if (c->reg_shm && !c->defer && c->reg_min && total * es >= c->reg_min && !inplace) {
+  if (allow_zc && c->reg_shm && !c->defer && c->reg_min && total * es >= c->reg_min && !inplace) {
     // zero-copy: rank r folds block r straight from every rank's registered
     // sbuf into its own rbuf (IN_PLACE stays staged: block 0 of a rank's
     // input is its output area, which rank 0 would still be reading)
@@ -1572,7 +1587,7 @@ extern "C" int mx_reduce_scatter(mx_comm_t *c, const void *sbuf, void *rbuf, con
   return finish(c, s);
 }
 
-extern "C" int mx_allgather(mx_comm_t *c, const void *sbuf, void *rbuf, size_t bytes, void *stream) {
+static int allgather_impl(mx_comm_t *c, const void *sbuf, void *rbuf, size_t bytes, void *stream, bool allow_zc) {
   if (!c || !rbuf) return MX_ERR_ARG;
   if (c->local) {
     if (c->size != 1) return MX_ERR_STATE;
@@ -1591,7 +1606,7 @@ extern "C" int mx_allgather(mx_comm_t *c, const void *sbuf, void *rbuf, size_t b
     return finish(c, s);
   }
   if (!(c->flags & MX_COMM_IPC)) return MX_ERR_STATE;
-  if (c->reg_shm && !c->defer && c->reg_min && (size_t)n * bytes >= c->reg_min) {
+  if (allow_zc && c->reg_shm && !c->defer && c->reg_min && (size_t)n * bytes >= c->reg_min) {
     // zero-copy: every rank reads the peers' blocks straight from their
     // registered sbufs into its own rbuf (remote reads, local writes only)
     const char *ps[MAXR];
@@ -1653,6 +1668,29 @@ extern "C" int mx_allgather(mx_comm_t *c, const void *sbuf, void *rbuf, size_t b
 // pushes the whole round to every peer.  Pure data movement: results are the
 // root's bytes.
 constexpr size_t kBcastDirectMax = 512 << 10;
+
+// the tuned entry points: candidate 0 zero-copy, 1 staged
+extern "C" int mx_reduce_scatter(mx_comm_t *c, const void *sbuf, void *rbuf, const size_t *rcounts, int type,
+                                 int op, int alg, void *stream) {
+  int bucket = -1, cand = -1;
+  const size_t es = mx_type_size(type);
+  if (c && !c->local && rcounts && es) {
+    size_t total = 0;
+    for (int j = 0; j < c->size; j++) total += rcounts[j];
+    cand = tune_pick(c, TUNE_REDUCE_SCATTER, total * es, &bucket);
+  }
+  const auto t0 = std::chrono::steady_clock::now();
+  const int rc = reduce_scatter_impl(c, sbuf, rbuf, rcounts, type, op, alg, stream, cand <= 0);
+  return rc || cand < 0 ? rc : tune_done(c, TUNE_REDUCE_SCATTER, bucket, cand, 2, secs_since(t0));
+}
+
+extern "C" int mx_allgather(mx_comm_t *c, const void *sbuf, void *rbuf, size_t bytes, void *stream) {
+  int bucket = -1, cand = -1;
+  if (c && !c->local) cand = tune_pick(c, TUNE_ALLGATHER, (size_t)c->size * bytes, &bucket);
+  const auto t0 = std::chrono::steady_clock::now();
+  const int rc = allgather_impl(c, sbuf, rbuf, bytes, stream, cand <= 0);
+  return rc || cand < 0 ? rc : tune_done(c, TUNE_ALLGATHER, bucket, cand, 2, secs_since(t0));
+}
 
 extern "C" int mx_bcast(mx_comm_t *c, void *buf, size_t bytes, int root, void *stream) {
   if (!c || !buf || root < 0 || root >= c->size) return MX_ERR_ARG;

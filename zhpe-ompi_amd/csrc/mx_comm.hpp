@@ -149,14 +149,16 @@ struct mx_comm {
   size_t reg_shm_bytes, reg_min;
   uint64_t reg_seq, reg_tick;
   std::vector<struct mx_reg_import> *reg_imp;
-  // data-movement autotuning of blocking allreduces >= 4 MiB: per
-  // power-of-two size class, the first call warms up, the next three time
-  // zero-copy / PULL / PUSH (max over ranks, exchanged in the registration
-  // page) and the fastest is kept.  tune_best: choice + 1, 0 = not yet.
+  // data-movement autotuning of blocking collectives >= 4 MiB per rank
+  // (DESIGN 7): per collective kind (TUNE_*) and power-of-two size class, the
+  // first call warms up, the next ones time each candidate (allreduce:
+  // zero-copy / PULL / PUSH; reduce_scatter, allgather: zero-copy / staged;
+  // max over ranks, exchanged in the registration page) and the fastest is
+  // kept.  tune_best: choice + 1, 0 = not yet.
   int tune_on;
-  uint8_t tune_calls[64];
-  int8_t tune_best[64];
-  double tune_t[64][3];
+  uint8_t tune_calls[3][64];
+  int8_t tune_best[3][64];
+  double tune_t[3][64][3];
   uint64_t tune_seq;
   double timeout_s;
   uint64_t timeout_ticks;
