@@ -156,12 +156,25 @@ typedef struct mx_coll_stats {
 int mx_comm_set_profiling(mx_comm_t *comm, int on);
 int mx_comm_get_stats(mx_comm_t *comm, mx_coll_stats_t *stats, int reset);
 
+/* Algorithm words.  The low byte selects the algorithm.  The algorithms
+ * built on a rooted reduce -- allreduce NONOVERLAPPING (reduce to 0 + bcast,
+ * coll_base_allreduce.c:54-86), reduce_scatter NONOVERLAPPING (reduce to 0 +
+ * scatterv, coll_base_reduce_scatter.c:47-110), reduce_scatter_block and the
+ * rooted reduce itself -- take the reduce algorithm the communicator's
+ * coll_reduce would run from bits 8-15 (MX_REDUCE_*, 0 = the tuned fixed
+ * decision; for mx_reduce / mx_reduce_scatter_block it is the low byte) and
+ * the fanout of the chain tree (MX_REDUCE_CHAIN) from bits 16-23 (0 = 4,
+ * coll_tuned's default chain fanout, coll_tuned_component.c:56) -- what
+ * coll_tuned_reduce_algorithm[_chain_fanout] choose in the reference. */
+#define MX_ALG_WORD(alg, reduce_alg, chain_fanout) \
+    ((int)(alg) | ((int)(reduce_alg) << 8) | ((int)(chain_fanout) << 16))
+
 /* Allreduce algorithm ids == coll_tuned_allreduce_algorithm values
  * (ompi/mca/coll/tuned/coll_tuned_allreduce_decision.c:37-46). */
 enum {
     MX_ALLREDUCE_AUTO = 0,           /* tuned fixed decision                 */
     MX_ALLREDUCE_BASIC_LINEAR = 1,
-    MX_ALLREDUCE_NONOVERLAPPING = 2, /* not provided: MX_ERR_UNSUPPORTED     */
+    MX_ALLREDUCE_NONOVERLAPPING = 2, /* rooted reduce to 0 + bcast           */
     MX_ALLREDUCE_RECURSIVE_DOUBLING = 3,
     MX_ALLREDUCE_RING = 4,
     MX_ALLREDUCE_SEGMENTED_RING = 5,
@@ -169,12 +182,14 @@ enum {
     MX_ALLREDUCE_RCCL = 100          /* RCCL ncclAllReduce (order differs:
                                         FP results within tolerance only)  */
 };
-/* Reduce-scatter algorithm ids (coll_tuned_reduce_scatter_decision.c). */
+/* Reduce-scatter algorithm ids == coll_tuned_reduce_scatter_algorithm
+ * (coll_tuned_reduce_scatter_decision.c:36-43). */
 enum {
     MX_RS_AUTO = 0,
-    MX_RS_NONOVERLAPPING = 1,        /* not provided                         */
+    MX_RS_NONOVERLAPPING = 1,        /* rooted reduce to 0 + scatterv        */
     MX_RS_RECURSIVE_HALVING = 2,
     MX_RS_RING = 3,
+    MX_RS_BUTTERFLY = 4,             /* coll_base_reduce_scatter.c:691-880   */
     MX_RS_RCCL = 100
 };
 
@@ -183,7 +198,8 @@ enum {
 enum {
     MX_REDUCE_AUTO = 0,              /* tuned fixed decision (decision_fixed.c:354-429) */
     MX_REDUCE_LINEAR = 1,
-    MX_REDUCE_CHAIN = 2,             /* fanout MX_REDUCE_CHAIN_FANOUT (tuned default 4,
+    MX_REDUCE_CHAIN = 2,             /* fanout from bits 16-23 of the word, default
+                                        MX_REDUCE_CHAIN_FANOUT (tuned's 4,
                                         coll_tuned_component.c:56) */
     MX_REDUCE_PIPELINE = 3,
     MX_REDUCE_BINARY = 4,

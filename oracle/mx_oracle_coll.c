@@ -407,10 +407,32 @@ int mxo_allreduce_decision(int n, size_t count, size_t es)
 
 /* Allreduce of `count` elements on n simulated ranks.  sbufs may be NULL
  * (MPI_IN_PLACE on every rank).  Returns 0, -1 bad args, -2 unsupported. */
+int mxo_reduce(int alg, int op, int type, int n, size_t count, int root, const void *const *sbufs, void *rbuf);
+
+/* ---- nonoverlapping (coll_base_allreduce.c:54-86): comm->c_coll->coll_reduce
+ * to rank 0 -- with MPI_IN_PLACE rank 0 reduces in place and the others send
+ * their rbuf -- then coll_bcast from 0.  `rword` is the reduce algorithm
+ * word coll_reduce runs (0 = the tuned fixed decision). */
+static int ar_nonoverlapping(int rword, int op, int type, int n, size_t count, const void *const *sbufs,
+                             void *const *rbufs)
+{
+    const void *sb[MAXN];
+    for (int r = 0; r < n; r++) sb[r] = sbufs ? sbufs[r] : (r == 0 ? NULL : rbufs[r]);
+    int rc = mxo_reduce(rword, op, type, n, count, 0, sb, rbufs[0]);
+    if (rc) return rc;
+    for (int r = 1; r < n; r++) memcpy(rbufs[r], rbufs[0], count * mxo_type_size(type));
+    return 0;
+}
+
 int mxo_allreduce(int alg, int op, int type, int n, size_t count, const void *const *sbufs, void *const *rbufs)
 {
     void *rb[MAXN];
     if (n < 1 || n > MAXN) return -1;
+    /* algorithm word (MX_ALG_WORD): low byte algorithm, bits 8-15 the reduce
+     * algorithm of nonoverlapping, bits 16-23 its chain fanout */
+    const int rword = ((alg >> 8) & 0xff) | (alg & 0xff0000);
+    alg &= 0xff;
+    if (alg == 2 && n > 1 && count > 0) return ar_nonoverlapping(rword, op, type, n, count, sbufs, rbufs);
     g_op = op; g_type = type; g_es = mxo_type_size(type);
     if (!g_es) return -1;
     for (int r = 0; r < n; r++) {
@@ -563,23 +585,147 @@ int mxo_reduce_scatter_decision(int n, size_t total_count, size_t es)
     return 3;
 }
 
-/* alg: 0 auto, 2 recursive halving, 3 ring */
+/* butterfly (coll_base_reduce_scatter.c:691-880), restated step by step over
+ * the n simulated ranks: psend/precv double buffers per rank, the sendrecv
+ * of every step snapshotted before any rank reduces. */
+static unsigned mirror_perm(unsigned x, int nbits)                  /* coll_base_util.c:88-96 */
+{
+    unsigned r = 0;
+    for (int i = 0; i < nbits; i++) if (x & (1u << i)) r |= 1u << (nbits - 1 - i);
+    return r;
+}
+static size_t sum_counts(const size_t *rc, const size_t *displs, int rem, int lo, int hi)   /* :629-635 */
+{
+    lo = lo < rem ? lo * 2 : lo + rem;
+    hi = hi < rem ? hi * 2 + 1 : hi + rem;
+    return displs[hi] + rc[hi] - displs[lo];
+}
+static void rs_butterfly(int n, const size_t *rc, char **work, void *const *rbufs)
+{
+    size_t displs[MAXN], total = 0;
+    for (int i = 0; i < n; i++) { displs[i] = total; total += rc[i]; }
+    const int pof2 = next_pow2_le(n), rem = n - pof2;
+    int log2 = 0;
+    while ((1 << log2) < pof2) log2++;
+    char *buf[MAXN][2];
+    int cur[MAXN], vrank[MAXN], sidx[MAXN], ridx[MAXN];
+    for (int r = 0; r < n; r++) {
+        buf[r][0] = malloc(total * g_es + 1);
+        buf[r][1] = malloc(total * g_es + 1);
+        cp(buf[r][0], work[r], total);            /* psend = copy of sbuf */
+        cur[r] = 0;
+        sidx[r] = ridx[r] = 0;
+    }
+#define PSEND(r) buf[r][cur[r]]
+#define PRECV(r) buf[r][cur[r] ^ 1]
+    /* step 1: even r < 2 rem send the whole vector to r+1, which reduces
+     * precv into psend (:764-776) */
+    for (int r = 0; r < n; r++) {
+        if (r < 2 * rem) {
+            if (r % 2 == 0) vrank[r] = -1;
+            else {
+                cp(PRECV(r), PSEND(r - 1), total);
+                red(PRECV(r), PSEND(r), total);
+                vrank[r] = r / 2;
+            }
+        } else vrank[r] = r - rem;
+    }
+    int nblocks = pof2;
+    for (int mask = 1; mask < pof2; mask <<= 1) {
+        int peer[MAXN];
+        size_t scnt[MAXN], sdsp[MAXN], rcnt[MAXN], rdsp[MAXN];
+        nblocks /= 2;
+        for (int r = 0; r < n; r++) {
+            if (vrank[r] < 0) continue;
+            const int vp = vrank[r] ^ mask;
+            peer[r] = vp < rem ? vp * 2 + 1 : vp + rem;
+            if ((vrank[r] & mask) == 0) sidx[r] += nblocks; else ridx[r] += nblocks;
+            scnt[r] = sum_counts(rc, displs, rem, sidx[r], sidx[r] + nblocks - 1);
+            int ix = sidx[r] < rem ? 2 * sidx[r] : rem + sidx[r];
+            sdsp[r] = displs[ix];
+            rcnt[r] = sum_counts(rc, displs, rem, ridx[r], ridx[r] + nblocks - 1);
+            ix = ridx[r] < rem ? 2 * ridx[r] : rem + ridx[r];
+            rdsp[r] = displs[ix];
+        }
+        /* sendrecv: every rank receives its peer's send part into precv at
+         * its own rdispl (the peer's sdispl), before anyone reduces */
+        for (int r = 0; r < n; r++) {
+            if (vrank[r] < 0) continue;
+            const int p = peer[r];
+            if (scnt[p] != rcnt[r] || sdsp[p] != rdsp[r]) abort();   /* the peer sends what I receive */
+            cp(AT(PRECV(r), rdsp[r]), AT(PSEND(p), sdsp[p]), rcnt[r]);
+        }
+        for (int r = 0; r < n; r++) {
+            if (vrank[r] < 0) continue;
+            const int vp = vrank[r] ^ mask;
+            if (vrank[r] < vp) {                      /* precv = psend OP precv; swap */
+                red(AT(PSEND(r), rdsp[r]), AT(PRECV(r), rdsp[r]), rcnt[r]);
+                cur[r] ^= 1;
+            } else {                                  /* psend = precv OP psend */
+                red(AT(PRECV(r), rdsp[r]), AT(PSEND(r), rdsp[r]), rcnt[r]);
+            }
+            sidx[r] = ridx[r];
+        }
+    }
+    /* mirror-permutation exchange of the result blocks (:846-887) */
+    for (int r = 0; r < n; r++) {
+        if (vrank[r] < 0) continue;
+        const int vp = (int)mirror_perm((unsigned)vrank[r], log2);
+        const int peer = vp < rem ? vp * 2 + 1 : vp + rem;
+        int ix = sidx[r] < rem ? 2 * sidx[r] : rem + sidx[r];
+        if (vp < rem) {                               /* first block to the excluded even rank */
+            if (rc[peer - 1]) cp(rbufs[peer - 1], AT(PSEND(r), displs[ix]), rc[ix]);
+            ix++;
+        }
+        if (rc[peer]) cp(rbufs[peer], AT(PSEND(r), displs[ix]), rc[ix]);
+    }
+#undef PSEND
+#undef PRECV
+    for (int r = 0; r < n; r++) { free(buf[r][0]); free(buf[r][1]); }
+}
+
+/* reduce_scatter NONOVERLAPPING (coll_base_reduce_scatter.c:47-110):
+ * coll_reduce of the whole vector to rank 0 (MPI_IN_PLACE: the root reduces
+ * in place), then scatterv */
+static int rs_nonoverlapping(int rword, int op, int type, int n, const size_t *rc, const void *const *sbufs,
+                             void *const *rbufs)
+{
+    size_t total = 0, es = mxo_type_size(type);
+    for (int i = 0; i < n; i++) total += rc[i];
+    const void *sb[MAXN];
+    for (int r = 0; r < n; r++) sb[r] = sbufs ? sbufs[r] : (r == 0 ? NULL : rbufs[r]);
+    char *full = malloc(total * es + 1);
+    if (!sbufs) memcpy(full, rbufs[0], total * es);   /* the root's in-place data */
+    int rc0 = mxo_reduce(rword, op, type, n, total, 0, sb, full);
+    size_t d = 0;
+    for (int r = 0; r < n && !rc0; r++) { memcpy(rbufs[r], full + d * es, rc[r] * es); d += rc[r]; }
+    free(full);
+    return rc0;
+}
+
+/* alg word: low byte 0 auto, 1 nonoverlapping (bits 8-23: its reduce word),
+ * 2 recursive halving, 3 ring, 4 butterfly.  sbufs NULL = MPI_IN_PLACE
+ * (rbufs hold the full vectors). */
 int mxo_reduce_scatter(int alg, int op, int type, int n, const size_t *rcounts, const void *const *sbufs,
                        void *const *rbufs)
 {
     size_t total = 0;
     char *work[MAXN];
     if (n < 1 || n > MAXN) return -1;
+    const int rword = ((alg >> 8) & 0xff) | (alg & 0xff0000);
+    alg &= 0xff;
     g_op = op; g_type = type; g_es = mxo_type_size(type);
     for (int i = 0; i < n; i++) total += rcounts[i];
+    if (alg == 1 && n > 1) return rs_nonoverlapping(rword, op, type, n, rcounts, sbufs, rbufs);
     for (int r = 0; r < n; r++) {
         work[r] = malloc(total * g_es + 1);
-        cp(work[r], sbufs[r], total);
+        cp(work[r], sbufs ? sbufs[r] : rbufs[r], total);
     }
     if (n == 1) { cp(rbufs[0], work[0], total); free(work[0]); return 0; }
     if (alg == 0) alg = mxo_reduce_scatter_decision(n, total, g_es);
     if (alg == 3) rs_ring(n, rcounts, work, rbufs);
     else if (alg == 2) rs_recursive_halving(n, rcounts, work, rbufs);
+    else if (alg == 4) rs_butterfly(n, rcounts, work, rbufs);
     else { for (int r = 0; r < n; r++) free(work[r]); return -2; }
     for (int r = 0; r < n; r++) free(work[r]);
     return 0;
@@ -775,12 +921,16 @@ static void reduce_linear(int n, size_t count, char *const *sendbuf, char *rbuf)
 
 /* MPI_Reduce of `count` elements on n simulated ranks.  sbufs[r] may be NULL
  * only for r == root (MPI_IN_PLACE: the root's data is in rbuf).  alg ids:
- * 0 tuned decision, 1 linear, 2 chain (fanout 4), 3 pipeline, 4 binary,
- * 5 binomial, 6 in-order binary. */
+ * 0 tuned decision, 1 linear, 2 chain (fanout 4 unless bits 16-23 give
+ * another), 3 pipeline, 4 binary, 5 binomial, 6 in-order binary. */
 int mxo_reduce(int alg, int op, int type, int n, size_t count, int root, const void *const *sbufs, void *rbuf)
 {
     char *sb[MAXN];
     int segsize = 0, inplace;
+    /* algorithm word (include/mx_coll.h MX_ALG_WORD): bits 16-23 carry the
+     * chain fanout (coll_tuned_reduce_algorithm_chain_fanout), 0 = 4 */
+    const int fanout = (alg >> 16) & 0xff;
+    alg &= 0xff;
     if (n < 1 || n > MAXN || root < 0 || root >= n || !rbuf) return -1;
     g_op = op; g_type = type; g_es = mxo_type_size(type);
     if (!g_es) return -1;
@@ -808,7 +958,7 @@ int mxo_reduce(int alg, int op, int type, int n, size_t count, int root, const v
     }
     if (alg < 2 || alg > 6) return -2;
     g_tree_kind = alg;
-    g_tree_fanout = 4;                                                  /* ompi_coll_tuned_init_chain_fanout */
+    g_tree_fanout = fanout ? fanout : 4;                                /* ompi_coll_tuned_init_chain_fanout */
     memset(rg_free, 0, sizeof rg_free);
     if (alg == 6) {
         /* in-order binary (:509-605): generic rooted at io_root = n-1 */

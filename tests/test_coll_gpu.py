@@ -701,3 +701,73 @@ def test_late_peer_poisons_instead_of_corrupting():
     assert rc0a == TIMEOUT and rc1a == TIMEOUT, out
     assert rc0b == TIMEOUT and rc1b == TIMEOUT, out          # poisoned: every later call fails
     assert t0b < 1.0 and t1b < 1.0, (t0b, t1b)               # ... without waiting again
+
+
+# ---------------------------------------------------------------------------
+# coll/tuned's forced algorithms beyond the fixed decision (round 3):
+# allreduce 2 nonoverlapping (coll_base_allreduce.c:54-86: coll_reduce to 0 +
+# bcast), reduce_scatter 1 nonoverlapping (coll_base_reduce_scatter.c:47-110:
+# coll_reduce to 0 + scatterv) and 4 butterfly (:691-880), with the reduce
+# algorithm and chain fanout coll_reduce would run carried in the word
+# ---------------------------------------------------------------------------
+WORDS_AR = [mxompi.alg_word(2, ra, fo) for ra, fo in ((0, 0), (1, 0), (2, 0), (2, 2), (3, 0), (4, 0), (5, 0),
+                                                      (6, 0))]
+
+
+@pytest.mark.parametrize("word", WORDS_AR, ids=lambda w: f"w{w:x}")
+@pytest.mark.parametrize("n", [2, 3, 5, 8])
+@pytest.mark.parametrize("op,t", [("SUM", "FLOAT"), ("MAX", "DOUBLE"), ("MAXLOC", "FLOAT_INT")])
+@pytest.mark.parametrize("inplace", [False, True])
+def test_allreduce_nonoverlapping_local(word, n, op, t, inplace):
+    L = _oracle()
+    es = mxompi.type_size(t)
+    for count in (1, 5, 1001, 70001):
+        xs = [gen(t, op, count, 700 + r) for r in range(n)]
+        exp = [x.copy() if inplace else np.zeros(count * es, np.uint8) for x in xs]
+        sp = None if inplace else (vp * n)(*[x.ctypes.data for x in xs])
+        assert L.mxo_allreduce(word, mxompi.OP[op], mxompi.TYPE[t], n, count, sp,
+                               (vp * n)(*[e.ctypes.data for e in exp])) == 0
+        comm = mxompi.Comm.local(n)
+        S = [_dev(x) for x in xs]
+        if inplace:
+            comm.allreduce_local([mxompi.IN_PLACE] * n, [s.data_ptr() for s in S], count, t, op, word, _stream())
+            R = S
+        else:
+            R = [torch.zeros(count * es, dtype=torch.uint8, device="cuda") for _ in range(n)]
+            comm.allreduce_local([s.data_ptr() for s in S], [r.data_ptr() for r in R], count, t, op, word, _stream())
+        for r in range(n):
+            golden_io.assert_coll_equal(R[r].cpu().numpy(), exp[r], mxompi.OP[op], mxompi.TYPE[t],
+                                        f"allreduce word {word:#x} n={n} count={count} rank {r}")
+        comm.close()
+
+
+@pytest.mark.parametrize("word", [4, mxompi.alg_word(1), mxompi.alg_word(1, 1), mxompi.alg_word(1, 2, 3),
+                                  mxompi.alg_word(1, 3), mxompi.alg_word(1, 5), mxompi.alg_word(1, 6)],
+                         ids=lambda w: f"w{w:x}")
+@pytest.mark.parametrize("n", [2, 3, 5, 8])
+@pytest.mark.parametrize("op,t", [("SUM", "FLOAT"), ("MAXLOC", "FLOAT_INT"), ("SUM", "INT64_T")])
+@pytest.mark.parametrize("inplace", [False, True])
+def test_reduce_scatter_forced_local(word, n, op, t, inplace):
+    L = _oracle()
+    es = mxompi.type_size(t)
+    rng = np.random.default_rng(n * 31 + word)
+    for rc in ([0] * (n - 1) + [5], [int(x) for x in rng.integers(0, 300, n)], [2000] * n):
+        total = sum(rc)
+        xs = [gen(t, op, total, 90 + r) for r in range(n)]
+        exp = [x.copy() if inplace else np.zeros(max(1, c) * es, np.uint8) for x, c in zip(xs, rc)]
+        assert L.mxo_reduce_scatter(word, mxompi.OP[op], mxompi.TYPE[t], n, (sz * n)(*rc),
+                                    None if inplace else (vp * n)(*[x.ctypes.data for x in xs]),
+                                    (vp * n)(*[e.ctypes.data for e in exp])) == 0
+        comm = mxompi.Comm.local(n)
+        S = [_dev(x) for x in xs]
+        if inplace:
+            comm.reduce_scatter_local(None, [s.data_ptr() for s in S], rc, t, op, word, _stream())
+            R = S
+        else:
+            R = [torch.zeros(max(1, c) * es, dtype=torch.uint8, device="cuda") for c in rc]
+            comm.reduce_scatter_local([s.data_ptr() for s in S], [r.data_ptr() for r in R], rc, t, op, word,
+                                      _stream())
+        for r in range(n):
+            golden_io.assert_coll_equal(R[r].cpu().numpy()[: rc[r] * es], exp[r][: rc[r] * es], mxompi.OP[op],
+                                        mxompi.TYPE[t], f"reduce_scatter word {word:#x} n={n} rc={rc} rank {r}")
+        comm.close()

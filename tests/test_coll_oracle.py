@@ -84,7 +84,7 @@ def test_ring_allreduce_fold_starts_at_block_owner():
             assert got[r][b] == exp
 
 
-ALGS = [1, 3, 4, 5, 6]
+ALGS = [1, 2, 3, 4, 5, 6]
 
 
 @pytest.mark.parametrize("alg", ALGS)
@@ -102,7 +102,7 @@ def test_allreduce_integer_exact(alg, n):
             np.testing.assert_array_equal(r, sum(xs))
 
 
-@pytest.mark.parametrize("alg", [2, 3])
+@pytest.mark.parametrize("alg", [1, 2, 3, 4])
 @pytest.mark.parametrize("n", list(range(1, 13)))
 def test_reduce_scatter_integer_exact(alg, n):
     L = _L()
@@ -131,3 +131,110 @@ def test_decisions_agree_with_product():
                 ref = L.mxo_allreduce_decision(n, count, es)
                 assert mine == ref, (n, t, count)
                 assert mxompi.reduce_scatter_decision(n, count, t) == L.mxo_reduce_scatter_decision(n, count, es)
+
+
+def _sym_tree(L, v):
+    """Canonical nested form of a symbolic node: leaves as (rank, elem)."""
+    if v < 0:
+        k = -v - 1
+        return (k // 1000, k % 1000)
+    t, s_ = ctypes.c_int64(), ctypes.c_int64()
+    assert L.mxo_sym_node(v, ctypes.byref(t), ctypes.byref(s_)) == 0
+    return ("op", _sym_tree(L, t.value), _sym_tree(L, s_.value))    # (target, source)
+
+
+def _sym_allreduce(L, alg, n, count, inplace=False):
+    L.mxo_sym_reset(1)
+    try:
+        xs = [np.array([_leaf(r, e) for e in range(count)], np.int64) for r in range(n)]
+        rb = [x.copy() if inplace else np.zeros(count, np.int64) for x in xs]
+        sp = None if inplace else (vp * n)(*[x.ctypes.data for x in xs])
+        rp = (vp * n)(*[r.ctypes.data for r in rb])
+        assert L.mxo_allreduce(alg, 3, mxompi.TYPE["INT64_T"], n, count, sp, rp) == 0
+        return [[_sym_tree(L, int(rb[r][e])) for e in range(count)] for r in range(n)]
+    finally:
+        L.mxo_sym_reset(0)
+
+
+def _sym_reduce_scatter(L, alg, n, rcounts, inplace=False):
+    total = sum(rcounts)
+    L.mxo_sym_reset(1)
+    try:
+        xs = [np.array([_leaf(r, e) for e in range(total)], np.int64) for r in range(n)]
+        rb = [x.copy() if inplace else np.zeros(max(1, c), np.int64) for x, c in zip(xs, rcounts)]
+        sp = None if inplace else (vp * n)(*[x.ctypes.data for x in xs])
+        rp = (vp * n)(*[r.ctypes.data for r in rb])
+        assert L.mxo_reduce_scatter(alg, 3, mxompi.TYPE["INT64_T"], n, (sz * n)(*rcounts), sp, rp) == 0
+        return [[_sym_tree(L, int(rb[r][e])) for e in range(rcounts[r])] for r in range(n)]
+    finally:
+        L.mxo_sym_reset(0)
+
+
+@pytest.mark.parametrize("n", list(range(2, 17)))
+def test_butterfly_reduce_scatter_is_the_recursive_doubling_tree(n):
+    """coll_base_reduce_scatter.c:691-880 restated step by step (psend /
+    precv swaps, mirror-permutation hand-off) gives every element the tree
+    recursive doubling allreduce gives it (coll_base_allreduce.c:130-274):
+    masks ascending, the higher virtual rank's partial the target, the odd
+    rank the target of the non-power-of-two leaf.  This is the identity the
+    device fold program relies on (mx_coll.hip reduce_scatter_segments)."""
+    L = _L()
+    rng = np.random.default_rng(n)
+    rcounts = [int(x) for x in rng.integers(0, 4, n)]
+    rcounts[0] += 1
+    total = sum(rcounts)
+    bf = _sym_reduce_scatter(L, 4, n, rcounts)
+    rd = _sym_allreduce(L, 3, n, total)
+    off = 0
+    for r in range(n):
+        for e in range(rcounts[r]):
+            assert bf[r][e] == rd[0][off + e], (n, r, e)
+        off += rcounts[r]
+
+
+def _sym_reduce(L, alg, n, count, root, inplace):
+    L.mxo_reduce.argtypes = [i, i, i, i, sz, i, ctypes.POINTER(vp), vp]
+    L.mxo_sym_reset(1)
+    try:
+        xs = [np.array([_leaf(r, e) for e in range(count)], np.int64) for r in range(n)]
+        out = xs[root].copy() if inplace else np.zeros(count, np.int64)
+        ptrs = [None if (inplace and r == root) else x.ctypes.data for r, x in enumerate(xs)]
+        assert L.mxo_reduce(alg, 3, mxompi.TYPE["INT64_T"], n, count, root, (vp * n)(*ptrs), out.ctypes.data) == 0
+        return [_sym_tree(L, int(v)) for v in out]
+    finally:
+        L.mxo_sym_reset(0)
+
+
+@pytest.mark.parametrize("inplace", [False, True])
+@pytest.mark.parametrize("ralg", [1, 2, 3, 4, 5, 6])
+@pytest.mark.parametrize("n", [2, 3, 5, 8])
+def test_nonoverlapping_is_the_rooted_reduce_tree(n, ralg, inplace):
+    """allreduce alg 2 (coll_base_allreduce.c:54-86) and reduce_scatter alg 1
+    (coll_base_reduce_scatter.c:47-110) are coll_reduce to rank 0 -- with the
+    reduce algorithm the communicator's coll_reduce runs, carried in bits
+    8-15 of the algorithm word -- then a bcast / scatterv.  MPI_IN_PLACE makes
+    rank 0 reduce in place (its data becomes the accumulator)."""
+    L = _L()
+    count = 7
+    red = _sym_reduce(L, ralg, n, count, 0, inplace)
+    ar = _sym_allreduce(L, 2 | (ralg << 8), n, count, inplace)
+    for r in range(n):
+        assert ar[r] == red, (r, ralg)
+    rcounts = [1 + (r % 3) for r in range(n)]
+    red = _sym_reduce(L, ralg, n, sum(rcounts), 0, inplace)
+    rs = _sym_reduce_scatter(L, 1 | (ralg << 8), n, rcounts, inplace)
+    off = 0
+    for r in range(n):
+        assert rs[r] == red[off:off + rcounts[r]], (r, ralg)
+        off += rcounts[r]
+
+
+def test_chain_fanout_changes_the_chain_tree():
+    """coll_tuned_reduce_algorithm_chain_fanout reaches the chain topology
+    (coll_base_topo.c:393-506) through bits 16-23 of the algorithm word:
+    0 means tuned's default 4, and distinct fanouts give distinct trees."""
+    L = _L()
+    n = 9
+    trees = {f: _sym_reduce(L, 2 | (f << 16), n, 1, 0, False)[0] for f in (1, 2, 3, 4, 7)}
+    assert trees[4] == _sym_reduce(L, 2, n, 1, 0, False)[0]
+    assert len({repr(t) for t in trees.values()}) == len(trees)

@@ -685,6 +685,10 @@ static void push_clip(std::vector<Seg> &out, size_t lo, size_t hi, size_t rlo, s
   if (a < b) out.push_back(Seg{a, b, p});
 }
 
+// the reduce word (MX_REDUCE_* | fanout << 16) carried by an algorithm word
+// (MX_ALG_WORD) of the algorithms built on a rooted reduce
+static inline int reduce_word_of(int alg) { return ((alg >> 8) & 0xff) | (alg & 0xff0000); }
+
 // Internal allreduce algorithm id: libnbc's ring (allred_sched_ring,
 // nbc_iallreduce.c:629-860), reached through mx_iallreduce.
 constexpr int kArNbcRing = 1001;
@@ -780,6 +784,16 @@ static int reduce_scatter_segments(int alg, int n, const size_t *rcounts, size_t
     int v = blk < 2 * rem ? blk / 2 : blk - rem;
     (void)P;
     push_clip(out, lo, hi, lo, hi, butterfly(n, false, (uint32_t)v, true));
+    return MX_SUCCESS;
+  }
+  if (alg == MX_RS_BUTTERFLY) {
+    // coll_base_reduce_scatter.c:691-880: masks 1, 2, 4, ... (ascending);
+    // at every level the lower virtual rank's partial is the source and the
+    // higher one's the target (vrank < vpeer: precv = psend OP precv, else
+    // psend = precv OP psend, :833-845), whichever rank keeps the block;
+    // the non-power-of-two leaves fold the even rank's vector into the odd
+    // one's (:772-776).  Per element that is the recursive-doubling tree.
+    push_clip(out, lo, hi, lo, hi, butterfly(n, true, 0xffffffffu, true));
     return MX_SUCCESS;
   }
   return MX_ERR_UNSUPPORTED;
@@ -890,11 +904,19 @@ extern "C" int mx_allreduce_local(mx_comm_t *c, const void *const *sbufs, void *
     if (int rc = copy_async(dst[0], src[0], count * es, s)) return rc;
     return finish(c, s);
   }
+  if ((alg & 0xff) == MX_ALLREDUCE_NONOVERLAPPING) {
+    // coll_base_allreduce.c:54-86: coll_reduce to rank 0 (rank 0 passes
+    // MPI_IN_PLACE when the call is in place), then coll_bcast from 0
+    const void *sb2[MAXR];
+    for (int j = 0; j < n; j++) sb2[j] = (sbufs && sbufs[j] != MX_IN_PLACE) ? sbufs[j] : (j ? rbufs[j] : MX_IN_PLACE);
+    if (int rc = mx_reduce_local(c, sb2, rbufs, count, type, op, 0, reduce_word_of(alg), stream)) return rc;
+    return mx_bcast_local(c, rbufs, count * es, 0, stream);
+  }
   size_t off[MAXR], len[MAXR];
   blockcount(count, n, off, len);
   for (int p = 0; p < n; p++) {
     std::vector<Seg> segs;
-    int rc = allreduce_segments(alg, n, count, es, off[p], off[p] + len[p], segs);
+    int rc = allreduce_segments(alg & 0xff, n, count, es, off[p], off[p] + len[p], segs);
     if (rc) return rc;
     const char *sp[MAXR];
     char *dp[MAXR];
@@ -906,6 +928,14 @@ extern "C" int mx_allreduce_local(mx_comm_t *c, const void *const *sbufs, void *
   }
   return finish(c, s);
 }
+
+// reduce_scatter NONOVERLAPPING (coll_base_reduce_scatter.c:47-110): the
+// rooted reduce DAG to rank 0, every rank folding its own block of it
+// (defined with the fold VM below)
+static int rs_nonoverlapping(mx_comm *c, const char *sb, char *rb, const size_t *rcounts, int type, int op, int alg,
+                             bool allow_zc, hipStream_t s);
+static int rs_nonoverlapping_local(mx_comm *c, const char *const *src, void *const *rbufs, const size_t *rcounts,
+                                   int type, int op, int alg, bool inplace, hipStream_t s);
 
 extern "C" int mx_reduce_scatter_local(mx_comm_t *c, const void *const *sbufs, void *const *rbufs,
                                        const size_t *rcounts, int type, int op, int alg, void *stream) {
@@ -927,6 +957,9 @@ extern "C" int mx_reduce_scatter_local(mx_comm_t *c, const void *const *sbufs, v
     if (int rc = copy_async(rbufs[0], src[0], total * es, s)) return rc;
     return finish(c, s);
   }
+  if ((alg & 0xff) == MX_RS_NONOVERLAPPING)
+    return rs_nonoverlapping_local(c, src, rbufs, rcounts, type, op, alg, !sbufs || sbufs[0] == MX_IN_PLACE, s);
+  alg &= 0xff;
   // IN_PLACE (or rbuf aliasing sbuf): rank p's result lands at rbufs[p][0..)
   // while other blocks of rbufs[p] are still inputs, so results go to a
   // temporary laid out like the full vector and are copied back at the end.
@@ -1464,6 +1497,16 @@ extern "C" int mx_allreduce(mx_comm_t *c, const void *sbuf, void *rbuf, size_t c
     return finish(c, s);
   }
   if (!(c->flags & MX_COMM_IPC)) return MX_ERR_STATE;
+  if ((alg & 0xff) == MX_ALLREDUCE_NONOVERLAPPING) {
+    // coll_base_allreduce.c:54-86: coll_reduce to rank 0, then coll_bcast;
+    // in place, rank 0 reduces MPI_IN_PLACE and the others send their rbuf
+    const bool inplace = sbuf == MX_IN_PLACE || !sbuf;
+    const void *rsb = (inplace && c->rank == 0) ? MX_IN_PLACE : (const void *)sb;
+    if (int rc = mx_reduce(c, rsb, c->rank == 0 ? rb : nullptr, count, type, op, 0, reduce_word_of(alg), stream))
+      return rc;
+    return mx_bcast(c, rb, count * es, 0, stream);
+  }
+  alg &= 0xff;
   if (c->os_max && count * es <= c->os_max) {
     std::vector<Seg> segs;
     int rc = allreduce_segments(alg, n, count, es, 0, count, segs);
@@ -1513,6 +1556,8 @@ static int reduce_scatter_impl(mx_comm_t *c, const void *sbuf, void *rbuf, const
     return finish(c, s);
   }
   if (!(c->flags & MX_COMM_IPC)) return MX_ERR_STATE;
+  if ((alg & 0xff) == MX_RS_NONOVERLAPPING) return rs_nonoverlapping(c, sb, (char *)rbuf, rcounts, type, op, alg, allow_zc, s);
+  alg &= 0xff;
   std::vector<Seg> segs;
   int rc = reduce_scatter_segments(alg, n, rcounts, es, r, segs);
   if (rc) return rc;
@@ -2042,7 +2087,7 @@ static int reduce_generic_expr(Dag &g, int v, int root, bool root_inplace, const
 
 // The fold expression of MPI_Reduce(root) under algorithm `alg`
 // (coll_tuned_reduce_decision.c:36-45 numbering).
-static int reduce_expr(Dag &g, int alg, int root, bool root_inplace) {
+static int reduce_expr(Dag &g, int alg, int root, bool root_inplace, int fanout = MX_REDUCE_CHAIN_FANOUT) {
   const int n = g.n;
   switch (alg) {
     case MX_REDUCE_LINEAR: {           // basic_linear (:699-722): rbuf = x_{n-1}; rbuf op= x_i
@@ -2052,7 +2097,7 @@ static int reduce_expr(Dag &g, int alg, int root, bool root_inplace) {
     }
     case MX_REDUCE_CHAIN:
       return reduce_generic_expr(g, root, root, root_inplace,
-                                 [&](int v) { return topo_chain(MX_REDUCE_CHAIN_FANOUT, n, root, v); }, 0);
+                                 [&](int v) { return topo_chain(fanout, n, root, v); }, 0);
     case MX_REDUCE_PIPELINE:
       return reduce_generic_expr(g, root, root, root_inplace, [&](int v) { return topo_chain(1, n, root, v); }, 0);
     case MX_REDUCE_BINARY:
@@ -2075,14 +2120,18 @@ static int reduce_expr(Dag &g, int alg, int root, bool root_inplace) {
 
 // root_inplace: 0 no, 1 yes, 2 unknown here (multi-process part owners):
 // both variants, guarded by the root's info bit, sharing every subtree
-static int reduce_dag(Dag &g, int alg, size_t count, size_t es, int root, int root_inplace) {
+// `word`: MX_REDUCE_* in the low byte, the chain fanout in bits 16-23
+// (MX_ALG_WORD; 0 = MX_REDUCE_CHAIN_FANOUT)
+static int reduce_dag(Dag &g, int word, size_t count, size_t es, int root, int root_inplace) {
+  int alg = word & 0xff;
+  const int fanout = ((word >> 16) & 0xff) ? ((word >> 16) & 0xff) : MX_REDUCE_CHAIN_FANOUT;
   if (alg == MX_REDUCE_AUTO) alg = mx_reduce_decision(g.n, count, -(int)es);
   if (g.n == 1) {
     g.emit(0, root);
     return MX_SUCCESS;
   }
-  const int e1 = root_inplace != 0 ? reduce_expr(g, alg, root, true) : -3;
-  const int e0 = root_inplace != 1 ? reduce_expr(g, alg, root, false) : -3;
+  const int e1 = root_inplace != 0 ? reduce_expr(g, alg, root, true, fanout) : -3;
+  const int e0 = root_inplace != 1 ? reduce_expr(g, alg, root, false, fanout) : -3;
   if (e1 == -2 || e0 == -2) return MX_ERR_UNSUPPORTED;
   if (e1 == -1 || e0 == -1) return MX_ERR_ARG;
   if (root_inplace == 1) g.emit(e1, root);
@@ -2368,6 +2417,66 @@ static uint32_t dest_mask_of(const Dag &g, int owner_rank) {
 }
 
 }  // namespace
+
+// coll_base_reduce_scatter.c:66-88: coll_reduce of the whole vector to rank
+// 0 (with MPI_IN_PLACE the root reduces in place: its own data is the
+// accumulator of its combination) and a scatterv; rank q's block of that
+// reduction is folded by q itself.
+static int rs_nonoverlapping(mx_comm *c, const char *sb, char *rb, const size_t *rcounts, int type, int op, int alg,
+                             bool allow_zc, hipStream_t s) {
+  vm_launch_fn vl;
+  size_t es, total = 0;
+  int rc = vm_setup(op, type, &vl, &es);
+  if (rc) return rc;
+  for (int j = 0; j < c->size; j++) total += rcounts[j];
+  Dag g(c->size);
+  if ((rc = reduce_dag(g, reduce_word_of(alg), total, es, 0, sb == rb ? 1 : 0))) return rc;
+  g.out.back().dst = -1;   // the block's owner
+  VmProg p;
+  if ((rc = dag_compile(g, c->rank, p))) return rc;
+  const size_t keep = c->reg_min;
+  if (!allow_zc) c->reg_min = 0;   // the autotuner's staged candidate
+  rc = vm_scatter_blocks(c, vl, p, sb, rb, rcounts, es, s);
+  c->reg_min = keep;
+  return rc;
+}
+
+static int rs_nonoverlapping_local(mx_comm *c, const char *const *src, void *const *rbufs, const size_t *rcounts,
+                                   int type, int op, int alg, bool inplace, hipStream_t s) {
+  vm_launch_fn vl;
+  size_t es, disp[MAXR], total = 0;
+  int rc = vm_setup(op, type, &vl, &es);
+  if (rc) return rc;
+  const int n = c->size;
+  for (int j = 0; j < n; j++) { disp[j] = total; total += rcounts[j]; }
+  Dag g(n);
+  if ((rc = reduce_dag(g, reduce_word_of(alg), total, es, 0, inplace ? 1 : 0))) return rc;
+  g.out.back().dst = -1;
+  // results go to a temporary laid out like the full vector when any rank's
+  // rbuf aliases its input (they are read until the last block is folded)
+  bool any_alias = false;
+  for (int q = 0; q < n; q++)
+    if ((const char *)rbufs[q] == src[q]) any_alias = true;
+  char *tmp = nullptr;
+  if (any_alias && hipMallocAsync((void **)&tmp, total * es + 16, s) != hipSuccess) return MX_ERR_NOMEM;
+  for (int q = 0; q < n && !rc; q++) {
+    if (!rcounts[q]) continue;
+    VmProg p;
+    if ((rc = dag_compile(g, q, p))) break;
+    char *dst[MAXR] = {};
+    dst[q] = tmp ? tmp + disp[q] * es : (char *)rbufs[q];
+    rc = vm_run_local(vl, p, src, dst, disp[q], disp[q] + rcounts[q], es, s);
+  }
+  if (tmp) {
+    CopyArgs ca;
+    memset(&ca, 0, sizeof ca);
+    for (int q = 0; q < n; q++)
+      if (rcounts[q]) ca.j[ca.n++] = CopyJob{tmp + disp[q] * es, (char *)rbufs[q], rcounts[q] * es};
+    if (!rc) rc = copy_launch(c, ca, s);
+    (void)hipFreeAsync(tmp, s);
+  }
+  return rc ? rc : finish(c, s);
+}
 
 // ---- rooted reduce ------------------------------------------------------
 extern "C" int mx_reduce_local(mx_comm_t *c, const void *const *sbufs, void *const *rbufs, size_t count, int type,

@@ -174,10 +174,19 @@ ANY_SOURCE = -1                    # MX_ANY_SOURCE (MPI_ANY_SOURCE)
 COMM_IPC, COMM_RCCL, COMM_P2P = 1, 2, 4
 ALLREDUCE = {"auto": 0, "basic_linear": 1, "nonoverlapping": 2, "recursive_doubling": 3,
              "ring": 4, "segmented_ring": 5, "rabenseifner": 6, "rccl": 100}
-REDUCE_SCATTER = {"auto": 0, "nonoverlapping": 1, "recursive_halving": 2, "ring": 3, "rccl": 100}
+REDUCE_SCATTER = {"auto": 0, "nonoverlapping": 1, "recursive_halving": 2, "ring": 3, "butterfly": 4, "rccl": 100}
 REDUCE = {"auto": 0, "linear": 1, "chain": 2, "pipeline": 3, "binary": 4, "binomial": 5,
           "in_order_binary": 6, "rabenseifner": 7}
 SCAN = {"auto": 0, "linear": 1, "recursive_doubling": 2}
+
+
+def alg_word(alg, reduce_alg=0, chain_fanout=0):
+    """MX_ALG_WORD (include/mx_coll.h): an algorithm id plus, for the
+    algorithms built on a rooted reduce, the reduce algorithm coll_reduce
+    runs (bits 8-15) and the chain fanout (bits 16-23)."""
+    if isinstance(reduce_alg, str):
+        reduce_alg = REDUCE[reduce_alg]
+    return int(alg) | (int(reduce_alg) << 8) | (int(chain_fanout) << 16)
 # libnbc numbering (coll_libnbc_component.c:58-92)
 IALLREDUCE = {"auto": 0, "ring": 1, "binomial": 2, "rabenseifner": 3, "recursive_doubling": 4}
 IREDUCE = {"auto": 0, "chain": 1, "binomial": 2, "rabenseifner": 3}
