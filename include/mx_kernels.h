@@ -165,6 +165,11 @@ int mx_stream_sync_fast(void *stream);
  * are in) and runs its kernels on streams it owns. */
 int mx_alloc(size_t bytes, void **p);      /* device memory                */
 int mx_free(void *p);
+/* Pinned host memory (hipHostMalloc): the coll component's host copies of
+ * device buffers when a collective runs on the saved host module (the
+ * coll/cuda staging direction, coll_cuda_allreduce.c:30-73). */
+int mx_host_alloc(size_t bytes, void **p);
+int mx_host_free(void *p);
 /* Any direction (host pageable / pinned / device), ordered on `stream`. */
 int mx_memcpy(void *dst, const void *src, size_t bytes, void *stream);
 /* A non-blocking stream (does not synchronise with the legacy default one),

@@ -2,7 +2,8 @@
 which loads the mi355x components from lib/libmx_ompi.so the way Open MPI's
 MCA repository would and restates op/coll selection and the MPI entry
 points.  TEST INFRASTRUCTURE: the base op functions it seeds the tables
-with are the oracle's (pinned to the reference's op_base_functions.c)."""
+with, and the algorithms of its host coll modules, are the oracle
+restatements (oracle/mx_oracle_op.c, oracle/mx_oracle_coll.c)."""
 import ctypes
 import os
 
@@ -32,6 +33,10 @@ def host(with_components=True):
     H.mxh_op.argtypes = [ctypes.c_char_p]
     H.mxh_op_slot_owner.argtypes = [vp, ci, ci]
     H.mxh_set_mca.argtypes = [ctypes.c_char_p, ci]
+    H.mxh_set_mca_str.argtypes = [ctypes.c_char_p, ctypes.c_char_p]
+    H.mxh_intercomm_create.restype = vp
+    H.mxh_intercomm_create.argtypes = [ci, ci, AG, vp]
+    H.mxh_set_coll_oracle.argtypes = [vp]
     H.mxh_comm_create.restype = vp
     H.mxh_comm_create.argtypes = [ci, ci, AG, vp]
     H.mxh_comm_self.restype = vp
@@ -64,6 +69,14 @@ def host(with_components=True):
     O = oracle_lib.oracle()
     base = ctypes.cast(O.mxo_reduce2, vp)
     pat = ctypes.cast(O.mxo_supported, vp)
+    # the host coll modules evaluate coll/tuned, coll/basic and coll/libnbc
+    # algorithms with the oracle restatement (mx_host.h mxh_coll_oracle_t)
+    fns = [ctypes.cast(getattr(O, f), vp).value for f in
+           ("mxo_allreduce", "mxo_reduce_scatter", "mxo_reduce", "mxo_scan", "mxo_exscan", "mxo_iallreduce",
+            "mxo_ireduce", "mxo_ireduce_scatter")]
+    table = (vp * len(fns))(*fns)
+    _state[("oracle_table",)] = table
+    H.mxh_set_coll_oracle(ctypes.cast(table, vp))
     comp = os.path.join(mxompi.LIB_DIR, "libmx_ompi.so").encode() if with_components else b""
     rc = H.mxh_init(comp, base, pat)
     assert rc == 0, rc

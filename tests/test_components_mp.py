@@ -3,18 +3,18 @@
 * CPU (gloo, world_size 2 and 3): host buffers.  The harness's MPI entry
   points dispatch through comm->c_coll; on a machine without a GPU the
   coll/mi355x component declines at init_query (no device), every slot stays
-  with the host base module, and the results equal the oracle's linear
-  orders.  Covers the bootstrap exchange (a host allgather over
-  torch.distributed/gloo, the role the saved lower allgather plays inside
-  Open MPI) and the N>1 host logic without a GPU.
+  with the host stand-ins of coll/tuned, coll/basic and coll/libnbc, and the
+  results equal the oracle's orders for them.  Covers the bootstrap exchange
+  (a host allgather over torch.distributed/gloo, the role the saved lower
+  allgather plays inside Open MPI) and the N>1 host logic without a GPU.
 * GPU (n processes sharing the one GPU): device buffers go through
-  coll/mi355x -> mx_* all-peer path and must be bit-identical to the
-  coll/tuned algorithm the oracle restates.
+  coll/mi355x -- on the device above coll_mi355x_host_max_kb, on the saved
+  host module through host copies at or below it -- and must be
+  bit-identical to the coll/tuned algorithm the oracle restates either way.
 * Nonblocking and persistent forms (MPI_Iallreduce, MPI_Ireduce, MPI_Iscan,
   MPI_Iexscan, MPI_Ireduce_scatter_block posted together, then MPI_Test /
-  MPI_Wait; MPI_Allreduce_init + MPI_Start twice): host buffers stay with
-  the host base module (libnbc's role), device buffers go through
-  coll/mi355x's requests and must match coll/libnbc's orders.
+  MPI_Wait; MPI_Allreduce_init + MPI_Start twice) must match coll/libnbc's
+  orders on either path.
 """
 import ctypes
 import os
@@ -233,14 +233,14 @@ def _expected_nbc(n, kind, is_max, what):
     return _expected(n, kind, is_max, what, lambda w: 1)     # libnbc scan / exscan: linear == coll/basic
 
 
-def _check_nb(n, got, gpu):
+def _check_nb(n, got):
     import golden_io
     import mxompi
     for kind in ("int", "flt"):
         for is_max in ((False,) if kind == "int" else (False, True)):
             for what in ("allreduce", "reduce", "scan", "exscan", "rsb", "pallreduce"):
                 base = "allreduce" if what == "pallreduce" else what
-                exp = _expected_nbc(n, kind, is_max, base) if gpu else _expected(n, kind, is_max, base, lambda w: 1)
+                exp = _expected_nbc(n, kind, is_max, base)
                 key = (what if what == "pallreduce" else "i" + what, kind, is_max)
                 items = exp.items() if isinstance(exp, dict) else enumerate(exp)
                 for r, e in items:
@@ -276,35 +276,41 @@ def test_multirank_host_buffers_gloo_cpu(n):
     got = _run(n, use_gpu=False)
     import torch
     if not torch.cuda.is_available():
-        assert set(got[0]["owners"].values()) == {"base"}, got[0]["owners"]
-    # the host base module runs the linear orders: allreduce / reduce basic
-    # linear (rbuf = x_{n-1}; op= x_i), linear scan / exscan, RSB = linear
-    # reduce + scatter: bit-identical to the oracle's linear algorithms
-    _check(n, got, lambda w: 1, bitexact_fp=True)
-    _check_nb(n, got, gpu=False)
+        assert set(got[0]["owners"].values()) == {"tuned", "basic", "libnbc"}, got[0]["owners"]
+        assert got[0]["owners"]["allreduce"] == "tuned" and got[0]["owners"]["scan"] == "basic"
+    # coll/tuned's fixed decisions (allreduce, reduce, RSB = coll_reduce +
+    # scatter), coll/basic's linear scan / exscan, coll/libnbc's orders for
+    # the nonblocking forms: bit-identical to the oracle
+    _check(n, got, lambda w: 0, bitexact_fp=True)
+    _check_nb(n, got)
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("path", ["default", "zero_copy"])
+@pytest.mark.parametrize("path", ["host_copies", "device", "zero_copy"])
 @pytest.mark.parametrize("n", [2, 3])
 def test_multirank_device_buffers_through_components(n, path, monkeypatch):
-    """Every slot through coll/mi355x on device buffers; `zero_copy` lowers
-    coll_mi355x_reg_min_kb to 1 KiB so the blocking reductions, allgather and
-    bcast of this job run between the ranks' registered buffers."""
+    """Every slot through coll/mi355x on device buffers.  `host_copies`: the
+    job's 20 KB calls are at or below coll_mi355x_host_max_kb (64), so they
+    run on the saved host modules through host copies of the device buffers
+    (coll/cuda's direction); `device` sets the threshold to 0, so they run on
+    the device; `zero_copy` also lowers coll_mi355x_reg_min_kb to 1 KiB so the
+    blocking reductions, allgather and bcast run between the ranks'
+    registered buffers.  Same results on every path."""
     import torch
     if not torch.cuda.is_available():
         pytest.skip("needs a GPU")
     os.environ["HSA_ENABLE_IPC_MODE_LEGACY"] = "0"
+    if path != "host_copies":
+        monkeypatch.setenv("OMPI_MCA_coll_mi355x_host_max_kb", "0")
     if path == "zero_copy":
         monkeypatch.setenv("OMPI_MCA_coll_mi355x_reg_min_kb", "1")
     got = _run(n, use_gpu=True)
     assert all(v == "mi355x" for v in got[0]["owners"].values()), got[0]["owners"]
-    import mxompi
 
     def alg_of(what):
         return 0       # coll/tuned fixed decisions (the oracle's alg 0)
     _check(n, got, alg_of, bitexact_fp=True)
-    _check_nb(n, got, gpu=True)
+    _check_nb(n, got)
 
 
 # ---------------------------------------------------------------------------
@@ -449,12 +455,15 @@ def _run_fn(fn, n):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("path", ["host_copies", "device"])
 @pytest.mark.parametrize("n", [2, 3])
-def test_mixed_host_and_device_buffers_take_one_protocol(n):
+def test_mixed_host_and_device_buffers_take_one_protocol(n, path, monkeypatch):
     import torch
     if not torch.cuda.is_available():
         pytest.skip("needs a GPU")
     os.environ["HSA_ENABLE_IPC_MODE_LEGACY"] = "0"
+    if path == "device":
+        monkeypatch.setenv("OMPI_MCA_coll_mi355x_host_max_kb", "0")
     got = _run_fn(_mixed_worker, n)
     assert got[0]["owners"] == {"allreduce": "mi355x", "allgather": "mi355x", "bcast": "mi355x"}
     import golden_io
@@ -550,12 +559,18 @@ def _noncontig_worker(rank, n, port, q):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("desc", [True, False], ids=["device_convertor", "host_convertor"])
-def test_noncontiguous_device_buffers(desc):
+@pytest.mark.parametrize("desc", [True, False, None], ids=["device_convertor", "host_convertor", "host_copies"])
+def test_noncontiguous_device_buffers(desc, monkeypatch):
+    """device_convertor / host_convertor: the device path (threshold 0) with
+    the layouts packed on the device or through the host convertor;
+    host_copies: the saved host module on host copies of the spans."""
     import torch
     if not torch.cuda.is_available():
         pytest.skip("needs a GPU")
     os.environ["HSA_ENABLE_IPC_MODE_LEGACY"] = "0"
+    if desc is not None:
+        monkeypatch.setenv("OMPI_MCA_coll_mi355x_host_max_kb", "0")
+    desc = bool(desc)
     if desc:
         os.environ.pop("MXH_NO_DTYPE_DESC", None)
     else:
@@ -687,6 +702,7 @@ def _dup_worker(rank, n, port, q):
         import mxompi
         os.environ["OMPI_MCA_coll_mi355x_wait_timeout"] = "60"
         os.environ["OMPI_MCA_coll_mi355x_staging_mb"] = "64"
+        os.environ["OMPI_MCA_coll_mi355x_host_max_kb"] = "0"     # the 4 KB calls on the device
         dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=n)
 
         @minihost.AG

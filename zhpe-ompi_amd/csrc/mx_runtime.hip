@@ -172,6 +172,19 @@ extern "C" int mx_free(void *p) {
   return mx_hip_rc(hipFree(p));
 }
 
+extern "C" int mx_host_alloc(size_t bytes, void **p) {
+  if (!p) return MX_ERR_ARG;
+  *p = nullptr;
+  if (!bytes) return MX_SUCCESS;
+  if (int rc = mx_ensure_init()) return rc;
+  return hipHostMalloc(p, bytes, hipHostMallocDefault) == hipSuccess ? MX_SUCCESS : MX_ERR_NOMEM;
+}
+
+extern "C" int mx_host_free(void *p) {
+  if (!p) return MX_SUCCESS;
+  return mx_hip_rc(hipHostFree(p));
+}
+
 extern "C" int mx_memcpy(void *dst, const void *src, size_t bytes, void *stream) {
   if (!bytes) return MX_SUCCESS;
   if (!dst || !src) return MX_ERR_ARG;

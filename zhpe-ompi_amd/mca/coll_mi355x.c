@@ -27,6 +27,23 @@
  * a non-contiguous layout) stages it through device scratch; device buffers
  * are used in place.
  *
+ * Size split and order (round 3).  A call of at most coll_mi355x_host_max_kb
+ * (default 64 KiB: count x type size, the same on every rank) runs on the
+ * saved host module -- device buffers are copied to host memory around it,
+ * coll/cuda's direction (coll_cuda_allreduce.c:30-73) -- so a host-only
+ * program never touches the GPU and small device calls get the host's
+ * latency.  Larger calls run on the device with the reduction order of the
+ * module they replaced: coll/tuned's fixed decision, or its forced algorithm
+ * / rules file when coll_tuned_use_dynamic_rules is set
+ * (coll_mi355x_rules.c); coll/basic's compositions (allreduce = coll_reduce
+ * to 0 + coll_bcast, coll_basic_allreduce.c:45-71; linear reduce up to
+ * coll_basic_crossover ranks; recursive-halving reduce_scatter below 8 MiB,
+ * coll_basic_reduce_scatter.c:107-108).  Whatever the device cannot
+ * reproduce bit for bit (an unknown lower module, coll/basic's log-tree
+ * reduce, tuned's redscat_gather reduce, RSB algorithms 2-4) runs on the
+ * saved module the same way small calls do.  Intercommunicators are declined
+ * at query (coll_tuned_module.c:66-69).
+ *
  * The device work runs on a stream the module owns (non-blocking: a wait
  * for a late peer never stalls the process's legacy default stream, e.g. a
  * PML copy), ordered after the work already queued on the default stream.
@@ -56,10 +73,15 @@
 #include "mx_convertor.h"
 #include "mx_kernels.h"
 #include "mx_ompi_abi.h"
+#include "coll_mi355x_rules.h"
 
-/* device scratch a staged buffer lives in (grown on demand, kept) */
+/* device scratch a staged buffer lives in (grown on demand, kept); the
+ * pinned host copies of device buffers for the saved module likewise */
 typedef struct { void *p; size_t bytes; } mx_scratch_t;
 enum { SCR_IN, SCR_OUT, SCR_N };
+
+/* the module a saved slot came from: its reduction order */
+enum { LOW_TUNED = 1, LOW_BASIC, LOW_LIBNBC, LOW_OTHER };
 
 /* device convertor handles of the datatypes this communicator moved, keyed
  * by the datatype AND a copy of its committed records (a freed datatype's
@@ -82,6 +104,13 @@ typedef struct {
     void *stream;         /* blocking collectives: module-owned stream ordered with the default one */
     void *nb_stream;      /* nonblocking / persistent requests: non-blocking stream */
     mx_scratch_t scratch[SCR_N];
+    mx_scratch_t hbuf[SCR_N];   /* pinned host copies for the saved module */
+    /* order of the saved reduction slots, coll/tuned's configuration, the
+     * size split */
+    int low_allreduce, low_reduce_scatter, low_reduce, low_rsb, low_scan, low_exscan, low_nbc;
+    int basic_crossover;
+    size_t host_max;
+    mx_tuned_cfg_t tuned;
     mx_ddt_slot_t ddt[MX_DDT_CACHE];
     unsigned long ddt_clock;
     /* delegation targets (the slots we replaced) */
@@ -144,7 +173,10 @@ static int map_rc(int rc)
 static void coll_module_destruct(mx_coll_module_t *m)
 {
     if (m->mx) mx_comm_destroy(m->mx);
-    for (int k = 0; k < SCR_N; k++) mx_free(m->scratch[k].p);
+    for (int k = 0; k < SCR_N; k++) {
+        mx_free(m->scratch[k].p);
+        mx_host_free(m->hbuf[k].p);
+    }
     for (int k = 0; k < MX_DDT_CACHE; k++) {
         if (m->ddt[k].h) mx_ddt_destroy(m->ddt[k].h);
         free(m->ddt[k].recs);
@@ -198,12 +230,15 @@ static int comm_ready(mx_coll_module_t *m)
          * zero-copy from coll_mi355x_reg_min_kb per rank (0 = off; the
          * communicator declines it collectively when /dev/shm is missing),
          * staged protocol 0 auto / 1 push / 2 pull */
-        const int kb = mx_ompi_host->mca_int("coll_mi355x_reg_min_kb", 256);
-        (void)mx_comm_set_reg_min(m->mx, kb > 0 ? (size_t)kb << 10 : 0);
+        const int kb = mx_ompi_host->mca_int("coll_mi355x_reg_min_kb", -1);
+        (void)mx_comm_set_reg_min(m->mx, kb > 0 ? (size_t)kb << 10 : kb < 0 ? (size_t)256 << 10 : 0);
         const int proto = mx_ompi_host->mca_int("coll_mi355x_protocol", MX_PROTO_AUTO);
         if (mx_comm_set_protocol(m->mx, proto) < 0) rc = MX_ERR_ARG;
-        /* data-movement autotuning of large allreduces (on by default) */
-        if (!mx_ompi_host->mca_int("coll_mi355x_autotune", 1)) (void)mx_comm_set_autotune(m->mx, 0);
+        /* data-movement autotuning of large allreduces (on by default); a
+         * data path forced through MCA (protocol, registration threshold)
+         * switches it off, as the environment overrides do */
+        if (!mx_ompi_host->mca_int("coll_mi355x_autotune", 1) || proto != MX_PROTO_AUTO || kb >= 0)
+            (void)mx_comm_set_autotune(m->mx, 0);
     }
     /* the streams are process-local: a failure here is reported by the calls
      * (or falls back to the default stream), never turned into a different
@@ -305,18 +340,22 @@ static int xfer_packed(mx_coll_module_t *m, const xbuf_t *x, void *packed_dev, i
 {
     ptrdiff_t lo = 0, hi = 0;
     const int on_dev = mx_is_device_ptr(x->user) == 1;
+    /* the packed length follows x->count: a staged rbuf that held the whole
+     * input vector (MPI_IN_PLACE reduce_scatter) is copied back as its own
+     * block only */
+    const size_t len = (size_t)x->count * mx_ompi_host->dtype_size(x->dt);
     if (on_dev) {
         mx_ddt_t *h = ddt_for(m, x->dt);
         if (h) {
-            int rc = to_device ? mx_pack(h, (size_t)x->count, x->user, packed_dev, 0, x->bytes, m->stream)
-                               : mx_unpack(h, (size_t)x->count, x->user, packed_dev, 0, x->bytes, m->stream);
+            int rc = to_device ? mx_pack(h, (size_t)x->count, x->user, packed_dev, 0, len, m->stream)
+                               : mx_unpack(h, (size_t)x->count, x->user, packed_dev, 0, len, m->stream);
             return rc ? rc : stream_wait(m->stream);
         }
     }
     if (!mx_ompi_host->dtype_pack || !mx_ompi_host->dtype_unpack || !mx_ompi_host->dtype_span ||
         mx_ompi_host->dtype_span(x->dt, x->count, &lo, &hi) != OMPI_SUCCESS || hi < lo)
         return MX_ERR_UNSUPPORTED;
-    char *span = NULL, *packed = malloc(x->bytes ? x->bytes : 1);
+    char *span = NULL, *packed = malloc(len ? len : 1);
     char *user = (char *)x->user;
     int rc = packed ? MX_SUCCESS : MX_ERR_NOMEM;
     if (!rc && on_dev) {   /* the convertor walks host memory: bring the span over */
@@ -327,10 +366,10 @@ static int xfer_packed(mx_coll_module_t *m, const xbuf_t *x, void *packed_dev, i
     }
     if (!rc && to_device) {
         if (mx_ompi_host->dtype_pack(x->dt, x->count, user, packed) != OMPI_SUCCESS) rc = MX_ERR_ARG;
-        if (!rc) rc = mx_memcpy(packed_dev, packed, x->bytes, m->stream);
+        if (!rc) rc = mx_memcpy(packed_dev, packed, len, m->stream);
         if (!rc) rc = stream_wait(m->stream);
     } else if (!rc) {
-        if (!(rc = mx_memcpy(packed, packed_dev, x->bytes, m->stream))) rc = stream_wait(m->stream);
+        if (!(rc = mx_memcpy(packed, packed_dev, len, m->stream))) rc = stream_wait(m->stream);
         if (!rc && mx_ompi_host->dtype_unpack(x->dt, x->count, packed, user) != OMPI_SUCCESS) rc = MX_ERR_ARG;
         if (!rc && on_dev && !(rc = mx_memcpy((char *)x->user + lo, span, (size_t)(hi - lo), m->stream)))
             rc = stream_wait(m->stream);
@@ -397,16 +436,256 @@ static int reducible(struct ompi_datatype_t *dtype, struct ompi_op_t *op, size_t
            mx_op_supported(*opi, *slot, MX_TABLE_WITH_FORTRAN);
 }
 
+/* ---- the saved module on host copies (coll/cuda's direction) -----------
+ * A call the device does not take runs on the saved lower module.  That
+ * module walks host memory, so a device buffer is copied to a host buffer
+ * over its whole span (coll_cuda_allreduce.c:41-61 does the same with
+ * opal_datatype_span) and an output is copied back after the call. */
+typedef struct {
+    void *user;        /* the caller's device buffer (NULL: used directly) */
+    char *copy;        /* host copy of its span                            */
+    ptrdiff_t lo;      /* span start relative to the buffer                */
+    size_t span;
+    int owned;         /* malloc'd (requests) vs the module's pinned buffer */
+} hview_t;
+
+static int ensure_stream(mx_coll_module_t *m)
+{
+    if (!m->stream && mx_stream_create_ordered(&m->stream) != MX_SUCCESS) m->stream = NULL;
+    return MX_SUCCESS;
+}
+
+static int hbuf(mx_coll_module_t *m, int k, size_t bytes, void **p)
+{
+    mx_scratch_t *s = &m->hbuf[k];
+    if (s->bytes < bytes) {
+        mx_host_free(s->p);
+        s->p = NULL;
+        s->bytes = 0;
+        const size_t want = bytes < ((size_t)64 << 10) ? ((size_t)64 << 10) : bytes;
+        if (mx_host_alloc(want, &s->p) != MX_SUCCESS) return MX_ERR_NOMEM;
+        s->bytes = want;
+    }
+    *p = s->p;
+    return MX_SUCCESS;
+}
+
+/* The buffer the saved module gets for `user` (count x dt): the buffer itself
+ * when it is host memory (or MPI_IN_PLACE / NULL), else a host copy of its
+ * span -- module pinned buffer k, or malloc'd when k < 0 (a request's own) --
+ * filled from the device when copy_in. */
+static int hview_in(mx_coll_module_t *m, int k, const void *user, struct ompi_datatype_t *dt, size_t count,
+                    int copy_in, hview_t *v, void **out)
+{
+    ptrdiff_t lo = 0, hi = (ptrdiff_t)(count * mx_ompi_host->dtype_size(dt));
+    memset(v, 0, sizeof *v);
+    *out = (void *)user;
+    if (!user || user == MPI_IN_PLACE || !count || mx_is_device_ptr(user) != 1) return MX_SUCCESS;
+    if (mx_ompi_host->dtype_span && mx_ompi_host->dtype_span(dt, (int)count, &lo, &hi) != OMPI_SUCCESS)
+        return MX_ERR_UNSUPPORTED;
+    if (hi < lo) return MX_ERR_UNSUPPORTED;
+    v->span = (size_t)(hi - lo);
+    void *p = NULL;
+    if (k >= 0) {
+        if (hbuf(m, k, v->span ? v->span : 1, &p)) return MX_ERR_NOMEM;
+    } else if (!(p = malloc(v->span ? v->span : 1))) {
+        return MX_ERR_NOMEM;
+    }
+    v->copy = p;
+    v->owned = k < 0;
+    v->user = (void *)user;
+    v->lo = lo;
+    *out = v->copy - lo;
+    if (!copy_in || !v->span) return MX_SUCCESS;
+    ensure_stream(m);
+    int rc = mx_memcpy(v->copy, (const char *)user + lo, v->span, m->stream);
+    return rc ? rc : stream_wait(m->stream);
+}
+
+/* the host copy of an output back into the caller's device buffer */
+static int hview_out(mx_coll_module_t *m, const hview_t *v)
+{
+    if (!v->user || !v->span) return MX_SUCCESS;
+    ensure_stream(m);
+    int rc = mx_memcpy((char *)v->user + v->lo, v->copy, v->span, m->stream);
+    return rc ? rc : stream_wait(m->stream);
+}
+
+static void hview_release(hview_t *v)
+{
+    if (v->owned) free(v->copy);
+    v->copy = NULL;
+    v->user = NULL;
+}
+
+/* the output view: copied in when the call reads it (MPI_IN_PLACE) or when
+ * the copy-back must keep the bytes between its elements */
+static int hview_out_in(mx_coll_module_t *m, int k, void *user, struct ompi_datatype_t *dt, size_t count,
+                        int reads, hview_t *v, void **out)
+{
+    const int keep = reads || !mx_ompi_host->dtype_contiguous(dt, count > INT_MAX ? INT_MAX : (int)count);
+    return hview_in(m, k, user, dt, count, keep, v, out);
+}
+
+/* ---- which reduction order the device must reproduce ---------------------
+ * Each saved reduction slot is classified by its module's OPAL class name
+ * (opal_object_t.obj_class->cls_name, OBJ_CLASS_INSTANCE in
+ * coll_tuned_component.c:291, coll_basic_component.c:109,
+ * coll_libnbc_component.c:504). */
+static int low_kind(mca_coll_base_module_t *pm)
+{
+    const opal_object_t *o = (const opal_object_t *)pm;
+    const char *nm = (o && o->obj_class) ? o->obj_class->cls_name : NULL;
+    if (!nm) return LOW_OTHER;
+    if (!strcmp(nm, "mca_coll_tuned_module_t")) return LOW_TUNED;
+    if (!strcmp(nm, "mca_coll_basic_module_t")) return LOW_BASIC;
+    if (!strcmp(nm, "ompi_coll_libnbc_module_t")) return LOW_LIBNBC;
+    return LOW_OTHER;
+}
+
+static int comm_n(mx_coll_module_t *m) { return mx_ompi_host->comm_size(m->comm); }
+
+/* The reduce word (MX_ALG_WORD: algorithm | chain fanout << 16) that this
+ * communicator's coll_reduce -- this module's own reduce slot, i.e. the
+ * saved module's order -- runs for count x es bytes; -1 when the device
+ * cannot reproduce it. */
+static int reduce_rule(mx_coll_module_t *m, size_t count, size_t es)
+{
+    switch (m->low_reduce) {
+    case LOW_TUNED: {
+        int fan;
+        const int a = mx_tuned_choice(&m->tuned, MX_CT_REDUCE, count * es, &fan);
+        if (a < 0 || a > MX_REDUCE_IN_ORDER_BINARY) return -1;   /* 7 redscat_gather: saved module */
+        return a | ((a == MX_REDUCE_CHAIN && fan > 0 && fan < 256) ? fan << 16 : 0);
+    }
+    case LOW_BASIC:
+        /* coll_basic_module.c:92-128: linear reduce up to coll_basic_crossover
+         * ranks, the log-tree reduce above (not on the device) */
+        return comm_n(m) <= m->basic_crossover ? MX_REDUCE_LINEAR : -1;
+    default:
+        return -1;
+    }
+}
+
+static int nonoverlapping_word(int alg, int rw)
+{
+    return rw < 0 ? -1 : MX_ALG_WORD(alg, rw & 0xff, (rw >> 16) & 0xff);
+}
+
+/* the allreduce algorithm word, -1 = the saved module */
+static int allreduce_rule(mx_coll_module_t *m, size_t count, size_t es, int slot)
+{
+    const int forced = mx_ompi_host->mca_int("coll_mi355x_allreduce_algorithm", MX_ALLREDUCE_AUTO);
+    if (forced) return forced;   /* an explicit device algorithm (not the lower module's) */
+    switch (m->low_allreduce) {
+    case LOW_TUNED: {
+        int fan;
+        int a = mx_tuned_choice(&m->tuned, MX_CT_ALLREDUCE, count * es, &fan);
+        if (a == 0 && mx_allreduce_decision(comm_n(m), count, slot) == MX_ALLREDUCE_NONOVERLAPPING)
+            a = MX_ALLREDUCE_NONOVERLAPPING;
+        if (a == MX_ALLREDUCE_NONOVERLAPPING) return nonoverlapping_word(a, reduce_rule(m, count, es));
+        return (a >= 0 && a <= MX_ALLREDUCE_RABENSEIFNER) ? a : -1;
+    }
+    case LOW_BASIC:   /* coll_reduce to 0 + coll_bcast (coll_basic_allreduce.c:45-71) */
+        return nonoverlapping_word(MX_ALLREDUCE_NONOVERLAPPING, reduce_rule(m, count, es));
+    default:
+        return -1;
+    }
+}
+
+/* the reduce_scatter algorithm word for `total` elements, -1 = saved module */
+static int reduce_scatter_rule(mx_coll_module_t *m, size_t total, size_t es, int inplace)
+{
+    const int forced = mx_ompi_host->mca_int("coll_mi355x_reduce_scatter_algorithm", MX_RS_AUTO);
+    if (forced) return forced;
+    switch (m->low_reduce_scatter) {
+    case LOW_TUNED: {
+        int fan;
+        const int a = mx_tuned_choice(&m->tuned, MX_CT_REDUCESCATTER, total * es, &fan);
+        if (a == MX_RS_NONOVERLAPPING) return nonoverlapping_word(a, reduce_rule(m, total, es));
+        return (a >= 0 && a <= MX_RS_BUTTERFLY) ? a : -1;
+    }
+    case LOW_BASIC:
+        /* coll_basic_reduce_scatter.c:107-108: recursive halving below
+         * COMMUTATIVE_LONG_MSG (8 MiB), else coll_reduce (sbuf = rbuf when in
+         * place, so the root never reduces in place) + scatterv */
+        if (total * es < ((size_t)8 << 20)) return MX_RS_RECURSIVE_HALVING;
+        return inplace ? -1 : nonoverlapping_word(MX_RS_NONOVERLAPPING, reduce_rule(m, total, es));
+    default:
+        return -1;
+    }
+}
+
+/* reduce_scatter_block: basic_linear (tuned fixed, coll_tuned_decision_fixed.c:
+ * 522-532; coll/basic, coll_basic_reduce_scatter_block.c:60) = coll_reduce
+ * to 0 + scatter; the reduce word, -1 = saved module */
+static int rsb_rule(mx_coll_module_t *m, size_t total, size_t es)
+{
+    const int forced = mx_ompi_host->mca_int("coll_mi355x_reduce_algorithm", MX_REDUCE_AUTO);
+    if (forced) return forced;
+    switch (m->low_rsb) {
+    case LOW_TUNED: {
+        int fan;
+        const int a = mx_tuned_choice(&m->tuned, MX_CT_REDUCESCATTERBLOCK, total * es, &fan);
+        return (a == 0 || a == 1) ? reduce_rule(m, total, es) : -1;   /* 2-4: saved module */
+    }
+    case LOW_BASIC:
+        return reduce_rule(m, total, es);
+    default:
+        return -1;
+    }
+}
+
+/* scan / exscan: MX_SCAN_*, -1 = saved module.  coll/tuned owns these slots
+ * only with dynamic rules that name them (coll_tuned_module.c:235-238);
+ * coll/basic's are linear (coll_basic_scan.c:43-50, coll_basic_exscan.c:45-52). */
+static int scan_rule(mx_coll_module_t *m, size_t es, int exclusive)
+{
+    const int forced = mx_ompi_host->mca_int(exclusive ? "coll_mi355x_exscan_algorithm" : "coll_mi355x_scan_algorithm",
+                                             MX_SCAN_AUTO);
+    if (forced) return forced;
+    switch (exclusive ? m->low_exscan : m->low_scan) {
+    case LOW_TUNED: {
+        int fan;
+        const int a = mx_tuned_choice(&m->tuned, exclusive ? MX_CT_EXSCAN : MX_CT_SCAN, es * comm_n(m), &fan);
+        return (a == 0 || a == 1) ? MX_SCAN_LINEAR : a == 2 ? MX_SCAN_RECURSIVE_DOUBLING : -1;
+    }
+    case LOW_BASIC:
+        return MX_SCAN_LINEAR;
+    default:
+        return -1;
+    }
+}
+
+/* a call of `bytes` (the same on every rank) for the device */
+static int big(mx_coll_module_t *m, size_t bytes) { return bytes > m->host_max; }
+
 /* ---- blocking slots -------------------------------------------------------- */
+
+/* Blocking calls on the saved module, device buffers through host copies
+ * (pinned buffers SCR_IN / SCR_OUT of the module). */
+static int host_allreduce(mx_coll_module_t *m, const void *sbuf, void *rbuf, int count, struct ompi_datatype_t *dt,
+                          struct ompi_op_t *op)
+{
+    hview_t s, r;
+    void *hs, *hr;
+    int rc = hview_in(m, SCR_IN, sbuf, dt, (size_t)count, 1, &s, &hs);
+    if (!rc) rc = hview_out_in(m, SCR_OUT, rbuf, dt, (size_t)count, sbuf == MPI_IN_PLACE, &r, &hr);
+    if (rc) return map_rc(rc);
+    int ret = m->prev_allreduce(hs, hr, count, dt, op, m->comm, m->prev_allreduce_module);
+    if (ret == OMPI_SUCCESS) ret = map_rc(hview_out(m, &r));
+    return ret;
+}
 
 static int mx_coll_allreduce(const void *sbuf, void *rbuf, int count, struct ompi_datatype_t *dtype,
                              struct ompi_op_t *op, struct ompi_communicator_t *comm, mca_coll_base_module_t *module)
 {
     mx_coll_module_t *m = (mx_coll_module_t *)module;
     const int n = mx_ompi_host->comm_size(comm);
-    int slot, opi;
-    if (reducible(dtype, op, (size_t)count, n, &slot, &opi) && comm_ready(m)) {
-        const int alg = mx_ompi_host->mca_int("coll_mi355x_allreduce_algorithm", MX_ALLREDUCE_AUTO);
+    const size_t es = mx_ompi_host->dtype_size(dtype);
+    int slot, opi, alg;
+    if (reducible(dtype, op, (size_t)count, n, &slot, &opi) && big(m, (size_t)count * es) &&
+        (alg = allreduce_rule(m, (size_t)count, es, slot)) >= 0 && comm_ready(m)) {
         const int inplace = sbuf == MPI_IN_PLACE;
         xbuf_t s, r;
         int rc = begin(m);
@@ -416,7 +695,23 @@ static int mx_coll_allreduce(const void *sbuf, void *rbuf, int count, struct omp
         if (!rc) rc = xout(m, &r, r.bytes);
         return map_rc(rc);
     }
-    return m->prev_allreduce(sbuf, rbuf, count, dtype, op, comm, m->prev_allreduce_module);
+    return host_allreduce(m, sbuf, rbuf, count, dtype, op);
+}
+
+static int host_reduce_scatter(mx_coll_module_t *m, const void *sbuf, void *rbuf, const int *rcounts, size_t total,
+                               struct ompi_datatype_t *dt, struct ompi_op_t *op)
+{
+    const int rank = mx_ompi_host->comm_rank(m->comm);
+    const int inplace = sbuf == MPI_IN_PLACE;
+    hview_t s, r;
+    void *hs, *hr;
+    int rc = hview_in(m, SCR_IN, sbuf, dt, total, 1, &s, &hs);
+    /* MPI_IN_PLACE: rbuf holds the whole input vector */
+    if (!rc) rc = hview_out_in(m, SCR_OUT, rbuf, dt, inplace ? total : (size_t)rcounts[rank], inplace, &r, &hr);
+    if (rc) return map_rc(rc);
+    int ret = m->prev_reduce_scatter(hs, hr, rcounts, dt, op, m->comm, m->prev_reduce_scatter_module);
+    if (ret == OMPI_SUCCESS) ret = map_rc(hview_out(m, &r));
+    return ret;
 }
 
 static int mx_coll_reduce_scatter(const void *sbuf, void *rbuf, const int *rcounts, struct ompi_datatype_t *dtype,
@@ -425,12 +720,16 @@ static int mx_coll_reduce_scatter(const void *sbuf, void *rbuf, const int *rcoun
 {
     mx_coll_module_t *m = (mx_coll_module_t *)module;
     const int n = mx_ompi_host->comm_size(comm), rank = mx_ompi_host->comm_rank(comm);
+    const size_t es = mx_ompi_host->dtype_size(dtype);
     size_t rc64[MX_MAX_RANKS], total = 0;
-    int slot, opi;
-    for (int i = 0; i < n && i < MX_MAX_RANKS; i++) { rc64[i] = (size_t)rcounts[i]; total += rc64[i]; }
-    if (reducible(dtype, op, total, n, &slot, &opi) && comm_ready(m)) {
-        const int alg = mx_ompi_host->mca_int("coll_mi355x_reduce_scatter_algorithm", MX_RS_AUTO);
-        const int inplace = sbuf == MPI_IN_PLACE;
+    int slot, opi, alg;
+    for (int i = 0; i < n; i++) {
+        if (i < MX_MAX_RANKS) rc64[i] = (size_t)rcounts[i];
+        total += (size_t)rcounts[i];
+    }
+    const int inplace = sbuf == MPI_IN_PLACE;
+    if (reducible(dtype, op, total, n, &slot, &opi) && big(m, total * es) &&
+        (alg = reduce_scatter_rule(m, total, es, inplace)) >= 0 && comm_ready(m)) {
         xbuf_t s, r;
         int rc = begin(m);
         if (!rc && !inplace) rc = xin(m, SCR_IN, sbuf, dtype, total, 1, &s);
@@ -439,11 +738,26 @@ static int mx_coll_reduce_scatter(const void *sbuf, void *rbuf, const int *rcoun
         if (!rc) rc = mx_reduce_scatter(m->mx, inplace ? MX_IN_PLACE : s.dev, r.dev, rc64, slot, opi, alg, m->stream);
         if (!rc) {
             r.count = rcounts[rank];
-            rc = xout(m, &r, rc64[rank] * mx_ompi_host->dtype_size(dtype));
+            r.bytes = rc64[rank] * es;
+            rc = xout(m, &r, r.bytes);
         }
         return map_rc(rc);
     }
-    return m->prev_reduce_scatter(sbuf, rbuf, rcounts, dtype, op, comm, m->prev_reduce_scatter_module);
+    return host_reduce_scatter(m, sbuf, rbuf, rcounts, total, dtype, op);
+}
+
+static int host_allgather(mx_coll_module_t *m, const void *sbuf, int scount, struct ompi_datatype_t *sdtype,
+                          void *rbuf, int rcount, struct ompi_datatype_t *rdtype)
+{
+    const int n = mx_ompi_host->comm_size(m->comm);
+    hview_t s, r;
+    void *hs, *hr;
+    int rc = hview_in(m, SCR_IN, sbuf, sdtype, (size_t)scount, 1, &s, &hs);
+    if (!rc) rc = hview_out_in(m, SCR_OUT, rbuf, rdtype, (size_t)rcount * n, sbuf == MPI_IN_PLACE, &r, &hr);
+    if (rc) return map_rc(rc);
+    int ret = m->prev_allgather(hs, scount, sdtype, hr, rcount, rdtype, m->comm, m->prev_allgather_module);
+    if (ret == OMPI_SUCCESS) ret = map_rc(hview_out(m, &r));
+    return ret;
 }
 
 static int mx_coll_allgather(const void *sbuf, int scount, struct ompi_datatype_t *sdtype, void *rbuf, int rcount,
@@ -452,9 +766,10 @@ static int mx_coll_allgather(const void *sbuf, int scount, struct ompi_datatype_
 {
     mx_coll_module_t *m = (mx_coll_module_t *)module;
     const size_t rbytes = (size_t)rcount * mx_ompi_host->dtype_size(rdtype);
-    const int n = mx_ompi_host->comm_size(comm), rank = mx_ompi_host->comm_rank(comm);
-    /* (rcount, rdtype) is significant, and its signature equal, on every rank */
-    if (rbytes && n <= MX_MAX_RANKS && comm_ready(m)) {
+    const int n = mx_ompi_host->comm_size(comm);
+    /* (rcount, rdtype) is significant, and its signature equal, on every
+     * rank; pure data movement: any lower module gives the same bytes */
+    if (rbytes && n <= MX_MAX_RANKS && big(m, rbytes * n) && comm_ready(m)) {
         const int inplace = sbuf == MPI_IN_PLACE;
         xbuf_t s, r;
         int rc = begin(m);
@@ -464,10 +779,9 @@ static int mx_coll_allgather(const void *sbuf, int scount, struct ompi_datatype_
         if (!rc)
             rc = mx_allgather(m->mx, inplace ? MX_IN_PLACE : s.dev, r.dev, rbytes, m->stream);
         if (!rc) rc = xout(m, &r, r.bytes);
-        (void)rank;
         return map_rc(rc);
     }
-    return m->prev_allgather(sbuf, scount, sdtype, rbuf, rcount, rdtype, comm, m->prev_allgather_module);
+    return host_allgather(m, sbuf, scount, sdtype, rbuf, rcount, rdtype);
 }
 
 static int mx_coll_bcast(void *buf, int count, struct ompi_datatype_t *dtype, int root,
@@ -476,7 +790,7 @@ static int mx_coll_bcast(void *buf, int count, struct ompi_datatype_t *dtype, in
     mx_coll_module_t *m = (mx_coll_module_t *)module;
     const size_t bytes = (size_t)count * mx_ompi_host->dtype_size(dtype);
     const int n = mx_ompi_host->comm_size(comm), rank = mx_ompi_host->comm_rank(comm);
-    if (bytes && n <= MX_MAX_RANKS && comm_ready(m)) {
+    if (bytes && n <= MX_MAX_RANKS && big(m, bytes) && comm_ready(m)) {
         xbuf_t b;
         int rc = begin(m);
         if (!rc) rc = xin(m, SCR_OUT, buf, dtype, (size_t)count, rank == root, &b);
@@ -484,7 +798,13 @@ static int mx_coll_bcast(void *buf, int count, struct ompi_datatype_t *dtype, in
         if (!rc && rank != root) rc = xout(m, &b, bytes);
         return map_rc(rc);
     }
-    return m->prev_bcast(buf, count, dtype, root, comm, m->prev_bcast_module);
+    hview_t v;
+    void *h;
+    int rc = hview_out_in(m, SCR_OUT, buf, dtype, (size_t)count, rank == root, &v, &h);
+    if (rc) return map_rc(rc);
+    int ret = m->prev_bcast(h, count, dtype, root, comm, m->prev_bcast_module);
+    if (ret == OMPI_SUCCESS && rank != root) ret = map_rc(hview_out(m, &v));
+    return ret;
 }
 
 /* MPI_Reduce_local has no peers: the per-call buffer check is all it needs */
@@ -517,10 +837,14 @@ static int mx_coll_reduce(const void *sbuf, void *rbuf, int count, struct ompi_d
 {
     mx_coll_module_t *m = (mx_coll_module_t *)module;
     const int n = mx_ompi_host->comm_size(comm), rank = mx_ompi_host->comm_rank(comm);
-    int slot, opi;
-    if (reducible(dtype, op, (size_t)count, n, &slot, &opi) && comm_ready(m)) {
-        const int alg = mx_ompi_host->mca_int("coll_mi355x_reduce_algorithm", MX_REDUCE_AUTO);
-        const int inplace = sbuf == MPI_IN_PLACE && rank == root;   /* rbuf matters on the root only */
+    const size_t es = mx_ompi_host->dtype_size(dtype);
+    const int inplace = sbuf == MPI_IN_PLACE && rank == root;   /* rbuf matters on the root only */
+    int slot, opi, alg = -1;
+    if (reducible(dtype, op, (size_t)count, n, &slot, &opi) && big(m, (size_t)count * es)) {
+        alg = mx_ompi_host->mca_int("coll_mi355x_reduce_algorithm", MX_REDUCE_AUTO);
+        if (!alg) alg = reduce_rule(m, (size_t)count, es);
+    }
+    if (alg >= 0 && comm_ready(m)) {
         xbuf_t s, r;
         memset(&r, 0, sizeof r);
         int rc = begin(m);
@@ -532,7 +856,15 @@ static int mx_coll_reduce(const void *sbuf, void *rbuf, int count, struct ompi_d
         if (!rc && rank == root) rc = xout(m, &r, r.bytes);
         return map_rc(rc);
     }
-    return m->prev_reduce(sbuf, rbuf, count, dtype, op, root, comm, m->prev_reduce_module);
+    hview_t sv, rv;
+    void *hs, *hr = rbuf;
+    int rc = hview_in(m, SCR_IN, sbuf, dtype, (size_t)count, 1, &sv, &hs);
+    memset(&rv, 0, sizeof rv);
+    if (!rc && rank == root) rc = hview_out_in(m, SCR_OUT, rbuf, dtype, (size_t)count, inplace, &rv, &hr);
+    if (rc) return map_rc(rc);
+    int ret = m->prev_reduce(hs, hr, count, dtype, op, root, comm, m->prev_reduce_module);
+    if (ret == OMPI_SUCCESS && rank == root) ret = map_rc(hview_out(m, &rv));
+    return ret;
 }
 
 static int mx_coll_reduce_scatter_block(const void *sbuf, void *rbuf, int rcount, struct ompi_datatype_t *dtype,
@@ -541,11 +873,11 @@ static int mx_coll_reduce_scatter_block(const void *sbuf, void *rbuf, int rcount
 {
     mx_coll_module_t *m = (mx_coll_module_t *)module;
     const int n = mx_ompi_host->comm_size(comm);
-    const size_t total = (size_t)rcount * (size_t)n;
-    int slot, opi;
-    if (reducible(dtype, op, total, n, &slot, &opi) && comm_ready(m)) {
-        const int alg = mx_ompi_host->mca_int("coll_mi355x_reduce_algorithm", MX_REDUCE_AUTO);
-        const int inplace = sbuf == MPI_IN_PLACE;
+    const size_t total = (size_t)rcount * (size_t)n, es = mx_ompi_host->dtype_size(dtype);
+    const int inplace = sbuf == MPI_IN_PLACE;
+    int slot, opi, alg;
+    if (reducible(dtype, op, total, n, &slot, &opi) && big(m, total * es) && (alg = rsb_rule(m, total, es)) >= 0 &&
+        comm_ready(m)) {
         xbuf_t s, r;
         int rc = begin(m);
         if (!rc && !inplace) rc = xin(m, SCR_IN, sbuf, dtype, total, 1, &s);
@@ -555,11 +887,19 @@ static int mx_coll_reduce_scatter_block(const void *sbuf, void *rbuf, int rcount
                                          m->stream);
         if (!rc) {
             r.count = rcount;
-            rc = xout(m, &r, (size_t)rcount * mx_ompi_host->dtype_size(dtype));
+            r.bytes = (size_t)rcount * es;
+            rc = xout(m, &r, r.bytes);
         }
         return map_rc(rc);
     }
-    return m->prev_reduce_scatter_block(sbuf, rbuf, rcount, dtype, op, comm, m->prev_reduce_scatter_block_module);
+    hview_t sv, rv;
+    void *hs, *hr;
+    int rc = hview_in(m, SCR_IN, sbuf, dtype, total, 1, &sv, &hs);
+    if (!rc) rc = hview_out_in(m, SCR_OUT, rbuf, dtype, inplace ? total : (size_t)rcount, inplace, &rv, &hr);
+    if (rc) return map_rc(rc);
+    int ret = m->prev_reduce_scatter_block(hs, hr, rcount, dtype, op, comm, m->prev_reduce_scatter_block_module);
+    if (ret == OMPI_SUCCESS) ret = map_rc(hview_out(m, &rv));
+    return ret;
 }
 
 /* returns 1 when the call should be delegated */
@@ -567,10 +907,11 @@ static int scan_common(mx_coll_module_t *m, const void *sbuf, void *rbuf, int co
                        struct ompi_op_t *op, int exclusive, int *ret)
 {
     const int n = mx_ompi_host->comm_size(m->comm);
-    int slot, opi;
-    if (!reducible(dtype, op, (size_t)count, n, &slot, &opi) || !comm_ready(m)) return 1;
-    const int alg = mx_ompi_host->mca_int(exclusive ? "coll_mi355x_exscan_algorithm" : "coll_mi355x_scan_algorithm",
-                                          MX_SCAN_AUTO);
+    const size_t es = mx_ompi_host->dtype_size(dtype);
+    int slot, opi, alg;
+    if (!reducible(dtype, op, (size_t)count, n, &slot, &opi) || !big(m, (size_t)count * es) ||
+        (alg = scan_rule(m, es, exclusive)) < 0 || !comm_ready(m))
+        return 1;
     const int inplace = sbuf == MPI_IN_PLACE;
     xbuf_t s, r;
     int rc = begin(m);
@@ -586,13 +927,29 @@ static int scan_common(mx_coll_module_t *m, const void *sbuf, void *rbuf, int co
     return 0;
 }
 
+static int host_scan(mx_coll_module_t *m, const void *sbuf, void *rbuf, int count, struct ompi_datatype_t *dtype,
+                     struct ompi_op_t *op, int exclusive)
+{
+    hview_t sv, rv;
+    void *hs, *hr;
+    int rc = hview_in(m, SCR_IN, sbuf, dtype, (size_t)count, 1, &sv, &hs);
+    /* exscan leaves rank 0's rbuf untouched: copy it in so the copy back keeps it */
+    if (!rc) rc = hview_out_in(m, SCR_OUT, rbuf, dtype, (size_t)count, sbuf == MPI_IN_PLACE || exclusive, &rv, &hr);
+    if (rc) return map_rc(rc);
+    int ret = exclusive ? m->prev_exscan(hs, hr, count, dtype, op, m->comm, m->prev_exscan_module)
+                        : m->prev_scan(hs, hr, count, dtype, op, m->comm, m->prev_scan_module);
+    if (ret == OMPI_SUCCESS) ret = map_rc(hview_out(m, &rv));
+    return ret;
+}
+
 static int mx_coll_scan(const void *sbuf, void *rbuf, int count, struct ompi_datatype_t *dtype,
                         struct ompi_op_t *op, struct ompi_communicator_t *comm, mca_coll_base_module_t *module)
 {
     mx_coll_module_t *m = (mx_coll_module_t *)module;
     int ret;
+    (void)comm;
     if (!scan_common(m, sbuf, rbuf, count, dtype, op, 0, &ret)) return ret;
-    return m->prev_scan(sbuf, rbuf, count, dtype, op, comm, m->prev_scan_module);
+    return host_scan(m, sbuf, rbuf, count, dtype, op, 0);
 }
 
 static int mx_coll_exscan(const void *sbuf, void *rbuf, int count, struct ompi_datatype_t *dtype,
@@ -600,8 +957,9 @@ static int mx_coll_exscan(const void *sbuf, void *rbuf, int count, struct ompi_d
 {
     mx_coll_module_t *m = (mx_coll_module_t *)module;
     int ret;
+    (void)comm;
     if (!scan_common(m, sbuf, rbuf, count, dtype, op, 1, &ret)) return ret;
-    return m->prev_exscan(sbuf, rbuf, count, dtype, op, comm, m->prev_exscan_module);
+    return host_scan(m, sbuf, rbuf, count, dtype, op, 1);
 }
 
 /* ---- nonblocking and persistent slots ------------------
@@ -623,6 +981,12 @@ typedef struct mx_coll_req {
     xbuf_t s, r;
     int s_in, r_in;
     size_t r_back;   /* bytes of r copied back */
+    /* a request of the saved module run on host copies of device buffers:
+     * hv[0] input, hv[1] output (copied in at every start when hv_in) */
+    struct ompi_request_t *inner;
+    hview_t hv[2];
+    int hv_in[2];
+    int persistent;
 } mx_coll_req_t;
 
 static mx_coll_req_t *g_active;
@@ -668,13 +1032,39 @@ static int req_fill(mx_coll_req_t *q)
     return rc;
 }
 
+/* completion of a host-path request: the output back to the device */
+static int hreq_complete(mx_coll_req_t *r, int status)
+{
+    if (status == OMPI_SUCCESS) status = map_rc(hview_out(r->m, &r->hv[1]));
+    if (!r->persistent && r->inner) mx_ompi_host->request_free(&r->inner);
+    return status;
+}
+
+static int g_in_progress;
 static int mx_coll_progress(void)
 {
     int completed = 0;
+    /* testing the saved module's requests must not re-enter (a host's
+     * request test may progress, and so call back here) */
+    if (g_in_progress) return 0;
+    g_in_progress = 1;
     mx_coll_req_t **pp = &g_active;
     while (*pp) {
         mx_coll_req_t *r = *pp;
-        int flag = 0;
+        int flag = 0, status = OMPI_SUCCESS;
+        if (r->inner) {
+            const int rc = mx_ompi_host->request_test(r->inner, &flag, &status);
+            if (rc != OMPI_SUCCESS) { flag = 1; status = rc; }
+            if (flag) {
+                *pp = r->next;
+                r->active = 0;
+                mx_ompi_host->request_complete(r->req, hreq_complete(r, status));
+                completed++;
+                continue;
+            }
+            pp = &r->next;
+            continue;
+        }
         int rc = mx_test(r->mx, &flag);
         if (flag || rc != MX_SUCCESS) {
             *pp = r->next;
@@ -686,6 +1076,7 @@ static int mx_coll_progress(void)
             pp = &r->next;
         }
     }
+    g_in_progress = 0;
     return completed;
 }
 
@@ -706,6 +1097,22 @@ static void deactivate(mx_coll_req_t *r)
 static int req_start_cb(struct ompi_request_t *req)     /* MPI_Start */
 {
     mx_coll_req_t *r = (mx_coll_req_t *)mx_ompi_host->request_ctx(req);
+    if (r->inner) {   /* host path: refresh the host copies, start the saved module's request */
+        int rc = MX_SUCCESS;
+        for (int i = 0; i < 2 && !rc; i++)
+            if (r->hv_in[i] && r->hv[i].user && r->hv[i].span) {
+                ensure_stream(r->m);
+                rc = mx_memcpy(r->hv[i].copy, (const char *)r->hv[i].user + r->hv[i].lo, r->hv[i].span,
+                               r->m->stream);
+                if (!rc) rc = stream_wait(r->m->stream);
+            }
+        if (rc) return map_rc(rc);
+        const int ret = mx_ompi_host->request_start(r->inner);
+        if (ret != OMPI_SUCCESS) return ret;
+        mx_ompi_host->request_activate(req);
+        activate(r);
+        return OMPI_SUCCESS;
+    }
     int rc = req_fill(r);
     if (!rc) rc = mx_start(r->mx);
     if (rc != MX_SUCCESS) return map_rc(rc);
@@ -718,11 +1125,93 @@ static int req_free_cb(struct ompi_request_t *req)      /* MPI_Request_free */
 {
     mx_coll_req_t *r = (mx_coll_req_t *)mx_ompi_host->request_ctx(req);
     if (r->active) deactivate(r);
-    const int rc = mx_request_free(r->mx);   /* lets an active operation finish */
+    int rc = MX_SUCCESS;
+    if (r->mx) rc = mx_request_free(r->mx);   /* lets an active operation finish */
+    if (r->inner) mx_ompi_host->request_free(&r->inner);
+    hview_release(&r->hv[0]);
+    hview_release(&r->hv[1]);
     req_release_staging(r);
     free(r);
     return map_rc(rc);
 }
+
+/* ---- nonblocking calls on the saved module ---------------------------------
+ * With host buffers the saved module's request is returned as is.  A device
+ * buffer is copied to a host buffer owned by a wrapper request: the saved
+ * module runs on the copy, the progress callback completes the wrapper
+ * (output copied back) when the inner request completes.  Persistent forms
+ * refresh the input copies at every MPI_Start. */
+static mx_coll_req_t *hreq_new(mx_coll_module_t *m, const void *sbuf, struct ompi_datatype_t *sdt, size_t scount,
+                               void *rbuf, struct ompi_datatype_t *rdt, size_t rcount, int r_reads, void **hs,
+                               void **hr, int *ret)
+{
+    mx_coll_req_t *r = calloc(1, sizeof *r);
+    int rc = r ? MX_SUCCESS : MX_ERR_NOMEM;
+    *hs = (void *)sbuf;
+    *hr = rbuf;
+    if (!rc && sbuf) {
+        rc = hview_in(m, -1, sbuf, sdt, scount, 1, &r->hv[0], hs);
+        r->hv_in[0] = 1;
+    }
+    if (!rc && rbuf) {
+        r->hv_in[1] = r_reads || !mx_ompi_host->dtype_contiguous(rdt, rcount > INT_MAX ? INT_MAX : (int)rcount);
+        rc = hview_in(m, -1, rbuf, rdt, rcount, r->hv_in[1], &r->hv[1], hr);
+    }
+    if (rc || !r || (!r->hv[0].user && !r->hv[1].user)) {   /* error, or host memory only: no wrapper */
+        if (r) { hview_release(&r->hv[0]); hview_release(&r->hv[1]); free(r); }
+        *ret = map_rc(rc);
+        return NULL;
+    }
+    r->m = m;
+    return r;
+}
+
+/* wraps the saved module's request `inner` (posted with status ret) */
+static int hreq_post(mx_coll_req_t *r, int ret, struct ompi_request_t *inner, int persistent,
+                     struct ompi_request_t **request)
+{
+    if (ret != OMPI_SUCCESS) {
+        hview_release(&r->hv[0]);
+        hview_release(&r->hv[1]);
+        free(r);
+        return ret;
+    }
+    r->inner = inner;
+    r->persistent = persistent;
+    r->req = mx_ompi_host->request_create(persistent, req_start_cb, req_free_cb, r);
+    if (!r->req) {
+        mx_ompi_host->request_free(&r->inner);
+        hview_release(&r->hv[0]);
+        hview_release(&r->hv[1]);
+        free(r);
+        return OMPI_ERR_OUT_OF_RESOURCE;
+    }
+    if (!g_progress_registered) {
+        mx_ompi_host->progress_register(mx_coll_progress);
+        g_progress_registered = 1;
+    }
+    if (!persistent) activate(r);
+    *request = r->req;
+    return OMPI_SUCCESS;
+}
+
+/* Delegation of one nonblocking / persistent slot: HCALL(hs, hr, req) is the
+ * saved module's call on the (possibly host-copied) buffers. */
+#define MX_HOST_NB(m, sbuf, sdt, scount, rbuf, rdt, rcount, r_reads, persistent, request, HCALL)               \
+    do {                                                                                                   \
+        void *hs_, *hr_;                                                                                   \
+        int ret_ = OMPI_SUCCESS;                                                                           \
+        mx_coll_req_t *w_ = hreq_new((m), (sbuf), (sdt), (scount), (rbuf), (rdt), (rcount), (r_reads), &hs_, \
+                                     &hr_, &ret_);                                                         \
+        if (!w_) {                                                                                         \
+            if (ret_ != OMPI_SUCCESS) return ret_;                                                         \
+            struct ompi_request_t **rq_ = (request);                                                       \
+            return HCALL(hs_, hr_, rq_);                                                                   \
+        }                                                                                                  \
+        struct ompi_request_t *in_ = NULL;                                                                 \
+        ret_ = HCALL(hs_, hr_, &in_);                                                                      \
+        return hreq_post(w_, ret_, in_, (persistent), (request));                                          \
+    } while (0)
 
 /* a request wrapper with its staged buffers (NULL on failure) */
 static mx_coll_req_t *req_new(mx_coll_module_t *m)
@@ -798,6 +1287,19 @@ static mx_coll_req_t *req_setup(mx_coll_module_t *m, const void *sbuf, size_t co
 }
 #define SB(r) ((r)->s.dev == MPI_IN_PLACE ? MX_IN_PLACE : (r)->s.dev)
 
+/* A nonblocking call takes the device only on a communicator whose device
+ * path already exists: creating it is a collective exchange, which a
+ * nonblocking call must not wait for (MPI-3.1 5.12; e.g. rank 0
+ * MPI_Iallreduce + MPI_Send while rank 1 MPI_Recv + MPI_Iallreduce).  It is
+ * created by the first eligible blocking collective (every rank issues the
+ * same collectives in the same order, so the state agrees on all ranks).
+ * Reductions also need the saved slot to be coll/libnbc, whose orders the
+ * device reproduces. */
+static int nb_device(mx_coll_module_t *m, size_t bytes, int reduction)
+{
+    return m->mx_state == 1 && big(m, bytes) && (!reduction || m->low_nbc == LOW_LIBNBC);
+}
+
 /* returns 1 when the call should be delegated */
 static int allreduce_like(mx_coll_module_t *m, const void *sbuf, void *rbuf, int count, struct ompi_datatype_t *dtype,
                           struct ompi_op_t *op, int persistent, struct ompi_request_t **request, int *ret)
@@ -805,8 +1307,8 @@ static int allreduce_like(mx_coll_module_t *m, const void *sbuf, void *rbuf, int
     const int n = mx_ompi_host->comm_size(m->comm);
     int slot, opi;
     mx_request_t *q = NULL;
-    if (!reducible(dtype, op, (size_t)count, n, &slot, &opi) || !comm_ready(m)) return 1;
     const size_t bytes = (size_t)count * mx_ompi_host->dtype_size(dtype);
+    if (!reducible(dtype, op, (size_t)count, n, &slot, &opi) || !nb_device(m, bytes, 1)) return 1;
     mx_coll_req_t *r = req_setup(m, sbuf, (size_t)count, dtype, rbuf, (size_t)count, dtype, sbuf == MPI_IN_PLACE,
                                  bytes, persistent, ret);
     if (!r) return 0;
@@ -824,7 +1326,9 @@ static int mx_coll_iallreduce(const void *sbuf, void *rbuf, int count, struct om
     mx_coll_module_t *m = (mx_coll_module_t *)module;
     int ret;
     if (!allreduce_like(m, sbuf, rbuf, count, dtype, op, 0, request, &ret)) return ret;
-    return m->prev_iallreduce(sbuf, rbuf, count, dtype, op, comm, request, m->prev_iallreduce_module);
+#define H(hs, hr, rq) m->prev_iallreduce(hs, hr, count, dtype, op, comm, rq, m->prev_iallreduce_module)
+    MX_HOST_NB(m, sbuf, dtype, (size_t)count, rbuf, dtype, (size_t)count, sbuf == MPI_IN_PLACE, 0, request, H);
+#undef H
 }
 
 static int mx_coll_allreduce_init(const void *sbuf, void *rbuf, int count, struct ompi_datatype_t *dtype,
@@ -834,8 +1338,9 @@ static int mx_coll_allreduce_init(const void *sbuf, void *rbuf, int count, struc
     mx_coll_module_t *m = (mx_coll_module_t *)module;
     int ret;
     if (!allreduce_like(m, sbuf, rbuf, count, dtype, op, 1, request, &ret)) return ret;
-    return m->prev_allreduce_init(sbuf, rbuf, count, dtype, op, comm, info, request,
-                                  m->prev_allreduce_init_module);
+#define H(hs, hr, rq) m->prev_allreduce_init(hs, hr, count, dtype, op, comm, info, rq, m->prev_allreduce_init_module)
+    MX_HOST_NB(m, sbuf, dtype, (size_t)count, rbuf, dtype, (size_t)count, sbuf == MPI_IN_PLACE, 1, request, H);
+#undef H
 }
 
 static int reduce_like(mx_coll_module_t *m, const void *sbuf, void *rbuf, int count, struct ompi_datatype_t *dtype,
@@ -845,9 +1350,9 @@ static int reduce_like(mx_coll_module_t *m, const void *sbuf, void *rbuf, int co
     const int n = mx_ompi_host->comm_size(comm), rank = mx_ompi_host->comm_rank(comm);
     int slot, opi;
     mx_request_t *q = NULL;
-    if (!reducible(dtype, op, (size_t)count, n, &slot, &opi) || !comm_ready(m)) return 1;
-    const int inplace = sbuf == MPI_IN_PLACE && rank == root;
     const size_t bytes = (size_t)count * mx_ompi_host->dtype_size(dtype);
+    if (!reducible(dtype, op, (size_t)count, n, &slot, &opi) || !nb_device(m, bytes, 1)) return 1;
+    const int inplace = sbuf == MPI_IN_PLACE && rank == root;
     mx_coll_req_t *r = req_setup(m, inplace ? MPI_IN_PLACE : sbuf, (size_t)count, dtype, rank == root ? rbuf : NULL,
                                  (size_t)count, dtype, inplace, bytes, persistent, ret);
     if (!r) return 0;
@@ -866,7 +1371,11 @@ static int mx_coll_ireduce(const void *sbuf, void *rbuf, int count, struct ompi_
     mx_coll_module_t *m = (mx_coll_module_t *)module;
     int ret;
     if (!reduce_like(m, sbuf, rbuf, count, dtype, op, root, comm, 0, request, &ret)) return ret;
-    return m->prev_ireduce(sbuf, rbuf, count, dtype, op, root, comm, request, m->prev_ireduce_module);
+    const int is_root = mx_ompi_host->comm_rank(comm) == root;
+#define H(hs, hr, rq) m->prev_ireduce(hs, hr, count, dtype, op, root, comm, rq, m->prev_ireduce_module)
+    MX_HOST_NB(m, sbuf, dtype, (size_t)count, is_root ? rbuf : NULL, dtype, (size_t)count, sbuf == MPI_IN_PLACE, 0,
+               request, H);
+#undef H
 }
 
 static int mx_coll_reduce_init(const void *sbuf, void *rbuf, int count, struct ompi_datatype_t *dtype,
@@ -877,7 +1386,11 @@ static int mx_coll_reduce_init(const void *sbuf, void *rbuf, int count, struct o
     mx_coll_module_t *m = (mx_coll_module_t *)module;
     int ret;
     if (!reduce_like(m, sbuf, rbuf, count, dtype, op, root, comm, 1, request, &ret)) return ret;
-    return m->prev_reduce_init(sbuf, rbuf, count, dtype, op, root, comm, info, request, m->prev_reduce_init_module);
+    const int is_root = mx_ompi_host->comm_rank(comm) == root;
+#define H(hs, hr, rq) m->prev_reduce_init(hs, hr, count, dtype, op, root, comm, info, rq, m->prev_reduce_init_module)
+    MX_HOST_NB(m, sbuf, dtype, (size_t)count, is_root ? rbuf : NULL, dtype, (size_t)count, sbuf == MPI_IN_PLACE, 1,
+               request, H);
+#undef H
 }
 
 /* rcounts == NULL: the _block form with `rcount` per rank */
@@ -891,9 +1404,9 @@ static int rs_like(mx_coll_module_t *m, const void *sbuf, void *rbuf, const int 
     mx_request_t *q = NULL;
     if (n > MX_MAX_RANKS) return 1;
     for (int i = 0; i < n; i++) { rc64[i] = (size_t)(rcounts ? rcounts[i] : rcount); total += rc64[i]; }
-    if (!reducible(dtype, op, total, n, &slot, &opi) || !comm_ready(m)) return 1;
-    const int inplace = sbuf == MPI_IN_PLACE;
     const size_t es = mx_ompi_host->dtype_size(dtype);
+    if (!reducible(dtype, op, total, n, &slot, &opi) || !nb_device(m, total * es, 1)) return 1;
+    const int inplace = sbuf == MPI_IN_PLACE;
     mx_coll_req_t *r = req_setup(m, sbuf, total, dtype, rbuf, inplace ? total : rc64[rank], dtype, inplace,
                                  rc64[rank] * es, persistent, ret);
     if (!r) return 0;
@@ -915,7 +1428,12 @@ static int mx_coll_ireduce_scatter(const void *sbuf, void *rbuf, const int *rcou
     mx_coll_module_t *m = (mx_coll_module_t *)module;
     int ret;
     if (!rs_like(m, sbuf, rbuf, rcounts, 0, dtype, op, comm, 0, request, &ret)) return ret;
-    return m->prev_ireduce_scatter(sbuf, rbuf, rcounts, dtype, op, comm, request, m->prev_ireduce_scatter_module);
+    size_t total = 0;
+    const int rank = mx_ompi_host->comm_rank(comm), inpl = sbuf == MPI_IN_PLACE;
+    for (int i = 0; i < mx_ompi_host->comm_size(comm); i++) total += (size_t)rcounts[i];
+#define H(hs, hr, rq) m->prev_ireduce_scatter(hs, hr, rcounts, dtype, op, comm, rq, m->prev_ireduce_scatter_module)
+    MX_HOST_NB(m, sbuf, dtype, total, rbuf, dtype, inpl ? total : (size_t)rcounts[rank], inpl, 0, request, H);
+#undef H
 }
 
 static int mx_coll_reduce_scatter_init(const void *sbuf, void *rbuf, const int *rcounts,
@@ -926,8 +1444,13 @@ static int mx_coll_reduce_scatter_init(const void *sbuf, void *rbuf, const int *
     mx_coll_module_t *m = (mx_coll_module_t *)module;
     int ret;
     if (!rs_like(m, sbuf, rbuf, rcounts, 0, dtype, op, comm, 1, request, &ret)) return ret;
-    return m->prev_reduce_scatter_init(sbuf, rbuf, rcounts, dtype, op, comm, info, request,
-                                       m->prev_reduce_scatter_init_module);
+    size_t total = 0;
+    const int rank = mx_ompi_host->comm_rank(comm), inpl = sbuf == MPI_IN_PLACE;
+    for (int i = 0; i < mx_ompi_host->comm_size(comm); i++) total += (size_t)rcounts[i];
+#define H(hs, hr, rq) \
+    m->prev_reduce_scatter_init(hs, hr, rcounts, dtype, op, comm, info, rq, m->prev_reduce_scatter_init_module)
+    MX_HOST_NB(m, sbuf, dtype, total, rbuf, dtype, inpl ? total : (size_t)rcounts[rank], inpl, 1, request, H);
+#undef H
 }
 
 static int mx_coll_ireduce_scatter_block(const void *sbuf, void *rbuf, int rcount, struct ompi_datatype_t *dtype,
@@ -937,8 +1460,12 @@ static int mx_coll_ireduce_scatter_block(const void *sbuf, void *rbuf, int rcoun
     mx_coll_module_t *m = (mx_coll_module_t *)module;
     int ret;
     if (!rs_like(m, sbuf, rbuf, NULL, rcount, dtype, op, comm, 0, request, &ret)) return ret;
-    return m->prev_ireduce_scatter_block(sbuf, rbuf, rcount, dtype, op, comm, request,
-                                         m->prev_ireduce_scatter_block_module);
+    const size_t total = (size_t)rcount * mx_ompi_host->comm_size(comm);
+    const int inpl = sbuf == MPI_IN_PLACE;
+#define H(hs, hr, rq) \
+    m->prev_ireduce_scatter_block(hs, hr, rcount, dtype, op, comm, rq, m->prev_ireduce_scatter_block_module)
+    MX_HOST_NB(m, sbuf, dtype, total, rbuf, dtype, inpl ? total : (size_t)rcount, inpl, 0, request, H);
+#undef H
 }
 
 static int mx_coll_reduce_scatter_block_init(const void *sbuf, void *rbuf, int rcount, struct ompi_datatype_t *dtype,
@@ -949,8 +1476,12 @@ static int mx_coll_reduce_scatter_block_init(const void *sbuf, void *rbuf, int r
     mx_coll_module_t *m = (mx_coll_module_t *)module;
     int ret;
     if (!rs_like(m, sbuf, rbuf, NULL, rcount, dtype, op, comm, 1, request, &ret)) return ret;
-    return m->prev_reduce_scatter_block_init(sbuf, rbuf, rcount, dtype, op, comm, info, request,
-                                             m->prev_reduce_scatter_block_init_module);
+    const size_t total = (size_t)rcount * mx_ompi_host->comm_size(comm);
+    const int inpl = sbuf == MPI_IN_PLACE;
+#define H(hs, hr, rq) m->prev_reduce_scatter_block_init(hs, hr, rcount, dtype, op, comm, info, rq, \
+                                                         m->prev_reduce_scatter_block_init_module)
+    MX_HOST_NB(m, sbuf, dtype, total, rbuf, dtype, inpl ? total : (size_t)rcount, inpl, 1, request, H);
+#undef H
 }
 
 static int scan_like(mx_coll_module_t *m, const void *sbuf, void *rbuf, int count, struct ompi_datatype_t *dtype,
@@ -959,8 +1490,8 @@ static int scan_like(mx_coll_module_t *m, const void *sbuf, void *rbuf, int coun
     const int n = mx_ompi_host->comm_size(m->comm);
     int slot, opi, rc;
     mx_request_t *q = NULL;
-    if (!reducible(dtype, op, (size_t)count, n, &slot, &opi) || !comm_ready(m)) return 1;
     const size_t bytes = (size_t)count * mx_ompi_host->dtype_size(dtype);
+    if (!reducible(dtype, op, (size_t)count, n, &slot, &opi) || !nb_device(m, bytes, 1)) return 1;
     mx_coll_req_t *r = req_setup(m, sbuf, (size_t)count, dtype, rbuf, (size_t)count, dtype,
                                  sbuf == MPI_IN_PLACE || exclusive, bytes, persistent, ret);
     if (!r) return 0;
@@ -982,7 +1513,9 @@ static int mx_coll_iscan(const void *sbuf, void *rbuf, int count, struct ompi_da
     mx_coll_module_t *m = (mx_coll_module_t *)module;
     int ret;
     if (!scan_like(m, sbuf, rbuf, count, dtype, op, 0, 0, request, &ret)) return ret;
-    return m->prev_iscan(sbuf, rbuf, count, dtype, op, comm, request, m->prev_iscan_module);
+#define H(hs, hr, rq) m->prev_iscan(hs, hr, count, dtype, op, comm, rq, m->prev_iscan_module)
+    MX_HOST_NB(m, sbuf, dtype, (size_t)count, rbuf, dtype, (size_t)count, sbuf == MPI_IN_PLACE, 0, request, H);
+#undef H
 }
 
 static int mx_coll_iexscan(const void *sbuf, void *rbuf, int count, struct ompi_datatype_t *dtype,
@@ -992,7 +1525,9 @@ static int mx_coll_iexscan(const void *sbuf, void *rbuf, int count, struct ompi_
     mx_coll_module_t *m = (mx_coll_module_t *)module;
     int ret;
     if (!scan_like(m, sbuf, rbuf, count, dtype, op, 1, 0, request, &ret)) return ret;
-    return m->prev_iexscan(sbuf, rbuf, count, dtype, op, comm, request, m->prev_iexscan_module);
+#define H(hs, hr, rq) m->prev_iexscan(hs, hr, count, dtype, op, comm, rq, m->prev_iexscan_module)
+    MX_HOST_NB(m, sbuf, dtype, (size_t)count, rbuf, dtype, (size_t)count, 1, 0, request, H);
+#undef H
 }
 
 static int mx_coll_scan_init(const void *sbuf, void *rbuf, int count, struct ompi_datatype_t *dtype,
@@ -1002,7 +1537,9 @@ static int mx_coll_scan_init(const void *sbuf, void *rbuf, int count, struct omp
     mx_coll_module_t *m = (mx_coll_module_t *)module;
     int ret;
     if (!scan_like(m, sbuf, rbuf, count, dtype, op, 0, 1, request, &ret)) return ret;
-    return m->prev_scan_init(sbuf, rbuf, count, dtype, op, comm, info, request, m->prev_scan_init_module);
+#define H(hs, hr, rq) m->prev_scan_init(hs, hr, count, dtype, op, comm, info, rq, m->prev_scan_init_module)
+    MX_HOST_NB(m, sbuf, dtype, (size_t)count, rbuf, dtype, (size_t)count, sbuf == MPI_IN_PLACE, 1, request, H);
+#undef H
 }
 
 static int mx_coll_exscan_init(const void *sbuf, void *rbuf, int count, struct ompi_datatype_t *dtype,
@@ -1012,7 +1549,9 @@ static int mx_coll_exscan_init(const void *sbuf, void *rbuf, int count, struct o
     mx_coll_module_t *m = (mx_coll_module_t *)module;
     int ret;
     if (!scan_like(m, sbuf, rbuf, count, dtype, op, 1, 1, request, &ret)) return ret;
-    return m->prev_exscan_init(sbuf, rbuf, count, dtype, op, comm, info, request, m->prev_exscan_init_module);
+#define H(hs, hr, rq) m->prev_exscan_init(hs, hr, count, dtype, op, comm, info, rq, m->prev_exscan_init_module)
+    MX_HOST_NB(m, sbuf, dtype, (size_t)count, rbuf, dtype, (size_t)count, 1, 1, request, H);
+#undef H
 }
 
 static int allgather_like(mx_coll_module_t *m, const void *sbuf, int scount, struct ompi_datatype_t *sdtype,
@@ -1022,7 +1561,7 @@ static int allgather_like(mx_coll_module_t *m, const void *sbuf, int scount, str
     const size_t rbytes = (size_t)rcount * mx_ompi_host->dtype_size(rdtype);
     const int n = mx_ompi_host->comm_size(comm);
     mx_request_t *q = NULL;
-    if (!rbytes || n > MX_MAX_RANKS || !comm_ready(m)) return 1;
+    if (!rbytes || n > MX_MAX_RANKS || !nb_device(m, rbytes * n, 0)) return 1;
     if (sbuf != MPI_IN_PLACE && (size_t)scount * mx_ompi_host->dtype_size(sdtype) != rbytes) {
         *ret = OMPI_ERROR;   /* type signatures differ: erroneous program */
         return 0;
@@ -1043,7 +1582,10 @@ static int mx_coll_iallgather(const void *sbuf, int scount, struct ompi_datatype
     mx_coll_module_t *m = (mx_coll_module_t *)module;
     int ret;
     if (!allgather_like(m, sbuf, scount, sdtype, rbuf, rcount, rdtype, comm, 0, request, &ret)) return ret;
-    return m->prev_iallgather(sbuf, scount, sdtype, rbuf, rcount, rdtype, comm, request, m->prev_iallgather_module);
+    const size_t nr = (size_t)rcount * mx_ompi_host->comm_size(comm);
+#define H(hs, hr, rq) m->prev_iallgather(hs, scount, sdtype, hr, rcount, rdtype, comm, rq, m->prev_iallgather_module)
+    MX_HOST_NB(m, sbuf, sdtype, (size_t)scount, rbuf, rdtype, nr, sbuf == MPI_IN_PLACE, 0, request, H);
+#undef H
 }
 
 static int mx_coll_allgather_init(const void *sbuf, int scount, struct ompi_datatype_t *sdtype, void *rbuf,
@@ -1054,8 +1596,11 @@ static int mx_coll_allgather_init(const void *sbuf, int scount, struct ompi_data
     mx_coll_module_t *m = (mx_coll_module_t *)module;
     int ret;
     if (!allgather_like(m, sbuf, scount, sdtype, rbuf, rcount, rdtype, comm, 1, request, &ret)) return ret;
-    return m->prev_allgather_init(sbuf, scount, sdtype, rbuf, rcount, rdtype, comm, info, request,
-                                  m->prev_allgather_init_module);
+    const size_t nr = (size_t)rcount * mx_ompi_host->comm_size(comm);
+#define H(hs, hr, rq) m->prev_allgather_init(hs, scount, sdtype, hr, rcount, rdtype, comm, info, rq, \
+                                             m->prev_allgather_init_module)
+    MX_HOST_NB(m, sbuf, sdtype, (size_t)scount, rbuf, rdtype, nr, sbuf == MPI_IN_PLACE, 1, request, H);
+#undef H
 }
 
 static int bcast_like(mx_coll_module_t *m, void *buf, int count, struct ompi_datatype_t *dtype, int root,
@@ -1064,7 +1609,7 @@ static int bcast_like(mx_coll_module_t *m, void *buf, int count, struct ompi_dat
     const size_t bytes = (size_t)count * mx_ompi_host->dtype_size(dtype);
     const int n = mx_ompi_host->comm_size(m->comm), rank = mx_ompi_host->comm_rank(m->comm);
     mx_request_t *q = NULL;
-    if (!bytes || n > MX_MAX_RANKS || !comm_ready(m)) return 1;
+    if (!bytes || n > MX_MAX_RANKS || !nb_device(m, bytes, 0)) return 1;
     mx_coll_req_t *r = req_setup(m, NULL, 0, NULL, buf, (size_t)count, dtype, rank == root,
                                  rank == root ? 0 : bytes, persistent, ret);
     if (!r) return 0;
@@ -1081,7 +1626,10 @@ static int mx_coll_ibcast(void *buf, int count, struct ompi_datatype_t *dtype, i
     mx_coll_module_t *m = (mx_coll_module_t *)module;
     int ret;
     if (!bcast_like(m, buf, count, dtype, root, 0, request, &ret)) return ret;
-    return m->prev_ibcast(buf, count, dtype, root, comm, request, m->prev_ibcast_module);
+    const int is_root = mx_ompi_host->comm_rank(comm) == root;
+#define H(hs, hr, rq) ((void)(hs), m->prev_ibcast(hr, count, dtype, root, comm, rq, m->prev_ibcast_module))
+    MX_HOST_NB(m, NULL, dtype, 0, buf, dtype, (size_t)count, is_root, 0, request, H);
+#undef H
 }
 
 static int mx_coll_bcast_init(void *buf, int count, struct ompi_datatype_t *dtype, int root,
@@ -1091,7 +1639,10 @@ static int mx_coll_bcast_init(void *buf, int count, struct ompi_datatype_t *dtyp
     mx_coll_module_t *m = (mx_coll_module_t *)module;
     int ret;
     if (!bcast_like(m, buf, count, dtype, root, 1, request, &ret)) return ret;
-    return m->prev_bcast_init(buf, count, dtype, root, comm, info, request, m->prev_bcast_init_module);
+    const int is_root = mx_ompi_host->comm_rank(comm) == root;
+#define H(hs, hr, rq) ((void)(hs), m->prev_bcast_init(hr, count, dtype, root, comm, info, rq, m->prev_bcast_init_module))
+    MX_HOST_NB(m, NULL, dtype, 0, buf, dtype, (size_t)count, is_root, 1, request, H);
+#undef H
 }
 
 /* ---- module enable / component query ------------------------------------ */
@@ -1134,6 +1685,22 @@ static int mx_coll_module_enable(mca_coll_base_module_t *module, struct ompi_com
     }
     MX_NB_SLOTS(SAVE_PREV_OPT)
 #undef SAVE_PREV_OPT
+    /* the reduction orders of the saved modules, coll/tuned's configuration
+     * (read at enable, as ompi_coll_tuned_forced_getvalues does), the size
+     * split (identical on every rank: MCA variables are job-wide) */
+    m->low_allreduce = low_kind(m->prev_allreduce_module);
+    m->low_reduce_scatter = low_kind(m->prev_reduce_scatter_module);
+    m->low_reduce = low_kind(m->prev_reduce_module);
+    m->low_rsb = low_kind(m->prev_reduce_scatter_block_module);
+    m->low_scan = low_kind(m->prev_scan_module);
+    m->low_exscan = low_kind(m->prev_exscan_module);
+    m->low_nbc = low_kind(m->prev_iallreduce_module);
+    m->basic_crossover = mx_ompi_host->mca_int("coll_basic_crossover", 4);   /* coll_basic_component.c:98-104 */
+    {
+        const int kb = mx_ompi_host->mca_int("coll_mi355x_host_max_kb", 64);
+        m->host_max = kb > 0 ? (size_t)kb << 10 : 0;
+    }
+    (void)mx_tuned_cfg_load(&m->tuned, n);
     /* the device communicator (IPC staging, flags) is created at the first
      * eligible collective, so a communicator that never runs one on the
      * device -- an MPI_Comm_dup kept for a library, say -- costs no device
@@ -1156,6 +1723,14 @@ static mca_coll_base_module_t *mx_coll_component_comm_query(struct ompi_communic
     const int n = mx_ompi_host->comm_size(comm);
     *priority = mx_ompi_host->mca_int("coll_mi355x_priority", 80);
     if (*priority < 0) return NULL;
+    /* intra-communicator semantics only: the intercommunicator forms
+     * (remote-group results, coll/inter and coll/basic's _inter functions)
+     * stay with the components built for them, as coll/tuned
+     * (coll_tuned_module.c:66-69) and coll/cuda (coll_cuda_module.c:141) do */
+    if (mx_ompi_host->comm_is_inter && mx_ompi_host->comm_is_inter(comm)) {
+        *priority = 0;
+        return NULL;
+    }
     m = MX_MODULE_NEW(mx_coll_module_t, super);
     if (!m) return NULL;
     m->super.coll_module_enable = mx_coll_module_enable;

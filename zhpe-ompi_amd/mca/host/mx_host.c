@@ -210,6 +210,7 @@ enum { S_IALLREDUCE = 9, S_IREDUCE, S_IREDUCE_SCATTER, S_IREDUCE_SCATTER_BLOCK, 
 
 struct ompi_communicator_t {
     int rank, size;
+    int inter;       /* an intercommunicator (OMPI_COMM_IS_INTER) */
     mxh_allgather_t ag;
     void *ag_ctx;
     /* c_coll: (fn, module, owner-name) per slot (coll.h:622-) */
@@ -306,6 +307,7 @@ static int dtype_desc(struct ompi_datatype_t *d, const void **recs, size_t *nrec
     return OMPI_SUCCESS;
 }
 static int comm_rank(struct ompi_communicator_t *c) { return c->rank; }
+static int comm_is_inter(struct ompi_communicator_t *c) { return c->inter; }
 static int comm_size(struct ompi_communicator_t *c) { return c->size; }
 static int op_index(struct ompi_op_t *op) { return op->o_f_to_c_index; }
 static uint32_t op_flags(struct ompi_op_t *op) { return op->o_flags; }
@@ -336,6 +338,23 @@ static struct ompi_request_t *request_create(int persistent, int (*start)(struct
     return r;
 }
 static void *request_ctx(struct ompi_request_t *r) { return r->ctx; }
+/* the host's side of a request a component drives itself (mx_ompi_abi.h) */
+static int inner_test(struct ompi_request_t *r, int *flag, int *status)
+{
+    *flag = r->complete;
+    *status = r->complete ? r->status : OMPI_SUCCESS;
+    return OMPI_SUCCESS;
+}
+static int inner_start(struct ompi_request_t *r) { return r->start(r); }
+static int inner_free(struct ompi_request_t **rp)
+{
+    struct ompi_request_t *r = *rp;
+    if (!r) return OMPI_SUCCESS;
+    const int rc = r->free_fn(r);
+    free(r);
+    *rp = NULL;
+    return rc;
+}
 static void request_activate(struct ompi_request_t *r) { r->active = 1; r->complete = 0; r->status = 0; }
 static void request_complete(struct ompi_request_t *r, int status) { r->status = status; r->complete = 1; }
 
@@ -363,128 +382,286 @@ static void op_reduce(struct ompi_op_t *op, const void *source, void *target, in
     op->intrinsic.fns[dt->slot]((void *)source, target, &cnt, &d, op->intrinsic.modules[dt->slot]);
 }
 
-/* ---- host base coll module (stands in for tuned/basic on host buffers) ---- */
+/* ---- host coll modules ---------------------------------------------------
+ * Stand-ins for the modules coll/mi355x stacks on, with the reference's
+ * class names (coll/mi355x reads the order it must reproduce from them):
+ *   tuned  (priority 30, "mca_coll_tuned_module_t"): coll/tuned's algorithms
+ *          -- the fixed decision, or with coll_tuned_use_dynamic_rules the
+ *          forced coll_tuned_<coll>_algorithm -- evaluated by the injected
+ *          oracle restatement over every rank's inputs; its compositions
+ *          (allreduce / reduce_scatter nonoverlapping, reduce_scatter_block
+ *          basic_linear) call the communicator's current coll_reduce /
+ *          coll_bcast like coll/base does (coll_base_allreduce.c:54-86);
+ *   basic  (priority 10, "mca_coll_basic_module_t"): coll/basic's
+ *          allreduce = coll_reduce to 0 + coll_bcast, linear reduce up to
+ *          coll_basic_crossover ranks (its log-tree reduce above that is not
+ *          restated: the call fails), recursive-halving reduce_scatter below
+ *          8 MiB else coll_reduce + scatterv, linear scan / exscan;
+ *   libnbc (priority 10, "ompi_coll_libnbc_module_t"): the nonblocking and
+ *          persistent slots with libnbc's orders (oracle), complete at post /
+ *          start.
+ * `coll` (OMPI_MCA_coll / mxh_set_mca_str) "^tuned" excludes tuned as
+ * --mca coll ^tuned does.  Host memory only: the harness transport is a
+ * host allgather. */
 static int dtype_pack(struct ompi_datatype_t *d, int count, const void *user, void *packed);
 static int dtype_unpack(struct ompi_datatype_t *d, int count, const void *packed, void *user);
 
+static mxh_coll_oracle_t g_or;
+int mxh_set_coll_oracle(const mxh_coll_oracle_t *o)
+{
+    g_or = *o;
+    return 0;
+}
+
+#define NSVARS 16
+static struct { char name[96]; char value[512]; int set; } g_svars[NSVARS];
+int mxh_set_mca_str(const char *name, const char *value)
+{
+    for (int i = 0; i < NSVARS; i++) {
+        if (!g_svars[i].set || !strcmp(g_svars[i].name, name)) {
+            snprintf(g_svars[i].name, sizeof g_svars[i].name, "%s", name);
+            if (value) snprintf(g_svars[i].value, sizeof g_svars[i].value, "%s", value);
+            g_svars[i].set = value != NULL;
+            return 0;
+        }
+    }
+    return -1;
+}
+static const char *mca_string(const char *name)
+{
+    char env[160];
+    for (int i = 0; i < NSVARS; i++)
+        if (g_svars[i].set && !strcmp(g_svars[i].name, name)) return g_svars[i].value;
+    snprintf(env, sizeof env, "OMPI_MCA_%s", name);
+    return getenv(env);
+}
+
+static int comm_is_inter(struct ompi_communicator_t *c);
+
+/* every rank's `bytes` (rank-major) through the harness transport */
+static char *gather(struct ompi_communicator_t *c, const void *mine, size_t bytes)
+{
+    char *all = malloc(bytes * (size_t)c->size + 1);
+    if (all && c->ag(mine, all, bytes, c->ag_ctx)) {
+        free(all);
+        all = NULL;
+    }
+    return all;
+}
+
+/* the current (top) entry of a slot: what coll/base's compositions call */
+#define TOP(c, name, T) ((T)(c)->fn[slot_index(#name)])
+#define TOPMOD(c, name) ((c)->mod[slot_index(#name)])
+
+/* coll/tuned's forced algorithm of a collective (dynamic rules only) */
+static int tuned_forced(const char *coll, int *fanout)
+{
+    char v[96];
+    *fanout = 0;
+    if (!mca_int("coll_tuned_use_dynamic_rules", 0)) return 0;
+    snprintf(v, sizeof v, "coll_tuned_%s_algorithm_chain_fanout", coll);
+    *fanout = mca_int(v, 0);
+    snprintf(v, sizeof v, "coll_tuned_%s_algorithm", coll);
+    return mca_int(v, 0);
+}
+
+/* n-rank oracle allreduce on everyone's inputs, my result to rbuf */
+static int oracle_allreduce(int alg, const void *sbuf, void *rbuf, int count, struct ompi_datatype_t *dt,
+                            struct ompi_op_t *op, struct ompi_communicator_t *c, int nbc)
+{
+    const int n = c->size, inplace = sbuf == MPI_IN_PLACE;
+    const size_t b = (size_t)count * dt->size;
+    char *all = gather(c, inplace ? rbuf : sbuf, b), *outs = malloc(b * n + 1);
+    const void *sp[256];
+    void *rp[256];
+    int rc = (all && outs && n <= 256) ? 0 : OMPI_ERR_OUT_OF_RESOURCE;
+    for (int r = 0; !rc && r < n; r++) {
+        sp[r] = all + (size_t)r * b;
+        rp[r] = outs + (size_t)r * b;
+        if (inplace) memcpy(rp[r], sp[r], b);
+    }
+    if (!rc) rc = nbc ? g_or.iallreduce(alg, op->o_f_to_c_index, dt->slot, n, (size_t)count, inplace ? NULL : sp, rp)
+                      : g_or.allreduce(alg, op->o_f_to_c_index, dt->slot, n, (size_t)count, inplace ? NULL : sp, rp);
+    if (!rc) memcpy(rbuf, outs + (size_t)c->rank * b, b);
+    free(all);
+    free(outs);
+    return rc ? OMPI_ERROR : OMPI_SUCCESS;
+}
+
+/* n-rank oracle rooted reduce (root's result to rbuf); nbc: libnbc's */
+static int oracle_reduce(int alg, const void *sbuf, void *rbuf, int count, struct ompi_datatype_t *dt,
+                         struct ompi_op_t *op, int root, struct ompi_communicator_t *c, int nbc)
+{
+    const int n = c->size, inplace = sbuf == MPI_IN_PLACE && c->rank == root;
+    const size_t b = (size_t)count * dt->size;
+    /* rank order of inputs; the root's flag travels in one extra byte */
+    char *mine = malloc(b + 1);
+    if (!mine) return OMPI_ERR_OUT_OF_RESOURCE;
+    memcpy(mine, inplace ? rbuf : sbuf, b);
+    mine[b] = (char)inplace;
+    char *all = gather(c, mine, b + 1);
+    free(mine);
+    if (!all) return OMPI_ERROR;
+    int rc = 0;
+    if (c->rank == root) {
+        const void *sp[256];
+        const int root_inplace = all[(size_t)root * (b + 1) + b];
+        for (int r = 0; r < n; r++) sp[r] = all + (size_t)r * (b + 1);
+        char *out = malloc(b + 1);
+        if (root_inplace) {
+            memcpy(out, sp[root], b);
+            sp[root] = NULL;
+        }
+        rc = nbc ? g_or.ireduce(alg, op->o_f_to_c_index, dt->slot, n, (size_t)count, root, sp, out)
+                 : g_or.reduce(alg, op->o_f_to_c_index, dt->slot, n, (size_t)count, root, sp, out);
+        if (!rc) memcpy(rbuf, out, b);
+        free(out);
+    }
+    free(all);
+    return rc ? OMPI_ERROR : OMPI_SUCCESS;
+}
+
+/* n-rank oracle reduce_scatter (alg < 0: libnbc's ireduce_scatter) */
+static int oracle_reduce_scatter(int alg, const void *sbuf, void *rbuf, const int *rcounts,
+                                 struct ompi_datatype_t *dt, struct ompi_op_t *op, struct ompi_communicator_t *c)
+{
+    const int n = c->size, inplace = sbuf == MPI_IN_PLACE;
+    size_t total = 0, rc64[256], disp = 0;
+    if (n > 256) return OMPI_ERR_NOT_SUPPORTED;
+    for (int r = 0; r < n; r++) {
+        rc64[r] = (size_t)rcounts[r];
+        if (r < c->rank) disp += rc64[r];
+        total += rc64[r];
+    }
+    const size_t b = total * dt->size;
+    char *all = gather(c, inplace ? rbuf : sbuf, b), *outs = malloc(b * n + 1);
+    const void *sp[256];
+    void *rp[256];
+    int rc = (all && outs) ? 0 : OMPI_ERR_OUT_OF_RESOURCE;
+    for (int r = 0; !rc && r < n; r++) {
+        sp[r] = all + (size_t)r * b;
+        rp[r] = outs + (size_t)r * b;
+        if (inplace) memcpy(rp[r], sp[r], b);
+    }
+    if (!rc)
+        rc = alg < 0 ? g_or.ireduce_scatter(op->o_f_to_c_index, dt->slot, n, rc64, inplace ? NULL : sp, rp)
+                     : g_or.reduce_scatter(alg, op->o_f_to_c_index, dt->slot, n, rc64, inplace ? NULL : sp, rp);
+    if (!rc) memcpy(rbuf, outs + (size_t)c->rank * b, rc64[c->rank] * dt->size);
+    (void)disp;
+    free(all);
+    free(outs);
+    return rc ? OMPI_ERROR : OMPI_SUCCESS;
+}
+
+static int oracle_scan(int alg, const void *sbuf, void *rbuf, int count, struct ompi_datatype_t *dt,
+                       struct ompi_op_t *op, struct ompi_communicator_t *c, int exclusive)
+{
+    const int n = c->size, inplace = sbuf == MPI_IN_PLACE;
+    const size_t b = (size_t)count * dt->size;
+    char *all = gather(c, inplace ? rbuf : sbuf, b), *outs = malloc(b * n + 1);
+    const void *sp[256];
+    void *rp[256];
+    int rc = (all && outs && n <= 256) ? 0 : OMPI_ERR_OUT_OF_RESOURCE;
+    for (int r = 0; !rc && r < n; r++) {
+        sp[r] = all + (size_t)r * b;
+        rp[r] = outs + (size_t)r * b;
+    }
+    if (!rc) rc = (exclusive ? g_or.exscan : g_or.scan)(alg, op->o_f_to_c_index, dt->slot, n, (size_t)count, sp, rp);
+    if (!rc && !(exclusive && c->rank == 0)) memcpy(rbuf, outs + (size_t)c->rank * b, b);
+    free(all);
+    free(outs);
+    return rc ? OMPI_ERROR : OMPI_SUCCESS;
+}
+
+/* scatterv of root 0's `full` vector (bytes) by rcounts: my block to rbuf */
+static int scatter_from0(struct ompi_communicator_t *c, const char *full, size_t total, const int *rcounts,
+                         struct ompi_datatype_t *dt, void *rbuf)
+{
+    const size_t b = total * dt->size;
+    char *zero = calloc(1, b + 1);
+    if (!zero) return OMPI_ERR_OUT_OF_RESOURCE;
+    char *all = gather(c, c->rank == 0 ? full : zero, b);
+    free(zero);
+    if (!all) return OMPI_ERROR;
+    size_t disp = 0;
+    for (int r = 0; r < c->rank; r++) disp += (size_t)rcounts[r];
+    memcpy(rbuf, all + disp * dt->size, (size_t)rcounts[c->rank] * dt->size);
+    free(all);
+    return OMPI_SUCCESS;
+}
+
+/* coll_reduce (the top entry) of `total` to root 0, then scatterv.  root_ip:
+ * an MPI_IN_PLACE call reduces MPI_IN_PLACE on the root (coll/base's
+ * nonoverlapping); else sbuf = rbuf (coll/basic, basic_linear) */
+static int reduce_then_scatter(const void *sbuf, void *rbuf, const int *rcounts, size_t total,
+                               struct ompi_datatype_t *dt, struct ompi_op_t *op, struct ompi_communicator_t *c,
+                               int root_ip)
+{
+    const int inplace = sbuf == MPI_IN_PLACE;
+    char *tmp = c->rank == 0 ? malloc(total * dt->size + 1) : NULL;
+    int rc;
+    if (c->rank == 0 && !tmp) return OMPI_ERR_OUT_OF_RESOURCE;
+    if (inplace && root_ip) {
+        if (c->rank == 0) memcpy(tmp, rbuf, total * dt->size);
+        rc = TOP(c, reduce, mca_coll_base_module_reduce_fn_t)(c->rank == 0 ? MPI_IN_PLACE : rbuf, tmp, (int)total,
+                                                              dt, op, 0, c, TOPMOD(c, reduce));
+    } else {
+        rc = TOP(c, reduce, mca_coll_base_module_reduce_fn_t)(inplace ? rbuf : sbuf, tmp, (int)total, dt, op, 0, c,
+                                                              TOPMOD(c, reduce));
+    }
+    if (rc == OMPI_SUCCESS) rc = scatter_from0(c, tmp, total, rcounts, dt, rbuf);
+    free(tmp);
+    return rc;
+}
+
+/* coll_reduce to 0 + coll_bcast (coll_base_allreduce.c:54-86,
+ * coll_basic_allreduce.c:45-71) */
+static int reduce_then_bcast(const void *sbuf, void *rbuf, int count, struct ompi_datatype_t *dt,
+                             struct ompi_op_t *op, struct ompi_communicator_t *c)
+{
+    int rc;
+    if (sbuf == MPI_IN_PLACE)
+        rc = TOP(c, reduce, mca_coll_base_module_reduce_fn_t)(c->rank == 0 ? MPI_IN_PLACE : rbuf,
+                                                              c->rank == 0 ? rbuf : NULL, count, dt, op, 0, c,
+                                                              TOPMOD(c, reduce));
+    else
+        rc = TOP(c, reduce, mca_coll_base_module_reduce_fn_t)(sbuf, rbuf, count, dt, op, 0, c, TOPMOD(c, reduce));
+    if (rc != OMPI_SUCCESS) return rc;
+    return TOP(c, bcast, mca_coll_base_module_bcast_fn_t)(rbuf, count, dt, 0, c, TOPMOD(c, bcast));
+}
+
+/* data movement (any module gives the same bytes) */
 static int base_allgather(const void *sbuf, int scount, struct ompi_datatype_t *sdt, void *rbuf, int rcount,
                           struct ompi_datatype_t *rdt, struct ompi_communicator_t *c, mca_coll_base_module_t *m)
 {
     (void)m;
     const size_t rb = (size_t)rcount * rdt->size, rext = (size_t)rcount * dtype_extent(rdt);
-    char *tmp = malloc(rb * c->size + 1), *mine = malloc(rb + 1);
-    int rc;
-    if (!tmp || !mine) { free(tmp); free(mine); return OMPI_ERR_OUT_OF_RESOURCE; }
+    char *mine = malloc(rb + 1), *tmp;
+    if (!mine) return OMPI_ERR_OUT_OF_RESOURCE;
     if (sbuf == MPI_IN_PLACE) dtype_pack(rdt, rcount, (char *)rbuf + (size_t)c->rank * rext, mine);
     else dtype_pack(sdt, scount, sbuf, mine);
-    rc = c->ag(mine, tmp, rb, c->ag_ctx);
-    for (int p = 0; p < c->size && !rc; p++) dtype_unpack(rdt, rcount, tmp + (size_t)p * rb, (char *)rbuf + p * rext);
-    free(tmp);
+    tmp = gather(c, mine, rb);
     free(mine);
-    return rc ? OMPI_ERROR : OMPI_SUCCESS;
-}
-
-static int base_allreduce(const void *sbuf, void *rbuf, int count, struct ompi_datatype_t *dt, struct ompi_op_t *op,
-                          struct ompi_communicator_t *c, mca_coll_base_module_t *m)
-{
-    size_t b = (size_t)count * dt->size;
-    char *all = malloc(b * c->size + 1);
-    (void)m;
-    if (!all) return OMPI_ERR_OUT_OF_RESOURCE;
-    if (c->ag(sbuf == MPI_IN_PLACE ? rbuf : sbuf, all, b, c->ag_ctx)) { free(all); return OMPI_ERROR; }
-    /* basic linear order (coll_base_reduce.c:627-720): x_{n-1} op x_{n-2} ... */
-    memcpy(rbuf, all + (size_t)(c->size - 1) * b, b);
-    for (int i = c->size - 2; i >= 0; i--) op_reduce(op, all + (size_t)i * b, rbuf, count, dt);
-    free(all);
+    if (!tmp) return OMPI_ERROR;
+    for (int p = 0; p < c->size; p++) dtype_unpack(rdt, rcount, tmp + (size_t)p * rb, (char *)rbuf + p * rext);
+    free(tmp);
     return OMPI_SUCCESS;
-}
-
-static int base_reduce_scatter(const void *sbuf, void *rbuf, const int *rcounts, struct ompi_datatype_t *dt,
-                               struct ompi_op_t *op, struct ompi_communicator_t *c, mca_coll_base_module_t *m)
-{
-    int total = 0, disp = 0;
-    char *full;
-    for (int i = 0; i < c->size; i++) { if (i < c->rank) disp += rcounts[i]; total += rcounts[i]; }
-    full = malloc((size_t)total * dt->size + 1);
-    if (!full) return OMPI_ERR_OUT_OF_RESOURCE;
-    int rc = base_allreduce(sbuf == MPI_IN_PLACE ? rbuf : sbuf, full, total, dt, op, c, m);
-    if (!rc) memcpy(rbuf, full + (size_t)disp * dt->size, (size_t)rcounts[c->rank] * dt->size);
-    free(full);
-    return rc;
 }
 
 static int base_bcast(void *buf, int count, struct ompi_datatype_t *dt, int root, struct ompi_communicator_t *c,
                       mca_coll_base_module_t *m)
 {
-    size_t b = (size_t)count * dt->size;
-    char *all = malloc(b * c->size + 1), *mine = malloc(b + 1);
     (void)m;
-    if (!all || !mine) { free(all); free(mine); return OMPI_ERR_OUT_OF_RESOURCE; }
+    const size_t b = (size_t)count * dt->size;
+    char *mine = malloc(b + 1), *all;
+    if (!mine) return OMPI_ERR_OUT_OF_RESOURCE;
     dtype_pack(dt, count, buf, mine);
-    if (c->ag(mine, all, b, c->ag_ctx)) { free(all); free(mine); return OMPI_ERROR; }
+    all = gather(c, mine, b);
+    free(mine);
+    if (!all) return OMPI_ERROR;
     dtype_unpack(dt, count, all + (size_t)root * b, buf);
     free(all);
-    free(mine);
     return OMPI_SUCCESS;
-}
-
-/* rooted reduce, basic linear order (coll_base_reduce.c:626-735) */
-static int base_reduce(const void *sbuf, void *rbuf, int count, struct ompi_datatype_t *dt, struct ompi_op_t *op,
-                       int root, struct ompi_communicator_t *c, mca_coll_base_module_t *m)
-{
-    size_t b = (size_t)count * dt->size;
-    char *all = malloc(b * c->size + 1);
-    (void)m;
-    if (!all) return OMPI_ERR_OUT_OF_RESOURCE;
-    if (c->ag(sbuf == MPI_IN_PLACE ? rbuf : sbuf, all, b, c->ag_ctx)) { free(all); return OMPI_ERROR; }
-    if (c->rank == root) {
-        memcpy(rbuf, all + (size_t)(c->size - 1) * b, b);
-        for (int i = c->size - 2; i >= 0; i--) op_reduce(op, all + (size_t)i * b, rbuf, count, dt);
-    }
-    free(all);
-    return OMPI_SUCCESS;
-}
-
-static int base_reduce_scatter_block(const void *sbuf, void *rbuf, int rcount, struct ompi_datatype_t *dt,
-                                     struct ompi_op_t *op, struct ompi_communicator_t *c, mca_coll_base_module_t *m)
-{
-    int rcounts[256];
-    if (c->size > 256) return OMPI_ERR_NOT_SUPPORTED;
-    for (int i = 0; i < c->size; i++) rcounts[i] = rcount;
-    return base_reduce_scatter(sbuf, rbuf, rcounts, dt, op, c, m);
-}
-
-/* linear scan / exscan (coll_base_scan.c:35-122, coll_base_exscan.c:35-107) */
-static int base_scan_common(const void *sbuf, void *rbuf, int count, struct ompi_datatype_t *dt, struct ompi_op_t *op,
-                            struct ompi_communicator_t *c, int exclusive)
-{
-    size_t b = (size_t)count * dt->size;
-    char *all = malloc(b * c->size + 1), *acc = malloc(b + 1), *tmp = malloc(b + 1);
-    int rc = OMPI_SUCCESS;
-    if (!all || !acc || !tmp) { rc = OMPI_ERR_OUT_OF_RESOURCE; goto out; }
-    if (c->ag(sbuf == MPI_IN_PLACE ? rbuf : sbuf, all, b, c->ag_ctx)) { rc = OMPI_ERROR; goto out; }
-    memcpy(acc, all, b);
-    for (int r = 1; r <= (exclusive ? c->rank - 1 : c->rank); r++) {
-        memcpy(tmp, all + (size_t)r * b, b);                 /* own data is the target */
-        op_reduce(op, acc, tmp, count, dt);
-        memcpy(acc, tmp, b);
-    }
-    if (!exclusive || c->rank > 0) memcpy(rbuf, acc, b);
-out:
-    free(all); free(acc); free(tmp);
-    return rc;
-}
-static int base_scan(const void *sbuf, void *rbuf, int count, struct ompi_datatype_t *dt, struct ompi_op_t *op,
-                     struct ompi_communicator_t *c, mca_coll_base_module_t *m)
-{
-    (void)m;
-    return base_scan_common(sbuf, rbuf, count, dt, op, c, 0);
-}
-static int base_exscan(const void *sbuf, void *rbuf, int count, struct ompi_datatype_t *dt, struct ompi_op_t *op,
-                       struct ompi_communicator_t *c, mca_coll_base_module_t *m)
-{
-    (void)m;
-    return base_scan_common(sbuf, rbuf, count, dt, op, c, 1);
 }
 
 /* coll/self-like reduce_local: mca_coll_base_reduce_local (coll_base_reduce.c:42-49) */
@@ -496,9 +673,120 @@ static int base_reduce_local(const void *in, void *inout, int count, struct ompi
     return OMPI_SUCCESS;
 }
 
-/* nonblocking / persistent stand-ins for coll/libnbc on host buffers: the
- * blocking base algorithm runs at post (or MPI_Start) time and the request
- * is complete at once */
+/* ---- tuned ---- */
+static int tuned_allreduce(const void *sbuf, void *rbuf, int count, struct ompi_datatype_t *dt, struct ompi_op_t *op,
+                           struct ompi_communicator_t *c, mca_coll_base_module_t *m)
+{
+    int fan;
+    const int alg = tuned_forced("allreduce", &fan);
+    (void)m;
+    if (alg == 2) return reduce_then_bcast(sbuf, rbuf, count, dt, op, c);   /* nonoverlapping */
+    return oracle_allreduce(alg, sbuf, rbuf, count, dt, op, c, 0);
+}
+
+static int tuned_reduce_scatter(const void *sbuf, void *rbuf, const int *rcounts, struct ompi_datatype_t *dt,
+                                struct ompi_op_t *op, struct ompi_communicator_t *c, mca_coll_base_module_t *m)
+{
+    int fan;
+    const int alg = tuned_forced("reduce_scatter", &fan);
+    size_t total = 0;
+    (void)m;
+    for (int r = 0; r < c->size; r++) total += (size_t)rcounts[r];
+    if (alg == 1) return reduce_then_scatter(sbuf, rbuf, rcounts, total, dt, op, c, 1);   /* nonoverlapping */
+    return oracle_reduce_scatter(alg, sbuf, rbuf, rcounts, dt, op, c);
+}
+
+static int tuned_reduce(const void *sbuf, void *rbuf, int count, struct ompi_datatype_t *dt, struct ompi_op_t *op,
+                        int root, struct ompi_communicator_t *c, mca_coll_base_module_t *m)
+{
+    int fan;
+    const int alg = tuned_forced("reduce", &fan);
+    (void)m;
+    if (alg == 7) return OMPI_ERR_NOT_SUPPORTED;   /* redscat_gather: not restated */
+    return oracle_reduce(alg | ((alg == 2 && fan > 0) ? fan << 16 : 0), sbuf, rbuf, count, dt, op, root, c, 0);
+}
+
+static int tuned_reduce_scatter_block(const void *sbuf, void *rbuf, int rcount, struct ompi_datatype_t *dt,
+                                      struct ompi_op_t *op, struct ompi_communicator_t *c, mca_coll_base_module_t *m)
+{
+    int fan, rcounts[256];
+    const int alg = tuned_forced("reduce_scatter_block", &fan);
+    (void)m;
+    if ((alg != 0 && alg != 1) || c->size > 256) return OMPI_ERR_NOT_SUPPORTED;   /* 2-4: not restated */
+    for (int r = 0; r < c->size; r++) rcounts[r] = rcount;
+    return reduce_then_scatter(sbuf, rbuf, rcounts, (size_t)rcount * c->size, dt, op, c, 0);   /* basic_linear */
+}
+
+static int tuned_scan_common(const void *sbuf, void *rbuf, int count, struct ompi_datatype_t *dt,
+                             struct ompi_op_t *op, struct ompi_communicator_t *c, int exclusive)
+{
+    int fan;
+    const int alg = tuned_forced(exclusive ? "exscan" : "scan", &fan);
+    return oracle_scan(alg == 2 ? 2 : 1, sbuf, rbuf, count, dt, op, c, exclusive);
+}
+static int tuned_scan(const void *sbuf, void *rbuf, int count, struct ompi_datatype_t *dt, struct ompi_op_t *op,
+                      struct ompi_communicator_t *c, mca_coll_base_module_t *m)
+{
+    (void)m;
+    return tuned_scan_common(sbuf, rbuf, count, dt, op, c, 0);
+}
+static int tuned_exscan(const void *sbuf, void *rbuf, int count, struct ompi_datatype_t *dt, struct ompi_op_t *op,
+                        struct ompi_communicator_t *c, mca_coll_base_module_t *m)
+{
+    (void)m;
+    return tuned_scan_common(sbuf, rbuf, count, dt, op, c, 1);
+}
+
+/* ---- basic ---- */
+static int basic_allreduce(const void *sbuf, void *rbuf, int count, struct ompi_datatype_t *dt, struct ompi_op_t *op,
+                           struct ompi_communicator_t *c, mca_coll_base_module_t *m)
+{
+    (void)m;
+    return reduce_then_bcast(sbuf, rbuf, count, dt, op, c);
+}
+
+static int basic_reduce(const void *sbuf, void *rbuf, int count, struct ompi_datatype_t *dt, struct ompi_op_t *op,
+                        int root, struct ompi_communicator_t *c, mca_coll_base_module_t *m)
+{
+    (void)m;
+    if (c->size > mca_int("coll_basic_crossover", 4)) return OMPI_ERR_NOT_SUPPORTED;   /* log tree: not restated */
+    return oracle_reduce(1, sbuf, rbuf, count, dt, op, root, c, 0);                      /* linear */
+}
+
+static int basic_reduce_scatter(const void *sbuf, void *rbuf, const int *rcounts, struct ompi_datatype_t *dt,
+                                struct ompi_op_t *op, struct ompi_communicator_t *c, mca_coll_base_module_t *m)
+{
+    size_t total = 0;
+    (void)m;
+    for (int r = 0; r < c->size; r++) total += (size_t)rcounts[r];
+    if (total * dt->size < ((size_t)8 << 20)) return oracle_reduce_scatter(2, sbuf, rbuf, rcounts, dt, op, c);
+    return reduce_then_scatter(sbuf, rbuf, rcounts, total, dt, op, c, 0);
+}
+
+static int basic_reduce_scatter_block(const void *sbuf, void *rbuf, int rcount, struct ompi_datatype_t *dt,
+                                      struct ompi_op_t *op, struct ompi_communicator_t *c, mca_coll_base_module_t *m)
+{
+    int rcounts[256];
+    (void)m;
+    if (c->size > 256) return OMPI_ERR_NOT_SUPPORTED;
+    for (int r = 0; r < c->size; r++) rcounts[r] = rcount;
+    return reduce_then_scatter(sbuf, rbuf, rcounts, (size_t)rcount * c->size, dt, op, c, 0);
+}
+
+static int basic_scan(const void *sbuf, void *rbuf, int count, struct ompi_datatype_t *dt, struct ompi_op_t *op,
+                      struct ompi_communicator_t *c, mca_coll_base_module_t *m)
+{
+    (void)m;
+    return oracle_scan(1, sbuf, rbuf, count, dt, op, c, 0);
+}
+static int basic_exscan(const void *sbuf, void *rbuf, int count, struct ompi_datatype_t *dt, struct ompi_op_t *op,
+                        struct ompi_communicator_t *c, mca_coll_base_module_t *m)
+{
+    (void)m;
+    return oracle_scan(1, sbuf, rbuf, count, dt, op, c, 1);
+}
+
+/* ---- libnbc: nonblocking / persistent, complete at post (or MPI_Start) ---- */
 typedef struct {
     int slot;
     const void *sbuf;
@@ -513,22 +801,50 @@ typedef struct {
 static int base_nb_run(const base_nb_t *a)
 {
     switch (a->slot) {
-    case S_IALLREDUCE: return base_allreduce(a->sbuf, a->rbuf, a->count, a->dt, a->op, a->c, NULL);
-    case S_IREDUCE: return base_reduce(a->sbuf, a->rbuf, a->count, a->dt, a->op, a->root, a->c, NULL);
-    case S_IREDUCE_SCATTER: return base_reduce_scatter(a->sbuf, a->rbuf, a->rcounts, a->dt, a->op, a->c, NULL);
-    case S_IREDUCE_SCATTER_BLOCK: return base_reduce_scatter_block(a->sbuf, a->rbuf, a->count, a->dt, a->op, a->c, NULL);
-    case S_ISCAN: return base_scan(a->sbuf, a->rbuf, a->count, a->dt, a->op, a->c, NULL);
-    case S_IEXSCAN: return base_exscan(a->sbuf, a->rbuf, a->count, a->dt, a->op, a->c, NULL);
+    case S_IALLREDUCE:
+        return oracle_allreduce(mca_int("coll_libnbc_iallreduce_algorithm", 0), a->sbuf, a->rbuf, a->count, a->dt,
+                                a->op, a->c, 1);
+    case S_IREDUCE:
+        return oracle_reduce(mca_int("coll_libnbc_ireduce_algorithm", 0), a->sbuf, a->rbuf, a->count, a->dt, a->op,
+                             a->root, a->c, 1);
+    case S_IREDUCE_SCATTER: return oracle_reduce_scatter(-1, a->sbuf, a->rbuf, a->rcounts, a->dt, a->op, a->c);
+    case S_IREDUCE_SCATTER_BLOCK: return oracle_reduce_scatter(-1, a->sbuf, a->rbuf, a->rcounts, a->dt, a->op, a->c);
+    case S_ISCAN: return oracle_scan(1, a->sbuf, a->rbuf, a->count, a->dt, a->op, a->c, 0);
+    case S_IEXSCAN: return oracle_scan(1, a->sbuf, a->rbuf, a->count, a->dt, a->op, a->c, 1);
     case S_IALLGATHER: return base_allgather(a->sbuf, a->scount, a->dt, a->rbuf, a->count, a->rdt, a->c, NULL);
     case S_IBCAST: return base_bcast(a->rbuf, a->count, a->dt, a->root, a->c, NULL);
     }
     return OMPI_ERROR;
 }
+/* Like libnbc, a posted operation does not wait for the peers: it runs (a
+ * blocking exchange over the harness transport) when the process next
+ * progresses -- MPI_Test / MPI_Wait -- in posting order, which every rank
+ * shares (collectives are issued in the same order everywhere). */
+#define NB_PENDING 256
+static struct ompi_request_t *g_nb_pending[NB_PENDING];
+static int g_nb_head, g_nb_tail;
+static int base_nb_progress(void)
+{
+    int done = 0;
+    while (g_nb_head != g_nb_tail) {
+        struct ompi_request_t *r = g_nb_pending[g_nb_head];
+        g_nb_head = (g_nb_head + 1) % NB_PENDING;
+        request_complete(r, base_nb_run(r->ctx));
+        done++;
+    }
+    return done;
+}
+static int base_nb_enqueue(struct ompi_request_t *r)
+{
+    if ((g_nb_tail + 1) % NB_PENDING == g_nb_head) return OMPI_ERR_OUT_OF_RESOURCE;
+    g_nb_pending[g_nb_tail] = r;
+    g_nb_tail = (g_nb_tail + 1) % NB_PENDING;
+    return OMPI_SUCCESS;
+}
 static int base_nb_start(struct ompi_request_t *r)
 {
     request_activate(r);
-    request_complete(r, base_nb_run(r->ctx));
-    return OMPI_SUCCESS;
+    return base_nb_enqueue(r);
 }
 static int base_nb_free(struct ompi_request_t *r)
 {
@@ -542,14 +858,14 @@ static int base_nb_post(const base_nb_t *a, int persistent, struct ompi_request_
     base_nb_t *h = malloc(sizeof *h);
     if (!h) return OMPI_ERR_OUT_OF_RESOURCE;
     *h = *a;
-    if (a->rcounts) {
+    if (a->rcounts || a->slot == S_IREDUCE_SCATTER_BLOCK) {
         h->rcounts = malloc(sizeof(int) * (size_t)a->c->size);
         if (!h->rcounts) { free(h); return OMPI_ERR_OUT_OF_RESOURCE; }
-        memcpy(h->rcounts, a->rcounts, sizeof(int) * (size_t)a->c->size);
+        for (int r = 0; r < a->c->size; r++) h->rcounts[r] = a->rcounts ? a->rcounts[r] : a->count;
     }
     *request = request_create(persistent, base_nb_start, base_nb_free, h);
     if (!*request) { free(h->rcounts); free(h); return OMPI_ERR_OUT_OF_RESOURCE; }
-    if (!persistent) request_complete(*request, base_nb_run(h));
+    if (!persistent) return base_nb_enqueue(*request);
     return OMPI_SUCCESS;
 }
 #define NB(...) base_nb_t a_ = {__VA_ARGS__}
@@ -669,7 +985,11 @@ static int base_bcast_init(void *buf, int count, struct ompi_datatype_t *dt, int
 }
 #undef NB
 
-static mca_coll_base_module_t g_base_coll;   /* static, never freed */
+/* modules: static, one of each (stateless), with the reference's class names */
+static mx_obj_class_t g_tuned_class = {"mca_coll_tuned_module_t", NULL};
+static mx_obj_class_t g_basic_class = {"mca_coll_basic_module_t", NULL};
+static mx_obj_class_t g_libnbc_class = {"ompi_coll_libnbc_module_t", NULL};
+static mca_coll_base_module_t g_tuned_coll, g_basic_coll, g_libnbc_coll;
 static mca_coll_base_module_t g_self_coll;
 
 static ompi_op_base_component_1_0_0_t *g_op_comp;
@@ -722,34 +1042,32 @@ static int op_select(struct ompi_op_t *op)
     return 0;
 }
 
-/* mca_coll_base_comm_select (coll_base_comm_select.c:108-309) */
+/* --mca coll ^a,b (mca_base_components_filter): excluded component names */
+static int coll_excluded(const char *name)
+{
+    const char *v = mca_string("coll");
+    if (!v || v[0] != '^') return 0;
+    const size_t l = strlen(name);
+    for (const char *p = v + 1; *p;) {
+        const char *e = strchr(p, ',');
+        const size_t k = e ? (size_t)(e - p) : strlen(p);
+        if (k == l && !strncmp(p, name, l)) return 1;
+        p += k + (e ? 1 : 0);
+    }
+    return 0;
+}
+
+static void static_module(mca_coll_base_module_t *b, mx_obj_class_t *cls)
+{
+    b->super.obj_class = cls;
+    b->super.obj_reference_count = 1000000;
+}
+
+/* mca_coll_base_comm_select (coll_base_comm_select.c:108-309): modules
+ * enabled lowest priority first, each non-NULL slot copied over */
 static int comm_select(struct ompi_communicator_t *c, int is_self)
 {
-    mca_coll_base_module_t *base = is_self ? &g_self_coll : &g_base_coll;
     memset(c->fn, 0, sizeof c->fn);
-    base->super.obj_class = &g_static_class;
-    base->super.obj_reference_count = 1000000;
-    if (is_self) {
-        base->coll_reduce_local = base_reduce_local;
-    } else {
-        base->coll_allreduce = base_allreduce;
-        base->coll_reduce_scatter = base_reduce_scatter;
-        base->coll_allgather = base_allgather;
-        base->coll_bcast = base_bcast;
-        base->coll_reduce_local = base_reduce_local;
-        base->coll_reduce = base_reduce;
-        base->coll_reduce_scatter_block = base_reduce_scatter_block;
-        base->coll_scan = base_scan;
-        base->coll_exscan = base_exscan;
-#define SET_BASE_NB(name) base->coll_##name = base_##name;
-        SET_BASE_NB(iallreduce) SET_BASE_NB(ireduce) SET_BASE_NB(ireduce_scatter) SET_BASE_NB(ireduce_scatter_block)
-        SET_BASE_NB(iscan) SET_BASE_NB(iexscan) SET_BASE_NB(iallgather) SET_BASE_NB(ibcast)
-        SET_BASE_NB(allreduce_init) SET_BASE_NB(reduce_init) SET_BASE_NB(reduce_scatter_init)
-        SET_BASE_NB(reduce_scatter_block_init) SET_BASE_NB(scan_init) SET_BASE_NB(exscan_init)
-        SET_BASE_NB(allgather_init) SET_BASE_NB(bcast_init)
-#undef SET_BASE_NB
-    }
-    /* lowest priority first: the base module (30 / 75) */
 #define COPY(MOD, OWNER)                                                                             \
     do {                                                                                             \
         void *f_[NSLOTS] = {(void *)(MOD)->coll_allreduce, (void *)(MOD)->coll_reduce_scatter,       \
@@ -768,11 +1086,61 @@ static int comm_select(struct ompi_communicator_t *c, int is_self)
         for (int i_ = 0; i_ < NSLOTS; i_++)                                                          \
             if (f_[i_]) { c->fn[i_] = f_[i_]; c->mod[i_] = (MOD); c->owner[i_] = (OWNER); }          \
     } while (0)
-    COPY(base, is_self ? "self" : "base");
-    if (g_coll_comp) {
+    int base_prio = 30;
+    if (is_self) {
+        mca_coll_base_module_t *b = &g_self_coll;
+        static_module(b, &g_static_class);
+        b->coll_reduce_local = base_reduce_local;
+        COPY(b, "self");
+        base_prio = 75;
+    } else {
+        /* basic (10): every blocking slot (coll_basic_module.c:92-128) */
+        mca_coll_base_module_t *b = &g_basic_coll;
+        memset(b, 0, sizeof *b);
+        static_module(b, &g_basic_class);
+        b->coll_allreduce = basic_allreduce;
+        b->coll_reduce_scatter = basic_reduce_scatter;
+        b->coll_allgather = base_allgather;
+        b->coll_bcast = base_bcast;
+        b->coll_reduce_local = base_reduce_local;
+        b->coll_reduce = basic_reduce;
+        b->coll_reduce_scatter_block = basic_reduce_scatter_block;
+        b->coll_scan = basic_scan;
+        b->coll_exscan = basic_exscan;
+        if (!coll_excluded("basic")) COPY(b, "basic");
+        /* libnbc (10): the nonblocking and persistent slots */
+        b = &g_libnbc_coll;
+        memset(b, 0, sizeof *b);
+        static_module(b, &g_libnbc_class);
+#define SET_BASE_NB(name) b->coll_##name = base_##name;
+        SET_BASE_NB(iallreduce) SET_BASE_NB(ireduce) SET_BASE_NB(ireduce_scatter) SET_BASE_NB(ireduce_scatter_block)
+        SET_BASE_NB(iscan) SET_BASE_NB(iexscan) SET_BASE_NB(iallgather) SET_BASE_NB(ibcast)
+        SET_BASE_NB(allreduce_init) SET_BASE_NB(reduce_init) SET_BASE_NB(reduce_scatter_init)
+        SET_BASE_NB(reduce_scatter_block_init) SET_BASE_NB(scan_init) SET_BASE_NB(exscan_init)
+        SET_BASE_NB(allgather_init) SET_BASE_NB(bcast_init)
+#undef SET_BASE_NB
+        if (!coll_excluded("libnbc")) COPY(b, "libnbc");
+        /* tuned (30): intra-communicators only (coll_tuned_module.c:66-69);
+         * scan / exscan only when dynamic rules force them (:235-238) */
+        b = &g_tuned_coll;
+        memset(b, 0, sizeof *b);
+        static_module(b, &g_tuned_class);
+        b->coll_allreduce = tuned_allreduce;
+        b->coll_reduce_scatter = tuned_reduce_scatter;
+        b->coll_allgather = base_allgather;
+        b->coll_bcast = base_bcast;
+        b->coll_reduce = tuned_reduce;
+        b->coll_reduce_scatter_block = tuned_reduce_scatter_block;
+        {
+            int fan;
+            if (tuned_forced("scan", &fan)) b->coll_scan = tuned_scan;
+            if (tuned_forced("exscan", &fan)) b->coll_exscan = tuned_exscan;
+        }
+        if (!coll_excluded("tuned") && !comm_is_inter(c)) COPY(b, "tuned");
+    }
+    if (g_coll_comp && !coll_excluded("mi355x")) {
         int prio = 0;
         mca_coll_base_module_t *m = g_coll_comp->collm_comm_query(c, &prio);
-        const int base_prio = is_self ? 75 : 30;
         if (m) {
             if (prio > base_prio && (!m->coll_module_enable || m->coll_module_enable(m, c) == OMPI_SUCCESS)) {
                 COPY(m, "mi355x");
@@ -816,7 +1184,14 @@ int mxh_init(const char *component_lib, mxh_reducer_t base, mxh_pattern_t patter
     g_host.dtype_unpack = dtype_unpack;
     g_host.dtype_span = dtype_span;
     g_host.dtype_desc = getenv("MXH_NO_DTYPE_DESC") ? NULL : dtype_desc;
+    g_host.comm_is_inter = comm_is_inter;
+    g_host.mca_string = mca_string;
+    g_host.request_test = inner_test;
+    g_host.request_start = inner_start;
+    g_host.request_free = inner_free;
     g_nprogress = 0;
+    g_nb_head = g_nb_tail = 0;
+    progress_register(base_nb_progress);
     g_op_comp = NULL;
     g_coll_comp = NULL;
     if (component_lib && *component_lib) {
@@ -862,6 +1237,21 @@ void *mxh_comm_create(int rank, int size, mxh_allgather_t ag, void *ctx)
     c->ag = ag;
     c->ag_ctx = ctx;
     comm_select(c, size == 1);
+    return c;
+}
+
+/* an intercommunicator (local group of `size`): only its selection is
+ * modelled -- which components take it */
+void *mxh_intercomm_create(int rank, int size, mxh_allgather_t ag, void *ctx)
+{
+    struct ompi_communicator_t *c = calloc(1, sizeof *c);
+    if (!c) return NULL;
+    c->rank = rank;
+    c->size = size;
+    c->inter = 1;
+    c->ag = ag;
+    c->ag_ctx = ctx;
+    comm_select(c, 0);
     return c;
 }
 

@@ -14,9 +14,14 @@
  *     through comm->c_coll;
  *   - requests (ompi/request/request.h:125-139), opal_progress_register and
  *     MPI_Start / MPI_Test / MPI_Wait / MPI_Request_free;
- *   - a host "base" coll module standing in for coll/tuned + basic on host
- *     buffers, and a coll/self-like module (priority 75) for COMM_SELF.
- * The base op functions and the host transport are injected by the test.
+ *   - host coll modules standing in for coll/tuned (30), coll/basic (10) and
+ *     coll/libnbc (10) on host buffers, under the reference's class names,
+ *     their algorithms evaluated by the injected oracle restatement (and
+ *     coll/base's compositions through the communicator's current slots),
+ *     and a coll/self-like module (priority 75) for COMM_SELF;
+ *   - --mca coll ^name exclusion, intercommunicator selection.
+ * The base op functions, the collective oracle and the host transport are
+ * injected by the test.
  */
 #ifndef MX_HOST_H
 #define MX_HOST_H
@@ -26,17 +31,35 @@
 extern "C" {
 #endif
 
-/* base op kernels injected by the test: the reference's own
- * op_base_functions.c (oracle/_ref) or the oracle restatement */
+/* base op kernels injected by the test: the oracle restatement of
+ * op_base_functions.c (oracle/mx_oracle_op.c) */
 typedef int (*mxh_reducer_t)(int op, int type, const void *in, void *inout, size_t n, int fortran);
 typedef int (*mxh_pattern_t)(int op, int type, int fortran);
 /* host transport: allgather `bytes` per rank (rank-major) */
 typedef int (*mxh_allgather_t)(const void *send, void *recv, size_t bytes, void *ctx);
 
+/* the collective oracle (oracle/mx_oracle_coll.c entry points) the host
+ * modules evaluate their algorithms with */
+typedef struct {
+    int (*allreduce)(int alg, int op, int type, int n, size_t count, const void *const *sbufs, void *const *rbufs);
+    int (*reduce_scatter)(int alg, int op, int type, int n, const size_t *rcounts, const void *const *sbufs,
+                          void *const *rbufs);
+    int (*reduce)(int alg, int op, int type, int n, size_t count, int root, const void *const *sbufs, void *rbuf);
+    int (*scan)(int alg, int op, int type, int n, size_t count, const void *const *sbufs, void *const *rbufs);
+    int (*exscan)(int alg, int op, int type, int n, size_t count, const void *const *sbufs, void *const *rbufs);
+    int (*iallreduce)(int alg, int op, int type, int n, size_t count, const void *const *sbufs, void *const *rbufs);
+    int (*ireduce)(int alg, int op, int type, int n, size_t count, int root, const void *const *sbufs, void *rbuf);
+    int (*ireduce_scatter)(int op, int type, int n, const size_t *rcounts, const void *const *sbufs,
+                           void *const *rbufs);
+} mxh_coll_oracle_t;
+int mxh_set_coll_oracle(const mxh_coll_oracle_t *o);
+
 int mxh_init(const char *component_lib, mxh_reducer_t base, mxh_pattern_t pattern);
 int mxh_finalize(void);
 /* MCA variable (OMPI_MCA_<name>), e.g. "coll_mi355x_priority" */
 int mxh_set_mca(const char *name, int value);
+/* string MCA variable (e.g. "coll" = "^tuned", coll_tuned_dynamic_rules_filename); NULL unsets */
+int mxh_set_mca_str(const char *name, const char *value);
 
 void *mxh_dtype(const char *mpi_name);   /* MPI_FLOAT, MPI_2INT, ...; NULL if unknown */
 void *mxh_dtype_contiguous(int count, void *oldtype);  /* MPI_Type_contiguous */
@@ -47,8 +70,11 @@ int mxh_op_slot_owner(void *op, int type, int three_buffer);
 
 void *mxh_comm_create(int rank, int size, mxh_allgather_t ag, void *ctx);
 void *mxh_comm_self(void);
+/* an intercommunicator whose local group has `size` ranks (selection only) */
+void *mxh_intercomm_create(int rank, int size, mxh_allgather_t ag, void *ctx);
 int mxh_comm_free(void *comm);
-/* name of the component whose module owns a coll slot ("mi355x", "base", "self") */
+/* name of the component whose module owns a coll slot ("mi355x", "tuned",
+ * "basic", "libnbc", "self") */
 const char *mxh_comm_slot_owner(void *comm, const char *slot);
 
 int mxh_op_reduce(void *op, const void *source, void *target, int count, void *dtype);

@@ -389,6 +389,23 @@ typedef struct mx_ompi_host {
      * (or an error return): device spans go through the host as above. */
     int (*dtype_desc)(struct ompi_datatype_t *dt, const void **recs, size_t *nrec, size_t *size, ptrdiff_t *lb,
                       ptrdiff_t *ub);
+    /* ---- round 3 ----
+     * comm_is_inter: OMPI_COMM_IS_INTER(comm) (communicator.h); every coll
+     *   component on this path declines intercommunicators
+     *   (coll_tuned_module.c:66-69, coll_cuda_module.c:141);
+     * mca_string: string MCA variable (coll_tuned_dynamic_rules_filename),
+     *   NULL if unset;
+     * requests of the saved module, driven by the component when it runs a
+     *   nonblocking collective on host copies of device buffers:
+     *   request_test = REQUEST_COMPLETE(req) + req_status.MPI_ERROR, without
+     *   progressing or freeing (the component polls from its own progress
+     *   callback); request_start = req->req_start(1, &req) (MPI_Start);
+     *   request_free = ompi_request_free(&req). */
+    int (*comm_is_inter)(struct ompi_communicator_t *comm);
+    const char *(*mca_string)(const char *name);
+    int (*request_test)(struct ompi_request_t *req, int *flag, int *status);
+    int (*request_start)(struct ompi_request_t *req);
+    int (*request_free)(struct ompi_request_t **req);
 } mx_ompi_host_t;
 
 /* Set by the host before component queries. */

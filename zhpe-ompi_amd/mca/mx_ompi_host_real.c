@@ -20,7 +20,12 @@
  *                                op->o_func.intrinsic, op->o_3buff_intrinsic
  *   comm_coll_fn                 comm->c_coll->coll_<slot> and its module
  *   obj_retain / obj_release     OBJ_RETAIN / OBJ_RELEASE
- *   mca_int                      mca_base_var_find + mca_base_var_get_value
+ *   mca_int / mca_string         mca_base_var_find + mca_base_var_get_value
+ *                                (bool, int and string variables)
+ *   comm_is_inter                OMPI_COMM_IS_INTER
+ *   request_test/_start/_free    REQUEST_COMPLETE + req_status, req_start,
+ *                                ompi_request_free (the saved module's
+ *                                requests, driven by the component)
  *   requests                     an ompi_request_t subclass carrying the
  *                                component's context, like
  *                                ompi_coll_libnbc_request_t
@@ -146,19 +151,54 @@ static void *h_coll(struct ompi_communicator_t *c, const char *slot, struct mca_
 static void h_retain(opal_object_t *o) { OBJ_RETAIN(o); }
 static void h_release(opal_object_t *o) { OBJ_RELEASE(o); }
 
-/* "coll_mi355x_<var>" / "op_mi355x_<var>" / "coll_libnbc_<var>" */
-static int h_mca_int(const char *name, int def)
+/* "coll_mi355x_<var>" / "op_mi355x_<var>" / "coll_libnbc_<var>" /
+ * "coll_tuned_<var>" / "coll_basic_<var>": framework, component, variable */
+static int h_var(const char *name)
 {
     char fw[16] = "", comp[16] = "";
     const char *u1 = strchr(name, '_'), *u2 = u1 ? strchr(u1 + 1, '_') : NULL;
-    if (!u1 || !u2 || (size_t)(u1 - name) >= sizeof fw || (size_t)(u2 - u1 - 1) >= sizeof comp) return def;
+    if (!u1 || !u2 || (size_t)(u1 - name) >= sizeof fw || (size_t)(u2 - u1 - 1) >= sizeof comp) return -1;
     memcpy(fw, name, (size_t)(u1 - name));
     memcpy(comp, u1 + 1, (size_t)(u2 - u1 - 1));
-    const int idx = mca_base_var_find("ompi", fw, comp, u2 + 1);
-    const int *p = NULL;
-    if (idx >= 0 && OPAL_SUCCESS == mca_base_var_get_value(idx, &p, NULL, NULL) && p) return *p;
-    return def;
+    return mca_base_var_find("ompi", fw, comp, u2 + 1);
 }
+static int h_mca_int(const char *name, int def)
+{
+    const int idx = h_var(name);
+    const mca_base_var_t *var = NULL;
+    const void *p = NULL;
+    if (idx < 0 || OPAL_SUCCESS != mca_base_var_get(idx, &var) || !var ||
+        OPAL_SUCCESS != mca_base_var_get_value(idx, &p, NULL, NULL) || !p)
+        return def;
+    switch (var->mbv_type) {   /* coll_tuned_use_dynamic_rules is a bool */
+    case MCA_BASE_VAR_TYPE_BOOL: return *(const bool *)p ? 1 : 0;
+    case MCA_BASE_VAR_TYPE_INT: case MCA_BASE_VAR_TYPE_UNSIGNED_INT: return *(const int *)p;
+    default: return def;
+    }
+}
+static const char *h_mca_string(const char *name)
+{
+    const int idx = h_var(name);
+    const mca_base_var_t *var = NULL;
+    const char *const *p = NULL;
+    if (idx < 0 || OPAL_SUCCESS != mca_base_var_get(idx, &var) || !var || var->mbv_type != MCA_BASE_VAR_TYPE_STRING ||
+        OPAL_SUCCESS != mca_base_var_get_value(idx, &p, NULL, NULL) || !p)
+        return NULL;
+    return *p;
+}
+
+static int h_is_inter(struct ompi_communicator_t *c) { return OMPI_COMM_IS_INTER(c) ? 1 : 0; }
+
+/* the saved module's requests (the component polls them from its progress
+ * callback, so no progress and no free here) */
+static int h_inner_test(struct ompi_request_t *r, int *flag, int *status)
+{
+    *flag = REQUEST_COMPLETE(r) ? 1 : 0;
+    *status = *flag ? r->req_status.MPI_ERROR : OMPI_SUCCESS;
+    return OMPI_SUCCESS;
+}
+static int h_inner_start(struct ompi_request_t *r) { return r->req_start(1, &r); }
+static int h_inner_free(struct ompi_request_t **r) { return ompi_request_free(r); }
 
 /* requests of the nonblocking / persistent slots */
 typedef struct {
@@ -250,5 +290,10 @@ int mx_ompi_host_real_register(void)
     real_host.dtype_unpack = h_unpack;
     real_host.dtype_span = h_span;
     real_host.dtype_desc = h_desc;
+    real_host.comm_is_inter = h_is_inter;
+    real_host.mca_string = h_mca_string;
+    real_host.request_test = h_inner_test;
+    real_host.request_start = h_inner_start;
+    real_host.request_free = h_inner_free;
     return mx_ompi_set_host(&real_host);
 }
