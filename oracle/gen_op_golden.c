@@ -7,14 +7,17 @@
  * Fortran types: 176 pairs), seeded inputs and the outputs of the C
  * restatement oracle/mx_oracle_op.c (mxo_reduce2 / mxo_reduce3).
  *
- * Provenance: the committed tests/golden/op_vectors.bin was first written in
- * round 1 by this generator linked against op_base_functions.c itself,
+ * Provenance: the committed tests/golden/op_vectors.bin is the round-1
+ * file, written by this generator linked against op_base_functions.c itself,
  * compiled through configuration stand-ins; that build is retired (a
  * reference build through stand-ins pins nothing).  Regenerated from the
- * restatement the file is byte-identical, so the restatement reproduces
- * those outputs exactly -- including every NaN payload -- but the vectors
- * remain regression vectors of our own restatement: the reference holds no
- * known answers for these kernels, op-kernel parity is
+ * restatement the file differs in ONE NaN payload: C_DOUBLE_COMPLEX SUM
+ * (op 3, type 28), output element 42, imaginary part -- the round-1 build
+ * kept the default quiet NaN 0x7ff8000000000000, the restatement keeps the
+ * other operand's signalling NaN quieted (0x7ffc000000000001): the
+ * operand order of NaN + NaN is the host compiler's choice.  Every other
+ * byte agrees.  The vectors remain regression vectors: the reference holds
+ * no known answers for these kernels, op-kernel parity is
  * unpinned.
  *
  * Output: tests/golden/op_vectors.bin (little endian):

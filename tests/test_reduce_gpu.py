@@ -1,7 +1,8 @@
-"""GPU parity: the HIP op kernels (K1-K4) vs the reference.
+"""GPU parity: the HIP op kernels (K1-K4) vs the oracle restatement.
 
-* every golden record (all 176 (op,type) pairs, 2- and 3-buffer, generated
-  by the reference's own op_base_functions.c) through mx_reduce2/3;
+* every golden record (all 176 (op,type) pairs, 2- and 3-buffer;
+  tests/golden/op_vectors.bin, written by oracle/gen_op_golden.c -- value
+  parity with the reference is unpinned) through mx_reduce2/3;
 * ragged counts and misaligned sub-buffers (the head/tail and element
   paths) vs the oracle restatement;
 * full-size (1 GiB) fp32 SUM vs the oracle (CFG-B).

@@ -421,6 +421,57 @@ extern "C" int mx_comm_create(int rank, int size, int device, size_t staging_byt
   return mx_comm_create_ex(rank, size, device, staging_bytes, 0, flags, ag, ctx, out);
 }
 
+// IPC-exported regions (staging, flags, heap region) outlive their
+// communicator in a process-wide pool.  Ranks destroy a communicator at
+// different times, so a peer may still map this rank's region when the
+// rank frees it, and the runtime then refused to export a new allocation
+// made in that place: hipIpcGetMemHandle failed (hsa_status 0x1000) on the
+// next communicator's staging in 8-process runs that create and free
+// communicators back to back.  A destroyed communicator's regions therefore
+// go back to the pool and the next communicator reuses them (same
+// allocation, same handle) instead of freeing and reallocating.
+static std::mutex g_ipc_pool_mu;
+static std::vector<std::pair<char *, size_t>> g_ipc_pool;
+
+static int ipc_region_alloc(size_t bytes, char **p) {
+  {
+    std::lock_guard<std::mutex> lk(g_ipc_pool_mu);
+    size_t best = (size_t)-1;
+    for (size_t i = 0; i < g_ipc_pool.size(); i++)   // smallest pooled region that fits, at most 2x
+      if (g_ipc_pool[i].second >= bytes && g_ipc_pool[i].second <= 2 * bytes &&
+          (best == (size_t)-1 || g_ipc_pool[i].second < g_ipc_pool[best].second))
+        best = i;
+    if (best != (size_t)-1) {
+      *p = g_ipc_pool[best].first;
+      g_ipc_pool.erase(g_ipc_pool.begin() + (long)best);
+      return MX_SUCCESS;
+    }
+  }
+  if (hipExtMallocWithFlags((void **)p, bytes, hipDeviceMallocUncached) != hipSuccess) {
+    (void)hipGetLastError();
+    *p = nullptr;
+    return MX_ERR_NOMEM;
+  }
+  return MX_SUCCESS;
+}
+
+static size_t ipc_region_size(const char *p) {
+  void *base = nullptr;
+  size_t size = 0;
+  if (hipMemGetAddressRange(&base, &size, (void *)p) != hipSuccess) {
+    (void)hipGetLastError();
+    return 0;
+  }
+  return size;
+}
+
+static void ipc_region_free(char *p) {
+  if (!p) return;
+  const size_t size = ipc_region_size(p);
+  std::lock_guard<std::mutex> lk(g_ipc_pool_mu);
+  g_ipc_pool.emplace_back(p, size);
+}
+
 // Every bootstrap exchange runs on every rank whatever happened locally:
 // each carries this rank's verdict so far, and the communicator exists only
 // if every rank says yes -- so either all ranks get one or none does (a rank
@@ -475,11 +526,10 @@ extern "C" int mx_comm_create_ex(int rank, int size, int device, size_t staging_
       c->p2p_off = (c->staging_bytes + 4095) & ~(size_t)4095;
       const uint64_t sig[2] = {0x5EED0000ull + (uint64_t)rank, 0x5EED1000ull + (uint64_t)rank};
       const size_t boxes = (flags & MX_COMM_P2P) ? (size_t)size * P2P_BOX : 0;
-      ok = hipExtMallocWithFlags((void **)&c->staging, c->p2p_off + boxes, hipDeviceMallocUncached) == hipSuccess &&
-           hipExtMallocWithFlags((void **)&c->flagmem, ALL_FLAG_WORDS * sizeof(uint64_t), hipDeviceMallocUncached) ==
-               hipSuccess &&
-           (!c->hregion_bytes ||
-            hipExtMallocWithFlags((void **)&c->hregion, c->hregion_bytes, hipDeviceMallocUncached) == hipSuccess) &&
+      c->staging_alloc = c->p2p_off + boxes;
+      ok = ipc_region_alloc(c->staging_alloc, &c->staging) == MX_SUCCESS &&
+           ipc_region_alloc(ALL_FLAG_WORDS * sizeof(uint64_t), (char **)&c->flagmem) == MX_SUCCESS &&
+           (!c->hregion_bytes || ipc_region_alloc(c->hregion_bytes, &c->hregion) == MX_SUCCESS) &&
            hipMemset(c->flagmem, 0, ALL_FLAG_WORDS * sizeof(uint64_t)) == hipSuccess &&
            hipDeviceSynchronize() == hipSuccess &&
            hipIpcGetMemHandle(&mine.staging, c->staging) == hipSuccess &&
@@ -489,6 +539,7 @@ extern "C" int mx_comm_create_ex(int rank, int size, int device, size_t staging_
            hipMemcpy(c->flagmem + FLAG_WORDS, sig, sizeof sig, hipMemcpyHostToDevice) == hipSuccess &&
            (!c->hregion || hipMemcpy(c->hregion, sig + 1, 8, hipMemcpyHostToDevice) == hipSuccess) &&
            hipDeviceSynchronize() == hipSuccess;
+      if (!ok) (void)hipGetLastError();   // a failed export must not surface at a later launch
       mine.staging_bytes = c->staging_bytes;
       mine.hregion_bytes = c->hregion_bytes;
     } else {
@@ -604,9 +655,9 @@ extern "C" int mx_comm_destroy(mx_comm_t *c) {
     if (c->peer_flags[p]) (void)hipIpcCloseMemHandle(c->peer_flags[p]);
     if (c->peer_hregion[p]) (void)hipIpcCloseMemHandle(c->peer_hregion[p]);
   }
-  if (c->staging) (void)hipFree(c->staging);
-  if (c->hregion) (void)hipFree(c->hregion);
-  if (c->flagmem) (void)hipFree(c->flagmem);
+  ipc_region_free(c->staging);
+  ipc_region_free(c->hregion);
+  ipc_region_free((char *)c->flagmem);
   if (c->err_host) (void)hipHostFree(c->err_host);
   if (c->poison) (void)hipFree(c->poison);
   if (c->nccl) ncclCommDestroy(c->nccl);
@@ -3162,12 +3213,22 @@ static inline bool fast_done(const mx_request *q) {
   return q->fast && q->status && __atomic_load_n(&q->status[4], __ATOMIC_ACQUIRE) != 0;
 }
 
+// A rendezvous send completes only through its status word; a communicator
+// error (a device wait that timed out, a corrupt channel) or poisoning ends
+// the host's wait too, with that error.
+static inline int rndv_failed(const mx_request *q) {
+  const mx_comm *c = q->c;
+  if (c->poisoned) return c->poisoned;
+  return c->err_host ? *(volatile int *)c->err_host : 0;
+}
+
 extern "C" int mx_test(mx_request_t *q, int *flag) {
   if (!q || !flag) return MX_ERR_ARG;
   *flag = 1;
   if (!q->active) return MX_SUCCESS;   // completed or inactive persistent: MPI_Test gives true
   if (fast_done(q)) return req_complete(q);
   if (q->fast == 2) {                  // a rendezvous send: only its status word tells
+    if (rndv_failed(q)) return req_complete(q);
     *flag = 0;
     return MX_SUCCESS;
   }
@@ -3194,6 +3255,7 @@ extern "C" int mx_wait(mx_request_t *q) {
       if (fast_done(q)) return req_complete(q);
       if (std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0).count() > kWaitSpinUs) {
         if (q->fast != 2) break;
+        if (rndv_failed(q)) return req_complete(q);
         std::this_thread::sleep_for(std::chrono::microseconds(20));   // a rendezvous send: no event to block on
       }
     }
@@ -3213,7 +3275,10 @@ extern "C" int mx_request_stream_wait(mx_request_t *q, void *stream) {
   if (!q) return MX_ERR_ARG;
   if (!q->active) return MX_SUCCESS;
   if (q->fast == 2) {   // a rendezvous send has no event: the host waits for its status word
-    while (!fast_done(q)) std::this_thread::sleep_for(std::chrono::microseconds(20));
+    while (!fast_done(q)) {
+      if (const int e = rndv_failed(q)) return e;
+      std::this_thread::sleep_for(std::chrono::microseconds(20));
+    }
     return MX_SUCCESS;
   }
   return hipStreamWaitEvent((hipStream_t)stream, q->done, 0) == hipSuccess ? MX_SUCCESS : MX_ERR_HIP;

@@ -119,6 +119,7 @@ struct mx_comm {
   int rank, size, device, local;
   int flags;
   size_t staging_bytes;
+  size_t staging_alloc;        // bytes of the staging allocation (+ mailboxes)
   size_t main_bytes;           // staging for the chunked paths: [0, main_bytes)
   size_t os_max, os_slot;      // one-shot: max bytes per rank, slot stride
   uint64_t os_count;           // one-shot workgroup completions so far

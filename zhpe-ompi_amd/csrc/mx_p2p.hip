@@ -296,6 +296,14 @@ __device__ __forceinline__ void rndv_pick(const P2PRndvArgs &a) {
     __hip_atomic_store(&c.gen, a.gen, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
   __syncthreads();   // the rest of this workgroup reads the pick too
+  // aborted (communicator teardown) or a CTS for no pending send: release
+  // every pending send as the timeout does, so no waiter sleeps forever on
+  // a status word nobody will raise (their requests complete with err)
+  if (d == -2 || (d >= 0 && s_hit < 0)) {
+    for (int i = threadIdx.x; i < P2P_RNDV_Q; i += blockDim.x)
+      if (a.tab->e[i].valid)
+        __hip_atomic_store(a.tab->e[i].done, (int64_t)1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
 }
 
 // one workgroup per rendezvous lane (workgroup 0 also picks); the last lane

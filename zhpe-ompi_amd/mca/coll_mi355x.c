@@ -159,8 +159,14 @@ typedef struct {
     X(ibcast) X(allreduce_init) X(reduce_init) X(reduce_scatter_init) X(reduce_scatter_block_init)        \
     X(scan_init) X(exscan_init) X(allgather_init) X(bcast_init)
 
+/* coll_mi355x_verbose > 0: device-path failures are reported on stderr */
+static int g_verbose = -1;
 static int map_rc(int rc)
 {
+    if (rc != MX_SUCCESS) {
+        if (g_verbose < 0) g_verbose = mx_ompi_host ? mx_ompi_host->mca_int("coll_mi355x_verbose", 0) : 0;
+        if (g_verbose > 0) fprintf(stderr, "coll/mi355x: %s (%d)\n", mx_strerror(rc), rc);
+    }
     switch (rc) {
     case MX_SUCCESS: return OMPI_SUCCESS;
     case MX_ERR_NOMEM: return OMPI_ERR_OUT_OF_RESOURCE;
