@@ -173,6 +173,12 @@ def bench_allreduce(torch, mx, dist, rank, world, dev, steps, warmup, nbytes=256
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         return float(t[0])
 
+    # the autotuner's trial calls for this size class run before the warmup
+    # (untimed; a few calls: warm-up + one per candidate)
+    tune_calls = 0
+    while comm.tuning(nbytes) is None and tune_calls < 16 and world > 1:
+        comm.allreduce(x.data_ptr(), out.data_ptr(), count, "FLOAT", "SUM", "auto", sp)
+        tune_calls += 1
     for _ in range(warmup):
         comm.allreduce(x.data_ptr(), out.data_ptr(), count, "FLOAT", "SUM", "auto", sp)
     t_max = timed("auto", steps)
@@ -220,8 +226,19 @@ def bench_allreduce(torch, mx, dist, rank, world, dev, steps, warmup, nbytes=256
             proto_ab[name]["parity"] = "ok" if all(h == exp_sha for h in hs) else \
                 f"MISMATCH on ranks {[r for r in range(world) if hs[r] != exp_sha]}"
     comm.set_protocol(proto_default)
+    try:   # the sweep and CFG-E run with the defaults: autotuning on, zero-copy from 256 KiB
+        comm.set_reg_min(256 << 10)
+        comm.set_autotune(True)
+    except mx.MxError:
+        pass
     sweep = allreduce_sweep(torch, mx, dist, comm, world, x, out, sp, flags)
     cfge = cfg_e(torch, mx, dist, comm, world, rank, sp)
+    # the data paths the autotuner kept per size class: where the
+    # one-shot / zero-copy / staged crossovers fell on this machine
+    tuned = {coll: {str(b): comm.tuning(b, coll) for b in (64 << 10, 256 << 10, 1 << 20, 4 << 20, 16 << 20,
+                                                           256 << 20)}
+             for coll in ("allreduce", "reduce_scatter", "allgather", "bcast")}
+    tuned = {coll: {b: v for b, v in d.items() if v is not None} for coll, d in tuned.items()}
     extra = {}
     if flags & mx.COMM_RCCL:
         try:
@@ -245,6 +262,7 @@ def bench_allreduce(torch, mx, dist, rank, world, dev, steps, warmup, nbytes=256
                    "count": count, "bytes": nbytes, "algorithm": "auto",
                    "parallelism": f"allreduce-{world}", "algbw_gbs": round(algbw, 2),
                    "data_path_ab": proto_ab,
+                   "autotune_calls_before_warmup": tune_calls, "autotuned_paths": tuned,
                    "busbw_formula": "algbw*2(n-1)/n", **extra},
         # N>1 is bound by the xGMI links, not HBM: the all-peer exchange puts
         # 2S/n on each of a rank's n-1 links, so the busBW ceiling is
@@ -365,8 +383,11 @@ def allreduce_sweep(torch, mx, dist, comm, world, x, out, sp, flags, budget_s=45
                 if alg == "rccl" and t == "UINT16_T":
                     continue
                 ok = torch.tensor([1.0])
+                # warm-up; the first call of a size class also runs the
+                # autotuner's trials (13 calls below 4 MiB, 4 above, from 64 KiB)
+                warm = 2 + ((13 if nbytes < (4 << 20) else 4) if nbytes >= (64 << 10) and alg == algs[0] else 0)
                 try:
-                    for _ in range(2):
+                    for _ in range(warm):
                         comm.allreduce(bx.data_ptr(), bo.data_ptr(), count, t, op, alg, sp)
                     torch.cuda.synchronize()
                 except mx.MxError:
@@ -412,7 +433,8 @@ def cfg_e(torch, mx, dist, comm, world, rank, sp, nbytes=256 << 20, iters=5):
 
     def timed(name, fn, algbw_bytes, factor):
         try:
-            fn()
+            for _ in range(4):   # warm-up + the autotuner's trials of this size class
+                fn()
             torch.cuda.synchronize()
             dist.barrier()
             t0 = time.perf_counter()

@@ -127,16 +127,24 @@ int mx_comm_set_reg_min(mx_comm_t *comm, size_t min_bytes);
 
 /* Autotuning of the data movement (default on when the registration page
  * exists and neither MX_ALLREDUCE_PROTO nor MX_REG_MIN forces a path;
- * MX_AUTOTUNE=0 switches it off): per power-of-two size class of blocking
- * allreduces >= 4 MiB per rank, the first call runs the defaults, the next
- * three run zero-copy, staged PULL and staged PUSH (reduce_scatter and
- * allgather: zero-copy and staged), each timed on the host
- * and the maximum over ranks exchanged through the registration page; the
- * fastest is kept for that class.  Results are identical on every path.
- * mx_comm_get_tuning returns the choice for a message size (0 zero-copy,
- * 1 PULL, 2 PUSH) or -1 while untuned.  Same setting on every rank. */
+ * MX_AUTOTUNE=0 switches it off).  Per collective and power-of-two size
+ * class of blocking calls, the first call runs candidate 0 as a warm-up, the
+ * next ones time each candidate (3 runs each below 4 MiB, the fastest
+ * counts), on the host, with the maximum over ranks exchanged through the
+ * registration page; the fastest candidate is kept for that class:
+ *   allreduce, from 64 KiB per rank: 0 zero-copy, 1 staged PULL, 2 staged
+ *     PUSH, 3 one-shot (size classes up to the one-shot slot capacity,
+ *     1 MiB or staging / (8 n));
+ *   reduce_scatter, allgather, from 256 KiB: 0 zero-copy, 1 staged;
+ *   bcast (n > 2), from 64 KiB: 0 zero-copy, 1 scatter + allgather, 2 direct.
+ * Results are identical on every path.  mx_comm_get_tuning_ex returns the
+ * choice of collective `coll` (MX_TUNE_*) for a message size, or -1 while
+ * untuned; mx_comm_get_tuning is the allreduce's.  Same setting on every
+ * rank. */
+enum { MX_TUNE_ALLREDUCE = 0, MX_TUNE_REDUCE_SCATTER = 1, MX_TUNE_ALLGATHER = 2, MX_TUNE_BCAST = 3 };
 int mx_comm_set_autotune(mx_comm_t *comm, int on);
 int mx_comm_get_tuning(const mx_comm_t *comm, size_t bytes);
+int mx_comm_get_tuning_ex(const mx_comm_t *comm, int coll, size_t bytes);
 
 /* Per-communicator kernel timing (HIP events on the collective's stream),
  * off by default.  Times are summed over calls since the last reset. */

@@ -245,8 +245,8 @@ def _mp_worker(rank, n, port, staging, jobs, q, env=None):
             elif kind == "stats":
                 sts = comm.stats()
                 results.append((sts["zero_copy_calls"], sts["staged_calls"]))
-            elif kind == "tuning":
-                results.append(comm.tuning(count * es))
+            elif kind.startswith("tuning"):   # tuning[_<coll>]: the kept choice for that size class
+                results.append(comm.tuning(count * es, kind[7:] or "allreduce"))
             elif kind == "reduce_scatter":
                 rc = [count + 3 * r for r in range(n)]
                 x = _dev(gen(t, op, sum(rc), 7000 + rank))
@@ -418,7 +418,7 @@ def _check_jobs(n, jobs, got):
     L = _oracle()
     for j, (kind, count, op, t, alg) in enumerate(jobs):
         es = mxompi.type_size(t)
-        if kind in ("stats", "tuning"):
+        if kind == "stats" or kind.startswith("tuning"):
             continue
         if kind.startswith("allreduce") or kind == "shmem":
             xs = [gen(t, op, count, 7000 + r) for r in range(n)]
@@ -602,6 +602,31 @@ def test_multiprocess_allreduce_autotune(n):
     for r in range(n):
         assert got[r][5] in ("zero_copy", "pull", "push"), got[r][5]   # the fp32 size class: 4 calls done
         assert got[r][5] == got[0][5] and got[r][7] == got[0][5]
+
+
+# autotuning of the crossovers below 4 MiB: one-shot / zero-copy / PULL /
+# PUSH for allreduces from 64 KiB (each candidate 3 times: 13 calls per size
+# class), zero-copy / scatter / direct for bcasts from 64 KiB (n > 2: 10
+# calls); every trial bit-exact, every rank keeping the same choice
+_JOBS_TUNE_SMALL = [*[("allreduce", 40_000, "SUM", "FLOAT", "auto")] * 13,            # 160 KB
+                    ("tuning", 40_000, "SUM", "FLOAT", "auto"),
+                    *[("allreduce", 200_000, "SUM", "FLOAT", "auto")] * 13,           # 800 KB
+                    ("tuning", 200_000, "SUM", "FLOAT", "auto"),
+                    *[("bcast", 300_000, "BAND", "UINT8_T", "auto")] * 10,
+                    ("tuning_bcast", 300_000, "BAND", "UINT8_T", "auto"),
+                    ("allreduce", 200_000, "SUM", "FLOAT", "auto")]
+
+
+@pytest.mark.parametrize("n", [2, 8])
+def test_multiprocess_autotune_crossovers(n):
+    got = _run_mp(n, _JOBS_TUNE_SMALL, staging=64 << 20)
+    _check_jobs(n, _JOBS_TUNE_SMALL, got)
+    idx = [j for j, job in enumerate(_JOBS_TUNE_SMALL) if job[0].startswith("tuning")]
+    for r in range(n):
+        for j in idx[:2]:
+            assert got[r][j] in ("zero_copy", "pull", "push", "one_shot"), got[r][j]
+        assert got[r][idx[2]] in (("zero_copy", "scatter", "direct") if n > 2 else (None,)), got[r][idx[2]]
+        assert [got[r][j] for j in idx] == [got[0][j] for j in idx]
 
 
 @pytest.mark.parametrize("env", [{"MX_FAST_SYNC_SPINS": "0"}, {"MX_FAST_SYNC": "0"}], ids=["fallback", "runtime"])

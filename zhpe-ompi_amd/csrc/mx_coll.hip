@@ -142,6 +142,7 @@ static int copy_launch(const mx_comm *c, CopyArgs &a, hipStream_t s) {
 // 51 us; profiles/r02/allreduce_oneshot_crossover.txt), so one-shot keeps
 // the messages up to 128 KiB (24.7 vs 26.3 us there).
 constexpr size_t kOneShotMax = 128 << 10;
+constexpr size_t kOneShotCap = 1 << 20;   // one-shot slot capacity per rank (autotuning range)
 
 static size_t oneshot_max() {
   const char *e = getenv("MX_ONESHOT_MAX");
@@ -156,12 +157,26 @@ __global__ void k_signal(SignalArgs a) {
   const int j = threadIdx.x;
   if (poisoned(a.poison)) return;   // a wait before this one timed out: tell no peer anything
   __threadfence_system();  // everything this stream wrote is visible first (the fence is the release)
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // keep the write-back ahead of the flag (guide G16 pitfall 12)
   if (j < a.n && a.peer_flag[j])
     __hip_atomic_store(a.peer_flag[j], a.value, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
 // Waits until flags[j] >= value for every j in `mask`; a timeout raises the
 // host error and poisons the communicator (timeout_ticks = ~0: wait forever).
+//
+// Cross-device memory model: a wait is the acquire before this
+// rank reads what its peers published -- their staging (uncached: never in an
+// L2) or, on the zero-copy paths, their cacheable user buffers over xGMI.
+// Remote lines may sit in this GPU's L2s from an earlier call, and each of
+// the 8 XCDs has its own L2, so every workgroup of the wait polls the flags
+// itself and then takes a SYSTEM-scope acquire (buffer_inv sc0 sc1, which
+// drops the non-coherent -- remote -- lines of its XCD's L2); kWaitBlocks
+// workgroups, dealt round-robin over the XCDs, cover all of them.  The
+// writer side is the signal's system-scope release (buffer_wbl2 sc0 sc1)
+// after the end-of-kernel release of the user's producing kernels.
+constexpr int kWaitBlocks = 16;
+
 __global__ void k_wait(const uint64_t *flags, uint32_t mask, uint64_t value, uint64_t timeout_ticks, int *err,
                        int *poison) {
   const int j = threadIdx.x;
@@ -186,9 +201,12 @@ __global__ void k_signal_wait(SignalArgs a, const uint64_t *flags, uint32_t mask
                               uint64_t timeout_ticks, int *err, int *poison) {
   const int j = threadIdx.x;
   if (!poisoned(a.poison)) {
-    __threadfence_system();
-    if (j < a.n && a.peer_flag[j])
-      __hip_atomic_store(a.peer_flag[j], a.value, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    if (blockIdx.x == 0) {   // the signal half: once
+      __threadfence_system();
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      if (j < a.n && a.peer_flag[j])
+        __hip_atomic_store(a.peer_flag[j], a.value, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
     if (j < MAXR && ((mask >> j) & 1)) {
       const uint64_t t0 = wall_clock64();
       while (__hip_atomic_load(&flags[j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) < value) {
@@ -327,7 +345,8 @@ static_assert(std::atomic<uint64_t>::is_always_lock_free, "shared-memory atomics
 // staged path at every size measured above the one-shot range
 constexpr size_t kRegMinDefault = (size_t)256 << 10;
 constexpr size_t kRegCachePerPeer = 8;
-constexpr size_t kTuneMin = (size_t)4 << 20;   // autotuned allreduces: bytes per rank
+constexpr size_t kTuneMin = (size_t)64 << 10;       // autotuned allreduces / bcasts: bytes per rank
+constexpr size_t kTuneMinMove = (size_t)256 << 10;  // autotuned reduce_scatters / allgathers
 
 static size_t reg_min() {
   const char *e = getenv("MX_REG_MIN");
@@ -404,9 +423,13 @@ extern "C" int mx_comm_set_autotune(mx_comm_t *c, int on) {
 }
 
 extern "C" int mx_comm_get_tuning(const mx_comm_t *c, size_t bytes) {
-  if (!c || !bytes) return MX_ERR_ARG;
+  return mx_comm_get_tuning_ex(c, 0, bytes);   // TUNE_ALLREDUCE
+}
+
+extern "C" int mx_comm_get_tuning_ex(const mx_comm_t *c, int coll, size_t bytes) {
+  if (!c || !bytes || coll < 0 || coll > 3) return MX_ERR_ARG;
   const int b = 63 - __builtin_clzll((unsigned long long)bytes);
-  return c->tune_best[0][b] ? c->tune_best[0][b] - 1 : -1;   // TUNE_ALLREDUCE
+  return c->tune_best[coll][b] ? c->tune_best[coll][b] - 1 : -1;
 }
 
 extern "C" int mx_comm_set_reg_min(mx_comm_t *c, size_t min_bytes) {
@@ -517,9 +540,15 @@ extern "C" int mx_comm_create_ex(int rank, int size, int device, size_t staging_
     if (ok) {
       c->staging_bytes = staging_bytes ? staging_bytes : ((size_t)64 << 20);
       // one-shot region at the top of staging: 2 parities x n slots
-      c->os_max = std::min<size_t>(oneshot_max(), c->staging_bytes / (8 * (size_t)size)) & ~(size_t)255;
-      if (c->os_max < 1024) c->os_max = 0;
-      c->os_slot = c->os_max ? c->os_max + 256 : 0;
+      // the region holds up to os_cap per rank (autotuning may move the
+      // one-shot crossover up to it); os_max is the default crossover
+      // (MX_ONESHOT_MAX forces the crossover: the capacity is that value)
+      const char *ose = getenv("MX_ONESHOT_MAX");
+      c->os_cap = std::min<size_t>((ose && *ose) ? oneshot_max() : std::max<size_t>(kOneShotCap, oneshot_max()),
+                                   c->staging_bytes / (8 * (size_t)size)) & ~(size_t)255;
+      if (c->os_cap < 1024) c->os_cap = 0;
+      c->os_max = std::min<size_t>(oneshot_max(), c->os_cap);
+      c->os_slot = c->os_cap ? c->os_cap + 256 : 0;
       c->main_bytes = (c->staging_bytes - 2 * (size_t)size * c->os_slot) & ~(size_t)255;
       c->hregion_bytes = heap_bytes ? ((heap_bytes + 4095) & ~(size_t)4095) : 0;
       // point-to-point mailboxes (one per source rank) follow the staging
@@ -742,7 +771,7 @@ static inline int reduce_word_of(int alg) { return ((alg >> 8) & 0xff) | (alg & 
 
 // Internal allreduce algorithm id: libnbc's ring (allred_sched_ring,
 // nbc_iallreduce.c:629-860), reached through mx_iallreduce.
-constexpr int kArNbcRing = 1001;
+constexpr int kArNbcRing = 201;   // fits the algorithm byte of an MX_ALG_WORD
 
 // Allreduce fold segments restricted to [rlo, rhi).
 static int allreduce_segments(int alg, int n, size_t count, size_t es, size_t rlo, size_t rhi,
@@ -1107,13 +1136,13 @@ static int signal_wait_all(mx_comm *c, int kind, uint64_t svalue, uint64_t wvalu
   for (int p = 0; p < c->size; p++)
     a.peer_flag[p] = (p == c->rank) ? nullptr : c->peer_flags[p] + kind * MAXR + c->rank;
   const uint32_t all = (c->size >= 32) ? 0xffffffffu : ((1u << c->size) - 1);
-  hipLaunchKernelGGL(k_signal_wait, dim3(1), dim3(64), 0, s, a, (const uint64_t *)(c->flagmem + kind * MAXR),
+  hipLaunchKernelGGL(k_signal_wait, dim3(kWaitBlocks), dim3(64), 0, s, a, (const uint64_t *)(c->flagmem + kind * MAXR),
                      all & ~(1u << c->rank), wvalue, c->timeout_ticks, c->err_dev, c->poison);
   return mx_check_launch();
 }
 
 static int wait_mask(mx_comm *c, int kind, uint32_t mask, uint64_t value, hipStream_t s) {
-  hipLaunchKernelGGL(k_wait, dim3(1), dim3(64), 0, s, (const uint64_t *)(c->flagmem + kind * MAXR), mask, value,
+  hipLaunchKernelGGL(k_wait, dim3(kWaitBlocks), dim3(64), 0, s, (const uint64_t *)(c->flagmem + kind * MAXR), mask, value,
                      c->timeout_ticks, c->err_dev, c->poison);
   return mx_check_launch();
 }
@@ -1228,15 +1257,23 @@ static int tune_exchange(mx_comm *c, double el, double *tmax) {
 // candidate this call runs (-1: the defaults, untuned), *bucket its size
 // class.  tune_done: after a successful call, record its time (trial calls
 // exchange the max over ranks) and keep the fastest once every candidate ran.
-enum { TUNE_ALLREDUCE = 0, TUNE_REDUCE_SCATTER = 1, TUNE_ALLGATHER = 2 };
-static int tune_pick(const mx_comm *c, int kind, size_t bytes, int *bucket) {
+enum { TUNE_ALLREDUCE = 0, TUNE_REDUCE_SCATTER = 1, TUNE_ALLGATHER = 2, TUNE_BCAST = 3 };
+// smallest size class tuned per kind: allreduce and bcast cover their
+// one-shot / direct crossovers, reduce_scatter and allgather the zero-copy one
+static size_t tune_min(int kind) {
+  return (kind == TUNE_ALLREDUCE || kind == TUNE_BCAST) ? kTuneMin : kTuneMinMove;
+}
+// trial calls per candidate: small calls are noisy, each runs 3 times and its
+// fastest counts
+static int tune_reps(int bucket) { return bucket < 22 ? 3 : 1; }
+static int tune_pick(const mx_comm *c, int kind, size_t bytes, int ncand, int *bucket) {
   *bucket = -1;
-  if (!c->tune_on || !c->reg_shm || c->defer || bytes < kTuneMin) return -1;
+  if (!c->tune_on || !c->reg_shm || c->defer || bytes < tune_min(kind)) return -1;
   const int b = 63 - __builtin_clzll((unsigned long long)bytes);
   *bucket = b;
   if (c->tune_best[kind][b]) return c->tune_best[kind][b] - 1;
   const int k = c->tune_calls[kind][b];
-  return k == 0 ? 0 : k - 1;   // call 0 warms up (and maps the peers' buffers) on candidate 0
+  return k == 0 ? 0 : (k - 1) % ncand;   // call 0 warms up (and maps the peers' buffers) on candidate 0
 }
 static int tune_done(mx_comm *c, int kind, int bucket, int cand, int ncand, double el) {
   if (cand < 0 || c->tune_best[kind][bucket]) return MX_SUCCESS;
@@ -1244,8 +1281,9 @@ static int tune_done(mx_comm *c, int kind, int bucket, int cand, int ncand, doub
   if (k == 0) return MX_SUCCESS;
   double tmax = 0;
   if (int rc = tune_exchange(c, el, &tmax)) return rc;
-  c->tune_t[kind][bucket][cand] = tmax;
-  if (k == ncand) {
+  double &t = c->tune_t[kind][bucket][cand];
+  if (k <= ncand || tmax < t) t = tmax;   // the first run of a candidate, or a faster one
+  if (k == ncand * tune_reps(bucket)) {
     int best = 0;
     for (int i = 1; i < ncand; i++)
       if (c->tune_t[kind][bucket][i] < c->tune_t[kind][bucket][best]) best = i;
@@ -1256,6 +1294,16 @@ static int tune_done(mx_comm *c, int kind, int bucket, int cand, int ncand, doub
 static double secs_since(std::chrono::steady_clock::time_point t0) {
   return std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
 }
+// zero-copy modes of the tuned data paths: never (a staged candidate), the
+// default (calls of reg_min bytes and more), always (the zero-copy
+// candidate, at any size; reg_min == 0 still switches zero-copy off)
+enum { ZC_NEVER = 0, ZC_DEFAULT = 1, ZC_ALWAYS = 2 };
+static bool zc_allowed(const mx_comm *c, int zc_mode, size_t bytes) {
+  if (zc_mode == ZC_NEVER || !c->reg_shm || c->defer || !c->reg_min) return false;
+  return zc_mode == ZC_ALWAYS || bytes >= c->reg_min;
+}
+// the zero-copy mode of a tuned call's candidate (0 is the zero-copy one)
+static int zc_mode_of(int cand) { return cand < 0 ? ZC_DEFAULT : cand == 0 ? ZC_ALWAYS : ZC_NEVER; }
 
 // the allocation holding [p, p+bytes): IPC handle, identity, offset of p.
 // Handles of recent allocations are kept per process (the runtime buffer id
@@ -1408,7 +1456,7 @@ static int reg_exchange(mx_comm *c, const char *sb, size_t sbytes, char *rb, siz
 
 // The staged / zero-copy allreduce above the one-shot range (mx_allreduce)
 static int allreduce_staged(mx_comm *c, fold_launch_fn fl, int alg, const char *sb, char *rb, size_t count,
-                            size_t es, bool allow_zc, hipStream_t s) {
+                            size_t es, int zc_mode, hipStream_t s) {
   const int n = c->size, r = c->rank;
   // Zero-copy input: with every rank's sbuf registered, the fold reads the
   // peers' parts straight from their sbufs over xGMI (the PULL fold without
@@ -1418,7 +1466,7 @@ static int allreduce_staged(mx_comm *c, fold_launch_fn fl, int alg, const char *
   const char *ps[MAXR];
   char *pr[MAXR];
   int zc = 0;
-  if (allow_zc && c->reg_shm && !c->defer && c->reg_min && count * es >= c->reg_min) {
+  if (zc_allowed(c, zc_mode, count * es)) {
     zc = reg_exchange(c, sb, count * es, rb, count * es, (int)((uintptr_t)sb & 15), true, ps, pr);
     if (zc < 0) return zc;
   }
@@ -1558,32 +1606,43 @@ extern "C" int mx_allreduce(mx_comm_t *c, const void *sbuf, void *rbuf, size_t c
     return mx_bcast(c, rb, count * es, 0, stream);
   }
   alg &= 0xff;
-  if (c->os_max && count * es <= c->os_max) {
-    std::vector<Seg> segs;
-    int rc = allreduce_segments(alg, n, count, es, 0, count, segs);
-    if (rc) return rc;
-    oneshot_launch_fn ol = fold_fns(op, type).oneshot;
-    if (ol && segs.size() <= (size_t)OS_MAXSEG) return allreduce_oneshot(c, ol, segs, sb, rb, count, es, s);
+  const size_t bytes = count * es;
+  // one-shot: possible up to the slot capacity os_cap, the default up to os_max
+  std::vector<Seg> ossegs;
+  oneshot_launch_fn ol = fold_fns(op, type).oneshot;
+  bool os_ok = false;
+  if (c->os_cap && bytes <= c->os_cap && ol) {
+    if (int rc = allreduce_segments(alg, n, count, es, 0, count, ossegs)) return rc;
+    os_ok = ossegs.size() <= (size_t)OS_MAXSEG;
   }
   {  // validate the algorithm once for the whole vector
     std::vector<Seg> probe;
     int rc = allreduce_segments(alg, n, count, es, 0, 0, probe);
     if (rc) return rc;
   }
-  // autotuning: cand 0 zero-copy, 1 staged PULL, 2 staged PUSH; -1 the defaults
+  // autotuning: cand 0 zero-copy, 1 staged PULL, 2 staged PUSH,
+  // 3 one-shot (size classes within the one-shot capacity); -1 the defaults
   int bucket;
-  const int cand = tune_pick(c, TUNE_ALLREDUCE, count * es, &bucket);
+  int cand = tune_pick(c, TUNE_ALLREDUCE, bytes, (c->os_cap && bytes <= c->os_cap) ? 4 : 3, &bucket);
+  if (cand == 3 && !os_ok) cand = -1;   // this op / type has no one-shot kernel: the defaults, untimed
+  if (cand == 3 || (cand < 0 && os_ok && bytes <= c->os_max)) {
+    const auto t0 = std::chrono::steady_clock::now();
+    const int rc = allreduce_oneshot(c, ol, ossegs, sb, rb, count, es, s);
+    return rc || cand < 0 ? rc : tune_done(c, TUNE_ALLREDUCE, bucket, cand, 4, secs_since(t0));
+  }
   const int proto0 = c->proto;
   if (cand == 1) c->proto = MX_PROTO_PULL;
   if (cand == 2) c->proto = MX_PROTO_PUSH;
   const auto t0 = std::chrono::steady_clock::now();
-  const int rc = allreduce_staged(c, fl, alg, sb, rb, count, es, cand <= 0, s);
+  const int rc = allreduce_staged(c, fl, alg, sb, rb, count, es, zc_mode_of(cand), s);
   c->proto = proto0;
-  return rc ? rc : tune_done(c, TUNE_ALLREDUCE, bucket, cand, 3, secs_since(t0));
+  return rc || cand < 0 ? rc
+                        : tune_done(c, TUNE_ALLREDUCE, bucket, cand, (c->os_cap && bytes <= c->os_cap) ? 4 : 3,
+                                    secs_since(t0));
 }
 
 static int reduce_scatter_impl(mx_comm_t *c, const void *sbuf, void *rbuf, const size_t *rcounts, int type, int op,
-                               int alg, void *stream, bool allow_zc) {
+                               int alg, void *stream, int zc_mode) {
   if (!c || !rbuf || !rcounts) return MX_ERR_ARG;
   if (c->local) {
     if (c->size != 1) return MX_ERR_STATE;
@@ -1607,7 +1666,7 @@ static int reduce_scatter_impl(mx_comm_t *c, const void *sbuf, void *rbuf, const
     return finish(c, s);
   }
   if (!(c->flags & MX_COMM_IPC)) return MX_ERR_STATE;
-  if ((alg & 0xff) == MX_RS_NONOVERLAPPING) return rs_nonoverlapping(c, sb, (char *)rbuf, rcounts, type, op, alg, allow_zc, s);
+  if ((alg & 0xff) == MX_RS_NONOVERLAPPING) return rs_nonoverlapping(c, sb, (char *)rbuf, rcounts, type, op, alg, zc_mode != ZC_NEVER, s);
   alg &= 0xff;
   std::vector<Seg> segs;
   int rc = reduce_scatter_segments(alg, n, rcounts, es, r, segs);
@@ -1617,7 +1676,7 @@ static int reduce_scatter_impl(mx_comm_t *c, const void *sbuf, void *rbuf, const
   // (the slot geometry must be the same on every rank: it depends only on
   // the collective IN_PLACE choice, not on this rank's block)
   const bool inplace = sb == (const char *)rbuf;
-  if (allow_zc && c->reg_shm && !c->defer && c->reg_min && total * es >= c->reg_min && !inplace) {
+  if (zc_allowed(c, zc_mode, total * es) && !inplace) {
     // zero-copy: rank r folds block r straight from every rank's registered
     // sbuf into its own rbuf (IN_PLACE stays staged: block 0 of a rank's
     // input is its output area, which rank 0 would still be reading)
@@ -1683,7 +1742,7 @@ static int reduce_scatter_impl(mx_comm_t *c, const void *sbuf, void *rbuf, const
   return finish(c, s);
 }
 
-static int allgather_impl(mx_comm_t *c, const void *sbuf, void *rbuf, size_t bytes, void *stream, bool allow_zc) {
+static int allgather_impl(mx_comm_t *c, const void *sbuf, void *rbuf, size_t bytes, void *stream, int zc_mode) {
   if (!c || !rbuf) return MX_ERR_ARG;
   if (c->local) {
     if (c->size != 1) return MX_ERR_STATE;
@@ -1702,7 +1761,7 @@ static int allgather_impl(mx_comm_t *c, const void *sbuf, void *rbuf, size_t byt
     return finish(c, s);
   }
   if (!(c->flags & MX_COMM_IPC)) return MX_ERR_STATE;
-  if (allow_zc && c->reg_shm && !c->defer && c->reg_min && (size_t)n * bytes >= c->reg_min) {
+  if (zc_allowed(c, zc_mode, (size_t)n * bytes)) {
     // zero-copy: every rank reads the peers' blocks straight from their
     // registered sbufs into its own rbuf (remote reads, local writes only)
     const char *ps[MAXR];
@@ -1765,7 +1824,8 @@ static int allgather_impl(mx_comm_t *c, const void *sbuf, void *rbuf, size_t byt
 // root's bytes.
 constexpr size_t kBcastDirectMax = 512 << 10;
 
-// the tuned entry points: candidate 0 zero-copy, 1 staged
+// the tuned entry points: candidate 0 zero-copy, 1 staged (bcast:
+// 1 scatter + allgather, 2 direct)
 extern "C" int mx_reduce_scatter(mx_comm_t *c, const void *sbuf, void *rbuf, const size_t *rcounts, int type,
                                  int op, int alg, void *stream) {
   int bucket = -1, cand = -1;
@@ -1773,22 +1833,24 @@ extern "C" int mx_reduce_scatter(mx_comm_t *c, const void *sbuf, void *rbuf, con
   if (c && !c->local && rcounts && es) {
     size_t total = 0;
     for (int j = 0; j < c->size; j++) total += rcounts[j];
-    cand = tune_pick(c, TUNE_REDUCE_SCATTER, total * es, &bucket);
+    cand = tune_pick(c, TUNE_REDUCE_SCATTER, total * es, 2, &bucket);
   }
   const auto t0 = std::chrono::steady_clock::now();
-  const int rc = reduce_scatter_impl(c, sbuf, rbuf, rcounts, type, op, alg, stream, cand <= 0);
+  const int rc = reduce_scatter_impl(c, sbuf, rbuf, rcounts, type, op, alg, stream, zc_mode_of(cand));
   return rc || cand < 0 ? rc : tune_done(c, TUNE_REDUCE_SCATTER, bucket, cand, 2, secs_since(t0));
 }
 
 extern "C" int mx_allgather(mx_comm_t *c, const void *sbuf, void *rbuf, size_t bytes, void *stream) {
   int bucket = -1, cand = -1;
-  if (c && !c->local) cand = tune_pick(c, TUNE_ALLGATHER, (size_t)c->size * bytes, &bucket);
+  if (c && !c->local) cand = tune_pick(c, TUNE_ALLGATHER, (size_t)c->size * bytes, 2, &bucket);
   const auto t0 = std::chrono::steady_clock::now();
-  const int rc = allgather_impl(c, sbuf, rbuf, bytes, stream, cand <= 0);
+  const int rc = allgather_impl(c, sbuf, rbuf, bytes, stream, zc_mode_of(cand));
   return rc || cand < 0 ? rc : tune_done(c, TUNE_ALLGATHER, bucket, cand, 2, secs_since(t0));
 }
 
-extern "C" int mx_bcast(mx_comm_t *c, void *buf, size_t bytes, int root, void *stream) {
+// bcast data paths: 0 zero-copy, 1 scatter + allgather, 2 direct push; -1
+// the defaults (zero-copy from reg_min, direct up to kBcastDirectMax)
+static int bcast_impl(mx_comm_t *c, void *buf, size_t bytes, int root, void *stream, int path) {
   if (!c || !buf || root < 0 || root >= c->size) return MX_ERR_ARG;
   if (c->local) {
     if (c->size != 1) return MX_ERR_STATE;
@@ -1807,7 +1869,7 @@ extern "C" int mx_bcast(mx_comm_t *c, void *buf, size_t bytes, int root, void *s
   const size_t cb = (slot - 32) * (size_t)m;
   const uint32_t all = (n >= 32) ? 0xffffffffu : ((1u << n) - 1);
   auto part_of = [&](int rank) { return rank < root ? rank : rank - 1; };   // non-root -> part index
-  if (c->reg_shm && !c->defer && c->reg_min && bytes >= c->reg_min) {
+  if (zc_allowed(c, zc_mode_of(path), bytes)) {
     // zero-copy scatter + allgather: non-root q reads its part from the
     // root's registered buffer, then the other parts from their owners'
     // buffers (remote reads, local writes only)
@@ -1843,7 +1905,7 @@ extern "C" int mx_bcast(mx_comm_t *c, void *buf, size_t bytes, int root, void *s
       return finish(c, s);
     }
   }
-  const bool direct = bytes <= kBcastDirectMax || m == 1;
+  const bool direct = m == 1 || (path < 0 ? bytes <= kBcastDirectMax : path == 2);
   for (size_t o = 0; o < bytes; o += cb) {
     const size_t l = std::min(cb, bytes - o);
     size_t off[MAXR], len[MAXR];
@@ -1891,6 +1953,14 @@ extern "C" int mx_bcast(mx_comm_t *c, void *buf, size_t bytes, int root, void *s
     if ((rc = signal_all(c, FLAG_DONE, g, s))) return rc;
   }
   return finish(c, s);
+}
+
+extern "C" int mx_bcast(mx_comm_t *c, void *buf, size_t bytes, int root, void *stream) {
+  int bucket = -1, cand = -1;
+  if (c && !c->local && c->size > 2) cand = tune_pick(c, TUNE_BCAST, bytes, 3, &bucket);
+  const auto t0 = std::chrono::steady_clock::now();
+  const int rc = bcast_impl(c, buf, bytes, root, stream, cand);
+  return rc || cand < 0 ? rc : tune_done(c, TUNE_BCAST, bucket, cand, 3, secs_since(t0));
 }
 
 // ---------------------------------------------------------------------------

@@ -121,7 +121,8 @@ struct mx_comm {
   size_t staging_bytes;
   size_t staging_alloc;        // bytes of the staging allocation (+ mailboxes)
   size_t main_bytes;           // staging for the chunked paths: [0, main_bytes)
-  size_t os_max, os_slot;      // one-shot: max bytes per rank, slot stride
+  size_t os_max, os_slot;      // one-shot: default max bytes per rank, slot stride
+  size_t os_cap;               // one-shot: the most a slot holds (autotuning may pick it up to here)
   uint64_t os_count;           // one-shot workgroup completions so far
   char *staging;               // mine (uncached, IPC-exported)
   char *peer_staging[mx::MAXR];    // mapped views (peer_staging[rank] = staging)
@@ -150,16 +151,18 @@ struct mx_comm {
   size_t reg_shm_bytes, reg_min;
   uint64_t reg_seq, reg_tick;
   std::vector<struct mx_reg_import> *reg_imp;
-  // data-movement autotuning of blocking collectives >= 4 MiB per rank
-  // (DESIGN 7): per collective kind (TUNE_*) and power-of-two size class, the
-  // first call warms up, the next ones time each candidate (allreduce:
-  // zero-copy / PULL / PUSH; reduce_scatter, allgather: zero-copy / staged;
-  // max over ranks, exchanged in the registration page) and the fastest is
-  // kept.  tune_best: choice + 1, 0 = not yet.
+  // data-movement autotuning of blocking collectives: per
+  // collective kind (TUNE_*) and power-of-two size class, the first call
+  // warms up, the next ones time each candidate (allreduce from 64 KiB:
+  // zero-copy / PULL / PUSH / one-shot; reduce_scatter, allgather from
+  // 256 KiB: zero-copy / staged; bcast from 64 KiB: zero-copy / scatter /
+  // direct; max over ranks, exchanged in the registration page; below 4 MiB
+  // every candidate runs 3 times and its fastest run counts) and the fastest
+  // is kept.  tune_best: choice + 1, 0 = not yet.
   int tune_on;
-  uint8_t tune_calls[3][64];
-  int8_t tune_best[3][64];
-  double tune_t[3][64][3];
+  uint8_t tune_calls[4][64];
+  int8_t tune_best[4][64];
+  double tune_t[4][64][4];
   uint64_t tune_seq;
   double timeout_s;
   uint64_t timeout_ticks;

@@ -216,6 +216,7 @@ def _coll_lib():
         L.mx_comm_set_reg_min.argtypes = [vp, sz]
         L.mx_comm_set_autotune.argtypes = [vp, i]
         L.mx_comm_get_tuning.argtypes = [vp, sz]
+        L.mx_comm_get_tuning_ex.argtypes = [vp, i, sz]
         L.mx_allreduce.argtypes = [vp, vp, vp, sz, i, i, i, vp]
         L.mx_allreduce_local.argtypes = [vp, pp, pp, sz, i, i, i, vp]
         L.mx_reduce_scatter.argtypes = [vp, vp, vp, ctypes.POINTER(sz), i, i, i, vp]
@@ -417,9 +418,16 @@ class Comm:
         """Data-movement autotuning of large blocking allreduces (mx_comm_set_autotune)."""
         check(_coll_lib().mx_comm_set_autotune(self.h, 1 if on else 0), "mx_comm_set_autotune")
 
-    def tuning(self, nbytes):
-        """The data movement autotuning kept for allreduces of nbytes per rank, or None."""
-        return {0: "zero_copy", 1: "pull", 2: "push"}.get(_coll_lib().mx_comm_get_tuning(self.h, nbytes))
+    _TUNE = {"allreduce": (0, {0: "zero_copy", 1: "pull", 2: "push", 3: "one_shot"}),
+             "reduce_scatter": (1, {0: "zero_copy", 1: "staged"}),
+             "allgather": (2, {0: "zero_copy", 1: "staged"}),
+             "bcast": (3, {0: "zero_copy", 1: "scatter", 2: "direct"})}
+
+    def tuning(self, nbytes, coll="allreduce"):
+        """The data movement autotuning kept for `coll` calls of nbytes per rank
+        (mx_comm_get_tuning_ex), or None while untuned."""
+        k, names = self._TUNE[coll]
+        return names.get(_coll_lib().mx_comm_get_tuning_ex(self.h, k, nbytes))
 
     def set_reg_min(self, min_bytes):
         """Zero-copy (registered user buffers) allreduce from min_bytes per rank; 0 = off
