@@ -489,6 +489,9 @@ def test_host_only_small_allreduce_allocates_no_device_memory():
 
 
 # ---------------------------------------------------------------------------
+_STALE_ITERS = 12
+
+
 def _stale_worker(rank, n, port, q):
     """The zero-copy paths read the peers' registered buffers.  The same
     sbuf / rbuf allocations are rewritten with new data before every call:
@@ -520,9 +523,13 @@ def _stale_worker(rank, n, port, q):
         X = torch.empty(count, device="cuda")
         R = torch.empty(count, device="cuda")
         G = torch.empty(count * n, device="cuda")
+        T = torch.empty(count, device="cuda")
         res = {}
-        for it in range(4):
-            X.copy_(torch.from_numpy(_gen("FLOAT", count, 5000 + 10 * it + rank)))
+        for it in range(_STALE_ITERS):
+            # new data written into the same allocation by a kernel on the
+            # caller's stream right before the call (through this GPU's L2s)
+            T.copy_(torch.from_numpy(_gen("FLOAT", count, 5000 + 10 * it + rank)))
+            X.copy_(T)
             R.fill_(float("nan"))
             assert H.mxh_allreduce(X.data_ptr(), R.data_ptr(), count, f32, SUM, comm) == 0
             res[("allreduce", it)] = R.cpu().numpy().tobytes()
@@ -549,7 +556,7 @@ def test_zero_copy_reused_buffers_never_read_stale_data(n):
     L = oracle_lib.oracle()
     L.mxo_allreduce.argtypes = [ci, ci, ci, ci, sz, ctypes.POINTER(vp), ctypes.POINTER(vp)]
     count = 65537
-    for it in range(4):
+    for it in range(_STALE_ITERS):
         xs = [_gen("FLOAT", count, 5000 + 10 * it + r) for r in range(n)]
         exp = [np.zeros(count, np.float32) for _ in range(n)]
         assert L.mxo_allreduce(0, mxompi.OP["SUM"], mxompi.TYPE["FLOAT"], n, count,
