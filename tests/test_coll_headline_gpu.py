@@ -12,7 +12,9 @@ metric's own shapes:
   and MAXLOC float_int allreduce at >= 64 MiB;
 * the same allreduces with a staging area far smaller than the message, so the
   chunked path runs (every chunk re-derives the fold partition from the full
-  count).
+  count);
+* the top of CFG-D's range at 2 processes: 1 GiB and 4 GiB fp32 SUM per rank
+  (the bench sweep's largest sizes), zero-copy and chunked staged.
 
 Each rank returns a SHA-256 of its result plus a strided sample; the parent
 runs the oracle restatement (oracle/mx_oracle_coll.c, step by step over n
@@ -66,7 +68,7 @@ def digest(b: np.ndarray):
     b = np.ascontiguousarray(b).view(np.uint8)
     idx = np.arange(0, max(0, b.size - 16), SAMPLE_STRIDE)
     sample = np.stack([b[i:i + 16] for i in idx]) if len(idx) else np.zeros((0, 16), np.uint8)
-    return hashlib.sha256(b.tobytes()).hexdigest(), sample
+    return hashlib.sha256(b.data).hexdigest(), sample   # no copy of a multi-GiB result
 
 
 def _free_port():
@@ -248,3 +250,24 @@ def test_allreduce_256mib_chunked_8_ranks(proto):
             ("allreduce", 100_000_007, "BAND", "UINT16_T", "ring"),
             ("reduce_scatter", (64 * MiB) // 4 // N + 7, "SUM", "FLOAT", "ring")]
     _check(jobs, _run(jobs, STAGING_CHUNKED, env={"MX_REG_MIN": "0", "MX_ALLREDUCE_PROTO": proto}))
+
+
+# CFG-D's range goes to 4 GiB per rank (BASELINE configs[3]; bench.py's
+# sweep): 2 processes, so the inputs, results and the oracle's copies fit
+# the box's host memory
+def test_allreduce_fp32_sum_1gib_per_rank_2_ranks():
+    """1 GiB fp32 SUM per rank: tuned decision (zero-copy between the
+    registered buffers, chunked by the staging size), forced Rabenseifner,
+    and the staged PULL path through a 48 MiB staging area (~40 chunks)."""
+    c = (1 << 30) // 4
+    jobs = [("allreduce", c, "SUM", "FLOAT", "auto"), ("allreduce", c - 7, "SUM", "FLOAT", "rabenseifner")]
+    _check(jobs, _run(jobs, STAGING_ONE_CHUNK, n=2), n=2)
+    jobs = [("allreduce", c + 3, "SUM", "FLOAT", "auto")]
+    _check(jobs, _run(jobs, STAGING_CHUNKED, n=2, env={"MX_REG_MIN": "0", "MX_ALLREDUCE_PROTO": "pull"}), n=2)
+
+
+def test_allreduce_fp32_sum_4gib_per_rank_2_ranks():
+    """4 GiB fp32 SUM per rank (2^30 elements: byte offsets past 2^32 in every
+    kernel's addressing), tuned decision."""
+    jobs = [("allreduce", (4 << 30) // 4, "SUM", "FLOAT", "auto")]
+    _check(jobs, _run(jobs, STAGING_ONE_CHUNK, n=2), n=2)
