@@ -97,20 +97,24 @@ __device__ __forceinline__ x87 x87_indefinite(const x87 &like) {
   return x87_make(like, 1, 0x7fff, 0xC000000000000000ull);
 }
 
-// NaN result for an operation with at least one NaN operand.
-__device__ __noinline__ x87 x87_nan_result(const x87 &like, const x87 &a, const x87 &b) {
+// NaN result for an operation with at least one NaN operand.  Inlined: a
+// call taking its operands by reference puts them in scratch on the hot path
+// (the reference escapes), which cost complex PROD a 304-byte frame.
+__device__ __forceinline__ x87 x87_nan_result(const x87 &like, const x87 &a, const x87 &b) {
   const bool na = x87_isnan(a), nb = x87_isnan(b);
   const uint64_t q = 1ull << 62;
+  // the operand chosen is selected by value (a select between references
+  // would force both operands into scratch)
+  bool take_a = na;
   if (na && nb) {
     const bool qa = (a.m & q) != 0, qb = (b.m & q) != 0;
-    const x87 *w;
-    if (qa != qb) w = qa ? &a : &b;
-    else if (a.m != b.m) w = (a.m > b.m) ? &a : &b;
-    else w = x87_sign(a) ? &b : &a;   // tie: positive sign
-    return x87_make(like, x87_sign(*w), 0x7fff, w->m | q);
+    if (qa != qb) take_a = qa;
+    else if (a.m != b.m) take_a = a.m > b.m;
+    else take_a = !x87_sign(a);   // tie: positive sign
   }
-  const x87 &w = na ? a : b;
-  return x87_make(like, x87_sign(w), 0x7fff, w.m | q);
+  const uint64_t wm = take_a ? a.m : b.m;
+  const int ws = take_a ? x87_sign(a) : x87_sign(b);
+  return x87_make(like, ws, 0x7fff, wm | q);
 }
 
 // value = S * 2^X with S normalised (bit 127 set): round to nearest even at
@@ -158,14 +162,46 @@ __device__ __forceinline__ void x87_unpack(const x87 &a, uint64_t &m, int &E) {
   E -= lz;
 }
 
+// both operands normal finite (exponent 1..0x7ffe, integer bit set): the
+// common case, taken with one test instead of the special-case ladder
+__device__ __forceinline__ bool x87_both_normal(const x87 &a, const x87 &b) {
+  return (unsigned)(x87_exp(a) - 1) < 0x7ffeu && (unsigned)(x87_exp(b) - 1) < 0x7ffeu && (int64_t)(a.m & b.m) < 0;
+}
+
+// sum of two normal finite values (x87_add's general case without unpacking)
+__device__ __forceinline__ x87 x87_add_normal(const x87 &like, const x87 &a, const x87 &b) {
+  const int sa = x87_sign(a), sb = x87_sign(b);
+  uint64_t ma = a.m, mb = b.m;
+  int ea = x87_exp(a), eb = x87_exp(b);
+  int s = sa;
+  if (ea < eb || (ea == eb && ma < mb)) {  // |a| >= |b|
+    const uint64_t tm = ma; ma = mb; mb = tm;
+    const int te = ea; ea = eb; eb = te;
+    s = sb;
+  }
+  const int d = ea - eb;
+  const u128 A = ((u128)ma) << 62;
+  u128 B = ((u128)mb) << 62;
+  if (d >= 128) {
+    B = 1;
+  } else if (d > 0) {
+    const u128 lost = B & ((((u128)1) << d) - 1);
+    B >>= d;
+    if (lost) B |= 1;
+  }
+  const u128 S = (sa == sb) ? A + B : A - B;
+  if (S == 0) return x87_make(like, 0, 0, 0);  // exact cancellation: +0 under RNE
+  return x87_round_pack(like, s, S, ea - 16446 - 62);
+}
+
 __device__ __forceinline__ x87 x87_add(const x87 &like, const x87 &a, const x87 &b) {
+  if (__builtin_expect(x87_both_normal(a, b), 1)) return x87_add_normal(like, a, b);
   if (x87_unsupported(a) || x87_unsupported(b)) return x87_indefinite(like);
   if (x87_isnan(a) || x87_isnan(b)) return x87_nan_result(like, a, b);
   const int sa = x87_sign(a), sb = x87_sign(b);
   if (x87_isinf(a) || x87_isinf(b)) {
     if (x87_isinf(a) && x87_isinf(b) && sa != sb) return x87_indefinite(like);
-    const x87 &w = x87_isinf(a) ? a : b;
-    return x87_make(like, x87_sign(w), 0x7fff, 1ull << 63);
+    return x87_make(like, x87_isinf(a) ? sa : sb, 0x7fff, 1ull << 63);
   }
   const bool za = x87_iszero(a), zb = x87_iszero(b);
   if (za && zb) return x87_make(like, sa & sb, 0, 0);
@@ -212,6 +248,12 @@ __device__ __forceinline__ x87 x87_sub(const x87 &like, const x87 &a, const x87 
 }
 
 __device__ __forceinline__ x87 x87_mul(const x87 &like, const x87 &a, const x87 &b) {
+  if (__builtin_expect(x87_both_normal(a, b), 1)) {   // no unpacking: both integer bits set
+    u128 P = (u128)a.m * (u128)b.m;
+    int X = x87_exp(a) + x87_exp(b) - 2 * 16446;
+    if (!(uint64_t)(P >> 127)) { P <<= 1; X--; }
+    return x87_round_norm(like, x87_sign(a) ^ x87_sign(b), P, X);
+  }
   if (x87_unsupported(a) || x87_unsupported(b)) return x87_indefinite(like);
   if (x87_isnan(a) || x87_isnan(b)) return x87_nan_result(like, a, b);
   const int s = x87_sign(a) ^ x87_sign(b);
@@ -254,11 +296,20 @@ __device__ __forceinline__ x87 x87_copysign01(const x87 &like, bool one, const x
 }
 
 // Annex-G recovery of an x87 complex product whose both parts came out NaN
-// (rare: out of line)
-__device__ __noinline__ x87c x87c_mul_recover(const x87c &p, const x87c &q, x87 x, x87 y, const x87 &ac,
-                                             const x87 &bd, const x87 &ad, const x87 &bc) {
-  x87 a = p.re, b = p.im, c = q.re, d = q.im;
-  const x87 &L = p.re;
+// (rare: out of line).  The operands travel as scalars and the partial
+// products are recomputed here: a call taking references would keep the
+// operands in scratch on the hot path.
+struct x87c_bits { uint64_t xm, ym; uint32_t xse, yse; };
+__device__ __noinline__ x87c_bits x87c_mul_recover(uint64_t am, uint32_t ase, uint64_t bm, uint32_t bse, uint64_t cm,
+                                                   uint32_t cse, uint64_t dm, uint32_t dse) {
+  x87 a{}, b{}, c{}, d{};
+  a.m = am; a.se = (uint16_t)ase;
+  b.m = bm; b.se = (uint16_t)bse;
+  c.m = cm; c.se = (uint16_t)cse;
+  d.m = dm; d.se = (uint16_t)dse;
+  const x87 L = a;
+  const x87 ac = x87_mul(L, a, c), bd = x87_mul(L, b, d), ad = x87_mul(L, a, d), bc = x87_mul(L, b, c);
+  x87 x = x87_sub(L, ac, bd), y = x87_add(L, ad, bc);
   {
     bool recalc = false;
     if (x87_isinf(a) || x87_isinf(b)) {
@@ -284,19 +335,23 @@ __device__ __noinline__ x87c x87c_mul_recover(const x87c &p, const x87c &q, x87 
     }
     if (recalc) {
       const x87 inf = x87_make(L, 0, 0x7fff, 1ull << 63);
-      x = x87_mul(p.re, inf, x87_sub(L, x87_mul(L, a, c), x87_mul(L, b, d)));
-      y = x87_mul(p.im, inf, x87_add(L, x87_mul(L, a, d), x87_mul(L, b, c)));
+      x = x87_mul(L, inf, x87_sub(L, x87_mul(L, a, c), x87_mul(L, b, d)));
+      y = x87_mul(L, inf, x87_add(L, x87_mul(L, a, d), x87_mul(L, b, c)));
     }
   }
-  return x87c{x, y};
+  return x87c_bits{x.m, y.m, x.se, y.se};
 }
 
 __device__ __forceinline__ x87c x87c_mul(const x87c &p, const x87c &q) {
   const x87 &a = p.re, &b = p.im, &c = q.re, &d = q.im;
   const x87 &L = p.re;
   const x87 ac = x87_mul(L, a, c), bd = x87_mul(L, b, d), ad = x87_mul(L, a, d), bc = x87_mul(L, b, c);
-  const x87 x = x87_sub(p.re, ac, bd), y = x87_add(p.im, ad, bc);
-  if (x87_isnan(x) && x87_isnan(y)) return x87c_mul_recover(p, q, x, y, ac, bd, ad, bc);
+  x87 x = x87_sub(p.re, ac, bd), y = x87_add(p.im, ad, bc);
+  if (__builtin_expect(x87_isnan(x) && x87_isnan(y), 0)) {
+    const x87c_bits r = x87c_mul_recover(a.m, a.se, b.m, b.se, c.m, c.se, d.m, d.se);
+    x.m = r.xm; x.se = (uint16_t)r.xse;
+    y.m = r.ym; y.se = (uint16_t)r.yse;
+  }
   return x87c{x, y};
 }
 
