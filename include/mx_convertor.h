@@ -54,6 +54,20 @@ size_t mx_ddt_runs(const mx_ddt_t *ddt);            /* flattened strided runs   
  * touch (true lb .. true ub of the whole message). */
 int mx_ddt_span(const mx_ddt_t *ddt, size_t count, int64_t *lo, int64_t *hi);
 
+/* Kernel family selection (tuning / tests; results are identical):
+ * MX_DDT_PATH_AUTO picks per layout and call (the default); MX_DDT_PATH_BLOCK
+ * sends every call the block table can take to the BLOCK kernels (one
+ * 16-byte packed granule per lane, the instance tabled as its contiguous
+ * user blocks).  Returns MX_ERR_UNSUPPORTED when the table cannot be built
+ * (instances >= 2 GiB, > 4M blocks). */
+#define MX_DDT_PATH_AUTO  0
+#define MX_DDT_PATH_BLOCK 1
+int mx_ddt_set_path(mx_ddt_t *ddt, int path);
+/* The kernel family of the last mx_pack / mx_unpack on this datatype:
+ * 1 copy (contiguous), 2 vector, 3 granule, 4 byte map, 5 piece,
+ * 6 block, 7 tile / pipelined tile; 0 before the first call. */
+int mx_ddt_last_path(const mx_ddt_t *ddt);
+
 /* Pack bytes [offset, offset+len) of the packed stream of `count`
  * instances starting at `user` into `packed` (which receives exactly len
  * bytes).  Asynchronous on `stream`. */

@@ -161,3 +161,173 @@ def test_device_pack_large_cfg_c(name, shift):
     O.mxo_ddt_convert(rec["desc"].ctypes.data, rec["nrec"], np.ascontiguousarray(BASIC).ctypes.data, rec["lb"],
                       rec["ub"], count, exp_u.ctypes.data - rec["true_lb"], exp.ctypes.data, 1)
     np.testing.assert_array_equal(got, exp_u)
+
+
+# ---- BLOCK kernels (k_convert_blk): large instances, and every golden type forced --------
+def _check_device_vs_oracle(d, dt, count, shift=0, pshift=0, chunks=(None,), rng_seed=11, expect_path="block"):
+    """pack whole / in fragments and unpack into a prefilled buffer, each vs the
+    oracle restatement; user buffer displaced by `shift` bytes, packed buffer
+    by `pshift` bytes; asserts the kernel family that ran."""
+    O = _oracle()
+    bs = np.ascontiguousarray(BASIC)
+    ext = d.ub - d.lb
+    # true span from the flattened records: [min disp, max disp + len) of instance 0 + (count-1) * ext
+    tl, tu = d.true_lb, d.true_ub
+    span = ext * (count - 1) + tu - tl
+    rng = np.random.default_rng(rng_seed)
+    user = rng.integers(0, 256, span, dtype=np.uint8)
+    total = d.size * count
+    exp = np.zeros(total, np.uint8)
+    O.mxo_ddt_convert(d.desc.ctypes.data, d.nrec, bs.ctypes.data, d.lb, d.ub, count, user.ctypes.data - tl,
+                      exp.ctypes.data, 0)
+    st = torch.cuda.current_stream().cuda_stream
+    U = torch.zeros(span + 32, dtype=torch.uint8, device="cuda")
+    U[shift:shift + span] = torch.from_numpy(user).cuda()
+    ubase = U.data_ptr() + shift - tl
+    for chunk in chunks:
+        P = torch.zeros(total + 32, dtype=torch.uint8, device="cuda")
+        off = 0
+        while off < total:
+            ln = total - off if chunk is None else min(chunk, total - off)
+            dt.pack(count, ubase, P.data_ptr() + pshift + off, offset=off, length=ln, stream=st)
+            off += ln
+        torch.cuda.synchronize()
+        assert dt.last_path == expect_path
+        got = P.cpu().numpy()
+        np.testing.assert_array_equal(got[pshift:pshift + total], exp, err_msg=f"pack chunk {chunk}")
+        assert not got[:pshift].any() and not got[pshift + total:].any(), "pack wrote outside its window"
+    pre = rng.integers(0, 256, span, dtype=np.uint8)
+    exp_u = pre.copy()
+    O.mxo_ddt_convert(d.desc.ctypes.data, d.nrec, bs.ctypes.data, d.lb, d.ub, count, exp_u.ctypes.data - tl,
+                      exp.ctypes.data, 1)
+    Pk = torch.zeros(total + 32, dtype=torch.uint8, device="cuda")
+    Pk[pshift:pshift + total] = torch.from_numpy(exp).cuda()
+    for chunk in chunks:
+        D = torch.zeros(span + 32, dtype=torch.uint8, device="cuda")
+        D[shift:shift + span] = torch.from_numpy(pre).cuda()
+        dbase = D.data_ptr() + shift - tl
+        off = 0
+        while off < total:
+            ln = total - off if chunk is None else min(chunk, total - off)
+            dt.unpack(count, dbase, Pk.data_ptr() + pshift + off, offset=off, length=ln, stream=st)
+            off += ln
+        torch.cuda.synchronize()
+        assert dt.last_path == expect_path
+        got = D.cpu().numpy()
+        np.testing.assert_array_equal(got[shift:shift + span], exp_u, err_msg=f"unpack chunk {chunk}")
+        assert not got[:shift].any() and not got[shift + span:].any(), "unpack wrote outside the span"
+
+
+class _Big:
+    """A synthetic committed description (ELEM records) with its true bounds."""
+
+    def __init__(self, elems, size, lb, ub):
+        import test_convertor_pins as P
+        dd = P.Desc(elems, size, lb, ub)
+        self.desc = np.frombuffer(dd.bytes, np.uint8).copy()
+        self.nrec, self.size, self.lb, self.ub = dd.nrec, size, lb, ub
+        self.true_lb = min(disp + min(0, (cnt - 1) * ext) for t, cnt, blen, ext, disp in elems)
+        self.true_ub = max(disp + max(0, (cnt - 1) * ext) + blen * _ES[t] for t, cnt, blen, ext, disp in elems)
+
+    def dt(self):
+        return mxompi.Datatype(self.desc.tobytes(), self.nrec, self.size, self.lb, self.ub)
+
+
+_ES = {4: 1, 6: 4, 15: 4, 16: 8}     # OPAL INT1, INT4, FLOAT4, FLOAT8
+
+
+def _random_indexed(nb, seed, t=15, max_bl=64, max_gap=16, shuffle=False):
+    """indexed_f32_random's recipe (oracle/gen_ddt_golden.c) at nb blocks:
+    1..max_bl-element blocks, 0..max_gap-element gaps; `shuffle` permutes the
+    blocks' order in the stream (a non-monotonic layout)."""
+    es = _ES[t]
+    rng = np.random.default_rng(seed)
+    bl = rng.integers(1, max_bl + 1, nb)
+    gaps = rng.integers(0, max_gap + 1, nb)
+    dp = np.cumsum(gaps) + np.concatenate(([0], np.cumsum(bl)[:-1]))
+    order = rng.permutation(nb) if shuffle else np.arange(nb)
+    elems = [(t, 1, int(bl[i]), int(bl[i]) * es, int(dp[i]) * es) for i in order]
+    lo = int(dp.min()) * es
+    hi = int((dp + bl).max()) * es
+    return _Big(elems, int(bl.sum()) * es, lo, hi)
+
+
+def _upper_triangle(n):
+    """upper triangle of an n x n double matrix (row i: n - i elements from (i, i))."""
+    elems = [(16, 1, n - i, (n - i) * 8, (i * n + i) * 8) for i in range(n)]
+    return _Big(elems, n * (n + 1) // 2 * 8, 0, n * n * 8)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("shift,pshift", [(0, 0), (3, 0), (8, 5), (1, 16)])
+def test_block_kernels_indexed_1e5_random_blocks(shift, pshift):
+    """An indexed type of 10^5 random blocks (a 13 MB instance: no byte map)
+    takes the BLOCK kernels by default; bit-exact vs the oracle, whole and in
+    odd fragments that cut blocks and granules, misaligned user and packed."""
+    mxompi.init(0)
+    d = _random_indexed(100000, 7)
+    dt = d.dt()
+    _check_device_vs_oracle(d, dt, 3, shift, pshift, chunks=(None, 1000003, 4099))
+    dt.close()
+
+
+@pytest.mark.gpu
+def test_block_kernels_upper_triangle_500():
+    """The 500 x 500 upper triangle (1 MB instances), 4 instances, fragments."""
+    mxompi.init(0)
+    d = _upper_triangle(500)
+    dt = d.dt()
+    _check_device_vs_oracle(d, dt, 4, 4, 0, chunks=(None, 65537))
+    dt.close()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("shuffle", [False, True])
+def test_block_kernels_byte_blocks(shuffle):
+    """1..3-byte blocks with 0..2-byte gaps (many parts per granule: the PACK
+    kernel's multi-round part loop), in stream order and shuffled."""
+    mxompi.init(0)
+    d = _random_indexed(120000, 9, t=4, max_bl=3, max_gap=2, shuffle=shuffle)
+    dt = d.dt()
+    _check_device_vs_oracle(d, dt, 2, 5, 3, chunks=(None, 7777))
+    dt.close()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("rec", RECS, ids=lambda r: r["name"])
+def test_block_kernels_forced_on_golden_types(rec):
+    """MX_DDT_PATH_BLOCK on every golden type (small instances, many per tile):
+    the reference's own packed streams and unpack results, whole and in odd
+    fragments."""
+    mxompi.init(0)
+    dt = _dt(rec)
+    dt.set_path("block")
+    total = rec["size"] * rec["count"]
+    contiguous = rec["size"] == rec["ub"] - rec["lb"] and dt.runs == 1
+    want = "copy" if contiguous else "block"
+    U = torch.from_numpy(rec["user"].copy()).cuda()
+    s = torch.cuda.current_stream().cuda_stream
+    base = U.data_ptr() - rec["true_lb"]
+    for chunk in (None, 11, 956):
+        P = torch.zeros(total + 64, dtype=torch.uint8, device="cuda")
+        off = 0
+        while off < total:
+            ln = total - off if chunk is None else min(chunk, total - off)
+            dt.pack(rec["count"], base, P.data_ptr() + off, offset=off, length=ln, stream=s)
+            off += ln
+        torch.cuda.synchronize()
+        assert dt.last_path == want
+        np.testing.assert_array_equal(P.cpu().numpy()[:total], rec["packed"], err_msg=f"{rec['name']} {chunk}")
+    for chunk in (None, 13, 1000):
+        D = torch.from_numpy(rec["prefill"].copy()).cuda()
+        Pk = torch.from_numpy(rec["packed"].copy()).cuda()
+        dbase = D.data_ptr() - rec["true_lb"]
+        off = 0
+        while off < total:
+            ln = total - off if chunk is None else min(chunk, total - off)
+            dt.unpack(rec["count"], dbase, Pk.data_ptr() + off, offset=off, length=ln, stream=s)
+            off += ln
+        torch.cuda.synchronize()
+        assert dt.last_path == want
+        np.testing.assert_array_equal(D.cpu().numpy(), rec["unpacked"], err_msg=f"{rec['name']} unpack {chunk}")
+    dt.close()

@@ -6,6 +6,11 @@ rocprofv3 --pmc passes.
 
 Types: golden names (tests/golden/ddt_vectors.bin), or
   vec:<f32|f64>:<blocklen>:<stride>   MPI_Type_vector(n, blocklen, stride)
+  tri:<n>                              upper triangle of an n x n double matrix (row i: n - i
+                                       elements from (i, i); ref_upper_matrix_60 at size n)
+  idx:<nblocks>:<seed>                 MPI_Type_indexed of f32, nblocks random blocks of 1..64
+                                       elements with 0..16-element gaps (the indexed_f32_random
+                                       recipe of oracle/gen_ddt_golden.c at large block counts)
 usage: conv_probe.py [--bytes N] [--dirs pack,unpack] [--reps R] TYPE [TYPE ...]
 Algorithmic bytes: 2 x packed bytes.  Prints one line per (type, direction).
 """
@@ -28,6 +33,21 @@ def make_type(mx, name):
         # `stride` elements (== MPI_Type_vector(n, blocklen, stride) as a whole)
         d = P.Desc([(tid, 1, int(blen), int(blen) * es, 0)], int(blen) * es, 0, int(stride) * es)
         return mx.Datatype(d.bytes, d.nrec, d.size, d.lb, d.ub), d.size, d.ub - d.lb, 0, int(blen) * es
+    if name.startswith("tri:"):
+        import test_convertor_pins as P
+        n = int(name.split(":")[1])
+        d = P.indexed([n - i for i in range(n)], [i * n + i for i in range(n)], 16, 8)
+        return mx.Datatype(d.bytes, d.nrec, d.size, d.lb, d.ub), d.size, d.ub - d.lb, d.lb, d.ub
+    if name.startswith("idx:"):
+        import numpy as np
+        import test_convertor_pins as P
+        _, nb, seed = name.split(":")
+        rng = np.random.default_rng(int(seed))
+        bl = rng.integers(1, 65, int(nb))
+        gaps = rng.integers(0, 17, int(nb))
+        dp = np.cumsum(gaps) + np.concatenate(([0], np.cumsum(bl)[:-1]))
+        d = P.indexed([int(x) for x in bl], [int(x) for x in dp], 15, 4)
+        return mx.Datatype(d.bytes, d.nrec, d.size, d.lb, d.ub), d.size, d.ub - d.lb, d.lb, d.ub
     import golden_io
     _, recs = golden_io.ddt_records()
     r = next(x for x in recs if x["name"] == name)

@@ -24,6 +24,7 @@
 #include <climits>
 #include <algorithm>
 #include <mutex>
+#include <atomic>
 
 #include "mx_internal.h"
 #include "../../include/mx_convertor.h"
@@ -838,6 +839,554 @@ __global__ void __launch_bounds__(kCB) k_pack_piece(PieceArgs a) {
   }
 }
 
+// ---------------------------------------------------------------------------
+// BLOCK kernels (instances the byte map / piece tables do not take: more
+// than kBmapMaxS packed bytes -- an indexed type with 10^5 blocks, a large
+// triangle -- whose run tables are too long for the LDS search of the tile
+// kernels; map_pos over 10^5 runs is 17 dependent global loads per lane).
+// The instance is tabled once on the host as its contiguous user blocks in
+// stream order (DBlk, 16 B), plus tfirst[k] = the block holding instance
+// stream byte k*G (G = 256).  A workgroup owns T bytes of packed MEMORY
+// (whole 16-byte granules, T <= 16 KiB chosen so that no T-byte stretch of
+// the stream overlaps more than kBlkCap blocks); two lanes locate its first
+// and last block (tfirst + a few-step search, L2-resident tables) and the
+// workgroup stages the blocks between them -- across instance boundaries,
+// user offsets relative to the first instance, stream offsets relative to
+// the tile -- in LDS.  Lane l then takes granule l: one aligned 16-byte
+// access on the packed side, an LDS search for its first block, and on the
+// user side
+//   UNPACK: the granule's bytes stored block part by block part, each part
+//           cut into naturally aligned 1/2/4/8/16-byte stores (gap bytes are
+//           never written);
+//   PACK:   each part fetched with the one or two aligned 16-byte loads
+//           under it (the loads of up to kBlkParts parts issued before any
+//           is used), funnel-shifted into place; one 16-byte store.
+// Only lines holding data are touched on the user side and no lane walks
+// more than its own 16 bytes.
+// ---------------------------------------------------------------------------
+constexpr uint32_t kBlkCap = 1024;         // staged blocks per tile (16 KiB of LDS)
+constexpr uint32_t kBlkG = 256;            // tfirst granularity (instance stream bytes)
+
+struct DBlk { int64_t uoff; uint32_t soff; uint32_t len; };
+struct SBlk { int64_t u; int32_t s; uint32_t len; };   // u: from instance ia's origin; s: from the tile start
+
+struct BlkArgs {
+  const DBlk *blk;
+  uint32_t nblk;
+  Magic mnblk;
+  const uint32_t *tfirst;  // tfirst[q / kBlkG]
+  uint64_t S;
+  Magic mS;
+  int64_t ext;
+  char *user;
+  char *packed;            // window [offset, offset + len) of the stream
+  uint64_t offset, len;
+  uint64_t T;              // packed-memory bytes per tile (multiple of 16)
+  uint64_t ntiles;
+  int w4;                  // UNPACK: a granule inside one block at a 4-byte-aligned user address is one dwordx4 store
+};
+
+// block holding instance stream byte q
+__device__ __forceinline__ uint32_t blk_find(const BlkArgs &a, uint64_t q) {
+  const uint32_t k = (uint32_t)(q / kBlkG);
+  uint32_t lo = a.tfirst[k], hi = a.tfirst[k + 1];
+  while (lo < hi) {
+    const uint32_t mid = (lo + hi + 1) >> 1;
+    if (a.blk[mid].soff <= q) lo = mid; else hi = mid - 1;
+  }
+  return lo;
+}
+
+// last staged block whose tile-relative start is <= x
+__device__ __forceinline__ uint32_t sblk_find(const SBlk *sb, uint32_t n, int32_t x) {
+  uint32_t lo = 0, hi = n - 1;
+  while (lo < hi) {
+    const uint32_t mid = (lo + hi + 1) >> 1;
+    if (sb[mid].s <= x) lo = mid; else hi = mid - 1;
+  }
+  return lo;
+}
+
+__device__ __forceinline__ unsigned __int128 u128(const uint4 v) {
+  return (unsigned __int128)v.x | ((unsigned __int128)v.y << 32) | ((unsigned __int128)v.z << 64) |
+         ((unsigned __int128)v.w << 96);
+}
+
+// widest naturally aligned store (<= 16 B, <= n bytes) at u, from the low bytes of w
+__device__ __forceinline__ uint32_t store_piece(char *u, unsigned __int128 w, uint32_t n) {
+  const uint32_t al = (uint32_t)__builtin_ctzll((uint64_t)(uintptr_t)u | 16);
+  const uint32_t ln = 31u - (uint32_t)__builtin_clz(n);
+  const uint32_t lg = al < ln ? al : ln;
+  const uint64_t w0 = (uint64_t)w, w1 = (uint64_t)(w >> 64);
+  switch (lg) {
+    case 0: *reinterpret_cast<uint8_t *>(u) = (uint8_t)w0; break;
+    case 1: *reinterpret_cast<uint16_t *>(u) = (uint16_t)w0; break;
+    case 2: *reinterpret_cast<uint32_t *>(u) = (uint32_t)w0; break;
+    case 3: *reinterpret_cast<uint64_t *>(u) = w0; break;
+    default: *reinterpret_cast<uint4 *>(u) = make_uint4((uint32_t)w0, (uint32_t)(w0 >> 32), (uint32_t)w1,
+                                                        (uint32_t)(w1 >> 32)); break;
+  }
+  return 1u << lg;
+}
+
+// One tile's staging, shared by the BLOCK kernels: the blocks overlapping
+// stream [tb, te) go to sb[] (n entries), and smap[i] = the staged block
+// holding tile-relative stream position x0 + 64 i (x0 = where the tile's
+// first packed-memory granule starts, <= 0), so that a lane's search is a
+// few steps inside [smap[i], smap[i + 1]].
+struct BlkTile {
+  uint64_t ia;       // first instance of the tile
+  uint32_t n;        // staged blocks
+};
+
+__device__ __forceinline__ BlkTile blk_stage(const BlkArgs &a, SBlk *sb, uint16_t *smap, uint32_t nmap,
+                                             uint64_t tb, uint64_t te, int32_t x0, uint64_t *s_i, uint32_t *s_b) {
+  __syncthreads();                                            // previous tile done with sb / smap
+  if (threadIdx.x == 0 || threadIdx.x == 64) {
+    const int w = threadIdx.x ? 1 : 0;
+    const uint64_t p = w ? te - 1 : tb;
+    const uint64_t i = udiv(p, a.mS);
+    s_i[w] = i;
+    s_b[w] = blk_find(a, p - i * a.S);
+  }
+  __syncthreads();
+  BlkTile T;
+  T.ia = s_i[0];
+  const uint32_t ba = s_b[0];
+  T.n = (uint32_t)((s_i[1] - T.ia) * a.nblk + s_b[1] - ba + 1);   // <= kBlkCap (host's choice of T)
+  for (uint32_t e = threadIdx.x; e < T.n; e += kCB) {
+    const uint32_t L = ba + e;
+    const uint32_t di = (uint32_t)udiv(L, a.mnblk);
+    const DBlk B = a.blk[L - di * a.nblk];
+    SBlk x;
+    x.u = (int64_t)di * a.ext + B.uoff;
+    x.s = (int32_t)((int64_t)((T.ia + di) * a.S + B.soff) - (int64_t)tb);
+    x.len = B.len;
+    sb[e] = x;
+  }
+  __syncthreads();
+  for (uint32_t i = threadIdx.x; i < nmap; i += kCB) {
+    const int32_t x = x0 + 64 * (int32_t)i;
+    smap[i] = (uint16_t)(x <= 0 ? 0 : sblk_find(sb, T.n, x));
+  }
+  __syncthreads();
+  return T;
+}
+
+// staged block holding tile-relative stream position x
+__device__ __forceinline__ uint32_t blk_search(const SBlk *sb, const uint16_t *smap, uint32_t n, uint32_t nmap,
+                                               int32_t x0, int32_t x) {
+  const uint32_t i = (uint32_t)(x - x0) >> 6;
+  uint32_t lo = smap[i], hi = i + 1 < nmap ? smap[i + 1] : n - 1;
+  while (lo < hi) {
+    const uint32_t mid = (lo + hi + 1) >> 1;
+    if (sb[mid].s <= x) lo = mid; else hi = mid - 1;
+  }
+  return lo;
+}
+
+constexpr uint32_t kBlkMaxT = 65536;       // largest tile (packed-memory bytes)
+constexpr uint32_t kBlkMaxMap = kBlkMaxT / 64;
+
+// 16 bytes at dword alignment: one dwordx4 access where the user address
+// is only 4-byte aligned (the compiler picks the instruction for align 4)
+struct __attribute__((aligned(4))) W4 { uint32_t x, y, z, w; };
+
+// Lane l owns the 16-byte packed-memory granules l, l + kCB, ... of the
+// tile, kBlkNG at a time: first every granule's block search and user
+// address, then every granule's loads (unconditional: a granule with
+// nothing to load reads g_blk_dummy, so no branch splits the batch), then
+// the stores -- the loads of kBlkNG granules are in flight together, and
+// the searches are LDS-only.  A granule inside one block (the common case
+// for blocks >> 16 B) is
+//   PACK:   one dwordx4 (+ one dword when the user address is not 4-byte
+//           aligned, joined with alignbyte) and one 16-byte store;
+//   UNPACK: one 16-byte load and one dwordx4 store (4-byte-aligned user
+//           address) or naturally aligned pieces.
+// A granule that straddles blocks or the window edge goes part by part:
+// UNPACK stores each part in aligned pieces; PACK loads the (at most 5)
+// dwords under each part, funnel-shifts them into place and ORs them in.
+__device__ uint32_t g_blk_dummy[8];
+
+// loads through an explicitly global pointer: global_load (vmcnt only), not
+// flat_load, whose lgkmcnt would tie the batch to the LDS searches
+typedef uint32_t v4u_a16 __attribute__((ext_vector_type(4), aligned(16)));
+typedef uint32_t v4u_a4 __attribute__((ext_vector_type(4), aligned(4)));
+__device__ __forceinline__ uint4 gld16(const char *p) {        // 16-byte aligned
+  const v4u_a16 v = *(const __attribute__((address_space(1))) v4u_a16 *)(p);
+  return make_uint4(v.x, v.y, v.z, v.w);
+}
+__device__ __forceinline__ W4 gld16a4(const char *p) {         // 4-byte aligned
+  const v4u_a4 v = *(const __attribute__((address_space(1))) v4u_a4 *)(p);
+  W4 w;
+  w.x = v.x; w.y = v.y; w.z = v.z; w.w = v.w;
+  return w;
+}
+__device__ __forceinline__ uint32_t gld4(const char *p) {
+  return *(const __attribute__((address_space(1))) uint32_t *)(p);
+}
+
+template <bool PACK, int kBlkNG>
+__global__ void __launch_bounds__(kCB) k_convert_blk(BlkArgs a) {
+  __shared__ SBlk sb[kBlkCap];
+  __shared__ uint16_t smap[kBlkMaxMap];
+  __shared__ uint64_t s_i[2];
+  __shared__ uint32_t s_b[2];
+  const uintptr_t pbase = (uintptr_t)a.packed - a.offset;   // memory address of stream byte 0
+  const uintptr_t wlo = (uintptr_t)a.packed, whi = wlo + a.len;
+  const uintptr_t MA = wlo & ~(uintptr_t)15;
+  char *const pk0 = a.packed - (wlo - MA);                    // MA as a (global) pointer
+  const uint32_t nmap = (uint32_t)(a.T / 64);
+  const char *const dummy = reinterpret_cast<const char *>(g_blk_dummy);
+  for (uint64_t t = blockIdx.x; t < a.ntiles; t += gridDim.x) {
+    const uintptr_t mlo = MA + t * a.T;
+    const uintptr_t mhi = mlo + a.T < whi ? mlo + a.T : whi;
+    const uint64_t tb = (mlo > wlo ? mlo : wlo) - pbase, te = mhi - pbase;   // stream [tb, te)
+    const int32_t x0 = (int32_t)((int64_t)(mlo - pbase) - (int64_t)tb);
+    const BlkTile TT = blk_stage(a, sb, smap, nmap, tb, te, x0, s_i, s_b);
+    const uint32_t n = TT.n;
+    char *ubase = a.user + (int64_t)TT.ia * a.ext;
+    for (uintptr_t gb = mlo + (uintptr_t)threadIdx.x * 16; gb < mhi; gb += (uintptr_t)kCB * 16 * kBlkNG) {
+      int32_t xs[kBlkNG], xe[kBlkNG];
+      uint32_t es[kBlkNG];
+      int st[kBlkNG];                                         // 0 none, 1 inside one block, 2 part by part
+      char *up[kBlkNG];
+#pragma unroll
+      for (int k = 0; k < kBlkNG; k++) {
+        const uintptr_t ga = gb + (uintptr_t)k * kCB * 16;
+        st[k] = 0;
+        up[k] = nullptr;
+        if (ga < mhi) {
+          const uintptr_t m0 = ga > wlo ? ga : wlo, m1 = ga + 16 < mhi ? ga + 16 : mhi;
+          xs[k] = (int32_t)(m0 - pbase - tb);                 // tile-relative stream positions
+          xe[k] = (int32_t)(m1 - pbase - tb);
+          es[k] = blk_search(sb, smap, n, nmap, x0, xs[k]);
+          const SBlk B = sb[es[k]];
+          up[k] = ubase + B.u + (xs[k] - B.s);
+          st[k] = (m0 == ga && m1 == ga + 16 && xs[k] + 16 <= B.s + (int32_t)B.len) ? 1 : 2;
+        }
+      }
+      if (!PACK) {
+        uint4 v[kBlkNG];
+#pragma unroll
+        for (int k = 0; k < kBlkNG; k++) {
+          const char *g = st[k] ? pk0 + (gb - MA) + (uintptr_t)k * kCB * 16 : dummy;
+          v[k] = gld16(g);
+        }
+#pragma unroll
+        for (int k = 0; k < kBlkNG; k++) {
+          if (st[k] == 1 && ((uintptr_t)up[k] & 3) == 0 && a.w4) {
+            W4 w;
+            w.x = v[k].x; w.y = v[k].y; w.z = v[k].z; w.w = v[k].w;
+            *reinterpret_cast<W4 *>(up[k]) = w;
+          } else if (st[k]) {
+            const int32_t xg = (int32_t)(gb + (uintptr_t)k * kCB * 16 - pbase - tb);
+            const unsigned __int128 vv = u128(v[k]);
+            int32_t x = xs[k];
+            uint32_t e = es[k];
+            while (x < xe[k]) {
+              const SBlk B = sb[e++];
+              const int32_t bend = B.s + (int32_t)B.len;
+              const int32_t stop = bend < xe[k] ? bend : xe[k];
+              char *u = ubase + B.u + (x - B.s);
+              unsigned __int128 w = vv >> (8 * (x - xg));
+              uint32_t left = (uint32_t)(stop - x);
+              while (left) {
+                const uint32_t q = store_piece(u, w, left);
+                u += q;
+                left -= q;
+                w = q == 16 ? 0 : (w >> (8 * q));
+              }
+              x = stop;
+            }
+          }
+        }
+      } else {
+        W4 l[kBlkNG];
+        uint32_t h[kBlkNG];
+#pragma unroll
+        for (int k = 0; k < kBlkNG; k++) {
+          const uint32_t sh = (uint32_t)((uintptr_t)up[k] & 3);
+          const char *p4 = st[k] == 1 ? up[k] - sh : dummy;
+          const char *ph = st[k] == 1 && sh ? up[k] - sh + 16 : dummy;
+          l[k] = gld16a4(p4);
+          h[k] = gld4(ph);
+        }
+#pragma unroll
+        for (int k = 0; k < kBlkNG; k++) {
+          char *gp = pk0 + (gb - MA) + (uintptr_t)k * kCB * 16;
+          if (st[k] == 1) {
+            const uint32_t sh = (uint32_t)((uintptr_t)up[k] & 3);
+            *reinterpret_cast<uint4 *>(gp) =
+                make_uint4(__builtin_amdgcn_alignbyte(l[k].y, l[k].x, sh), __builtin_amdgcn_alignbyte(l[k].z, l[k].y, sh),
+                           __builtin_amdgcn_alignbyte(l[k].w, l[k].z, sh), __builtin_amdgcn_alignbyte(h[k], l[k].w, sh));
+          } else if (st[k] == 2) {
+            const int32_t xg = (int32_t)(gb + (uintptr_t)k * kCB * 16 - pbase - tb);
+            unsigned __int128 acc = 0;
+            int32_t x = xs[k];
+            uint32_t e = es[k];
+            while (x < xe[k]) {
+              const SBlk B = sb[e++];
+              const int32_t bend = B.s + (int32_t)B.len;
+              const int32_t stop = bend < xe[k] ? bend : xe[k];
+              const char *u = ubase + B.u + (x - B.s);
+              const uint32_t pn = (uint32_t)(stop - x), sh = (uint32_t)((uintptr_t)u & 3);
+              const char *u4 = u - sh;
+              const uint32_t nd = (sh + pn + 3) / 4;            // dwords holding the part (<= 5)
+              uint32_t d[5];
+#pragma unroll
+              for (int j = 0; j < 5; j++)
+                d[j] = gld4((uint32_t)j < nd ? u4 + 4 * j : dummy);
+              const uint32_t w0 = __builtin_amdgcn_alignbyte(d[1], d[0], sh);
+              const uint32_t w1 = __builtin_amdgcn_alignbyte(d[2], d[1], sh);
+              const uint32_t w2 = __builtin_amdgcn_alignbyte(d[3], d[2], sh);
+              const uint32_t w3 = __builtin_amdgcn_alignbyte(d[4], d[3], sh);
+              unsigned __int128 w = (unsigned __int128)w0 | ((unsigned __int128)w1 << 32) |
+                                    ((unsigned __int128)w2 << 64) | ((unsigned __int128)w3 << 96);
+              if (pn < 16) w &= (((unsigned __int128)1) << (8 * pn)) - 1;
+              acc |= w << (8 * (x - xg));
+              x = stop;
+            }
+            if (xs[k] == xg && xe[k] == xg + 16) {
+              *reinterpret_cast<uint4 *>(gp) = make_uint4((uint32_t)acc, (uint32_t)(acc >> 32), (uint32_t)(acc >> 64),
+                                                          (uint32_t)(acc >> 96));
+            } else {                                          // window edge: the bytes inside only
+              for (int32_t i = xs[k]; i < xe[k]; i++) gp[i - xg] = (char)(acc >> (8 * (i - xg)));
+            }
+          }
+        }
+      }
+    }
+  }
+}
+
+// PACK of monotonic layouts, span-staged: a tile's user bytes all lie in
+// [addr(first byte), addr(last byte)] (at most kBlkSpan bytes: the host's
+// choice of T), so the workgroup stages that span in LDS with coalesced
+// 16-byte loads (every lane's loads in flight at once) and each lane then
+// gathers its granule from LDS -- one 16-byte run of LDS dwords joined with
+// alignbyte when the granule lies inside one block, part by part otherwise
+// -- and leaves with one 16-byte store.  User lines are read once, whole;
+// no lane waits on a dependent global load after the staging.
+constexpr uint32_t kBlkSpan = 24576;
+constexpr int kBlkSpanPer = kBlkSpan / 16 / kCB;   // uint4 per lane
+
+// (pointer arithmetic, not an integer round trip: the compiler must keep
+// seeing an LDS pointer -- a flat access would merge the dwords into one
+// 16-byte load that LDS cannot serve at 4-byte alignment)
+__device__ __forceinline__ unsigned __int128 lds16(const char *p) {   // 16 bytes at any LDS alignment
+  const uint32_t *w = reinterpret_cast<const uint32_t *>(p - ((uintptr_t)p & 3));
+  const uint32_t sh = (uint32_t)((uintptr_t)p & 3);
+  const uint32_t d0 = w[0], d1 = w[1], d2 = w[2], d3 = w[3], d4 = w[4];
+  return (unsigned __int128)__builtin_amdgcn_alignbyte(d1, d0, sh) |
+         ((unsigned __int128)__builtin_amdgcn_alignbyte(d2, d1, sh) << 32) |
+         ((unsigned __int128)__builtin_amdgcn_alignbyte(d3, d2, sh) << 64) |
+         ((unsigned __int128)__builtin_amdgcn_alignbyte(d4, d3, sh) << 96);
+}
+
+// Software pipeline (persistent workgroups, tiles t, t + grid, ...): while
+// the lanes gather tile t out of LDS, tile t + grid's block entries and user
+// span are already in flight into registers; lanes 0-1 of wave 0 then run
+// the two table searches of tile t + 2 grid -- a tile's chain of dependent
+// latencies (search -> block entries -> span) is spread over two gathers.
+constexpr int kBlkPre = 4;                         // block entries per lane (cap <= 1024)
+
+struct SpanTile {          // what the pipeline knows of a tile before staging it
+  uint64_t ia;             // first instance
+  uint32_t ba, n;          // first block (instance ia), blocks overlapping
+  uint32_t nv;             // 16-byte vectors of its user span
+  int64_t lo;              // span start (16-aligned) as a byte offset from a.user
+};
+
+__device__ __forceinline__ void tile_geom(const BlkArgs &a, uint64_t t, uintptr_t &mlo, uintptr_t &mhi, uint64_t &tb,
+                                          uint64_t &te, int32_t &x0) {
+  const uintptr_t pbase = (uintptr_t)a.packed - a.offset;
+  const uintptr_t wlo = (uintptr_t)a.packed, whi = wlo + a.len;
+  mlo = (wlo & ~(uintptr_t)15) + t * a.T;
+  mhi = mlo + a.T < whi ? mlo + a.T : whi;
+  tb = (mlo > wlo ? mlo : wlo) - pbase;
+  te = mhi - pbase;
+  x0 = (int32_t)((int64_t)(mlo - pbase) - (int64_t)tb);
+}
+
+// lanes 0 and 1 of wave 0: the tile's first / last byte -> instance, block,
+// user offset; lane 0 returns the combined SpanTile
+__device__ __forceinline__ SpanTile span_search(const BlkArgs &a, uint64_t t) {
+  uintptr_t mlo, mhi;
+  uint64_t tb, te;
+  int32_t x0;
+  tile_geom(a, t, mlo, mhi, tb, te, x0);
+  const uint32_t lane = threadIdx.x;
+  const uint64_t p = lane ? te - 1 : tb;
+  const uint64_t i = udiv(p, a.mS);
+  const uint64_t q = p - i * a.S;
+  const uint32_t b = blk_find(a, q);
+  const DBlk B = a.blk[b];
+  const int64_t u = (int64_t)i * a.ext + B.uoff + (int64_t)(q - B.soff);   // user offset of byte p
+  const uint64_t i1 = __shfl(i, 1);
+  const uint32_t b1 = __shfl(b, 1);
+  const int64_t u1 = __shfl(u, 1);
+  SpanTile S;
+  S.ia = i;
+  S.ba = b;
+  S.n = (uint32_t)((i1 - i) * a.nblk + b1 - b + 1);
+  const uintptr_t lo = ((uintptr_t)a.user + u) & ~(uintptr_t)15;
+  const uintptr_t hi = ((uintptr_t)a.user + u1 + 16) & ~(uintptr_t)15;
+  S.lo = (int64_t)(lo - (uintptr_t)a.user);
+  S.nv = (uint32_t)((hi - lo) / 16);
+  return S;
+}
+
+__global__ void __launch_bounds__(kCB) k_pack_blk_span(BlkArgs a, uint32_t cap) {
+  extern __shared__ __align__(16) char smem[];
+  char *span = smem;                                          // kBlkSpan + 32
+  SBlk *sb = reinterpret_cast<SBlk *>(smem + kBlkSpan + 32);  // cap
+  uint16_t *smap = reinterpret_cast<uint16_t *>(sb + cap);    // T / 64
+  __shared__ SpanTile s_t[2];
+  const uintptr_t pbase = (uintptr_t)a.packed - a.offset;
+  const uintptr_t wlo = (uintptr_t)a.packed;
+  const uintptr_t MA = wlo & ~(uintptr_t)15;
+  char *const pk0 = a.packed - (wlo - MA);
+  const uint32_t nmap = (uint32_t)(a.T / 64);
+  const uint64_t g = gridDim.x;
+  uint64_t t = blockIdx.x;
+  if (t >= a.ntiles) return;
+  int cur = 0;
+  // registers of the tile in flight
+  DBlk pb[kBlkPre];
+  uint4 ps[kBlkSpanPer];
+  // issue the loads of tile u (its SpanTile in s_t[slot]) into pb / ps
+  auto prefetch = [&](int slot) {
+    const SpanTile U = s_t[slot];
+#pragma unroll
+    for (int k = 0; k < kBlkPre; k++) {
+      const uint32_t e = threadIdx.x + k * kCB;
+      if (e < U.n) {
+        const uint32_t L = U.ba + e;
+        const uint32_t di = (uint32_t)udiv(L, a.mnblk);
+        pb[k] = a.blk[L - di * a.nblk];
+      }
+    }
+    const char *lo = a.user + U.lo;
+#pragma unroll
+    for (int k = 0; k < kBlkSpanPer; k++) {
+      const uint32_t i = threadIdx.x + k * kCB;
+      if (i < U.nv) ps[k] = gld16(lo + 16 * i);
+    }
+  };
+  // move the registers of tile u into LDS (blocks tile-relative)
+  auto commit = [&](int slot, uint64_t u) {
+    const SpanTile U = s_t[slot];
+    uintptr_t mlo, mhi;
+    uint64_t tb, te;
+    int32_t x0;
+    tile_geom(a, u, mlo, mhi, tb, te, x0);
+#pragma unroll
+    for (int k = 0; k < kBlkPre; k++) {
+      const uint32_t e = threadIdx.x + k * kCB;
+      if (e < U.n) {
+        const uint32_t L = U.ba + e;
+        const uint32_t di = (uint32_t)udiv(L, a.mnblk);
+        SBlk x;
+        x.u = (int64_t)di * a.ext + pb[k].uoff;
+        x.s = (int32_t)((int64_t)((U.ia + di) * a.S + pb[k].soff) - (int64_t)tb);
+        x.len = pb[k].len;
+        sb[e] = x;
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < kBlkSpanPer; k++) {
+      const uint32_t i = threadIdx.x + k * kCB;
+      if (i < U.nv) reinterpret_cast<uint4 *>(span)[i] = ps[k];
+    }
+  };
+  auto build_map = [&](int slot, uint64_t u) {
+    uintptr_t mlo, mhi;
+    uint64_t tb, te;
+    int32_t x0;
+    tile_geom(a, u, mlo, mhi, tb, te, x0);
+    const uint32_t n = s_t[slot].n;
+    for (uint32_t i = threadIdx.x; i < nmap; i += kCB) {
+      const int32_t x = x0 + 64 * (int32_t)i;
+      smap[i] = (uint16_t)(x <= 0 ? 0 : sblk_find(sb, n, x));
+    }
+  };
+  // prologue: tile t staged, tile t + g's search in s_t[1]
+  if (threadIdx.x < 2) {
+    const SpanTile S0 = span_search(a, t);
+    const SpanTile S1 = t + g < a.ntiles ? span_search(a, t + g) : S0;
+    if (threadIdx.x == 0) { s_t[0] = S0; s_t[1] = S1; }
+  }
+  __syncthreads();
+  prefetch(0);
+  commit(0, t);
+  __syncthreads();
+  build_map(0, t);
+  __syncthreads();
+  for (;;) {
+    const uint64_t u = t + g, w = t + 2 * g;
+    const bool has_u = u < a.ntiles;
+    if (has_u) prefetch(cur ^ 1);
+    // gather tile t
+    {
+      const SpanTile T0 = s_t[cur];
+      uintptr_t mlo, mhi;
+      uint64_t tb, te;
+      int32_t x0;
+      tile_geom(a, t, mlo, mhi, tb, te, x0);
+      const uint32_t n = T0.n;
+      const char *ubase = a.user + (int64_t)T0.ia * a.ext;
+      const int64_t d0 = (int64_t)(ubase - (a.user + T0.lo));   // LDS offset of user offset 0 of instance ia
+      for (uintptr_t ga = mlo + (uintptr_t)threadIdx.x * 16; ga < mhi; ga += (uintptr_t)kCB * 16) {
+        const uintptr_t m0 = ga > wlo ? ga : wlo, m1 = ga + 16 < mhi ? ga + 16 : mhi;
+        const int32_t xs = (int32_t)(m0 - pbase - tb), xe = (int32_t)(m1 - pbase - tb);
+        const int32_t xg = (int32_t)(ga - pbase - tb);
+        uint32_t e = blk_search(sb, smap, n, nmap, x0, xs);
+        char *gp = pk0 + (ga - MA);
+        SBlk B = sb[e];
+        if (xs == xg && xe == xg + 16 && xs + 16 <= B.s + (int32_t)B.len) {
+          const unsigned __int128 v = lds16(span + d0 + B.u + (xs - B.s));
+          *reinterpret_cast<uint4 *>(gp) =
+              make_uint4((uint32_t)v, (uint32_t)(v >> 32), (uint32_t)(v >> 64), (uint32_t)(v >> 96));
+          continue;
+        }
+        unsigned __int128 acc = 0;
+        int32_t x = xs;
+        while (x < xe) {
+          B = sb[e++];
+          const int32_t bend = B.s + (int32_t)B.len;
+          const int32_t stop = bend < xe ? bend : xe;
+          const uint32_t pn = (uint32_t)(stop - x);
+          unsigned __int128 v = lds16(span + d0 + B.u + (x - B.s));
+          if (pn < 16) v &= (((unsigned __int128)1) << (8 * pn)) - 1;
+          acc |= v << (8 * (x - xg));
+          x = stop;
+        }
+        if (xs == xg && xe == xg + 16) {
+          *reinterpret_cast<uint4 *>(gp) =
+              make_uint4((uint32_t)acc, (uint32_t)(acc >> 32), (uint32_t)(acc >> 64), (uint32_t)(acc >> 96));
+        } else {
+          for (int32_t i = xs; i < xe; i++) gp[i - xg] = (char)(acc >> (8 * (i - xg)));
+        }
+      }
+    }
+    // tile w's searches after the gather: their waits (vmcnt counts in
+    // order) then find the prefetch above mostly landed, instead of
+    // holding wave 0 until it has
+    SpanTile Sw;
+    if (w < a.ntiles && threadIdx.x < 2) Sw = span_search(a, w);
+    __syncthreads();                                          // tile t's LDS and s_t[cur] are free
+    if (!has_u) break;
+    commit(cur ^ 1, u);
+    if (w < a.ntiles && threadIdx.x == 0) s_t[cur] = Sw;
+    __syncthreads();
+    build_map(cur ^ 1, u);
+    __syncthreads();
+    t = u;
+    cur ^= 1;
+  }
+}
+
 }  // namespace mx
 
 using namespace mx;
@@ -867,6 +1416,20 @@ struct mx_ddt {
     uint32_t K = 0;                // pieces per tile
     int built = 0;                 // 1 ok, -1 not applicable
   } ptab[16];
+  // contiguous user blocks of one instance in stream order + tfirst (BLOCK
+  // kernels k_convert_blk), built on first use for instances the byte map
+  // does not take
+  struct BlkTab {
+    std::vector<DBlk> host;
+    DBlk *dev = nullptr;
+    uint32_t *tfirst = nullptr;
+    uint64_t T = 0;                // packed-memory bytes per tile
+    uint64_t Tspan = 0;            // PACK through k_pack_blk_span: its tile (0: not applicable)
+    uint32_t capspan = 0;          // most blocks one of its tiles overlaps
+    int built = 0;                 // 1 ok, -1 not applicable
+  } btab;
+  int force_blk = 0;               // mx_ddt_set_path(MX_DDT_PATH_BLOCK)
+  std::atomic<int> last_path{0};   // mx_ddt_last_path
   std::mutex mu;
 };
 
@@ -1116,6 +1679,166 @@ static mx_ddt::PieceTab *piece_tab(mx_ddt *d, int al) {
   return &P;
 }
 
+// BLOCK kernel geometry (A/B switches; results are identical):
+// MX_CONV_BLK_T = largest tile (4096 .. 65536 packed bytes, default 16384),
+// MX_CONV_BLK_NG = granules per lane in flight (1, 2, 4; default 4 for
+// PACK, 1 for UNPACK: measured, profiles/r03/convertor_r3.txt),
+// MX_CONV_BLK_W4=0 stores every UNPACK granule in naturally aligned pieces.
+static uint64_t conv_blk_tmax() {
+  static const uint64_t t = [] {
+    const char *e = getenv("MX_CONV_BLK_T");
+    const long v = e ? atol(e) : 16384;
+    return (uint64_t)((v >= 4096 && v <= (long)kBlkMaxT && (v & (v - 1)) == 0) ? v : 16384);
+  }();
+  return t;
+}
+static int conv_blk_ng(bool pack) {
+  static const int g = [] {
+    const char *e = getenv("MX_CONV_BLK_NG");
+    const int v = e ? atoi(e) : 0;
+    return (v == 1 || v == 2 || v == 4) ? v : 0;
+  }();
+  return g ? g : (pack ? 4 : 1);
+}
+// MX_CONV_BLK_SPAN=0 keeps PACK of monotonic layouts on the granule
+// kernel instead of the span-staged one (A/B switch).
+static bool conv_blk_span() {
+  static const int on = [] {
+    const char *e = getenv("MX_CONV_BLK_SPAN");
+    return (e && *e == '0') ? 0 : 1;
+  }();
+  return on != 0;
+}
+static int conv_blk_w4() {
+  static const int w = [] {
+    const char *e = getenv("MX_CONV_BLK_W4");
+    return (e && *e == '0') ? 0 : 1;
+  }();
+  return w;
+}
+
+// The block table of k_convert_blk (caller holds d->mu): the instance's
+// contiguous user blocks in stream order (touching blocks merged), tfirst[k]
+// = the block holding instance stream byte k * kBlkG (one entry past the
+// last stretch, so [tfirst[k], tfirst[k + 1]] always brackets the search),
+// and the tile T: the largest of 16 KiB .. 512 B of packed memory whose
+// stream stretch never overlaps more than kBlkCap blocks (a T-byte stretch
+// overlaps at most the blocks from b to the one holding end(b) - 2 + T,
+// over every block b, across instance boundaries).
+static mx_ddt::BlkTab *blk_tab(mx_ddt *d) {
+  mx_ddt::BlkTab &B = d->btab;
+  if (B.built) return B.built > 0 ? &B : nullptr;
+  B.built = -1;
+  const uint64_t S = d->size;
+  const int64_t ext = d->ub - d->lb;
+  constexpr uint64_t kMaxBlocks = (uint64_t)1 << 22;
+  if (S == 0 || S >= ((uint64_t)1 << 31) || ext <= 0) return nullptr;
+  std::vector<DBlk> v;
+  uint64_t soff = 0;
+  for (const DRun &r : d->host) {
+    if (v.size() + r.cnt1 * r.cnt2 > kMaxBlocks + 1) return nullptr;
+    for (uint64_t l2 = 0; l2 < r.cnt2; l2++)
+      for (uint64_t l1 = 0; l1 < r.cnt1; l1++) {
+        const int64_t u = r.disp + (int64_t)l2 * r.stride2 + (int64_t)l1 * r.stride1;
+        if (!v.empty() && v.back().uoff + (int64_t)v.back().len == u && v.back().len + r.blen < ((uint64_t)1 << 31)) {
+          v.back().len += (uint32_t)r.blen;
+        } else {
+          DBlk b;
+          b.uoff = u;
+          b.soff = (uint32_t)soff;
+          b.len = (uint32_t)r.blen;
+          v.push_back(b);
+        }
+        soff += r.blen;
+      }
+  }
+  if (v.empty() || v.size() > kMaxBlocks || soff != S) return nullptr;
+  const uint64_t nb = v.size();
+  auto max_overlap = [&](uint64_t T) {
+    uint64_t mx = 0, j = 0;
+    for (uint64_t b = 0; b < nb; b++) {
+      const uint64_t last = (uint64_t)v[b].soff + v[b].len - 1 + T - 1;   // end(b) - 2 + T
+      if (j < b) j = b;
+      // advance j to the block holding `last` (monotonic in b)
+      while (true) {
+        const uint64_t jn = j + 1, i = jn / nb;
+        const uint64_t start = i * S + v[jn - i * nb].soff;
+        if (start > last) break;
+        j = jn;
+      }
+      mx = std::max<uint64_t>(mx, j - b + 1);
+    }
+    return mx;
+  };
+  uint64_t T = conv_blk_tmax();
+  while (T > 512 && max_overlap(T) > kBlkCap) T /= 2;
+  if (max_overlap(T) > kBlkCap) return nullptr;
+  // span PACK (k_pack_blk_span): monotonic blocks; the user span of a
+  // T-byte stretch that starts in block b and ends in block j is
+  // T + G(j) - G(b), G = user offset - stream offset (non-decreasing), so
+  // its maximum over stretches starting in b is at the last j reachable
+  bool mono = true;
+  for (uint64_t b = 0; b + 1 < nb && mono; b++) mono = v[b].uoff + (int64_t)v[b].len <= v[b + 1].uoff;
+  mono = mono && v[nb - 1].uoff + (int64_t)v[nb - 1].len <= v[0].uoff + ext;
+  uint64_t Ts = 0, caps = 0;
+  if (mono && conv_blk_span()) {
+    auto G = [&](uint64_t j) {
+      const uint64_t i = j / nb;
+      return ((int64_t)i * ext + v[j - i * nb].uoff) - (int64_t)(i * S + v[j - i * nb].soff);
+    };
+    auto max_span = [&](uint64_t TT) {
+      int64_t mx = 0;
+      uint64_t j = 0;
+      for (uint64_t b = 0; b < nb; b++) {
+        const uint64_t last = (uint64_t)v[b].soff + v[b].len - 1 + TT - 1;
+        if (j < b) j = b;
+        while (true) {
+          const uint64_t jn = j + 1, i = jn / nb;
+          if (i * S + v[jn - i * nb].soff > last) break;
+          j = jn;
+        }
+        mx = std::max<int64_t>(mx, G(j) - G(b));
+      }
+      return (int64_t)TT + mx;
+    };
+    for (uint64_t TT = 16384; TT >= 2048; TT /= 2) {
+      if (max_overlap(TT) <= kBlkCap && max_span(TT) + 32 <= (int64_t)kBlkSpan) {
+        Ts = TT;
+        caps = max_overlap(TT) + 1;
+        break;
+      }
+    }
+  }
+  const uint64_t nk = (S + kBlkG - 1) / kBlkG;
+  std::vector<uint32_t> tf(nk + 1);
+  for (uint64_t k = 0, b = 0; k < nk; k++) {
+    while (b + 1 < nb && v[b + 1].soff <= k * kBlkG) b++;
+    tf[k] = (uint32_t)b;
+  }
+  tf[nk] = (uint32_t)(nb - 1);
+  if (hipMalloc((void **)&B.dev, nb * sizeof(DBlk)) != hipSuccess) { B.dev = nullptr; return nullptr; }
+  if (hipMalloc((void **)&B.tfirst, (nk + 1) * sizeof(uint32_t)) != hipSuccess) {
+    (void)hipFree(B.dev);
+    B.dev = nullptr;
+    B.tfirst = nullptr;
+    return nullptr;
+  }
+  if (hipMemcpy(B.dev, v.data(), nb * sizeof(DBlk), hipMemcpyHostToDevice) != hipSuccess ||
+      hipMemcpy(B.tfirst, tf.data(), (nk + 1) * sizeof(uint32_t), hipMemcpyHostToDevice) != hipSuccess) {
+    (void)hipFree(B.dev);
+    (void)hipFree(B.tfirst);
+    B.dev = nullptr;
+    B.tfirst = nullptr;
+    return nullptr;
+  }
+  B.host.swap(v);
+  B.T = T;
+  B.Tspan = Ts;
+  B.capspan = (uint32_t)caps;
+  B.built = 1;
+  return &B;
+}
+
 // index of the piece holding packed byte b of an instance
 static uint32_t piece_of(const std::vector<DPiece> &v, uint64_t b) {
   uint32_t lo = 0, hi = (uint32_t)v.size() - 1;
@@ -1193,6 +1916,8 @@ extern "C" int mx_ddt_destroy(mx_ddt_t *d) {
   if (d->map_dev) (void)hipFree(d->map_dev);
   for (auto &P : d->ptab)
     if (P.dev) (void)hipFree(P.dev);
+  if (d->btab.dev) (void)hipFree(d->btab.dev);
+  if (d->btab.tfirst) (void)hipFree(d->btab.tfirst);
   delete d;
   return MX_SUCCESS;
 }
@@ -1283,6 +2008,19 @@ static bool conv_bmap_dw() {
   return on != 0;
 }
 
+// MX_CONV_BLK: 0 keeps every layout off the BLOCK kernels, 1 (default)
+// sends instances without a byte map (> kBmapMaxS packed bytes) to them,
+// 2 also small instances (A/B against the byte-map / piece kernels; results
+// are identical).
+static int conv_blk_mode() {
+  static const int m = [] {
+    const char *e = getenv("MX_CONV_BLK");
+    const int v = e ? atoi(e) : 1;
+    return (v >= 0 && v <= 2) ? v : 1;
+  }();
+  return m;
+}
+
 static int conv_pipe_geom() {
   static const int g = [] {
     const char *e = getenv("MX_CONV_PIPE_GEOM");
@@ -1324,12 +2062,14 @@ static int convert(const mx_ddt_t *d, size_t count, char *user, char *packed, si
   a.len = len;
   a.pk_vec = ((uintptr_t)packed & 15) == 0;
   hipStream_t s = (hipStream_t)stream;
+  mx_ddt *dm = const_cast<mx_ddt *>(d);
   // a contiguous type (one block, extent = size): the stream is the user
   // bytes themselves -- one copy (ref_contiguous_int2_77 unpack 2.27 TB/s
   // through the piece kernel)
   if (a.nruns == 1 && d->host[0].cnt1 == 1 && d->host[0].cnt2 == 1 && d->host[0].blen == d->size &&
       a.ext == (int64_t)d->size) {
     char *u = user + d->host[0].disp + offset;
+    dm->last_path.store(1, std::memory_order_relaxed);
     return PACK ? copy_async(packed, u, len, s) : copy_async(u, packed, len, s);
   }
   // widest unit that every piece of every granule respects: layout gcd,
@@ -1344,7 +2084,8 @@ static int convert(const mx_ddt_t *d, size_t count, char *user, char *packed, si
   // for 16-byte blocks at 1 GiB, while 4-byte blocks go 2.1 -> 3.5 TB/s here;
   // profiles/r01/convertor_vec_ab.txt)
   if (a.nruns == 1 && d->host[0].cnt2 == 1 && u % 4 == 0 && u != 16 && d->host[0].blen <= kVecMaxBlen &&
-      conv_vec_enabled()) {
+      conv_vec_enabled() && !d->force_blk) {
+    dm->last_path.store(2, std::memory_order_relaxed);
     const DRun &R = d->host[0];
     const uint64_t W = (u % 8 == 0) ? 8 : 4;
     const uint64_t nw = len / W;
@@ -1354,7 +2095,50 @@ static int convert(const mx_ddt_t *d, size_t count, char *user, char *packed, si
     else hipLaunchKernelGGL((k_convert_vec<4, PACK>), grid, block, 0, s, a, R, rblen);
     return mx_check_launch();
   }
+  const int blk = d->force_blk ? 2 : conv_blk_mode();
+  if (blk && (blk == 2 || d->bmap.empty())) {
+    mx_ddt::BlkTab *bt;
+    {
+      std::lock_guard<std::mutex> g(dm->mu);
+      bt = blk_tab(dm);
+    }
+    if (bt) {
+      BlkArgs b;
+      b.blk = bt->dev;
+      b.nblk = (uint32_t)bt->host.size();
+      b.mnblk = make_magic(b.nblk);
+      b.tfirst = bt->tfirst;
+      b.S = d->size;
+      b.mS = d->mS;
+      b.ext = d->ub - d->lb;
+      b.user = user;
+      b.packed = packed;
+      b.offset = offset;
+      b.len = len;
+      b.T = bt->T;
+      const uintptr_t MA = (uintptr_t)packed & ~(uintptr_t)15;
+      b.ntiles = ((uintptr_t)packed + len - MA + b.T - 1) / b.T;
+      const uint64_t grid = std::min<uint64_t>(b.ntiles, (uint64_t)g_num_cus * 8);
+      dm->last_path.store(6, std::memory_order_relaxed);
+      b.w4 = conv_blk_w4();
+      if (PACK && bt->Tspan) {
+        b.T = bt->Tspan;
+        b.ntiles = ((uintptr_t)packed + len - MA + b.T - 1) / b.T;
+        const size_t lds = kBlkSpan + 32 + (size_t)bt->capspan * sizeof(SBlk) + (b.T / 64) * 2;
+        const uint64_t per_cu = std::max<uint64_t>(1, std::min<uint64_t>(8, (160 * 1024) / (lds + 128)));
+        const uint64_t gs = std::min<uint64_t>(b.ntiles, (uint64_t)g_num_cus * per_cu);
+        hipLaunchKernelGGL(k_pack_blk_span, dim3((unsigned)gs), dim3(kCB), lds, s, b, bt->capspan);
+        return mx_check_launch();
+      }
+      const int ng = conv_blk_ng(PACK);
+      if (ng == 1) hipLaunchKernelGGL((k_convert_blk<PACK, 1>), dim3((unsigned)grid), dim3(kCB), 0, s, b);
+      else if (ng == 2) hipLaunchKernelGGL((k_convert_blk<PACK, 2>), dim3((unsigned)grid), dim3(kCB), 0, s, b);
+      else hipLaunchKernelGGL((k_convert_blk<PACK, 4>), dim3((unsigned)grid), dim3(kCB), 0, s, b);
+      return mx_check_launch();
+    }
+  }
   if (u == 16) {
+    dm->last_path.store(3, std::memory_order_relaxed);
     const uint64_t g = (len + 15) / 16;
     hipLaunchKernelGGL((k_convert<16, PACK>), dim3((unsigned)((g + kCB - 1) / kCB)), dim3(kCB), run_lds, s, a);
     return mx_check_launch();
@@ -1384,6 +2168,7 @@ static int convert(const mx_ddt_t *d, size_t count, char *user, char *packed, si
       b.adv_b = (uint32_t)((kCB * 4) % d->size);
       b.adv_io = (int64_t)((kCB * 4) / d->size) * b.ext;
       const bool dw = conv_bmap_dw();
+      dm->last_path.store(4, std::memory_order_relaxed);
 #define MX_BMAP_LAUNCH(M, DW) \
   hipLaunchKernelGGL((k_pack_bmap<kBmapSpan, M, DW>), dim3((unsigned)grid), dim3(kCB), lds, s, b)
       if (d->map16) { if (dw) MX_BMAP_LAUNCH(uint16_t, true); else MX_BMAP_LAUNCH(uint16_t, false); }
@@ -1392,7 +2177,6 @@ static int convert(const mx_ddt_t *d, size_t count, char *user, char *packed, si
       return mx_check_launch();
     }
     if (!PACK || conv_ppack_enabled()) {
-      mx_ddt *dm = const_cast<mx_ddt *>(d);
       mx_ddt::PieceTab *pt;
       {
         std::lock_guard<std::mutex> g(dm->mu);
@@ -1421,6 +2205,7 @@ static int convert(const mx_ddt_t *d, size_t count, char *user, char *packed, si
         const size_t lds = kPieceStage + 48 + (p.tbl_lds ? npi * sizeof(DPiece) : 0);
         const uint64_t per_cu = std::max<uint64_t>(1, std::min<uint64_t>(8, (160 * 1024) / lds));
         const uint64_t grid = std::min<uint64_t>(p.ntiles, (uint64_t)g_num_cus * per_cu);
+        dm->last_path.store(5, std::memory_order_relaxed);
         if (PACK) hipLaunchKernelGGL(k_pack_piece, dim3((unsigned)grid), dim3(kCB), lds, s, p);
         else hipLaunchKernelGGL(k_unpack_piece, dim3((unsigned)grid), dim3(kCB), lds, s, p);
         return mx_check_launch();
@@ -1430,6 +2215,7 @@ static int convert(const mx_ddt_t *d, size_t count, char *user, char *packed, si
   // narrow pieces: tile kernels (PACK needs a monotonic layout so that a
   // tile's user bytes form one span)
   if (!PACK || d->monotonic) {
+    dm->last_path.store(7, std::memory_order_relaxed);
     const int nlds = a.nruns <= 64 ? 1 : 0;
     const size_t rb = nlds ? (size_t)a.nruns * sizeof(DRun) : 0;
     if (PACK && conv_pipe_enabled()) {
@@ -1469,6 +2255,7 @@ static int convert(const mx_ddt_t *d, size_t count, char *user, char *packed, si
     return mx_check_launch();
   }
   const dim3 grid((unsigned)(((len + 15) / 16 + kCB - 1) / kCB)), block(kCB);
+  dm->last_path.store(3, std::memory_order_relaxed);
   switch (u) {
     case 8: hipLaunchKernelGGL((k_convert<8, PACK>), grid, block, run_lds, s, a); break;
     case 4: hipLaunchKernelGGL((k_convert<4, PACK>), grid, block, run_lds, s, a); break;
@@ -1477,6 +2264,20 @@ static int convert(const mx_ddt_t *d, size_t count, char *user, char *packed, si
   }
   return mx_check_launch();
 }
+
+extern "C" int mx_ddt_set_path(mx_ddt_t *d, int path) {
+  if (!d || (path != MX_DDT_PATH_AUTO && path != MX_DDT_PATH_BLOCK)) return MX_ERR_ARG;
+  if (path == MX_DDT_PATH_BLOCK) {
+    int rc = mx_ensure_init();
+    if (rc) return rc;
+    std::lock_guard<std::mutex> g(d->mu);
+    if (!blk_tab(d)) return MX_ERR_UNSUPPORTED;
+  }
+  d->force_blk = path == MX_DDT_PATH_BLOCK;
+  return MX_SUCCESS;
+}
+
+extern "C" int mx_ddt_last_path(const mx_ddt_t *d) { return d ? d->last_path.load(std::memory_order_relaxed) : 0; }
 
 extern "C" int mx_pack(const mx_ddt_t *d, size_t count, const void *user, void *packed, size_t offset, size_t len,
                        void *stream) {

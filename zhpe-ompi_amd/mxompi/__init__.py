@@ -723,6 +723,8 @@ def _ddt_lib():
         L.mx_ddt_runs.argtypes = [vp]
         L.mx_pack.argtypes = [vp, sz, vp, vp, sz, sz, vp]
         L.mx_unpack.argtypes = [vp, sz, vp, vp, sz, sz, vp]
+        L.mx_ddt_set_path.argtypes = [vp, ctypes.c_int]
+        L.mx_ddt_last_path.argtypes = [vp]
         L._mx_ddt_typed = True
     return L
 
@@ -751,6 +753,18 @@ class Datatype:
     @property
     def runs(self):
         return int(_ddt_lib().mx_ddt_runs(self.h))
+
+    # kernel families (include/mx_convertor.h, mx_ddt_last_path)
+    PATHS = {0: None, 1: "copy", 2: "vector", 3: "granule", 4: "bytemap", 5: "piece", 6: "block", 7: "tile"}
+
+    def set_path(self, path):
+        """'auto' or 'block' (mx_ddt_set_path)."""
+        check(_ddt_lib().mx_ddt_set_path(self.h, {"auto": 0, "block": 1}[path]), "mx_ddt_set_path")
+
+    @property
+    def last_path(self):
+        """Kernel family of the last pack / unpack (mx_ddt_last_path)."""
+        return self.PATHS[int(_ddt_lib().mx_ddt_last_path(self.h))]
 
     def pack(self, count, user, packed, offset=0, length=None, stream=0):
         length = self.size * count - offset if length is None else length
