@@ -929,50 +929,6 @@ __device__ __forceinline__ uint32_t store_piece(char *u, unsigned __int128 w, ui
   return 1u << lg;
 }
 
-// One tile's staging, shared by the BLOCK kernels: the blocks overlapping
-// stream [tb, te) go to sb[] (n entries), and smap[i] = the staged block
-// holding tile-relative stream position x0 + 64 i (x0 = where the tile's
-// first packed-memory granule starts, <= 0), so that a lane's search is a
-// few steps inside [smap[i], smap[i + 1]].
-struct BlkTile {
-  uint64_t ia;       // first instance of the tile
-  uint32_t n;        // staged blocks
-};
-
-__device__ __forceinline__ BlkTile blk_stage(const BlkArgs &a, SBlk *sb, uint16_t *smap, uint32_t nmap,
-                                             uint64_t tb, uint64_t te, int32_t x0, uint64_t *s_i, uint32_t *s_b) {
-  __syncthreads();                                            // previous tile done with sb / smap
-  if (threadIdx.x == 0 || threadIdx.x == 64) {
-    const int w = threadIdx.x ? 1 : 0;
-    const uint64_t p = w ? te - 1 : tb;
-    const uint64_t i = udiv(p, a.mS);
-    s_i[w] = i;
-    s_b[w] = blk_find(a, p - i * a.S);
-  }
-  __syncthreads();
-  BlkTile T;
-  T.ia = s_i[0];
-  const uint32_t ba = s_b[0];
-  T.n = (uint32_t)((s_i[1] - T.ia) * a.nblk + s_b[1] - ba + 1);   // <= kBlkCap (host's choice of T)
-  for (uint32_t e = threadIdx.x; e < T.n; e += kCB) {
-    const uint32_t L = ba + e;
-    const uint32_t di = (uint32_t)udiv(L, a.mnblk);
-    const DBlk B = a.blk[L - di * a.nblk];
-    SBlk x;
-    x.u = (int64_t)di * a.ext + B.uoff;
-    x.s = (int32_t)((int64_t)((T.ia + di) * a.S + B.soff) - (int64_t)tb);
-    x.len = B.len;
-    sb[e] = x;
-  }
-  __syncthreads();
-  for (uint32_t i = threadIdx.x; i < nmap; i += kCB) {
-    const int32_t x = x0 + 64 * (int32_t)i;
-    smap[i] = (uint16_t)(x <= 0 ? 0 : sblk_find(sb, T.n, x));
-  }
-  __syncthreads();
-  return T;
-}
-
 // staged block holding tile-relative stream position x
 __device__ __forceinline__ uint32_t blk_search(const SBlk *sb, const uint16_t *smap, uint32_t n, uint32_t nmap,
                                                int32_t x0, int32_t x) {
@@ -983,6 +939,117 @@ __device__ __forceinline__ uint32_t blk_search(const SBlk *sb, const uint16_t *s
     if (sb[mid].s <= x) lo = mid; else hi = mid - 1;
   }
   return lo;
+}
+
+constexpr int kBlkPre = 4;                         // block entries per lane (cap <= 1024)
+
+struct SpanTile {          // what the pipeline knows of a tile before staging it
+  uint64_t ia;             // first instance
+  uint32_t ba, n;          // first block (instance ia), blocks overlapping
+  uint32_t nv;             // 16-byte vectors of its user span
+  int64_t lo;              // span start (16-aligned) as a byte offset from a.user
+};
+
+__device__ __forceinline__ void tile_geom(const BlkArgs &a, uint64_t t, uintptr_t &mlo, uintptr_t &mhi, uint64_t &tb,
+                                          uint64_t &te, int32_t &x0) {
+  const uintptr_t pbase = (uintptr_t)a.packed - a.offset;
+  const uintptr_t wlo = (uintptr_t)a.packed, whi = wlo + a.len;
+  mlo = (wlo & ~(uintptr_t)15) + t * a.T;
+  mhi = mlo + a.T < whi ? mlo + a.T : whi;
+  tb = (mlo > wlo ? mlo : wlo) - pbase;
+  te = mhi - pbase;
+  x0 = (int32_t)((int64_t)(mlo - pbase) - (int64_t)tb);
+}
+
+// lanes 2j and 2j + 1 of wave 0: the first / last byte of tile t ->
+// instance, block, user offset; lane 2j returns the combined SpanTile
+// (every lane of the wave must call it: the pair exchange is a shuffle)
+__device__ __forceinline__ SpanTile span_search(const BlkArgs &a, uint64_t t) {
+  uintptr_t mlo, mhi;
+  uint64_t tb, te;
+  int32_t x0;
+  tile_geom(a, t, mlo, mhi, tb, te, x0);
+  const uint32_t odd = threadIdx.x & 1;
+  const uint64_t p = odd ? te - 1 : tb;
+  const uint64_t i = udiv(p, a.mS);
+  const uint64_t q = p - i * a.S;
+  const uint32_t b = blk_find(a, q);
+  const DBlk B = a.blk[b];
+  const int64_t u = (int64_t)i * a.ext + B.uoff + (int64_t)(q - B.soff);   // user offset of byte p
+  const int src = (int)(threadIdx.x | 1);
+  const uint64_t i1 = __shfl(i, src);
+  const uint32_t b1 = __shfl(b, src);
+  const int64_t u1 = __shfl(u, src);
+  SpanTile S;
+  S.ia = i;
+  S.ba = b;
+  S.n = (uint32_t)((i1 - i) * a.nblk + b1 - b + 1);
+  const uintptr_t lo = ((uintptr_t)a.user + u) & ~(uintptr_t)15;
+  const uintptr_t hi = ((uintptr_t)a.user + u1 + 16) & ~(uintptr_t)15;
+  S.lo = (int64_t)(lo - (uintptr_t)a.user);
+  S.nv = (uint32_t)((hi - lo) / 16);
+  return S;
+}
+
+// The tile directory: wave 0 searches the workgroup's next kSpanBatch tiles
+// at once (one chain of dependent table loads per batch instead of per
+// tile) into a ring of 2 * kSpanBatch SpanTiles.
+constexpr int kSpanBatch = 32;
+
+__device__ __forceinline__ void span_batch(const BlkArgs &a, SpanTile *dir, uint64_t i0) {
+  if (threadIdx.x >= 64) return;
+  const uint64_t j = i0 + threadIdx.x / 2;                    // the workgroup's j-th tile
+  const uint64_t t = blockIdx.x + j * gridDim.x;
+  const SpanTile S = span_search(a, t < a.ntiles ? t : blockIdx.x);
+  if (!(threadIdx.x & 1) && t < a.ntiles) dir[j % (2 * kSpanBatch)] = S;
+}
+
+// The block-entry half of a tile's staging, shared by both BLOCK kernels:
+// blk_prefetch issues the loads of tile U's block entries into registers
+// (kBlkPre per lane), blk_commit writes them into LDS tile-relative once the
+// previous tile is done with it, blk_map builds the 64-byte search map.
+__device__ __forceinline__ void blk_prefetch(const BlkArgs &a, const SpanTile &U, DBlk *pb) {
+#pragma unroll
+  for (int k = 0; k < kBlkPre; k++) {
+    const uint32_t e = threadIdx.x + k * kCB;
+    if (e < U.n) {
+      const uint32_t L = U.ba + e;
+      const uint32_t di = (uint32_t)udiv(L, a.mnblk);
+      pb[k] = a.blk[L - di * a.nblk];
+    }
+  }
+}
+
+__device__ __forceinline__ void blk_commit(const BlkArgs &a, const SpanTile &U, uint64_t u, const DBlk *pb, SBlk *sb) {
+  uintptr_t mlo, mhi;
+  uint64_t tb, te;
+  int32_t x0;
+  tile_geom(a, u, mlo, mhi, tb, te, x0);
+#pragma unroll
+  for (int k = 0; k < kBlkPre; k++) {
+    const uint32_t e = threadIdx.x + k * kCB;
+    if (e < U.n) {
+      const uint32_t L = U.ba + e;
+      const uint32_t di = (uint32_t)udiv(L, a.mnblk);
+      SBlk x;
+      x.u = (int64_t)di * a.ext + pb[k].uoff;
+      x.s = (int32_t)((int64_t)((U.ia + di) * a.S + pb[k].soff) - (int64_t)tb);
+      x.len = pb[k].len;
+      sb[e] = x;
+    }
+  }
+}
+
+__device__ __forceinline__ void blk_map(const BlkArgs &a, uint32_t n, uint64_t u, const SBlk *sb, uint16_t *smap,
+                                        uint32_t nmap) {
+  uintptr_t mlo, mhi;
+  uint64_t tb, te;
+  int32_t x0;
+  tile_geom(a, u, mlo, mhi, tb, te, x0);
+  for (uint32_t i = threadIdx.x; i < nmap; i += kCB) {
+    const int32_t x = x0 + 64 * (int32_t)i;
+    smap[i] = (uint16_t)(x <= 0 ? 0 : sblk_find(sb, n, x));
+  }
 }
 
 constexpr uint32_t kBlkMaxT = 65536;       // largest tile (packed-memory bytes)
@@ -1030,22 +1097,43 @@ template <bool PACK, int kBlkNG>
 __global__ void __launch_bounds__(kCB) k_convert_blk(BlkArgs a) {
   __shared__ SBlk sb[kBlkCap];
   __shared__ uint16_t smap[kBlkMaxMap];
-  __shared__ uint64_t s_i[2];
-  __shared__ uint32_t s_b[2];
+  __shared__ SpanTile s_t[2 * kSpanBatch];
   const uintptr_t pbase = (uintptr_t)a.packed - a.offset;   // memory address of stream byte 0
-  const uintptr_t wlo = (uintptr_t)a.packed, whi = wlo + a.len;
+  const uintptr_t wlo = (uintptr_t)a.packed;
   const uintptr_t MA = wlo & ~(uintptr_t)15;
   char *const pk0 = a.packed - (wlo - MA);                    // MA as a (global) pointer
   const uint32_t nmap = (uint32_t)(a.T / 64);
   const char *const dummy = reinterpret_cast<const char *>(g_blk_dummy);
-  for (uint64_t t = blockIdx.x; t < a.ntiles; t += gridDim.x) {
-    const uintptr_t mlo = MA + t * a.T;
-    const uintptr_t mhi = mlo + a.T < whi ? mlo + a.T : whi;
-    const uint64_t tb = (mlo > wlo ? mlo : wlo) - pbase, te = mhi - pbase;   // stream [tb, te)
-    const int32_t x0 = (int32_t)((int64_t)(mlo - pbase) - (int64_t)tb);
-    const BlkTile TT = blk_stage(a, sb, smap, nmap, tb, te, x0, s_i, s_b);
-    const uint32_t n = TT.n;
-    char *ubase = a.user + (int64_t)TT.ia * a.ext;
+  const uint64_t g = gridDim.x;
+  uint64_t t = blockIdx.x;
+  if (t >= a.ntiles) return;
+  uint64_t it = 0;                                            // t = blockIdx.x + it * g
+  constexpr int kRing = 2 * kSpanBatch;
+  DBlk pb[kBlkPre];
+  // the directory's first batch, tile t staged (prefetching the next
+  // tile's block entries during this one's conversion measured no faster
+  // here: profiles/r03/convertor_r3.txt)
+  span_batch(a, s_t, 0);
+  __syncthreads();
+  blk_prefetch(a, s_t[0], pb);
+  blk_commit(a, s_t[0], t, pb, sb);
+  __syncthreads();
+  blk_map(a, s_t[0].n, t, sb, smap, nmap);
+  __syncthreads();
+  for (;;) {
+    const uint64_t u = t + g;
+    const bool has_u = u < a.ntiles;
+    const int cur = (int)(it % kRing), nxt = (int)((it + 1) % kRing);
+    if (has_u && (it + 1) % kSpanBatch == 0) {               // tiles it + 1 .. it + kSpanBatch
+      span_batch(a, s_t, it + 1);
+      __syncthreads();
+    }
+    uintptr_t mlo, mhi;
+    uint64_t tb, te;
+    int32_t x0;
+    tile_geom(a, t, mlo, mhi, tb, te, x0);
+    const uint32_t n = s_t[cur].n;
+    char *ubase = a.user + (int64_t)s_t[cur].ia * a.ext;
     for (uintptr_t gb = mlo + (uintptr_t)threadIdx.x * 16; gb < mhi; gb += (uintptr_t)kCB * 16 * kBlkNG) {
       int32_t xs[kBlkNG], xe[kBlkNG];
       uint32_t es[kBlkNG];
@@ -1157,6 +1245,15 @@ __global__ void __launch_bounds__(kCB) k_convert_blk(BlkArgs a) {
         }
       }
     }
+    __syncthreads();                                          // tile t's LDS is free
+    if (!has_u) break;
+    blk_prefetch(a, s_t[nxt], pb);
+    blk_commit(a, s_t[nxt], u, pb, sb);
+    __syncthreads();
+    blk_map(a, s_t[nxt].n, u, sb, smap, nmap);
+    __syncthreads();
+    t = u;
+    it++;
   }
 }
 
@@ -1186,63 +1283,14 @@ __device__ __forceinline__ unsigned __int128 lds16(const char *p) {   // 16 byte
 
 // Software pipeline (persistent workgroups, tiles t, t + grid, ...): while
 // the lanes gather tile t out of LDS, tile t + grid's block entries and user
-// span are already in flight into registers; lanes 0-1 of wave 0 then run
-// the two table searches of tile t + 2 grid -- a tile's chain of dependent
-// latencies (search -> block entries -> span) is spread over two gathers.
-constexpr int kBlkPre = 4;                         // block entries per lane (cap <= 1024)
-
-struct SpanTile {          // what the pipeline knows of a tile before staging it
-  uint64_t ia;             // first instance
-  uint32_t ba, n;          // first block (instance ia), blocks overlapping
-  uint32_t nv;             // 16-byte vectors of its user span
-  int64_t lo;              // span start (16-aligned) as a byte offset from a.user
-};
-
-__device__ __forceinline__ void tile_geom(const BlkArgs &a, uint64_t t, uintptr_t &mlo, uintptr_t &mhi, uint64_t &tb,
-                                          uint64_t &te, int32_t &x0) {
-  const uintptr_t pbase = (uintptr_t)a.packed - a.offset;
-  const uintptr_t wlo = (uintptr_t)a.packed, whi = wlo + a.len;
-  mlo = (wlo & ~(uintptr_t)15) + t * a.T;
-  mhi = mlo + a.T < whi ? mlo + a.T : whi;
-  tb = (mlo > wlo ? mlo : wlo) - pbase;
-  te = mhi - pbase;
-  x0 = (int32_t)((int64_t)(mlo - pbase) - (int64_t)tb);
-}
-
-// lanes 0 and 1 of wave 0: the tile's first / last byte -> instance, block,
-// user offset; lane 0 returns the combined SpanTile
-__device__ __forceinline__ SpanTile span_search(const BlkArgs &a, uint64_t t) {
-  uintptr_t mlo, mhi;
-  uint64_t tb, te;
-  int32_t x0;
-  tile_geom(a, t, mlo, mhi, tb, te, x0);
-  const uint32_t lane = threadIdx.x;
-  const uint64_t p = lane ? te - 1 : tb;
-  const uint64_t i = udiv(p, a.mS);
-  const uint64_t q = p - i * a.S;
-  const uint32_t b = blk_find(a, q);
-  const DBlk B = a.blk[b];
-  const int64_t u = (int64_t)i * a.ext + B.uoff + (int64_t)(q - B.soff);   // user offset of byte p
-  const uint64_t i1 = __shfl(i, 1);
-  const uint32_t b1 = __shfl(b, 1);
-  const int64_t u1 = __shfl(u, 1);
-  SpanTile S;
-  S.ia = i;
-  S.ba = b;
-  S.n = (uint32_t)((i1 - i) * a.nblk + b1 - b + 1);
-  const uintptr_t lo = ((uintptr_t)a.user + u) & ~(uintptr_t)15;
-  const uintptr_t hi = ((uintptr_t)a.user + u1 + 16) & ~(uintptr_t)15;
-  S.lo = (int64_t)(lo - (uintptr_t)a.user);
-  S.nv = (uint32_t)((hi - lo) / 16);
-  return S;
-}
-
+// span are already in flight into registers, located through the tile
+// directory (span_batch) -- no tile waits on a chain of dependent loads.
 __global__ void __launch_bounds__(kCB) k_pack_blk_span(BlkArgs a, uint32_t cap) {
   extern __shared__ __align__(16) char smem[];
   char *span = smem;                                          // kBlkSpan + 32
   SBlk *sb = reinterpret_cast<SBlk *>(smem + kBlkSpan + 32);  // cap
   uint16_t *smap = reinterpret_cast<uint16_t *>(sb + cap);    // T / 64
-  __shared__ SpanTile s_t[2];
+  __shared__ SpanTile s_t[2 * kSpanBatch];
   const uintptr_t pbase = (uintptr_t)a.packed - a.offset;
   const uintptr_t wlo = (uintptr_t)a.packed;
   const uintptr_t MA = wlo & ~(uintptr_t)15;
@@ -1251,22 +1299,15 @@ __global__ void __launch_bounds__(kCB) k_pack_blk_span(BlkArgs a, uint32_t cap) 
   const uint64_t g = gridDim.x;
   uint64_t t = blockIdx.x;
   if (t >= a.ntiles) return;
-  int cur = 0;
+  uint64_t it = 0;                                            // t = blockIdx.x + it * g
+  constexpr int kRing = 2 * kSpanBatch;
   // registers of the tile in flight
   DBlk pb[kBlkPre];
   uint4 ps[kBlkSpanPer];
   // issue the loads of tile u (its SpanTile in s_t[slot]) into pb / ps
   auto prefetch = [&](int slot) {
     const SpanTile U = s_t[slot];
-#pragma unroll
-    for (int k = 0; k < kBlkPre; k++) {
-      const uint32_t e = threadIdx.x + k * kCB;
-      if (e < U.n) {
-        const uint32_t L = U.ba + e;
-        const uint32_t di = (uint32_t)udiv(L, a.mnblk);
-        pb[k] = a.blk[L - di * a.nblk];
-      }
-    }
+    blk_prefetch(a, U, pb);
     const char *lo = a.user + U.lo;
 #pragma unroll
     for (int k = 0; k < kBlkSpanPer; k++) {
@@ -1277,46 +1318,16 @@ __global__ void __launch_bounds__(kCB) k_pack_blk_span(BlkArgs a, uint32_t cap) 
   // move the registers of tile u into LDS (blocks tile-relative)
   auto commit = [&](int slot, uint64_t u) {
     const SpanTile U = s_t[slot];
-    uintptr_t mlo, mhi;
-    uint64_t tb, te;
-    int32_t x0;
-    tile_geom(a, u, mlo, mhi, tb, te, x0);
-#pragma unroll
-    for (int k = 0; k < kBlkPre; k++) {
-      const uint32_t e = threadIdx.x + k * kCB;
-      if (e < U.n) {
-        const uint32_t L = U.ba + e;
-        const uint32_t di = (uint32_t)udiv(L, a.mnblk);
-        SBlk x;
-        x.u = (int64_t)di * a.ext + pb[k].uoff;
-        x.s = (int32_t)((int64_t)((U.ia + di) * a.S + pb[k].soff) - (int64_t)tb);
-        x.len = pb[k].len;
-        sb[e] = x;
-      }
-    }
+    blk_commit(a, U, u, pb, sb);
 #pragma unroll
     for (int k = 0; k < kBlkSpanPer; k++) {
       const uint32_t i = threadIdx.x + k * kCB;
       if (i < U.nv) reinterpret_cast<uint4 *>(span)[i] = ps[k];
     }
   };
-  auto build_map = [&](int slot, uint64_t u) {
-    uintptr_t mlo, mhi;
-    uint64_t tb, te;
-    int32_t x0;
-    tile_geom(a, u, mlo, mhi, tb, te, x0);
-    const uint32_t n = s_t[slot].n;
-    for (uint32_t i = threadIdx.x; i < nmap; i += kCB) {
-      const int32_t x = x0 + 64 * (int32_t)i;
-      smap[i] = (uint16_t)(x <= 0 ? 0 : sblk_find(sb, n, x));
-    }
-  };
-  // prologue: tile t staged, tile t + g's search in s_t[1]
-  if (threadIdx.x < 2) {
-    const SpanTile S0 = span_search(a, t);
-    const SpanTile S1 = t + g < a.ntiles ? span_search(a, t + g) : S0;
-    if (threadIdx.x == 0) { s_t[0] = S0; s_t[1] = S1; }
-  }
+  auto build_map = [&](int slot, uint64_t u) { blk_map(a, s_t[slot].n, u, sb, smap, nmap); };
+  // prologue: the first batch of the directory, tile t staged
+  span_batch(a, s_t, 0);
   __syncthreads();
   prefetch(0);
   commit(0, t);
@@ -1324,9 +1335,14 @@ __global__ void __launch_bounds__(kCB) k_pack_blk_span(BlkArgs a, uint32_t cap) 
   build_map(0, t);
   __syncthreads();
   for (;;) {
-    const uint64_t u = t + g, w = t + 2 * g;
+    const uint64_t u = t + g;
     const bool has_u = u < a.ntiles;
-    if (has_u) prefetch(cur ^ 1);
+    const int cur = (int)(it % kRing), nxt = (int)((it + 1) % kRing);
+    if (has_u && (it + 1) % kSpanBatch == 0) {               // tiles it + 1 .. it + kSpanBatch
+      span_batch(a, s_t, it + 1);
+      __syncthreads();
+    }
+    if (has_u) prefetch(nxt);
     // gather tile t
     {
       const SpanTile T0 = s_t[cur];
@@ -1370,20 +1386,14 @@ __global__ void __launch_bounds__(kCB) k_pack_blk_span(BlkArgs a, uint32_t cap) 
         }
       }
     }
-    // tile w's searches after the gather: their waits (vmcnt counts in
-    // order) then find the prefetch above mostly landed, instead of
-    // holding wave 0 until it has
-    SpanTile Sw;
-    if (w < a.ntiles && threadIdx.x < 2) Sw = span_search(a, w);
-    __syncthreads();                                          // tile t's LDS and s_t[cur] are free
+    __syncthreads();                                          // tile t's LDS is free
     if (!has_u) break;
-    commit(cur ^ 1, u);
-    if (w < a.ntiles && threadIdx.x == 0) s_t[cur] = Sw;
+    commit(nxt, u);
     __syncthreads();
-    build_map(cur ^ 1, u);
+    build_map(nxt, u);
     __syncthreads();
     t = u;
-    cur ^= 1;
+    it++;
   }
 }
 
@@ -1681,8 +1691,9 @@ static mx_ddt::PieceTab *piece_tab(mx_ddt *d, int al) {
 
 // BLOCK kernel geometry (A/B switches; results are identical):
 // MX_CONV_BLK_T = largest tile (4096 .. 65536 packed bytes, default 16384),
-// MX_CONV_BLK_NG = granules per lane in flight (1, 2, 4; default 4 for
-// PACK, 1 for UNPACK: measured, profiles/r03/convertor_r3.txt),
+// MX_CONV_BLK_NG = granules per lane in flight (1, 2, 4; default 2 for
+// PACK -- layouts the span kernel does not take -- and 4 for UNPACK:
+// measured, profiles/r03/convertor_r3.txt),
 // MX_CONV_BLK_W4=0 stores every UNPACK granule in naturally aligned pieces.
 static uint64_t conv_blk_tmax() {
   static const uint64_t t = [] {
@@ -1698,7 +1709,7 @@ static int conv_blk_ng(bool pack) {
     const int v = e ? atoi(e) : 0;
     return (v == 1 || v == 2 || v == 4) ? v : 0;
   }();
-  return g ? g : (pack ? 4 : 1);
+  return g ? g : (pack ? 2 : 4);
 }
 // MX_CONV_BLK_SPAN=0 keeps PACK of monotonic layouts on the granule
 // kernel instead of the span-staged one (A/B switch).
