@@ -118,17 +118,29 @@ def bench_reduce_local(torch, mx, steps, warmup, nbytes=1 << 30):
     for _ in range(warmup):
         mx.reduce2("SUM", "FLOAT", a.data_ptr(), b.data_ptr(), n, sp)
     torch.cuda.synchronize()
-    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
-           for _ in range(steps)]
+    # one HIP event pair around the whole timed region (on the launch
+    # stream): per-step event records would put 2 * steps marker packets
+    # between the kernels and slow the very thing being timed
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     t0 = time.perf_counter()
-    for s, e in evs:
-        s.record(stream)
+    e0.record(stream)
+    for _ in range(steps):
         mx.reduce2("SUM", "FLOAT", a.data_ptr(), b.data_ptr(), n, sp)
-        e.record(stream)
+    e1.record(stream)
     torch.cuda.synchronize()
     wall = time.perf_counter() - t0
-    kms = [s.elapsed_time(e) for s, e in evs]
-    return wall, kms, 3.0 * n * 4
+    kms = [e0.elapsed_time(e1) / steps] * steps      # average launch duration incl. the kernel boundaries
+    # parity, outside the timed region: one more call on a fresh copy of b0
+    # against the same IEEE fp32 sum computed by a torch kernel (a 2-operand
+    # fp32 add has one correctly rounded result, so the check is bit-exact)
+    c = b0.clone()
+    mx.reduce2("SUM", "FLOAT", a.data_ptr(), c.data_ptr(), n, sp)
+    ref = a + b0
+    torch.cuda.synchronize()
+    diff = (c.view(torch.int32) != ref.view(torch.int32))
+    nbad = int(diff.sum().item())
+    parity = "ok" if nbad == 0 else f"MISMATCH: {nbad} of {n} elements, first at {int(diff.nonzero()[0, 0])}"
+    return wall, kms, 3.0 * n * 4, parity
 
 
 def bench_allreduce(torch, mx, dist, rank, world, dev, steps, warmup, nbytes=256 << 20):
@@ -544,7 +556,7 @@ def main():
         torch.cuda.synchronize()
         if dist is not None:
             dist.barrier()
-        wall, kms, algo_bytes = bench_reduce_local(torch, mx, args.steps, args.warmup)
+        wall, kms, algo_bytes, parity = bench_reduce_local(torch, mx, args.steps, args.warmup)
         torch.cuda.synchronize()
         t_max = wall
         if dist is not None:
@@ -567,6 +579,9 @@ def main():
                          "kernel": "k_reduce2<float, mx::OpSum, true> (non-temporal instance at >= 384 MiB footprint)",
                          "algorithmic_bytes_per_launch": algo_bytes,
                          "avg_kernel_ms": round(avg_kernel_ms, 4)},
+            "parity": parity,
+            "parity_check": {"what": "one more mx_reduce2 fp32 SUM of the 1 GiB inputs after the timed region, "
+                                     "bit-compared with the same sum by a torch kernel (IEEE fp32 add)"},
         })
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         result["cpu_baseline"] = cpu_baseline_reduce_local(args.cpu_seconds)
