@@ -26,6 +26,11 @@
 namespace mx {
 
 constexpr int kBlock = 256;
+// The non-temporal (>= 384 MiB) vector instances run 128-lane workgroups:
+// tools/bw_probe5.hip, 3 interleaved rounds on one MI355X (fp32 SUM, nt
+// loads + store): 1 GiB 6.49 (256 lanes) -> 6.73 TB/s (128), 2 GiB 6.45 ->
+// 6.64 (64 lanes 6.71), 192 lanes 6.16-6.26; profiles/r03/bw_probe5.txt.
+constexpr int kBlockNT = 128;
 
 template <class T>
 struct alignas(16) vec16 {
@@ -47,12 +52,12 @@ __device__ __forceinline__ void red2_elem(const T *__restrict__ a, T *__restrict
 // loop): measured on MI355X at 1 GiB this dense block->address mapping
 // streams at ~5.9 TB/s vs 4.3-5.6 TB/s for grid-stride variants
 // (tools/bw_probe*.hip).
-template <class T, class OP, bool NT>
-__global__ void __launch_bounds__(kBlock)
+template <class T, class OP, bool NT, int BS = NT ? kBlockNT : kBlock>
+__global__ void __launch_bounds__(BS)
 k_reduce2(const T *__restrict__ a, T *__restrict__ b, size_t n, size_t head, size_t nvec) {
   using V = vec16<T>;
   constexpr int N = V::N;
-  const size_t tid = (size_t)blockIdx.x * kBlock + threadIdx.x;
+  const size_t tid = (size_t)blockIdx.x * BS + threadIdx.x;
   OP op;
   if (tid < nvec) {
     const V *__restrict__ av = reinterpret_cast<const V *>(a + head);
@@ -78,13 +83,13 @@ k_reduce2_elem(const T *__restrict__ a, T *__restrict__ b, size_t n) {
   if (i < n) red2_elem<T, OP>(a, b, i);
 }
 
-template <class T, class OP, bool NT>
-__global__ void __launch_bounds__(kBlock)
+template <class T, class OP, bool NT, int BS = NT ? kBlockNT : kBlock>
+__global__ void __launch_bounds__(BS)
 k_reduce3(const T *__restrict__ a1, const T *__restrict__ a2, T *__restrict__ o, size_t n,
           size_t head, size_t nvec) {
   using V = vec16<T>;
   constexpr int N = V::N;
-  const size_t tid = (size_t)blockIdx.x * kBlock + threadIdx.x;
+  const size_t tid = (size_t)blockIdx.x * BS + threadIdx.x;
   OP op;
   if (tid < nvec) {
     const V *__restrict__ p = reinterpret_cast<const V *>(a1 + head);
@@ -116,11 +121,11 @@ k_reduce3_elem(const T *__restrict__ a1, const T *__restrict__ a2, T *__restrict
 
 // One lane per work item; counts beyond 2^31 blocks x 256 lanes (> 8 TiB of
 // fp32) are rejected by the callers' size check.
-static inline unsigned grid_for(size_t work_items) {
-  size_t g = (work_items + kBlock - 1) / kBlock;
+static inline unsigned grid_for(size_t work_items, size_t bs = kBlock) {
+  size_t g = (work_items + bs - 1) / bs;
   return (unsigned)(g < 1 ? 1 : g);
 }
-static constexpr size_t kMaxItems = ((size_t)1 << 31) * kBlock - kBlock;
+static constexpr size_t kMaxItems = ((size_t)1 << 31) * kBlockNT - kBlockNT;
 
 template <class T, class OP>
 static int launch2(const void *in, void *inout, size_t n, hipStream_t s) {
@@ -139,7 +144,8 @@ static int launch2(const void *in, void *inout, size_t n, hipStream_t s) {
   size_t work = nvec;
   if (work < head + N) work = head + N;  // enough lanes for head + tail
   if (mx_nt_for(2 * n * sizeof(T)))
-    hipLaunchKernelGGL((k_reduce2<T, OP, true>), dim3(grid_for(work)), dim3(kBlock), 0, s, a, b, n, head, nvec);
+    hipLaunchKernelGGL((k_reduce2<T, OP, true>), dim3(grid_for(work, kBlockNT)), dim3(kBlockNT), 0, s, a, b, n, head,
+                       nvec);
   else
     hipLaunchKernelGGL((k_reduce2<T, OP, false>), dim3(grid_for(work)), dim3(kBlock), 0, s, a, b, n, head, nvec);
   return mx_check_launch();
@@ -163,7 +169,8 @@ static int launch3(const void *in1, const void *in2, void *out, size_t n, hipStr
   size_t work = nvec;
   if (work < head + N) work = head + N;
   if (mx_nt_for(3 * n * sizeof(T)))
-    hipLaunchKernelGGL((k_reduce3<T, OP, true>), dim3(grid_for(work)), dim3(kBlock), 0, s, a1, a2, o, n, head, nvec);
+    hipLaunchKernelGGL((k_reduce3<T, OP, true>), dim3(grid_for(work, kBlockNT)), dim3(kBlockNT), 0, s, a1, a2, o, n,
+                       head, nvec);
   else
     hipLaunchKernelGGL((k_reduce3<T, OP, false>), dim3(grid_for(work)), dim3(kBlock), 0, s, a1, a2, o, n, head, nvec);
   return mx_check_launch();
