@@ -124,12 +124,53 @@ def test_full_size_fp32_sum_1gib():
     np.testing.assert_array_equal(got.view(np.uint32), b.view(np.uint32))
 
 
-# CFG-B at full size beyond fp32 SUM: one pair per kernel family / operator
-# class, 1 GiB per buffer (the non-temporal instance), checked against the
-# restatement element for element.  Inputs: full-range bytes for integer and
-# bitwise ops, ties-heavy pairs for the LOC ops, [0.5, 2) for FP PROD.
+# CFG-B at full size beyond fp32 SUM: one pair per kernel family x element
+# size (arithmetic, MAX/MIN, bitwise, logical, complex, x87 soft-float, every
+# LOC pair layout), 1 GiB per buffer (the non-temporal 128-lane instance),
+# checked against the restatement element for element.  Inputs: full-range
+# bytes for integer and bitwise ops, a small value range for MAX/MIN and the
+# LOC ops (ties), [0.5, 2) for FP PROD.
 _FULL = [("BAND", "UINT16_T"), ("PROD", "INT64_T"), ("MAX", "DOUBLE"), ("MAXLOC", "FLOAT_INT"),
-         ("MINLOC", "DOUBLE_INT"), ("PROD", "C_FLOAT_COMPLEX"), ("LXOR", "INT8_T"), ("SUM", "LONG_DOUBLE")]
+         ("MINLOC", "DOUBLE_INT"), ("PROD", "C_FLOAT_COMPLEX"), ("LXOR", "INT8_T"), ("SUM", "LONG_DOUBLE"),
+         # round 3: the rest of (family x element size)
+         ("SUM", "INT8_T"), ("SUM", "INT16_T"), ("MIN", "INT32_T"), ("SUM", "UINT64_T"), ("MIN", "FLOAT"),
+         ("PROD", "DOUBLE"), ("MAX", "UINT8_T"), ("SUM", "C_DOUBLE_COMPLEX"), ("PROD", "C_LONG_DOUBLE_COMPLEX"),
+         ("MAX", "LONG_DOUBLE"), ("BOR", "INT32_T"), ("BXOR", "UINT64_T"), ("BAND", "INT8_T"), ("LAND", "INT16_T"),
+         ("LOR", "UINT32_T"), ("MAXLOC", "2INT"), ("MINLOC", "SHORT_INT"), ("MAXLOC", "LONG_INT"),
+         ("MINLOC", "LONG_DOUBLE_INT"), ("PROD", "FLOAT")]
+
+# LOC pair layouts (value dtype, value offset, index offset) -- op.h pair structs, x86-64
+_LOC = {"FLOAT_INT": ("<f4", 0, 4), "DOUBLE_INT": ("<f8", 0, 8), "LONG_INT": ("<i8", 0, 8), "2INT": ("<i4", 0, 4),
+        "SHORT_INT": ("<i2", 0, 4), "LONG_DOUBLE_INT": (np.longdouble, 0, 16)}
+_FP = {"FLOAT": np.float32, "DOUBLE": np.float64, "SHORT_FLOAT": np.float16, "C_FLOAT_COMPLEX": np.float32,
+       "C_DOUBLE_COMPLEX": np.float64}
+
+
+def _full_input(op, t, n, es, rng):
+    raw = [rng.integers(0, 256, n * es, dtype=np.uint8) for _ in range(2)]   # padding bytes stay random
+    for r in raw:
+        rows = r.reshape(n, es)
+        if t in _LOC:
+            vt, vo, io = _LOC[t]
+            vs = np.dtype(vt).itemsize
+            vals = rng.integers(0, 16, n).astype(vt)                    # ties
+            vb = vals.view(np.uint8).reshape(n, -1)[:, :min(vs, 10 if vt is np.longdouble else vs)]
+            rows[:, vo:vo + vb.shape[1]] = vb
+            rows[:, io:io + 4] = rng.integers(-1000, 1000, n).astype("<i4").view(np.uint8).reshape(n, 4)
+        elif t in ("LONG_DOUBLE", "C_LONG_DOUBLE_COMPLEX"):
+            k = es // 16
+            lo, hi = (0.5, 2.0) if op == "PROD" else (-4.0, 4.0)
+            v = rng.uniform(lo, hi, n * k).astype(np.longdouble).view(np.uint8).reshape(n * k, 16)[:, :10]
+            rows.reshape(n * k, 16)[:, :10] = v
+        elif t in _FP:
+            ft = _FP[t]
+            k = es // np.dtype(ft).itemsize
+            lo, hi = (0.5, 2.0) if op == "PROD" else ((0, 16) if op in ("MAX", "MIN") else (-1e3, 1e3))
+            v = rng.uniform(lo, hi, n * k).astype(ft)
+            if op in ("MAX", "MIN"):
+                v = np.floor(v).astype(ft)
+            rows[:] = v.view(np.uint8).reshape(n, es)
+    return raw
 
 
 @pytest.mark.parametrize("op,t", _FULL, ids=[f"{o}-{t}" for o, t in _FULL])
@@ -138,29 +179,7 @@ def test_full_size_1gib_pairs(op, t):
     es = mxompi.type_size(t)
     n = (1 << 30) // es
     rng = np.random.default_rng(0x5EEDC0DE + mxompi.TYPE[t])
-    if t == "FLOAT_INT":
-        v = np.zeros((2, n), dtype=[("v", "<f4"), ("k", "<i4")])
-        v["v"] = rng.integers(0, 16, (2, n))
-        v["k"] = rng.integers(-1000, 1000, (2, n))
-        raw = [v[0].view(np.uint8), v[1].view(np.uint8)]
-    elif t == "DOUBLE_INT":
-        v = np.zeros((2, n), dtype=[("v", "<f8"), ("k", "<i4"), ("pad", "<i4")])
-        v["v"] = rng.integers(0, 16, (2, n))
-        v["k"] = rng.integers(-1000, 1000, (2, n))
-        v["pad"] = rng.integers(-1 << 31, 1 << 31, (2, n))
-        raw = [v[0].view(np.uint8), v[1].view(np.uint8)]
-    elif t == "C_FLOAT_COMPLEX":
-        raw = [rng.uniform(0.5, 2.0, 2 * n).astype(np.float32).view(np.uint8) for _ in range(2)]
-    elif t == "DOUBLE":
-        raw = [rng.uniform(-1e6, 1e6, n).view(np.uint8) for _ in range(2)]
-    elif t == "LONG_DOUBLE":
-        raw = []
-        for _ in range(2):
-            r = rng.integers(0, 256, n * 16, dtype=np.uint8)
-            r.reshape(-1, 16)[:] = rng.uniform(-4, 4, n).astype(np.longdouble).view(np.uint8).reshape(-1, 16)
-            raw.append(r)
-    else:
-        raw = [rng.integers(0, 256, n * es, dtype=np.uint8) for _ in range(2)]
+    raw = _full_input(op, t, n, es, rng)
     A, B = _dev(raw[0]), _dev(raw[1])
     mxompi.reduce2(op, t, A.data_ptr(), B.data_ptr(), n, _stream())
     torch.cuda.synchronize()

@@ -845,7 +845,7 @@ __global__ void __launch_bounds__(kCB) k_pack_piece(PieceArgs a) {
 // triangle -- whose run tables are too long for the LDS search of the tile
 // kernels; map_pos over 10^5 runs is 17 dependent global loads per lane).
 // The instance is tabled once on the host as its contiguous user blocks in
-// stream order (DBlk, 16 B), plus tfirst[k] = the block holding instance
+// stream order (DBlk, 8 B), plus tfirst[k] = the block holding instance
 // stream byte k*G (G = 256).  A workgroup owns T bytes of packed MEMORY
 // (whole 16-byte granules, T <= 16 KiB chosen so that no T-byte stretch of
 // the stream overlaps more than kBlkCap blocks); two lanes locate its first
@@ -867,7 +867,11 @@ __global__ void __launch_bounds__(kCB) k_pack_piece(PieceArgs a) {
 constexpr uint32_t kBlkCap = 1024;         // staged blocks per tile (16 KiB of LDS)
 constexpr uint32_t kBlkG = 256;            // tfirst granularity (instance stream bytes)
 
-struct DBlk { int64_t uoff; uint32_t soff; uint32_t len; };
+// device block table entry (8 B): user offset from the instance origin and
+// stream offset; a block's length is the next entry's soff minus its own
+// (the table carries one sentinel entry with soff = the instance size)
+struct DBlk { int32_t uoff; uint32_t soff; };
+struct DBlkL { int32_t uoff; uint32_t soff, send; };   // an entry with its end, in registers
 struct SBlk { int64_t u; int32_t s; uint32_t len; };   // u: from instance ia's origin; s: from the tile start
 
 struct BlkArgs {
@@ -1008,19 +1012,23 @@ __device__ __forceinline__ void span_batch(const BlkArgs &a, SpanTile *dir, uint
 // blk_prefetch issues the loads of tile U's block entries into registers
 // (kBlkPre per lane), blk_commit writes them into LDS tile-relative once the
 // previous tile is done with it, blk_map builds the 64-byte search map.
-__device__ __forceinline__ void blk_prefetch(const BlkArgs &a, const SpanTile &U, DBlk *pb) {
+__device__ __forceinline__ void blk_prefetch(const BlkArgs &a, const SpanTile &U, DBlkL *pb) {
 #pragma unroll
   for (int k = 0; k < kBlkPre; k++) {
     const uint32_t e = threadIdx.x + k * kCB;
     if (e < U.n) {
       const uint32_t L = U.ba + e;
       const uint32_t di = (uint32_t)udiv(L, a.mnblk);
-      pb[k] = a.blk[L - di * a.nblk];
+      const DBlk *p = a.blk + (L - di * a.nblk);
+      const DBlk b0 = p[0];
+      pb[k].uoff = b0.uoff;
+      pb[k].soff = b0.soff;
+      pb[k].send = p[1].soff;
     }
   }
 }
 
-__device__ __forceinline__ void blk_commit(const BlkArgs &a, const SpanTile &U, uint64_t u, const DBlk *pb, SBlk *sb) {
+__device__ __forceinline__ void blk_commit(const BlkArgs &a, const SpanTile &U, uint64_t u, const DBlkL *pb, SBlk *sb) {
   uintptr_t mlo, mhi;
   uint64_t tb, te;
   int32_t x0;
@@ -1034,7 +1042,7 @@ __device__ __forceinline__ void blk_commit(const BlkArgs &a, const SpanTile &U, 
       SBlk x;
       x.u = (int64_t)di * a.ext + pb[k].uoff;
       x.s = (int32_t)((int64_t)((U.ia + di) * a.S + pb[k].soff) - (int64_t)tb);
-      x.len = pb[k].len;
+      x.len = pb[k].send - pb[k].soff;
       sb[e] = x;
     }
   }
@@ -1109,7 +1117,7 @@ __global__ void __launch_bounds__(kCB) k_convert_blk(BlkArgs a) {
   if (t >= a.ntiles) return;
   uint64_t it = 0;                                            // t = blockIdx.x + it * g
   constexpr int kRing = 2 * kSpanBatch;
-  DBlk pb[kBlkPre];
+  DBlkL pb[kBlkPre];
   // the directory's first batch, tile t staged (prefetching the next
   // tile's block entries during this one's conversion measured no faster
   // here: profiles/r03/convertor_r3.txt)
@@ -1302,7 +1310,7 @@ __global__ void __launch_bounds__(kCB) k_pack_blk_span(BlkArgs a, uint32_t cap) 
   uint64_t it = 0;                                            // t = blockIdx.x + it * g
   constexpr int kRing = 2 * kSpanBatch;
   // registers of the tile in flight
-  DBlk pb[kBlkPre];
+  DBlkL pb[kBlkPre];
   uint4 ps[kBlkSpanPer];
   // issue the loads of tile u (its SpanTile in s_t[slot]) into pb / ps
   auto prefetch = [&](int slot) {
@@ -1401,6 +1409,8 @@ __global__ void __launch_bounds__(kCB) k_pack_blk_span(BlkArgs a, uint32_t cap) 
 
 using namespace mx;
 
+struct HBlk { int64_t uoff; uint32_t soff; uint32_t len; };   // host side of the block table (blk_tab)
+
 struct mx_ddt {
   std::vector<DRun> host;
   DRun *dev;
@@ -1430,7 +1440,7 @@ struct mx_ddt {
   // kernels k_convert_blk), built on first use for instances the byte map
   // does not take
   struct BlkTab {
-    std::vector<DBlk> host;
+    std::vector<HBlk> host;        // the blocks (the device table adds the sentinel)
     DBlk *dev = nullptr;
     uint32_t *tfirst = nullptr;
     uint64_t T = 0;                // packed-memory bytes per tile
@@ -1744,7 +1754,7 @@ static mx_ddt::BlkTab *blk_tab(mx_ddt *d) {
   const int64_t ext = d->ub - d->lb;
   constexpr uint64_t kMaxBlocks = (uint64_t)1 << 22;
   if (S == 0 || S >= ((uint64_t)1 << 31) || ext <= 0) return nullptr;
-  std::vector<DBlk> v;
+  std::vector<HBlk> v;
   uint64_t soff = 0;
   for (const DRun &r : d->host) {
     if (v.size() + r.cnt1 * r.cnt2 > kMaxBlocks + 1) return nullptr;
@@ -1754,7 +1764,7 @@ static mx_ddt::BlkTab *blk_tab(mx_ddt *d) {
         if (!v.empty() && v.back().uoff + (int64_t)v.back().len == u && v.back().len + r.blen < ((uint64_t)1 << 31)) {
           v.back().len += (uint32_t)r.blen;
         } else {
-          DBlk b;
+          HBlk b;
           b.uoff = u;
           b.soff = (uint32_t)soff;
           b.len = (uint32_t)r.blen;
@@ -1827,14 +1837,22 @@ static mx_ddt::BlkTab *blk_tab(mx_ddt *d) {
     tf[k] = (uint32_t)b;
   }
   tf[nk] = (uint32_t)(nb - 1);
-  if (hipMalloc((void **)&B.dev, nb * sizeof(DBlk)) != hipSuccess) { B.dev = nullptr; return nullptr; }
+  std::vector<DBlk> dv(nb + 1);
+  for (uint64_t b = 0; b < nb; b++) {
+    if (v[b].uoff < INT32_MIN || v[b].uoff > INT32_MAX) return nullptr;   // instance offsets beyond +-2 GiB
+    dv[b].uoff = (int32_t)v[b].uoff;
+    dv[b].soff = v[b].soff;
+  }
+  dv[nb].uoff = 0;
+  dv[nb].soff = (uint32_t)S;
+  if (hipMalloc((void **)&B.dev, (nb + 1) * sizeof(DBlk)) != hipSuccess) { B.dev = nullptr; return nullptr; }
   if (hipMalloc((void **)&B.tfirst, (nk + 1) * sizeof(uint32_t)) != hipSuccess) {
     (void)hipFree(B.dev);
     B.dev = nullptr;
     B.tfirst = nullptr;
     return nullptr;
   }
-  if (hipMemcpy(B.dev, v.data(), nb * sizeof(DBlk), hipMemcpyHostToDevice) != hipSuccess ||
+  if (hipMemcpy(B.dev, dv.data(), (nb + 1) * sizeof(DBlk), hipMemcpyHostToDevice) != hipSuccess ||
       hipMemcpy(B.tfirst, tf.data(), (nk + 1) * sizeof(uint32_t), hipMemcpyHostToDevice) != hipSuccess) {
     (void)hipFree(B.dev);
     (void)hipFree(B.tfirst);
