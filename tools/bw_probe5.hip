@@ -8,7 +8,7 @@
 #include <cstdio>
 typedef float f4 __attribute__((ext_vector_type(4)));
 
-template <int SWZ, int B, int V>
+template <int SWZ, int B, int V, bool NT = true>
 __global__ void __launch_bounds__(B) k_sum(const f4 *__restrict__ a, f4 *__restrict__ b, size_t nvec) {
   size_t blk = blockIdx.x;
   if (SWZ) {  // the blocks one XCD receives (blockIdx % 8 equal) cover one contiguous eighth
@@ -20,12 +20,18 @@ __global__ void __launch_bounds__(B) k_sum(const f4 *__restrict__ a, f4 *__restr
 #pragma unroll
   for (int v = 0; v < V; v++) {
     const size_t i = i0 + (size_t)v * B;
-    if (i < nvec) { x[v] = __builtin_nontemporal_load(&b[i]); y[v] = __builtin_nontemporal_load(&a[i]); }
+    if (i < nvec) {
+      if (NT) { x[v] = __builtin_nontemporal_load(&b[i]); y[v] = __builtin_nontemporal_load(&a[i]); }
+      else { x[v] = b[i]; y[v] = a[i]; }
+    }
   }
 #pragma unroll
   for (int v = 0; v < V; v++) {
     const size_t i = i0 + (size_t)v * B;
-    if (i < nvec) __builtin_nontemporal_store(x[v] + y[v], &b[i]);
+    if (i < nvec) {
+      if (NT) __builtin_nontemporal_store(x[v] + y[v], &b[i]);
+      else b[i] = x[v] + y[v];
+    }
   }
 }
 
@@ -39,8 +45,26 @@ template <class F> float timeit(F f, int it) {
   }
   return best;
 }
-int main() {
-  for (size_t mib : {1024, 2048, 256}) {
+int main(int argc, char **argv) {
+  if (argc > 1 && argv[1][0] == 'c') {   // `bw_probe5 cached`: the default-policy instance below 384 MiB
+    for (size_t mib : {4, 16, 64, 128}) {
+      size_t bytes = mib << 20, nvec = bytes / 16;
+      f4 *a, *b;
+      if (hipMalloc(&a, bytes) != hipSuccess || hipMalloc(&b, bytes) != hipSuccess) return 1;
+      hipMemset(a, 0, bytes); hipMemset(b, 0, bytes);
+      const double algo = 3.0 * bytes;
+      printf("== %zu MiB per buffer (cached policy)\n", mib);
+      auto rep = [&](const char *n, float ms) { printf("%-30s %8.4f ms %8.1f GB/s\n", n, ms, algo / ms / 1e6); };
+      for (int round = 0; round < 3; round++) {
+        rep("B256", timeit([&] { k_sum<0, 256, 1, false><<<(unsigned)((nvec + 255) / 256), 256>>>(a, b, nvec); }, 50));
+        rep("B128", timeit([&] { k_sum<0, 128, 1, false><<<(unsigned)((nvec + 127) / 128), 128>>>(a, b, nvec); }, 50));
+        rep("B64", timeit([&] { k_sum<0, 64, 1, false><<<(unsigned)((nvec + 63) / 64), 64>>>(a, b, nvec); }, 50));
+      }
+      hipFree(a); hipFree(b);
+    }
+    return 0;
+  }
+  for (size_t mib : {4096, 1024}) {
     size_t bytes = mib << 20, nvec = bytes / 16;
     f4 *a, *b;
     if (hipMalloc(&a, bytes) != hipSuccess || hipMalloc(&b, bytes) != hipSuccess) return 1;

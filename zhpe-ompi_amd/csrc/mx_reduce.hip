@@ -26,11 +26,14 @@
 namespace mx {
 
 constexpr int kBlock = 256;
-// The non-temporal (>= 384 MiB) vector instances run 128-lane workgroups:
-// tools/bw_probe5.hip, 3 interleaved rounds on one MI355X (fp32 SUM, nt
-// loads + store): 1 GiB 6.49 (256 lanes) -> 6.73 TB/s (128), 2 GiB 6.45 ->
-// 6.64 (64 lanes 6.71), 192 lanes 6.16-6.26; profiles/r03/bw_probe5.txt.
-constexpr int kBlockNT = 128;
+// The non-temporal (>= 384 MiB) vector instances run one-wave (64-lane)
+// workgroups: tools/bw_probe5.hip, 3 interleaved rounds per box (fp32 SUM,
+// nt loads + store), 256 / 128 / 64 lanes in TB/s -- box A: 1 GiB 6.49 /
+// 6.73 / 6.70, 2 GiB 6.45 / 6.64 / 6.71; box B: 1 GiB 6.17 / 6.44 / 6.75,
+// 4 GiB 6.19 / 6.03 / 6.25 (profiles/r03/bw_probe5*.txt).  The cached
+// instance keeps 256 lanes (64 lanes lose up to 25 % below 64 MiB,
+// bw_probe5_cached.txt).
+constexpr int kBlockNT = 64;
 
 template <class T>
 struct alignas(16) vec16 {
