@@ -128,7 +128,9 @@ static inline unsigned grid_for(size_t work_items, size_t bs = kBlock) {
   size_t g = (work_items + bs - 1) / bs;
   return (unsigned)(g < 1 ? 1 : g);
 }
-static constexpr size_t kMaxItems = ((size_t)1 << 31) * kBlockNT - kBlockNT;
+static constexpr size_t kMaxItems = ((size_t)1 << 31) * kBlock - kBlock;
+// one-wave workgroups while the grid fits 2^31 - 1 of them (vectors up to 2^37: 2 TiB)
+static inline bool nt_small_wg(size_t work) { return work < ((size_t)1 << 31) * kBlockNT - kBlockNT; }
 
 template <class T, class OP>
 static int launch2(const void *in, void *inout, size_t n, hipStream_t s) {
@@ -146,11 +148,16 @@ static int launch2(const void *in, void *inout, size_t n, hipStream_t s) {
   const size_t nvec = N ? (n - head) / N : 0;
   size_t work = nvec;
   if (work < head + N) work = head + N;  // enough lanes for head + tail
-  if (mx_nt_for(2 * n * sizeof(T)))
-    hipLaunchKernelGGL((k_reduce2<T, OP, true>), dim3(grid_for(work, kBlockNT)), dim3(kBlockNT), 0, s, a, b, n, head,
-                       nvec);
-  else
+  if (mx_nt_for(2 * n * sizeof(T))) {
+    if (nt_small_wg(work))
+      hipLaunchKernelGGL((k_reduce2<T, OP, true>), dim3(grid_for(work, kBlockNT)), dim3(kBlockNT), 0, s, a, b, n, head,
+                         nvec);
+    else
+      hipLaunchKernelGGL((k_reduce2<T, OP, true, kBlock>), dim3(grid_for(work)), dim3(kBlock), 0, s, a, b, n, head,
+                         nvec);
+  } else {
     hipLaunchKernelGGL((k_reduce2<T, OP, false>), dim3(grid_for(work)), dim3(kBlock), 0, s, a, b, n, head, nvec);
+  }
   return mx_check_launch();
 }
 
@@ -171,11 +178,16 @@ static int launch3(const void *in1, const void *in2, void *out, size_t n, hipStr
   const size_t nvec = N ? (n - head) / N : 0;
   size_t work = nvec;
   if (work < head + N) work = head + N;
-  if (mx_nt_for(3 * n * sizeof(T)))
-    hipLaunchKernelGGL((k_reduce3<T, OP, true>), dim3(grid_for(work, kBlockNT)), dim3(kBlockNT), 0, s, a1, a2, o, n,
-                       head, nvec);
-  else
+  if (mx_nt_for(3 * n * sizeof(T))) {
+    if (nt_small_wg(work))
+      hipLaunchKernelGGL((k_reduce3<T, OP, true>), dim3(grid_for(work, kBlockNT)), dim3(kBlockNT), 0, s, a1, a2, o, n,
+                         head, nvec);
+    else
+      hipLaunchKernelGGL((k_reduce3<T, OP, true, kBlock>), dim3(grid_for(work)), dim3(kBlock), 0, s, a1, a2, o, n,
+                         head, nvec);
+  } else {
     hipLaunchKernelGGL((k_reduce3<T, OP, false>), dim3(grid_for(work)), dim3(kBlock), 0, s, a1, a2, o, n, head, nvec);
+  }
   return mx_check_launch();
 }
 
