@@ -89,10 +89,13 @@ def cpu_baseline_reduce_local(seconds=10.0):
 
 def cpu_baseline_allreduce(ranks=8, nbytes=256 << 20, iters=10):
     """The host MPI_Allreduce the reference runs with coll/tuned + vader,
-    restated as `ranks` pinned processes over shared memory (ring,
-    single-copy; oracle/cpu_coll_proxy.c, BASELINE.md 2 "Fallback": no Open
-    MPI on the box), fp32 SUM through a plain C loop of the reference's
-    OP_FUNC shape (kind "port": the reference's loop cannot be built here)."""
+    restated as `ranks` pinned processes over shared memory (single-copy;
+    oracle/cpu_coll_proxy.c, BASELINE.md 2 "Fallback": no Open MPI on the
+    box): coll/tuned's fixed decision (the 1 MiB segmented ring at 256 MiB)
+    as `value`, the ring and Rabenseifner (coll_tuned_allreduce_algorithm
+    4 / 6) beside it; fp32 SUM through a plain C loop of the
+    reference's OP_FUNC shape (kind "port": the reference's loop cannot be
+    built here)."""
     import subprocess
     exe = os.path.join(ROOT, "oracle", "build", "cpu_coll_proxy")
     if not os.path.exists(exe):

@@ -4,22 +4,30 @@
  * coll/tuned + the vader (sm) BTL, restated as N forked processes over one
  * shared-memory segment, because no Open MPI install exists on the GPU box.
  *
- * Algorithm: ompi_coll_base_allreduce_intra_ring (coll_base_allreduce.c:
- * 341-536): rbuf = sbuf (copy_content_same_ddt, :408); reduce-scatter in
- * n-1 steps, step k receiving block (r-k) mod n from the left neighbour and
- * computing rbuf[b] = inbuf OP rbuf[b] (:470-477, :488-496); allgather in
- * n-1 steps, step k receiving block (r-k) mod n (:500-530).  Blocks follow
- * COLL_BASE_COMPUTE_BLOCKCOUNT (coll_base_functions.h:428-435).  Transport
- * is modelled as vader's single-copy path (CMA): the receiver copies the
- * block straight out of the sender's buffer; one process-shared barrier per
- * step stands in for the send/recv completion.  (Tuned selects the 1 MiB
- * segmented ring at 256 MiB; it moves the same bytes in smaller messages.)
+ * Algorithms (coll/tuned's ids, coll_tuned_allreduce_decision.c:37-46):
+ *  4 ring, ompi_coll_base_allreduce_intra_ring (coll_base_allreduce.c:
+ *    341-536): rbuf = sbuf (copy_content_same_ddt, :408); reduce-scatter in
+ *    n-1 steps, step k receiving block (r-k) mod n from the left neighbour
+ *    and computing rbuf[b] = inbuf OP rbuf[b] (:470-477, :488-496);
+ *    allgather in n-1 steps, step k receiving block (r-k) mod n (:500-530);
+ *  5 segmented ring (:618-856), what the fixed decision picks for
+ *    commutative ops above n x 1 MiB (coll_tuned_decision_fixed.c:72-82):
+ *    the reduce-scatter runs num_phases times (phase rule :663-667), each
+ *    time on one segment of every block, then one allgather of the blocks;
+ *  6 Rabenseifner (:970-1243), power-of-two rank counts: recursive-halving
+ *    reduce-scatter, recursive-doubling allgather.
+ * Blocks follow COLL_BASE_COMPUTE_BLOCKCOUNT (coll_base_functions.h:
+ * 428-435).  Transport is modelled as vader's single-copy path (CMA): the
+ * receiver copies the part straight out of the sender's buffer; one
+ * process-shared barrier per step stands in for the send/recv completion.
+ * Every algorithm is timed; "value" is the fixed decision's.
  * The local reduction is a plain C loop of the OP_FUNC shape
  * (op_base_functions.c:40-51) ("port"); an optional shared library
  * exporting the reference's table may be named instead (not built here).
  *
  * usage: cpu_coll_proxy RANKS BYTES ITERS [lib exporting ompi_op_base_functions]
- * prints one JSON object: busBW GB/s = S/t * 2(n-1)/n, t = median.
+ * prints one JSON object: busBW GB/s = S/t * 2(n-1)/n, t = median, for the
+ * fixed decision's algorithm, and every algorithm's busBW beside it.
  */
 #define _GNU_SOURCE
 #include <dlfcn.h>
@@ -61,7 +69,7 @@ static double now(void)
 
 struct shared {
     pthread_barrier_t bar;
-    double times[64];
+    double times[8];          /* per algorithm id */
     int mismatch;
 };
 
@@ -76,6 +84,63 @@ static int cmp_double(const void *a, const void *b)
 {
     double x = *(const double *)a, y = *(const double *)b;
     return x < y ? -1 : x > y;
+}
+
+/* ring reduce-scatter over `nph` phases (1: the plain ring; the segmented
+ * ring's phase p covers segment p of every block, COLL_BASE_COMPUTE_BLOCKCOUNT
+ * of the block over the phases), then the ring allgather of whole blocks */
+static void ring(struct shared *sh, int r, int n, size_t count, float *rbuf, float *inbuf, const float *lrbuf,
+                 int nph)
+{
+    for (int ph = 0; ph < nph; ph++) {
+        for (int k = 1; k < n; k++) {
+            const int b = (r - k + 2 * n) % n;
+            size_t bo, bl, po, pl;
+            blockcount(count, n, b, &bo, &bl);
+            blockcount(bl, nph, ph, &po, &pl);
+            pthread_barrier_wait(&sh->bar);
+            memcpy(inbuf, lrbuf + bo + po, pl * 4);
+            reduce_sum_float(inbuf, rbuf + bo + po, pl);
+        }
+    }
+    for (int k = 0; k < n - 1; k++) {
+        const int b = (r - k + 2 * n) % n;
+        size_t bo, bl;
+        blockcount(count, n, b, &bo, &bl);
+        pthread_barrier_wait(&sh->bar);
+        memcpy(rbuf + bo, lrbuf + bo, bl * 4);
+    }
+}
+
+/* recursive halving reduce-scatter + recursive doubling allgather (power-of-
+ * two n): at distance d the rank keeps the half of its current range on its
+ * side of the partner r ^ d and folds the partner's copy of that half in */
+static void rabenseifner(struct shared *sh, char *mem, size_t per_rank, int r, int n, size_t count, float *rbuf,
+                         float *inbuf)
+{
+    size_t lo = 0, hi = count;
+    size_t los[32], his[32];
+    int steps = 0;
+    for (int d = n / 2; d >= 1; d /= 2) {
+        const int p = r ^ d;
+        const float *prbuf = (const float *)(mem + per_rank * p) + count;
+        const size_t mid = lo + (hi - lo + 1) / 2;
+        los[steps] = lo; his[steps] = hi; steps++;
+        if (r < p) hi = mid; else lo = mid;                  /* the half kept */
+        pthread_barrier_wait(&sh->bar);
+        memcpy(inbuf, prbuf + lo, (hi - lo) * 4);
+        reduce_sum_float(inbuf, rbuf + lo, hi - lo);
+    }
+    for (int d = 1; d < n; d *= 2) {
+        const int p = r ^ d;
+        const float *prbuf = (const float *)(mem + per_rank * p) + count;
+        steps--;
+        const size_t plo = los[steps], phi = his[steps];     /* the range both held before the split */
+        pthread_barrier_wait(&sh->bar);
+        if (lo > plo) memcpy(rbuf + plo, prbuf + plo, (lo - plo) * 4);
+        if (phi > hi) memcpy(rbuf + hi, prbuf + hi, (phi - hi) * 4);
+        lo = plo; hi = phi;
+    }
 }
 
 int main(int argc, char **argv)
@@ -100,9 +165,25 @@ int main(int argc, char **argv)
     }
     if (n < 2 || n > 64 || iters < 1) return 2;
     const size_t count = bytes / 4;
+    /* the fixed decision (coll_tuned_decision_fixed.c:64-85) and the phase
+     * count of the segmented ring (coll_base_allreduce.c:652-667, 1 MiB) */
+    const size_t segcount = (1u << 20) / 4;
+    int decided = bytes < 10000 ? 3 : ((size_t)n * (1u << 20) >= bytes ? 4 : 5);
+    int phases = (int)(count / ((size_t)n * segcount));
+    if (count % ((size_t)n * segcount) >= (size_t)n && count % ((size_t)n * segcount) > ((size_t)n * segcount) / 2)
+        phases++;
+    if (phases < 1) { phases = 1; if (decided == 5) decided = 4; }
+    int algs[3], nalg = 0;
+    algs[nalg++] = 4;
+    algs[nalg++] = 5;
+    if ((n & (n - 1)) == 0) algs[nalg++] = 6;
+    if (decided == 3) decided = 4;   /* recursive doubling below 10 kB: not a bandwidth case; ring stands in */
     size_t off, maxblk;
     blockcount(count, n, 0, &off, &maxblk);
-    const size_t per_rank = 2 * count * 4 + maxblk * 4 + 4096;
+    /* the receive buffer holds one ring block, or the first half a
+     * Rabenseifner exchange moves */
+    const size_t inmax = maxblk > count / 2 + 1 ? maxblk : count / 2 + 1;
+    const size_t per_rank = 2 * count * 4 + inmax * 4 + 4096;
     struct shared *sh = mmap(NULL, sizeof *sh, PROT_READ | PROT_WRITE, MAP_SHARED | MAP_ANONYMOUS, -1, 0);
     char *mem = mmap(NULL, per_rank * n, PROT_READ | PROT_WRITE, MAP_SHARED | MAP_ANONYMOUS | MAP_NORESERVE, -1, 0);
     if (sh == MAP_FAILED || mem == MAP_FAILED) { perror("mmap"); return 1; }
@@ -137,33 +218,24 @@ int main(int argc, char **argv)
         const int left = (r + n - 1) % n;
         const float *lrbuf = (const float *)(mem + per_rank * left) + count;
         double *ts = malloc(sizeof(double) * (iters + 2));
-        for (int it = 0; it < iters + 2; it++) {   /* 2 warmup iterations */
-            pthread_barrier_wait(&sh->bar);
-            const double t0 = now();
-            memcpy(rbuf, sbuf, count * 4);
-            for (int k = 1; k < n; k++) {          /* reduce-scatter */
-                const int b = (r - k + 2 * n) % n;
-                size_t bo, bl;
-                blockcount(count, n, b, &bo, &bl);
+        for (int ai = 0; ai < nalg; ai++) {
+            const int alg = algs[ai];
+            for (int it = 0; it < iters + 2; it++) {   /* 2 warmup iterations */
                 pthread_barrier_wait(&sh->bar);
-                memcpy(inbuf, lrbuf + bo, bl * 4);
-                reduce_sum_float(inbuf, rbuf + bo, bl);
+                const double t0 = now();
+                memcpy(rbuf, sbuf, count * 4);
+                if (alg == 6) rabenseifner(sh, mem, per_rank, r, n, count, rbuf, inbuf);
+                else ring(sh, r, n, count, rbuf, inbuf, lrbuf, alg == 5 ? phases : 1);
+                pthread_barrier_wait(&sh->bar);
+                ts[it] = now() - t0;
             }
-            for (int k = 0; k < n - 1; k++) {      /* allgather */
-                const int b = (r - k + 2 * n) % n;
-                size_t bo, bl;
-                blockcount(count, n, b, &bo, &bl);
-                pthread_barrier_wait(&sh->bar);
-                memcpy(rbuf + bo, lrbuf + bo, bl * 4);
+            /* all ranks hold the same vector (each element is reduced by one rank and then copied) */
+            if (r > 0 && memcmp(rbuf, (const float *)mem + count, count * 4) != 0) sh->mismatch = 1;
+            if (r == 0) {
+                qsort(ts + 2, iters, sizeof(double), cmp_double);
+                sh->times[alg] = ts[2 + iters / 2];
             }
             pthread_barrier_wait(&sh->bar);
-            ts[it] = now() - t0;
-        }
-        /* all ranks hold the same vector */
-        if (r > 0 && memcmp(rbuf, (const float *)mem + count, count * 4) != 0) sh->mismatch = 1;
-        if (r == 0) {
-            qsort(ts + 2, iters, sizeof(double), cmp_double);
-            sh->times[0] = ts[2 + iters / 2];
         }
         _exit(0);
     }
@@ -174,12 +246,18 @@ int main(int argc, char **argv)
         if (!WIFEXITED(st) || WEXITSTATUS(st)) bad = 1;
     }
     if (bad || sh->mismatch) { fprintf(stderr, "cpu_coll_proxy: rank failure or mismatch\n"); return 1; }
-    const double t = sh->times[0];
+    static const char *names[8] = {"", "", "", "", "ring", "segmented_ring", "rabenseifner", ""};
+    const double t = sh->times[decided];
     const double algbw = (double)count * 4 / t / 1e9;
     printf("{\"value\": %.3f, \"unit\": \"GB/s\", \"cores\": %d, \"kind\": \"%s\", "
-           "\"algbw_gbs\": %.3f, \"ms_per_call\": %.3f, \"sample\": \"MPI_Allreduce fp32 SUM %zu B, %d ranks "
-           "(processes pinned one per core), ring (coll_base_allreduce.c:341-536) over shared memory with "
-           "single-copy transfers, median of %d calls; busBW = S/t*2(n-1)/n\"}\n",
-           algbw * 2.0 * (n - 1) / n, n, kind, algbw, t * 1e3, count * 4, n, iters);
+           "\"algorithm\": \"%s\", \"algbw_gbs\": %.3f, \"ms_per_call\": %.3f, \"algorithms_busbw_gbs\": {",
+           algbw * 2.0 * (n - 1) / n, n, kind, names[decided], algbw, t * 1e3);
+    for (int ai = 0; ai < nalg; ai++)
+        printf("%s\"%s\": %.3f", ai ? ", " : "", names[algs[ai]],
+               (double)count * 4 / sh->times[algs[ai]] / 1e9 * 2.0 * (n - 1) / n);
+    printf("}, \"sample\": \"MPI_Allreduce fp32 SUM %zu B, %d ranks (processes pinned one per core), coll/tuned's "
+           "fixed decision (%s, %d phases of 1 MiB segments) over shared memory with single-copy transfers, "
+           "median of %d calls; busBW = S/t*2(n-1)/n\"}\n",
+           count * 4, n, names[decided], decided == 5 ? phases : 1, iters);
     return 0;
 }
