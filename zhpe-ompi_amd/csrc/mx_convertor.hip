@@ -128,6 +128,28 @@ template <> struct unit_t<4> { using T = uint32_t; };
 template <> struct unit_t<2> { using T = uint16_t; };
 template <> struct unit_t<1> { using T = uint8_t; };
 
+// 16 bytes at dword alignment: one dwordx4 access where the user address
+// is only 4-byte aligned (the compiler picks the instruction for align 4)
+struct __attribute__((aligned(4))) W4 { uint32_t x, y, z, w; };
+
+// loads through an explicitly global pointer: global_load (vmcnt only), not
+// flat_load, whose lgkmcnt would tie a load in flight to every LDS wait
+typedef uint32_t v4u_a16 __attribute__((ext_vector_type(4), aligned(16)));
+typedef uint32_t v4u_a4 __attribute__((ext_vector_type(4), aligned(4)));
+__device__ __forceinline__ uint4 gld16(const char *p) {        // 16-byte aligned
+  const v4u_a16 v = *(const __attribute__((address_space(1))) v4u_a16 *)(p);
+  return make_uint4(v.x, v.y, v.z, v.w);
+}
+__device__ __forceinline__ W4 gld16a4(const char *p) {         // 4-byte aligned
+  const v4u_a4 v = *(const __attribute__((address_space(1))) v4u_a4 *)(p);
+  W4 w;
+  w.x = v.x; w.y = v.y; w.z = v.z; w.w = v.w;
+  return w;
+}
+__device__ __forceinline__ uint32_t gld4(const char *p) {
+  return *(const __attribute__((address_space(1))) uint32_t *)(p);
+}
+
 // ---------------------------------------------------------------------------
 // GRANULE kernel: one lane = one 16-byte granule of the packed buffer
 // (granule g = stream bytes [offset + 16g, +16)), staged in 16/UNIT
@@ -577,40 +599,45 @@ struct BmapArgs {
   int64_t adv_io;
 };
 
-// M = uint16_t when the instance's user span is below 64 KiB, else uint32_t
-template <int SPAN, class M, bool DW>
+// M = uint16_t when the instance's user span is below 64 KiB, else uint32_t.
+// PIPE (round 3): persistent workgroups keep the NEXT tile's user span in
+// flight in registers (SPAN / 16 / kCB uint4 per lane) while the lanes
+// gather the current tile out of LDS -- without it every tile's span load
+// and gather run back to back inside the workgroup.
+template <int SPAN, class M, bool DW, bool PIPE>
 __global__ void __launch_bounds__(kCB) k_pack_bmap(BmapArgs a) {
   extern __shared__ __align__(16) char smem[];
   char *span = smem;                                         // SPAN + 32
   M *bmap = reinterpret_cast<M *>(smem + SPAN + 32);
-  __shared__ uintptr_t s_lo, s_hi;
+  __shared__ uintptr_t s_lo[2], s_hi[2];
+  constexpr int kPre = SPAN / 16 / kCB;
   for (uint32_t i = threadIdx.x; i < a.S; i += kCB) bmap[i] = reinterpret_cast<const M *>(a.map)[i];
   const uint64_t wend = a.offset + a.len;
-  for (uint64_t t = blockIdx.x; t < a.ntiles; t += gridDim.x) {
-    const uint64_t s0 = a.g0 * 16 + t * a.T;                 // absolute stream bytes [s0, s1)
-    const uint64_t sa = s0 < a.offset ? a.offset : s0;
-    const uint64_t s1 = s0 + a.T < wend ? s0 + a.T : wend;
-    const uint64_t ia = udiv(sa, a.mS), ib = udiv(s1 - 1, a.mS);
+  // tile t: absolute stream bytes [s0, s1) (window-clipped from sa), instances ia..ib
+  auto geom = [&](uint64_t t, uint64_t &s0, uint64_t &sa, uint64_t &s1, uint64_t &ia, uint64_t &ib) {
+    s0 = a.g0 * 16 + t * a.T;
+    sa = s0 < a.offset ? a.offset : s0;
+    s1 = s0 + a.T < wend ? s0 + a.T : wend;
+    ia = udiv(sa, a.mS);
+    ib = udiv(s1 - 1, a.mS);
+  };
+  // one thread: the 16-aligned user span [lo, hi) tile t reads (bmap staged)
+  auto bounds = [&](uint64_t t, int slot) {
+    uint64_t s0, sa, s1, ia, ib;
+    geom(t, s0, sa, s1, ia, ib);
+    const uintptr_t ubase = (uintptr_t)a.user + (int64_t)ia * a.ext + a.umin;
+    uintptr_t lo = ubase, hi = ubase + (int64_t)(ib - ia) * a.ext + a.uspan;
+    if (a.mono) {
+      lo = ubase + bmap[sa - ia * a.S];
+      hi = ubase + (int64_t)(ib - ia) * a.ext + bmap[s1 - 1 - ib * a.S] + 1;
+    }
+    s_lo[slot] = lo & ~(uintptr_t)15;
+    s_hi[slot] = (hi + 15) & ~(uintptr_t)15;
+  };
+  auto gather = [&](uint64_t t, uintptr_t lo) {
+    uint64_t s0, sa, s1, ia, ib;
+    geom(t, s0, sa, s1, ia, ib);
     const uintptr_t ubase = (uintptr_t)a.user + (int64_t)ia * a.ext + a.umin;   // instance ia, + umin
-    __syncthreads();                                          // map staged; previous tile done with span
-    if (threadIdx.x == 0) {
-      uintptr_t lo = ubase, hi = ubase + (int64_t)(ib - ia) * a.ext + a.uspan;
-      if (a.mono) {
-        lo = ubase + bmap[sa - ia * a.S];
-        hi = ubase + (int64_t)(ib - ia) * a.ext + bmap[s1 - 1 - ib * a.S] + 1;
-      }
-      s_lo = lo & ~(uintptr_t)15;
-      s_hi = (hi + 15) & ~(uintptr_t)15;
-    }
-    __syncthreads();
-    const uintptr_t lo = s_lo;
-    {
-      const uint4 *g = reinterpret_cast<const uint4 *>(lo);
-      uint4 *d = reinterpret_cast<uint4 *>(span);
-      const uint32_t nv = (uint32_t)((s_hi - lo) / 16);
-      for (uint32_t i = threadIdx.x; i < nv; i += kCB) d[i] = g[i];
-    }
-    __syncthreads();
     const int64_t d0 = (int64_t)(ubase - lo);
     if (DW) {
       // lane = one packed dword per step, consecutive lanes consecutive
@@ -643,7 +670,7 @@ __global__ void __launch_bounds__(kCB) k_pack_bmap(BmapArgs a) {
         io += a.adv_io;
         if (b >= a.S) { b -= a.S; io += a.ext; }
       }
-      continue;
+      return;
     }
     for (uint64_t g = s0 / 16 + threadIdx.x; g * 16 < s1; g += kCB) {
       const uint64_t p = g * 16;
@@ -670,6 +697,59 @@ __global__ void __launch_bounds__(kCB) k_pack_bmap(BmapArgs a) {
       }
       *reinterpret_cast<uint4 *>(a.packed + (p - a.offset)) = make_uint4(w[0], w[1], w[2], w[3]);
     }
+  };
+  if (!PIPE) {
+    for (uint64_t t = blockIdx.x; t < a.ntiles; t += gridDim.x) {
+      __syncthreads();                                        // map staged; previous tile done with span
+      if (threadIdx.x == 0) bounds(t, 0);
+      __syncthreads();
+      {
+        const char *g = reinterpret_cast<const char *>(s_lo[0]);
+        uint4 *d = reinterpret_cast<uint4 *>(span);
+        const uint32_t nv = (uint32_t)((s_hi[0] - s_lo[0]) / 16);
+        for (uint32_t i = threadIdx.x; i < nv; i += kCB) d[i] = gld16(g + 16 * (size_t)i);
+      }
+      __syncthreads();
+      gather(t, s_lo[0]);
+    }
+    return;
+  }
+  uint64_t t = blockIdx.x;
+  if (t >= a.ntiles) return;
+  __syncthreads();                                            // map staged
+  if (threadIdx.x == 0) bounds(t, 0);
+  __syncthreads();
+  {
+    const char *g = reinterpret_cast<const char *>(s_lo[0]);
+    uint4 *d = reinterpret_cast<uint4 *>(span);
+    const uint32_t nv = (uint32_t)((s_hi[0] - s_lo[0]) / 16);
+    for (uint32_t i = threadIdx.x; i < nv; i += kCB) d[i] = gld16(g + 16 * (size_t)i);
+  }
+  int cur = 0;
+  for (;;) {
+    const uint64_t tn = t + gridDim.x;
+    const bool has_next = tn < a.ntiles;
+    if (has_next && threadIdx.x == 0) bounds(tn, cur ^ 1);
+    __syncthreads();                                          // span of t in LDS; bounds of tn visible
+    uint4 pre[kPre];
+    const uint32_t nvn = has_next ? (uint32_t)((s_hi[cur ^ 1] - s_lo[cur ^ 1]) / 16) : 0;
+    {
+      const char *g = reinterpret_cast<const char *>(s_lo[cur ^ 1]);
+#pragma unroll
+      for (int k = 0; k < kPre; k++)
+        if (threadIdx.x + k * kCB < nvn) pre[k] = gld16(g + 16 * (size_t)(threadIdx.x + k * kCB));
+    }
+    gather(t, s_lo[cur]);
+    if (!has_next) break;
+    __syncthreads();                                          // tile t's span is free
+    {
+      uint4 *d = reinterpret_cast<uint4 *>(span);
+#pragma unroll
+      for (int k = 0; k < kPre; k++)
+        if (threadIdx.x + k * kCB < nvn) d[threadIdx.x + k * kCB] = pre[k];
+    }
+    t = tn;
+    cur ^= 1;
   }
 }
 
@@ -1063,10 +1143,6 @@ __device__ __forceinline__ void blk_map(const BlkArgs &a, uint32_t n, uint64_t u
 constexpr uint32_t kBlkMaxT = 65536;       // largest tile (packed-memory bytes)
 constexpr uint32_t kBlkMaxMap = kBlkMaxT / 64;
 
-// 16 bytes at dword alignment: one dwordx4 access where the user address
-// is only 4-byte aligned (the compiler picks the instruction for align 4)
-struct __attribute__((aligned(4))) W4 { uint32_t x, y, z, w; };
-
 // Lane l owns the 16-byte packed-memory granules l, l + kCB, ... of the
 // tile, kBlkNG at a time: first every granule's block search and user
 // address, then every granule's loads (unconditional: a granule with
@@ -1082,24 +1158,6 @@ struct __attribute__((aligned(4))) W4 { uint32_t x, y, z, w; };
 // UNPACK stores each part in aligned pieces; PACK loads the (at most 5)
 // dwords under each part, funnel-shifts them into place and ORs them in.
 __device__ uint32_t g_blk_dummy[8];
-
-// loads through an explicitly global pointer: global_load (vmcnt only), not
-// flat_load, whose lgkmcnt would tie the batch to the LDS searches
-typedef uint32_t v4u_a16 __attribute__((ext_vector_type(4), aligned(16)));
-typedef uint32_t v4u_a4 __attribute__((ext_vector_type(4), aligned(4)));
-__device__ __forceinline__ uint4 gld16(const char *p) {        // 16-byte aligned
-  const v4u_a16 v = *(const __attribute__((address_space(1))) v4u_a16 *)(p);
-  return make_uint4(v.x, v.y, v.z, v.w);
-}
-__device__ __forceinline__ W4 gld16a4(const char *p) {         // 4-byte aligned
-  const v4u_a4 v = *(const __attribute__((address_space(1))) v4u_a4 *)(p);
-  W4 w;
-  w.x = v.x; w.y = v.y; w.z = v.z; w.w = v.w;
-  return w;
-}
-__device__ __forceinline__ uint32_t gld4(const char *p) {
-  return *(const __attribute__((address_space(1))) uint32_t *)(p);
-}
 
 template <bool PACK, int kBlkNG>
 __global__ void __launch_bounds__(kCB) k_convert_blk(BlkArgs a) {
@@ -2050,6 +2108,16 @@ static int conv_blk_mode() {
   return m;
 }
 
+// MX_CONV_BMAP_PIPE=0 runs the byte-map PACK kernel without the span
+// prefetch of the next tile (A/B switch; results are identical).
+static bool conv_bmap_pipe() {
+  static const int on = [] {
+    const char *e = getenv("MX_CONV_BMAP_PIPE");
+    return (e && *e == '0') ? 0 : 1;
+  }();
+  return on != 0;
+}
+
 static int conv_pipe_geom() {
   static const int g = [] {
     const char *e = getenv("MX_CONV_PIPE_GEOM");
@@ -2198,8 +2266,13 @@ static int convert(const mx_ddt_t *d, size_t count, char *user, char *packed, si
       b.adv_io = (int64_t)((kCB * 4) / d->size) * b.ext;
       const bool dw = conv_bmap_dw();
       dm->last_path.store(4, std::memory_order_relaxed);
-#define MX_BMAP_LAUNCH(M, DW) \
-  hipLaunchKernelGGL((k_pack_bmap<kBmapSpan, M, DW>), dim3((unsigned)grid), dim3(kCB), lds, s, b)
+#define MX_BMAP_LAUNCH(M, DW)                                                                                   \
+  do {                                                                                                           \
+    if (conv_bmap_pipe())                                                                                        \
+      hipLaunchKernelGGL((k_pack_bmap<kBmapSpan, M, DW, true>), dim3((unsigned)grid), dim3(kCB), lds, s, b);     \
+    else                                                                                                         \
+      hipLaunchKernelGGL((k_pack_bmap<kBmapSpan, M, DW, false>), dim3((unsigned)grid), dim3(kCB), lds, s, b);    \
+  } while (0)
       if (d->map16) { if (dw) MX_BMAP_LAUNCH(uint16_t, true); else MX_BMAP_LAUNCH(uint16_t, false); }
       else { if (dw) MX_BMAP_LAUNCH(uint32_t, true); else MX_BMAP_LAUNCH(uint32_t, false); }
 #undef MX_BMAP_LAUNCH
