@@ -18,6 +18,7 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include <stddef.h>
+#include <stdlib.h>
 
 #include "mx_dispatch.hpp"
 #include "mx_internal.h"
@@ -78,6 +79,38 @@ k_reduce2(const T *__restrict__ a, T *__restrict__ b, size_t n, size_t head, siz
   if (tid < n - tail0) red2_elem<T, OP>(a, b, tail0 + tid);
 }
 
+// 2-buffer, 32-byte elements (complex long double, long double + int):
+// one element per lane moved as two raw 16-byte vectors, the result's value
+// fields merged into the destination's own bytes (store_fields on the
+// loaded copy), so its padding travels back unchanged and every 128-byte
+// line is written whole -- field-by-field stores leave 12 of every 32
+// bytes unwritten, which costs a partial-line write-back per line
+// (tools/sector_probe.hip).  Both buffers 16-byte aligned.
+template <class T, class OP, bool NT, int BS>
+__global__ void __launch_bounds__(BS) k_reduce2_w32(const T *__restrict__ a, T *__restrict__ b, size_t n) {
+  static_assert(sizeof(T) == 32, "32-byte elements");
+  const size_t i = (size_t)blockIdx.x * BS + threadIdx.x;
+  if (i >= n) return;
+  const u32x4 *pa = reinterpret_cast<const u32x4 *>(a + i);
+  u32x4 *pb = reinterpret_cast<u32x4 *>(b + i);
+  u32x4 ra[2], rb[2];
+#pragma unroll
+  for (int k = 0; k < 2; k++) {
+    if constexpr (NT) { ra[k] = __builtin_nontemporal_load(pa + k); rb[k] = __builtin_nontemporal_load(pb + k); }
+    else { ra[k] = pa[k]; rb[k] = pb[k]; }
+  }
+  T x, y;
+  __builtin_memcpy(&x, rb, 32);
+  __builtin_memcpy(&y, ra, 32);
+  store_fields(&x, OP()(x, y));
+  __builtin_memcpy(rb, &x, 32);
+#pragma unroll
+  for (int k = 0; k < 2; k++) {
+    if constexpr (NT) __builtin_nontemporal_store(rb[k], pb + k);
+    else pb[k] = rb[k];
+  }
+}
+
 // 2-buffer, one element per lane (mismatched alignment, or element > 16 B).
 template <class T, class OP>
 __global__ void __launch_bounds__(kBlock)
@@ -132,6 +165,16 @@ static constexpr size_t kMaxItems = ((size_t)1 << 31) * kBlock - kBlock;
 // one-wave workgroups while the grid fits 2^31 - 1 of them (vectors up to 2^37: 2 TiB)
 static inline bool nt_small_wg(size_t work) { return work < ((size_t)1 << 31) * kBlockNT - kBlockNT; }
 
+// MX_REDUCE_W32=0 keeps 32-byte elements on the field-by-field element
+// kernel (A/B switch; results are identical)
+static bool conv_w32() {
+  static const int on = [] {
+    const char *e = getenv("MX_REDUCE_W32");
+    return (e && *e == '0') ? 0 : 1;
+  }();
+  return on != 0;
+}
+
 template <class T, class OP>
 static int launch2(const void *in, void *inout, size_t n, hipStream_t s) {
   const T *a = static_cast<const T *>(in);
@@ -139,6 +182,16 @@ static int launch2(const void *in, void *inout, size_t n, hipStream_t s) {
   if (n == 0) return MX_SUCCESS;
   constexpr size_t N = (sizeof(T) <= 16 && 16 % sizeof(T) == 0) ? 16 / sizeof(T) : 0;
   const uintptr_t ma = (uintptr_t)a & 15, mb = (uintptr_t)b & 15;
+  if constexpr (sizeof(T) == 32) {
+    if (ma == 0 && mb == 0 && conv_w32()) {
+      if (mx_nt_for(2 * n * sizeof(T)) && nt_small_wg(n))
+        hipLaunchKernelGGL((k_reduce2_w32<T, OP, true, kBlockNT>), dim3(grid_for(n, kBlockNT)), dim3(kBlockNT), 0, s,
+                           a, b, n);
+      else
+        hipLaunchKernelGGL((k_reduce2_w32<T, OP, false, kBlock>), dim3(grid_for(n)), dim3(kBlock), 0, s, a, b, n);
+      return mx_check_launch();
+    }
+  }
   if (N == 0 || ma != mb || (ma % sizeof(T)) != 0) {
     hipLaunchKernelGGL((k_reduce2_elem<T, OP>), dim3(grid_for(n)), dim3(kBlock), 0, s, a, b, n);
     return mx_check_launch();
