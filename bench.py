@@ -113,9 +113,15 @@ def cpu_baseline_allreduce(ranks=8, nbytes=256 << 20, iters=10):
 def bench_reduce_local(torch, mx, steps, warmup, nbytes=1 << 30):
     n = nbytes // 4
     g = torch.Generator(device="cuda").manual_seed(0x5EEDC0DE)
-    a = torch.rand(n, device="cuda", generator=g) * 2 - 1
-    b0 = torch.rand(n, device="cuda", generator=g) * 2 - 1
-    b = b0.clone()
+    # the three 1 GiB buffers are allocated first, as whole fresh segments,
+    # and filled in place: temporaries of an out-of-place fill (rand * 2 - 1)
+    # would leave the timed buffers in recycled, fragmented allocator blocks
+    a = torch.empty(n, device="cuda")
+    b0 = torch.empty(n, device="cuda")
+    b = torch.empty(n, device="cuda")
+    a.uniform_(-1, 1, generator=g)
+    b0.uniform_(-1, 1, generator=g)
+    b.copy_(b0)
     stream = torch.cuda.current_stream()
     sp = stream.cuda_stream
     for _ in range(warmup):
