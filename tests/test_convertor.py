@@ -164,10 +164,13 @@ def test_device_pack_large_cfg_c(name, shift):
 
 
 # ---- BLOCK kernels (k_convert_blk): large instances, and every golden type forced --------
-def _check_device_vs_oracle(d, dt, count, shift=0, pshift=0, chunks=(None,), rng_seed=11, expect_path="block"):
+def _check_device_vs_oracle(d, dt, count, shift=0, pshift=0, chunks=(None,), rng_seed=11, expect_path="block",
+                            expect_unpack="same"):
     """pack whole / in fragments and unpack into a prefilled buffer, each vs the
     oracle restatement; user buffer displaced by `shift` bytes, packed buffer
-    by `pshift` bytes; asserts the kernel family that ran."""
+    by `pshift` bytes; asserts the kernel family that ran (None: any)."""
+    if expect_unpack == "same":
+        expect_unpack = expect_path
     O = _oracle()
     bs = np.ascontiguousarray(BASIC)
     ext = d.ub - d.lb
@@ -192,7 +195,7 @@ def _check_device_vs_oracle(d, dt, count, shift=0, pshift=0, chunks=(None,), rng
             dt.pack(count, ubase, P.data_ptr() + pshift + off, offset=off, length=ln, stream=st)
             off += ln
         torch.cuda.synchronize()
-        assert dt.last_path == expect_path
+        assert expect_path is None or dt.last_path == expect_path
         got = P.cpu().numpy()
         np.testing.assert_array_equal(got[pshift:pshift + total], exp, err_msg=f"pack chunk {chunk}")
         assert not got[:pshift].any() and not got[pshift + total:].any(), "pack wrote outside its window"
@@ -212,7 +215,7 @@ def _check_device_vs_oracle(d, dt, count, shift=0, pshift=0, chunks=(None,), rng
             dt.unpack(count, dbase, Pk.data_ptr() + pshift + off, offset=off, length=ln, stream=st)
             off += ln
         torch.cuda.synchronize()
-        assert dt.last_path == expect_path
+        assert expect_unpack is None or dt.last_path == expect_unpack
         got = D.cpu().numpy()
         np.testing.assert_array_equal(got[shift:shift + span], exp_u, err_msg=f"unpack chunk {chunk}")
         assert not got[:shift].any() and not got[shift + span:].any(), "unpack wrote outside the span"
@@ -290,6 +293,31 @@ def test_block_kernels_byte_blocks(shuffle):
     d = _random_indexed(120000, 9, t=4, max_bl=3, max_gap=2, shuffle=shuffle)
     dt = d.dt()
     _check_device_vs_oracle(d, dt, 2, 5, 3, chunks=(None, 7777))
+    dt.close()
+
+
+# ---- periodic small-block PACK (k_pack_vec_span) ------------------------------------------
+@pytest.mark.gpu
+@pytest.mark.parametrize("t,blen,stride", [(15, 1, 8), (16, 1, 16), (15, 1, 16), (15, 2, 16)])
+@pytest.mark.parametrize("layout", ["resized", "plain1", "plain3"])
+@pytest.mark.parametrize("shift,pshift", [(0, 0), (0, 5), (3, 0), (16, 8)])
+def test_vec_span_pack(t, blen, stride, layout, shift, pshift):
+    """A vector of blen-element blocks every `stride` bytes: resized so
+    instances continue the period (the span kernel over every instance), a
+    plain MPI vector packed as one instance, and three plain instances (the
+    span kernel only for fragments inside instance 0).  Aligned user buffers
+    take the span kernel; shifted user / odd packed buffers the run-walking
+    VEC kernel -- both bit-exact vs the oracle, whole and in odd fragments."""
+    mxompi.init(0)
+    es = _ES[t]
+    cnt = 100003
+    ub = cnt * stride if layout == "resized" else (cnt - 1) * stride + blen * es
+    d = _Big([(t, cnt, blen, stride, 0)], cnt * blen * es, 0, ub)
+    dt = d.dt()
+    count = 1 if layout == "plain1" else 3
+    span_ok = shift % 16 == 0 and pshift % 4 == 0 and layout != "plain3"
+    _check_device_vs_oracle(d, dt, count, shift, pshift, chunks=(None, 4099, 65536, 1000003),
+                            expect_path="vector" if span_ok else None, expect_unpack=None)
     dt.close()
 
 

@@ -270,6 +270,57 @@ __global__ void __launch_bounds__(kCB) k_convert_vec(ConvArgs a, DRun R, float r
   }
 }
 
+// PACK of a periodic strided layout with small blocks (round 3): one run of
+// blen-byte blocks every stride bytes, instances continuing the period
+// (extent = cnt1 * stride) or one instance, stride 8 or 16, the first block
+// 16-byte aligned.  Lane q reads user chunk q (16 bytes, one aligned load: a wave
+// streams 1 KiB of span) holding M = 16 / stride whole blocks, and writes
+// their M * blen packed bytes with one store (a wave writes M * blen * 64
+// contiguous bytes).  The run-walking VEC kernel reads the same lines as
+// one 4-byte word per lane at the stride (twice the load instructions for
+// 4-byte blocks every 8 bytes).
+template <int STRIDE, int BLEN>
+__global__ void __launch_bounds__(kCB) k_pack_vec_span(const char *ubase, char *packed, uint64_t offset,
+                                                       uint64_t len, uint64_t q0, uint64_t q1) {
+  constexpr int M = 16 / STRIDE, OUT = M * BLEN;
+  static_assert(16 % STRIDE == 0 && BLEN < STRIDE && (BLEN == 4 || BLEN == 8 || BLEN == 2 || BLEN == 1),
+                "periodic small blocks");
+  const uint64_t q = q0 + (uint64_t)blockIdx.x * kCB + threadIdx.x;
+  if (q >= q1) return;
+  const uint4 v = gld16(ubase + 16 * q);
+  const uint32_t d[4] = {v.x, v.y, v.z, v.w};
+  uint8_t o[OUT];
+#pragma unroll
+  for (int k = 0; k < M; k++)
+#pragma unroll
+    for (int i = 0; i < BLEN; i++) {
+      const int b = k * STRIDE + i;                          // byte of the chunk
+      o[k * BLEN + i] = (uint8_t)(d[b >> 2] >> (8 * (b & 3)));
+    }
+  const uint64_t p = q * OUT;                                // stream offset of the chunk's first packed byte
+  if (p >= offset && p + OUT <= offset + len) {
+    char *dst = packed + (p - offset);
+    if constexpr (OUT == 8) {
+      uint32_t w0 = 0, w1 = 0;
+#pragma unroll
+      for (int i = 0; i < 4; i++) { w0 |= (uint32_t)o[i] << (8 * i); w1 |= (uint32_t)o[4 + i] << (8 * i); }
+      *reinterpret_cast<uint2 *>(dst) = make_uint2(w0, w1);
+    } else if constexpr (OUT == 4) {
+      uint32_t w0 = 0;
+#pragma unroll
+      for (int i = 0; i < 4; i++) w0 |= (uint32_t)o[i] << (8 * i);
+      *reinterpret_cast<uint32_t *>(dst) = w0;
+    } else {
+#pragma unroll
+      for (int i = 0; i < OUT; i++) dst[i] = (char)o[i];
+    }
+  } else {                                                   // window edge: the bytes inside only
+#pragma unroll
+    for (int i = 0; i < OUT; i++)
+      if (p + i >= offset && p + i < offset + len) packed[p + i - offset] = (char)o[i];
+  }
+}
+
 // ---------------------------------------------------------------------------
 // TILE kernels (pieces narrower than 16 bytes): a workgroup owns kTP bytes
 // of the stream.  PACK loads the user span the tile reads (monotonic
@@ -2118,6 +2169,16 @@ static bool conv_bmap_pipe() {
   return on != 0;
 }
 
+// MX_CONV_VEC_SPAN=0 packs periodic small-block vectors through the VEC
+// kernel instead of k_pack_vec_span (A/B switch; results are identical).
+static bool conv_vec_span() {
+  static const int on = [] {
+    const char *e = getenv("MX_CONV_VEC_SPAN");
+    return (e && *e == '0') ? 0 : 1;
+  }();
+  return on != 0;
+}
+
 static int conv_pipe_geom() {
   static const int g = [] {
     const char *e = getenv("MX_CONV_PIPE_GEOM");
@@ -2180,6 +2241,30 @@ static int convert(const mx_ddt_t *d, size_t count, char *user, char *packed, si
   // (16-byte-granular layouts stay on k_convert<16>: measured 3.9 vs 2.8 TB/s
   // for 16-byte blocks at 1 GiB, while 4-byte blocks go 2.1 -> 3.5 TB/s here;
   // profiles/r01/convertor_vec_ab.txt)
+  // periodic small blocks, PACK: whole 16-byte chunks of the span (k_pack_vec_span)
+  if (PACK && a.nruns == 1 && d->host[0].cnt2 == 1 && !d->force_blk && conv_vec_span()) {
+    const DRun &R = d->host[0];
+    // the period: the block stride, or the extent for one block per instance;
+    // instances continue it when extent == cnt1 * period, or the window stays
+    // inside instance 0 (one plain MPI vector)
+    const int64_t st = R.cnt1 > 1 ? R.stride1 : a.ext;
+    const char *ub = user + R.disp;
+    const bool periodic = (st == 8 || st == 16) && (int64_t)R.blen < st &&
+                          (a.ext == (int64_t)R.cnt1 * st || offset + len <= a.S) &&
+                          ((uintptr_t)ub & 15) == 0 && (R.blen == 4 || R.blen == 8) &&
+                          (((uintptr_t)packed - offset) & (16 / st * R.blen - 1)) == 0;
+    if (periodic) {
+      const uint64_t outb = (uint64_t)(16 / st) * R.blen;   // packed bytes per chunk
+      const uint64_t q0 = offset / outb, q1 = (offset + len + outb - 1) / outb;
+      const uint64_t nq = q1 - q0;
+      const dim3 grid((unsigned)((nq + kCB - 1) / kCB)), block(kCB);
+      dm->last_path.store(2, std::memory_order_relaxed);
+      if (st == 8) hipLaunchKernelGGL((k_pack_vec_span<8, 4>), grid, block, 0, s, ub, packed, offset, len, q0, q1);
+      else if (R.blen == 8) hipLaunchKernelGGL((k_pack_vec_span<16, 8>), grid, block, 0, s, ub, packed, offset, len, q0, q1);
+      else hipLaunchKernelGGL((k_pack_vec_span<16, 4>), grid, block, 0, s, ub, packed, offset, len, q0, q1);
+      return mx_check_launch();
+    }
+  }
   if (a.nruns == 1 && d->host[0].cnt2 == 1 && u % 4 == 0 && u != 16 && d->host[0].blen <= kVecMaxBlen &&
       conv_vec_enabled() && !d->force_blk) {
     dm->last_path.store(2, std::memory_order_relaxed);
