@@ -2237,10 +2237,6 @@ static int convert(const mx_ddt_t *d, size_t count, char *user, char *packed, si
   u = gcd64(u, len & 15 ? (len & 15) : 16);
   if (!a.pk_vec) u = gcd64(u, (uintptr_t)packed & 15);
   const size_t run_lds = a.nruns <= kLdsRuns ? (size_t)a.nruns * sizeof(DRun) : 0;
-  // one strided 1-level run of whole aligned 4/8-byte words: the VEC kernel
-  // (16-byte-granular layouts stay on k_convert<16>: measured 3.9 vs 2.8 TB/s
-  // for 16-byte blocks at 1 GiB, while 4-byte blocks go 2.1 -> 3.5 TB/s here;
-  // profiles/r01/convertor_vec_ab.txt)
   // periodic small blocks, PACK: whole 16-byte chunks of the span (k_pack_vec_span)
   if (PACK && a.nruns == 1 && d->host[0].cnt2 == 1 && !d->force_blk && conv_vec_span()) {
     const DRun &R = d->host[0];
@@ -2265,6 +2261,10 @@ static int convert(const mx_ddt_t *d, size_t count, char *user, char *packed, si
       return mx_check_launch();
     }
   }
+  // one strided 1-level run of whole aligned 4/8-byte words: the VEC kernel
+  // (16-byte-granular layouts stay on k_convert<16>: measured 3.9 vs 2.8 TB/s
+  // for 16-byte blocks at 1 GiB, while 4-byte blocks go 2.1 -> 3.5 TB/s here;
+  // profiles/r01/convertor_vec_ab.txt)
   if (a.nruns == 1 && d->host[0].cnt2 == 1 && u % 4 == 0 && u != 16 && d->host[0].blen <= kVecMaxBlen &&
       conv_vec_enabled() && !d->force_blk) {
     dm->last_path.store(2, std::memory_order_relaxed);
