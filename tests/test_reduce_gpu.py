@@ -21,7 +21,10 @@ RECS = golden_io.op_records()
 
 
 def _dev(arr):
-    return torch.from_numpy(np.ascontiguousarray(arr)).to("cuda")
+    a = np.ascontiguousarray(arr)
+    if not a.flags.writeable:          # golden records are read-only views of the fixture file
+        a = a.copy()
+    return torch.from_numpy(a).to("cuda")
 
 
 def _stream():
