@@ -201,6 +201,14 @@ int mx_op_supported(int op, int type, int table_variant);
  * device-accessible.  count is size_t: no INT_MAX limit. */
 int mx_reduce2(int op, int type, const void *in, void *inout,
                size_t count, void *stream);
+/* As mx_reduce2, and returns when the result is complete: the blocking form
+ * the op component's handler needs (ompi_op_reduce, ompi/op/op.h:547-610,
+ * returns with `inout` final).  The reduce kernel's last workgroup raises a
+ * completion word in mapped host memory that the host polls, so no marker
+ * kernel follows it (mx_stream_sync_fast semantics otherwise: after ~2 ms
+ * the wait falls back to hipStreamSynchronize, which also reports faults). */
+int mx_reduce2_sync(int op, int type, const void *in, void *inout,
+                    size_t count, void *stream);
 /* out[i] = in1[i] OP in2[i].  out may alias neither input (restrict, as
  * in the reference's 3-buffer functions). */
 int mx_reduce3(int op, int type, const void *in1, const void *in2,

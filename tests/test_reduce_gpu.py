@@ -217,3 +217,53 @@ def test_count_zero_is_noop():
     mxompi.reduce2("SUM", "FLOAT", B.data_ptr(), B.data_ptr(), 0, _stream())
     torch.cuda.synchronize()
     assert float(B.sum()) == 16.0
+
+
+# ---- mx_reduce2_sync: the kernel's own completion mark ---------------------
+@pytest.mark.parametrize("op,t", CASES + [("PROD", "C_LONG_DOUBLE_COMPLEX"), ("MAXLOC", "LONG_DOUBLE_INT")])
+@pytest.mark.parametrize("offs", [(0, 0), (1, 1), (0, 1)])
+@pytest.mark.parametrize("n", [1, 1000, 16384, 16385, 300001])
+def test_reduce2_sync_complete_on_return(op, t, offs, n):
+    """mx_reduce2_sync on a side stream returns with the result complete:
+    read back on the default stream with no synchronisation against the side
+    stream, bit-exact vs the oracle.  Vector, per-element and 32-byte kernels
+    (aligned / same / different misalignment), launches under and over the
+    fused-mark cap (2^14 elements and 256 KiB: over it a marker kernel
+    follows)."""
+    O = oracle_lib.oracle()
+    es = mxompi.type_size(t)
+    rng = np.random.default_rng(n + 17 * offs[1])
+    nb = es * n
+    raw = [rng.integers(0, 2 if t == "BOOL" else 256, nb + 8 * es + 64, dtype=np.uint8) for _ in range(2)]
+    if "LONG_DOUBLE" in t:
+        for r in raw:
+            v = r[: len(r) // 16 * 16].reshape(-1, 16)
+            v[:] = rng.uniform(-4, 4, len(v)).astype(np.longdouble).view(np.uint8).reshape(-1, 16)
+    A = _dev(raw[0]); B = _dev(raw[1])
+    torch.cuda.synchronize()
+    ea, eb = es * offs[0], es * offs[1]
+    side = torch.cuda.Stream()
+    mxompi.reduce2_sync(op, t, A.data_ptr() + ea, B.data_ptr() + eb, n, side.cuda_stream)
+    got = B.cpu().numpy()                    # default stream: not ordered after `side`
+    exp_b = raw[1].copy()
+    assert O.mxo_reduce2(mxompi.OP[op], mxompi.TYPE[t], raw[0][ea:].ctypes.data,
+                         exp_b[eb:].ctypes.data, n, 1) == 0
+    golden_io.assert_op_equal(got[eb:eb + nb], exp_b[eb:eb + nb], mxompi.OP[op], mxompi.TYPE[t],
+                              f"{op} {t} offs={offs} n={n}")
+    np.testing.assert_array_equal(got[:eb], raw[1][:eb])
+    np.testing.assert_array_equal(got[eb + nb:], raw[1][eb + nb:])
+
+
+@pytest.mark.parametrize("n", [4099, 262144])
+def test_reduce2_sync_chain_across_streams(n):
+    """300 dependent calls alternating between two streams with no event
+    between them: each call must see the previous one's result, so every
+    return must mean complete and visible (the mark's counter is reused by
+    every call of the thread)."""
+    a = torch.ones(n, dtype=torch.int32, device="cuda")
+    b = torch.zeros(n, dtype=torch.int32, device="cuda")
+    torch.cuda.synchronize()
+    s1, s2 = torch.cuda.Stream(), torch.cuda.Stream()
+    for i in range(300):
+        mxompi.reduce2_sync("SUM", "INT32_T", a.data_ptr(), b.data_ptr(), n, (s1 if i % 2 else s2).cuda_stream)
+    assert torch.equal(b.cpu(), torch.full((n,), 300, dtype=torch.int32))

@@ -9,7 +9,10 @@ is read once per process):
            call, launch + synchronise on the legacy default stream
   cache    pointer-range cache, legacy default stream
   stream   pointer-range cache, the calling thread's own stream, hipStreamSynchronize
-  fastsync as stream, completion through the marker kernel's mapped word (default)
+  marker   as stream, completion through a marker kernel's mapped word
+           (MX_FUSED_MARK=0; the round-2 default)
+  fastsync as stream, the reduce kernel's last workgroup raises the word
+           itself (mx_reduce2_sync, round 3 default)
 
 Prints one JSON line per configuration and size: avg us per call and the
 kernel-only time (HIP events around 200 mx_reduce2 launches) for reference.
@@ -23,6 +26,8 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 CONFIGS = {"round1": {"MX_PTR_CACHE": "0", "OMPI_MCA_op_mi355x_stream": "0"},
            "cache": {"MX_PTR_CACHE": "1", "OMPI_MCA_op_mi355x_stream": "0"},
            "stream": {"MX_PTR_CACHE": "1", "OMPI_MCA_op_mi355x_stream": "1", "OMPI_MCA_op_mi355x_fast_sync": "0"},
+           "marker": {"MX_PTR_CACHE": "1", "OMPI_MCA_op_mi355x_stream": "1", "OMPI_MCA_op_mi355x_fast_sync": "1",
+                      "MX_FUSED_MARK": "0"},
            "fastsync": {"MX_PTR_CACHE": "1", "OMPI_MCA_op_mi355x_stream": "1", "OMPI_MCA_op_mi355x_fast_sync": "1"}}
 SIZES = [4 << 10, 64 << 10, 1 << 20]
 
@@ -64,8 +69,9 @@ def main():
     if len(sys.argv) > 1 and sys.argv[1] == "--child":
         child(sys.argv[2])
         return
-    for cfg, env in CONFIGS.items():
-        e = dict(os.environ, **env)
+    order = sys.argv[1:] or list(CONFIGS)     # e.g. `marker fastsync marker fastsync` (interleaved A/B)
+    for cfg in order:
+        e = dict(os.environ, **CONFIGS[cfg])
         r = subprocess.run([sys.executable, os.path.abspath(__file__), "--child", cfg], env=e, timeout=300)
         if r.returncode:
             sys.exit(r.returncode)

@@ -8,6 +8,17 @@ extern int g_num_cus;      // CUs of the current device (256 on MI355X)
 extern int g_device;       // device selected by mx_init
 // 16-byte streaming device copy (mx_coll.hip), falls back to the runtime copy
 int copy_async(void *dst, const void *src, size_t bytes, hipStream_t s);
+// Completion mark carried by a kernel launch: its last workgroup raises
+// *word (mapped host memory) to v; word == nullptr = no mark.
+struct Mark {
+  uint64_t *word;
+  unsigned *ctr;     // workgroups done (device memory, back to 0 by the last one)
+  uint64_t v;
+};
+// Arms the calling thread's mark (word = nullptr when mapped memory is unavailable).
+void mark_arm(Mark *m);
+// Polls the mark's word (~2 ms), then falls back to hipStreamSynchronize(s).
+int mark_wait(const Mark &m, hipStream_t s);
 }  // namespace mx
 
 // Lazily performs mx_init(current device) if the caller did not.

@@ -42,6 +42,29 @@ struct alignas(16) vec16 {
   T e[N];
 };
 
+// Completion mark (mx_reduce2_sync): every workgroup, after its stores,
+// releases them at system scope (its XCD's L2 written back, as a kernel's
+// end would) and counts itself done on a counter in uncached memory; the
+// last one returns the counter to 0 and raises the caller's word in mapped
+// host memory.  The host sees the word instead of waiting for a second,
+// marker kernel -- one dispatch less per blocking call (op/mi355x's handler,
+// ompi_op_reduce op.h:547-610).  Used for launches of <= 64 workgroups
+// only (kFusedMarkMax).  mk.word is a kernel
+// argument, so the branch is uniform; without a mark it costs nothing.
+__device__ __forceinline__ void mark_done(const Mark &mk) {
+  if (mk.word == nullptr) return;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    __threadfence_system();
+    const unsigned done = __hip_atomic_fetch_add(mk.ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    if (done == gridDim.x - 1) {
+      __hip_atomic_store(mk.ctr, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      __threadfence_system();
+      __hip_atomic_store(mk.word, mk.v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+  }
+}
+
 // Scalar per-element application, inout-form (x = b, y = a) or 3-buffer.
 // Results are stored field by field (store_fields): bytes of the target
 // outside the value fields (pair-type padding, x87 pad) keep their content,
@@ -58,7 +81,7 @@ __device__ __forceinline__ void red2_elem(const T *__restrict__ a, T *__restrict
 // (tools/bw_probe*.hip).
 template <class T, class OP, bool NT, int BS = NT ? kBlockNT : kBlock>
 __global__ void __launch_bounds__(BS)
-k_reduce2(const T *__restrict__ a, T *__restrict__ b, size_t n, size_t head, size_t nvec) {
+k_reduce2(const T *__restrict__ a, T *__restrict__ b, size_t n, size_t head, size_t nvec, Mark mk) {
   using V = vec16<T>;
   constexpr int N = V::N;
   const size_t tid = (size_t)blockIdx.x * BS + threadIdx.x;
@@ -77,6 +100,7 @@ k_reduce2(const T *__restrict__ a, T *__restrict__ b, size_t n, size_t head, siz
   const size_t tail0 = head + nvec * N;
   if (tid < head) red2_elem<T, OP>(a, b, tid);
   if (tid < n - tail0) red2_elem<T, OP>(a, b, tail0 + tid);
+  mark_done(mk);
 }
 
 // 2-buffer, 32-byte elements (complex long double, long double + int):
@@ -86,11 +110,8 @@ k_reduce2(const T *__restrict__ a, T *__restrict__ b, size_t n, size_t head, siz
 // line is written whole -- field-by-field stores leave 12 of every 32
 // bytes unwritten, which costs a partial-line write-back per line
 // (tools/sector_probe.hip).  Both buffers 16-byte aligned.
-template <class T, class OP, bool NT, int BS>
-__global__ void __launch_bounds__(BS) k_reduce2_w32(const T *__restrict__ a, T *__restrict__ b, size_t n) {
-  static_assert(sizeof(T) == 32, "32-byte elements");
-  const size_t i = (size_t)blockIdx.x * BS + threadIdx.x;
-  if (i >= n) return;
+template <class T, class OP, bool NT>
+__device__ __forceinline__ void red2_w32(const T *__restrict__ a, T *__restrict__ b, size_t i) {
   const u32x4 *pa = reinterpret_cast<const u32x4 *>(a + i);
   u32x4 *pb = reinterpret_cast<u32x4 *>(b + i);
   u32x4 ra[2], rb[2];
@@ -111,12 +132,21 @@ __global__ void __launch_bounds__(BS) k_reduce2_w32(const T *__restrict__ a, T *
   }
 }
 
+template <class T, class OP, bool NT, int BS>
+__global__ void __launch_bounds__(BS) k_reduce2_w32(const T *__restrict__ a, T *__restrict__ b, size_t n, Mark mk) {
+  static_assert(sizeof(T) == 32, "32-byte elements");
+  const size_t i = (size_t)blockIdx.x * BS + threadIdx.x;
+  if (i < n) red2_w32<T, OP, NT>(a, b, i);
+  mark_done(mk);
+}
+
 // 2-buffer, one element per lane (mismatched alignment, or element > 16 B).
 template <class T, class OP>
 __global__ void __launch_bounds__(kBlock)
-k_reduce2_elem(const T *__restrict__ a, T *__restrict__ b, size_t n) {
+k_reduce2_elem(const T *__restrict__ a, T *__restrict__ b, size_t n, Mark mk) {
   const size_t i = (size_t)blockIdx.x * kBlock + threadIdx.x;
   if (i < n) red2_elem<T, OP>(a, b, i);
+  mark_done(mk);
 }
 
 template <class T, class OP, bool NT, int BS = NT ? kBlockNT : kBlock>
@@ -175,8 +205,28 @@ static bool conv_w32() {
   return on != 0;
 }
 
+// launches that carry their own completion mark: at most 64 workgroups of
+// 256 lanes (<= 16384 elements and <= 256 KiB).  Every workgroup pays a
+// system-scope release before it counts itself done; measured per
+// ompi_op_reduce call, fp32 SUM, interleaved A/B (profiles/r03/
+// op_call_cost_r3.txt): 4 KiB (1 wg) 9.23 -> 7.27 us, 64 KiB (16 wgs)
+// 10.59 -> 8.44, but uncapped at 1 MiB (256 wgs) 9.64 -> 12.31, so larger
+// launches keep the marker kernel.
+constexpr size_t kFusedMarkMax = (size_t)1 << 14;
+constexpr size_t kFusedMarkMaxBytes = (size_t)256 << 10;
+
+// MX_FUSED_MARK=0: mx_reduce2_sync waits through a separate marker kernel
+// (mx_stream_sync_fast) instead of the reduce kernel's own mark (A/B switch)
+static bool fused_mark() {
+  static const int on = [] {
+    const char *e = getenv("MX_FUSED_MARK");
+    return (e && *e == '0') ? 0 : 1;
+  }();
+  return on != 0;
+}
+
 template <class T, class OP>
-static int launch2(const void *in, void *inout, size_t n, hipStream_t s) {
+static int launch2(const void *in, void *inout, size_t n, hipStream_t s, const Mark &mk) {
   const T *a = static_cast<const T *>(in);
   T *b = static_cast<T *>(inout);
   if (n == 0) return MX_SUCCESS;
@@ -186,14 +236,14 @@ static int launch2(const void *in, void *inout, size_t n, hipStream_t s) {
     if (ma == 0 && mb == 0 && conv_w32()) {
       if (mx_nt_for(2 * n * sizeof(T)) && nt_small_wg(n))
         hipLaunchKernelGGL((k_reduce2_w32<T, OP, true, kBlockNT>), dim3(grid_for(n, kBlockNT)), dim3(kBlockNT), 0, s,
-                           a, b, n);
+                           a, b, n, mk);
       else
-        hipLaunchKernelGGL((k_reduce2_w32<T, OP, false, kBlock>), dim3(grid_for(n)), dim3(kBlock), 0, s, a, b, n);
+        hipLaunchKernelGGL((k_reduce2_w32<T, OP, false, kBlock>), dim3(grid_for(n)), dim3(kBlock), 0, s, a, b, n, mk);
       return mx_check_launch();
     }
   }
   if (N == 0 || ma != mb || (ma % sizeof(T)) != 0) {
-    hipLaunchKernelGGL((k_reduce2_elem<T, OP>), dim3(grid_for(n)), dim3(kBlock), 0, s, a, b, n);
+    hipLaunchKernelGGL((k_reduce2_elem<T, OP>), dim3(grid_for(n)), dim3(kBlock), 0, s, a, b, n, mk);
     return mx_check_launch();
   }
   size_t head = ma ? (16 - ma) / sizeof(T) : 0;
@@ -204,12 +254,12 @@ static int launch2(const void *in, void *inout, size_t n, hipStream_t s) {
   if (mx_nt_for(2 * n * sizeof(T))) {
     if (nt_small_wg(work))
       hipLaunchKernelGGL((k_reduce2<T, OP, true>), dim3(grid_for(work, kBlockNT)), dim3(kBlockNT), 0, s, a, b, n, head,
-                         nvec);
+                         nvec, mk);
     else
       hipLaunchKernelGGL((k_reduce2<T, OP, true, kBlock>), dim3(grid_for(work)), dim3(kBlock), 0, s, a, b, n, head,
-                         nvec);
+                         nvec, mk);
   } else {
-    hipLaunchKernelGGL((k_reduce2<T, OP, false>), dim3(grid_for(work)), dim3(kBlock), 0, s, a, b, n, head, nvec);
+    hipLaunchKernelGGL((k_reduce2<T, OP, false>), dim3(grid_for(work)), dim3(kBlock), 0, s, a, b, n, head, nvec, mk);
   }
   return mx_check_launch();
 }
@@ -245,7 +295,7 @@ static int launch3(const void *in1, const void *in2, void *out, size_t n, hipStr
 }
 
 // ---- type-slot dispatch ---------------------------------------------------
-typedef int (*launch2_fn)(const void *, void *, size_t, hipStream_t);
+typedef int (*launch2_fn)(const void *, void *, size_t, hipStream_t, const Mark &);
 typedef int (*launch3_fn)(const void *, const void *, void *, size_t, hipStream_t);
 
 struct entry { launch2_fn f2; launch3_fn f3; };
@@ -314,7 +364,26 @@ extern "C" int mx_reduce2(int op, int type, const void *in, void *inout, size_t 
   if (!in || !inout || count > kMaxItems) return MX_ERR_ARG;
   int rc = mx_ensure_init();
   if (rc) return rc;
-  return e.f2(in, inout, count, (hipStream_t)stream);
+  return e.f2(in, inout, count, (hipStream_t)stream, Mark{nullptr, nullptr, 0});
+}
+
+extern "C" int mx_reduce2_sync(int op, int type, const void *in, void *inout, size_t count, void *stream) {
+  if (op < 0 || op >= MX_OP_COUNT || type < 0 || type >= MX_TYPE_COUNT) return MX_ERR_ARG;
+  entry e = lookup(op, type);
+  if (!e.f2) return MX_ERR_UNSUPPORTED;
+  if (count == 0) return MX_SUCCESS;
+  if (!in || !inout || count > kMaxItems) return MX_ERR_ARG;
+  int rc = mx_ensure_init();
+  if (rc) return rc;
+  hipStream_t s = (hipStream_t)stream;
+  if (!fused_mark() || count > kFusedMarkMax || count * mx_type_size(type) > kFusedMarkMaxBytes) {
+    rc = e.f2(in, inout, count, s, Mark{nullptr, nullptr, 0});
+    return rc ? rc : mx_stream_sync_fast(stream);
+  }
+  Mark mk;
+  mark_arm(&mk);
+  rc = e.f2(in, inout, count, s, mk);
+  return rc ? rc : mark_wait(mk, s);
 }
 
 extern "C" int mx_reduce3(int op, int type, const void *in1, const void *in2, void *out, size_t count,

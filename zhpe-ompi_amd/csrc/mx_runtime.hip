@@ -255,12 +255,59 @@ __global__ void k_mark(uint64_t *w, uint64_t v) {
 }
 struct MarkWord {
   uint64_t *host = nullptr, *dev = nullptr;
+  unsigned *ctr = nullptr;   // workgroup counter of kernels that raise the word themselves (uncached)
   uint64_t seq = 0;
   bool failed = false;
-  ~MarkWord() { if (host) (void)hipHostFree(host); }
+  ~MarkWord() {
+    if (host) (void)hipHostFree(host);
+    if (ctr) (void)hipFree(ctr);
+  }
 };
 thread_local MarkWord t_mark;
+
+MarkWord &mark_word() {
+  MarkWord &m = t_mark;
+  if (!m.host && !m.failed) {
+    if (hipHostMalloc((void **)&m.host, 64, hipHostMallocMapped) != hipSuccess ||
+        hipHostGetDevicePointer((void **)&m.dev, m.host, 0) != hipSuccess ||
+        hipExtMallocWithFlags((void **)&m.ctr, 64, hipDeviceMallocUncached) != hipSuccess ||
+        hipMemset(m.ctr, 0, 64) != hipSuccess || hipStreamSynchronize(nullptr) != hipSuccess) {
+      (void)hipGetLastError();
+      if (m.host) (void)hipHostFree(m.host);
+      if (m.ctr) (void)hipFree(m.ctr);
+      m.host = nullptr;
+      m.ctr = nullptr;
+      m.failed = true;
+    } else {
+      *(volatile uint64_t *)m.host = 0;
+    }
+  }
+  return m;
+}
 }  // namespace
+
+void mx::mark_arm(Mark *out) {
+  MarkWord &m = mark_word();
+  if (!m.host) {
+    *out = Mark{nullptr, nullptr, 0};
+    return;
+  }
+  *out = Mark{m.dev, m.ctr, ++m.seq};
+}
+
+int mx::mark_wait(const Mark &mk, hipStream_t s) {
+  MarkWord &m = t_mark;
+  if (!mk.word || !m.host) return mx_hip_rc(hipStreamSynchronize(s));
+  static const long spins = [] {            // ~2 ms of polling; MX_FAST_SYNC_SPINS overrides (tests)
+    const char *e = getenv("MX_FAST_SYNC_SPINS");
+    return e && *e ? atol(e) : (1L << 16);
+  }();
+  for (long i = 0; i < spins; i++) {
+    if (__atomic_load_n(m.host, __ATOMIC_ACQUIRE) >= mk.v) return MX_SUCCESS;
+    __builtin_ia32_pause();
+  }
+  return mx_hip_rc(hipStreamSynchronize(s));
+}
 
 // hipStreamSynchronize wakes the host several microseconds after the GPU is
 // done; a word in mapped host memory is seen as soon as the marker kernel
@@ -268,32 +315,13 @@ thread_local MarkWord t_mark;
 // word (a long kernel, or a fault) the call falls back to the runtime's wait,
 // which also reports errors.
 extern "C" int mx_stream_sync_fast(void *stream) {
-  MarkWord &m = t_mark;
-  if (!m.host && !m.failed) {
-    if (hipHostMalloc((void **)&m.host, 64, hipHostMallocMapped) != hipSuccess ||
-        hipHostGetDevicePointer((void **)&m.dev, m.host, 0) != hipSuccess) {
-      (void)hipGetLastError();
-      if (m.host) (void)hipHostFree(m.host);
-      m.host = nullptr;
-      m.failed = true;
-    } else {
-      *(volatile uint64_t *)m.host = 0;
-    }
-  }
   hipStream_t s = (hipStream_t)stream;
-  if (!m.host) return mx_hip_rc(hipStreamSynchronize(s));
-  const uint64_t v = ++m.seq;
-  hipLaunchKernelGGL(k_mark, dim3(1), dim3(64), 0, s, m.dev, v);
+  Mark mk;
+  mark_arm(&mk);
+  if (!mk.word) return mx_hip_rc(hipStreamSynchronize(s));
+  hipLaunchKernelGGL(k_mark, dim3(1), dim3(64), 0, s, mk.word, mk.v);
   if (int rc = mx_check_launch()) return rc;
-  static const long spins = [] {            // ~2 ms of polling; MX_FAST_SYNC_SPINS overrides (tests)
-    const char *e = getenv("MX_FAST_SYNC_SPINS");
-    return e && *e ? atol(e) : (1L << 16);
-  }();
-  for (long i = 0; i < spins; i++) {
-    if (__atomic_load_n(m.host, __ATOMIC_ACQUIRE) >= v) return MX_SUCCESS;
-    __builtin_ia32_pause();
-  }
-  return mx_hip_rc(hipStreamSynchronize(s));
+  return mark_wait(mk, s);
 }
 
 extern "C" int mx_copy(void *dst, const void *src, size_t bytes, void *stream) {

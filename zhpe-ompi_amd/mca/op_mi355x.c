@@ -126,8 +126,12 @@ static void mx_op_2buff(void *in, void *inout, int *count, struct ompi_datatype_
     if (slot < 0) die("datatype lookup", MX_ERR_ARG);
     if (*count > 0 && both_on_device(in, inout)) {
         void *s = op_stream();
-        int rc = mx_reduce2(m->op_index, slot, in, inout, (size_t)*count, s);
-        rc = run_sync(s, rc);
+        int rc;
+        if (g_fast_sync < 0) g_fast_sync = mx_ompi_host->mca_int("op_mi355x_fast_sync", 1) != 0;
+        if (g_fast_sync)   /* the reduce kernel raises the completion word itself */
+            rc = mx_reduce2_sync(m->op_index, slot, in, inout, (size_t)*count, s);
+        else
+            rc = run_sync(s, mx_reduce2(m->op_index, slot, in, inout, (size_t)*count, s));
         if (rc != MX_SUCCESS) die("mx_reduce2", rc);
         return;
     }

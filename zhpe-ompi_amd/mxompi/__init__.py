@@ -111,6 +111,7 @@ def lib() -> ctypes.CDLL:
         L.mx_type_size.argtypes = [i]
         L.mx_op_supported.argtypes = [i, i, i]
         L.mx_reduce2.argtypes = [i, i, vp, vp, sz, vp]
+        L.mx_reduce2_sync.argtypes = [i, i, vp, vp, sz, vp]
         L.mx_reduce3.argtypes = [i, i, vp, vp, vp, sz, vp]
         L.mx_copy.argtypes = [vp, vp, sz, vp]
         L.mx_shmem_to_mpi.argtypes = [i, i, sz, ctypes.POINTER(i), ctypes.POINTER(i)]
@@ -150,6 +151,13 @@ def reduce2(op, t, in_ptr: int, inout_ptr: int, count: int, stream: int = 0) -> 
     """inout = inout OP in on the device (asynchronous on `stream`)."""
     check(lib().mx_reduce2(_op(op), _slot(t), in_ptr, inout_ptr, count, stream or None),
           f"mx_reduce2({op},{t})")
+
+
+def reduce2_sync(op, t, in_ptr: int, inout_ptr: int, count: int, stream: int = 0) -> None:
+    """inout = inout OP in on the device; returns with the result complete
+    (mx_reduce2_sync: the kernel's last workgroup raises the completion word)."""
+    check(lib().mx_reduce2_sync(_op(op), _slot(t), in_ptr, inout_ptr, count, stream or None),
+          f"mx_reduce2_sync({op},{t})")
 
 
 def reduce3(op, t, in1_ptr: int, in2_ptr: int, out_ptr: int, count: int, stream: int = 0) -> None:
