@@ -823,8 +823,13 @@ static int mx_coll_reduce_local(const void *inbuf, void *inoutbuf, int count, st
         mx_is_device_ptr(inoutbuf) == 1) {
         if (!m->stream && mx_stream_create_ordered(&m->stream) != MX_SUCCESS) m->stream = NULL;
         int rc = begin(m);
-        if (!rc) rc = mx_reduce2(opi, slot, inbuf, inoutbuf, (size_t)count, m->stream);
-        if (!rc) rc = stream_wait(m->stream);
+        if (g_fast_sync < 0) g_fast_sync = mx_ompi_host->mca_int("coll_mi355x_fast_sync", 1) != 0;
+        if (!rc && g_fast_sync) {   /* small launches raise the completion word themselves */
+            rc = mx_reduce2_sync(opi, slot, inbuf, inoutbuf, (size_t)count, m->stream);
+        } else {
+            if (!rc) rc = mx_reduce2(opi, slot, inbuf, inoutbuf, (size_t)count, m->stream);
+            if (!rc) rc = stream_wait(m->stream);
+        }
         return map_rc(rc);
     }
     return m->prev_reduce_local(inbuf, inoutbuf, count, dtype, op, m->prev_reduce_local_module);
