@@ -203,10 +203,12 @@ int mx_reduce2(int op, int type, const void *in, void *inout,
                size_t count, void *stream);
 /* As mx_reduce2, and returns when the result is complete: the blocking form
  * the op component's handler needs (ompi_op_reduce, ompi/op/op.h:547-610,
- * returns with `inout` final).  The reduce kernel's last workgroup raises a
- * completion word in mapped host memory that the host polls, so no marker
- * kernel follows it (mx_stream_sync_fast semantics otherwise: after ~2 ms
- * the wait falls back to hipStreamSynchronize, which also reports faults). */
+ * returns with `inout` final).  The reduce launch followed by
+ * mx_stream_sync_fast's marker kernel (after ~2 ms the wait falls back to
+ * hipStreamSynchronize, which also reports faults).  MX_FUSED_MARK=1
+ * (measurement only) lets launches of <= 64 workgroups raise the completion
+ * word from their last workgroup instead -- not safe for consumers in other
+ * processes. */
 int mx_reduce2_sync(int op, int type, const void *in, void *inout,
                     size_t count, void *stream);
 /* out[i] = in1[i] OP in2[i].  out may alias neither input (restrict, as

@@ -12,7 +12,8 @@ is read once per process):
   marker   as stream, completion through a marker kernel's mapped word
            (MX_FUSED_MARK=0; the round-2 default)
   fastsync as stream, the reduce kernel's last workgroup raises the word
-           itself (mx_reduce2_sync, round 3 default)
+           itself (MX_FUSED_MARK=1; measurement only -- not safe for
+           consumers in other processes, off by default)
 
 Prints one JSON line per configuration and size: avg us per call and the
 kernel-only time (HIP events around 200 mx_reduce2 launches) for reference.
@@ -28,7 +29,8 @@ CONFIGS = {"round1": {"MX_PTR_CACHE": "0", "OMPI_MCA_op_mi355x_stream": "0"},
            "stream": {"MX_PTR_CACHE": "1", "OMPI_MCA_op_mi355x_stream": "1", "OMPI_MCA_op_mi355x_fast_sync": "0"},
            "marker": {"MX_PTR_CACHE": "1", "OMPI_MCA_op_mi355x_stream": "1", "OMPI_MCA_op_mi355x_fast_sync": "1",
                       "MX_FUSED_MARK": "0"},
-           "fastsync": {"MX_PTR_CACHE": "1", "OMPI_MCA_op_mi355x_stream": "1", "OMPI_MCA_op_mi355x_fast_sync": "1"}}
+           "fastsync": {"MX_PTR_CACHE": "1", "OMPI_MCA_op_mi355x_stream": "1", "OMPI_MCA_op_mi355x_fast_sync": "1",
+                        "MX_FUSED_MARK": "1"}}
 SIZES = [4 << 10, 64 << 10, 1 << 20]
 
 

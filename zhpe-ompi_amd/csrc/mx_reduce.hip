@@ -211,16 +211,22 @@ static bool conv_w32() {
 // ompi_op_reduce call, fp32 SUM, interleaved A/B (profiles/r03/
 // op_call_cost_r3.txt): 4 KiB (1 wg) 9.23 -> 7.27 us, 64 KiB (16 wgs)
 // 10.59 -> 8.44, but uncapped at 1 MiB (256 wgs) 9.64 -> 12.31, so larger
-// launches keep the marker kernel.
+// launches keep the marker kernel.  The whole path is opt-in (fused_mark()).
 constexpr size_t kFusedMarkMax = (size_t)1 << 14;
 constexpr size_t kFusedMarkMaxBytes = (size_t)256 << 10;
 
-// MX_FUSED_MARK=0: mx_reduce2_sync waits through a separate marker kernel
-// (mx_stream_sync_fast) instead of the reduce kernel's own mark (A/B switch)
+// MX_FUSED_MARK=1 lets small launches raise the completion word themselves
+// (measurement only, OFF by default): the in-kernel system-scope release
+// does not publish the workgroups' stores to coarse-grained device memory the
+// way a kernel's end does, and a consumer in another process read stale data
+// (tests/test_components_rules.py, 8 processes, tuned recursive doubling:
+// one 5000-element block wrong on one rank).  By default mx_reduce2_sync
+// is the reduce launch + the marker kernel (mx_stream_sync_fast), which
+// waits for the reduce kernel's end.
 static bool fused_mark() {
   static const int on = [] {
     const char *e = getenv("MX_FUSED_MARK");
-    return (e && *e == '0') ? 0 : 1;
+    return (e && *e == '1') ? 1 : 0;
   }();
   return on != 0;
 }
