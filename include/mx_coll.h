@@ -125,6 +125,12 @@ int mx_comm_get_protocol(const mx_comm_t *comm);
  * (single rank, local communicator, or /dev/shm unavailable on some rank). */
 int mx_comm_set_reg_min(mx_comm_t *comm, size_t min_bytes);
 
+/* One-shot allreduce (one kernel: push, flag, fold) up to `max_bytes` per
+ * rank; clamped to the one-shot slot capacity reserved at creation (1 MiB or
+ * staging / (8 n); MX_ONESHOT_MAX at creation sets both).  0 = off.  Same
+ * value on every rank.  Returns the crossover in force (bytes). */
+long long mx_comm_set_oneshot_max(mx_comm_t *comm, size_t max_bytes);
+
 /* Autotuning of the data movement (default on when the registration page
  * exists and neither MX_ALLREDUCE_PROTO nor MX_REG_MIN forces a path;
  * MX_AUTOTUNE=0 switches it off).  Per collective and power-of-two size

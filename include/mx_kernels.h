@@ -203,12 +203,14 @@ int mx_reduce2(int op, int type, const void *in, void *inout,
                size_t count, void *stream);
 /* As mx_reduce2, and returns when the result is complete: the blocking form
  * the op component's handler needs (ompi_op_reduce, ompi/op/op.h:547-610,
- * returns with `inout` final).  The reduce launch followed by
- * mx_stream_sync_fast's marker kernel (after ~2 ms the wait falls back to
- * hipStreamSynchronize, which also reports faults).  MX_FUSED_MARK=1
- * (measurement only) lets launches of <= 64 workgroups raise the completion
- * word from their last workgroup instead -- not safe for consumers in other
- * processes. */
+ * returns with `inout` final, for every agent).  Launches of <= 64
+ * workgroups raise a completion word in mapped host memory from their last
+ * workgroup, after every workgroup released its stores at system scope;
+ * larger ones are followed by mx_stream_sync_fast's marker kernel
+ * (MX_FUSED_MARK=0: always the marker).  The host polls the word; after
+ * ~2 ms the wait falls back to hipStreamSynchronize, which also reports
+ * faults.  A peer process reading `inout` right after return is tested in
+ * tests/test_op_consumer_gpu.py. */
 int mx_reduce2_sync(int op, int type, const void *in, void *inout,
                     size_t count, void *stream);
 /* out[i] = in1[i] OP in2[i].  out may alias neither input (restrict, as

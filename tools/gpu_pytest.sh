@@ -1,4 +1,5 @@
-# GPU pytest runner. usage on the box: bash tools/gpu_pytest.sh TAG 'pytest args' [more pytest arg sets...]
+# GPU pytest runner. usage on the box: bash tools/gpu_pytest.sh TAG "pytest args" [more pytest arg sets...]
+# (each set is eval'd: quote a -k expression inside it, e.g. "t.py -k 'a or b'")
 # Each argument set runs as one pytest process under its own time limit;
 # the first failure ends the script (nothing more runs on the GPU after it).
 set -o pipefail
@@ -11,7 +12,7 @@ i=0
 for args in "$@"; do
   i=$((i+1))
   echo "[$(date +%T)] pytest $args" | tee -a $O/${T}_log.txt
-  timeout -k 10 ${STEP_TIMEOUT:-900} python -u -m pytest -x -v --timeout ${TEST_TIMEOUT:-300} --timeout-method thread $args \
+  eval timeout -k 10 ${STEP_TIMEOUT:-900} python -u -m pytest -x -v --timeout ${TEST_TIMEOUT:-300} --timeout-method thread $args \
       > $O/${T}_pytest$i.txt 2>&1
   rc=$?
   echo "[$(date +%T)] rc=$rc" | tee -a $O/${T}_log.txt

@@ -439,6 +439,12 @@ extern "C" int mx_comm_set_reg_min(mx_comm_t *c, size_t min_bytes) {
   return MX_SUCCESS;
 }
 
+extern "C" long long mx_comm_set_oneshot_max(mx_comm_t *c, size_t max_bytes) {
+  if (!c) return MX_ERR_ARG;
+  c->os_max = std::min(max_bytes, c->os_cap);
+  return (long long)c->os_max;
+}
+
 extern "C" int mx_comm_create(int rank, int size, int device, size_t staging_bytes, int flags,
                               mx_allgather_fn ag, void *ctx, mx_comm_t **out) {
   return mx_comm_create_ex(rank, size, device, staging_bytes, 0, flags, ag, ctx, out);
@@ -451,10 +457,60 @@ extern "C" int mx_comm_create(int rank, int size, int device, size_t staging_byt
 // made in that place: hipIpcGetMemHandle failed (hsa_status 0x1000) on the
 // next communicator's staging in 8-process runs that create and free
 // communicators back to back.  A destroyed communicator's regions therefore
-// go back to the pool and the next communicator reuses them (same
+// go back to the pool and a later communicator reuses them (same
 // allocation, same handle) instead of freeing and reallocating.
+//
+// A region goes back to the pool only once every peer has said BYE
+// (round 4).  A rank may finish its last call of a communicator while a
+// peer's trailing signals of that call are still on their way into its
+// flags: DONE(g) ends every round and is waited for only by the next call,
+// and a rooted reduce's non-roots never wait for PUSHED(g).  Round 3
+// recycled the flags at once; the next communicator zeroed them at creation,
+// the late DONE / PUSHED of the old one landed after that, and a wait of
+// the new one for PUSHED(2) passed on the stale PUSHED(6): one rank gathered
+// one peer's part before that peer had written it (the 5000-element block of
+// test_tuned_forced_rules_and_basic_orders[8-device]).  Now
+// mx_comm_destroy waits for its own device to go idle and then writes BYE
+// into every peer's flags; a destroyed communicator's regions wait in
+// quarantine until the BYE row of its flags shows every peer.
 static std::mutex g_ipc_pool_mu;
 static std::vector<std::pair<char *, size_t>> g_ipc_pool;
+struct IpcQuarantine { char *staging, *hregion; uint64_t *flags; uint32_t peers; };
+static std::vector<IpcQuarantine> g_ipc_quarantine;
+
+static size_t ipc_region_size(const char *p);
+
+// MX_IPC_QUARANTINE=0: round 3's immediate recycling (the regression
+// demonstration of tools/stale_flag_repro.py only)
+static bool ipc_quarantine_on() {
+  static const bool on = [] {
+    const char *e = getenv("MX_IPC_QUARANTINE");
+    return !(e && *e == '0');
+  }();
+  return on;
+}
+
+static void ipc_pool_put(char *p) {   // caller holds g_ipc_pool_mu
+  if (p) g_ipc_pool.emplace_back(p, ipc_region_size(p));
+}
+
+// move every quarantined group whose peers have all said BYE to the pool
+static void ipc_quarantine_scan() {
+  std::lock_guard<std::mutex> lk(g_ipc_pool_mu);
+  for (size_t i = 0; i < g_ipc_quarantine.size();) {
+    IpcQuarantine &q = g_ipc_quarantine[i];
+    uint64_t bye[MAXR];
+    bool clear = hipMemcpy(bye, q.flags + BYE_BASE, sizeof bye, hipMemcpyDeviceToHost) == hipSuccess;
+    if (!clear) (void)hipGetLastError();
+    for (int p = 0; clear && p < MAXR; p++)
+      if (((q.peers >> p) & 1) && bye[p] != BYE_WORD) clear = false;
+    if (!clear) { i++; continue; }
+    ipc_pool_put(q.staging);
+    ipc_pool_put(q.hregion);
+    ipc_pool_put((char *)q.flags);
+    g_ipc_quarantine.erase(g_ipc_quarantine.begin() + (long)i);
+  }
+}
 
 static int ipc_region_alloc(size_t bytes, char **p) {
   {
@@ -488,11 +544,34 @@ static size_t ipc_region_size(const char *p) {
   return size;
 }
 
-static void ipc_region_free(char *p) {
-  if (!p) return;
-  const size_t size = ipc_region_size(p);
+// a destroyed communicator's regions: to the pool once `peers` said BYE
+static void ipc_regions_release(char *staging, char *hregion, uint64_t *flags, uint32_t peers) {
   std::lock_guard<std::mutex> lk(g_ipc_pool_mu);
-  g_ipc_pool.emplace_back(p, size);
+  if (!flags || !peers || !ipc_quarantine_on()) {
+    ipc_pool_put(staging);
+    ipc_pool_put(hregion);
+    ipc_pool_put((char *)flags);
+    return;
+  }
+  g_ipc_quarantine.push_back(IpcQuarantine{staging, hregion, flags, peers});
+}
+
+// BYE: written after this rank's device went idle (no poison check: a
+// poisoned communicator's kernels have ended too)
+__global__ void k_bye(SignalArgs a) {
+  const int j = threadIdx.x;
+  __threadfence_system();
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  if (j < a.n && a.peer_flag[j])
+    __hip_atomic_store(a.peer_flag[j], BYE_WORD, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+// fault injection (tests only, MX_DEBUG_LAG_RANK / _US): that rank's fold
+// kernels start `ticks` of the wall clock late, so its results and its
+// trailing signals reach the peers late
+__global__ void k_lag(uint64_t ticks) {
+  const uint64_t t0 = wall_clock64();
+  while (wall_clock64() - t0 < ticks) __builtin_amdgcn_s_sleep(127);
 }
 
 // Every bootstrap exchange runs on every rank whatever happened locally:
@@ -556,6 +635,7 @@ extern "C" int mx_comm_create_ex(int rank, int size, int device, size_t staging_
       const uint64_t sig[2] = {0x5EED0000ull + (uint64_t)rank, 0x5EED1000ull + (uint64_t)rank};
       const size_t boxes = (flags & MX_COMM_P2P) ? (size_t)size * P2P_BOX : 0;
       c->staging_alloc = c->p2p_off + boxes;
+      ipc_quarantine_scan();
       ok = ipc_region_alloc(c->staging_alloc, &c->staging) == MX_SUCCESS &&
            ipc_region_alloc(ALL_FLAG_WORDS * sizeof(uint64_t), (char **)&c->flagmem) == MX_SUCCESS &&
            (!c->hregion_bytes || ipc_region_alloc(c->hregion_bytes, &c->hregion) == MX_SUCCESS) &&
@@ -642,6 +722,9 @@ extern "C" int mx_comm_create_ex(int rank, int size, int device, size_t staging_
       c->tune_on = !(at && *at == '0') && !getenv("MX_ALLREDUCE_PROTO") && !getenv("MX_REG_MIN");
     }
     if (reg_all != 1 || !c->reg_imp) reg_release(c);
+    c->live = 1;
+    const char *lr = getenv("MX_DEBUG_LAG_RANK"), *lu = getenv("MX_DEBUG_LAG_US");
+    if (lr && lu && atoi(lr) == rank) c->lag_ticks = ticks_for(atof(lu) * 1e-6);
   } else {
     const int all_ok = agree(ag, ctx, size, ok);
     if (all_ok != 1) {
@@ -678,15 +761,31 @@ extern "C" int mx_comm_create_ex(int rank, int size, int device, size_t staging_
 extern "C" int mx_comm_destroy(mx_comm_t *c) {
   if (!c) return MX_SUCCESS;
   (void)hipDeviceSynchronize();
+  uint32_t peers = 0;
+  if (c->live) {
+    // this rank's last access to its peers' regions is over: say BYE to each
+    // (their regions leave quarantine once every peer said it)
+    SignalArgs a;
+    memset(&a, 0, sizeof a);
+    a.n = c->size;
+    for (int p = 0; p < c->size; p++)
+      if (p != c->rank) {
+        a.peer_flag[p] = c->peer_flags[p] + BYE_BASE + c->rank;
+        peers |= 1u << p;
+      }
+    hipLaunchKernelGGL(k_bye, dim3(1), dim3(64), 0, nullptr, a);
+    if (hipGetLastError() != hipSuccess || hipStreamSynchronize(nullptr) != hipSuccess) (void)hipGetLastError();
+  }
   for (int p = 0; p < c->size && p < MAXR; p++) {
     if (p == c->rank) continue;
     if (c->peer_staging[p]) (void)hipIpcCloseMemHandle(c->peer_staging[p]);
     if (c->peer_flags[p]) (void)hipIpcCloseMemHandle(c->peer_flags[p]);
     if (c->peer_hregion[p]) (void)hipIpcCloseMemHandle(c->peer_hregion[p]);
   }
-  ipc_region_free(c->staging);
-  ipc_region_free(c->hregion);
-  ipc_region_free((char *)c->flagmem);
+  // creation failed (not live): a peer may have mapped the regions and will
+  // never say BYE, so they stay allocated -- never reused, never freed under
+  // a peer's mapping
+  if (c->live || c->size == 1) ipc_regions_release(c->staging, c->hregion, c->flagmem, peers);
   if (c->err_host) (void)hipHostFree(c->err_host);
   if (c->poison) (void)hipFree(c->poison);
   if (c->nccl) ncclCommDestroy(c->nccl);
@@ -924,6 +1023,7 @@ static int run_fold(mx_comm *c, fold_launch_fn fl, const Seg &sg, size_t part_lo
   a.p = sg.p;
   a.poison = c ? c->poison : nullptr;
   a.nt_force = nt_force;
+  if (c && c->lag_ticks) hipLaunchKernelGGL(k_lag, dim3(1), dim3(1), 0, s, c->lag_ticks);   // tests only
   prof_begin(c, s);
   const int rc = fl(a, s);
   prof_end(c, s, 0, (double)(nsrc + ndst) * (double)a.n * (double)es);
@@ -1622,13 +1722,15 @@ extern "C" int mx_allreduce(mx_comm_t *c, const void *sbuf, void *rbuf, size_t c
   }
   // autotuning: cand 0 zero-copy, 1 staged PULL, 2 staged PUSH,
   // 3 one-shot (size classes within the one-shot capacity); -1 the defaults
+  // one-shot is a candidate only where it can run (os_ok depends on op,
+  // type, size and algorithm only: the same on every rank)
   int bucket;
-  int cand = tune_pick(c, TUNE_ALLREDUCE, bytes, (c->os_cap && bytes <= c->os_cap) ? 4 : 3, &bucket);
-  if (cand == 3 && !os_ok) cand = -1;   // this op / type has no one-shot kernel: the defaults, untimed
+  const int ncand = os_ok ? 4 : 3;
+  int cand = tune_pick(c, TUNE_ALLREDUCE, bytes, ncand, &bucket);
   if (cand == 3 || (cand < 0 && os_ok && bytes <= c->os_max)) {
     const auto t0 = std::chrono::steady_clock::now();
     const int rc = allreduce_oneshot(c, ol, ossegs, sb, rb, count, es, s);
-    return rc || cand < 0 ? rc : tune_done(c, TUNE_ALLREDUCE, bucket, cand, 4, secs_since(t0));
+    return rc || cand < 0 ? rc : tune_done(c, TUNE_ALLREDUCE, bucket, cand, ncand, secs_since(t0));
   }
   const int proto0 = c->proto;
   if (cand == 1) c->proto = MX_PROTO_PULL;
@@ -1636,9 +1738,7 @@ extern "C" int mx_allreduce(mx_comm_t *c, const void *sbuf, void *rbuf, size_t c
   const auto t0 = std::chrono::steady_clock::now();
   const int rc = allreduce_staged(c, fl, alg, sb, rb, count, es, zc_mode_of(cand), s);
   c->proto = proto0;
-  return rc || cand < 0 ? rc
-                        : tune_done(c, TUNE_ALLREDUCE, bucket, cand, (c->os_cap && bytes <= c->os_cap) ? 4 : 3,
-                                    secs_since(t0));
+  return rc || cand < 0 ? rc : tune_done(c, TUNE_ALLREDUCE, bucket, cand, ncand, secs_since(t0));
 }
 
 static int reduce_scatter_impl(mx_comm_t *c, const void *sbuf, void *rbuf, const size_t *rcounts, int type, int op,
@@ -2411,6 +2511,7 @@ static int vm_partitioned(mx_comm *c, vm_launch_fn vl, const std::vector<VmSeg> 
       a.p = sg.p;
       int nemit = 0;
       for (int i = 0; i < sg.p.nins; i++) nemit += (sg.p.ins[i].op & 3) == VM_EMIT;
+      if (c->lag_ticks) hipLaunchKernelGGL(k_lag, dim3(1), dim3(1), 0, s, c->lag_ticks);   // tests only
       prof_begin(c, s);
       if ((rc = vl(a, s))) return rc;
       prof_end(c, s, 0, (double)(n + nemit) * (double)a.n * (double)es);
@@ -3611,8 +3712,13 @@ extern "C" int mx_heap_create(mx_comm_t *c, size_t bytes, mx_heap_t **out) {
     h->mem = c->hregion + h->region_off;
     h->flags = (uint64_t *)h->mem;
     h->base = h->mem + kHeapFlagBytes;
-    // flag words start at 0 on every PE before anyone signals
-    int ok = hipMemset(h->mem, 0, kHeapFlagBytes) == hipSuccess && hipDeviceSynchronize() == hipSuccess;
+    // flag words start at 0 on every PE before anyone signals.  The slice may
+    // have served an earlier heap: zero it only once every PE is past that
+    // heap's destroy (its device idle, its trailing sequence writes landed),
+    // else a late write of the old heap survives the zeroing (as the
+    // communicator flags did in round 3)
+    int ok = heap_agree(c, 1) && hipMemset(h->mem, 0, kHeapFlagBytes) == hipSuccess &&
+             hipDeviceSynchronize() == hipSuccess;
     if (!heap_agree(c, ok)) {
       c->hregion_used = h->region_off;
       delete h;

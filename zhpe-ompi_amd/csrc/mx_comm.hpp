@@ -46,7 +46,12 @@ constexpr size_t P2P_FILLED = P2P_POSTED + MAXR;
 constexpr size_t P2P_SEEN = P2P_FILLED + (size_t)MAXR * P2P_L;
 constexpr size_t P2P_DRAINED = P2P_SEEN + (size_t)MAXR * P2P_L;
 constexpr size_t P2P_CTS = P2P_DRAINED + (size_t)MAXR * P2P_L;
-constexpr size_t ALL_FLAG_WORDS = P2P_CTS + 2 * (size_t)MAXR;
+// BYE[src]: written once by src in mx_comm_destroy, after its device was
+// idle -- its last access to this rank's regions is over, so the regions may
+// serve another communicator (mx_coll.hip, the IPC region pool)
+constexpr size_t BYE_BASE = P2P_CTS + 2 * (size_t)MAXR;
+constexpr size_t ALL_FLAG_WORDS = BYE_BASE + (size_t)MAXR;
+constexpr uint64_t BYE_WORD = 0xB7EB7EB7EB7EB7EBull;
 
 // Unexpected messages: a receive whose tag does not match the pair's next
 // envelope sets that message aside and goes on to the next envelope; later
@@ -137,6 +142,11 @@ struct mx_comm {
   int *poison;
   int poisoned;
   uint64_t gen;
+  // created on every rank (peers map this rank's regions): destroy says BYE
+  int live;
+  // fault injection for the regression tests only (MX_DEBUG_LAG_RANK /
+  // MX_DEBUG_LAG_US): this rank starts every fold kernel lag_ticks late
+  uint64_t lag_ticks;
   // staged allreduce data movement (MX_PROTO_*): PUSH writes each part to
   // its owner before the fold (two xGMI phases); PULL copies the input into
   // the rank's own staging and the owner's fold reads the parts over xGMI

@@ -15,8 +15,11 @@ struct Mark {
   unsigned *ctr;     // workgroups done (device memory, back to 0 by the last one)
   uint64_t v;
 };
-// Arms the calling thread's mark (word = nullptr when mapped memory is unavailable).
-void mark_arm(Mark *m);
+// Arms the calling thread's mark (word = nullptr when mapped memory is
+// unavailable).  counter_stream: a kernel that raises the word itself needs
+// the workgroup counter, allocated on first use and zeroed on that stream
+// (ctr = nullptr, and no mark, when that fails); nullptr: the marker kernel.
+void mark_arm(Mark *m, hipStream_t counter_stream = nullptr, bool need_counter = false);
 // Polls the mark's word (~2 ms), then falls back to hipStreamSynchronize(s).
 int mark_wait(const Mark &m, hipStream_t s);
 }  // namespace mx

@@ -53,6 +53,10 @@ struct alignas(16) vec16 {
 // argument, so the branch is uniform; without a mark it costs nothing.
 __device__ __forceinline__ void mark_done(const Mark &mk) {
   if (mk.word == nullptr) return;
+  // every wave's stores have reached its L2 before thread 0's write-back:
+  // the barrier alone orders issue, not completion, and the system fence
+  // below waits only for thread 0's own wave
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   if (threadIdx.x == 0) {
     __threadfence_system();
@@ -211,22 +215,24 @@ static bool conv_w32() {
 // ompi_op_reduce call, fp32 SUM, interleaved A/B (profiles/r03/
 // op_call_cost_r3.txt): 4 KiB (1 wg) 9.23 -> 7.27 us, 64 KiB (16 wgs)
 // 10.59 -> 8.44, but uncapped at 1 MiB (256 wgs) 9.64 -> 12.31, so larger
-// launches keep the marker kernel.  The whole path is opt-in (fused_mark()).
+// launches keep the marker kernel.
 constexpr size_t kFusedMarkMax = (size_t)1 << 14;
 constexpr size_t kFusedMarkMaxBytes = (size_t)256 << 10;
 
-// MX_FUSED_MARK=1 lets small launches raise the completion word themselves
-// (measurement only, OFF by default): the in-kernel system-scope release
-// does not publish the workgroups' stores to coarse-grained device memory the
-// way a kernel's end does, and a consumer in another process read stale data
-// (tests/test_components_rules.py, 8 processes, tuned recursive doubling:
-// one 5000-element block wrong on one rank).  By default mx_reduce2_sync
-// is the reduce launch + the marker kernel (mx_stream_sync_fast), which
-// waits for the reduce kernel's end.
+// Small launches raise the completion word themselves (default; MX_FUSED_MARK=0
+// keeps the marker kernel).  Round 3 switched this off after an 8-process
+// failure (one 5000-element block wrong at one rank) that was later traced
+// to a different cause -- a freed communicator's flags recycled while a
+// peer's trailing signals were still in flight (mx_coll.hip, the IPC region
+// pool); that run never called this function.  The contract,
+// inout complete for every agent on return (ompi/mca/op/op.h:258-273), is
+// tested from another process: tests/test_op_consumer_gpu.py (8 processes,
+// coll/base recursive doubling through op/mi355x, each step's result copied
+// by the peer through an IPC mapping as soon as the handler returns).
 static bool fused_mark() {
   static const int on = [] {
     const char *e = getenv("MX_FUSED_MARK");
-    return (e && *e == '1') ? 1 : 0;
+    return (e && *e == '0') ? 0 : 1;
   }();
   return on != 0;
 }
@@ -387,7 +393,11 @@ extern "C" int mx_reduce2_sync(int op, int type, const void *in, void *inout, si
     return rc ? rc : mx_stream_sync_fast(stream);
   }
   Mark mk;
-  mark_arm(&mk);
+  mark_arm(&mk, s, true);
+  if (!mk.ctr) {   // no counter: the marker kernel
+    rc = e.f2(in, inout, count, s, Mark{nullptr, nullptr, 0});
+    return rc ? rc : mx_stream_sync_fast(stream);
+  }
   rc = e.f2(in, inout, count, s, mk);
   return rc ? rc : mark_wait(mk, s);
 }

@@ -269,14 +269,10 @@ MarkWord &mark_word() {
   MarkWord &m = t_mark;
   if (!m.host && !m.failed) {
     if (hipHostMalloc((void **)&m.host, 64, hipHostMallocMapped) != hipSuccess ||
-        hipHostGetDevicePointer((void **)&m.dev, m.host, 0) != hipSuccess ||
-        hipExtMallocWithFlags((void **)&m.ctr, 64, hipDeviceMallocUncached) != hipSuccess ||
-        hipMemset(m.ctr, 0, 64) != hipSuccess || hipStreamSynchronize(nullptr) != hipSuccess) {
+        hipHostGetDevicePointer((void **)&m.dev, m.host, 0) != hipSuccess) {
       (void)hipGetLastError();
       if (m.host) (void)hipHostFree(m.host);
-      if (m.ctr) (void)hipFree(m.ctr);
       m.host = nullptr;
-      m.ctr = nullptr;
       m.failed = true;
     } else {
       *(volatile uint64_t *)m.host = 0;
@@ -286,13 +282,24 @@ MarkWord &mark_word() {
 }
 }  // namespace
 
-void mx::mark_arm(Mark *out) {
+void mx::mark_arm(Mark *out, hipStream_t counter_stream, bool need_counter) {
   MarkWord &m = mark_word();
-  if (!m.host) {
-    *out = Mark{nullptr, nullptr, 0};
-    return;
+  *out = Mark{nullptr, nullptr, 0};
+  if (!m.host) return;
+  if (need_counter && !m.ctr) {
+    // the workgroup counter of kernels that raise the word themselves, made
+    // on first use only (the marker-kernel path never needs it), zeroed on
+    // the caller's stream ahead of the kernel that counts on it
+    unsigned *ctr = nullptr;
+    if (hipExtMallocWithFlags((void **)&ctr, 64, hipDeviceMallocUncached) != hipSuccess ||
+        hipMemsetAsync(ctr, 0, 64, counter_stream) != hipSuccess) {
+      (void)hipGetLastError();
+      if (ctr) (void)hipFree(ctr);
+      return;
+    }
+    m.ctr = ctr;
   }
-  *out = Mark{m.dev, m.ctr, ++m.seq};
+  *out = Mark{m.dev, need_counter ? m.ctr : nullptr, ++m.seq};
 }
 
 int mx::mark_wait(const Mark &mk, hipStream_t s) {

@@ -44,9 +44,11 @@
  * saved module the same way small calls do.  Intercommunicators are declined
  * at query (coll_tuned_module.c:66-69).
  *
- * The device work runs on a stream the module owns (non-blocking: a wait
- * for a late peer never stalls the process's legacy default stream, e.g. a
- * PML copy), ordered after the work already queued on the default stream.
+ * Blocking collectives run on a stream the module owns, created blocking
+ * (mx_stream_create_ordered): implicitly ordered with the legacy default
+ * stream, with no event per call.  Nonblocking and persistent requests run
+ * on a second, non-blocking high-priority stream (mx_stream_create), so a
+ * request waiting for a late peer never stalls the default stream.
  * Peer waits are unbounded by default (a peer may legally arrive arbitrarily
  * late); coll_mi355x_wait_timeout bounds them, and a timeout poisons the
  * communicator (include/mx_coll.h).
@@ -824,7 +826,7 @@ static int mx_coll_reduce_local(const void *inbuf, void *inoutbuf, int count, st
         if (!m->stream && mx_stream_create_ordered(&m->stream) != MX_SUCCESS) m->stream = NULL;
         int rc = begin(m);
         if (g_fast_sync < 0) g_fast_sync = mx_ompi_host->mca_int("coll_mi355x_fast_sync", 1) != 0;
-        if (!rc && g_fast_sync) {   /* small launches raise the completion word themselves */
+        if (!rc && g_fast_sync) {   /* completion word: from small reduce launches themselves, else a marker kernel */
             rc = mx_reduce2_sync(opi, slot, inbuf, inoutbuf, (size_t)count, m->stream);
         } else {
             if (!rc) rc = mx_reduce2(opi, slot, inbuf, inoutbuf, (size_t)count, m->stream);

@@ -155,7 +155,8 @@ def reduce2(op, t, in_ptr: int, inout_ptr: int, count: int, stream: int = 0) -> 
 
 def reduce2_sync(op, t, in_ptr: int, inout_ptr: int, count: int, stream: int = 0) -> None:
     """inout = inout OP in on the device; returns with the result complete
-    (mx_reduce2_sync: the kernel's last workgroup raises the completion word)."""
+    (mx_reduce2_sync: a completion word raised by the kernel's last workgroup
+    for launches of <= 64 workgroups, else by a marker kernel)."""
     check(lib().mx_reduce2_sync(_op(op), _slot(t), in_ptr, inout_ptr, count, stream or None),
           f"mx_reduce2_sync({op},{t})")
 
@@ -222,6 +223,8 @@ def _coll_lib():
         L.mx_comm_set_protocol.argtypes = [vp, i]
         L.mx_comm_get_protocol.argtypes = [vp]
         L.mx_comm_set_reg_min.argtypes = [vp, sz]
+        L.mx_comm_set_oneshot_max.argtypes = [vp, sz]
+        L.mx_comm_set_oneshot_max.restype = ctypes.c_longlong
         L.mx_comm_set_autotune.argtypes = [vp, i]
         L.mx_comm_get_tuning.argtypes = [vp, sz]
         L.mx_comm_get_tuning_ex.argtypes = [vp, i, sz]
@@ -441,6 +444,14 @@ class Comm:
         """Zero-copy (registered user buffers) allreduce from min_bytes per rank; 0 = off
         (mx_comm_set_reg_min).  Every rank must set the same value."""
         check(_coll_lib().mx_comm_set_reg_min(self.h, min_bytes), "mx_comm_set_reg_min")
+
+    def set_oneshot_max(self, max_bytes):
+        """One-shot allreduce up to max_bytes per rank, clamped to the slot
+        capacity (mx_comm_set_oneshot_max); 0 = off.  Every rank must set the
+        same value.  Returns the crossover in force."""
+        rc = _coll_lib().mx_comm_set_oneshot_max(self.h, max_bytes)
+        check(min(rc, 0), "mx_comm_set_oneshot_max")
+        return rc
 
     def close(self):
         if getattr(self, "h", None):
