@@ -59,19 +59,32 @@ def load_traffic(kernel_key):
         return None
 
 
+def _oracle_bench():
+    """The CPU oracle built with the reference's default optimisation flags
+    (oracle/Makefile build/libmx_oracle_bench.so: -O3 -finline-functions
+    -fno-strict-aliasing, config/opal_setup_cc.m4:351-365, 481-493)."""
+    import subprocess
+    path = os.path.join(ROOT, "oracle", "build", "libmx_oracle_bench.so")
+    if not os.path.exists(path):
+        subprocess.run(["make", "-s", "-C", os.path.join(ROOT, "oracle"), "build/libmx_oracle_bench.so"], check=True)
+    L = ctypes.CDLL(path)
+    vp, sz, i = ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int
+    L.mxo_reduce2.argtypes = [i, i, vp, vp, sz, i]
+    L.mxo_ddt_convert.argtypes = [vp, sz, vp, ctypes.c_int64, ctypes.c_int64, sz, vp, vp, ctypes.c_int]
+    return L
+
+
 def cpu_baseline_reduce_local(seconds=10.0):
     """Time the 2-buffer fp32 SUM of the CPU oracle -- oracle/mx_oracle_op.c,
     the restatement of op_base_functions.c:40-51 (OP_FUNC, instantiated for
-    float at :312), compiled -O2 for the x86-64 baseline like the reference's
-    own loop -- on one host core, on a bounded sample: 2 x 256 MiB host
-    buffers, repeated ~`seconds`."""
+    float at :312), compiled with the reference's default flags (-O3
+    -finline-functions, x86-64 baseline ISA) -- on one host core, on a
+    bounded sample: 2 x 256 MiB host buffers, repeated ~`seconds`."""
     import numpy as np
-    sys.path.insert(0, os.path.join(ROOT, "tests"))
-    import oracle_lib
     n = 1 << 26
     a = np.random.default_rng(1).uniform(-1, 1, n).astype(np.float32)
     b = np.random.default_rng(2).uniform(-1, 1, n).astype(np.float32)
-    O = oracle_lib.oracle()
+    O = _oracle_bench()
     call = lambda: O.mxo_reduce2(3, 15, a.ctypes.data, b.ctypes.data, n, 1)   # [MPI_SUM][FLOAT]
     call()
     iters, t0 = 0, time.perf_counter()
@@ -82,9 +95,100 @@ def cpu_baseline_reduce_local(seconds=10.0):
         if el >= seconds:
             break
     gbs = 3.0 * n * 4 * iters / el / 1e9
-    return {"value": round(gbs, 3), "unit": "GB/s", "cores": 1, "kind": "port",
+    return {"value": round(gbs, 3), "unit": "GB/s", "cores": 1, "kind": "port", "host_cpu": _cpu_model(),
             "sample": f"fp32 SUM 2-buffer, 2 x 256 MiB host buffers, {iters} calls in {el:.1f} s "
-                      f"(1 host thread; algorithmic 3*N*4 B per call)"}
+                      f"(1 host thread; algorithmic 3*N*4 B per call; -O3 -finline-functions)"}
+
+
+def _cpu_model():
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
+# CFG-C (BASELINE configs[2]): derived-datatype pack / unpack, one type of
+# each constructor, 256 MiB packed per call
+PACK_BENCH_TYPES = ["vector_f32_b4_s8", "indexed_f32_random", "struct_char_d3_int_resized48"]
+
+
+def pack_side_by_side(torch, mx, cpu=True, packed_bytes=256 << 20, cpu_seconds=1.5):
+    """MPI_Pack / MPI_Unpack of the CFG-C types on the device (mx_pack /
+    mx_unpack, HIP events on the launch stream, median of 5 batches) and --
+    `cpu` -- the convertor walk on one host core beside it (the oracle's
+    restatement of opal_generic_simple_pack_function, opal_datatype_pack.c:
+    235-370, and opal_datatype_unpack.c:245-427, -O3 build, kind "port").
+    GB/s = 2 x packed bytes / time."""
+    import numpy as np
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import golden_io
+    basic, recs = golden_io.ddt_records()
+    BASIC = np.ascontiguousarray(basic)
+    O = _oracle_bench() if cpu else None
+    stream = torch.cuda.current_stream()
+    sp = stream.cuda_stream
+    rows = []
+    for name in PACK_BENCH_TYPES:
+        rec = next(r for r in recs if r["name"] == name)
+        ext = rec["ub"] - rec["lb"]
+        count = packed_bytes // rec["size"]
+        nbp = count * rec["size"]
+        span = ext * (count - 1) + rec["true_ub"] - rec["true_lb"]
+        row = {"type": name, "count": count, "packed_bytes": nbp}
+        dt = mx.Datatype(rec["desc"].tobytes(), rec["nrec"], rec["size"], rec["lb"], rec["ub"])
+        U = torch.randint(0, 256, (span,), dtype=torch.uint8, device="cuda")
+        P = torch.empty(nbp, dtype=torch.uint8, device="cuda")
+        ubase = U.data_ptr() - rec["true_lb"]
+        for direction in ("pack", "unpack"):
+            fn = (lambda: dt.pack(count, ubase, P.data_ptr(), stream=sp)) if direction == "pack" else \
+                 (lambda: dt.unpack(count, ubase, P.data_ptr(), stream=sp))
+            fn()
+            torch.cuda.synchronize()
+            ts = []
+            for _ in range(5):
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                e0.record(stream)
+                for _ in range(4):
+                    fn()
+                e1.record(stream)
+                torch.cuda.synchronize()
+                ts.append(e0.elapsed_time(e1) / 4)
+            ms = sorted(ts)[2]
+            row[f"gpu_{direction}_gbs"] = round(2.0 * nbp / (ms * 1e-3) / 1e9, 1)
+        del U, P
+        dt.close()
+        torch.cuda.empty_cache()
+        if O is not None:
+            user = np.random.default_rng(1).integers(0, 256, span, dtype=np.uint8)
+            packed = np.zeros(nbp, np.uint8)
+            for direction, unpack in (("pack", 0), ("unpack", 1)):
+                call = lambda: O.mxo_ddt_convert(rec["desc"].ctypes.data, rec["nrec"], BASIC.ctypes.data, rec["lb"],
+                                                 rec["ub"], count, user.ctypes.data - rec["true_lb"],
+                                                 packed.ctypes.data, unpack)
+                call()
+                k, t0 = 0, time.perf_counter()
+                while True:
+                    call()
+                    k += 1
+                    el = time.perf_counter() - t0
+                    if el >= cpu_seconds:
+                        break
+                row[f"cpu_{direction}_gbs"] = round(2.0 * nbp * k / el / 1e9, 3)
+            del user, packed
+            for d in ("pack", "unpack"):
+                row[f"gpu_over_cpu_{d}"] = round(row[f"gpu_{d}_gbs"] / row[f"cpu_{d}_gbs"], 1)
+        rows.append(row)
+    out = {"unit": "GB/s", "types": rows,
+           "gpu": "mx_pack / mx_unpack on one MI355X, HIP events, median of 5 x 4 calls"}
+    if cpu:
+        out["cpu"] = {"cores": 1, "kind": "port", "host_cpu": _cpu_model(),
+                      "sample": f"the convertor walk restated (oracle/mx_oracle_ddt.c, -O3), one host thread, "
+                                f"{packed_bytes >> 20} MiB packed per call, >= {cpu_seconds} s per type and direction"}
+    return out
 
 
 def cpu_baseline_allreduce(ranks=8, nbytes=256 << 20, iters=10):
@@ -592,8 +696,16 @@ def main():
             "parity_check": {"what": "one more mx_reduce2 fp32 SUM of the 1 GiB inputs after the timed region, "
                                      "bit-compared with the same sum by a torch kernel (IEEE fp32 add)"},
         })
+    if rank == 0 and world == 1:
+        # CFG-C beside the headline: device pack / unpack (+ the CPU walk)
+        try:
+            result["pack_unpack"] = pack_side_by_side(torch, mx, cpu=not args.no_cpu_baseline)
+        except Exception as e:  # noqa: BLE001 - reported in the JSON line
+            result["pack_unpack"] = {"error": repr(e)}
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         result["cpu_baseline"] = cpu_baseline_reduce_local(args.cpu_seconds)
+        result["cpu_baseline_pack"] = {k: result["pack_unpack"].get(k) for k in ("cpu", "types")} \
+            if "types" in result.get("pack_unpack", {}) else result.get("pack_unpack")
         result["cpu_baseline_allreduce"] = cpu_baseline_allreduce()
     elif world > 1 and done and not args.no_cpu_baseline:
         # the host allreduce of the same shape (world ranks, 256 MiB fp32

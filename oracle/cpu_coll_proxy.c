@@ -18,8 +18,15 @@
  *    reduce-scatter, recursive-doubling allgather.
  * Blocks follow COLL_BASE_COMPUTE_BLOCKCOUNT (coll_base_functions.h:
  * 428-435).  Transport is modelled as vader's single-copy path (CMA): the
- * receiver copies the part straight out of the sender's buffer; one
- * process-shared barrier per step stands in for the send/recv completion.
+ * receiver copies the part straight out of the sender's buffer.  Round 4:
+ * a ring step waits only for its left neighbour to have finished the step
+ * before (a per-rank step counter in shared memory: the pairwise
+ * send/recv completion), not for every rank (round 3 put a process-shared
+ * barrier around every copy, which held all ranks to the slowest); one
+ * barrier separates the reduce-scatter from the allgather.  Ranks are
+ * pinned one per core, spread over the L3 domains first (MX_PROXY_PLACEMENT=
+ * packed: consecutive cores, round 3's placement): 8 ranks on one CCD share
+ * that CCD's link to memory.
  * Every algorithm is timed; "value" is the fixed decision's.
  * The local reduction is a plain C loop of the OP_FUNC shape
  * (op_base_functions.c:40-51) ("port"); an optional shared library
@@ -71,13 +78,55 @@ struct shared {
     pthread_barrier_t bar;
     double times[8];          /* per algorithm id */
     int mismatch;
+    volatile uint64_t done[64] __attribute__((aligned(64)));   /* last ring step each rank finished */
 };
+
+/* the left neighbour has finished step s (its send of this step is ready) */
+static void wait_step(struct shared *sh, int p, uint64_t s)
+{
+    while (__atomic_load_n(&sh->done[p], __ATOMIC_ACQUIRE) < s) __builtin_ia32_pause();
+}
+static void post_step(struct shared *sh, int r, uint64_t s)
+{
+    __atomic_store_n(&sh->done[r], s, __ATOMIC_RELEASE);
+}
 
 static void blockcount(size_t count, int n, int b, size_t *off, size_t *len)
 {
     const size_t late = count / n, split = count % n, early = late + (split ? 1 : 0);
     *off = (size_t)b < split ? b * early : b * late + split;
     *len = (size_t)b < split ? early : late;
+}
+
+/* order cpus[] round-robin over their L3 domains (first core of every
+ * domain, then the second, ...); returns the number of domains */
+static int spread_over_l3(int *cpus, int ncpu)
+{
+    char (*key)[128] = calloc((size_t)ncpu, 128);
+    int *dom = calloc((size_t)ncpu, sizeof(int)), *out = calloc((size_t)ncpu, sizeof(int));
+    int ndom = 0;
+    if (!key || !dom || !out) { free(key); free(dom); free(out); return 1; }
+    for (int i = 0; i < ncpu; i++) {
+        char path[128];
+        snprintf(path, sizeof path, "/sys/devices/system/cpu/cpu%d/cache/index3/shared_cpu_list", cpus[i]);
+        FILE *f = fopen(path, "r");
+        if (!f || !fgets(key[i], 128, f)) snprintf(key[i], 128, "cpu%d", cpus[i] / 8);   /* unknown: groups of 8 */
+        if (f) fclose(f);
+        dom[i] = -1;
+        for (int j = 0; j < i; j++)
+            if (!strcmp(key[i], key[j])) { dom[i] = dom[j]; break; }
+        if (dom[i] < 0) dom[i] = ndom++;
+    }
+    int k = 0;
+    for (int round = 0; k < ncpu; round++)
+        for (int d = 0; d < ndom; d++) {
+            int seen = 0;
+            for (int i = 0; i < ncpu; i++)
+                if (dom[i] == d && seen++ == round) { out[k++] = cpus[i]; break; }
+        }
+    memcpy(cpus, out, sizeof(int) * (size_t)ncpu);
+    free(key); free(dom); free(out);
+    return ndom;
 }
 
 static int cmp_double(const void *a, const void *b)
@@ -90,25 +139,29 @@ static int cmp_double(const void *a, const void *b)
  * ring's phase p covers segment p of every block, COLL_BASE_COMPUTE_BLOCKCOUNT
  * of the block over the phases), then the ring allgather of whole blocks */
 static void ring(struct shared *sh, int r, int n, size_t count, float *rbuf, float *inbuf, const float *lrbuf,
-                 int nph)
+                 int nph, uint64_t *step)
 {
+    const int left = (r + n - 1) % n;
     for (int ph = 0; ph < nph; ph++) {
         for (int k = 1; k < n; k++) {
             const int b = (r - k + 2 * n) % n;
             size_t bo, bl, po, pl;
             blockcount(count, n, b, &bo, &bl);
             blockcount(bl, nph, ph, &po, &pl);
-            pthread_barrier_wait(&sh->bar);
+            wait_step(sh, left, *step);         /* left reduced this segment of block b one step ago */
             memcpy(inbuf, lrbuf + bo + po, pl * 4);
             reduce_sum_float(inbuf, rbuf + bo + po, pl);
+            post_step(sh, r, ++*step);
         }
     }
+    pthread_barrier_wait(&sh->bar);             /* every block final before any is overwritten */
     for (int k = 0; k < n - 1; k++) {
         const int b = (r - k + 2 * n) % n;
         size_t bo, bl;
         blockcount(count, n, b, &bo, &bl);
-        pthread_barrier_wait(&sh->bar);
+        if (k) wait_step(sh, left, *step);      /* left holds block b (final) since its step before */
         memcpy(rbuf + bo, lrbuf + bo, bl * 4);
+        post_step(sh, r, ++*step);
     }
 }
 
@@ -196,6 +249,10 @@ int main(int argc, char **argv)
     sched_getaffinity(0, sizeof allowed, &allowed);
     int cpus[1024], ncpu = 0;
     for (int i = 0; i < CPU_SETSIZE && ncpu < 1024; i++) if (CPU_ISSET(i, &allowed)) cpus[ncpu++] = i;
+    const char *pl = getenv("MX_PROXY_PLACEMENT");
+    const int spread = !(pl && !strcmp(pl, "packed"));
+    int ndom = 1;
+    if (spread && ncpu) ndom = spread_over_l3(cpus, ncpu);
 
     for (int r = 0; r < n; r++) {
         pid_t pid = fork();
@@ -218,6 +275,7 @@ int main(int argc, char **argv)
         const int left = (r + n - 1) % n;
         const float *lrbuf = (const float *)(mem + per_rank * left) + count;
         double *ts = malloc(sizeof(double) * (iters + 2));
+        uint64_t step = 0;   /* ring steps done by this rank (the same count on every rank) */
         for (int ai = 0; ai < nalg; ai++) {
             const int alg = algs[ai];
             for (int it = 0; it < iters + 2; it++) {   /* 2 warmup iterations */
@@ -225,7 +283,7 @@ int main(int argc, char **argv)
                 const double t0 = now();
                 memcpy(rbuf, sbuf, count * 4);
                 if (alg == 6) rabenseifner(sh, mem, per_rank, r, n, count, rbuf, inbuf);
-                else ring(sh, r, n, count, rbuf, inbuf, lrbuf, alg == 5 ? phases : 1);
+                else ring(sh, r, n, count, rbuf, inbuf, lrbuf, alg == 5 ? phases : 1, &step);
                 pthread_barrier_wait(&sh->bar);
                 ts[it] = now() - t0;
             }
@@ -255,9 +313,11 @@ int main(int argc, char **argv)
     for (int ai = 0; ai < nalg; ai++)
         printf("%s\"%s\": %.3f", ai ? ", " : "", names[algs[ai]],
                (double)count * 4 / sh->times[algs[ai]] / 1e9 * 2.0 * (n - 1) / n);
-    printf("}, \"sample\": \"MPI_Allreduce fp32 SUM %zu B, %d ranks (processes pinned one per core), coll/tuned's "
-           "fixed decision (%s, %d phases of 1 MiB segments) over shared memory with single-copy transfers, "
-           "median of %d calls; busBW = S/t*2(n-1)/n\"}\n",
-           count * 4, n, names[decided], decided == 5 ? phases : 1, iters);
+    printf("}, \"placement\": \"%s\", \"l3_domains\": %d, \"sample\": \"MPI_Allreduce fp32 SUM %zu B, %d ranks "
+           "(processes pinned one per core, %s over %d L3 domains), coll/tuned's fixed decision (%s, %d phases of 1 MiB "
+           "segments) over shared memory with single-copy transfers and pairwise step completion, median of %d "
+           "calls; busBW = S/t*2(n-1)/n\"}\n",
+           spread ? "spread" : "packed", ndom, count * 4, n, spread ? "spread" : "packed", ndom, names[decided],
+           decided == 5 ? phases : 1, iters);
     return 0;
 }
