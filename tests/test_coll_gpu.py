@@ -283,6 +283,27 @@ def _mp_worker(rank, n, port, staging, jobs, q, env=None):
                 out = torch.zeros(count * 4, dtype=torch.uint8, device="cuda")
                 comm.shmem_reduce("MAX", "FLOAT", 4, out.data_ptr(), x.data_ptr(), count, st)
                 results.append(out.cpu().numpy().tobytes())
+            elif kind == "oshmem_max_example":
+                # examples/oshmem_max_reduction.c:36-46: long src[N] = my_pe + i,
+                # shmem_long_max_to_all(dst, src, N, 0, 0, num_pes, ...) -- through
+                # scoll/mpi (MPI_LONG MAX allreduce) and on the device symmetric heap
+                src = torch.tensor([rank + i for i in range(count)], dtype=torch.int64, device="cuda")
+                dst = torch.full((count,), -1, dtype=torch.int64, device="cuda")
+                comm.shmem_reduce("MAX", "LONG", 8, dst.data_ptr(), src.data_ptr(), count, st)
+                heap = mxompi.Heap(comm, 1 << 20)
+                hs, hd = heap.alloc(count * 8), heap.alloc(count * 8)
+                mxompi.lib().mx_copy(hs, src.data_ptr(), count * 8, None)
+                mxompi.sync()
+                heap.barrier_all()
+                heap.reduce("MAX", "LONG", 8, hd, hs, count)
+                hdst = torch.empty(count, dtype=torch.int64, device="cuda")
+                mxompi.lib().mx_copy(hdst.data_ptr(), hd, count * 8, None)
+                mxompi.sync()
+                heap.barrier_all()
+                heap.free(hd)
+                heap.free(hs)
+                heap.close()
+                results.append((dst.cpu().tolist(), hdst.cpu().tolist()))
             elif kind in ("bcast", "bcast_root0"):
                 x = _dev(gen("UINT8_T", "BAND", count, 7000 + rank))
                 comm.bcast(x.data_ptr(), count, n - 1 if kind == "bcast" else 0, st)
@@ -704,6 +725,17 @@ _JOBS_RECYCLE = [j for op in ("SUM", "MAX", "MIN", "SUM") for j in (
     ("allreduce", 40001, op, "FLOAT", "recursive_doubling"),         # staged PULL: waits PUSHED(2)
     ("reduce", 30001, "SUM", "FLOAT", "auto"),                       # staged VM, root n-1
     ("recreate", 0, "SUM", "FLOAT", "auto"))]
+
+
+@pytest.mark.parametrize("n", [2, 3, 8])
+def test_oshmem_max_reduction_example(n):
+    """The reference's one OpenSHMEM known answer (examples/oshmem_max_reduction.c:
+    36-46, N = 3): after shmem_long_max_to_all every PE holds dst[i] = npes-1+i."""
+    got = _run_mp(n, [("oshmem_max_example", 3, "MAX", "INT64_T", "auto")], staging=16 << 20)
+    for r in range(n):
+        staged, heap = got[r][0]
+        assert staged == [n - 1 + i for i in range(3)], (r, staged)
+        assert heap == [n - 1 + i for i in range(3)], (r, heap)
 
 
 def test_communicator_recycling_with_a_late_peer_8_ranks():

@@ -357,3 +357,203 @@ def test_reset_position_resumes_exactly_device(chunk):
         torch.cuda.synchronize()
         assert torch.equal(R, full)
         dt.close()
+
+
+# ---- position.c (round 4) ----------------------------------------------------------
+# test/datatype/position.c:220-275: MPI_LONG_DOUBLE_INT x 2048 (struct {long
+# double ld; int i;}: ld at 0 with its 16-byte storage, i at 16, extent 32,
+# size 20 -- DECLARE_MPI2_COMPOSED_STRUCT_DDT, ompi_datatype_module.c:404-434,
+# 525), packed in 113-byte segments whose positions create_segments (:44-87)
+# finds with opal_convertor_set_position, the segment order shuffled
+# (shuffle_segments :89-101), every segment packed at its position
+# (pack_segments :103-141) and unpacked at its position in the shuffled order
+# (unpack_segments :143-180); expected (:254-268): recv[i].ld == send[i].ld and
+# recv[i].i == send[i].i for every i.  send[i].ld = i + i / 100000.0, send[i].i = i.
+# The reference starts recv as a copy of send (:236), which the positioned
+# unpack must leave intact; the stronger variant starts recv filled with 0xEE:
+# every packed byte must arrive and the 12 bytes of struct padding after `i`
+# stay 0xEE (the convertor never writes outside the description).
+FLOAT16 = 18                       # OPAL_DATATYPE_FLOAT16: long double on x86-64 (16-byte storage)
+LDI = np.dtype([("ld", np.longdouble), ("i", "<i4"), ("pad", "<i4", 3)])   # 32 B
+POS_COUNT, POS_FRAG = 2048, 113
+
+
+def _long_double_int():
+    return Desc([(FLOAT16, 1, 1, 16, 0), (INT4, 1, 1, 4, 16)], 20, 0, 32)
+
+
+def _position_send():
+    send = np.zeros(POS_COUNT, LDI)
+    i = np.arange(POS_COUNT)
+    send["ld"] = i.astype(np.longdouble) + i.astype(np.longdouble) / np.longdouble(100000.0)
+    send["i"] = i
+    return send
+
+
+def _position_check(recv, send, strong):
+    assert np.array_equal(recv["ld"], send["ld"]) and np.array_equal(recv["i"], send["i"]), \
+        f"{int(np.sum((recv['ld'] != send['ld']) | (recv['i'] != send['i'])))} errors"
+    if strong:
+        rb, sb = recv.view(np.uint8).reshape(-1, 32), send.view(np.uint8).reshape(-1, 32)
+        np.testing.assert_array_equal(rb[:, :20], sb[:, :20])       # every packed byte (incl. the x87 pad)
+        assert np.all(rb[:, 20:] == 0xEE)                            # struct padding untouched
+
+
+def test_position_long_double_int_segments_cover_the_stream():
+    d = _long_double_int()
+    assert d.size == 20 and d.ub - d.lb == LDI.itemsize == 32
+    segs = _segments(d.size * POS_COUNT, POS_FRAG)
+    assert len(segs) == -(-d.size * POS_COUNT // POS_FRAG)
+    cover = np.zeros(d.size * POS_COUNT, np.int32)
+    for p, l in segs:
+        cover[p:p + l] += 1
+    assert np.all(cover == 1)
+
+
+@pytest.mark.parametrize("strong", [False, True], ids=["reference", "recv_filled"])
+def test_position_long_double_int_cpu(strong):
+    d = _long_double_int()
+    send = _position_send()
+    recv = send.copy()
+    if strong:
+        recv.view(np.uint8)[:] = 0xEE
+    segs = _segments(d.size * POS_COUNT, POS_FRAG)
+    bufs = {}
+    for p, l in segs:
+        buf = np.zeros(l, np.uint8)
+        cpu_fragment(d, POS_COUNT, send.view(np.uint8), buf, p, l, False)
+        bufs[p] = buf
+    for p, l in segs:
+        cpu_fragment(d, POS_COUNT, recv.view(np.uint8), bufs[p], p, l, True)
+    _position_check(recv, send, strong)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("strong", [False, True], ids=["reference", "recv_filled"])
+def test_position_long_double_int_device(strong):
+    dev = Device(torch)
+    d = _long_double_int()
+    dt = dev.dt(d)
+    send = _position_send()
+    recv = send.copy()
+    if strong:
+        recv.view(np.uint8)[:] = 0xEE
+    S, R = _dev(send), _dev(recv)
+    segs = _segments(d.size * POS_COUNT, POS_FRAG)
+    bufs = {p: torch.zeros(l, dtype=torch.uint8, device="cuda") for p, l in segs}
+    for p, l in segs:                     # pack_segments: the shuffled order, each at its position
+        dt.pack(POS_COUNT, S.data_ptr(), bufs[p].data_ptr(), offset=p, length=l, stream=dev.s)
+    for p, l in segs:                     # unpack_segments
+        dt.unpack(POS_COUNT, R.data_ptr(), bufs[p].data_ptr(), offset=p, length=l, stream=dev.s)
+    torch.cuda.synchronize()
+    got = np.frombuffer(R.cpu().numpy().tobytes(), LDI)
+    _position_check(got, send, strong)
+    dt.close()
+
+
+# ---- large_data.c (round 4) --------------------------------------------------------
+# test/datatype/large_data.c:87-174: types over 4 GB -- a contiguous of
+# 20,000,000 floats indexed twice with blocks of 192 at displacements {576, 0}
+# (sparse, 30.72 GB of data over a 61.44 GB span) and {192, 384} (adjacent
+# blocks), a vector of INT_MAX/2 blocks of 4 floats at stride 4 (> 2^31
+# elements), and contiguous(INT_MAX/2, contiguous(4, float)); expected: the
+# bytes the convertor's raw walk covers (count_length_via_convertor_raw
+# :34-85) == the type size.  Here that is mx_ddt_create's own check (the
+# flattened walk's total must equal `size`, else MX_ERR_ARG), plus the span,
+# plus pack / unpack windows at packed offsets above 4 GiB (and across the
+# indexed type's block boundary) compared byte for byte with the user bytes
+# they map to.
+PER_TYPE, PER_PROC = 20_000_000, 192
+CONTIG_BYTES = PER_TYPE * 4                         # ddt = contiguous(20M, MPI_FLOAT)
+INT_MAX = 2 ** 31 - 1
+FLOAT4 = 15
+
+
+def _large_types():
+    blk = PER_PROC * CONTIG_BYTES                   # one indexed block: 192 x 80 MB
+    vcount = INT_MAX // 2
+    return {
+        # ompi_datatype_create_indexed(2, {192,192}, {576,0}, ddt)
+        "1. INDEX": (Desc([(FLOAT4, 1, blk // 4, blk, 576 * CONTIG_BYTES), (FLOAT4, 1, blk // 4, blk, 0)],
+                          2 * blk, 0, (576 + 192) * CONTIG_BYTES),
+                     [(576 * CONTIG_BYTES, blk), (0, blk)]),
+        # {192, 384}: adjacent blocks
+        "2. INDEX": (Desc([(FLOAT4, 1, blk // 4, blk, 192 * CONTIG_BYTES), (FLOAT4, 1, blk // 4, blk, 384 * CONTIG_BYTES)],
+                          2 * blk, 192 * CONTIG_BYTES, 576 * CONTIG_BYTES),
+                     [(192 * CONTIG_BYTES, blk), (384 * CONTIG_BYTES, blk)]),
+        # ompi_datatype_create_vector(INT_MAX/2, 4, 4, MPI_FLOAT)
+        "3. VECTOR": (Desc([(FLOAT4, vcount, 4, 16, 0)], vcount * 16, 0, vcount * 16), [(0, vcount * 16)]),
+        # contiguous(INT_MAX/2, contiguous(4, MPI_FLOAT))
+        "4. CONTIG": (Desc([(FLOAT4, 1, vcount * 4, vcount * 16, 0)], vcount * 16, 0, vcount * 16),
+                      [(0, vcount * 16)]),
+    }
+
+
+def _stream_to_user(blocks, off):
+    """packed offset -> user byte offset (the blocks in packed order)"""
+    for disp, n in blocks:
+        if off < n:
+            return disp + off
+        off -= n
+    raise ValueError(off)
+
+
+def test_large_data_sizes_are_the_reference_formulas():
+    T = _large_types()
+    assert T["1. INDEX"][0].size == 2 * 192 * 20_000_000 * 4 == 30_720_000_000
+    assert T["3. VECTOR"][0].size == (INT_MAX // 2) * 4 * 4 > 2 ** 32
+    for name, (d, blocks) in T.items():
+        assert sum(n for _, n in blocks) == d.size, name       # the raw walk's bytes == the type size
+
+
+@pytest.mark.gpu
+def test_large_data_device():
+    dev = Device(torch)
+    T = _large_types()
+    for name, (d, blocks) in T.items():
+        dt = dev.dt(d)                                          # raw length == size, checked at creation
+        assert dt.size == d.size
+        lo, hi = ctypes.c_int64(), ctypes.c_int64()
+        assert mxompi.lib().mx_ddt_span(dt.h, 1, ctypes.byref(lo), ctypes.byref(hi)) == 0
+        assert (lo.value, hi.value) == (min(b for b, _ in blocks), max(b + n for b, n in blocks)), name
+        dt.close()
+        with pytest.raises(mxompi.MxError):                    # a size the walk does not give is refused
+            mxompi.Datatype(d.bytes, d.nrec, d.size + 4, d.lb, d.ub)
+    # windows above 4 GiB: one user allocation covering the largest span (61.44 GB)
+    span = max(max(b + n for b, n in bl) for _, bl in T.values())
+    U = torch.empty(span, dtype=torch.uint8, device="cuda")
+    gen = torch.Generator(device="cuda").manual_seed(4)
+    W = (1 << 20) + 7
+    cases = [("1. INDEX", (4 << 30) + 12345), ("1. INDEX", T["1. INDEX"][1][0][1] - 1000),   # across blocks
+             ("1. INDEX", (20 << 30) + 3), ("3. VECTOR", (4 << 30) + 5), ("3. VECTOR", T["3. VECTOR"][0].size - W),
+             ("4. CONTIG", (9 << 30) + 1)]
+    for name, off in cases:
+        d, blocks = T[name]
+        dt = dev.dt(d)
+        u0 = [_stream_to_user(blocks, off + k) for k in (0, W - 1)]
+        pieces = []                                             # the user bytes of the window, in stream order
+        k = 0
+        while k < W:
+            ua = _stream_to_user(blocks, off + k)
+            run = W - k
+            for disp, n in blocks:                              # stay inside one block
+                if disp <= ua < disp + n:
+                    run = min(run, disp + n - ua)
+            pieces.append((ua, run))
+            k += run
+        for ua, n in pieces:
+            U[ua:ua + n] = torch.randint(0, 256, (n,), dtype=torch.uint8, device="cuda", generator=gen)
+        exp = torch.cat([U[ua:ua + n] for ua, n in pieces])
+        P = torch.zeros(W, dtype=torch.uint8, device="cuda")
+        dt.pack(1, U.data_ptr(), P.data_ptr(), offset=off, length=W, stream=dev.s)
+        torch.cuda.synchronize()
+        assert torch.equal(P, exp), f"{name} pack window at {off} (user {u0})"
+        # unpack the window back over zeroed user bytes
+        for ua, n in pieces:
+            U[ua:ua + n] = 0
+        dt.unpack(1, U.data_ptr(), P.data_ptr(), offset=off, length=W, stream=dev.s)
+        torch.cuda.synchronize()
+        assert torch.equal(torch.cat([U[ua:ua + n] for ua, n in pieces]), exp), f"{name} unpack window at {off}"
+        dt.close()
+    del U
+    torch.cuda.empty_cache()
