@@ -150,3 +150,75 @@ def test_op_component_compiles_against_reference_op_h(tmp_path):
     assert re.search(r" D mx_op_module_t_class$", syms, re.M)            # OBJ_CLASS_INSTANCE
     assert re.search(r" U ompi_op_base_module_t_class$", syms, re.M)     # parent class from libmpi
     assert re.search(r" U mx_ompi_host_real_register$", syms, re.M)      # the real host table (open fn)
+
+
+# ---------------------------------------------------------------------------
+# mca/mx_ompi_host_real.c: the real-tree host table (round 4)
+# ---------------------------------------------------------------------------
+HOST_REAL = os.path.join(ABI, "mx_ompi_host_real.c")
+
+
+def test_real_host_table_is_blocked_only_by_the_configure_generated_mpi_h(tmp_path):
+    """The table cannot be compiled here, and exactly one header stops it:
+    mpi.h, which configure generates from ompi/include/mpi.h.in (its
+    @OMPI_...@ / #undef substitutions).  The op-side functions need it too:
+    ompi/op/op.h:42 (ompi_op_t, ompi_op_ddt_map) and ompi/datatype/
+    ompi_datatype.h:41 include it.  Writing a stand-in for a configure output
+    is excluded, so the proof is: the first and only error is that header."""
+    mpi_h_in = open(os.path.join(REF, "ompi", "include", "mpi.h.in")).read()
+    assert "@OMPI_BEGIN_CONFIGURE_SECTION@" in mpi_h_in and mpi_h_in.count("#undef") > 30
+    for hdr, line in (("ompi/op/op.h", 42), ("ompi/datatype/ompi_datatype.h", 41)):
+        assert open(os.path.join(REF, hdr)).read().splitlines()[line - 1].strip() == '#include "mpi.h"', hdr
+    cmd = ["gcc", "-std=gnu11", "-fsyntax-only", "-DMX_OMPI_REAL", *[f"-I{i}" for i in REAL_INCS],
+           f"-I{os.path.join(ROOT, 'include')}", f"-I{ABI}", HOST_REAL]
+    r = subprocess.run(cmd, capture_output=True, text=True)
+    assert r.returncode != 0
+    errors = [ln for ln in r.stderr.splitlines() if "error" in ln]
+    assert len(errors) == 1 and "mpi.h: No such file or directory" in errors[0], r.stderr[-2000:]
+
+
+def _ref_headers():
+    out = {}
+    for sub in ("ompi", "opal"):
+        for dp, _, fns in os.walk(os.path.join(REF, sub)):
+            for fn in fns:
+                if fn.endswith(".h"):
+                    p = os.path.join(dp, fn)
+                    out[os.path.relpath(p, REF)] = open(p, errors="replace").read()
+    return out
+
+
+def test_real_host_table_uses_only_internals_the_reference_declares():
+    """Every Open MPI internal the table calls is declared in the reference's
+    headers (a function prototype, a macro, or -- ompi_op_ddt_map -- an
+    extern array), and every struct member it reads exists in the struct the
+    reference defines: the table would compile inside a configured tree
+     up to the signatures the headers give."""
+    src = open(HOST_REAL).read()
+    body = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    hdrs = _ref_headers()
+    alltext = "\n".join(hdrs.values())
+    calls = set(re.findall(r"\b((?:ompi|opal|mca_base)_[A-Za-z0-9_]+)\s*\(", body))
+    macros = set(re.findall(r"\b((?:OBJ|OMPI_REQUEST|OMPI_COMM)_[A-Z_]+)\b", body))
+    assert {"ompi_comm_rank", "ompi_datatype_type_size", "opal_convertor_pack", "mca_base_var_find"} <= calls
+    missing = [f for f in sorted(calls) if not re.search(r"\b" + f + r"\s*\(", alltext)]
+    assert not missing, f"called but not declared by the reference: {missing}"
+    missing = [m for m in sorted(macros) if not re.search(r"(#\s*define\s+" + m + r"\b|\b" + m + r"\b\s*[,=}])",
+                                                           alltext)]
+    assert not missing, f"macros / enumerators not defined by the reference: {missing}"
+    assert re.search(r"OMPI_DECLSPEC\s+extern\s+int\s+ompi_op_ddt_map\s*\[", hdrs["ompi/op/op.h"])   # op.h:246
+    members = {
+        "ompi/op/op.h": ["o_f_to_c_index", "o_flags", "o_func", "o_3buff_intrinsic"],
+        "ompi/datatype/ompi_datatype.h": ["super", "id"],
+        "opal/datatype/opal_datatype.h": ["opt_desc", "desc", "size", "lb", "ub", "used"],
+        "ompi/communicator/communicator.h": ["c_coll"],
+        "ompi/request/request.h": ["req_status", "req_start", "req_free", "req_type", "req_state"],
+        "opal/mca/base/mca_base_var.h": ["mbv_type"],
+    }
+    for hdr, mems in members.items():
+        text = hdrs[hdr]
+        for m in mems:
+            assert re.search(r"[\s\*]" + m + r"\s*(;|\[|:)", text) or re.search(r"\(\s*\*\s*" + m + r"\s*\)", text), \
+                f"{hdr} has no member {m}"
+        for m in mems:
+            assert re.search(r"(->|\.)" + m + r"\b", body), f"{m} listed but unused"
