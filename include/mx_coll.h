@@ -392,9 +392,20 @@ enum { MX_SHMEM_SHORT, MX_SHMEM_INT, MX_SHMEM_LONG, MX_SHMEM_LLONG, MX_SHMEM_INT
 int mx_shmem_to_mpi(int shmem_op, int shmem_type, size_t dt_size, int *mx_op, int *mx_type);
 /* target[i] = reduction over the active set of source[i], i < nreduce
  * (target may equal source).  Runs mx_allreduce with the tuned decision,
- * exactly what scoll/mpi asks of coll/tuned. */
+ * exactly what scoll/mpi asks of coll/tuned (mca_scoll_mpi_reduce,
+ * scoll_mpi_ops.c:212-275); above INT_MAX elements scoll/mpi falls back to
+ * the previous scoll module (:246-259), and so does this call:
+ * mx_shmem_reduce_basic. */
 int mx_shmem_reduce(mx_comm_t *comm, int shmem_op, int shmem_type, size_t dt_size, void *target,
                     const void *source, size_t nreduce, void *stream);
+/* scoll/basic's reduce on the device, its default recursive-doubling order
+ * (oshmem/mca/scoll/basic/scoll_basic_reduce.c:374-542): every PE folds the
+ * partner's value into its own, so for MAX / MIN with NaNs or signed zeros
+ * the PEs' results can differ, as they do in the reference.  FINT2 folds
+ * 2-byte integers (the reference's scoll/basic applies integer4 functions
+ * there and overruns its buffers, oshmem/op/op.c:195; not reproduced). */
+int mx_shmem_reduce_basic(mx_comm_t *comm, int shmem_op, int shmem_type, size_t dt_size, void *target,
+                          const void *source, size_t nreduce, void *stream);
 
 /* ---- device symmetric heap (OpenSHMEM on device memory) ------------------
  * Replaces, for GPU-resident symmetric data, the host-only symmetric heap of

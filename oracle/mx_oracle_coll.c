@@ -1332,3 +1332,50 @@ int mxo_ireduce_scatter(int op, int type, int n, const size_t *rcounts, const vo
     free(copies);
     return 0;
 }
+
+/* ========================================================================
+ * OpenSHMEM scoll/basic reduce, recursive doubling -- the module's default
+ * (mca_scoll_basic_param_reduce_algorithm = SCOLL_ALG_REDUCE_RECURSIVE_
+ * DOUBLING, scoll_basic_component.c:35), restated step by step from
+ * _algorithm_recursive_doubling (scoll_basic_reduce.c:374-542):
+ *   floor2_proc: :392-398;  target_cur = copy of source: :400-405;
+ *   extra PE (my_id >= floor2) puts target_cur into its partner's target
+ *   and waits: :413-440;  partner folds it: :441-465,
+ *     op->o_func.c_fn(target, target_cur, n)  (in = received, out = own);
+ *   pairwise rounds peer = my_id ^ (1 << round) while exit_flag
+ *   (floor2 - 1 >> per round): :467-507, each PE folding the partner's
+ *   target_cur (put into its target) into its own target_cur;
+ *   memcpy(target, target_cur) and the extra gets the same: :509-528.
+ * oshmem's c_fn is *out = calc(*out, *in) (oshmem/op/op.c:165-178), i.e.
+ * ompi_op_reduce(op, source = received, target = own) -- the MPI op's
+ * operand roles -- so red() evaluates it with the op restatement.  Rounds
+ * exchange the values of the previous round (every put precedes its
+ * partner's fold).  sbufs NULL: MPI-style in place (target holds the input).
+ * ======================================================================== */
+int mxo_shmem_basic_reduce(int op, int type, int n, size_t count, const void *const *sbufs, void *const *rbufs)
+{
+    if (n < 1 || n > MAXN) return -1;
+    g_op = op; g_type = type; g_es = mxo_type_size(type);
+    if (!g_es) return -1;
+    if (count == 0) return 0;
+    void *cur[MAXN], *prev[MAXN];
+    int rc = 0;
+    for (int r = 0; r < n; r++) {
+        cur[r] = malloc(count * g_es);
+        prev[r] = malloc(count * g_es);
+        if (!cur[r] || !prev[r]) rc = -3;
+        else cp(cur[r], (sbufs && sbufs[r]) ? sbufs[r] : rbufs[r], count);
+    }
+    if (rc == 0) {
+        int floor2 = 1;
+        for (int i = n >> 1; i; i >>= 1) floor2 <<= 1;
+        for (int r = 0; r + floor2 < n; r++) red(cur[r + floor2], cur[r], count);   /* the extra's source */
+        for (int round = 0, exit_flag = floor2 - 1; exit_flag; exit_flag >>= 1, round++) {
+            for (int r = 0; r < floor2; r++) cp(prev[r], cur[r], count);
+            for (int r = 0; r < floor2; r++) red(prev[r ^ (1 << round)], cur[r], count);
+        }
+        for (int r = 0; r < n; r++) cp(rbufs[r], cur[r < floor2 ? r : r - floor2], count);
+    }
+    for (int r = 0; r < n; r++) { free(cur[r]); free(prev[r]); }
+    return rc;
+}

@@ -283,6 +283,30 @@ def _mp_worker(rank, n, port, staging, jobs, q, env=None):
                 out = torch.zeros(count * 4, dtype=torch.uint8, device="cuda")
                 comm.shmem_reduce("MAX", "FLOAT", 4, out.data_ptr(), x.data_ptr(), count, st)
                 results.append(out.cpu().numpy().tobytes())
+            elif kind == "shmem_basic":
+                # scoll/basic's recursive-doubling shmem_<t>_<op>_to_all (alg = the shmem type)
+                mt = _SHMEM_MPI[alg]
+                es = mxompi.type_size(mt)
+                x = _dev(gen(mt, op, count, 7000 + rank))
+                out = torch.zeros(count * es, dtype=torch.uint8, device="cuda")
+                comm.shmem_reduce_basic(op, alg, es, out.data_ptr(), x.data_ptr(), count, st)
+                results.append(out.cpu().numpy().tobytes())
+            elif kind == "shmem_big":
+                # > INT_MAX elements: scoll/mpi falls back to scoll/basic
+                # (shmem_short_max_to_all; inputs made on the device from
+                # per-rank seeds, the result checked there)
+                def src_of(r):
+                    g = torch.Generator(device="cuda").manual_seed(99 + r)
+                    return torch.randint(-32768, 32768, (count,), dtype=torch.int16, device="cuda", generator=g)
+                x = src_of(rank)
+                out = torch.empty(count, dtype=torch.int16, device="cuda")
+                comm.shmem_reduce("MAX", "SHORT", 2, out.data_ptr(), x.data_ptr(), count, st)
+                exp = src_of(0)
+                for r in range(1, n):
+                    exp = torch.maximum(exp, src_of(r))
+                results.append(int((out != exp).sum().item()))
+                del x, out, exp
+                torch.cuda.empty_cache()
             elif kind == "oshmem_max_example":
                 # examples/oshmem_max_reduction.c:36-46: long src[N] = my_pe + i,
                 # shmem_long_max_to_all(dst, src, N, 0, 0, num_pes, ...) -- through
@@ -692,6 +716,8 @@ def test_multiprocess_allreduce_staged_protocols(n, proto):
 # kept choice).  Every call bit-exact vs the recursive-doubling oracle
 # (coll_base_allreduce.c:130-274); the per-call counters prove each path ran.
 _AR40K = ("allreduce", 40001, "SUM", "FLOAT", "recursive_doubling")
+# shmem type -> the MPI type scoll/mpi maps it to (scoll_mpi_dtypes.h; FINT2 by size)
+_SHMEM_MPI = {"FLOAT": "FLOAT", "DOUBLE": "DOUBLE", "FINT2": "INT16_T", "LONG": "INT64_T"}
 _PATHS = ["one_shot", "pull", "zero_copy", "push"]
 _JOBS_SWITCH = [j for _ in range(2) for p in _PATHS
                 for j in (("path", 0, "SUM", "FLOAT", p), _AR40K, ("stats_reset", 0, "SUM", "FLOAT", "auto"))]
@@ -725,6 +751,47 @@ _JOBS_RECYCLE = [j for op in ("SUM", "MAX", "MIN", "SUM") for j in (
     ("allreduce", 40001, op, "FLOAT", "recursive_doubling"),         # staged PULL: waits PUSHED(2)
     ("reduce", 30001, "SUM", "FLOAT", "auto"),                       # staged VM, root n-1
     ("recreate", 0, "SUM", "FLOAT", "auto"))]
+
+
+_JOBS_SHMEM_BASIC = [("shmem_basic", c, op, _SHMEM_MPI[st], st) for c, op, st in (
+    (3001, "MAX", "FLOAT"), (20011, "SUM", "DOUBLE"), (5003, "MIN", "DOUBLE"), (4099, "SUM", "FINT2"),
+    (3, "MAX", "LONG"), (300001, "SUM", "FLOAT"))]
+
+
+def _check_shmem_basic(n, jobs, got):
+    L = _oracle()
+    L.mxo_shmem_basic_reduce.argtypes = [ci, ci, ci, sz, ctypes.POINTER(vp), ctypes.POINTER(vp)]
+    for j, (kind, count, op, _, st) in enumerate(jobs):
+        if kind != "shmem_basic":
+            continue
+        mt = _SHMEM_MPI[st]
+        es = mxompi.type_size(mt)
+        xs = [gen(mt, op, count, 7000 + r) for r in range(n)]
+        exp = [np.zeros(count * es, np.uint8) for _ in range(n)]
+        assert L.mxo_shmem_basic_reduce(mxompi.OP[op], mxompi.TYPE[mt], n, count, (vp * n)(*[x.ctypes.data for x in xs]),
+                                        (vp * n)(*[e.ctypes.data for e in exp])) == 0
+        for r in range(n):
+            golden_io.assert_coll_equal(np.frombuffer(got[r][j], np.uint8), exp[r], mxompi.OP[op], mxompi.TYPE[mt],
+                                        f"shmem_basic {st} {op} n={n} PE {r}")
+
+
+@pytest.mark.parametrize("n", [2, 3, 5, 8])
+def test_shmem_reduce_scoll_basic_order(n):
+    """scoll/basic's recursive doubling (scoll_basic_reduce.c:374-542) on the
+    device, every PE's result bit-exact vs the oracle's step-by-step
+    restatement -- including MAX / MIN with NaNs and signed zeros, where the
+    two PEs of a pair keep different values (each is the target of its own
+    fold), non-powers of two (extras), FINT2 as 2-byte integers, and a
+    zero-copy size."""
+    _check_shmem_basic(n, _JOBS_SHMEM_BASIC, _run_mp(n, _JOBS_SHMEM_BASIC, staging=16 << 20))
+
+
+def test_shmem_reduce_above_int_max_falls_back_to_scoll_basic():
+    """2^31 + 5 shorts per PE (> INT_MAX elements, 4 GiB): mca_scoll_mpi_reduce
+    hands such a count to scoll/basic (scoll_mpi_ops.c:246-259); the call
+    completes and every element is the maximum over the PEs."""
+    got = _run_mp(2, [("shmem_big", 2 ** 31 + 5, "MAX", "INT16_T", "auto")], staging=512 << 20)
+    assert got[0][0] == 0 and got[1][0] == 0, got
 
 
 @pytest.mark.parametrize("n", [2, 3, 8])

@@ -54,3 +54,41 @@ def test_fortran_types_and_real16():
     assert _map("OR", "FINT2", 2)[2] == mxompi.TYPE["INT16_T"]     # by size (default branch)
     rc, mo, mt = _map("SUM", "FREAL16", 16)
     assert mt == mxompi.TYPE["REAL16"] and not mxompi.op_supported(mo, mt)
+
+
+# ---- scoll/basic recursive doubling (round 4): the oracle restatement -------------
+def _basic(op, t, n, xs):
+    import ctypes
+    import numpy as np
+    import oracle_lib
+    vp, sz, ci = ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int
+    L = oracle_lib.oracle()
+    L.mxo_shmem_basic_reduce.argtypes = [ci, ci, ci, sz, ctypes.POINTER(vp), ctypes.POINTER(vp)]
+    outs = [np.zeros_like(xs[0]) for _ in range(n)]
+    assert L.mxo_shmem_basic_reduce(mxompi.OP[op], mxompi.TYPE[t], n, len(xs[0]),
+                                    (vp * n)(*[x.ctypes.data for x in xs]),
+                                    (vp * n)(*[o.ctypes.data for o in outs])) == 0
+    return outs
+
+
+@pytest.mark.parametrize("n", range(1, 17))
+def test_scoll_basic_oracle_gives_the_examples_answer(n):
+    """examples/oshmem_max_reduction.c:36-46 (N = 3): src[i] = my_pe + i,
+    shmem_long_max_to_all -> dst[i] = npes - 1 + i on every PE, for every PE
+    count (extras when n is not a power of two)."""
+    import numpy as np
+    outs = _basic("MAX", "INT64_T", n, [np.array([r + i for i in range(3)], np.int64) for r in range(n)])
+    for o in outs:
+        assert o.tolist() == [n - 1 + i for i in range(3)]
+
+
+def test_scoll_basic_oracle_keeps_each_pes_own_operand_roles():
+    """Each PE folds the partner's value into its own (c_fn(in = received,
+    out = own), scoll_basic_reduce.c:502-504): with MAX = (own > received ?
+    own : received) a NaN on one side of a pair stays with that side only,
+    so the two PEs of a pair end with different values (n = 2: PE 0 holds
+    NaN, PE 1 holds 1.0 -> PE 0: NaN > 1 false -> 1.0; PE 1: 1 > NaN false ->
+    NaN)."""
+    import numpy as np
+    outs = _basic("MAX", "DOUBLE", 2, [np.array([np.nan]), np.array([1.0])])
+    assert outs[0][0] == 1.0 and np.isnan(outs[1][0])

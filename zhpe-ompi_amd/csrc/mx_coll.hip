@@ -39,6 +39,7 @@
 #include <string.h>
 #include <vector>
 #include <algorithm>
+#include <climits>
 #include <chrono>
 #include <map>
 #include <mutex>
@@ -2632,6 +2633,35 @@ static int vm_setup(int op, int type, vm_launch_fn *vl, size_t *es) {
   return *es ? MX_SUCCESS : MX_ERR_ARG;
 }
 
+// OpenSHMEM scoll/basic reduce, its default algorithm (recursive doubling,
+// mca_scoll_basic_param_reduce_algorithm, scoll_basic_component.c:35;
+// _algorithm_recursive_doubling, scoll_basic_reduce.c:374-542): floor2 = the
+// largest power of two <= n; PE r + floor2 (an "extra") puts its source to
+// PE r, which folds it first; then floor2 - 1 pairwise rounds, PE r with
+// r ^ (1 << round), each PE folding the partner's current value into its
+// own; every PE keeps its own result and hands it to its extra.  Every fold
+// is op->o_func.c_fn(in = received, out = target_cur) = *out = calc(*out,
+// *in) (oshmem/op/op.c:165-178): COMB(target = own, source = received),
+// the MPI op functions' operand roles, so the op kernels evaluate it.  For
+// MAX / MIN with NaNs or signed zeros the two PEs of a pair can end with
+// different values (each is the target of its own fold), so every PE gets
+// its own tree.
+static int shmem_basic_rd_dag(Dag &g) {
+  const int n = g.n;
+  int floor2 = 1;
+  for (int i = n >> 1; i; i >>= 1) floor2 <<= 1;
+  std::vector<int> cur(n);
+  for (int r = 0; r < n; r++) cur[r] = r;
+  for (int r = 0; r + floor2 < n; r++) cur[r] = g.comb(cur[r], r + floor2);
+  for (int round = 0, exit_flag = floor2 - 1; exit_flag; exit_flag >>= 1, round++) {
+    std::vector<int> next(cur);
+    for (int r = 0; r < floor2; r++) next[r] = g.comb(cur[r], cur[r ^ (1 << round)]);
+    cur.swap(next);
+  }
+  for (int r = 0; r < n; r++) g.emit(cur[r < floor2 ? r : r - floor2], r);
+  return MX_SUCCESS;
+}
+
 static uint32_t dest_mask_of(const Dag &g, int owner_rank) {
   uint32_t m = 0;
   for (const auto &o : g.out) m |= 1u << (o.dst < 0 ? owner_rank : o.dst);
@@ -3505,6 +3535,47 @@ extern "C" int mx_shmem_to_mpi(int sop, int st, size_t dt_size, int *mx_op, int 
   return MX_SUCCESS;
 }
 
+// scoll/basic's reduce (recursive doubling, shmem_basic_rd_dag above) on the
+// device: what mca_scoll_mpi_reduce runs instead of the allreduce when the
+// element count exceeds INT_MAX (scoll_mpi_ops.c:246-259).  The reference's
+// scoll/basic folds through oshmem's own op table, whose FINT2 AND / XOR /
+// MAX / MIN / SUM functions are instantiated on ompi_fortran_integer4_t
+// while the op object's dt_size is sizeof(integer2) (oshmem/op/op.c:195,
+// 221, 237, 258, 281 vs :342-423): count = nlong / 2 four-byte elements,
+// twice the bytes of the buffers -- an overrun of the caller's target and of
+// scoll/basic's malloc(nlong) scratch.  That is not reproduced: FINT2 folds
+// 2-byte integers here, as scoll/mpi's mapping gives (scoll_mpi_dtypes.h,
+// FINT2 by size -> MPI_INT16_T).
+extern "C" int mx_shmem_reduce_basic(mx_comm_t *c, int sop, int st, size_t dt_size, void *target, const void *source,
+                                     size_t nreduce, void *stream) {
+  int op, type;
+  int rc = mx_shmem_to_mpi(sop, st, dt_size, &op, &type);
+  if (rc) return rc;
+  if (!c || !target) return MX_ERR_ARG;
+  vm_launch_fn vl;
+  size_t es;
+  if ((rc = vm_setup(op, type, &vl, &es))) return rc;
+  hipStream_t s = (hipStream_t)stream;
+  if ((rc = order(c, s))) return rc;
+  if (nreduce == 0) return MX_SUCCESS;
+  if (c->local) {
+    if (c->size != 1) return MX_ERR_STATE;
+    if ((rc = copy_async(target, source, nreduce * es, s))) return rc;
+    return finish(c, s);
+  }
+  if (c->size == 1) {
+    if ((rc = copy_async(target, source, nreduce * es, s))) return rc;
+    return finish(c, s);
+  }
+  if (!(c->flags & MX_COMM_IPC)) return MX_ERR_STATE;
+  Dag g(c->size);
+  if ((rc = shmem_basic_rd_dag(g))) return rc;
+  VmProg p;
+  if ((rc = dag_compile(g, c->rank, p))) return rc;
+  return vm_partitioned(c, vl, p, (const char *)source, (char *)target, nreduce, es, dest_mask_of(g, c->rank), -1,
+                        0, s);
+}
+
 extern "C" int mx_shmem_reduce(mx_comm_t *c, int sop, int st, size_t dt_size, void *target, const void *source,
                                size_t nreduce, void *stream) {
   int op, type;
@@ -3512,6 +3583,10 @@ extern "C" int mx_shmem_reduce(mx_comm_t *c, int sop, int st, size_t dt_size, vo
   if (rc) return rc;
   if (!mx_op_supported(op, type, MX_TABLE_WITH_FORTRAN)) return MX_ERR_UNSUPPORTED;
   if (nreduce == 0) return MX_SUCCESS;
+  // scoll/mpi casts the count to int for coll_allreduce and falls back to
+  // the previous scoll module above INT_MAX (scoll_mpi_ops.c:246-259)
+  if (nreduce > (size_t)INT_MAX)
+    return mx_shmem_reduce_basic(c, sop, st, dt_size, target, source, nreduce, stream);
   return mx_allreduce(c, source == target ? MX_IN_PLACE : source, target, nreduce, type, op, MX_ALLREDUCE_AUTO,
                       stream);
 }

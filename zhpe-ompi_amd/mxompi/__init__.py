@@ -239,6 +239,7 @@ def _coll_lib():
         L.mx_allreduce_decision.argtypes = [i, sz, i]
         L.mx_comm_set_profiling.argtypes = [vp, i]
         L.mx_shmem_reduce.argtypes = [vp, i, i, sz, vp, vp, sz, vp]
+        L.mx_shmem_reduce_basic.argtypes = [vp, i, i, sz, vp, vp, sz, vp]
         L.mx_comm_get_stats.argtypes = [vp, ctypes.POINTER(CollStats), i]
         L.mx_reduce_scatter_decision.argtypes = [i, sz, i]
         L.mx_reduce_decision.argtypes = [i, sz, i]
@@ -484,6 +485,11 @@ class Comm:
                "FCOMPLEX", "DCOMPLEX", "FINT2", "FINT4", "FINT8", "FREAL4", "FREAL8", "FREAL16"]
         check(_coll_lib().mx_shmem_reduce(self.h, sops.index(op), sts.index(t), dt_size, target, source, nreduce,
                                           stream or None), "mx_shmem_reduce")
+
+    def shmem_reduce_basic(self, op, t, dt_size, target, source, nreduce, stream=0):
+        """scoll/basic's recursive-doubling shmem_<t>_<op>_to_all (mx_shmem_reduce_basic)."""
+        check(_coll_lib().mx_shmem_reduce_basic(self.h, SHMEM_OPS.index(op), SHMEM_TYPES.index(t), dt_size, target,
+                                                source, nreduce, stream or None), "mx_shmem_reduce_basic")
 
     def bcast(self, buf, nbytes, root, stream=0):
         check(_coll_lib().mx_bcast(self.h, buf, nbytes, root, stream or None), "mx_bcast")
