@@ -830,6 +830,14 @@ __device__ __forceinline__ void piece_store(char *u, int lg, uint32_t v0, uint32
   }
 }
 
+// PIPE: the packed range of the workgroup's next tile is loaded into
+// registers (kPieceStage / 16 / kCB 16-byte vectors per lane) while the
+// lanes store the current tile from LDS.  Measured slower (round 4,
+// interleaved A/B at 1 GiB, profiles/r04/unpack_pipe_ab.txt: BLACS 1540 ->
+// 1577 us, struct 949 -> 1071 us): the unpack is bound by its partial-line
+// stores, and loads kept in flight beside them only compete (64 more VGPRs
+// per lane, fewer waves); so it is off (MX_CONV_UNPACK_PIPE=1 turns it on).
+template <bool PIPE>
 __global__ void __launch_bounds__(kCB) k_unpack_piece(PieceArgs a) {
   extern __shared__ __align__(16) char smem[];
   char *stage = smem;                                        // kPieceStage + 48
@@ -838,27 +846,25 @@ __global__ void __launch_bounds__(kCB) k_unpack_piece(PieceArgs a) {
   if (a.tbl_lds) {
     for (uint32_t i = threadIdx.x; i < a.npi; i += kCB) stbl[i] = a.pieces[i];
     tbl = stbl;
+    __syncthreads();
   }
   const uint64_t wend = a.offset + a.len;
-  for (uint64_t t = blockIdx.x; t < a.ntiles; t += gridDim.x) {
+  // stream range of tile t: first byte of piece Pa .. last byte of Pb - 1,
+  // as 16-byte aligned addresses of the packed buffer
+  auto range = [&](uint64_t t, uintptr_t &lo, uintptr_t &hi) {
     const uint64_t Pa = a.P0 + t * a.K;
     const uint64_t Pb = Pa + a.K < a.P1 ? Pa + a.K : a.P1;
-    __syncthreads();                                          // table staged / previous tile consumed
-    // stream range of the tile: first byte of piece Pa .. last byte of Pb - 1
     const uint64_t ia = udiv(Pa, a.mnpi), ib = udiv(Pb - 1, a.mnpi);
     const DPiece fa = tbl[Pa - ia * a.npi], fb = tbl[Pb - 1 - ib * a.npi];
     uint64_t sa = ia * a.S + fa.soff, sb = ib * a.S + fb.soff + (1u << fb.lg);
     sa = sa < a.offset ? a.offset : sa;
     sb = sb < wend ? sb : wend;
-    const uintptr_t lo = (uintptr_t)(a.packed + (sa - a.offset)) & ~(uintptr_t)15;
-    const uintptr_t hi = ((uintptr_t)(a.packed + (sb - a.offset)) + 15) & ~(uintptr_t)15;
-    {
-      const uint4 *g = reinterpret_cast<const uint4 *>(lo);
-      uint4 *d = reinterpret_cast<uint4 *>(stage);
-      const uint32_t nv = (uint32_t)((hi - lo) / 16);
-      for (uint32_t i = threadIdx.x; i < nv; i += kCB) d[i] = g[i];
-    }
-    __syncthreads();
+    lo = (uintptr_t)(a.packed + (sa - a.offset)) & ~(uintptr_t)15;
+    hi = ((uintptr_t)(a.packed + (sb - a.offset)) + 15) & ~(uintptr_t)15;
+  };
+  auto store_tile = [&](uint64_t t, uintptr_t lo) {
+    const uint64_t Pa = a.P0 + t * a.K;
+    const uint64_t Pb = Pa + a.K < a.P1 ? Pa + a.K : a.P1;
     uint64_t P = Pa + threadIdx.x;
     uint64_t inst = udiv(P, a.mnpi);
     uint32_t j = (uint32_t)(P - inst * a.npi);
@@ -881,6 +887,56 @@ __global__ void __launch_bounds__(kCB) k_unpack_piece(PieceArgs a) {
       j += a.dj;
       inst += a.dinst;
       if (j >= a.npi) { j -= a.npi; inst++; }
+    }
+  };
+  if constexpr (!PIPE) {
+    for (uint64_t t = blockIdx.x; t < a.ntiles; t += gridDim.x) {
+      uintptr_t lo, hi;
+      range(t, lo, hi);
+      __syncthreads();                                        // previous tile consumed
+      {
+        const uint4 *g = reinterpret_cast<const uint4 *>(lo);
+        uint4 *d = reinterpret_cast<uint4 *>(stage);
+        const uint32_t nv = (uint32_t)((hi - lo) / 16);
+        for (uint32_t i = threadIdx.x; i < nv; i += kCB) d[i] = g[i];
+      }
+      __syncthreads();
+      store_tile(t, lo);
+    }
+  } else {
+    constexpr int kPre = kPieceStage / 16 / kCB;
+    uint64_t t = blockIdx.x;
+    if (t >= a.ntiles) return;
+    uintptr_t lo, hi;
+    range(t, lo, hi);
+    {
+      const uint4 *g = reinterpret_cast<const uint4 *>(lo);
+      uint4 *d = reinterpret_cast<uint4 *>(stage);
+      const uint32_t nv = (uint32_t)((hi - lo) / 16);
+      for (uint32_t i = threadIdx.x; i < nv; i += kCB) d[i] = g[i];
+    }
+    for (;;) {
+      const uint64_t tn = t + gridDim.x;
+      const bool has_next = tn < a.ntiles;
+      uintptr_t nlo = 0, nhi = 0;
+      if (has_next) range(tn, nlo, nhi);
+      uint4 pre[kPre];
+      const uint32_t nvn = (uint32_t)((nhi - nlo) / 16);
+#pragma unroll
+      for (int k = 0; k < kPre; k++)
+        if (threadIdx.x + k * kCB < nvn) pre[k] = reinterpret_cast<const uint4 *>(nlo)[threadIdx.x + k * kCB];
+      __syncthreads();                                        // tile t staged
+      store_tile(t, lo);
+      if (!has_next) break;
+      __syncthreads();                                        // tile t consumed
+      {
+        uint4 *d = reinterpret_cast<uint4 *>(stage);
+#pragma unroll
+        for (int k = 0; k < kPre; k++)
+          if (threadIdx.x + k * kCB < nvn) d[threadIdx.x + k * kCB] = pre[k];
+      }
+      t = tn;
+      lo = nlo;
     }
   }
 }
@@ -2169,6 +2225,17 @@ static bool conv_bmap_pipe() {
   return on != 0;
 }
 
+// MX_CONV_UNPACK_PIPE=1 runs the piece UNPACK kernel with the register
+// prefetch of the next tile's packed range (A/B switch, off: measured
+// slower; results are identical).
+static bool conv_unpack_pipe() {
+  static const int on = [] {
+    const char *e = getenv("MX_CONV_UNPACK_PIPE");
+    return (e && *e == '1') ? 1 : 0;
+  }();
+  return on != 0;
+}
+
 // MX_CONV_VEC_SPAN=0 packs periodic small-block vectors through the VEC
 // kernel instead of k_pack_vec_span (A/B switch; results are identical).
 static bool conv_vec_span() {
@@ -2394,7 +2461,8 @@ static int convert(const mx_ddt_t *d, size_t count, char *user, char *packed, si
         const uint64_t grid = std::min<uint64_t>(p.ntiles, (uint64_t)g_num_cus * per_cu);
         dm->last_path.store(5, std::memory_order_relaxed);
         if (PACK) hipLaunchKernelGGL(k_pack_piece, dim3((unsigned)grid), dim3(kCB), lds, s, p);
-        else hipLaunchKernelGGL(k_unpack_piece, dim3((unsigned)grid), dim3(kCB), lds, s, p);
+        else if (conv_unpack_pipe()) hipLaunchKernelGGL(k_unpack_piece<true>, dim3((unsigned)grid), dim3(kCB), lds, s, p);
+        else hipLaunchKernelGGL(k_unpack_piece<false>, dim3((unsigned)grid), dim3(kCB), lds, s, p);
         return mx_check_launch();
       }
     }
