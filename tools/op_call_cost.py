@@ -12,8 +12,9 @@ is read once per process):
   marker   as stream, completion through a marker kernel's mapped word
            (MX_FUSED_MARK=0; the round-2 default)
   fastsync as stream, the reduce kernel's last workgroup raises the word
-           itself (MX_FUSED_MARK=1; measurement only -- not safe for
-           consumers in other processes, off by default)
+           itself (MX_FUSED_MARK=1, MX_OP_SERVICE=0)
+  service  the resident reduce service (MX_OP_SERVICE=1, round 4's
+           default): no launch per call
 
 Prints one JSON line per configuration and size: avg us per call and the
 kernel-only time (HIP events around 200 mx_reduce2 launches) for reference.
@@ -28,9 +29,11 @@ CONFIGS = {"round1": {"MX_PTR_CACHE": "0", "OMPI_MCA_op_mi355x_stream": "0"},
            "cache": {"MX_PTR_CACHE": "1", "OMPI_MCA_op_mi355x_stream": "0"},
            "stream": {"MX_PTR_CACHE": "1", "OMPI_MCA_op_mi355x_stream": "1", "OMPI_MCA_op_mi355x_fast_sync": "0"},
            "marker": {"MX_PTR_CACHE": "1", "OMPI_MCA_op_mi355x_stream": "1", "OMPI_MCA_op_mi355x_fast_sync": "1",
-                      "MX_FUSED_MARK": "0"},
+                      "MX_FUSED_MARK": "0", "MX_OP_SERVICE": "0"},
            "fastsync": {"MX_PTR_CACHE": "1", "OMPI_MCA_op_mi355x_stream": "1", "OMPI_MCA_op_mi355x_fast_sync": "1",
-                        "MX_FUSED_MARK": "1"}}
+                        "MX_FUSED_MARK": "1", "MX_OP_SERVICE": "0"},
+           "service": {"MX_PTR_CACHE": "1", "OMPI_MCA_op_mi355x_stream": "1", "OMPI_MCA_op_mi355x_fast_sync": "1",
+                       "MX_FUSED_MARK": "1", "MX_OP_SERVICE": "1"}}
 SIZES = [4 << 10, 64 << 10, 1 << 20]
 
 

@@ -22,6 +22,9 @@ struct Mark {
 void mark_arm(Mark *m, hipStream_t counter_stream = nullptr, bool need_counter = false);
 // Polls the mark's word (~2 ms), then falls back to hipStreamSynchronize(s).
 int mark_wait(const Mark &m, hipStream_t s);
+// The resident reduce service (mx_service.hip): 1 = served, inout final for
+// every agent; 0 = not served (the caller launches); < 0 = error.
+int svc_reduce2(int op, int type, const void *in, void *inout, size_t count);
 }  // namespace mx
 
 // Lazily performs mx_init(current device) if the caller did not.

@@ -388,6 +388,18 @@ extern "C" int mx_reduce2_sync(int op, int type, const void *in, void *inout, si
   int rc = mx_ensure_init();
   if (rc) return rc;
   hipStream_t s = (hipStream_t)stream;
+  // the resident service (mx_service.hip) when ordering allows: the caller's
+  // stream (the op component's own, blocking) and the legacy default stream
+  // it is implicitly ordered after are idle, so nothing queued before this
+  // call is left for the kernel a launch would have waited behind
+  if (s) {
+    if (hipStreamQuery(nullptr) == hipSuccess && hipStreamQuery(s) == hipSuccess) {
+      rc = svc_reduce2(op, type, in, inout, count);
+      if (rc) return rc < 0 ? rc : MX_SUCCESS;
+    } else {
+      (void)hipGetLastError();
+    }
+  }
   if (!fused_mark() || count > kFusedMarkMax || count * mx_type_size(type) > kFusedMarkMaxBytes) {
     rc = e.f2(in, inout, count, s, Mark{nullptr, nullptr, 0});
     return rc ? rc : mx_stream_sync_fast(stream);

@@ -115,6 +115,7 @@ def lib() -> ctypes.CDLL:
         L.mx_reduce3.argtypes = [i, i, vp, vp, vp, sz, vp]
         L.mx_copy.argtypes = [vp, vp, sz, vp]
         L.mx_shmem_to_mpi.argtypes = [i, i, sz, ctypes.POINTER(i), ctypes.POINTER(i)]
+        L.mx_op_service_stats.argtypes = [ctypes.POINTER(ctypes.c_ulonglong), ctypes.POINTER(ctypes.c_ulonglong)]
         L._mx_typed = True
     return L
 
@@ -165,6 +166,14 @@ def reduce3(op, t, in1_ptr: int, in2_ptr: int, out_ptr: int, count: int, stream:
     """out = in1 OP in2 on the device (asynchronous on `stream`)."""
     check(lib().mx_reduce3(_op(op), _slot(t), in1_ptr, in2_ptr, out_ptr, count, stream or None),
           f"mx_reduce3({op},{t})")
+
+
+def op_service_stats():
+    """(state, commands served, service launches) of the resident reduce
+    service behind mx_reduce2_sync (include/mx_kernels.h)."""
+    a, b = ctypes.c_ulonglong(), ctypes.c_ulonglong()
+    st = lib().mx_op_service_stats(ctypes.byref(a), ctypes.byref(b))
+    return st, a.value, b.value
 
 
 def init(device: int = 0) -> None:
