@@ -213,11 +213,13 @@ int mx_reduce2(int op, int type, const void *in, void *inout,
  * tests/test_op_consumer_gpu.py. */
 int mx_reduce2_sync(int op, int type, const void *in, void *inout,
                     size_t count, void *stream);
-/* mx_reduce2_sync on a non-NULL stream, when that stream and the legacy
- * default stream are idle, hands calls of <= 1 MiB per buffer (16-byte
- * aligned buffers, element types without padding or x87) to a resident
- * service kernel instead of launching (no launch and no dispatch per call;
- * it leaves after 2 ms without calls; MX_OP_SERVICE=0 switches it off).
+/* mx_reduce2_sync on a non-NULL stream hands calls of <= 1 MiB per buffer
+ * (16-byte aligned buffers, element types without padding or x87) to a
+ * resident service kernel instead of launching (no launch and no dispatch
+ * per call; it leaves after 2 ms without calls; MX_OP_SERVICE=0 switches it
+ * off).  A served call is not ordered after work still queued on any
+ * stream: its operands must be complete when it is made (the CUDA-aware MPI
+ * contract for buffers handed to MPI).
  * Commands served and service launches so far; returns 1 when the service
  * is usable, 0 before first use, -1 when off. */
 int mx_op_service_stats(unsigned long long *served, unsigned long long *launches);

@@ -11,7 +11,8 @@
 //   piece_rd  piece + each lane first loads its packed bytes (coalesced
 //             16-byte loads of the 1 GiB packed stream): reads + writes
 // Types: blacs (ref_blacs_indexed: 6 x 52 B every 88 B, then 48..4 B every
-// 92 B, extent 1548, 624 B of data), struct48 (char @0, 28 B @8, extent 48).
+// 92 B, extent 1548, 624 B of data), struct48 (char @0, 28 B @8, extent 48),
+// u4s32 (vector_f32_b4_s8: 16 B every 32 B).
 // Prints the median of 7 timed launches per variant (HIP events).
 #include <hip/hip_runtime.h>
 #include <cstdio>
@@ -92,6 +93,9 @@ int main(int argc, char **argv) {
     for (int k = 0; k < 6; k++) blocks.push_back({(uint32_t)(88 * k), 52});
     for (int k = 0; k < 12; k++) blocks.push_back({(uint32_t)(532 + 92 * k), (uint32_t)(48 - 4 * k)});
     ext = 1548;
+  } else if (!strcmp(type, "u4s32")) {   // vector_f32_b4_s8: 16 B every 32 B
+    blocks.push_back({0, 16});
+    ext = 32;
   } else if (!strcmp(type, "struct48")) {
     blocks.push_back({0, 1});
     blocks.push_back({8, 28});

@@ -388,17 +388,18 @@ extern "C" int mx_reduce2_sync(int op, int type, const void *in, void *inout, si
   int rc = mx_ensure_init();
   if (rc) return rc;
   hipStream_t s = (hipStream_t)stream;
-  // the resident service (mx_service.hip) when ordering allows: the caller's
-  // stream (the op component's own, blocking) and the legacy default stream
-  // it is implicitly ordered after are idle, so nothing queued before this
-  // call is left for the kernel a launch would have waited behind
+  // the resident service (mx_service.hip) for calls on a non-default stream:
+  // a served call is ordered after nothing queued on any stream -- its
+  // operands must be ready when it is made, which is the CUDA-aware MPI
+  // contract (buffers handed to MPI are complete) and what coll/base's
+  // operands are (results of completed receives and earlier reductions);
+  // the launch path (MX_OP_SERVICE=0, or the legacy default stream) keeps
+  // the blocking stream's implicit order after the default stream.  (Asking
+  // the runtime whether both streams are idle costs ~10 us per query on this
+  // runtime, more than the service saves.)
   if (s) {
-    if (hipStreamQuery(nullptr) == hipSuccess && hipStreamQuery(s) == hipSuccess) {
-      rc = svc_reduce2(op, type, in, inout, count);
-      if (rc) return rc < 0 ? rc : MX_SUCCESS;
-    } else {
-      (void)hipGetLastError();
-    }
+    rc = svc_reduce2(op, type, in, inout, count);
+    if (rc) return rc < 0 ? rc : MX_SUCCESS;
   }
   if (!fused_mark() || count > kFusedMarkMax || count * mx_type_size(type) > kFusedMarkMaxBytes) {
     rc = e.f2(in, inout, count, s, Mark{nullptr, nullptr, 0});
