@@ -227,6 +227,12 @@ int mx_op_service_stats(unsigned long long *served, unsigned long long *launches
  * in the reference's 3-buffer functions). */
 int mx_reduce3(int op, int type, const void *in1, const void *in2,
                void *out, size_t count, void *stream);
+/* As mx_reduce3, and returns when `out` is complete for every agent (the
+ * op component's 3-buffer handler, ompi_3buff_op_reduce, op.h:618-660):
+ * the resident service on a non-NULL stream, as mx_reduce2_sync, else the
+ * launch followed by mx_stream_sync_fast's marker kernel. */
+int mx_reduce3_sync(int op, int type, const void *in1, const void *in2,
+                    void *out, size_t count, void *stream);
 
 /* Contiguous device copy (K7), asynchronous on stream. */
 int mx_copy(void *dst, const void *src, size_t bytes, void *stream);

@@ -101,3 +101,33 @@ def test_service_back_to_back_same_buffers():
             assert int(b[n - 1].item()) == i + 1 and int(b[0].item()) == i + 1
     assert torch.all(b == 500).item()
     assert mxompi.op_service_stats()[1] - served0 == 500
+
+
+def test_service_three_buffer_form():
+    """mx_reduce3_sync (the op component's 3-buffer handler): out = in1 OP in2
+    through the service (aligned, <= 1 MiB) and through the launch (misaligned),
+    bit-exact vs the oracle's 3-buffer functions, out read straight after."""
+    mxompi.init(0)
+    s = torch.cuda.Stream()
+    O = oracle_lib.oracle()
+    served0 = mxompi.op_service_stats()[1]
+    served_calls = 0
+    for op, t in PAIRS:
+        es = mxompi.type_size(t)
+        for count, off in ((1000, 0), ((256 << 10) // es + 1, 0), (3001, 4)):
+            a, b = _gen(op, t, count, 5 + count), _gen(op, t, count, 6 + count)
+            A = torch.zeros(count * es + 16, dtype=torch.uint8, device="cuda")
+            B = torch.zeros(count * es + 16, dtype=torch.uint8, device="cuda")
+            C = torch.full((count * es + 16,), 0x5A, dtype=torch.uint8, device="cuda")
+            A[off:off + count * es] = torch.from_numpy(a).cuda()
+            B[off:off + count * es] = torch.from_numpy(b).cuda()
+            torch.cuda.synchronize()
+            mxompi.reduce3_sync(op, t, A.data_ptr() + off, B.data_ptr() + off, C.data_ptr() + off, count,
+                                s.cuda_stream)
+            got = C[off:off + count * es].cpu().numpy()
+            exp = np.zeros(count * es, np.uint8)
+            assert O.mxo_reduce3(mxompi.OP[op], mxompi.TYPE[t], a.ctypes.data, b.ctypes.data, exp.ctypes.data,
+                                 count, 1) == 0
+            golden_io.assert_op_equal(got, exp, mxompi.OP[op], mxompi.TYPE[t], f"3-buffer {op} {t} {count}+{off}")
+            served_calls += off == 0                      # aligned: the service; misaligned: a launch
+    assert mxompi.op_service_stats()[1] - served0 == served_calls

@@ -23,8 +23,9 @@ void mark_arm(Mark *m, hipStream_t counter_stream = nullptr, bool need_counter =
 // Polls the mark's word (~2 ms), then falls back to hipStreamSynchronize(s).
 int mark_wait(const Mark &m, hipStream_t s);
 // The resident reduce service (mx_service.hip): 1 = served, inout final for
-// every agent; 0 = not served (the caller launches); < 0 = error.
-int svc_reduce2(int op, int type, const void *in, void *inout, size_t count);
+// every agent; 0 = not served (the caller launches); < 0 = error.  in2:
+// nullptr for the 2-buffer form (inout = inout OP in), else inout = in OP in2.
+int svc_reduce(int op, int type, const void *in, const void *in2, void *inout, size_t count);
 }  // namespace mx
 
 // Lazily performs mx_init(current device) if the caller did not.

@@ -398,7 +398,7 @@ extern "C" int mx_reduce2_sync(int op, int type, const void *in, void *inout, si
   // the runtime whether both streams are idle costs ~10 us per query on this
   // runtime, more than the service saves.)
   if (s) {
-    rc = svc_reduce2(op, type, in, inout, count);
+    rc = svc_reduce(op, type, in, nullptr, inout, count);
     if (rc) return rc < 0 ? rc : MX_SUCCESS;
   }
   if (!fused_mark() || count > kFusedMarkMax || count * mx_type_size(type) > kFusedMarkMaxBytes) {
@@ -413,6 +413,27 @@ extern "C" int mx_reduce2_sync(int op, int type, const void *in, void *inout, si
   }
   rc = e.f2(in, inout, count, s, mk);
   return rc ? rc : mark_wait(mk, s);
+}
+
+// As mx_reduce3, returning with `out` complete for every agent: the op
+// component's 3-buffer handler (ompi_3buff_op_reduce, op.h:618-660).  The
+// resident service on a non-default stream (as mx_reduce2_sync), else the
+// launch and the marker kernel.
+extern "C" int mx_reduce3_sync(int op, int type, const void *in1, const void *in2, void *out, size_t count,
+                               void *stream) {
+  if (op < 0 || op >= MX_OP_COUNT || type < 0 || type >= MX_TYPE_COUNT) return MX_ERR_ARG;
+  entry e = lookup(op, type);
+  if (!e.f3) return MX_ERR_UNSUPPORTED;
+  if (count == 0) return MX_SUCCESS;
+  if (!in1 || !in2 || !out || count > kMaxItems) return MX_ERR_ARG;
+  int rc = mx_ensure_init();
+  if (rc) return rc;
+  if (stream) {
+    rc = svc_reduce(op, type, in1, in2, out, count);
+    if (rc) return rc < 0 ? rc : MX_SUCCESS;
+  }
+  rc = e.f3(in1, in2, out, count, (hipStream_t)stream);
+  return rc ? rc : mx_stream_sync_fast(stream);
 }
 
 extern "C" int mx_reduce3(int op, int type, const void *in1, const void *in2, void *out, size_t count,

@@ -56,6 +56,7 @@ struct alignas(64) SvcCmd {                // coherent mapped host memory, writt
   uint64_t seq;
   uint64_t in, inout, count;
   uint64_t exit;
+  uint64_t in2;                            // 3-buffer commands: inout = in OP in2; 0: inout = inout OP in
 };
 struct alignas(64) SvcHost {               // mapped host memory, written by the kernel
   uint64_t done;                           // last command completed
@@ -63,7 +64,7 @@ struct alignas(64) SvcHost {               // mapped host memory, written by the
 };
 struct SvcDev {                            // device (uncached): workgroup 0 -> the others
   uint64_t tag;                            // (launch epoch << 32) | broadcast number of this launch
-  uint64_t in, inout, count, exit, q;      // the command (q: its host sequence number)
+  uint64_t in, inout, count, exit, q, in2; // the command (q: its host sequence number)
   uint64_t done_tag;                       // (epoch << 32) | last broadcast every workgroup finished
   unsigned ctr;                            // workgroups done with the current broadcast
 };
@@ -77,10 +78,10 @@ __device__ __forceinline__ uint64_t svc_ld(const uint64_t *p) {
 // matches.  Workgroup 0 starts its idle clock only once every workgroup has
 // finished the last broadcast (done_tag), so a workgroup that became resident
 // late never misses a command.
-template <class T, class OP>
+template <class T, class OP, class OP3>
 __global__ void __launch_bounds__(kSvcB) k_svc(const SvcCmd *cmd, SvcHost *host, SvcDev *dev, uint64_t last,
                                                uint64_t epoch, uint64_t idle_ticks) {
-  __shared__ uint64_t s_in, s_inout, s_count, s_exit, s_q;
+  __shared__ uint64_t s_in, s_inout, s_count, s_exit, s_q, s_in2;
   uint64_t seen = last;                    // host command sequence number taken last
   uint32_t k = 0;                          // broadcasts of this launch
   if (blockIdx.x == 0 && threadIdx.x == 0)
@@ -107,6 +108,7 @@ __global__ void __launch_bounds__(kSvcB) k_svc(const SvcCmd *cmd, SvcHost *host,
           s_inout = svc_ld(&cmd->inout);
           s_count = svc_ld(&cmd->count);
           s_exit = svc_ld(&cmd->exit);
+          s_in2 = svc_ld(&cmd->in2);
           s_q = q;
           seen = q;
         }
@@ -115,6 +117,7 @@ __global__ void __launch_bounds__(kSvcB) k_svc(const SvcCmd *cmd, SvcHost *host,
         dev->count = s_count;
         dev->exit = s_exit;
         dev->q = s_q;
+        dev->in2 = s_in2;
         __hip_atomic_store(&dev->tag, (epoch << 32) | k, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
       } else {
         const uint64_t want = (epoch << 32) | k;
@@ -125,6 +128,7 @@ __global__ void __launch_bounds__(kSvcB) k_svc(const SvcCmd *cmd, SvcHost *host,
         s_count = dev->count;
         s_exit = dev->exit;
         s_q = dev->q;
+        s_in2 = dev->in2;
       }
     }
     __syncthreads();
@@ -133,21 +137,36 @@ __global__ void __launch_bounds__(kSvcB) k_svc(const SvcCmd *cmd, SvcHost *host,
     const T *a = reinterpret_cast<const T *>(s_in);
     T *b = reinterpret_cast<T *>(s_inout);
     const size_t n = s_count;
-    OP op;
     constexpr size_t N = 16 / sizeof(T);
     struct alignas(16) V { T e[N]; };
     const size_t nvec = n / N;
     const size_t stride = (size_t)gridDim.x * kSvcB;
-    for (size_t i = (size_t)blockIdx.x * kSvcB + threadIdx.x; i < nvec; i += stride) {
-      V x, y;
-      ld16<false>(x, reinterpret_cast<const V *>(b) + i);
-      ld16<false>(y, reinterpret_cast<const V *>(a) + i);
+    if (!s_in2) {                          // 2-buffer: inout = inout OP in (the op kernels' K1)
+      OP op;
+      for (size_t i = (size_t)blockIdx.x * kSvcB + threadIdx.x; i < nvec; i += stride) {
+        V x, y;
+        ld16<false>(x, reinterpret_cast<const V *>(b) + i);
+        ld16<false>(y, reinterpret_cast<const V *>(a) + i);
 #pragma unroll
-      for (size_t j = 0; j < N; j++) store_fields(&x.e[j], op(x.e[j], y.e[j]));
-      st16<false>(reinterpret_cast<V *>(b) + i, x);
+        for (size_t j = 0; j < N; j++) store_fields(&x.e[j], op(x.e[j], y.e[j]));
+        st16<false>(reinterpret_cast<V *>(b) + i, x);
+      }
+      for (size_t i = nvec * N + (size_t)blockIdx.x * kSvcB + threadIdx.x; i < n; i += stride)
+        store_fields(&b[i], op(b[i], a[i]));
+    } else {                               // 3-buffer: out = in1 OP in2 (K2)
+      OP3 op;
+      const T *a2 = reinterpret_cast<const T *>(s_in2);
+      for (size_t i = (size_t)blockIdx.x * kSvcB + threadIdx.x; i < nvec; i += stride) {
+        V x, y;
+        ld16<false>(x, reinterpret_cast<const V *>(a) + i);
+        ld16<false>(y, reinterpret_cast<const V *>(a2) + i);
+#pragma unroll
+        for (size_t j = 0; j < N; j++) x.e[j] = op(x.e[j], y.e[j]);
+        st16<false>(reinterpret_cast<V *>(b) + i, x);
+      }
+      for (size_t i = nvec * N + (size_t)blockIdx.x * kSvcB + threadIdx.x; i < n; i += stride)
+        b[i] = op(a[i], a2[i]);
     }
-    for (size_t i = nvec * N + (size_t)blockIdx.x * kSvcB + threadIdx.x; i < n; i += stride)
-      store_fields(&b[i], op(b[i], a[i]));
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this wave's stores reached L2
     __syncthreads();
     if (threadIdx.x == 0) {
@@ -165,17 +184,17 @@ __global__ void __launch_bounds__(kSvcB) k_svc(const SvcCmd *cmd, SvcHost *host,
 
 typedef void (*svc_launch_fn)(const SvcCmd *, SvcHost *, SvcDev *, uint64_t, uint64_t, uint64_t, hipStream_t);
 
-template <class T, class OP>
+template <class T, class OP, class OP3>
 static void svc_launch(const SvcCmd *c, SvcHost *h, SvcDev *d, uint64_t last, uint64_t epoch, uint64_t idle,
                        hipStream_t s) {
-  hipLaunchKernelGGL((k_svc<T, OP>), dim3(kSvcWG), dim3(kSvcB), 0, s, c, h, d, last, epoch, idle);
+  hipLaunchKernelGGL((k_svc<T, OP, OP3>), dim3(kSvcWG), dim3(kSvcB), 0, s, c, h, d, last, epoch, idle);
 }
 
 // pairs served: element types that tile 16-byte vectors with no bytes
 // outside their value fields (no x87, no padded pair types)
 struct SvcVisitor {
   template <class T, class OP2, class OP3> svc_launch_fn go() {
-    if constexpr (sizeof(T) <= 16 && 16 % sizeof(T) == 0 && !has_pad<T>::value) return &svc_launch<T, OP2>;
+    if constexpr (sizeof(T) <= 16 && 16 % sizeof(T) == 0 && !has_pad<T>::value) return &svc_launch<T, OP2, OP3>;
     else return nullptr;
   }
   svc_launch_fn none() { return nullptr; }
@@ -272,11 +291,12 @@ bool svc_poll(const uint64_t *w, uint64_t target, double us) {
 }
 }  // namespace
 
-// 1: served (inout final); 0: not served (the caller launches); < 0 error
-int svc_reduce2(int op, int type, const void *in, void *inout, size_t count) {
+// 1: served (inout final); 0: not served (the caller launches); < 0 error.
+// in2 != nullptr: the 3-buffer form, inout = in OP in2.
+int svc_reduce(int op, int type, const void *in, const void *in2, void *inout, size_t count) {
   if (!svc_enabled()) return 0;
   const size_t es = mx_type_size(type);
-  if (!es || count * es > kSvcMaxBytes || (((uintptr_t)in | (uintptr_t)inout) & 15)) return 0;
+  if (!es || count * es > kSvcMaxBytes || (((uintptr_t)in | (uintptr_t)in2 | (uintptr_t)inout) & 15)) return 0;
   SvcVisitor vis;
   const svc_launch_fn fn = dispatch(op, type, vis);
   if (!fn) return 0;
@@ -305,6 +325,7 @@ int svc_reduce2(int op, int type, const void *in, void *inout, size_t count) {
   v.cmd->in = (uint64_t)(uintptr_t)in;
   v.cmd->inout = (uint64_t)(uintptr_t)inout;
   v.cmd->count = count;
+  v.cmd->in2 = (uint64_t)(uintptr_t)in2;
   v.cmd->exit = 0;
   const uint64_t q = ++v.seq;
   __atomic_store_n(&v.cmd->seq, q, __ATOMIC_RELEASE);

@@ -147,8 +147,12 @@ static void mx_op_3buff(void *in1, void *in2, void *out, int *count, struct ompi
     if (slot < 0) die("datatype lookup", MX_ERR_ARG);
     if (*count > 0 && both_on_device(in1, in2) && mx_is_device_ptr(out) == 1) {
         void *s = op_stream();
-        int rc = mx_reduce3(m->op_index, slot, in1, in2, out, (size_t)*count, s);
-        rc = run_sync(s, rc);
+        int rc;
+        if (g_fast_sync < 0) g_fast_sync = mx_ompi_host->mca_int("op_mi355x_fast_sync", 1) != 0;
+        if (g_fast_sync)   /* the resident service, or the launch + completion word */
+            rc = mx_reduce3_sync(m->op_index, slot, in1, in2, out, (size_t)*count, s);
+        else
+            rc = run_sync(s, mx_reduce3(m->op_index, slot, in1, in2, out, (size_t)*count, s));
         if (rc != MX_SUCCESS) die("mx_reduce3", rc);
         return;
     }

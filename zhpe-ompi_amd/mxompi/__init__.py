@@ -113,6 +113,7 @@ def lib() -> ctypes.CDLL:
         L.mx_reduce2.argtypes = [i, i, vp, vp, sz, vp]
         L.mx_reduce2_sync.argtypes = [i, i, vp, vp, sz, vp]
         L.mx_reduce3.argtypes = [i, i, vp, vp, vp, sz, vp]
+        L.mx_reduce3_sync.argtypes = [i, i, vp, vp, vp, sz, vp]
         L.mx_copy.argtypes = [vp, vp, sz, vp]
         L.mx_shmem_to_mpi.argtypes = [i, i, sz, ctypes.POINTER(i), ctypes.POINTER(i)]
         L.mx_op_service_stats.argtypes = [ctypes.POINTER(ctypes.c_ulonglong), ctypes.POINTER(ctypes.c_ulonglong)]
@@ -166,6 +167,12 @@ def reduce3(op, t, in1_ptr: int, in2_ptr: int, out_ptr: int, count: int, stream:
     """out = in1 OP in2 on the device (asynchronous on `stream`)."""
     check(lib().mx_reduce3(_op(op), _slot(t), in1_ptr, in2_ptr, out_ptr, count, stream or None),
           f"mx_reduce3({op},{t})")
+
+
+def reduce3_sync(op, t, in1_ptr: int, in2_ptr: int, out_ptr: int, count: int, stream: int = 0) -> None:
+    """out = in1 OP in2, returning with `out` complete (mx_reduce3_sync)."""
+    check(lib().mx_reduce3_sync(_op(op), _slot(t), in1_ptr, in2_ptr, out_ptr, count, stream or None),
+          f"mx_reduce3_sync({op},{t})")
 
 
 def op_service_stats():
