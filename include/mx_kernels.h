@@ -213,11 +213,11 @@ int mx_reduce2(int op, int type, const void *in, void *inout,
  * tests/test_op_consumer_gpu.py. */
 int mx_reduce2_sync(int op, int type, const void *in, void *inout,
                     size_t count, void *stream);
-/* mx_reduce2_sync on a non-NULL stream hands calls of <= 1 MiB per buffer
+/* mx_reduce2_sync on a non-NULL stream hands calls of <= 128 KiB per buffer
  * (16-byte aligned buffers, element types without padding or x87) to a
- * resident service kernel instead of launching (no launch and no dispatch
- * per call; it leaves after 2 ms without calls; MX_OP_SERVICE=0 switches it
- * off).  A served call is not ordered after work still queued on any
+ * resident one-workgroup service kernel instead of launching (no launch and
+ * no dispatch per call: 4 KiB 7.4 -> 3.8 us; it
+ * leaves after 2 ms without calls; MX_OP_SERVICE=0 switches it off).  A served call is not ordered after work still queued on any
  * stream: its operands must be complete when it is made (the CUDA-aware MPI
  * contract for buffers handed to MPI).
  * Commands served and service launches so far; returns 1 when the service

@@ -1,10 +1,11 @@
 """The resident reduce service behind mx_reduce2_sync (round 4,
-csrc/mx_service.hip): calls of <= 1 MiB on an idle non-default stream are
-served by a kernel that stays resident instead of a launch per call.
+csrc/mx_service.hip): calls of <= 128 KiB on a non-default stream are
+served by a one-workgroup kernel that stays resident instead of a launch per
+call.
 
 Bit-exact vs the op oracle (op_base_functions.c restated; op values
 parity-unpinned) for every element family the service takes, at
-ragged sizes up to its 1 MiB cap; pairs interleaved (the service is rebound
+ragged sizes up to its 128 KiB cap; pairs interleaved (the service is rebound
 to each pair), pauses longer than its 2 ms idle exit (relaunch), a call over
 the cap and a misaligned call (launch path), and the per-call counters show
 which calls the service took."""
@@ -22,6 +23,7 @@ pytestmark = pytest.mark.gpu
 
 PAIRS = [("SUM", "FLOAT"), ("MAX", "DOUBLE"), ("BXOR", "UINT16_T"), ("MAXLOC", "FLOAT_INT"),
          ("PROD", "C_FLOAT_COMPLEX"), ("LAND", "BOOL"), ("MIN", "INT8_T"), ("SUM", "INT64_T")]
+SVC_MAX = 128 << 10          # kSvcMaxBytes
 
 
 def _gen(op, t, count, seed):
@@ -68,7 +70,7 @@ def test_service_serves_and_matches_the_oracle():
     for rnd in range(2):
         for op, t in PAIRS:
             es = mxompi.type_size(t)
-            for count in (1, 17, 1000, 4099, (64 << 10) // es + 3, (1 << 20) // es):
+            for count in (1, 17, 1000, 4099, (64 << 10) // es + 3, SVC_MAX // es):
                 _check(op, t, count, 100 * rnd + count, s)
                 calls += 1
         time.sleep(0.01)                               # > the 2 ms idle exit: the next call relaunches
@@ -76,8 +78,9 @@ def test_service_serves_and_matches_the_oracle():
     assert st == 1, "service unusable on this box"
     assert served - served0 == calls, (served - served0, calls)
     assert launches - launches0 >= 2 * len(PAIRS)      # rebound to every pair, every round
-    # not served: over the 1 MiB cap, misaligned buffers, the legacy default stream
-    _check("SUM", "FLOAT", (1 << 20) // 4 + 4, 7, s)
+    # not served: over the cap, misaligned buffers
+    _check("SUM", "FLOAT", SVC_MAX // 4 + 4, 7, s)
+    _check("SUM", "FLOAT", (1 << 20) // 4, 9, s)
     _check("SUM", "FLOAT", 5000, 8, s, off=4)
     O = oracle_lib.oracle()
     assert mxompi.op_service_stats()[1] == served
@@ -90,7 +93,7 @@ def test_service_back_to_back_same_buffers():
     (the service's acquire after a command, its release before done)."""
     mxompi.init(0)
     s = torch.cuda.Stream()
-    n = 65536
+    n = 16384              # 128 KiB: the service cap
     a = torch.ones(n, dtype=torch.int64, device="cuda")
     b = torch.zeros(n, dtype=torch.int64, device="cuda")
     torch.cuda.synchronize()
@@ -105,7 +108,8 @@ def test_service_back_to_back_same_buffers():
 
 def test_service_three_buffer_form():
     """mx_reduce3_sync (the op component's 3-buffer handler): out = in1 OP in2
-    through the service (aligned, <= 1 MiB) and through the launch (misaligned),
+    through the service (aligned, <= 128 KiB) and through the launch (misaligned
+    or larger),
     bit-exact vs the oracle's 3-buffer functions, out read straight after."""
     mxompi.init(0)
     s = torch.cuda.Stream()
@@ -114,7 +118,7 @@ def test_service_three_buffer_form():
     served_calls = 0
     for op, t in PAIRS:
         es = mxompi.type_size(t)
-        for count, off in ((1000, 0), ((256 << 10) // es + 1, 0), (3001, 4)):
+        for count, off in ((1000, 0), (SVC_MAX // es, 0), (SVC_MAX // es + 1, 0), (3001, 4)):
             a, b = _gen(op, t, count, 5 + count), _gen(op, t, count, 6 + count)
             A = torch.zeros(count * es + 16, dtype=torch.uint8, device="cuda")
             B = torch.zeros(count * es + 16, dtype=torch.uint8, device="cuda")
@@ -129,5 +133,5 @@ def test_service_three_buffer_form():
             assert O.mxo_reduce3(mxompi.OP[op], mxompi.TYPE[t], a.ctypes.data, b.ctypes.data, exp.ctypes.data,
                                  count, 1) == 0
             golden_io.assert_op_equal(got, exp, mxompi.OP[op], mxompi.TYPE[t], f"3-buffer {op} {t} {count}+{off}")
-            served_calls += off == 0                      # aligned: the service; misaligned: a launch
+            served_calls += off == 0 and count * es <= SVC_MAX   # else a launch
     assert mxompi.op_service_stats()[1] - served0 == served_calls

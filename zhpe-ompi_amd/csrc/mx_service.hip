@@ -1,43 +1,44 @@
 // mx_service.hip -- a resident reduce service for the op component's
 // synchronous calls (ompi_op_reduce on device buffers, ompi/op/op.h:547-610,
-// op/mi355x's 2-buffer handler; round 4).
+// op/mi355x's 2- and 3-buffer handlers; round 4).
 //
-// A blocking ompi_op_reduce of a few KiB costs ~7.5 us with a launch per
+// A blocking ompi_op_reduce of a few KiB costs ~7.3 us with a launch per
 // call (profiles/r04/op_call_cost_r4_fused_default.txt): the host's launch,
 // the packet processor's dispatch and the wake-up, not the ~0.5 us of work.
-// The service removes the launch and the dispatch: one kernel of kSvcWG
-// workgroups stays resident on a stream of its own (highest priority, whose
-// hardware queues the process's ordinary streams do not share)
-// and serves commands the host writes into coherent mapped host memory:
+// The service removes the launch and the dispatch: one workgroup stays
+// resident on a stream of its own (highest priority, whose hardware queues
+// the process's ordinary streams do not share) and serves the
+// calls of up to kSvcMaxBytes that the host writes into coherent mapped host
+// memory:
 //   * the host fills the command (operands, count) and raises its sequence
-//     number (a release store); workgroup 0 polls that word over PCIe,
-//     copies the command into device memory and raises a device word that
-//     the other workgroups poll (L2, not PCIe);
-//   * every workgroup takes a system-scope acquire (its XCD's L2 drops stale
-//     lines of the operands: the service never passes a kernel boundary),
-//     reduces its grid-stride share with the op kernels' element functors,
-//     waits for its stores, releases at system scope and counts itself done;
-//     the last one raises the done word in mapped host memory, which the
-//     host polls -- the completion contract of mx_reduce2_sync (inout final
-//     for every agent on return).
+//     number (a release store); the workgroup reads the 64-byte command
+//     line over PCIe;
+//   * it takes a system-scope acquire (stale operand lines dropped: the
+//     service never passes a kernel boundary), reduces with the op kernels'
+//     element functors, waits for its stores, releases at system scope and
+//     raises the done word in mapped host memory, which the host polls --
+//     the completion contract of mx_reduce2_sync (inout final for every
+//     agent on return).
 // One service per process, bound to one (op, type) at a time (a kernel per
 // pair, like the op kernels); a call for another pair stops it and starts
-// that pair's.  It leaves by itself after kSvcIdle of wall clock without a
-// command, so it holds its CUs only while calls keep coming (the segmented
+// that pair's.  It leaves by itself after kSvcIdleS of wall clock without a
+// command, so it holds its CU only while calls keep coming (the segmented
 // ring's one ompi_op_reduce per segment); the host relaunches it on demand
 // and, at exit, stops it (atexit), so the grid has drained before the
 // process ends.  A command is taken only by a running kernel: if the kernel
-// left (idle) before taking the posted one, the host sees the stream idle
-// with the command undone and relaunches it from that sequence number --
-// a command never runs twice.  Before the first command the host waits for
-// the kernel to report itself running; a kernel that does not start within
-// kSvcStartUs (its hardware queue held by another spinning kernel) is told
-// to leave and the process falls back to launches for good.
+// left (idle, reported in a mapped word -- a stream query per call costs
+// more than the service saves) before taking the posted one, the host drains
+// the stream, sees the command undone and relaunches the kernel from that
+// sequence number -- a command never runs twice.  Before the first command
+// the host waits for the kernel to report itself running; a kernel that does
+// not start within kSvcStartUs (its hardware queue held by another spinning
+// kernel) is told to leave and the process falls back to launches for good.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include <stdlib.h>
 #include <string.h>
 #include <chrono>
+#include <algorithm>
 #include <mutex>
 
 #include "mx_dispatch.hpp"
@@ -46,148 +47,181 @@
 
 namespace mx {
 
-constexpr int kSvcWG = 64;                 // resident workgroups
-constexpr int kSvcB = 256;                 // lanes per workgroup
-constexpr size_t kSvcMaxBytes = 1 << 20;   // calls up to 1 MiB per buffer
+constexpr int kSvcB = 256;                 // lanes of the one resident workgroup (4 waves; 16 waves cost
+                                           // ~1 us more per command, svc_pingpong_probe mode 9)
+constexpr int kSvcU = 8;                   // 16-byte vectors in flight per lane and operand
+constexpr size_t kSvcMaxBytes = 128 << 10; // calls up to 128 KiB per buffer (one CU's share; larger: launches)
 constexpr double kSvcIdleS = 2e-3;         // leave after 2 ms without a command
 constexpr double kSvcStartUs = 2000;       // a kernel not running after 2 ms: no service
 
 struct alignas(64) SvcCmd {                // coherent mapped host memory, written by the host
-  uint64_t seq;
-  uint64_t in, inout, count;
-  uint64_t exit;
-  uint64_t in2;                            // 3-buffer commands: inout = in OP in2; 0: inout = inout OP in
+  uint64_t seq;                            // raised last (release): a new command
+  uint64_t q;                              // = seq of the command the fields below belong to
+  uint64_t in, inout, in2, count;          // in2 != 0: inout = in OP in2; else inout = inout OP in
+  uint64_t exit;                           // leave
+  uint64_t chk;                            // svc_chk of the words above seq: a torn read never matches
 };
+static_assert(sizeof(SvcCmd) == 64, "one line");
 struct alignas(64) SvcHost {               // mapped host memory, written by the kernel
   uint64_t done;                           // last command completed
   uint64_t running;                        // launch epoch the kernel reported at start
-};
-struct SvcDev {                            // device (uncached): workgroup 0 -> the others
-  uint64_t tag;                            // (launch epoch << 32) | broadcast number of this launch
-  uint64_t in, inout, count, exit, q, in2; // the command (q: its host sequence number)
-  uint64_t done_tag;                       // (epoch << 32) | last broadcast every workgroup finished
-  unsigned ctr;                            // workgroups done with the current broadcast
+  uint64_t left;                           // launch epoch that left idle (before leaving)
 };
 
-__device__ __forceinline__ uint64_t svc_ld(const uint64_t *p) {
-  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+// The command line is read by one load instruction of wave 0 (lanes 0..7
+// one 8-byte system-scope load each): one PCIe round trip.  Eight loads
+// from one lane cost ~1.1 us more per command and plain or nontemporal
+// loads may be served from the CU's vector cache and never see the host's
+// store (tools/svc_pingpong_probe.hip modes 8, 6).  PCIe may serve the
+// lanes' words at different times around the host's stores; seq is raised
+// last, and a read whose fields are older than its seq would pair a new q
+// with old operands, which the checksum over (q, operands) catches (a
+// 64-bit mix: a stale set of operands that matches is the same set).  A
+// mismatch is read again.
+__host__ __device__ __forceinline__ uint64_t svc_mix(uint64_t h, uint64_t x) {
+  h ^= x + 0x9E3779B97F4A7C15ull + (h << 6) + (h >> 2);
+  h ^= h >> 31;
+  h *= 0xBF58476D1CE4E5B9ull;
+  return h ^ (h >> 29);
+}
+__host__ __device__ __forceinline__ uint64_t svc_chk(const uint64_t w[8]) {
+  uint64_t h = 0x6A09E667F3BCC909ull;
+  for (int k = 1; k < 7; k++) h = svc_mix(h, w[k]);
+  return h;
 }
 
-// Broadcasts are numbered per launch (k = 1, 2, ...) and tagged with the
-// launch's epoch, so a tag left in device memory by an earlier launch never
-// matches.  Workgroup 0 starts its idle clock only once every workgroup has
-// finished the last broadcast (done_tag), so a workgroup that became resident
-// late never misses a command.
+// wave 0, all lanes: w[] = the command line
+__device__ __forceinline__ void svc_read_cmd(const SvcCmd *c, uint64_t w[8]) {
+  const int lane = threadIdx.x & 63;
+  const uint64_t x = lane < 8 ? __hip_atomic_load(reinterpret_cast<const uint64_t *>(c) + lane, __ATOMIC_RELAXED,
+                                                  __HIP_MEMORY_SCOPE_SYSTEM)
+                              : 0;
+#pragma unroll
+  for (int k = 0; k < 8; k++) w[k] = __shfl(x, k);
+}
+
+// One workgroup, resident.  Measured on the box (tools/svc_pingpong_probe,
+// profiles/r04/svc_pingpong_*.txt): a host -> kernel -> host round trip with
+// the service's fences and a 4 KiB reduce costs ~3.5 us; 63 more resident
+// workgroups polling a device word for broadcasts add ~1.9 us to every
+// command (the service's first form), so the service is one CU's: the calls
+// it takes are the small ones, where the launch is the cost.
 template <class T, class OP, class OP3>
-__global__ void __launch_bounds__(kSvcB) k_svc(const SvcCmd *cmd, SvcHost *host, SvcDev *dev, uint64_t last,
-                                               uint64_t epoch, uint64_t idle_ticks) {
-  __shared__ uint64_t s_in, s_inout, s_count, s_exit, s_q, s_in2;
-  uint64_t seen = last;                    // host command sequence number taken last
-  uint32_t k = 0;                          // broadcasts of this launch
-  if (blockIdx.x == 0 && threadIdx.x == 0)
+__global__ void __launch_bounds__(kSvcB) k_svc(const SvcCmd *cmd, SvcHost *host, uint64_t last, uint64_t epoch,
+                                               uint64_t idle_ticks) {
+  __shared__ uint64_t s_in, s_inout, s_count, s_q, s_in2;
+  __shared__ int s_exit;
+  uint64_t seen = last;                    // command sequence number taken last (wave 0)
+  if (threadIdx.x == 0)
     __hip_atomic_store(&host->running, epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
   for (;;) {
-    k++;
-    if (threadIdx.x == 0) {
-      if (blockIdx.x == 0) {
-        uint64_t t0 = wall_clock64();
-        uint64_t q;
-        bool idle = false;
-        while ((q = svc_ld(&cmd->seq)) <= seen) {
-          if (k > 1 && __hip_atomic_load(&dev->done_tag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) !=
-                           ((epoch << 32) | (k - 1)))
-            t0 = wall_clock64();           // a broadcast still in progress: not idle
-          else if (wall_clock64() - t0 > idle_ticks) { idle = true; break; }
-          __builtin_amdgcn_s_sleep(1);
-        }
-        if (idle) {
-          s_exit = 1;                      // nothing taken: the others leave with it
-        } else {
-          __atomic_thread_fence(__ATOMIC_ACQUIRE);
-          s_in = svc_ld(&cmd->in);
-          s_inout = svc_ld(&cmd->inout);
-          s_count = svc_ld(&cmd->count);
-          s_exit = svc_ld(&cmd->exit);
-          s_in2 = svc_ld(&cmd->in2);
-          s_q = q;
-          seen = q;
-        }
-        dev->in = s_in;
-        dev->inout = s_inout;
-        dev->count = s_count;
-        dev->exit = s_exit;
-        dev->q = s_q;
-        dev->in2 = s_in2;
-        __hip_atomic_store(&dev->tag, (epoch << 32) | k, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
-      } else {
-        const uint64_t want = (epoch << 32) | k;
-        while (__hip_atomic_load(&dev->tag, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) != want)
-          __builtin_amdgcn_s_sleep(1);
-        s_in = dev->in;
-        s_inout = dev->inout;
-        s_count = dev->count;
-        s_exit = dev->exit;
-        s_q = dev->q;
-        s_in2 = dev->in2;
+    if (threadIdx.x < 64) {                // wave 0 polls
+      uint64_t t0 = wall_clock64();
+      uint64_t w[8];
+      int ex = 0;
+      for (;;) {
+        svc_read_cmd(cmd, w);
+        if (w[0] > seen && w[1] == w[0] && w[7] == svc_chk(w)) break;   // a whole new command
+        if (wall_clock64() - t0 > idle_ticks) { ex = 1; break; }
+        __builtin_amdgcn_s_sleep(1);
+      }
+      if (threadIdx.x == 0) s_exit = ex;
+      if (!ex) seen = w[0];
+      if (threadIdx.x == 0 && !ex) {
+        s_q = w[1];
+        s_in = w[2];
+        s_inout = w[3];
+        s_in2 = w[4];
+        s_count = w[5];
+        s_exit = w[6] != 0;
+        // system-scope acquire: stale operand lines dropped from this CU's
+        // caches and its XCD's L2 (the service never passes a kernel boundary)
+        __atomic_thread_fence(__ATOMIC_ACQUIRE);
       }
     }
     __syncthreads();
-    if (s_exit) return;                    // every workgroup leaves from here
-    __atomic_thread_fence(__ATOMIC_ACQUIRE);   // system scope: stale operand lines of this XCD's L2 dropped
+    if (s_exit) {
+      if (threadIdx.x == 0)
+        __hip_atomic_store(&host->left, epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      return;
+    }
     const T *a = reinterpret_cast<const T *>(s_in);
     T *b = reinterpret_cast<T *>(s_inout);
     const size_t n = s_count;
     constexpr size_t N = 16 / sizeof(T);
     struct alignas(16) V { T e[N]; };
     const size_t nvec = n / N;
-    const size_t stride = (size_t)gridDim.x * kSvcB;
+    const V *va = reinterpret_cast<const V *>(a);
+    V *vb = reinterpret_cast<V *>(b);
     if (!s_in2) {                          // 2-buffer: inout = inout OP in (the op kernels' K1)
       OP op;
-      for (size_t i = (size_t)blockIdx.x * kSvcB + threadIdx.x; i < nvec; i += stride) {
+      size_t i = threadIdx.x;
+      for (; i + (kSvcU - 1) * kSvcB < nvec; i += kSvcU * kSvcB) {   // kSvcU vectors per operand in flight
+        V x[kSvcU], y[kSvcU];
+#pragma unroll
+        for (int u = 0; u < kSvcU; u++) {
+          ld16<false>(x[u], vb + i + u * kSvcB);
+          ld16<false>(y[u], va + i + u * kSvcB);
+        }
+#pragma unroll
+        for (int u = 0; u < kSvcU; u++) {
+#pragma unroll
+          for (size_t j = 0; j < N; j++) store_fields(&x[u].e[j], op(x[u].e[j], y[u].e[j]));
+          st16<false>(vb + i + u * kSvcB, x[u]);
+        }
+      }
+      for (; i < nvec; i += kSvcB) {
         V x, y;
-        ld16<false>(x, reinterpret_cast<const V *>(b) + i);
-        ld16<false>(y, reinterpret_cast<const V *>(a) + i);
+        ld16<false>(x, vb + i);
+        ld16<false>(y, va + i);
 #pragma unroll
         for (size_t j = 0; j < N; j++) store_fields(&x.e[j], op(x.e[j], y.e[j]));
-        st16<false>(reinterpret_cast<V *>(b) + i, x);
+        st16<false>(vb + i, x);
       }
-      for (size_t i = nvec * N + (size_t)blockIdx.x * kSvcB + threadIdx.x; i < n; i += stride)
-        store_fields(&b[i], op(b[i], a[i]));
+      for (size_t k = nvec * N + threadIdx.x; k < n; k += kSvcB) store_fields(&b[k], op(b[k], a[k]));
     } else {                               // 3-buffer: out = in1 OP in2 (K2)
       OP3 op;
       const T *a2 = reinterpret_cast<const T *>(s_in2);
-      for (size_t i = (size_t)blockIdx.x * kSvcB + threadIdx.x; i < nvec; i += stride) {
+      const V *va2 = reinterpret_cast<const V *>(a2);
+      size_t i = threadIdx.x;
+      for (; i + (kSvcU - 1) * kSvcB < nvec; i += kSvcU * kSvcB) {
+        V x[kSvcU], y[kSvcU];
+#pragma unroll
+        for (int u = 0; u < kSvcU; u++) {
+          ld16<false>(x[u], va + i + u * kSvcB);
+          ld16<false>(y[u], va2 + i + u * kSvcB);
+        }
+#pragma unroll
+        for (int u = 0; u < kSvcU; u++) {
+#pragma unroll
+          for (size_t j = 0; j < N; j++) x[u].e[j] = op(x[u].e[j], y[u].e[j]);
+          st16<false>(vb + i + u * kSvcB, x[u]);
+        }
+      }
+      for (; i < nvec; i += kSvcB) {
         V x, y;
-        ld16<false>(x, reinterpret_cast<const V *>(a) + i);
-        ld16<false>(y, reinterpret_cast<const V *>(a2) + i);
+        ld16<false>(x, va + i);
+        ld16<false>(y, va2 + i);
 #pragma unroll
         for (size_t j = 0; j < N; j++) x.e[j] = op(x.e[j], y.e[j]);
-        st16<false>(reinterpret_cast<V *>(b) + i, x);
+        st16<false>(vb + i, x);
       }
-      for (size_t i = nvec * N + (size_t)blockIdx.x * kSvcB + threadIdx.x; i < n; i += stride)
-        b[i] = op(a[i], a2[i]);
+      for (size_t k = nvec * N + threadIdx.x; k < n; k += kSvcB) b[k] = op(a[k], a2[k]);
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this wave's stores reached L2
     __syncthreads();
     if (threadIdx.x == 0) {
       __threadfence_system();              // release: this XCD's L2 written back
-      const unsigned d = __hip_atomic_fetch_add(&dev->ctr, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
-      if (d == gridDim.x - 1) {
-        __hip_atomic_store(&dev->ctr, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        __hip_atomic_store(&dev->done_tag, (epoch << 32) | k, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
-        __threadfence_system();
-        __hip_atomic_store(&host->done, s_q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-      }
+      __hip_atomic_store(&host->done, s_q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     }
   }
 }
 
-typedef void (*svc_launch_fn)(const SvcCmd *, SvcHost *, SvcDev *, uint64_t, uint64_t, uint64_t, hipStream_t);
+typedef void (*svc_launch_fn)(const SvcCmd *, SvcHost *, uint64_t, uint64_t, uint64_t, hipStream_t);
 
 template <class T, class OP, class OP3>
-static void svc_launch(const SvcCmd *c, SvcHost *h, SvcDev *d, uint64_t last, uint64_t epoch, uint64_t idle,
-                       hipStream_t s) {
-  hipLaunchKernelGGL((k_svc<T, OP, OP3>), dim3(kSvcWG), dim3(kSvcB), 0, s, c, h, d, last, epoch, idle);
+static void svc_launch(const SvcCmd *c, SvcHost *h, uint64_t last, uint64_t epoch, uint64_t idle, hipStream_t s) {
+  hipLaunchKernelGGL((k_svc<T, OP, OP3>), dim3(1), dim3(kSvcB), 0, s, c, h, last, epoch, idle);
 }
 
 // pairs served: element types that tile 16-byte vectors with no bytes
@@ -207,7 +241,6 @@ struct Service {
   SvcCmd *cmd = nullptr;  // host pointer
   SvcCmd *cmd_d = nullptr;
   SvcHost *host = nullptr, *host_d = nullptr;
-  SvcDev *dev = nullptr;
   hipStream_t s = nullptr;
   uint64_t seq = 0;       // commands posted
   uint64_t epoch = 0;     // launches
@@ -234,11 +267,20 @@ bool svc_left(Service &v) {
   return true;
 }
 
+// post the command in v.cmd's operand fields as number ++v.seq
+uint64_t svc_post(Service &v) {
+  const uint64_t q = ++v.seq;
+  v.cmd->q = q;
+  v.cmd->chk = svc_chk(reinterpret_cast<const uint64_t *>(v.cmd));
+  __atomic_store_n(&v.cmd->seq, q, __ATOMIC_RELEASE);
+  return q;
+}
+
 void svc_stop_locked(Service &v) {
   if (!v.live) return;
   if (!svc_left(v)) {
     v.cmd->exit = 1;
-    __atomic_store_n(&v.cmd->seq, ++v.seq, __ATOMIC_RELEASE);
+    svc_post(v);
     (void)hipStreamSynchronize(v.s);
     v.cmd->exit = 0;
     // the EXIT command counts as done: later kernels start after it
@@ -265,8 +307,6 @@ int svc_setup(Service &v) {
       hipHostGetDevicePointer((void **)&v.cmd_d, v.cmd, 0) != hipSuccess ||
       hipHostMalloc((void **)&v.host, sizeof(SvcHost), hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess ||
       hipHostGetDevicePointer((void **)&v.host_d, v.host, 0) != hipSuccess ||
-      hipExtMallocWithFlags((void **)&v.dev, sizeof(SvcDev), hipDeviceMallocUncached) != hipSuccess ||
-      hipMemset(v.dev, 0, sizeof(SvcDev)) != hipSuccess ||
       hipStreamCreateWithPriority(&v.s, hipStreamNonBlocking, greatest) != hipSuccess ||
       hipDeviceSynchronize() != hipSuccess) {
     (void)hipGetLastError();
@@ -305,16 +345,19 @@ int svc_reduce(int op, int type, const void *in, const void *in2, void *inout, s
   if (v.state == 0) v.state = svc_setup(v);
   if (v.state != 1) return 0;
   if (v.live && (v.op != op || v.type != type)) svc_stop_locked(v);
-  if (v.live && svc_left(v)) v.live = false;   // left while idle
+  if (v.live && __atomic_load_n(&v.host->left, __ATOMIC_ACQUIRE) == v.epoch) {   // left while idle
+    (void)hipStreamSynchronize(v.s);
+    v.live = false;
+  }
   if (!v.live) {
     const uint64_t ep = ++v.epoch;
-    fn(v.cmd_d, v.host_d, v.dev, v.seq, ep, v.idle_ticks, v.s);
+    fn(v.cmd_d, v.host_d, v.seq, ep, v.idle_ticks, v.s);
     if (hipGetLastError() != hipSuccess) { v.state = -1; return 0; }
     if (!svc_poll(&v.host->running, ep, kSvcStartUs)) {
       // not running (its hardware queue is held): tell it to leave when it
       // starts, and launch per call from now on
       v.cmd->exit = 1;
-      __atomic_store_n(&v.cmd->seq, ++v.seq, __ATOMIC_RELEASE);
+      svc_post(v);
       v.state = -1;
       return 0;
     }
@@ -327,18 +370,20 @@ int svc_reduce(int op, int type, const void *in, const void *in2, void *inout, s
   v.cmd->count = count;
   v.cmd->in2 = (uint64_t)(uintptr_t)in2;
   v.cmd->exit = 0;
-  const uint64_t q = ++v.seq;
-  __atomic_store_n(&v.cmd->seq, q, __ATOMIC_RELEASE);
-  for (;;) {
-    if (svc_poll(&v.host->done, q, 200)) { v.served++; return 1; }
-    if (svc_left(v)) {
-      // it left before taking the command (idle exit): the command is not
-      // taken -- run a new kernel from the one before
+  const uint64_t q = svc_post(v);
+  for (unsigned k = 0;; k++) {
+    if (__atomic_load_n(&v.host->done, __ATOMIC_ACQUIRE) >= q) { v.served++; return 1; }
+    if ((k & 255) == 255 && __atomic_load_n(&v.host->left, __ATOMIC_ACQUIRE) == v.epoch) {
+      // it left idle before taking the command; once its grid has drained
+      // (every write of it landed) the done word tells whether q ran, and
+      // if not a new kernel takes it -- a command never runs twice
+      if (hipStreamSynchronize(v.s) != hipSuccess) { v.live = false; v.state = -1; return MX_ERR_HIP; }
       if (__atomic_load_n(&v.host->done, __ATOMIC_ACQUIRE) >= q) { v.served++; return 1; }
       const uint64_t ep = ++v.epoch;
-      fn(v.cmd_d, v.host_d, v.dev, q - 1, ep, v.idle_ticks, v.s);
+      fn(v.cmd_d, v.host_d, q - 1, ep, v.idle_ticks, v.s);
       if (hipGetLastError() != hipSuccess) { v.live = false; v.state = -1; return MX_ERR_HIP; }
     }
+    __builtin_ia32_pause();
   }
 }
 
