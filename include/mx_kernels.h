@@ -216,13 +216,23 @@ int mx_reduce2_sync(int op, int type, const void *in, void *inout,
 /* mx_reduce2_sync on a non-NULL stream hands calls of <= 128 KiB per buffer
  * (16-byte aligned buffers, element types without padding or x87) to a
  * resident one-workgroup service kernel instead of launching (no launch and
- * no dispatch per call: 4 KiB 7.4 -> 3.8 us; it
- * leaves after 2 ms without calls; MX_OP_SERVICE=0 switches it off).  A served call is not ordered after work still queued on any
+ * no dispatch per call: 4 KiB 7.4 -> 3.9 us; it
+ * leaves after 200 us without calls or, between calls, once 1 ms old, and
+ * is relaunched on demand; MX_OP_SERVICE=0 switches it off).  A served call is not ordered after work still queued on any
  * stream: its operands must be complete when it is made (the CUDA-aware MPI
  * contract for buffers handed to MPI).
  * Commands served and service launches so far; returns 1 when the service
  * is usable, 0 before first use, -1 when off. */
 int mx_op_service_stats(unsigned long long *served, unsigned long long *launches);
+/* Service launches that did not start within 200 us (their hardware queue
+ * held by a spinning kernel of another stream) so far; returns 1 while such
+ * a kernel has not yet left (calls launch meanwhile), else 0. */
+int mx_op_service_held(unsigned long long *held);
+/* Test support: launch on `stream` one wave that spins on a mapped host
+ * word, as a p2p receive waiting for its peer holds its hardware queue,
+ * until mx_debug_release() or timeout_ms pass. */
+int mx_debug_hold(void *stream, unsigned timeout_ms);
+int mx_debug_release(void);
 /* out[i] = in1[i] OP in2[i].  out may alias neither input (restrict, as
  * in the reference's 3-buffer functions). */
 int mx_reduce3(int op, int type, const void *in1, const void *in2,

@@ -6,9 +6,10 @@ call.
 Bit-exact vs the op oracle (op_base_functions.c restated; op values
 parity-unpinned) for every element family the service takes, at
 ragged sizes up to its 128 KiB cap; pairs interleaved (the service is rebound
-to each pair), pauses longer than its 2 ms idle exit (relaunch), a call over
+to each pair), pauses longer than its 200 us idle exit (relaunch), a call over
 the cap and a misaligned call (launch path), and the per-call counters show
-which calls the service took."""
+which calls the service took; a relaunch behind a held hardware queue
+launches instead of waiting."""
 import time
 
 import numpy as np
@@ -73,7 +74,7 @@ def test_service_serves_and_matches_the_oracle():
             for count in (1, 17, 1000, 4099, (64 << 10) // es + 3, SVC_MAX // es):
                 _check(op, t, count, 100 * rnd + count, s)
                 calls += 1
-        time.sleep(0.01)                               # > the 2 ms idle exit: the next call relaunches
+        time.sleep(0.01)                               # > the 200 us idle exit: the next call relaunches
     st, served, launches = mxompi.op_service_stats()
     assert st == 1, "service unusable on this box"
     assert served - served0 == calls, (served - served0, calls)
@@ -135,3 +136,50 @@ def test_service_three_buffer_form():
             golden_io.assert_op_equal(got, exp, mxompi.OP[op], mxompi.TYPE[t], f"3-buffer {op} {t} {count}+{off}")
             served_calls += off == 0 and count * es <= SVC_MAX   # else a launch
     assert mxompi.op_service_stats()[1] - served0 == served_calls
+
+
+def test_service_never_waits_on_a_held_queue():
+    """A relaunch (after the idle exit) whose hardware queue is held by a
+    spinning kernel of another high-priority stream -- as a p2p receive
+    waiting for its peer holds it -- must not wait for that
+    kernel, which may be waiting for this very thread: the call launches
+    instead, bit-exact, and the service serves again once the queue is free."""
+    import ctypes
+    mxompi.init(0)
+    L = mxompi.lib()
+    s = torch.cuda.Stream()
+    n = 1000
+    a = torch.ones(n, dtype=torch.int64, device="cuda")
+    b = torch.zeros(n, dtype=torch.int64, device="cuda")
+    torch.cuda.synchronize()
+    mxompi.reduce2_sync("SUM", "INT64_T", a.data_ptr(), b.data_ptr(), n, s.cuda_stream)
+    time.sleep(0.01)                                   # past the idle exit: the next call relaunches
+    held0 = mxompi.op_service_held()[1]
+    holders = []
+    try:
+        for _ in range(8):                             # more than the 4 hardware queues per priority
+            p = ctypes.c_void_p()
+            mxompi.check(L.mx_stream_create(ctypes.byref(p)), "mx_stream_create")
+            holders.append(p)
+            mxompi.debug_hold(p.value, 20000)
+        t0 = time.time()
+        for _ in range(20):
+            mxompi.reduce2_sync("SUM", "INT64_T", a.data_ptr(), b.data_ptr(), n, s.cuda_stream)
+        dt = time.time() - t0
+        assert torch.all(b == 21).item()
+        held = mxompi.op_service_held()[1] - held0
+        print(f"20 calls with every high-priority queue held: {dt * 1e3:.1f} ms, launches held {held}")
+        assert dt < 5.0, dt                            # the holders wait 20 s
+        assert held >= 1                               # the relaunch did meet a held queue
+    finally:
+        mxompi.debug_release()
+        for p in holders:
+            mxompi.check(L.mx_stream_sync(p), "mx_stream_sync")
+            mxompi.check(L.mx_stream_destroy(p), "mx_stream_destroy")
+    torch.cuda.synchronize()
+    served0 = mxompi.op_service_stats()[1]
+    for _ in range(3):                                 # the held kernel left on release: served again
+        mxompi.reduce2_sync("SUM", "INT64_T", a.data_ptr(), b.data_ptr(), n, s.cuda_stream)
+    assert torch.all(b == 24).item()
+    assert mxompi.op_service_stats()[1] - served0 == 3
+    assert not mxompi.op_service_held()[0]

@@ -21,18 +21,17 @@
 //     agent on return).
 // One service per process, bound to one (op, type) at a time (a kernel per
 // pair, like the op kernels); a call for another pair stops it and starts
-// that pair's.  It leaves by itself after kSvcIdleS of wall clock without a
-// command, so it holds its CU only while calls keep coming (the segmented
-// ring's one ompi_op_reduce per segment); the host relaunches it on demand
-// and, at exit, stops it (atexit), so the grid has drained before the
-// process ends.  A command is taken only by a running kernel: if the kernel
-// left (idle, reported in a mapped word -- a stream query per call costs
-// more than the service saves) before taking the posted one, the host drains
-// the stream, sees the command undone and relaunches the kernel from that
-// sequence number -- a command never runs twice.  Before the first command
-// the host waits for the kernel to report itself running; a kernel that does
-// not start within kSvcStartUs (its hardware queue held by another spinning
-// kernel) is told to leave and the process falls back to launches for good.
+// that pair's.  It leaves by itself after kSvcIdleS without a command, and
+// between commands once kSvcLifeS old, so it holds its CU only while calls
+// keep coming and never holds its hardware queue for long: streams of other
+// components that share that queue wait at most that long
+// behind it.  The host relaunches it on demand, waits until it runs and
+// only then posts -- a launched kernel takes only the commands after the
+// last one posted, so a command never runs twice; one that does not start
+// within kSvcStartUs (its queue held by a spinning kernel that may wait for
+// this very thread) is told to leave and the call launches instead, as do
+// the calls after it until that kernel has left.  At exit the host stops
+// the kernel (atexit), so the grid has drained before the process ends.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include <stdlib.h>
@@ -51,8 +50,9 @@ constexpr int kSvcB = 256;                 // lanes of the one resident workgrou
                                            // ~1 us more per command, svc_pingpong_probe mode 9)
 constexpr int kSvcU = 8;                   // 16-byte vectors in flight per lane and operand
 constexpr size_t kSvcMaxBytes = 128 << 10; // calls up to 128 KiB per buffer (one CU's share; larger: launches)
-constexpr double kSvcIdleS = 2e-3;         // leave after 2 ms without a command
-constexpr double kSvcStartUs = 2000;       // a kernel not running after 2 ms: no service
+constexpr double kSvcIdleS = 200e-6;      // leave after 200 us without a command
+constexpr double kSvcLifeS = 1e-3;         // and between commands once 1 ms old (then relaunched)
+constexpr double kSvcStartUs = 200;        // a kernel not running 200 us after its launch is held
 
 struct alignas(64) SvcCmd {                // coherent mapped host memory, written by the host
   uint64_t seq;                            // raised last (release): a new command
@@ -108,21 +108,23 @@ __device__ __forceinline__ void svc_read_cmd(const SvcCmd *c, uint64_t w[8]) {
 // it takes are the small ones, where the launch is the cost.
 template <class T, class OP, class OP3>
 __global__ void __launch_bounds__(kSvcB) k_svc(const SvcCmd *cmd, SvcHost *host, uint64_t last, uint64_t epoch,
-                                               uint64_t idle_ticks) {
+                                               uint64_t idle_ticks, uint64_t life_ticks) {
   __shared__ uint64_t s_in, s_inout, s_count, s_q, s_in2;
   __shared__ int s_exit;
   uint64_t seen = last;                    // command sequence number taken last (wave 0)
+  const uint64_t born = wall_clock64();
   if (threadIdx.x == 0)
     __hip_atomic_store(&host->running, epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
   for (;;) {
     if (threadIdx.x < 64) {                // wave 0 polls
-      uint64_t t0 = wall_clock64();
+      const uint64_t t0 = wall_clock64();
       uint64_t w[8];
       int ex = 0;
       for (;;) {
         svc_read_cmd(cmd, w);
         if (w[0] > seen && w[1] == w[0] && w[7] == svc_chk(w)) break;   // a whole new command
-        if (wall_clock64() - t0 > idle_ticks) { ex = 1; break; }
+        const uint64_t now = wall_clock64();
+        if (now - t0 > idle_ticks || now - born > life_ticks) { ex = 1; break; }
         __builtin_amdgcn_s_sleep(1);
       }
       if (threadIdx.x == 0) s_exit = ex;
@@ -217,11 +219,12 @@ __global__ void __launch_bounds__(kSvcB) k_svc(const SvcCmd *cmd, SvcHost *host,
   }
 }
 
-typedef void (*svc_launch_fn)(const SvcCmd *, SvcHost *, uint64_t, uint64_t, uint64_t, hipStream_t);
+typedef void (*svc_launch_fn)(const SvcCmd *, SvcHost *, uint64_t, uint64_t, uint64_t, uint64_t, hipStream_t);
 
 template <class T, class OP, class OP3>
-static void svc_launch(const SvcCmd *c, SvcHost *h, uint64_t last, uint64_t epoch, uint64_t idle, hipStream_t s) {
-  hipLaunchKernelGGL((k_svc<T, OP, OP3>), dim3(1), dim3(kSvcB), 0, s, c, h, last, epoch, idle);
+static void svc_launch(const SvcCmd *c, SvcHost *h, uint64_t last, uint64_t epoch, uint64_t idle, uint64_t life,
+                       hipStream_t s) {
+  hipLaunchKernelGGL((k_svc<T, OP, OP3>), dim3(1), dim3(kSvcB), 0, s, c, h, last, epoch, idle, life);
 }
 
 // pairs served: element types that tile 16-byte vectors with no bytes
@@ -244,10 +247,12 @@ struct Service {
   hipStream_t s = nullptr;
   uint64_t seq = 0;       // commands posted
   uint64_t epoch = 0;     // launches
-  bool live = false;      // a kernel was launched and has not been seen to leave
+  bool live = false;      // a kernel is running and has not been seen to leave
+  uint64_t pending = 0;   // epoch of a kernel launched but not seen running, told to leave
   int op = -1, type = -1;
-  uint64_t idle_ticks = 0;
+  uint64_t idle_ticks = 0, life_ticks = 0;
   uint64_t served = 0;    // commands completed by the service
+  uint64_t held = 0;      // launches that did not start within kSvcStartUs
 };
 Service g_svc;
 
@@ -259,14 +264,21 @@ bool svc_enabled() {
   return on != 0;
 }
 
-// the kernel has left (its stream is idle)
-bool svc_left(Service &v) {
-  const hipError_t e = hipStreamQuery(v.s);
-  if (e == hipErrorNotReady) return false;
-  (void)hipGetLastError();
-  return true;
-}
+// the kernel launched as `ep` has left (it writes `left` after its last
+// `done`, from the same thread: once `left` shows, `done` is final)
+bool svc_gone(const Service &v, uint64_t ep) { return __atomic_load_n(&v.host->left, __ATOMIC_ACQUIRE) >= ep; }
 
+// wait for host word *w >= target: `us` microseconds of polling, then false
+bool svc_poll(const uint64_t *w, uint64_t target, double us) {
+  const auto t0 = std::chrono::steady_clock::now();
+  for (unsigned k = 0;; k++) {
+    if (__atomic_load_n(w, __ATOMIC_ACQUIRE) >= target) return true;
+    if ((k & 255) == 255 &&
+        std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0).count() > us)
+      return false;
+    __builtin_ia32_pause();
+  }
+}
 // post the command in v.cmd's operand fields as number ++v.seq
 uint64_t svc_post(Service &v) {
   const uint64_t q = ++v.seq;
@@ -276,15 +288,16 @@ uint64_t svc_post(Service &v) {
   return q;
 }
 
+// stop a running kernel (rebinding to another pair, process exit)
 void svc_stop_locked(Service &v) {
   if (!v.live) return;
-  if (!svc_left(v)) {
+  if (!svc_gone(v, v.epoch)) {
     v.cmd->exit = 1;
     svc_post(v);
-    (void)hipStreamSynchronize(v.s);
     v.cmd->exit = 0;
-    // the EXIT command counts as done: later kernels start after it
-    __atomic_store_n(&v.host->done, v.seq, __ATOMIC_RELEASE);
+    // a running kernel reads it within microseconds; a second of silence
+    // means something else went wrong: wait for the stream instead
+    if (!svc_poll(&v.host->left, v.epoch, 1e6)) (void)hipStreamSynchronize(v.s);
   }
   v.live = false;
 }
@@ -303,6 +316,7 @@ int svc_setup(Service &v) {
       rate_khz <= 0)
     rate_khz = 100000;
   v.idle_ticks = (uint64_t)(kSvcIdleS * rate_khz * 1000.0);
+  v.life_ticks = (uint64_t)(kSvcLifeS * rate_khz * 1000.0);
   if (hipHostMalloc((void **)&v.cmd, sizeof(SvcCmd), hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess ||
       hipHostGetDevicePointer((void **)&v.cmd_d, v.cmd, 0) != hipSuccess ||
       hipHostMalloc((void **)&v.host, sizeof(SvcHost), hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess ||
@@ -318,21 +332,32 @@ int svc_setup(Service &v) {
   return 1;
 }
 
-// wait for host word *w >= target: ~2 ms of polling, then false
-bool svc_poll(const uint64_t *w, uint64_t target, double us) {
-  const auto t0 = std::chrono::steady_clock::now();
-  for (unsigned k = 0;; k++) {
-    if (__atomic_load_n(w, __ATOMIC_ACQUIRE) >= target) return true;
-    if ((k & 255) == 255 &&
-        std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0).count() > us)
-      return false;
-    __builtin_ia32_pause();
-  }
-}
 }  // namespace
 
+// Launch a kernel that takes the commands after v.seq and wait until it
+// runs.  A kernel that does not start within kSvcStartUs has its hardware
+// queue held -- possibly by a spinning kernel of another stream (a p2p
+// receive) that waits for what this thread does after this
+// call, so waiting longer could deadlock.  It is told to leave when it
+// starts (an EXIT command it will read first) and calls launch until it has.
+static bool svc_start(Service &v, svc_launch_fn fn) {
+  const uint64_t ep = ++v.epoch;
+  fn(v.cmd_d, v.host_d, v.seq, ep, v.idle_ticks, v.life_ticks, v.s);
+  if (hipGetLastError() != hipSuccess) { v.state = -1; return false; }
+  if (svc_poll(&v.host->running, ep, kSvcStartUs)) { v.live = true; return true; }
+  v.cmd->exit = 1;
+  svc_post(v);
+  v.cmd->exit = 0;
+  v.pending = ep;
+  v.live = false;
+  v.held++;
+  return false;
+}
+
 // 1: served (inout final); 0: not served (the caller launches); < 0 error.
-// in2 != nullptr: the 3-buffer form, inout = in OP in2.
+// in2 != nullptr: the 3-buffer form, inout = in OP in2.  A command is posted
+// only to a kernel seen running that was launched after every earlier
+// command, so no command runs twice and none waits on a held queue.
 int svc_reduce(int op, int type, const void *in, const void *in2, void *inout, size_t count) {
   if (!svc_enabled()) return 0;
   const size_t es = mx_type_size(type);
@@ -344,44 +369,31 @@ int svc_reduce(int op, int type, const void *in, const void *in2, void *inout, s
   std::lock_guard<std::mutex> lk(v.mu);
   if (v.state == 0) v.state = svc_setup(v);
   if (v.state != 1) return 0;
-  if (v.live && (v.op != op || v.type != type)) svc_stop_locked(v);
-  if (v.live && __atomic_load_n(&v.host->left, __ATOMIC_ACQUIRE) == v.epoch) {   // left while idle
-    (void)hipStreamSynchronize(v.s);
-    v.live = false;
+  if (v.pending) {
+    if (!svc_gone(v, v.pending)) return 0;    // still held: launch
+    v.pending = 0;
   }
+  if (v.live && (v.op != op || v.type != type)) svc_stop_locked(v);
+  if (v.live && svc_gone(v, v.epoch)) v.live = false;   // left (idle or lifetime)
   if (!v.live) {
-    const uint64_t ep = ++v.epoch;
-    fn(v.cmd_d, v.host_d, v.seq, ep, v.idle_ticks, v.s);
-    if (hipGetLastError() != hipSuccess) { v.state = -1; return 0; }
-    if (!svc_poll(&v.host->running, ep, kSvcStartUs)) {
-      // not running (its hardware queue is held): tell it to leave when it
-      // starts, and launch per call from now on
-      v.cmd->exit = 1;
-      svc_post(v);
-      v.state = -1;
-      return 0;
-    }
-    v.live = true;
     v.op = op;
     v.type = type;
+    if (!svc_start(v, fn)) return 0;
   }
   v.cmd->in = (uint64_t)(uintptr_t)in;
   v.cmd->inout = (uint64_t)(uintptr_t)inout;
   v.cmd->count = count;
   v.cmd->in2 = (uint64_t)(uintptr_t)in2;
   v.cmd->exit = 0;
-  const uint64_t q = svc_post(v);
+  uint64_t q = svc_post(v);
   for (unsigned k = 0;; k++) {
     if (__atomic_load_n(&v.host->done, __ATOMIC_ACQUIRE) >= q) { v.served++; return 1; }
-    if ((k & 255) == 255 && __atomic_load_n(&v.host->left, __ATOMIC_ACQUIRE) == v.epoch) {
-      // it left idle before taking the command; once its grid has drained
-      // (every write of it landed) the done word tells whether q ran, and
-      // if not a new kernel takes it -- a command never runs twice
-      if (hipStreamSynchronize(v.s) != hipSuccess) { v.live = false; v.state = -1; return MX_ERR_HIP; }
+    if ((k & 15) == 15 && svc_gone(v, v.epoch)) {
+      // it left before taking q (or took it: done is final once left shows)
       if (__atomic_load_n(&v.host->done, __ATOMIC_ACQUIRE) >= q) { v.served++; return 1; }
-      const uint64_t ep = ++v.epoch;
-      fn(v.cmd_d, v.host_d, q - 1, ep, v.idle_ticks, v.s);
-      if (hipGetLastError() != hipSuccess) { v.live = false; v.state = -1; return MX_ERR_HIP; }
+      v.live = false;
+      if (!svc_start(v, fn)) return 0;        // the new kernel starts after q: it never takes it
+      q = svc_post(v);                         // the same operands, a new number
     }
     __builtin_ia32_pause();
   }
@@ -395,4 +407,57 @@ extern "C" int mx_op_service_stats(unsigned long long *served, unsigned long lon
   if (served) *served = v.served;
   if (launches) *launches = v.epoch;
   return v.state;
+}
+
+extern "C" int mx_op_service_held(unsigned long long *held) {
+  mx::Service &v = mx::g_svc;
+  std::lock_guard<std::mutex> lk(v.mu);
+  if (held) *held = v.held;
+  return v.pending ? 1 : 0;
+}
+
+// Test support: a kernel that holds its stream's hardware queue the way a
+// p2p receive waiting for a peer does, to test that the
+// service never waits on a held queue.  One wave spins on a mapped host
+// word until mx_debug_release() raises it or timeout_ms of wall clock
+// pass, so the grid always drains.
+namespace {
+uint64_t *g_hold_word = nullptr, *g_hold_word_d = nullptr;
+uint64_t g_hold_gen = 0;
+std::mutex g_hold_mu;
+}  // namespace
+
+__global__ void __launch_bounds__(64) k_debug_hold(const uint64_t *word, uint64_t gen, uint64_t ticks) {
+  const uint64_t t0 = wall_clock64();
+  if (threadIdx.x == 0)
+    while (__hip_atomic_load(word, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) < gen && wall_clock64() - t0 < ticks)
+      __builtin_amdgcn_s_sleep(8);
+}
+
+extern "C" int mx_debug_hold(void *stream, unsigned timeout_ms) {
+  if (int rc = mx_ensure_init()) return rc;
+  std::lock_guard<std::mutex> lk(g_hold_mu);
+  if (!g_hold_word) {
+    if (hipHostMalloc((void **)&g_hold_word, 64, hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess ||
+        hipHostGetDevicePointer((void **)&g_hold_word_d, g_hold_word, 0) != hipSuccess) {
+      (void)hipGetLastError();
+      g_hold_word = nullptr;
+      return MX_ERR_HIP;
+    }
+    *g_hold_word = 0;
+  }
+  int rate_khz = 0;
+  if (hipDeviceGetAttribute(&rate_khz, hipDeviceAttributeWallClockRate, mx::g_device < 0 ? 0 : mx::g_device) !=
+          hipSuccess || rate_khz <= 0)
+    rate_khz = 100000;
+  hipLaunchKernelGGL(k_debug_hold, dim3(1), dim3(64), 0, (hipStream_t)stream, g_hold_word_d, g_hold_gen + 1,
+                     (uint64_t)timeout_ms * (uint64_t)rate_khz);
+  return hipGetLastError() == hipSuccess ? MX_SUCCESS : MX_ERR_HIP;
+}
+
+extern "C" int mx_debug_release(void) {
+  std::lock_guard<std::mutex> lk(g_hold_mu);
+  if (!g_hold_word) return MX_SUCCESS;
+  __atomic_store_n(g_hold_word, ++g_hold_gen, __ATOMIC_RELEASE);
+  return MX_SUCCESS;
 }

@@ -117,6 +117,8 @@ def lib() -> ctypes.CDLL:
         L.mx_copy.argtypes = [vp, vp, sz, vp]
         L.mx_shmem_to_mpi.argtypes = [i, i, sz, ctypes.POINTER(i), ctypes.POINTER(i)]
         L.mx_op_service_stats.argtypes = [ctypes.POINTER(ctypes.c_ulonglong), ctypes.POINTER(ctypes.c_ulonglong)]
+        L.mx_op_service_held.argtypes = [ctypes.POINTER(ctypes.c_ulonglong)]
+        L.mx_debug_hold.argtypes = [vp, ctypes.c_uint]
         L._mx_typed = True
     return L
 
@@ -181,6 +183,24 @@ def op_service_stats():
     a, b = ctypes.c_ulonglong(), ctypes.c_ulonglong()
     st = lib().mx_op_service_stats(ctypes.byref(a), ctypes.byref(b))
     return st, a.value, b.value
+
+
+def op_service_held():
+    """(a held kernel has not yet left, launches held so far): service
+    launches that did not start within 200 us (include/mx_kernels.h)."""
+    a = ctypes.c_ulonglong()
+    st = lib().mx_op_service_held(ctypes.byref(a))
+    return bool(st), a.value
+
+
+def debug_hold(stream: int, timeout_ms: int = 5000) -> None:
+    """Test support: hold `stream`'s hardware queue with a spinning wave
+    until debug_release() or timeout_ms."""
+    check(lib().mx_debug_hold(stream, timeout_ms), "mx_debug_hold")
+
+
+def debug_release() -> None:
+    check(lib().mx_debug_release(), "mx_debug_release")
 
 
 def init(device: int = 0) -> None:
