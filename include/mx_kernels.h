@@ -203,11 +203,11 @@ int mx_reduce2(int op, int type, const void *in, void *inout,
                size_t count, void *stream);
 /* As mx_reduce2, and returns when the result is complete: the blocking form
  * the op component's handler needs (ompi_op_reduce, ompi/op/op.h:547-610,
- * returns with `inout` final, for every agent).  Launches of <= 64
- * workgroups raise a completion word in mapped host memory from their last
- * workgroup, after every workgroup released its stores at system scope;
+ * returns with `inout` final, for every agent).  Launches of <= 1024
+ * workgroups (count <= 262128) mark themselves: every workgroup releases
+ * its stores at system scope and writes its own flag in mapped host memory;
  * larger ones are followed by mx_stream_sync_fast's marker kernel
- * (MX_FUSED_MARK=0: always the marker).  The host polls the word; after
+ * (MX_FUSED_MARK=0: always the marker).  The host polls the flags; after
  * ~2 ms the wait falls back to hipStreamSynchronize, which also reports
  * faults.  A peer process reading `inout` right after return is tested in
  * tests/test_op_consumer_gpu.py. */
@@ -224,7 +224,7 @@ int mx_reduce2_sync(int op, int type, const void *in, void *inout,
  * Commands served and service launches so far; returns 1 when the service
  * is usable, 0 before first use, -1 when off. */
 int mx_op_service_stats(unsigned long long *served, unsigned long long *launches);
-/* Service launches that did not start within 200 us (their hardware queue
+/* Service launches that did not start within 1 ms (their hardware queue
  * held by a spinning kernel of another stream) so far; returns 1 while such
  * a kernel has not yet left (calls launch meanwhile), else 0. */
 int mx_op_service_held(unsigned long long *held);

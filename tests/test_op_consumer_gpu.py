@@ -13,9 +13,10 @@ Nothing orders the peer's copy after the reduce kernel except the handler's
 return -- so a result published early (a completion word raised before the
 stores are visible to another agent) shows up as a wrong part.
 
-Both completion paths: the fused mark (the reduce kernel's last workgroup
-raises the completion word; launches of <= 64 workgroups) and the marker
-kernel.  Every rank's result bit-exact vs the recursive-doubling oracle
+Every completion path: the resident service (calls <= 128 KiB on the
+handler's stream), the launch marking itself (every workgroup writes its
+own flag after its system-scope release; MX_OP_SERVICE=0) and the marker
+kernel (MX_OP_SERVICE=0 MX_FUSED_MARK=0).  Every rank's result bit-exact vs the recursive-doubling oracle
 (mxo_allreduce alg 3, coll_base_allreduce.c:130-274) -- 32 allreduces of
 4 KiB - 1 MiB with fresh inputs each.
 """
@@ -37,7 +38,7 @@ pytestmark = pytest.mark.gpu
 vp, ci, sz = ctypes.c_void_p, ctypes.c_int, ctypes.c_size_t
 N = 8
 STEPS = 3                                        # log2(N)
-SIZES = [1000, 16384, 65536, 262144]             # floats: 4 KiB (1 wg) .. 256 KiB (fused cap) .. 1 MiB (marker)
+SIZES = [1000, 16384, 65536, 262144, 300000]     # floats: 4 KiB (1 wg) .. 1 MiB (256 wgs) .. 1.14 MiB (marker)
 ITERS = 8
 
 
@@ -144,7 +145,9 @@ def _worker(rank, port, env, flags, q):
         q.put((rank, "err", traceback.format_exc()))
 
 
-@pytest.mark.parametrize("env", [{"MX_FUSED_MARK": "1"}, {"MX_FUSED_MARK": "0"}], ids=["fused_mark", "marker_kernel"])
+@pytest.mark.parametrize("env", [{"MX_OP_SERVICE": "1"}, {"MX_OP_SERVICE": "0", "MX_FUSED_MARK": "1"},
+                                 {"MX_OP_SERVICE": "0", "MX_FUSED_MARK": "0"}],
+                         ids=["service", "fused_mark", "marker_kernel"])
 def test_op_reduce_result_read_by_peer_process_recursive_doubling(env):
     import torch.multiprocessing as mp
     ctx = mp.get_context("spawn")

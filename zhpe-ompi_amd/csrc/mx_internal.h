@@ -8,19 +8,23 @@ extern int g_num_cus;      // CUs of the current device (256 on MI355X)
 extern int g_device;       // device selected by mx_init
 // 16-byte streaming device copy (mx_coll.hip), falls back to the runtime copy
 int copy_async(void *dst, const void *src, size_t bytes, hipStream_t s);
-// Completion mark carried by a kernel launch: its last workgroup raises
-// *word (mapped host memory) to v; word == nullptr = no mark.
+// Completion mark.  word: the marker kernel (k_mark) raises *word (mapped
+// host memory) to v.  flags: a kernel launch marks itself -- workgroup b,
+// after its stores and a system-scope release, writes
+// flags[b] = (v << 12) | (gridDim.x - 1) (mapped host memory, kMarkFlags
+// entries, so grids of at most kMarkFlags workgroups); the host waits for
+// every entry of the grid.  Both nullptr: no mark.
+constexpr unsigned kMarkFlags = 1024;
 struct Mark {
   uint64_t *word;
-  unsigned *ctr;     // workgroups done (device memory, back to 0 by the last one)
+  uint64_t *flags;
   uint64_t v;
 };
-// Arms the calling thread's mark (word = nullptr when mapped memory is
-// unavailable).  counter_stream: a kernel that raises the word itself needs
-// the workgroup counter, allocated on first use and zeroed on that stream
-// (ctr = nullptr, and no mark, when that fails); nullptr: the marker kernel.
-void mark_arm(Mark *m, hipStream_t counter_stream = nullptr, bool need_counter = false);
-// Polls the mark's word (~2 ms), then falls back to hipStreamSynchronize(s).
+// Arms the calling thread's mark (its pointers nullptr when mapped memory is
+// unavailable): the marker kernel's word, or with `flags` the per-workgroup
+// flags of a launch that marks itself.
+void mark_arm(Mark *m, bool flags = false);
+// Polls the mark (~2 ms), then falls back to hipStreamSynchronize(s).
 int mark_wait(const Mark &m, hipStream_t s);
 // The resident reduce service (mx_service.hip): 1 = served, inout final for
 // every agent; 0 = not served (the caller launches); < 0 = error.  in2:

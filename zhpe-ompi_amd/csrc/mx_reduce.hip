@@ -44,28 +44,24 @@ struct alignas(16) vec16 {
 
 // Completion mark (mx_reduce2_sync): every workgroup, after its stores,
 // releases them at system scope (its XCD's L2 written back, as a kernel's
-// end would) and counts itself done on a counter in uncached memory; the
-// last one returns the counter to 0 and raises the caller's word in mapped
-// host memory.  The host sees the word instead of waiting for a second,
-// marker kernel -- one dispatch less per blocking call (op/mi355x's handler,
-// ompi_op_reduce op.h:547-610).  Used for launches of <= 64 workgroups
-// only (kFusedMarkMax).  mk.word is a kernel
-// argument, so the branch is uniform; without a mark it costs nothing.
+// end would) and writes its own flag in mapped host memory -- no atomics,
+// no counter (a counter's system-scope atomics serialise: 32 workgroups
+// cost ~2.7 us, profiles/r04/op_call_cost_r4_flags.txt).  The host sees the
+// flags instead of waiting for a second, marker kernel -- one dispatch less
+// per blocking call (op/mi355x's handler, ompi_op_reduce op.h:547-610).
+// mk.flags is a kernel argument, so the branch is uniform; without a mark it
+// costs nothing.
 __device__ __forceinline__ void mark_done(const Mark &mk) {
-  if (mk.word == nullptr) return;
+  if (mk.flags == nullptr) return;
   // every wave's stores have reached its L2 before thread 0's write-back:
   // the barrier alone orders issue, not completion, and the system fence
   // below waits only for thread 0's own wave
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
-  if (threadIdx.x == 0) {
+  if (threadIdx.x == 0 && blockIdx.x < kMarkFlags) {
     __threadfence_system();
-    const unsigned done = __hip_atomic_fetch_add(mk.ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-    if (done == gridDim.x - 1) {
-      __hip_atomic_store(mk.ctr, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-      __threadfence_system();
-      __hip_atomic_store(mk.word, mk.v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-    }
+    __hip_atomic_store(mk.flags + blockIdx.x, (mk.v << 12) | (uint64_t)(gridDim.x - 1), __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_SYSTEM);
   }
 }
 
@@ -209,17 +205,14 @@ static bool conv_w32() {
   return on != 0;
 }
 
-// launches that carry their own completion mark: at most 64 workgroups of
-// 256 lanes (<= 16384 elements and <= 256 KiB).  Every workgroup pays a
-// system-scope release before it counts itself done; measured per
-// ompi_op_reduce call, fp32 SUM, interleaved A/B (profiles/r03/
-// op_call_cost_r3.txt): 4 KiB (1 wg) 9.23 -> 7.27 us, 64 KiB (16 wgs)
-// 10.59 -> 8.44, but uncapped at 1 MiB (256 wgs) 9.64 -> 12.31, so larger
-// launches keep the marker kernel.
-constexpr size_t kFusedMarkMax = (size_t)1 << 14;
-constexpr size_t kFusedMarkMaxBytes = (size_t)256 << 10;
+// launches that carry their own completion mark: grids of at most
+// kMarkFlags workgroups.  Every launch mx_reduce2_sync makes for count
+// elements has at most ceil((count + 16) / 256) workgroups (one 16-byte
+// vector, or one element, per lane of 256; the 64-lane non-temporal
+// instances start at 384 MiB footprints), so counts up to this bound fit.
+constexpr size_t kFusedMarkMax = (size_t)kMarkFlags * 256 - 16;
 
-// Small launches raise the completion word themselves (default; MX_FUSED_MARK=0
+// Launches mark themselves (default; MX_FUSED_MARK=0
 // keeps the marker kernel).  Round 3 switched this off after an 8-process
 // failure (one 5000-element block wrong at one rank) that was later traced
 // to a different cause -- a freed communicator's flags recycled while a
@@ -401,13 +394,13 @@ extern "C" int mx_reduce2_sync(int op, int type, const void *in, void *inout, si
     rc = svc_reduce(op, type, in, nullptr, inout, count);
     if (rc) return rc < 0 ? rc : MX_SUCCESS;
   }
-  if (!fused_mark() || count > kFusedMarkMax || count * mx_type_size(type) > kFusedMarkMaxBytes) {
+  if (!fused_mark() || count > kFusedMarkMax) {
     rc = e.f2(in, inout, count, s, Mark{nullptr, nullptr, 0});
     return rc ? rc : mx_stream_sync_fast(stream);
   }
   Mark mk;
-  mark_arm(&mk, s, true);
-  if (!mk.ctr) {   // no counter: the marker kernel
+  mark_arm(&mk, true);
+  if (!mk.flags) {   // no flags: the marker kernel
     rc = e.f2(in, inout, count, s, Mark{nullptr, nullptr, 0});
     return rc ? rc : mx_stream_sync_fast(stream);
   }

@@ -255,12 +255,12 @@ __global__ void k_mark(uint64_t *w, uint64_t v) {
 }
 struct MarkWord {
   uint64_t *host = nullptr, *dev = nullptr;
-  unsigned *ctr = nullptr;   // workgroup counter of kernels that raise the word themselves (uncached)
+  uint64_t *flags = nullptr, *flags_dev = nullptr;   // kMarkFlags per-workgroup flags (mapped host memory)
   uint64_t seq = 0;
-  bool failed = false;
+  bool failed = false, flags_failed = false;
   ~MarkWord() {
     if (host) (void)hipHostFree(host);
-    if (ctr) (void)hipFree(ctr);
+    if (flags) (void)hipHostFree(flags);
   }
 };
 thread_local MarkWord t_mark;
@@ -282,33 +282,62 @@ MarkWord &mark_word() {
 }
 }  // namespace
 
-void mx::mark_arm(Mark *out, hipStream_t counter_stream, bool need_counter) {
+void mx::mark_arm(Mark *out, bool flags) {
   MarkWord &m = mark_word();
   *out = Mark{nullptr, nullptr, 0};
   if (!m.host) return;
-  if (need_counter && !m.ctr) {
-    // the workgroup counter of kernels that raise the word themselves, made
-    // on first use only (the marker-kernel path never needs it), zeroed on
-    // the caller's stream ahead of the kernel that counts on it
-    unsigned *ctr = nullptr;
-    if (hipExtMallocWithFlags((void **)&ctr, 64, hipDeviceMallocUncached) != hipSuccess ||
-        hipMemsetAsync(ctr, 0, 64, counter_stream) != hipSuccess) {
-      (void)hipGetLastError();
-      if (ctr) (void)hipFree(ctr);
-      return;
+  if (flags) {
+    // made on first use only (the marker-kernel path never needs them); the
+    // entries carry the call's sequence number, so they are never reset
+    if (!m.flags && !m.flags_failed) {
+      if (hipHostMalloc((void **)&m.flags, kMarkFlags * sizeof(uint64_t), hipHostMallocMapped) != hipSuccess ||
+          hipHostGetDevicePointer((void **)&m.flags_dev, m.flags, 0) != hipSuccess) {
+        (void)hipGetLastError();
+        if (m.flags) (void)hipHostFree(m.flags);
+        m.flags = nullptr;
+        m.flags_failed = true;
+      } else {
+        memset(m.flags, 0, kMarkFlags * sizeof(uint64_t));
+      }
     }
-    m.ctr = ctr;
+    if (!m.flags) return;
+    *out = Mark{nullptr, m.flags_dev, ++m.seq};
+    return;
   }
-  *out = Mark{m.dev, need_counter ? m.ctr : nullptr, ++m.seq};
+  *out = Mark{m.dev, nullptr, ++m.seq};
+}
+
+// every entry of the grid carries v: workgroup 0's entry gives the grid
+// size; the rest are read with independent loads (the host overlaps the
+// misses on lines the device rewrote)
+static bool flags_done(const uint64_t *f, uint64_t v) {
+  const uint64_t f0 = __atomic_load_n(f, __ATOMIC_RELAXED);
+  if ((f0 >> 12) < v) return false;
+  const unsigned n = (unsigned)(f0 & 4095) + 1;
+  uint64_t lo = f0;
+  for (unsigned b = 1; b < n && b < kMarkFlags; b++) {
+    const uint64_t x = __atomic_load_n(f + b, __ATOMIC_RELAXED);
+    lo = x < lo ? x : lo;
+  }
+  if ((lo >> 12) < v) return false;
+  __atomic_thread_fence(__ATOMIC_ACQUIRE);
+  return true;
 }
 
 int mx::mark_wait(const Mark &mk, hipStream_t s) {
   MarkWord &m = t_mark;
-  if (!mk.word || !m.host) return mx_hip_rc(hipStreamSynchronize(s));
+  if ((!mk.word && !mk.flags) || !m.host) return mx_hip_rc(hipStreamSynchronize(s));
   static const long spins = [] {            // ~2 ms of polling; MX_FAST_SYNC_SPINS overrides (tests)
     const char *e = getenv("MX_FAST_SYNC_SPINS");
     return e && *e ? atol(e) : (1L << 16);
   }();
+  if (mk.flags) {
+    for (long i = 0; i < spins; i++) {
+      if (flags_done(m.flags, mk.v)) return MX_SUCCESS;
+      __builtin_ia32_pause();
+    }
+    return mx_hip_rc(hipStreamSynchronize(s));
+  }
   for (long i = 0; i < spins; i++) {
     if (__atomic_load_n(m.host, __ATOMIC_ACQUIRE) >= mk.v) return MX_SUCCESS;
     __builtin_ia32_pause();

@@ -39,6 +39,7 @@
 #include <chrono>
 #include <algorithm>
 #include <mutex>
+#include <vector>
 
 #include "mx_dispatch.hpp"
 #include "mx_internal.h"
@@ -52,7 +53,8 @@ constexpr int kSvcU = 8;                   // 16-byte vectors in flight per lane
 constexpr size_t kSvcMaxBytes = 128 << 10; // calls up to 128 KiB per buffer (one CU's share; larger: launches)
 constexpr double kSvcIdleS = 200e-6;      // leave after 200 us without a command
 constexpr double kSvcLifeS = 1e-3;         // and between commands once 1 ms old (then relaunched)
-constexpr double kSvcStartUs = 200;        // a kernel not running 200 us after its launch is held
+constexpr double kSvcStartUs = 1000;       // a kernel not running 1 ms after its launch is held
+constexpr double kSvcFirstStartUs = 50000; // (50 ms for a pair's first launch: its code object loads)
 
 struct alignas(64) SvcCmd {                // coherent mapped host memory, written by the host
   uint64_t seq;                            // raised last (release): a new command
@@ -253,6 +255,7 @@ struct Service {
   uint64_t idle_ticks = 0, life_ticks = 0;
   uint64_t served = 0;    // commands completed by the service
   uint64_t held = 0;      // launches that did not start within kSvcStartUs
+  std::vector<svc_launch_fn> started;   // pairs whose kernel has run in this process
 };
 Service g_svc;
 
@@ -344,7 +347,12 @@ static bool svc_start(Service &v, svc_launch_fn fn) {
   const uint64_t ep = ++v.epoch;
   fn(v.cmd_d, v.host_d, v.seq, ep, v.idle_ticks, v.life_ticks, v.s);
   if (hipGetLastError() != hipSuccess) { v.state = -1; return false; }
-  if (svc_poll(&v.host->running, ep, kSvcStartUs)) { v.live = true; return true; }
+  const bool first = std::find(v.started.begin(), v.started.end(), fn) == v.started.end();
+  if (svc_poll(&v.host->running, ep, first ? kSvcFirstStartUs : kSvcStartUs)) {
+    if (first) v.started.push_back(fn);
+    v.live = true;
+    return true;
+  }
   v.cmd->exit = 1;
   svc_post(v);
   v.cmd->exit = 0;

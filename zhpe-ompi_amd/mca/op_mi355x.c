@@ -128,7 +128,7 @@ static void mx_op_2buff(void *in, void *inout, int *count, struct ompi_datatype_
         void *s = op_stream();
         int rc;
         if (g_fast_sync < 0) g_fast_sync = mx_ompi_host->mca_int("op_mi355x_fast_sync", 1) != 0;
-        if (g_fast_sync)   /* completion word: from the reduce kernel (<= 64 workgroups) or a marker kernel */
+        if (g_fast_sync)   /* the resident service, or the launch marking itself (per-workgroup flags) */
             rc = mx_reduce2_sync(m->op_index, slot, in, inout, (size_t)*count, s);
         else
             rc = run_sync(s, mx_reduce2(m->op_index, slot, in, inout, (size_t)*count, s));

@@ -187,7 +187,7 @@ def op_service_stats():
 
 def op_service_held():
     """(a held kernel has not yet left, launches held so far): service
-    launches that did not start within 200 us (include/mx_kernels.h)."""
+    launches that did not start within 1 ms (include/mx_kernels.h)."""
     a = ctypes.c_ulonglong()
     st = lib().mx_op_service_held(ctypes.byref(a))
     return bool(st), a.value
