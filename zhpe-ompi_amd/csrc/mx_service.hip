@@ -252,6 +252,7 @@ struct Service {
   bool live = false;      // a kernel is running and has not been seen to leave
   uint64_t pending = 0;   // epoch of a kernel launched but not seen running, told to leave
   int op = -1, type = -1;
+  int device = -1;        // the device the service runs on (the caller's at setup)
   uint64_t idle_ticks = 0, life_ticks = 0;
   uint64_t served = 0;    // commands completed by the service
   uint64_t held = 0;      // launches that did not start within kSvcStartUs
@@ -312,10 +313,14 @@ void svc_atexit() {
 }
 
 int svc_setup(Service &v) {
+  if (hipGetDevice(&v.device) != hipSuccess) {
+    (void)hipGetLastError();
+    return -1;
+  }
   int least = 0, greatest = 0;
   if (hipDeviceGetStreamPriorityRange(&least, &greatest) != hipSuccess) greatest = 0;
   int rate_khz = 0;
-  if (hipDeviceGetAttribute(&rate_khz, hipDeviceAttributeWallClockRate, g_device < 0 ? 0 : g_device) != hipSuccess ||
+  if (hipDeviceGetAttribute(&rate_khz, hipDeviceAttributeWallClockRate, v.device) != hipSuccess ||
       rate_khz <= 0)
     rate_khz = 100000;
   v.idle_ticks = (uint64_t)(kSvcIdleS * rate_khz * 1000.0);
@@ -377,6 +382,8 @@ int svc_reduce(int op, int type, const void *in, const void *in2, void *inout, s
   std::lock_guard<std::mutex> lk(v.mu);
   if (v.state == 0) v.state = svc_setup(v);
   if (v.state != 1) return 0;
+  int dev = -1;                               // a caller on another device launches there
+  if (hipGetDevice(&dev) != hipSuccess || dev != v.device) return 0;
   if (v.pending) {
     if (!svc_gone(v, v.pending)) return 0;    // still held: launch
     v.pending = 0;
