@@ -217,7 +217,7 @@ int mx_reduce2_sync(int op, int type, const void *in, void *inout,
  * (16-byte aligned buffers, element types without padding or x87) to a
  * resident one-workgroup service kernel instead of launching (no launch and
  * no dispatch per call: 4 KiB 7.4 -> 3.9 us; it
- * leaves after 200 us without calls or, between calls, once 1 ms old, and
+ * leaves after 100 us without calls or, between calls, once 1 ms old, and
  * is relaunched on demand; MX_OP_SERVICE=0 switches it off).  A served call is not ordered after work still queued on any
  * stream: its operands must be complete when it is made (the CUDA-aware MPI
  * contract for buffers handed to MPI).
@@ -225,13 +225,16 @@ int mx_reduce2_sync(int op, int type, const void *in, void *inout,
  * is usable, 0 before first use, -1 when off. */
 int mx_op_service_stats(unsigned long long *served, unsigned long long *launches);
 /* Service launches that did not start within 1 ms (their hardware queue
- * held by a spinning kernel of another stream) so far; returns 1 while such
+ * held by a kernel of another stream) so far; returns 1 while such
  * a kernel has not yet left (calls launch meanwhile), else 0. */
 int mx_op_service_held(unsigned long long *held);
 /* Test support: launch on `stream` one wave that spins on a mapped host
  * word, as a p2p receive waiting for its peer holds its hardware queue,
  * until mx_debug_release() or timeout_ms pass. */
 int mx_debug_hold(void *stream, unsigned timeout_ms);
+/* The same on the op service's own stream (MX_ERR_NOT_INIT before its
+ * first use): its next relaunch finds its hardware queue held. */
+int mx_debug_hold_service(unsigned timeout_ms);
 int mx_debug_release(void);
 /* out[i] = in1[i] OP in2[i].  out may alias neither input (restrict, as
  * in the reference's 3-buffer functions). */

@@ -6,7 +6,7 @@ call.
 Bit-exact vs the op oracle (op_base_functions.c restated; op values
 parity-unpinned) for every element family the service takes, at
 ragged sizes up to its 128 KiB cap; pairs interleaved (the service is rebound
-to each pair), pauses longer than its 200 us idle exit (relaunch), a call over
+to each pair), pauses longer than its 100 us idle exit (relaunch), a call over
 the cap and a misaligned call (launch path), and the per-call counters show
 which calls the service took; a relaunch behind a held hardware queue
 launches instead of waiting."""
@@ -74,7 +74,7 @@ def test_service_serves_and_matches_the_oracle():
             for count in (1, 17, 1000, 4099, (64 << 10) // es + 3, SVC_MAX // es):
                 _check(op, t, count, 100 * rnd + count, s)
                 calls += 1
-        time.sleep(0.01)                               # > the 200 us idle exit: the next call relaunches
+        time.sleep(0.01)                               # > the 100 us idle exit: the next call relaunches
     st, served, launches = mxompi.op_service_stats()
     assert st == 1, "service unusable on this box"
     assert served - served0 == calls, (served - served0, calls)
@@ -139,47 +139,137 @@ def test_service_three_buffer_form():
 
 
 def test_service_never_waits_on_a_held_queue():
-    """A relaunch (after the idle exit) whose hardware queue is held by a
-    spinning kernel of another high-priority stream -- as a p2p receive
-    waiting for its peer holds it -- must not wait for that
-    kernel, which may be waiting for this very thread: the call launches
-    instead, bit-exact, and the service serves again once the queue is free."""
+    """A relaunch (after the idle exit) whose hardware queue is held -- here
+    by a wave spinning on the service's own stream until released, as a
+    kernel waiting for this very thread would hold it -- must not wait: the
+    call launches instead, bit-exact, and the service serves again once the
+    queue is free."""
     import ctypes
     mxompi.init(0)
+    # the calls' own stream at the highest priority: a launch on it is not
+    # queued behind the held ordinary-priority queue of the service
     L = mxompi.lib()
-    s = torch.cuda.Stream()
+    hp = ctypes.c_void_p()
+    mxompi.check(L.mx_stream_create(ctypes.byref(hp)), "mx_stream_create")
+    sp = hp.value
     n = 1000
     a = torch.ones(n, dtype=torch.int64, device="cuda")
     b = torch.zeros(n, dtype=torch.int64, device="cuda")
     torch.cuda.synchronize()
-    mxompi.reduce2_sync("SUM", "INT64_T", a.data_ptr(), b.data_ptr(), n, s.cuda_stream)
+    mxompi.reduce2_sync("SUM", "INT64_T", a.data_ptr(), b.data_ptr(), n, sp)
     time.sleep(0.01)                                   # past the idle exit: the next call relaunches
     held0 = mxompi.op_service_held()[1]
-    holders = []
     try:
-        for _ in range(8):                             # more than the 4 hardware queues per priority
-            p = ctypes.c_void_p()
-            mxompi.check(L.mx_stream_create(ctypes.byref(p)), "mx_stream_create")
-            holders.append(p)
-            mxompi.debug_hold(p.value, 20000)
+        mxompi.debug_hold_service(20000)
         t0 = time.time()
         for _ in range(20):
-            mxompi.reduce2_sync("SUM", "INT64_T", a.data_ptr(), b.data_ptr(), n, s.cuda_stream)
+            mxompi.reduce2_sync("SUM", "INT64_T", a.data_ptr(), b.data_ptr(), n, sp)
         dt = time.time() - t0
-        assert torch.all(b == 21).item()
         held = mxompi.op_service_held()[1] - held0
-        print(f"20 calls with every high-priority queue held: {dt * 1e3:.1f} ms, launches held {held}")
-        assert dt < 5.0, dt                            # the holders wait 20 s
-        assert held >= 1                               # the relaunch did meet a held queue
+        print(f"20 calls with the service's queue held: {dt * 1e3:.1f} ms, launches held {held}")
+        assert dt < 5.0, dt                            # the holder waits 20 s
+        assert held >= 1                               # the relaunch did meet the held queue
+        assert mxompi.op_service_held()[0]             # that kernel is still queued
+        mxompi.check(L.mx_stream_sync(hp), "mx_stream_sync")
+        assert torch.all(b == 21).item()
     finally:
         mxompi.debug_release()
-        for p in holders:
-            mxompi.check(L.mx_stream_sync(p), "mx_stream_sync")
-            mxompi.check(L.mx_stream_destroy(p), "mx_stream_destroy")
-    torch.cuda.synchronize()
+    torch.cuda.synchronize()                           # the holder, then the held kernel (EXIT first)
     served0 = mxompi.op_service_stats()[1]
-    for _ in range(3):                                 # the held kernel left on release: served again
-        mxompi.reduce2_sync("SUM", "INT64_T", a.data_ptr(), b.data_ptr(), n, s.cuda_stream)
+    for _ in range(3):                                 # served again
+        mxompi.reduce2_sync("SUM", "INT64_T", a.data_ptr(), b.data_ptr(), n, sp)
     assert torch.all(b == 24).item()
     assert mxompi.op_service_stats()[1] - served0 == 3
     assert not mxompi.op_service_held()[0]
+    mxompi.check(L.mx_stream_destroy(hp), "mx_stream_destroy")
+
+
+def _free_port():
+    import socket
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _irecv_reduce_send_worker(rank, n, port, q, env):
+    """Irecv; Reduce_local x k (relaunching the service between them); Send;
+    Wait -- on both ranks.  The receive spins on a channel stream at the
+    highest priority, the queues the service also uses; a
+    service that waited for a queue held by that receive would never get to
+    the Send, and neither rank would finish."""
+    import os
+    import torch.distributed as dist
+    os.environ["HSA_ENABLE_IPC_MODE_LEGACY"] = "0"
+    os.environ.update(env)
+    try:
+        dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=n)
+        torch.cuda.set_device(0)
+        mxompi.init(0)
+
+        def ag(b):
+            out = [None] * n
+            dist.all_gather_object(out, b)
+            return out
+
+        comm = mxompi.Comm(rank, n, ag, device=0, staging_bytes=1 << 20)
+        comm.set_timeout(20.0)
+        s = torch.cuda.Stream()
+        peer = 1 - rank
+        m = 4096
+        a = torch.ones(m, dtype=torch.int64, device="cuda")
+        b = torch.zeros(m, dtype=torch.int64, device="cuda")
+        t0 = time.time()
+        out = []
+        for it in range(6):
+            nb = 4096 if it % 2 == 0 else 3 << 20          # eager, rendezvous
+            x = torch.full((nb,), (rank + 3 * it) & 0xff, dtype=torch.uint8, device="cuda")
+            y = torch.zeros(nb, dtype=torch.uint8, device="cuda")
+            torch.cuda.synchronize()
+            r = comm.irecv(y.data_ptr(), nb, peer, tag=it)
+            dist.barrier()                                  # both receives are spinning
+            for _ in range(5):
+                time.sleep(0.001)                           # past the idle exit: each call relaunches
+                mxompi.reduce2_sync("SUM", "INT64_T", a.data_ptr(), b.data_ptr(), m, s.cuda_stream)
+            sreq = comm.isend(x.data_ptr(), nb, peer, tag=it)
+            r.wait(); sreq.wait(); r.free(); sreq.free()
+            out.append(int(y[0].item()) == ((peer + 3 * it) & 0xff) and bool(torch.all(y == y[0]).item()))
+        res = {"seconds": time.time() - t0, "ok": out, "b": int(b[0].item()), "b_all": bool(torch.all(b == b[0]).item()),
+               "held": mxompi.op_service_held()[1], "stats": mxompi.op_service_stats()}
+        comm.close()
+        dist.destroy_process_group()
+        q.put((rank, "ok", res))
+    except Exception as e:  # noqa: BLE001
+        import traceback
+        q.put((rank, "err", traceback.format_exc() + str(e)))
+
+
+@pytest.mark.parametrize("env", [{"MX_OP_SERVICE": "1"}, {"MX_OP_SERVICE": "0"}], ids=["served", "launched"])
+def test_service_irecv_reduce_send_does_not_deadlock(env):
+    import torch.multiprocessing as mp
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_irecv_reduce_send_worker, args=(r, 2, port, q, env)) for r in range(2)]
+    for p in procs:
+        p.start()
+    got = {}
+    try:
+        for _ in range(2):
+            rank, status, payload = q.get(timeout=120)
+            assert status == "ok", payload
+            got[rank] = payload
+    finally:
+        for p in procs:
+            p.join(timeout=30 if len(got) == 2 else 5)
+            if p.is_alive():
+                p.terminate()
+                p.join(timeout=10)
+    for r in range(2):
+        print(f"rank {r}: {got[r]['seconds']:.2f} s, launches held {got[r]['held']}, service {got[r]['stats']}")
+        assert got[r]["ok"] == [True] * 6
+        assert got[r]["b"] == 30 and got[r]["b_all"]
+        assert got[r]["seconds"] < 15.0, got[r]["seconds"]
+        if env["MX_OP_SERVICE"] == "1":
+            assert got[r]["stats"][1] > 0                  # the service took calls

@@ -6,10 +6,14 @@
 // call (profiles/r04/op_call_cost_r4_fused_default.txt): the host's launch,
 // the packet processor's dispatch and the wake-up, not the ~0.5 us of work.
 // The service removes the launch and the dispatch: one workgroup stays
-// resident on a stream of its own (highest priority, whose hardware queues
-// the process's ordinary streams do not share) and serves the
-// calls of up to kSvcMaxBytes that the host writes into coherent mapped host
-// memory:
+// resident on a non-blocking stream of its own and serves the calls of up to
+// kSvcMaxBytes that the host writes into coherent mapped host memory.  The
+// stream has ordinary priority: the high-priority hardware queues (4 per
+// process) belong to a communicator's spinning p2p channel and request
+// streams, and a fifth high-priority stream made a channel
+// stream share a queue with another -- a send queued behind its own
+// spinning receive (tests/test_op_service_gpu.py, Irecv; Reduce_local;
+// Send on two ranks).  Per call:
 //   * the host fills the command (operands, count) and raises its sequence
 //     number (a release store); the workgroup reads the 64-byte command
 //     line over PCIe;
@@ -23,13 +27,12 @@
 // pair, like the op kernels); a call for another pair stops it and starts
 // that pair's.  It leaves by itself after kSvcIdleS without a command, and
 // between commands once kSvcLifeS old, so it holds its CU only while calls
-// keep coming and never holds its hardware queue for long: streams of other
-// components that share that queue wait at most that long
-// behind it.  The host relaunches it on demand, waits until it runs and
+// keep coming and never holds its hardware queue for long: the streams that
+// share that queue wait at most that long behind it.  The host relaunches it on demand, waits until it runs and
 // only then posts -- a launched kernel takes only the commands after the
 // last one posted, so a command never runs twice; one that does not start
-// within kSvcStartUs (its queue held by a spinning kernel that may wait for
-// this very thread) is told to leave and the call launches instead, as do
+// within kSvcStartUs (its queue held by a kernel that may wait for this
+// very thread) is told to leave and the call launches instead, as do
 // the calls after it until that kernel has left.  At exit the host stops
 // the kernel (atexit), so the grid has drained before the process ends.
 #include <hip/hip_runtime.h>
@@ -51,7 +54,7 @@ constexpr int kSvcB = 256;                 // lanes of the one resident workgrou
                                            // ~1 us more per command, svc_pingpong_probe mode 9)
 constexpr int kSvcU = 8;                   // 16-byte vectors in flight per lane and operand
 constexpr size_t kSvcMaxBytes = 128 << 10; // calls up to 128 KiB per buffer (one CU's share; larger: launches)
-constexpr double kSvcIdleS = 200e-6;      // leave after 200 us without a command
+constexpr double kSvcIdleS = 100e-6;      // leave after 100 us without a command
 constexpr double kSvcLifeS = 1e-3;         // and between commands once 1 ms old (then relaunched)
 constexpr double kSvcStartUs = 1000;       // a kernel not running 1 ms after its launch is held
 constexpr double kSvcFirstStartUs = 50000; // (50 ms for a pair's first launch: its code object loads)
@@ -312,13 +315,22 @@ void svc_atexit() {
   if (v.state == 1) svc_stop_locked(v);
 }
 
+// MX_SVC_PRIORITY=least|normal|greatest: the service stream's priority
+// (measurement switch; default normal)
+hipError_t svc_stream_create(hipStream_t *s) {
+  const char *e = getenv("MX_SVC_PRIORITY");
+  int least = 0, greatest = 0;
+  if (hipDeviceGetStreamPriorityRange(&least, &greatest) != hipSuccess) least = greatest = 0;
+  if (e && !strcmp(e, "least")) return hipStreamCreateWithPriority(s, hipStreamNonBlocking, least);
+  if (e && !strcmp(e, "greatest")) return hipStreamCreateWithPriority(s, hipStreamNonBlocking, greatest);
+  return hipStreamCreateWithFlags(s, hipStreamNonBlocking);
+}
+
 int svc_setup(Service &v) {
   if (hipGetDevice(&v.device) != hipSuccess) {
     (void)hipGetLastError();
     return -1;
   }
-  int least = 0, greatest = 0;
-  if (hipDeviceGetStreamPriorityRange(&least, &greatest) != hipSuccess) greatest = 0;
   int rate_khz = 0;
   if (hipDeviceGetAttribute(&rate_khz, hipDeviceAttributeWallClockRate, v.device) != hipSuccess ||
       rate_khz <= 0)
@@ -329,8 +341,7 @@ int svc_setup(Service &v) {
       hipHostGetDevicePointer((void **)&v.cmd_d, v.cmd, 0) != hipSuccess ||
       hipHostMalloc((void **)&v.host, sizeof(SvcHost), hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess ||
       hipHostGetDevicePointer((void **)&v.host_d, v.host, 0) != hipSuccess ||
-      hipStreamCreateWithPriority(&v.s, hipStreamNonBlocking, greatest) != hipSuccess ||
-      hipDeviceSynchronize() != hipSuccess) {
+      svc_stream_create(&v.s) != hipSuccess) {   // no device-wide sync: other streams may hold spinning kernels
     (void)hipGetLastError();
     return -1;
   }
@@ -344,9 +355,9 @@ int svc_setup(Service &v) {
 
 // Launch a kernel that takes the commands after v.seq and wait until it
 // runs.  A kernel that does not start within kSvcStartUs has its hardware
-// queue held -- possibly by a spinning kernel of another stream (a p2p
-// receive) that waits for what this thread does after this
-// call, so waiting longer could deadlock.  It is told to leave when it
+// queue held -- possibly by a kernel of another stream that waits for what
+// this thread does after this call (a spinning wait on a host flag), so
+// waiting longer could deadlock.  It is told to leave when it
 // starts (an EXIT command it will read first) and calls launch until it has.
 static bool svc_start(Service &v, svc_launch_fn fn) {
   const uint64_t ep = ++v.epoch;
@@ -470,9 +481,21 @@ extern "C" int mx_debug_hold(void *stream, unsigned timeout_ms) {
   return hipGetLastError() == hipSuccess ? MX_SUCCESS : MX_ERR_HIP;
 }
 
+extern "C" int mx_debug_hold_service(unsigned timeout_ms) {
+  hipStream_t s = nullptr;
+  {
+    mx::Service &v = mx::g_svc;
+    std::lock_guard<std::mutex> lk(v.mu);
+    if (v.state != 1) return MX_ERR_NOT_INIT;
+    s = v.s;
+  }
+  return mx_debug_hold(s, timeout_ms);
+}
+
 extern "C" int mx_debug_release(void) {
   std::lock_guard<std::mutex> lk(g_hold_mu);
   if (!g_hold_word) return MX_SUCCESS;
   __atomic_store_n(g_hold_word, ++g_hold_gen, __ATOMIC_RELEASE);
   return MX_SUCCESS;
 }
+

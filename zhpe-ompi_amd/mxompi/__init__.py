@@ -119,6 +119,7 @@ def lib() -> ctypes.CDLL:
         L.mx_op_service_stats.argtypes = [ctypes.POINTER(ctypes.c_ulonglong), ctypes.POINTER(ctypes.c_ulonglong)]
         L.mx_op_service_held.argtypes = [ctypes.POINTER(ctypes.c_ulonglong)]
         L.mx_debug_hold.argtypes = [vp, ctypes.c_uint]
+        L.mx_debug_hold_service.argtypes = [ctypes.c_uint]
         L._mx_typed = True
     return L
 
@@ -197,6 +198,11 @@ def debug_hold(stream: int, timeout_ms: int = 5000) -> None:
     """Test support: hold `stream`'s hardware queue with a spinning wave
     until debug_release() or timeout_ms."""
     check(lib().mx_debug_hold(stream, timeout_ms), "mx_debug_hold")
+
+
+def debug_hold_service(timeout_ms: int = 5000) -> None:
+    """Test support: hold the op service's own stream the same way."""
+    check(lib().mx_debug_hold_service(timeout_ms), "mx_debug_hold_service")
 
 
 def debug_release() -> None:
