@@ -6,14 +6,10 @@
 // call (profiles/r04/op_call_cost_r4_fused_default.txt): the host's launch,
 // the packet processor's dispatch and the wake-up, not the ~0.5 us of work.
 // The service removes the launch and the dispatch: one workgroup stays
-// resident on a non-blocking stream of its own and serves the calls of up to
-// kSvcMaxBytes that the host writes into coherent mapped host memory.  The
-// stream has ordinary priority: the high-priority hardware queues (4 per
-// process) belong to a communicator's spinning p2p channel and request
-// streams, and a fifth high-priority stream made a channel
-// stream share a queue with another -- a send queued behind its own
-// spinning receive (tests/test_op_service_gpu.py, Irecv; Reduce_local;
-// Send on two ranks).  Per call:
+// resident on a non-blocking stream of its own, at the least priority, whose
+// hardware queue nothing else of the process shares (svc_stream_create),
+// and serves the calls of up to kSvcMaxBytes that the host writes into
+// coherent mapped host memory.  Per call:
 //   * the host fills the command (operands, count) and raises its sequence
 //     number (a release store); the workgroup reads the 64-byte command
 //     line over PCIe;
@@ -315,15 +311,23 @@ void svc_atexit() {
   if (v.state == 1) svc_stop_locked(v);
 }
 
-// MX_SVC_PRIORITY=least|normal|greatest: the service stream's priority
-// (measurement switch; default normal)
+// The service stream takes the LEAST priority: HIP keeps a pool of hardware
+// queues per priority (range 1..-1 here: low, normal, high), and nothing
+// else of the process runs at low priority, so the service gets a queue of
+// its own -- not shared with the application's ordinary streams (whose
+// kernels would wait behind a resident service) nor with a communicator's
+// high-priority p2p channels (whose spinning receives would hold a
+// relaunch).  tools/svc_queue_probe.py: every ordinary and high-priority
+// queue held by spinning waves, 20 calls all served at low priority, held
+// at normal or high (profiles/r04/svc_queue_probe.txt).
+// MX_SVC_PRIORITY=normal|greatest: measurement switch.
 hipError_t svc_stream_create(hipStream_t *s) {
   const char *e = getenv("MX_SVC_PRIORITY");
   int least = 0, greatest = 0;
   if (hipDeviceGetStreamPriorityRange(&least, &greatest) != hipSuccess) least = greatest = 0;
-  if (e && !strcmp(e, "least")) return hipStreamCreateWithPriority(s, hipStreamNonBlocking, least);
+  if (e && !strcmp(e, "normal")) return hipStreamCreateWithFlags(s, hipStreamNonBlocking);
   if (e && !strcmp(e, "greatest")) return hipStreamCreateWithPriority(s, hipStreamNonBlocking, greatest);
-  return hipStreamCreateWithFlags(s, hipStreamNonBlocking);
+  return hipStreamCreateWithPriority(s, hipStreamNonBlocking, least);
 }
 
 int svc_setup(Service &v) {
