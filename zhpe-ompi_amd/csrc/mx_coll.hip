@@ -989,9 +989,15 @@ static bool fast_sync() {
   return v;
 }
 
-static int finish(mx_comm *c, hipStream_t s) {
+// mk: the completion flags the last kernel raises itself (mark_arm(&mk,
+// true) before its launch), else the marker kernel
+static int finish(mx_comm *c, hipStream_t s, const Mark *mk = nullptr) {
   if (c->defer) return MX_SUCCESS;   // request path: completion through the request's event
-  if (fast_sync() ? mx_stream_sync_fast(s) != MX_SUCCESS : hipStreamSynchronize(s) != hipSuccess) return MX_ERR_HIP;
+  if (mk && mk->flags) {
+    if (mark_wait(*mk, s) != MX_SUCCESS) return MX_ERR_HIP;
+  } else if (fast_sync() ? mx_stream_sync_fast(s) != MX_SUCCESS : hipStreamSynchronize(s) != hipSuccess) {
+    return MX_ERR_HIP;
+  }
   c->tail_valid = 0;                 // everything enqueued before is done
   if (!c->pending) prof_collect(c);
   if (c->err_host && *(volatile int *)c->err_host) {
@@ -1280,6 +1286,16 @@ static size_t chunk_elems(const mx_comm *c, size_t count, size_t es, bool gather
   return ce ? ce : 1;
 }
 
+// MX_OS_SELF_MARK=0: a blocking one-shot allreduce ends with the marker
+// kernel instead of raising its own completion flags (A/B switch)
+static bool os_self_mark() {
+  static const bool v = [] {
+    const char *e = getenv("MX_OS_SELF_MARK");
+    return !(e && *e == '0');
+  }();
+  return v;
+}
+
 // one-shot allreduce (small messages): one kernel, see k_oneshot
 static int allreduce_oneshot(mx_comm *c, oneshot_launch_fn ol, const std::vector<Seg> &segs, const char *sb,
                              char *rb, size_t count, size_t es, hipStream_t s) {
@@ -1319,11 +1335,15 @@ static int allreduce_oneshot(mx_comm *c, oneshot_launch_fn ol, const std::vector
   c->os_count += nwg;
   a.nseg = (int)segs.size();
   for (size_t i = 0; i < segs.size(); i++) a.seg[i] = OsSeg{segs[i].lo, segs[i].hi, segs[i].p};
+  Mark mk{nullptr, nullptr, 0};
+  if (!c->defer && fast_sync() && os_self_mark()) mark_arm(&mk, true);
+  a.mflags = mk.flags;
+  a.mv = mk.v;
   prof_begin(c, s);
   int rc = ol(a, (int)nwg, s);
   prof_end(c, s, 0, (double)(n + 1) * (double)bytes);
   if (rc) return rc;
-  return finish(c, s);
+  return finish(c, s, &mk);
 }
 
 // Autotuning: publish this rank's elapsed time of a trial call, return the

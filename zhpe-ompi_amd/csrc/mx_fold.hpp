@@ -218,6 +218,8 @@ struct OneShotArgs {
   int *poison;
   int n, rank, nseg;
   size_t count, es, slice;
+  uint64_t *mflags;             // the blocking call's completion flags (Mark.flags), or null
+  uint64_t mv;                  // their sequence number
   OsSeg seg[OS_MAXSEG];
 };
 
@@ -294,6 +296,18 @@ __global__ void __launch_bounds__(kOSB) k_oneshot(OneShotArgs a) {
       __threadfence_system();
       for (int p = 0; p < a.n; p++)
         if (p != a.rank) __hip_atomic_store(a.peer_done[p], a.gen, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+  }
+  // (7) a blocking call: every workgroup, once its stores of rb have landed,
+  // releases them at system scope and raises its own completion flag (the
+  // host waits for the grid's flags instead of a marker kernel, mark_wait)
+  if (a.mflags) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (t == 0 && w < (int)kMarkFlags) {
+      __threadfence_system();
+      __hip_atomic_store(a.mflags + w, (a.mv << 12) | (uint64_t)(gridDim.x - 1), __ATOMIC_RELAXED,
+                         __HIP_MEMORY_SCOPE_SYSTEM);
     }
   }
 }
