@@ -418,6 +418,22 @@ int svc_reduce(int op, int type, const void *in, const void *in2, void *inout, s
   uint64_t q = svc_post(v);
   for (unsigned k = 0;; k++) {
     if (__atomic_load_n(&v.host->done, __ATOMIC_ACQUIRE) >= q) { v.served++; return 1; }
+    if ((k & 0xfffff) == 0xfffff) {
+      // ~tens of ms without the word: a kernel that faulted or was killed
+      // writes neither `done` nor `left` -- the runtime reports it
+      const hipError_t e = hipStreamQuery(v.s);
+      if (e != hipSuccess && e != hipErrorNotReady) {
+        (void)hipGetLastError();
+        v.live = false;
+        v.state = -1;
+        return MX_ERR_HIP;
+      }
+      if (e == hipSuccess && __atomic_load_n(&v.host->done, __ATOMIC_ACQUIRE) < q && !svc_gone(v, v.epoch)) {
+        v.live = false;                        // gone without a word: inout unknown, no retry
+        v.state = -1;
+        return MX_ERR_HIP;
+      }
+    }
     if ((k & 15) == 15 && svc_gone(v, v.epoch)) {
       // it left before taking q (or took it: done is final once left shows)
       if (__atomic_load_n(&v.host->done, __ATOMIC_ACQUIRE) >= q) { v.served++; return 1; }
