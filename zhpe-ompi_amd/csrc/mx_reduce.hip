@@ -140,6 +140,49 @@ __global__ void __launch_bounds__(BS) k_reduce2_w32(const T *__restrict__ a, T *
   mark_done(mk);
 }
 
+// The same through LDS: the workgroup's BS elements (2*BS 16-byte vectors
+// per operand) are loaded with consecutive lanes on consecutive vectors --
+// every wave instruction reads / writes whole lines, where the per-element
+// form's two accesses 32 bytes apart each touch half of every line -- then
+// lane t takes element t from LDS.
+template <class T, class OP, bool NT, int BS>
+__global__ void __launch_bounds__(BS) k_reduce2_w32t(const T *__restrict__ a, T *__restrict__ b, size_t n, Mark mk) {
+  static_assert(sizeof(T) == 32, "32-byte elements");
+  __shared__ u32x4 sa[2 * BS], sb[2 * BS];
+  const size_t e0 = (size_t)blockIdx.x * BS;
+  const unsigned nel = (unsigned)(n - e0 < (size_t)BS ? n - e0 : (size_t)BS);
+  const unsigned nv = 2 * nel;
+  const u32x4 *pa = reinterpret_cast<const u32x4 *>(a + e0);
+  u32x4 *pb = reinterpret_cast<u32x4 *>(b + e0);
+  const unsigned t = threadIdx.x;
+#pragma unroll
+  for (int k = 0; k < 2; k++) {
+    const unsigned v = t + k * BS;
+    if (v < nv) {
+      if constexpr (NT) { sa[v] = __builtin_nontemporal_load(pa + v); sb[v] = __builtin_nontemporal_load(pb + v); }
+      else { sa[v] = pa[v]; sb[v] = pb[v]; }
+    }
+  }
+  __syncthreads();
+  if (t < nel) {
+    T x, y;
+    __builtin_memcpy(&x, &sb[2 * t], 32);
+    __builtin_memcpy(&y, &sa[2 * t], 32);
+    store_fields(&x, OP()(x, y));
+    __builtin_memcpy(&sb[2 * t], &x, 32);
+  }
+  __syncthreads();
+#pragma unroll
+  for (int k = 0; k < 2; k++) {
+    const unsigned v = t + k * BS;
+    if (v < nv) {
+      if constexpr (NT) __builtin_nontemporal_store(sb[v], pb + v);
+      else pb[v] = sb[v];
+    }
+  }
+  mark_done(mk);
+}
+
 // 2-buffer, one element per lane (mismatched alignment, or element > 16 B).
 template <class T, class OP>
 __global__ void __launch_bounds__(kBlock)
@@ -205,6 +248,16 @@ static bool conv_w32() {
   return on != 0;
 }
 
+// MX_REDUCE_W32T=0: 32-byte elements move per element (two accesses 32
+// bytes apart) instead of through LDS (A/B switch; results are identical)
+static bool w32_lds() {
+  static const int on = [] {
+    const char *e = getenv("MX_REDUCE_W32T");
+    return (e && *e == '0') ? 0 : 1;
+  }();
+  return on != 0;
+}
+
 // launches that carry their own completion mark: grids of at most
 // kMarkFlags workgroups.  Every launch mx_reduce2_sync makes for count
 // elements has at most ceil((count + 16) / 256) workgroups (one 16-byte
@@ -239,11 +292,20 @@ static int launch2(const void *in, void *inout, size_t n, hipStream_t s, const M
   const uintptr_t ma = (uintptr_t)a & 15, mb = (uintptr_t)b & 15;
   if constexpr (sizeof(T) == 32) {
     if (ma == 0 && mb == 0 && conv_w32()) {
-      if (mx_nt_for(2 * n * sizeof(T)) && nt_small_wg(n))
+      const bool nt = mx_nt_for(2 * n * sizeof(T)) && nt_small_wg(n);
+      if (w32_lds()) {
+        if (nt)
+          hipLaunchKernelGGL((k_reduce2_w32t<T, OP, true, kBlockNT>), dim3(grid_for(n, kBlockNT)), dim3(kBlockNT), 0,
+                             s, a, b, n, mk);
+        else
+          hipLaunchKernelGGL((k_reduce2_w32t<T, OP, false, kBlock>), dim3(grid_for(n)), dim3(kBlock), 0, s, a, b, n,
+                             mk);
+      } else if (nt) {
         hipLaunchKernelGGL((k_reduce2_w32<T, OP, true, kBlockNT>), dim3(grid_for(n, kBlockNT)), dim3(kBlockNT), 0, s,
                            a, b, n, mk);
-      else
+      } else {
         hipLaunchKernelGGL((k_reduce2_w32<T, OP, false, kBlock>), dim3(grid_for(n)), dim3(kBlock), 0, s, a, b, n, mk);
+      }
       return mx_check_launch();
     }
   }
