@@ -1,11 +1,11 @@
 """The resident reduce service behind mx_reduce2_sync (round 4,
-csrc/mx_service.hip): calls of <= 128 KiB on a non-default stream are
-served by a one-workgroup kernel that stays resident instead of a launch per
-call.
+csrc/mx_service.hip): calls of <= 2 MiB on a non-default stream are served
+by a kernel that stays resident instead of a launch per call -- workgroup 0
+alone up to 64 KiB, the whole grid above.
 
 Bit-exact vs the op oracle (op_base_functions.c restated; op values
 parity-unpinned) for every element family the service takes, at
-ragged sizes up to its 128 KiB cap; pairs interleaved (the service is rebound
+ragged sizes up to its 2 MiB cap and either side of the 64 KiB solo bound; pairs interleaved (the service is rebound
 to each pair), pauses longer than its 100 us idle exit (relaunch), a call over
 the cap and a misaligned call (launch path), and the per-call counters show
 which calls the service took; a relaunch behind a held hardware queue
@@ -24,7 +24,8 @@ pytestmark = pytest.mark.gpu
 
 PAIRS = [("SUM", "FLOAT"), ("MAX", "DOUBLE"), ("BXOR", "UINT16_T"), ("MAXLOC", "FLOAT_INT"),
          ("PROD", "C_FLOAT_COMPLEX"), ("LAND", "BOOL"), ("MIN", "INT8_T"), ("SUM", "INT64_T")]
-SVC_MAX = 128 << 10          # kSvcMaxBytes
+SVC_MAX = 2 << 20            # kSvcMaxBytes
+SVC_SOLO = 64 << 10          # kSvcSoloBytes: above, the whole grid takes the command
 
 
 def _gen(op, t, count, seed):
@@ -71,7 +72,8 @@ def test_service_serves_and_matches_the_oracle():
     for rnd in range(2):
         for op, t in PAIRS:
             es = mxompi.type_size(t)
-            for count in (1, 17, 1000, 4099, (64 << 10) // es + 3, SVC_MAX // es):
+            for count in (1, 17, 1000, 4099, SVC_SOLO // es, SVC_SOLO // es + 1, (256 << 10) // es + 3,
+                          SVC_MAX // es):
                 _check(op, t, count, 100 * rnd + count, s)
                 calls += 1
         time.sleep(0.01)                               # > the 100 us idle exit: the next call relaunches
@@ -81,20 +83,21 @@ def test_service_serves_and_matches_the_oracle():
     assert launches - launches0 >= 2 * len(PAIRS)      # rebound to every pair, every round
     # not served: over the cap, misaligned buffers
     _check("SUM", "FLOAT", SVC_MAX // 4 + 4, 7, s)
-    _check("SUM", "FLOAT", (1 << 20) // 4, 9, s)
+    _check("SUM", "FLOAT", (8 << 20) // 4, 9, s)
     _check("SUM", "FLOAT", 5000, 8, s, off=4)
     O = oracle_lib.oracle()
     assert mxompi.op_service_stats()[1] == served
     del O
 
 
-def test_service_back_to_back_same_buffers():
+@pytest.mark.parametrize("n", [4096, 16384, 262144], ids=["32KiB_solo", "128KiB_grid", "2MiB_grid"])
+def test_service_back_to_back_same_buffers(n):
     """A segmented-ring-like sequence: 500 calls on the same buffers, each
     folding the previous result -- every call must see the last one's result
-    (the service's acquire after a command, its release before done)."""
+    (the service's acquire after a command, its release before done), by
+    workgroup 0 alone and by the whole grid."""
     mxompi.init(0)
     s = torch.cuda.Stream()
-    n = 16384              # 128 KiB: the service cap
     a = torch.ones(n, dtype=torch.int64, device="cuda")
     b = torch.zeros(n, dtype=torch.int64, device="cuda")
     torch.cuda.synchronize()
@@ -109,7 +112,7 @@ def test_service_back_to_back_same_buffers():
 
 def test_service_three_buffer_form():
     """mx_reduce3_sync (the op component's 3-buffer handler): out = in1 OP in2
-    through the service (aligned, <= 128 KiB) and through the launch (misaligned
+    through the service (aligned, <= 2 MiB) and through the launch (misaligned
     or larger),
     bit-exact vs the oracle's 3-buffer functions, out read straight after."""
     mxompi.init(0)

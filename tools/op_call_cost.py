@@ -2,7 +2,7 @@
 """Cost of one ompi_op_reduce call through op/mi355x (the coll/base segmented
 ring calls it once per 1 MiB segment, coll_base_allreduce.c:782), measured
 through the mini-host's op table on device buffers, fp32 SUM, at 4 KiB
-to 1 MiB.  One process per configuration (the pointer-cache switch
+to 4 MiB.  One process per configuration (the pointer-cache switch
 is read once per process):
 
   round1   MX_PTR_CACHE=0, op_mi355x_stream=0: hipPointerGetAttributes x2 per
@@ -34,7 +34,7 @@ CONFIGS = {"round1": {"MX_PTR_CACHE": "0", "OMPI_MCA_op_mi355x_stream": "0"},
                         "MX_FUSED_MARK": "1", "MX_OP_SERVICE": "0"},
            "service": {"MX_PTR_CACHE": "1", "OMPI_MCA_op_mi355x_stream": "1", "OMPI_MCA_op_mi355x_fast_sync": "1",
                        "MX_FUSED_MARK": "1", "MX_OP_SERVICE": "1"}}
-SIZES = [4 << 10, 16 << 10, 64 << 10, 128 << 10, 256 << 10, 1 << 20]
+SIZES = [4 << 10, 16 << 10, 64 << 10, 128 << 10, 256 << 10, 1 << 20, 2 << 20, 4 << 20]
 
 
 def child(cfg):

@@ -2,35 +2,38 @@
 // synchronous calls (ompi_op_reduce on device buffers, ompi/op/op.h:547-610,
 // op/mi355x's 2- and 3-buffer handlers; round 4).
 //
-// A blocking ompi_op_reduce of a few KiB costs ~7.3 us with a launch per
-// call (profiles/r04/op_call_cost_r4_fused_default.txt): the host's launch,
-// the packet processor's dispatch and the wake-up, not the ~0.5 us of work.
-// The service removes the launch and the dispatch: one workgroup stays
-// resident on a non-blocking stream of its own, at the least priority, whose
-// hardware queue nothing else of the process shares (svc_stream_create),
-// and serves the calls of up to kSvcMaxBytes that the host writes into
-// coherent mapped host memory.  Per call:
+// A blocking ompi_op_reduce of a few KiB costs ~7 us with a launch per call
+// (profiles/r04/op_call_cost_r4_fused_default.txt): the host's launch, the
+// packet processor's dispatch and the wake-up, not the ~0.5 us of work.  The
+// service removes the launch and the dispatch: a grid of kSvcGrid workgroups
+// stays resident on a non-blocking stream of its own, at the least priority,
+// whose hardware queue nothing else of the process shares
+// (svc_stream_create), and serves the calls of up to kSvcMaxBytes that the
+// host writes into coherent mapped host memory.  Per call:
 //   * the host fills the command (operands, count) and raises its sequence
-//     number (a release store); the workgroup reads the 64-byte command
-//     line over PCIe;
-//   * it takes a system-scope acquire (stale operand lines dropped: the
-//     service never passes a kernel boundary), reduces with the op kernels'
-//     element functors, waits for its stores, releases at system scope and
-//     raises the done word in mapped host memory, which the host polls --
-//     the completion contract of mx_reduce2_sync (inout final for every
-//     agent on return).
+//     number (a release store); workgroup 0 reads the 64-byte command line
+//     over PCIe;
+//   * up to kSvcSoloBytes workgroup 0 serves it alone: a system-scope
+//     acquire (stale operand lines dropped: the service never passes a
+//     kernel boundary), the op kernels' element functors, a wait for its
+//     stores, a system-scope release and the done word in mapped host
+//     memory, which the host polls -- mx_reduce2_sync's completion contract
+//     (inout final for every agent on return);
+//   * above, it broadcasts the command through device memory to the helper
+//     workgroups, which sleep between polls; every workgroup takes a share
+//     and raises its own flag after its release, and the host waits for all.
 // One service per process, bound to one (op, type) at a time (a kernel per
 // pair, like the op kernels); a call for another pair stops it and starts
 // that pair's.  It leaves by itself after kSvcIdleS without a command, and
-// between commands once kSvcLifeS old, so it holds its CU only while calls
-// keep coming and never holds its hardware queue for long: the streams that
-// share that queue wait at most that long behind it.  The host relaunches it on demand, waits until it runs and
-// only then posts -- a launched kernel takes only the commands after the
-// last one posted, so a command never runs twice; one that does not start
-// within kSvcStartUs (its queue held by a kernel that may wait for this
-// very thread) is told to leave and the call launches instead, as do
-// the calls after it until that kernel has left.  At exit the host stops
-// the kernel (atexit), so the grid has drained before the process ends.
+// between commands once kSvcLifeS old, so it holds its CUs only while calls
+// keep coming and never holds its hardware queue for long.  The host
+// relaunches it on demand, waits until it runs and only then posts -- a
+// launched kernel takes only the commands after the last one posted, so a
+// command never runs twice; one that does not start within kSvcStartUs (its
+// queue held by a kernel that may wait for this very thread) is told to
+// leave and the call launches instead, as do the calls after it until that
+// kernel has left.  At exit the host stops the kernel (atexit), so the grid
+// has drained before the process ends.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include <stdlib.h>
@@ -49,7 +52,11 @@ namespace mx {
 constexpr int kSvcB = 256;                 // lanes of the one resident workgroup (4 waves; 16 waves cost
                                            // ~1 us more per command, svc_pingpong_probe mode 9)
 constexpr int kSvcU = 8;                   // 16-byte vectors in flight per lane and operand
-constexpr size_t kSvcMaxBytes = 128 << 10; // calls up to 128 KiB per buffer (one CU's share; larger: launches)
+constexpr size_t kSvcMaxBytes = 2 << 20;   // calls up to 2 MiB per buffer (larger: launches, faster from
+                                           // ~3 MiB on: profiles/r04/svc_grid_ab.txt)
+constexpr size_t kSvcSoloBytes = 64 << 10; // up to 64 KiB workgroup 0 alone; above, the whole grid
+constexpr unsigned kSvcGridMax = 64;       // workgroups at most: 0 serves the host, the rest join large commands
+constexpr unsigned kSvcGrid = 32;          // (default)
 constexpr double kSvcIdleS = 100e-6;      // leave after 100 us without a command
 constexpr double kSvcLifeS = 1e-3;         // and between commands once 1 ms old (then relaunched)
 constexpr double kSvcStartUs = 1000;       // a kernel not running 1 ms after its launch is held
@@ -63,6 +70,10 @@ struct alignas(64) SvcCmd {                // coherent mapped host memory, writt
   uint64_t chk;                            // svc_chk of the words above seq: a torn read never matches
 };
 static_assert(sizeof(SvcCmd) == 64, "one line");
+struct alignas(64) SvcBcast {              // device memory (uncached): workgroup 0 -> the helpers
+  uint64_t tag;                            // (launch epoch << 32) | broadcast number, written last
+  uint64_t q, in, inout, in2, count, exit, pad;
+};
 struct alignas(64) SvcHost {               // mapped host memory, written by the kernel
   uint64_t done;                           // last command completed
   uint64_t running;                        // launch epoch the kernel reported at start
@@ -101,18 +112,135 @@ __device__ __forceinline__ void svc_read_cmd(const SvcCmd *c, uint64_t w[8]) {
   for (int k = 0; k < 8; k++) w[k] = __shfl(x, k);
 }
 
-// One workgroup, resident.  Measured on the box (tools/svc_pingpong_probe,
+// workgroup w of nwg: its share of inout = inout OP in (2-buffer, the op
+// kernels' K1) or out = in1 OP in2 (3-buffer, K2) -- 16-byte vectors
+// w*kSvcB + t + j*nwg*kSvcB, kSvcU of them per operand in flight, then the
+// elements past the last whole vector
+template <class T, class OP, class OP3>
+__device__ __forceinline__ void svc_work(uint64_t in, uint64_t inout, uint64_t in2, size_t n, unsigned w,
+                                         unsigned nwg) {
+  const T *a = reinterpret_cast<const T *>(in);
+  T *b = reinterpret_cast<T *>(inout);
+  constexpr size_t N = 16 / sizeof(T);
+  struct alignas(16) V { T e[N]; };
+  const size_t nvec = n / N;
+  const size_t st = (size_t)nwg * kSvcB;
+  const V *va = reinterpret_cast<const V *>(a);
+  V *vb = reinterpret_cast<V *>(b);
+  size_t i = (size_t)w * kSvcB + threadIdx.x;
+  if (!in2) {
+    OP op;
+    for (; i + (kSvcU - 1) * st < nvec; i += kSvcU * st) {
+      V x[kSvcU], y[kSvcU];
+#pragma unroll
+      for (int u = 0; u < kSvcU; u++) {
+        ld16<false>(x[u], vb + i + u * st);
+        ld16<false>(y[u], va + i + u * st);
+      }
+#pragma unroll
+      for (int u = 0; u < kSvcU; u++) {
+#pragma unroll
+        for (size_t j = 0; j < N; j++) store_fields(&x[u].e[j], op(x[u].e[j], y[u].e[j]));
+        st16<false>(vb + i + u * st, x[u]);
+      }
+    }
+    for (; i < nvec; i += st) {
+      V x, y;
+      ld16<false>(x, vb + i);
+      ld16<false>(y, va + i);
+#pragma unroll
+      for (size_t j = 0; j < N; j++) store_fields(&x.e[j], op(x.e[j], y.e[j]));
+      st16<false>(vb + i, x);
+    }
+    for (size_t k = nvec * N + (size_t)w * kSvcB + threadIdx.x; k < n; k += st) store_fields(&b[k], op(b[k], a[k]));
+  } else {
+    OP3 op;
+    const T *a2 = reinterpret_cast<const T *>(in2);
+    const V *va2 = reinterpret_cast<const V *>(a2);
+    for (; i + (kSvcU - 1) * st < nvec; i += kSvcU * st) {
+      V x[kSvcU], y[kSvcU];
+#pragma unroll
+      for (int u = 0; u < kSvcU; u++) {
+        ld16<false>(x[u], va + i + u * st);
+        ld16<false>(y[u], va2 + i + u * st);
+      }
+#pragma unroll
+      for (int u = 0; u < kSvcU; u++) {
+#pragma unroll
+        for (size_t j = 0; j < N; j++) x[u].e[j] = op(x[u].e[j], y[u].e[j]);
+        st16<false>(vb + i + u * st, x[u]);
+      }
+    }
+    for (; i < nvec; i += st) {
+      V x, y;
+      ld16<false>(x, va + i);
+      ld16<false>(y, va2 + i);
+#pragma unroll
+      for (size_t j = 0; j < N; j++) x.e[j] = op(x.e[j], y.e[j]);
+      st16<false>(vb + i, x);
+    }
+    for (size_t k = nvec * N + (size_t)w * kSvcB + threadIdx.x; k < n; k += st) b[k] = op(a[k], a2[k]);
+  }
+}
+
+// The grid: workgroup 0 serves the host; the helpers 1..nwg-1 join the
+// large commands.  Measured on the box (tools/svc_pingpong_probe,
 // profiles/r04/svc_pingpong_*.txt): a host -> kernel -> host round trip with
 // the service's fences and a 4 KiB reduce costs ~3.5 us; 63 more resident
-// workgroups polling a device word for broadcasts add ~1.9 us to every
-// command (the service's first form), so the service is one CU's: the calls
-// it takes are the small ones, where the launch is the cost.
+// workgroups polling a device word between 64-clock sleeps add ~1.9 us to
+// every command, with 127 x 64-clock sleeps nothing.  So a command up to
+// solo_max bytes is workgroup 0's alone (one release, the host's `done`
+// word); a larger one is broadcast through device memory and every
+// workgroup takes a share and raises its own flag in mapped host memory
+// (`flags[w] = (q << 12) | (nwg - 1)`, the launch marks' format).  Leaving
+// (a host EXIT, idle, lifetime) is broadcast too, so the helpers never
+// outlive workgroup 0's decision.
 template <class T, class OP, class OP3>
-__global__ void __launch_bounds__(kSvcB) k_svc(const SvcCmd *cmd, SvcHost *host, uint64_t last, uint64_t epoch,
-                                               uint64_t idle_ticks, uint64_t life_ticks) {
+__global__ void __launch_bounds__(kSvcB) k_svc(const SvcCmd *cmd, SvcHost *host, uint64_t *flags, SvcBcast *bc,
+                                               uint64_t *acks, uint64_t last, uint64_t epoch, uint64_t idle_ticks,
+                                               uint64_t life_ticks, uint64_t solo_max, int hsleep) {
   __shared__ uint64_t s_in, s_inout, s_count, s_q, s_in2;
-  __shared__ int s_exit;
+  __shared__ int s_exit, s_bcast;
+  const unsigned nwg = gridDim.x;
+  if (blockIdx.x > 0) {                    // helper: the broadcasts of this launch, in order
+    for (uint64_t k = 1;; k++) {
+      if (threadIdx.x == 0) {
+        const uint64_t want = (epoch << 32) | k;
+        while (__hip_atomic_load(&bc->tag, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) != want) {
+          switch (hsleep) {                // s_sleep takes an immediate
+            case 0: __builtin_amdgcn_s_sleep(8); break;
+            case 1: __builtin_amdgcn_s_sleep(32); break;
+            case 2: __builtin_amdgcn_s_sleep(64); break;
+            default: __builtin_amdgcn_s_sleep(127); break;
+          }
+        }
+        s_q = bc->q;
+        s_in = bc->in;
+        s_inout = bc->inout;
+        s_in2 = bc->in2;
+        s_count = bc->count;
+        s_exit = bc->exit != 0;
+        __atomic_thread_fence(__ATOMIC_ACQUIRE);   // system scope: stale operand lines dropped
+      }
+      __syncthreads();
+      if (s_exit) return;
+      svc_work<T, OP, OP3>(s_in, s_inout, s_in2, s_count, blockIdx.x, nwg);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this wave's stores reached L2
+      __syncthreads();
+      if (threadIdx.x == 0) {
+        // the ack first (workgroup 0 reads it before it may broadcast
+        // again), then the release, then the host's flag
+        __hip_atomic_store(acks + blockIdx.x, (epoch << 32) | k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __threadfence_system();            // release: this XCD's L2 written back
+        __hip_atomic_store(flags + blockIdx.x, (s_q << 12) | (uint64_t)(nwg - 1), __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_SYSTEM);
+      }
+      __syncthreads();                     // s_* are rewritten next round
+    }
+  }
   uint64_t seen = last;                    // command sequence number taken last (wave 0)
+  uint64_t nb = 0;                         // broadcasts of this launch (wave 0)
+  uint64_t kc = 0;                         // the last command broadcast's number (wave 0)
   const uint64_t born = wall_clock64();
   if (threadIdx.x == 0)
     __hip_atomic_store(&host->running, epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
@@ -128,18 +256,48 @@ __global__ void __launch_bounds__(kSvcB) k_svc(const SvcCmd *cmd, SvcHost *host,
         if (now - t0 > idle_ticks || now - born > life_ticks) { ex = 1; break; }
         __builtin_amdgcn_s_sleep(1);
       }
-      if (threadIdx.x == 0) s_exit = ex;
       if (!ex) seen = w[0];
-      if (threadIdx.x == 0 && !ex) {
-        s_q = w[1];
-        s_in = w[2];
-        s_inout = w[3];
-        s_in2 = w[4];
-        s_count = w[5];
-        s_exit = w[6] != 0;
+      const bool exit_now = ex || w[6] != 0;
+      const bool bc_now = !exit_now && nwg > 1 && w[5] * sizeof(T) > solo_max;
+      if (nwg > 1 && ex && kc) {
+        // no broadcast overwrites the last command's before every helper has
+        // acknowledged it.  The host posts a command (or EXIT) only once
+        // every flag of the last one is up, so only a leaving decision of
+        // this workgroup's own (lifetime, idle) can come while a slow helper
+        // has not even read it.
+        const unsigned lane = threadIdx.x;
+        for (;;) {
+          const bool ok = lane == 0 || lane >= nwg ||
+                          __hip_atomic_load(acks + lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
+                              ((epoch << 32) | kc);
+          if (__all(ok)) break;
+          __builtin_amdgcn_s_sleep(1);
+        }
+      }
+      if (bc_now) kc = nb + 1;
+      if (nwg > 1 && (exit_now || bc_now)) nb++;
+      if (threadIdx.x == 0) {
+        s_exit = exit_now;
+        if (!ex) {
+          s_q = w[1];
+          s_in = w[2];
+          s_inout = w[3];
+          s_in2 = w[4];
+          s_count = w[5];
+        }
+        s_bcast = bc_now;
+        if (nwg > 1 && (exit_now || bc_now)) {   // the helpers take part (or leave)
+          bc->q = s_q;
+          bc->in = s_in;
+          bc->inout = s_inout;
+          bc->in2 = s_in2;
+          bc->count = s_count;
+          bc->exit = exit_now;
+          __hip_atomic_store(&bc->tag, (epoch << 32) | nb, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+        }
         // system-scope acquire: stale operand lines dropped from this CU's
         // caches and its XCD's L2 (the service never passes a kernel boundary)
-        __atomic_thread_fence(__ATOMIC_ACQUIRE);
+        if (!s_exit) __atomic_thread_fence(__ATOMIC_ACQUIRE);
       }
     }
     __syncthreads();
@@ -148,84 +306,30 @@ __global__ void __launch_bounds__(kSvcB) k_svc(const SvcCmd *cmd, SvcHost *host,
         __hip_atomic_store(&host->left, epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
       return;
     }
-    const T *a = reinterpret_cast<const T *>(s_in);
-    T *b = reinterpret_cast<T *>(s_inout);
-    const size_t n = s_count;
-    constexpr size_t N = 16 / sizeof(T);
-    struct alignas(16) V { T e[N]; };
-    const size_t nvec = n / N;
-    const V *va = reinterpret_cast<const V *>(a);
-    V *vb = reinterpret_cast<V *>(b);
-    if (!s_in2) {                          // 2-buffer: inout = inout OP in (the op kernels' K1)
-      OP op;
-      size_t i = threadIdx.x;
-      for (; i + (kSvcU - 1) * kSvcB < nvec; i += kSvcU * kSvcB) {   // kSvcU vectors per operand in flight
-        V x[kSvcU], y[kSvcU];
-#pragma unroll
-        for (int u = 0; u < kSvcU; u++) {
-          ld16<false>(x[u], vb + i + u * kSvcB);
-          ld16<false>(y[u], va + i + u * kSvcB);
-        }
-#pragma unroll
-        for (int u = 0; u < kSvcU; u++) {
-#pragma unroll
-          for (size_t j = 0; j < N; j++) store_fields(&x[u].e[j], op(x[u].e[j], y[u].e[j]));
-          st16<false>(vb + i + u * kSvcB, x[u]);
-        }
-      }
-      for (; i < nvec; i += kSvcB) {
-        V x, y;
-        ld16<false>(x, vb + i);
-        ld16<false>(y, va + i);
-#pragma unroll
-        for (size_t j = 0; j < N; j++) store_fields(&x.e[j], op(x.e[j], y.e[j]));
-        st16<false>(vb + i, x);
-      }
-      for (size_t k = nvec * N + threadIdx.x; k < n; k += kSvcB) store_fields(&b[k], op(b[k], a[k]));
-    } else {                               // 3-buffer: out = in1 OP in2 (K2)
-      OP3 op;
-      const T *a2 = reinterpret_cast<const T *>(s_in2);
-      const V *va2 = reinterpret_cast<const V *>(a2);
-      size_t i = threadIdx.x;
-      for (; i + (kSvcU - 1) * kSvcB < nvec; i += kSvcU * kSvcB) {
-        V x[kSvcU], y[kSvcU];
-#pragma unroll
-        for (int u = 0; u < kSvcU; u++) {
-          ld16<false>(x[u], va + i + u * kSvcB);
-          ld16<false>(y[u], va2 + i + u * kSvcB);
-        }
-#pragma unroll
-        for (int u = 0; u < kSvcU; u++) {
-#pragma unroll
-          for (size_t j = 0; j < N; j++) x[u].e[j] = op(x[u].e[j], y[u].e[j]);
-          st16<false>(vb + i + u * kSvcB, x[u]);
-        }
-      }
-      for (; i < nvec; i += kSvcB) {
-        V x, y;
-        ld16<false>(x, va + i);
-        ld16<false>(y, va2 + i);
-#pragma unroll
-        for (size_t j = 0; j < N; j++) x.e[j] = op(x.e[j], y.e[j]);
-        st16<false>(vb + i, x);
-      }
-      for (size_t k = nvec * N + threadIdx.x; k < n; k += kSvcB) b[k] = op(a[k], a2[k]);
-    }
+    const bool bcast = s_bcast;
+    svc_work<T, OP, OP3>(s_in, s_inout, s_in2, s_count, 0, bcast ? nwg : 1);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this wave's stores reached L2
     __syncthreads();
     if (threadIdx.x == 0) {
       __threadfence_system();              // release: this XCD's L2 written back
-      __hip_atomic_store(&host->done, s_q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      if (bcast)
+        __hip_atomic_store(flags, (s_q << 12) | (uint64_t)(nwg - 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      else
+        __hip_atomic_store(&host->done, s_q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     }
+    __syncthreads();                       // s_* are rewritten next round
   }
 }
 
-typedef void (*svc_launch_fn)(const SvcCmd *, SvcHost *, uint64_t, uint64_t, uint64_t, uint64_t, hipStream_t);
+typedef void (*svc_launch_fn)(const SvcCmd *, SvcHost *, uint64_t *, SvcBcast *, uint64_t *, uint64_t, uint64_t,
+                              uint64_t, uint64_t, uint64_t, int, unsigned, hipStream_t);
 
 template <class T, class OP, class OP3>
-static void svc_launch(const SvcCmd *c, SvcHost *h, uint64_t last, uint64_t epoch, uint64_t idle, uint64_t life,
+static void svc_launch(const SvcCmd *c, SvcHost *h, uint64_t *f, SvcBcast *bc, uint64_t *acks, uint64_t last,
+                       uint64_t epoch, uint64_t idle, uint64_t life, uint64_t solo, int hsleep, unsigned grid,
                        hipStream_t s) {
-  hipLaunchKernelGGL((k_svc<T, OP, OP3>), dim3(1), dim3(kSvcB), 0, s, c, h, last, epoch, idle, life);
+  hipLaunchKernelGGL((k_svc<T, OP, OP3>), dim3(grid), dim3(kSvcB), 0, s, c, h, f, bc, acks, last, epoch, idle, life,
+                     solo, hsleep);
 }
 
 // pairs served: element types that tile 16-byte vectors with no bytes
@@ -246,6 +350,12 @@ struct Service {
   SvcCmd *cmd_d = nullptr;
   SvcHost *host = nullptr, *host_d = nullptr;
   hipStream_t s = nullptr;
+  uint64_t *flags = nullptr, *flags_d = nullptr;   // per-workgroup flags (mapped host memory, kSvcGridMax)
+  SvcBcast *bc = nullptr;                          // workgroup 0 -> helpers (device, uncached)
+  uint64_t *acks = nullptr;                        // helpers -> workgroup 0 (device, uncached, kSvcGridMax)
+  unsigned grid = kSvcGrid;
+  uint64_t solo = kSvcSoloBytes;
+  int hsleep = 2;         // helpers' sleep between polls: 8 / 32 / 64 / 127 x 64 clocks
   uint64_t seq = 0;       // commands posted
   uint64_t epoch = 0;     // launches
   bool live = false;      // a kernel is running and has not been seen to leave
@@ -345,12 +455,29 @@ int svc_setup(Service &v) {
       hipHostGetDevicePointer((void **)&v.cmd_d, v.cmd, 0) != hipSuccess ||
       hipHostMalloc((void **)&v.host, sizeof(SvcHost), hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess ||
       hipHostGetDevicePointer((void **)&v.host_d, v.host, 0) != hipSuccess ||
-      svc_stream_create(&v.s) != hipSuccess) {   // no device-wide sync: other streams may hold spinning kernels
+      hipHostMalloc((void **)&v.flags, kSvcGridMax * sizeof(uint64_t), hipHostMallocMapped | hipHostMallocCoherent) !=
+          hipSuccess ||
+      hipHostGetDevicePointer((void **)&v.flags_d, v.flags, 0) != hipSuccess ||
+      hipExtMallocWithFlags((void **)&v.bc, sizeof(SvcBcast), hipDeviceMallocUncached) != hipSuccess ||
+      hipExtMallocWithFlags((void **)&v.acks, kSvcGridMax * sizeof(uint64_t), hipDeviceMallocUncached) !=
+          hipSuccess ||
+      svc_stream_create(&v.s) != hipSuccess ||   // no device-wide sync: other streams may hold spinning kernels
+      hipMemsetAsync(v.bc, 0, sizeof(SvcBcast), v.s) != hipSuccess ||
+      hipMemsetAsync(v.acks, 0, kSvcGridMax * sizeof(uint64_t), v.s) != hipSuccess) {
     (void)hipGetLastError();
     return -1;
   }
   memset(v.cmd, 0, sizeof(SvcCmd));
   memset(v.host, 0, sizeof(SvcHost));
+  memset(v.flags, 0, kSvcGridMax * sizeof(uint64_t));
+  // MX_SVC_GRID (1..kSvcGridMax workgroups), MX_SVC_SOLO (bytes workgroup 0
+  // takes alone), MX_SVC_HSLEEP (0..3): measurement switches
+  if (const char *e = getenv("MX_SVC_GRID")) {
+    const long g = atol(e);
+    v.grid = g < 1 ? 1 : g > (long)kSvcGridMax ? kSvcGridMax : (unsigned)g;
+  }
+  if (const char *e = getenv("MX_SVC_HSLEEP")) v.hsleep = atoi(e);
+  if (const char *e = getenv("MX_SVC_SOLO")) v.solo = (uint64_t)atoll(e);
   atexit(svc_atexit);
   return 1;
 }
@@ -365,7 +492,8 @@ int svc_setup(Service &v) {
 // starts (an EXIT command it will read first) and calls launch until it has.
 static bool svc_start(Service &v, svc_launch_fn fn) {
   const uint64_t ep = ++v.epoch;
-  fn(v.cmd_d, v.host_d, v.seq, ep, v.idle_ticks, v.life_ticks, v.s);
+  fn(v.cmd_d, v.host_d, v.flags_d, v.bc, v.acks, v.seq, ep, v.idle_ticks, v.life_ticks, v.solo, v.hsleep, v.grid,
+     v.s);
   if (hipGetLastError() != hipSuccess) { v.state = -1; return false; }
   const bool first = std::find(v.started.begin(), v.started.end(), fn) == v.started.end();
   if (svc_poll(&v.host->running, ep, first ? kSvcFirstStartUs : kSvcStartUs)) {
@@ -415,9 +543,20 @@ int svc_reduce(int op, int type, const void *in, const void *in2, void *inout, s
   v.cmd->count = count;
   v.cmd->in2 = (uint64_t)(uintptr_t)in2;
   v.cmd->exit = 0;
+  // the kernel makes the same choice (count * sizeof(T) > solo): a large
+  // command completes through every workgroup's flag, a small one through
+  // workgroup 0's `done`
+  const bool bcast = v.grid > 1 && count * es > v.solo;
+  auto finished = [&](uint64_t q) {
+    if (!bcast) return __atomic_load_n(&v.host->done, __ATOMIC_ACQUIRE) >= q;
+    for (unsigned w = 0; w < v.grid; w++)
+      if ((__atomic_load_n(v.flags + w, __ATOMIC_RELAXED) >> 12) < q) return false;
+    __atomic_thread_fence(__ATOMIC_ACQUIRE);
+    return true;
+  };
   uint64_t q = svc_post(v);
   for (unsigned k = 0;; k++) {
-    if (__atomic_load_n(&v.host->done, __ATOMIC_ACQUIRE) >= q) { v.served++; return 1; }
+    if (finished(q)) { v.served++; return 1; }
     if ((k & 0xfffff) == 0xfffff) {
       // ~tens of ms without the word: a kernel that faulted or was killed
       // writes neither `done` nor `left` -- the runtime reports it
@@ -428,15 +567,22 @@ int svc_reduce(int op, int type, const void *in, const void *in2, void *inout, s
         v.state = -1;
         return MX_ERR_HIP;
       }
-      if (e == hipSuccess && __atomic_load_n(&v.host->done, __ATOMIC_ACQUIRE) < q && !svc_gone(v, v.epoch)) {
+      if (e == hipSuccess && !finished(q) && !svc_gone(v, v.epoch)) {
         v.live = false;                        // gone without a word: inout unknown, no retry
         v.state = -1;
         return MX_ERR_HIP;
       }
     }
     if ((k & 15) == 15 && svc_gone(v, v.epoch)) {
-      // it left before taking q (or took it: done is final once left shows)
-      if (__atomic_load_n(&v.host->done, __ATOMIC_ACQUIRE) >= q) { v.served++; return 1; }
+      // it left: before taking q, or after (a helper may still be finishing
+      // its share) -- once the grid has drained the words are final
+      if (hipStreamSynchronize(v.s) != hipSuccess) {
+        (void)hipGetLastError();
+        v.live = false;
+        v.state = -1;
+        return MX_ERR_HIP;
+      }
+      if (finished(q)) { v.served++; return 1; }
       v.live = false;
       if (!svc_start(v, fn)) return 0;        // the new kernel starts after q: it never takes it
       q = svc_post(v);                         // the same operands, a new number
