@@ -116,6 +116,35 @@ def _cpu_model():
 PACK_BENCH_TYPES = ["vector_f32_b4_s8", "indexed_f32_random", "struct_char_d3_int_resized48"]
 
 
+def op_reduce_call_cost(torch, mx, sizes=(4 << 10, 64 << 10, 1 << 20)):
+    """One blocking ompi_op_reduce on device buffers (fp32 SUM) through
+    op/mi355x as Open MPI's op framework calls it (the mini-host's op table,
+    ompi/op/op.h:547-610), microseconds per call measured in C: the resident
+    service (default) and the launch marking itself (service off), A/B
+    interleaved twice (tools/op_call_cost.py is the same loop)."""
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import minihost
+    H = minihost.host(with_components=True)
+    H.mxh_time_op_reduce.restype = ctypes.c_double
+    H.mxh_time_op_reduce.argtypes = [ctypes.c_void_p] * 3 + [ctypes.c_int, ctypes.c_void_p, ctypes.c_int]
+    f32, SUM = minihost.dtype(H, "MPI_FLOAT"), minihost.op(H, "MPI_SUM")
+    out = {"what": "ompi_op_reduce fp32 SUM, device buffers, op/mi355x via the mini-host op table",
+           "service": {}, "launch": {}}
+    for nbytes in sizes:
+        n = nbytes // 4
+        a = torch.rand(n, device="cuda")
+        b = torch.rand(n, device="cuda")
+        torch.cuda.synchronize()
+        iters = 2000 if nbytes <= (64 << 10) else 500
+        for rnd in range(2):
+            for mode in ("service", "launch"):
+                mx.op_service_set(mode == "service")
+                ns = H.mxh_time_op_reduce(SUM, a.data_ptr(), b.data_ptr(), n, f32, iters)
+                out[mode].setdefault(str(nbytes), []).append(round(ns / 1e3, 2))
+    mx.op_service_set(True)
+    return out
+
+
 def pack_side_by_side(torch, mx, cpu=True, packed_bytes=256 << 20, cpu_seconds=1.5):
     """MPI_Pack / MPI_Unpack of the CFG-C types on the device (mx_pack /
     mx_unpack, HIP events on the launch stream, median of 5 batches) and --
@@ -702,6 +731,10 @@ def main():
             result["pack_unpack"] = pack_side_by_side(torch, mx, cpu=not args.no_cpu_baseline)
         except Exception as e:  # noqa: BLE001 - reported in the JSON line
             result["pack_unpack"] = {"error": repr(e)}
+        try:
+            result["op_reduce_call_us"] = op_reduce_call_cost(torch, mx)
+        except Exception as e:  # noqa: BLE001 - reported in the JSON line
+            result["op_reduce_call_us"] = {"error": repr(e)}
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         result["cpu_baseline"] = cpu_baseline_reduce_local(args.cpu_seconds)
         result["cpu_baseline_pack"] = {k: result["pack_unpack"].get(k) for k in ("cpu", "types")} \

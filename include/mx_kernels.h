@@ -225,6 +225,9 @@ int mx_reduce2_sync(int op, int type, const void *in, void *inout,
  * Commands served and service launches so far; returns 1 when the service
  * is usable, 0 before first use, -1 when off. */
 int mx_op_service_stats(unsigned long long *served, unsigned long long *launches);
+/* Turns the service on or off at run time (overrides MX_OP_SERVICE; off
+ * stops a running service kernel). */
+int mx_op_service_set(int on);
 /* Service launches that did not start within 1 ms (their hardware queue
  * held by a kernel of another stream) so far; returns 1 while such
  * a kernel has not yet left (calls launch meanwhile), else 0. */

@@ -40,6 +40,7 @@
 #include <string.h>
 #include <chrono>
 #include <algorithm>
+#include <atomic>
 #include <mutex>
 #include <vector>
 
@@ -369,11 +370,16 @@ struct Service {
 };
 Service g_svc;
 
+// MX_OP_SERVICE (default on); mx_op_service_set() overrides it at run time
+std::atomic<int> g_svc_on{-1};
 bool svc_enabled() {
-  static const int on = [] {
+  int on = g_svc_on.load(std::memory_order_relaxed);
+  if (on < 0) {
     const char *e = getenv("MX_OP_SERVICE");
-    return (e && *e == '0') ? 0 : 1;
-  }();
+    int v = (e && *e == '0') ? 0 : 1;
+    g_svc_on.compare_exchange_strong(on, v);
+    on = g_svc_on.load(std::memory_order_relaxed);
+  }
   return on != 0;
 }
 
@@ -599,6 +605,14 @@ extern "C" int mx_op_service_stats(unsigned long long *served, unsigned long lon
   if (served) *served = v.served;
   if (launches) *launches = v.epoch;
   return v.state;
+}
+
+extern "C" int mx_op_service_set(int on) {
+  mx::Service &v = mx::g_svc;
+  std::lock_guard<std::mutex> lk(v.mu);
+  mx::g_svc_on.store(on ? 1 : 0, std::memory_order_relaxed);
+  if (!on && v.state == 1) mx::svc_stop_locked(v);
+  return MX_SUCCESS;
 }
 
 extern "C" int mx_op_service_held(unsigned long long *held) {

@@ -118,6 +118,7 @@ def lib() -> ctypes.CDLL:
         L.mx_shmem_to_mpi.argtypes = [i, i, sz, ctypes.POINTER(i), ctypes.POINTER(i)]
         L.mx_op_service_stats.argtypes = [ctypes.POINTER(ctypes.c_ulonglong), ctypes.POINTER(ctypes.c_ulonglong)]
         L.mx_op_service_held.argtypes = [ctypes.POINTER(ctypes.c_ulonglong)]
+        L.mx_op_service_set.argtypes = [ctypes.c_int]
         L.mx_debug_hold.argtypes = [vp, ctypes.c_uint]
         L.mx_debug_hold_service.argtypes = [ctypes.c_uint]
         L._mx_typed = True
@@ -184,6 +185,11 @@ def op_service_stats():
     a, b = ctypes.c_ulonglong(), ctypes.c_ulonglong()
     st = lib().mx_op_service_stats(ctypes.byref(a), ctypes.byref(b))
     return st, a.value, b.value
+
+
+def op_service_set(on: bool) -> None:
+    """Turn the resident reduce service on or off (overrides MX_OP_SERVICE)."""
+    check(lib().mx_op_service_set(1 if on else 0), "mx_op_service_set")
 
 
 def op_service_held():
