@@ -276,3 +276,46 @@ def test_service_irecv_reduce_send_does_not_deadlock(env):
         assert got[r]["seconds"] < 15.0, got[r]["seconds"]
         if env["MX_OP_SERVICE"] == "1":
             assert got[r]["stats"][1] > 0                  # the service took calls
+
+
+def test_service_concurrent_threads():
+    """MPI_THREAD_MULTIPLE: four threads, each with its own stream and pair,
+    call the blocking reduce 150 times on their own buffers -- the service
+    is rebound between pairs as calls interleave; every result exact."""
+    import threading
+    mxompi.init(0)
+    jobs = [("SUM", "INT64_T", 3000), ("BXOR", "UINT32_T", 70000), ("MAX", "INT32_T", 300000), ("SUM", "INT32_T", 17)]
+    errs = []
+
+    def run(op, t, n, seed):
+        try:
+            torch.cuda.set_device(0)
+            s = torch.cuda.Stream()
+            dt = {"INT64_T": torch.int64, "UINT32_T": torch.int32, "INT32_T": torch.int32}[t]
+            g = torch.Generator(device="cpu").manual_seed(seed)
+            a = torch.randint(-1000, 1000, (n,), generator=g, dtype=dt).cuda()
+            b = torch.zeros(n, dtype=dt, device="cuda")
+            ref = b.clone()
+            torch.cuda.synchronize()
+            for i in range(150):
+                mxompi.reduce2_sync(op, t, a.data_ptr(), b.data_ptr(), n, s.cuda_stream)
+                if op == "SUM":
+                    ref += a
+                elif op == "BXOR":
+                    ref ^= a
+                else:
+                    ref = torch.maximum(ref, a)
+            torch.cuda.synchronize()
+            if not torch.equal(b, ref):
+                errs.append(f"{op} {t} {n}: mismatch")
+        except Exception as e:  # noqa: BLE001
+            errs.append(f"{op} {t} {n}: {e!r}")
+
+    served0 = mxompi.op_service_stats()[1]
+    th = [threading.Thread(target=run, args=(op, t, n, 10 + i)) for i, (op, t, n) in enumerate(jobs)]
+    for x in th:
+        x.start()
+    for x in th:
+        x.join(120)
+    assert not errs, errs
+    print(f"served {mxompi.op_service_stats()[1] - served0} of {150 * len(jobs)}")
