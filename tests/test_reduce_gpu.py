@@ -267,3 +267,42 @@ def test_reduce2_sync_chain_across_streams(n):
     for i in range(300):
         mxompi.reduce2_sync("SUM", "INT32_T", a.data_ptr(), b.data_ptr(), n, (s1 if i % 2 else s2).cuda_stream)
     assert torch.equal(b.cpu(), torch.full((n,), 300, dtype=torch.int32))
+
+
+# value bytes of the padded element types (the rest is padding the 3-buffer
+# form must leave as the destination held it: LOC_FUNC_3BUF assigns members)
+_VALUE_BYTES = {"SHORT_INT": [(0, 2), (4, 8)], "DOUBLE_INT": [(0, 12)], "LONG_DOUBLE": [(0, 10)],
+                "LONG_DOUBLE_INT": [(0, 10), (16, 20)], "C_LONG_DOUBLE_COMPLEX": [(0, 10), (16, 26)]}
+
+
+@pytest.mark.parametrize("op,t", [("MINLOC", "SHORT_INT"), ("MAXLOC", "DOUBLE_INT"), ("SUM", "LONG_DOUBLE"),
+                                  ("MAXLOC", "LONG_DOUBLE_INT"), ("PROD", "C_LONG_DOUBLE_COMPLEX")])
+@pytest.mark.parametrize("n,eo", [(100003, 0), (4099, 1), (2, 0)])
+def test_three_buffer_keeps_destination_padding(op, t, n, eo):
+    """The 3-buffer kernels of padded types merge the results' value fields
+    into the destination's own bytes (whole-line writes): values bit-exact
+    vs the oracle, every padding byte of `out` as it was."""
+    O = oracle_lib.oracle()
+    es = mxompi.type_size(t)
+    rng = np.random.default_rng(n + es)
+    raw = [rng.integers(0, 256, es * (n + eo) + 64, dtype=np.uint8) for _ in range(3)]
+    if "LONG_DOUBLE" in t:
+        for r in raw[:2]:
+            v = r[: len(r) // 16 * 16].reshape(-1, 16)
+            v[:] = rng.uniform(-4, 4, len(v)).astype(np.longdouble).view(np.uint8).reshape(-1, 16)
+    A = _dev(raw[0]); B = _dev(raw[1]); OUT = _dev(raw[2])
+    e = es * eo
+    mxompi.reduce3(op, t, A.data_ptr() + e, B.data_ptr() + e, OUT.data_ptr() + e, n, _stream())
+    torch.cuda.synchronize()
+    got = OUT.cpu().numpy()
+    exp = raw[2].copy()
+    assert O.mxo_reduce3(mxompi.OP[op], mxompi.TYPE[t], raw[0][e:].ctypes.data, raw[1][e:].ctypes.data,
+                         exp[e:].ctypes.data, n, 1) == 0
+    golden_io.assert_op_equal(got[e:e + es * n], exp[e:e + es * n], mxompi.OP[op], mxompi.TYPE[t], f"{op} {t} n={n}")
+    pad = np.ones(es, bool)
+    for lo, hi in _VALUE_BYTES[t]:
+        pad[lo:hi] = False
+    padmask = np.tile(pad, n)
+    np.testing.assert_array_equal(got[e:e + es * n][padmask], raw[2][e:e + es * n][padmask])
+    np.testing.assert_array_equal(got[:e], raw[2][:e])
+    np.testing.assert_array_equal(got[e + es * n:], raw[2][e + es * n:])

@@ -192,7 +192,12 @@ k_reduce2_elem(const T *__restrict__ a, T *__restrict__ b, size_t n, Mark mk) {
   mark_done(mk);
 }
 
-template <class T, class OP, bool NT, int BS = NT ? kBlockNT : kBlock>
+// PAD (element types with padding: pairs, x87): the results' value fields
+// are merged into the destination's own loaded bytes, so its padding keeps
+// its content (LOC_FUNC_3BUF's member stores) and every line is written
+// whole -- a field-by-field store leaves holes in every line, a partial-line
+// write-back each (tools/sector_probe.hip).
+template <class T, class OP, bool NT, int BS = NT ? kBlockNT : kBlock, bool PAD = false>
 __global__ void __launch_bounds__(BS)
 k_reduce3(const T *__restrict__ a1, const T *__restrict__ a2, T *__restrict__ o, size_t n,
           size_t head, size_t nvec) {
@@ -207,13 +212,76 @@ k_reduce3(const T *__restrict__ a1, const T *__restrict__ a2, T *__restrict__ o,
     V x, y;
     ld16<NT>(x, p + tid);
     ld16<NT>(y, q + tid);
+    if constexpr (PAD) {
+      V z;
+      ld16<NT>(z, ov + tid);
 #pragma unroll
-    for (int j = 0; j < N; j++) x.e[j] = op(x.e[j], y.e[j]);
-    st16<NT>(ov + tid, x);
+      for (int j = 0; j < N; j++) store_fields(&z.e[j], op(x.e[j], y.e[j]));
+      st16<NT>(ov + tid, z);
+    } else {
+#pragma unroll
+      for (int j = 0; j < N; j++) x.e[j] = op(x.e[j], y.e[j]);
+      st16<NT>(ov + tid, x);
+    }
   }
   const size_t tail0 = head + nvec * N;
-  if (tid < head) o[tid] = op(a1[tid], a2[tid]);
-  if (tid < n - tail0) o[tail0 + tid] = op(a1[tail0 + tid], a2[tail0 + tid]);
+  if constexpr (PAD) {
+    if (tid < head) store_fields(&o[tid], op(a1[tid], a2[tid]));
+    if (tid < n - tail0) store_fields(&o[tail0 + tid], op(a1[tail0 + tid], a2[tail0 + tid]));
+  } else {
+    if (tid < head) o[tid] = op(a1[tid], a2[tid]);
+    if (tid < n - tail0) o[tail0 + tid] = op(a1[tail0 + tid], a2[tail0 + tid]);
+  }
+}
+
+// 3-buffer, 32-byte elements (complex long double, long double + int): as
+// k_reduce2_w32t, with the destination's own bytes loaded too so its
+// padding travels back unchanged and every line is written whole.
+template <class T, class OP, bool NT, int BS>
+__global__ void __launch_bounds__(BS) k_reduce3_w32t(const T *__restrict__ a1, const T *__restrict__ a2,
+                                                     T *__restrict__ o, size_t n) {
+  static_assert(sizeof(T) == 32, "32-byte elements");
+  __shared__ u32x4 s1[2 * BS], s2[2 * BS], so[2 * BS];
+  const size_t e0 = (size_t)blockIdx.x * BS;
+  const unsigned nel = (unsigned)(n - e0 < (size_t)BS ? n - e0 : (size_t)BS);
+  const unsigned nv = 2 * nel;
+  const u32x4 *p1 = reinterpret_cast<const u32x4 *>(a1 + e0);
+  const u32x4 *p2 = reinterpret_cast<const u32x4 *>(a2 + e0);
+  u32x4 *po = reinterpret_cast<u32x4 *>(o + e0);
+  const unsigned t = threadIdx.x;
+#pragma unroll
+  for (int k = 0; k < 2; k++) {
+    const unsigned v = t + k * BS;
+    if (v < nv) {
+      if constexpr (NT) {
+        s1[v] = __builtin_nontemporal_load(p1 + v);
+        s2[v] = __builtin_nontemporal_load(p2 + v);
+        so[v] = __builtin_nontemporal_load(po + v);
+      } else {
+        s1[v] = p1[v];
+        s2[v] = p2[v];
+        so[v] = po[v];
+      }
+    }
+  }
+  __syncthreads();
+  if (t < nel) {
+    T x, y, z;
+    __builtin_memcpy(&x, &s1[2 * t], 32);
+    __builtin_memcpy(&y, &s2[2 * t], 32);
+    __builtin_memcpy(&z, &so[2 * t], 32);
+    store_fields(&z, OP()(x, y));
+    __builtin_memcpy(&so[2 * t], &z, 32);
+  }
+  __syncthreads();
+#pragma unroll
+  for (int k = 0; k < 2; k++) {
+    const unsigned v = t + k * BS;
+    if (v < nv) {
+      if constexpr (NT) __builtin_nontemporal_store(so[v], po + v);
+      else po[v] = so[v];
+    }
+  }
 }
 
 // 3-buffer results are stored field by field for element types with
@@ -338,8 +406,20 @@ static int launch3(const void *in1, const void *in2, void *out, size_t n, hipStr
   T *o = static_cast<T *>(out);
   if (n == 0) return MX_SUCCESS;
   constexpr size_t N = (sizeof(T) <= 16 && 16 % sizeof(T) == 0) ? 16 / sizeof(T) : 0;
+  constexpr bool PAD = has_pad<T>::value;
   const uintptr_t m1 = (uintptr_t)a1 & 15, m2 = (uintptr_t)a2 & 15, mo = (uintptr_t)o & 15;
-  if (N == 0 || has_pad<T>::value || m1 != m2 || m1 != mo || (m1 % sizeof(T)) != 0) {
+  if constexpr (sizeof(T) == 32) {
+    if (m1 == 0 && m2 == 0 && mo == 0 && w32_lds()) {
+      if (mx_nt_for(3 * n * sizeof(T)) && nt_small_wg(n))
+        hipLaunchKernelGGL((k_reduce3_w32t<T, OP, true, kBlockNT>), dim3(grid_for(n, kBlockNT)), dim3(kBlockNT), 0, s,
+                           a1, a2, o, n);
+      else
+        hipLaunchKernelGGL((k_reduce3_w32t<T, OP, false, kBlock>), dim3(grid_for(n)), dim3(kBlock), 0, s, a1, a2, o,
+                           n);
+      return mx_check_launch();
+    }
+  }
+  if (N == 0 || (PAD && !w32_lds()) || m1 != m2 || m1 != mo || (m1 % sizeof(T)) != 0) {
     hipLaunchKernelGGL((k_reduce3_elem<T, OP>), dim3(grid_for(n)), dim3(kBlock), 0, s, a1, a2, o, n);
     return mx_check_launch();
   }
@@ -350,13 +430,14 @@ static int launch3(const void *in1, const void *in2, void *out, size_t n, hipStr
   if (work < head + N) work = head + N;
   if (mx_nt_for(3 * n * sizeof(T))) {
     if (nt_small_wg(work))
-      hipLaunchKernelGGL((k_reduce3<T, OP, true>), dim3(grid_for(work, kBlockNT)), dim3(kBlockNT), 0, s, a1, a2, o, n,
-                         head, nvec);
+      hipLaunchKernelGGL((k_reduce3<T, OP, true, kBlockNT, PAD>), dim3(grid_for(work, kBlockNT)), dim3(kBlockNT), 0, s,
+                         a1, a2, o, n, head, nvec);
     else
-      hipLaunchKernelGGL((k_reduce3<T, OP, true, kBlock>), dim3(grid_for(work)), dim3(kBlock), 0, s, a1, a2, o, n,
-                         head, nvec);
+      hipLaunchKernelGGL((k_reduce3<T, OP, true, kBlock, PAD>), dim3(grid_for(work)), dim3(kBlock), 0, s, a1, a2, o,
+                         n, head, nvec);
   } else {
-    hipLaunchKernelGGL((k_reduce3<T, OP, false>), dim3(grid_for(work)), dim3(kBlock), 0, s, a1, a2, o, n, head, nvec);
+    hipLaunchKernelGGL((k_reduce3<T, OP, false, kBlock, PAD>), dim3(grid_for(work)), dim3(kBlock), 0, s, a1, a2, o, n,
+                       head, nvec);
   }
   return mx_check_launch();
 }
