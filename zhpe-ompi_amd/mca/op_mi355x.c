@@ -209,6 +209,14 @@ static ompi_op_base_module_t *mx_op_component_op_query(struct ompi_op_t *op, int
     return &m->super;
 }
 
+/* MPI_Finalize closes the framework: the resident reduce service (if it
+ * ran) is stopped here, so its grid has drained before the process ends */
+static int mx_op_component_close(void)
+{
+    (void)mx_op_service_set(0);
+    return OMPI_SUCCESS;
+}
+
 ompi_op_base_component_1_0_0_t mca_op_mi355x_component = {
     .opc_version = {
         .mca_major_version = 2, .mca_minor_version = 1, .mca_release_version = 0,
@@ -218,6 +226,7 @@ ompi_op_base_component_1_0_0_t mca_op_mi355x_component = {
 #ifdef MX_OMPI_REAL
         .mca_open_component = mx_op_component_open,
 #endif
+        .mca_close_component = mx_op_component_close,
     },
     .opc_init_query = mx_op_component_init_query,
     .opc_op_query = mx_op_component_op_query,
