@@ -218,10 +218,9 @@ int mx_reduce2_sync(int op, int type, const void *in, void *inout,
  * resident service kernel instead of launching (no launch and no dispatch
  * per call: 4 KiB 7 -> 4 us, 1 MiB 9.8 -> 7.5 us; it
  * leaves after 100 us without calls or, between calls, once 1 ms old, and
- * is relaunched on demand; MX_OP_SERVICE=0 switches it off).  A served call
- * is not ordered after work still queued on any stream: its operands must
- * be complete when it is made (the CUDA-aware MPI contract for buffers
- * handed to MPI).
+ * is relaunched on demand; MX_OP_SERVICE=0 switches it off).  A call is
+ * served only when `stream` and the legacy default stream hold no pending
+ * work, so it keeps the launch's stream order.
  * Commands served and service launches so far; returns 1 when the service
  * is usable, 0 before first use, -1 when off. */
 int mx_op_service_stats(unsigned long long *served, unsigned long long *launches);

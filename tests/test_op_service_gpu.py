@@ -1,5 +1,5 @@
 """The resident reduce service behind mx_reduce2_sync (round 4,
-csrc/mx_service.hip): calls of <= 2 MiB on a non-default stream are served
+csrc/mx_service.hip): calls of <= 2 MiB on an idle non-default stream are served
 by a kernel that stays resident instead of a launch per call -- workgroup 0
 alone up to 64 KiB, the whole grid above.
 
@@ -319,3 +319,27 @@ def test_service_concurrent_threads():
         x.join(120)
     assert not errs, errs
     print(f"served {mxompi.op_service_stats()[1] - served0} of {150 * len(jobs)}")
+
+
+def test_service_keeps_stream_order():
+    """Work still queued on the caller's stream when the call is made (here a
+    wave holding the stream for 20 ms, then a fill of `in`): the call is not
+    served -- the launch runs after that work, as on any stream -- and the
+    result sees the fill.  On an idle stream the next call is served."""
+    mxompi.init(0)
+    s = torch.cuda.Stream()
+    n = 5000
+    a = torch.ones(n, dtype=torch.int64, device="cuda")
+    b = torch.zeros(n, dtype=torch.int64, device="cuda")
+    torch.cuda.synchronize()
+    mxompi.reduce2_sync("SUM", "INT64_T", a.data_ptr(), b.data_ptr(), n, s.cuda_stream)   # served: b = 1
+    served0 = mxompi.op_service_stats()[1]
+    mxompi.debug_hold(s.cuda_stream, 20)           # leaves by itself after 20 ms
+    with torch.cuda.stream(s):
+        a.fill_(5)
+    mxompi.reduce2_sync("SUM", "INT64_T", a.data_ptr(), b.data_ptr(), n, s.cuda_stream)   # launched after the fill
+    assert torch.all(b == 6).item()
+    assert mxompi.op_service_stats()[1] == served0
+    mxompi.reduce2_sync("SUM", "INT64_T", a.data_ptr(), b.data_ptr(), n, s.cuda_stream)   # idle again: served
+    assert torch.all(b == 11).item()
+    assert mxompi.op_service_stats()[1] == served0 + 1

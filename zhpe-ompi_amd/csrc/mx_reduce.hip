@@ -515,6 +515,13 @@ extern "C" int mx_reduce2(int op, int type, const void *in, void *inout, size_t 
   return e.f2(in, inout, count, (hipStream_t)stream, Mark{nullptr, nullptr, 0});
 }
 
+// s and the legacy default stream hold no pending work
+static bool svc_may_serve(hipStream_t s) {
+  const bool idle = hipStreamQuery(s) == hipSuccess && hipStreamQuery(nullptr) == hipSuccess;
+  if (!idle) (void)hipGetLastError();   // hipErrorNotReady is no error
+  return idle;
+}
+
 extern "C" int mx_reduce2_sync(int op, int type, const void *in, void *inout, size_t count, void *stream) {
   if (op < 0 || op >= MX_OP_COUNT || type < 0 || type >= MX_TYPE_COUNT) return MX_ERR_ARG;
   entry e = lookup(op, type);
@@ -524,16 +531,11 @@ extern "C" int mx_reduce2_sync(int op, int type, const void *in, void *inout, si
   int rc = mx_ensure_init();
   if (rc) return rc;
   hipStream_t s = (hipStream_t)stream;
-  // the resident service (mx_service.hip) for calls on a non-default stream:
-  // a served call is ordered after nothing queued on any stream -- its
-  // operands must be ready when it is made, which is the CUDA-aware MPI
-  // contract (buffers handed to MPI are complete) and what coll/base's
-  // operands are (results of completed receives and earlier reductions);
-  // the launch path (MX_OP_SERVICE=0, or the legacy default stream) keeps
-  // the blocking stream's implicit order after the default stream.  (Asking
-  // the runtime whether both streams are idle costs ~10 us per query on this
-  // runtime, more than the service saves.)
-  if (s) {
+  // the resident service (mx_service.hip) for calls on a non-default stream
+  // that is idle, with the legacy default stream idle too: nothing the
+  // launch would be ordered after is pending, so the served call keeps the
+  // launch path's order (two queries, ~0.2 us: tools/query_cost_probe.py)
+  if (s && svc_may_serve(s)) {
     rc = svc_reduce(op, type, in, nullptr, inout, count);
     if (rc) return rc < 0 ? rc : MX_SUCCESS;
   }
@@ -553,8 +555,8 @@ extern "C" int mx_reduce2_sync(int op, int type, const void *in, void *inout, si
 
 // As mx_reduce3, returning with `out` complete for every agent: the op
 // component's 3-buffer handler (ompi_3buff_op_reduce, op.h:618-660).  The
-// resident service on a non-default stream (as mx_reduce2_sync), else the
-// launch and the marker kernel.
+// resident service on an idle non-default stream (as mx_reduce2_sync), else
+// the launch and the marker kernel.
 extern "C" int mx_reduce3_sync(int op, int type, const void *in1, const void *in2, void *out, size_t count,
                                void *stream) {
   if (op < 0 || op >= MX_OP_COUNT || type < 0 || type >= MX_TYPE_COUNT) return MX_ERR_ARG;
@@ -564,7 +566,7 @@ extern "C" int mx_reduce3_sync(int op, int type, const void *in1, const void *in
   if (!in1 || !in2 || !out || count > kMaxItems) return MX_ERR_ARG;
   int rc = mx_ensure_init();
   if (rc) return rc;
-  if (stream) {
+  if (stream && svc_may_serve((hipStream_t)stream)) {
     rc = svc_reduce(op, type, in1, in2, out, count);
     if (rc) return rc < 0 ? rc : MX_SUCCESS;
   }
