@@ -152,7 +152,14 @@ static size_t oneshot_max() {
   return v > 0 ? (size_t)v : 0;
 }
 
-struct SignalArgs { uint64_t *peer_flag[MAXR]; int n; uint64_t value; const int *poison; };
+struct SignalArgs {
+  uint64_t *peer_flag[MAXR];
+  int n;
+  uint64_t value;
+  const int *poison;
+  uint64_t *mark;     // a blocking call's completion word (Mark.word), raised after the flags, or null
+  uint64_t mark_v;
+};
 
 __global__ void k_signal(SignalArgs a) {
   const int j = threadIdx.x;
@@ -161,6 +168,7 @@ __global__ void k_signal(SignalArgs a) {
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // keep the write-back ahead of the flag (guide G16 pitfall 12)
   if (j < a.n && a.peer_flag[j])
     __hip_atomic_store(a.peer_flag[j], a.value, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  if (a.mark && j == 0) __hip_atomic_store(a.mark, a.mark_v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
 // Waits until flags[j] >= value for every j in `mask`; a timeout raises the
@@ -993,7 +1001,7 @@ static bool fast_sync() {
 // true) before its launch), else the marker kernel
 static int finish(mx_comm *c, hipStream_t s, const Mark *mk = nullptr) {
   if (c->defer) return MX_SUCCESS;   // request path: completion through the request's event
-  if (mk && mk->flags) {
+  if (mk && (mk->flags || mk->word)) {
     if (mark_wait(*mk, s) != MX_SUCCESS) return MX_ERR_HIP;
   } else if (fast_sync() ? mx_stream_sync_fast(s) != MX_SUCCESS : hipStreamSynchronize(s) != hipSuccess) {
     return MX_ERR_HIP;
@@ -1221,12 +1229,18 @@ extern "C" int mx_bcast_local(mx_comm_t *c, void *const *bufs, size_t bytes, int
 // ---------------------------------------------------------------------------
 namespace {
 
-static int signal_all(mx_comm *c, int kind, uint64_t value, hipStream_t s) {
+// mk: the blocking call's completion word, raised by this signal as the
+// call's last kernel (finish then waits for it instead of a marker kernel)
+static int signal_all(mx_comm *c, int kind, uint64_t value, hipStream_t s, const Mark *mk = nullptr) {
   SignalArgs a;
   memset(&a, 0, sizeof a);
   a.n = c->size;
   a.value = value;
   a.poison = c->poison;
+  if (mk && mk->word) {
+    a.mark = mk->word;
+    a.mark_v = mk->v;
+  }
   for (int p = 0; p < c->size; p++)
     a.peer_flag[p] = (p == c->rank) ? nullptr : c->peer_flags[p] + kind * MAXR + c->rank;
   hipLaunchKernelGGL(k_signal, dim3(1), dim3(64), 0, s, a);
@@ -1292,6 +1306,17 @@ static bool os_self_mark() {
   static const bool v = [] {
     const char *e = getenv("MX_OS_SELF_MARK");
     return !(e && *e == '0');
+  }();
+  return v;
+}
+
+// MX_DONE_SELF_MARK=1: a blocking staged / zero-copy allreduce's last DONE
+// signal raises the completion word instead of a marker kernel after it
+// (default off until measured)
+static bool done_self_mark() {
+  static const bool v = [] {
+    const char *e = getenv("MX_DONE_SELF_MARK");
+    return e && *e == '1';
   }();
   return v;
 }
@@ -1594,6 +1619,9 @@ static int allreduce_staged(mx_comm *c, fold_launch_fn fl, int alg, const char *
   const size_t ce = chunk_elems(c, count, es, zc);
   if (zc) c->st.zero_copy_calls++;
   else c->st.staged_calls++;
+  // a blocking call: the last round's DONE signal raises the completion word
+  Mark mk{nullptr, nullptr, 0};
+  if (!c->defer && fast_sync() && done_self_mark()) mark_arm(&mk, false);
   for (size_t c0 = 0; c0 < count; c0 += ce) {
     const size_t cl = std::min(ce, count - c0);
     const Layout L = layout_for(n, ce, es, zc);
@@ -1663,9 +1691,9 @@ static int allreduce_staged(mx_comm *c, fold_launch_fn fl, int alg, const char *
     prof_begin(c, s);
     if ((rc = copy_launch(c, ca, s))) return rc;
     prof_end(c, s, 2, 0);
-    if ((rc = signal_all(c, FLAG_DONE, g, s))) return rc;
+    if ((rc = signal_all(c, FLAG_DONE, g, s, c0 + cl >= count ? &mk : nullptr))) return rc;
   }
-  return finish(c, s);
+  return finish(c, s, &mk);
 }
 
 extern "C" int mx_allreduce(mx_comm_t *c, const void *sbuf, void *rbuf, size_t count, int type, int op, int alg,
