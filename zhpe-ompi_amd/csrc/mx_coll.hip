@@ -1310,13 +1310,14 @@ static bool os_self_mark() {
   return v;
 }
 
-// MX_DONE_SELF_MARK=1: a blocking staged / zero-copy allreduce's last DONE
-// signal raises the completion word instead of a marker kernel after it
-// (default off until measured)
+// MX_DONE_SELF_MARK=0: a blocking staged / zero-copy allreduce ends with the
+// marker kernel instead of its last DONE signal raising the completion word
+// (n=2 on one GPU, 256 KiB - 4 MiB: 1.5-4 us of 23-30 us saved,
+// profiles/r04/done_self_mark_ab.txt)
 static bool done_self_mark() {
   static const bool v = [] {
     const char *e = getenv("MX_DONE_SELF_MARK");
-    return e && *e == '1';
+    return !(e && *e == '0');
   }();
   return v;
 }
