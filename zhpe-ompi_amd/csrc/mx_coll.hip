@@ -997,6 +997,18 @@ static bool fast_sync() {
   return v;
 }
 
+// MX_DONE_SELF_MARK=0: a blocking staged / zero-copy collective ends with the
+// marker kernel instead of its last DONE signal raising the completion word
+// (n=2 on one GPU, 256 KiB - 4 MiB: 1.5-4 us of 23-30 us saved,
+// profiles/r04/done_self_mark_ab.txt)
+static bool done_self_mark() {
+  static const bool v = [] {
+    const char *e = getenv("MX_DONE_SELF_MARK");
+    return !(e && *e == '0');
+  }();
+  return v;
+}
+
 // mk: the completion flags the last kernel raises itself (mark_arm(&mk,
 // true) before its launch), else the marker kernel
 static int finish(mx_comm *c, hipStream_t s, const Mark *mk = nullptr) {
@@ -1247,6 +1259,24 @@ static int signal_all(mx_comm *c, int kind, uint64_t value, hipStream_t s, const
   return mx_check_launch();
 }
 
+// A blocking call's completion word raised by its last DONE signal (the
+// call's last kernel): armed at the start of the call, attached to the final
+// signal only, and used by finish only if that signal went out.
+struct DoneMark {
+  Mark mk{nullptr, nullptr, 0};
+  bool sent = false;
+};
+static void done_mark_arm(mx_comm *c, DoneMark &d) {
+  if (c && !c->defer && fast_sync() && done_self_mark()) mark_arm(&d.mk, false);
+}
+static int signal_done(mx_comm *c, uint64_t value, hipStream_t s, DoneMark *last) {
+  const Mark *mk = last && last->mk.word ? &last->mk : nullptr;
+  const int rc = signal_all(c, FLAG_DONE, value, s, mk);
+  if (!rc && mk) last->sent = true;
+  return rc;
+}
+static int finish_done(mx_comm *c, hipStream_t s, const DoneMark &d) { return finish(c, s, d.sent ? &d.mk : nullptr); }
+
 // signal_all(kind, svalue) + wait_all(kind, wvalue) as one launch
 static int signal_wait_all(mx_comm *c, int kind, uint64_t svalue, uint64_t wvalue, hipStream_t s) {
   SignalArgs a;
@@ -1310,17 +1340,6 @@ static bool os_self_mark() {
   return v;
 }
 
-// MX_DONE_SELF_MARK=0: a blocking staged / zero-copy allreduce ends with the
-// marker kernel instead of its last DONE signal raising the completion word
-// (n=2 on one GPU, 256 KiB - 4 MiB: 1.5-4 us of 23-30 us saved,
-// profiles/r04/done_self_mark_ab.txt)
-static bool done_self_mark() {
-  static const bool v = [] {
-    const char *e = getenv("MX_DONE_SELF_MARK");
-    return !(e && *e == '0');
-  }();
-  return v;
-}
 
 // one-shot allreduce (small messages): one kernel, see k_oneshot
 static int allreduce_oneshot(mx_comm *c, oneshot_launch_fn ol, const std::vector<Seg> &segs, const char *sb,
@@ -1620,9 +1639,8 @@ static int allreduce_staged(mx_comm *c, fold_launch_fn fl, int alg, const char *
   const size_t ce = chunk_elems(c, count, es, zc);
   if (zc) c->st.zero_copy_calls++;
   else c->st.staged_calls++;
-  // a blocking call: the last round's DONE signal raises the completion word
-  Mark mk{nullptr, nullptr, 0};
-  if (!c->defer && fast_sync() && done_self_mark()) mark_arm(&mk, false);
+  DoneMark dm;   // a blocking call: the last round's DONE signal raises the completion word
+  done_mark_arm(c, dm);
   for (size_t c0 = 0; c0 < count; c0 += ce) {
     const size_t cl = std::min(ce, count - c0);
     const Layout L = layout_for(n, ce, es, zc);
@@ -1692,9 +1710,9 @@ static int allreduce_staged(mx_comm *c, fold_launch_fn fl, int alg, const char *
     prof_begin(c, s);
     if ((rc = copy_launch(c, ca, s))) return rc;
     prof_end(c, s, 2, 0);
-    if ((rc = signal_all(c, FLAG_DONE, g, s, c0 + cl >= count ? &mk : nullptr))) return rc;
+    if ((rc = signal_done(c, g, s, c0 + cl >= count ? &dm : nullptr))) return rc;
   }
-  return finish(c, s, &mk);
+  return finish_done(c, s, dm);
 }
 
 extern "C" int mx_allreduce(mx_comm_t *c, const void *sbuf, void *rbuf, size_t count, int type, int op, int alg,
@@ -1793,6 +1811,8 @@ extern "C" int mx_allreduce(mx_comm_t *c, const void *sbuf, void *rbuf, size_t c
 
 static int reduce_scatter_impl(mx_comm_t *c, const void *sbuf, void *rbuf, const size_t *rcounts, int type, int op,
                                int alg, void *stream, int zc_mode) {
+  DoneMark dm;   // the call's last DONE signal raises the completion word (blocking calls)
+  done_mark_arm(c, dm);
   if (!c || !rbuf || !rcounts) return MX_ERR_ARG;
   if (c->local) {
     if (c->size != 1) return MX_ERR_STATE;
@@ -1848,8 +1868,8 @@ static int reduce_scatter_impl(mx_comm_t *c, const void *sbuf, void *rbuf, const
           if ((rc = run_fold(c, fl, sg, disp[r], sp, n, dp, 1, es, s, true))) return rc;
       }
       if ((rc = signal_wait_all(c, FLAG_PUSHED, g, g, s))) return rc;     // every peer is done with my sbuf
-      if ((rc = signal_all(c, FLAG_DONE, g, s))) return rc;
-      return finish(c, s);
+      if ((rc = signal_done(c, g, s, &dm))) return rc;
+      return finish_done(c, s, dm);
     }
   }
   const bool overlap = inplace && disp[r] != 0;
@@ -1887,12 +1907,14 @@ static int reduce_scatter_impl(mx_comm_t *c, const void *sbuf, void *rbuf, const
       }
       if (overlap && (rc = copy_async((char *)rbuf + k0 * es, dst, kl * es, s))) return rc;
     }
-    if ((rc = signal_all(c, FLAG_DONE, g, s))) return rc;
+    if ((rc = signal_done(c, g, s, k0 + kc >= maxc ? &dm : nullptr))) return rc;
   }
-  return finish(c, s);
+  return finish_done(c, s, dm);
 }
 
 static int allgather_impl(mx_comm_t *c, const void *sbuf, void *rbuf, size_t bytes, void *stream, int zc_mode) {
+  DoneMark dm;   // the call's last DONE signal raises the completion word (blocking calls)
+  done_mark_arm(c, dm);
   if (!c || !rbuf) return MX_ERR_ARG;
   if (c->local) {
     if (c->size != 1) return MX_ERR_STATE;
@@ -1931,8 +1953,8 @@ static int allgather_impl(mx_comm_t *c, const void *sbuf, void *rbuf, size_t byt
       if (sb != rb + (size_t)r * bytes) ca.j[ca.n++] = CopyJob{sb, rb + (size_t)r * bytes, bytes};
       if ((rc = copy_launch(c, ca, s))) return rc;
       if ((rc = signal_wait_all(c, FLAG_PUSHED, g, g, s))) return rc;     // done reading the peers' sbufs
-      if ((rc = signal_all(c, FLAG_DONE, g, s))) return rc;
-      return finish(c, s);
+      if ((rc = signal_done(c, g, s, &dm))) return rc;
+      return finish_done(c, s, dm);
     }
   }
   // n slots of `slot` bytes; each round moves up to `cb` bytes per rank
@@ -1956,9 +1978,9 @@ static int allgather_impl(mx_comm_t *c, const void *sbuf, void *rbuf, size_t byt
       if (p != r)
         ca.j[ca.n++] = CopyJob{c->staging + (size_t)p * slot + ((p * bytes + o) & 15), rb + (size_t)p * bytes + o, l};
     if ((rc = copy_launch(c, ca, s))) return rc;
-    if ((rc = signal_all(c, FLAG_DONE, g, s))) return rc;
+    if ((rc = signal_done(c, g, s, o + cb >= bytes ? &dm : nullptr))) return rc;
   }
-  return finish(c, s);
+  return finish_done(c, s, dm);
 }
 
 // MPI_Bcast, all-peer scatter + allgather (the reference's large-message
@@ -2502,6 +2524,8 @@ struct VmSeg { size_t lo, hi; VmProg p; };   // program for elements [lo, hi)
 
 static int vm_partitioned(mx_comm *c, vm_launch_fn vl, const std::vector<VmSeg> &segs, const char *sb, char *rb,
                           size_t count, size_t es, uint32_t dest_mask, int info_rank, int info_bit, hipStream_t s) {
+  DoneMark dm;   // the call's last DONE signal raises the completion word (blocking calls)
+  done_mark_arm(c, dm);
   const int n = c->size, r = c->rank;
   const bool me_dest = (dest_mask >> r) & 1;
   // zero-copy input (as mx_allreduce): part owners read the contributions
@@ -2582,9 +2606,9 @@ static int vm_partitioned(mx_comm *c, vm_launch_fn vl, const std::vector<VmSeg> 
       if ((rc = copy_launch(c, ca, s))) return rc;
       prof_end(c, s, 2, 0);
     }
-    if ((rc = signal_all(c, FLAG_DONE, g, s))) return rc;
+    if ((rc = signal_done(c, g, s, c0 + ce >= count ? &dm : nullptr))) return rc;
   }
-  return finish(c, s);
+  return finish_done(c, s, dm);
 }
 static int vm_partitioned(mx_comm *c, vm_launch_fn vl, const VmProg &p, const char *sb, char *rb, size_t count,
                           size_t es, uint32_t dest_mask, int info_rank, int info_bit, hipStream_t s) {
@@ -2597,6 +2621,8 @@ static int vm_partitioned(mx_comm *c, vm_launch_fn vl, const VmProg &p, const ch
 // its rbuf.  Chunked over the largest block.
 static int vm_scatter_blocks(mx_comm *c, vm_launch_fn vl, const VmProg &p, const char *sb, char *rb,
                              const size_t *rcounts, size_t es, hipStream_t s) {
+  DoneMark dm;   // the call's last DONE signal raises the completion word (blocking calls)
+  done_mark_arm(c, dm);
   const int n = c->size, r = c->rank;
   size_t disp[MAXR], total = 0, maxc = 0;
   for (int j = 0; j < n; j++) { disp[j] = total; total += rcounts[j]; maxc = std::max(maxc, rcounts[j]); }
@@ -2627,8 +2653,8 @@ static int vm_scatter_blocks(mx_comm *c, vm_launch_fn vl, const VmProg &p, const
         prof_end(c, s, 0, (double)(n + 1) * (double)rcounts[r] * (double)es);
       }
       if ((rc = signal_wait_all(c, FLAG_PUSHED, gen, gen, s))) return rc;   // done reading the peers' sbufs
-      if ((rc = signal_all(c, FLAG_DONE, gen, s))) return rc;
-      return finish(c, s);
+      if ((rc = signal_done(c, gen, s, &dm))) return rc;
+      return finish_done(c, s, dm);
     }
   }
   // IN_PLACE with my block starting inside the range my result overwrites:
@@ -2670,9 +2696,9 @@ static int vm_scatter_blocks(mx_comm *c, vm_launch_fn vl, const VmProg &p, const
       prof_end(c, s, 0, (double)(n + 1) * (double)kl * (double)es);
       if (overlap && (rc = copy_async(rb + k0 * es, dst, kl * es, s))) return rc;
     }
-    if ((rc = signal_all(c, FLAG_DONE, gen, s))) return rc;
+    if ((rc = signal_done(c, gen, s, k0 + kc >= maxc ? &dm : nullptr))) return rc;
   }
-  return finish(c, s);
+  return finish_done(c, s, dm);
 }
 
 static int vm_setup(int op, int type, vm_launch_fn *vl, size_t *es) {
