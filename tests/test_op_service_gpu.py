@@ -343,3 +343,24 @@ def test_service_keeps_stream_order():
     mxompi.reduce2_sync("SUM", "INT64_T", a.data_ptr(), b.data_ptr(), n, s.cuda_stream)   # idle again: served
     assert torch.all(b == 11).item()
     assert mxompi.op_service_stats()[1] == served0 + 1
+
+
+def test_service_resumes_after_a_launch():
+    """A call over the cap launches on the caller's stream; the small calls
+    straight after it must be served again (the launched kernel's stream
+    turns idle a little after its completion word -- the idleness check
+    waits that out instead of launching every call that follows)."""
+    mxompi.init(0)
+    s = torch.cuda.Stream()
+    big = torch.ones((8 << 20) // 8, dtype=torch.int64, device="cuda")
+    bigo = torch.zeros_like(big)
+    a = torch.ones(1000, dtype=torch.int64, device="cuda")
+    b = torch.zeros(1000, dtype=torch.int64, device="cuda")
+    torch.cuda.synchronize()
+    for rnd in range(3):
+        mxompi.reduce2_sync("SUM", "INT64_T", big.data_ptr(), bigo.data_ptr(), big.numel(), s.cuda_stream)
+        served0 = mxompi.op_service_stats()[1]
+        for _ in range(20):
+            mxompi.reduce2_sync("SUM", "INT64_T", a.data_ptr(), b.data_ptr(), 1000, s.cuda_stream)
+        assert mxompi.op_service_stats()[1] - served0 == 20, rnd
+    assert torch.all(b == 60).item() and torch.all(bigo == 3).item()

@@ -29,7 +29,9 @@ int mark_wait(const Mark &m, hipStream_t s);
 // The resident reduce service (mx_service.hip): 1 = served, inout final for
 // every agent; 0 = not served (the caller launches); < 0 = error.  in2:
 // nullptr for the 2-buffer form (inout = inout OP in), else inout = in OP in2.
-int svc_reduce(int op, int type, const void *in, const void *in2, void *inout, size_t count);
+// Served only when `stream` and the legacy default stream hold no pending
+// work (the launch's order is kept).
+int svc_reduce(int op, int type, const void *in, const void *in2, void *inout, size_t count, hipStream_t stream);
 }  // namespace mx
 
 // Lazily performs mx_init(current device) if the caller did not.

@@ -16,6 +16,7 @@
 // Algorithmic bytes per launch: 2-buffer 3*n*size (read in, read inout,
 // write inout), 3-buffer 3*n*size.
 #include <hip/hip_runtime.h>
+#include <chrono>
 #include <stdint.h>
 #include <stddef.h>
 #include <stdlib.h>
@@ -515,13 +516,6 @@ extern "C" int mx_reduce2(int op, int type, const void *in, void *inout, size_t 
   return e.f2(in, inout, count, (hipStream_t)stream, Mark{nullptr, nullptr, 0});
 }
 
-// s and the legacy default stream hold no pending work
-static bool svc_may_serve(hipStream_t s) {
-  const bool idle = hipStreamQuery(s) == hipSuccess && hipStreamQuery(nullptr) == hipSuccess;
-  if (!idle) (void)hipGetLastError();   // hipErrorNotReady is no error
-  return idle;
-}
-
 extern "C" int mx_reduce2_sync(int op, int type, const void *in, void *inout, size_t count, void *stream) {
   if (op < 0 || op >= MX_OP_COUNT || type < 0 || type >= MX_TYPE_COUNT) return MX_ERR_ARG;
   entry e = lookup(op, type);
@@ -532,11 +526,11 @@ extern "C" int mx_reduce2_sync(int op, int type, const void *in, void *inout, si
   if (rc) return rc;
   hipStream_t s = (hipStream_t)stream;
   // the resident service (mx_service.hip) for calls on a non-default stream
-  // that is idle, with the legacy default stream idle too: nothing the
-  // launch would be ordered after is pending, so the served call keeps the
-  // launch path's order (two queries, ~0.2 us: tools/query_cost_probe.py)
-  if (s && svc_may_serve(s)) {
-    rc = svc_reduce(op, type, in, nullptr, inout, count);
+  // that is idle, with the legacy default stream idle too (svc_reduce checks):
+  // nothing the launch would be ordered after is pending, so the served call
+  // keeps the launch path's order
+  if (s) {
+    rc = svc_reduce(op, type, in, nullptr, inout, count, s);
     if (rc) return rc < 0 ? rc : MX_SUCCESS;
   }
   if (!fused_mark() || count > kFusedMarkMax) {
@@ -566,8 +560,8 @@ extern "C" int mx_reduce3_sync(int op, int type, const void *in1, const void *in
   if (!in1 || !in2 || !out || count > kMaxItems) return MX_ERR_ARG;
   int rc = mx_ensure_init();
   if (rc) return rc;
-  if (stream && svc_may_serve((hipStream_t)stream)) {
-    rc = svc_reduce(op, type, in1, in2, out, count);
+  if (stream) {
+    rc = svc_reduce(op, type, in1, in2, out, count, (hipStream_t)stream);
     if (rc) return rc < 0 ? rc : MX_SUCCESS;
   }
   rc = e.f3(in1, in2, out, count, (hipStream_t)stream);

@@ -490,6 +490,26 @@ int svc_setup(Service &v) {
 
 }  // namespace
 
+// `s` and the legacy default stream hold no pending work -- now or within a
+// short spin: a launch of ours whose completion word was already seen
+// retires in the runtime's books several microseconds later (without the
+// spin, one launched call keeps every back-to-back call after it on the
+// launch path: test_service_resumes_after_a_launch), and work the caller
+// still has queued would hold a launch just as long.  Two queries, ~0.2 us
+// when idle (tools/query_cost_probe.py).
+static bool svc_streams_idle(hipStream_t s) {
+  constexpr double kIdleSpinUs = 50;
+  std::chrono::steady_clock::time_point t0;
+  for (unsigned k = 0;; k++) {
+    if (hipStreamQuery(s) == hipSuccess && hipStreamQuery(nullptr) == hipSuccess) return true;
+    (void)hipGetLastError();   // hipErrorNotReady is no error
+    if (k == 0) t0 = std::chrono::steady_clock::now();
+    else if (std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0).count() > kIdleSpinUs)
+      return false;
+    __builtin_ia32_pause();
+  }
+}
+
 // Launch a kernel that takes the commands after v.seq and wait until it
 // runs.  A kernel that does not start within kSvcStartUs has its hardware
 // queue held -- possibly by a kernel of another stream that waits for what
@@ -520,13 +540,14 @@ static bool svc_start(Service &v, svc_launch_fn fn) {
 // in2 != nullptr: the 3-buffer form, inout = in OP in2.  A command is posted
 // only to a kernel seen running that was launched after every earlier
 // command, so no command runs twice and none waits on a held queue.
-int svc_reduce(int op, int type, const void *in, const void *in2, void *inout, size_t count) {
+int svc_reduce(int op, int type, const void *in, const void *in2, void *inout, size_t count, hipStream_t stream) {
   if (!svc_enabled()) return 0;
   const size_t es = mx_type_size(type);
   if (!es || count * es > kSvcMaxBytes || (((uintptr_t)in | (uintptr_t)in2 | (uintptr_t)inout) & 15)) return 0;
   SvcVisitor vis;
   const svc_launch_fn fn = dispatch(op, type, vis);
   if (!fn) return 0;
+  if (!svc_streams_idle(stream)) return 0;
   Service &v = g_svc;
   std::lock_guard<std::mutex> lk(v.mu);
   if (v.state == 0) v.state = svc_setup(v);
