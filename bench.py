@@ -285,7 +285,7 @@ def bench_reduce_local(torch, mx, steps, warmup, nbytes=1 << 30):
     return wall, kms, 3.0 * n * 4, parity
 
 
-def bench_allreduce(torch, mx, dist, rank, world, dev, steps, warmup, nbytes=256 << 20):
+def bench_allreduce(torch, mx, dist, rank, world, dev, steps, warmup, nbytes=256 << 20, extras=True):
     """MPI_Allreduce 256 MiB fp32 SUM per rank through the all-peer path
     (coll/tuned's fixed decision -> segmented-ring fold order).  Returns
     the result dict fields, or raises if the path is unavailable."""
@@ -385,8 +385,8 @@ def bench_allreduce(torch, mx, dist, rank, world, dev, steps, warmup, nbytes=256
         comm.set_autotune(True)
     except mx.MxError:
         pass
-    sweep = allreduce_sweep(torch, mx, dist, comm, world, x, out, sp, flags)
-    cfge = cfg_e(torch, mx, dist, comm, world, rank, sp)
+    sweep = allreduce_sweep(torch, mx, dist, comm, world, x, out, sp, flags) if extras else "skipped (--no-sweep)"
+    cfge = cfg_e(torch, mx, dist, comm, world, rank, sp) if extras else "skipped (--no-sweep)"
     # the data paths the autotuner kept per size class: where the
     # one-shot / zero-copy / staged crossovers fell on this machine
     tuned = {coll: {str(b): comm.tuning(b, coll) for b in (64 << 10, 256 << 10, 1 << 20, 4 << 20, 16 << 20,
@@ -660,6 +660,44 @@ def cfg_e(torch, mx, dist, comm, world, rank, sp, nbytes=256 << 20, iters=5):
     return res
 
 
+def _free_port():
+    import socket
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def spawn_ranks(n, argv):
+    """`bench.py --gpus N` started without a launcher: form the N ranks here,
+    one process per GPU, through torch.distributed.run as a child process
+    (this process has not touched the GPU -- torch is not even imported yet
+    -- and it never execs), relay rank 0's JSON line and return the launcher's
+    exit code.  Ranks inherit the environment (HSA_ENABLE_IPC_MODE_LEGACY=0
+    included) and rendezvous on 127.0.0.1."""
+    import subprocess
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr", "127.0.0.1", f"--master-port={_free_port()}",
+           os.path.abspath(__file__)] + argv
+    env = dict(os.environ)
+    env["MX_BENCH_SPAWNED"] = "1"
+    env.setdefault("OMP_NUM_THREADS", "4")
+    p = subprocess.Popen(cmd, stdout=subprocess.PIPE, text=True, env=env)
+    line = None
+    for out in p.stdout:            # ranks' other stdout passes through
+        if out.lstrip().startswith("{") and '"metric"' in out:
+            line = out.strip()
+        else:
+            sys.stdout.write(out)
+            sys.stdout.flush()
+    rc = p.wait()
+    if line is not None:
+        print(line, flush=True)
+    elif rc == 0:
+        print(json.dumps({"metric": METRIC, "error": f"{n} ranks exited 0 without a result line"}), flush=True)
+        rc = 1
+    return rc
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -667,12 +705,26 @@ def main():
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-sweep", action="store_true",
+                    help="N>1: skip the CFG-D size sweep and the CFG-E lines (the headline allreduce, its parity "
+                         "check and the data-path A/B still run)")
     args = ap.parse_args()
+    if args.gpus < 1:
+        ap.error("--gpus must be >= 1")
+
+    launched = "WORLD_SIZE" in os.environ
+    if not launched and args.gpus > 1:
+        # the driver's `python3 bench.py --gpus N`: form the N ranks ourselves
+        return spawn_ranks(args.gpus, sys.argv[1:])
+    world = _env_int("WORLD_SIZE", 1)
+    if launched and world != args.gpus:
+        print(json.dumps({"metric": METRIC, "error": f"--gpus {args.gpus} but the launcher formed WORLD_SIZE={world} "
+                                                     "ranks"}), flush=True)
+        return 2
 
     import torch
     import mxompi as mx
 
-    world = _env_int("WORLD_SIZE", 1)
     rank = _env_int("RANK", 0)
     local_rank = _env_int("LOCAL_RANK", 0)
     dev = local_rank % max(1, torch.cuda.device_count())
@@ -690,7 +742,8 @@ def main():
     done = False
     if world > 1:
         try:
-            result.update(bench_allreduce(torch, mx, dist, rank, world, dev, args.steps, args.warmup))
+            result.update(bench_allreduce(torch, mx, dist, rank, world, dev, args.steps, args.warmup,
+                                          extras=not args.no_sweep))
             done = True
         except Exception as e:  # noqa: BLE001 - reported in the JSON line
             result["allreduce_error"] = repr(e)
@@ -750,7 +803,8 @@ def main():
         print(json.dumps(result), flush=True)
     if dist is not None:
         dist.destroy_process_group()
+    return 0
 
 
 if __name__ == "__main__":
-    main()
+    sys.exit(main())

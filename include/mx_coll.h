@@ -125,6 +125,24 @@ int mx_comm_get_protocol(const mx_comm_t *comm);
  * (single rank, local communicator, or /dev/shm unavailable on some rank). */
 int mx_comm_set_reg_min(mx_comm_t *comm, size_t min_bytes);
 
+/* Zero-copy allreduce results written straight into every peer's registered
+ * rbuf by the rank that folds each part (1, the default; env MX_ZC_DIRECT=0
+ * at creation switches it off), or through the peers' uncached gather areas
+ * and a local gather copy (0).  Results are identical either way.  Direct
+ * needs sbuf and rbuf at the same misalignment mod 16 (else the gather path
+ * runs).  Same value on every rank. */
+int mx_comm_set_zc_direct(mx_comm_t *comm, int on);
+
+/* Lifecycle calls (communicator / heap create and destroy, first
+ * point-to-point on a communicator, datatype destroy) never wait for the
+ * whole device: another communicator's nonblocking work may be spinning on a
+ * peer that waits for this rank.  The runtime calls that do wait for every
+ * stream (hipFree, hipHostFree, hipIpcCloseMemHandle) are deferred while any
+ * live communicator has device work pending and run at the next lifecycle
+ * call that finds the process quiet.  Returns how many are still deferred
+ * (test support). */
+int mx_release_pending(void);
+
 /* One-shot allreduce (one kernel: push, flag, fold) up to `max_bytes` per
  * rank; clamped to the one-shot slot capacity reserved at creation (1 MiB or
  * staging / (8 n); MX_ONESHOT_MAX at creation sets both).  0 = off.  Same
@@ -166,6 +184,8 @@ typedef struct mx_coll_stats {
     uint64_t zero_copy_calls;  /* allreduces folded between registered user
                                   buffers (no staging copies)               */
     uint64_t staged_calls;     /* allreduces through the staging chunks     */
+    uint64_t direct_calls;     /* zero-copy allreduces whose results went
+                                  straight into the peers' rbufs            */
 } mx_coll_stats_t;
 int mx_comm_set_profiling(mx_comm_t *comm, int on);
 int mx_comm_get_stats(mx_comm_t *comm, mx_coll_stats_t *stats, int reset);

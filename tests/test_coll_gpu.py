@@ -245,6 +245,12 @@ def _mp_worker(rank, n, port, staging, jobs, q, env=None):
             elif kind in ("stats", "stats_reset"):
                 sts = comm.stats(reset=kind == "stats_reset")
                 results.append((sts["zero_copy_calls"], sts["staged_calls"]))
+            elif kind == "direct_stats":
+                results.append(comm.stats()["direct_calls"])
+            elif kind == "zc_direct":
+                # zero-copy results straight into the peers' rbufs, or through the gather areas
+                comm.set_zc_direct(alg == "on")
+                results.append(None)
             elif kind == "path":
                 # force the data path of the next allreduces (same on every rank)
                 comm.set_autotune(alg == "autotune")
@@ -477,7 +483,7 @@ def _check_jobs(n, jobs, got):
     L = _oracle()
     for j, (kind, count, op, t, alg) in enumerate(jobs):
         es = mxompi.type_size(t)
-        if kind == "stats" or kind.startswith("tuning"):
+        if kind in ("stats", "direct_stats", "zc_direct") or kind.startswith("tuning"):
             continue
         if kind.startswith("allreduce") or kind == "shmem":
             xs = [gen(t, op, count, 7000 + r) for r in range(n)]
@@ -607,15 +613,29 @@ _JOBS_ZC = [j for j in _JOBS if j[0].startswith(("allreduce", "reduce_scatter", 
     ("stats", 0, "SUM", "FLOAT", "auto")]
 
 
-@pytest.mark.parametrize("n", [2, 3, 8])
-def test_multiprocess_allreduce_zero_copy(n):
+@pytest.mark.parametrize("n,direct", [(2, True), (3, True), (8, True), (2, False), (8, False)],
+                         ids=["2-direct", "3-direct", "8-direct", "2-gather", "8-gather"])
+def test_multiprocess_allreduce_zero_copy(n, direct):
+    """direct: every zero-copy allreduce's results go straight into the peers'
+    rbufs (the default); gather: through the peers' uncached gather areas and a
+    local gather copy (round 4's path, mx_comm_set_zc_direct(0))."""
     import glob
     before = set(glob.glob("/dev/shm/mx_reg_*"))
     env = {"MX_REG_MIN": "1", "MX_ONESHOT_MAX": "0"}
-    got = _run_mp(n, _JOBS_ZC, env=env)
+    jobs = [("zc_direct", 0, "SUM", "FLOAT", "on" if direct else "off")] + _JOBS_ZC + \
+        [("direct_stats", 0, "SUM", "FLOAT", "auto")]
+    got = _run_mp(n, jobs, env=env)
     assert set(glob.glob("/dev/shm/mx_reg_*")) <= before, "registration page left in /dev/shm"
-    _check_jobs(n, _JOBS_ZC, got)
-    zc, staged = got[0][-1]
+    _check_jobs(n, jobs, got)
+    zc, staged = got[0][-2]
+    n_direct = got[0][-1]
+    if direct:
+        # every zero-copy allreduce of the list whose sbuf and rbuf share a
+        # misalignment (all of them here) took the direct path
+        n_ar = sum(1 for j in _JOBS_ZC if j[0] in ("allreduce", "allreduce_inplace") and "nonoverlapping" not in j[4])
+        assert n_direct == n_ar, (n_direct, n_ar)
+    else:
+        assert n_direct == 0
 
     def eligible(kind, count, t):
         # registered path: every rank's blocks at one misalignment mod 16
@@ -635,7 +655,7 @@ def test_multiprocess_allreduce_zero_copy(n):
     n_zc = sum(1 for j in _JOBS_ZC if eligible(j[0], j[1], j[3]))
     assert staged == n_mis and zc == n_zc, (zc, staged, n_zc)
     for r in range(n):
-        assert got[r][-1] == got[0][-1]
+        assert got[r][-2:] == got[0][-2:]
 
 
 # autotuning (mx_comm_set_autotune, on by default): five allreduces of one

@@ -530,9 +530,13 @@ def _stale_worker(rank, n, port, q):
             # caller's stream right before the call (through this GPU's L2s)
             T.copy_(torch.from_numpy(_gen("FLOAT", count, 5000 + 10 * it + rank)))
             X.copy_(T)
+            # R's lines are in this GPU's L2s (written by the fill kernel); the
+            # zero-copy allreduce's peers write their parts straight into R, and a
+            # kernel reads R right after the call returns (the clone): a line the
+            # call's final acquire left stale would show the NaNs
             R.fill_(float("nan"))
             assert H.mxh_allreduce(X.data_ptr(), R.data_ptr(), count, f32, SUM, comm) == 0
-            res[("allreduce", it)] = R.cpu().numpy().tobytes()
+            res[("allreduce", it)] = R.clone().cpu().numpy().tobytes()
             assert H.mxh_allgather(X.data_ptr(), count, f32, G.data_ptr(), count, f32, comm) == 0
             res[("allgather", it)] = G.cpu().numpy().tobytes()
         H.mxh_comm_free(comm)

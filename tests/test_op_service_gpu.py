@@ -364,3 +364,56 @@ def test_service_resumes_after_a_launch():
             mxompi.reduce2_sync("SUM", "INT64_T", a.data_ptr(), b.data_ptr(), 1000, s.cuda_stream)
         assert mxompi.op_service_stats()[1] - served0 == 20, rnd
     assert torch.all(b == 60).item() and torch.all(bigo == 3).item()
+
+
+_NT_MARK_CHILD = r"""
+import sys, numpy as np, torch
+sys.path.insert(0, sys.argv[1]); sys.path.insert(0, sys.argv[2])
+import mxompi, oracle_lib
+mxompi.init(0)
+O = oracle_lib.oracle()
+side = torch.cuda.Stream()
+bad = []
+# kFusedMarkMax = 1024 * 256 - 16 elements: with every launch forced onto the
+# 64-lane non-temporal instances the grid is up to 4x kMarkFlags workgroups
+for op, t, count in (("SUM", "FLOAT", 1024 * 256 - 16), ("SUM", "FLOAT", 1024 * 64 + 5), ("MAX", "DOUBLE", 1024 * 256 - 17),
+                     ("MAXLOC", "LONG_DOUBLE_INT", 1024 * 256 - 16), ("BXOR", "UINT8_T", 1024 * 256 - 16)):
+    es = mxompi.type_size(t)
+    rng = np.random.default_rng(count)
+    a = rng.integers(0, 7, count * es, dtype=np.uint8)
+    b = rng.integers(0, 7, count * es, dtype=np.uint8)
+    if t in ("FLOAT", "DOUBLE"):
+        a = rng.uniform(-1, 1, count).astype(np.float32 if t == "FLOAT" else np.float64).view(np.uint8)
+        b = rng.uniform(-1, 1, count).astype(np.float32 if t == "FLOAT" else np.float64).view(np.uint8)
+    for rep in range(20):
+        A = torch.from_numpy(a).cuda(); B = torch.from_numpy(b).cuda()
+        torch.cuda.synchronize()
+        # the call returns with inout final for every agent: read it at once
+        # through a copy on another (non-blocking) stream, which is not ordered
+        # after the launch on the default stream
+        mxompi.reduce2_sync(op, t, A.data_ptr(), B.data_ptr(), count, 0)
+        with torch.cuda.stream(side):
+            got = B.cpu().numpy()
+        exp = b.copy()
+        assert O.mxo_reduce2(mxompi.OP[op], mxompi.TYPE[t], a.ctypes.data, exp.ctypes.data, count, 1) == 0
+        if not np.array_equal(got, exp):
+            bad.append((op, t, count, rep)); break
+print("BAD", bad)
+sys.exit(1 if bad else 0)
+"""
+
+
+def test_fused_mark_with_nt_forced_everywhere():
+    """with MX_NT_MIN_BYTES=0 every launch takes the 64-lane
+    non-temporal instances, whose grids near kFusedMarkMax exceed the
+    kMarkFlags per-workgroup flags.  The mark must not ride on such a grid
+    (mark_fit drops it and the call waits through the marker kernel): every
+    result bit-exact vs the oracle."""
+    import os
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, MX_NT_MIN_BYTES="0", MX_OP_SERVICE="0")
+    p = subprocess.run([sys.executable, "-c", _NT_MARK_CHILD, os.path.join(root, "zhpe-ompi_amd"),
+                        os.path.join(root, "tests")], capture_output=True, text=True, env=env, timeout=200)
+    assert p.returncode == 0, p.stdout[-2000:] + p.stderr[-3000:]

@@ -150,7 +150,8 @@ _FP = {"FLOAT": np.float32, "DOUBLE": np.float64, "SHORT_FLOAT": np.float16, "C_
 
 
 def _full_input(op, t, n, es, rng):
-    raw = [rng.integers(0, 256, n * es, dtype=np.uint8) for _ in range(2)]   # padding bytes stay random
+    # padding bytes stay random (raw generator words: 3x faster than integers() at 1 GiB)
+    raw = [rng.bit_generator.random_raw((n * es + 7) // 8).view(np.uint8)[:n * es] for _ in range(2)]
     for r in raw:
         rows = r.reshape(n, es)
         if t in _LOC:

@@ -4,7 +4,8 @@
   pairs : MPI_Reduce_local on the host, every (op, type) pair of the C-only
           op table (116; op_base_functions.c:1485-1569 without the Fortran
           slots), 2-buffer, one host thread, bounded sample (2 x 64 MiB
-          buffers, each pair repeated for ~0.2 s).
+          buffers; per pair the median of >= 20 calls, each from pristine
+          operands; SURVEY 8(d) value distributions, seed 0x5EEDC0DE).
   pack  : MPI_Pack / MPI_Unpack of the CFG-C derived types (the pack sweep's
           types, tools/sweep.py PACK_TYPES) through the convertor walk, one
           host thread, 256 MiB packed per call, ~0.5 s per type and direction.
@@ -80,30 +81,52 @@ def _timed(fn, min_s):
             return el / n, n
 
 
-def _fill(buf, tname, rng):
-    """sane values per type, as tools/sweep.py fill(): FP uniform [0.5, 2),
-    finite normal x87 values, random bytes for integers"""
-    buf[:] = rng.integers(0, 256, buf.size, dtype=np.uint8)
-    if tname in ("FLOAT", "C_FLOAT_COMPLEX"):
-        buf.view(np.float32)[:] = rng.uniform(0.5, 2.0, buf.size // 4)
-    elif tname in ("DOUBLE", "C_DOUBLE_COMPLEX"):
-        buf.view(np.float64)[:] = rng.uniform(0.5, 2.0, buf.size // 8)
-    elif tname in ("LONG_DOUBLE", "C_LONG_DOUBLE_COMPLEX"):
+# SURVEY 8(d)'s value distributions, per (op, type): integers full-range
+# uniform; FP (and complex parts, and x87 values) uniform [-1, 1) for SUM and
+# MAX / MIN, [0.5, 2) for PROD; the LOC pairs' values drawn from 16 distinct
+# values (ties) with random int indices.  tools/sweep.py fill() makes the same
+# distributions on the device.
+_LOC = {"FLOAT_INT": (np.float32, 8), "DOUBLE_INT": (np.float64, 16), "LONG_INT": (np.int64, 16),
+        "2INT": (np.int32, 8), "SHORT_INT": (np.int16, 8), "LONG_DOUBLE_INT": (np.longdouble, 32),
+        "2REAL": (np.float32, 8), "2DOUBLE_PRECISION": (np.float64, 16), "2INTEGER": (np.int32, 8)}
+_F32 = {"FLOAT", "REAL", "REAL4", "C_FLOAT_COMPLEX"}
+_F64 = {"DOUBLE", "REAL8", "DOUBLE_PRECISION", "C_DOUBLE_COMPLEX"}
+_X87 = {"LONG_DOUBLE", "C_LONG_DOUBLE_COMPLEX"}
+
+
+def fill(buf, tname, opname, rng):
+    buf[:] = rng.bit_generator.random_raw((buf.size + 7) // 8).view(np.uint8)[:buf.size]
+    lo, hi = (0.5, 2.0) if opname == "PROD" else (-1.0, 1.0)
+    if tname in _F32:
+        buf.view(np.float32)[:] = rng.uniform(lo, hi, buf.size // 4)
+    elif tname in _F64:
+        buf.view(np.float64)[:] = rng.uniform(lo, hi, buf.size // 8)
+    elif tname in _X87:
         v = buf.view(np.longdouble)
-        v[:] = rng.uniform(0.5, 2.0, v.size).astype(np.longdouble)
-    elif tname == "LONG_DOUBLE_INT":
-        w = buf.view(np.longdouble).reshape(-1, 2)
-        w[:, 0] = rng.uniform(0.5, 2.0, w.shape[0]).astype(np.longdouble)
-    elif tname == "FLOAT_INT":
-        buf.view(np.float32).reshape(-1, 2)[:, 0] = rng.uniform(0.5, 2.0, buf.size // 8)
-    elif tname == "DOUBLE_INT":
-        buf.view(np.float64).reshape(-1, 2)[:, 0] = rng.uniform(0.5, 2.0, buf.size // 16)
+        v[:] = rng.uniform(lo, hi, v.size).astype(np.longdouble)
+    elif tname in _LOC:
+        vt, es = _LOC[tname]
+        n = buf.size // es
+        rows = buf[:n * es].reshape(n, es)
+        vals = rng.integers(0, 16, n).astype(vt)                     # 16 distinct values: ties
+        vs = 10 if vt is np.longdouble else np.dtype(vt).itemsize
+        rows[:, :vs] = vals.view(np.uint8).reshape(n, -1)[:, :vs]
+        io = 16 if vt is np.longdouble else np.dtype(vt).itemsize
+        io = 4 if tname == "SHORT_INT" else io                       # {short; int} at offset 4
+        rows[:, io:io + 4] = rng.integers(-(1 << 31), 1 << 31, n, dtype=np.int64).astype("<i4").view(
+            np.uint8).reshape(n, 4)
 
 
-def sweep_pairs(L, nbytes, min_s):
+def sweep_pairs(L, nbytes, min_s, reps_min=20):
+    """Every timed call starts from pristine operands: `inout` is restored
+    from its untouched copy before each call, outside the timed region
+    (a sweep that ran every op in place over the same
+    buffer measured MINLOC on data converged to all ties).  Median of at
+    least `reps_min` calls and `min_s` seconds of calls."""
     import mxompi as mx
-    rng = np.random.default_rng(0x5EED)
+    rng = np.random.default_rng(0x5EEDC0DE)
     a = np.empty(nbytes, np.uint8)
+    b0 = np.empty(nbytes, np.uint8)
     b = np.empty(nbytes, np.uint8)
     rows = []
     for t, tname in enumerate(mx.TYPES):
@@ -112,12 +135,31 @@ def sweep_pairs(L, nbytes, min_s):
             continue
         es = L.mxo_type_size(t)
         count = nbytes // es
-        _fill(a, tname, rng)
-        _fill(b, tname, rng)
         for o in ops:
-            sec, n = _timed(lambda: L.mxo_reduce2(o, t, a.ctypes.data, b.ctypes.data, count, 0), min_s)
+            fill(a, tname, mx.OPS[o], rng)
+            fill(b0, tname, mx.OPS[o], rng)
+            ts = []
+            spent = 0.0
+            for k in range(reps_min + 2):
+                np.copyto(b, b0)                      # pristine inout, untimed
+                t0 = time.perf_counter()
+                L.mxo_reduce2(o, t, a.ctypes.data, b.ctypes.data, count, 0)
+                dt = time.perf_counter() - t0
+                if k >= 2:                            # two warm calls
+                    ts.append(dt)
+                    spent += dt
+                if k >= reps_min + 1 and spent >= min_s:
+                    break
+            while spent < min_s:
+                np.copyto(b, b0)
+                t0 = time.perf_counter()
+                L.mxo_reduce2(o, t, a.ctypes.data, b.ctypes.data, count, 0)
+                dt = time.perf_counter() - t0
+                ts.append(dt)
+                spent += dt
+            sec = float(np.median(ts))
             gbs = 3.0 * count * es / sec / 1e9
-            rows.append({"op": mx.OPS[o], "type": tname, "elem_bytes": es, "count": count, "calls": n,
+            rows.append({"op": mx.OPS[o], "type": tname, "elem_bytes": es, "count": count, "calls": len(ts),
                          "ms": round(sec * 1e3, 3), "gbs": round(gbs, 2)})
             print(f"cpu pair {mx.OPS[o]:>6} {tname:<22} {sec * 1e3:9.2f} ms {gbs:8.2f} GB/s", flush=True)
     return rows
@@ -197,10 +239,13 @@ def main():
         doc = {"host_cpu": cpu_model(), "cores": 1, "kind": "port",
                "build": "oracle/build/libmx_oracle_bench.so: -O3 -finline-functions -fno-strict-aliasing (the "
                         "reference's default optimisation flags, config/opal_setup_cc.m4), x86-64 baseline ISA",
-               "sample": f"pairs: 2 x {args.pair_bytes >> 20} MiB host buffers, each pair >= {args.min_s} s; pack: "
+               "sample": f"pairs: 2 x {args.pair_bytes >> 20} MiB host buffers, per pair the median of >= 20 calls "
+                         f"(>= {args.min_s} s of calls), every call from pristine operands (inout restored outside the "
+                         "timed region), SURVEY 8(d) distributions (seed 0x5EEDC0DE: integers full range, FP SUM/MAX/MIN "
+                         "uniform [-1,1), PROD [0.5,2), LOC 16 distinct values); pack: "
                          f"{args.pack_bytes >> 20} MiB packed per call, >= {2.5 * args.min_s} s per direction; "
                          "1 host thread",
-               "when": time.strftime("%F %T")}
+               "when": time.strftime("%F %T"), "source_run": os.environ.get("MX_SWEEP_RUN", "")}
         what = args.what.split(",")
         if "pairs" in what:
             doc["pairs"] = sweep_pairs(L, args.pair_bytes, args.min_s)

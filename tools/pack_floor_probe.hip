@@ -1,0 +1,88 @@
+// pack_floor_probe.hip -- diagnostic (not product): the HBM floor of a PACK
+// of a layout whose user span is `span` bytes for `packed` packed bytes
+// (VERDICT r4 next 3).  A pack must read the user span (every line holding
+// data; for the CFG-C types that is the whole span) and write the packed
+// stream once.  The floor kernel does exactly that with no layout work:
+// lane k writes packed granule k (16 B) and reads span granules
+// [k*r, (k+1)*r) (r = span / packed, coalesced: a wave reads 64*r*16
+// consecutive bytes), xor-folding them so no load is dead.
+//   plain   cached loads and stores
+//   nt      non-temporal loads and stores (the product's policy at >= 384 MiB)
+// usage: pack_floor_probe NAME SPAN_BYTES PACKED_BYTES [NAME SPAN PACKED ...]
+// Prints the median of 9 timed launches per variant (HIP events), the time,
+// and GB/s as 2 x packed (algorithmic, the product's unit) and as
+// span + packed (bytes moved).
+#include <hip/hip_runtime.h>
+#include <algorithm>
+#include <cstdio>
+#include <cstdlib>
+#include <vector>
+
+#define CK(x) do { hipError_t e_ = (x); if (e_ != hipSuccess) { printf("HIP %s at %d\n", hipGetErrorString(e_), __LINE__); return 1; } } while (0)
+
+typedef uint32_t v4u __attribute__((ext_vector_type(4)));
+constexpr int kB = 256;
+
+template <bool NT>
+__global__ void __launch_bounds__(kB) k_floor(const v4u *span, uint64_t nspan, v4u *packed, uint64_t npk,
+                                              uint64_t r_num, uint64_t r_den) {
+  const uint64_t k = (uint64_t)blockIdx.x * kB + threadIdx.x;
+  if (k >= npk) return;
+  uint64_t j0 = k * r_num / r_den, j1 = (k + 1) * r_num / r_den;
+  if (j1 > nspan) j1 = nspan;
+  v4u acc = {(uint32_t)k, 0, 0, 0};
+  for (uint64_t j = j0; j < j1; j++) {
+    const v4u v = NT ? __builtin_nontemporal_load(span + j) : span[j];
+    acc ^= v;
+  }
+  if (NT) __builtin_nontemporal_store(acc, packed + k);
+  else packed[k] = acc;
+}
+
+int main(int argc, char **argv) {
+  if (argc < 4 || (argc - 1) % 3) {
+    printf("usage: %s NAME SPAN_BYTES PACKED_BYTES [...]\n", argv[0]);
+    return 2;
+  }
+  hipEvent_t e0, e1;
+  CK(hipEventCreate(&e0));
+  CK(hipEventCreate(&e1));
+  for (int a = 1; a + 2 < argc; a += 3) {
+    const char *name = argv[a];
+    const uint64_t span = strtoull(argv[a + 1], nullptr, 0), pk = strtoull(argv[a + 2], nullptr, 0);
+    const uint64_t nspan = (span + 15) / 16, npk = (pk + 15) / 16;
+    v4u *s = nullptr, *p = nullptr;
+    CK(hipMalloc(&s, nspan * 16));
+    CK(hipMalloc(&p, npk * 16));
+    CK(hipMemset(s, 1, nspan * 16));
+    CK(hipMemset(p, 0, npk * 16));
+    for (int nt = 0; nt < 2; nt++) {
+      auto launch = [&] {
+        const dim3 g((unsigned)((npk + kB - 1) / kB)), b(kB);
+        if (nt) hipLaunchKernelGGL(k_floor<true>, g, b, 0, 0, s, nspan, p, npk, nspan, npk);
+        else hipLaunchKernelGGL(k_floor<false>, g, b, 0, 0, s, nspan, p, npk, nspan, npk);
+      };
+      launch();
+      CK(hipDeviceSynchronize());
+      std::vector<float> ts;
+      for (int r = 0; r < 9; r++) {
+        CK(hipEventRecord(e0, 0));
+        launch();
+        CK(hipEventRecord(e1, 0));
+        CK(hipEventSynchronize(e1));
+        float ms = 0;
+        CK(hipEventElapsedTime(&ms, e0, e1));
+        ts.push_back(ms);
+      }
+      std::sort(ts.begin(), ts.end());
+      const double us = ts[4] * 1e3;
+      printf("%-32s %-5s span %12llu packed %12llu  %9.1f us  2x packed %7.1f GB/s  moved %7.1f GB/s\n", name,
+             nt ? "nt" : "plain", (unsigned long long)span, (unsigned long long)pk, us, 2.0 * pk / us / 1e3,
+             (double)(span + pk) / us / 1e3);
+      fflush(stdout);
+    }
+    CK(hipFree(s));
+    CK(hipFree(p));
+  }
+  return 0;
+}

@@ -31,37 +31,56 @@ F64 = {"DOUBLE", "REAL8", "DOUBLE_PRECISION", "C_DOUBLE_COMPLEX", "2DOUBLE_PRECI
 X87 = {"LONG_DOUBLE", "C_LONG_DOUBLE_COMPLEX"}
 
 
-def fill(torch, buf, tname, gen):
-    """Overwrite a uint8 device buffer with sane values of type `tname`
-    (random bytes for integers; uniform [0.5, 2) for floating point; finite
-    normal x87 values for long double) so FP timing is not dominated by NaN
-    paths."""
+LOC = {"FLOAT_INT": ("f4", 8, 4), "DOUBLE_INT": ("f8", 16, 8), "LONG_INT": ("i8", 16, 8), "2INT": ("i4", 8, 4),
+       "SHORT_INT": ("i2", 8, 4), "2REAL": ("f4", 8, 4), "2DOUBLE_PRECISION": ("f8", 16, 8), "2INTEGER": ("i4", 8, 4)}
+
+
+def fill(torch, buf, tname, gen, opname=None):
+    """Overwrite a uint8 device buffer with values of type `tname` drawn from
+    SURVEY 8(d)'s distributions (tools/cpu_sweep.py fill() is the host twin):
+    integers full-range uniform; FP SUM / MAX / MIN uniform [-1, 1), PROD
+    [0.5, 2) (complex parts alike); x87 values of magnitude ~1 (random sign
+    and mantissa, exponent 16382..16383); LOC pairs' values from 16 distinct
+    values (ties) with random int indices."""
     nb = buf.numel()
     buf.copy_(torch.randint(0, 256, (nb,), dtype=torch.uint8, device=buf.device, generator=gen))
+    lo, hi = (0.5, 2.0) if opname == "PROD" else (-1.0, 1.0)
     if tname in F32:
-        v = buf.view(torch.float32)
-        v.uniform_(0.5, 2.0, generator=gen)
+        buf.view(torch.float32).uniform_(lo, hi, generator=gen)
     elif tname in F64:
-        v = buf.view(torch.float64)
-        v.uniform_(0.5, 2.0, generator=gen)
+        buf.view(torch.float64).uniform_(lo, hi, generator=gen)
     elif tname in X87 or tname == "LONG_DOUBLE_INT":
         stride = 4 if tname == "LONG_DOUBLE_INT" else 2   # int64 words per element
         w = buf.view(torch.int64).view(-1, stride)
         w[:, 0] |= torch.iinfo(torch.int64).min             # explicit integer bit
-        w[:, 1] = 16383 + torch.randint(-2, 3, (w.shape[0],), device=buf.device, generator=gen)
-    elif tname == "FLOAT_INT":
-        buf.view(torch.float32).view(-1, 2)[:, 0].uniform_(0.5, 2.0, generator=gen)
-    elif tname == "DOUBLE_INT":
-        buf.view(torch.float64).view(-1, 2)[:, 0].uniform_(0.5, 2.0, generator=gen)
+        sign = (torch.randint(0, 2, (w.shape[0],), device=buf.device, generator=gen) << 15) if opname != "PROD" else 0
+        w[:, 1] = (16382 + torch.randint(0, 2, (w.shape[0],), device=buf.device, generator=gen)) | sign
+        if tname == "LONG_DOUBLE_INT":                       # 16 distinct values (ties)
+            w[:, 0] = torch.iinfo(torch.int64).min | (torch.randint(0, 16, (w.shape[0],), device=buf.device,
+                                                                    generator=gen) << 59)
+    elif tname in LOC:
+        vt, es, io = LOC[tname]
+        rows = buf.view(-1, es)
+        n = rows.shape[0]
+        tv = {"f4": torch.float32, "f8": torch.float64, "i8": torch.int64, "i4": torch.int32, "i2": torch.int16}[vt]
+        vals = torch.randint(0, 16, (n,), device=buf.device, generator=gen).to(tv)
+        vs = vals.element_size()
+        rows[:, :vs] = vals.view(torch.uint8).view(n, vs)
 
 
-def time_launches(torch, fn, iters, reps):
-    """median over `iters` batches of `reps` back-to-back launches, ms per launch"""
+def time_launches(torch, fn, iters, reps, prep=None):
+    """median over `iters` batches of `reps` back-to-back launches, ms per
+    launch; `prep` runs before each batch, outside the timed region (restores
+    the in-place operand, so every batch starts from pristine data)"""
     stream = torch.cuda.current_stream()
+    if prep:
+        prep()
     fn()
     torch.cuda.synchronize()
     out = []
     for _ in range(iters):
+        if prep:
+            prep()
         s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         s.record(stream)
         for _ in range(reps):
@@ -77,6 +96,7 @@ def sweep_pairs(torch, mx, nbytes, iters, only=None):
     sp = torch.cuda.current_stream().cuda_stream
     gen = torch.Generator(device="cuda").manual_seed(0x5EEDC0DE)
     a = torch.empty(nbytes, dtype=torch.uint8, device="cuda")
+    b0 = torch.empty(nbytes, dtype=torch.uint8, device="cuda")
     b = torch.empty(nbytes, dtype=torch.uint8, device="cuda")
     rows = []
     for t, tname in enumerate(mx.TYPES):
@@ -87,10 +107,12 @@ def sweep_pairs(torch, mx, nbytes, iters, only=None):
             continue
         es = mx.type_size(t)
         count = nbytes // es
-        fill(torch, a, tname, gen)
-        fill(torch, b, tname, gen)
         for o in ops:
-            ms = time_launches(torch, lambda: mx.reduce2(o, t, a.data_ptr(), b.data_ptr(), count, sp), iters, 1)
+            fill(torch, a, tname, gen, mx.OPS[o])
+            fill(torch, b0, tname, gen, mx.OPS[o])
+            # every timed launch starts from pristine inout (b restored from b0)
+            ms = time_launches(torch, lambda: mx.reduce2(o, t, a.data_ptr(), b.data_ptr(), count, sp), iters, 1,
+                               prep=lambda: b.copy_(b0))
             gbs = 3.0 * count * es / (ms * 1e-3) / 1e9
             rows.append({"op": mx.OPS[o], "type": tname, "elem_bytes": es, "count": count,
                          "ms": round(ms, 4), "gbs": round(gbs, 1), "frac_hbm": round(gbs / HBM_PEAK_GBS, 4)})

@@ -301,6 +301,8 @@ extern "C" int mx_comm_set_timeout(mx_comm_t *c, double seconds) {
 extern "C" int mx_comm_size(const mx_comm_t *c) { return c ? c->size : MX_ERR_ARG; }
 extern "C" int mx_comm_rank(const mx_comm_t *c) { return c ? c->rank : MX_ERR_ARG; }
 
+static void live_add(mx_comm *c);
+
 extern "C" int mx_comm_create_local(int size, int device, mx_comm_t **out) {
   if (!out || size < 1 || size > MAXR) return MX_ERR_ARG;
   int rc = mx_init(device);
@@ -312,6 +314,7 @@ extern "C" int mx_comm_create_local(int size, int device, mx_comm_t **out) {
   c->device = g_device;
   c->local = 1;
   mx_comm_set_timeout(c, 60.0);
+  live_add(c);
   *out = c;
   return MX_SUCCESS;
 }
@@ -364,9 +367,78 @@ static size_t reg_min() {
   return v > 0 ? (size_t)v : 0;
 }
 
+// ---------------------------------------------------------------------------
+// live communicators and deferred releases.  On this runtime
+// hipFree, hipHostFree and hipIpcCloseMemHandle wait for every stream of the
+// device (tools/lifecycle_sync_probe.hip, profiles/r05/lifecycle_sync_probe.txt),
+// so a communicator freed -- or a stale zero-copy mapping closed -- while
+// another communicator's request spins on a peer could deadlock a legal
+// program.  They run when no live communicator has device work pending.
+// ---------------------------------------------------------------------------
+static std::mutex g_live_mu;
+static std::vector<mx_comm *> g_live;
+struct Deferred { void *p; int kind; };
+static std::vector<Deferred> g_graveyard;
+
+static void live_add(mx_comm *c) {
+  std::lock_guard<std::mutex> lk(g_live_mu);
+  g_live.push_back(c);
+}
+static void live_del(mx_comm *c) {
+  std::lock_guard<std::mutex> lk(g_live_mu);
+  for (size_t i = 0; i < g_live.size(); i++)
+    if (g_live[i] == c) { g_live[i] = g_live.back(); g_live.pop_back(); break; }
+}
+static bool pending(hipError_t e) {
+  if (e == hipErrorNotReady) { (void)hipGetLastError(); return true; }
+  if (e != hipSuccess) (void)hipGetLastError();   // a failed request reports itself at its wait
+  return false;
+}
+static bool device_quiet_locked() {
+  for (mx_comm *c : g_live) {
+    if (c->tail_valid && c->tail && pending(hipEventQuery(c->tail))) return false;
+    for (int i = 0; i < 3; i++)
+      if (c->p2p_stream[i] && pending(hipStreamQuery(c->p2p_stream[i]))) return false;
+  }
+  return true;
+}
+bool mx::device_quiet() {
+  std::lock_guard<std::mutex> lk(g_live_mu);
+  return device_quiet_locked();
+}
+static void release_now(void *p, int kind) {
+  hipError_t e = kind == REL_IPC ? hipIpcCloseMemHandle(p) : kind == REL_HOST ? hipHostFree(p) : hipFree(p);
+  if (e != hipSuccess) (void)hipGetLastError();
+}
+bool mx::release_now_if_quiet(void *p, int kind) {
+  if (!p) return true;
+  std::unique_lock<std::mutex> lk(g_live_mu);
+  if (!device_quiet_locked()) {
+    g_graveyard.push_back(Deferred{p, kind});
+    return false;
+  }
+  lk.unlock();
+  release_now(p, kind);
+  return true;
+}
+void mx::release_later(void *p, int kind) { (void)release_now_if_quiet(p, kind); }
+void mx::release_flush() {
+  std::vector<Deferred> go;
+  {
+    std::lock_guard<std::mutex> lk(g_live_mu);
+    if (g_graveyard.empty() || !device_quiet_locked()) return;
+    go.swap(g_graveyard);
+  }
+  for (const Deferred &d : go) release_now(d.p, d.kind);
+}
+extern "C" int mx_release_pending(void) {   // tests: deferred releases not yet run
+  std::lock_guard<std::mutex> lk(g_live_mu);
+  return (int)g_graveyard.size();
+}
+
 static void reg_release(mx_comm *c) {
   if (c->reg_imp) {
-    for (const mx_reg_import &m : *c->reg_imp) (void)hipIpcCloseMemHandle(m.ptr);
+    for (const mx_reg_import &m : *c->reg_imp) release_later(m.ptr, REL_IPC);
     delete c->reg_imp;
     c->reg_imp = nullptr;
   }
@@ -423,6 +495,19 @@ extern "C" int mx_comm_set_protocol(mx_comm_t *c, int proto) {
 }
 
 extern "C" int mx_comm_get_protocol(const mx_comm_t *c) { return c ? c->proto : MX_ERR_ARG; }
+
+// MX_ZC_DIRECT=0: zero-copy allreduce results go through the peers' uncached
+// gather areas and a gather copy (round 4's path; A/B switch)
+static int zc_direct_default() {
+  const char *e = getenv("MX_ZC_DIRECT");
+  return !(e && *e == '0');
+}
+
+extern "C" int mx_comm_set_zc_direct(mx_comm_t *c, int on) {
+  if (!c) return MX_ERR_ARG;
+  c->zc_direct = on ? 1 : 0;
+  return MX_SUCCESS;
+}
 
 extern "C" int mx_comm_set_autotune(mx_comm_t *c, int on) {
   if (!c) return MX_ERR_ARG;
@@ -509,7 +594,9 @@ static void ipc_quarantine_scan() {
   for (size_t i = 0; i < g_ipc_quarantine.size();) {
     IpcQuarantine &q = g_ipc_quarantine[i];
     uint64_t bye[MAXR];
-    bool clear = hipMemcpy(bye, q.flags + BYE_BASE, sizeof bye, hipMemcpyDeviceToHost) == hipSuccess;
+    hipStream_t ls = life_stream();
+    bool clear = ls && hipMemcpyAsync(bye, q.flags + BYE_BASE, sizeof bye, hipMemcpyDeviceToHost, ls) == hipSuccess &&
+                 hipStreamSynchronize(ls) == hipSuccess;
     if (!clear) (void)hipGetLastError();
     for (int p = 0; clear && p < MAXR; p++)
       if (((q.peers >> p) & 1) && bye[p] != BYE_WORD) clear = false;
@@ -603,6 +690,7 @@ extern "C" int mx_comm_create_ex(int rank, int size, int device, size_t staging_
   if (!out || !ag || size < 1 || rank < 0 || rank >= size) return MX_ERR_ARG;
   if ((flags & MX_COMM_IPC) && size > MAXR) return MX_ERR_ARG;
   int ok = mx_init(device) == MX_SUCCESS;
+  if (ok) release_flush();
   mx_comm *c = (mx_comm *)calloc(1, sizeof(mx_comm));
   ok = ok && c;
   int rc = MX_ERR_HIP;
@@ -613,13 +701,20 @@ extern "C" int mx_comm_create_ex(int rank, int size, int device, size_t staging_
     c->flags = flags;
     c->ag = ag;
     c->ag_ctx = ctx;
+    c->zc_direct = zc_direct_default();
     mx_comm_set_timeout(c, 60.0);
   }
-  ok = ok && hipHostMalloc((void **)&c->err_host, sizeof(int), hipHostMallocMapped) == hipSuccess;
+  // no device-wide synchronisation anywhere in creation: another
+  // communicator's collective or receive may be spinning on a peer that is
+  // about to enter this very creation; small buffers come
+  // from the process pools, memsets and copies run on the lifecycle stream
+  hipStream_t ls = ok ? life_stream() : nullptr;
+  ok = ok && ls;
+  ok = ok && (c->err_host = (int *)pool_host_get(sizeof(int))) != nullptr;
   if (ok) *c->err_host = 0;
   ok = ok && hipHostGetDevicePointer((void **)&c->err_dev, c->err_host, 0) == hipSuccess;
-  ok = ok && hipMalloc((void **)&c->poison, sizeof(int)) == hipSuccess &&
-       hipMemset(c->poison, 0, sizeof(int)) == hipSuccess;
+  ok = ok && (c->poison = (int *)pool_dev_get(sizeof(int))) != nullptr &&
+       hipMemsetAsync(c->poison, 0, sizeof(int), ls) == hipSuccess;
 
   if (flags & MX_COMM_IPC) {
     ipc_info mine, all[MAXR];
@@ -648,15 +743,14 @@ extern "C" int mx_comm_create_ex(int rank, int size, int device, size_t staging_
       ok = ipc_region_alloc(c->staging_alloc, &c->staging) == MX_SUCCESS &&
            ipc_region_alloc(ALL_FLAG_WORDS * sizeof(uint64_t), (char **)&c->flagmem) == MX_SUCCESS &&
            (!c->hregion_bytes || ipc_region_alloc(c->hregion_bytes, &c->hregion) == MX_SUCCESS) &&
-           hipMemset(c->flagmem, 0, ALL_FLAG_WORDS * sizeof(uint64_t)) == hipSuccess &&
-           hipDeviceSynchronize() == hipSuccess &&
+           hipMemsetAsync(c->flagmem, 0, ALL_FLAG_WORDS * sizeof(uint64_t), ls) == hipSuccess &&
            hipIpcGetMemHandle(&mine.staging, c->staging) == hipSuccess &&
            hipIpcGetMemHandle(&mine.flags, c->flagmem) == hipSuccess &&
            (!c->hregion || hipIpcGetMemHandle(&mine.hregion, c->hregion) == hipSuccess) &&
            // signature words, read back through every mapping below
-           hipMemcpy(c->flagmem + FLAG_WORDS, sig, sizeof sig, hipMemcpyHostToDevice) == hipSuccess &&
-           (!c->hregion || hipMemcpy(c->hregion, sig + 1, 8, hipMemcpyHostToDevice) == hipSuccess) &&
-           hipDeviceSynchronize() == hipSuccess;
+           hipMemcpyAsync(c->flagmem + FLAG_WORDS, sig, sizeof sig, hipMemcpyHostToDevice, ls) == hipSuccess &&
+           (!c->hregion || hipMemcpyAsync(c->hregion, sig + 1, 8, hipMemcpyHostToDevice, ls) == hipSuccess) &&
+           hipStreamSynchronize(ls) == hipSuccess;
       if (!ok) (void)hipGetLastError();   // a failed export must not surface at a later launch
       mine.staging_bytes = c->staging_bytes;
       mine.hregion_bytes = c->hregion_bytes;
@@ -704,10 +798,10 @@ extern "C" int mx_comm_create_ex(int rank, int size, int device, size_t staging_
     // creation here instead of corrupting data later)
     for (int p = 0; ok && p < size; p++) {
       uint64_t v[2] = {0, 0};
-      if (hipMemcpy(v, c->peer_flags[p] + FLAG_WORDS, 8, hipMemcpyDeviceToHost) != hipSuccess ||
-          v[0] != 0x5EED0000ull + (uint64_t)p ||
-          (c->hregion && (hipMemcpy(v + 1, c->peer_hregion[p], 8, hipMemcpyDeviceToHost) != hipSuccess ||
-                          v[1] != 0x5EED1000ull + (uint64_t)p))) {
+      if (hipMemcpyAsync(v, c->peer_flags[p] + FLAG_WORDS, 8, hipMemcpyDeviceToHost, ls) != hipSuccess ||
+          (c->hregion && hipMemcpyAsync(v + 1, c->peer_hregion[p], 8, hipMemcpyDeviceToHost, ls) != hipSuccess) ||
+          hipStreamSynchronize(ls) != hipSuccess || v[0] != 0x5EED0000ull + (uint64_t)p ||
+          (c->hregion && v[1] != 0x5EED1000ull + (uint64_t)p)) {
         fprintf(stderr, "mx_comm_create: rank %d: mapping of rank %d shows 0x%llx/0x%llx\n", rank, p,
                 (unsigned long long)v[0], (unsigned long long)v[1]);
         ok = 0;
@@ -763,13 +857,21 @@ extern "C" int mx_comm_create_ex(int rank, int size, int device, size_t staging_
       return rc < 0 ? MX_ERR_HIP : MX_ERR_RCCL;
     }
   }
+  live_add(c);
   *out = c;
   return MX_SUCCESS;
 }
 
 extern "C" int mx_comm_destroy(mx_comm_t *c) {
   if (!c) return MX_SUCCESS;
-  (void)hipDeviceSynchronize();
+  // wait for this communicator's own work only -- its last deferred
+  // collective (requests run in issue order behind the tail event) and its
+  // point-to-point channels -- never for the whole device: another
+  // communicator's request may be spinning on a peer that waits for this
+  // rank's next step (example 2).  Blocking calls ended
+  // before they returned.
+  if (c->tail_valid && c->tail && hipEventSynchronize(c->tail) != hipSuccess) (void)hipGetLastError();
+  p2p_quiesce(c);
   uint32_t peers = 0;
   if (c->live) {
     // this rank's last access to its peers' regions is over: say BYE to each
@@ -782,21 +884,23 @@ extern "C" int mx_comm_destroy(mx_comm_t *c) {
         a.peer_flag[p] = c->peer_flags[p] + BYE_BASE + c->rank;
         peers |= 1u << p;
       }
-    hipLaunchKernelGGL(k_bye, dim3(1), dim3(64), 0, nullptr, a);
-    if (hipGetLastError() != hipSuccess || hipStreamSynchronize(nullptr) != hipSuccess) (void)hipGetLastError();
+    hipStream_t ls = life_stream();
+    hipLaunchKernelGGL(k_bye, dim3(1), dim3(64), 0, ls, a);
+    if (hipGetLastError() != hipSuccess || hipStreamSynchronize(ls) != hipSuccess) (void)hipGetLastError();
   }
+  live_del(c);
   for (int p = 0; p < c->size && p < MAXR; p++) {
     if (p == c->rank) continue;
-    if (c->peer_staging[p]) (void)hipIpcCloseMemHandle(c->peer_staging[p]);
-    if (c->peer_flags[p]) (void)hipIpcCloseMemHandle(c->peer_flags[p]);
-    if (c->peer_hregion[p]) (void)hipIpcCloseMemHandle(c->peer_hregion[p]);
+    release_later(c->peer_staging[p], REL_IPC);
+    release_later(c->peer_flags[p], REL_IPC);
+    release_later(c->peer_hregion[p], REL_IPC);
   }
   // creation failed (not live): a peer may have mapped the regions and will
   // never say BYE, so they stay allocated -- never reused, never freed under
   // a peer's mapping
   if (c->live || c->size == 1) ipc_regions_release(c->staging, c->hregion, c->flagmem, peers);
-  if (c->err_host) (void)hipHostFree(c->err_host);
-  if (c->poison) (void)hipFree(c->poison);
+  pool_host_put(c->err_host, sizeof(int));
+  pool_dev_put(c->poison, sizeof(int));
   if (c->nccl) ncclCommDestroy(c->nccl);
   if (c->prof)
     for (int i = 0; i < 64; i++) (void)hipEventDestroy(c->ev[i]);
@@ -804,6 +908,7 @@ extern "C" int mx_comm_destroy(mx_comm_t *c) {
   reg_release(c);
   p2p_release(c);
   free(c);
+  release_flush();
   return MX_SUCCESS;
 }
 
@@ -1529,8 +1634,12 @@ static char *reg_import(mx_comm *c, int p, const RegBuf &b, const RegBuf *own, i
   for (size_t i = 0; i < v.size();) {
     const mx_reg_import &m = v[i];
     if (m.peer == p && m.base < b.base + b.size && b.base < m.base + m.size) {   // overlaps: stale
-      (void)hipIpcCloseMemHandle(m.ptr);
+      char *stale = m.ptr;
       v.erase(v.begin() + (long)i);
+      // the stale import must be gone before the new handle opens; while
+      // another communicator's work is pending the close waits in the list
+      // and this call declines (every rank falls back to the staged path)
+      if (!release_now_if_quiet(stale, REL_IPC)) return nullptr;
       continue;
     }
     held += m.peer == p;
@@ -1540,7 +1649,7 @@ static char *reg_import(mx_comm *c, int p, const RegBuf &b, const RegBuf *own, i
     size_t lru = (size_t)-1;
     for (size_t i = 0; i < v.size(); i++)
       if (v[i].peer == p && (lru == (size_t)-1 || v[i].used < v[lru].used)) lru = i;
-    (void)hipIpcCloseMemHandle(v[lru].ptr);
+    release_later(v[lru].ptr, REL_IPC);
     v.erase(v.begin() + (long)lru);
   }
   char *ptr = nullptr;
@@ -1553,7 +1662,7 @@ static char *reg_import(mx_comm *c, int p, const RegBuf &b, const RegBuf *own, i
   // staged path
   for (int i = 0; i < nown; i++)
     if ((uint64_t)(uintptr_t)ptr < own[i].base + own[i].size && own[i].base < (uint64_t)(uintptr_t)ptr + b.size) {
-      (void)hipIpcCloseMemHandle(ptr);
+      release_later(ptr, REL_IPC);
       return nullptr;
     }
   v.push_back(mx_reg_import{p, b.base, b.size, b.id, ptr, ++c->reg_tick});
@@ -1624,21 +1733,32 @@ static int reg_exchange(mx_comm *c, const char *sb, size_t sbytes, char *rb, siz
 static int allreduce_staged(mx_comm *c, fold_launch_fn fl, int alg, const char *sb, char *rb, size_t count,
                             size_t es, int zc_mode, hipStream_t s) {
   const int n = c->size, r = c->rank;
-  // Zero-copy input: with every rank's sbuf registered, the fold reads the
-  // peers' parts straight from their sbufs over xGMI (the PULL fold without
-  // its input copy).  Results still travel through the peers' uncached
-  // gather areas: every remote WRITE of this library lands in uncached
-  // memory, so no GPU's L2 can hold a stale copy of it.
+  // Zero-copy: with every rank's sbuf and rbuf registered, the fold of part
+  // r reads the peers' parts straight from their sbufs over xGMI and
+  // (zc_direct, the default) stores the result straight into every peer's
+  // rbuf: one kernel moves every byte of the call, both directions of every
+  // link at once, and no staging is used (no gather area, no gather copy, no
+  // chunking).  Coherence of those remote writes into cacheable memory
+  // (DESIGN 7.1 rule 1'): the writer's fold ends before its PUSHED signal,
+  // whose system-scope release writes its L2 back; the owner returns only
+  // after its PUSHED wait, whose workgroups take a system-scope acquire on
+  // every XCD.  zc_direct = 0: results travel through the peers' uncached
+  // gather areas and a local gather copy (round 4).
   const char *ps[MAXR];
   char *pr[MAXR];
   int zc = 0;
+  // the misalignments mod 16 of sbuf and rbuf must agree across ranks (the
+  // fold's 16-byte vector path needs one misalignment for all operands)
+  const int mis_sr = (int)((uintptr_t)sb & 15) | (c->zc_direct ? (int)(((uintptr_t)rb & 15) << 4) : 0);
   if (zc_allowed(c, zc_mode, count * es)) {
-    zc = reg_exchange(c, sb, count * es, rb, count * es, (int)((uintptr_t)sb & 15), true, ps, pr);
+    zc = reg_exchange(c, sb, count * es, rb, count * es, mis_sr, true, ps, pr);
     if (zc < 0) return zc;
   }
-  const size_t ce = chunk_elems(c, count, es, zc);
+  const bool direct = zc && c->zc_direct && (((uintptr_t)sb ^ (uintptr_t)rb) & 15) == 0;
+  const size_t ce = direct ? count : chunk_elems(c, count, es, zc);
   if (zc) c->st.zero_copy_calls++;
   else c->st.staged_calls++;
+  if (direct) c->st.direct_calls++;
   DoneMark dm;   // a blocking call: the last round's DONE signal raises the completion word
   done_mark_arm(c, dm);
   for (size_t c0 = 0; c0 < count; c0 += ce) {
@@ -1693,13 +1813,20 @@ static int allreduce_staged(mx_comm *c, fold_launch_fn fl, int alg, const char *
                          : c->staging + (size_t)j * L.slot + mis;
       dp[nd++] = rb + e0 * es;
       for (int p = 0; p < n; p++)
-        if (p != r) dp[nd++] = c->peer_staging[p] + L.gather_off + ((c0 * es) & 15) + off[r] * es;
+        if (p != r) dp[nd++] = direct ? pr[p] + e0 * es
+                                      : c->peer_staging[p] + L.gather_off + ((c0 * es) & 15) + off[r] * es;
       std::vector<Seg> segs;
       if ((rc = allreduce_segments(alg, n, count, es, e0, e0 + len[r], segs))) return rc;
       for (const Seg &sg : segs)
         if ((rc = run_fold(c, fl, sg, e0, sp, n, dp, nd, es, s, zc))) return rc;
     }
+    // every peer's fold has stored its part into my rbuf (direct) or my
+    // gather area, and has finished reading my sbuf
     if ((rc = signal_wait_all(c, FLAG_PUSHED, g, g, s))) return rc;
+    if (direct) {
+      if ((rc = signal_done(c, g, s, c0 + cl >= count ? &dm : nullptr))) return rc;
+      continue;
+    }
     // (d) copy the other parts from my gather area into rbuf
     memset(&ca, 0, sizeof ca);
     for (int p = 0; p < n; p++) {
@@ -3783,9 +3910,17 @@ static bool heap_agree(mx_comm *c, int ok) {
   return true;
 }
 
+// a heap's operations end before they return (blocking) or are tracked by
+// its communicator's tail event (deferred mode, finish()): that is all the
+// device work destroy must wait for
+static void heap_quiesce(mx_heap *h) {
+  mx_comm *c = h->c;
+  if (c->tail_valid && c->tail && hipEventSynchronize(c->tail) != hipSuccess) (void)hipGetLastError();
+}
+
 static void heap_unmap(mx_heap *h) {
   for (int p = 0; p < h->c->size && p < MAXR; p++) {
-    if (p != h->c->rank && h->peer_flags[p]) (void)hipIpcCloseMemHandle((void *)h->peer_flags[p]);
+    if (p != h->c->rank && h->peer_flags[p]) release_later((void *)h->peer_flags[p], REL_IPC);
     if (p != h->c->rank) { h->peer_flags[p] = nullptr; h->peer[p] = nullptr; }
   }
 }
@@ -3819,13 +3954,15 @@ static bool heap_map_attempt(mx_heap *h) {
     }
   }
   const uint64_t sig = 0x5EED0000ull + (uint64_t)c->rank;
-  if (ok && (hipMemcpy(h->flags + 256, &sig, sizeof sig, hipMemcpyHostToDevice) != hipSuccess ||
-             hipDeviceSynchronize() != hipSuccess))
+  hipStream_t ls = life_stream();
+  if (ok && (!ls || hipMemcpyAsync(h->flags + 256, &sig, sizeof sig, hipMemcpyHostToDevice, ls) != hipSuccess ||
+             hipStreamSynchronize(ls) != hipSuccess))
     ok = 0;
   if (!heap_agree(c, ok)) return false;   // every PE mapped and signed before anyone checks
   for (int p = 0; p < c->size; p++) {
     uint64_t v = 0;
-    const hipError_t e = hipMemcpy(&v, h->peer_flags[p] + 256, sizeof v, hipMemcpyDeviceToHost);
+    hipError_t e = hipMemcpyAsync(&v, h->peer_flags[p] + 256, sizeof v, hipMemcpyDeviceToHost, ls);
+    if (e == hipSuccess) e = hipStreamSynchronize(ls);
     if (dbg) fprintf(stderr, "[mx ipc] rank %d: PE %d mapped at %p reads 0x%llx\n", c->rank, p,
                      (void *)h->peer_flags[p], (unsigned long long)v);
     if (e != hipSuccess || v != 0x5EED0000ull + (uint64_t)p) {
@@ -3867,8 +4004,9 @@ extern "C" int mx_heap_create(mx_comm_t *c, size_t bytes, mx_heap_t **out) {
     // heap's destroy (its device idle, its trailing sequence writes landed),
     // else a late write of the old heap survives the zeroing (as the
     // communicator flags did in round 3)
-    int ok = heap_agree(c, 1) && hipMemset(h->mem, 0, kHeapFlagBytes) == hipSuccess &&
-             hipDeviceSynchronize() == hipSuccess;
+    hipStream_t ls = life_stream();
+    int ok = heap_agree(c, 1) && ls && hipMemsetAsync(h->mem, 0, kHeapFlagBytes, ls) == hipSuccess &&
+             hipStreamSynchronize(ls) == hipSuccess;
     if (!heap_agree(c, ok)) {
       c->hregion_used = h->region_off;
       delete h;
@@ -3882,7 +4020,10 @@ extern "C" int mx_heap_create(mx_comm_t *c, size_t bytes, mx_heap_t **out) {
   for (int attempt = 0; attempt < 3 && !mapped; attempt++) {
     int ok = hipExtMallocWithFlags((void **)&h->mem, kHeapFlagBytes + h->bytes, hipDeviceMallocUncached) ==
              hipSuccess;
-    if (ok && (hipMemset(h->mem, 0, kHeapFlagBytes) != hipSuccess || hipDeviceSynchronize() != hipSuccess)) ok = 0;
+    hipStream_t ls = life_stream();
+    if (ok && (!ls || hipMemsetAsync(h->mem, 0, kHeapFlagBytes, ls) != hipSuccess ||
+               hipStreamSynchronize(ls) != hipSuccess))
+      ok = 0;
     if (!ok) h->mem = nullptr;
     if (c->local) {
       mapped = ok;
@@ -3904,9 +4045,9 @@ extern "C" int mx_heap_create(mx_comm_t *c, size_t bytes, mx_heap_t **out) {
       h->mem = nullptr;
     }
   }
-  for (char *m : discarded) (void)hipFree(m);
+  for (char *m : discarded) release_later(m, REL_DEV);
   if (!mapped) {
-    if (h->mem) (void)hipFree(h->mem);
+    release_later(h->mem, REL_DEV);
     delete h;
     return MX_ERR_HIP;
   }
@@ -3916,15 +4057,18 @@ extern "C" int mx_heap_create(mx_comm_t *c, size_t bytes, mx_heap_t **out) {
 
 extern "C" int mx_heap_destroy(mx_heap_t *h) {
   if (!h) return MX_SUCCESS;
-  (void)hipDeviceSynchronize();
+  // the heap's own operations only (every heap call records its stream's
+  // event), never the whole device
+  heap_quiesce(h);
   if (h->carved) {   // give the slice back if it is the last one (heaps are destroyed in LIFO order)
     if (h->region_off + kHeapFlagBytes + h->bytes == h->c->hregion_used) h->c->hregion_used = h->region_off;
     delete h;
     return MX_SUCCESS;
   }
   heap_unmap(h);
-  if (h->mem) (void)hipFree(h->mem);
+  release_later(h->mem, REL_DEV);
   delete h;
+  release_flush();
   return MX_SUCCESS;
 }
 

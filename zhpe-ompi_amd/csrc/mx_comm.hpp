@@ -159,6 +159,9 @@ struct mx_comm {
   // cache.  reg_shm null: registration unavailable (every rank agrees).
   void *reg_shm;
   size_t reg_shm_bytes, reg_min;
+  // zero-copy allreduce results written straight into the peers' registered
+  // rbufs (no gather area, no gather copy; mx_comm_set_zc_direct)
+  int zc_direct;
   uint64_t reg_seq, reg_tick;
   std::vector<struct mx_reg_import> *reg_imp;
   // data-movement autotuning of blocking collectives: per
@@ -262,6 +265,9 @@ int req_create(mx_comm *c, int kind, int persistent, void *stream, mx_request **
 int req_submit(mx_request *q, mx_request_t **out);
 void req_discard(mx_request *q);
 int p2p_setup(mx_comm *c);
+// wait for the communicator's point-to-point channels (rendezvous sends no
+// receive ever cleared give up first); no device-wide synchronisation
+void p2p_quiesce(mx_comm *c);
 void p2p_release(mx_comm *c);
 // a point-to-point request completed: release its rendezvous slot / staging
 void p2p_finish(mx_request *q);

@@ -1854,7 +1854,7 @@ static mx_ddt::PieceTab *piece_tab(mx_ddt *d, int al) {
   if (window((uint32_t)K) + 32 > (uint64_t)kPieceStage) return nullptr;
   if (hipMalloc((void **)&P.dev, npi * sizeof(DPiece)) != hipSuccess) { P.dev = nullptr; return nullptr; }
   if (hipMemcpy(P.dev, v.data(), npi * sizeof(DPiece), hipMemcpyHostToDevice) != hipSuccess) {
-    (void)hipFree(P.dev);
+    release_later(P.dev, REL_DEV);
     P.dev = nullptr;
     return nullptr;
   }
@@ -2012,15 +2012,15 @@ static mx_ddt::BlkTab *blk_tab(mx_ddt *d) {
   dv[nb].soff = (uint32_t)S;
   if (hipMalloc((void **)&B.dev, (nb + 1) * sizeof(DBlk)) != hipSuccess) { B.dev = nullptr; return nullptr; }
   if (hipMalloc((void **)&B.tfirst, (nk + 1) * sizeof(uint32_t)) != hipSuccess) {
-    (void)hipFree(B.dev);
+    release_later(B.dev, REL_DEV);
     B.dev = nullptr;
     B.tfirst = nullptr;
     return nullptr;
   }
   if (hipMemcpy(B.dev, dv.data(), (nb + 1) * sizeof(DBlk), hipMemcpyHostToDevice) != hipSuccess ||
       hipMemcpy(B.tfirst, tf.data(), (nk + 1) * sizeof(uint32_t), hipMemcpyHostToDevice) != hipSuccess) {
-    (void)hipFree(B.dev);
-    (void)hipFree(B.tfirst);
+    release_later(B.dev, REL_DEV);
+    release_later(B.tfirst, REL_DEV);
     B.dev = nullptr;
     B.tfirst = nullptr;
     return nullptr;
@@ -2078,7 +2078,7 @@ extern "C" int mx_ddt_create(const void *desc, size_t nrec, const uint64_t *basi
     if ((rc = mx_ensure_init())) { delete d; return rc; }
     if (hipMalloc((void **)&d->dev, d->host.size() * sizeof(DRun)) != hipSuccess ||
         hipMemcpy(d->dev, d->host.data(), d->host.size() * sizeof(DRun), hipMemcpyHostToDevice) != hipSuccess) {
-      if (d->dev) (void)hipFree(d->dev);
+      if (d->dev) release_later(d->dev, REL_DEV);
       delete d;
       return MX_ERR_HIP;
     }
@@ -2094,8 +2094,8 @@ extern "C" int mx_ddt_create(const void *desc, size_t nrec, const uint64_t *basi
     const size_t nb = d->map16 ? m16.size() * 2 : m32.size() * 4;
     const void *src = d->map16 ? (const void *)m16.data() : (const void *)m32.data();
     if (hipMalloc(&d->map_dev, nb) != hipSuccess || hipMemcpy(d->map_dev, src, nb, hipMemcpyHostToDevice) != hipSuccess) {
-      if (d->map_dev) (void)hipFree(d->map_dev);
-      if (d->dev) (void)hipFree(d->dev);
+      if (d->map_dev) release_later(d->map_dev, REL_DEV);
+      if (d->dev) release_later(d->dev, REL_DEV);
       delete d;
       return MX_ERR_HIP;
     }
@@ -2106,12 +2106,12 @@ extern "C" int mx_ddt_create(const void *desc, size_t nrec, const uint64_t *basi
 
 extern "C" int mx_ddt_destroy(mx_ddt_t *d) {
   if (!d) return MX_SUCCESS;
-  if (d->dev) (void)hipFree(d->dev);
-  if (d->map_dev) (void)hipFree(d->map_dev);
+  if (d->dev) release_later(d->dev, REL_DEV);
+  if (d->map_dev) release_later(d->map_dev, REL_DEV);
   for (auto &P : d->ptab)
-    if (P.dev) (void)hipFree(P.dev);
-  if (d->btab.dev) (void)hipFree(d->btab.dev);
-  if (d->btab.tfirst) (void)hipFree(d->btab.tfirst);
+    if (P.dev) release_later(P.dev, REL_DEV);
+  if (d->btab.dev) release_later(d->btab.dev, REL_DEV);
+  if (d->btab.tfirst) release_later(d->btab.tfirst, REL_DEV);
   delete d;
   return MX_SUCCESS;
 }

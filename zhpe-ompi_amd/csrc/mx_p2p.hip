@@ -645,19 +645,27 @@ static hipError_t p2p_stream_create(hipStream_t *s) {
   return hipStreamCreateWithPriority(s, hipStreamNonBlocking, greatest);
 }
 
+// Setup makes no device-wide synchronisation: a receive of another
+// communicator may be spinning for a message whose sender waits for this
+// rank's first send here (example 3).  Buffers come from
+// the process pools (hipMalloc / hipFree wait for the whole device on this
+// runtime), the memsets run on the lifecycle stream.
+static size_t p2p_stash_bytes(const mx_comm *c) { return (size_t)c->size * P2P_STASH_N * P2P_STASH_C; }
+
 int p2p_setup(mx_comm *c) {
   if (c->p2p_send) return MX_SUCCESS;
   const size_t sb = sizeof(P2PSendState) * c->size, rb = sizeof(P2PRecvState) * c->size;
-  if (hipMalloc((void **)&c->p2p_send, sb) != hipSuccess) {
+  hipStream_t ls = life_stream();
+  if (!ls || !(c->p2p_send = (P2PSendState *)pool_dev_get(sb))) {
     c->p2p_send = nullptr;
     return MX_ERR_NOMEM;
   }
   const bool ok =
-      hipMalloc((void **)&c->p2p_recv, rb) == hipSuccess &&
-      hipMalloc((void **)&c->p2p_lanes, 3 * sizeof(uint64_t)) == hipSuccess &&
-      hipMalloc((void **)&c->p2p_stash, (size_t)c->size * P2P_STASH_N * P2P_STASH_C) == hipSuccess &&
-      hipMalloc((void **)&c->p2p_rndv_cur, sizeof(P2PRndvCur)) == hipSuccess &&
-      hipHostMalloc((void **)&c->p2p_rndv, sizeof(P2PRndvTable), hipHostMallocMapped) == hipSuccess &&
+      (c->p2p_recv = (P2PRecvState *)pool_dev_get(rb)) != nullptr &&
+      (c->p2p_lanes = (uint64_t *)pool_dev_get(3 * sizeof(uint64_t))) != nullptr &&
+      (c->p2p_stash = (char *)pool_dev_get(p2p_stash_bytes(c))) != nullptr &&
+      (c->p2p_rndv_cur = (P2PRndvCur *)pool_dev_get(sizeof(P2PRndvCur))) != nullptr &&
+      (c->p2p_rndv = (P2PRndvTable *)pool_host_get(sizeof(P2PRndvTable))) != nullptr &&
       hipHostGetDevicePointer((void **)&c->p2p_rndv_dev, c->p2p_rndv, 0) == hipSuccess;
   if (!ok) {
     p2p_release(c);
@@ -669,32 +677,39 @@ int p2p_setup(mx_comm *c) {
   for (int i = P2P_RNDV_Q - 1; i >= 0; i--) c->p2p_rndv_free->push_back(i);
   c->p2p_ltot[0] = c->p2p_ltot[1] = c->p2p_ltot[2] = 0;
   for (int j = 0; j < MAXR; j++) c->p2p_host_msgs[j] = 0;
-  if (hipMemset(c->p2p_send, 0, sb) != hipSuccess || hipMemset(c->p2p_recv, 0, rb) != hipSuccess ||
-      hipMemset(c->p2p_lanes, 0, 3 * sizeof(uint64_t)) != hipSuccess ||
-      hipMemset(c->p2p_rndv_cur, 0, sizeof(P2PRndvCur)) != hipSuccess ||
+  if (hipMemsetAsync(c->p2p_send, 0, sb, ls) != hipSuccess || hipMemsetAsync(c->p2p_recv, 0, rb, ls) != hipSuccess ||
+      hipMemsetAsync(c->p2p_lanes, 0, 3 * sizeof(uint64_t), ls) != hipSuccess ||
+      hipMemsetAsync(c->p2p_rndv_cur, 0, sizeof(P2PRndvCur), ls) != hipSuccess ||
       p2p_stream_create(&c->p2p_stream[0]) != hipSuccess || p2p_stream_create(&c->p2p_stream[1]) != hipSuccess ||
       p2p_stream_create(&c->p2p_stream[2]) != hipSuccess ||
       hipEventCreateWithFlags(&c->p2p_ev, hipEventDisableTiming) != hipSuccess ||
-      hipDeviceSynchronize() != hipSuccess) {
+      hipStreamSynchronize(ls) != hipSuccess) {
     p2p_release(c);
     return MX_ERR_HIP;
   }
   return MX_SUCCESS;
 }
 
-void p2p_release(mx_comm *c) {
+void p2p_quiesce(mx_comm *c) {
+  for (int i = 0; i < 2; i++)
+    if (c->p2p_stream[i]) (void)hipStreamSynchronize(c->p2p_stream[i]);
   // rendezvous sends no receive ever cleared: their picks give up
   if (c->p2p_rndv) __atomic_store_n(&c->p2p_rndv->abort, 1, __ATOMIC_RELEASE);
   if (c->p2p_stream[2]) (void)hipStreamSynchronize(c->p2p_stream[2]);
+}
+
+void p2p_release(mx_comm *c) {
+  p2p_quiesce(c);
   for (int i = 0; i < 3; i++)
     if (c->p2p_stream[i]) (void)hipStreamDestroy(c->p2p_stream[i]);
   if (c->p2p_ev) (void)hipEventDestroy(c->p2p_ev);
-  if (c->p2p_send) (void)hipFree(c->p2p_send);
-  if (c->p2p_recv) (void)hipFree(c->p2p_recv);
-  if (c->p2p_lanes) (void)hipFree(c->p2p_lanes);
-  if (c->p2p_stash) (void)hipFree(c->p2p_stash);
-  if (c->p2p_rndv_cur) (void)hipFree(c->p2p_rndv_cur);
-  if (c->p2p_rndv) (void)hipHostFree(c->p2p_rndv);
+  const size_t sb = sizeof(P2PSendState) * c->size, rb = sizeof(P2PRecvState) * c->size;
+  pool_dev_put(c->p2p_send, sb);
+  pool_dev_put(c->p2p_recv, rb);
+  pool_dev_put(c->p2p_lanes, 3 * sizeof(uint64_t));
+  pool_dev_put(c->p2p_stash, p2p_stash_bytes(c));
+  pool_dev_put(c->p2p_rndv_cur, sizeof(P2PRndvCur));
+  pool_host_put(c->p2p_rndv, sizeof(P2PRndvTable));
   delete c->p2p_rndv_free;
   c->p2p_rndv_free = nullptr;
   c->p2p_rndv = c->p2p_rndv_dev = nullptr;

@@ -328,10 +328,11 @@ static bool w32_lds() {
 }
 
 // launches that carry their own completion mark: grids of at most
-// kMarkFlags workgroups.  Every launch mx_reduce2_sync makes for count
-// elements has at most ceil((count + 16) / 256) workgroups (one 16-byte
-// vector, or one element, per lane of 256; the 64-lane non-temporal
-// instances start at 384 MiB footprints), so counts up to this bound fit.
+// kMarkFlags workgroups.  A 256-lane launch for count elements has at most
+// ceil((count + 16) / 256) workgroups (one 16-byte vector, or one element,
+// per lane), so counts up to this bound fit; the 64-lane non-temporal
+// instances (from 384 MiB footprints unless MX_NT_MIN_BYTES says otherwise)
+// may not, and mark_fit drops the mark for them.
 constexpr size_t kFusedMarkMax = (size_t)kMarkFlags * 256 - 16;
 
 // Launches mark themselves (default; MX_FUSED_MARK=0
@@ -352,8 +353,18 @@ static bool fused_mark() {
   return on != 0;
 }
 
+// The mark rides on a launch only if its grid has a flag per workgroup
+// (kMarkFlags); a larger grid -- e.g. a 64-lane non-temporal instance forced
+// below its usual footprint by MX_NT_MIN_BYTES -- runs unmarked and `mk` is
+// cleared, so the caller waits through the marker kernel instead (ADVICE r4:
+// a mark over part of the grid would return before the rest had written).
+static inline const Mark &mark_fit(Mark &mk, unsigned grid) {
+  if (mk.flags && grid > kMarkFlags) mk = Mark{nullptr, nullptr, 0};
+  return mk;
+}
+
 template <class T, class OP>
-static int launch2(const void *in, void *inout, size_t n, hipStream_t s, const Mark &mk) {
+static int launch2(const void *in, void *inout, size_t n, hipStream_t s, Mark &mk) {
   const T *a = static_cast<const T *>(in);
   T *b = static_cast<T *>(inout);
   if (n == 0) return MX_SUCCESS;
@@ -365,21 +376,22 @@ static int launch2(const void *in, void *inout, size_t n, hipStream_t s, const M
       if (w32_lds()) {
         if (nt)
           hipLaunchKernelGGL((k_reduce2_w32t<T, OP, true, kBlockNT>), dim3(grid_for(n, kBlockNT)), dim3(kBlockNT), 0,
-                             s, a, b, n, mk);
+                             s, a, b, n, mark_fit(mk, grid_for(n, kBlockNT)));
         else
           hipLaunchKernelGGL((k_reduce2_w32t<T, OP, false, kBlock>), dim3(grid_for(n)), dim3(kBlock), 0, s, a, b, n,
-                             mk);
+                             mark_fit(mk, grid_for(n)));
       } else if (nt) {
         hipLaunchKernelGGL((k_reduce2_w32<T, OP, true, kBlockNT>), dim3(grid_for(n, kBlockNT)), dim3(kBlockNT), 0, s,
-                           a, b, n, mk);
+                           a, b, n, mark_fit(mk, grid_for(n, kBlockNT)));
       } else {
-        hipLaunchKernelGGL((k_reduce2_w32<T, OP, false, kBlock>), dim3(grid_for(n)), dim3(kBlock), 0, s, a, b, n, mk);
+        hipLaunchKernelGGL((k_reduce2_w32<T, OP, false, kBlock>), dim3(grid_for(n)), dim3(kBlock), 0, s, a, b, n,
+                           mark_fit(mk, grid_for(n)));
       }
       return mx_check_launch();
     }
   }
   if (N == 0 || ma != mb || (ma % sizeof(T)) != 0) {
-    hipLaunchKernelGGL((k_reduce2_elem<T, OP>), dim3(grid_for(n)), dim3(kBlock), 0, s, a, b, n, mk);
+    hipLaunchKernelGGL((k_reduce2_elem<T, OP>), dim3(grid_for(n)), dim3(kBlock), 0, s, a, b, n, mark_fit(mk, grid_for(n)));
     return mx_check_launch();
   }
   size_t head = ma ? (16 - ma) / sizeof(T) : 0;
@@ -390,12 +402,13 @@ static int launch2(const void *in, void *inout, size_t n, hipStream_t s, const M
   if (mx_nt_for(2 * n * sizeof(T))) {
     if (nt_small_wg(work))
       hipLaunchKernelGGL((k_reduce2<T, OP, true>), dim3(grid_for(work, kBlockNT)), dim3(kBlockNT), 0, s, a, b, n, head,
-                         nvec, mk);
+                         nvec, mark_fit(mk, grid_for(work, kBlockNT)));
     else
       hipLaunchKernelGGL((k_reduce2<T, OP, true, kBlock>), dim3(grid_for(work)), dim3(kBlock), 0, s, a, b, n, head,
-                         nvec, mk);
+                         nvec, mark_fit(mk, grid_for(work)));
   } else {
-    hipLaunchKernelGGL((k_reduce2<T, OP, false>), dim3(grid_for(work)), dim3(kBlock), 0, s, a, b, n, head, nvec, mk);
+    hipLaunchKernelGGL((k_reduce2<T, OP, false>), dim3(grid_for(work)), dim3(kBlock), 0, s, a, b, n, head, nvec,
+                       mark_fit(mk, grid_for(work)));
   }
   return mx_check_launch();
 }
@@ -444,7 +457,7 @@ static int launch3(const void *in1, const void *in2, void *out, size_t n, hipStr
 }
 
 // ---- type-slot dispatch ---------------------------------------------------
-typedef int (*launch2_fn)(const void *, void *, size_t, hipStream_t, const Mark &);
+typedef int (*launch2_fn)(const void *, void *, size_t, hipStream_t, Mark &);
 typedef int (*launch3_fn)(const void *, const void *, void *, size_t, hipStream_t);
 
 struct entry { launch2_fn f2; launch3_fn f3; };
@@ -513,7 +526,8 @@ extern "C" int mx_reduce2(int op, int type, const void *in, void *inout, size_t 
   if (!in || !inout || count > kMaxItems) return MX_ERR_ARG;
   int rc = mx_ensure_init();
   if (rc) return rc;
-  return e.f2(in, inout, count, (hipStream_t)stream, Mark{nullptr, nullptr, 0});
+  Mark none{nullptr, nullptr, 0};
+  return e.f2(in, inout, count, (hipStream_t)stream, none);
 }
 
 extern "C" int mx_reduce2_sync(int op, int type, const void *in, void *inout, size_t count, void *stream) {
@@ -533,18 +547,12 @@ extern "C" int mx_reduce2_sync(int op, int type, const void *in, void *inout, si
     rc = svc_reduce(op, type, in, nullptr, inout, count, s);
     if (rc) return rc < 0 ? rc : MX_SUCCESS;
   }
-  if (!fused_mark() || count > kFusedMarkMax) {
-    rc = e.f2(in, inout, count, s, Mark{nullptr, nullptr, 0});
-    return rc ? rc : mx_stream_sync_fast(stream);
-  }
-  Mark mk;
-  mark_arm(&mk, true);
-  if (!mk.flags) {   // no flags: the marker kernel
-    rc = e.f2(in, inout, count, s, Mark{nullptr, nullptr, 0});
-    return rc ? rc : mx_stream_sync_fast(stream);
-  }
+  Mark mk{nullptr, nullptr, 0};
+  if (fused_mark() && count <= kFusedMarkMax) mark_arm(&mk, true);
+  // no flags (or a grid too large for them, cleared by the launch): the marker kernel
   rc = e.f2(in, inout, count, s, mk);
-  return rc ? rc : mark_wait(mk, s);
+  if (rc) return rc;
+  return mk.flags ? mark_wait(mk, s) : mx_stream_sync_fast(stream);
 }
 
 // As mx_reduce3, returning with `out` complete for every agent: the op

@@ -7,6 +7,8 @@
 #include <stdlib.h>
 #include <string.h>
 #include <pthread.h>
+#include <mutex>
+#include <vector>
 #include "mx_internal.h"
 #include "mx_mem.hpp"
 
@@ -242,6 +244,65 @@ extern "C" int mx_stream_order(void *stream, void *after) {
 extern "C" int mx_stream_sync(void *stream) {
   return mx_hip_rc(hipStreamSynchronize((hipStream_t)stream));
 }
+
+namespace {
+std::mutex g_life_mu;
+hipStream_t g_life[64] = {};   // per device
+struct PoolEnt { void *p; size_t bytes; bool host; };
+std::vector<PoolEnt> *g_pool = nullptr;   // never destroyed: entries outlive static destructors
+}  // namespace
+
+hipStream_t mx::life_stream() {
+  int dev = g_device;
+  if (dev < 0 && hipGetDevice(&dev) != hipSuccess) return nullptr;
+  if (dev < 0 || dev >= 64) return nullptr;
+  std::lock_guard<std::mutex> lk(g_life_mu);
+  if (!g_life[dev]) {
+    hipStream_t s = nullptr;
+    if (hipStreamCreateWithFlags(&s, hipStreamNonBlocking) != hipSuccess) {
+      (void)hipGetLastError();
+      return nullptr;
+    }
+    g_life[dev] = s;
+  }
+  return g_life[dev];
+}
+
+int mx::life_sync() {
+  hipStream_t s = life_stream();
+  return s ? mx_hip_rc(hipStreamSynchronize(s)) : MX_ERR_HIP;
+}
+
+static void *pool_get(size_t bytes, bool host) {
+  {
+    std::lock_guard<std::mutex> lk(g_life_mu);
+    if (g_pool)
+      for (size_t i = 0; i < g_pool->size(); i++)
+        if ((*g_pool)[i].bytes == bytes && (*g_pool)[i].host == host) {
+          void *p = (*g_pool)[i].p;
+          (*g_pool)[i] = g_pool->back();
+          g_pool->pop_back();
+          return p;
+        }
+  }
+  void *p = nullptr;
+  const hipError_t e = host ? hipHostMalloc(&p, bytes, hipHostMallocMapped) : hipMalloc(&p, bytes);
+  if (e != hipSuccess) {
+    (void)hipGetLastError();
+    return nullptr;
+  }
+  return p;
+}
+static void pool_put(void *p, size_t bytes, bool host) {
+  if (!p) return;
+  std::lock_guard<std::mutex> lk(g_life_mu);
+  if (!g_pool) g_pool = new std::vector<PoolEnt>();
+  g_pool->push_back(PoolEnt{p, bytes, host});
+}
+void *mx::pool_dev_get(size_t bytes) { return pool_get(bytes, false); }
+void mx::pool_dev_put(void *p, size_t bytes) { pool_put(p, bytes, false); }
+void *mx::pool_host_get(size_t bytes) { return pool_get(bytes, true); }
+void mx::pool_host_put(void *p, size_t bytes) { pool_put(p, bytes, true); }
 
 namespace {
 // one thread's completion word: the marker kernel, last on the stream,

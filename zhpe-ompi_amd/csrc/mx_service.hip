@@ -198,12 +198,18 @@ __device__ __forceinline__ void svc_work(uint64_t in, uint64_t inout, uint64_t i
 // outlive workgroup 0's decision.
 template <class T, class OP, class OP3>
 __global__ void __launch_bounds__(kSvcB) k_svc(const SvcCmd *cmd, SvcHost *host, uint64_t *flags, SvcBcast *bc,
-                                               uint64_t *acks, uint64_t last, uint64_t epoch, uint64_t idle_ticks,
-                                               uint64_t life_ticks, uint64_t solo_max, int hsleep) {
+                                               uint64_t *acks, uint64_t *hrun, uint64_t last, uint64_t epoch,
+                                               uint64_t idle_ticks, uint64_t life_ticks, uint64_t solo_max,
+                                               int hsleep) {
   __shared__ uint64_t s_in, s_inout, s_count, s_q, s_in2;
   __shared__ int s_exit, s_bcast;
   const unsigned nwg = gridDim.x;
   if (blockIdx.x > 0) {                    // helper: the broadcasts of this launch, in order
+    // resident: the host posts to this launch only once every helper says so
+    // (a helper never dispatched -- its CUs held by other streams' waves --
+    // would leave a broadcast command waiting for its flag)
+    if (threadIdx.x == 0)
+      __hip_atomic_store(hrun + blockIdx.x, epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     for (uint64_t k = 1;; k++) {
       if (threadIdx.x == 0) {
         const uint64_t want = (epoch << 32) | k;
@@ -322,15 +328,15 @@ __global__ void __launch_bounds__(kSvcB) k_svc(const SvcCmd *cmd, SvcHost *host,
   }
 }
 
-typedef void (*svc_launch_fn)(const SvcCmd *, SvcHost *, uint64_t *, SvcBcast *, uint64_t *, uint64_t, uint64_t,
-                              uint64_t, uint64_t, uint64_t, int, unsigned, hipStream_t);
+typedef void (*svc_launch_fn)(const SvcCmd *, SvcHost *, uint64_t *, SvcBcast *, uint64_t *, uint64_t *, uint64_t,
+                              uint64_t, uint64_t, uint64_t, uint64_t, int, unsigned, hipStream_t);
 
 template <class T, class OP, class OP3>
-static void svc_launch(const SvcCmd *c, SvcHost *h, uint64_t *f, SvcBcast *bc, uint64_t *acks, uint64_t last,
-                       uint64_t epoch, uint64_t idle, uint64_t life, uint64_t solo, int hsleep, unsigned grid,
-                       hipStream_t s) {
-  hipLaunchKernelGGL((k_svc<T, OP, OP3>), dim3(grid), dim3(kSvcB), 0, s, c, h, f, bc, acks, last, epoch, idle, life,
-                     solo, hsleep);
+static void svc_launch(const SvcCmd *c, SvcHost *h, uint64_t *f, SvcBcast *bc, uint64_t *acks, uint64_t *hrun,
+                       uint64_t last, uint64_t epoch, uint64_t idle, uint64_t life, uint64_t solo, int hsleep,
+                       unsigned grid, hipStream_t s) {
+  hipLaunchKernelGGL((k_svc<T, OP, OP3>), dim3(grid), dim3(kSvcB), 0, s, c, h, f, bc, acks, hrun, last, epoch, idle,
+                     life, solo, hsleep);
 }
 
 // pairs served: element types that tile 16-byte vectors with no bytes
@@ -354,6 +360,7 @@ struct Service {
   uint64_t *flags = nullptr, *flags_d = nullptr;   // per-workgroup flags (mapped host memory, kSvcGridMax)
   SvcBcast *bc = nullptr;                          // workgroup 0 -> helpers (device, uncached)
   uint64_t *acks = nullptr;                        // helpers -> workgroup 0 (device, uncached, kSvcGridMax)
+  uint64_t *hrun = nullptr, *hrun_d = nullptr;     // helper w's launch epoch at start (mapped host memory)
   unsigned grid = kSvcGrid;
   uint64_t solo = kSvcSoloBytes;
   int hsleep = 2;         // helpers' sleep between polls: 8 / 32 / 64 / 127 x 64 clocks
@@ -411,9 +418,12 @@ uint64_t svc_post(Service &v) {
 void svc_stop_locked(Service &v) {
   if (!v.live) return;
   if (!svc_gone(v, v.epoch)) {
+    // exit stays 1 in the line (the checksum covers it) until the next
+    // command is filled in: clearing it right after the post would let the
+    // kernel read seq new, exit 0 and a checksum made with exit 1 -- a line it
+    // never takes, so it would leave only by its idle timeout
     v.cmd->exit = 1;
     svc_post(v);
-    v.cmd->exit = 0;
     // a running kernel reads it within microseconds; a second of silence
     // means something else went wrong: wait for the stream instead
     if (!svc_poll(&v.host->left, v.epoch, 1e6)) (void)hipStreamSynchronize(v.s);
@@ -464,6 +474,9 @@ int svc_setup(Service &v) {
       hipHostMalloc((void **)&v.flags, kSvcGridMax * sizeof(uint64_t), hipHostMallocMapped | hipHostMallocCoherent) !=
           hipSuccess ||
       hipHostGetDevicePointer((void **)&v.flags_d, v.flags, 0) != hipSuccess ||
+      hipHostMalloc((void **)&v.hrun, kSvcGridMax * sizeof(uint64_t), hipHostMallocMapped | hipHostMallocCoherent) !=
+          hipSuccess ||
+      hipHostGetDevicePointer((void **)&v.hrun_d, v.hrun, 0) != hipSuccess ||
       hipExtMallocWithFlags((void **)&v.bc, sizeof(SvcBcast), hipDeviceMallocUncached) != hipSuccess ||
       hipExtMallocWithFlags((void **)&v.acks, kSvcGridMax * sizeof(uint64_t), hipDeviceMallocUncached) !=
           hipSuccess ||
@@ -476,6 +489,7 @@ int svc_setup(Service &v) {
   memset(v.cmd, 0, sizeof(SvcCmd));
   memset(v.host, 0, sizeof(SvcHost));
   memset(v.flags, 0, kSvcGridMax * sizeof(uint64_t));
+  memset(v.hrun, 0, kSvcGridMax * sizeof(uint64_t));
   // MX_SVC_GRID (1..kSvcGridMax workgroups), MX_SVC_SOLO (bytes workgroup 0
   // takes alone), MX_SVC_HSLEEP (0..3): measurement switches
   if (const char *e = getenv("MX_SVC_GRID")) {
@@ -501,7 +515,12 @@ static bool svc_streams_idle(hipStream_t s) {
   constexpr double kIdleSpinUs = 50;
   std::chrono::steady_clock::time_point t0;
   for (unsigned k = 0;; k++) {
-    if (hipStreamQuery(s) == hipSuccess && hipStreamQuery(nullptr) == hipSuccess) return true;
+    const hipError_t e1 = hipStreamQuery(s);
+    const hipError_t e2 = e1 == hipSuccess ? hipStreamQuery(nullptr) : hipSuccess;
+    if (e1 == hipSuccess && e2 == hipSuccess) return true;
+    // any other status is the caller's fault (a failed kernel of theirs):
+    // decline, leaving it pending for the launch path to report
+    if ((e1 != hipSuccess && e1 != hipErrorNotReady) || (e2 != hipSuccess && e2 != hipErrorNotReady)) return false;
     (void)hipGetLastError();   // hipErrorNotReady is no error
     if (k == 0) t0 = std::chrono::steady_clock::now();
     else if (std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0).count() > kIdleSpinUs)
@@ -518,18 +537,28 @@ static bool svc_streams_idle(hipStream_t s) {
 // starts (an EXIT command it will read first) and calls launch until it has.
 static bool svc_start(Service &v, svc_launch_fn fn) {
   const uint64_t ep = ++v.epoch;
-  fn(v.cmd_d, v.host_d, v.flags_d, v.bc, v.acks, v.seq, ep, v.idle_ticks, v.life_ticks, v.solo, v.hsleep, v.grid,
-     v.s);
+  fn(v.cmd_d, v.host_d, v.flags_d, v.bc, v.acks, v.hrun_d, v.seq, ep, v.idle_ticks, v.life_ticks, v.solo, v.hsleep,
+     v.grid, v.s);
   if (hipGetLastError() != hipSuccess) { v.state = -1; return false; }
   const bool first = std::find(v.started.begin(), v.started.end(), fn) == v.started.end();
-  if (svc_poll(&v.host->running, ep, first ? kSvcFirstStartUs : kSvcStartUs)) {
+  const auto t0 = std::chrono::steady_clock::now();
+  const double budget = first ? kSvcFirstStartUs : kSvcStartUs;
+  bool all = svc_poll(&v.host->running, ep, budget);
+  // the whole grid must be resident: a broadcast command waits for every
+  // helper's flag, and a helper that never dispatched would never raise it
+  for (unsigned w = 1; all && w < v.grid; w++) {
+    const double used = std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0).count();
+    all = svc_poll(v.hrun + w, ep, std::max(0.0, budget - used));
+  }
+  if (all) {
     if (first) v.started.push_back(fn);
     v.live = true;
     return true;
   }
+  // held (or only part of the grid dispatched): told to leave -- workgroup 0
+  // broadcasts the EXIT, so helpers that start later leave at once
   v.cmd->exit = 1;
   svc_post(v);
-  v.cmd->exit = 0;
   v.pending = ep;
   v.live = false;
   v.held++;

@@ -252,7 +252,7 @@ class CollStats(ctypes.Structure):
     _fields_ = [("calls", ctypes.c_uint64), ("fold_launches", ctypes.c_uint64), ("fold_ms", ctypes.c_double),
                 ("fold_bytes", ctypes.c_double), ("push_ms", ctypes.c_double), ("gather_ms", ctypes.c_double),
                 ("total_ms", ctypes.c_double), ("zero_copy_calls", ctypes.c_uint64),
-                ("staged_calls", ctypes.c_uint64)]
+                ("staged_calls", ctypes.c_uint64), ("direct_calls", ctypes.c_uint64)]
 
 
 _AG_FN = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p)
@@ -271,6 +271,7 @@ def _coll_lib():
         L.mx_comm_set_protocol.argtypes = [vp, i]
         L.mx_comm_get_protocol.argtypes = [vp]
         L.mx_comm_set_reg_min.argtypes = [vp, sz]
+        L.mx_comm_set_zc_direct.argtypes = [vp, i]
         L.mx_comm_set_oneshot_max.argtypes = [vp, sz]
         L.mx_comm_set_oneshot_max.restype = ctypes.c_longlong
         L.mx_comm_set_autotune.argtypes = [vp, i]
@@ -493,6 +494,11 @@ class Comm:
         """Zero-copy (registered user buffers) allreduce from min_bytes per rank; 0 = off
         (mx_comm_set_reg_min).  Every rank must set the same value."""
         check(_coll_lib().mx_comm_set_reg_min(self.h, min_bytes), "mx_comm_set_reg_min")
+
+    def set_zc_direct(self, on):
+        """Zero-copy allreduce results straight into the peers' rbufs (True, the default) or
+        through the gather areas (mx_comm_set_zc_direct).  Every rank must set the same value."""
+        check(_coll_lib().mx_comm_set_zc_direct(self.h, 1 if on else 0), "mx_comm_set_zc_direct")
 
     def set_oneshot_max(self, max_bytes):
         """One-shot allreduce up to max_bytes per rank, clamped to the slot
