@@ -222,3 +222,109 @@ def test_real_host_table_uses_only_internals_the_reference_declares():
                 f"{hdr} has no member {m}"
         for m in mems:
             assert re.search(r"(->|\.)" + m + r"\b", body), f"{m} listed but unused"
+
+
+# ---------------------------------------------------------------------------
+# round 5: the convertor hook and the BTL GPU RDMA slots (VERDICT r4 missing 3, 4)
+# ---------------------------------------------------------------------------
+CONV_H = os.path.join(REF, "opal", "datatype", "opal_convertor.h")
+DT_H = os.path.join(REF, "opal", "datatype", "opal_datatype.h")
+BTL_H = os.path.join(REF, "opal", "mca", "btl", "btl.h")
+
+
+def test_convertor_and_datatype_layouts_match_reference(tmp_path):
+    """opal_convertor_t / opal_datatype_t / dt_type_desc_t / dt_stack_t of
+    the mirror (mca/mx_opal_convertor_abi.h) vs the reference's own headers,
+    which compile here (an x86-64 gcc build without CUDA)."""
+    items = []
+    for typ, hdr in (("opal_convertor_t", CONV_H), ("dt_stack_t", CONV_H), ("opal_datatype_t", DT_H),
+                     ("dt_type_desc_t", DT_H)):
+        mems = struct_members(hdr, typ)
+        if typ == "opal_convertor_t":        # OPAL_CUDA_SUPPORT = 0: cbmemcpy / stream are not there
+            mems = [m for m in mems if m not in ("cbmemcpy", "stream")]
+        for mem in mems:
+            items.append((f"{typ}.{mem}", typ, mem))
+        items.append((f"sizeof {typ}", typ, None))
+    real = compile_run(tmp_path, "real_conv", probe_src(["opal/datatype/opal_convertor.h"], items), REAL_INCS)
+    mirror = compile_run(tmp_path, "mirror_conv", probe_src(["mx_opal_convertor_abi.h"], items),
+                         [ABI, os.path.join(ROOT, "include")])
+    diff = {k: (real[k], mirror[k]) for k in real if real[k] != mirror[k]}
+    assert not diff, f"mirror differs from the reference headers (reference, mirror): {diff}"
+
+
+def test_convertor_hook_compiles_against_reference_convertor_h(tmp_path):
+    """-DMX_OMPI_REAL: mca/convertor_mi355x.c against the real
+    opal/datatype/opal_convertor.h; fAdvance has the reference's
+    convertor_advance_fct_t type (a mismatch is an error under -Werror)."""
+    src = tmp_path / "conv_real_check.c"
+    src.write_text('#include "mx_opal_convertor_abi.h"\n'
+                   "int32_t mca_convertor_mi355x_pack(opal_convertor_t *, struct iovec *, uint32_t *, size_t *);\n"
+                   "int32_t mca_convertor_mi355x_unpack(opal_convertor_t *, struct iovec *, uint32_t *, size_t *);\n"
+                   "convertor_advance_fct_t mx_check_pack = mca_convertor_mi355x_pack;\n"
+                   "convertor_advance_fct_t mx_check_unpack = mca_convertor_mi355x_unpack;\n")
+    for c in (os.path.join(ABI, "convertor_mi355x.c"), str(src)):
+        obj = tmp_path / (os.path.basename(c) + ".o")
+        cmd = ["gcc", "-std=gnu11", "-Wall", "-Werror", "-c", "-DMX_OMPI_REAL", *[f"-I{i}" for i in REAL_INCS],
+               f"-I{os.path.join(ROOT, 'include')}", f"-I{ABI}", c, "-o", str(obj)]
+        r = subprocess.run(cmd, capture_output=True, text=True)
+        assert r.returncode == 0, r.stderr[-4000:]
+    syms = subprocess.run(["nm", str(tmp_path / "convertor_mi355x.c.o")], capture_output=True, text=True,
+                          check=True).stdout
+    for s in ("mca_convertor_mi355x_pack", "mca_convertor_mi355x_unpack", "mca_convertor_mi355x_prepare"):
+        assert re.search(rf" T {s}$", syms, re.M), s
+
+
+def _btl_reference_offsets():
+    """mca_btl_base_module_t offsets from btl.h's text (the header needs
+    configure-generated threads headers): every member is a size_t, a
+    uint32_t, a pointer (function or object) or the 256-byte padding; the
+    CUDA members (#if OPAL_CUDA_GDR_SUPPORT / OPAL_CUDA_SUPPORT) are left out,
+    as an MI355X build has neither."""
+    text = open(BTL_H).read()
+    m = re.search(r"struct\s+mca_btl_base_module_t\s*\{", text)
+    depth, i = 1, m.end()
+    while depth:
+        depth += {"{": 1, "}": -1}.get(text[i], 0)
+        i += 1
+    body = re.sub(r"/\*.*?\*/", "", text[m.end():i - 1], flags=re.S)
+    # drop the conditional CUDA blocks
+    body = re.sub(r"#if OPAL_CUDA[^\n]*\n.*?#endif[^\n]*\n", "", body, flags=re.S)
+    off, out = 0, {}
+    for decl in body.split(";"):
+        decl = decl.strip()
+        if not decl:
+            continue
+        name = re.findall(r"[A-Za-z_]\w*", re.sub(r"\[[^\]]*\]", "", decl))[-1]
+        if "[" in decl:                                  # unsigned char padding[256]
+            size, align = int(re.search(r"\[(\d+)\]", decl).group(1)), 1
+        elif decl.startswith("uint32_t"):
+            size = align = 4
+        else:                                            # size_t, pointers, *_fn_t
+            size = align = 8
+        off = (off + align - 1) // align * align
+        out[name] = off
+        off += size
+    out["sizeof"] = (off + 7) // 8 * 8
+    return out
+
+
+def test_btl_module_layout_matches_reference(tmp_path):
+    ref = _btl_reference_offsets()
+    assert "btl_get" in ref and "btl_flush" in ref and "padding" in ref
+    assert "btl_cuda_eager_limit" not in ref
+    items = [(k, "mca_btl_base_module_t", k) for k in ref if k != "sizeof"] + \
+            [("sizeof", "mca_btl_base_module_t", None)]
+    mirror = compile_run(tmp_path, "mirror_btl", probe_src(["mx_btl_abi.h"], items),
+                         [ABI, os.path.join(ROOT, "include")])
+    diff = {k: (ref[k], mirror[k]) for k in ref if ref[k] != mirror[k]}
+    assert not diff, f"BTL module mirror differs from btl.h (reference, mirror): {diff}"
+    # the slot signatures: the get / put / register typedefs restated from the header text
+    text = open(BTL_H).read()
+    for typedef in ("mca_btl_base_module_get_fn_t", "mca_btl_base_module_put_fn_t",
+                    "mca_btl_base_module_register_mem_fn_t", "mca_btl_base_module_deregister_mem_fn_t",
+                    "mca_btl_base_module_flush_fn_t", "mca_btl_base_rdma_completion_fn_t"):
+        assert typedef in text
+    g = re.search(r"typedef int \(\*mca_btl_base_module_get_fn_t\)\s*\((.*?)\);", text, re.S).group(1)
+    assert [p.strip().split()[-1].lstrip("*") for p in g.replace("\n", " ").split(",")] == [
+        "btl", "endpoint", "local_address", "remote_address", "local_handle", "remote_handle", "size", "flags",
+        "order", "cbfunc", "cbcontext", "cbdata"]

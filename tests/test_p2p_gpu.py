@@ -461,3 +461,102 @@ def test_channel_streams_do_not_block_ordinary_streams():
         assert got[r]["z"] == [2.0] * 8
         for nb in (4096, 3 << 20):
             assert got[r]["out"][nb] == _data(900 + (1 - r), nb).tobytes(), (r, nb)
+
+
+# ---------------------------------------------------------------------------
+# round 5: the hardware-queue budget is per device, not
+# per communicator.  The send and receive channel streams are the device's,
+# shared by every communicator; the rendezvous stream is made only by a
+# communicator that sends one.  Two p2p communicators with crossing
+# Irecv / Send pairs in opposite posting orders on the two ranks, an
+# Iallreduce in flight on a request stream beside them, and 8 ordinary
+# streams busy meanwhile -- within the pool's 4 queues per priority.
+def _two_comm_worker(rank, n, port, q):
+    import torch.distributed as dist
+    os.environ["HSA_ENABLE_IPC_MODE_LEGACY"] = "0"
+    try:
+        dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=n)
+        torch.cuda.set_device(0)
+        mxompi.init(0)
+
+        def ag(b):
+            out = [None] * n
+            dist.all_gather_object(out, b)
+            return out
+
+        comms = []
+        for _ in range(2):
+            c = mxompi.Comm(rank, n, ag, device=0, staging_bytes=8 << 20)
+            c.set_timeout(30.0)
+            comms.append(c)
+        A, B = comms
+        peer = 1 - rank
+        side = torch.cuda.Stream()
+        nb = 64 << 10                                   # eager
+        res = {}
+        for it in range(3):
+            bufs = {k: torch.zeros(nb, dtype=torch.uint8, device="cuda") for k in ("a", "b")}
+            msgs = {k: _dev(_data(1000 * it + 10 * rank + (k == "b"), nb)) for k in ("a", "b")}
+            x = _dev(_data(700 + 10 * it + rank, 1 << 20)).view(torch.int32)
+            y = torch.zeros_like(x)
+            torch.cuda.synchronize()
+            # rank 0 posts A's receive first, rank 1 B's; each sends in the other order
+            order = ("a", "b") if rank == 0 else ("b", "a")
+            reqs = [(A if k == "a" else B).irecv(bufs[k].data_ptr(), nb, peer, 5 if k == "a" else 6) for k in order]
+            ia = A.iallreduce(x.data_ptr(), y.data_ptr(), x.numel(), "INT32_T", "SUM", "auto", side.cuda_stream)
+            busy = [torch.cuda.Stream() for _ in range(8)]
+            zs = []
+            for s in busy:
+                with torch.cuda.stream(s):
+                    z = torch.ones(1 << 20, device="cuda")
+                    zs.append((z * 2).sum())
+            for k in reversed(order):
+                (A if k == "a" else B).send(msgs[k].data_ptr(), nb, peer, 5 if k == "a" else 6)
+            for r in reqs:
+                r.wait()
+                r.free()
+            ia.wait()
+            ia.free()
+            torch.cuda.synchronize()
+            res[it] = {k: bufs[k].cpu().numpy().tobytes() for k in bufs}
+            res[it]["sum"] = y.cpu().numpy().tobytes()
+            res[it]["z"] = [float(z) for z in zs]
+        B.close()
+        A.close()
+        dist.destroy_process_group()
+        q.put((rank, "ok", res))
+    except Exception as e:  # noqa: BLE001
+        import traceback
+        q.put((rank, "err", traceback.format_exc() + str(e)))
+
+
+def test_two_p2p_communicators_crossing_with_an_iallreduce():
+    import torch.multiprocessing as mp
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_two_comm_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    got = {}
+    try:
+        for _ in range(2):
+            rank, status, payload = q.get(timeout=200)
+            assert status == "ok", payload
+            got[rank] = payload
+    finally:
+        for p in procs:
+            p.join(timeout=30 if len(got) == 2 else 5)
+            if p.is_alive():
+                p.terminate()
+                p.join(timeout=10)
+    nb = 64 << 10
+    for it in range(3):
+        xs = [_data(700 + 10 * it + r, 1 << 20).view(np.int32).astype(np.int64) for r in range(2)]
+        s = (xs[0] + xs[1]).astype(np.int32).tobytes()
+        for r in range(2):
+            p = 1 - r
+            assert got[r][it]["a"] == _data(1000 * it + 10 * p, nb).tobytes(), (it, r, "a")
+            assert got[r][it]["b"] == _data(1000 * it + 10 * p + 1, nb).tobytes(), (it, r, "b")
+            assert got[r][it]["sum"] == s, (it, r)
+            assert got[r][it]["z"] == [float(2 << 20)] * 8

@@ -397,8 +397,7 @@ static bool pending(hipError_t e) {
 static bool device_quiet_locked() {
   for (mx_comm *c : g_live) {
     if (c->tail_valid && c->tail && pending(hipEventQuery(c->tail))) return false;
-    for (int i = 0; i < 3; i++)
-      if (c->p2p_stream[i] && pending(hipStreamQuery(c->p2p_stream[i]))) return false;
+    if (p2p_pending(c)) return false;
   }
   return true;
 }

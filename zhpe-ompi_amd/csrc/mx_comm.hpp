@@ -217,7 +217,14 @@ struct mx_comm {
   // data; all three spin on the device, so they are created at the highest
   // priority, whose hardware queues the process's ordinary streams do not
   // share
+  // the device's three channel streams (send, receive, rendezvous pick),
+  // shared by every communicator of the process (p2p_setup): the spinning
+  // channels hold 3 high-priority hardware queues per device, whatever the
+  // number of communicators.  p2p_last[i]: event after this communicator's
+  // last kernel on channel i (its own work, for destroy and quiet checks).
   hipStream_t p2p_stream[3];
+  hipEvent_t p2p_last[3];
+  int p2p_last_valid[3];
   hipEvent_t p2p_ev;
   uint64_t *p2p_lanes;     // device: finished-lane counters of the three streams
   uint64_t p2p_ltot[3];    // lanes (workgroups) of the transfer kernels enqueued per stream
@@ -268,6 +275,7 @@ int p2p_setup(mx_comm *c);
 // wait for the communicator's point-to-point channels (rendezvous sends no
 // receive ever cleared give up first); no device-wide synchronisation
 void p2p_quiesce(mx_comm *c);
+bool p2p_pending(mx_comm *c);   // this communicator's channel kernels not yet done
 void p2p_release(mx_comm *c);
 // a point-to-point request completed: release its rendezvous slot / staging
 void p2p_finish(mx_request *q);

@@ -645,6 +645,53 @@ static hipError_t p2p_stream_create(hipStream_t *s) {
   return hipStreamCreateWithPriority(s, hipStreamNonBlocking, greatest);
 }
 
+// The send and receive channel streams of a device are shared by all its
+// communicators: HIP maps a process's streams onto 4
+// hardware queues per priority, and a kernel spinning on a queue holds back
+// every kernel behind it there, whatever its stream.  Three streams per
+// communicator overran the 4 high-priority queues from the second
+// communicator on, so two communicators' channels landed on one queue in an
+// order nothing controlled.  Shared, sends and receives take 2 queues
+// however many communicators exist, and the channel work of all
+// communicators runs in post order per direction -- the order one
+// communicator's work always had.  The rendezvous stream stays
+// per communicator and is made at its first rendezvous send: its kernels
+// wait for that communicator's CTS tickets only, so on a shared stream a
+// send of one communicator would hold back a cleared send of another.
+static std::mutex g_chan_mu;
+static hipStream_t g_chan[64][2];
+static int p2p_channels(hipStream_t out[3]) {
+  int dev = g_device;
+  if (dev < 0 && hipGetDevice(&dev) != hipSuccess) return MX_ERR_HIP;
+  if (dev < 0 || dev >= 64) return MX_ERR_HIP;
+  std::lock_guard<std::mutex> lk(g_chan_mu);
+  for (int i = 0; i < 2; i++) {
+    if (!g_chan[dev][i] && p2p_stream_create(&g_chan[dev][i]) != hipSuccess) {
+      g_chan[dev][i] = nullptr;
+      (void)hipGetLastError();
+      return MX_ERR_HIP;
+    }
+    out[i] = g_chan[dev][i];
+  }
+  return MX_SUCCESS;
+}
+static int p2p_rndv_stream(mx_comm *c) {
+  if (c->p2p_stream[2]) return MX_SUCCESS;
+  if (p2p_stream_create(&c->p2p_stream[2]) != hipSuccess) {
+    c->p2p_stream[2] = nullptr;
+    (void)hipGetLastError();
+    return MX_ERR_HIP;
+  }
+  return MX_SUCCESS;
+}
+
+// this communicator's kernel just enqueued on channel i
+static int p2p_note(mx_comm *c, int i) {
+  if (hipEventRecord(c->p2p_last[i], c->p2p_stream[i]) != hipSuccess) return MX_ERR_HIP;
+  c->p2p_last_valid[i] = 1;
+  return MX_SUCCESS;
+}
+
 // Setup makes no device-wide synchronisation: a receive of another
 // communicator may be spinning for a message whose sender waits for this
 // rank's first send here (example 3).  Buffers come from
@@ -680,8 +727,10 @@ int p2p_setup(mx_comm *c) {
   if (hipMemsetAsync(c->p2p_send, 0, sb, ls) != hipSuccess || hipMemsetAsync(c->p2p_recv, 0, rb, ls) != hipSuccess ||
       hipMemsetAsync(c->p2p_lanes, 0, 3 * sizeof(uint64_t), ls) != hipSuccess ||
       hipMemsetAsync(c->p2p_rndv_cur, 0, sizeof(P2PRndvCur), ls) != hipSuccess ||
-      p2p_stream_create(&c->p2p_stream[0]) != hipSuccess || p2p_stream_create(&c->p2p_stream[1]) != hipSuccess ||
-      p2p_stream_create(&c->p2p_stream[2]) != hipSuccess ||
+      p2p_channels(c->p2p_stream) != MX_SUCCESS ||
+      hipEventCreateWithFlags(&c->p2p_last[0], hipEventDisableTiming) != hipSuccess ||
+      hipEventCreateWithFlags(&c->p2p_last[1], hipEventDisableTiming) != hipSuccess ||
+      hipEventCreateWithFlags(&c->p2p_last[2], hipEventDisableTiming) != hipSuccess ||
       hipEventCreateWithFlags(&c->p2p_ev, hipEventDisableTiming) != hipSuccess ||
       hipStreamSynchronize(ls) != hipSuccess) {
     p2p_release(c);
@@ -691,17 +740,32 @@ int p2p_setup(mx_comm *c) {
 }
 
 void p2p_quiesce(mx_comm *c) {
+  // this communicator's kernels only (the streams are shared)
   for (int i = 0; i < 2; i++)
-    if (c->p2p_stream[i]) (void)hipStreamSynchronize(c->p2p_stream[i]);
+    if (c->p2p_last_valid[i] && hipEventSynchronize(c->p2p_last[i]) != hipSuccess) (void)hipGetLastError();
   // rendezvous sends no receive ever cleared: their picks give up
   if (c->p2p_rndv) __atomic_store_n(&c->p2p_rndv->abort, 1, __ATOMIC_RELEASE);
-  if (c->p2p_stream[2]) (void)hipStreamSynchronize(c->p2p_stream[2]);
+  if (c->p2p_last_valid[2] && hipEventSynchronize(c->p2p_last[2]) != hipSuccess) (void)hipGetLastError();
+  c->p2p_last_valid[0] = c->p2p_last_valid[1] = c->p2p_last_valid[2] = 0;
+}
+
+bool p2p_pending(mx_comm *c) {
+  for (int i = 0; i < 3; i++)
+    if (c->p2p_last_valid[i]) {
+      const hipError_t e = hipEventQuery(c->p2p_last[i]);
+      if (e == hipErrorNotReady) { (void)hipGetLastError(); return true; }
+      if (e != hipSuccess) (void)hipGetLastError();
+    }
+  return false;
 }
 
 void p2p_release(mx_comm *c) {
   p2p_quiesce(c);
-  for (int i = 0; i < 3; i++)
-    if (c->p2p_stream[i]) (void)hipStreamDestroy(c->p2p_stream[i]);
+  for (int i = 0; i < 3; i++) {
+    if (c->p2p_last[i]) (void)hipEventDestroy(c->p2p_last[i]);
+    c->p2p_last[i] = nullptr;
+  }
+  if (c->p2p_stream[2]) (void)hipStreamDestroy(c->p2p_stream[2]);   // its own; [0], [1] are the device's
   if (c->p2p_ev) (void)hipEventDestroy(c->p2p_ev);
   const size_t sb = sizeof(P2PSendState) * c->size, rb = sizeof(P2PRecvState) * c->size;
   pool_dev_put(c->p2p_send, sb);
@@ -818,6 +882,7 @@ int p2p_enqueue(mx_request *q, hipStream_t *done_stream) {
   const size_t bytes = q->ddt ? q->count * mx_ddt_size(q->ddt) : q->count;
   const bool rndv = send && bytes > P2P_STASH_C;
   if (rndv && c->p2p_rndv_free->empty()) return MX_ERR_NOMEM;   // P2P_RNDV_Q rendezvous sends pending
+  if (rndv && (rc = p2p_rndv_stream(c))) return rc;
   // completion through status[4] when the transfer kernel is the last one
   // (a send's pack runs before it on the same stream; a receive's unpack
   // after it); a rendezvous send completes only through status[4], raised
@@ -864,7 +929,7 @@ int p2p_enqueue(mx_request *q, hipStream_t *done_stream) {
     a.err = c->err_dev;
     a.fin = fin;
     hipLaunchKernelGGL(k_p2p_send, dim3(P2P_LE), dim3(kP2PThreads), 0, s, a);
-    if ((rc = mx_check_launch())) return rc;
+    if ((rc = mx_check_launch()) || (rc = p2p_note(c, 0))) return rc;
     if (rndv) {
       // the rendezvous kernel needs no event: the CTS it waits for follows
       // the envelope, which follows the caller's stream and the pack
@@ -888,7 +953,7 @@ int p2p_enqueue(mx_request *q, hipStream_t *done_stream) {
       ra.fin.done = nullptr;
       c->p2p_ltot[2] += P2P_LR;
       hipLaunchKernelGGL(k_p2p_rndv, dim3(P2P_LR), dim3(kP2PThreads), 0, c->p2p_stream[2], ra);
-      if ((rc = mx_check_launch())) return rc;
+      if ((rc = mx_check_launch()) || (rc = p2p_note(c, 2))) return rc;
       return MX_SUCCESS;   // tmp is freed when the request completes (p2p_finish)
     }
   } else {
@@ -920,6 +985,7 @@ int p2p_enqueue(mx_request *q, hipStream_t *done_stream) {
     hipLaunchKernelGGL(k_p2p_recv, dim3(P2P_L), dim3(kP2PThreads), 0, s, a);
     if ((rc = mx_check_launch())) return rc;
     if (tmp && (rc = mx_unpack(q->ddt, q->count, q->rbuf, tmp, 0, bytes, s))) return rc;
+    if ((rc = p2p_note(c, 1))) return rc;
   }
   if (tmp) (void)hipFreeAsync(tmp, s);
   return MX_SUCCESS;

@@ -12,6 +12,8 @@
 #include <time.h>
 
 #include "../mx_ompi_abi.h"
+#include "../mx_opal_convertor_abi.h"
+#include "../mx_btl_abi.h"
 #include "mx_host.h"
 
 /* ---- objects -------------------------------------------------------------- */
@@ -1479,4 +1481,201 @@ int mxh_request_free(void **rp)
     free(r);
     *rp = NULL;
     return rc;
+}
+
+/* ---------------------------------------------------------------------------
+ * The datatype engine around the mi355x convertor hook.  Restates what
+ * opal_convertor_prepare_for_send / _for_recv leave in the convertor for a
+ * homogeneous committed type (OPAL_CONVERTOR_PREPARE, opal_convertor.c:
+ * 520-560: pDesc, use_desc = &opt_desc, count, pBaseBuf, local_size), where a
+ * fragmenting sender / receiver starts (opal_convertor_set_position: the
+ * packed byte `start`), calls the hook the maintainer adds after the loop
+ * choice, then drives fAdvance the way
+ * opal_convertor_pack / _unpack do (opal_convertor.c:218-330) with `niov`
+ * iovecs of `frag` bytes per call, until the message is complete.
+ * `packed` holds the stream bytes [start, local_size).  Returns 0, or < 0
+ * (the hook declined: -10; an fAdvance error: -11; a contract violation:
+ * -12).  *calls: fAdvance calls made.
+ * ------------------------------------------------------------------------- */
+int mxh_convertor_run(const void *desc, size_t nrec, size_t size, int64_t lb, int64_t ub, int64_t true_lb,
+                      int64_t true_ub, size_t count, void *user, void *packed, size_t start, size_t frag,
+                      int niov, int recv, int *calls)
+{
+    int (*prep)(opal_convertor_t *) = g_dl ? (int (*)(opal_convertor_t *))dlsym(g_dl, "mca_convertor_mi355x_prepare")
+                                           : NULL;
+    if (!prep || niov < 1 || niov > 8 || !frag) return -1;
+    opal_datatype_t dt;
+    memset(&dt, 0, sizeof dt);
+    dt.size = size;
+    dt.lb = lb;
+    dt.ub = ub;
+    dt.true_lb = true_lb;
+    dt.true_ub = true_ub;
+    dt.flags = 0x0004;                              /* OPAL_DATATYPE_FLAG_COMMITTED */
+    dt.opt_desc.desc = (void *)desc;
+    dt.opt_desc.used = nrec - 1;                    /* the closing END_LOOP is not counted */
+    dt.opt_desc.length = nrec;
+    dt.desc = dt.opt_desc;
+    opal_convertor_t c;
+    memset(&c, 0, sizeof c);
+    c.flags = CONVERTOR_HOMOGENEOUS | (recv ? CONVERTOR_RECV : CONVERTOR_SEND);
+    c.pDesc = &dt;
+    c.use_desc = &dt.opt_desc;
+    c.count = count;
+    c.pBaseBuf = (unsigned char *)user;
+    c.local_size = count * size;
+    c.remote_size = c.local_size;
+    c.pStack = c.static_stack;
+    c.stack_size = DT_STATIC_STACK_SIZE;
+    c.bConverted = start;
+    if (!prep(&c) || !c.fAdvance) return -10;
+    *calls = 0;
+    char *p = (char *)packed;
+    while (!(c.flags & CONVERTOR_COMPLETED)) {
+        struct iovec iov[8];
+        for (int i = 0; i < niov; i++) {
+            iov[i].iov_base = p + (size_t)i * frag;
+            iov[i].iov_len = frag;
+        }
+        uint32_t out = (uint32_t)niov;
+        size_t max = (size_t)niov * frag;
+        const size_t before = c.bConverted;
+        const int32_t rc = c.fAdvance(&c, iov, &out, &max);
+        (*calls)++;
+        if (rc < 0) return -11;
+        size_t sum = 0;
+        for (uint32_t i = 0; i < out; i++) sum += iov[i].iov_len;
+        /* the contract: max_data = the bytes moved = the iovecs' lengths,
+         * bConverted advanced by them, 1 exactly at the end of the message */
+        if (sum != max || c.bConverted != before + max || (rc == 1) != (c.bConverted == c.local_size) ||
+            (!max && rc != 1))
+            return -12;
+        /* iovecs are filled in order: only the last one used may be short */
+        for (uint32_t i = 0; i + 1 < out; i++)
+            if (iov[i].iov_len != frag) return -12;
+        p += max;
+    }
+    /* a completed convertor packs nothing more (OPAL_CONVERTOR_SET_STATUS_BEFORE_PACK_UNPACK) */
+    struct iovec extra = {p, frag};
+    uint32_t out = 1;
+    size_t max = frag;
+    if (c.fAdvance(&c, &extra, &out, &max) != 1 || out != 0 || max != 0) return -12;
+    return 0;
+}
+
+/* ---------------------------------------------------------------------------
+ * A host shared-memory BTL module (vader / smcuda stand-in: eager and send
+ * limits only, no transport of its own) with the mi355x GPU RDMA slots
+ * installed by the component's mca_btl_mi355x_install, the way smcuda's
+ * component init installs its CUDA get (btl_smcuda_component.c:936), and
+ * ob1's RGET / PUT steps on device buffers restated around it: the owner
+ * registers its buffer (btl_register_mem) and ships the handle bytes
+ * (btl_registration_handle_size of them, in the PML header); the peer calls
+ * btl_get / btl_put with them and drives opal_progress -- here the
+ * component's progress function -- until the completion callback runs.
+ * ------------------------------------------------------------------------- */
+static mca_btl_base_module_t g_btl;
+static int (*g_btl_progress)(void);
+static int g_btl_ready;
+
+int mxh_btl_init(uint32_t *flags, size_t *handle_bytes)
+{
+    int (*install)(mca_btl_base_module_t *) =
+        g_dl ? (int (*)(mca_btl_base_module_t *))dlsym(g_dl, "mca_btl_mi355x_install") : NULL;
+    g_btl_progress = g_dl ? (int (*)(void))dlsym(g_dl, "mca_btl_mi355x_progress") : NULL;
+    if (!install || !g_btl_progress) return -1;
+    memset(&g_btl, 0, sizeof g_btl);
+    g_btl.btl_eager_limit = 4096;                 /* vader's defaults (btl_vader_component.c) */
+    g_btl.btl_rndv_eager_limit = 32768;
+    g_btl.btl_max_send_size = 32768;
+    g_btl.btl_exclusivity = 65536;                /* MCA_BTL_EXCLUSIVITY_HIGH */
+    g_btl.btl_flags = 0x0001;                     /* MCA_BTL_FLAGS_SEND */
+    if (install(&g_btl) != OPAL_SUCCESS) return -2;
+    *flags = g_btl.btl_flags;
+    *handle_bytes = g_btl.btl_registration_handle_size;
+    g_btl_ready = 1;
+    return 0;
+}
+
+/* the owner: register [base, base + size) and copy the handle bytes out */
+int mxh_btl_register(void *base, size_t size, void *handle_out, void **reg)
+{
+    if (!g_btl_ready) return -1;
+    struct mca_btl_base_registration_handle_t *h = g_btl.btl_register_mem(&g_btl, NULL, base, size, 0);
+    if (!h) return -2;
+    memcpy(handle_out, h, g_btl.btl_registration_handle_size);
+    *reg = h;
+    return 0;
+}
+
+int mxh_btl_deregister(void *reg)
+{
+    return g_btl_ready ? g_btl.btl_deregister_mem(&g_btl, reg) : -1;
+}
+
+typedef struct { volatile int done; int status; void *local; void *ctx; void *data; } mxh_rdma_cb_t;
+
+static void rdma_cb(mca_btl_base_module_t *module, struct mca_btl_base_endpoint_t *ep, void *local_address,
+                    struct mca_btl_base_registration_handle_t *local_handle, void *context, void *cbdata, int status)
+{
+    (void)module; (void)ep; (void)local_handle;
+    mxh_rdma_cb_t *cb = (mxh_rdma_cb_t *)cbdata;
+    cb->status = status;
+    cb->local = local_address;
+    cb->ctx = context;
+    cb->done = 1;
+}
+
+/* the peer: get (1) or put (0) `size` bytes between `local` and the owner's
+ * remote_addr, then progress until the callback; returns the callback's
+ * status, or < -100 (-101 the slot refused, -102 no callback within 30 s,
+ * -103 a callback with other arguments than those given) */
+int mxh_btl_rdma(int get, void *local, uint64_t remote_addr, const void *remote_handle, size_t size, int ntimes)
+{
+    if (!g_btl_ready) return -100;
+    mxh_rdma_cb_t cbs[16];
+    if (ntimes < 1 || ntimes > 16) return -100;
+    void *lreg = NULL;
+    struct mca_btl_base_registration_handle_t *lh = g_btl.btl_register_mem(&g_btl, NULL, local, size ? size : 1, 0);
+    lreg = lh;
+    /* several operations in flight before any progress call */
+    for (int k = 0; k < ntimes; k++) {
+        memset(&cbs[k], 0, sizeof cbs[k]);
+        mca_btl_base_module_get_fn_t fn = get ? g_btl.btl_get : g_btl.btl_put;
+        const int rc = fn(&g_btl, NULL, local, remote_addr, lh, (struct mca_btl_base_registration_handle_t *)remote_handle,
+                          size, 0, 255, rdma_cb, (void *)(intptr_t)(k + 1), &cbs[k]);
+        if (rc != OPAL_SUCCESS) return -101;
+    }
+    struct timespec t0, t1;
+    clock_gettime(CLOCK_MONOTONIC, &t0);
+    int st = 0;
+    for (int k = 0; k < ntimes; k++) {
+        while (!cbs[k].done) {
+            g_btl_progress();
+            clock_gettime(CLOCK_MONOTONIC, &t1);
+            if ((t1.tv_sec - t0.tv_sec) > 30) return -102;
+        }
+        if (cbs[k].local != local || cbs[k].ctx != (void *)(intptr_t)(k + 1)) return -103;
+        if (cbs[k].status != OPAL_SUCCESS) st = cbs[k].status;
+    }
+    if (lreg) g_btl.btl_deregister_mem(&g_btl, lreg);
+    return st;
+}
+
+/* queue `n` gets without progress, then btl_flush: every callback has run */
+int mxh_btl_flush_gets(void *local, uint64_t remote_addr, const void *remote_handle, size_t size, int n)
+{
+    if (!g_btl_ready || n < 1 || n > 16) return -100;
+    mxh_rdma_cb_t cbs[16];
+    for (int k = 0; k < n; k++) {
+        memset(&cbs[k], 0, sizeof cbs[k]);
+        if (g_btl.btl_get(&g_btl, NULL, (char *)local + (size_t)k * size, remote_addr + (uint64_t)k * size, NULL,
+                          (struct mca_btl_base_registration_handle_t *)remote_handle, size, 0, 255, rdma_cb, NULL,
+                          &cbs[k]) != OPAL_SUCCESS)
+            return -101;
+    }
+    if (g_btl.btl_flush(&g_btl, NULL) != OPAL_SUCCESS) return -104;
+    for (int k = 0; k < n; k++)
+        if (!cbs[k].done || cbs[k].status != OPAL_SUCCESS) return -102;
+    return 0;
 }

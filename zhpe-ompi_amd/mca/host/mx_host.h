@@ -110,6 +110,17 @@ int mxh_wait(void **req);
 int mxh_request_free(void **req);
 #define MXH_IN_PLACE ((void *)1)
 
+/* the datatype engine around the mi355x convertor hook (mca/convertor_mi355x.c) */
+/* a host shared-memory BTL module with the mi355x GPU RDMA slots (mca/btl_mi355x.c) */
+int mxh_btl_init(uint32_t *flags, size_t *handle_bytes);
+int mxh_btl_register(void *base, size_t size, void *handle_out, void **reg);
+int mxh_btl_deregister(void *reg);
+int mxh_btl_rdma(int get, void *local, uint64_t remote_addr, const void *remote_handle, size_t size, int ntimes);
+int mxh_btl_flush_gets(void *local, uint64_t remote_addr, const void *remote_handle, size_t size, int n);
+int mxh_convertor_run(const void *desc, size_t nrec, size_t size, int64_t lb, int64_t ub, int64_t true_lb,
+                      int64_t true_ub, size_t count, void *user, void *packed, size_t start, size_t frag,
+                      int niov, int recv, int *calls);
+
 #ifdef __cplusplus
 }
 #endif
