@@ -358,13 +358,17 @@ def bench_allreduce(torch, mx, dist, rank, world, dev, steps, warmup, nbytes=256
         comm.set_autotune(False)   # the A/B below forces each path
     except mx.MxError:
         pass
-    for name, reg, proto in (("staged_push", 0, "push"), ("staged_pull", 0, "pull"), ("zero_copy", 256 << 10, None)):
+    # zero_copy: results stored straight into the peers' rbufs (the default);
+    # zero_copy_gather: through the peers' gather areas + a local copy (round 4)
+    for name, reg, proto, direct in (("staged_push", 0, "push", True), ("staged_pull", 0, "pull", True),
+                                     ("zero_copy_gather", 256 << 10, None, False), ("zero_copy", 256 << 10, None, True)):
         try:
             comm.set_reg_min(reg)
         except mx.MxError:
             if reg:
                 proto_ab[name] = {"error": "registration unavailable"}
                 continue
+        comm.set_zc_direct(direct)
         comm.set_protocol(proto or proto_default)
         for _ in range(2):
             comm.allreduce(x.data_ptr(), out.data_ptr(), count, "FLOAT", "SUM", "auto", sp)

@@ -143,6 +143,12 @@ int mx_comm_set_zc_direct(mx_comm_t *comm, int on);
  * (test support). */
 int mx_release_pending(void);
 
+/* IPC regions of destroyed communicators waiting for every peer's BYE
+ * before reuse, and groups given up on (a peer that never destroyed the
+ * communicator: after 64 scans, or beyond 32 groups, a group stays allocated
+ * and unused).  Test support. */
+int mx_ipc_quarantine_stats(int *held, unsigned long long *abandoned);
+
 /* One-shot allreduce (one kernel: push, flag, fold) up to `max_bytes` per
  * rank; clamped to the one-shot slot capacity reserved at creation (1 MiB or
  * staging / (8 n); MX_ONESHOT_MAX at creation sets both).  0 = off.  Same

@@ -32,7 +32,7 @@ def test_bench_gpus_2_without_launcher_runs_the_allreduce():
     assert "MPI_Allreduce fp32 SUM 256 MiB" in d["config"]["workload"], d.get("allreduce_error")
     assert d["parity"] == "ok", d.get("parity")
     assert d["value"] > 0 and d["unit"] == "GB/s"
-    for name in ("staged_push", "staged_pull", "zero_copy"):
+    for name in ("staged_push", "staged_pull", "zero_copy_gather", "zero_copy"):
         ab = d["config"]["data_path_ab"][name]
         assert ab.get("parity") == "ok", (name, ab)
 

@@ -87,17 +87,20 @@ def _worker(rank, port, q):
         if rank == 0:
             for nbytes, off in ((0, 0), (1, 0), (4099, 1237), (big, 0)):
                 dst = torch.zeros(max(nbytes, 1), dtype=torch.uint8, device="cuda")
+                torch.cuda.synchronize()
                 hbuf = ctypes.create_string_buffer(peer_handle, len(peer_handle))
                 rc = H.mxh_btl_rdma(1, dst.data_ptr(), peer_addr + off, hbuf, nbytes, 3)
                 assert rc == 0, (nbytes, rc)
                 got[f"get{nbytes}"] = dst[:nbytes].cpu().numpy().tobytes()
             # a flush completes gets queued with no progress call
             dst = torch.zeros(8 * 4096, dtype=torch.uint8, device="cuda")
+            torch.cuda.synchronize()
             hbuf = ctypes.create_string_buffer(peer_handle, len(peer_handle))
             assert H.mxh_btl_flush_gets(dst.data_ptr(), peer_addr, hbuf, 4096, 8) == 0
             got["flush"] = dst.cpu().numpy().tobytes()
             # this process's own registration (the PML's self path)
             mine = torch.zeros(4099, dtype=torch.uint8, device="cuda")
+            torch.cuda.synchronize()
             hself = ctypes.create_string_buffer(handle, len(handle))
             assert H.mxh_btl_rdma(1, mine.data_ptr(), own.data_ptr() + 77, hself, 4099, 1) == 0
             got["self"] = mine.cpu().numpy().tobytes()
@@ -132,6 +135,7 @@ def _worker(rank, port, q):
             else:
                 ph, pa = exchange(None)
                 dst = torch.zeros(1 << 20, dtype=torch.uint8, device="cuda")
+                torch.cuda.synchronize()
                 hbuf = ctypes.create_string_buffer(ph, len(ph))
                 assert H.mxh_btl_rdma(1, dst.data_ptr(), pa, hbuf, 1 << 20, 1) == 0
                 got[f"remade{cycle}"] = dst.cpu().numpy().tobytes()

@@ -55,7 +55,8 @@ def _oracle_pack(rec, count, user, unpack=False, packed=None):
     if packed is None:
         packed = np.zeros(count * rec["size"], np.uint8)
     assert O.mxo_ddt_convert(rec["desc"].ctypes.data, rec["nrec"], B.ctypes.data, rec["lb"], rec["ub"], count,
-                             user.ctypes.data - rec["true_lb"], packed.ctypes.data, 1 if unpack else 0) == 0
+                             user.ctypes.data - rec["true_lb"], packed.ctypes.data,
+                             1 if unpack else 0) == count * rec["size"]          # bytes converted
     return packed
 
 

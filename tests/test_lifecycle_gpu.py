@@ -135,6 +135,22 @@ def _worker(rank, n, port, q):
         C = comm()
         C.close()
         res["pending_releases"] = int(mxompi.lib().mx_release_pending())
+
+        # a peer that never frees a communicator (rank 1 keeps D): rank 0's
+        # regions of D wait for a BYE that never comes; the quarantine gives
+        # the group up after its scans instead of rescanning it forever
+        D = comm()
+        if rank == 0:
+            D.close()
+        for _ in range(66):
+            E = comm()
+            E.close()
+        import ctypes
+        held, abandoned = ctypes.c_int(), ctypes.c_ulonglong()
+        mxompi.lib().mx_ipc_quarantine_stats(ctypes.byref(held), ctypes.byref(abandoned))
+        res["quarantine"] = (held.value, abandoned.value)
+        if rank == 1:
+            D.close()
         dist.destroy_process_group()
         q.put((rank, "ok", res))
     except Exception:  # noqa: BLE001
@@ -168,5 +184,7 @@ def test_lifecycle_never_waits_for_another_communicators_work():
         for k, v in exp.items():
             assert out[r][k] == v, (r, k)
         assert out[r]["pending_releases"] == 0
+    held, abandoned = out[0]["quarantine"]
+    assert abandoned >= 1 and held <= 2, out[0]["quarantine"]
     assert out[0]["c_recv"] == _x(1, 5).tobytes()       # rank 1's A message
     assert out[1]["c_recv"] == _x(0, 6).tobytes()       # rank 0's B message

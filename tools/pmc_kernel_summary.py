@@ -19,7 +19,12 @@ def main():
                 for row in csv.DictReader(f):
                     acc[(row["Kernel_Name"], row["Counter_Name"])].append(float(row["Counter_Value"]))
         for (k, c), v in sorted(acc.items()):
-            m = sum(v) / len(v) * 1024.0
+            m = sum(v) / len(v)
+            if c not in ("FETCH_SIZE", "WRITE_SIZE"):      # event counts, not KiB
+                print(json.dumps({"dir": os.path.basename(d.rstrip("/")), "kernel": k[:120], "counter": c,
+                                  "per_dispatch": round(m), "dispatches": len(v)}))
+                continue
+            m *= 1024.0
             if c == "FETCH_SIZE":
                 m *= 2.0
             print(json.dumps({"dir": os.path.basename(d.rstrip("/")), "kernel": k[:120], "counter": c,

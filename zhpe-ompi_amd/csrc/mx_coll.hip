@@ -568,8 +568,17 @@ extern "C" int mx_comm_create(int rank, int size, int device, size_t staging_byt
 // quarantine until the BYE row of its flags shows every peer.
 static std::mutex g_ipc_pool_mu;
 static std::vector<std::pair<char *, size_t>> g_ipc_pool;
-struct IpcQuarantine { char *staging, *hregion; uint64_t *flags; uint32_t peers; };
+struct IpcQuarantine { char *staging, *hregion; uint64_t *flags; uint32_t peers, scans; };
 static std::vector<IpcQuarantine> g_ipc_quarantine;
+// A peer that never destroys the communicator (it aborted, or exits without
+// MPI_Comm_free) never says BYE: its regions would be rescanned at every
+// creation for the rest of the process.  After kQuarantineScans scans (or
+// beyond kQuarantineMax groups, oldest first) a group is given up: it stays
+// allocated -- never reused, never freed under a peer's mapping -- and is
+// no longer scanned.
+constexpr uint32_t kQuarantineScans = 64;
+constexpr size_t kQuarantineMax = 32;
+static uint64_t g_ipc_abandoned;
 
 static size_t ipc_region_size(const char *p);
 
@@ -590,11 +599,20 @@ static void ipc_pool_put(char *p) {   // caller holds g_ipc_pool_mu
 // move every quarantined group whose peers have all said BYE to the pool
 static void ipc_quarantine_scan() {
   std::lock_guard<std::mutex> lk(g_ipc_pool_mu);
+  while (g_ipc_quarantine.size() > kQuarantineMax) {
+    g_ipc_quarantine.erase(g_ipc_quarantine.begin());
+    g_ipc_abandoned++;
+  }
   for (size_t i = 0; i < g_ipc_quarantine.size();) {
     IpcQuarantine &q = g_ipc_quarantine[i];
+    if (++q.scans > kQuarantineScans) {
+      g_ipc_quarantine.erase(g_ipc_quarantine.begin() + (long)i);
+      g_ipc_abandoned++;
+      continue;
+    }
     uint64_t bye[MAXR];
     hipStream_t ls = life_stream();
-    bool clear = ls && hipMemcpyAsync(bye, q.flags + BYE_BASE, sizeof bye, hipMemcpyDeviceToHost, ls) == hipSuccess &&
+    bool clear = hipMemcpyAsync(bye, q.flags + BYE_BASE, sizeof bye, hipMemcpyDeviceToHost, ls) == hipSuccess &&
                  hipStreamSynchronize(ls) == hipSuccess;
     if (!clear) (void)hipGetLastError();
     for (int p = 0; clear && p < MAXR; p++)
@@ -648,7 +666,14 @@ static void ipc_regions_release(char *staging, char *hregion, uint64_t *flags, u
     ipc_pool_put((char *)flags);
     return;
   }
-  g_ipc_quarantine.push_back(IpcQuarantine{staging, hregion, flags, peers});
+  g_ipc_quarantine.push_back(IpcQuarantine{staging, hregion, flags, peers, 0});
+}
+
+extern "C" int mx_ipc_quarantine_stats(int *held, unsigned long long *abandoned) {   // tests
+  std::lock_guard<std::mutex> lk(g_ipc_pool_mu);
+  if (held) *held = (int)g_ipc_quarantine.size();
+  if (abandoned) *abandoned = g_ipc_abandoned;
+  return MX_SUCCESS;
 }
 
 // BYE: written after this rank's device went idle (no poison check: a
@@ -708,7 +733,6 @@ extern "C" int mx_comm_create_ex(int rank, int size, int device, size_t staging_
   // about to enter this very creation; small buffers come
   // from the process pools, memsets and copies run on the lifecycle stream
   hipStream_t ls = ok ? life_stream() : nullptr;
-  ok = ok && ls;
   ok = ok && (c->err_host = (int *)pool_host_get(sizeof(int))) != nullptr;
   if (ok) *c->err_host = 0;
   ok = ok && hipHostGetDevicePointer((void **)&c->err_dev, c->err_host, 0) == hipSuccess;
@@ -1113,6 +1137,41 @@ static bool done_self_mark() {
   return v;
 }
 
+// A wait that timed out: one line per kind on stderr with this rank's
+// generation and what every peer has raised in its flags, and the peers'
+// registration-page sequence numbers -- enough to tell which peer stopped
+// where (the communicator is poisoned after it; no kernel runs on it).
+static void timeout_dump(mx_comm *c, const char *where) {
+  if (!c || c->local || !c->flagmem) return;
+  static std::atomic<int> dumps{0};
+  if (dumps.fetch_add(1) >= 4) return;
+  uint64_t f[NFLAGS * MAXR];
+  hipStream_t ls = life_stream();
+  if (hipMemcpyAsync(f, c->flagmem, sizeof f, hipMemcpyDeviceToHost, ls) != hipSuccess ||
+      hipStreamSynchronize(ls) != hipSuccess) {
+    (void)hipGetLastError();
+    return;
+  }
+  static const char *names[3] = {"READY", "PUSHED", "DONE"};
+  fprintf(stderr, "mx: rank %d/%d timed out (%s), gen %llu\n", c->rank, c->size, where, (unsigned long long)c->gen);
+  for (int k = 0; k < 3 && k < NFLAGS; k++) {
+    char line[512];
+    int o = snprintf(line, sizeof line, "mx:   %-6s from peers:", names[k]);
+    for (int p = 0; p < c->size && o < (int)sizeof line - 24; p++)
+      o += snprintf(line + o, sizeof line - o, " %llu", (unsigned long long)f[k * MAXR + p]);
+    fprintf(stderr, "%s\n", line);
+  }
+  if (c->reg_shm) {
+    const RegRec *R = (const RegRec *)c->reg_shm;
+    char line[512];
+    int o = snprintf(line, sizeof line, "mx:   reg seq/vseq:");
+    for (int p = 0; p < c->size && o < (int)sizeof line - 40; p++)
+      o += snprintf(line + o, sizeof line - o, " %llu/%llu", (unsigned long long)R[p].seq.load(),
+                    (unsigned long long)R[p].vseq.load());
+    fprintf(stderr, "%s (mine %llu)\n", line, (unsigned long long)c->reg_seq);
+  }
+}
+
 // mk: the completion flags the last kernel raises itself (mark_arm(&mk,
 // true) before its launch), else the marker kernel
 static int finish(mx_comm *c, hipStream_t s, const Mark *mk = nullptr) {
@@ -1127,7 +1186,10 @@ static int finish(mx_comm *c, hipStream_t s, const Mark *mk = nullptr) {
   if (c->err_host && *(volatile int *)c->err_host) {
     int e = *(volatile int *)c->err_host;
     *c->err_host = 0;
-    if (e == MX_ERR_TIMEOUT) c->poisoned = e;   // sticky: the device side is poisoned too
+    if (e == MX_ERR_TIMEOUT) {
+      c->poisoned = e;   // sticky: the device side is poisoned too
+      timeout_dump(c, "device wait");
+    }
     return e;
   }
   return MX_SUCCESS;
@@ -1513,6 +1575,7 @@ static int tune_exchange(mx_comm *c, double el, double *tmax) {
         if (c->timeout_s > 0 &&
             std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count() > c->timeout_s) {
           c->poisoned = MX_ERR_TIMEOUT;
+          timeout_dump(c, "tuning exchange");
           return MX_ERR_TIMEOUT;
         }
       }
@@ -1681,6 +1744,7 @@ static int reg_wait(mx_comm *c, bool verdict, uint64_t k) {
         if (c->timeout_s > 0 &&
             std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count() > c->timeout_s) {
           c->poisoned = MX_ERR_TIMEOUT;
+          timeout_dump(c, verdict ? "registration verdicts" : "registration records");
           return MX_ERR_TIMEOUT;
         }
       }
@@ -3954,7 +4018,7 @@ static bool heap_map_attempt(mx_heap *h) {
   }
   const uint64_t sig = 0x5EED0000ull + (uint64_t)c->rank;
   hipStream_t ls = life_stream();
-  if (ok && (!ls || hipMemcpyAsync(h->flags + 256, &sig, sizeof sig, hipMemcpyHostToDevice, ls) != hipSuccess ||
+  if (ok && (hipMemcpyAsync(h->flags + 256, &sig, sizeof sig, hipMemcpyHostToDevice, ls) != hipSuccess ||
              hipStreamSynchronize(ls) != hipSuccess))
     ok = 0;
   if (!heap_agree(c, ok)) return false;   // every PE mapped and signed before anyone checks
@@ -4004,7 +4068,7 @@ extern "C" int mx_heap_create(mx_comm_t *c, size_t bytes, mx_heap_t **out) {
     // else a late write of the old heap survives the zeroing (as the
     // communicator flags did in round 3)
     hipStream_t ls = life_stream();
-    int ok = heap_agree(c, 1) && ls && hipMemsetAsync(h->mem, 0, kHeapFlagBytes, ls) == hipSuccess &&
+    int ok = heap_agree(c, 1) && hipMemsetAsync(h->mem, 0, kHeapFlagBytes, ls) == hipSuccess &&
              hipStreamSynchronize(ls) == hipSuccess;
     if (!heap_agree(c, ok)) {
       c->hregion_used = h->region_off;
@@ -4020,7 +4084,7 @@ extern "C" int mx_heap_create(mx_comm_t *c, size_t bytes, mx_heap_t **out) {
     int ok = hipExtMallocWithFlags((void **)&h->mem, kHeapFlagBytes + h->bytes, hipDeviceMallocUncached) ==
              hipSuccess;
     hipStream_t ls = life_stream();
-    if (ok && (!ls || hipMemsetAsync(h->mem, 0, kHeapFlagBytes, ls) != hipSuccess ||
+    if (ok && (hipMemsetAsync(h->mem, 0, kHeapFlagBytes, ls) != hipSuccess ||
                hipStreamSynchronize(ls) != hipSuccess))
       ok = 0;
     if (!ok) h->mem = nullptr;

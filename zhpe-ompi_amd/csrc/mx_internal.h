@@ -36,9 +36,10 @@ int svc_reduce(int op, int type, const void *in, const void *in2, void *inout, s
 // Lifecycle work (communicator / heap / p2p create and destroy) never waits
 // for the whole device: another communicator's collective or receive may be
 // spinning on a peer that waits for what this thread does next (VERDICT r4
-// weak 3).  life_stream(): a process-wide non-blocking stream (created once
-// per device) for the memsets, copies and signals of those paths;
-// life_sync() waits for it alone.
+// weak 3).  life_stream(): the stream of the memsets, copies and signals of
+// those paths -- the legacy default stream, which never waits for kernels
+// on non-blocking streams (where all of this library's spinning work runs);
+// life_sync() waits for it.
 hipStream_t life_stream();
 int life_sync();
 // Device / mapped-host allocations of the lifecycle paths come from

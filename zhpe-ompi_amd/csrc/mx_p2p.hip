@@ -703,7 +703,7 @@ int p2p_setup(mx_comm *c) {
   if (c->p2p_send) return MX_SUCCESS;
   const size_t sb = sizeof(P2PSendState) * c->size, rb = sizeof(P2PRecvState) * c->size;
   hipStream_t ls = life_stream();
-  if (!ls || !(c->p2p_send = (P2PSendState *)pool_dev_get(sb))) {
+  if (!(c->p2p_send = (P2PSendState *)pool_dev_get(sb))) {
     c->p2p_send = nullptr;
     return MX_ERR_NOMEM;
   }

@@ -55,8 +55,11 @@ std::vector<hipEvent_t> g_ev_free;
 struct Export { uint64_t base, size, id; hipIpcMemHandle_t h; };
 std::vector<Export> g_exp;            // most recent last, at most 16
 
+// a blocking stream: implicitly after the work already queued on the legacy
+// default stream (a receive buffer the application just zeroed or wrote
+// there is written by the get only after that), with no event per call
 hipStream_t rdma_stream() {
-  if (!g_stream && hipStreamCreateWithFlags(&g_stream, hipStreamNonBlocking) != hipSuccess) {
+  if (!g_stream && hipStreamCreateWithFlags(&g_stream, hipStreamDefault) != hipSuccess) {
     (void)hipGetLastError();
     g_stream = nullptr;
   }

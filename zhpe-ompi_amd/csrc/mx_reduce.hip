@@ -11,8 +11,11 @@
 //    ring step);
 //  * buffers whose misalignment differs mod 16 fall back to an
 //    element-per-lane kernel (still coalesced);
-//  * large launches use non-temporal loads AND stores (mx_mem.hpp): 1 GiB
-//    fp32 SUM 5.65-5.86 -> 6.30-6.46 TB/s on MI355X (bw_probe3).
+//  * large launches (>= 384 MiB footprint) use non-temporal loads AND
+//    stores in one-wave workgroups (mx_mem.hpp): 1 GiB fp32 SUM 0.475-0.483
+//    ms per launch, 6.67-6.78 TB/s = 0.83-0.85 of 8 TB/s, PMC traffic =
+//    the algorithmic bytes (profiles/r04/,
+//    profiles/r05/reduce_local_kernel_stats_r5.csv).
 // Algorithmic bytes per launch: 2-buffer 3*n*size (read in, read inout,
 // write inout), 3-buffer 3*n*size.
 #include <hip/hip_runtime.h>

@@ -171,7 +171,8 @@ extern "C" int mx_free(void *p) {
   size_t bytes = 0;
   if (hipMemGetAddressRange(&base, &bytes, p) == hipSuccess) mx_ptr_cache_forget(base, bytes);
   else (void)hipGetLastError();
-  return mx_hip_rc(hipFree(p));
+  release_later(p, REL_DEV);   // hipFree waits for every stream of the device
+  return MX_SUCCESS;
 }
 
 extern "C" int mx_host_alloc(size_t bytes, void **p) {
@@ -184,7 +185,8 @@ extern "C" int mx_host_alloc(size_t bytes, void **p) {
 
 extern "C" int mx_host_free(void *p) {
   if (!p) return MX_SUCCESS;
-  return mx_hip_rc(hipHostFree(p));
+  release_later(p, REL_HOST);
+  return MX_SUCCESS;
 }
 
 extern "C" int mx_memcpy(void *dst, const void *src, size_t bytes, void *stream) {
@@ -247,31 +249,22 @@ extern "C" int mx_stream_sync(void *stream) {
 
 namespace {
 std::mutex g_life_mu;
-hipStream_t g_life[64] = {};   // per device
 struct PoolEnt { void *p; size_t bytes; bool host; };
 std::vector<PoolEnt> *g_pool = nullptr;   // never destroyed: entries outlive static destructors
 }  // namespace
 
-hipStream_t mx::life_stream() {
-  int dev = g_device;
-  if (dev < 0 && hipGetDevice(&dev) != hipSuccess) return nullptr;
-  if (dev < 0 || dev >= 64) return nullptr;
-  std::lock_guard<std::mutex> lk(g_life_mu);
-  if (!g_life[dev]) {
-    hipStream_t s = nullptr;
-    if (hipStreamCreateWithFlags(&s, hipStreamNonBlocking) != hipSuccess) {
-      (void)hipGetLastError();
-      return nullptr;
-    }
-    g_life[dev] = s;
-  }
-  return g_life[dev];
-}
+// The legacy default stream.  tools/lifecycle_sync_probe.hip: its copies,
+// memsets and kernels never wait for a kernel spinning on a NON-BLOCKING
+// stream -- where every request collective (the coll component's request
+// stream) and point-to-point channel of this library spins -- while
+// hipDeviceSynchronize, hipFree, hipHostFree and hipIpcCloseMemHandle do.  A
+// private stream was tried first: it is one more hardware queue per process,
+// and with 8 processes sharing one GPU (the test pool's multi-rank setup) the
+// extra queues made staged collectives time out waiting for peers whose
+// kernels were not scheduled (profiles/r05/gpu_r5f_staged_push_timeout.txt).
+hipStream_t mx::life_stream() { return nullptr; }
 
-int mx::life_sync() {
-  hipStream_t s = life_stream();
-  return s ? mx_hip_rc(hipStreamSynchronize(s)) : MX_ERR_HIP;
-}
+int mx::life_sync() { return mx_hip_rc(hipStreamSynchronize(life_stream())); }
 
 static void *pool_get(size_t bytes, bool host) {
   {
