@@ -259,7 +259,10 @@ def main():
     if doc.get("pairs_side_by_side") or doc.get("pack_side_by_side"):
         with open(os.path.splitext(args.out)[0] + ".txt", "w") as f:
             f.write(f"# CPU ({doc.get('host_cpu')}, {doc.get('cores')} core, {doc.get('kind')}; {doc.get('build')})\n"
-                    f"# vs GPU ({', '.join(doc.get('gpu_sources', []))}); GB/s algorithmic\n")
+                    f"# vs GPU ({', '.join(doc.get('gpu_sources', []))}); GB/s algorithmic\n"
+                    f"# source run: {doc.get('source_run') or '(unnamed)'}, CPU column at {doc.get('when')}; the GPU "
+                    f"and CPU columns come from this one run on one box\n"
+                    f"# sample: {doc.get('sample')}\n")
             f.write(f"{'op':>7} {'type':<24} {'GPU GB/s':>10} {'CPU GB/s':>10} {'GPU/CPU':>8}\n")
             for r in doc.get("pairs_side_by_side", []):
                 f.write(f"{r['op']:>7} {r['type']:<24} {r['gpu_gbs']:10.1f} {r['cpu_gbs']:10.2f} {r['gpu_over_cpu']:8.1f}\n")

@@ -1,0 +1,19 @@
+# round 5 (n): byte-map PACK non-temporal span loads + packed stores: parity, A/B vs ordinary accesses, floors same box
+set -o pipefail
+cd "$GRAFT_REPO_ROOT"
+export TMPDIR=/tmp HSA_ENABLE_IPC_MODE_LEGACY=0
+O=gpurun_out
+mkdir -p $O
+STEP_TIMEOUT=400 bash tools/gpu_pytest.sh r5n_conv "tests/test_convertor.py tests/test_convertor_pins.py tests/test_convertor_hook_gpu.py -m gpu" || exit $?
+T="struct_char_d3_int_resized48 indexed_f32_random ref_blacs_indexed ref_struct ref_strange"
+for rep in 1 2; do
+for v in "" "MX_CONV_BMAP_NT=0" "MX_CONV_BMAP_DW=0"; do
+  echo "== $v (rep $rep)" >> $O/conv_ab_r5n.txt
+  env $v timeout -k 10 200 python tools/conv_probe.py --bytes $((256<<20)) --dirs pack $T >> $O/conv_ab_r5n.txt 2>&1 || exit $?
+  env $v timeout -k 10 200 python tools/conv_probe.py --bytes $((1<<30)) --dirs pack $T >> $O/conv_ab_r5n.txt 2>&1 || exit $?
+done
+done
+grep -v amdgpu.ids $O/conv_ab_r5n.txt
+timeout -k 10 120 ./tools/pack_floor_probe $(python tools/pack_floor_args.py $((256<<20))) > $O/pack_floor_r5n.txt 2>&1 || exit $?
+timeout -k 10 120 ./tools/pack_floor_probe $(python tools/pack_floor_args.py $((1<<30))) >> $O/pack_floor_r5n.txt 2>&1 || exit $?
+grep -E "struct_char|indexed_f32|blacs|ref_struct|ref_strange" $O/pack_floor_r5n.txt

@@ -39,6 +39,21 @@ __global__ void __launch_bounds__(kB) k_floor(const v4u *span, uint64_t nspan, v
   else packed[k] = acc;
 }
 
+// split: the two streams each perfectly coalesced (consecutive lanes on
+// consecutive granules, grid-stride), the span folded per thread into what
+// it stores -- the plain streaming floor of reading `span` + writing `packed`
+template <bool NT>
+__global__ void __launch_bounds__(kB) k_floor_split(const v4u *span, uint64_t nspan, v4u *packed, uint64_t npk) {
+  const uint64_t nth = (uint64_t)gridDim.x * kB, k0 = (uint64_t)blockIdx.x * kB + threadIdx.x;
+  v4u acc = {(uint32_t)k0, 0, 0, 0};
+  for (uint64_t j = k0; j < nspan; j += nth) acc ^= NT ? __builtin_nontemporal_load(span + j) : span[j];
+  for (uint64_t k = k0; k < npk; k += nth) {
+    const v4u v = acc + (uint32_t)k;
+    if (NT) __builtin_nontemporal_store(v, packed + k);
+    else packed[k] = v;
+  }
+}
+
 int main(int argc, char **argv) {
   if (argc < 4 || (argc - 1) % 3) {
     printf("usage: %s NAME SPAN_BYTES PACKED_BYTES [...]\n", argv[0]);
@@ -56,11 +71,20 @@ int main(int argc, char **argv) {
     CK(hipMalloc(&p, npk * 16));
     CK(hipMemset(s, 1, nspan * 16));
     CK(hipMemset(p, 0, npk * 16));
-    for (int nt = 0; nt < 2; nt++) {
+    // PFP_SHIFT=16: the span starts 16 bytes past a 128-byte line (as a
+    // product tile's 16-aligned span usually does)
+    const uint64_t shift = getenv("PFP_SHIFT") ? strtoull(getenv("PFP_SHIFT"), nullptr, 0) / 16 : 0;
+    const v4u *ss = s + shift;
+    const uint64_t nss = nspan - shift;
+    for (int mode = 0; mode < 4; mode++) {
+      const int nt = mode & 1, split = mode >> 1;
       auto launch = [&] {
         const dim3 g((unsigned)((npk + kB - 1) / kB)), b(kB);
-        if (nt) hipLaunchKernelGGL(k_floor<true>, g, b, 0, 0, s, nspan, p, npk, nspan, npk);
-        else hipLaunchKernelGGL(k_floor<false>, g, b, 0, 0, s, nspan, p, npk, nspan, npk);
+        const dim3 gs((unsigned)(256 * 8)), bs(kB);
+        if (split && nt) hipLaunchKernelGGL(k_floor_split<true>, gs, bs, 0, 0, ss, nss, p, npk);
+        else if (split) hipLaunchKernelGGL(k_floor_split<false>, gs, bs, 0, 0, ss, nss, p, npk);
+        else if (nt) hipLaunchKernelGGL(k_floor<true>, g, b, 0, 0, ss, nss, p, npk, nss, npk);
+        else hipLaunchKernelGGL(k_floor<false>, g, b, 0, 0, ss, nss, p, npk, nss, npk);
       };
       launch();
       CK(hipDeviceSynchronize());
@@ -76,8 +100,8 @@ int main(int argc, char **argv) {
       }
       std::sort(ts.begin(), ts.end());
       const double us = ts[4] * 1e3;
-      printf("%-32s %-5s span %12llu packed %12llu  %9.1f us  2x packed %7.1f GB/s  moved %7.1f GB/s\n", name,
-             nt ? "nt" : "plain", (unsigned long long)span, (unsigned long long)pk, us, 2.0 * pk / us / 1e3,
+      printf("%-32s %-11s span %12llu packed %12llu  %9.1f us  2x packed %7.1f GB/s  moved %7.1f GB/s\n", name,
+             split ? (nt ? "split-nt" : "split-plain") : (nt ? "nt" : "plain"), (unsigned long long)span, (unsigned long long)pk, us, 2.0 * pk / us / 1e3,
              (double)(span + pk) / us / 1e3);
       fflush(stdout);
     }

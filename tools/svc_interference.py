@@ -91,10 +91,13 @@ def main():
                 name = "service" if served else "launch"
                 row = {"round": rnd, "config": name, "call_bytes": nbytes, "copy_gbs": round(gbs, 1),
                        "slowdown_pct": round(100.0 * (alone / gbs - 1.0), 2), "calls": made,
-                       "calls_per_s": round(made / el, 0), "service_state_served_launches": st}
+                       "calls_per_s": round(made / el, 0), "service_state_served_launches": st,
+                       # application time lost per call: the copy's wall time times the share it lost
+                       "app_us_lost_per_call": round(1e6 * el * (1.0 - gbs / alone) / max(1, made), 3)}
                 rows.append(row)
                 print(f"round {rnd} {name:7s} {nbytes:>8} B  copy {gbs:8.1f} GB/s  slowdown {row['slowdown_pct']:6.2f} %"
-                      f"  calls {made} ({row['calls_per_s']:.0f}/s)", flush=True)
+                      f"  calls {made} ({row['calls_per_s']:.0f}/s)  app lost {row['app_us_lost_per_call']:.2f} us/call",
+                      flush=True)
     if args.out:
         with open(args.out, "w") as f:
             json.dump({"what": __doc__.strip().splitlines()[0], "reps": args.reps, "rows": rows}, f, indent=1)

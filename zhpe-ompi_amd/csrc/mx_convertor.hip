@@ -140,6 +140,15 @@ __device__ __forceinline__ uint4 gld16(const char *p) {        // 16-byte aligne
   const v4u_a16 v = *(const __attribute__((address_space(1))) v4u_a16 *)(p);
   return make_uint4(v.x, v.y, v.z, v.w);
 }
+template <bool NT>
+__device__ __forceinline__ uint4 gld16p(const char *p) {       // 16-byte aligned, nt when NT
+  if constexpr (NT) {
+    const v4u_a16 v = __builtin_nontemporal_load((const __attribute__((address_space(1))) v4u_a16 *)(p));
+    return make_uint4(v.x, v.y, v.z, v.w);
+  } else {
+    return gld16(p);
+  }
+}
 __device__ __forceinline__ W4 gld16a4(const char *p) {         // 4-byte aligned
   const v4u_a4 v = *(const __attribute__((address_space(1))) v4u_a4 *)(p);
   W4 w;
@@ -624,6 +633,7 @@ __global__ void __launch_bounds__(kCB) k_pack_tile_pipe(ConvArgs a, int nruns_ld
 constexpr uint32_t kBmapMaxS = 65535;      // packed bytes per instance (piece soff is 16-bit)
 constexpr size_t kBmapLds = 20480;         // PACK: map bytes staged in LDS
 constexpr int kBmapSpan = 24576;           // PACK: user span staged per tile
+constexpr int kBmapSpans[3] = {12288, kBmapSpan, 49152};   // MX_CONV_BMAP_SPAN choices
 constexpr int kPieceStage = 16384;         // UNPACK: packed bytes staged per tile
 
 struct DPiece {
@@ -648,6 +658,9 @@ struct BmapArgs {
   uint64_t ntiles;
   uint32_t adv_b;          // kCB * 4 stream bytes = adv_io / ext instances + adv_b bytes
   int64_t adv_io;
+  uint64_t lo_mask;        // a tile's staged span starts at lo & ~lo_mask (15, or 127: whole lines)
+  uint32_t qsh;            // 2: the map is staged as quads (entry b at [4b], its dword's bytes at [4b..4b+3])
+  uint32_t cw;             // try one LDS dword read per packed dword (word-piece layouts)
 };
 
 // M = uint16_t when the instance's user span is below 64 KiB, else uint32_t.
@@ -655,14 +668,30 @@ struct BmapArgs {
 // flight in registers (SPAN / 16 / kCB uint4 per lane) while the lanes
 // gather the current tile out of LDS -- without it every tile's span load
 // and gather run back to back inside the workgroup.
-template <int SPAN, class M, bool DW, bool PIPE>
+template <int SPAN, class M, bool DW, bool PIPE, bool NT>
 __global__ void __launch_bounds__(kCB) k_pack_bmap(BmapArgs a) {
   extern __shared__ __align__(16) char smem[];
   char *span = smem;                                         // SPAN + 32
+  // The map in LDS, entry x = user offset of packed byte x (x >= S: of the
+  // next instance, + ext), so a dword at instance byte b reads its four
+  // entries x = b..b+3 with no wrap test:
+  //   qsh 0: entries 0 .. S+2 in a row -- one 8-byte LDS read when b is a
+  //          multiple of 4 (S % 4 == 0);
+  //   qsh 2: quads, [4b + j] = entry b + j -- every dword's four entries in
+  //          one aligned 8-byte read for any S (a misaligned read of the row
+  //          stalled the struct type's gather: SQ_WAIT_INST_LDS 388M vs 23M,
+  //          profiles/r05/pmc_pack_r5j.jsonl).
+  // bmap[x << qsh] is entry x either way.
   M *bmap = reinterpret_cast<M *>(smem + SPAN + 32);
   __shared__ uintptr_t s_lo[2], s_hi[2];
   constexpr int kPre = SPAN / 16 / kCB;
-  for (uint32_t i = threadIdx.x; i < a.S; i += kCB) bmap[i] = reinterpret_cast<const M *>(a.map)[i];
+  const uint32_t qsh = a.qsh;
+  const uint32_t nent = qsh ? 4 * a.S : a.S + 3;
+  for (uint32_t i = threadIdx.x; i < nent; i += kCB) {
+    const uint32_t x = qsh ? (i >> 2) + (i & 3) : i;
+    const uint32_t k = x / a.S;
+    bmap[i] = (M)(reinterpret_cast<const M *>(a.map)[x - k * a.S] + k * (uint32_t)a.ext);
+  }
   const uint64_t wend = a.offset + a.len;
   // tile t: absolute stream bytes [s0, s1) (window-clipped from sa), instances ia..ib
   auto geom = [&](uint64_t t, uint64_t &s0, uint64_t &sa, uint64_t &s1, uint64_t &ia, uint64_t &ib) {
@@ -679,10 +708,10 @@ __global__ void __launch_bounds__(kCB) k_pack_bmap(BmapArgs a) {
     const uintptr_t ubase = (uintptr_t)a.user + (int64_t)ia * a.ext + a.umin;
     uintptr_t lo = ubase, hi = ubase + (int64_t)(ib - ia) * a.ext + a.uspan;
     if (a.mono) {
-      lo = ubase + bmap[sa - ia * a.S];
-      hi = ubase + (int64_t)(ib - ia) * a.ext + bmap[s1 - 1 - ib * a.S] + 1;
+      lo = ubase + bmap[(sa - ia * a.S) << qsh];
+      hi = ubase + (int64_t)(ib - ia) * a.ext + bmap[(s1 - 1 - ib * a.S) << qsh] + 1;
     }
-    s_lo[slot] = lo & ~(uintptr_t)15;
+    s_lo[slot] = lo & ~(uintptr_t)a.lo_mask;
     s_hi[slot] = (hi + 15) & ~(uintptr_t)15;
   };
   auto gather = [&](uint64_t t, uintptr_t lo) {
@@ -694,32 +723,46 @@ __global__ void __launch_bounds__(kCB) k_pack_bmap(BmapArgs a) {
       // lane = one packed dword per step, consecutive lanes consecutive
       // dwords: the map reads of a wave are 8 bytes apart (2-way bank
       // conflicts; 16-byte lanes read it 32 bytes apart, 8-way) and each
-      // store instruction writes 256 contiguous bytes
-      const uint64_t q0 = s0 / 4 + threadIdx.x;
-      uint64_t inst = udiv(q0 * 4, a.mS);
-      uint32_t b = (uint32_t)(q0 * 4 - inst * a.S);
-      int64_t io = (int64_t)(inst - ia) * a.ext + d0;
-      for (uint64_t q = q0; q * 4 < s1; q += kCB) {
-        const uint64_t p = q * 4;
-        if (p >= a.offset && p + 4 <= wend) {
-          uint32_t v = 0;
-          uint32_t bb = b;
-          int64_t ii = io;
-#pragma unroll
-          for (int i = 0; i < 4; i++) {
-            v |= (uint32_t)(uint8_t)span[ii + bmap[bb]] << (8 * i);
-            if (++bb == a.S) { bb = 0; ii += a.ext; }
+      // store instruction writes 256 contiguous bytes.  Everything inside the
+      // tile is 32-bit: dword j of the tile is stream bytes s0 + 4j (the tile
+      // is < 64 KiB of stream, its span < 64 KiB of LDS), so the loop is 4
+      // map reads, 4 byte reads and ~16 VALU per dword (round 4's 64-bit
+      // loop with a wrap test per byte took 55, PMC SQ_INSTS_VALU,
+      // profiles/r05/pmc_pack_r5.jsonl)
+      const uint32_t nq = (uint32_t)((s1 - s0 + 3) / 4);
+      const uint32_t jlo = (uint32_t)((sa - s0 + 3) / 4);     // dwords [jlo, jhi) lie inside the window
+      const uint32_t jhi = (uint32_t)((s1 - s0) / 4);
+      char *const pk = a.packed + (int64_t)(s0 - a.offset);   // dword j at pk + 4j (j >= jlo)
+      const uint64_t p0 = s0 + 4 * (uint64_t)threadIdx.x;
+      const uint64_t inst = udiv(p0, a.mS);
+      uint32_t b = (uint32_t)(p0 - inst * a.S);
+      int32_t io = (int32_t)((int64_t)(inst - ia) * a.ext + d0);
+      const int32_t adv_io = (int32_t)a.adv_io, ext = (int32_t)a.ext;
+      for (uint32_t j = threadIdx.x; j < nq; j += kCB) {
+        if (j >= jlo && j < jhi) {
+          const M *m = bmap + (b << qsh);
+          const int32_t e0 = m[0], e1 = m[1], e2 = m[2], e3 = m[3];
+          uint32_t v;
+          // a wave whose every dword is 4 user-contiguous bytes (word
+          // pieces: indexed / BLACS) reads each with one LDS dword read
+          if (a.cw && __all((e1 == e0 + 1) & (e2 == e0 + 2) & (e3 == e0 + 3))) {
+            v = *reinterpret_cast<const uint32_t *>(span + io + e0);
+          } else {
+            v = (uint32_t)(uint8_t)span[io + e0] | (uint32_t)(uint8_t)span[io + e1] << 8 |
+                (uint32_t)(uint8_t)span[io + e2] << 16 | (uint32_t)(uint8_t)span[io + e3] << 24;
           }
-          *reinterpret_cast<uint32_t *>(a.packed + (p - a.offset)) = v;
+          if (NT) __builtin_nontemporal_store(v, reinterpret_cast<uint32_t *>(pk + 4 * j));
+          else *reinterpret_cast<uint32_t *>(pk + 4 * j) = v;
         } else {                                              // window edge: the bytes inside only
+          const uint64_t p = s0 + 4 * (uint64_t)j;
           for (uint64_t x = p < a.offset ? a.offset : p; x < p + 4 && x < wend; x++) {
             const uint64_t i = udiv(x, a.mS);
-            a.packed[x - a.offset] = span[(int64_t)(i - ia) * a.ext + d0 + bmap[x - i * a.S]];
+            a.packed[x - a.offset] = span[(int64_t)(i - ia) * a.ext + d0 + bmap[(x - i * a.S) << qsh]];
           }
         }
         b += a.adv_b;                                         // next: kCB dwords further
-        io += a.adv_io;
-        if (b >= a.S) { b -= a.S; io += a.ext; }
+        io += adv_io;
+        if (b >= a.S) { b -= a.S; io += ext; }
       }
       return;
     }
@@ -728,7 +771,7 @@ __global__ void __launch_bounds__(kCB) k_pack_bmap(BmapArgs a) {
       if (p < a.offset || p + 16 > wend) {                    // window edge: the bytes inside only
         for (uint64_t q = p < a.offset ? a.offset : p; q < p + 16 && q < wend; q++) {
           const uint64_t i = udiv(q, a.mS);
-          a.packed[q - a.offset] = span[(int64_t)(i - ia) * a.ext + d0 + bmap[q - i * a.S]];
+          a.packed[q - a.offset] = span[(int64_t)(i - ia) * a.ext + d0 + bmap[(q - i * a.S) << qsh]];
         }
         continue;
       }
@@ -741,12 +784,17 @@ __global__ void __launch_bounds__(kCB) k_pack_bmap(BmapArgs a) {
         uint32_t v = 0;
 #pragma unroll
         for (int i = 0; i < 4; i++) {
-          v |= (uint32_t)(uint8_t)span[io + bmap[b]] << (8 * i);
+          v |= (uint32_t)(uint8_t)span[io + bmap[b << qsh]] << (8 * i);
           if (++b == a.S) { b = 0; io += a.ext; }
         }
         w[k] = v;
       }
-      *reinterpret_cast<uint4 *>(a.packed + (p - a.offset)) = make_uint4(w[0], w[1], w[2], w[3]);
+      if (NT) {
+        const v4u_a16 x = {w[0], w[1], w[2], w[3]};
+        __builtin_nontemporal_store(x, reinterpret_cast<v4u_a16 *>(a.packed + (p - a.offset)));
+      } else {
+        *reinterpret_cast<uint4 *>(a.packed + (p - a.offset)) = make_uint4(w[0], w[1], w[2], w[3]);
+      }
     }
   };
   if (!PIPE) {
@@ -758,7 +806,7 @@ __global__ void __launch_bounds__(kCB) k_pack_bmap(BmapArgs a) {
         const char *g = reinterpret_cast<const char *>(s_lo[0]);
         uint4 *d = reinterpret_cast<uint4 *>(span);
         const uint32_t nv = (uint32_t)((s_hi[0] - s_lo[0]) / 16);
-        for (uint32_t i = threadIdx.x; i < nv; i += kCB) d[i] = gld16(g + 16 * (size_t)i);
+        for (uint32_t i = threadIdx.x; i < nv; i += kCB) d[i] = gld16p<NT>(g + 16 * (size_t)i);
       }
       __syncthreads();
       gather(t, s_lo[0]);
@@ -774,7 +822,7 @@ __global__ void __launch_bounds__(kCB) k_pack_bmap(BmapArgs a) {
     const char *g = reinterpret_cast<const char *>(s_lo[0]);
     uint4 *d = reinterpret_cast<uint4 *>(span);
     const uint32_t nv = (uint32_t)((s_hi[0] - s_lo[0]) / 16);
-    for (uint32_t i = threadIdx.x; i < nv; i += kCB) d[i] = gld16(g + 16 * (size_t)i);
+    for (uint32_t i = threadIdx.x; i < nv; i += kCB) d[i] = gld16p<NT>(g + 16 * (size_t)i);
   }
   int cur = 0;
   for (;;) {
@@ -788,7 +836,7 @@ __global__ void __launch_bounds__(kCB) k_pack_bmap(BmapArgs a) {
       const char *g = reinterpret_cast<const char *>(s_lo[cur ^ 1]);
 #pragma unroll
       for (int k = 0; k < kPre; k++)
-        if (threadIdx.x + k * kCB < nvn) pre[k] = gld16(g + 16 * (size_t)(threadIdx.x + k * kCB));
+        if (threadIdx.x + k * kCB < nvn) pre[k] = gld16p<NT>(g + 16 * (size_t)(threadIdx.x + k * kCB));
     }
     gather(t, s_lo[cur]);
     if (!has_next) break;
@@ -1592,6 +1640,9 @@ struct mx_ddt {
   int map16 = 0;
   int64_t umin = 0, uspan = 0;
   uint64_t bmap_T = 0;             // stream bytes per PACK tile (0: no PACK kernel)
+  uint64_t bmap_Ts[3] = {0, 0, 0}; // the same for staged spans kBmapSpans[0..2] (bmap_T = [1])
+  bool bmap_quad = false;          // the PACK kernel stages the map as quads (BmapArgs::qsh)
+  bool bmap_cw = false;            // >= 90 % of packed dwords are 4 user-contiguous bytes (BmapArgs::cw)
   bool piece_pack = false;         // PACK takes the piece kernel (wide word-aligned pieces, build_bmap)
   // piece tables per user-origin alignment (address mod 16), built on first
   // use: UNPACK kernel k_unpack_piece
@@ -1795,7 +1846,9 @@ static void build_bmap(mx_ddt *d) {
   d->bmap.swap(m);
   d->umin = lo;
   d->uspan = hi - lo;
-  d->map16 = d->uspan <= 65536;
+  // 16-bit map entries when every entry of the kernel's wrapped table
+  // (bmap + ext for the three bytes past an instance) fits
+  d->map16 = d->uspan + (int64_t)((S + 2) / S) * ext <= 65536;
   // PACK kernel choice: pieces of >= 8 bytes on average that all land on
   // whole packed words move with few wide accesses through the piece kernel;
   // narrow or misaligned pieces go through the byte map, whose cost per
@@ -1814,7 +1867,14 @@ static void build_bmap(mx_ddt *d) {
   // packed byte; a sparse one reads mostly gaps -- ref_matrix_borders at 23:
   // 0.83 -> 0.42 TB/s) and maps small enough for >= 3 workgroups per CU
   // (ref_upper_matrix_60's 29 KiB map: 1.32 -> 1.25 TB/s)
-  if (S * (d->map16 ? 2 : 4) > kBmapLds || ext > 4 * (int64_t)S || d->uspan > 4 * (int64_t)S) return;
+  if ((S + 3) * (d->map16 ? 2 : 4) > kBmapLds || ext > 4 * (int64_t)S || d->uspan > 4 * (int64_t)S) return;
+  d->bmap_quad = S % 4 != 0 && 4 * S * (d->map16 ? 2 : 4) <= kBmapLds;
+  {                                // packed dwords whose 4 bytes are user-contiguous, by instance phase
+    auto Ux = [&](uint64_t x) { return (int64_t)(x / S) * ext + d->bmap[x % S]; };
+    uint64_t c = 0;
+    for (uint64_t b = 0; b < S; b++) c += Ux(b + 3) == Ux(b) + 3 && Ux(b + 1) == Ux(b) + 1 && Ux(b + 2) == Ux(b) + 2;
+    d->bmap_cw = c * 10 >= 9 * S;
+  }
   // user bytes a tile of T stream bytes starting at instance byte b touches
   auto U = [&](uint64_t x) { return (int64_t)(x / S) * ext + d->bmap[x % S]; };
   auto worst = [&](uint64_t T) {
@@ -1823,9 +1883,20 @@ static void build_bmap(mx_ddt *d) {
     for (uint64_t b = 0; b < S; b++) w = std::max<int64_t>(w, U(b + T - 1) - U(b) + 1);
     return w;
   };
-  uint64_t T = 16384;
-  while (T >= 256 && worst(T) + 32 > kBmapSpan) T -= 256;
-  d->bmap_T = T >= 256 ? T : 0;
+  // the largest T (a multiple of 256, at most 2/3 of the span) whose worst
+  // user span + 160 fits: the span staged from a 128-byte line start
+  // (MX_CONV_BMAP_ALIGN) plus its 16-byte rounding up.  worst() grows with T.
+  for (int k = 0; k < 3; k++) {
+    const int64_t span = kBmapSpans[k];
+    uint64_t lo = 0, hi = (uint64_t)span * 2 / 3 / 256;      // in units of 256
+    while (lo < hi) {
+      const uint64_t mid = (lo + hi + 1) / 2;
+      if (worst(mid * 256) + 160 <= span) lo = mid;
+      else hi = mid - 1;
+    }
+    d->bmap_Ts[k] = lo * 256;
+  }
+  d->bmap_T = d->bmap_Ts[1];
 }
 
 // The piece table for a user origin at address `al` mod 16 (cut_pieces),
@@ -2225,6 +2296,61 @@ static bool conv_bmap_pipe() {
   return on != 0;
 }
 
+// MX_CONV_BMAP_ALIGN=16|128: the byte-map PACK stages a tile's user span
+// from its first 16-byte granule or from the start of that granule's
+// 128-byte line, so that a wave's 1 KiB loads cover whole lines
+static uint64_t conv_bmap_align() {
+  static const uint64_t v = [] {
+    const char *e = getenv("MX_CONV_BMAP_ALIGN");
+    return (uint64_t)((e && atoi(e) == 16) ? 16 : 128);
+  }();
+  return v;
+}
+
+// MX_CONV_BMAP_QUAD=0 stages the byte-map PACK's map as one row also where
+// S % 4 != 0 (A/B switch; results identical)
+static bool conv_bmap_quad() {
+  static const int on = [] {
+    const char *e = getenv("MX_CONV_BMAP_QUAD");
+    return (e && *e == '0') ? 0 : 1;
+  }();
+  return on != 0;
+}
+
+// MX_CONV_BMAP_CW=0: the byte-map PACK reads every packed byte on its own
+// also where whole waves of packed dwords are user-contiguous (A/B switch)
+static bool conv_bmap_cw() {
+  static const int on = [] {
+    const char *e = getenv("MX_CONV_BMAP_CW");
+    return (e && *e == '0') ? 0 : 1;
+  }();
+  return on != 0;
+}
+
+// MX_CONV_BMAP_NT=0: the byte-map PACK reads the user span and writes the
+// packed stream with ordinary accesses instead of non-temporal ones (A/B
+// switch).  The span is staged with one coalesced 16-byte load per lane, the
+// pattern whose floor is 1.23x faster non-temporal at 256 MiB
+// (tools/pack_floor_probe split-nt vs split-plain, profiles/r05/pack_floor_r5j.txt)
+static bool conv_bmap_nt() {
+  static const int on = [] {
+    const char *e = getenv("MX_CONV_BMAP_NT");
+    return (e && *e == '0') ? 0 : 1;
+  }();
+  return on != 0;
+}
+
+// MX_CONV_BMAP_SPAN=12288|24576|49152: user span the byte-map PACK stages
+// per tile (A/B switch; the tile's stream bytes follow from it)
+static int conv_bmap_span_idx() {
+  static const int v = [] {
+    const char *e = getenv("MX_CONV_BMAP_SPAN");
+    const long x = e ? atol(e) : kBmapSpan;
+    return x == kBmapSpans[0] ? 0 : x == kBmapSpans[2] ? 2 : 1;
+  }();
+  return v;
+}
+
 // MX_CONV_UNPACK_PIPE=1 runs the piece UNPACK kernel with the register
 // prefetch of the next tile's packed range (A/B switch, off: measured
 // slower; results are identical).
@@ -2409,25 +2535,48 @@ static int convert(const mx_ddt_t *d, size_t count, char *user, char *packed, si
       b.offset = offset;
       b.len = len;
       b.g0 = offset / 16;
-      b.T = d->bmap_T;
+      const bool dw = conv_bmap_dw(), nt = conv_bmap_nt(), pipe = conv_bmap_pipe();
+      int si = conv_bmap_span_idx();
+      const size_t map_lds = (d->bmap_quad && conv_bmap_quad() ? 4 * d->size : d->size + 3) * (d->map16 ? 2 : 4);
+      if (!d->bmap_Ts[si] || !(dw && nt && pipe) || kBmapSpans[si] + 32 + map_lds > 65536)
+        si = 1;                                       // other spans: the default kernel shape only
+      b.T = d->bmap_Ts[si];
       b.ntiles = ((offset + len + 15) / 16 * 16 - b.g0 * 16 + b.T - 1) / b.T;
-      const size_t lds = kBmapSpan + 32 + d->size * (d->map16 ? 2 : 4);
+      b.qsh = d->bmap_quad && conv_bmap_quad() ? 2 : 0;
+      b.cw = d->bmap_cw && conv_bmap_cw();
+      const size_t lds = kBmapSpans[si] + 32 + (b.qsh ? 4 * d->size : d->size + 3) * (d->map16 ? 2 : 4);
       const uint64_t per_cu = std::max<uint64_t>(1, std::min<uint64_t>(8, (160 * 1024) / lds));
       const uint64_t grid = std::min<uint64_t>(b.ntiles, (uint64_t)g_num_cus * per_cu);
       b.adv_b = (uint32_t)((kCB * 4) % d->size);
       b.adv_io = (int64_t)((kCB * 4) / d->size) * b.ext;
-      const bool dw = conv_bmap_dw();
+      b.lo_mask = conv_bmap_align() - 1;
       dm->last_path.store(4, std::memory_order_relaxed);
+      if (si != 1) {
+        if (d->map16) {
+          if (si == 0) hipLaunchKernelGGL((k_pack_bmap<kBmapSpans[0], uint16_t, true, true, true>), dim3((unsigned)grid), dim3(kCB), lds, s, b);
+          else hipLaunchKernelGGL((k_pack_bmap<kBmapSpans[2], uint16_t, true, true, true>), dim3((unsigned)grid), dim3(kCB), lds, s, b);
+        } else {
+          if (si == 0) hipLaunchKernelGGL((k_pack_bmap<kBmapSpans[0], uint32_t, true, true, true>), dim3((unsigned)grid), dim3(kCB), lds, s, b);
+          else hipLaunchKernelGGL((k_pack_bmap<kBmapSpans[2], uint32_t, true, true, true>), dim3((unsigned)grid), dim3(kCB), lds, s, b);
+        }
+        return mx_check_launch();
+      }
+#define MX_BMAP_LAUNCH2(M, DW, NT)                                                                               \
+  do {                                                                                                           \
+    if (pipe)                                                                                                    \
+      hipLaunchKernelGGL((k_pack_bmap<kBmapSpan, M, DW, true, NT>), dim3((unsigned)grid), dim3(kCB), lds, s, b); \
+    else                                                                                                         \
+      hipLaunchKernelGGL((k_pack_bmap<kBmapSpan, M, DW, false, NT>), dim3((unsigned)grid), dim3(kCB), lds, s, b);\
+  } while (0)
 #define MX_BMAP_LAUNCH(M, DW)                                                                                   \
   do {                                                                                                           \
-    if (conv_bmap_pipe())                                                                                        \
-      hipLaunchKernelGGL((k_pack_bmap<kBmapSpan, M, DW, true>), dim3((unsigned)grid), dim3(kCB), lds, s, b);     \
-    else                                                                                                         \
-      hipLaunchKernelGGL((k_pack_bmap<kBmapSpan, M, DW, false>), dim3((unsigned)grid), dim3(kCB), lds, s, b);    \
+    if (nt) MX_BMAP_LAUNCH2(M, DW, true);                                                                        \
+    else MX_BMAP_LAUNCH2(M, DW, false);                                                                          \
   } while (0)
       if (d->map16) { if (dw) MX_BMAP_LAUNCH(uint16_t, true); else MX_BMAP_LAUNCH(uint16_t, false); }
       else { if (dw) MX_BMAP_LAUNCH(uint32_t, true); else MX_BMAP_LAUNCH(uint32_t, false); }
 #undef MX_BMAP_LAUNCH
+#undef MX_BMAP_LAUNCH2
       return mx_check_launch();
     }
     if (!PACK || conv_ppack_enabled()) {

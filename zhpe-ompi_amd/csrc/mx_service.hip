@@ -58,6 +58,9 @@ constexpr size_t kSvcMaxBytes = 2 << 20;   // calls up to 2 MiB per buffer (larg
 constexpr size_t kSvcSoloBytes = 64 << 10; // up to 64 KiB workgroup 0 alone; above, the whole grid
 constexpr unsigned kSvcGridMax = 64;       // workgroups at most: 0 serves the host, the rest join large commands
 constexpr unsigned kSvcGrid = 32;          // (default)
+// MX_SVC_DIAG (measurement only, wrong results): bits above the helpers'
+// sleep select (16) no acquire, (32) no release, (64) no reduce per command
+constexpr int kSvcDiagNoAcq = 16, kSvcDiagNoRel = 32, kSvcDiagNoWork = 64;
 constexpr double kSvcIdleS = 100e-6;      // leave after 100 us without a command
 constexpr double kSvcLifeS = 1e-3;         // and between commands once 1 ms old (then relaunched)
 constexpr double kSvcStartUs = 1000;       // a kernel not running 1 ms after its launch is held
@@ -213,32 +216,40 @@ __global__ void __launch_bounds__(kSvcB) k_svc(const SvcCmd *cmd, SvcHost *host,
     for (uint64_t k = 1;; k++) {
       if (threadIdx.x == 0) {
         const uint64_t want = (epoch << 32) | k;
-        while (__hip_atomic_load(&bc->tag, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) != want) {
-          switch (hsleep) {                // s_sleep takes an immediate
+        // a relaxed poll: an acquire load is followed by an L2 invalidate
+        // (buffer_inv sc1) on every iteration, and 31 helpers polling that
+        // way dropped the lines of whatever else ran on their XCDs (a
+        // concurrent copy lost 33 % at 1 MiB calls, tools/svc_interference.py,
+        // profiles/r05/svc_interference_r5.txt).  One acquire once it matches.
+        while (__hip_atomic_load(&bc->tag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != want) {
+          switch (hsleep & 3) {                // s_sleep takes an immediate
             case 0: __builtin_amdgcn_s_sleep(8); break;
             case 1: __builtin_amdgcn_s_sleep(32); break;
             case 2: __builtin_amdgcn_s_sleep(64); break;
             default: __builtin_amdgcn_s_sleep(127); break;
           }
         }
+        // system scope: the broadcast's fields below, and no stale operand line
+        if (!(hsleep & kSvcDiagNoAcq)) __atomic_thread_fence(__ATOMIC_ACQUIRE);
         s_q = bc->q;
         s_in = bc->in;
         s_inout = bc->inout;
         s_in2 = bc->in2;
         s_count = bc->count;
         s_exit = bc->exit != 0;
-        __atomic_thread_fence(__ATOMIC_ACQUIRE);   // system scope: stale operand lines dropped
       }
       __syncthreads();
       if (s_exit) return;
-      svc_work<T, OP, OP3>(s_in, s_inout, s_in2, s_count, blockIdx.x, nwg);
+      if (!(hsleep & kSvcDiagNoWork)) svc_work<T, OP, OP3>(s_in, s_inout, s_in2, s_count, blockIdx.x, nwg);
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this wave's stores reached L2
       __syncthreads();
       if (threadIdx.x == 0) {
         // the ack first (workgroup 0 reads it before it may broadcast
         // again), then the release, then the host's flag
         __hip_atomic_store(acks + blockIdx.x, (epoch << 32) | k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        __threadfence_system();            // release: this XCD's L2 written back
+        // release only (system scope: this XCD's L2 written back); a seq_cst
+        // __threadfence_system also invalidates the XCD's L2 per call
+        if (!(hsleep & kSvcDiagNoRel)) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
         __hip_atomic_store(flags + blockIdx.x, (s_q << 12) | (uint64_t)(nwg - 1), __ATOMIC_RELAXED,
                            __HIP_MEMORY_SCOPE_SYSTEM);
       }
@@ -304,7 +315,7 @@ __global__ void __launch_bounds__(kSvcB) k_svc(const SvcCmd *cmd, SvcHost *host,
         }
         // system-scope acquire: stale operand lines dropped from this CU's
         // caches and its XCD's L2 (the service never passes a kernel boundary)
-        if (!s_exit) __atomic_thread_fence(__ATOMIC_ACQUIRE);
+        if (!s_exit && !(hsleep & kSvcDiagNoAcq)) __atomic_thread_fence(__ATOMIC_ACQUIRE);
       }
     }
     __syncthreads();
@@ -314,11 +325,11 @@ __global__ void __launch_bounds__(kSvcB) k_svc(const SvcCmd *cmd, SvcHost *host,
       return;
     }
     const bool bcast = s_bcast;
-    svc_work<T, OP, OP3>(s_in, s_inout, s_in2, s_count, 0, bcast ? nwg : 1);
+    if (!(hsleep & kSvcDiagNoWork)) svc_work<T, OP, OP3>(s_in, s_inout, s_in2, s_count, 0, bcast ? nwg : 1);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this wave's stores reached L2
     __syncthreads();
     if (threadIdx.x == 0) {
-      __threadfence_system();              // release: this XCD's L2 written back
+      if (!(hsleep & kSvcDiagNoRel)) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");   // release (system)
       if (bcast)
         __hip_atomic_store(flags, (s_q << 12) | (uint64_t)(nwg - 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
       else
@@ -363,6 +374,7 @@ struct Service {
   uint64_t *hrun = nullptr, *hrun_d = nullptr;     // helper w's launch epoch at start (mapped host memory)
   unsigned grid = kSvcGrid;
   uint64_t solo = kSvcSoloBytes;
+  uint64_t maxb = kSvcMaxBytes;   // calls served up to this many bytes per buffer
   int hsleep = 2;         // helpers' sleep between polls: 8 / 32 / 64 / 127 x 64 clocks
   uint64_t seq = 0;       // commands posted
   uint64_t epoch = 0;     // launches
@@ -496,8 +508,10 @@ int svc_setup(Service &v) {
     const long g = atol(e);
     v.grid = g < 1 ? 1 : g > (long)kSvcGridMax ? kSvcGridMax : (unsigned)g;
   }
-  if (const char *e = getenv("MX_SVC_HSLEEP")) v.hsleep = atoi(e);
+  if (const char *e = getenv("MX_SVC_HSLEEP")) v.hsleep = atoi(e) & 3;
+  if (const char *e = getenv("MX_SVC_DIAG")) v.hsleep |= (atoi(e) & 7) << 4;
   if (const char *e = getenv("MX_SVC_SOLO")) v.solo = (uint64_t)atoll(e);
+  if (const char *e = getenv("MX_SVC_MAX")) v.maxb = std::min<uint64_t>((uint64_t)atoll(e), kSvcMaxBytes);
   atexit(svc_atexit);
   return 1;
 }
@@ -580,7 +594,7 @@ int svc_reduce(int op, int type, const void *in, const void *in2, void *inout, s
   Service &v = g_svc;
   std::lock_guard<std::mutex> lk(v.mu);
   if (v.state == 0) v.state = svc_setup(v);
-  if (v.state != 1) return 0;
+  if (v.state != 1 || count * es > v.maxb) return 0;
   int dev = -1;                               // a caller on another device launches there
   if (hipGetDevice(&dev) != hipSuccess || dev != v.device) return 0;
   if (v.pending) {
