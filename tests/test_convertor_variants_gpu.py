@@ -1,0 +1,71 @@
+"""The byte-map PACK kernel's shapes other than each type's default
+(csrc/mx_convertor.hip k_pack_bmap): every A/B switch selects
+a different kernel or a different gather inside it, and each must give the
+reference walk's bytes (opal_datatype_pack.c:235-370, restated by the
+oracle).  One child process per switch (the switches are read once per
+process); in each, the struct / indexed / BLACS / "strange" types at ~4 MiB
+packed, user pointer aligned and shifted by 3 bytes, whole and as a window
+starting inside an element."""
+import os
+import subprocess
+import sys
+
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+CHILD = r"""
+import sys, numpy as np, torch
+sys.path.insert(0, sys.argv[1] + "/zhpe-ompi_amd"); sys.path.insert(0, sys.argv[1] + "/tests")
+import ctypes, golden_io, mxompi, oracle_lib
+vp, sz, ci, i64 = ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int, ctypes.c_int64
+basic, recs = golden_io.ddt_records()
+B = np.ascontiguousarray(basic)
+O = oracle_lib.oracle()
+O.mxo_ddt_convert.argtypes = [vp, sz, vp, i64, i64, sz, vp, vp, ci]
+mxompi.init(0)
+bad = []
+for name in ["struct_char_d3_int_resized48", "indexed_f32_random", "ref_blacs_indexed", "ref_strange"]:
+    rec = next(r for r in recs if r["name"] == name)
+    dt = mxompi.Datatype(rec["desc"].tobytes(), rec["nrec"], rec["size"], rec["lb"], rec["ub"])
+    count = (4 << 20) // rec["size"] + 7
+    nb = count * rec["size"]
+    ext = rec["ub"] - rec["lb"]
+    span = ext * (count - 1) + rec["true_ub"] - rec["true_lb"]
+    user = np.random.default_rng(11).integers(0, 256, span, dtype=np.uint8)
+    exp = np.zeros(nb, np.uint8)
+    O.mxo_ddt_convert(rec["desc"].ctypes.data, rec["nrec"], B.ctypes.data, rec["lb"], rec["ub"], count,
+                      user.ctypes.data - rec["true_lb"], exp.ctypes.data, 0)
+    st = torch.cuda.current_stream().cuda_stream
+    for shift in (0, 3):
+        U = torch.zeros(span + 16, dtype=torch.uint8, device="cuda")
+        U[shift:shift + span] = torch.from_numpy(user).cuda()
+        base = U.data_ptr() + shift - rec["true_lb"]
+        P = torch.zeros(nb, dtype=torch.uint8, device="cuda")
+        dt.pack(count, base, P.data_ptr(), stream=st)
+        # a window starting inside an element, its bytes at their stream
+        # positions (packed - offset 16-aligned: the byte-map kernel's case)
+        off, ln = nb // 3 + 5, nb // 2 + 3
+        W = torch.zeros(nb, dtype=torch.uint8, device="cuda")
+        dt.pack(count, base, W.data_ptr() + off, offset=off, length=ln, stream=st)
+        torch.cuda.synchronize()
+        if not np.array_equal(P.cpu().numpy(), exp):
+            bad.append((name, shift, "whole"))
+        w = W.cpu().numpy()
+        if not (np.array_equal(w[off:off + ln], exp[off:off + ln]) and not w[:off].any() and not w[off + ln:].any()):
+            bad.append((name, shift, "window"))
+print("BAD", bad)
+sys.exit(1 if bad else 0)
+"""
+
+
+@pytest.mark.parametrize("env", ["MX_CONV_BMAP_SPAN=12288", "MX_CONV_BMAP_SPAN=24576", "MX_CONV_BMAP_UNROLL=0",
+                                 "MX_CONV_BMAP_QUAD=0", "MX_CONV_BMAP_WORD=0", "MX_CONV_BMAP_NT=0",
+                                 "MX_CONV_BMAP_DW=0", "MX_CONV_BMAP_CW=0"])
+def test_byte_map_pack_switches(env):
+    k, v = env.split("=")
+    e = dict(os.environ, **{k: v})
+    p = subprocess.run([sys.executable, "-c", CHILD, ROOT], capture_output=True, text=True, env=e, timeout=240)
+    assert p.returncode == 0, (env, p.stdout[-2000:], p.stderr[-3000:])

@@ -661,7 +661,10 @@ struct BmapArgs {
   uint64_t lo_mask;        // a tile's staged span starts at lo & ~lo_mask (15, or 127: whole lines)
   uint32_t qsh;            // 2: the map is staged as quads (entry b at [4b], its dword's bytes at [4b..4b+3])
   uint32_t cw;             // try one LDS dword read per packed dword (word-piece layouts)
+  uint32_t unroll;         // kBmapU dwords per lane per step in the DW gather
+  uint32_t word;           // word map: entries 4k only (S % 4 == 0, every packed dword user-contiguous)
 };
+constexpr int kBmapU = 4;
 
 // M = uint16_t when the instance's user span is below 64 KiB, else uint32_t.
 // PIPE (round 3): persistent workgroups keep the NEXT tile's user span in
@@ -669,7 +672,9 @@ struct BmapArgs {
 // gather the current tile out of LDS -- without it every tile's span load
 // and gather run back to back inside the workgroup.
 template <int SPAN, class M, bool DW, bool PIPE, bool NT>
-__global__ void __launch_bounds__(kCB) k_pack_bmap(BmapArgs a) {
+// waves per SIMD the LDS allows (workgroups per CU: 6 at a 24 KiB span), so
+// the register budget never lowers the occupancy below it
+__global__ void __launch_bounds__(kCB, SPAN >= 49152 ? 3 : SPAN >= 24576 ? 6 : 7) k_pack_bmap(BmapArgs a) {
   extern __shared__ __align__(16) char smem[];
   char *span = smem;                                         // SPAN + 32
   // The map in LDS, entry x = user offset of packed byte x (x >= S: of the
@@ -682,16 +687,25 @@ __global__ void __launch_bounds__(kCB) k_pack_bmap(BmapArgs a) {
   //          stalled the struct type's gather: SQ_WAIT_INST_LDS 388M vs 23M,
   //          profiles/r05/pmc_pack_r5j.jsonl).
   // bmap[x << qsh] is entry x either way.
+  //   word (S % 4 == 0, every packed dword 4 user-contiguous bytes: word
+  //          pieces): only entries 4k are staged, [k] = entry 4k, and entry
+  //          x = [x >> 2] + (x & 3) -- a quarter of the LDS (indexed's 10 KiB
+  //          map: 2.6 KiB, so the 24 KiB span keeps five workgroups per CU)
+  //          and one byte-map read + one dword read per packed dword.
   M *bmap = reinterpret_cast<M *>(smem + SPAN + 32);
   __shared__ uintptr_t s_lo[2], s_hi[2];
   constexpr int kPre = SPAN / 16 / kCB;
   const uint32_t qsh = a.qsh;
-  const uint32_t nent = qsh ? 4 * a.S : a.S + 3;
+  const bool word = a.word != 0;
+  const uint32_t nent = word ? a.S / 4 : qsh ? 4 * a.S : a.S + 3;
   for (uint32_t i = threadIdx.x; i < nent; i += kCB) {
-    const uint32_t x = qsh ? (i >> 2) + (i & 3) : i;
+    const uint32_t x = word ? 4 * i : qsh ? (i >> 2) + (i & 3) : i;
     const uint32_t k = x / a.S;
     bmap[i] = (M)(reinterpret_cast<const M *>(a.map)[x - k * a.S] + k * (uint32_t)a.ext);
   }
+  auto ent = [&](uint64_t x) -> int64_t {                    // entry x < S
+    return word ? (int64_t)bmap[x >> 2] + (int64_t)(x & 3) : (int64_t)bmap[x << qsh];
+  };
   const uint64_t wend = a.offset + a.len;
   // tile t: absolute stream bytes [s0, s1) (window-clipped from sa), instances ia..ib
   auto geom = [&](uint64_t t, uint64_t &s0, uint64_t &sa, uint64_t &s1, uint64_t &ia, uint64_t &ib) {
@@ -708,8 +722,8 @@ __global__ void __launch_bounds__(kCB) k_pack_bmap(BmapArgs a) {
     const uintptr_t ubase = (uintptr_t)a.user + (int64_t)ia * a.ext + a.umin;
     uintptr_t lo = ubase, hi = ubase + (int64_t)(ib - ia) * a.ext + a.uspan;
     if (a.mono) {
-      lo = ubase + bmap[(sa - ia * a.S) << qsh];
-      hi = ubase + (int64_t)(ib - ia) * a.ext + bmap[(s1 - 1 - ib * a.S) << qsh] + 1;
+      lo = ubase + ent(sa - ia * a.S);
+      hi = ubase + (int64_t)(ib - ia) * a.ext + ent(s1 - 1 - ib * a.S) + 1;
     }
     s_lo[slot] = lo & ~(uintptr_t)a.lo_mask;
     s_hi[slot] = (hi + 15) & ~(uintptr_t)15;
@@ -738,8 +752,80 @@ __global__ void __launch_bounds__(kCB) k_pack_bmap(BmapArgs a) {
       uint32_t b = (uint32_t)(p0 - inst * a.S);
       int32_t io = (int32_t)((int64_t)(inst - ia) * a.ext + d0);
       const int32_t adv_io = (int32_t)a.adv_io, ext = (int32_t)a.ext;
-      for (uint32_t j = threadIdx.x; j < nq; j += kCB) {
-        if (j >= jlo && j < jhi) {
+      uint32_t j = threadIdx.x;
+      if (a.unroll) {
+        // kBmapU dwords per lane per step (j, j + kCB, ...), all inside the
+        // window: their map reads, then their byte reads, are independent and
+        // in flight together (one dword per step waits out two LDS round
+        // trips back to back)
+        for (; j >= jlo && j + (kBmapU - 1) * kCB < jhi; j += kBmapU * kCB) {
+          uint32_t bu[kBmapU];
+          int32_t iu[kBmapU];
+          bu[0] = b;
+          iu[0] = io;
+#pragma unroll
+          for (int u = 1; u < kBmapU; u++) {
+            uint32_t nb = bu[u - 1] + a.adv_b;
+            int32_t ni = iu[u - 1] + adv_io;
+            if (nb >= a.S) { nb -= a.S; ni += ext; }
+            bu[u] = nb;
+            iu[u] = ni;
+          }
+          uint32_t v[kBmapU];
+          if (word) {                                         // b % 4 == 0 here (S % 4 == 0)
+            int32_t w[kBmapU];
+#pragma unroll
+            for (int u = 0; u < kBmapU; u++) w[u] = bmap[bu[u] >> 2];
+#pragma unroll
+            for (int u = 0; u < kBmapU; u++) v[u] = *reinterpret_cast<const uint32_t *>(span + iu[u] + w[u]);
+#pragma unroll
+            for (int u = 0; u < kBmapU; u++) {
+              uint32_t *q = reinterpret_cast<uint32_t *>(pk + 4 * (j + u * kCB));
+              if (NT) __builtin_nontemporal_store(v[u], q);
+              else *q = v[u];
+            }
+            b = bu[kBmapU - 1] + a.adv_b;
+            io = iu[kBmapU - 1] + adv_io;
+            if (b >= a.S) { b -= a.S; io += ext; }
+            continue;
+          }
+          int32_t e[kBmapU][4];
+#pragma unroll
+          for (int u = 0; u < kBmapU; u++) {
+            const M *m = bmap + (bu[u] << qsh);
+#pragma unroll
+            for (int k = 0; k < 4; k++) e[u][k] = m[k];
+          }
+          bool cont = a.cw != 0;
+#pragma unroll
+          for (int u = 0; u < kBmapU; u++)
+            cont = cont && (e[u][1] == e[u][0] + 1) & (e[u][2] == e[u][0] + 2) & (e[u][3] == e[u][0] + 3);
+          if (a.cw && __all(cont)) {
+#pragma unroll
+            for (int u = 0; u < kBmapU; u++) v[u] = *reinterpret_cast<const uint32_t *>(span + iu[u] + e[u][0]);
+          } else {
+#pragma unroll
+            for (int u = 0; u < kBmapU; u++)
+              v[u] = (uint32_t)(uint8_t)span[iu[u] + e[u][0]] | (uint32_t)(uint8_t)span[iu[u] + e[u][1]] << 8 |
+                     (uint32_t)(uint8_t)span[iu[u] + e[u][2]] << 16 | (uint32_t)(uint8_t)span[iu[u] + e[u][3]] << 24;
+          }
+#pragma unroll
+          for (int u = 0; u < kBmapU; u++) {
+            uint32_t *q = reinterpret_cast<uint32_t *>(pk + 4 * (j + u * kCB));
+            if (NT) __builtin_nontemporal_store(v[u], q);
+            else *q = v[u];
+          }
+          b = bu[kBmapU - 1] + a.adv_b;
+          io = iu[kBmapU - 1] + adv_io;
+          if (b >= a.S) { b -= a.S; io += ext; }
+        }
+      }
+      for (; j < nq; j += kCB) {
+        if (j >= jlo && j < jhi && word) {
+          const uint32_t v = *reinterpret_cast<const uint32_t *>(span + io + (int32_t)bmap[b >> 2]);
+          if (NT) __builtin_nontemporal_store(v, reinterpret_cast<uint32_t *>(pk + 4 * j));
+          else *reinterpret_cast<uint32_t *>(pk + 4 * j) = v;
+        } else if (j >= jlo && j < jhi) {
           const M *m = bmap + (b << qsh);
           const int32_t e0 = m[0], e1 = m[1], e2 = m[2], e3 = m[3];
           uint32_t v;
@@ -757,7 +843,7 @@ __global__ void __launch_bounds__(kCB) k_pack_bmap(BmapArgs a) {
           const uint64_t p = s0 + 4 * (uint64_t)j;
           for (uint64_t x = p < a.offset ? a.offset : p; x < p + 4 && x < wend; x++) {
             const uint64_t i = udiv(x, a.mS);
-            a.packed[x - a.offset] = span[(int64_t)(i - ia) * a.ext + d0 + bmap[(x - i * a.S) << qsh]];
+            a.packed[x - a.offset] = span[(int64_t)(i - ia) * a.ext + d0 + ent(x - i * a.S)];
           }
         }
         b += a.adv_b;                                         // next: kCB dwords further
@@ -771,7 +857,7 @@ __global__ void __launch_bounds__(kCB) k_pack_bmap(BmapArgs a) {
       if (p < a.offset || p + 16 > wend) {                    // window edge: the bytes inside only
         for (uint64_t q = p < a.offset ? a.offset : p; q < p + 16 && q < wend; q++) {
           const uint64_t i = udiv(q, a.mS);
-          a.packed[q - a.offset] = span[(int64_t)(i - ia) * a.ext + d0 + bmap[(q - i * a.S) << qsh]];
+          a.packed[q - a.offset] = span[(int64_t)(i - ia) * a.ext + d0 + ent(q - i * a.S)];
         }
         continue;
       }
@@ -784,7 +870,7 @@ __global__ void __launch_bounds__(kCB) k_pack_bmap(BmapArgs a) {
         uint32_t v = 0;
 #pragma unroll
         for (int i = 0; i < 4; i++) {
-          v |= (uint32_t)(uint8_t)span[io + bmap[b << qsh]] << (8 * i);
+          v |= (uint32_t)(uint8_t)span[io + ent(b)] << (8 * i);
           if (++b == a.S) { b = 0; io += a.ext; }
         }
         w[k] = v;
@@ -1643,6 +1729,7 @@ struct mx_ddt {
   uint64_t bmap_Ts[3] = {0, 0, 0}; // the same for staged spans kBmapSpans[0..2] (bmap_T = [1])
   bool bmap_quad = false;          // the PACK kernel stages the map as quads (BmapArgs::qsh)
   bool bmap_cw = false;            // >= 90 % of packed dwords are 4 user-contiguous bytes (BmapArgs::cw)
+  bool bmap_word = false;          // every dword at a phase 4k is (BmapArgs::word)
   bool piece_pack = false;         // PACK takes the piece kernel (wide word-aligned pieces, build_bmap)
   // piece tables per user-origin alignment (address mod 16), built on first
   // use: UNPACK kernel k_unpack_piece
@@ -1874,6 +1961,10 @@ static void build_bmap(mx_ddt *d) {
     uint64_t c = 0;
     for (uint64_t b = 0; b < S; b++) c += Ux(b + 3) == Ux(b) + 3 && Ux(b + 1) == Ux(b) + 1 && Ux(b + 2) == Ux(b) + 2;
     d->bmap_cw = c * 10 >= 9 * S;
+    uint64_t cwd = 0;                // at the phases a dword of a 16-aligned tile starts at
+    for (uint64_t b = 0; b < S; b += 4)
+      cwd += Ux(b + 3) == Ux(b) + 3 && Ux(b + 1) == Ux(b) + 1 && Ux(b + 2) == Ux(b) + 2;
+    d->bmap_word = S % 4 == 0 && cwd == S / 4;
   }
   // user bytes a tile of T stream bytes starting at instance byte b touches
   auto U = [&](uint64_t x) { return (int64_t)(x / S) * ext + d->bmap[x % S]; };
@@ -2340,12 +2431,34 @@ static bool conv_bmap_nt() {
   return on != 0;
 }
 
+// MX_CONV_BMAP_WORD=0: the byte-map PACK stages the whole byte map also for
+// word-piece layouts (A/B switch)
+static bool conv_bmap_word() {
+  static const int on = [] {
+    const char *e = getenv("MX_CONV_BMAP_WORD");
+    return (e && *e == '0') ? 0 : 1;
+  }();
+  return on != 0;
+}
+
+// MX_CONV_BMAP_UNROLL=0: one packed dword per lane per step in the byte-map
+// PACK's gather instead of kBmapU (A/B switch)
+static bool conv_bmap_unroll() {
+  static const int on = [] {
+    const char *e = getenv("MX_CONV_BMAP_UNROLL");
+    return (e && *e == '0') ? 0 : 1;
+  }();
+  return on != 0;
+}
+
 // MX_CONV_BMAP_SPAN=12288|24576|49152: user span the byte-map PACK stages
-// per tile (A/B switch; the tile's stream bytes follow from it)
+// per tile (A/B switch; the tile's stream bytes follow from it; unset: 24 KiB
+// where five workgroups fit a CU, else 12 KiB)
 static int conv_bmap_span_idx() {
   static const int v = [] {
     const char *e = getenv("MX_CONV_BMAP_SPAN");
-    const long x = e ? atol(e) : kBmapSpan;
+    if (!e) return -1;                                   // by the map's size
+    const long x = atol(e);
     return x == kBmapSpans[0] ? 0 : x == kBmapSpans[2] ? 2 : 1;
   }();
   return v;
@@ -2537,14 +2650,24 @@ static int convert(const mx_ddt_t *d, size_t count, char *user, char *packed, si
       b.g0 = offset / 16;
       const bool dw = conv_bmap_dw(), nt = conv_bmap_nt(), pipe = conv_bmap_pipe();
       int si = conv_bmap_span_idx();
-      const size_t map_lds = (d->bmap_quad && conv_bmap_quad() ? 4 * d->size : d->size + 3) * (d->map16 ? 2 : 4);
+      const bool word = d->bmap_word && conv_bmap_word() && dw;
+      const size_t map_lds = (word ? d->size / 4 : d->bmap_quad && conv_bmap_quad() ? 4 * d->size : d->size + 3) *
+                             (d->map16 ? 2 : 4);
+      // default: the 24 KiB span where five or more workgroups fit a CU (a
+      // small map), else 12 KiB, which keeps seven (indexed's 10 KiB map: four
+      // at 24 KiB).  On one box against the floors (profiles/r05/conv_ab_r5q.txt,
+      // pack_floor_r5q.txt), 256 MiB: struct 24 KiB 123 us / 12 KiB 159 /
+      // 48 KiB 157 (floor 125); indexed 123 / 116 / 180 (floor 109)
+      if (si < 0) si = (160 * 1024) / (kBmapSpans[1] + 32 + map_lds + 128) >= 5 ? 1 : 0;
       if (!d->bmap_Ts[si] || !(dw && nt && pipe) || kBmapSpans[si] + 32 + map_lds > 65536)
         si = 1;                                       // other spans: the default kernel shape only
       b.T = d->bmap_Ts[si];
       b.ntiles = ((offset + len + 15) / 16 * 16 - b.g0 * 16 + b.T - 1) / b.T;
-      b.qsh = d->bmap_quad && conv_bmap_quad() ? 2 : 0;
+      b.word = word;
+      b.qsh = !word && d->bmap_quad && conv_bmap_quad() ? 2 : 0;
       b.cw = d->bmap_cw && conv_bmap_cw();
-      const size_t lds = kBmapSpans[si] + 32 + (b.qsh ? 4 * d->size : d->size + 3) * (d->map16 ? 2 : 4);
+      b.unroll = conv_bmap_unroll();
+      const size_t lds = kBmapSpans[si] + 32 + map_lds;
       const uint64_t per_cu = std::max<uint64_t>(1, std::min<uint64_t>(8, (160 * 1024) / lds));
       const uint64_t grid = std::min<uint64_t>(b.ntiles, (uint64_t)g_num_cus * per_cu);
       b.adv_b = (uint32_t)((kCB * 4) % d->size);
