@@ -62,7 +62,7 @@ sys.exit(1 if bad else 0)
 
 
 @pytest.mark.parametrize("env", ["MX_CONV_BMAP_SPAN=12288", "MX_CONV_BMAP_SPAN=24576", "MX_CONV_BMAP_UNROLL=0",
-                                 "MX_CONV_BMAP_QUAD=0", "MX_CONV_BMAP_WORD=0", "MX_CONV_BMAP_NT=0",
+                                 "MX_CONV_BMAP_QUAD=0", "MX_CONV_BMAP_WORD=1", "MX_CONV_BMAP_NT=0",
                                  "MX_CONV_BMAP_DW=0", "MX_CONV_BMAP_CW=0"])
 def test_byte_map_pack_switches(env):
     k, v = env.split("=")

@@ -5,7 +5,7 @@ cd "$GRAFT_REPO_ROOT"
 export TMPDIR=/tmp HSA_ENABLE_IPC_MODE_LEGACY=0
 O=gpurun_out
 mkdir -p $O
-STEP_TIMEOUT=400 bash tools/gpu_pytest.sh r5r_conv "tests/test_convertor.py tests/test_convertor_pins.py tests/test_convertor_hook_gpu.py -m gpu" || exit $?
+STEP_TIMEOUT=500 bash tools/gpu_pytest.sh r5r_conv "tests/test_convertor.py tests/test_convertor_pins.py tests/test_convertor_hook_gpu.py tests/test_convertor_variants_gpu.py -m gpu --durations=10" || exit $?
 T="vector_f32_b1_s2 vector_f32_b4_s8 vector_f64_b3_s5 vector_f32_b16_s32 vector_f32_b64_s128 indexed_f32_random struct_char_d3_int_resized48 ref_blacs_indexed ref_struct ref_strange"
 for rep in 1 2; do
   echo "== default (rep $rep)" >> $O/conv_r5r.txt

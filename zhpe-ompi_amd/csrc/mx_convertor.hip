@@ -2431,12 +2431,14 @@ static bool conv_bmap_nt() {
   return on != 0;
 }
 
-// MX_CONV_BMAP_WORD=0: the byte-map PACK stages the whole byte map also for
-// word-piece layouts (A/B switch)
+// MX_CONV_BMAP_WORD=1: the byte-map PACK stages a word map for word-piece
+// layouts (A/B switch, off: indexed 112 -> 137 us at 256 MiB with it, BLACS
+// equal, profiles/r05/conv_r5r.txt -- the gather gets shorter and the tile's
+// span prefetch, which it hid, is waited for instead)
 static bool conv_bmap_word() {
   static const int on = [] {
     const char *e = getenv("MX_CONV_BMAP_WORD");
-    return (e && *e == '0') ? 0 : 1;
+    return (e && *e == '1') ? 1 : 0;
   }();
   return on != 0;
 }
