@@ -1,4 +1,4 @@
-"""The byte-map PACK kernel's shapes other than each type's default
+"""The PACK kernels' shapes other than each type's default
 (csrc/mx_convertor.hip k_pack_bmap): every A/B switch selects
 a different kernel or a different gather inside it, and each must give the
 reference walk's bytes (opal_datatype_pack.c:235-370, restated by the
@@ -27,7 +27,7 @@ O = oracle_lib.oracle()
 O.mxo_ddt_convert.argtypes = [vp, sz, vp, i64, i64, sz, vp, vp, ci]
 mxompi.init(0)
 bad = []
-for name in ["struct_char_d3_int_resized48", "indexed_f32_random", "ref_blacs_indexed", "ref_strange"]:
+for name in sys.argv[2].split(","):
     rec = next(r for r in recs if r["name"] == name)
     dt = mxompi.Datatype(rec["desc"].tobytes(), rec["nrec"], rec["size"], rec["lb"], rec["ub"])
     count = (4 << 20) // rec["size"] + 7
@@ -61,11 +61,30 @@ sys.exit(1 if bad else 0)
 """
 
 
+BMAP_TYPES = "struct_char_d3_int_resized48,indexed_f32_random,ref_blacs_indexed,ref_strange"
+VEC_TYPES = "vector_f32_b1_s2,vector_f64_b3_s5,vector_f32_b4_s8"
+
+
+def _run(env, types):
+    e = dict(os.environ)
+    for kv in env.split():
+        k, v = kv.split("=")
+        e[k] = v
+    p = subprocess.run([sys.executable, "-c", CHILD, ROOT, types], capture_output=True, text=True, env=e,
+                       timeout=240)
+    assert p.returncode == 0, (env, p.stdout[-2000:], p.stderr[-3000:])
+
+
 @pytest.mark.parametrize("env", ["MX_CONV_BMAP_SPAN=12288", "MX_CONV_BMAP_SPAN=24576", "MX_CONV_BMAP_UNROLL=0",
                                  "MX_CONV_BMAP_QUAD=0", "MX_CONV_BMAP_WORD=1", "MX_CONV_BMAP_NT=0",
                                  "MX_CONV_BMAP_DW=0", "MX_CONV_BMAP_CW=0"])
 def test_byte_map_pack_switches(env):
-    k, v = env.split("=")
-    e = dict(os.environ, **{k: v})
-    p = subprocess.run([sys.executable, "-c", CHILD, ROOT], capture_output=True, text=True, env=e, timeout=240)
-    assert p.returncode == 0, (env, p.stdout[-2000:], p.stderr[-3000:])
+    _run(env, BMAP_TYPES)
+
+
+@pytest.mark.parametrize("env", ["MX_NT_MIN_BYTES=0", "MX_CONV_VEC_NT=0 MX_NT_MIN_BYTES=0"])
+def test_vec_pack_nontemporal(env):
+    """The VEC and VEC-span PACK kernels' non-temporal instances (taken from
+    MX_NT_MIN_BYTES of span + stream on; forced here at 4 MiB) and their
+    ordinary ones."""
+    _run(env, VEC_TYPES)

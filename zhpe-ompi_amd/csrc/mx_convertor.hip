@@ -27,6 +27,7 @@
 #include <atomic>
 
 #include "mx_internal.h"
+#include "mx_mem.hpp"
 #include "../../include/mx_convertor.h"
 
 namespace mx {
@@ -235,7 +236,7 @@ __global__ void __launch_bounds__(kCB) k_convert(ConvArgs a) {
 constexpr int kVIt = 8;
 constexpr uint64_t kVecMaxBlen = (uint64_t)1 << 22;   // keeps t / blen exact in fp32 + 1 correction
 
-template <int W, bool PACK>
+template <int W, bool PACK, bool NT = false>
 __global__ void __launch_bounds__(kCB) k_convert_vec(ConvArgs a, DRun R, float rblen) {
   using U = typename unit_t<W>::T;
   const uint64_t nw = a.len / W;
@@ -266,14 +267,16 @@ __global__ void __launch_bounds__(kCB) k_convert_vec(ConvArgs a, DRun R, float r
         l1 -= d * R.cnt1;
       }
       ua[k] = reinterpret_cast<U *>(a.user + (int64_t)inst * a.ext + R.disp + (int64_t)l1 * R.stride1 + r);
-      v[k] = PACK ? *ua[k] : reinterpret_cast<const U *>(a.packed)[wbase + rel];
+      if (PACK && NT) v[k] = __builtin_nontemporal_load(ua[k]);
+      else v[k] = PACK ? *ua[k] : reinterpret_cast<const U *>(a.packed)[wbase + rel];
     }
   }
 #pragma unroll
   for (int k = 0; k < kVIt; k++) {
     const uint32_t rel = (uint32_t)(k * kCB + threadIdx.x);
     if (wbase + rel < nw) {
-      if (PACK) reinterpret_cast<U *>(a.packed)[wbase + rel] = v[k];
+      if (PACK && NT) __builtin_nontemporal_store(v[k], reinterpret_cast<U *>(a.packed) + wbase + rel);
+      else if (PACK) reinterpret_cast<U *>(a.packed)[wbase + rel] = v[k];
       else *ua[k] = v[k];
     }
   }
@@ -288,7 +291,7 @@ __global__ void __launch_bounds__(kCB) k_convert_vec(ConvArgs a, DRun R, float r
 // contiguous bytes).  The run-walking VEC kernel reads the same lines as
 // one 4-byte word per lane at the stride (twice the load instructions for
 // 4-byte blocks every 8 bytes).
-template <int STRIDE, int BLEN>
+template <int STRIDE, int BLEN, bool NT = false>
 __global__ void __launch_bounds__(kCB) k_pack_vec_span(const char *ubase, char *packed, uint64_t offset,
                                                        uint64_t len, uint64_t q0, uint64_t q1) {
   constexpr int M = 16 / STRIDE, OUT = M * BLEN;
@@ -296,7 +299,7 @@ __global__ void __launch_bounds__(kCB) k_pack_vec_span(const char *ubase, char *
                 "periodic small blocks");
   const uint64_t q = q0 + (uint64_t)blockIdx.x * kCB + threadIdx.x;
   if (q >= q1) return;
-  const uint4 v = gld16(ubase + 16 * q);
+  const uint4 v = gld16p<NT>(ubase + 16 * q);
   const uint32_t d[4] = {v.x, v.y, v.z, v.w};
   uint8_t o[OUT];
 #pragma unroll
@@ -313,12 +316,14 @@ __global__ void __launch_bounds__(kCB) k_pack_vec_span(const char *ubase, char *
       uint32_t w0 = 0, w1 = 0;
 #pragma unroll
       for (int i = 0; i < 4; i++) { w0 |= (uint32_t)o[i] << (8 * i); w1 |= (uint32_t)o[4 + i] << (8 * i); }
-      *reinterpret_cast<uint2 *>(dst) = make_uint2(w0, w1);
+      if constexpr (NT) __builtin_nontemporal_store((uint64_t)w0 | (uint64_t)w1 << 32, reinterpret_cast<uint64_t *>(dst));
+      else *reinterpret_cast<uint2 *>(dst) = make_uint2(w0, w1);
     } else if constexpr (OUT == 4) {
       uint32_t w0 = 0;
 #pragma unroll
       for (int i = 0; i < 4; i++) w0 |= (uint32_t)o[i] << (8 * i);
-      *reinterpret_cast<uint32_t *>(dst) = w0;
+      if constexpr (NT) __builtin_nontemporal_store(w0, reinterpret_cast<uint32_t *>(dst));
+      else *reinterpret_cast<uint32_t *>(dst) = w0;
     } else {
 #pragma unroll
       for (int i = 0; i < OUT; i++) dst[i] = (char)o[i];
@@ -2431,6 +2436,16 @@ static bool conv_bmap_nt() {
   return on != 0;
 }
 
+// MX_CONV_VEC_NT=0: the VEC and VEC-span PACK kernels keep ordinary accesses
+// at the streaming sizes too (A/B switch)
+static bool conv_vec_nt() {
+  static const int on = [] {
+    const char *e = getenv("MX_CONV_VEC_NT");
+    return (e && *e == '0') ? 0 : 1;
+  }();
+  return on != 0;
+}
+
 // MX_CONV_BMAP_WORD=1: the byte-map PACK stages a word map for word-piece
 // layouts (A/B switch, off: indexed 112 -> 137 us at 256 MiB with it, BLACS
 // equal, profiles/r05/conv_r5r.txt -- the gather gets shorter and the tile's
@@ -2563,9 +2578,17 @@ static int convert(const mx_ddt_t *d, size_t count, char *user, char *packed, si
       const uint64_t nq = q1 - q0;
       const dim3 grid((unsigned)((nq + kCB - 1) / kCB)), block(kCB);
       dm->last_path.store(2, std::memory_order_relaxed);
-      if (st == 8) hipLaunchKernelGGL((k_pack_vec_span<8, 4>), grid, block, 0, s, ub, packed, offset, len, q0, q1);
-      else if (R.blen == 8) hipLaunchKernelGGL((k_pack_vec_span<16, 8>), grid, block, 0, s, ub, packed, offset, len, q0, q1);
-      else hipLaunchKernelGGL((k_pack_vec_span<16, 4>), grid, block, 0, s, ub, packed, offset, len, q0, q1);
+      // non-temporal at the streaming sizes (span + stream >= MX_NT_MIN_BYTES)
+      const bool nt = conv_vec_nt() && mx_nt_for((size_t)(len + len * (uint64_t)st / R.blen));
+#define MX_VSPAN(S_, B_)                                                                                      \
+  do {                                                                                                        \
+    if (nt) hipLaunchKernelGGL((k_pack_vec_span<S_, B_, true>), grid, block, 0, s, ub, packed, offset, len, q0, q1); \
+    else hipLaunchKernelGGL((k_pack_vec_span<S_, B_, false>), grid, block, 0, s, ub, packed, offset, len, q0, q1);   \
+  } while (0)
+      if (st == 8) MX_VSPAN(8, 4);
+      else if (R.blen == 8) MX_VSPAN(16, 8);
+      else MX_VSPAN(16, 4);
+#undef MX_VSPAN
       return mx_check_launch();
     }
   }
@@ -2581,7 +2604,13 @@ static int convert(const mx_ddt_t *d, size_t count, char *user, char *packed, si
     const uint64_t nw = len / W;
     const dim3 grid((unsigned)((nw + kCB * kVIt - 1) / (kCB * kVIt))), block(kCB);
     const float rblen = 1.0f / (float)R.blen;
-    if (W == 8) hipLaunchKernelGGL((k_convert_vec<8, PACK>), grid, block, 0, s, a, R, rblen);
+    // PACK: non-temporal at the streaming sizes (the user lines read + the
+    // stream written >= MX_NT_MIN_BYTES); UNPACK keeps cached stores (its
+    // partial-line writes)
+    const bool nt = PACK && conv_vec_nt() && mx_nt_for((size_t)(len + len * (uint64_t)R.stride1 / R.blen));
+    if (nt && W == 8) hipLaunchKernelGGL((k_convert_vec<8, PACK, true>), grid, block, 0, s, a, R, rblen);
+    else if (nt) hipLaunchKernelGGL((k_convert_vec<4, PACK, true>), grid, block, 0, s, a, R, rblen);
+    else if (W == 8) hipLaunchKernelGGL((k_convert_vec<8, PACK>), grid, block, 0, s, a, R, rblen);
     else hipLaunchKernelGGL((k_convert_vec<4, PACK>), grid, block, 0, s, a, R, rblen);
     return mx_check_launch();
   }
