@@ -395,6 +395,11 @@ __global__ void k_p2p_pick(const uint64_t *flag0, const P2PRecvState *st0, const
       return;
     }
   }
+  // envelopes of source p already read without a match (< 64 sources): the
+  // acquire before a scan invalidates the XCD's L2, so a source whose pending
+  // messages carry other tags is not rescanned on every pass
+  __shared__ uint64_t s_scanned[64];
+  for (int p = 0; p < n && p < 64; p++) s_scanned[p] = 0;
   for (;;) {
     for (int i = 0; i < n; i++) {
       const int p = (start + i) % n;
@@ -403,6 +408,8 @@ __global__ void k_p2p_pick(const uint64_t *flag0, const P2PRecvState *st0, const
       if (posted <= m0) continue;
       bool hit = tag < 0;
       if (!hit) {
+        if (p < 64 && posted <= s_scanned[p]) continue;
+        if (p < 64) s_scanned[p] = posted;
         __atomic_thread_fence(__ATOMIC_ACQUIRE);   // the envelopes before their `posted` count
         const char *box = box0 + (size_t)p * P2P_BOX;
         for (uint64_t m = m0; !hit && m < posted && m < m0 + P2P_H; m++)
