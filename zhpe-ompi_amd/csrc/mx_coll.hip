@@ -421,6 +421,15 @@ bool mx::release_now_if_quiet(void *p, int kind) {
   return true;
 }
 void mx::release_later(void *p, int kind) { (void)release_now_if_quiet(p, kind); }
+bool mx::release_now_or_keep(void *p, int kind) {   // nothing queued when not quiet: the caller keeps p
+  if (!p) return true;
+  {
+    std::lock_guard<std::mutex> lk(g_live_mu);
+    if (!device_quiet_locked()) return false;
+  }
+  release_now(p, kind);
+  return true;
+}
 void mx::release_flush() {
   std::vector<Deferred> go;
   {
@@ -1696,12 +1705,12 @@ static char *reg_import(mx_comm *c, int p, const RegBuf &b, const RegBuf *own, i
   for (size_t i = 0; i < v.size();) {
     const mx_reg_import &m = v[i];
     if (m.peer == p && m.base < b.base + b.size && b.base < m.base + m.size) {   // overlaps: stale
-      char *stale = m.ptr;
+      // the stale import must be closed before the new handle opens; while
+      // another communicator's work is pending it stays in the cache and this
+      // call declines (every rank falls back to the staged path), so the next
+      // call finds it and tries again -- it is never dropped unclosed
+      if (!release_now_or_keep(m.ptr, REL_IPC)) return nullptr;
       v.erase(v.begin() + (long)i);
-      // the stale import must be gone before the new handle opens; while
-      // another communicator's work is pending the close waits in the list
-      // and this call declines (every rank falls back to the staged path)
-      if (!release_now_if_quiet(stale, REL_IPC)) return nullptr;
       continue;
     }
     held += m.peer == p;

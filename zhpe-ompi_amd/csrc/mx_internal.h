@@ -61,6 +61,7 @@ bool device_quiet();
 void release_later(void *p, int kind);
 void release_flush();
 bool release_now_if_quiet(void *p, int kind);   // false: deferred
+bool release_now_or_keep(void *p, int kind);    // false: not quiet, nothing done (the caller keeps p)
 }  // namespace mx
 
 // Lazily performs mx_init(current device) if the caller did not.

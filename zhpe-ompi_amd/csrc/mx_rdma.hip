@@ -82,10 +82,10 @@ int import_locked(const mx_rdma_handle_t &h, char **out) {
     Import &m = g_imp[i];
     if (m.pid == h.pid && m.base < h.base + h.size && h.base < m.base + m.size) {
       // the owner freed that allocation and made another in its place: the
-      // stale import must be closed before the new handle is opened
-      char *stale = m.ptr;
+      // stale import must be closed before the new handle is opened; while
+      // the device is not quiet it stays cached and the call is retried
+      if (!release_now_or_keep(m.ptr, REL_IPC)) return MX_ERR_STATE;
       g_imp.erase(g_imp.begin() + (long)i);
-      if (!release_now_if_quiet(stale, REL_IPC)) return MX_ERR_STATE;   // retry once quiet
       continue;
     }
     i++;
