@@ -957,6 +957,7 @@ struct PieceArgs {
   uint32_t dinst, dj;      // kCB pieces = dinst instances + dj pieces
   uint64_t ntiles;
   int tbl_lds;             // table staged in LDS
+  int u32;                 // UNPACK: the tile's store loop in 32-bit LDS coordinates
 };
 
 __device__ __forceinline__ void piece_store(char *u, int lg, uint32_t v0, uint32_t v1, uint32_t v2, uint32_t v3) {
@@ -1001,7 +1002,50 @@ __global__ void __launch_bounds__(kCB) k_unpack_piece(PieceArgs a) {
     lo = (uintptr_t)(a.packed + (sa - a.offset)) & ~(uintptr_t)15;
     hi = ((uintptr_t)(a.packed + (sb - a.offset)) + 15) & ~(uintptr_t)15;
   };
+  // the same loop with everything inside the tile 32-bit: instance origins
+  // as LDS offsets (a tile's packed range is < kPieceStage), the window as
+  // clamped LDS bounds, the user pointer advanced by whole instances
+  auto store_tile32 = [&](uint64_t t, uintptr_t lo) {
+    const uint64_t Pa = a.P0 + t * a.K;
+    const uint64_t Pb = Pa + a.K < a.P1 ? Pa + a.K : a.P1;
+    const uint64_t P = Pa + threadIdx.x;
+    if (P >= Pb) return;
+    const uint64_t inst = udiv(P, a.mnpi);
+    uint32_t j = (uint32_t)(P - inst * a.npi);
+    const int64_t base = (int64_t)((uintptr_t)a.packed - lo) - (int64_t)a.offset;   // LDS offset of stream byte 0
+    int32_t ib = (int32_t)(base + (int64_t)(inst * a.S));
+    char *ub = a.user + (int64_t)inst * a.ext;
+    const int64_t w0 = (int64_t)((uintptr_t)a.packed - lo), w1 = w0 + (int64_t)a.len;
+    const int32_t wlo = w0 < INT32_MIN ? INT32_MIN : (int32_t)w0, whi = w1 > INT32_MAX ? INT32_MAX : (int32_t)w1;
+    const int32_t S32 = (int32_t)a.S, dS = (int32_t)(a.dinst * a.S);
+    const int64_t dE = (int64_t)a.dinst * a.ext;
+    const uint32_t iters = (uint32_t)((Pb - P + kCB - 1) / kCB);
+    for (uint32_t it = 0; it < iters; it++) {
+      const DPiece pc = tbl[j];
+      const int32_t li = ib + (int32_t)pc.soff;
+      const int32_t n = 1 << pc.lg;
+      char *u = ub + pc.uoff;
+      if (li >= wlo && li + n <= whi) {
+        const uint32_t *w = reinterpret_cast<const uint32_t *>(stage + (li & ~3));
+        const int sh = li & 3;
+        const uint32_t x0 = w[0], x1 = w[1], x2 = w[2], x3 = w[3], x4 = w[4];
+        piece_store(u, pc.lg, __builtin_amdgcn_alignbyte(x1, x0, sh), __builtin_amdgcn_alignbyte(x2, x1, sh),
+                    __builtin_amdgcn_alignbyte(x3, x2, sh), __builtin_amdgcn_alignbyte(x4, x3, sh));
+      } else {                                                // piece cut by the window
+        for (int32_t i = 0; i < n; i++)
+          if (li + i >= wlo && li + i < whi) u[i] = stage[li + i];
+      }
+      j += a.dj;
+      ib += dS;
+      ub += dE;
+      if (j >= a.npi) { j -= a.npi; ib += S32; ub += a.ext; }
+    }
+  };
   auto store_tile = [&](uint64_t t, uintptr_t lo) {
+    if (a.u32) {
+      store_tile32(t, lo);
+      return;
+    }
     const uint64_t Pa = a.P0 + t * a.K;
     const uint64_t Pb = Pa + a.K < a.P1 ? Pa + a.K : a.P1;
     uint64_t P = Pa + threadIdx.x;
@@ -2446,6 +2490,16 @@ static bool conv_vec_nt() {
   return on != 0;
 }
 
+// MX_CONV_UNPACK_U32=0: the piece UNPACK kernel's store loop in 64-bit
+// stream coordinates (round 4's form; A/B switch)
+static bool conv_unpack_u32() {
+  static const int on = [] {
+    const char *e = getenv("MX_CONV_UNPACK_U32");
+    return (e && *e == '0') ? 0 : 1;
+  }();
+  return on != 0;
+}
+
 // MX_CONV_BMAP_WORD=1: the byte-map PACK stages a word map for word-piece
 // layouts (A/B switch, off: indexed 112 -> 137 us at 256 MiB with it, BLACS
 // equal, profiles/r05/conv_r5r.txt -- the gather gets shorter and the tile's
@@ -2759,6 +2813,7 @@ static int convert(const mx_ddt_t *d, size_t count, char *user, char *packed, si
         p.dj = (uint32_t)(kCB % npi);
         p.ntiles = (p.P1 - p.P0 + p.K - 1) / p.K;
         p.tbl_lds = npi * sizeof(DPiece) <= 16384;
+        p.u32 = conv_unpack_u32();
         const size_t lds = kPieceStage + 48 + (p.tbl_lds ? npi * sizeof(DPiece) : 0);
         const uint64_t per_cu = std::max<uint64_t>(1, std::min<uint64_t>(8, (160 * 1024) / lds));
         const uint64_t grid = std::min<uint64_t>(p.ntiles, (uint64_t)g_num_cus * per_cu);
