@@ -5,7 +5,8 @@ reference walk's bytes (opal_datatype_pack.c:235-370, restated by the
 oracle).  One child process per switch (the switches are read once per
 process); in each, the struct / indexed / BLACS / "strange" types at ~4 MiB
 packed, user pointer aligned and shifted by 3 bytes, whole and as a window
-starting inside an element."""
+starting inside an element, and the unpack of the stream into a pre-filled
+buffer (gap bytes keep theirs)."""
 import os
 import subprocess
 import sys
@@ -56,6 +57,17 @@ for name in sys.argv[2].split(","):
         w = W.cpu().numpy()
         if not (np.array_equal(w[off:off + ln], exp[off:off + ln]) and not w[:off].any() and not w[off + ln:].any()):
             bad.append((name, shift, "window"))
+        # unpack the stream into a pre-filled buffer: gap bytes keep theirs
+        pre = np.random.default_rng(12).integers(0, 256, span, dtype=np.uint8)
+        want = pre.copy()
+        O.mxo_ddt_convert(rec["desc"].ctypes.data, rec["nrec"], B.ctypes.data, rec["lb"], rec["ub"], count,
+                          want.ctypes.data - rec["true_lb"], exp.ctypes.data, 1)
+        R = torch.zeros(span + 16, dtype=torch.uint8, device="cuda")
+        R[shift:shift + span] = torch.from_numpy(pre).cuda()
+        dt.unpack(count, R.data_ptr() + shift - rec["true_lb"], P.data_ptr(), stream=st)
+        torch.cuda.synchronize()
+        if not np.array_equal(R[shift:shift + span].cpu().numpy(), want):
+            bad.append((name, shift, "unpack"))
 print("BAD", bad)
 sys.exit(1 if bad else 0)
 """
@@ -77,7 +89,8 @@ def _run(env, types):
 
 @pytest.mark.parametrize("env", ["MX_CONV_BMAP_SPAN=12288", "MX_CONV_BMAP_SPAN=24576", "MX_CONV_BMAP_UNROLL=0",
                                  "MX_CONV_BMAP_QUAD=0", "MX_CONV_BMAP_WORD=1", "MX_CONV_BMAP_NT=0",
-                                 "MX_CONV_BMAP_DW=0", "MX_CONV_BMAP_CW=0"])
+                                 "MX_CONV_BMAP_DW=0", "MX_CONV_BMAP_CW=0", "MX_NT_MIN_BYTES=0 MX_CONV_UNPACK_NTLD=1",
+                                 "MX_CONV_UNPACK_U32=0"])
 def test_byte_map_pack_switches(env):
     _run(env, BMAP_TYPES)
 

@@ -72,6 +72,7 @@ struct ConvArgs {
   char *packed;      // receives / holds stream bytes [offset, offset + len)
   uint64_t offset, len;
   int pk_vec;        // packed is 16-byte aligned
+  int ntld;          // UNPACK: the packed stream read non-temporal (read once)
 };
 
 __device__ __forceinline__ int find_run(const DRun *runs, int n, uint64_t q) {
@@ -182,7 +183,7 @@ __device__ __forceinline__ void convert_granule(const ConvArgs &a, const DRun *r
   U regs[K];
   if (!PACK) {
     if (full) {
-      const uint4 v = *reinterpret_cast<const uint4 *>(a.packed + rel0);
+      const uint4 v = a.ntld ? gld16p<true>(a.packed + rel0) : *reinterpret_cast<const uint4 *>(a.packed + rel0);
       memcpy(regs, &v, 16);
     } else {
 #pragma unroll
@@ -958,6 +959,7 @@ struct PieceArgs {
   uint64_t ntiles;
   int tbl_lds;             // table staged in LDS
   int u32;                 // UNPACK: the tile's store loop in 32-bit LDS coordinates
+  int ntld;                // UNPACK: the packed stream read non-temporal (read once)
 };
 
 __device__ __forceinline__ void piece_store(char *u, int lg, uint32_t v0, uint32_t v1, uint32_t v2, uint32_t v3) {
@@ -1081,7 +1083,10 @@ __global__ void __launch_bounds__(kCB) k_unpack_piece(PieceArgs a) {
         const uint4 *g = reinterpret_cast<const uint4 *>(lo);
         uint4 *d = reinterpret_cast<uint4 *>(stage);
         const uint32_t nv = (uint32_t)((hi - lo) / 16);
-        for (uint32_t i = threadIdx.x; i < nv; i += kCB) d[i] = g[i];
+        if (a.ntld)
+          for (uint32_t i = threadIdx.x; i < nv; i += kCB) d[i] = gld16p<true>(reinterpret_cast<const char *>(g + i));
+        else
+          for (uint32_t i = threadIdx.x; i < nv; i += kCB) d[i] = g[i];
       }
       __syncthreads();
       store_tile(t, lo);
@@ -2490,6 +2495,18 @@ static bool conv_vec_nt() {
   return on != 0;
 }
 
+// MX_CONV_UNPACK_NTLD=1: the UNPACK kernels read the packed stream with
+// non-temporal loads at the streaming sizes (A/B switch, off: -5 % / +5 %
+// on indexed at 256 MiB / 1 GiB, within 1 % elsewhere, profiles/r05/conv_ab_r5y.txt;
+// the unpack is bound by its partial-line stores)
+static bool conv_unpack_ntld() {
+  static const int on = [] {
+    const char *e = getenv("MX_CONV_UNPACK_NTLD");
+    return (e && *e == '1') ? 1 : 0;
+  }();
+  return on != 0;
+}
+
 // MX_CONV_UNPACK_U32=0: the piece UNPACK kernel's store loop in 64-bit
 // stream coordinates (round 4's form; A/B switch)
 static bool conv_unpack_u32() {
@@ -2596,6 +2613,7 @@ static int convert(const mx_ddt_t *d, size_t count, char *user, char *packed, si
   a.offset = offset;
   a.len = len;
   a.pk_vec = ((uintptr_t)packed & 15) == 0;
+  a.ntld = !PACK && conv_unpack_ntld() && mx_nt_for((size_t)(2 * len));
   hipStream_t s = (hipStream_t)stream;
   mx_ddt *dm = const_cast<mx_ddt *>(d);
   // a contiguous type (one block, extent = size): the stream is the user
@@ -2814,6 +2832,7 @@ static int convert(const mx_ddt_t *d, size_t count, char *user, char *packed, si
         p.ntiles = (p.P1 - p.P0 + p.K - 1) / p.K;
         p.tbl_lds = npi * sizeof(DPiece) <= 16384;
         p.u32 = conv_unpack_u32();
+        p.ntld = !PACK && conv_unpack_ntld() && mx_nt_for((size_t)(2 * len));
         const size_t lds = kPieceStage + 48 + (p.tbl_lds ? npi * sizeof(DPiece) : 0);
         const uint64_t per_cu = std::max<uint64_t>(1, std::min<uint64_t>(8, (160 * 1024) / lds));
         const uint64_t grid = std::min<uint64_t>(p.ntiles, (uint64_t)g_num_cus * per_cu);
