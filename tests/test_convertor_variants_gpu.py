@@ -90,7 +90,7 @@ def _run(env, types):
 @pytest.mark.parametrize("env", ["MX_CONV_BMAP_SPAN=12288", "MX_CONV_BMAP_SPAN=24576", "MX_CONV_BMAP_UNROLL=0",
                                  "MX_CONV_BMAP_QUAD=0", "MX_CONV_BMAP_WORD=1", "MX_CONV_BMAP_NT=0",
                                  "MX_CONV_BMAP_DW=0", "MX_CONV_BMAP_CW=0", "MX_NT_MIN_BYTES=0 MX_CONV_UNPACK_NTLD=1",
-                                 "MX_CONV_UNPACK_U32=0"])
+                                 "MX_CONV_UNPACK_U32=0", "MX_CONV_BMAP_INST=0"])
 def test_byte_map_pack_switches(env):
     _run(env, BMAP_TYPES)
 

@@ -1966,6 +1966,17 @@ static void cut_pieces(const mx_ddt *d, int al, std::vector<DPiece> &v) {
 // whose user span, rounded out to 16 bytes, always fits kBmapSpan -- whole
 // instances for a non-monotonic layout, [addr(first), addr(last)] for a
 // monotonic one.
+// MX_CONV_BMAP_INST=0: the byte-map PACK's tiles of non-monotonic layouts
+// stay multiples of 256 stream bytes instead of whole instances (A/B switch;
+// read at datatype creation)
+static bool conv_bmap_inst_tiles() {
+  static const int on = [] {
+    const char *e = getenv("MX_CONV_BMAP_INST");
+    return (e && *e == '0') ? 0 : 1;
+  }();
+  return on != 0;
+}
+
 static void build_bmap(mx_ddt *d) {
   const int64_t ext = d->ub - d->lb;
   const uint64_t S = d->size;
@@ -2040,6 +2051,16 @@ static void build_bmap(mx_ddt *d) {
       else hi = mid - 1;
     }
     d->bmap_Ts[k] = lo * 256;
+    // a layout that is not monotonic stages whole instances per tile; when
+    // S % 16 == 0 a tile of exactly k instances starts (from offset 0) on an
+    // instance boundary and stages k of them, not the k + 1 a tile cut
+    // mid-instance does (indexed: 12.9 instead of 19.3 KiB per 10 KiB of stream)
+    if (!d->monotonic && S % 16 == 0) {
+      const int64_t kk = (span - 160 - d->uspan) / ext;   // worst(kk * S) + 160 <= span
+      if (kk >= 1 && (uint64_t)kk * S >= 256 && (uint64_t)kk * S <= (uint64_t)span * 2 / 3 &&
+          worst((uint64_t)kk * S) + 160 <= span && conv_bmap_inst_tiles())
+        d->bmap_Ts[k] = (uint64_t)kk * S;
+    }
   }
   d->bmap_T = d->bmap_Ts[1];
 }
