@@ -425,10 +425,17 @@ def bench_allreduce(torch, mx, dist, rank, world, dev, steps, warmup, nbytes=256
         # N>1 is bound by the xGMI links, not HBM: the all-peer exchange puts
         # 2S/n on each of a rank's n-1 links, so the busBW ceiling is
         # (n-1) x 153 GB/s (7 x 153 on a full node); the fold kernel's own
-        # HBM fraction is reported beside it
-        "roofline": {"bound": "xgmi", "achieved": round(busbw, 2), "peak": round(peak_links, 1), "unit": "GB/s",
-                     "frac": round(busbw / peak_links, 4), "traffic": None,
-                     "metric": "busBW = algbw*2(n-1)/n vs (n-1) links x 153 GB/s",
+        # HBM fraction is reported beside it.  With the ranks sharing one GPU
+        # (no link involved) the bound is that GPU's HBM: every rank's fold
+        # bytes in one fold time
+        "roofline": ({"bound": "xgmi", "achieved": round(busbw, 2), "peak": round(peak_links, 1), "unit": "GB/s",
+                      "frac": round(busbw / peak_links, 4), "traffic": None,
+                      "metric": "busBW = algbw*2(n-1)/n vs (n-1) links x 153 GB/s"} if not shared_gpu or not fold_gbs else
+                     {"bound": "hbm", "achieved": round(world * fold_gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                      "frac": round(world * fold_gbs / HBM_PEAK_GBS, 4), "traffic": None,
+                      "metric": "ranks sharing one GPU: every rank's fold bytes per fold time vs the GPU's HBM "
+                                "(no xGMI link involved); busBW in value",
+                      "busbw_vs_links_if_separate_gpus": round(busbw / peak_links, 4)}) | {
                      "peak_all_links": 7 * XGMI_LINK_GBS, "frac_all_links": round(busbw / (7 * XGMI_LINK_GBS), 4),
                      "shared_gpu": shared_gpu,
                      "fold_kernel": {"kernel": "k_fold<float, mx::OpSum> (n reads + n writes, n-1 of them remote)",
