@@ -192,6 +192,9 @@ typedef struct mx_coll_stats {
     uint64_t staged_calls;     /* allreduces through the staging chunks     */
     uint64_t direct_calls;     /* zero-copy allreduces whose results went
                                   straight into the peers' rbufs            */
+    uint64_t reg_fast_calls;   /* registration exchanges that found every
+                                  rank's buffers as in the last one (one
+                                  host round instead of two)                */
 } mx_coll_stats_t;
 int mx_comm_set_profiling(mx_comm_t *comm, int on);
 int mx_comm_get_stats(mx_comm_t *comm, mx_coll_stats_t *stats, int reset);

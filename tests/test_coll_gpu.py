@@ -979,3 +979,98 @@ def test_reduce_scatter_forced_local(word, n, op, t, inplace):
             golden_io.assert_coll_equal(R[r].cpu().numpy()[: rc[r] * es], exp[r][: rc[r] * es], mxompi.OP[op],
                                         mxompi.TYPE[t], f"reduce_scatter word {word:#x} n={n} rc={rc} rank {r}")
         comm.close()
+
+
+# ---------------------------------------------------------------------------
+# registration fast path (round 5): consecutive zero-copy calls on the same
+# buffers skip the verdict round; new contents every call, and an rbuf freed
+# and re-made (a new runtime buffer id, possibly at the same address) takes
+# the full exchange again -- every result exact
+# ---------------------------------------------------------------------------
+def _fast_x(rank, i, count):
+    return np.random.default_rng(9000 + 97 * i + rank).integers(-(1 << 31), 1 << 31, count,
+                                                                 dtype=np.int64).astype(np.int32)
+
+
+def _reg_fast_worker(rank, n, port, q):
+    import ctypes
+    import torch.distributed as dist
+    os.environ["HSA_ENABLE_IPC_MODE_LEGACY"] = "0"
+    try:
+        dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=n)
+        torch.cuda.set_device(0)
+        mxompi.init(0)
+
+        def ag(b):
+            out = [None] * n
+            dist.all_gather_object(out, b)
+            return out
+
+        comm = mxompi.Comm(rank, n, ag, device=0, staging_bytes=16 << 20)
+        comm.set_timeout(30.0)
+        comm.set_autotune(False)
+        comm.set_reg_min(1)                       # zero-copy at every size
+        st = torch.cuda.current_stream().cuda_stream
+        count = 1 << 20
+        X = torch.empty(count, dtype=torch.int32, device="cuda")
+        Y = torch.zeros(count, dtype=torch.int32, device="cuda")
+        res = []
+        for i in range(8):
+            X.copy_(torch.from_numpy(_fast_x(rank, i, count)).cuda())   # new contents on the stream
+            comm.allreduce(X.data_ptr(), Y.data_ptr(), count, "INT32_T", "SUM", "auto", st)
+            res.append(Y.cpu().numpy().tobytes())
+        s1 = comm.stats()
+        L = mxompi.lib()
+        vp, sz = ctypes.c_void_p, ctypes.c_size_t
+        for i in range(8, 11):                    # rbuf re-made every call: full exchanges
+            p = vp()
+            assert L.mx_alloc(sz(4 * count), ctypes.byref(p)) == 0
+            X.copy_(torch.from_numpy(_fast_x(rank, i, count)).cuda())
+            torch.cuda.synchronize()
+            comm.allreduce(X.data_ptr(), p.value, count, "INT32_T", "SUM", "auto", st)
+            host = np.empty(count, np.int32)
+            assert L.mx_memcpy(vp(host.ctypes.data), p, sz(4 * count), None) == 0
+            res.append(host.tobytes())
+            torch.cuda.synchronize()
+            assert L.mx_free(p) == 0
+        s2 = comm.stats()
+        comm.close()
+        dist.destroy_process_group()
+        q.put((rank, "ok", {"res": res, "fast1": s1["reg_fast_calls"], "zc1": s1["zero_copy_calls"],
+                            "fast2": s2["reg_fast_calls"], "zc2": s2["zero_copy_calls"]}))
+    except Exception:  # noqa: BLE001
+        import traceback
+        q.put((rank, "err", traceback.format_exc()))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("n", [2, 3])
+def test_registration_fast_path_reused_and_remade_buffers(n):
+    import torch.multiprocessing as mp
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_reg_fast_worker, args=(r, n, port, q)) for r in range(n)]
+    for p in procs:
+        p.start()
+    out = {}
+    try:
+        for _ in range(n):
+            rank, status, payload = q.get(timeout=240)
+            assert status == "ok", payload
+            out[rank] = payload
+    finally:
+        for p in procs:
+            p.join(timeout=60 if len(out) == n else 5)
+            if p.is_alive():
+                p.terminate()
+                p.join(timeout=10)
+    count = 1 << 20
+    for i in range(11):
+        exp = sum(_fast_x(r, i, count).astype(np.int64) for r in range(n)).astype(np.int32).tobytes()
+        for r in range(n):
+            assert out[r]["res"][i] == exp, (i, r)
+    for r in range(n):
+        assert out[r]["zc1"] == 8 and out[r]["fast1"] == 7, out[r]      # the first call registers
+        assert out[r]["zc2"] == 11, out[r]
+        assert out[r]["fast2"] == 7, out[r]                             # re-made rbufs: never the fast path

@@ -164,6 +164,7 @@ struct mx_comm {
   int zc_direct;
   uint64_t reg_seq, reg_tick;
   std::vector<struct mx_reg_import> *reg_imp;
+  void *reg_fast;   // the last exchange's records and mappings (mx_coll.hip RegFast)
   // data-movement autotuning of blocking collectives: per
   // collective kind (TUNE_*) and power-of-two size class, the first call
   // warms up, the next ones time each candidate (allreduce from 64 KiB:
