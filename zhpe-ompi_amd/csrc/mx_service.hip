@@ -509,7 +509,12 @@ int svc_setup(Service &v) {
     v.grid = g < 1 ? 1 : g > (long)kSvcGridMax ? kSvcGridMax : (unsigned)g;
   }
   if (const char *e = getenv("MX_SVC_HSLEEP")) v.hsleep = atoi(e) & 3;
-  if (const char *e = getenv("MX_SVC_DIAG")) v.hsleep |= (atoi(e) & 7) << 4;
+  if (const char *e = getenv("MX_SVC_DIAG")) {
+    v.hsleep |= (atoi(e) & 7) << 4;
+    if (v.hsleep >> 4)   // measurement only: served results are wrong
+      fprintf(stderr, "mx: MX_SVC_DIAG=%d: the op service skips its acquire / release / reduce -- "
+                      "interference measurements only, served results are NOT valid\n", (v.hsleep >> 4) & 7);
+  }
   if (const char *e = getenv("MX_SVC_SOLO")) v.solo = (uint64_t)atoll(e);
   if (const char *e = getenv("MX_SVC_MAX")) v.maxb = std::min<uint64_t>((uint64_t)atoll(e), kSvcMaxBytes);
   atexit(svc_atexit);
