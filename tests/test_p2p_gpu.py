@@ -560,3 +560,159 @@ def test_two_p2p_communicators_crossing_with_an_iallreduce():
             assert got[r][it]["b"] == _data(1000 * it + 10 * p + 1, nb).tobytes(), (it, r, "b")
             assert got[r][it]["sum"] == s, (it, r)
             assert got[r][it]["z"] == [float(2 << 20)] * 8
+
+
+# ---------------------------------------------------------------------------
+# round 5: receives that yield.  Receive kernels share one
+# receive stream per device; a receive waiting for its message used to hold
+# back every receive posted after it, so a blocking rendezvous send whose
+# receive was posted second could never be cleared -- legal MPI programs
+# deadlocked.  Each case below did; each must now finish with every payload
+# exact, and messages must still go to the earliest posted receive that
+# matches them (pml/ob1's order) when a displaced receive runs again.
+BIG = (1 << 20) + 5        # rendezvous
+
+
+def _yield_worker(rank, n, port, q):
+    import torch.distributed as dist
+    os.environ["HSA_ENABLE_IPC_MODE_LEGACY"] = "0"
+    try:
+        dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=n)
+        torch.cuda.set_device(0)
+        mxompi.init(0)
+
+        def ag(b):
+            out = [None] * n
+            dist.all_gather_object(out, b)
+            return out
+
+        A = mxompi.Comm(rank, n, ag, device=0, staging_bytes=1 << 20)
+        B = mxompi.Comm(rank, n, ag, device=0, staging_bytes=1 << 20)
+        for c in (A, B):
+            c.set_timeout(30.0)
+        right, left = (rank + 1) % n, (rank - 1) % n
+        res = {}
+
+        def buf():
+            return torch.zeros(BIG, dtype=torch.uint8, device="cuda")
+
+        # (1) halo: both receives posted, then blocking sends leftwards first
+        for it in range(3):
+            fl, fr = buf(), buf()
+            r1 = A.irecv(fl.data_ptr(), BIG, left, tag=1)
+            r2 = A.irecv(fr.data_ptr(), BIG, right, tag=2)
+            A.send(_dev(_data(10 * it + 100 * rank + 2, BIG)).data_ptr(), BIG, left, tag=2)
+            A.send(_dev(_data(10 * it + 100 * rank + 1, BIG)).data_ptr(), BIG, right, tag=1)
+            for r in (r1, r2):
+                r.wait()
+                r.free()
+            res[("halo", it)] = (fl.cpu().numpy().tobytes(), fr.cpu().numpy().tobytes())
+        dist.barrier()
+
+        # (2) one source, tags crossed: the second-posted receive's message comes first
+        if rank == 0:
+            ba, bb = buf(), buf()
+            ra = A.irecv(ba.data_ptr(), BIG, 1, tag=10)
+            rb = A.irecv(bb.data_ptr(), BIG, 1, tag=11)
+            ra.wait(); rb.wait(); ra.free(); rb.free()
+            res["cross"] = (ba.cpu().numpy().tobytes(), bb.cpu().numpy().tobytes())
+        elif rank == 1:
+            A.send(_dev(_data(511, BIG)).data_ptr(), BIG, 0, tag=11)
+            A.send(_dev(_data(510, BIG)).data_ptr(), BIG, 0, tag=10)
+        dist.barrier()
+
+        # (3) two communicators, the receive of the second-posted one first
+        if rank == 0:
+            ba, bb = buf(), buf()
+            ra = A.irecv(ba.data_ptr(), BIG, 1, tag=5)
+            rb = B.irecv(bb.data_ptr(), BIG, 1, tag=6)
+            rb.wait(); ra.wait(); ra.free(); rb.free()
+            res["comms"] = (ba.cpu().numpy().tobytes(), bb.cpu().numpy().tobytes())
+        elif rank == 1:
+            B.send(_dev(_data(606, BIG)).data_ptr(), BIG, 0, tag=6)
+            A.send(_dev(_data(605, BIG)).data_ptr(), BIG, 0, tag=5)
+        dist.barrier()
+
+        # (4) order after a yield: R1 (source 1, tag 7) yields to R2 (source
+        # 2); R3 (source 1, tag 7, posted after R1) runs while R1 is
+        # displaced and must leave source 1's first tag-7 message to R1
+        if rank == 0:
+            b1, b2, b3 = buf(), buf(), buf()
+            r1 = A.irecv(b1.data_ptr(), BIG, 1, tag=7)
+            r2 = A.irecv(b2.data_ptr(), BIG, 2, tag=8)
+            r3 = A.irecv(b3.data_ptr(), BIG, 1, tag=7)
+            r2.wait()
+            r1.wait()
+            r3.wait()
+            st = [r.status() for r in (r1, r2, r3)]
+            for r in (r1, r2, r3):
+                r.free()
+            res["order"] = (st, [b.cpu().numpy().tobytes() for b in (b1, b2, b3)])
+        elif rank == 2:
+            A.send(_dev(_data(708, BIG)).data_ptr(), BIG, 0, tag=8)
+            dist.send(torch.ones(1), dst=1)          # R1 has yielded by now
+        elif rank == 1:
+            dist.recv(torch.zeros(1), src=2)
+            A.send(_dev(_data(701, BIG)).data_ptr(), BIG, 0, tag=7)
+            A.send(_dev(_data(702, BIG)).data_ptr(), BIG, 0, tag=7)
+        dist.barrier()
+
+        # (5) MPI_ANY_SOURCE posted first, a specific receive behind it whose
+        # blocking sender comes first
+        if rank == 0:
+            ba, bb = buf(), buf()
+            ra = A.irecv(ba.data_ptr(), BIG, -1, tag=20)
+            rb = A.irecv(bb.data_ptr(), BIG, 2, tag=21)
+            rb.wait(); ra.wait()
+            res["any"] = (ra.source(), ba.cpu().numpy().tobytes(), bb.cpu().numpy().tobytes())
+            ra.free(); rb.free()
+        elif rank == 2:
+            A.send(_dev(_data(821, BIG)).data_ptr(), BIG, 0, tag=21)
+            dist.send(torch.ones(1), dst=1)
+        elif rank == 1:
+            dist.recv(torch.zeros(1), src=2)
+            A.send(_dev(_data(820, BIG)).data_ptr(), BIG, 0, tag=20)
+        dist.barrier()
+        B.close()
+        A.close()
+        dist.destroy_process_group()
+        q.put((rank, "ok", res))
+    except Exception as e:  # noqa: BLE001
+        import traceback
+        q.put((rank, "err", traceback.format_exc() + str(e)))
+
+
+def test_receives_yield_to_receives_posted_after_them():
+    import torch.multiprocessing as mp
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    n = 3
+    procs = [ctx.Process(target=_yield_worker, args=(r, n, port, q)) for r in range(n)]
+    for p in procs:
+        p.start()
+    got = {}
+    try:
+        for _ in range(n):
+            rank, status, payload = q.get(timeout=200)
+            assert status == "ok", payload
+            got[rank] = payload
+    finally:
+        for p in procs:
+            p.join(timeout=30 if len(got) == n else 5)
+            if p.is_alive():
+                p.terminate()
+                p.join(timeout=10)
+    for r in range(n):
+        left, right = (r - 1) % n, (r + 1) % n
+        for it in range(3):
+            fl, fr = got[r][("halo", it)]
+            assert fl == _data(10 * it + 100 * left + 1, BIG).tobytes(), ("halo from left", r, it)
+            assert fr == _data(10 * it + 100 * right + 2, BIG).tobytes(), ("halo from right", r, it)
+    assert got[0]["cross"] == (_data(510, BIG).tobytes(), _data(511, BIG).tobytes())
+    assert got[0]["comms"] == (_data(605, BIG).tobytes(), _data(606, BIG).tobytes())
+    st, data = got[0]["order"]
+    assert [tuple(s)[:2] for s in st] == [(BIG, 7), (BIG, 8), (BIG, 7)], st
+    assert data == [_data(701, BIG).tobytes(), _data(708, BIG).tobytes(), _data(702, BIG).tobytes()]
+    src, da, db = got[0]["any"]
+    assert src == 1 and da == _data(820, BIG).tobytes() and db == _data(821, BIG).tobytes()

@@ -3786,6 +3786,7 @@ extern "C" int mx_test(mx_request_t *q, int *flag) {
   if (!q || !flag) return MX_ERR_ARG;
   *flag = 1;
   if (!q->active) return MX_SUCCESS;   // completed or inactive persistent: MPI_Test gives true
+  mx::p2p_progress();
   if (fast_done(q)) return req_complete(q);
   if (q->fast == 2) {                  // a rendezvous send: only its status word tells
     if (rndv_failed(q)) return req_complete(q);
@@ -3798,6 +3799,10 @@ extern "C" int mx_test(mx_request_t *q, int *flag) {
     return MX_SUCCESS;
   }
   if (e != hipSuccess) return MX_ERR_HIP;
+  if (mx::p2p_yielded(q)) {            // that launch yielded: launched again by p2p_progress
+    *flag = 0;
+    return MX_SUCCESS;
+  }
   return req_complete(q);
 }
 
@@ -3806,9 +3811,37 @@ extern "C" int mx_test(mx_request_t *q, int *flag) {
 // small message's latency), then block.
 constexpr double kWaitSpinUs = 2000.0;
 
+// A point-to-point wait polls and never blocks in the runtime: every pass
+// launches again the receives that yielded (mx_p2p.hip, p2p_progress) --
+// this request's, or another one a peer's send waits for -- and a receive's
+// event completes also when its launch yielded.
+static int p2p_wait(mx_request *q) {
+  const auto t0 = std::chrono::steady_clock::now();
+  for (;;) {
+    mx::p2p_progress();
+    if (fast_done(q)) return req_complete(q);
+    const bool late =
+        std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0).count() > kWaitSpinUs;
+    if (q->fast == 2) {
+      if (late) {
+        if (rndv_failed(q)) return req_complete(q);
+        std::this_thread::sleep_for(std::chrono::microseconds(20));
+      }
+      continue;
+    }
+    if (!q->fast || late) {
+      const hipError_t e = hipEventQuery(q->done);
+      if (e == hipSuccess && !mx::p2p_yielded(q)) return req_complete(q);
+      if (e != hipSuccess && e != hipErrorNotReady) return MX_ERR_HIP;
+      if (late) std::this_thread::sleep_for(std::chrono::microseconds(20));
+    }
+  }
+}
+
 extern "C" int mx_wait(mx_request_t *q) {
   if (!q) return MX_ERR_ARG;
   if (!q->active) return MX_SUCCESS;
+  if (q->kind == RQ_SEND || q->kind == RQ_RECV) return p2p_wait(q);
   const auto t0 = std::chrono::steady_clock::now();
   if (q->fast && q->status) {
     for (;;) {
@@ -3836,10 +3869,23 @@ extern "C" int mx_request_stream_wait(mx_request_t *q, void *stream) {
   if (!q->active) return MX_SUCCESS;
   if (q->fast == 2) {   // a rendezvous send has no event: the host waits for its status word
     while (!fast_done(q)) {
+      mx::p2p_progress();
       if (const int e = rndv_failed(q)) return e;
       std::this_thread::sleep_for(std::chrono::microseconds(20));
     }
     return MX_SUCCESS;
+  }
+  if (q->kind == RQ_RECV && q->launch) {
+    // a receive that may yield: its event is not its completion, so the host
+    // waits (launching yielded receives again) until it is delivered
+    for (;;) {
+      mx::p2p_progress();
+      if (fast_done(q)) return MX_SUCCESS;
+      const hipError_t e = hipEventQuery(q->done);
+      if (e == hipSuccess && !mx::p2p_yielded(q)) return MX_SUCCESS;
+      if (e != hipSuccess && e != hipErrorNotReady) return MX_ERR_HIP;
+      std::this_thread::sleep_for(std::chrono::microseconds(5));
+    }
   }
   return hipStreamWaitEvent((hipStream_t)stream, q->done, 0) == hipSuccess ? MX_SUCCESS : MX_ERR_HIP;
 }

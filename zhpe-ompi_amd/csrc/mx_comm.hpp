@@ -78,7 +78,40 @@ struct P2PRecvState {
   uint64_t held;                       // valid entries in stash + defer (0: skip the scan)
   P2PStashEntry stash[P2P_STASH_N];    // written only by the last lane of a receive kernel
   P2PStashEntry defer[P2P_DEFER_N];    // likewise
+  uint64_t msgs_done;                  // envelopes consumed by finished kernels (lane_msgs at their end)
 };
+
+// Receives that yield.  Receive kernels run one at a
+// time on the device's receive stream; one that waits for its message while
+// a receive queued behind it could take a message that has arrived (or that
+// was set aside) stops at an envelope boundary instead of blocking the
+// stream ("yields"), and the host launches it again behind the others.  A
+// receive that yielded is "displaced": later receives of its communicator
+// leave the messages it matches alone, so each message still goes to the
+// earliest posted receive that matches it (pml/ob1's order).
+constexpr int P2P_Q = 256;        // launches a blocked receive looks at behind it
+constexpr int P2P_DISP_N = 32;    // displaced receives per communicator
+struct P2PQEntry {                // one receive launch (mapped host, written before the launch)
+  uint64_t launch;                // launch number (written last)
+  uint64_t post;                  // its post number in its communicator
+  const uint64_t *flag0;          // its communicator's flag array
+  const P2PRecvState *st0;        // ... receive state per source
+  const char *box0;               // ... mailboxes
+  const struct P2PDisplaced *disp;
+  int32_t n, src;                 // src < 0: MPI_ANY_SOURCE
+  int64_t tag;                    // < 0: MPI_ANY_TAG
+};
+struct P2PRxQueue {               // one per device, mapped host memory
+  uint64_t enq;                   // receive launches enqueued (host)
+  uint64_t yields;                // launch number of the latest yield (device)
+  P2PQEntry e[P2P_Q];             // launch L at e[L % P2P_Q]
+};
+struct P2PDispEntry { uint64_t post; int32_t src, pad; int64_t tag; };
+struct P2PDisplaced {             // device memory, changed only by a receive kernel's last lane
+  uint64_t n;
+  P2PDispEntry d[P2P_DISP_N];
+};
+constexpr int P2P_DEC = 16;       // decision ring: envelope k of a launch taken or stopped at
 
 // Rendezvous sends waiting for their CTS (mapped host memory, written by the
 // host when the send is posted, read by the rendezvous pick kernel)
@@ -236,6 +269,8 @@ struct mx_comm {
   uint64_t p2p_rndv_gen;             // rendezvous kernels enqueued
   std::vector<int> *p2p_rndv_free;   // free table slots
   unsigned p2p_any_rr;   // MPI_ANY_SOURCE: source the next pick scans first
+  mx::P2PDisplaced *p2p_disp;        // device: receives of this communicator that yielded
+  uint64_t p2p_posts;                // receives posted (their post numbers)
 };
 
 
@@ -259,8 +294,12 @@ struct mx_request {
   int fast;          // completion by status[4]: 1 also by the event, 2 only by status[4]
                      // (a rendezvous send: its data moves on whichever kernel takes its CTS)
   int rndv;          // rendezvous send: table slot + 1, else 0
-  void *tmp;         // packed staging freed at completion (a rendezvous send of a datatype)
+  void *tmp;         // packed staging freed at completion (a rendezvous send or a receive of a datatype)
   const struct mx_ddt *ddt;   // non-contiguous user layout (count instances), or null
+  // a receive: its post number, its current launch (status[5] == launch: that
+  // launch yielded) and its kernel arguments, kept for the next launch
+  uint64_t post, launch;
+  void *rx;
 };
 
 namespace mx {
@@ -280,6 +319,10 @@ bool p2p_pending(mx_comm *c);   // this communicator's channel kernels not yet d
 void p2p_release(mx_comm *c);
 // a point-to-point request completed: release its rendezvous slot / staging
 void p2p_finish(mx_request *q);
+// launch again the receives whose kernels yielded (from every wait / test)
+void p2p_progress();
+// a receive request's current launch yielded (it is not complete)
+bool p2p_yielded(const mx_request *q);
 // status blocks (P2P_STATUS_WORDS x int64, mapped host memory): from a process-wide
 // pool allocated once (never released, so a request may outlive its
 // communicator), else one hipHostMalloc each

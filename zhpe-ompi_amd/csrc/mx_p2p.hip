@@ -35,7 +35,10 @@
 // status; the receive kernel then takes its mailbox and flags from that
 // slot.  Receives run in issue order on one stream, so an ANY_SOURCE
 // receive consumes exactly one message and later receives -- specific or
-// not -- see the channel advanced (MPI only orders messages per pair).  A message longer than the receive buffer delivers what
+// not -- see the channel advanced (MPI only orders messages per pair); a
+// receive still waiting when one queued behind it could progress yields
+// and is launched again by the host's wait (round 5, rx_control /
+// p2p_progress).  A message longer than the receive buffer delivers what
 // fits and completes with MX_ERR_TRUNCATE (MPI_ERR_TRUNCATE); the status
 // holds the delivered byte count.  Non-contiguous layouts are packed /
 // unpacked by the device convertor (mx_convertor.h) around the stream.
@@ -349,31 +352,111 @@ struct P2PRecvArgs {
   P2PRecvState *st0;
   char *stash0;              // stash payloads of source 0 (source p at + p * N * C)
   P2PDone fin;
+  // yielding (round 5): this launch's number and the receive's
+  // post number, the device's launch queue (mapped; null: never yield) and
+  // decision ring, and this communicator's displaced receives
+  uint64_t launch, post;
+  const P2PRxQueue *rq;
+  uint64_t *dec;
+  P2PDisplaced *disp;
 };
 
-// oldest message set aside in `st` (stashed eager payload or deferred
-// rendezvous envelope) that a receive with `tag` (< 0: any) matches:
-// {kind 0 stash / 1 defer, slot}, or {-1, -1}
-__device__ __forceinline__ int2 held_match(const P2PRecvState *st, int64_t tag) {
+// A message of source p with `tag` is reserved when a displaced receive of
+// the communicator posted before `post` matches it: that receive gets it
+// when it runs again.  (The displaced set changes only at a receive
+// kernel's end, so every lane of a kernel sees the same one.)
+__device__ __forceinline__ bool reserved(const P2PDisplaced *d, uint64_t post, int p, int64_t tag) {
+  if (!d) return false;
+  const uint64_t n = d->n;
+  for (uint64_t i = 0; i < n && i < P2P_DISP_N; i++) {
+    const P2PDispEntry &e = d->d[i];
+    if (e.post < post && (e.src < 0 || e.src == p) && (e.tag < 0 || e.tag == tag)) return true;
+  }
+  return false;
+}
+
+// oldest message set aside in `st` (source p; stashed eager payload or
+// deferred rendezvous envelope) that a receive with `tag` (< 0: any) posted
+// as `post` matches and no earlier displaced receive does: {kind 0 stash /
+// 1 defer, slot}, or {-1, -1}
+__device__ __forceinline__ int2 held_match(const P2PRecvState *st, int64_t tag, const P2PDisplaced *disp = nullptr,
+                                           uint64_t post = 0, int p = 0) {
   int2 hit{-1, -1};
   if (!st->held) return hit;
   uint64_t best = ~(uint64_t)0;
   for (int k = 0; k < P2P_STASH_N; k++) {
     const P2PStashEntry &e = st->stash[k];
-    if (e.valid && (tag < 0 || e.tag == tag) && e.seq < best) {
+    if (e.valid && (tag < 0 || e.tag == tag) && e.seq < best && !reserved(disp, post, p, e.tag)) {
       best = e.seq;
       hit = int2{0, k};
     }
   }
   for (int k = 0; k < P2P_DEFER_N; k++) {
     const P2PStashEntry &e = st->defer[k];
-    if (e.valid && (tag < 0 || e.tag == tag) && e.seq < best) {
+    if (e.valid && (tag < 0 || e.tag == tag) && e.seq < best && !reserved(disp, post, p, e.tag)) {
       best = e.seq;
       hit = int2{1, k};
     }
   }
   return hit;
 }
+
+// Could a receive launched behind launch `me` take a message now?  For each
+// queued launch (the device's launch queue, up to P2P_Q of them): a held
+// message of one of its sources that it matches (and no earlier displaced
+// receive reserves), or an envelope it matches that its source posted and
+// no finished kernel consumed.  The running receive's own source p of its
+// communicator is judged by what the running launch set aside (`aside`, the
+// tags of the envelopes it took and did not keep), since its lanes consume
+// that source's envelopes themselves.  One thread; reads mapped host memory
+// (the queue) and, after an acquire, envelope headers.
+__device__ bool rx_queued_can_progress(const P2PRxQueue *rq, uint64_t me, const P2PRecvState *my_st0, int my_p,
+                                       const int64_t *aside, int naside) {
+  const uint64_t enq = __hip_atomic_load(&rq->enq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  bool fenced = false;
+  for (uint64_t L = me + 1; L <= enq && L <= me + P2P_Q; L++) {
+    const P2PQEntry *e = &rq->e[L % P2P_Q];
+    if (__hip_atomic_load(&e->launch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != L) continue;
+    if (!fenced) {
+      __atomic_thread_fence(__ATOMIC_ACQUIRE);   // the entries' fields, the envelopes
+      fenced = true;
+    }
+    const int n = e->n, src = e->src;
+    const int64_t tag = e->tag;
+    for (int q = src < 0 ? 0 : src; q < (src < 0 ? n : src + 1); q++) {
+      const P2PRecvState *s = e->st0 + q;
+      const bool own = my_p >= 0 && s == my_st0 + my_p;
+      if (own) {
+        for (int i = 0; i < naside; i++)
+          if ((tag < 0 || aside[i] == tag) && !reserved(e->disp, e->post, q, aside[i])) return true;
+      }
+      if (held_match(s, tag, e->disp, e->post, q).x >= 0) return true;
+      if (own) continue;
+      const uint64_t done = s->msgs_done;
+      const uint64_t posted = __hip_atomic_load(e->flag0 + P2P_POSTED + q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      if (posted <= done) continue;
+      if (tag < 0) return true;
+      __atomic_thread_fence(__ATOMIC_ACQUIRE);   // the envelopes before their `posted` count
+      const char *box = e->box0 + (size_t)q * P2P_BOX;
+      for (uint64_t m = done; m < posted && m < done + P2P_H; m++)
+        if ((int64_t)reinterpret_cast<const volatile uint64_t *>(box + (m % P2P_H) * P2P_HDR)[1] == tag) return true;
+    }
+  }
+  return false;
+}
+
+// may a receive posted as `post` yield (the displaced set has room for it,
+// or holds it already from an earlier launch)?
+__device__ __forceinline__ bool disp_room(const P2PDisplaced *d, uint64_t post) {
+  if (!d) return false;
+  const uint64_t n = d->n;
+  for (uint64_t i = 0; i < n && i < P2P_DISP_N; i++)
+    if (d->d[i].post == post) return true;
+  return n < P2P_DISP_N;
+}
+
+// how often a blocked receive asks whether to yield (wall-clock ticks, 100 MHz)
+constexpr uint64_t kYieldPollTicks = 500;
 
 // MX_ANY_SOURCE: wait until some source p has a message this receive can
 // take -- a matching held one, or, among the envelopes p has posted beyond
@@ -384,36 +467,62 @@ __device__ __forceinline__ int2 held_match(const P2PRecvState *st, int64_t tag) 
 // (pml/ob1 matches an ANY_SOURCE receive against every peer's queue).  The
 // envelope ring slots read here cannot be rewritten meanwhile: a sender
 // reuses slot m % P2P_H only after this process has consumed message m.
-__global__ void k_p2p_pick(const uint64_t *flag0, const P2PRecvState *st0, const char *box0, int n, int start,
-                           int64_t tag, int64_t *status, uint64_t timeout_ticks, int *err) {
+// Yielding (round 5): with a receive queued behind it that could take a
+// message, the pick stores -2 (its receive kernel then yields too); with
+// displaced receives in the communicator it reads envelope tags for
+// MPI_ANY_TAG as well, and skips messages they reserve.
+struct P2PPickArgs {
+  const uint64_t *flag0;
+  const P2PRecvState *st0;
+  const char *box0;
+  int n, start;
+  int64_t tag;
+  int64_t *status;
+  uint64_t timeout_ticks;
+  int *err;
+  uint64_t launch, post;
+  const P2PRxQueue *rq;
+  const P2PDisplaced *disp;
+};
+
+__global__ void k_p2p_pick(P2PPickArgs a) {
   if (threadIdx.x != 0) return;
+  const uint64_t *flag0 = a.flag0;
+  const P2PRecvState *st0 = a.st0;
+  const int n = a.n, start = a.start;
+  const int64_t tag = a.tag;
+  int64_t *status = a.status;
   const uint64_t t0 = wall_clock64();
   for (int i = 0; i < n; i++) {
     const int p = (start + i) % n;
-    if (held_match(st0 + p, tag).x >= 0) {
+    if (held_match(st0 + p, tag, a.disp, a.post, p).x >= 0) {
       __hip_atomic_store(&status[3], (int64_t)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
       return;
     }
   }
+  const bool filter = a.disp && a.disp->n > 0;   // reserved messages: read every tag
   // envelopes of source p already read without a match (< 64 sources): the
   // acquire before a scan invalidates the XCD's L2, so a source whose pending
   // messages carry other tags is not rescanned on every pass
   __shared__ uint64_t s_scanned[64];
   for (int p = 0; p < n && p < 64; p++) s_scanned[p] = 0;
+  uint64_t polled = t0;
   for (;;) {
     for (int i = 0; i < n; i++) {
       const int p = (start + i) % n;
       const uint64_t posted = __hip_atomic_load(flag0 + P2P_POSTED + p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
       const uint64_t m0 = st0[p].lane_msgs[0];
       if (posted <= m0) continue;
-      bool hit = tag < 0;
+      bool hit = tag < 0 && !filter;
       if (!hit) {
         if (p < 64 && posted <= s_scanned[p]) continue;
         if (p < 64) s_scanned[p] = posted;
         __atomic_thread_fence(__ATOMIC_ACQUIRE);   // the envelopes before their `posted` count
-        const char *box = box0 + (size_t)p * P2P_BOX;
-        for (uint64_t m = m0; !hit && m < posted && m < m0 + P2P_H; m++)
-          hit = (int64_t)reinterpret_cast<const volatile uint64_t *>(box + (m % P2P_H) * P2P_HDR)[1] == tag;
+        const char *box = a.box0 + (size_t)p * P2P_BOX;
+        for (uint64_t m = m0; !hit && m < posted && m < m0 + P2P_H; m++) {
+          const int64_t et = (int64_t)reinterpret_cast<const volatile uint64_t *>(box + (m % P2P_H) * P2P_HDR)[1];
+          hit = (tag < 0 || et == tag) && !reserved(a.disp, a.post, p, et);
+        }
       }
       if (hit) {
         __hip_atomic_store(&status[3], (int64_t)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
@@ -421,9 +530,17 @@ __global__ void k_p2p_pick(const uint64_t *flag0, const P2PRecvState *st0, const
       }
     }
     __builtin_amdgcn_s_sleep(2);
-    if (wall_clock64() - t0 > timeout_ticks) {
+    const uint64_t now = wall_clock64();
+    if (a.rq && now - polled > kYieldPollTicks) {
+      polled = now;
+      if (disp_room(a.disp, a.post) && rx_queued_can_progress(a.rq, a.launch, st0, -1, nullptr, 0)) {
+        __hip_atomic_store(&status[3], (int64_t)-2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        return;
+      }
+    }
+    if (wall_clock64() - t0 > a.timeout_ticks) {
       __hip_atomic_store(&status[3], (int64_t)-1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-      __hip_atomic_store(err, MX_ERR_TIMEOUT, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      __hip_atomic_store(a.err, MX_ERR_TIMEOUT, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
       return;
     }
   }
@@ -482,8 +599,42 @@ __device__ __forceinline__ int held_free(const P2PStashEntry *tab, int n, const 
   return -1;
 }
 
-// one lane of a receive; returns whether this lane stored user data
-__device__ __forceinline__ bool recv_body(const P2PRecvArgs &a, HoldPlan &plan, P2PRecvState **stp) {
+// Envelope k of this launch (the pair's envelope m), thread 0 of a lane:
+// 1 take it, 0 the launch stopped there (yield), -1 timed out.  The first
+// lane to see the envelope posted claims "go" for it in the device's
+// decision ring; the control workgroup claims "stop" for an envelope not
+// posted yet when a receive queued behind could progress; whichever claim
+// lands first holds for every lane.
+constexpr uint64_t kDecGo = 1, kDecStop = 2;
+__device__ __forceinline__ uint64_t dec_key(uint64_t launch, uint64_t k) {
+  return ((launch & 0xffffffffull) << 30) | (k & 0x3fffffffull);
+}
+__device__ int gate_wait(const P2PRecvArgs &a, const uint64_t *posted, uint64_t m, uint64_t k, uint64_t t0) {
+  uint64_t *w = a.dec + (k % P2P_DEC);
+  const uint64_t key = dec_key(a.launch, k);
+  for (;;) {
+    uint64_t v = __hip_atomic_load(w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if ((v >> 2) == key) {
+      if ((v & 3) != kDecGo) return 0;
+      __atomic_thread_fence(__ATOMIC_ACQUIRE);
+      return 1;
+    }
+    if (__hip_atomic_load(posted, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) > m) {
+      __hip_atomic_compare_exchange_strong(w, &v, (key << 2) | kDecGo, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
+                                           __HIP_MEMORY_SCOPE_AGENT);
+      continue;   // re-read: this claim or the other one
+    }
+    __builtin_amdgcn_s_sleep(2);
+    if (wall_clock64() - t0 > a.timeout_ticks) {
+      __hip_atomic_store(a.err, MX_ERR_TIMEOUT, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      return -1;
+    }
+  }
+}
+
+// one lane of a receive; returns whether this lane stored user data;
+// *yielded: the launch stopped at an envelope boundary (nothing delivered)
+__device__ __forceinline__ bool recv_body(const P2PRecvArgs &a, HoldPlan &plan, P2PRecvState **stp, bool *yielded) {
   const int l = blockIdx.x;
   const uint64_t t0 = wall_clock64();
   __shared__ int ok;
@@ -492,9 +643,11 @@ __device__ __forceinline__ bool recv_body(const P2PRecvArgs &a, HoldPlan &plan, 
   __shared__ uint64_t s_seq;
   __shared__ int s_rndv;
   int p = a.src;
+  *yielded = false;
   if (a.any) {
     p = (int)__hip_atomic_load(&a.status[3], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-    if (p < 0) return false;   // the pick timed out (error already raised)
+    if (p == -2) *yielded = true;   // the pick yielded
+    if (p < 0) return false;        // ... or timed out (error already raised)
   }
   const char *box = a.box0 + (size_t)p * P2P_BOX;
   const uint64_t *posted = a.flag0 + P2P_POSTED + p, *filled = a.flag0 + P2P_FILLED + (size_t)p * P2P_L;
@@ -526,7 +679,7 @@ __device__ __forceinline__ bool recv_body(const P2PRecvArgs &a, HoldPlan &plan, 
     }
   };
   // (1) a held message this receive matches: deliver it, consume no envelope
-  const int2 h = held_match(st, a.tag);
+  const int2 h = held_match(st, a.tag, a.disp, a.post, p);
   if (h.x >= 0) {
     if (threadIdx.x == 0) {
       plan.kind = h.x;
@@ -546,13 +699,15 @@ __device__ __forceinline__ bool recv_body(const P2PRecvArgs &a, HoldPlan &plan, 
     deliver_status(e.bytes, e.tag, 0);
     return wrote;
   }
-  // (2) envelopes in order: a mismatch is set aside (eager payload stashed,
-  // rendezvous envelope deferred) while a slot is free
+  // (2) envelopes in order: a mismatch (or a message an earlier displaced
+  // receive reserves) is set aside (eager payload stashed, rendezvous
+  // envelope deferred) while a slot is free
+  const uint64_t m0 = st->msgs_done;
   for (;;) {
     if (threadIdx.x == 0) {
       const uint64_t m = st->lane_msgs[l];
-      ok = p2p_wait_ge(posted, m + 1, t0, a.timeout_ticks, a.err);
-      if (ok) {
+      ok = a.rq ? gate_wait(a, posted, m, m - m0, t0) : p2p_wait_ge(posted, m + 1, t0, a.timeout_ticks, a.err);
+      if (ok == 1) {
         const volatile uint64_t *hd = reinterpret_cast<const volatile uint64_t *>(box + (m % P2P_H) * P2P_HDR);
         s_bytes = hd[0];
         s_tag = (int64_t)hd[1];
@@ -563,14 +718,18 @@ __device__ __forceinline__ bool recv_body(const P2PRecvArgs &a, HoldPlan &plan, 
       }
     }
     __syncthreads();
-    if (!ok) return wrote;
+    if (ok == 0 && a.rq) {    // stopped here: yield
+      *yielded = true;
+      return wrote;
+    }
+    if (ok != 1) return wrote;
     const uint64_t bytes = s_bytes;
     const int64_t tag = s_tag;
     const uint64_t seq = s_seq;
     const int rndv = s_rndv;
     __syncthreads();          // every thread has read the envelope before the next one
     int slot = -1;
-    if (a.tag >= 0 && tag != a.tag) {
+    if ((a.tag >= 0 && tag != a.tag) || reserved(a.disp, a.post, p, tag)) {
       slot = rndv ? held_free(st->defer, P2P_DEFER_N, plan, 1)
                   : bytes <= P2P_STASH_C ? held_free(st->stash, P2P_STASH_N, plan, 0) : -1;
     }
@@ -598,12 +757,60 @@ __device__ __forceinline__ bool recv_body(const P2PRecvArgs &a, HoldPlan &plan, 
     } else if (!recv_stream(l, 0, P2P_LE, bytes, a.buf, a.cap, box, filled, drained, st, t0, a, &wrote)) {
       return wrote;
     }
-    deliver_status(bytes, tag, (a.tag >= 0 && tag != a.tag) ? MX_ERR_TAG : 0);
+    deliver_status(bytes, tag, ((a.tag >= 0 && tag != a.tag) || reserved(a.disp, a.post, p, tag)) ? MX_ERR_TAG : 0);
     return wrote;
   }
 }
 
+// The control workgroup of a launch that may yield (the last workgroup, not
+// a lane): follows the envelopes the lanes take, and while the next one is
+// not posted asks every kYieldPollTicks whether a receive queued behind
+// could progress -- if so it claims "stop" there.  Ends with the lanes.
+__device__ void rx_control(const P2PRecvArgs &a) {
+  if (threadIdx.x != 0) return;
+  int p = a.src;
+  if (a.any) p = (int)__hip_atomic_load(&a.status[3], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  if (p < 0) return;
+  const P2PRecvState *st = a.st0 + p;
+  const uint64_t *posted = a.flag0 + P2P_POSTED + p;
+  const char *box = a.box0 + (size_t)p * P2P_BOX;
+  const uint64_t m0 = st->msgs_done;
+  int64_t aside[P2P_STASH_N + P2P_DEFER_N];
+  int naside = 0;
+  uint64_t k = 0, polled = wall_clock64();
+  for (;;) {
+    if (__hip_atomic_load(a.fin.lanes, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= a.fin.target) return;
+    uint64_t *w = a.dec + (k % P2P_DEC);
+    uint64_t v = __hip_atomic_load(w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const uint64_t key = dec_key(a.launch, k);
+    if ((v >> 2) == key) {
+      if ((v & 3) != kDecGo) return;
+      // taken and the lanes go on: it was not this receive's message
+      __atomic_thread_fence(__ATOMIC_ACQUIRE);
+      if (naside < P2P_STASH_N + P2P_DEFER_N)
+        aside[naside++] = (int64_t)reinterpret_cast<const volatile uint64_t *>(box + ((m0 + k) % P2P_H) * P2P_HDR)[1];
+      k++;
+      continue;
+    }
+    __builtin_amdgcn_s_sleep(2);
+    if (__hip_atomic_load(posted, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) > m0 + k) continue;   // lanes take it
+    const uint64_t now = wall_clock64();
+    if (now - polled < kYieldPollTicks) continue;
+    polled = now;
+    if (disp_room(a.disp, a.post) && rx_queued_can_progress(a.rq, a.launch, a.st0, p, aside, naside) &&
+        __hip_atomic_compare_exchange_strong(w, &v, (key << 2) | kDecStop, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
+                                             __HIP_MEMORY_SCOPE_AGENT))
+      return;
+  }
+}
+
+// workgroups [0, P2P_L) are the lanes; with a launch queue one more, the
+// control workgroup (rx_control)
 __global__ void __launch_bounds__(kP2PThreads) k_p2p_recv(P2PRecvArgs a) {
+  if (blockIdx.x >= P2P_L) {
+    rx_control(a);
+    return;
+  }
   __shared__ HoldPlan plan;
   if (threadIdx.x == 0) {
     plan.kind = plan.hit = -1;
@@ -611,7 +818,8 @@ __global__ void __launch_bounds__(kP2PThreads) k_p2p_recv(P2PRecvArgs a) {
   }
   __syncthreads();
   P2PRecvState *st = nullptr;
-  const bool wrote = recv_body(a, plan, &st);
+  bool yielded = false;
+  const bool wrote = recv_body(a, plan, &st, &yielded);
   // the last lane out commits the held-table changes (the tables are read by
   // every lane during the kernel, so they only change between kernels)
   __syncthreads();
@@ -629,9 +837,32 @@ __global__ void __launch_bounds__(kP2PThreads) k_p2p_recv(P2PRecvArgs a) {
           e.seq = plan.seq[j];
           e.valid = 1;
         }
-        __threadfence();
+        st->msgs_done = st->lane_msgs[blockIdx.x];
       }
-      if (a.fin.done) __hip_atomic_store(a.fin.done, (int64_t)1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      if (P2PDisplaced *d = a.disp) {   // join or leave the displaced receives
+        const uint64_t n = d->n;
+        uint64_t at = n;
+        for (uint64_t i = 0; i < n; i++)
+          if (d->d[i].post == a.post) at = i;
+        if (yielded && at == n && n < P2P_DISP_N) {
+          d->d[n].post = a.post;
+          d->d[n].src = a.any ? -1 : a.src;
+          d->d[n].tag = a.tag;
+          d->n = n + 1;
+        } else if (!yielded && at < n) {
+          d->d[at] = d->d[n - 1];
+          d->n = n - 1;
+        }
+      }
+      __threadfence();
+      if (yielded) {   // the host launches this receive again (p2p_progress)
+        __hip_atomic_store(&a.status[5], (int64_t)a.launch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        __threadfence_system();
+        __hip_atomic_store(const_cast<uint64_t *>(&a.rq->yields), a.launch, __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_SYSTEM);
+      } else if (a.fin.done) {
+        __hip_atomic_store(a.fin.done, (int64_t)1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      }
     }
   }
 }
@@ -667,6 +898,28 @@ static hipError_t p2p_stream_create(hipStream_t *s) {
 // send of one communicator would hold back a cleared send of another.
 static std::mutex g_chan_mu;
 static hipStream_t g_chan[64][2];
+
+// Per device, like the receive stream the receive kernels share: the launch
+// queue a blocked receive reads (mapped host), the decision ring (device),
+// and the receive requests in flight in the order of their first launch
+// (the host launches yielded ones again in that order, p2p_progress).
+// MX_P2P_YIELD=0: receives never yield (each blocks the receive stream
+// until its message comes -- the round-4 behaviour).
+struct RxDev {
+  P2PRxQueue *rq = nullptr, *rq_dev = nullptr;
+  uint64_t *dec = nullptr;
+  uint64_t launches = 0, seen = 0;
+  std::vector<mx_request *> active;
+};
+static RxDev g_rx[64];
+static int g_rx_dev[64], g_rx_ndev;
+static bool rx_yield_on() {
+  static const bool on = [] {
+    const char *e = getenv("MX_P2P_YIELD");
+    return !(e && *e == '0');
+  }();
+  return on;
+}
 static int p2p_channels(hipStream_t out[3]) {
   int dev = g_device;
   if (dev < 0 && hipGetDevice(&dev) != hipSuccess) return MX_ERR_HIP;
@@ -720,10 +973,33 @@ int p2p_setup(mx_comm *c) {
       (c->p2p_stash = (char *)pool_dev_get(p2p_stash_bytes(c))) != nullptr &&
       (c->p2p_rndv_cur = (P2PRndvCur *)pool_dev_get(sizeof(P2PRndvCur))) != nullptr &&
       (c->p2p_rndv = (P2PRndvTable *)pool_host_get(sizeof(P2PRndvTable))) != nullptr &&
-      hipHostGetDevicePointer((void **)&c->p2p_rndv_dev, c->p2p_rndv, 0) == hipSuccess;
+      hipHostGetDevicePointer((void **)&c->p2p_rndv_dev, c->p2p_rndv, 0) == hipSuccess &&
+      (c->p2p_disp = (P2PDisplaced *)pool_dev_get(sizeof(P2PDisplaced))) != nullptr;
   if (!ok) {
     p2p_release(c);
     return MX_ERR_NOMEM;
+  }
+  c->p2p_posts = 0;
+  if (rx_yield_on() && c->device >= 0 && c->device < 64) {
+    std::lock_guard<std::mutex> lk(g_chan_mu);
+    RxDev &D = g_rx[c->device];
+    if (!D.rq) {
+      P2PRxQueue *rq = (P2PRxQueue *)pool_host_get(sizeof(P2PRxQueue));
+      uint64_t *dec = (uint64_t *)pool_dev_get(P2P_DEC * sizeof(uint64_t));
+      P2PRxQueue *rq_dev = nullptr;
+      if (!rq || !dec || hipHostGetDevicePointer((void **)&rq_dev, rq, 0) != hipSuccess ||
+          hipMemsetAsync(dec, 0, P2P_DEC * sizeof(uint64_t), ls) != hipSuccess) {
+        if (rq) pool_host_put(rq, sizeof(P2PRxQueue));
+        if (dec) pool_dev_put(dec, P2P_DEC * sizeof(uint64_t));
+        p2p_release(c);
+        return MX_ERR_NOMEM;
+      }
+      memset(rq, 0, sizeof(P2PRxQueue));
+      D.rq = rq;
+      D.rq_dev = rq_dev;
+      D.dec = dec;
+      g_rx_dev[g_rx_ndev++] = c->device;
+    }
   }
   memset(c->p2p_rndv, 0, sizeof(P2PRndvTable));
   c->p2p_rndv_gen = 0;
@@ -734,6 +1010,7 @@ int p2p_setup(mx_comm *c) {
   if (hipMemsetAsync(c->p2p_send, 0, sb, ls) != hipSuccess || hipMemsetAsync(c->p2p_recv, 0, rb, ls) != hipSuccess ||
       hipMemsetAsync(c->p2p_lanes, 0, 3 * sizeof(uint64_t), ls) != hipSuccess ||
       hipMemsetAsync(c->p2p_rndv_cur, 0, sizeof(P2PRndvCur), ls) != hipSuccess ||
+      hipMemsetAsync(c->p2p_disp, 0, sizeof(P2PDisplaced), ls) != hipSuccess ||
       p2p_channels(c->p2p_stream) != MX_SUCCESS ||
       hipEventCreateWithFlags(&c->p2p_last[0], hipEventDisableTiming) != hipSuccess ||
       hipEventCreateWithFlags(&c->p2p_last[1], hipEventDisableTiming) != hipSuccess ||
@@ -780,6 +1057,8 @@ void p2p_release(mx_comm *c) {
   pool_dev_put(c->p2p_lanes, 3 * sizeof(uint64_t));
   pool_dev_put(c->p2p_stash, p2p_stash_bytes(c));
   pool_dev_put(c->p2p_rndv_cur, sizeof(P2PRndvCur));
+  pool_dev_put(c->p2p_disp, sizeof(P2PDisplaced));
+  c->p2p_disp = nullptr;
   pool_host_put(c->p2p_rndv, sizeof(P2PRndvTable));
   delete c->p2p_rndv_free;
   c->p2p_rndv_free = nullptr;
@@ -800,8 +1079,24 @@ void p2p_finish(mx_request *q) {
     c->p2p_rndv_free->push_back(q->rndv - 1);
   }
   q->rndv = 0;
-  if (q->tmp) (void)hipFreeAsync(q->tmp, c->p2p_stream[2] ? c->p2p_stream[2] : nullptr);
+  const int ch = q->kind == RQ_RECV ? 1 : 2;
+  if (q->tmp) (void)hipFreeAsync(q->tmp, c->p2p_stream[ch] ? c->p2p_stream[ch] : nullptr);
   q->tmp = nullptr;
+  if (q->kind == RQ_RECV) {
+    if (c->device >= 0 && c->device < 64) {
+      std::vector<mx_request *> &v = g_rx[c->device].active;
+      const auto it = std::find(v.begin(), v.end(), q);
+      if (it != v.end()) v.erase(it);
+    }
+    delete static_cast<P2PRecvArgs *>(q->rx);
+    q->rx = nullptr;
+    q->launch = 0;
+  }
+}
+
+bool p2p_yielded(const mx_request *q) {
+  return q->kind == RQ_RECV && q->status && q->launch &&
+         __atomic_load_n(&q->status[5], __ATOMIC_ACQUIRE) == (int64_t)q->launch;
 }
 
 namespace {
@@ -860,6 +1155,8 @@ void p2p_status_put(int64_t *st) {
   }
   (void)hipHostFree(st);
 }
+
+int p2p_rx_launch(mx_request *q);
 
 // Enqueue request q (RQ_SEND / RQ_RECV) on the internal stream, after the
 // caller's stream; *done_stream receives the stream completion is on.
@@ -965,37 +1262,123 @@ int p2p_enqueue(mx_request *q, hipStream_t *done_stream) {
     }
   } else {
     q->status[3] = p;
-    P2PRecvArgs a;
+    P2PRecvArgs *ap = static_cast<P2PRecvArgs *>(q->rx);
+    if (!ap && !(ap = new (std::nothrow) P2PRecvArgs())) {
+      if (tmp) (void)hipFreeAsync(tmp, s);
+      return MX_ERR_NOMEM;
+    }
+    q->rx = ap;
+    P2PRecvArgs &a = *ap;
     memset(&a, 0, sizeof a);
     a.buf = tmp ? tmp : (char *)q->rbuf;
     a.cap = bytes;
     a.tag = q->tag;
     a.src = p;
+    a.any = p < 0;
     a.me = me;
     a.box0 = c->staging + c->p2p_off;
     a.flag0 = c->flagmem;
     for (int j = 0; j < c->size; j++) a.peer_flags[j] = c->peer_flags[j];
     a.st0 = c->p2p_recv;
     a.stash0 = c->p2p_stash;
-    if (p < 0) {   // MX_ANY_SOURCE
-      a.any = 1;
-      const int start = (int)(c->p2p_any_rr++ % (unsigned)c->size);
-      hipLaunchKernelGGL(k_p2p_pick, dim3(1), dim3(64), 0, s, (const uint64_t *)c->flagmem,
-                         (const P2PRecvState *)c->p2p_recv, (const char *)(c->staging + c->p2p_off), c->size,
-                         start, (int64_t)q->tag, st_dev, c->timeout_ticks, c->err_dev);
-      if ((rc = mx_check_launch())) return rc;
-    }
     a.status = st_dev;
     a.timeout_ticks = c->timeout_ticks;
     a.err = c->err_dev;
-    a.fin = fin;
-    hipLaunchKernelGGL(k_p2p_recv, dim3(P2P_L), dim3(kP2PThreads), 0, s, a);
-    if ((rc = mx_check_launch())) return rc;
-    if (tmp && (rc = mx_unpack(q->ddt, q->count, q->rbuf, tmp, 0, bytes, s))) return rc;
-    if ((rc = p2p_note(c, 1))) return rc;
+    q->tmp = tmp;   // freed at completion: a receive that yields runs (and unpacks) again
+    q->post = ++c->p2p_posts;
+    c->p2p_ltot[dir] -= nl;   // p2p_rx_launch counts the lanes of each launch
+    if ((rc = p2p_rx_launch(q))) {
+      p2p_finish(q);
+      return rc;
+    }
+    if (g_rx[c->device].rq) g_rx[c->device].active.push_back(q);
+    return MX_SUCCESS;
   }
   if (tmp) (void)hipFreeAsync(tmp, s);
   return MX_SUCCESS;
+}
+
+// One launch of receive q on the receive stream: the pick (MPI_ANY_SOURCE),
+// the receive kernel, the unpack (a datatype).  With yielding on, the launch
+// is first published in the device's launch queue, so a receive blocked
+// ahead of it can see it; the kernel gets one workgroup more (rx_control).
+int p2p_rx_launch(mx_request *q) {
+  mx_comm *c = q->c;
+  hipStream_t s = c->p2p_stream[1];
+  P2PRecvArgs &a = *static_cast<P2PRecvArgs *>(q->rx);
+  RxDev &D = g_rx[c->device];
+  a.launch = a.post = 0;
+  a.rq = nullptr;
+  a.dec = nullptr;
+  a.disp = nullptr;
+  if (D.rq) {
+    const uint64_t L = ++D.launches;
+    P2PQEntry &e = D.rq->e[L % P2P_Q];
+    __atomic_store_n(&e.launch, (uint64_t)0, __ATOMIC_RELAXED);
+    e.post = q->post;
+    e.flag0 = c->flagmem;
+    e.st0 = c->p2p_recv;
+    e.box0 = c->staging + c->p2p_off;
+    e.disp = c->p2p_disp;
+    e.n = c->size;
+    e.src = a.src;
+    e.tag = a.tag;
+    __atomic_store_n(&e.launch, L, __ATOMIC_RELEASE);
+    __atomic_store_n(&D.rq->enq, L, __ATOMIC_RELEASE);
+    a.launch = L;
+    a.post = q->post;
+    a.rq = D.rq_dev;
+    a.dec = D.dec;
+    a.disp = c->p2p_disp;
+  }
+  q->launch = a.launch;
+  a.fin.lanes = c->p2p_lanes + 1;
+  a.fin.target = c->p2p_ltot[1] + P2P_L;
+  a.fin.done = q->fast == 1 ? a.status + 4 : nullptr;
+  c->p2p_ltot[1] += P2P_L;
+  int rc;
+  if (a.any) {
+    P2PPickArgs pa;
+    memset(&pa, 0, sizeof pa);
+    pa.flag0 = c->flagmem;
+    pa.st0 = c->p2p_recv;
+    pa.box0 = c->staging + c->p2p_off;
+    pa.n = c->size;
+    pa.start = (int)(c->p2p_any_rr++ % (unsigned)c->size);
+    pa.tag = a.tag;
+    pa.status = a.status;
+    pa.timeout_ticks = c->timeout_ticks;
+    pa.err = c->err_dev;
+    pa.launch = a.launch;
+    pa.post = a.post;
+    pa.rq = a.rq;
+    pa.disp = a.disp;
+    hipLaunchKernelGGL(k_p2p_pick, dim3(1), dim3(64), 0, s, pa);
+    if ((rc = mx_check_launch())) return rc;
+  }
+  hipLaunchKernelGGL(k_p2p_recv, dim3(a.rq ? P2P_L + 1 : P2P_L), dim3(kP2PThreads), 0, s, a);
+  if ((rc = mx_check_launch())) return rc;
+  if (q->tmp && (rc = mx_unpack(q->ddt, q->count, q->rbuf, q->tmp, 0, a.cap, s))) return rc;
+  return p2p_note(c, 1);
+}
+
+// Launch again every receive whose last launch yielded, in the order of
+// their first launches (the kernels record the latest yield in the queue,
+// so nothing is scanned while no receive yielded).
+void p2p_progress() {
+  for (int i = 0; i < g_rx_ndev; i++) {
+    RxDev &D = g_rx[g_rx_dev[i]];
+    if (!D.rq || D.active.empty()) continue;
+    const uint64_t y = __atomic_load_n(&D.rq->yields, __ATOMIC_ACQUIRE);
+    if (y == D.seen) continue;
+    D.seen = y;
+    for (size_t j = 0; j < D.active.size(); j++) {
+      mx_request *q = D.active[j];
+      if (!q->active || !p2p_yielded(q)) continue;
+      if (p2p_rx_launch(q) == MX_SUCCESS)
+        (void)hipEventRecord(q->done, q->c->p2p_stream[1]);
+    }
+  }
 }
 
 }  // namespace mx
