@@ -195,6 +195,8 @@ typedef struct mx_coll_stats {
     uint64_t reg_fast_calls;   /* registration exchanges that found every
                                   rank's buffers as in the last one (one
                                   host round instead of two)                */
+    uint64_t p2p_relaunches;   /* receive launches that yielded to receives
+                                  posted after them and were launched again */
 } mx_coll_stats_t;
 int mx_comm_set_profiling(mx_comm_t *comm, int on);
 int mx_comm_get_stats(mx_comm_t *comm, mx_coll_stats_t *stats, int reset);

@@ -607,6 +607,7 @@ def _yield_worker(rank, n, port, q):
                 r.wait()
                 r.free()
             res[("halo", it)] = (fl.cpu().numpy().tobytes(), fr.cpu().numpy().tobytes())
+        res["relaunch_halo"] = A.stats(reset=True)["p2p_relaunches"]
         dist.barrier()
 
         # (2) one source, tags crossed: the second-posted receive's message comes first
@@ -616,6 +617,7 @@ def _yield_worker(rank, n, port, q):
             rb = A.irecv(bb.data_ptr(), BIG, 1, tag=11)
             ra.wait(); rb.wait(); ra.free(); rb.free()
             res["cross"] = (ba.cpu().numpy().tobytes(), bb.cpu().numpy().tobytes())
+            res["relaunch_cross"] = A.stats(reset=True)["p2p_relaunches"]
         elif rank == 1:
             A.send(_dev(_data(511, BIG)).data_ptr(), BIG, 0, tag=11)
             A.send(_dev(_data(510, BIG)).data_ptr(), BIG, 0, tag=10)
@@ -628,6 +630,7 @@ def _yield_worker(rank, n, port, q):
             rb = B.irecv(bb.data_ptr(), BIG, 1, tag=6)
             rb.wait(); ra.wait(); ra.free(); rb.free()
             res["comms"] = (ba.cpu().numpy().tobytes(), bb.cpu().numpy().tobytes())
+            res["relaunch_comms"] = A.stats(reset=True)["p2p_relaunches"] + B.stats(reset=True)["p2p_relaunches"]
         elif rank == 1:
             B.send(_dev(_data(606, BIG)).data_ptr(), BIG, 0, tag=6)
             A.send(_dev(_data(605, BIG)).data_ptr(), BIG, 0, tag=5)
@@ -648,6 +651,7 @@ def _yield_worker(rank, n, port, q):
             for r in (r1, r2, r3):
                 r.free()
             res["order"] = (st, [b.cpu().numpy().tobytes() for b in (b1, b2, b3)])
+            res["relaunch_order"] = A.stats(reset=True)["p2p_relaunches"]
         elif rank == 2:
             A.send(_dev(_data(708, BIG)).data_ptr(), BIG, 0, tag=8)
             dist.send(torch.ones(1), dst=1)          # R1 has yielded by now
@@ -665,6 +669,7 @@ def _yield_worker(rank, n, port, q):
             rb = A.irecv(bb.data_ptr(), BIG, 2, tag=21)
             rb.wait(); ra.wait()
             res["any"] = (ra.source(), ba.cpu().numpy().tobytes(), bb.cpu().numpy().tobytes())
+            res["relaunch_any"] = A.stats(reset=True)["p2p_relaunches"]
             ra.free(); rb.free()
         elif rank == 2:
             A.send(_dev(_data(821, BIG)).data_ptr(), BIG, 0, tag=21)
@@ -716,3 +721,152 @@ def test_receives_yield_to_receives_posted_after_them():
     assert data == [_data(701, BIG).tobytes(), _data(708, BIG).tobytes(), _data(702, BIG).tobytes()]
     src, da, db = got[0]["any"]
     assert src == 1 and da == _data(820, BIG).tobytes() and db == _data(821, BIG).tobytes()
+    # the yields happened: a receive launched again in every case (the halo
+    # on some rank: whose receive waits first depends on timing)
+    assert sum(got[r]["relaunch_halo"] for r in range(n)) >= 1
+    for case in ("cross", "comms", "order", "any"):
+        assert got[0]["relaunch_" + case] >= 1, (case, got[0]["relaunch_" + case])
+    assert got[0]["relaunch_order"] >= 2      # R1, then R3 behind R1's second launch
+
+
+def _yield_worker2(rank, n, port, q):
+    """A datatype receive, a persistent receive and mx_test-driven progress
+    across a yield, and the order rule with eager messages (set aside in the
+    device stash rather than deferred)."""
+    import torch.distributed as dist
+    os.environ["HSA_ENABLE_IPC_MODE_LEGACY"] = "0"
+    try:
+        dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=n)
+        torch.cuda.set_device(0)
+        mxompi.init(0)
+
+        def ag(b):
+            out = [None] * n
+            dist.all_gather_object(out, b)
+            return out
+
+        A = mxompi.Comm(rank, n, ag, device=0, staging_bytes=1 << 20)
+        A.set_timeout(30.0)
+        res = {}
+
+        def buf(nb=BIG):
+            return torch.zeros(nb, dtype=torch.uint8, device="cuda")
+
+        def first_from_2_then_1(tag2, tag1, nb1, payload1):
+            """rank 2 sends (blocking) first; rank 1 sends only after it"""
+            if rank == 2:
+                A.send(_dev(_data(900 + tag2, BIG)).data_ptr(), BIG, 0, tag=tag2)
+                dist.send(torch.ones(1), dst=1)
+            elif rank == 1:
+                dist.recv(torch.zeros(1), src=2)
+                A.send(_dev(payload1).data_ptr(), nb1, 0, tag=tag1)
+
+        # (1) a datatype receive yields, runs again, unpacks once more
+        tv = REC["vector_f64_b3_s5"]
+        dt = mxompi.Datatype(tv["desc"].tobytes(), tv["nrec"], tv["size"], tv["lb"], tv["ub"])
+        nbp = tv["size"] * tv["count"]
+        if rank == 0:
+            ub = _dev(tv["prefill"])
+            r1 = A.irecv_ddt(ub.data_ptr() - tv["true_lb"], tv["count"], dt, 1, tag=30)
+            b2 = buf()
+            r2 = A.irecv(b2.data_ptr(), BIG, 2, tag=31)
+            r2.wait(); r1.wait(); r1.free(); r2.free()
+            res["ddt"] = (ub.cpu().numpy().tobytes(), b2.cpu().numpy().tobytes())
+            res["relaunch_ddt"] = A.stats(reset=True)["p2p_relaunches"]
+        first_from_2_then_1(31, 30, nbp, tv["packed"])
+        dist.barrier()
+
+        # (2) progress from mx_test only
+        if rank == 0:
+            b1, b2 = buf(), buf()
+            r1 = A.irecv(b1.data_ptr(), BIG, 1, tag=40)
+            r2 = A.irecv(b2.data_ptr(), BIG, 2, tag=41)
+            import time
+            t0 = time.time()
+            while not (r1.test() and r2.test()):
+                assert time.time() - t0 < 60
+            r1.free(); r2.free()
+            res["test"] = (b1.cpu().numpy().tobytes(), b2.cpu().numpy().tobytes())
+            res["relaunch_test"] = A.stats(reset=True)["p2p_relaunches"]
+        first_from_2_then_1(41, 40, BIG, _data(940, BIG))
+        dist.barrier()
+
+        # (3) a persistent receive yields on each of its starts
+        pb = buf()
+        if rank == 0:
+            pr = A.irecv(pb.data_ptr(), BIG, 1, tag=50, persistent=True)
+        reps = []
+        for it in range(2):
+            if rank == 0:
+                pr.start()
+                b2 = buf()
+                r2 = A.irecv(b2.data_ptr(), BIG, 2, tag=51)
+                r2.wait(); pr.wait(); r2.free()
+                reps.append(pb.cpu().numpy().tobytes())
+            first_from_2_then_1(51, 50, BIG, _data(950 + it, BIG))
+            dist.barrier()
+        if rank == 0:
+            pr.free()
+            res["persistent"] = reps
+            res["relaunch_persistent"] = A.stats(reset=True)["p2p_relaunches"]
+
+        # (4) the order rule with eager messages: both of source 1's tag-7
+        # messages land in the stash while R1 is displaced
+        E = 64 << 10
+        if rank == 0:
+            b1, b2, b3 = buf(E), buf(), buf(E)
+            r1 = A.irecv(b1.data_ptr(), E, 1, tag=7)
+            r2 = A.irecv(b2.data_ptr(), BIG, 2, tag=8)
+            r3 = A.irecv(b3.data_ptr(), E, 1, tag=7)
+            r2.wait(); r1.wait(); r3.wait()
+            res["order"] = [b.cpu().numpy().tobytes() for b in (b1, b3)]
+            res["relaunch_order"] = A.stats(reset=True)["p2p_relaunches"]
+            for r in (r1, r2, r3):
+                r.free()
+        elif rank == 2:
+            A.send(_dev(_data(908, BIG)).data_ptr(), BIG, 0, tag=8)
+            dist.send(torch.ones(1), dst=1)
+        elif rank == 1:
+            dist.recv(torch.zeros(1), src=2)
+            A.send(_dev(_data(971, E)).data_ptr(), E, 0, tag=7)
+            A.send(_dev(_data(972, E)).data_ptr(), E, 0, tag=7)
+        dist.barrier()
+        dt.close()
+        A.close()
+        dist.destroy_process_group()
+        q.put((rank, "ok", res))
+    except Exception as e:  # noqa: BLE001
+        import traceback
+        q.put((rank, "err", traceback.format_exc() + str(e)))
+
+
+def test_yield_with_datatypes_test_polling_and_persistent():
+    import torch.multiprocessing as mp
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    n = 3
+    procs = [ctx.Process(target=_yield_worker2, args=(r, n, port, q)) for r in range(n)]
+    for p in procs:
+        p.start()
+    got = {}
+    try:
+        for _ in range(n):
+            rank, status, payload = q.get(timeout=200)
+            assert status == "ok", payload
+            got[rank] = payload
+    finally:
+        for p in procs:
+            p.join(timeout=30 if len(got) == n else 5)
+            if p.is_alive():
+                p.terminate()
+                p.join(timeout=10)
+    tv = REC["vector_f64_b3_s5"]
+    ub, b2 = got[0]["ddt"]
+    np.testing.assert_array_equal(np.frombuffer(ub, np.uint8), tv["unpacked"])
+    assert b2 == _data(931, BIG).tobytes()
+    assert got[0]["test"] == (_data(940, BIG).tobytes(), _data(941, BIG).tobytes())
+    assert got[0]["persistent"] == [_data(950, BIG).tobytes(), _data(951, BIG).tobytes()]
+    assert got[0]["order"] == [_data(971, 64 << 10).tobytes(), _data(972, 64 << 10).tobytes()]
+    for case, least in (("ddt", 1), ("test", 1), ("persistent", 2), ("order", 2)):
+        assert got[0]["relaunch_" + case] >= least, (case, got[0]["relaunch_" + case])

@@ -1375,8 +1375,10 @@ void p2p_progress() {
     for (size_t j = 0; j < D.active.size(); j++) {
       mx_request *q = D.active[j];
       if (!q->active || !p2p_yielded(q)) continue;
-      if (p2p_rx_launch(q) == MX_SUCCESS)
+      if (p2p_rx_launch(q) == MX_SUCCESS) {
         (void)hipEventRecord(q->done, q->c->p2p_stream[1]);
+        q->c->st.p2p_relaunches++;
+      }
     }
   }
 }
