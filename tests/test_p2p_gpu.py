@@ -678,6 +678,30 @@ def _yield_worker(rank, n, port, q):
             dist.recv(torch.zeros(1), src=2)
             A.send(_dev(_data(820, BIG)).data_ptr(), BIG, 0, tag=20)
         dist.barrier()
+
+        # (6) a blocking collective progresses a yielded receive: rank 0
+        # enters an allreduce with R1 yielded; rank 1 joins it only after its
+        # blocking send to R1 completed
+        x = torch.full((1024,), rank + 1, dtype=torch.int32, device="cuda")
+        y = torch.zeros_like(x)
+        if rank == 0:
+            ba, bb = buf(), buf()
+            ra = A.irecv(ba.data_ptr(), BIG, 1, tag=60)
+            rb = A.irecv(bb.data_ptr(), BIG, 2, tag=61)
+            B.allreduce(x.data_ptr(), y.data_ptr(), 1024, "INT32_T", "SUM")
+            ra.wait(); rb.wait()
+            res["coll"] = (ba.cpu().numpy().tobytes(), bb.cpu().numpy().tobytes(), int(y[0]),
+                           A.stats(reset=True)["p2p_relaunches"])
+            ra.free(); rb.free()
+        else:
+            if rank == 2:
+                A.send(_dev(_data(861, BIG)).data_ptr(), BIG, 0, tag=61)
+                dist.send(torch.ones(1), dst=1)
+            else:
+                dist.recv(torch.zeros(1), src=2)
+                A.send(_dev(_data(860, BIG)).data_ptr(), BIG, 0, tag=60)
+            B.allreduce(x.data_ptr(), y.data_ptr(), 1024, "INT32_T", "SUM")
+        dist.barrier()
         B.close()
         A.close()
         dist.destroy_process_group()
@@ -727,6 +751,9 @@ def test_receives_yield_to_receives_posted_after_them():
     for case in ("cross", "comms", "order", "any"):
         assert got[0]["relaunch_" + case] >= 1, (case, got[0]["relaunch_" + case])
     assert got[0]["relaunch_order"] >= 2      # R1, then R3 behind R1's second launch
+    ca, cb, total, relaunched = got[0]["coll"]
+    assert ca == _data(860, BIG).tobytes() and cb == _data(861, BIG).tobytes() and total == 6
+    assert relaunched >= 1
 
 
 def _yield_worker2(rank, n, port, q):

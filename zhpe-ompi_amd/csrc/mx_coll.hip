@@ -1214,7 +1214,21 @@ static void timeout_dump(mx_comm *c, const char *where) {
 // true) before its launch), else the marker kernel
 static int finish(mx_comm *c, hipStream_t s, const Mark *mk = nullptr) {
   if (c->defer) return MX_SUCCESS;   // request path: completion through the request's event
-  if (mk && (mk->flags || mk->word)) {
+  if (mx::p2p_rx_active()) {
+    // receives of this process are in flight: a peer may be in a blocking
+    // send that waits for one of them to be launched again after a yield
+    // (mx_p2p.hip) before it joins this collective, so the wait
+    // polls the stream and progresses them instead of blocking
+    const auto t0 = std::chrono::steady_clock::now();
+    for (;;) {
+      mx::p2p_progress();
+      const hipError_t e = hipStreamQuery(s);
+      if (e == hipSuccess) break;
+      if (e != hipErrorNotReady) return MX_ERR_HIP;
+      if (std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0).count() > 2000.0)
+        std::this_thread::sleep_for(std::chrono::microseconds(20));
+    }
+  } else if (mk && (mk->flags || mk->word)) {
     if (mark_wait(*mk, s) != MX_SUCCESS) return MX_ERR_HIP;
   } else if (fast_sync() ? mx_stream_sync_fast(s) != MX_SUCCESS : hipStreamSynchronize(s) != hipSuccess) {
     return MX_ERR_HIP;

@@ -323,6 +323,8 @@ void p2p_finish(mx_request *q);
 void p2p_progress();
 // a receive request's current launch yielded (it is not complete)
 bool p2p_yielded(const mx_request *q);
+// some receive of this process is in flight (its launches may yield)
+bool p2p_rx_active();
 // status blocks (P2P_STATUS_WORDS x int64, mapped host memory): from a process-wide
 // pool allocated once (never released, so a request may outlive its
 // communicator), else one hipHostMalloc each

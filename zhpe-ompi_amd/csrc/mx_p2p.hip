@@ -1362,6 +1362,12 @@ int p2p_rx_launch(mx_request *q) {
   return p2p_note(c, 1);
 }
 
+bool p2p_rx_active() {
+  for (int i = 0; i < g_rx_ndev; i++)
+    if (!g_rx[g_rx_dev[i]].active.empty()) return true;
+  return false;
+}
+
 // Launch again every receive whose last launch yielded, in the order of
 // their first launches (the kernels record the latest yield in the queue,
 // so nothing is scanned while no receive yielded).
