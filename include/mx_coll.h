@@ -364,6 +364,21 @@ int mx_startall(size_t n, mx_request_t *const *reqs);
  * persistent request); the return value is the operation's status. */
 int mx_test(mx_request_t *req, int *flag);
 int mx_wait(mx_request_t *req);
+/* MPI_Waitall / MPI_Waitany / MPI_Testall / MPI_Testany over an array of
+ * requests (ompi_request_default_wait_all / _wait_any, ompi/request/
+ * req_wait.c:84-383; _test_any / _test_all, req_test.c:105-294).  Null and
+ * inactive entries are skipped; completed requests become inactive (free them
+ * with mx_request_free, as after mx_wait).  Waitall completes every request
+ * and returns the first error among them.  Waitany / Testany: *index of the
+ * request completed, MX_UNDEFINED when none is active (Testany: *flag = 1
+ * then).  Testall completes the requests only when every one is complete
+ * (*flag = 1); otherwise nothing changes.  Every pass progresses yielded
+ * receives. */
+#define MX_UNDEFINED (-32766)   /* MPI_UNDEFINED, mpi.h.in:488 */
+int mx_waitall(size_t n, mx_request_t *const *reqs);
+int mx_waitany(size_t n, mx_request_t *const *reqs, int *index);
+int mx_testall(size_t n, mx_request_t *const *reqs, int *flag);
+int mx_testany(size_t n, mx_request_t *const *reqs, int *index, int *flag);
 /* Make `stream` wait for the request on the device, without a host wait. */
 int mx_request_stream_wait(mx_request_t *req, void *stream);
 int mx_request_is_active(const mx_request_t *req);

@@ -858,6 +858,34 @@ def _yield_worker2(rank, n, port, q):
             A.send(_dev(_data(971, E)).data_ptr(), E, 0, tag=7)
             A.send(_dev(_data(972, E)).data_ptr(), E, 0, tag=7)
         dist.barrier()
+
+        # (5) MPI_Waitall / Waitany / Testall / Testany over receives that
+        # yield (ompi/request/req_wait.c, req_test.c semantics)
+        if rank == 0:
+            b1, b2 = buf(), buf()
+            r1 = A.irecv(b1.data_ptr(), BIG, 1, tag=60)
+            r2 = A.irecv(b2.data_ptr(), BIG, 2, tag=61)
+            flag0 = mxompi.testall([r1, None, r2])        # nothing sent yet: no change
+            first = mxompi.waitany([None, r1, r2])       # rank 2's comes first
+            second = mxompi.waitany([None, r1, r2])
+            none_left = mxompi.waitany([None, r1, r2])
+            any_done = mxompi.testany([r1, r2])
+            r1.free(); r2.free()
+            res["any_all"] = (flag0, first, second, none_left, any_done, b1.cpu().numpy().tobytes(),
+                              b2.cpu().numpy().tobytes())
+        first_from_2_then_1(61, 60, BIG, _data(960, BIG))
+        dist.barrier()
+        right, left = (rank + 1) % n, (rank - 1) % n
+        fl, fr = buf(), buf()
+        reqs = [A.irecv(fl.data_ptr(), BIG, left, tag=1), A.irecv(fr.data_ptr(), BIG, right, tag=2)]
+        A.send(_dev(_data(1100 + rank, BIG)).data_ptr(), BIG, left, tag=2)
+        reqs.append(A.isend(_dev(_data(1200 + rank, BIG)).data_ptr(), BIG, right, tag=1))
+        mxompi.waitall(reqs)
+        done = mxompi.testall(reqs)                     # inactive: true
+        for r in reqs:
+            r.free()
+        res["waitall"] = (done, fl.cpu().numpy().tobytes(), fr.cpu().numpy().tobytes())
+        dist.barrier()
         dt.close()
         A.close()
         dist.destroy_process_group()
@@ -897,3 +925,9 @@ def test_yield_with_datatypes_test_polling_and_persistent():
     assert got[0]["order"] == [_data(971, 64 << 10).tobytes(), _data(972, 64 << 10).tobytes()]
     for case, least in (("ddt", 1), ("test", 1), ("persistent", 2), ("order", 2)):
         assert got[0]["relaunch_" + case] >= least, (case, got[0]["relaunch_" + case])
+    flag0, first, second, none_left, any_done, b1, b2 = got[0]["any_all"]
+    assert (flag0, first, second, none_left, any_done) == (False, 2, 1, mxompi.UNDEFINED, (True, mxompi.UNDEFINED))
+    assert b1 == _data(960, BIG).tobytes() and b2 == _data(961, BIG).tobytes()
+    for r in range(n):
+        done, fl, fr = got[r]["waitall"]
+        assert done and fl == _data(1200 + (r - 1) % n, BIG).tobytes() and fr == _data(1100 + (r + 1) % n, BIG).tobytes()

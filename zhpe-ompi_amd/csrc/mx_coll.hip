@@ -3878,6 +3878,75 @@ extern "C" int mx_wait(mx_request_t *q) {
   return req_complete(q);
 }
 
+// complete, without completing it (nothing changes): the tests of mx_test
+static bool req_done_peek(mx_request *q) {
+  if (!q->active || fast_done(q)) return true;
+  if (q->fast == 2) return rndv_failed(q) != 0;
+  const hipError_t e = hipEventQuery(q->done);
+  if (e == hipErrorNotReady) return false;
+  if (e != hipSuccess) return true;   // mx_wait reports it
+  return !mx::p2p_yielded(q);
+}
+
+extern "C" int mx_waitall(size_t n, mx_request_t *const *reqs) {
+  if (n && !reqs) return MX_ERR_ARG;
+  int rc = MX_SUCCESS;
+  for (size_t i = 0; i < n; i++) {   // each wait progresses every yielded receive, not just its own
+    if (!reqs[i]) continue;
+    const int r = mx_wait(reqs[i]);
+    if (r && !rc) rc = r;
+  }
+  return rc;
+}
+
+// one pass of Testany: the first complete active request (completed), or
+// MX_UNDEFINED with *active = whether any entry is active
+static int test_any_pass(size_t n, mx_request_t *const *reqs, int *index, bool *active) {
+  mx::p2p_progress();
+  *active = false;
+  for (size_t i = 0; i < n; i++) {
+    mx_request *q = reqs[i];
+    if (!q || !q->active) continue;
+    *active = true;
+    if (req_done_peek(q)) {
+      *index = (int)i;
+      return mx_wait(q);
+    }
+  }
+  *index = MX_UNDEFINED;
+  return MX_SUCCESS;
+}
+
+extern "C" int mx_testany(size_t n, mx_request_t *const *reqs, int *index, int *flag) {
+  if (!index || !flag || (n && !reqs)) return MX_ERR_ARG;
+  bool active;
+  const int rc = test_any_pass(n, reqs, index, &active);
+  *flag = *index != MX_UNDEFINED || !active;
+  return rc;
+}
+
+extern "C" int mx_waitany(size_t n, mx_request_t *const *reqs, int *index) {
+  if (!index || (n && !reqs)) return MX_ERR_ARG;
+  const auto t0 = std::chrono::steady_clock::now();
+  for (;;) {
+    bool active;
+    const int rc = test_any_pass(n, reqs, index, &active);
+    if (*index != MX_UNDEFINED || !active) return rc;
+    if (std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0).count() > kWaitSpinUs)
+      std::this_thread::sleep_for(std::chrono::microseconds(20));
+  }
+}
+
+extern "C" int mx_testall(size_t n, mx_request_t *const *reqs, int *flag) {
+  if (!flag || (n && !reqs)) return MX_ERR_ARG;
+  mx::p2p_progress();
+  *flag = 0;
+  for (size_t i = 0; i < n; i++)
+    if (reqs[i] && !req_done_peek(reqs[i])) return MX_SUCCESS;
+  *flag = 1;
+  return mx_waitall(n, reqs);
+}
+
 extern "C" int mx_request_stream_wait(mx_request_t *q, void *stream) {
   if (!q) return MX_ERR_ARG;
   if (!q->active) return MX_SUCCESS;

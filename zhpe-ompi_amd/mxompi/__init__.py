@@ -315,6 +315,10 @@ def _coll_lib():
             getattr(L, name).argtypes = [vp, vp, sz, i, vp, rq]
         L.mx_start.argtypes = [vp]
         L.mx_startall.argtypes = [sz, pp]
+        L.mx_waitall.argtypes = [sz, pp]
+        L.mx_waitany.argtypes = [sz, pp, ctypes.POINTER(i)]
+        L.mx_testall.argtypes = [sz, pp, ctypes.POINTER(i)]
+        L.mx_testany.argtypes = [sz, pp, ctypes.POINTER(i), ctypes.POINTER(i)]
         L.mx_test.argtypes = [vp, ctypes.POINTER(i)]
         L.mx_wait.argtypes = [vp]
         L.mx_request_stream_wait.argtypes = [vp, vp]
@@ -401,6 +405,39 @@ class Request:
 def startall(reqs):
     arr = _ptrs([r.h for r in reqs])
     check(_coll_lib().mx_startall(len(reqs), arr), "mx_startall")
+
+
+UNDEFINED = -32766   # MX_UNDEFINED (MPI_UNDEFINED)
+
+
+def _hs(reqs):
+    return _ptrs([r.h if r is not None else None for r in reqs])
+
+
+def waitall(reqs):
+    """MPI_Waitall: complete every request (None entries skipped)."""
+    check(_coll_lib().mx_waitall(len(reqs), _hs(reqs)), "mx_waitall")
+
+
+def waitany(reqs):
+    """MPI_Waitany: index of the request completed, UNDEFINED if none is active."""
+    idx = ctypes.c_int(0)
+    check(_coll_lib().mx_waitany(len(reqs), _hs(reqs), ctypes.byref(idx)), "mx_waitany")
+    return idx.value
+
+
+def testall(reqs):
+    """MPI_Testall: True (and all completed) once every request is complete."""
+    flag = ctypes.c_int(0)
+    check(_coll_lib().mx_testall(len(reqs), _hs(reqs), ctypes.byref(flag)), "mx_testall")
+    return bool(flag.value)
+
+
+def testany(reqs):
+    """MPI_Testany: (flag, index)."""
+    idx, flag = ctypes.c_int(0), ctypes.c_int(0)
+    check(_coll_lib().mx_testany(len(reqs), _hs(reqs), ctypes.byref(idx), ctypes.byref(flag)), "mx_testany")
+    return bool(flag.value), idx.value
 
 
 def iallreduce_decision(n, count, t, inplace=False):
