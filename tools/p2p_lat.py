@@ -24,7 +24,11 @@ def worker(rank, n, port, q):
     x = torch.zeros(64 << 20, dtype=torch.uint8, device="cuda")
     peer = 1 - rank
     rows = []
-    for nb in [8, 4096, 65536, 256 << 10, (256 << 10) + 16, 1 << 20, 16 << 20, 64 << 20]:
+    sizes = [8, 4096, 65536, 256 << 10, (256 << 10) + 16, 1 << 20, 16 << 20, 64 << 20]
+    if os.environ.get("P2P_LAT_SIZES"):          # e.g. "8,4096" (diagnostics)
+        sizes = [int(x) for x in os.environ["P2P_LAT_SIZES"].split(",")]
+    dist_out = {}
+    for nb in sizes:
         for form in ("blocking", "nonblocking"):
             def one():
                 if form == "blocking":
@@ -44,18 +48,22 @@ def worker(rank, n, port, q):
             for _ in range(10):
                 one()
             dist.barrier()
-            it = 100 if nb <= (1 << 20) else 20
+            it = int(os.environ.get("P2P_LAT_ITERS", 100 if nb <= (1 << 20) else 20))
             ts = []
             for _ in range(it):
                 t0 = time.perf_counter()
                 one()
                 ts.append(time.perf_counter() - t0)
+            if os.environ.get("P2P_LAT_DIST"):     # the first 40 half round trips in order + percentiles
+                dist_out[(nb, form)] = ([round(t / 2 * 1e6, 1) for t in ts[:40]],
+                                        [round(sorted(ts)[int(q * (len(ts) - 1))] / 2 * 1e6, 1)
+                                         for q in (0.1, 0.25, 0.5, 0.75, 0.9)])
             ts.sort()
             us = ts[len(ts) // 2] / 2 * 1e6      # median round trip (the mean is at the box's mercy)
             rows.append((nb, form, round(us, 1), round(nb / us / 1e3, 2)))
     comm.close()
     dist.destroy_process_group()
-    q.put((rank, rows))
+    q.put((rank, (rows, dist_out)))
 
 
 if __name__ == "__main__":
@@ -70,4 +78,6 @@ if __name__ == "__main__":
     res = dict(q.get(timeout=300) for _ in range(2))
     for p in ps:
         p.join(timeout=60)
-    print("p2p half-round-trip (bytes, form, us, GB/s):", res[0], flush=True)
+    for k, v in res[0][1].items():
+        print("rank 0", k, "first 40:", v[0], "p10/25/50/75/90:", v[1], flush=True)
+    print("p2p half-round-trip (bytes, form, us, GB/s):", res[0][0], flush=True)
