@@ -931,3 +931,97 @@ def test_yield_with_datatypes_test_polling_and_persistent():
     for r in range(n):
         done, fl, fr = got[r]["waitall"]
         assert done and fl == _data(1200 + (r - 1) % n, BIG).tobytes() and fr == _data(1100 + (r + 1) % n, BIG).tobytes()
+
+
+def _tables_worker(rank, n, port, q):
+    """16 unexpected eager messages wait in the device stash and 64
+    unexpected rendezvous messages as deferred envelopes (their data stays
+    with the sender); the receive that meets one unexpected message more than
+    the stash holds completes with MX_ERR_TAG (the documented bound) and the
+    channel stays usable."""
+    import torch.distributed as dist
+    os.environ["HSA_ENABLE_IPC_MODE_LEGACY"] = "0"
+    try:
+        dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=n)
+        torch.cuda.set_device(0)
+        mxompi.init(0)
+
+        def ag(b):
+            out = [None] * n
+            dist.all_gather_object(out, b)
+            return out
+
+        A = mxompi.Comm(rank, n, ag, device=0, staging_bytes=1 << 20)
+        A.set_timeout(30.0)
+        res = {}
+        E, R = 1000, 300 << 10
+        if rank == 0:
+            keep = []
+            reqs = []
+            for t in range(200, 217):                   # 17 eager: one more than the stash
+                b = _dev(_data(t, E)); keep.append(b)
+                reqs.append(A.isend(b.data_ptr(), E, 1, tag=t))
+            b = _dev(_data(299, E)); keep.append(b)
+            reqs.append(A.isend(b.data_ptr(), E, 1, tag=299))
+            for t in range(400, 464):                   # 64 rendezvous: the deferred table
+                b = _dev(_data(t, R)); keep.append(b)
+                reqs.append(A.isend(b.data_ptr(), R, 1, tag=t))
+            b = _dev(_data(499, E)); keep.append(b)
+            reqs.append(A.isend(b.data_ptr(), E, 1, tag=499))
+            mxompi.waitall(reqs)
+            for r in reqs:
+                r.free()
+        else:
+            d = torch.zeros(R, dtype=torch.uint8, device="cuda")
+            r = A.irecv(d.data_ptr(), E, 0, tag=299)    # stashes 200..215, then meets 216
+            try:
+                r.wait()
+                res["overflow"] = ("no error", r.status())
+            except mxompi.MxError as e:
+                res["overflow"] = (e.rc, tuple(r.status())[:2], d[:E].cpu().numpy().tobytes())
+            r.free()
+            res["299"] = (A.recv(d.data_ptr(), E, 0, tag=299), d[:E].cpu().numpy().tobytes())
+            res["499"] = (A.recv(d.data_ptr(), E, 0, tag=499), d[:E].cpu().numpy().tobytes())   # defers 400..463
+            got = {}
+            for t in list(range(215, 199, -1)) + list(range(463, 399, -1)):
+                nb = E if t < 300 else R
+                got[t] = (A.recv(d.data_ptr(), nb, 0, tag=t), d[:nb].cpu().numpy().tobytes())
+            res["held"] = got
+        dist.barrier()
+        A.close()
+        dist.destroy_process_group()
+        q.put((rank, "ok", res))
+    except Exception as e:  # noqa: BLE001
+        import traceback
+        q.put((rank, "err", traceback.format_exc() + str(e)))
+
+
+def test_unexpected_message_tables_and_their_bound():
+    import torch.multiprocessing as mp
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_tables_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    got = {}
+    try:
+        for _ in range(2):
+            rank, status, payload = q.get(timeout=200)
+            assert status == "ok", payload
+            got[rank] = payload
+    finally:
+        for p in procs:
+            p.join(timeout=30 if len(got) == 2 else 5)
+            if p.is_alive():
+                p.terminate()
+                p.join(timeout=10)
+    E, R = 1000, 300 << 10
+    res = got[1]
+    rc, st, data = res["overflow"]
+    assert rc == -10 and st == (E, 216) and data == _data(216, E).tobytes(), (rc, st)   # MX_ERR_TAG
+    assert res["299"] == (E, _data(299, E).tobytes())
+    assert res["499"] == (E, _data(499, E).tobytes())
+    for t, (nb, data) in res["held"].items():
+        want = _data(t, E if t < 300 else R)
+        assert nb == len(want) and data == want.tobytes(), t

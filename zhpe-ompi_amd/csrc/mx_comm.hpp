@@ -60,9 +60,9 @@ constexpr uint64_t BYE_WORD = 0xB7EB7EB7EB7EB7EBull;
 // drained into a stash slot (P2P_STASH_N per source, P2P_STASH_C bytes
 // each); a rendezvous message only has its envelope recorded (P2P_DEFER_N
 // per source) -- its data stays with the sender until a receive clears it.
-constexpr int P2P_STASH_N = 8;
+constexpr int P2P_STASH_N = 16;
 constexpr size_t P2P_STASH_C = 256 << 10;
-constexpr int P2P_DEFER_N = 32;
+constexpr int P2P_DEFER_N = 64;
 struct P2PStashEntry { uint64_t valid; int64_t tag; uint64_t bytes; uint64_t seq; };
 
 // device-local sequence state of the channels (not shared)

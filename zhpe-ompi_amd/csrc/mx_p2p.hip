@@ -775,7 +775,8 @@ __device__ void rx_control(const P2PRecvArgs &a) {
   const uint64_t *posted = a.flag0 + P2P_POSTED + p;
   const char *box = a.box0 + (size_t)p * P2P_BOX;
   const uint64_t m0 = st->msgs_done;
-  int64_t aside[P2P_STASH_N + P2P_DEFER_N];
+  constexpr int kAside = 32;   // tags of the envelopes set aside, the first 32 (a yield heuristic)
+  int64_t aside[kAside];
   int naside = 0;
   uint64_t k = 0, polled = wall_clock64();
   for (;;) {
@@ -787,7 +788,7 @@ __device__ void rx_control(const P2PRecvArgs &a) {
       if ((v & 3) != kDecGo) return;
       // taken and the lanes go on: it was not this receive's message
       __atomic_thread_fence(__ATOMIC_ACQUIRE);
-      if (naside < P2P_STASH_N + P2P_DEFER_N)
+      if (naside < kAside)
         aside[naside++] = (int64_t)reinterpret_cast<const volatile uint64_t *>(box + ((m0 + k) % P2P_H) * P2P_HDR)[1];
       k++;
       continue;
