@@ -1025,3 +1025,115 @@ def test_unexpected_message_tables_and_their_bound():
     for t, (nb, data) in res["held"].items():
         want = _data(t, E if t < 300 else R)
         assert nb == len(want) and data == want.tobytes(), t
+
+
+def _plan(seed, n, per_rank=12):
+    """Every rank's sends (destination, tag, size, payload seed) in send
+    order, and every rank's receive posting order: a list of (source, tag)."""
+    import random
+    rng = random.Random(seed)
+    sends = {r: [] for r in range(n)}
+    for r in range(n):
+        for k in range(per_rank):
+            dst = rng.choice([d for d in range(n) if d != r])
+            tag = rng.randrange(3)
+            size = rng.choice([2048 + rng.randrange(64), (300 << 10) + rng.randrange(64)])
+            sends[r].append((dst, tag, size, 10000 * seed + 100 * r + k))
+    posts = {}
+    for d in range(n):
+        incoming = [(s, t) for s in range(n) for (dst, t, _, _) in sends[s] if dst == d]
+        rng.shuffle(incoming)
+        posts[d] = incoming
+    return sends, posts
+
+
+def _random_worker(rank, n, port, q, seed):
+    import torch.distributed as dist
+    import random
+    os.environ["HSA_ENABLE_IPC_MODE_LEGACY"] = "0"
+    try:
+        dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=n)
+        torch.cuda.set_device(0)
+        mxompi.init(0)
+
+        def ag(b):
+            out = [None] * n
+            dist.all_gather_object(out, b)
+            return out
+
+        A = mxompi.Comm(rank, n, ag, device=0, staging_bytes=1 << 20)
+        A.set_timeout(30.0)
+        sends, posts = _plan(seed, n)
+        cap = (300 << 10) + 64
+        bufs, reqs = [], []
+        for (src, tag) in posts[rank]:                   # every receive posted before any send
+            b = torch.zeros(cap, dtype=torch.uint8, device="cuda")
+            bufs.append(b)
+            reqs.append(A.irecv(b.data_ptr(), cap, src, tag=tag))
+        dist.barrier()
+        order = list(range(len(sends[rank])))
+        random.Random(seed * 7 + rank).shuffle(order)    # blocking sends in a random order...
+        per_pair = {}
+        for k in order:                                  # ...but each (dst, tag) stream in plan order
+            dst, tag, _, _ = sends[rank][k]
+            per_pair.setdefault((dst, tag), []).append(k)
+        for key in per_pair:
+            per_pair[key].sort()
+        for k in order:
+            dst, tag, _, _ = sends[rank][k]
+            kk = per_pair[(dst, tag)].pop(0)
+            _, _, size, ps = sends[rank][kk]
+            x = _dev(_data(ps, size))
+            A.send(x.data_ptr(), size, dst, tag=tag)
+        mxompi.waitall(reqs)
+        got = [(tuple(r.status())[:2], b[: r.status()[0]].cpu().numpy().tobytes()) for r, b in zip(reqs, bufs)]
+        for r in reqs:
+            r.free()
+        relaunched = A.stats(reset=True)["p2p_relaunches"]
+        dist.barrier()
+        A.close()
+        dist.destroy_process_group()
+        q.put((rank, "ok", {"got": got, "relaunched": relaunched}))
+    except Exception as e:  # noqa: BLE001
+        import traceback
+        q.put((rank, "err", traceback.format_exc() + str(e)))
+
+
+@pytest.mark.parametrize("n,seed", [(3, 1), (3, 2), (3, 3), (4, 4), (4, 5)])
+def test_randomised_posting_orders_complete_in_match_order(n, seed):
+    """A safe program (every receive posted before any send) with receives
+    posted in a random order and blocking sends in a random order: it must
+    complete, and the k-th receive posted for (source, tag) must get the k-th
+    message sent on (source, tag) (MPI's non-overtaking rule)."""
+    import torch.multiprocessing as mp
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_random_worker, args=(r, n, port, q, seed)) for r in range(n)]
+    for p in procs:
+        p.start()
+    got = {}
+    try:
+        for _ in range(n):
+            rank, status, payload = q.get(timeout=200)
+            assert status == "ok", payload
+            got[rank] = payload
+    finally:
+        for p in procs:
+            p.join(timeout=30 if len(got) == n else 5)
+            if p.is_alive():
+                p.terminate()
+                p.join(timeout=10)
+    sends, posts = _plan(seed, n)
+    for d in range(n):
+        streams = {}
+        for s in range(n):
+            for (dst, tag, size, ps) in sends[s]:
+                if dst == d:
+                    streams.setdefault((s, tag), []).append((size, ps))
+        for i, (src, tag) in enumerate(posts[d]):
+            size, ps = streams[(src, tag)].pop(0)
+            (nb, t), data = got[d]["got"][i]
+            assert (nb, t) == (size, tag) and data == _data(ps, size).tobytes(), (d, i, src, tag)
+    print(f"seed {seed}: receive launches that yielded per rank",
+          [got[r]["relaunched"] for r in range(n)])          # (-s / the log shows how much yielding ran)
