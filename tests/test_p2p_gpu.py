@@ -1137,3 +1137,139 @@ def test_randomised_posting_orders_complete_in_match_order(n, seed):
             assert (nb, t) == (size, tag) and data == _data(ps, size).tobytes(), (d, i, src, tag)
     print(f"seed {seed}: receive launches that yielded per rank",
           [got[r]["relaunched"] for r in range(n)])          # (-s / the log shows how much yielding ran)
+
+
+def _wild_plan(seed, n, per_rank=12):
+    """Like _plan, with each rank's blocking-send sequence fixed here and part
+    of each destination's receives made wildcards.  Specific receives take the
+    first messages of their (source, tag) stream and are posted first (random
+    order); per destination the remaining messages are covered by (source,
+    MPI_ANY_TAG) receives, then by (MPI_ANY_SOURCE, MPI_ANY_TAG) ones, posted
+    in that order -- whatever the arrival order, every receive then has a
+    message (a safe program)."""
+    import random
+    rng = random.Random(seed)
+    sends, _ = _plan(seed, n, per_rank)
+    seqs = {}
+    for r in range(n):                                   # the blocking-send sequence of rank r
+        order = list(range(per_rank))
+        rng.shuffle(order)
+        per = {}
+        for k in range(per_rank):
+            dst, tag, _, _ = sends[r][k]
+            per.setdefault((dst, tag), []).append(k)
+        seqs[r] = [per[(sends[r][k][0], sends[r][k][1])].pop(0) for k in order]
+    posts = {}
+    for d in range(n):
+        streams = {}
+        for s in range(n):
+            for k in seqs[s]:
+                dst, tag, _, _ = sends[s][k]
+                if dst == d:
+                    streams.setdefault((s, tag), []).append(k)
+        specific, by_src, anyany = [], [], []
+        for (s, t), ks in streams.items():
+            keep = rng.randrange(len(ks) + 1)
+            specific += [(s, t)] * keep
+            for _ in ks[keep:]:
+                (by_src if rng.random() < 0.5 else anyany).append((s, -1))
+        rng.shuffle(specific)
+        rng.shuffle(by_src)
+        posts[d] = specific + by_src + [(-1, -1)] * len(anyany)
+    return sends, seqs, posts
+
+
+def _wild_worker(rank, n, port, q, seed):
+    import torch.distributed as dist
+    os.environ["HSA_ENABLE_IPC_MODE_LEGACY"] = "0"
+    try:
+        dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=n)
+        torch.cuda.set_device(0)
+        mxompi.init(0)
+
+        def ag(b):
+            out = [None] * n
+            dist.all_gather_object(out, b)
+            return out
+
+        A = mxompi.Comm(rank, n, ag, device=0, staging_bytes=1 << 20)
+        A.set_timeout(30.0)
+        sends, seqs, posts = _wild_plan(seed, n)
+        cap = (300 << 10) + 64
+        bufs, reqs = [], []
+        for (src, tag) in posts[rank]:
+            b = torch.zeros(cap, dtype=torch.uint8, device="cuda")
+            bufs.append(b)
+            reqs.append(A.irecv(b.data_ptr(), cap, src, tag=tag))
+        dist.barrier()
+        for k in seqs[rank]:
+            dst, tag, size, ps = sends[rank][k]
+            A.send(_dev(_data(ps, size)).data_ptr(), size, dst, tag=tag)
+        mxompi.waitall(reqs)
+        got = [(r.source(), tuple(r.status())[:2], b[: r.status()[0]].cpu().numpy().tobytes())
+               for r, b in zip(reqs, bufs)]
+        for r in reqs:
+            r.free()
+        relaunched = A.stats(reset=True)["p2p_relaunches"]
+        dist.barrier()
+        A.close()
+        dist.destroy_process_group()
+        q.put((rank, "ok", {"got": got, "relaunched": relaunched}))
+    except Exception as e:  # noqa: BLE001
+        import traceback
+        q.put((rank, "err", traceback.format_exc() + str(e)))
+
+
+@pytest.mark.parametrize("n,seed", [(3, 11), (3, 12), (4, 13)])
+def test_randomised_wildcard_receives_keep_non_overtaking(n, seed):
+    """Every message is delivered once, to a receive whose pattern matches it;
+    specific receives get their streams' messages in order; and for two
+    receives that both got messages from one source and could each have taken
+    the other's, the earlier-posted one got the earlier-sent message (MPI's
+    non-overtaking rule, which ob1's matching keeps)."""
+    import torch.multiprocessing as mp
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_wild_worker, args=(r, n, port, q, seed)) for r in range(n)]
+    for p in procs:
+        p.start()
+    got = {}
+    try:
+        for _ in range(n):
+            rank, status, payload = q.get(timeout=200)
+            assert status == "ok", payload
+            got[rank] = payload
+    finally:
+        for p in procs:
+            p.join(timeout=30 if len(got) == n else 5)
+            if p.is_alive():
+                p.terminate()
+                p.join(timeout=10)
+    sends, seqs, posts = _wild_plan(seed, n)
+    for d in range(n):
+        # every message to d by payload: (source, tag, position in the source's send sequence)
+        msgs = {}
+        for s in range(n):
+            pos = 0
+            for k in seqs[s]:
+                dst, tag, size, ps = sends[s][k]
+                if dst == d:
+                    msgs[_data(ps, size).tobytes()] = (s, tag, pos)
+                    pos += 1
+        seen = []
+        for i, (src_pat, tag_pat) in enumerate(posts[d]):
+            source, (nb, tag), data = got[d]["got"][i]
+            assert data in msgs, (d, i)
+            s, t, pos = msgs.pop(data)
+            assert (source, tag, nb) == (s, t, len(data)), (d, i)
+            assert src_pat in (-1, s) and tag_pat in (-1, t), (d, i, src_pat, tag_pat, s, t)
+            seen.append((src_pat, tag_pat, s, t, pos))
+        assert not msgs, f"undelivered at {d}"
+        for i in range(len(seen)):
+            for j in range(i + 1, len(seen)):
+                pi, ti, si, tgi, posi = seen[i]
+                pj, tj, sj, tgj, posj = seen[j]
+                both = (si == sj and pi in (-1, sj) and ti in (-1, tgj) and pj in (-1, si) and tj in (-1, tgi))
+                assert not both or posi < posj, ("overtaken", d, i, j, seen[i], seen[j])
+    print(f"seed {seed}: receive launches that yielded per rank", [got[r]["relaunched"] for r in range(n)])
