@@ -859,6 +859,22 @@ def _yield_worker2(rank, n, port, q):
             A.send(_dev(_data(972, E)).data_ptr(), E, 0, tag=7)
         dist.barrier()
 
+        # (4b) mx_request_stream_wait on a receive that yields: the host waits
+        # (progressing the yield) and work on the stream sees the payload
+        if rank == 0:
+            b1, b2 = buf(), buf()
+            r1 = A.irecv(b1.data_ptr(), BIG, 1, tag=80)
+            r2 = A.irecv(b2.data_ptr(), BIG, 2, tag=81)
+            side = torch.cuda.Stream()
+            r1.stream_wait(side.cuda_stream)
+            with torch.cuda.stream(side):
+                c1 = b1.clone()
+            side.synchronize()
+            r1.wait(); r2.wait(); r1.free(); r2.free()
+            res["stream_wait"] = (c1.cpu().numpy().tobytes(), b2.cpu().numpy().tobytes())
+        first_from_2_then_1(81, 80, BIG, _data(980, BIG))
+        dist.barrier()
+
         # (5) MPI_Waitall / Waitany / Testall / Testany over receives that
         # yield (ompi/request/req_wait.c, req_test.c semantics)
         if rank == 0:
@@ -925,6 +941,7 @@ def test_yield_with_datatypes_test_polling_and_persistent():
     assert got[0]["order"] == [_data(971, 64 << 10).tobytes(), _data(972, 64 << 10).tobytes()]
     for case, least in (("ddt", 1), ("test", 1), ("persistent", 2), ("order", 2)):
         assert got[0]["relaunch_" + case] >= least, (case, got[0]["relaunch_" + case])
+    assert got[0]["stream_wait"] == (_data(980, BIG).tobytes(), _data(981, BIG).tobytes())
     flag0, first, second, none_left, any_done, b1, b2 = got[0]["any_all"]
     assert (flag0, first, second, none_left, any_done) == (False, 2, 1, mxompi.UNDEFINED, (True, mxompi.UNDEFINED))
     assert b1 == _data(960, BIG).tobytes() and b2 == _data(961, BIG).tobytes()
