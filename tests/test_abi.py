@@ -58,3 +58,22 @@ def test_unsupported_pair_is_rejected_without_device():
     assert L.mx_reduce2(mxompi.OP["LAND"], mxompi.TYPE["FLOAT"], None, None, 4, None) == -2
     assert L.mx_reduce2(99, 0, None, None, 4, None) == -1
     assert L.mx_strerror(-2) == b"operation not defined for this datatype"
+
+
+def test_request_array_helpers_on_null_and_inactive_entries():
+    """mx_waitall / mx_waitany / mx_testall / mx_testany over arrays whose
+    entries are all null (MPI_REQUEST_NULL): ompi_request_default_wait_any /
+    test_any give MPI_UNDEFINED and, for Testany, flag = true
+    (req_wait.c:84-125, req_test.c:172-185); Waitall / Testall complete at
+    once.  No request is active, so no GPU call is made."""
+    assert mxompi.UNDEFINED == -32766            # MPI_UNDEFINED, mpi.h.in:488
+    mxompi.waitall([None, None])
+    assert mxompi.waitany([None, None, None]) == mxompi.UNDEFINED
+    assert mxompi.testany([None]) == (True, mxompi.UNDEFINED)
+    assert mxompi.testall([None, None]) is True
+    mxompi.waitall([])
+    assert mxompi.waitany([]) == mxompi.UNDEFINED
+    L = mxompi._coll_lib()
+    idx, flag = ctypes.c_int(0), ctypes.c_int(0)
+    assert L.mx_waitany(1, None, ctypes.byref(idx)) == -1           # MX_ERR_ARG: n > 0, no array
+    assert L.mx_testany(0, None, None, ctypes.byref(flag)) == -1    # no index
