@@ -1046,6 +1046,12 @@ bool p2p_pending(mx_comm *c) {
 
 void p2p_release(mx_comm *c) {
   p2p_quiesce(c);
+  // receives of this communicator still in flight (yielded, never launched
+  // again) are launched by nobody from now on
+  if (c->device >= 0 && c->device < 64) {
+    std::vector<mx_request *> &v = g_rx[c->device].active;
+    v.erase(std::remove_if(v.begin(), v.end(), [c](mx_request *q) { return q->c == c; }), v.end());
+  }
   for (int i = 0; i < 3; i++) {
     if (c->p2p_last[i]) (void)hipEventDestroy(c->p2p_last[i]);
     c->p2p_last[i] = nullptr;
