@@ -254,11 +254,12 @@ struct mx_comm {
   // the device's three channel streams (send, receive, rendezvous pick),
   // shared by every communicator of the process (p2p_setup): the spinning
   // channels hold 3 high-priority hardware queues per device, whatever the
-  // number of communicators.  p2p_last[i]: event after this communicator's
-  // last kernel on channel i (its own work, for destroy and quiet checks).
+  // number of communicators.  p2p_hfin[i] reaching p2p_ltot[i]: this
+  // communicator's last kernel on channel i has finished (its own work, for
+  // destroy and quiet checks; raised by that kernel's last lane).
   hipStream_t p2p_stream[3];
-  hipEvent_t p2p_last[3];
-  int p2p_last_valid[3];
+  int p2p_last_valid[3];             // work was enqueued on channel i since the last quiesce
+  uint64_t *p2p_hfin, *p2p_hfin_dev; // mapped [3]: target of the last finished kernel per channel
   hipEvent_t p2p_ev;
   uint64_t *p2p_lanes;     // device: finished-lane counters of the three streams
   uint64_t p2p_ltot[3];    // lanes (workgroups) of the transfer kernels enqueued per stream

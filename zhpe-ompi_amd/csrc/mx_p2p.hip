@@ -47,7 +47,9 @@
 #include <string.h>
 
 #include <algorithm>
+#include <chrono>
 #include <mutex>
+#include <thread>
 
 #include "mx_comm.hpp"
 #include "../../include/mx_convertor.h"
@@ -122,6 +124,8 @@ struct P2PDone {
   uint64_t *lanes;       // device counter of finished lanes (per stream)
   uint64_t target;
   int64_t *done;         // mapped host word, or null
+  uint64_t *hfin;        // mapped host word: `target` of the communicator's last finished kernel on this
+                         // channel (what its destroy and quiet check wait for; no event per kernel)
 };
 
 // `wrote`: this lane stored user data without a fence after it (a receive
@@ -137,6 +141,7 @@ __device__ __forceinline__ bool lane_finished(const P2PDone &f, bool wrote) {
     const uint64_t old = __hip_atomic_fetch_add(f.lanes, (uint64_t)1, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
     last = old + 1 == f.target;
     if (last && f.done) __hip_atomic_store(f.done, (int64_t)1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    if (last && f.hfin) __hip_atomic_store(f.hfin, f.target, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
   }
   return last;
 }
@@ -864,6 +869,7 @@ __global__ void __launch_bounds__(kP2PThreads) k_p2p_recv(P2PRecvArgs a) {
       } else if (a.fin.done) {
         __hip_atomic_store(a.fin.done, (int64_t)1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
       }
+      if (a.fin.hfin) __hip_atomic_store(a.fin.hfin, a.fin.target, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     }
   }
 }
@@ -946,11 +952,31 @@ static int p2p_rndv_stream(mx_comm *c) {
   return MX_SUCCESS;
 }
 
-// this communicator's kernel just enqueued on channel i
+// this communicator's kernel just enqueued on channel i.  Its completion is
+// the mapped word its last lane raises (P2PDone::hfin reaching p2p_ltot[i]):
+// an event recorded after every kernel put a second packet behind each one
+// on the channel's queue, and a kernel enqueued while the one before had not
+// retired then waited ~27 us more to start -- the 8 B hop's slow mode
+// (profiles/r05/p2p_latency_modes_r5ar.txt)
 static int p2p_note(mx_comm *c, int i) {
-  if (hipEventRecord(c->p2p_last[i], c->p2p_stream[i]) != hipSuccess) return MX_ERR_HIP;
   c->p2p_last_valid[i] = 1;
   return MX_SUCCESS;
+}
+
+// the communicator's kernels on channel i have all finished (the word their
+// last lanes raise), or the channel's stream failed
+static bool p2p_channel_idle(mx_comm *c, int i) {
+  if (!c->p2p_last_valid[i] || !c->p2p_hfin) return true;
+  if (__atomic_load_n(&c->p2p_hfin[i], __ATOMIC_ACQUIRE) >= c->p2p_ltot[i]) return true;
+  const hipError_t e = c->p2p_stream[i] ? hipStreamQuery(c->p2p_stream[i]) : hipSuccess;
+  if (e == hipErrorNotReady) return false;
+  (void)hipGetLastError();
+  return e != hipSuccess;   // a failed stream never raises the word
+}
+
+static void p2p_channel_wait(mx_comm *c, int i) {
+  for (int k = 0; !p2p_channel_idle(c, i); k++)
+    if (k > 1000) std::this_thread::sleep_for(std::chrono::microseconds(50));
 }
 
 // Setup makes no device-wide synchronisation: a receive of another
@@ -975,12 +1001,15 @@ int p2p_setup(mx_comm *c) {
       (c->p2p_rndv_cur = (P2PRndvCur *)pool_dev_get(sizeof(P2PRndvCur))) != nullptr &&
       (c->p2p_rndv = (P2PRndvTable *)pool_host_get(sizeof(P2PRndvTable))) != nullptr &&
       hipHostGetDevicePointer((void **)&c->p2p_rndv_dev, c->p2p_rndv, 0) == hipSuccess &&
-      (c->p2p_disp = (P2PDisplaced *)pool_dev_get(sizeof(P2PDisplaced))) != nullptr;
+      (c->p2p_disp = (P2PDisplaced *)pool_dev_get(sizeof(P2PDisplaced))) != nullptr &&
+      (c->p2p_hfin = (uint64_t *)pool_host_get(3 * sizeof(uint64_t))) != nullptr &&
+      hipHostGetDevicePointer((void **)&c->p2p_hfin_dev, c->p2p_hfin, 0) == hipSuccess;
   if (!ok) {
     p2p_release(c);
     return MX_ERR_NOMEM;
   }
   c->p2p_posts = 0;
+  c->p2p_hfin[0] = c->p2p_hfin[1] = c->p2p_hfin[2] = 0;
   if (rx_yield_on() && c->device >= 0 && c->device < 64) {
     std::lock_guard<std::mutex> lk(g_chan_mu);
     RxDev &D = g_rx[c->device];
@@ -1013,9 +1042,6 @@ int p2p_setup(mx_comm *c) {
       hipMemsetAsync(c->p2p_rndv_cur, 0, sizeof(P2PRndvCur), ls) != hipSuccess ||
       hipMemsetAsync(c->p2p_disp, 0, sizeof(P2PDisplaced), ls) != hipSuccess ||
       p2p_channels(c->p2p_stream) != MX_SUCCESS ||
-      hipEventCreateWithFlags(&c->p2p_last[0], hipEventDisableTiming) != hipSuccess ||
-      hipEventCreateWithFlags(&c->p2p_last[1], hipEventDisableTiming) != hipSuccess ||
-      hipEventCreateWithFlags(&c->p2p_last[2], hipEventDisableTiming) != hipSuccess ||
       hipEventCreateWithFlags(&c->p2p_ev, hipEventDisableTiming) != hipSuccess ||
       hipStreamSynchronize(ls) != hipSuccess) {
     p2p_release(c);
@@ -1026,21 +1052,16 @@ int p2p_setup(mx_comm *c) {
 
 void p2p_quiesce(mx_comm *c) {
   // this communicator's kernels only (the streams are shared)
-  for (int i = 0; i < 2; i++)
-    if (c->p2p_last_valid[i] && hipEventSynchronize(c->p2p_last[i]) != hipSuccess) (void)hipGetLastError();
+  for (int i = 0; i < 2; i++) p2p_channel_wait(c, i);
   // rendezvous sends no receive ever cleared: their picks give up
   if (c->p2p_rndv) __atomic_store_n(&c->p2p_rndv->abort, 1, __ATOMIC_RELEASE);
-  if (c->p2p_last_valid[2] && hipEventSynchronize(c->p2p_last[2]) != hipSuccess) (void)hipGetLastError();
+  p2p_channel_wait(c, 2);
   c->p2p_last_valid[0] = c->p2p_last_valid[1] = c->p2p_last_valid[2] = 0;
 }
 
 bool p2p_pending(mx_comm *c) {
   for (int i = 0; i < 3; i++)
-    if (c->p2p_last_valid[i]) {
-      const hipError_t e = hipEventQuery(c->p2p_last[i]);
-      if (e == hipErrorNotReady) { (void)hipGetLastError(); return true; }
-      if (e != hipSuccess) (void)hipGetLastError();
-    }
+    if (!p2p_channel_idle(c, i)) return true;
   return false;
 }
 
@@ -1052,10 +1073,8 @@ void p2p_release(mx_comm *c) {
     std::vector<mx_request *> &v = g_rx[c->device].active;
     v.erase(std::remove_if(v.begin(), v.end(), [c](mx_request *q) { return q->c == c; }), v.end());
   }
-  for (int i = 0; i < 3; i++) {
-    if (c->p2p_last[i]) (void)hipEventDestroy(c->p2p_last[i]);
-    c->p2p_last[i] = nullptr;
-  }
+  pool_host_put(c->p2p_hfin, 3 * sizeof(uint64_t));
+  c->p2p_hfin = c->p2p_hfin_dev = nullptr;
   if (c->p2p_stream[2]) (void)hipStreamDestroy(c->p2p_stream[2]);   // its own; [0], [1] are the device's
   if (c->p2p_ev) (void)hipEventDestroy(c->p2p_ev);
   const size_t sb = sizeof(P2PSendState) * c->size, rb = sizeof(P2PRecvState) * c->size;
@@ -1204,6 +1223,7 @@ int p2p_enqueue(mx_request *q, hipStream_t *done_stream) {
   fin.lanes = c->p2p_lanes + dir;
   fin.target = c->p2p_ltot[dir] + nl;
   fin.done = q->fast == 1 ? st_dev + 4 : nullptr;
+  fin.hfin = c->p2p_hfin_dev + dir;
   c->p2p_ltot[dir] += nl;   // every transfer kernel counts its lanes, flagged or not
   char *tmp = nullptr;
   if (q->ddt && bytes && hipMallocAsync((void **)&tmp, bytes, s) != hipSuccess) return MX_ERR_NOMEM;
@@ -1262,6 +1282,7 @@ int p2p_enqueue(mx_request *q, hipStream_t *done_stream) {
       ra.fin.lanes = c->p2p_lanes + 2;
       ra.fin.target = c->p2p_ltot[2] + P2P_LR;
       ra.fin.done = nullptr;
+      ra.fin.hfin = c->p2p_hfin_dev + 2;
       c->p2p_ltot[2] += P2P_LR;
       hipLaunchKernelGGL(k_p2p_rndv, dim3(P2P_LR), dim3(kP2PThreads), 0, c->p2p_stream[2], ra);
       if ((rc = mx_check_launch()) || (rc = p2p_note(c, 2))) return rc;
@@ -1342,6 +1363,7 @@ int p2p_rx_launch(mx_request *q) {
   a.fin.lanes = c->p2p_lanes + 1;
   a.fin.target = c->p2p_ltot[1] + P2P_L;
   a.fin.done = q->fast == 1 ? a.status + 4 : nullptr;
+  a.fin.hfin = c->p2p_hfin_dev + 1;
   c->p2p_ltot[1] += P2P_L;
   int rc;
   if (a.any) {
