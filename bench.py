@@ -145,6 +145,48 @@ def op_reduce_call_cost(torch, mx, sizes=(4 << 10, 64 << 10, 1 << 20)):
     return out
 
 
+def allreduce_n1(torch, mx, nbytes=256 << 20, iters=20):
+    """The 1-GPU point of the metric's "MPI_Allreduce ... 1/2/4/8 GPU": a
+    size-1 communicator (MPI_COMM_SELF, a one-rank MPI_COMM_WORLD), 256 MiB
+    fp32 SUM, sbuf -> rbuf.  coll/self would copy it with host memcpy
+    (coll_self_allreduce.c:41-44); coll/mi355x's size-1 slot runs one device
+    copy kernel.  Called as Open MPI calls it: the communicator's allreduce
+    slot through the mini-host's MPI_Allreduce entry (the oracle is only the
+    harness's base op table, never called here).  GB/s = 2 x S (read sbuf,
+    write rbuf) / the blocking call's wall time; bit-exact copy
+    checked after the timed calls."""
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import minihost
+    H = minihost.host(with_components=True)
+    H.mxh_self_calls.argtypes = []
+    f32, SUM, self_comm = minihost.dtype(H, "MPI_FLOAT"), minihost.op(H, "MPI_SUM"), H.mxh_comm_self()
+    owner = H.mxh_comm_slot_owner(self_comm, b"allreduce").decode()
+    count = nbytes // 4
+    g = torch.Generator(device="cuda").manual_seed(0x5EED)
+    s_buf = torch.empty(count, device="cuda")
+    r_buf = torch.empty(count, device="cuda")
+    s_buf.uniform_(-1, 1, generator=g)
+    r_buf.zero_()
+    torch.cuda.synchronize()
+    calls0 = H.mxh_self_calls()
+    for _ in range(3):
+        assert H.mxh_allreduce(s_buf.data_ptr(), r_buf.data_ptr(), count, f32, SUM, self_comm) == 0
+    t0 = time.perf_counter()
+    for _ in range(iters):
+        H.mxh_allreduce(s_buf.data_ptr(), r_buf.data_ptr(), count, f32, SUM, self_comm)
+    per = (time.perf_counter() - t0) / iters
+    torch.cuda.synchronize()
+    same = bool(torch.equal(s_buf.view(torch.int32), r_buf.view(torch.int32)))
+    gbs = 2.0 * nbytes / per / 1e9
+    return {"what": "MPI_Allreduce fp32 SUM 256 MiB on a size-1 communicator (MPI_COMM_SELF), device buffers, "
+                    "through the communicator's allreduce slot (coll/mi355x size-1 path: one k_copy kernel)",
+            "slot_owner": owner, "bytes": nbytes, "ms": round(per * 1e3, 4), "hbm_gbs": round(gbs, 1),
+            "hbm_frac": round(gbs / HBM_PEAK_GBS, 4), "algorithmic_bytes": 2 * nbytes,
+            "busbw_gbs": 0.0, "busbw_note": "busBW = algbw*2(n-1)/n is 0 at n = 1: nothing crosses a link",
+            "delegated_to_coll_self": H.mxh_self_calls() - calls0,
+            "parity": "ok" if same else "MISMATCH: rbuf differs from sbuf"}
+
+
 def pack_side_by_side(torch, mx, cpu=True, packed_bytes=256 << 20, cpu_seconds=1.5):
     """MPI_Pack / MPI_Unpack of the CFG-C types on the device (mx_pack /
     mx_unpack, HIP events on the launch stream, median of 5 batches) and --
@@ -797,6 +839,10 @@ def main():
                                      "bit-compared with the same sum by a torch kernel (IEEE fp32 add)"},
         })
     if rank == 0 and world == 1:
+        try:
+            result["allreduce_n1"] = allreduce_n1(torch, mx)
+        except Exception as e:  # noqa: BLE001 - reported in the JSON line
+            result["allreduce_n1"] = {"error": repr(e)}
         # CFG-C beside the headline: device pack / unpack (+ the CPU walk)
         try:
             result["pack_unpack"] = pack_side_by_side(torch, mx, cpu=not args.no_cpu_baseline)

@@ -45,6 +45,8 @@ def host(with_components=True):
     H.mxh_comm_slot_owner.argtypes = [vp, ctypes.c_char_p]
     H.mxh_reduce_local.argtypes = [vp, vp, ci, vp, vp]
     H.mxh_op_reduce.argtypes = [vp, vp, vp, ci, vp]
+    H.mxh_3buff_op_reduce.argtypes = [vp, vp, vp, vp, ci, vp]
+    H.mxh_self_calls.argtypes = []
     H.mxh_allreduce.argtypes = [vp, vp, ci, vp, vp, vp]
     H.mxh_reduce_scatter.argtypes = [vp, vp, ctypes.POINTER(ci), vp, vp, vp]
     H.mxh_allgather.argtypes = [vp, ci, vp, vp, ci, vp, vp]

@@ -55,6 +55,34 @@ def test_base_path_without_components_matches_oracle():
                               minihost.op(H, "MPI_BXOR")) == -1
 
 
+def test_self_comm_host_buffers_run_coll_self():
+    """MPI_COMM_SELF without the components (no GPU): every slot is the
+    coll/self stand-in's local copy (coll_self_allreduce.c:41-44 ...), in
+    place a no-op, exscan untouched."""
+    H = minihost.host(with_components=False)
+    c = H.mxh_comm_self()
+    f32 = minihost.dtype(H, "MPI_FLOAT")
+    SUM = minihost.op(H, "MPI_SUM")
+    for s in ("allreduce", "reduce", "scan", "exscan", "reduce_scatter", "reduce_scatter_block", "allgather"):
+        assert H.mxh_comm_slot_owner(c, s.encode()) == b"self", s
+    src = np.arange(64, dtype=np.float32)
+    for call in (lambda r: H.mxh_allreduce(src.ctypes.data, r.ctypes.data, 64, f32, SUM, c),
+                 lambda r: H.mxh_reduce(src.ctypes.data, r.ctypes.data, 64, f32, SUM, 0, c),
+                 lambda r: H.mxh_scan(src.ctypes.data, r.ctypes.data, 64, f32, SUM, c),
+                 lambda r: H.mxh_reduce_scatter_block(src.ctypes.data, r.ctypes.data, 64, f32, SUM, c),
+                 lambda r: H.mxh_allgather(src.ctypes.data, 64, f32, r.ctypes.data, 64, f32, c)):
+        r = np.zeros(64, dtype=np.float32)
+        before = H.mxh_self_calls()
+        assert call(r) == 0
+        assert H.mxh_self_calls() == before + 1
+        np.testing.assert_array_equal(r, src)
+    r = np.full(64, 7, dtype=np.float32)
+    assert H.mxh_exscan(src.ctypes.data, r.ctypes.data, 64, f32, SUM, c) == 0
+    np.testing.assert_array_equal(r, 7)
+    assert H.mxh_allreduce(1, r.ctypes.data, 64, f32, SUM, c) == 0      # MPI_IN_PLACE
+    np.testing.assert_array_equal(r, 7)
+
+
 # ---------------------------------------------------------------------------
 torch = pytest.importorskip("torch")
 

@@ -147,3 +147,29 @@ def test_hook_declines_host_user_buffers():
                              rec["true_lb"], rec["true_ub"], rec["count"], user.ctypes.data - rec["true_lb"],
                              packed.ctypes.data, 0, 4096, 1, 0, ctypes.byref(calls))
     assert rc == -10
+
+
+def test_hook_recreated_datatype_at_the_same_address():
+    """A datatype freed and re-created with another stride often comes back
+    at the same addresses with the same record count: the hook's
+    handle cache keys on the records' contents too, so each layout packs its
+    own bytes.  The harness's datatype lives at one stack address; the records
+    are rewritten in place between calls."""
+    H = _host()
+    recs = np.zeros(2, dtype=[("flags", "<u2"), ("type", "<u2"), ("count", "<u4"), ("blocklen", "<u8"),
+                              ("extent", "<i8"), ("disp", "<i8")])
+    count, ext, size = 4099, 32, 16          # 4 blocks of 4 bytes in a 32-byte extent
+    rng = np.random.default_rng(9)
+    user = rng.integers(0, 256, count * ext, dtype=np.uint8)
+    U = torch.from_numpy(user).cuda()
+    for stride in (8, 6, 8, 4):
+        recs[0] = (0x0100, 9, 4, 4, stride, 0)   # DATA | OPAL_UINT1, 4 blocks of 4 bytes every `stride`
+        recs[1] = (0, 1, 1, 0, size, 0)          # END_LOOP
+        P = torch.zeros(count * size, dtype=torch.uint8, device="cuda")
+        calls = ci(0)
+        rc = H.mxh_convertor_run(recs.ctypes.data, 2, size, 0, ext, 0, 3 * stride + 4, count, U.data_ptr(),
+                                 P.data_ptr(), 0, count * size, 1, 0, ctypes.byref(calls))
+        assert rc == 0, rc
+        idx = (np.arange(count)[:, None, None] * ext + np.arange(4)[None, :, None] * stride
+               + np.arange(4)[None, None, :]).ravel()
+        assert np.array_equal(P.cpu().numpy(), user[idx]), f"stride {stride}"

@@ -261,8 +261,11 @@ struct mx_comm {
   int p2p_last_valid[3];             // work was enqueued on channel i since the last quiesce
   uint64_t *p2p_hfin, *p2p_hfin_dev; // mapped [3]: target of the last finished kernel per channel
   hipEvent_t p2p_ev;
-  uint64_t *p2p_lanes;     // device: finished-lane counters of the three streams
+  uint64_t *p2p_lanes;     // device: finished-lane counters of the three streams, [3] receive-launch exits
   uint64_t p2p_ltot[3];    // lanes (workgroups) of the transfer kernels enqueued per stream
+  uint64_t p2p_xtot;       // exits of the receive launches with a control workgroup (p2p_lanes[3])
+  hipEvent_t p2p_unpack_ev;          // after the last datatype receive's unpack
+  int p2p_unpack_pending;            // ... which p2p_channel_idle has not yet seen complete
   uint64_t p2p_host_msgs[mx::MAXR];   // envelopes enqueued per destination (the device's msgs)
   mx::P2PRndvTable *p2p_rndv;        // mapped host: pending rendezvous sends
   mx::P2PRndvTable *p2p_rndv_dev;    // its device address

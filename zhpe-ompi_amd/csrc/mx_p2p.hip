@@ -126,7 +126,21 @@ struct P2PDone {
   int64_t *done;         // mapped host word, or null
   uint64_t *hfin;        // mapped host word: `target` of the communicator's last finished kernel on this
                          // channel (what its destroy and quiet check wait for; no event per kernel)
+  uint64_t *exits;       // receive launches with a control workgroup: device count of the launch's
+  uint64_t xtarget;      // two exits (last lane, control); whichever makes it xtarget raises hfin
 };
+
+// the last lane's or the control workgroup's exit from a receive launch:
+// hfin is raised once both have left, so a communicator seen idle has no
+// workgroup of its own still reading its channel state (thread 0 only)
+__device__ __forceinline__ void rx_exit(const P2PDone &f) {
+  if (!f.hfin) return;
+  if (f.exits) {
+    const uint64_t old = __hip_atomic_fetch_add(f.exits, (uint64_t)1, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+    if (old + 1 != f.xtarget) return;
+  }
+  __hip_atomic_store(f.hfin, f.target, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
 
 // `wrote`: this lane stored user data without a fence after it (a receive
 // lane with data): make it visible device-wide before counting out -- work
@@ -814,7 +828,10 @@ __device__ void rx_control(const P2PRecvArgs &a) {
 // control workgroup (rx_control)
 __global__ void __launch_bounds__(kP2PThreads) k_p2p_recv(P2PRecvArgs a) {
   if (blockIdx.x >= P2P_L) {
-    rx_control(a);
+    if (threadIdx.x == 0) {
+      rx_control(a);
+      rx_exit(a.fin);
+    }
     return;
   }
   __shared__ HoldPlan plan;
@@ -869,7 +886,7 @@ __global__ void __launch_bounds__(kP2PThreads) k_p2p_recv(P2PRecvArgs a) {
       } else if (a.fin.done) {
         __hip_atomic_store(a.fin.done, (int64_t)1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
       }
-      if (a.fin.hfin) __hip_atomic_store(a.fin.hfin, a.fin.target, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      rx_exit(a.fin);
     }
   }
 }
@@ -967,11 +984,22 @@ static int p2p_note(mx_comm *c, int i) {
 // last lanes raise), or the channel's stream failed
 static bool p2p_channel_idle(mx_comm *c, int i) {
   if (!c->p2p_last_valid[i] || !c->p2p_hfin) return true;
+  // a datatype receive's unpack runs after the receive kernel raised the word
+  if (i == 1 && c->p2p_unpack_pending) {
+    if (hipEventQuery(c->p2p_unpack_ev) == hipErrorNotReady) {
+      (void)hipGetLastError();   // NotReady is no error of a later launch
+      return false;
+    }
+    (void)hipGetLastError();
+    c->p2p_unpack_pending = 0;
+  }
   if (__atomic_load_n(&c->p2p_hfin[i], __ATOMIC_ACQUIRE) >= c->p2p_ltot[i]) return true;
+  // a drained stream ran every kernel of the channel (a failed stream never
+  // raises the word either); the streams are shared, so idle is also idle
+  // for this communicator
   const hipError_t e = c->p2p_stream[i] ? hipStreamQuery(c->p2p_stream[i]) : hipSuccess;
-  if (e == hipErrorNotReady) return false;
   (void)hipGetLastError();
-  return e != hipSuccess;   // a failed stream never raises the word
+  return e != hipErrorNotReady;
 }
 
 static void p2p_channel_wait(mx_comm *c, int i) {
@@ -996,7 +1024,7 @@ int p2p_setup(mx_comm *c) {
   }
   const bool ok =
       (c->p2p_recv = (P2PRecvState *)pool_dev_get(rb)) != nullptr &&
-      (c->p2p_lanes = (uint64_t *)pool_dev_get(3 * sizeof(uint64_t))) != nullptr &&
+      (c->p2p_lanes = (uint64_t *)pool_dev_get(4 * sizeof(uint64_t))) != nullptr &&
       (c->p2p_stash = (char *)pool_dev_get(p2p_stash_bytes(c))) != nullptr &&
       (c->p2p_rndv_cur = (P2PRndvCur *)pool_dev_get(sizeof(P2PRndvCur))) != nullptr &&
       (c->p2p_rndv = (P2PRndvTable *)pool_host_get(sizeof(P2PRndvTable))) != nullptr &&
@@ -1036,13 +1064,16 @@ int p2p_setup(mx_comm *c) {
   c->p2p_rndv_free = new std::vector<int>();
   for (int i = P2P_RNDV_Q - 1; i >= 0; i--) c->p2p_rndv_free->push_back(i);
   c->p2p_ltot[0] = c->p2p_ltot[1] = c->p2p_ltot[2] = 0;
+  c->p2p_xtot = 0;
+  c->p2p_unpack_pending = 0;
   for (int j = 0; j < MAXR; j++) c->p2p_host_msgs[j] = 0;
   if (hipMemsetAsync(c->p2p_send, 0, sb, ls) != hipSuccess || hipMemsetAsync(c->p2p_recv, 0, rb, ls) != hipSuccess ||
-      hipMemsetAsync(c->p2p_lanes, 0, 3 * sizeof(uint64_t), ls) != hipSuccess ||
+      hipMemsetAsync(c->p2p_lanes, 0, 4 * sizeof(uint64_t), ls) != hipSuccess ||
       hipMemsetAsync(c->p2p_rndv_cur, 0, sizeof(P2PRndvCur), ls) != hipSuccess ||
       hipMemsetAsync(c->p2p_disp, 0, sizeof(P2PDisplaced), ls) != hipSuccess ||
       p2p_channels(c->p2p_stream) != MX_SUCCESS ||
       hipEventCreateWithFlags(&c->p2p_ev, hipEventDisableTiming) != hipSuccess ||
+      hipEventCreateWithFlags(&c->p2p_unpack_ev, hipEventDisableTiming) != hipSuccess ||
       hipStreamSynchronize(ls) != hipSuccess) {
     p2p_release(c);
     return MX_ERR_HIP;
@@ -1077,10 +1108,13 @@ void p2p_release(mx_comm *c) {
   c->p2p_hfin = c->p2p_hfin_dev = nullptr;
   if (c->p2p_stream[2]) (void)hipStreamDestroy(c->p2p_stream[2]);   // its own; [0], [1] are the device's
   if (c->p2p_ev) (void)hipEventDestroy(c->p2p_ev);
+  if (c->p2p_unpack_ev) (void)hipEventDestroy(c->p2p_unpack_ev);
+  c->p2p_unpack_ev = nullptr;
+  c->p2p_unpack_pending = 0;
   const size_t sb = sizeof(P2PSendState) * c->size, rb = sizeof(P2PRecvState) * c->size;
   pool_dev_put(c->p2p_send, sb);
   pool_dev_put(c->p2p_recv, rb);
-  pool_dev_put(c->p2p_lanes, 3 * sizeof(uint64_t));
+  pool_dev_put(c->p2p_lanes, 4 * sizeof(uint64_t));
   pool_dev_put(c->p2p_stash, p2p_stash_bytes(c));
   pool_dev_put(c->p2p_rndv_cur, sizeof(P2PRndvCur));
   pool_dev_put(c->p2p_disp, sizeof(P2PDisplaced));
@@ -1224,7 +1258,8 @@ int p2p_enqueue(mx_request *q, hipStream_t *done_stream) {
   fin.target = c->p2p_ltot[dir] + nl;
   fin.done = q->fast == 1 ? st_dev + 4 : nullptr;
   fin.hfin = c->p2p_hfin_dev + dir;
-  c->p2p_ltot[dir] += nl;   // every transfer kernel counts its lanes, flagged or not
+  fin.exits = nullptr;
+  fin.xtarget = 0;
   char *tmp = nullptr;
   if (q->ddt && bytes && hipMallocAsync((void **)&tmp, bytes, s) != hipSuccess) return MX_ERR_NOMEM;
   if (send) {
@@ -1260,7 +1295,9 @@ int p2p_enqueue(mx_request *q, hipStream_t *done_stream) {
     a.err = c->err_dev;
     a.fin = fin;
     hipLaunchKernelGGL(k_p2p_send, dim3(P2P_LE), dim3(kP2PThreads), 0, s, a);
-    if ((rc = mx_check_launch()) || (rc = p2p_note(c, 0))) return rc;
+    if ((rc = mx_check_launch())) return rc;
+    c->p2p_ltot[0] += nl;   // every launched transfer kernel counts its lanes, flagged or not
+    p2p_note(c, 0);
     if (rndv) {
       // the rendezvous kernel needs no event: the CTS it waits for follows
       // the envelope, which follows the caller's stream and the pack
@@ -1283,9 +1320,12 @@ int p2p_enqueue(mx_request *q, hipStream_t *done_stream) {
       ra.fin.target = c->p2p_ltot[2] + P2P_LR;
       ra.fin.done = nullptr;
       ra.fin.hfin = c->p2p_hfin_dev + 2;
-      c->p2p_ltot[2] += P2P_LR;
+      ra.fin.exits = nullptr;
+      ra.fin.xtarget = 0;
       hipLaunchKernelGGL(k_p2p_rndv, dim3(P2P_LR), dim3(kP2PThreads), 0, c->p2p_stream[2], ra);
-      if ((rc = mx_check_launch()) || (rc = p2p_note(c, 2))) return rc;
+      if ((rc = mx_check_launch())) return rc;
+      c->p2p_ltot[2] += P2P_LR;
+      p2p_note(c, 2);
       return MX_SUCCESS;   // tmp is freed when the request completes (p2p_finish)
     }
   } else {
@@ -1314,7 +1354,6 @@ int p2p_enqueue(mx_request *q, hipStream_t *done_stream) {
     a.err = c->err_dev;
     q->tmp = tmp;   // freed at completion: a receive that yields runs (and unpacks) again
     q->post = ++c->p2p_posts;
-    c->p2p_ltot[dir] -= nl;   // p2p_rx_launch counts the lanes of each launch
     if ((rc = p2p_rx_launch(q))) {
       p2p_finish(q);
       return rc;
@@ -1364,7 +1403,8 @@ int p2p_rx_launch(mx_request *q) {
   a.fin.target = c->p2p_ltot[1] + P2P_L;
   a.fin.done = q->fast == 1 ? a.status + 4 : nullptr;
   a.fin.hfin = c->p2p_hfin_dev + 1;
-  c->p2p_ltot[1] += P2P_L;
+  a.fin.exits = a.rq ? c->p2p_lanes + 3 : nullptr;
+  a.fin.xtarget = c->p2p_xtot + 2;
   int rc;
   if (a.any) {
     P2PPickArgs pa;
@@ -1387,8 +1427,15 @@ int p2p_rx_launch(mx_request *q) {
   }
   hipLaunchKernelGGL(k_p2p_recv, dim3(a.rq ? P2P_L + 1 : P2P_L), dim3(kP2PThreads), 0, s, a);
   if ((rc = mx_check_launch())) return rc;
-  if (q->tmp && (rc = mx_unpack(q->ddt, q->count, q->rbuf, q->tmp, 0, a.cap, s))) return rc;
-  return p2p_note(c, 1);
+  c->p2p_ltot[1] += P2P_L;   // counted once launched: a failed launch never raises the word
+  if (a.rq) c->p2p_xtot += 2;
+  p2p_note(c, 1);
+  if (q->tmp) {   // the unpack reads tmp and writes the user buffer after the word is raised
+    if ((rc = mx_unpack(q->ddt, q->count, q->rbuf, q->tmp, 0, a.cap, s))) return rc;
+    if (hipEventRecord(c->p2p_unpack_ev, s) != hipSuccess) return MX_ERR_HIP;
+    c->p2p_unpack_pending = 1;
+  }
+  return MX_SUCCESS;
 }
 
 bool p2p_rx_active() {

@@ -815,26 +815,178 @@ static int mx_coll_bcast(void *buf, int count, struct ompi_datatype_t *dtype, in
     return ret;
 }
 
-/* MPI_Reduce_local has no peers: the per-call buffer check is all it needs */
+/* inout = inout OP in on device memory */
+static int reduce_local_dev(mx_coll_module_t *m, int opi, int slot, const void *in, void *inout, size_t count)
+{
+    int rc = begin(m);
+    if (g_fast_sync < 0) g_fast_sync = mx_ompi_host->mca_int("coll_mi355x_fast_sync", 1) != 0;
+    if (!rc && g_fast_sync) {   /* completion word: from small reduce launches themselves, else a marker kernel */
+        rc = mx_reduce2_sync(opi, slot, in, inout, count, m->stream);
+    } else {
+        if (!rc) rc = mx_reduce2(opi, slot, in, inout, count, m->stream);
+        if (!rc) rc = stream_wait(m->stream);
+    }
+    return rc;
+}
+
+/* MPI_Reduce_local has no peers: the per-call buffer check is all it needs.
+ * Operands in different memories (MPI_Reduce_local(device_in, host_inout) is
+ * legal) are staged one by one, as coll/cuda checks each buffer
+ * (coll_cuda_allreduce.c:44-62): a device inout gets a host `in` copied to
+ * device scratch; a host inout gets the device `in` copied to host memory and
+ * the saved slot runs when the call is at most coll_mi355x_mixed_host_max_kb
+ * (default 64 KiB), else inout goes to device scratch and comes back. */
 static int mx_coll_reduce_local(const void *inbuf, void *inoutbuf, int count, struct ompi_datatype_t *dtype,
                                 struct ompi_op_t *op, mca_coll_base_module_t *module)
 {
     mx_coll_module_t *m = (mx_coll_module_t *)module;
     int slot, opi;
-    if (reducible(dtype, op, (size_t)count, 1, &slot, &opi) && mx_is_device_ptr(inbuf) == 1 &&
-        mx_is_device_ptr(inoutbuf) == 1) {
-        if (!m->stream && mx_stream_create_ordered(&m->stream) != MX_SUCCESS) m->stream = NULL;
-        int rc = begin(m);
-        if (g_fast_sync < 0) g_fast_sync = mx_ompi_host->mca_int("coll_mi355x_fast_sync", 1) != 0;
-        if (!rc && g_fast_sync) {   /* completion word: from small reduce launches themselves, else a marker kernel */
-            rc = mx_reduce2_sync(opi, slot, inbuf, inoutbuf, (size_t)count, m->stream);
-        } else {
-            if (!rc) rc = mx_reduce2(opi, slot, inbuf, inoutbuf, (size_t)count, m->stream);
-            if (!rc) rc = stream_wait(m->stream);
+    const int din = mx_is_device_ptr(inbuf) == 1, dio = mx_is_device_ptr(inoutbuf) == 1;
+    if ((din || dio) && reducible(dtype, op, (size_t)count, 1, &slot, &opi)) {
+        ensure_stream(m);
+        if (din && dio) return map_rc(reduce_local_dev(m, opi, slot, inbuf, inoutbuf, (size_t)count));
+        const size_t bytes = (size_t)count * mx_type_size(slot);
+        const int kb = mx_ompi_host->mca_int("coll_mi355x_mixed_host_max_kb", 64);
+        void *a, *b;
+        int rc;
+        if (!dio && bytes <= (kb > 0 ? (size_t)kb << 10 : 0)) {   /* small, host result: `in` to the host */
+            if ((rc = hbuf(m, SCR_IN, bytes, &a)) || (rc = mx_memcpy(a, inbuf, bytes, m->stream)) ||
+                (rc = stream_wait(m->stream)))
+                return map_rc(rc);
+            return m->prev_reduce_local(a, inoutbuf, count, dtype, op, m->prev_reduce_local_module);
         }
+        a = (void *)inbuf;
+        b = inoutbuf;
+        if (!din && ((rc = scratch(m, SCR_IN, bytes, &a)) || (rc = mx_memcpy(a, inbuf, bytes, m->stream))))
+            return map_rc(rc);
+        if (!dio && ((rc = scratch(m, SCR_OUT, bytes, &b)) || (rc = mx_memcpy(b, inoutbuf, bytes, m->stream))))
+            return map_rc(rc);
+        rc = reduce_local_dev(m, opi, slot, a, b, (size_t)count);
+        if (!rc && b != inoutbuf && !(rc = mx_memcpy(inoutbuf, b, bytes, m->stream))) rc = stream_wait(m->stream);
         return map_rc(rc);
     }
     return m->prev_reduce_local(inbuf, inoutbuf, count, dtype, op, m->prev_reduce_local_module);
+}
+
+/* ---- size-1 communicators (MPI_COMM_SELF, a one-rank MPI_COMM_WORLD) -------
+ * coll/self answers every collective of a size-1 communicator with a local
+ * copy: ompi_datatype_copy_content_same_ddt for allreduce / reduce / scan /
+ * reduce_scatter (coll_self_allreduce.c:41-44, coll_self_reduce.c,
+ * coll_self_scan.c, coll_self_reduce_scatter.c:44), ompi_datatype_sndrcv for
+ * allgather; exscan and bcast touch nothing.  Those walk host memory: without
+ * the CUDA copy hooks (opal_datatype_copy.c:75-136, SET_CUDA_COPY_FCT) a
+ * device buffer is read and written with host memcpy.  coll/cuda does not
+ * exclude size 1 and stages every device buffer (coll_cuda_module.c:78-113,
+ * coll_cuda_allreduce.c:44-72).  Here the copy runs on the device when either
+ * buffer is device memory -- one K7 copy kernel (2 x bytes of HBM traffic)
+ * for contiguous layouts, the device convertor for derived ones (packed
+ * straight into a contiguous destination, unpacked straight from a contiguous
+ * source) -- and host-only calls go to the saved slot. */
+static int self_device(const void *sbuf, const void *rbuf)
+{
+    return (sbuf != MPI_IN_PLACE && mx_is_device_ptr(sbuf) == 1) || mx_is_device_ptr(rbuf) == 1;
+}
+
+/* scount x sdt at sbuf -> rcount x rdt at rbuf (equal type signatures) */
+static int self_copy(mx_coll_module_t *m, const void *sbuf, struct ompi_datatype_t *sdt, size_t scount, void *rbuf,
+                     struct ompi_datatype_t *rdt, size_t rcount)
+{
+    const size_t bytes = scount * mx_ompi_host->dtype_size(sdt);
+    if (bytes != rcount * mx_ompi_host->dtype_size(rdt)) return MX_ERR_ARG;
+    if (!bytes) return MX_SUCCESS;
+    if (scount > INT_MAX || rcount > INT_MAX) return MX_ERR_UNSUPPORTED;
+    ensure_stream(m);
+    const int sc = mx_ompi_host->dtype_contiguous(sdt, (int)scount);
+    const int rcn = mx_ompi_host->dtype_contiguous(rdt, (int)rcount);
+    const int rdev = mx_is_device_ptr(rbuf) == 1;
+    int rc;
+    if (sc && rcn) {
+        rc = (rdev && mx_is_device_ptr(sbuf) == 1) ? mx_copy(rbuf, sbuf, bytes, m->stream)
+                                                   : mx_memcpy(rbuf, sbuf, bytes, m->stream);
+    } else if (rcn && rdev) {   /* pack straight into the destination */
+        xbuf_t s = {.user = (void *)sbuf, .bytes = bytes, .dt = sdt, .count = (int)scount, .contiguous = 0};
+        rc = xfer_packed(m, &s, rbuf, 1);
+    } else {                    /* the packed input on the device, unpacked into rbuf */
+        xbuf_t s;
+        rc = xin(m, SCR_IN, sbuf, sdt, scount, 1, &s);
+        if (!rc && rcn) {
+            rc = mx_memcpy(rbuf, s.dev, bytes, m->stream);
+        } else if (!rc) {
+            xbuf_t r = {.user = rbuf, .bytes = bytes, .dt = rdt, .count = (int)rcount, .contiguous = 0};
+            rc = xfer_packed(m, &r, s.dev, 0);
+        }
+    }
+    return rc ? rc : stream_wait(m->stream);
+}
+
+static int mx_self_allreduce(const void *sbuf, void *rbuf, int count, struct ompi_datatype_t *dtype,
+                             struct ompi_op_t *op, struct ompi_communicator_t *comm, mca_coll_base_module_t *module)
+{
+    mx_coll_module_t *m = (mx_coll_module_t *)module;
+    if (sbuf == MPI_IN_PLACE) return OMPI_SUCCESS;
+    if (!self_device(sbuf, rbuf)) return m->prev_allreduce(sbuf, rbuf, count, dtype, op, comm, m->prev_allreduce_module);
+    return map_rc(self_copy(m, sbuf, dtype, (size_t)count, rbuf, dtype, (size_t)count));
+}
+
+static int mx_self_reduce_scatter(const void *sbuf, void *rbuf, const int *rcounts, struct ompi_datatype_t *dtype,
+                                  struct ompi_op_t *op, struct ompi_communicator_t *comm,
+                                  mca_coll_base_module_t *module)
+{
+    mx_coll_module_t *m = (mx_coll_module_t *)module;
+    if (sbuf == MPI_IN_PLACE) return OMPI_SUCCESS;
+    if (!self_device(sbuf, rbuf))
+        return m->prev_reduce_scatter(sbuf, rbuf, rcounts, dtype, op, comm, m->prev_reduce_scatter_module);
+    return map_rc(self_copy(m, sbuf, dtype, (size_t)rcounts[0], rbuf, dtype, (size_t)rcounts[0]));
+}
+
+static int mx_self_reduce_scatter_block(const void *sbuf, void *rbuf, int rcount, struct ompi_datatype_t *dtype,
+                                        struct ompi_op_t *op, struct ompi_communicator_t *comm,
+                                        mca_coll_base_module_t *module)
+{
+    mx_coll_module_t *m = (mx_coll_module_t *)module;
+    if (sbuf == MPI_IN_PLACE) return OMPI_SUCCESS;   /* the result is rbuf's first rcount elements already */
+    if (!self_device(sbuf, rbuf))
+        return m->prev_reduce_scatter_block(sbuf, rbuf, rcount, dtype, op, comm, m->prev_reduce_scatter_block_module);
+    return map_rc(self_copy(m, sbuf, dtype, (size_t)rcount, rbuf, dtype, (size_t)rcount));
+}
+
+static int mx_self_allgather(const void *sbuf, int scount, struct ompi_datatype_t *sdtype, void *rbuf, int rcount,
+                             struct ompi_datatype_t *rdtype, struct ompi_communicator_t *comm,
+                             mca_coll_base_module_t *module)
+{
+    mx_coll_module_t *m = (mx_coll_module_t *)module;
+    if (sbuf == MPI_IN_PLACE) return OMPI_SUCCESS;
+    if (!self_device(sbuf, rbuf))
+        return m->prev_allgather(sbuf, scount, sdtype, rbuf, rcount, rdtype, comm, m->prev_allgather_module);
+    return map_rc(self_copy(m, sbuf, sdtype, (size_t)scount, rbuf, rdtype, (size_t)rcount));
+}
+
+static int mx_self_reduce(const void *sbuf, void *rbuf, int count, struct ompi_datatype_t *dtype, struct ompi_op_t *op,
+                          int root, struct ompi_communicator_t *comm, mca_coll_base_module_t *module)
+{
+    mx_coll_module_t *m = (mx_coll_module_t *)module;
+    if (sbuf == MPI_IN_PLACE) return OMPI_SUCCESS;
+    if (!self_device(sbuf, rbuf))
+        return m->prev_reduce(sbuf, rbuf, count, dtype, op, root, comm, m->prev_reduce_module);
+    return map_rc(self_copy(m, sbuf, dtype, (size_t)count, rbuf, dtype, (size_t)count));
+}
+
+static int mx_self_scan(const void *sbuf, void *rbuf, int count, struct ompi_datatype_t *dtype, struct ompi_op_t *op,
+                        struct ompi_communicator_t *comm, mca_coll_base_module_t *module)
+{
+    mx_coll_module_t *m = (mx_coll_module_t *)module;
+    if (sbuf == MPI_IN_PLACE) return OMPI_SUCCESS;
+    if (!self_device(sbuf, rbuf)) return m->prev_scan(sbuf, rbuf, count, dtype, op, comm, m->prev_scan_module);
+    return map_rc(self_copy(m, sbuf, dtype, (size_t)count, rbuf, dtype, (size_t)count));
+}
+
+/* rank 0's exscan result is undefined: nothing is read or written
+ * (coll_self_exscan.c), whatever memory the buffers are in */
+static int mx_self_exscan(const void *sbuf, void *rbuf, int count, struct ompi_datatype_t *dtype, struct ompi_op_t *op,
+                          struct ompi_communicator_t *comm, mca_coll_base_module_t *module)
+{
+    (void)sbuf; (void)rbuf; (void)count; (void)dtype; (void)op; (void)comm; (void)module;
+    return OMPI_SUCCESS;
 }
 
 /* Reduction slots beyond the four of the north star:
@@ -1674,6 +1826,24 @@ static int mx_coll_module_enable(mca_coll_base_module_t *module, struct ompi_com
     mx_coll_module_t *m = (mx_coll_module_t *)module;
     const int n = mx_ompi_host->comm_size(comm);
     m->comm = comm;
+    if (n == 1) {
+        /* size 1: a slot whose lower module is missing is left to the
+         * framework (cleared before mca_coll_base_comm_select copies it) */
+#define SAVE_PREV_SELF(name)                                                                        \
+    if (m->super.coll_##name) {                                                                     \
+        mca_coll_base_module_t *pm_ = NULL;                                                         \
+        m->prev_##name = (__typeof__(m->prev_##name))mx_ompi_host->comm_coll_fn(comm, #name, &pm_); \
+        m->prev_##name##_module = pm_;                                                              \
+        if (m->prev_##name && pm_) MX_OBJ_RETAIN(pm_);                                              \
+        else { m->prev_##name = NULL; m->prev_##name##_module = NULL; m->super.coll_##name = NULL; } \
+    }
+        SAVE_PREV_SELF(allreduce) SAVE_PREV_SELF(reduce_scatter) SAVE_PREV_SELF(allgather) SAVE_PREV_SELF(reduce)
+        SAVE_PREV_SELF(reduce_scatter_block) SAVE_PREV_SELF(scan)
+#undef SAVE_PREV_SELF
+        if (m->super.coll_reduce_local) SAVE_PREV(m, comm, reduce_local, mca_coll_base_module_reduce_local_fn_t);
+        m->mx_state = -1;   /* no peers: no device communicator */
+        return OMPI_SUCCESS;
+    }
     if (m->super.coll_allreduce) {
         SAVE_PREV(m, comm, allreduce, mca_coll_base_module_allreduce_fn_t);
         SAVE_PREV(m, comm, reduce_scatter, mca_coll_base_module_reduce_scatter_fn_t);
@@ -1760,15 +1930,18 @@ static mca_coll_base_module_t *mx_coll_component_comm_query(struct ompi_communic
         MX_NB_SLOTS(SET_NB)
 #undef SET_NB
     } else {
-        /* size-1 comms (MPI_COMM_SELF): MPI_Reduce_local lands here when
-         * our priority beats coll/self's 75 (coll_self_module.c:60,84) */
-        m->super.coll_allreduce = NULL;
+        /* size-1 comms (MPI_COMM_SELF): coll/self's slots (priority 75,
+         * coll_self_module.c:60-84) with device copies for device buffers;
+         * MPI_Reduce_local lands here when our priority beats 75 */
+        m->super.coll_allreduce = mx_self_allreduce;
+        m->super.coll_reduce_scatter = mx_self_reduce_scatter;
+        m->super.coll_allgather = mx_self_allgather;
+        m->super.coll_reduce = mx_self_reduce;
+        m->super.coll_reduce_scatter_block = mx_self_reduce_scatter_block;
+        m->super.coll_scan = mx_self_scan;
+        m->super.coll_exscan = mx_self_exscan;
     }
     if (*priority > 75) m->super.coll_reduce_local = mx_coll_reduce_local;
-    if (n == 1 && !m->super.coll_reduce_local) {
-        MX_OBJ_RELEASE(m);
-        return NULL;
-    }
     return &m->super;
 }
 

@@ -43,11 +43,20 @@
 #include "mx_kernels.h"
 
 #define MX_CONV_CACHE 64
+#define MX_REC_BYTES 32                   /* sizeof(dt_elem_desc_t) */
 
+/* Cached device handles, keyed by the datatype AND a copy of its committed
+ * records, size and bounds: a datatype freed and re-created per iteration
+ * (MPI_Type_vector with a new stride, say) often comes back at the same
+ * addresses with the same record count.  g_mu is held from the lookup to the
+ * end of the fragment's kernels, so an eviction never destroys a handle in
+ * use. */
 static pthread_mutex_t g_mu = PTHREAD_MUTEX_INITIALIZER;
 static struct {
     const void *dt, *desc;
-    size_t used;
+    size_t used, size;
+    ptrdiff_t lb, ub;
+    void *recs;
     mx_ddt_t *h;
     uint64_t tick;
 } g_cache[MX_CONV_CACHE];
@@ -57,30 +66,41 @@ static void *g_bounce;                    /* device staging for host fragments *
 static size_t g_bounce_bytes;
 
 /* the device representation of a committed datatype: its opt_desc records
- * verbatim (opal_datatype.h:126), built once per (datatype, description) */
-static mx_ddt_t *ddt_for(const opal_datatype_t *dt, const dt_type_desc_t *d)
+ * verbatim (opal_datatype.h:126), built once per (datatype, description);
+ * the caller holds g_mu */
+static mx_ddt_t *ddt_for_locked(const opal_datatype_t *dt, const dt_type_desc_t *d)
 {
-    mx_ddt_t *h = NULL;
-    pthread_mutex_lock(&g_mu);
+    const size_t rb = ((size_t)d->used + 1) * MX_REC_BYTES;
     int victim = 0;
     for (int i = 0; i < MX_CONV_CACHE; i++) {
-        if (g_cache[i].dt == dt && g_cache[i].desc == d->desc && g_cache[i].used == d->used && g_cache[i].h) {
+        if (g_cache[i].h && g_cache[i].dt == dt && g_cache[i].desc == d->desc && g_cache[i].used == d->used &&
+            g_cache[i].size == dt->size && g_cache[i].lb == dt->lb && g_cache[i].ub == dt->ub &&
+            !memcmp(g_cache[i].recs, d->desc, rb)) {
             g_cache[i].tick = ++g_tick;
-            h = g_cache[i].h;
-            break;
+            return g_cache[i].h;
         }
         if (g_cache[i].tick < g_cache[victim].tick) victim = i;
     }
-    if (!h && mx_ddt_create(d->desc, d->used + 1, NULL, dt->size, dt->lb, dt->ub, &h) == MX_SUCCESS) {
-        if (g_cache[victim].h) mx_ddt_destroy(g_cache[victim].h);
-        g_cache[victim].dt = dt;
-        g_cache[victim].desc = d->desc;
-        g_cache[victim].used = d->used;
-        g_cache[victim].h = h;
-        g_cache[victim].tick = ++g_tick;
+    void *recs = malloc(rb);
+    mx_ddt_t *h = NULL;
+    if (!recs) return NULL;
+    memcpy(recs, d->desc, rb);
+    if (mx_ddt_create(d->desc, d->used + 1, NULL, dt->size, dt->lb, dt->ub, &h) != MX_SUCCESS) {
+        free(recs);
+        return NULL;
     }
-    if (h && !g_stream && mx_stream_create_ordered(&g_stream) != MX_SUCCESS) g_stream = NULL;
-    pthread_mutex_unlock(&g_mu);
+    if (g_cache[victim].h) mx_ddt_destroy(g_cache[victim].h);
+    free(g_cache[victim].recs);
+    g_cache[victim].dt = dt;
+    g_cache[victim].desc = d->desc;
+    g_cache[victim].used = d->used;
+    g_cache[victim].size = dt->size;
+    g_cache[victim].lb = dt->lb;
+    g_cache[victim].ub = dt->ub;
+    g_cache[victim].recs = recs;
+    g_cache[victim].h = h;
+    g_cache[victim].tick = ++g_tick;
+    if (!g_stream && mx_stream_create_ordered(&g_stream) != MX_SUCCESS) g_stream = NULL;
     return h;
 }
 
@@ -104,12 +124,15 @@ static int32_t advance(opal_convertor_t *c, struct iovec *iov, uint32_t *out_siz
         *max_data = 0;
         return 1;
     }
-    mx_ddt_t *h = ddt_for(c->pDesc, c->use_desc);
-    if (!h) return -1;
+    pthread_mutex_lock(&g_mu);              /* the handle and the one bounce buffer */
+    mx_ddt_t *h = ddt_for_locked(c->pDesc, c->use_desc);
+    if (!h || !g_stream) {
+        pthread_mutex_unlock(&g_mu);
+        return -1;
+    }
     size_t done = 0;
     uint32_t i = 0;
     int rc = MX_SUCCESS;
-    pthread_mutex_lock(&g_mu);              /* one bounce buffer */
     for (; i < *out_size && c->bConverted + done < c->local_size && rc == MX_SUCCESS; i++) {
         size_t len = iov[i].iov_len;
         if (len > c->local_size - (c->bConverted + done)) len = c->local_size - (c->bConverted + done);
@@ -168,7 +191,10 @@ int mca_convertor_mi355x_prepare(opal_convertor_t *c)
     if ((c->flags & (CONVERTOR_NO_OP | CONVERTOR_WITH_CHECKSUM)) || !(c->flags & CONVERTOR_HOMOGENEOUS)) return 0;
     if (!(c->flags & (CONVERTOR_SEND | CONVERTOR_RECV))) return 0;
     if (!mx_is_device_ptr(c->pBaseBuf + c->pDesc->true_lb)) return 0;
-    if (!ddt_for(c->pDesc, c->use_desc) || !g_stream) return 0;
+    pthread_mutex_lock(&g_mu);
+    const int ok = ddt_for_locked(c->pDesc, c->use_desc) && g_stream;
+    pthread_mutex_unlock(&g_mu);
+    if (!ok) return 0;
     c->fAdvance = (c->flags & CONVERTOR_SEND) ? mca_convertor_mi355x_pack : mca_convertor_mi355x_unpack;
     return 1;
 }

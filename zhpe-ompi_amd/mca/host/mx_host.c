@@ -7,6 +7,8 @@
 #define _GNU_SOURCE
 #include <dlfcn.h>
 #include <stdio.h>
+#include <sys/uio.h>
+#include <unistd.h>
 #include <stdlib.h>
 #include <string.h>
 #include <time.h>
@@ -675,6 +677,80 @@ static int base_reduce_local(const void *in, void *inout, int count, struct ompi
     return OMPI_SUCCESS;
 }
 
+/* ---- coll/self (priority 75, coll_self_module.c:60-84) on size-1
+ * communicators: local copies over HOST memory (ompi_datatype_copy_content_
+ * same_ddt, coll_self_allreduce.c:41-44; ompi_datatype_sndrcv for allgather),
+ * in place a no-op; exscan and bcast touch nothing.  reduce_scatter_block is
+ * coll/basic's on one rank (reduce to 0, then scatter): the same copy.
+ * g_self_calls counts the calls that reached these functions, so a test sees
+ * what was delegated to them. */
+static int g_self_calls;
+int mxh_self_calls(void) { return g_self_calls; }
+static int self_copy(const void *s, struct ompi_datatype_t *sdt, int scount, void *r, struct ompi_datatype_t *rdt,
+                     int rcount)
+{
+    g_self_calls++;
+    if (s == MPI_IN_PLACE) return OMPI_SUCCESS;
+    const size_t b = (size_t)scount * sdt->size;
+    if (b != (size_t)rcount * rdt->size) return OMPI_ERROR;
+    char *tmp = malloc(b + 1);
+    if (!tmp) return OMPI_ERR_OUT_OF_RESOURCE;
+    dtype_pack(sdt, scount, s, tmp);
+    dtype_unpack(rdt, rcount, tmp, r);
+    free(tmp);
+    return OMPI_SUCCESS;
+}
+static int self_allreduce(const void *sbuf, void *rbuf, int count, struct ompi_datatype_t *dt, struct ompi_op_t *op,
+                          struct ompi_communicator_t *c, mca_coll_base_module_t *m)
+{
+    (void)op; (void)c; (void)m;
+    return self_copy(sbuf, dt, count, rbuf, dt, count);
+}
+static int self_reduce_scatter(const void *sbuf, void *rbuf, const int *rcounts, struct ompi_datatype_t *dt,
+                               struct ompi_op_t *op, struct ompi_communicator_t *c, mca_coll_base_module_t *m)
+{
+    (void)op; (void)c; (void)m;
+    return self_copy(sbuf, dt, rcounts[0], rbuf, dt, rcounts[0]);
+}
+static int self_reduce_scatter_block(const void *sbuf, void *rbuf, int rcount, struct ompi_datatype_t *dt,
+                                     struct ompi_op_t *op, struct ompi_communicator_t *c, mca_coll_base_module_t *m)
+{
+    (void)op; (void)c; (void)m;
+    return self_copy(sbuf, dt, rcount, rbuf, dt, rcount);
+}
+static int self_allgather(const void *sbuf, int scount, struct ompi_datatype_t *sdt, void *rbuf, int rcount,
+                          struct ompi_datatype_t *rdt, struct ompi_communicator_t *c, mca_coll_base_module_t *m)
+{
+    (void)c; (void)m;
+    return self_copy(sbuf, sdt, scount, rbuf, rdt, rcount);
+}
+static int self_bcast(void *buf, int count, struct ompi_datatype_t *dt, int root, struct ompi_communicator_t *c,
+                      mca_coll_base_module_t *m)
+{
+    (void)buf; (void)count; (void)dt; (void)root; (void)c; (void)m;
+    g_self_calls++;
+    return OMPI_SUCCESS;
+}
+static int self_reduce(const void *sbuf, void *rbuf, int count, struct ompi_datatype_t *dt, struct ompi_op_t *op,
+                       int root, struct ompi_communicator_t *c, mca_coll_base_module_t *m)
+{
+    (void)op; (void)root; (void)c; (void)m;
+    return self_copy(sbuf, dt, count, rbuf, dt, count);
+}
+static int self_scan(const void *sbuf, void *rbuf, int count, struct ompi_datatype_t *dt, struct ompi_op_t *op,
+                     struct ompi_communicator_t *c, mca_coll_base_module_t *m)
+{
+    (void)op; (void)c; (void)m;
+    return self_copy(sbuf, dt, count, rbuf, dt, count);
+}
+static int self_exscan(const void *sbuf, void *rbuf, int count, struct ompi_datatype_t *dt, struct ompi_op_t *op,
+                       struct ompi_communicator_t *c, mca_coll_base_module_t *m)
+{
+    (void)sbuf; (void)rbuf; (void)count; (void)dt; (void)op; (void)c; (void)m;
+    g_self_calls++;
+    return OMPI_SUCCESS;
+}
+
 /* ---- tuned ---- */
 static int tuned_allreduce(const void *sbuf, void *rbuf, int count, struct ompi_datatype_t *dt, struct ompi_op_t *op,
                            struct ompi_communicator_t *c, mca_coll_base_module_t *m)
@@ -1093,6 +1169,14 @@ static int comm_select(struct ompi_communicator_t *c, int is_self)
         mca_coll_base_module_t *b = &g_self_coll;
         static_module(b, &g_static_class);
         b->coll_reduce_local = base_reduce_local;
+        b->coll_allreduce = self_allreduce;
+        b->coll_reduce_scatter = self_reduce_scatter;
+        b->coll_allgather = self_allgather;
+        b->coll_bcast = self_bcast;
+        b->coll_reduce = self_reduce;
+        b->coll_reduce_scatter_block = self_reduce_scatter_block;
+        b->coll_scan = self_scan;
+        b->coll_exscan = self_exscan;
         COPY(b, "self");
         base_prio = 75;
     } else {
@@ -1281,6 +1365,18 @@ int mxh_op_reduce(void *opv, const void *source, void *target, int count, void *
     struct ompi_datatype_t *d = dt;
     if (!d || d->slot < 0 || !op->intrinsic.fns[d->slot]) return -1;
     op_reduce(op, source, target, count, d);
+    return 0;
+}
+
+/* ompi_3buff_op_reduce(op, source1, source2, target, count, dtype) (op.h:618-660) */
+int mxh_3buff_op_reduce(void *opv, const void *source1, const void *source2, void *target, int count, void *dt)
+{
+    struct ompi_op_t *op = opv;
+    struct ompi_datatype_t *d = dt;
+    int cnt = count;
+    if (!d || d->slot < 0 || !op->o_3buff_intrinsic.fns[d->slot]) return -1;
+    op->o_3buff_intrinsic.fns[d->slot]((void *)source1, (void *)source2, target, &cnt, &d,
+                                       op->o_3buff_intrinsic.modules[d->slot]);
     return 0;
 }
 
@@ -1578,6 +1674,68 @@ static mca_btl_base_module_t g_btl;
 static int (*g_btl_progress)(void);
 static int g_btl_ready;
 
+/* The stand-in's own host single-copy RDMA (vader's CMA / xpmem path,
+ * btl_sm_component.c:487, btl_sm_xpmem.c:70): a registration is {pid, base,
+ * size}; get / put copy with process_vm_readv / _writev (memcpy within the
+ * process) and call back at once, as vader's CMA get does.  g_host_btl_calls
+ * counts what reached these slots. */
+typedef struct { uint64_t magic; int64_t pid; uint64_t base, size; } mxh_host_reg_t;
+#define MXH_HOST_REG_MAGIC 0x484f5354524547ull
+static int g_host_btl_calls;
+int mxh_btl_host_calls(void) { return g_host_btl_calls; }
+static struct mca_btl_base_registration_handle_t *host_btl_register(mca_btl_base_module_t *btl,
+                                                                    struct mca_btl_base_endpoint_t *ep, void *base,
+                                                                    size_t size, uint32_t flags)
+{
+    (void)btl; (void)ep; (void)flags;
+    g_host_btl_calls++;
+    mxh_host_reg_t *r = calloc(1, sizeof *r);
+    if (!r) return NULL;
+    *r = (mxh_host_reg_t){MXH_HOST_REG_MAGIC, (int64_t)getpid(), (uint64_t)(uintptr_t)base, size};
+    return (struct mca_btl_base_registration_handle_t *)r;
+}
+static int host_btl_deregister(mca_btl_base_module_t *btl, struct mca_btl_base_registration_handle_t *h)
+{
+    (void)btl;
+    g_host_btl_calls++;
+    free(h);
+    return OPAL_SUCCESS;
+}
+static int host_btl_rdma(int get, mca_btl_base_module_t *btl, struct mca_btl_base_endpoint_t *ep, void *local,
+                         uint64_t raddr, struct mca_btl_base_registration_handle_t *rh, size_t size,
+                         mca_btl_base_rdma_completion_fn_t cb, void *ctx, void *data)
+{
+    const mxh_host_reg_t *r = (const mxh_host_reg_t *)rh;
+    g_host_btl_calls++;
+    if (!r || r->magic != MXH_HOST_REG_MAGIC || raddr < r->base || raddr + size > r->base + r->size)
+        return OPAL_ERR_BAD_PARAM;
+    if (r->pid == (int64_t)getpid()) {
+        if (get) memcpy(local, (void *)(uintptr_t)raddr, size);
+        else memcpy((void *)(uintptr_t)raddr, local, size);
+    } else {
+        struct iovec l = {local, size}, rv = {(void *)(uintptr_t)raddr, size};
+        const ssize_t n = get ? process_vm_readv((pid_t)r->pid, &l, 1, &rv, 1, 0)
+                              : process_vm_writev((pid_t)r->pid, &l, 1, &rv, 1, 0);
+        if (n != (ssize_t)size) return OPAL_ERROR;
+    }
+    if (cb) cb(btl, ep, local, NULL, ctx, data, OPAL_SUCCESS);
+    return OPAL_SUCCESS;
+}
+static int host_btl_get(mca_btl_base_module_t *btl, struct mca_btl_base_endpoint_t *ep, void *local, uint64_t raddr,
+                        struct mca_btl_base_registration_handle_t *lh, struct mca_btl_base_registration_handle_t *rh,
+                        size_t size, int flags, int order, mca_btl_base_rdma_completion_fn_t cb, void *ctx, void *data)
+{
+    (void)lh; (void)flags; (void)order;
+    return host_btl_rdma(1, btl, ep, local, raddr, rh, size, cb, ctx, data);
+}
+static int host_btl_put(mca_btl_base_module_t *btl, struct mca_btl_base_endpoint_t *ep, void *local, uint64_t raddr,
+                        struct mca_btl_base_registration_handle_t *lh, struct mca_btl_base_registration_handle_t *rh,
+                        size_t size, int flags, int order, mca_btl_base_rdma_completion_fn_t cb, void *ctx, void *data)
+{
+    (void)lh; (void)flags; (void)order;
+    return host_btl_rdma(0, btl, ep, local, raddr, rh, size, cb, ctx, data);
+}
+
 int mxh_btl_init(uint32_t *flags, size_t *handle_bytes)
 {
     int (*install)(mca_btl_base_module_t *) =
@@ -1590,6 +1748,11 @@ int mxh_btl_init(uint32_t *flags, size_t *handle_bytes)
     g_btl.btl_max_send_size = 32768;
     g_btl.btl_exclusivity = 65536;                /* MCA_BTL_EXCLUSIVITY_HIGH */
     g_btl.btl_flags = 0x0001;                     /* MCA_BTL_FLAGS_SEND */
+    g_btl.btl_register_mem = host_btl_register;   /* the host single-copy slots install keeps */
+    g_btl.btl_deregister_mem = host_btl_deregister;
+    g_btl.btl_get = host_btl_get;
+    g_btl.btl_put = host_btl_put;
+    g_btl.btl_registration_handle_size = sizeof(mxh_host_reg_t);
     if (install(&g_btl) != OPAL_SUCCESS) return -2;
     *flags = g_btl.btl_flags;
     *handle_bytes = g_btl.btl_registration_handle_size;

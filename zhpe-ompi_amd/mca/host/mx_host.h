@@ -78,6 +78,9 @@ int mxh_comm_free(void *comm);
 const char *mxh_comm_slot_owner(void *comm, const char *slot);
 
 int mxh_op_reduce(void *op, const void *source, void *target, int count, void *dtype);
+int mxh_3buff_op_reduce(void *op, const void *source1, const void *source2, void *target, int count, void *dtype);
+/* calls that reached the coll/self stand-in's slots so far */
+int mxh_self_calls(void);
 /* average ns of one ompi_op_reduce through the op table over `iters` calls */
 double mxh_time_op_reduce(void *op, const void *source, void *target, int count, void *dtype, int iters);
 int mxh_reduce_local(const void *in, void *inout, int count, void *dtype, void *op);
@@ -115,6 +118,8 @@ int mxh_request_free(void **req);
 int mxh_btl_init(uint32_t *flags, size_t *handle_bytes);
 int mxh_btl_register(void *base, size_t size, void *handle_out, void **reg);
 int mxh_btl_deregister(void *reg);
+/* calls that reached the stand-in BTL's own host RDMA slots (delegation from the installed ones) */
+int mxh_btl_host_calls(void);
 int mxh_btl_rdma(int get, void *local, uint64_t remote_addr, const void *remote_handle, size_t size, int ntimes);
 int mxh_btl_flush_gets(void *local, uint64_t remote_addr, const void *remote_handle, size_t size, int n);
 int mxh_convertor_run(const void *desc, size_t nrec, size_t size, int64_t lb, int64_t ub, int64_t true_lb,

@@ -72,11 +72,6 @@ static void op_module_destruct(mx_op_module_t *m)
 
 MX_MODULE_CLASS(mx_op_module_t, ompi_op_base_module_t, op_module_destruct);
 
-static int both_on_device(const void *a, const void *b)
-{
-    return mx_is_device_ptr(a) == 1 && mx_is_device_ptr(b) == 1;   /* range-cached: no runtime call */
-}
-
 /* The kernels run on a stream of the calling thread: one per thread, so
  * concurrent callers under MPI_THREAD_MULTIPLE neither share a stream nor
  * synchronise each other's work; a blocking stream, so it is implicitly
@@ -117,6 +112,87 @@ static void die(const char *what, int rc)
     abort();
 }
 
+/* ---- operands in different memories ---------------------------------------
+ * MPI_Reduce_local(device_in, host_inout), or any coll/base algorithm mixing a
+ * device user buffer with its host temporaries, is legal MPI.  The reference's
+ * accelerator path checks and stages each buffer on its own
+ * (coll_cuda_allreduce.c:44-62, through opal_cuda_check_bufs,
+ * opal_datatype_cuda.c:70).  Here the result is produced in the memory it
+ * lives in:
+ *  - result in device memory: each host operand is copied to device scratch
+ *    (one copy per operand) and the kernel runs;
+ *  - result in host memory, at most op_mi355x_mixed_host_max_kb (default
+ *    64 KiB): each device operand is copied to host scratch and the host
+ *    function the module replaced runs (no device round trip of the result);
+ *  - result in host memory, larger: host operands go to device scratch, the
+ *    kernel writes device scratch, the result is copied back.
+ * Both routes are bit-exact with the base function (the kernels are).
+ * Scratch belongs to the calling thread: device buffers for up to three
+ * operands, pinned host buffers for two. */
+typedef struct { void *p; size_t bytes; } mx_tscratch_t;
+static _Thread_local mx_tscratch_t t_dev[3], t_host[2];
+static size_t g_mixed_host_max = (size_t)-1;
+
+static void *tscratch(mx_tscratch_t *s, size_t bytes, int host)
+{
+    if (s->bytes < bytes) {
+        if (host) mx_host_free(s->p); else mx_free(s->p);
+        s->p = NULL;
+        s->bytes = 0;
+        const size_t want = bytes < ((size_t)1 << 20) ? ((size_t)1 << 20) : bytes;
+        if ((host ? mx_host_alloc(want, &s->p) : mx_alloc(want, &s->p)) != MX_SUCCESS) return NULL;
+        s->bytes = want;
+    }
+    return s->p;
+}
+
+static size_t mixed_host_max(void)
+{
+    if (g_mixed_host_max == (size_t)-1) {
+        const int kb = mx_ompi_host->mca_int("op_mi355x_mixed_host_max_kb", 64);
+        g_mixed_host_max = kb > 0 ? (size_t)kb << 10 : 0;
+    }
+    return g_mixed_host_max;
+}
+
+/* `p` in the memory the call computes in: itself, or a copy in scratch k
+ * (filled when `read`); NULL when the copy cannot be made */
+static void *stage(void *p, int on_dev, int want_dev, size_t bytes, int k, int read, void *s)
+{
+    if (on_dev == want_dev) return p;
+    void *q = tscratch(want_dev ? &t_dev[k] : &t_host[k], bytes, !want_dev);
+    if (!q) die("scratch allocation", MX_ERR_NOMEM);
+    if (read) {
+        int rc = mx_memcpy(q, p, bytes, s);
+        if (rc == MX_SUCCESS && !want_dev) rc = mx_stream_sync(s);   /* the host function reads it next */
+        if (rc != MX_SUCCESS) die("operand staging", rc);
+    }
+    return q;
+}
+
+/* the kernel on device operands (every pointer device memory) */
+static void run2(mx_op_module_t *m, int slot, void *in, void *inout, size_t count, void *s)
+{
+    int rc;
+    if (g_fast_sync < 0) g_fast_sync = mx_ompi_host->mca_int("op_mi355x_fast_sync", 1) != 0;
+    if (g_fast_sync)   /* the resident service, or the launch marking itself (per-workgroup flags) */
+        rc = mx_reduce2_sync(m->op_index, slot, in, inout, count, s);
+    else
+        rc = run_sync(s, mx_reduce2(m->op_index, slot, in, inout, count, s));
+    if (rc != MX_SUCCESS) die("mx_reduce2", rc);
+}
+
+static void run3(mx_op_module_t *m, int slot, void *in1, void *in2, void *out, size_t count, void *s)
+{
+    int rc;
+    if (g_fast_sync < 0) g_fast_sync = mx_ompi_host->mca_int("op_mi355x_fast_sync", 1) != 0;
+    if (g_fast_sync)   /* the resident service, or the launch + completion word */
+        rc = mx_reduce3_sync(m->op_index, slot, in1, in2, out, count, s);
+    else
+        rc = run_sync(s, mx_reduce3(m->op_index, slot, in1, in2, out, count, s));
+    if (rc != MX_SUCCESS) die("mx_reduce3", rc);
+}
+
 /* 2-buffer handler: inout = inout OP in (op.h:258-262) */
 static void mx_op_2buff(void *in, void *inout, int *count, struct ompi_datatype_t **dtype,
                         ompi_op_base_module_t *module)
@@ -124,18 +200,31 @@ static void mx_op_2buff(void *in, void *inout, int *count, struct ompi_datatype_
     mx_op_module_t *m = (mx_op_module_t *)module;
     const int slot = mx_ompi_host->dtype_slot(*dtype);
     if (slot < 0) die("datatype lookup", MX_ERR_ARG);
-    if (*count > 0 && both_on_device(in, inout)) {
-        void *s = op_stream();
-        int rc;
-        if (g_fast_sync < 0) g_fast_sync = mx_ompi_host->mca_int("op_mi355x_fast_sync", 1) != 0;
-        if (g_fast_sync)   /* the resident service, or the launch marking itself (per-workgroup flags) */
-            rc = mx_reduce2_sync(m->op_index, slot, in, inout, (size_t)*count, s);
-        else
-            rc = run_sync(s, mx_reduce2(m->op_index, slot, in, inout, (size_t)*count, s));
-        if (rc != MX_SUCCESS) die("mx_reduce2", rc);
+    const int din = *count > 0 && mx_is_device_ptr(in) == 1, dio = *count > 0 && mx_is_device_ptr(inout) == 1;
+    if (*count <= 0 || (!din && !dio)) {
+        m->fallback[slot](in, inout, count, dtype, m->fallback_module[slot]);
         return;
     }
-    m->fallback[slot](in, inout, count, dtype, m->fallback_module[slot]);
+    void *s = op_stream();
+    if (din && dio) {
+        run2(m, slot, in, inout, (size_t)*count, s);
+        return;
+    }
+    const size_t bytes = (size_t)*count * mx_type_size(slot);
+    if (dio || bytes > mixed_host_max()) {   /* compute on the device */
+        void *din_p = stage(in, din, 1, bytes, 0, 1, s);
+        void *dio_p = stage(inout, dio, 1, bytes, 1, 1, s);
+        run2(m, slot, din_p, dio_p, (size_t)*count, s);
+        if (dio_p != inout) {
+            int rc = mx_memcpy(inout, dio_p, bytes, s);
+            if (rc == MX_SUCCESS) rc = mx_stream_sync(s);
+            if (rc != MX_SUCCESS) die("result copy", rc);
+        }
+        return;
+    }
+    /* small, result in host memory: the device operand comes to the host */
+    void *hin = stage(in, 1, 0, bytes, 0, 1, s);
+    m->fallback[slot](hin, inout, count, dtype, m->fallback_module[slot]);
 }
 
 /* 3-buffer handler: out = in1 OP in2 (op.h:267-273) */
@@ -145,18 +234,34 @@ static void mx_op_3buff(void *in1, void *in2, void *out, int *count, struct ompi
     mx_op_module_t *m = (mx_op_module_t *)module;
     const int slot = mx_ompi_host->dtype_slot(*dtype);
     if (slot < 0) die("datatype lookup", MX_ERR_ARG);
-    if (*count > 0 && both_on_device(in1, in2) && mx_is_device_ptr(out) == 1) {
-        void *s = op_stream();
-        int rc;
-        if (g_fast_sync < 0) g_fast_sync = mx_ompi_host->mca_int("op_mi355x_fast_sync", 1) != 0;
-        if (g_fast_sync)   /* the resident service, or the launch + completion word */
-            rc = mx_reduce3_sync(m->op_index, slot, in1, in2, out, (size_t)*count, s);
-        else
-            rc = run_sync(s, mx_reduce3(m->op_index, slot, in1, in2, out, (size_t)*count, s));
-        if (rc != MX_SUCCESS) die("mx_reduce3", rc);
+    const int pos = *count > 0;
+    const int d1 = pos && mx_is_device_ptr(in1) == 1, d2 = pos && mx_is_device_ptr(in2) == 1;
+    const int dout = pos && mx_is_device_ptr(out) == 1;
+    if (!pos || (!d1 && !d2 && !dout)) {
+        m->fallback3[slot](in1, in2, out, count, dtype, m->fallback3_module[slot]);
         return;
     }
-    m->fallback3[slot](in1, in2, out, count, dtype, m->fallback3_module[slot]);
+    void *s = op_stream();
+    if (d1 && d2 && dout) {
+        run3(m, slot, in1, in2, out, (size_t)*count, s);
+        return;
+    }
+    const size_t bytes = (size_t)*count * mx_type_size(slot);
+    if (dout || bytes > mixed_host_max()) {   /* compute on the device */
+        void *a = stage(in1, d1, 1, bytes, 0, 1, s);
+        void *b = stage(in2, d2, 1, bytes, 1, 1, s);
+        void *o = stage(out, dout, 1, bytes, 2, 0, s);
+        run3(m, slot, a, b, o, (size_t)*count, s);
+        if (o != out) {
+            int rc = mx_memcpy(out, o, bytes, s);
+            if (rc == MX_SUCCESS) rc = mx_stream_sync(s);
+            if (rc != MX_SUCCESS) die("result copy", rc);
+        }
+        return;
+    }
+    void *a = stage(in1, d1, 0, bytes, 0, 1, s);
+    void *b = stage(in2, d2, 0, bytes, 1, 1, s);
+    m->fallback3[slot](a, b, out, count, dtype, m->fallback3_module[slot]);
 }
 
 static int mx_op_component_init_query(bool enable_progress_threads, bool enable_mpi_threads)
