@@ -339,19 +339,10 @@ def bench_allreduce(torch, mx, dist, rank, world, dev, steps, warmup, nbytes=256
         return out
 
     ndev = torch.cuda.device_count()
-    # The RCCL leg is opt-in (MX_BENCH_RCCL=1): no parity test covers it yet
-    # (RCCL refuses two ranks on one GPU, the only multi-rank setup the test
-    # pool offers), so it stays out of the default 8-GPU measurement.
-    want_rccl = os.environ.get("MX_BENCH_RCCL", "0") == "1" and ndev >= world
-    flags = mx.COMM_IPC | mx.COMM_P2P | (mx.COMM_RCCL if want_rccl else 0)
-    try:
-        comm = mx.Comm(rank, world, ag, device=dev, staging_bytes=2 * nbytes + (64 << 20), flags=flags,
-                       heap_bytes=2 * nbytes + (4 << 20))
-    except mx.MxError:
-        comm = mx.Comm(rank, world, ag, device=dev, staging_bytes=2 * nbytes + (64 << 20),
-                       flags=mx.COMM_IPC | mx.COMM_P2P,
-                       heap_bytes=2 * nbytes + (4 << 20))
-        flags = mx.COMM_IPC | mx.COMM_P2P
+    # RCCL runs on a communicator of its own after everything else (rccl_leg)
+    flags = mx.COMM_IPC | mx.COMM_P2P
+    comm = mx.Comm(rank, world, ag, device=dev, staging_bytes=2 * nbytes + (64 << 20), flags=flags,
+                   heap_bytes=2 * nbytes + (4 << 20))
     x = _bench_input(torch, rank, count)
     out = torch.empty_like(x)
     stream = torch.cuda.current_stream()
@@ -389,6 +380,7 @@ def bench_allreduce(torch, mx, dist, rank, world, dev, steps, warmup, nbytes=256
     comm.set_profiling(False)
     par = allreduce_parity(torch, mx, dist, rank, world, x, out, count)
     exp_sha = par.pop("_expected_sha", None)
+    rccl_ref = (par.pop("_oracle_out", None), par.pop("_abs_sum", None))
     # data-movement A/B at the headline size (results are identical under
     # all three): zero-copy between registered user buffers (the default above
     # 256 KiB per rank), and the staged path under PUSH and PULL (the staged
@@ -440,14 +432,6 @@ def bench_allreduce(torch, mx, dist, rank, world, dev, steps, warmup, nbytes=256
              for coll in ("allreduce", "reduce_scatter", "allgather", "bcast")}
     tuned = {coll: {b: v for b, v in d.items() if v is not None} for coll, d in tuned.items()}
     extra = {}
-    if flags & mx.COMM_RCCL:
-        try:
-            for _ in range(2):
-                comm.allreduce(x.data_ptr(), out.data_ptr(), count, "FLOAT", "SUM", "rccl", sp)
-            tr = timed("rccl", max(3, steps // 2))
-            extra["rccl_busbw_gbs"] = round(nbytes / (tr / max(3, steps // 2)) / 1e9 * 2 * (world - 1) / world, 2)
-        except mx.MxError as e:
-            extra["rccl_error"] = str(e)
     comm.close()
     fold_ms = st["fold_ms"] / max(1, st["fold_launches"])
     fold_bytes = st["fold_bytes"] / max(1, st["fold_launches"])
@@ -496,7 +480,91 @@ def bench_allreduce(torch, mx, dist, rank, world, dev, steps, warmup, nbytes=256
                                            for k in ("fold_ms", "push_ms", "gather_ms", "total_ms")}},
         "sweep": sweep,
         "cfg_e": cfge,
+        "_rccl_ref": rccl_ref,
     }
+
+
+U_FP32 = 2.0 ** -24   # unit roundoff of IEEE binary32
+
+
+def order_bound_check(got, ref, abs_sum, n):
+    """Tolerance of an fp32 SUM over n ranks computed in another reduction
+    order (BASELINE north_star: "within a stated relative tolerance
+    (reduction-order bounded, scaled by rank count)").  Any order of the n-1
+    additions rounds to within gamma_{n-1} * sum_i |x_i| of the exact sum
+    (gamma_k = k u / (1 - k u), u = 2^-24, Higham 4.2), so two orders differ
+    elementwise by at most 2 gamma_{n-1} sum_i |x_i|.  Returns (ok, worst
+    |got - ref| / bound, index of the worst element); NaN / Inf positions must
+    agree exactly."""
+    import numpy as np
+    got = np.asarray(got, np.float32)
+    ref = np.asarray(ref, np.float32)
+    k = max(1, n - 1)
+    gamma = k * U_FP32 / (1.0 - k * U_FP32)
+    bound = 2.0 * gamma * np.asarray(abs_sum, np.float64)
+    fin = np.isfinite(ref)
+    if not np.array_equal(fin, np.isfinite(got)):
+        return False, float("inf"), int(np.nonzero(fin != np.isfinite(got))[0][0])
+    diff = np.abs(got[fin].astype(np.float64) - ref[fin].astype(np.float64))
+    b = bound[fin]
+    over = np.where(b > 0, diff / np.where(b > 0, b, 1.0), np.where(diff > 0, np.inf, 0.0))
+    if over.size == 0:
+        return True, 0.0, -1
+    i = int(np.argmax(over))
+    return bool(over[i] <= 1.0), float(over[i]), int(np.nonzero(fin)[0][i])
+
+
+def rccl_leg(torch, mx, dist, rank, world, dev, steps, rccl_ref, nbytes=256 << 20):
+    """ncclAllReduce (RCCL over xGMI) on the headline buffers, on its own
+    communicator, after every other measurement -- only when each rank has a
+    GPU of its own (RCCL refuses two ranks on one device).  Timed like the
+    headline (barrier + synchronize, max over ranks); its result is checked
+    against the oracle's coll/tuned order (coll_base_allreduce.c:618-856) with
+    order_bound_check: rank 0 against the bound, every other rank equal to
+    rank 0 (SHA-256).  Returns the fields for the JSON line."""
+    count = nbytes // 4
+
+    def ag(b):
+        out = [None] * world
+        dist.all_gather_object(out, b)
+        return out
+    comm = mx.Comm(rank, world, ag, device=dev, staging_bytes=64 << 20, flags=mx.COMM_IPC | mx.COMM_RCCL)
+    x = _bench_input(torch, rank, count)
+    out = torch.empty_like(x)
+    sp = torch.cuda.current_stream().cuda_stream
+    for _ in range(3):
+        comm.allreduce(x.data_ptr(), out.data_ptr(), count, "FLOAT", "SUM", "rccl", sp)
+    k = max(3, steps // 2)
+    torch.cuda.synchronize()
+    dist.barrier()
+    t0 = time.perf_counter()
+    for _ in range(k):
+        comm.allreduce(x.data_ptr(), out.data_ptr(), count, "FLOAT", "SUM", "rccl", sp)
+    torch.cuda.synchronize()
+    dist.barrier()
+    t = torch.tensor([time.perf_counter() - t0], dtype=torch.float64)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    per = float(t[0]) / k
+    hs = [None] * world
+    dist.all_gather_object(hs, _sha(torch, out))
+    res = {"rccl_busbw_gbs": round(nbytes / per / 1e9 * 2 * (world - 1) / world, 2),
+           "rccl_ms": round(per * 1e3, 4)}
+    if rank == 0:
+        ref, abs_sum = rccl_ref
+        if ref is None:
+            res["rccl_parity"] = "unchecked: no oracle result"
+        else:
+            ok, worst, at = order_bound_check(out.cpu().numpy(), ref, abs_sum, world)
+            same = all(h == hs[0] for h in hs)
+            res["rccl_parity"] = ("ok" if ok and same else
+                                  f"MISMATCH: worst |rccl - oracle| / bound = {worst:.3g} at element {at}"
+                                  + ("" if same else "; ranks' results differ"))
+            res["rccl_parity_check"] = {
+                "what": "ncclAllReduce fp32 SUM vs the oracle's coll/tuned order, elementwise |d| <= "
+                        "2 gamma_{n-1} sum_i |x_i| (gamma_k = k u / (1 - k u), u = 2^-24); every rank's result "
+                        "equal to rank 0's", "worst_fraction_of_bound": round(worst, 4)}
+    comm.close()
+    return res
 
 
 def _sha(torch, t):
@@ -561,6 +629,11 @@ def allreduce_parity(torch, mx, dist, rank, world, x, out, count):
             where = f", rank 0 first differing byte offset {int(d[0]) * 4}" if len(d) else ""
         res["parity"] = f"MISMATCH on ranks {bad}{where}"
     res["_expected_sha"] = exp
+    res["_oracle_out"] = outs[0]
+    abs_sum = np.zeros(count, np.float64)
+    for xr in xs:
+        abs_sum += np.abs(xr.astype(np.float64))
+    res["_abs_sum"] = abs_sum
     return res
 
 
@@ -807,6 +880,30 @@ def main():
             done = True
         except Exception as e:  # noqa: BLE001 - reported in the JSON line
             result["allreduce_error"] = repr(e)
+        rccl_ref = result.pop("_rccl_ref", (None, None))
+        if done and torch.cuda.device_count() >= world and os.environ.get("MX_BENCH_RCCL", "1") != "0":
+            # RCCL over xGMI beside the default path.  A watchdog ends the
+            # ranks with the line printed if RCCL's bootstrap or a collective
+            # never returns, so the headline is not lost with it.
+            import threading
+
+            def _expire():
+                if rank == 0:
+                    result["rccl_error"] = "timed out after 150 s"
+                    print(json.dumps(result), flush=True)
+                os._exit(0)
+            wd = threading.Timer(150.0, _expire)
+            wd.daemon = True
+            wd.start()
+            try:
+                result.update(rccl_leg(torch, mx, dist, rank, world, dev, args.steps, rccl_ref))
+            except Exception as e:  # noqa: BLE001 - reported in the JSON line
+                result["rccl_error"] = repr(e)
+            wd.cancel()
+        elif done:
+            result["rccl_busbw_gbs"] = None
+            result["rccl_parity"] = f"not run: {torch.cuda.device_count()} GPU(s) for {world} ranks " \
+                                    "(RCCL needs one GPU per rank)"
     if not done:
         torch.cuda.synchronize()
         if dist is not None:
