@@ -197,6 +197,8 @@ typedef struct mx_coll_stats {
                                   host round instead of two)                */
     uint64_t p2p_relaunches;   /* receive launches that yielded to receives
                                   posted after them and were launched again */
+    uint64_t p2p_pulls;        /* rendezvous receives pulled straight from the
+                                  sender's buffer (single copy)             */
 } mx_coll_stats_t;
 int mx_comm_set_profiling(mx_comm_t *comm, int on);
 int mx_comm_get_stats(mx_comm_t *comm, mx_coll_stats_t *stats, int reset);

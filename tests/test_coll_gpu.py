@@ -1014,11 +1014,12 @@ def _reg_fast_worker(rank, n, port, q):
         count = 1 << 20
         X = torch.empty(count, dtype=torch.int32, device="cuda")
         Y = torch.zeros(count, dtype=torch.int32, device="cuda")
-        res = []
+        res, diag = [], []
         for i in range(8):
             X.copy_(torch.from_numpy(_fast_x(rank, i, count)).cuda())   # new contents on the stream
             comm.allreduce(X.data_ptr(), Y.data_ptr(), count, "INT32_T", "SUM", "auto", st)
             res.append(Y.cpu().numpy().tobytes())
+        diag.append({"x": X.data_ptr(), "y": Y.data_ptr()})
         s1 = comm.stats()
         L = mxompi.lib()
         vp, sz = ctypes.c_void_p, ctypes.c_size_t
@@ -1027,7 +1028,14 @@ def _reg_fast_worker(rank, n, port, q):
             assert L.mx_alloc(sz(4 * count), ctypes.byref(p)) == 0
             X.copy_(torch.from_numpy(_fast_x(rank, i, count)).cuda())
             torch.cuda.synchronize()
+            before = comm.stats()
             comm.allreduce(X.data_ptr(), p.value, count, "INT32_T", "SUM", "auto", st)
+            after = comm.stats()
+            # where each rank's rbuf was, and which path the call took (kept
+            # for the failure message: a wrong block names the peer that wrote it)
+            diag.append({"i": i, "rbuf": p.value, **{k: after[k] - before[k] for k in
+                                                    ("zero_copy_calls", "direct_calls", "staged_calls",
+                                                     "reg_fast_calls")}})
             host = np.empty(count, np.int32)
             assert L.mx_memcpy(vp(host.ctypes.data), p, sz(4 * count), None) == 0
             res.append(host.tobytes())
@@ -1036,7 +1044,7 @@ def _reg_fast_worker(rank, n, port, q):
         s2 = comm.stats()
         comm.close()
         dist.destroy_process_group()
-        q.put((rank, "ok", {"res": res, "fast1": s1["reg_fast_calls"], "zc1": s1["zero_copy_calls"],
+        q.put((rank, "ok", {"res": res, "diag": diag, "fast1": s1["reg_fast_calls"], "zc1": s1["zero_copy_calls"],
                             "fast2": s2["reg_fast_calls"], "zc2": s2["zero_copy_calls"]}))
     except Exception:  # noqa: BLE001
         import traceback
@@ -1069,7 +1077,22 @@ def test_registration_fast_path_reused_and_remade_buffers(n):
     for i in range(11):
         exp = sum(_fast_x(r, i, count).astype(np.int64) for r in range(n)).astype(np.int32).tobytes()
         for r in range(n):
-            assert out[r]["res"][i] == exp, (i, r)
+            if out[r]["res"][i] != exp:
+                # which peers' parts are wrong (zero-copy direct: peer j stores
+                # part j into every rank's rbuf), how, and where every rank's
+                # buffers were
+                got = np.frombuffer(out[r]["res"][i], np.int32)
+                want = np.frombuffer(exp, np.int32)
+                base, rem = divmod(count, n)
+                parts, lo = [], 0
+                for j in range(n):
+                    hi = lo + base + (1 if j < rem else 0)
+                    bad = np.nonzero(got[lo:hi] != want[lo:hi])[0]
+                    parts.append((j, len(bad), int(bad[0]) if len(bad) else -1,
+                                  int(np.count_nonzero(got[lo:hi][bad] == 0))))
+                    lo = hi
+                raise AssertionError(f"iteration {i} rank {r}: (part, wrong, first, zeros) {parts}; "
+                                     f"diag {[out[k]['diag'] for k in range(n)]}")
     for r in range(n):
         assert out[r]["zc1"] == 8 and out[r]["fast1"] == 7, out[r]      # the first call registers
         assert out[r]["zc2"] == 11, out[r]

@@ -114,13 +114,13 @@ def test_device_pack_unpack_match_reference(rec):
                                   "vector_f32_b64_s128", "indexed_f32_random", "struct_char_d3_int_resized48",
                                   "ref_lower_matrix_47", "ref_strange", "ref_blacs_indexed"])
 def test_device_pack_large_cfg_c(name, shift):
-    """CFG-C sizes: the golden type description with a large instance count
-    (many tiles), user buffer aligned or shifted by 3 bytes, checked against
-    the oracle restatement."""
+    """The golden type description with a large instance count (16 MiB
+    packed: thousands of tiles), user buffer aligned or shifted by 3, 4, 8
+    bytes, checked against the oracle restatement."""
     mxompi.init(0)
     rec = next(r for r in RECS if r["name"] == name)
     dt = _dt(rec)
-    count = max(1, (64 << 20) // rec["size"]) + 7
+    count = max(1, (16 << 20) // rec["size"]) + 7      # thousands of tiles (below the 384 MiB nt threshold either way)
     ext = rec["ub"] - rec["lb"]
     span = ext * (count - 1) + rec["true_ub"] - rec["true_lb"]
     rng = np.random.default_rng(5)

@@ -77,27 +77,44 @@ BMAP_TYPES = "struct_char_d3_int_resized48,indexed_f32_random,ref_blacs_indexed,
 VEC_TYPES = "vector_f32_b1_s2,vector_f64_b3_s5,vector_f32_b4_s8"
 
 
-def _run(env, types):
+def _env(env):
     e = dict(os.environ)
     for kv in env.split():
         k, v = kv.split("=")
         e[k] = v
-    p = subprocess.run([sys.executable, "-c", CHILD, ROOT, types], capture_output=True, text=True, env=e,
-                       timeout=240)
-    assert p.returncode == 0, (env, p.stdout[-2000:], p.stderr[-3000:])
+    return e
 
 
-@pytest.mark.parametrize("env", ["MX_CONV_BMAP_SPAN=12288", "MX_CONV_BMAP_SPAN=24576", "MX_CONV_BMAP_UNROLL=0",
-                                 "MX_CONV_BMAP_QUAD=0", "MX_CONV_BMAP_WORD=1", "MX_CONV_BMAP_NT=0",
-                                 "MX_CONV_BMAP_DW=0", "MX_CONV_BMAP_CW=0", "MX_NT_MIN_BYTES=0 MX_CONV_UNPACK_NTLD=1",
-                                 "MX_CONV_UNPACK_U32=0", "MX_CONV_BMAP_INST=0"])
-def test_byte_map_pack_switches(env):
-    _run(env, BMAP_TYPES)
+def _run_all(cases):
+    """Every (env, types) case in its own child process, all at once (the
+    switches are read once per process; a child's run is mostly its own
+    start-up, so they overlap it): each must exit 0."""
+    procs = [(env, subprocess.Popen([sys.executable, "-c", CHILD, ROOT, types], stdout=subprocess.PIPE,
+                                    stderr=subprocess.PIPE, text=True, env=_env(env))) for env, types in cases]
+    failed = []
+    for env, p in procs:
+        try:
+            out, err = p.communicate(timeout=240)
+        except subprocess.TimeoutExpired:
+            p.kill()
+            out, err = p.communicate()
+        if p.returncode != 0:
+            failed.append((env, p.returncode, out[-2000:], err[-3000:]))
+    assert not failed, failed
 
 
-@pytest.mark.parametrize("env", ["MX_NT_MIN_BYTES=0", "MX_CONV_VEC_NT=0 MX_NT_MIN_BYTES=0"])
-def test_vec_pack_nontemporal(env):
+BMAP_SWITCHES = ["MX_CONV_BMAP_SPAN=12288", "MX_CONV_BMAP_SPAN=24576", "MX_CONV_BMAP_UNROLL=0", "MX_CONV_BMAP_QUAD=0",
+                 "MX_CONV_BMAP_WORD=1", "MX_CONV_BMAP_NT=0", "MX_CONV_BMAP_DW=0", "MX_CONV_BMAP_CW=0",
+                 "MX_NT_MIN_BYTES=0 MX_CONV_UNPACK_NTLD=1", "MX_CONV_UNPACK_U32=0", "MX_CONV_BMAP_INST=0"]
+
+
+def test_byte_map_pack_switches():
+    """Every byte-map switch, each in its own process, run concurrently."""
+    _run_all([(env, BMAP_TYPES) for env in BMAP_SWITCHES])
+
+
+def test_vec_pack_nontemporal():
     """The VEC and VEC-span PACK kernels' non-temporal instances (taken from
     MX_NT_MIN_BYTES of span + stream on; forced here at 4 MiB) and their
     ordinary ones."""
-    _run(env, VEC_TYPES)
+    _run_all([(env, VEC_TYPES) for env in ("MX_NT_MIN_BYTES=0", "MX_CONV_VEC_NT=0 MX_NT_MIN_BYTES=0")])

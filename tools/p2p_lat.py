@@ -24,7 +24,7 @@ def worker(rank, n, port, q):
     x = torch.zeros(64 << 20, dtype=torch.uint8, device="cuda")
     peer = 1 - rank
     rows = []
-    sizes = [8, 4096, 65536, 256 << 10, (256 << 10) + 16, 1 << 20, 16 << 20, 64 << 20]
+    sizes = [8, 4096, 65536, 256 << 10, (256 << 10) + 16, 1 << 20, 4 << 20, 8 << 20, 16 << 20, 64 << 20, 256 << 20]
     if os.environ.get("P2P_LAT_SIZES"):          # e.g. "8,4096" (diagnostics)
         sizes = [int(x) for x in os.environ["P2P_LAT_SIZES"].split(",")]
     dist_out = {}

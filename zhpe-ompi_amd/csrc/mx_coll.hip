@@ -3813,7 +3813,7 @@ extern "C" int mx_test(mx_request_t *q, int *flag) {
     return MX_SUCCESS;
   }
   if (e != hipSuccess) return MX_ERR_HIP;
-  if (mx::p2p_yielded(q)) {            // that launch yielded: launched again by p2p_progress
+  if (mx::p2p_rx_waiting(q)) {            // that launch yielded: launched again by p2p_progress
     *flag = 0;
     return MX_SUCCESS;
   }
@@ -3845,7 +3845,7 @@ static int p2p_wait(mx_request *q) {
     }
     if (!q->fast || late) {
       const hipError_t e = hipEventQuery(q->done);
-      if (e == hipSuccess && !mx::p2p_yielded(q)) return req_complete(q);
+      if (e == hipSuccess && !mx::p2p_rx_waiting(q)) return req_complete(q);
       if (e != hipSuccess && e != hipErrorNotReady) return MX_ERR_HIP;
       if (late) std::this_thread::sleep_for(std::chrono::microseconds(20));
     }
@@ -3885,7 +3885,7 @@ static bool req_done_peek(mx_request *q) {
   const hipError_t e = hipEventQuery(q->done);
   if (e == hipErrorNotReady) return false;
   if (e != hipSuccess) return true;   // mx_wait reports it
-  return !mx::p2p_yielded(q);
+  return !mx::p2p_rx_waiting(q);
 }
 
 extern "C" int mx_waitall(size_t n, mx_request_t *const *reqs) {
@@ -3958,14 +3958,20 @@ extern "C" int mx_request_stream_wait(mx_request_t *q, void *stream) {
     }
     return MX_SUCCESS;
   }
-  if (q->kind == RQ_RECV && q->launch) {
-    // a receive that may yield: its event is not its completion, so the host
-    // waits (launching yielded receives again) until it is delivered
+  if (q->kind == RQ_RECV) {
+    // a receive may yield or leave a rendezvous for the host to pull: its
+    // event is not its completion, so the host waits (launching yielded
+    // receives again, pulls) until it is delivered
     for (;;) {
       mx::p2p_progress();
       if (fast_done(q)) return MX_SUCCESS;
+      if (q->fast == 2) {   // pulled: only its status word tells
+        if (const int e = rndv_failed(q)) return e;
+        std::this_thread::sleep_for(std::chrono::microseconds(5));
+        continue;
+      }
       const hipError_t e = hipEventQuery(q->done);
-      if (e == hipSuccess && !mx::p2p_yielded(q)) return MX_SUCCESS;
+      if (e == hipSuccess && !mx::p2p_rx_waiting(q)) return MX_SUCCESS;
       if (e != hipSuccess && e != hipErrorNotReady) return MX_ERR_HIP;
       std::this_thread::sleep_for(std::chrono::microseconds(5));
     }

@@ -8,6 +8,7 @@
 
 #include "mx_fold.hpp"
 #include "mx_coll.h"
+#include "mx_rdma.h"
 
 namespace mx {
 
@@ -32,14 +33,24 @@ constexpr size_t FLAG_WORDS = OS_COUNTER + 8;
 //   filled[src][lane]    my flags: chunks src has written into my lane
 //   seen[dst][lane]      my flags (written by dst): envelopes dst has read
 //   drained[dst][lane]   my flags (written by dst): chunks dst has consumed
-//   cts[dst]             my flags (written by dst): {seq, ticket} of the
-//                        rendezvous message dst has cleared last
+//   cts[dst][P2P_RNDV_Q] my flags (written by dst): a ring of the rendezvous
+//                        messages dst has cleared, one word each (cts_word):
+//                        stream the data through the lanes (CTS), or dst
+//                        already pulled it straight from my buffer (FIN)
+// Rendezvous send with a descriptor (single copy, round 6): the envelope's
+// mode word has bit 1 set and the sender's buffer descriptor (P2PRgetDesc:
+// the allocation's IPC handle and the buffer address) sits in the mailbox's
+// descriptor slot m % P2P_H; the receiver's host maps the allocation and
+// one copy kernel pulls the payload, then FIN goes into the ring.
+constexpr int P2P_RNDV_Q = 256;   // rendezvous sends pending per communicator (and CTS ring entries per pair)
 constexpr int P2P_LE = 8;
 constexpr int P2P_L = P2P_LE + 64;
 constexpr int P2P_S = 4;
 constexpr size_t P2P_C = 64 << 10;
 constexpr int P2P_H = 8;
 constexpr size_t P2P_HDR = 64;
+constexpr size_t P2P_DESC_OFF = 512;   // descriptor slots after the header ring (P2P_H x P2P_HDR)
+constexpr size_t P2P_DESC = 128;
 constexpr size_t P2P_BOX = 4096 + (size_t)P2P_L * P2P_S * P2P_C;
 constexpr size_t P2P_POSTED = FLAG_WORDS + 8;
 constexpr size_t P2P_FILLED = P2P_POSTED + MAXR;
@@ -49,7 +60,7 @@ constexpr size_t P2P_CTS = P2P_DRAINED + (size_t)MAXR * P2P_L;
 // BYE[src]: written once by src in mx_comm_destroy, after its device was
 // idle -- its last access to this rank's regions is over, so the regions may
 // serve another communicator (mx_coll.hip, the IPC region pool)
-constexpr size_t BYE_BASE = P2P_CTS + 2 * (size_t)MAXR;
+constexpr size_t BYE_BASE = P2P_CTS + (size_t)MAXR * P2P_RNDV_Q;
 constexpr size_t ALL_FLAG_WORDS = BYE_BASE + (size_t)MAXR;
 constexpr uint64_t BYE_WORD = 0xB7EB7EB7EB7EB7EBull;
 
@@ -69,12 +80,12 @@ struct P2PStashEntry { uint64_t valid; int64_t tag; uint64_t bytes; uint64_t seq
 struct P2PSendState {
   uint64_t msgs;
   uint64_t lane_chunks[P2P_L];
-  uint64_t cts_served;                 // CTS tickets of this destination taken
+  uint64_t cts_served;                 // entries of this destination's CTS ring taken
 };
 struct P2PRecvState {
   uint64_t lane_msgs[P2P_L];
   uint64_t lane_chunks[P2P_L];
-  uint64_t cts_sent;                   // CTS tickets issued to this source
+  uint64_t cts_sent;                   // CTS ring entries issued to this source (atomic: receive kernels and pulls)
   uint64_t held;                       // valid entries in stash + defer (0: skip the scan)
   P2PStashEntry stash[P2P_STASH_N];    // written only by the last lane of a receive kernel
   P2PStashEntry defer[P2P_DEFER_N];    // likewise
@@ -113,9 +124,20 @@ struct P2PDisplaced {             // device memory, changed only by a receive ke
 };
 constexpr int P2P_DEC = 16;       // decision ring: envelope k of a launch taken or stopped at
 
+// one CTS ring word: stamp (entry index + 1, 24 bits) | FIN | message seq
+__host__ __device__ constexpr uint64_t cts_word(uint64_t ticket, bool fin, uint64_t seq) {
+  return ((ticket + 1) & 0xffffffull) << 40 | (fin ? 1ull << 39 : 0) | (seq & ((1ull << 39) - 1));
+}
+// the sender's descriptor of a rendezvous buffer (13 words in the mailbox's
+// descriptor slot, copied by the receive kernel into status[8..21))
+struct P2PRgetDesc {
+  mx_rdma_handle_t h;
+  uint64_t addr;
+};
+static_assert(sizeof(P2PRgetDesc) == 13 * 8 && sizeof(P2PRgetDesc) <= P2P_DESC, "descriptor slot");
+
 // Rendezvous sends waiting for their CTS (mapped host memory, written by the
 // host when the send is posted, read by the rendezvous pick kernel)
-constexpr int P2P_RNDV_Q = 256;
 struct P2PRndvEntry {
   const char *buf;
   uint64_t bytes, seq;
@@ -266,6 +288,8 @@ struct mx_comm {
   uint64_t p2p_xtot;       // exits of the receive launches with a control workgroup (p2p_lanes[3])
   hipEvent_t p2p_unpack_ev;          // after the last datatype receive's unpack
   int p2p_unpack_pending;            // ... which p2p_channel_idle has not yet seen complete
+  hipEvent_t p2p_pull_ev;            // after the last single-copy pull (+ unpack + FIN) of this communicator
+  int p2p_pull_pending;
   uint64_t p2p_host_msgs[mx::MAXR];   // envelopes enqueued per destination (the device's msgs)
   mx::P2PRndvTable *p2p_rndv;        // mapped host: pending rendezvous sends
   mx::P2PRndvTable *p2p_rndv_dev;    // its device address
@@ -294,7 +318,8 @@ struct mx_request {
   // point-to-point: peer, tag, and the status the receiving kernel writes
   // (mapped host memory: received bytes, envelope tag, error)
   int peer, tag;
-  int64_t *status;   // [0] bytes [1] tag [2] error [3] source [4] done (P2P_STATUS_WORDS)
+  int64_t *status;   // [0] bytes [1] tag [2] error [3] source [4] done [5] yielded launch
+                     // [6] rendezvous to pull [7] its seq [8..21) its P2PRgetDesc (P2P_STATUS_WORDS)
   int fast;          // completion by status[4]: 1 also by the event, 2 only by status[4]
                      // (a rendezvous send: its data moves on whichever kernel takes its CTS)
   int rndv;          // rendezvous send: table slot + 1, else 0
@@ -304,6 +329,7 @@ struct mx_request {
   // launch yielded) and its kernel arguments, kept for the next launch
   uint64_t post, launch;
   void *rx;
+  int rget;          // the host launched this receive's pull (single-copy rendezvous)
 };
 
 namespace mx {
@@ -327,12 +353,15 @@ void p2p_finish(mx_request *q);
 void p2p_progress();
 // a receive request's current launch yielded (it is not complete)
 bool p2p_yielded(const mx_request *q);
+// ... or it is a receive whose kernel ended without completing it (yielded,
+// or a rendezvous left to pull): what the completion checks ask
+bool p2p_rx_waiting(const mx_request *q);
 // some receive of this process is in flight (its launches may yield)
 bool p2p_rx_active();
 // status blocks (P2P_STATUS_WORDS x int64, mapped host memory): from a process-wide
 // pool allocated once (never released, so a request may outlive its
 // communicator), else one hipHostMalloc each
-constexpr int P2P_STATUS_WORDS = 8;
+constexpr int P2P_STATUS_WORDS = 24;
 int64_t *p2p_status_get();
 void p2p_status_put(int64_t *st);
 }  // namespace mx

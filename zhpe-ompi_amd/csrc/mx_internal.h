@@ -2,6 +2,7 @@
 #pragma once
 #include <hip/hip_runtime.h>
 #include "../../include/mx_kernels.h"
+#include "../../include/mx_rdma.h"
 
 namespace mx {
 extern int g_num_cus;      // CUs of the current device (256 on MI355X)
@@ -62,6 +63,8 @@ void release_later(void *p, int kind);
 void release_flush();
 bool release_now_if_quiet(void *p, int kind);   // false: deferred
 bool release_now_or_keep(void *p, int kind);    // false: not quiet, nothing done (the caller keeps p)
+// a get through mx_rdma's import cache, without a completion event (mx_rdma.hip)
+int rdma_pull(void *local, const mx_rdma_handle_t *remote, uint64_t remote_addr, size_t bytes, hipStream_t s);
 }  // namespace mx
 
 // Lazily performs mx_init(current device) if the caller did not.

@@ -187,6 +187,8 @@ struct P2PSendArgs {
   uint64_t bytes;
   int64_t tag;
   int rndv;                  // rendezvous: the envelope only (the data follows its CTS)
+  int has_desc;              // rendezvous with a descriptor of `buf` (the receiver may pull it)
+  P2PRgetDesc desc;
   char *box;                 // the receiver's mailbox for me
   uint64_t *posted;          // receiver's flags: posted[me]
   uint64_t *filled;          // receiver's flags: filled[me][lane]
@@ -217,9 +219,14 @@ __global__ void __launch_bounds__(kP2PThreads) k_p2p_send(P2PSendArgs a) {
     __syncthreads();
     if (threadIdx.x == 0 && !s_seen_bad) {
       volatile uint64_t *h = reinterpret_cast<volatile uint64_t *>(a.box + (m % P2P_H) * P2P_HDR);
+      if (a.has_desc) {   // the descriptor slot of this envelope, before the envelope is posted
+        volatile uint64_t *dd = reinterpret_cast<volatile uint64_t *>(a.box + P2P_DESC_OFF + (m % P2P_H) * P2P_DESC);
+        const uint64_t *src = reinterpret_cast<const uint64_t *>(&a.desc);
+        for (int w = 0; w < (int)(sizeof(P2PRgetDesc) / 8); w++) dd[w] = src[w];
+      }
       h[0] = a.bytes;
       h[1] = (uint64_t)a.tag;
-      h[2] = (uint64_t)a.rndv;
+      h[2] = (uint64_t)a.rndv | (a.has_desc ? 2u : 0u);
       __threadfence_system();
       __hip_atomic_store(a.posted, m + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
       a.st->msgs = m + 1;
@@ -245,7 +252,7 @@ __global__ void __launch_bounds__(kP2PThreads) k_p2p_send(P2PSendArgs a) {
 struct P2PRndvArgs {
   P2PRndvCur *cur;
   uint64_t gen;              // this kernel's publication number
-  const uint64_t *cts0;      // my flags: cts[0]
+  const uint64_t *cts0;      // my flags: cts[0][0] (the ring of destination d at + d * P2P_RNDV_Q)
   int n;
   const P2PRndvTable *tab;   // device address of the mapped table
   char *box[MAXR];           // box[d]: d's mailbox for me
@@ -258,18 +265,22 @@ struct P2PRndvArgs {
 };
 
 __device__ __forceinline__ void rndv_pick(const P2PRndvArgs &a) {
-  __shared__ int s_dst, s_hit;
+  __shared__ int s_dst, s_hit, s_fin;
   __shared__ uint64_t s_seq;
   const uint64_t t0 = wall_clock64();
   if (threadIdx.x == 0) {
     s_dst = -1;
     for (;;) {
       for (int d = 0; d < a.n && s_dst < 0; d++) {
-        const uint64_t t = __hip_atomic_load(a.cts0 + 2 * d + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-        if (t > a.st0[d].cts_served) {
+        // d's next ring entry, taken once its stamp is the entry's index + 1
+        const uint64_t k = a.st0[d].cts_served;
+        const uint64_t w =
+            __hip_atomic_load(a.cts0 + (size_t)d * P2P_RNDV_Q + k % P2P_RNDV_Q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        if ((w >> 40) == ((k + 1) & 0xffffffull)) {
           __atomic_thread_fence(__ATOMIC_ACQUIRE);
-          s_seq = __hip_atomic_load(a.cts0 + 2 * d, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-          a.st0[d].cts_served = t;
+          s_seq = w & ((1ull << 39) - 1);
+          s_fin = (int)((w >> 39) & 1);
+          a.st0[d].cts_served = k + 1;
           s_dst = d;
         }
       }
@@ -310,7 +321,7 @@ __device__ __forceinline__ void rndv_pick(const P2PRndvArgs &a) {
       c.bytes = e.bytes;
       c.done = e.done;
       c.dst = d;
-      c.ok = 1;
+      c.ok = s_fin ? 2 : 1;   // 2: the receiver pulled the data (FIN): nothing to stream
     } else if (d >= 0) {   // a CTS for no pending send: the channel is corrupt
       __hip_atomic_store(a.err, MX_ERR_STATE, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     }
@@ -343,7 +354,7 @@ __global__ void __launch_bounds__(kP2PThreads) k_p2p_rndv(P2PRndvArgs a) {
     __syncthreads();
   }
   const P2PRndvCur c = *a.cur;   // after the acquire fence (or written by this workgroup)
-  if (c.ok) {
+  if (c.ok == 1) {
     uint64_t lo, hi;
     p2p_lane(c.bytes, l, P2P_LE, P2P_LR, &lo, &hi);
     send_stream(l, lo, hi, c.buf, a.box[c.dst], a.filled[c.dst], a.drained0 + (size_t)c.dst * P2P_L,
@@ -371,6 +382,7 @@ struct P2PRecvArgs {
   P2PRecvState *st0;
   char *stash0;              // stash payloads of source 0 (source p at + p * N * C)
   P2PDone fin;
+  int rget_ok;               // a rendezvous envelope with a descriptor is left for the host to pull
   // yielding (round 5): this launch's number and the receive's
   // post number, the device's launch queue (mapped; null: never yield) and
   // decision ring, and this communicator's displaced receives
@@ -653,16 +665,18 @@ __device__ int gate_wait(const P2PRecvArgs &a, const uint64_t *posted, uint64_t 
 
 // one lane of a receive; returns whether this lane stored user data;
 // *yielded: the launch stopped at an envelope boundary (nothing delivered)
-__device__ __forceinline__ bool recv_body(const P2PRecvArgs &a, HoldPlan &plan, P2PRecvState **stp, bool *yielded) {
+__device__ __forceinline__ bool recv_body(const P2PRecvArgs &a, HoldPlan &plan, P2PRecvState **stp, bool *yielded,
+                                          bool *rget) {
   const int l = blockIdx.x;
   const uint64_t t0 = wall_clock64();
   __shared__ int ok;
   __shared__ uint64_t s_bytes;
   __shared__ int64_t s_tag;
   __shared__ uint64_t s_seq;
-  __shared__ int s_rndv;
+  __shared__ int s_rndv, s_desc;
   int p = a.src;
   *yielded = false;
+  *rget = false;
   if (a.any) {
     p = (int)__hip_atomic_load(&a.status[3], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     if (p == -2) *yielded = true;   // the pick yielded
@@ -672,7 +686,7 @@ __device__ __forceinline__ bool recv_body(const P2PRecvArgs &a, HoldPlan &plan, 
   const uint64_t *posted = a.flag0 + P2P_POSTED + p, *filled = a.flag0 + P2P_FILLED + (size_t)p * P2P_L;
   uint64_t *seen = a.peer_flags[p] + P2P_SEEN + (size_t)a.me * P2P_L;
   uint64_t *drained = a.peer_flags[p] + P2P_DRAINED + (size_t)a.me * P2P_L;
-  uint64_t *cts = a.peer_flags[p] + P2P_CTS + 2 * (size_t)a.me;
+  uint64_t *cts = a.peer_flags[p] + P2P_CTS + (size_t)a.me * P2P_RNDV_Q;   // my ring at the sender
   P2PRecvState *st = a.st0 + p;
   char *stash = a.stash0 + (size_t)p * P2P_STASH_N * P2P_STASH_C;
   *stp = st;
@@ -681,11 +695,9 @@ __device__ __forceinline__ bool recv_body(const P2PRecvArgs &a, HoldPlan &plan, 
   // through the rendezvous lanes
   auto rndv_take = [&](uint64_t seq, uint64_t bytes) -> bool {
     if (l == 0 && threadIdx.x == 0) {
-      const uint64_t t = st->cts_sent + 1;
-      __hip_atomic_store(cts, seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      const uint64_t t = __hip_atomic_fetch_add(&st->cts_sent, (uint64_t)1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       __threadfence_system();
-      __hip_atomic_store(cts + 1, t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-      st->cts_sent = t;
+      __hip_atomic_store(cts + t % P2P_RNDV_Q, cts_word(t, false, seq), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     }
     return recv_stream(l, P2P_LE, P2P_LR, bytes, a.buf, a.cap, box, filled, drained, st, t0, a, &wrote);
   };
@@ -730,8 +742,15 @@ __device__ __forceinline__ bool recv_body(const P2PRecvArgs &a, HoldPlan &plan, 
         const volatile uint64_t *hd = reinterpret_cast<const volatile uint64_t *>(box + (m % P2P_H) * P2P_HDR);
         s_bytes = hd[0];
         s_tag = (int64_t)hd[1];
-        s_rndv = (int)hd[2];
+        s_rndv = (int)(hd[2] & 1);
+        s_desc = (int)((hd[2] >> 1) & 1);
         s_seq = m;
+        if (l == 0 && s_desc && a.rget_ok) {   // the descriptor, before the slot is handed back (seen)
+          const volatile uint64_t *dd =
+              reinterpret_cast<const volatile uint64_t *>(box + P2P_DESC_OFF + (m % P2P_H) * P2P_DESC);
+          for (int w = 0; w < (int)(sizeof(P2PRgetDesc) / 8); w++)
+            __hip_atomic_store(&a.status[8 + w], (int64_t)dd[w], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        }
         __hip_atomic_store(seen + l, m + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
         st->lane_msgs[l] = m + 1;
       }
@@ -746,6 +765,7 @@ __device__ __forceinline__ bool recv_body(const P2PRecvArgs &a, HoldPlan &plan, 
     const int64_t tag = s_tag;
     const uint64_t seq = s_seq;
     const int rndv = s_rndv;
+    const int desc = s_desc;
     __syncthreads();          // every thread has read the envelope before the next one
     int slot = -1;
     if ((a.tag >= 0 && tag != a.tag) || reserved(a.disp, a.post, p, tag)) {
@@ -771,6 +791,21 @@ __device__ __forceinline__ bool recv_body(const P2PRecvArgs &a, HoldPlan &plan, 
       continue;
     }
     // this receive's message (or one that cannot be set aside: MX_ERR_TAG)
+    if (rndv && desc && a.rget_ok) {
+      // single copy: the host maps the sender's buffer and pulls the payload
+      // (p2p_rget_launch); the status tells it which message
+      *rget = true;
+      if (l == 0 && threadIdx.x == 0) {
+        __hip_atomic_store(&a.status[7], (int64_t)seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        __hip_atomic_store(&a.status[3], (int64_t)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      }
+      deliver_status(bytes, tag, ((a.tag >= 0 && tag != a.tag) || reserved(a.disp, a.post, p, tag)) ? MX_ERR_TAG : 0);
+      if (l == 0 && threadIdx.x == 0) {
+        __threadfence_system();
+        __hip_atomic_store(&a.status[6], (int64_t)1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      }
+      return wrote;
+    }
     if (rndv) {
       if (!rndv_take(seq, bytes)) return wrote;
     } else if (!recv_stream(l, 0, P2P_LE, bytes, a.buf, a.cap, box, filled, drained, st, t0, a, &wrote)) {
@@ -841,8 +876,8 @@ __global__ void __launch_bounds__(kP2PThreads) k_p2p_recv(P2PRecvArgs a) {
   }
   __syncthreads();
   P2PRecvState *st = nullptr;
-  bool yielded = false;
-  const bool wrote = recv_body(a, plan, &st, &yielded);
+  bool yielded = false, rget = false;
+  const bool wrote = recv_body(a, plan, &st, &yielded, &rget);
   // the last lane out commits the held-table changes (the tables are read by
   // every lane during the kernel, so they only change between kernels)
   __syncthreads();
@@ -883,12 +918,29 @@ __global__ void __launch_bounds__(kP2PThreads) k_p2p_recv(P2PRecvArgs a) {
         __threadfence_system();
         __hip_atomic_store(const_cast<uint64_t *>(&a.rq->yields), a.launch, __ATOMIC_RELAXED,
                            __HIP_MEMORY_SCOPE_SYSTEM);
-      } else if (a.fin.done) {
+      } else if (a.fin.done && !rget) {   // a pulled message completes after its pull (p2p_rget_launch)
         __hip_atomic_store(a.fin.done, (int64_t)1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
       }
       rx_exit(a.fin);
     }
   }
+}
+
+// The end of a single-copy rendezvous receive (after its pull and, for a
+// datatype, its unpack, on the pull stream): FIN into the sender's CTS ring
+// -- its buffer is free, its send completes -- and the receive's status word.
+struct P2PFinArgs {
+  uint64_t *ring;      // the sender's ring of this pair
+  uint64_t *alloc;     // my P2PRecvState.cts_sent of this pair
+  uint64_t seq;
+  int64_t *done;       // the receive's status[4] (mapped host)
+};
+__global__ void k_p2p_rget_fin(P2PFinArgs a) {
+  if (threadIdx.x != 0) return;
+  __threadfence_system();
+  const uint64_t t = __hip_atomic_fetch_add(a.alloc, (uint64_t)1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  __hip_atomic_store(a.ring + t % P2P_RNDV_Q, cts_word(t, true, a.seq), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  __hip_atomic_store(a.done, (int64_t)1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
 // The internal streams spin on the device (a receive waits for its message,
@@ -934,9 +986,35 @@ struct RxDev {
   uint64_t *dec = nullptr;
   uint64_t launches = 0, seen = 0;
   std::vector<mx_request *> active;
+  std::vector<mx_request *> rget;   // receives in flight that may be left a rendezvous to pull
+  hipStream_t pull = nullptr;       // the pulls: an ordinary-priority stream (they never spin)
 };
 static RxDev g_rx[64];
 static int g_rx_dev[64], g_rx_ndev;
+// MX_P2P_RGET=0: rendezvous messages always stream through the mailbox
+// (round 5's two-copy path); default: single copy from registered buffers
+static bool rget_on() {
+  static const bool on = [] {
+    const char *e = getenv("MX_P2P_RGET");
+    return !(e && *e == '0');
+  }();
+  return on;
+}
+// smallest rendezvous message sent with its descriptor (MX_P2P_RGET_MIN,
+// bytes): below it the mailbox's two copies beat the pull's host round trip
+// (one GPU, profiles/r06/p2p_lat_r6*.txt: 1 MiB 37 vs 52 us, 16 MiB 81 vs 58 us)
+static size_t rget_min() {
+  static const size_t m = [] {
+    const char *e = getenv("MX_P2P_RGET_MIN");
+    return e ? (size_t)strtoull(e, nullptr, 0) : (size_t)4 << 20;
+  }();
+  return m;
+}
+static void rx_dev_note(int dev) {   // caller holds g_chan_mu
+  for (int i = 0; i < g_rx_ndev; i++)
+    if (g_rx_dev[i] == dev) return;
+  g_rx_dev[g_rx_ndev++] = dev;
+}
 static bool rx_yield_on() {
   static const bool on = [] {
     const char *e = getenv("MX_P2P_YIELD");
@@ -992,6 +1070,14 @@ static bool p2p_channel_idle(mx_comm *c, int i) {
     }
     (void)hipGetLastError();
     c->p2p_unpack_pending = 0;
+  }
+  if (i == 1 && c->p2p_pull_pending) {   // the host-launched pulls of this communicator
+    if (hipEventQuery(c->p2p_pull_ev) == hipErrorNotReady) {
+      (void)hipGetLastError();
+      return false;
+    }
+    (void)hipGetLastError();
+    c->p2p_pull_pending = 0;
   }
   if (__atomic_load_n(&c->p2p_hfin[i], __ATOMIC_ACQUIRE) >= c->p2p_ltot[i]) return true;
   // a drained stream ran every kernel of the channel (a failed stream never
@@ -1056,8 +1142,17 @@ int p2p_setup(mx_comm *c) {
       D.rq = rq;
       D.rq_dev = rq_dev;
       D.dec = dec;
-      g_rx_dev[g_rx_ndev++] = c->device;
+      rx_dev_note(c->device);
     }
+  }
+  if (rget_on() && c->device >= 0 && c->device < 64) {
+    std::lock_guard<std::mutex> lk(g_chan_mu);
+    RxDev &D = g_rx[c->device];
+    if (!D.pull && hipStreamCreateWithFlags(&D.pull, hipStreamNonBlocking) != hipSuccess) {
+      (void)hipGetLastError();
+      D.pull = nullptr;
+    }
+    rx_dev_note(c->device);
   }
   memset(c->p2p_rndv, 0, sizeof(P2PRndvTable));
   c->p2p_rndv_gen = 0;
@@ -1066,6 +1161,7 @@ int p2p_setup(mx_comm *c) {
   c->p2p_ltot[0] = c->p2p_ltot[1] = c->p2p_ltot[2] = 0;
   c->p2p_xtot = 0;
   c->p2p_unpack_pending = 0;
+  c->p2p_pull_pending = 0;
   for (int j = 0; j < MAXR; j++) c->p2p_host_msgs[j] = 0;
   if (hipMemsetAsync(c->p2p_send, 0, sb, ls) != hipSuccess || hipMemsetAsync(c->p2p_recv, 0, rb, ls) != hipSuccess ||
       hipMemsetAsync(c->p2p_lanes, 0, 4 * sizeof(uint64_t), ls) != hipSuccess ||
@@ -1074,6 +1170,7 @@ int p2p_setup(mx_comm *c) {
       p2p_channels(c->p2p_stream) != MX_SUCCESS ||
       hipEventCreateWithFlags(&c->p2p_ev, hipEventDisableTiming) != hipSuccess ||
       hipEventCreateWithFlags(&c->p2p_unpack_ev, hipEventDisableTiming) != hipSuccess ||
+      hipEventCreateWithFlags(&c->p2p_pull_ev, hipEventDisableTiming) != hipSuccess ||
       hipStreamSynchronize(ls) != hipSuccess) {
     p2p_release(c);
     return MX_ERR_HIP;
@@ -1103,6 +1200,8 @@ void p2p_release(mx_comm *c) {
   if (c->device >= 0 && c->device < 64) {
     std::vector<mx_request *> &v = g_rx[c->device].active;
     v.erase(std::remove_if(v.begin(), v.end(), [c](mx_request *q) { return q->c == c; }), v.end());
+    std::vector<mx_request *> &w = g_rx[c->device].rget;
+    w.erase(std::remove_if(w.begin(), w.end(), [c](mx_request *q) { return q->c == c; }), w.end());
   }
   pool_host_put(c->p2p_hfin, 3 * sizeof(uint64_t));
   c->p2p_hfin = c->p2p_hfin_dev = nullptr;
@@ -1111,6 +1210,9 @@ void p2p_release(mx_comm *c) {
   if (c->p2p_unpack_ev) (void)hipEventDestroy(c->p2p_unpack_ev);
   c->p2p_unpack_ev = nullptr;
   c->p2p_unpack_pending = 0;
+  if (c->p2p_pull_ev) (void)hipEventDestroy(c->p2p_pull_ev);
+  c->p2p_pull_ev = nullptr;
+  c->p2p_pull_pending = 0;
   const size_t sb = sizeof(P2PSendState) * c->size, rb = sizeof(P2PRecvState) * c->size;
   pool_dev_put(c->p2p_send, sb);
   pool_dev_put(c->p2p_recv, rb);
@@ -1147,7 +1249,11 @@ void p2p_finish(mx_request *q) {
       std::vector<mx_request *> &v = g_rx[c->device].active;
       const auto it = std::find(v.begin(), v.end(), q);
       if (it != v.end()) v.erase(it);
+      std::vector<mx_request *> &w = g_rx[c->device].rget;
+      const auto jt = std::find(w.begin(), w.end(), q);
+      if (jt != w.end()) w.erase(jt);
     }
+    q->rget = 0;
     delete static_cast<P2PRecvArgs *>(q->rx);
     q->rx = nullptr;
     q->launch = 0;
@@ -1157,6 +1263,15 @@ void p2p_finish(mx_request *q) {
 bool p2p_yielded(const mx_request *q) {
   return q->kind == RQ_RECV && q->status && q->launch &&
          __atomic_load_n(&q->status[5], __ATOMIC_ACQUIRE) == (int64_t)q->launch;
+}
+
+// not complete although its launch ended: the launch yielded (launched again
+// by p2p_progress), or it left a rendezvous for the host to pull that
+// p2p_progress has not launched yet
+bool p2p_rx_waiting(const mx_request *q) {
+  if (q->kind != RQ_RECV || !q->status) return false;
+  if (!q->rget && __atomic_load_n(&q->status[6], __ATOMIC_ACQUIRE)) return true;
+  return p2p_yielded(q);
 }
 
 namespace {
@@ -1285,6 +1400,15 @@ int p2p_enqueue(mx_request *q, hipStream_t *done_stream) {
     a.bytes = bytes;
     a.tag = q->tag;
     a.rndv = rndv;
+    // single copy: a contiguous device buffer (one runtime allocation) goes
+    // out with its descriptor, the receiver pulls it (btl_smcuda_get_cuda's
+    // role, btl_smcuda.c:1077-1180); the mailbox stream stays the fallback
+    // (a packed datatype lives in stream-ordered memory, which has no IPC
+    // handle; a receiver that set the envelope aside clears it with a CTS)
+    if (rndv && !tmp && rget_on() && bytes >= rget_min() && mx_rdma_register(src, bytes, &a.desc.h) == MX_SUCCESS) {
+      a.desc.addr = (uint64_t)(uintptr_t)src;
+      a.has_desc = 1;
+    }
     a.box = c->peer_staging[p] + c->p2p_off + (size_t)me * P2P_BOX;
     a.posted = c->peer_flags[p] + P2P_POSTED + me;
     a.filled = c->peer_flags[p] + P2P_FILLED + (size_t)me * P2P_L;
@@ -1352,6 +1476,8 @@ int p2p_enqueue(mx_request *q, hipStream_t *done_stream) {
     a.status = st_dev;
     a.timeout_ticks = c->timeout_ticks;
     a.err = c->err_dev;
+    a.rget_ok = rget_on() && g_rx[c->device].pull != nullptr;
+    q->rget = 0;
     q->tmp = tmp;   // freed at completion: a receive that yields runs (and unpacks) again
     q->post = ++c->p2p_posts;
     if ((rc = p2p_rx_launch(q))) {
@@ -1359,6 +1485,7 @@ int p2p_enqueue(mx_request *q, hipStream_t *done_stream) {
       return rc;
     }
     if (g_rx[c->device].rq) g_rx[c->device].active.push_back(q);
+    if (a.rget_ok) g_rx[c->device].rget.push_back(q);
     return MX_SUCCESS;
   }
   if (tmp) (void)hipFreeAsync(tmp, s);
@@ -1447,9 +1574,49 @@ bool p2p_rx_active() {
 // Launch again every receive whose last launch yielded, in the order of
 // their first launches (the kernels record the latest yield in the queue,
 // so nothing is scanned while no receive yielded).
+// The pull of a single-copy rendezvous receive whose kernel noted the
+// message (status[6]): map the sender's allocation (mx_rdma's import cache),
+// one copy kernel from it into the receive buffer (the packed staging for a
+// datatype, unpacked after), then FIN to the sender and the receive's status
+// word -- all on the device's pull stream.  The request completes through the
+// status word from then on (fast 2).  A mapping that cannot be made yet (a
+// stale import still waiting for its close) is tried again at the next
+// progress; a failed one completes the receive with the error, and FIN still
+// releases the sender.
+static void p2p_rget_launch(mx_request *q) {
+  mx_comm *c = q->c;
+  RxDev &D = g_rx[c->device];
+  P2PRecvArgs &a = *static_cast<P2PRecvArgs *>(q->rx);
+  const int p = (int)__atomic_load_n(&q->status[3], __ATOMIC_ACQUIRE);
+  if (p < 0 || p >= c->size || !D.pull) return;
+  P2PRgetDesc d;
+  memcpy(&d, (const void *)&q->status[8], sizeof d);
+  const uint64_t n = (uint64_t)q->status[0];
+  int rc = n ? rdma_pull(a.buf, &d.h, d.addr, n, D.pull) : MX_SUCCESS;
+  if (rc == MX_ERR_STATE) return;   // retried at the next progress
+  if (!rc && q->tmp) rc = mx_unpack(q->ddt, q->count, q->rbuf, q->tmp, 0, a.cap, D.pull);
+  if (rc && !q->status[2]) q->status[2] = rc;
+  P2PFinArgs f;
+  f.ring = c->peer_flags[p] + P2P_CTS + (size_t)c->rank * P2P_RNDV_Q;
+  f.alloc = &c->p2p_recv[p].cts_sent;
+  f.seq = (uint64_t)q->status[7];
+  f.done = a.status + 4;
+  hipLaunchKernelGGL(k_p2p_rget_fin, dim3(1), dim3(64), 0, D.pull, f);
+  if (mx_check_launch() != MX_SUCCESS) return;
+  if (hipEventRecord(c->p2p_pull_ev, D.pull) == hipSuccess) c->p2p_pull_pending = 1;
+  c->p2p_last_valid[1] = 1;
+  q->fast = 2;   // complete through status[4] only
+  q->rget = 1;
+  c->st.p2p_pulls++;
+}
+
 void p2p_progress() {
   for (int i = 0; i < g_rx_ndev; i++) {
     RxDev &D = g_rx[g_rx_dev[i]];
+    for (size_t j = 0; j < D.rget.size(); j++) {
+      mx_request *q = D.rget[j];
+      if (q->active && !q->rget && q->status && __atomic_load_n(&q->status[6], __ATOMIC_ACQUIRE)) p2p_rget_launch(q);
+    }
     if (!D.rq || D.active.empty()) continue;
     const uint64_t y = __atomic_load_n(&D.rq->yields, __ATOMIC_ACQUIRE);
     if (y == D.seen) continue;

@@ -132,10 +132,10 @@ int op_new(hipStream_t s, mx_rdma_op_t **op) {
 
 int rdma_copy(void *dst_local, const void *src_local, const mx_rdma_handle_t *remote, uint64_t remote_addr,
               size_t bytes, void *stream, mx_rdma_op_t **op, bool get) {
-  if (!remote || !op || (!dst_local && get) || (!src_local && !get)) return MX_ERR_ARG;
+  if (!remote || (!dst_local && get) || (!src_local && !get)) return MX_ERR_ARG;
   if (remote_addr < remote->base || remote_addr + bytes > remote->base + remote->size) return MX_ERR_ARG;
   if (int rc = mx_ensure_init()) return rc;
-  *op = nullptr;
+  if (op) *op = nullptr;
   char *map = nullptr;
   hipStream_t s = (hipStream_t)stream;
   {
@@ -153,10 +153,16 @@ int rdma_copy(void *dst_local, const void *src_local, const mx_rdma_handle_t *re
       return rc;
     }
   }
-  return op_new(s, op);
+  return op ? op_new(s, op) : MX_SUCCESS;
 }
 
 }  // namespace
+
+// the pull of a single-copy rendezvous receive (mx_p2p.hip): a get with no
+// completion event (the caller's next kernel on `stream` follows it)
+int mx::rdma_pull(void *local, const mx_rdma_handle_t *remote, uint64_t remote_addr, size_t bytes, hipStream_t s) {
+  return rdma_copy(local, nullptr, remote, remote_addr, bytes, s, nullptr, true);
+}
 
 extern "C" int mx_rdma_register(const void *ptr, size_t bytes, mx_rdma_handle_t *h) {
   if (!ptr || !h) return MX_ERR_ARG;
@@ -199,11 +205,13 @@ extern "C" int mx_rdma_register(const void *ptr, size_t bytes, mx_rdma_handle_t 
 
 extern "C" int mx_rdma_get(void *local, const mx_rdma_handle_t *remote, uint64_t remote_addr, size_t bytes,
                            void *stream, mx_rdma_op_t **op) {
+  if (!op) return MX_ERR_ARG;
   return rdma_copy(local, nullptr, remote, remote_addr, bytes, stream, op, true);
 }
 
 extern "C" int mx_rdma_put(const void *local, const mx_rdma_handle_t *remote, uint64_t remote_addr, size_t bytes,
                            void *stream, mx_rdma_op_t **op) {
+  if (!op) return MX_ERR_ARG;
   return rdma_copy(nullptr, local, remote, remote_addr, bytes, stream, op, false);
 }
 
