@@ -21,12 +21,15 @@ def worker(rank, n, port, q):
         dist.all_gather_object(out, b)
         return out
     comm = mxompi.Comm(rank, n, ag, device=0, staging_bytes=64 << 20)
-    x = torch.zeros(64 << 20, dtype=torch.uint8, device="cuda")
     peer = 1 - rank
     rows = []
     sizes = [8, 4096, 65536, 256 << 10, (256 << 10) + 16, 1 << 20, 4 << 20, 8 << 20, 16 << 20, 64 << 20, 256 << 20]
     if os.environ.get("P2P_LAT_SIZES"):          # e.g. "8,4096" (diagnostics)
-        sizes = [int(x) for x in os.environ["P2P_LAT_SIZES"].split(",")]
+        sizes = [int(v) for v in os.environ["P2P_LAT_SIZES"].split(",")]
+    # one buffer that holds the largest message (a send or receive past its
+    # end reads / writes outside the allocation)
+    x = torch.zeros(max(sizes), dtype=torch.uint8, device="cuda")
+    assert x.numel() >= max(sizes)
     dist_out = {}
     for nb in sizes:
         for form in ("blocking", "nonblocking"):
