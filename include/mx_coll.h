@@ -199,7 +199,15 @@ typedef struct mx_coll_stats {
                                   posted after them and were launched again */
     uint64_t p2p_pulls;        /* rendezvous receives pulled straight from the
                                   sender's buffer (single copy)             */
+    uint64_t service_calls;    /* small allreduces served by the resident
+                                  service (no launch)                       */
 } mx_coll_stats_t;
+/* The resident small-allreduce service (csrc/mx_coll_svc.hip): commands served
+ * and kernel launches so far in this process; returns 1 usable, 0 before first
+ * use, -1 off.  mx_coll_service_set turns it on or off at run time (overrides
+ * MX_COLL_SERVICE; off stops a running service). */
+int mx_coll_service_stats(unsigned long long *served, unsigned long long *launches);
+int mx_coll_service_set(int on);
 int mx_comm_set_profiling(mx_comm_t *comm, int on);
 int mx_comm_get_stats(mx_comm_t *comm, mx_coll_stats_t *stats, int reset);
 

@@ -830,8 +830,14 @@ extern "C" int mx_comm_create_ex(int rank, int size, int device, size_t staging_
         ok = 0;
       }
     if (ok) {
-      for (int p = 0; p < size; p++)
+      int per_dev = 1;   // most ranks on one device (the same on every rank)
+      for (int p = 0; p < size; p++) {
         if (strncmp(all[p].pci, mine.pci, sizeof mine.pci)) c->xdev = 1;
+        int k = 0;
+        for (int q = 0; q < size; q++) k += !strncmp(all[p].pci, all[q].pci, sizeof mine.pci);
+        per_dev = std::max(per_dev, k);
+      }
+      c->csv_ok = per_dev <= 2;
       c->proto = proto_default(c);   // the same on every rank: xdev is symmetric, the env is job-wide
     }
     for (int p = 0; ok && p < size; p++) {
@@ -923,6 +929,7 @@ extern "C" int mx_comm_create_ex(int rank, int size, int device, size_t staging_
 
 extern "C" int mx_comm_destroy(mx_comm_t *c) {
   if (!c) return MX_SUCCESS;
+  csv_comm_gone(c);   // a resident service bound to this communicator leaves first
   // wait for this communicator's own work only -- its last deferred
   // collective (requests run in issue order behind the tail event) and its
   // point-to-point channels -- never for the whole device: another
@@ -1559,9 +1566,24 @@ static bool os_self_mark() {
 }
 
 
+// a call the resident service completed: nothing is pending on the stream;
+// the device side's error word as finish() reports it
+static int finish_served(mx_comm *c) {
+  if (c->err_host && *(volatile int *)c->err_host) {
+    const int e = *(volatile int *)c->err_host;
+    *c->err_host = 0;
+    if (e == MX_ERR_TIMEOUT) {
+      c->poisoned = e;
+      timeout_dump(c, "device wait (service)");
+    }
+    return e;
+  }
+  return MX_SUCCESS;
+}
+
 // one-shot allreduce (small messages): one kernel, see k_oneshot
 static int allreduce_oneshot(mx_comm *c, oneshot_launch_fn ol, const std::vector<Seg> &segs, const char *sb,
-                             char *rb, size_t count, size_t es, hipStream_t s) {
+                             char *rb, size_t count, size_t es, hipStream_t s, int op, int type) {
   const int n = c->size, r = c->rank;
   const uint64_t g = ++c->gen;
   char *const region = c->staging + c->main_bytes + (g & 1) * (size_t)n * c->os_slot;
@@ -1598,6 +1620,16 @@ static int allreduce_oneshot(mx_comm *c, oneshot_launch_fn ol, const std::vector
   c->os_count += nwg;
   a.nseg = (int)segs.size();
   for (size_t i = 0; i < segs.size(); i++) a.seg[i] = OsSeg{segs[i].lo, segs[i].hi, segs[i].p};
+  // the resident service takes the call when it can (the same arguments and
+  // protocol: peers cannot tell), else the launch below
+  if (!c->defer) {
+    const int sv = csv_allreduce(c, a, op, type, s);
+    if (sv < 0) return sv;
+    if (sv == 1) {
+      c->st.service_calls++;
+      return finish_served(c);
+    }
+  }
   Mark mk{nullptr, nullptr, 0};
   if (!c->defer && fast_sync() && os_self_mark()) mark_arm(&mk, true);
   a.mflags = mk.flags;
@@ -2095,7 +2127,7 @@ extern "C" int mx_allreduce(mx_comm_t *c, const void *sbuf, void *rbuf, size_t c
   int cand = tune_pick(c, TUNE_ALLREDUCE, bytes, ncand, &bucket);
   if (cand == 3 || (cand < 0 && os_ok && bytes <= c->os_max)) {
     const auto t0 = std::chrono::steady_clock::now();
-    const int rc = allreduce_oneshot(c, ol, ossegs, sb, rb, count, es, s);
+    const int rc = allreduce_oneshot(c, ol, ossegs, sb, rb, count, es, s, op, type);
     return rc || cand < 0 ? rc : tune_done(c, TUNE_ALLREDUCE, bucket, cand, ncand, secs_since(t0));
   }
   const int proto0 = c->proto;

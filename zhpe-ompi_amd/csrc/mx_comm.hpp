@@ -290,6 +290,9 @@ struct mx_comm {
   int p2p_unpack_pending;            // ... which p2p_channel_idle has not yet seen complete
   hipEvent_t p2p_pull_ev;            // after the last single-copy pull (+ unpack + FIN) of this communicator
   int p2p_pull_pending;
+  // small allreduces may be served by the resident service (mx_coll_svc.hip):
+  // at most two ranks of the communicator per device (set at creation)
+  int csv_ok;
   uint64_t p2p_host_msgs[mx::MAXR];   // envelopes enqueued per destination (the device's msgs)
   mx::P2PRndvTable *p2p_rndv;        // mapped host: pending rendezvous sends
   mx::P2PRndvTable *p2p_rndv_dev;    // its device address
@@ -362,6 +365,11 @@ bool p2p_rx_active();
 // pool allocated once (never released, so a request may outlive its
 // communicator), else one hipHostMalloc each
 constexpr int P2P_STATUS_WORDS = 24;
+// the resident small-allreduce service (mx_coll_svc.hip): 1 served, 0 the
+// caller launches the same one-shot arguments, < 0 error; csv_comm_gone
+// stops a service bound to a communicator about to be destroyed
+int csv_allreduce(mx_comm *c, const OneShotArgs &a, int op, int type, hipStream_t s);
+void csv_comm_gone(const mx_comm *c);
 int64_t *p2p_status_get();
 void p2p_status_put(int64_t *st);
 }  // namespace mx
