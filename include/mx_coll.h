@@ -201,6 +201,9 @@ typedef struct mx_coll_stats {
                                   sender's buffer (single copy)             */
     uint64_t service_calls;    /* small allreduces served by the resident
                                   service (no launch)                       */
+    uint64_t reg_stale_refused; /* zero-copy imports refused: the runtime
+                                  handed back the import of a peer's freed
+                                  allocation (the call took the staged path) */
 } mx_coll_stats_t;
 /* The resident small-allreduce service (csrc/mx_coll_svc.hip): commands served
  * and kernel launches so far in this process; returns 1 usable, 0 before first
@@ -208,6 +211,11 @@ typedef struct mx_coll_stats {
  * MX_COLL_SERVICE; off stops a running service). */
 int mx_coll_service_stats(unsigned long long *served, unsigned long long *launches);
 int mx_coll_service_set(int on);
+/* Where a served call's time goes, means over the served calls (microseconds):
+ * out[0] calls, [1] host preparation, [2] host wait from the post to `done`,
+ * and the kernel's phases [3] argument read, [4] the call (push, gather,
+ * fold, DONE, result words acknowledged).  Fills min(n, 5) entries. */
+int mx_coll_service_trace(double *out, int n);
 int mx_comm_set_profiling(mx_comm_t *comm, int on);
 int mx_comm_get_stats(mx_comm_t *comm, mx_coll_stats_t *stats, int reset);
 

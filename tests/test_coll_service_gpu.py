@@ -1,16 +1,22 @@
 """GPU: the resident small-message allreduce service (csrc/mx_coll_svc.hip;
 VERDICT r5 missing 5).
 
-Blocking allreduces on the one-shot path (8 B .. 64 KiB per rank) are taken by
-a workgroup kept resident per process, which speaks the launched one-shot
-kernel's protocol exactly.  Checked on 2 processes sharing the GPU:
+Blocking allreduces of the tagged-word class (os_ll in csrc/mx_fold.hpp:
+4- and 8-byte elements, up to 4 KiB per rank) are taken by a workgroup kept
+resident per process, which speaks the launched one-shot kernel's protocol
+exactly.  Checked on 2 processes sharing the GPU:
   * bit-exact against the oracle's coll/tuned order (recursive doubling at
     these sizes, coll_base_allreduce.c:130-274) for fp32 SUM, fp64 MAX,
     MAXLOC float_int (ties) and int64 SUM, 8 B to 32 KiB, inputs changing
     every call, results read right after each call;
-  * every call served (the stats say so) -- and with the service switched
-    off on ONE rank only, the served rank and the launching rank still agree
-    bit for bit (the protocol is the launch's);
+  * every call of the class served (the stats say so), the 32 KiB calls
+    launched (raw protocol) -- and with the service switched off on ONE rank
+    only, the served rank and the launching rank still agree bit for bit
+    (the protocol is the launch's);
+  * tagged-word and raw calls alternating on one communicator, int64 data
+    whose upper words are small integers (what a generation tag looks like):
+    the tagged words live in an area of their own, so raw bytes left in a
+    slot are never taken for a peer's words;
   * at 3 ranks on one device the service stays off (more than two ranks per
     device), and the calls launch;
   * the 8 B latency with and without the service, median of 300 calls, is
@@ -32,6 +38,14 @@ pytestmark = pytest.mark.gpu
 
 CASES = [("SUM", "FLOAT"), ("MAX", "DOUBLE"), ("MAXLOC", "FLOAT_INT"), ("SUM", "INT64_T")]
 SIZES = [8, 4096, 32768]          # below the autotuned range (64 KiB): always the one-shot path
+SERVED = [8, 4096]                # the tagged-word class (OS_LL_MAX = 4 KiB)
+ALT = [4096, 8192] * 8            # tagged-word / raw alternation, int64 SUM
+
+
+def _alt_gen(count, seed):
+    rng = np.random.default_rng(seed)
+    hi = rng.integers(0, 256, count).astype(np.int64)   # (generations here: ~70-110)
+    return ((hi << 32) | rng.integers(0, 1 << 20, count)).astype(np.int64).view(np.uint8)
 
 
 def _gen(t, count, seed):
@@ -80,6 +94,12 @@ def _worker(rank, n, port, q, off_rank):
                     outs.append(y.cpu().numpy().tobytes())      # read right after the call
                 res[(op, t, nb)] = outs
         res["served"] = comm.stats()["service_calls"]
+        for k, nb in enumerate(ALT):
+            x = torch.from_numpy(_alt_gen(nb // 8, 5000 + 10 * k + rank)).cuda()
+            y = torch.empty_like(x)
+            torch.cuda.synchronize()
+            comm.allreduce(x.data_ptr(), y.data_ptr(), nb // 8, "INT64_T", "SUM", "auto", st)
+            res[("alt", k)] = y.cpu().numpy().tobytes()
         # 8 B latency, service on / off (this rank), median of 300
         L = mxompi.lib()
         x = torch.ones(2, device="cuda")
@@ -145,12 +165,16 @@ def _check(out, n):
                                        (vp * n)(*[e.ctypes.data for e in exp])) == 0
                 for r in range(n):
                     assert out[r][(op, t, nb)][it] == exp[r].tobytes(), (op, t, nb, it, r)
+    for k, nb in enumerate(ALT):
+        want = sum(_alt_gen(nb // 8, 5000 + 10 * k + r).view(np.int64) for r in range(n))
+        for r in range(n):
+            assert out[r][("alt", k)] == want.tobytes(), (k, nb, r)
 
 
 def test_service_serves_small_allreduces_bit_exact():
     out = _run(2)
     _check(out, 2)
-    calls = len(CASES) * len(SIZES) * 6
+    calls = len(CASES) * len(SERVED) * 6
     for r in range(2):
         assert out[r]["served"] == calls, (r, out[r]["served"], calls)
     print("8 B allreduce, n = 2 on one GPU, median us:", [out[r]["lat_us"] for r in range(2)])
@@ -159,7 +183,7 @@ def test_service_serves_small_allreduces_bit_exact():
 def test_served_and_launched_ranks_interoperate():
     out = _run(2, off_rank=1)
     _check(out, 2)
-    calls = len(CASES) * len(SIZES) * 6
+    calls = len(CASES) * len(SERVED) * 6
     assert out[0]["served"] == calls and out[1]["served"] == 0, (out[0]["served"], out[1]["served"])
 
 

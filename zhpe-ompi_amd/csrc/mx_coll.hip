@@ -430,6 +430,47 @@ bool mx::release_now_or_keep(void *p, int kind) {   // nothing queued when not q
   release_now(p, kind);
   return true;
 }
+uint64_t mx::ipc_object_id(const void *p) {
+  unsigned long long id = 0;
+  if (!p || hipPointerGetAttribute(&id, HIP_POINTER_ATTRIBUTE_BUFFER_ID, (hipDeviceptr_t)p) != hipSuccess) {
+    (void)hipGetLastError();
+    return 0;
+  }
+  return id;
+}
+void mx::ipc_gone_add(std::vector<IpcGone> &g, int64_t owner, uint64_t base, uint64_t size, const void *mapping) {
+  const uint64_t oid = ipc_object_id(mapping);
+  if (!oid) return;
+  if (g.size() >= 64) g.erase(g.begin());
+  g.push_back(IpcGone{owner, base, size, oid});
+}
+int mx::ipc_open_checked(const void *handle, std::vector<IpcGone> &g, int64_t owner, uint64_t base, uint64_t size,
+                         char **out, uint64_t *oid) {
+  hipIpcMemHandle_t h;
+  memcpy(&h, handle, sizeof h);
+  char *p = nullptr;
+  if (hipIpcOpenMemHandle((void **)&p, h, hipIpcMemLazyEnablePeerAccess) != hipSuccess || !p) {
+    (void)hipGetLastError();
+    return MX_ERR_HIP;
+  }
+  const uint64_t id = ipc_object_id(p);
+  bool old = false;
+  for (const IpcGone &d : g)
+    if (id && d.owner == owner && d.base < base + size && base < d.base + d.size && d.oid == id) old = true;
+  if (!old && id) {   // a new object at that range: the closed ones are gone
+    for (size_t i = 0; i < g.size();) {
+      if (g[i].owner == owner && g[i].base < base + size && base < g[i].base + g[i].size) g.erase(g.begin() + (long)i);
+      else i++;
+    }
+  }
+  if (old) {
+    release_later(p, REL_IPC);   // drop the reference this open took
+    return 0;
+  }
+  *out = p;
+  *oid = id;
+  return 1;
+}
 void mx::release_flush() {
   std::vector<Deferred> go;
   {
@@ -465,6 +506,8 @@ static void reg_release(mx_comm *c) {
     for (const mx_reg_import &m : *c->reg_imp) release_later(m.ptr, REL_IPC);
     delete c->reg_imp;
     c->reg_imp = nullptr;
+    delete c->reg_gone;
+    c->reg_gone = nullptr;
   }
   if (c->reg_shm) munmap(c->reg_shm, c->reg_shm_bytes);
   c->reg_shm = nullptr;
@@ -779,7 +822,10 @@ extern "C" int mx_comm_create_ex(int rank, int size, int device, size_t staging_
                                    c->staging_bytes / (8 * (size_t)size)) & ~(size_t)255;
       if (c->os_cap < 1024) c->os_cap = 0;
       c->os_max = std::min<size_t>(oneshot_max(), c->os_cap);
-      c->os_slot = c->os_cap ? c->os_cap + 256 : 0;
+      // (MX_ONESHOT_LL=0: the raw protocol at every size; same on every rank)
+      const char *lle = getenv("MX_ONESHOT_LL");
+      c->os_ll = (lle && *lle == '0') ? 0 : std::min<size_t>(OS_LL_MAX, c->os_cap);
+      c->os_slot = c->os_cap ? c->os_cap + 256 + 2 * c->os_ll : 0;
       c->main_bytes = (c->staging_bytes - 2 * (size_t)size * c->os_slot) & ~(size_t)255;
       c->hregion_bytes = heap_bytes ? ((heap_bytes + 4095) & ~(size_t)4095) : 0;
       // point-to-point mailboxes (one per source rank) follow the staging
@@ -885,11 +931,12 @@ extern "C" int mx_comm_create_ex(int rank, int size, int device, size_t staging_
     if (reg_all == 1) {
       c->reg_min = reg_min();
       c->reg_imp = new (std::nothrow) std::vector<mx_reg_import>();
+      c->reg_gone = new (std::nothrow) std::vector<IpcGone>();
       // autotuning unless switched off, or a data path is forced through the environment
       const char *at = getenv("MX_AUTOTUNE");
       c->tune_on = !(at && *at == '0') && !getenv("MX_ALLREDUCE_PROTO") && !getenv("MX_REG_MIN");
     }
-    if (reg_all != 1 || !c->reg_imp) reg_release(c);
+    if (reg_all != 1 || !c->reg_imp || !c->reg_gone) reg_release(c);
     c->live = 1;
     const char *lr = getenv("MX_DEBUG_LAG_RANK"), *lu = getenv("MX_DEBUG_LAG_US");
     if (lr && lu && atoi(lr) == rank) c->lag_ticks = ticks_for(atof(lu) * 1e-6);
@@ -1586,15 +1633,21 @@ static int allreduce_oneshot(mx_comm *c, oneshot_launch_fn ol, const std::vector
                              char *rb, size_t count, size_t es, hipStream_t s, int op, int type) {
   const int n = c->size, r = c->rank;
   const uint64_t g = ++c->gen;
+  const size_t bytes = count * es;
+  // tagged words (os_ll in mx_fold.hpp) for one-workgroup calls of 4- and
+  // 8-byte elements: decided from size and type alone, so every rank agrees
+  const bool ll = (es == 4 || es == 8) && bytes <= c->os_ll;
+  const size_t sub = ll ? c->os_cap + 256 : 0;   // the slot's LL area
   char *const region = c->staging + c->main_bytes + (g & 1) * (size_t)n * c->os_slot;
   OneShotArgs a;
   memset(&a, 0, sizeof a);
   a.sb = sb;
   a.rb = rb;
+  a.ll = ll;
   for (int p = 0; p < n; p++) {
     const size_t peer_region = c->main_bytes + (g & 1) * (size_t)n * c->os_slot;
-    a.peer_slot[p] = p == r ? nullptr : c->peer_staging[p] + peer_region + (size_t)r * c->os_slot;
-    a.src[p] = p == r ? sb : region + (size_t)p * c->os_slot;
+    a.peer_slot[p] = p == r ? nullptr : c->peer_staging[p] + peer_region + (size_t)r * c->os_slot + sub;
+    a.src[p] = p == r ? sb : region + (size_t)p * c->os_slot + sub;
     a.peer_ready[p] = p == r ? nullptr : c->peer_flags[p] + OS_FLAG_BASE + (size_t)r * OSWG;
     a.peer_done[p] = p == r ? nullptr : c->peer_flags[p] + FLAG_DONE * MAXR + r;
   }
@@ -1610,14 +1663,17 @@ static int allreduce_oneshot(mx_comm *c, oneshot_launch_fn ol, const std::vector
   a.count = count;
   a.es = es;
   // slices of ~4 KiB, 16-byte aligned when the element size allows
-  const size_t bytes = count * es;
   size_t nwg = std::min<size_t>(OSWG, std::max<size_t>(1, (bytes + 4095) / 4096));
   size_t slice = (count + nwg - 1) / nwg;
   if (16 % es == 0) slice = rup(slice, 16 / es);
   nwg = (count + slice - 1) / slice;
+  if (ll) {   // one workgroup, no completion counter (it is the last one out)
+    nwg = 1;
+    slice = count;
+  }
   a.slice = slice;
   a.counter_last = c->os_count + nwg - 1;
-  c->os_count += nwg;
+  if (!ll) c->os_count += nwg;
   a.nseg = (int)segs.size();
   for (size_t i = 0; i < segs.size(); i++) a.seg[i] = OsSeg{segs[i].lo, segs[i].hi, segs[i].p};
   // the resident service takes the call when it can (the same arguments and
@@ -1766,9 +1822,12 @@ static bool reg_export(const void *p, size_t bytes, RegBuf *b) {
 
 // peer p's allocation, mapped once and kept (LRU, kRegCachePerPeer per
 // peer).  A cached mapping of an allocation the peer has since freed (same
-// peer range, other buffer id) is closed BEFORE the new handle is opened, so
-// the runtime can never hand back the stale import.  Closing is safe: no
-// kernel of this communicator is in flight between blocking calls.
+// peer range, other buffer id) is closed before the new handle is opened,
+// and the open is checked against the imports closed at that range
+// (ipc_open_checked: the runtime may hand the closed import back -- then the
+// call declines, every rank takes the staged path, and the next call tries
+// again).  Closing is safe: no kernel of this communicator is in flight
+// between blocking calls.
 static char *reg_import(mx_comm *c, int p, const RegBuf &b, const RegBuf *own, int nown) {
   std::vector<mx_reg_import> &v = *c->reg_imp;
   for (mx_reg_import &m : v)
@@ -1777,6 +1836,7 @@ static char *reg_import(mx_comm *c, int p, const RegBuf &b, const RegBuf *own, i
       return m.ptr;
     }
   size_t held = 0;
+  bool closed = false;
   for (size_t i = 0; i < v.size();) {
     const mx_reg_import &m = v[i];
     if (m.peer == p && m.base < b.base + b.size && b.base < m.base + m.size) {   // overlaps: stale
@@ -1784,8 +1844,10 @@ static char *reg_import(mx_comm *c, int p, const RegBuf &b, const RegBuf *own, i
       // another communicator's work is pending it stays in the cache and this
       // call declines (every rank falls back to the staged path), so the next
       // call finds it and tries again -- it is never dropped unclosed
+      ipc_gone_add(*c->reg_gone, p, m.base, m.size, m.ptr);
       if (!release_now_or_keep(m.ptr, REL_IPC)) return nullptr;
       v.erase(v.begin() + (long)i);
+      closed = true;
       continue;
     }
     held += m.peer == p;
@@ -1795,12 +1857,20 @@ static char *reg_import(mx_comm *c, int p, const RegBuf &b, const RegBuf *own, i
     size_t lru = (size_t)-1;
     for (size_t i = 0; i < v.size(); i++)
       if (v[i].peer == p && (lru == (size_t)-1 || v[i].used < v[lru].used)) lru = i;
+    ipc_gone_add(*c->reg_gone, p, v[lru].base, v[lru].size, v[lru].ptr);
     release_later(v[lru].ptr, REL_IPC);
     v.erase(v.begin() + (long)lru);
   }
+  if (closed) {   // (experiment MX_REG_REOPEN: 1 device sync, 2 sleep 2 ms, 3 both, after closing a stale import)
+    static const int ro = [] { const char *e = getenv("MX_REG_REOPEN"); return e && *e ? atoi(e) : 0; }();
+    if (ro & 1) { if (hipDeviceSynchronize() != hipSuccess) (void)hipGetLastError(); }
+    if (ro & 2) usleep(2000);
+  }
   char *ptr = nullptr;
-  if (hipIpcOpenMemHandle((void **)&ptr, b.h, hipIpcMemLazyEnablePeerAccess) != hipSuccess || !ptr) {
-    (void)hipGetLastError();
+  uint64_t oid = 0;
+  const int oc = ipc_open_checked(&b.h, *c->reg_gone, p, b.base, b.size, &ptr, &oid);
+  if (oc <= 0) {
+    if (oc == 0) c->st.reg_stale_refused++;
     return nullptr;
   }
   // a mapping must never overlap one of this rank's own allocations (the

@@ -11,20 +11,20 @@
 // (communicator, op, type), and takes the call from coherent mapped host
 // memory: the host writes the call's one-shot arguments (the very
 // OneShotArgs a launch would get) and raises the command number; the
-// workgroup reads them, runs the one-shot protocol for every slice of the
-// call, and raises `done`, which the host polls.
+// workgroup reads them, runs the call, and raises `done`, which the host
+// polls.  It takes the calls of the tagged-word class (os_ll, mx_fold.hpp:
+// 4- and 8-byte elements, at most OS_LL_MAX bytes per rank, one workgroup's
+// work); larger one-shot calls launch (one workgroup would fold what the
+// launch spreads over several).
 //
 // Protocol compatibility is the point: the workgroup speaks the launched
-// kernel's protocol exactly -- it pushes the whole vector into the peers'
-// slots of this generation's parity region, raises READY(me, w) for every
-// slice w the launch would have had, waits for every peer's READY(p, w),
-// folds every element with the call's fold program, adds the launch's
-// workgroup count to the completion counter and raises DONE(gen) at every
-// peer.  So whether a rank's call is served or launched is invisible to its
-// peers, and each rank decides alone: a service that is not running (idle
-// exit, a held hardware queue, another pair bound) means a launch, never a
-// protocol disagreement.  Results are the launch's bit for bit (the same
-// fold program per element).
+// kernel's protocol exactly -- tagged words into the peers' LL areas of this
+// generation's parity, the peers' tagged words gathered and folded with the
+// call's fold program, DONE(gen) at every peer.  So whether a rank's call is
+// served or launched is invisible to its peers, and each rank decides
+// alone: a service that is not running (idle exit, a held hardware queue,
+// another pair bound) means a launch, never a protocol disagreement.
+// Results are the launch's bit for bit (the same fold program per element).
 //
 // Like the op service (mx_service.hip): a stream of the least priority
 // (nothing else of the process runs there), the host waits until a
@@ -36,6 +36,7 @@
 // condition: each rank keeps one workgroup of its device resident while
 // calls come) and only while the communicator has no request in flight.
 #include <hip/hip_runtime.h>
+#include <stddef.h>
 #include <stdint.h>
 #include <stdlib.h>
 #include <string.h>
@@ -58,86 +59,35 @@ constexpr double kCsvStartUs = 1000;        // a kernel not running 1 ms after i
 constexpr double kCsvFirstStartUs = 50000;  // (50 ms for a pair's first launch: its code object loads)
 constexpr size_t kCsvArgWords = (sizeof(OneShotArgs) + 7) / 8;
 
+// per-call phase stamps (wall clock ticks, thread 0): the service's own
+// breakdown, summed by the host for mx_coll_service_trace
+enum { TK_SEEN, TK_ARGS, TK_CALL, TK_N };
+
 struct alignas(64) CsvCtl {   // coherent mapped host memory, written by the host
   uint64_t seq;               // command number, raised last (release)
   uint64_t exit;              // the command is "leave"
+  uint64_t words;             // 8-byte words of the arguments in use (the segments the call has)
 };
 struct alignas(64) CsvHost {  // mapped host memory, written by the kernel
   uint64_t done;              // last command completed
   uint64_t running;           // launch epoch the kernel reported at start
   uint64_t left;              // launch epoch that left (written after its last `done`)
+  uint64_t last[TK_N];        // the last call's phases: [k] = stamp k - stamp k-1 (ticks)
 };
 
-// One workgroup: the one-shot protocol of k_oneshot for all `nwg` slices.
-template <class T, class OP>
-__device__ void csv_call(const OneShotArgs &a) {
-  const int t = threadIdx.x, n = a.n, r = a.rank;
-  const size_t nwg = (a.count + a.slice - 1) / a.slice;
-  __shared__ int s_bad;
-  if (t == 0) s_bad = poisoned(a.poison);
-  __syncthreads();
-  if (s_bad) return;
-  // (1) every peer is past gen-2: its reads of this parity buffer are over
-  if (t < n && t != r && a.gen > 2) os_spin(a.my_done + t, a.gen - 2, a.timeout_ticks, a.err, a.poison);
-  __syncthreads();
-  if (t == 0) s_bad = poisoned(a.poison);
-  __syncthreads();
-  if (s_bad) return;
-  // (2) push the whole vector to every peer
-  const size_t bytes = a.count * a.es;
-  const bool vec = (((uintptr_t)a.sb | bytes) & 15) == 0;
-  for (int p = 0; p < n; p++) {
-    if (p == r) continue;
-    char *d = a.peer_slot[p];
-    if (vec) {
-      for (size_t i = t; i < bytes / 16; i += kOSB)
-        reinterpret_cast<uint4 *>(d)[i] = reinterpret_cast<const uint4 *>(a.sb)[i];
-    } else {
-      for (size_t i = t; i < bytes; i += kOSB) d[i] = a.sb[i];
-    }
-  }
-  __threadfence_system();
-  __syncthreads();
-  // (3) READY(me, w) at every peer for every slice; (4) every peer's READY(p, w)
-  for (size_t k = t; k < (size_t)n * nwg; k += kOSB) {
-    const int p = (int)(k / nwg);
-    if (p != r) __hip_atomic_store(a.peer_ready[p] + k % nwg, a.gen, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-  }
-  for (size_t k = t; k < (size_t)n * nwg; k += kOSB) {
-    const int p = (int)(k / nwg);
-    if (p != r) os_spin(a.my_ready + (size_t)p * OSWG + k % nwg, a.gen, a.timeout_ticks, a.err, a.poison);
-  }
-  __syncthreads();
-  if (t == 0) s_bad = poisoned(a.poison);
-  __syncthreads();
-  __atomic_thread_fence(__ATOMIC_ACQUIRE);
-  if (s_bad) return;   // stale slots: no fold, and DONE is never raised
-  // (5) fold every element with its segment's program
-  int sidx = 0;
-  for (size_t e = t; e < a.count; e += kOSB) {
-    while (sidx + 1 < a.nseg && e >= a.seg[sidx].hi) sidx++;
-    const size_t off = e * sizeof(T);
-    const T v = eval_prog<OP, T>(a.seg[sidx].p, [&](int j) { return *reinterpret_cast<const T *>(a.src[j] + off); });
-    store_fields(reinterpret_cast<T *>(a.rb + off), v);
-  }
-  // (6) the launch's workgroups counted out, DONE(gen) at every peer
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  if (t == 0) {
-    __threadfence();
-    (void)__hip_atomic_fetch_add(a.counter, (uint64_t)nwg, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
-    __threadfence_system();
-    for (int p = 0; p < n; p++)
-      if (p != r) __hip_atomic_store(a.peer_done[p], a.gen, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-  }
-}
-
+// The call itself is os_ll<T, OP, SYS = true> (mx_fold.hpp): the launched
+// kernel's tagged-word protocol with the operand and result words read and
+// written at system scope too, so no cache maintenance is needed between
+// calls -- the service never crosses a kernel boundary, and what it reads
+// (sbuf, the peers' words) and writes (rbuf, the peers' LL areas, DONE) all
+// bypass this XCD's L2.
 template <class T, class OP>
 __global__ void __launch_bounds__(kOSB) k_csv(const CsvCtl *ctl, const uint64_t *args, CsvHost *host, uint64_t last,
                                               uint64_t epoch, uint64_t idle_ticks, uint64_t life_ticks) {
   __shared__ OneShotArgs A;
   __shared__ int s_exit;
-  __shared__ uint64_t s_q;
+  __shared__ uint64_t s_q, s_words;
+  __shared__ uint64_t tk[TK_N];
   const int t = threadIdx.x;
   uint64_t seen = last;
   const uint64_t born = wall_clock64();
@@ -154,30 +104,44 @@ __global__ void __launch_bounds__(kOSB) k_csv(const CsvCtl *ctl, const uint64_t 
         if (now - t0 > idle_ticks || now - born > life_ticks) { ex = 1; break; }
         __builtin_amdgcn_s_sleep(1);
       }
+      uint64_t words = kCsvArgWords;
       if (!ex) {
-        // system-scope acquire: the arguments written before `seq`, and no
-        // stale operand line in this XCD's L2 (the service never passes a
-        // kernel boundary between calls)
-        __atomic_thread_fence(__ATOMIC_ACQUIRE);
+        // the loads below are issued after `seq` returned (the host wrote
+        // them before it): ordering only, no cache maintenance (they bypass
+        // the L2 like every other access of the service)
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
         if (__hip_atomic_load(&ctl->exit, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM)) ex = 1;
+        words = __hip_atomic_load(&ctl->words, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
         seen = q;
       }
       s_exit = ex;
       s_q = q;
+      tk[TK_SEEN] = wall_clock64();
+      s_words = words < kCsvArgWords ? words : kCsvArgWords;
     }
     __syncthreads();
     if (s_exit) {
       if (t == 0) __hip_atomic_store(&host->left, epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
       return;
     }
+    // the arguments in use: one load per lane, all in flight at once (one
+    // PCIe round trip for up to kOSB words)
     uint64_t *dst = reinterpret_cast<uint64_t *>(&A);
-    for (size_t i = t; i < kCsvArgWords; i += kOSB)
+    for (size_t i = t; i < s_words; i += kOSB)
       dst[i] = __hip_atomic_load(args + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     __syncthreads();
-    csv_call<T, OP>(A);
+    if (t == 0) tk[TK_ARGS] = wall_clock64();
+    const bool ok = os_ll<T, OP, true>(A);
+    // every lane's result words acknowledged before `done`
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     if (t == 0) {
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");   // rb's stores (this XCD's L2) written back
+      tk[TK_CALL] = wall_clock64();
+      // the call's phases (ticks), ahead of `done` (a failed call: none;
+      // the host finds the error word set)
+      for (int k = 1; k < TK_N; k++)
+        __hip_atomic_store(&host->last[k], ok ? tk[k] - tk[k - 1] : 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
       __hip_atomic_store(&host->done, s_q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     }
     __syncthreads();   // A and s_* are rewritten next round
@@ -223,6 +187,8 @@ struct Csv {
   uint64_t idle_ticks = 0, life_ticks = 0;
   uint64_t served = 0, held = 0;
   std::vector<csv_launch_fn> started;
+  double tick_us = 0.01;         // wall clock period
+  double prep_us = 0, wait_us = 0, phase_us[TK_N] = {};   // sums over `served` (mx_coll_service_trace)
 };
 Csv g_csv;
 std::atomic<int> g_csv_on{-1};
@@ -280,6 +246,7 @@ int csv_setup(Csv &v) {
   int rate_khz = 0;
   if (hipDeviceGetAttribute(&rate_khz, hipDeviceAttributeWallClockRate, v.device) != hipSuccess || rate_khz <= 0)
     rate_khz = 100000;
+  v.tick_us = 1e3 / rate_khz;
   v.idle_ticks = (uint64_t)(kCsvIdleS * rate_khz * 1000.0);
   v.life_ticks = (uint64_t)(kCsvLifeS * rate_khz * 1000.0);
   int least = 0, greatest = 0;
@@ -343,7 +310,11 @@ bool csv_start(Csv &v, csv_launch_fn fn) {
 // 1: served (rb final, DONE raised at the peers); 0: not served (the caller
 // launches k_oneshot with the same arguments); < 0: error
 int csv_allreduce(mx_comm *c, const OneShotArgs &a, int op, int type, hipStream_t s) {
-  if (!csv_enabled() || !c->csv_ok || c->defer || c->poisoned) return 0;
+  // the tagged-word calls only (one workgroup's work), operands on 4-byte
+  // boundaries (the service moves 4-byte words at system scope)
+  if (!csv_enabled() || !c->csv_ok || c->defer || c->poisoned || !a.ll || (((uintptr_t)a.sb | (uintptr_t)a.rb) & 3))
+    return 0;
+  const auto t_in = std::chrono::steady_clock::now();
   CsvVisitor vis;
   const csv_launch_fn fn = dispatch(op, type, vis);
   if (!fn || !csv_streams_idle(s)) return 0;
@@ -363,10 +334,18 @@ int csv_allreduce(mx_comm *c, const OneShotArgs &a, int op, int type, hipStream_
     v.type = type;
     if (!csv_start(v, fn)) return 0;
   }
-  memcpy(v.args, &a, sizeof a);
+  // only the segments the call has travel (the kernel reads `words` of them)
+  const size_t used = offsetof(OneShotArgs, seg) + (size_t)a.nseg * sizeof(OsSeg);
+  memcpy(v.args, &a, used);
+  v.ctl->words = (used + 7) / 8;
+  const auto t_post = std::chrono::steady_clock::now();
   uint64_t q = csv_post(v, false);
   for (unsigned k = 0;; k++) {
     if (__atomic_load_n(&v.host->done, __ATOMIC_ACQUIRE) >= q) {
+      const auto t_done = std::chrono::steady_clock::now();
+      v.prep_us += std::chrono::duration<double, std::micro>(t_post - t_in).count();
+      v.wait_us += std::chrono::duration<double, std::micro>(t_done - t_post).count();
+      for (int j = 1; j < TK_N; j++) v.phase_us[j] += v.tick_us * (double)v.host->last[j];
       v.served++;
       return 1;
     }
@@ -418,6 +397,16 @@ extern "C" int mx_coll_service_stats(unsigned long long *served, unsigned long l
   std::lock_guard<std::mutex> lk(v.mu);
   if (served) *served = v.served;
   if (launches) *launches = v.epoch;
+  return v.state;
+}
+
+extern "C" int mx_coll_service_trace(double *out, int n) {
+  mx::Csv &v = mx::g_csv;
+  std::lock_guard<std::mutex> lk(v.mu);
+  const double d = v.served ? (double)v.served : 1.0;
+  const double t[5] = {(double)v.served, v.prep_us / d, v.wait_us / d, v.phase_us[mx::TK_ARGS] / d,
+                       v.phase_us[mx::TK_CALL] / d};
+  for (int i = 0; i < n && i < 5; i++) out[i] = t[i];
   return v.state;
 }
 

@@ -183,6 +183,8 @@ struct mx_comm {
   size_t main_bytes;           // staging for the chunked paths: [0, main_bytes)
   size_t os_max, os_slot;      // one-shot: default max bytes per rank, slot stride
   size_t os_cap;               // one-shot: the most a slot holds (autotuning may pick it up to here)
+  size_t os_ll;                // one-shot: the tagged-word (LL) protocol up to this many bytes per rank
+                               // (its area, 2 * os_ll, follows the raw os_cap + 256 in each slot)
   uint64_t os_count;           // one-shot workgroup completions so far
   char *staging;               // mine (uncached, IPC-exported)
   char *peer_staging[mx::MAXR];    // mapped views (peer_staging[rank] = staging)
@@ -219,6 +221,7 @@ struct mx_comm {
   int zc_direct;
   uint64_t reg_seq, reg_tick;
   std::vector<struct mx_reg_import> *reg_imp;
+  std::vector<mx::IpcGone> *reg_gone;   // the imports closed (ipc_open_checked)
   void *reg_fast;   // the last exchange's records and mappings (mx_coll.hip RegFast)
   // data-movement autotuning of blocking collectives: per
   // collective kind (TUNE_*) and power-of-two size class, the first call
@@ -333,6 +336,7 @@ struct mx_request {
   uint64_t post, launch;
   void *rx;
   int rget;          // the host launched this receive's pull (single-copy rendezvous)
+  int64_t rget_t0;   // steady-clock ns of the pull's first refused mapping (0: none)
 };
 
 namespace mx {

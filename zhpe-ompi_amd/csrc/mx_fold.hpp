@@ -220,6 +220,7 @@ struct OneShotArgs {
   size_t count, es, slice;
   uint64_t *mflags;             // the blocking call's completion flags (Mark.flags), or null
   uint64_t mv;                  // their sequence number
+  int ll;                       // the tagged-word protocol (os_ll): peer_slot / src[p] point at the LL areas
   OsSeg seg[OS_MAXSEG];
 };
 
@@ -236,8 +237,148 @@ __device__ __forceinline__ void os_spin(const uint64_t *f, uint64_t v, uint64_t 
   }
 }
 
+// ---------------------------------------------------------------------------
+// The tagged-word (LL) variant for one-workgroup calls (4- and 8-byte element
+// types, at most OS_LL_MAX bytes per rank): every 4-byte word of my
+// contribution travels to each peer as one 8-byte store {gen, word} into the
+// LL area of my slot there, so the data is its own READY -- no release fence
+// between data and flag, no READY row, no acquire before the fold.  A peer's
+// word is taken when its tag reads this generation (stale words carry gen-2
+// or older; the LL area is never written by the raw path, so raw bytes can
+// never pass for a tag).  Each lane gathers its elements' words from every
+// peer into its own LDS column and evaluates the call's fold program there
+// (the same program as the raw path: the results are bit for bit the raw
+// path's).  DONE(gen) follows once every lane's gathers have returned.  The
+// loads and stores are system-scope (L2 bypassed), so the resident service
+// (SYS: its operand and result words too) runs with no cache maintenance at
+// all.  Returns false when the call failed (poisoned, or a peer timed out).
+// ---------------------------------------------------------------------------
+constexpr size_t OS_LL_MAX = 4096;   // bytes per rank (one slice of the raw path)
+
+__device__ __forceinline__ uint64_t ll_ld(const uint64_t *p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+template <class T, class OP, bool SYS>
+__device__ bool os_ll(const OneShotArgs &a) {
+  constexpr int W = (int)(sizeof(T) / 4);
+  static_assert(sizeof(T) == 4 || sizeof(T) == 8, "LL carries 4- and 8-byte elements");
+  // lane t's gathered words, [f * kOSB + t]: at most (MAXR - 1) peers x
+  // OS_LL_MAX / 4 / kOSB words = 60 per lane
+  __shared__ uint32_t col[(MAXR - 1) * (OS_LL_MAX / 4 / kOSB) * kOSB];
+  __shared__ int s_bad;
+  const int t = threadIdx.x, n = a.n, r = a.rank;
+  const uint32_t g = (uint32_t)a.gen;
+  const uint64_t tag = (uint64_t)g << 32;
+  if (t == 0) s_bad = poisoned(a.poison);
+  __syncthreads();
+  if (s_bad) return false;
+  // (1) every peer is past gen-2: its reads of this parity's LL area are over
+  if (t < n && t != r && a.gen > 2) os_spin(a.my_done + t, a.gen - 2, a.timeout_ticks, a.err, a.poison);
+  __syncthreads();
+  if (t == 0) s_bad = poisoned(a.poison);
+  __syncthreads();
+  if (s_bad) return false;
+  // (2) my words, tagged, into every peer's LL area
+  const size_t nw = a.count * W;
+  const bool al = ((uintptr_t)a.sb & 3) == 0;
+  const uint32_t *sw = reinterpret_cast<const uint32_t *>(a.sb);
+  for (size_t i = t; i < nw; i += kOSB) {
+    uint32_t v;
+    if (SYS) v = __hip_atomic_load(sw + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    else if (al) v = sw[i];
+    else __builtin_memcpy(&v, a.sb + 4 * i, 4);
+    for (int p = 0; p < n; p++)
+      if (p != r)
+        __hip_atomic_store(reinterpret_cast<uint64_t *>(a.peer_slot[p]) + i, tag | v, __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_SYSTEM);
+  }
+  // (3) gather: lane t's words of every peer -- E elements (t, t + kOSB, ...)
+  // of W words each -- flattened as f = (peer * E + i) * W + k and loaded
+  // eight at a time (all eight in flight), into LDS column t
+  const int E = (int)((a.count + kOSB - 1) / kOSB);
+  const int Lw = (n - 1) * E * W;
+  bool bad = false;
+  const uint64_t t0 = wall_clock64();
+  for (int f0 = 0; f0 < Lw && !bad; f0 += 8) {
+    uint64_t v[8];
+    const uint64_t *ad[8];
+#pragma unroll
+    for (int u = 0; u < 8; u++) {
+      const int f = f0 + u;
+      ad[u] = nullptr;
+      if (f < Lw) {
+        const int k = f % W, ii = (f / W) % E, jj = f / (W * E);
+        const size_t e = (size_t)t + (size_t)ii * kOSB;
+        if (e < a.count) {
+          ad[u] = reinterpret_cast<const uint64_t *>(a.src[jj < r ? jj : jj + 1]) + e * W + k;
+          v[u] = ll_ld(ad[u]);
+        }
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < 8; u++) {
+      if (!ad[u]) continue;
+      while ((uint32_t)(v[u] >> 32) != g && !bad) {
+        __builtin_amdgcn_s_sleep(1);
+        if (wall_clock64() - t0 > a.timeout_ticks) {
+          raise_timeout(a.err, a.poison);
+          bad = true;
+        } else {
+          v[u] = ll_ld(ad[u]);
+        }
+      }
+      col[(f0 + u) * kOSB + t] = (uint32_t)v[u];
+    }
+  }
+  if (bad) s_bad = 1;
+  __syncthreads();
+  if (s_bad) return false;   // a peer's words never came: no DONE
+  // (4) fold lane t's elements from its column
+  int sidx = 0;
+  for (int ii = 0; ii < E; ii++) {
+    const size_t e = (size_t)t + (size_t)ii * kOSB;
+    if (e >= a.count) break;
+    while (sidx + 1 < a.nseg && e >= a.seg[sidx].hi) sidx++;
+    const size_t off = e * sizeof(T);
+    const T v = eval_prog<OP, T>(a.seg[sidx].p, [&](int j) {
+      T x;
+      uint32_t u[W];
+      if (j != r) {
+        const int jj = j < r ? j : j - 1;
+#pragma unroll
+        for (int k = 0; k < W; k++) u[k] = col[((jj * E + ii) * W + k) * kOSB + t];
+        __builtin_memcpy(&x, u, sizeof(T));
+      } else if (SYS) {
+#pragma unroll
+        for (int k = 0; k < W; k++) u[k] = __hip_atomic_load(sw + e * W + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        __builtin_memcpy(&x, u, sizeof(T));
+      } else {
+        x = *reinterpret_cast<const T *>(a.sb + off);
+      }
+      return x;
+    });
+    if (SYS) {
+      uint32_t u[W];
+      __builtin_memcpy(u, &v, sizeof(T));
+#pragma unroll
+      for (int k = 0; k < W; k++)
+        __hip_atomic_store(reinterpret_cast<uint32_t *>(a.rb) + e * W + k, u[k], __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_SYSTEM);
+    } else {
+      store_fields(reinterpret_cast<T *>(a.rb + off), v);
+    }
+  }
+  // (5) every lane's gathers returned before the barrier above: DONE(gen) at every peer
+  if (t == 0)
+    for (int p = 0; p < n; p++)
+      if (p != r) __hip_atomic_store(a.peer_done[p], a.gen, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  return true;
+}
+
+// the raw protocol, steps (1)-(6) of k_oneshot; false when the call failed
 template <class T, class OP>
-__global__ void __launch_bounds__(kOSB) k_oneshot(OneShotArgs a) {
+__device__ bool os_raw(const OneShotArgs &a) {
   const int w = blockIdx.x, t = threadIdx.x;
   const size_t lo = (size_t)w * a.slice, hi = lo + a.slice < a.count ? lo + a.slice : a.count;
   // poison checks are taken by thread 0 and shared, so the whole workgroup
@@ -245,13 +386,13 @@ __global__ void __launch_bounds__(kOSB) k_oneshot(OneShotArgs a) {
   __shared__ int s_bad;
   if (t == 0) s_bad = poisoned(a.poison);
   __syncthreads();
-  if (s_bad) return;
+  if (s_bad) return false;
   // (1) every peer is past gen-2: its reads of this parity buffer are over
   if (t < a.n && t != a.rank && a.gen > 2) os_spin(a.my_done + t, a.gen - 2, a.timeout_ticks, a.err, a.poison);
   __syncthreads();
   if (t == 0) s_bad = poisoned(a.poison);
   __syncthreads();
-  if (s_bad) return;   // a peer never freed its buffer: push nothing
+  if (s_bad) return false;   // a peer never freed its buffer: push nothing
   // (2) push my slice (bytes [lo*es, hi*es)) to every peer
   if (lo < hi) {
     const size_t b0 = lo * a.es, b1 = hi * a.es;
@@ -278,7 +419,7 @@ __global__ void __launch_bounds__(kOSB) k_oneshot(OneShotArgs a) {
   if (t == 0) s_bad = poisoned(a.poison);
   __syncthreads();
   __atomic_thread_fence(__ATOMIC_ACQUIRE);
-  if (s_bad) return;   // stale slots: no fold, and DONE is never raised
+  if (s_bad) return false;   // stale slots: no fold, and DONE is never raised
   // (5) fold the slice
   int sidx = 0;
   for (size_t e = lo + t; e < hi; e += kOSB) {
@@ -298,6 +439,18 @@ __global__ void __launch_bounds__(kOSB) k_oneshot(OneShotArgs a) {
         if (p != a.rank) __hip_atomic_store(a.peer_done[p], a.gen, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     }
   }
+  return true;
+}
+
+template <class T, class OP>
+__global__ void __launch_bounds__(kOSB) k_oneshot(OneShotArgs a) {
+  const int w = blockIdx.x, t = threadIdx.x;
+  bool ok;
+  if constexpr (sizeof(T) == 4 || sizeof(T) == 8)
+    ok = a.ll ? os_ll<T, OP, false>(a) : os_raw<T, OP>(a);
+  else
+    ok = os_raw<T, OP>(a);
+  if (!ok) return;
   // (7) a blocking call: every workgroup, once its stores of rb have landed,
   // releases them at system scope and raises its own completion flag (the
   // host waits for the grid's flags instead of a marker kernel, mark_wait)

@@ -4,6 +4,8 @@
 #include "../../include/mx_kernels.h"
 #include "../../include/mx_rdma.h"
 
+#include <vector>
+
 namespace mx {
 extern int g_num_cus;      // CUs of the current device (256 on MI355X)
 extern int g_device;       // device selected by mx_init
@@ -63,6 +65,21 @@ void release_later(void *p, int kind);
 void release_flush();
 bool release_now_if_quiet(void *p, int kind);   // false: deferred
 bool release_now_or_keep(void *p, int kind);    // false: not quiet, nothing done (the caller keeps p)
+// IPC imports and the runtime's reuse of them (DESIGN 7.5,
+// tools/reg_remade_probe.py): opening the handle of an allocation its owner
+// re-made at a freed one's address can hand back this process's import of the
+// FREED allocation -- every time while that import is still open, and about
+// one time in four right after it was closed -- and the mapping then reaches
+// the old memory.  Each import cache keeps the runtime object ids of the
+// imports it closed (per owner and address range); ipc_open_checked closes an
+// open that returns one of them again and refuses it (the caller takes its
+// fallback path; a later call tries again).
+struct IpcGone { int64_t owner; uint64_t base, size, oid; };
+uint64_t ipc_object_id(const void *p);   // 0: unknown
+void ipc_gone_add(std::vector<IpcGone> &g, int64_t owner, uint64_t base, uint64_t size, const void *mapping);
+// 1 mapped (*out, *oid), 0 refused (the runtime handed back a closed import), < 0 error
+int ipc_open_checked(const void *handle, std::vector<IpcGone> &g, int64_t owner, uint64_t base, uint64_t size,
+                     char **out, uint64_t *oid);
 // a get through mx_rdma's import cache, without a completion event (mx_rdma.hip)
 int rdma_pull(void *local, const mx_rdma_handle_t *remote, uint64_t remote_addr, size_t bytes, hipStream_t s);
 }  // namespace mx

@@ -1254,6 +1254,7 @@ void p2p_finish(mx_request *q) {
       if (jt != w.end()) w.erase(jt);
     }
     q->rget = 0;
+    q->rget_t0 = 0;
     delete static_cast<P2PRecvArgs *>(q->rx);
     q->rx = nullptr;
     q->launch = 0;
@@ -1478,6 +1479,7 @@ int p2p_enqueue(mx_request *q, hipStream_t *done_stream) {
     a.err = c->err_dev;
     a.rget_ok = rget_on() && g_rx[c->device].pull != nullptr;
     q->rget = 0;
+    q->rget_t0 = 0;
     q->tmp = tmp;   // freed at completion: a receive that yields runs (and unpacks) again
     q->post = ++c->p2p_posts;
     if ((rc = p2p_rx_launch(q))) {
@@ -1593,7 +1595,14 @@ static void p2p_rget_launch(mx_request *q) {
   memcpy(&d, (const void *)&q->status[8], sizeof d);
   const uint64_t n = (uint64_t)q->status[0];
   int rc = n ? rdma_pull(a.buf, &d.h, d.addr, n, D.pull) : MX_SUCCESS;
-  if (rc == MX_ERR_STATE) return;   // retried at the next progress
+  if (rc == MX_ERR_STATE) {   // retried at the next progress, for at most the communicator's timeout (or 60 s)
+    const int64_t now = std::chrono::duration_cast<std::chrono::nanoseconds>(
+                            std::chrono::steady_clock::now().time_since_epoch()).count();
+    if (!q->rget_t0) q->rget_t0 = now;
+    const double lim = c->timeout_s > 0 ? c->timeout_s : 60.0;
+    if ((double)(now - q->rget_t0) * 1e-9 < lim) return;
+    rc = MX_ERR_HIP;   // the sender's allocation could not be mapped: the receive fails, FIN still goes
+  }
   if (!rc && q->tmp) rc = mx_unpack(q->ddt, q->count, q->rbuf, q->tmp, 0, a.cap, D.pull);
   if (rc && !q->status[2]) q->status[2] = rc;
   P2PFinArgs f;

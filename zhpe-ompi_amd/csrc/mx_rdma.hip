@@ -48,6 +48,7 @@ struct Import {
 
 std::mutex g_mu;
 std::vector<Import> g_imp;
+std::vector<IpcGone> g_gone;          // the imports closed (ipc_open_checked)
 uint64_t g_tick;
 hipStream_t g_stream;
 std::vector<hipEvent_t> g_ev_free;
@@ -84,6 +85,7 @@ int import_locked(const mx_rdma_handle_t &h, char **out) {
       // the owner freed that allocation and made another in its place: the
       // stale import must be closed before the new handle is opened; while
       // the device is not quiet it stays cached and the call is retried
+      ipc_gone_add(g_gone, m.pid, m.base, m.size, m.ptr);
       if (!release_now_or_keep(m.ptr, REL_IPC)) return MX_ERR_STATE;
       g_imp.erase(g_imp.begin() + (long)i);
       continue;
@@ -94,16 +96,17 @@ int import_locked(const mx_rdma_handle_t &h, char **out) {
     size_t lru = 0;
     for (size_t i = 1; i < g_imp.size(); i++)
       if (g_imp[i].used < g_imp[lru].used) lru = i;
+    ipc_gone_add(g_gone, g_imp[lru].pid, g_imp[lru].base, g_imp[lru].size, g_imp[lru].ptr);
     release_later(g_imp[lru].ptr, REL_IPC);
     g_imp.erase(g_imp.begin() + (long)lru);
   }
-  hipIpcMemHandle_t ih;
-  memcpy(&ih, h.ipc, sizeof ih);
+  // checked against the imports closed at that range: the runtime may hand
+  // one back (then MX_ERR_STATE: the caller's fallback, as a busy device)
   char *p = nullptr;
-  if (hipIpcOpenMemHandle((void **)&p, ih, hipIpcMemLazyEnablePeerAccess) != hipSuccess || !p) {
-    (void)hipGetLastError();
-    return MX_ERR_HIP;
-  }
+  uint64_t oid = 0;
+  const int oc = ipc_open_checked(h.ipc, g_gone, h.pid, h.base, h.size, &p, &oid);
+  if (oc < 0) return oc;
+  if (oc == 0) return MX_ERR_STATE;
   g_imp.push_back(Import{h.pid, h.base, h.size, h.id, p, ++g_tick});
   *out = p;
   return MX_SUCCESS;

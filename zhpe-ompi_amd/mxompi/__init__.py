@@ -254,7 +254,8 @@ class CollStats(ctypes.Structure):
                 ("total_ms", ctypes.c_double), ("zero_copy_calls", ctypes.c_uint64),
                 ("staged_calls", ctypes.c_uint64), ("direct_calls", ctypes.c_uint64),
                 ("reg_fast_calls", ctypes.c_uint64), ("p2p_relaunches", ctypes.c_uint64),
-                ("p2p_pulls", ctypes.c_uint64), ("service_calls", ctypes.c_uint64)]
+                ("p2p_pulls", ctypes.c_uint64), ("service_calls", ctypes.c_uint64),
+                ("reg_stale_refused", ctypes.c_uint64)]
 
 
 _AG_FN = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p)
