@@ -1096,9 +1096,8 @@ def test_registration_fast_path_reused_and_remade_buffers(n):
                                      f"diag {[out[k]['diag'] for k in range(n)]}")
     for r in range(n):
         assert out[r]["zc1"] == 8 and out[r]["fast1"] == 7, out[r]      # the first call registers
-        # a re-made rbuf is zero-copy unless the runtime handed a peer back its
-        # import of the freed one (refused: that call runs staged)
-        assert 8 <= out[r]["zc2"] <= 11, out[r]
+        # an rbuf re-made at a freed one's address is not exported (DESIGN 7.5:
+        # a peer's import of it can reach the freed memory): those calls run
+        # staged; the first re-made rbuf is zero-copy only if its address is new
+        assert 8 <= out[r]["zc2"] <= 9, out[r]
         assert out[r]["fast2"] == 7, out[r]                             # re-made rbufs: never the fast path
-    print("re-made rbufs: zero-copy calls", [out[r]["zc2"] - 8 for r in range(n)], "of 3; refused imports",
-          [out[r]["refused"] for r in range(n)])

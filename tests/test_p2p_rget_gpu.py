@@ -11,7 +11,8 @@ receive buffer shorter than the message (MPI_ERR_TRUNCATE, the channel stays
 usable), a datatype receive (pulled into staging, unpacked), a datatype send
 (packed in stream-ordered memory: no handle, the mailbox path), a send to
 self, an allocation freed and re-made by the sender between two messages
-(the receiver must read the new one, not the stale mapping), and the whole
+(not exported when re-made at an address exported before: the mailbox
+carries it; either way the receiver must read the new bytes), and the whole
 set again with MX_P2P_RGET=0 (the two-copy mailbox path, no pulls).
 """
 import os
@@ -178,8 +179,11 @@ def test_rendezvous_single_copy_and_mailbox(rget):
         assert out[r]["self"] == _data(40 + r, 2 << 20).tobytes()
     for cycle in range(3):
         assert r1[f"remade{cycle}"] == _data(50 + cycle, 1 << 20).tobytes(), cycle
-    # the pulls: sizes (3) + trunc (2) + ddt receive (1) + self (1) + remade (3) on rank 1
+    # the pulls: sizes (3) + trunc (2) + ddt receive (1) + self (1) on rank 1, and
+    # the re-made allocations' messages only where the address was new (an
+    # allocation re-made at an address exported before goes by the mailbox,
+    # DESIGN 7.5)
     if rget:
-        assert r1["pulls"] >= 9, r1["pulls"]
+        assert r1["pulls"] >= 7, r1["pulls"]
     else:
         assert r1["pulls"] == 0 and out[0]["pulls"] == 0

@@ -54,6 +54,7 @@ def worker(rank, port, q, cycles):
     vp, sz = ctypes.c_void_p, ctypes.c_size_t
     X = torch.empty(COUNT, dtype=torch.int32, device="cuda")
     bad = [0, 0]
+    fails = []
     st0 = comm.stats()
     for cyc in range(cycles):
         p = vp()
@@ -65,13 +66,16 @@ def worker(rank, port, q, cycles):
             host = np.empty(COUNT, np.int32)
             assert L.mx_memcpy(vp(host.ctypes.data), p, sz(4 * COUNT), None) == 0
             want = sum(_x(r, cyc, rep).astype(np.int64) for r in range(N)).astype(np.int32)
-            bad[rep] += int(not np.array_equal(host, want))
+            if not np.array_equal(host, want):
+                bad[rep] += 1
+                wrong = np.nonzero(host != want)[0]
+                fails.append((cyc, rep, int(wrong[0]), len(wrong), hex(p.value)))
         torch.cuda.synchronize()
         assert L.mx_free(p) == 0
     st1 = comm.stats()
     comm.close()
     dist.destroy_process_group()
-    q.put((rank, {"bad": bad, "zc": st1["zero_copy_calls"] - st0["zero_copy_calls"],
+    q.put((rank, {"bad": bad, "fails": fails, "zc": st1["zero_copy_calls"] - st0["zero_copy_calls"],
                   "refused": st1["reg_stale_refused"] - st0["reg_stale_refused"]}))
 
 
@@ -93,3 +97,5 @@ if __name__ == "__main__":
         p.join(timeout=60)
     print(f"cycles {cycles}, per rank (wrong results of call 1, call 2; zero-copy calls; refused imports):",
           [(res[r]["bad"], res[r]["zc"], res[r]["refused"]) for r in range(N)], flush=True)
+for r in range(N):
+    print(f"rank {r} wrong (cycle, call, first wrong element, wrong elements, rbuf):", res[r]["fails"][:12], flush=True)

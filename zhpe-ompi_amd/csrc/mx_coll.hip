@@ -430,6 +430,20 @@ bool mx::release_now_or_keep(void *p, int kind) {   // nothing queued when not q
   release_now(p, kind);
   return true;
 }
+bool mx::export_remade(uint64_t base, uint64_t size, uint64_t id) {
+  struct Ex { uint64_t base, size, id; };
+  static std::mutex mu;
+  static std::vector<Ex> hist;   // every allocation exported (the last 4096)
+  std::lock_guard<std::mutex> lk(mu);
+  for (const Ex &e : hist)
+    if (e.base < base + size && base < e.base + e.size) {
+      if (e.base == base && e.size == size && e.id == id) return false;   // the same allocation
+      return true;   // another allocation was exported over this range
+    }
+  if (hist.size() >= 4096) hist.erase(hist.begin());
+  hist.push_back(Ex{base, size, id});
+  return false;
+}
 uint64_t mx::ipc_object_id(const void *p) {
   unsigned long long id = 0;
   if (!p || hipPointerGetAttribute(&id, HIP_POINTER_ATTRIBUTE_BUFFER_ID, (hipDeviceptr_t)p) != hipSuccess) {
@@ -1805,6 +1819,7 @@ static bool reg_export(const void *p, size_t bytes, RegBuf *b) {
       }
   }
   if (!hit) {
+    if (export_remade((uint64_t)(uintptr_t)base, size, id)) return false;
     if (hipIpcGetMemHandle(&b->h, base) != hipSuccess) {
       (void)hipGetLastError();
       return false;
@@ -1837,6 +1852,7 @@ static char *reg_import(mx_comm *c, int p, const RegBuf &b, const RegBuf *own, i
     }
   size_t held = 0;
   bool closed = false;
+  mx_reg_import old{};   // (diagnostic MX_REG_DIAG) the stale import closed here
   for (size_t i = 0; i < v.size();) {
     const mx_reg_import &m = v[i];
     if (m.peer == p && m.base < b.base + b.size && b.base < m.base + m.size) {   // overlaps: stale
@@ -1845,6 +1861,8 @@ static char *reg_import(mx_comm *c, int p, const RegBuf &b, const RegBuf *own, i
       // call declines (every rank falls back to the staged path), so the next
       // call finds it and tries again -- it is never dropped unclosed
       ipc_gone_add(*c->reg_gone, p, m.base, m.size, m.ptr);
+      old = m;
+      old.used = ipc_object_id(m.ptr);
       if (!release_now_or_keep(m.ptr, REL_IPC)) return nullptr;
       v.erase(v.begin() + (long)i);
       closed = true;
@@ -1861,11 +1879,6 @@ static char *reg_import(mx_comm *c, int p, const RegBuf &b, const RegBuf *own, i
     release_later(v[lru].ptr, REL_IPC);
     v.erase(v.begin() + (long)lru);
   }
-  if (closed) {   // (experiment MX_REG_REOPEN: 1 device sync, 2 sleep 2 ms, 3 both, after closing a stale import)
-    static const int ro = [] { const char *e = getenv("MX_REG_REOPEN"); return e && *e ? atoi(e) : 0; }();
-    if (ro & 1) { if (hipDeviceSynchronize() != hipSuccess) (void)hipGetLastError(); }
-    if (ro & 2) usleep(2000);
-  }
   char *ptr = nullptr;
   uint64_t oid = 0;
   const int oc = ipc_open_checked(&b.h, *c->reg_gone, p, b.base, b.size, &ptr, &oid);
@@ -1873,6 +1886,12 @@ static char *reg_import(mx_comm *c, int p, const RegBuf &b, const RegBuf *own, i
     if (oc == 0) c->st.reg_stale_refused++;
     return nullptr;
   }
+  static const bool diag = [] { const char *e = getenv("MX_REG_DIAG"); return e && *e == '1'; }();
+  if (diag && closed)
+    fprintf(stderr, "[mx diag] rank %d call %llu peer %d: re-made base %#llx id %llu->%llu handle %s ptr %p->%p oid %llu->%llu\n",
+            c->rank, (unsigned long long)c->reg_seq, p, (unsigned long long)b.base, (unsigned long long)old.id,
+            (unsigned long long)b.id, memcmp(old.h, &b.h, sizeof old.h) ? "differs" : "IDENTICAL", (void *)old.ptr,
+            (void *)ptr, (unsigned long long)old.used, (unsigned long long)oid);
   // a mapping must never overlap one of this rank's own allocations (the
   // round-1 IPC aliasing symptom): refuse it, the call takes the
   // staged path
@@ -1881,7 +1900,9 @@ static char *reg_import(mx_comm *c, int p, const RegBuf &b, const RegBuf *own, i
       release_later(ptr, REL_IPC);
       return nullptr;
     }
-  v.push_back(mx_reg_import{p, b.base, b.size, b.id, ptr, ++c->reg_tick});
+  mx_reg_import ni{p, b.base, b.size, b.id, ptr, ++c->reg_tick, {}};
+  memcpy(ni.h, &b.h, sizeof ni.h);
+  v.push_back(ni);
   return ptr;
 }
 

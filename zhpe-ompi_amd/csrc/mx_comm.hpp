@@ -170,6 +170,7 @@ struct mx_reg_import {
   uint64_t base, size, id;
   char *ptr;
   uint64_t used;
+  unsigned char h[64];   // the handle it was opened from
 };
 
 // ---------------------------------------------------------------------------

@@ -80,6 +80,14 @@ void ipc_gone_add(std::vector<IpcGone> &g, int64_t owner, uint64_t base, uint64_
 // 1 mapped (*out, *oid), 0 refused (the runtime handed back a closed import), < 0 error
 int ipc_open_checked(const void *handle, std::vector<IpcGone> &g, int64_t owner, uint64_t base, uint64_t size,
                      char **out, uint64_t *oid);
+// Exports of allocations re-made at an address this process exported before
+// are refused: a peer's import of one reached the freed
+// allocation's memory in about one case in four on this runtime
+// (tools/reg_remade_probe.py), with a handle and a runtime object of its own
+// -- nothing the importer can check.  True: refuse (the zero-copy collectives
+// take the staged path, the rendezvous the mailbox, BTL registration fails).
+// Records the allocation otherwise.
+bool export_remade(uint64_t base, uint64_t size, uint64_t id);
 // a get through mx_rdma's import cache, without a completion event (mx_rdma.hip)
 int rdma_pull(void *local, const mx_rdma_handle_t *remote, uint64_t remote_addr, size_t bytes, hipStream_t s);
 }  // namespace mx

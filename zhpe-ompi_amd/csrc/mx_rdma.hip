@@ -189,6 +189,7 @@ extern "C" int mx_rdma_register(const void *ptr, size_t bytes, mx_rdma_handle_t 
       break;
     }
   if (!hit) {
+    if (export_remade((uint64_t)(uintptr_t)base, size, id)) return MX_ERR_UNSUPPORTED;   // 
     hipIpcMemHandle_t ih;
     if (hipIpcGetMemHandle(&ih, base) != hipSuccess) {
       (void)hipGetLastError();
