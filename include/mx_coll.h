@@ -213,8 +213,10 @@ int mx_coll_service_stats(unsigned long long *served, unsigned long long *launch
 int mx_coll_service_set(int on);
 /* Where a served call's time goes, means over the served calls (microseconds):
  * out[0] calls, [1] host preparation, [2] host wait from the post to `done`,
- * and the kernel's phases [3] argument read, [4] the call (push, gather,
- * fold, DONE, result words acknowledged).  Fills min(n, 5) entries. */
+ * and the kernel's phases [3] arguments (the command line, and the
+ * arguments block when the call carried it), [4] the call (push, gather,
+ * fold, DONE, result words acknowledged); [5] commands that carried the
+ * arguments block (a count).  Fills min(n, 6) entries. */
 int mx_coll_service_trace(double *out, int n);
 int mx_comm_set_profiling(mx_comm_t *comm, int on);
 int mx_comm_get_stats(mx_comm_t *comm, mx_coll_stats_t *stats, int reset);

@@ -127,18 +127,23 @@ def _worker(rank, port, q):
                 torch.cuda.synchronize()
                 hbuf = ctypes.create_string_buffer(hb.value)
                 r2 = vp()
-                assert H.mxh_btl_register(p, 1 << 20, hbuf, ctypes.byref(r2)) == 0
-                exchange((hbuf.raw, p.value))
+                # refused for an allocation re-made at an address exported
+                # before: ob1 then moves the message by copy
+                rc = H.mxh_btl_register(p, 1 << 20, hbuf, ctypes.byref(r2))
+                exchange((rc, hbuf.raw, p.value))
                 dist.barrier()                    # the peer has read it
-                H.mxh_btl_deregister(r2)
+                if rc == 0:
+                    H.mxh_btl_deregister(r2)
                 assert L.mx_free(p) == 0
             else:
-                ph, pa = exchange(None)
-                dst = torch.zeros(1 << 20, dtype=torch.uint8, device="cuda")
-                torch.cuda.synchronize()
-                hbuf = ctypes.create_string_buffer(ph, len(ph))
-                assert H.mxh_btl_rdma(1, dst.data_ptr(), pa, hbuf, 1 << 20, 1) == 0
-                got[f"remade{cycle}"] = dst.cpu().numpy().tobytes()
+                rc, ph, pa = exchange(None)
+                got[f"remade{cycle}_rc"] = rc
+                if rc == 0:
+                    dst = torch.zeros(1 << 20, dtype=torch.uint8, device="cuda")
+                    torch.cuda.synchronize()
+                    hbuf = ctypes.create_string_buffer(ph, len(ph))
+                    assert H.mxh_btl_rdma(1, dst.data_ptr(), pa, hbuf, 1 << 20, 1) == 0
+                    got[f"remade{cycle}"] = dst.cpu().numpy().tobytes()
                 got[f"remade{cycle}_addr"] = pa
                 dist.barrier()
         dist.destroy_process_group()
@@ -181,4 +186,7 @@ def test_btl_rdma_get_put_between_processes():
     assert r1["put"] == _data(50, 1 << 20).tobytes()
     assert r1["put_edges"] == (int(owner[2]), int(owner[3 + (1 << 20)]))
     for cycle in range(3):
-        assert r0[f"remade{cycle}"] == _data(100 + cycle, 1 << 20).tobytes(), cycle
+        if r0[f"remade{cycle}_rc"] == 0:       # registered: the get reads the new allocation's bytes
+            assert r0[f"remade{cycle}"] == _data(100 + cycle, 1 << 20).tobytes(), cycle
+        else:                                    # refused only for a re-made allocation
+            assert cycle > 0, cycle

@@ -4,9 +4,10 @@ usage: python tools/coll_lat.py [N] [sizes]   (N processes sharing GPU 0,
 default 2; sizes a comma list of bytes, default 8,1024,32768)
 
 Per size and mode: the median of 1000 blocking fp32 SUM allreduces timed one
-by one from Python, the maximum over ranks; the Python + ctypes cost of one
-library call (mx_coll_service_stats, no GPU work) is printed beside it so the
-library's own time can be read off.  With the service on, rank 0 also prints
+by one from Python through the Comm wrapper, and (`*_abi`) of 1000 more
+through the bare C-ABI entry point mx_allreduce (ctypes, arguments converted
+once), the maximum over ranks; the Python + ctypes cost of one two-argument
+library call (mx_coll_service_stats, no GPU work) is printed beside it.  With the service on, rank 0 also prints
 mx_coll_service_trace: where a served call's time goes (host preparation,
 host wait from post to `done`, and the kernel's argument read and the call
 itself)."""
@@ -54,18 +55,31 @@ def worker(rank, n, port, q, sizes):
             for _ in range(50):
                 comm.allreduce(x.data_ptr(), y.data_ptr(), cnt, "FLOAT", "SUM", "auto", st)
             dist.barrier()
-            tr0 = (ctypes.c_double * 5)()
-            L.mx_coll_service_trace(tr0, 5)
+            tr0 = (ctypes.c_double * 6)()
+            L.mx_coll_service_trace(tr0, 6)
             ts = []
             for _ in range(ITERS):
                 t0 = time.perf_counter()
                 comm.allreduce(x.data_ptr(), y.data_ptr(), cnt, "FLOAT", "SUM", "auto", st)
                 ts.append(time.perf_counter() - t0)
-            tr1 = (ctypes.c_double * 5)()
-            L.mx_coll_service_trace(tr1, 5)
-            med = torch.tensor([sorted(ts)[len(ts) // 2] * 1e6])
+            # the C-ABI call itself: mx_allreduce through ctypes with its
+            # arguments converted once (no wrapper, no name lookups)
+            fn = mxompi._coll_lib().mx_allreduce
+            args = (comm.h, ctypes.c_void_p(x.data_ptr()), ctypes.c_void_p(y.data_ptr()), ctypes.c_size_t(cnt),
+                    mxompi._slot("FLOAT"), mxompi._op("SUM"), mxompi._alg(mxompi.ALLREDUCE, "auto"),
+                    ctypes.c_void_p(st) if st else None)
+            ta = []
+            for _ in range(ITERS):
+                t0 = time.perf_counter()
+                rc = fn(*args)
+                ta.append(time.perf_counter() - t0)
+                assert rc == 0, rc
+            tr1 = (ctypes.c_double * 6)()
+            L.mx_coll_service_trace(tr1, 6)
+            med = torch.tensor([sorted(ts)[len(ts) // 2] * 1e6, sorted(ta)[len(ta) // 2] * 1e6])
             dist.all_reduce(med, op=dist.ReduceOp.MAX)
             row[mode] = round(float(med[0]), 2)
+            row[mode + "_abi"] = round(float(med[1]), 2)
             if mode == "service":
                 # means over this size's served calls only
                 k = tr1[0] - tr0[0]
@@ -74,6 +88,7 @@ def worker(rank, n, port, q, sizes):
                     names = ("prep", "wait", "k_args", "k_call")
                     row["trace_us"] = {nm: round((tr1[i + 1] * tr1[0] - tr0[i + 1] * tr0[0]) / k, 2)
                                        for i, nm in enumerate(names)}
+                    row["full_commands"] = int(tr1[5] - tr0[5])
         rows.append(row)
         if rank == 0:
             print(f"n={n}", row, flush=True)

@@ -97,5 +97,5 @@ if __name__ == "__main__":
         p.join(timeout=60)
     print(f"cycles {cycles}, per rank (wrong results of call 1, call 2; zero-copy calls; refused imports):",
           [(res[r]["bad"], res[r]["zc"], res[r]["refused"]) for r in range(N)], flush=True)
-for r in range(N):
-    print(f"rank {r} wrong (cycle, call, first wrong element, wrong elements, rbuf):", res[r]["fails"][:12], flush=True)
+    for r in range(N):
+        print(f"rank {r} wrong (cycle, call, first wrong element, wrong elements, rbuf):", res[r]["fails"][:12], flush=True)

@@ -63,10 +63,19 @@ constexpr size_t kCsvArgWords = (sizeof(OneShotArgs) + 7) / 8;
 // breakdown, summed by the host for mx_coll_service_trace
 enum { TK_SEEN, TK_ARGS, TK_CALL, TK_N };
 
-struct alignas(64) CsvCtl {   // coherent mapped host memory, written by the host
-  uint64_t seq;               // command number, raised last (release)
-  uint64_t exit;              // the command is "leave"
-  uint64_t words;             // 8-byte words of the arguments in use (the segments the call has)
+// The command line: one 64-byte line of coherent mapped host memory,
+// written by the host word by word, w[0] (the command number) last with a
+// release.  Every other word carries the low 16 bits of its command number
+// in its top 16 bits (addresses and counts fit in 48), so a line read while
+// the host was still writing it shows a mismatched tag and is read again --
+// the kernel takes a whole call from ONE read of the line (its eight words
+// in flight together) instead of a read for the number and another for the
+// arguments.
+enum { CW_SEQ = 0, CW_SB, CW_RB, CW_COUNT, CW_GEN, CW_FLAGS, CW_N = 8 };
+enum { CF_EXIT = 1, CF_FULL = 2 };   // CW_FLAGS bits; bits 8..23: argument words of a full call
+constexpr uint64_t kCwMask = (1ull << 48) - 1;
+struct alignas(64) CsvCtl {
+  uint64_t w[CW_N];
 };
 struct alignas(64) CsvHost {  // mapped host memory, written by the kernel
   uint64_t done;              // last command completed
@@ -81,57 +90,76 @@ struct alignas(64) CsvHost {  // mapped host memory, written by the kernel
 // calls -- the service never crosses a kernel boundary, and what it reads
 // (sbuf, the peers' words) and writes (rbuf, the peers' LL areas, DONE) all
 // bypass this XCD's L2.
+//
+// Arguments: the kernel keeps one OneShotArgs per generation parity (the
+// peer pointers differ by parity); a call whose arguments differ from the
+// kept ones in more than sbuf, rbuf, count and generation (first call of a
+// parity after a launch, another size's segments) comes as a FULL command
+// and the kernel reads the arguments block first.
 template <class T, class OP>
 __global__ void __launch_bounds__(kOSB) k_csv(const CsvCtl *ctl, const uint64_t *args, CsvHost *host, uint64_t last,
                                               uint64_t epoch, uint64_t idle_ticks, uint64_t life_ticks) {
-  __shared__ OneShotArgs A;
+  __shared__ OneShotArgs A[2];
+  __shared__ uint64_t line[CW_N];
   __shared__ int s_exit;
-  __shared__ uint64_t s_q, s_words;
   __shared__ uint64_t tk[TK_N];
   const int t = threadIdx.x;
   uint64_t seen = last;
   const uint64_t born = wall_clock64();
   if (t == 0) __hip_atomic_store(&host->running, epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
   for (;;) {
-    if (t == 0) {
+    if (t < 64) {   // wave 0 polls the line, lanes 0-7 a word each
       const uint64_t t0 = wall_clock64();
       int ex = 0;
-      uint64_t q = 0;
       for (;;) {
-        q = __hip_atomic_load(&ctl->seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-        if (q > seen) break;
+        const uint64_t w = t < CW_N ? __hip_atomic_load(&ctl->w[t], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) : 0;
+        const uint64_t q = __shfl(w, 0);
+        if (q > seen) {
+          const bool tagged = t == CW_SEQ || t >= CW_N || t > CW_FLAGS || (w >> 48) == (q & 0xffff);
+          if (__all(tagged)) {
+            if (t < CW_N) line[t] = w;
+            break;
+          }
+          continue;   // caught mid-write: read it again
+        }
         const uint64_t now = wall_clock64();
         if (now - t0 > idle_ticks || now - born > life_ticks) { ex = 1; break; }
         __builtin_amdgcn_s_sleep(1);
       }
-      uint64_t words = kCsvArgWords;
-      if (!ex) {
-        // the loads below are issued after `seq` returned (the host wrote
-        // them before it): ordering only, no cache maintenance (they bypass
-        // the L2 like every other access of the service)
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-        if (__hip_atomic_load(&ctl->exit, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM)) ex = 1;
-        words = __hip_atomic_load(&ctl->words, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-        seen = q;
+      if (t == 0) {
+        s_exit = ex || ((line[CW_FLAGS] & CF_EXIT) != 0);
+        if (!ex) seen = line[CW_SEQ];
+        tk[TK_SEEN] = wall_clock64();
       }
-      s_exit = ex;
-      s_q = q;
-      tk[TK_SEEN] = wall_clock64();
-      s_words = words < kCsvArgWords ? words : kCsvArgWords;
+      seen = __shfl(seen, 0);
     }
     __syncthreads();
     if (s_exit) {
       if (t == 0) __hip_atomic_store(&host->left, epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
       return;
     }
-    // the arguments in use: one load per lane, all in flight at once (one
-    // PCIe round trip for up to kOSB words)
-    uint64_t *dst = reinterpret_cast<uint64_t *>(&A);
-    for (size_t i = t; i < s_words; i += kOSB)
-      dst[i] = __hip_atomic_load(args + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    const uint64_t fl = line[CW_FLAGS] & kCwMask;
+    const uint64_t gen = line[CW_GEN] & kCwMask;
+    OneShotArgs &a = A[gen & 1];
+    if (fl & CF_FULL) {   // the arguments block: one load per lane, all in flight at once
+      size_t words = (fl >> 8) & 0xffff;
+      if (words > kCsvArgWords) words = kCsvArgWords;
+      uint64_t *dst = reinterpret_cast<uint64_t *>(&a);
+      for (size_t i = t; i < words; i += kOSB)
+        dst[i] = __hip_atomic_load(args + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      __syncthreads();
+    }
+    if (t == 0) {   // this call's own fields
+      a.sb = reinterpret_cast<const char *>(line[CW_SB] & kCwMask);
+      a.rb = reinterpret_cast<char *>(line[CW_RB] & kCwMask);
+      a.src[a.rank] = a.sb;
+      a.count = line[CW_COUNT] & kCwMask;
+      a.slice = a.count;
+      a.gen = gen;
+      tk[TK_ARGS] = wall_clock64();
+    }
     __syncthreads();
-    if (t == 0) tk[TK_ARGS] = wall_clock64();
-    const bool ok = os_ll<T, OP, true>(A);
+    const bool ok = os_ll<T, OP, true>(a);
     // every lane's result words acknowledged before `done`
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
@@ -142,9 +170,9 @@ __global__ void __launch_bounds__(kOSB) k_csv(const CsvCtl *ctl, const uint64_t 
       for (int k = 1; k < TK_N; k++)
         __hip_atomic_store(&host->last[k], ok ? tk[k] - tk[k - 1] : 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-      __hip_atomic_store(&host->done, s_q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      __hip_atomic_store(&host->done, seen, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     }
-    __syncthreads();   // A and s_* are rewritten next round
+    __syncthreads();   // A, line and s_* are rewritten next round
   }
 }
 
@@ -189,6 +217,9 @@ struct Csv {
   std::vector<csv_launch_fn> started;
   double tick_us = 0.01;         // wall clock period
   double prep_us = 0, wait_us = 0, phase_us[TK_N] = {};   // sums over `served` (mx_coll_service_trace)
+  OneShotArgs kept[2];           // the arguments the kernel of epoch kept_ep[parity] holds
+  uint64_t kept_ep[2] = {0, 0};
+  uint64_t full = 0;             // commands that carried the arguments block
 };
 Csv g_csv;
 std::atomic<int> g_csv_on{-1};
@@ -215,10 +246,49 @@ bool csv_poll(const uint64_t *w, uint64_t target, double us) {
 }
 bool csv_gone(const Csv &v, uint64_t ep) { return __atomic_load_n(&v.host->left, __ATOMIC_ACQUIRE) >= ep; }
 
-uint64_t csv_post(Csv &v, bool exit) {
-  v.ctl->exit = exit ? 1 : 0;
-  const uint64_t q = ++v.seq;
-  __atomic_store_n(&v.ctl->seq, q, __ATOMIC_RELEASE);
+// Writes command v.seq + 1 (a call, or "leave") into the line and raises it.
+// A call carries the arguments block too when the kernel running now does
+// not hold this parity's arguments, or they differ in more than the call's
+// own fields (sbuf, rbuf, count, generation).
+uint64_t csv_post(Csv &v, bool exit, const OneShotArgs *a = nullptr) {
+  const uint64_t q = v.seq + 1;
+  const uint64_t tag = (q & 0xffff) << 48;
+  uint64_t fl = exit ? CF_EXIT : 0, sb = 0, rb = 0, cnt = 0, gen = 0;
+  if (a) {
+    const int par = (int)(a->gen & 1);
+    const size_t used = offsetof(OneShotArgs, seg) + (size_t)a->nseg * sizeof(OsSeg);
+    bool full = v.kept_ep[par] != v.epoch;
+    if (!full) {
+      OneShotArgs cmp;
+      memcpy(&cmp, a, sizeof cmp);
+      const OneShotArgs &k = v.kept[par];
+      cmp.sb = k.sb;
+      cmp.rb = k.rb;
+      cmp.src[a->rank] = k.src[a->rank];
+      cmp.count = k.count;
+      cmp.slice = k.slice;
+      cmp.gen = k.gen;
+      full = memcmp(&cmp, &k, used) != 0;
+    }
+    if (full) {
+      memcpy(v.args, a, used);
+      memcpy(&v.kept[par], a, sizeof *a);
+      v.kept_ep[par] = v.epoch;
+      fl |= CF_FULL | (uint64_t)((used + 7) / 8) << 8;
+      v.full++;
+    }
+    sb = (uint64_t)(uintptr_t)a->sb;
+    rb = (uint64_t)(uintptr_t)a->rb;
+    cnt = a->count;
+    gen = a->gen;
+  }
+  v.ctl->w[CW_SB] = tag | (sb & kCwMask);
+  v.ctl->w[CW_RB] = tag | (rb & kCwMask);
+  v.ctl->w[CW_COUNT] = tag | (cnt & kCwMask);
+  v.ctl->w[CW_GEN] = tag | (gen & kCwMask);
+  v.ctl->w[CW_FLAGS] = tag | fl;
+  v.seq = q;
+  __atomic_store_n(&v.ctl->w[CW_SEQ], q, __ATOMIC_RELEASE);
   return q;
 }
 
@@ -312,7 +382,8 @@ bool csv_start(Csv &v, csv_launch_fn fn) {
 int csv_allreduce(mx_comm *c, const OneShotArgs &a, int op, int type, hipStream_t s) {
   // the tagged-word calls only (one workgroup's work), operands on 4-byte
   // boundaries (the service moves 4-byte words at system scope)
-  if (!csv_enabled() || !c->csv_ok || c->defer || c->poisoned || !a.ll || (((uintptr_t)a.sb | (uintptr_t)a.rb) & 3))
+  if (!csv_enabled() || !c->csv_ok || c->defer || c->poisoned || !a.ll || (((uintptr_t)a.sb | (uintptr_t)a.rb) & 3) ||
+      (((uintptr_t)a.sb | (uintptr_t)a.rb | a.count | a.gen) >> 48))   // (the line's 48-bit fields)
     return 0;
   const auto t_in = std::chrono::steady_clock::now();
   CsvVisitor vis;
@@ -334,12 +405,8 @@ int csv_allreduce(mx_comm *c, const OneShotArgs &a, int op, int type, hipStream_
     v.type = type;
     if (!csv_start(v, fn)) return 0;
   }
-  // only the segments the call has travel (the kernel reads `words` of them)
-  const size_t used = offsetof(OneShotArgs, seg) + (size_t)a.nseg * sizeof(OsSeg);
-  memcpy(v.args, &a, used);
-  v.ctl->words = (used + 7) / 8;
   const auto t_post = std::chrono::steady_clock::now();
-  uint64_t q = csv_post(v, false);
+  uint64_t q = csv_post(v, false, &a);
   for (unsigned k = 0;; k++) {
     if (__atomic_load_n(&v.host->done, __ATOMIC_ACQUIRE) >= q) {
       const auto t_done = std::chrono::steady_clock::now();
@@ -366,7 +433,7 @@ int csv_allreduce(mx_comm *c, const OneShotArgs &a, int op, int type, hipStream_
       }
       v.live = false;
       if (!csv_start(v, fn)) return 0;
-      q = csv_post(v, false);
+      q = csv_post(v, false, &a);
     }
     if ((k & 0xfffff) == 0xfffff) {
       const hipError_t e = hipStreamQuery(v.s);
@@ -404,9 +471,9 @@ extern "C" int mx_coll_service_trace(double *out, int n) {
   mx::Csv &v = mx::g_csv;
   std::lock_guard<std::mutex> lk(v.mu);
   const double d = v.served ? (double)v.served : 1.0;
-  const double t[5] = {(double)v.served, v.prep_us / d, v.wait_us / d, v.phase_us[mx::TK_ARGS] / d,
-                       v.phase_us[mx::TK_CALL] / d};
-  for (int i = 0; i < n && i < 5; i++) out[i] = t[i];
+  const double t[6] = {(double)v.served, v.prep_us / d, v.wait_us / d, v.phase_us[mx::TK_ARGS] / d,
+                       v.phase_us[mx::TK_CALL] / d, (double)v.full};
+  for (int i = 0; i < n && i < 6; i++) out[i] = t[i];
   return v.state;
 }
 
