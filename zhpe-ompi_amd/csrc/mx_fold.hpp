@@ -266,6 +266,7 @@ __device__ bool os_ll(const OneShotArgs &a) {
   // lane t's gathered words, [f * kOSB + t]: at most (MAXR - 1) peers x
   // OS_LL_MAX / 4 / kOSB words = 60 per lane
   __shared__ uint32_t col[(MAXR - 1) * (OS_LL_MAX / 4 / kOSB) * kOSB];
+  __shared__ uint32_t mine[OS_LL_MAX / 4];   // my words, for the fold
   __shared__ int s_bad;
   const int t = threadIdx.x, n = a.n, r = a.rank;
   const uint32_t g = (uint32_t)a.gen;
@@ -279,19 +280,32 @@ __device__ bool os_ll(const OneShotArgs &a) {
   if (t == 0) s_bad = poisoned(a.poison);
   __syncthreads();
   if (s_bad) return false;
-  // (2) my words, tagged, into every peer's LL area
+  // (2) my words (at most MW per lane, all loads in flight at once), tagged,
+  // into every peer's LL area, and into LDS for my own operand of the fold
+  constexpr int MW = (int)(OS_LL_MAX / 4 / kOSB);
   const size_t nw = a.count * W;
   const bool al = ((uintptr_t)a.sb & 3) == 0;
   const uint32_t *sw = reinterpret_cast<const uint32_t *>(a.sb);
-  for (size_t i = t; i < nw; i += kOSB) {
-    uint32_t v;
-    if (SYS) v = __hip_atomic_load(sw + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-    else if (al) v = sw[i];
-    else __builtin_memcpy(&v, a.sb + 4 * i, 4);
-    for (int p = 0; p < n; p++)
-      if (p != r)
-        __hip_atomic_store(reinterpret_cast<uint64_t *>(a.peer_slot[p]) + i, tag | v, __ATOMIC_RELAXED,
-                           __HIP_MEMORY_SCOPE_SYSTEM);
+  uint32_t mv[MW];
+#pragma unroll
+  for (int u = 0; u < MW; u++) {
+    const size_t i = (size_t)t + (size_t)u * kOSB;
+    if (i < nw) {
+      if (SYS) mv[u] = __hip_atomic_load(sw + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      else if (al) mv[u] = sw[i];
+      else __builtin_memcpy(&mv[u], a.sb + 4 * i, 4);
+    }
+  }
+#pragma unroll
+  for (int u = 0; u < MW; u++) {
+    const size_t i = (size_t)t + (size_t)u * kOSB;
+    if (i < nw) {
+      mine[i] = mv[u];
+      for (int p = 0; p < n; p++)
+        if (p != r)
+          __hip_atomic_store(reinterpret_cast<uint64_t *>(a.peer_slot[p]) + i, tag | mv[u], __ATOMIC_RELAXED,
+                             __HIP_MEMORY_SCOPE_SYSTEM);
+    }
   }
   // (3) gather: lane t's words of every peer -- E elements (t, t + kOSB, ...)
   // of W words each -- flattened as f = (peer * E + i) * W + k and loaded
@@ -316,20 +330,26 @@ __device__ bool os_ll(const OneShotArgs &a) {
         }
       }
     }
+    // words not yet of this generation are loaded again, all together
+    for (;;) {
+      bool all = true;
 #pragma unroll
-    for (int u = 0; u < 8; u++) {
-      if (!ad[u]) continue;
-      while ((uint32_t)(v[u] >> 32) != g && !bad) {
-        __builtin_amdgcn_s_sleep(1);
-        if (wall_clock64() - t0 > a.timeout_ticks) {
-          raise_timeout(a.err, a.poison);
-          bad = true;
-        } else {
-          v[u] = ll_ld(ad[u]);
-        }
+      for (int u = 0; u < 8; u++)
+        if (ad[u] && (uint32_t)(v[u] >> 32) != g) all = false;
+      if (all) break;
+      __builtin_amdgcn_s_sleep(1);
+      if (wall_clock64() - t0 > a.timeout_ticks) {
+        raise_timeout(a.err, a.poison);
+        bad = true;
+        break;
       }
-      col[(f0 + u) * kOSB + t] = (uint32_t)v[u];
+#pragma unroll
+      for (int u = 0; u < 8; u++)
+        if (ad[u] && (uint32_t)(v[u] >> 32) != g) v[u] = ll_ld(ad[u]);
     }
+#pragma unroll
+    for (int u = 0; u < 8; u++)
+      if (ad[u]) col[(f0 + u) * kOSB + t] = (uint32_t)v[u];
   }
   if (bad) s_bad = 1;
   __syncthreads();
@@ -348,14 +368,11 @@ __device__ bool os_ll(const OneShotArgs &a) {
         const int jj = j < r ? j : j - 1;
 #pragma unroll
         for (int k = 0; k < W; k++) u[k] = col[((jj * E + ii) * W + k) * kOSB + t];
-        __builtin_memcpy(&x, u, sizeof(T));
-      } else if (SYS) {
-#pragma unroll
-        for (int k = 0; k < W; k++) u[k] = __hip_atomic_load(sw + e * W + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-        __builtin_memcpy(&x, u, sizeof(T));
       } else {
-        x = *reinterpret_cast<const T *>(a.sb + off);
+#pragma unroll
+        for (int k = 0; k < W; k++) u[k] = mine[e * W + k];
       }
+      __builtin_memcpy(&x, u, sizeof(T));
       return x;
     });
     if (SYS) {
