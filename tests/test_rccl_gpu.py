@@ -1,5 +1,7 @@
-"""The RCCL data path of mx_allreduce (MX_ALLREDUCE_RCCL, algorithm id 100;
-bench.py's opt-in `MX_BENCH_RCCL=1` leg).
+"""The RCCL data path of mx_allreduce (MX_ALLREDUCE_RCCL, algorithm id 100).
+bench.py's N>1 run times ncclAllReduce on its own RCCL communicator whenever
+every rank has a GPU of its own (`rccl_leg`, checked against the oracle under
+the reduction-order bound of `order_bound_check`, tests/test_bench_tolerance.py).
 
 RCCL refuses two ranks on one GPU, and the test pool has one GPU per box, so
 this covers what one GPU can: communicator creation with MX_COMM_RCCL
