@@ -214,9 +214,10 @@ int mx_coll_service_set(int on);
 /* Where a served call's time goes, means over the served calls (microseconds):
  * out[0] calls, [1] host preparation, [2] host wait from the post to `done`,
  * and the kernel's phases [3] arguments (the command line, and the
- * arguments block when the call carried it), [4] the call (push, gather,
- * fold, DONE, result words acknowledged); [5] commands that carried the
- * arguments block (a count).  Fills min(n, 6) entries. */
+ * arguments block when the call carried it), [4] the peers' gen-2 check,
+ * [5] the push issued, [6] the gather of the peers' words, [7] the fold,
+ * [8] DONE and the result words acknowledged; [9] commands that carried the
+ * arguments block (a count).  Fills min(n, 10) entries. */
 int mx_coll_service_trace(double *out, int n);
 int mx_comm_set_profiling(mx_comm_t *comm, int on);
 int mx_comm_get_stats(mx_comm_t *comm, mx_coll_stats_t *stats, int reset);

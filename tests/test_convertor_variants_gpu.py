@@ -105,7 +105,10 @@ def _run_all(cases):
 
 BMAP_SWITCHES = ["MX_CONV_BMAP_SPAN=12288", "MX_CONV_BMAP_SPAN=24576", "MX_CONV_BMAP_UNROLL=0", "MX_CONV_BMAP_QUAD=0",
                  "MX_CONV_BMAP_WORD=1", "MX_CONV_BMAP_NT=0", "MX_CONV_BMAP_DW=0", "MX_CONV_BMAP_CW=0",
-                 "MX_NT_MIN_BYTES=0 MX_CONV_UNPACK_NTLD=1", "MX_CONV_UNPACK_U32=0", "MX_CONV_BMAP_INST=0"]
+                 "MX_NT_MIN_BYTES=0 MX_CONV_UNPACK_NTLD=1", "MX_CONV_BMAP_INST=0",
+                 # the piece unpack forms (by default measured per datatype: staged or one piece per lane)
+                 "MX_CONV_UNPACK_DIRECT=0", "MX_CONV_UNPACK_DIRECT=1", "MX_CONV_UNPACK_DIRECT=0 MX_CONV_UNPACK_U32=0",
+                 "MX_CONV_UNPACK_DIRECT=0 MX_NT_MIN_BYTES=0 MX_CONV_UNPACK_NTLD=1"]
 
 
 def test_byte_map_pack_switches():

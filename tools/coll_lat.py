@@ -55,8 +55,8 @@ def worker(rank, n, port, q, sizes):
             for _ in range(50):
                 comm.allreduce(x.data_ptr(), y.data_ptr(), cnt, "FLOAT", "SUM", "auto", st)
             dist.barrier()
-            tr0 = (ctypes.c_double * 6)()
-            L.mx_coll_service_trace(tr0, 6)
+            tr0 = (ctypes.c_double * 10)()
+            L.mx_coll_service_trace(tr0, 10)
             ts = []
             for _ in range(ITERS):
                 t0 = time.perf_counter()
@@ -74,8 +74,8 @@ def worker(rank, n, port, q, sizes):
                 rc = fn(*args)
                 ta.append(time.perf_counter() - t0)
                 assert rc == 0, rc
-            tr1 = (ctypes.c_double * 6)()
-            L.mx_coll_service_trace(tr1, 6)
+            tr1 = (ctypes.c_double * 10)()
+            L.mx_coll_service_trace(tr1, 10)
             med = torch.tensor([sorted(ts)[len(ts) // 2] * 1e6, sorted(ta)[len(ta) // 2] * 1e6])
             dist.all_reduce(med, op=dist.ReduceOp.MAX)
             row[mode] = round(float(med[0]), 2)
@@ -85,10 +85,10 @@ def worker(rank, n, port, q, sizes):
                 k = tr1[0] - tr0[0]
                 row["served"] = int(k)
                 if k > 0:
-                    names = ("prep", "wait", "k_args", "k_call")
+                    names = ("prep", "wait", "k_args", "k_dchk", "k_push", "k_gather", "k_fold", "k_ack")
                     row["trace_us"] = {nm: round((tr1[i + 1] * tr1[0] - tr0[i + 1] * tr0[0]) / k, 2)
                                        for i, nm in enumerate(names)}
-                    row["full_commands"] = int(tr1[5] - tr0[5])
+                    row["full_commands"] = int(tr1[9] - tr0[9])
         rows.append(row)
         if rank == 0:
             print(f"n={n}", row, flush=True)

@@ -61,7 +61,7 @@ constexpr size_t kCsvArgWords = (sizeof(OneShotArgs) + 7) / 8;
 
 // per-call phase stamps (wall clock ticks, thread 0): the service's own
 // breakdown, summed by the host for mx_coll_service_trace
-enum { TK_SEEN, TK_ARGS, TK_CALL, TK_N };
+enum { TK_SEEN, TK_ARGS, TK_DCHK, TK_PUSH, TK_GATH, TK_FOLD, TK_CALL, TK_N };
 
 // The command line: one 64-byte line of coherent mapped host memory,
 // written by the host word by word, w[0] (the command number) last with a
@@ -159,7 +159,7 @@ __global__ void __launch_bounds__(kOSB) k_csv(const CsvCtl *ctl, const uint64_t 
       tk[TK_ARGS] = wall_clock64();
     }
     __syncthreads();
-    const bool ok = os_ll<T, OP, true>(a);
+    const bool ok = os_ll<T, OP, true>(a, &tk[TK_DCHK]);
     // every lane's result words acknowledged before `done`
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
@@ -471,9 +471,17 @@ extern "C" int mx_coll_service_trace(double *out, int n) {
   mx::Csv &v = mx::g_csv;
   std::lock_guard<std::mutex> lk(v.mu);
   const double d = v.served ? (double)v.served : 1.0;
-  const double t[6] = {(double)v.served, v.prep_us / d, v.wait_us / d, v.phase_us[mx::TK_ARGS] / d,
-                       v.phase_us[mx::TK_CALL] / d, (double)v.full};
-  for (int i = 0; i < n && i < 6; i++) out[i] = t[i];
+  const double t[10] = {(double)v.served,
+                        v.prep_us / d,
+                        v.wait_us / d,
+                        v.phase_us[mx::TK_ARGS] / d,
+                        v.phase_us[mx::TK_DCHK] / d,
+                        v.phase_us[mx::TK_PUSH] / d,
+                        v.phase_us[mx::TK_GATH] / d,
+                        v.phase_us[mx::TK_FOLD] / d,
+                        v.phase_us[mx::TK_CALL] / d,
+                        (double)v.full};
+  for (int i = 0; i < n && i < 10; i++) out[i] = t[i];
   return v.state;
 }
 

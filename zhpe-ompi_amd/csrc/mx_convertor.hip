@@ -25,6 +25,7 @@
 #include <algorithm>
 #include <mutex>
 #include <atomic>
+#include <type_traits>
 
 #include "mx_internal.h"
 #include "mx_mem.hpp"
@@ -116,12 +117,6 @@ __device__ __forceinline__ void next_block(Pos &P, const DRun *runs, int nruns, 
   }
 }
 
-__device__ __forceinline__ const DRun *stage_runs(const ConvArgs &a, DRun *sruns) {
-  if (a.nruns > kLdsRuns) return a.runs;
-  for (int i = threadIdx.x; i < a.nruns; i += kCB) sruns[i] = a.runs[i];
-  __syncthreads();
-  return sruns;
-}
 
 template <int UNIT> struct unit_t;
 template <> struct unit_t<16> { using T = uint4; };
@@ -160,6 +155,36 @@ __device__ __forceinline__ W4 gld16a4(const char *p) {         // 4-byte aligned
 __device__ __forceinline__ uint32_t gld4(const char *p) {
   return *(const __attribute__((address_space(1))) uint32_t *)(p);
 }
+// ... and stores / loads of any unit the same way (16-byte units as a plain
+// vector: HIP's vector classes have no address-space-1 assignment)
+template <class U>
+__device__ __forceinline__ U gload(const char *p) {
+  if constexpr (sizeof(U) == 16) {
+    const v4u_a16 v = *(const __attribute__((address_space(1))) v4u_a16 *)(p);
+    U r;
+    __builtin_memcpy(&r, &v, 16);
+    return r;
+  } else if constexpr (std::is_scalar<U>::value) {
+    return *(const __attribute__((address_space(1))) U *)(p);
+  } else {   // a small struct: as the unsigned integer of its size
+    static_assert(sizeof(U) == 8 || sizeof(U) == 4, "gload: 4, 8 or 16 bytes");
+    using I = typename std::conditional<sizeof(U) == 8, uint64_t, uint32_t>::type;
+    const I v = *(const __attribute__((address_space(1))) I *)(p);
+    U r;
+    __builtin_memcpy(&r, &v, sizeof(U));
+    return r;
+  }
+}
+template <class U>
+__device__ __forceinline__ void gstore(char *p, const U &x) {
+  if constexpr (sizeof(U) == 16) {
+    v4u_a16 v;
+    __builtin_memcpy(&v, &x, 16);
+    *(__attribute__((address_space(1))) v4u_a16 *)(p) = v;
+  } else {
+    *(__attribute__((address_space(1))) U *)(p) = x;
+  }
+}
 
 // ---------------------------------------------------------------------------
 // GRANULE kernel: one lane = one 16-byte granule of the packed buffer
@@ -183,20 +208,20 @@ __device__ __forceinline__ void convert_granule(const ConvArgs &a, const DRun *r
   U regs[K];
   if (!PACK) {
     if (full) {
-      const uint4 v = a.ntld ? gld16p<true>(a.packed + rel0) : *reinterpret_cast<const uint4 *>(a.packed + rel0);
+      const uint4 v = a.ntld ? gld16p<true>(a.packed + rel0) : gld16(a.packed + rel0);
       memcpy(regs, &v, 16);
     } else {
 #pragma unroll
       for (int k = 0; k < K; k++)
-        if ((uint64_t)k * UNIT < n) regs[k] = *reinterpret_cast<const U *>(a.packed + rel0 + k * UNIT);
+        if ((uint64_t)k * UNIT < n) regs[k] = gload<U>(a.packed + rel0 + k * UNIT);
     }
   }
 #pragma unroll
   for (int k = 0; k < K; k++) {
     if ((uint64_t)k * UNIT < n) {
       char *p = a.user + block_addr(P, R, a.ext) + P.o;
-      if (PACK) regs[k] = *reinterpret_cast<const U *>(p);
-      else *reinterpret_cast<U *>(p) = regs[k];
+      if (PACK) regs[k] = gload<U>(p);
+      else gstore<U>(p, regs[k]);
       P.o += UNIT;
       if (P.o == R.blen) next_block(P, runs, a.nruns, R);
     }
@@ -205,20 +230,33 @@ __device__ __forceinline__ void convert_granule(const ConvArgs &a, const DRun *r
     if (full) {
       uint4 v;
       memcpy(&v, regs, 16);
-      *reinterpret_cast<uint4 *>(a.packed + rel0) = v;
+      gstore<uint4>(a.packed + rel0, v);
     } else {
 #pragma unroll
       for (int k = 0; k < K; k++)
-        if ((uint64_t)k * UNIT < n) *reinterpret_cast<U *>(a.packed + rel0 + k * UNIT) = regs[k];
+        if ((uint64_t)k * UNIT < n) gstore<U>(a.packed + rel0 + k * UNIT, regs[k]);
     }
   }
 }
 
-template <int UNIT, bool PACK>
+// RL: the run table staged in LDS (a.nruns <= kLdsRuns), read through the LDS
+// array itself -- a pointer that may point at either memory is generic, and
+// its flat loads would tie LDS waits to the global accesses in flight
+template <int UNIT, bool PACK, bool RL>
 __global__ void __launch_bounds__(kCB) k_convert(ConvArgs a) {
   extern __shared__ DRun sruns[];
-  const DRun *runs = stage_runs(a, sruns);
-  convert_granule<UNIT, PACK>(a, runs, (uint64_t)blockIdx.x * kCB + threadIdx.x);
+  const uint64_t g = (uint64_t)blockIdx.x * kCB + threadIdx.x;
+  if constexpr (RL) {
+    static_assert(sizeof(DRun) % 8 == 0, "DRun is copied as 8-byte words");
+    uint64_t *d = reinterpret_cast<uint64_t *>(sruns);
+    const char *src = reinterpret_cast<const char *>(a.runs);
+    for (uint32_t i = threadIdx.x; i < (uint32_t)a.nruns * (sizeof(DRun) / 8); i += kCB)
+      d[i] = gload<uint64_t>(src + 8 * (size_t)i);
+    __syncthreads();
+    convert_granule<UNIT, PACK>(a, sruns, g);
+  } else {
+    convert_granule<UNIT, PACK>(a, a.runs, g);
+  }
 }
 
 // ---------------------------------------------------------------------------
@@ -963,12 +1001,12 @@ struct PieceArgs {
 };
 
 __device__ __forceinline__ void piece_store(char *u, int lg, uint32_t v0, uint32_t v1, uint32_t v2, uint32_t v3) {
-  switch (lg) {
-    case 0: *reinterpret_cast<uint8_t *>(u) = (uint8_t)v0; break;
-    case 1: *reinterpret_cast<uint16_t *>(u) = (uint16_t)v0; break;
-    case 2: *reinterpret_cast<uint32_t *>(u) = v0; break;
-    case 3: *reinterpret_cast<uint2 *>(u) = make_uint2(v0, v1); break;
-    default: *reinterpret_cast<uint4 *>(u) = make_uint4(v0, v1, v2, v3); break;
+  switch (lg) {   // (global stores: gstore)
+    case 0: gstore<uint8_t>(u, (uint8_t)v0); break;
+    case 1: gstore<uint16_t>(u, (uint16_t)v0); break;
+    case 2: gstore<uint32_t>(u, v0); break;
+    case 3: gstore<uint64_t>(u, (uint64_t)v0 | ((uint64_t)v1 << 32)); break;
+    default: gstore<uint4>(u, make_uint4(v0, v1, v2, v3)); break;
   }
 }
 
@@ -979,17 +1017,25 @@ __device__ __forceinline__ void piece_store(char *u, int lg, uint32_t v0, uint32
 // 1577 us, struct 949 -> 1071 us): the unpack is bound by its partial-line
 // stores, and loads kept in flight beside them only compete (64 more VGPRs
 // per lane, fewer waves); so it is off (MX_CONV_UNPACK_PIPE=1 turns it on).
-template <bool PIPE>
+template <bool PIPE, bool TL>
 __global__ void __launch_bounds__(kCB) k_unpack_piece(PieceArgs a) {
   extern __shared__ __align__(16) char smem[];
   char *stage = smem;                                        // kPieceStage + 48
   DPiece *stbl = reinterpret_cast<DPiece *>(smem + kPieceStage + 48);
-  const DPiece *tbl = a.pieces;
-  if (a.tbl_lds) {
-    for (uint32_t i = threadIdx.x; i < a.npi; i += kCB) stbl[i] = a.pieces[i];
-    tbl = stbl;
+  if (TL) {
+    for (uint32_t i = threadIdx.x; i < a.npi; i += kCB) stbl[i] = gload<DPiece>(reinterpret_cast<const char *>(a.pieces + i));
     __syncthreads();
   }
+  // the piece table from LDS (TL: a.tbl_lds) or from global memory, each
+  // through a pointer of its own address space (one that may be either is
+  // generic: flat loads, whose waits also wait for the stores in flight)
+  auto piece_at = [&](uint64_t k) -> DPiece {
+    if constexpr (TL) {
+      return stbl[k];
+    } else {
+      return gload<DPiece>(reinterpret_cast<const char *>(a.pieces + k));
+    }
+  };
   const uint64_t wend = a.offset + a.len;
   // stream range of tile t: first byte of piece Pa .. last byte of Pb - 1,
   // as 16-byte aligned addresses of the packed buffer
@@ -997,7 +1043,7 @@ __global__ void __launch_bounds__(kCB) k_unpack_piece(PieceArgs a) {
     const uint64_t Pa = a.P0 + t * a.K;
     const uint64_t Pb = Pa + a.K < a.P1 ? Pa + a.K : a.P1;
     const uint64_t ia = udiv(Pa, a.mnpi), ib = udiv(Pb - 1, a.mnpi);
-    const DPiece fa = tbl[Pa - ia * a.npi], fb = tbl[Pb - 1 - ib * a.npi];
+    const DPiece fa = piece_at(Pa - ia * a.npi), fb = piece_at(Pb - 1 - ib * a.npi);
     uint64_t sa = ia * a.S + fa.soff, sb = ib * a.S + fb.soff + (1u << fb.lg);
     sa = sa < a.offset ? a.offset : sa;
     sb = sb < wend ? sb : wend;
@@ -1023,7 +1069,7 @@ __global__ void __launch_bounds__(kCB) k_unpack_piece(PieceArgs a) {
     const int64_t dE = (int64_t)a.dinst * a.ext;
     const uint32_t iters = (uint32_t)((Pb - P + kCB - 1) / kCB);
     for (uint32_t it = 0; it < iters; it++) {
-      const DPiece pc = tbl[j];
+      const DPiece pc = piece_at(j);
       const int32_t li = ib + (int32_t)pc.soff;
       const int32_t n = 1 << pc.lg;
       char *u = ub + pc.uoff;
@@ -1035,7 +1081,7 @@ __global__ void __launch_bounds__(kCB) k_unpack_piece(PieceArgs a) {
                     __builtin_amdgcn_alignbyte(x3, x2, sh), __builtin_amdgcn_alignbyte(x4, x3, sh));
       } else {                                                // piece cut by the window
         for (int32_t i = 0; i < n; i++)
-          if (li + i >= wlo && li + i < whi) u[i] = stage[li + i];
+          if (li + i >= wlo && li + i < whi) *gp(u + i) = stage[li + i];
       }
       j += a.dj;
       ib += dS;
@@ -1054,7 +1100,7 @@ __global__ void __launch_bounds__(kCB) k_unpack_piece(PieceArgs a) {
     uint64_t inst = udiv(P, a.mnpi);
     uint32_t j = (uint32_t)(P - inst * a.npi);
     for (; P < Pb; P += kCB) {
-      const DPiece pc = tbl[j];
+      const DPiece pc = piece_at(j);
       const uint64_t sp = inst * a.S + pc.soff;
       const uint32_t n = 1u << pc.lg;
       char *u = a.user + (int64_t)inst * a.ext + pc.uoff;
@@ -1067,7 +1113,7 @@ __global__ void __launch_bounds__(kCB) k_unpack_piece(PieceArgs a) {
                     __builtin_amdgcn_alignbyte(w3, w2, sh), __builtin_amdgcn_alignbyte(w4, w3, sh));
       } else {                                                // piece cut by the window
         for (uint32_t i = 0; i < n; i++)
-          if (sp + i >= a.offset && sp + i < wend) u[i] = stage[li + i];
+          if (sp + i >= a.offset && sp + i < wend) *gp(u + i) = stage[li + i];
       }
       j += a.dj;
       inst += a.dinst;
@@ -1086,7 +1132,7 @@ __global__ void __launch_bounds__(kCB) k_unpack_piece(PieceArgs a) {
         if (a.ntld)
           for (uint32_t i = threadIdx.x; i < nv; i += kCB) d[i] = gld16p<true>(reinterpret_cast<const char *>(g + i));
         else
-          for (uint32_t i = threadIdx.x; i < nv; i += kCB) d[i] = g[i];
+          for (uint32_t i = threadIdx.x; i < nv; i += kCB) d[i] = gld16(reinterpret_cast<const char *>(g + i));
       }
       __syncthreads();
       store_tile(t, lo);
@@ -1126,6 +1172,50 @@ __global__ void __launch_bounds__(kCB) k_unpack_piece(PieceArgs a) {
       t = tn;
       lo = nlo;
     }
+  }
+}
+
+// UNPACK, pieces, one piece per lane (round 6): lane P stores piece P of the
+// window straight from the packed stream -- the one or two aligned 16-byte
+// granules holding its bytes, loaded by the lane itself (the L2 merges the
+// neighbours' overlapping loads) -- with no tile staging, no barrier and no
+// persistent loop: the form of tools/pattern_floor_probe's `piece_ld2`,
+// which runs at the layout's read + store floor.  Pieces cut
+// by the window's ends move byte by byte.
+template <bool NTLD>
+__global__ void __launch_bounds__(kCB) k_unpack_piece_direct(PieceArgs a) {
+  const uint64_t P = a.P0 + (uint64_t)blockIdx.x * kCB + threadIdx.x;
+  if (P >= a.P1) return;
+  const uint64_t inst = udiv(P, a.mnpi);
+  const DPiece pc = gload<DPiece>(reinterpret_cast<const char *>(a.pieces + (P - inst * a.npi)));
+  const uint64_t sp = inst * a.S + pc.soff;            // stream offset of the piece
+  const uint32_t n = 1u << pc.lg;
+  char *u = a.user + (int64_t)inst * a.ext + pc.uoff;
+  const uint64_t wend = a.offset + a.len;
+  if (sp >= a.offset && sp + n <= wend) {
+    const uintptr_t src = (uintptr_t)(a.packed + (sp - a.offset));
+    const char *g = reinterpret_cast<const char *>(src & ~(uintptr_t)15);
+    const uint32_t sh = (uint32_t)(src & 15);
+    // (a granule holding a byte of the window lies inside its 4 KiB page)
+    const uint4 A = gld16p<NTLD>(g);
+    const uint4 B = sh + n > 16 ? gld16p<NTLD>(g + 16) : make_uint4(0, 0, 0, 0);
+    const uint32_t w[8] = {A.x, A.y, A.z, A.w, B.x, B.y, B.z, B.w};
+    const uint32_t q = sh >> 2, r = sh & 3;
+    uint32_t o[4];
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+      uint32_t lo = 0, hi = 0;
+#pragma unroll
+      for (int i = 0; i < 8; i++) {   // w[q + k], w[q + k + 1] by selects (no indexed registers)
+        lo = (uint32_t)i == q + k ? w[i] : lo;
+        hi = (uint32_t)i == q + k + 1 ? w[i] : hi;
+      }
+      o[k] = __builtin_amdgcn_alignbyte(hi, lo, r);
+    }
+    piece_store(u, pc.lg, o[0], o[1], o[2], o[3]);
+  } else {                                             // piece cut by the window
+    for (uint32_t i = 0; i < n; i++)
+      if (sp + i >= a.offset && sp + i < wend) u[i] = a.packed[sp + i - a.offset];
   }
 }
 
@@ -1793,6 +1883,18 @@ struct mx_ddt {
     uint32_t K = 0;                // pieces per tile
     int built = 0;                 // 1 ok, -1 not applicable
   } ptab[16];
+  // UNPACK through piece tables: the LDS-staged tile kernel or one piece per
+  // lane, chosen per datatype by measurement (round 6: one piece per lane is
+  // 0.83x the staged kernel's time for BLACS and 1.4-1.6x for `ref_struct` /
+  // `ref_strange`, profiles/r06/unpack_direct_ab_r6x.txt).  The first two
+  // unpacks of >= 4 MiB run one form each between HIP events; once both
+  // have completed, the faster per byte is kept (0 undecided, 1 staged,
+  // 2 one piece per lane).  Both forms write the same bytes.
+  std::mutex up_mu;
+  int up_choice = 0;
+  int up_tried = 0;                // bit v: form v + 1 launched with events
+  hipEvent_t up_ev[2][2] = {{nullptr, nullptr}, {nullptr, nullptr}};
+  double up_bytes[2] = {0, 0};
   // contiguous user blocks of one instance in stream order + tfirst (BLOCK
   // kernels k_convert_blk), built on first use for instances the byte map
   // does not take
@@ -2349,6 +2451,9 @@ extern "C" int mx_ddt_destroy(mx_ddt_t *d) {
     if (P.dev) release_later(P.dev, REL_DEV);
   if (d->btab.dev) release_later(d->btab.dev, REL_DEV);
   if (d->btab.tfirst) release_later(d->btab.tfirst, REL_DEV);
+  for (auto &e : d->up_ev)
+    for (hipEvent_t ev : e)
+      if (ev) (void)hipEventDestroy(ev);
   delete d;
   return MX_SUCCESS;
 }
@@ -2584,6 +2689,57 @@ static bool conv_unpack_pipe() {
   return on != 0;
 }
 
+// The piece UNPACK form: MX_CONV_UNPACK_DIRECT=0 always the LDS-staged tile
+// kernel, =1 always one piece per lane, unset: measured per datatype
+// (mx_ddt::up_choice).  Results are identical.
+static int conv_unpack_direct() {
+  static const int v = [] {
+    const char *e = getenv("MX_CONV_UNPACK_DIRECT");
+    return (e && *e == '0') ? 1 : (e && *e == '1') ? 2 : 0;
+  }();
+  return v;
+}
+
+// The form of this piece unpack (1 staged, 2 one piece per lane) and, during
+// the trials, the events to bracket it with (null otherwise).
+static int unpack_piece_form(mx_ddt *dm, uint64_t len, hipEvent_t *ev0, hipEvent_t *ev1) {
+  *ev0 = *ev1 = nullptr;
+  if (const int f = conv_unpack_direct()) return f;
+  std::lock_guard<std::mutex> lk(dm->up_mu);
+  if (dm->up_choice) return dm->up_choice;
+  if (len < ((uint64_t)4 << 20)) return 1;
+  for (int v = 0; v < 2; v++) {
+    if (dm->up_tried & (1 << v)) continue;
+    for (int k = 0; k < 2; k++)
+      if (!dm->up_ev[v][k] && hipEventCreate(&dm->up_ev[v][k]) != hipSuccess) {
+        (void)hipGetLastError();
+        dm->up_choice = 1;   // no events: keep the staged form
+        return 1;
+      }
+    dm->up_tried |= 1 << v;
+    dm->up_bytes[v] = (double)len;
+    *ev0 = dm->up_ev[v][0];
+    *ev1 = dm->up_ev[v][1];
+    return v + 1;
+  }
+  // both tried: decide once both have completed (never waits)
+  float ms[2];
+  for (int v = 0; v < 2; v++) {
+    const hipError_t e = hipEventQuery(dm->up_ev[v][1]);
+    if (e == hipErrorNotReady) {
+      (void)hipGetLastError();
+      return 1;
+    }
+    if (e != hipSuccess || hipEventElapsedTime(&ms[v], dm->up_ev[v][0], dm->up_ev[v][1]) != hipSuccess) {
+      (void)hipGetLastError();
+      dm->up_choice = 1;
+      return 1;
+    }
+  }
+  dm->up_choice = ms[1] / dm->up_bytes[1] < ms[0] / dm->up_bytes[0] ? 2 : 1;
+  return dm->up_choice;
+}
+
 // MX_CONV_VEC_SPAN=0 packs periodic small-block vectors through the VEC
 // kernel instead of k_pack_vec_span (A/B switch; results are identical).
 static bool conv_vec_span() {
@@ -2752,7 +2908,8 @@ static int convert(const mx_ddt_t *d, size_t count, char *user, char *packed, si
   if (u == 16) {
     dm->last_path.store(3, std::memory_order_relaxed);
     const uint64_t g = (len + 15) / 16;
-    hipLaunchKernelGGL((k_convert<16, PACK>), dim3((unsigned)((g + kCB - 1) / kCB)), dim3(kCB), run_lds, s, a);
+    if (run_lds) hipLaunchKernelGGL((k_convert<16, PACK, true>), dim3((unsigned)((g + kCB - 1) / kCB)), dim3(kCB), run_lds, s, a);
+    else hipLaunchKernelGGL((k_convert<16, PACK, false>), dim3((unsigned)((g + kCB - 1) / kCB)), dim3(kCB), 0, s, a);
     return mx_check_launch();
   }
   // small irregular instances: byte-map PACK / piece UNPACK (see the kernels)
@@ -2858,10 +3015,26 @@ static int convert(const mx_ddt_t *d, size_t count, char *user, char *packed, si
         const uint64_t per_cu = std::max<uint64_t>(1, std::min<uint64_t>(8, (160 * 1024) / lds));
         const uint64_t grid = std::min<uint64_t>(p.ntiles, (uint64_t)g_num_cus * per_cu);
         dm->last_path.store(5, std::memory_order_relaxed);
+        const uint64_t npieces = p.P1 - p.P0;
+        hipEvent_t ev0 = nullptr, ev1 = nullptr;
+        const int form = PACK ? 1 : unpack_piece_form(dm, len, &ev0, &ev1);
+        if (ev0 && hipEventRecord(ev0, s) != hipSuccess) (void)hipGetLastError();
         if (PACK) hipLaunchKernelGGL(k_pack_piece, dim3((unsigned)grid), dim3(kCB), lds, s, p);
-        else if (conv_unpack_pipe()) hipLaunchKernelGGL(k_unpack_piece<true>, dim3((unsigned)grid), dim3(kCB), lds, s, p);
-        else hipLaunchKernelGGL(k_unpack_piece<false>, dim3((unsigned)grid), dim3(kCB), lds, s, p);
-        return mx_check_launch();
+        else if (form == 2 && npieces <= (uint64_t)UINT32_MAX * kCB) {
+          const unsigned g2 = (unsigned)((npieces + kCB - 1) / kCB);
+          if (p.ntld) hipLaunchKernelGGL(k_unpack_piece_direct<true>, dim3(g2), dim3(kCB), 0, s, p);
+          else hipLaunchKernelGGL(k_unpack_piece_direct<false>, dim3(g2), dim3(kCB), 0, s, p);
+        } else if (conv_unpack_pipe()) {
+          if (p.tbl_lds) hipLaunchKernelGGL((k_unpack_piece<true, true>), dim3((unsigned)grid), dim3(kCB), lds, s, p);
+          else hipLaunchKernelGGL((k_unpack_piece<true, false>), dim3((unsigned)grid), dim3(kCB), lds, s, p);
+        } else if (p.tbl_lds) {
+          hipLaunchKernelGGL((k_unpack_piece<false, true>), dim3((unsigned)grid), dim3(kCB), lds, s, p);
+        } else {
+          hipLaunchKernelGGL((k_unpack_piece<false, false>), dim3((unsigned)grid), dim3(kCB), lds, s, p);
+        }
+        const int lrc = mx_check_launch();
+        if (ev1 && hipEventRecord(ev1, s) != hipSuccess) (void)hipGetLastError();
+        return lrc;
       }
     }
   }
@@ -2909,12 +3082,18 @@ static int convert(const mx_ddt_t *d, size_t count, char *user, char *packed, si
   }
   const dim3 grid((unsigned)(((len + 15) / 16 + kCB - 1) / kCB)), block(kCB);
   dm->last_path.store(3, std::memory_order_relaxed);
+#define MX_CONV_LAUNCH(U)                                                                   \
+  do {                                                                                      \
+    if (run_lds) hipLaunchKernelGGL((k_convert<U, PACK, true>), grid, block, run_lds, s, a); \
+    else hipLaunchKernelGGL((k_convert<U, PACK, false>), grid, block, 0, s, a);              \
+  } while (0)
   switch (u) {
-    case 8: hipLaunchKernelGGL((k_convert<8, PACK>), grid, block, run_lds, s, a); break;
-    case 4: hipLaunchKernelGGL((k_convert<4, PACK>), grid, block, run_lds, s, a); break;
-    case 2: hipLaunchKernelGGL((k_convert<2, PACK>), grid, block, run_lds, s, a); break;
-    default: hipLaunchKernelGGL((k_convert<1, PACK>), grid, block, run_lds, s, a); break;
+    case 8: MX_CONV_LAUNCH(8); break;
+    case 4: MX_CONV_LAUNCH(4); break;
+    case 2: MX_CONV_LAUNCH(2); break;
+    default: MX_CONV_LAUNCH(1); break;
   }
+#undef MX_CONV_LAUNCH
   return mx_check_launch();
 }
 

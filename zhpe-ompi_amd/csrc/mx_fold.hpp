@@ -37,11 +37,12 @@ enum { FLAG_READY = 0, FLAG_PUSHED = 1, FLAG_DONE = 2, NFLAGS = 3 };
 constexpr int OSWG = 64;
 constexpr int OS_MAXSEG = 16;
 
+
 // Poisoned communicator (mx_comm::poison): a peer wait of an earlier kernel
 // timed out.  The word is device memory written at agent scope; kernels of
 // the same stream that run later see it (kernel boundaries order it).
 __device__ __forceinline__ bool poisoned(const int *poison) {
-  return poison && __hip_atomic_load(poison, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0;
+  return poison && __hip_atomic_load(gp(poison), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0;
 }
 __device__ __forceinline__ void raise_timeout(int *err, int *poison) {
   __hip_atomic_store(err, MX_ERR_TIMEOUT, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
@@ -228,7 +229,7 @@ constexpr int kOSB = 256;
 
 __device__ __forceinline__ void os_spin(const uint64_t *f, uint64_t v, uint64_t ticks, int *err, int *poison) {
   const uint64_t t0 = wall_clock64();
-  while (__hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) < v) {
+  while (__hip_atomic_load(gp(f), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) < v) {
     __builtin_amdgcn_s_sleep(1);
     if (wall_clock64() - t0 > ticks) {
       raise_timeout(err, poison);
@@ -256,11 +257,13 @@ __device__ __forceinline__ void os_spin(const uint64_t *f, uint64_t v, uint64_t 
 constexpr size_t OS_LL_MAX = 4096;   // bytes per rank (one slice of the raw path)
 
 __device__ __forceinline__ uint64_t ll_ld(const uint64_t *p) {
-  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  return __hip_atomic_load(gp(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
+// tk (the service's phase trace, or null): thread 0 stamps [0] the gen-2
+// check, [1] the push issued, [2] the gather, [3] the fold
 template <class T, class OP, bool SYS>
-__device__ bool os_ll(const OneShotArgs &a) {
+__device__ bool os_ll(const OneShotArgs &a, uint64_t *tk = nullptr) {
   constexpr int W = (int)(sizeof(T) / 4);
   static_assert(sizeof(T) == 4 || sizeof(T) == 8, "LL carries 4- and 8-byte elements");
   // lane t's gathered words, [f * kOSB + t]: at most (MAXR - 1) peers x
@@ -277,7 +280,10 @@ __device__ bool os_ll(const OneShotArgs &a) {
   // (1) every peer is past gen-2: its reads of this parity's LL area are over
   if (t < n && t != r && a.gen > 2) os_spin(a.my_done + t, a.gen - 2, a.timeout_ticks, a.err, a.poison);
   __syncthreads();
-  if (t == 0) s_bad = poisoned(a.poison);
+  if (t == 0) {
+    s_bad = poisoned(a.poison);
+    if (tk) tk[0] = wall_clock64();
+  }
   __syncthreads();
   if (s_bad) return false;
   // (2) my words (at most MW per lane, all loads in flight at once), tagged,
@@ -291,7 +297,7 @@ __device__ bool os_ll(const OneShotArgs &a) {
   for (int u = 0; u < MW; u++) {
     const size_t i = (size_t)t + (size_t)u * kOSB;
     if (i < nw) {
-      if (SYS) mv[u] = __hip_atomic_load(sw + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      if (SYS) mv[u] = __hip_atomic_load(gp(sw + i), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
       else if (al) mv[u] = sw[i];
       else __builtin_memcpy(&mv[u], a.sb + 4 * i, 4);
     }
@@ -303,10 +309,11 @@ __device__ bool os_ll(const OneShotArgs &a) {
       mine[i] = mv[u];
       for (int p = 0; p < n; p++)
         if (p != r)
-          __hip_atomic_store(reinterpret_cast<uint64_t *>(a.peer_slot[p]) + i, tag | mv[u], __ATOMIC_RELAXED,
+          __hip_atomic_store(gp(reinterpret_cast<uint64_t *>(a.peer_slot[p]) + i), tag | mv[u], __ATOMIC_RELAXED,
                              __HIP_MEMORY_SCOPE_SYSTEM);
     }
   }
+  if (tk && t == 0) tk[1] = wall_clock64();
   // (3) gather: lane t's words of every peer -- E elements (t, t + kOSB, ...)
   // of W words each -- flattened as f = (peer * E + i) * W + k and loaded
   // eight at a time (all eight in flight), into LDS column t
@@ -354,6 +361,7 @@ __device__ bool os_ll(const OneShotArgs &a) {
   if (bad) s_bad = 1;
   __syncthreads();
   if (s_bad) return false;   // a peer's words never came: no DONE
+  if (tk && t == 0) tk[2] = wall_clock64();
   // (4) fold lane t's elements from its column
   int sidx = 0;
   for (int ii = 0; ii < E; ii++) {
@@ -380,16 +388,17 @@ __device__ bool os_ll(const OneShotArgs &a) {
       __builtin_memcpy(u, &v, sizeof(T));
 #pragma unroll
       for (int k = 0; k < W; k++)
-        __hip_atomic_store(reinterpret_cast<uint32_t *>(a.rb) + e * W + k, u[k], __ATOMIC_RELAXED,
+        __hip_atomic_store(gp(reinterpret_cast<uint32_t *>(a.rb) + e * W + k), u[k], __ATOMIC_RELAXED,
                            __HIP_MEMORY_SCOPE_SYSTEM);
     } else {
       store_fields(reinterpret_cast<T *>(a.rb + off), v);
     }
   }
+  if (tk && t == 0) tk[3] = wall_clock64();
   // (5) every lane's gathers returned before the barrier above: DONE(gen) at every peer
   if (t == 0)
     for (int p = 0; p < n; p++)
-      if (p != r) __hip_atomic_store(a.peer_done[p], a.gen, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      if (p != r) __hip_atomic_store(gp(a.peer_done[p]), a.gen, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
   return true;
 }
 

@@ -18,6 +18,17 @@ namespace mx {
 
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 
+// The global-address-space view of a pointer.  Through a generic pointer the
+// compiler emits flat instructions, which count on lgkmcnt as well as vmcnt,
+// so in a kernel that also uses LDS every LDS wait then waits for the
+// outstanding global stores too (round 6: found in the service's tagged-word
+// loop and the LDS-staged convertor kernels).  Use it on every global access
+// of a kernel that mixes them with LDS.
+template <class T>
+__device__ __forceinline__ __attribute__((address_space(1))) T *gp(T *p) {
+  return (__attribute__((address_space(1))) T *)p;
+}
+
 // Both policies move the 16 bytes as one u32x4 copied straight into the
 // destination object, so bytes outside a struct's fields (padding of the
 // pair types) travel unchanged.  (Returning the struct by value would let
