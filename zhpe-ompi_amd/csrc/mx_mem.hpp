@@ -33,10 +33,11 @@ __device__ __forceinline__ __attribute__((address_space(1))) T *gp(T *p) {
 // destination object, so bytes outside a struct's fields (padding of the
 // pair types) travel unchanged.  (Returning the struct by value would let
 // the compiler treat those bytes as undefined.)
+// (global memory only: the accesses are global_*, never flat -- see gp)
 template <bool NT, class V>
 __device__ __forceinline__ void ld16(V &out, const V *p) {
   if constexpr (sizeof(V) == 16) {   // other sizes: never on a vector path
-    const u32x4 *q = reinterpret_cast<const u32x4 *>(p);
+    const __attribute__((address_space(1))) u32x4 *q = gp(reinterpret_cast<const u32x4 *>(p));
     u32x4 r;
     if constexpr (NT) r = __builtin_nontemporal_load(q);
     else r = *q;
@@ -51,7 +52,7 @@ __device__ __forceinline__ void st16(V *p, const V &v) {
   if constexpr (sizeof(V) == 16) {
     u32x4 r;
     __builtin_memcpy(&r, &v, 16);
-    u32x4 *q = reinterpret_cast<u32x4 *>(p);
+    __attribute__((address_space(1))) u32x4 *q = gp(reinterpret_cast<u32x4 *>(p));
     if constexpr (NT) __builtin_nontemporal_store(r, q);
     else *q = r;
   } else {

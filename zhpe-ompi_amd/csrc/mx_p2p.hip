@@ -64,7 +64,7 @@ constexpr int kP2PThreads = 256;
 // acquire fence when it succeeds.  Release / acquire atomics in the loops
 // themselves cost an L2 write-back / invalidate per access on gfx950.
 __device__ __forceinline__ bool p2p_wait_ge(const uint64_t *f, uint64_t v, uint64_t t0, uint64_t tmo, int *err) {
-  while (__hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) < v) {
+  while (__hip_atomic_load(gp(f), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) < v) {
     __builtin_amdgcn_s_sleep(2);
     if (wall_clock64() - t0 > tmo) {
       __hip_atomic_store(err, MX_ERR_TIMEOUT, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
@@ -81,8 +81,8 @@ __device__ __forceinline__ void p2p_copy(char *dst, const char *src, uint64_t le
   const int t = threadIdx.x;
   if ((((uintptr_t)dst | (uintptr_t)src) & 15) == 0) {
     const uint64_t nv = len / 16;
-    for (uint64_t i = t; i < nv; i += kP2PThreads)
-      reinterpret_cast<uint4 *>(dst)[i] = reinterpret_cast<const uint4 *>(src)[i];
+    for (uint64_t i = t; i < nv; i += kP2PThreads)   // (global accesses, mx_mem.hpp gp)
+      gp(reinterpret_cast<u32x4 *>(dst))[i] = gp(reinterpret_cast<const u32x4 *>(src))[i];
     for (uint64_t i = nv * 16 + t; i < len; i += kP2PThreads) dst[i] = src[i];
   } else if ((((uintptr_t)dst | (uintptr_t)src) & 3) == 0) {
     const uint64_t nw = len / 4;
