@@ -91,12 +91,15 @@ __device__ __forceinline__ fvec<T> comb(const fvec<T> &x, const fvec<T> &y) {
 }
 
 // Evaluates the program; LD(j) returns operand j at this lane's position.
-template <class OP, class V, class L>
-__device__ __forceinline__ V eval_prog(const FoldProg &p, L LD) {
+// NM bounds the program's operand count (p.n <= NM): the loops unroll to
+// NM steps, so a small program costs a few instructions, not MAXR guarded
+// steps (eval_prog_small picks NM from p.n).
+template <int NM, class OP, class V, class L>
+__device__ __forceinline__ V eval_prog_nm(const FoldProg &p, L LD) {
   if (p.kind == PROG_CHAIN) {
     V acc = LD(p.ord[0]);
 #pragma unroll
-    for (int j = 1; j < MAXR; j++) {
+    for (int j = 1; j < NM; j++) {
       if (j < p.n) {
         const V v = LD(p.ord[j]);
         acc = p.acc_first ? comb<OP>(acc, v) : comb<OP>(v, acc);
@@ -104,9 +107,9 @@ __device__ __forceinline__ V eval_prog(const FoldProg &p, L LD) {
     }
     return acc;
   }
-  V R[MAXR];
+  V R[NM];
 #pragma unroll
-  for (int i = 0; i < MAXR; i++) {
+  for (int i = 0; i < NM; i++) {
     if (i < p.n) {
       V a = LD(p.la[i]);
       if (p.lb[i] >= 0) a = comb<OP>(a, LD(p.lb[i]));
@@ -114,17 +117,30 @@ __device__ __forceinline__ V eval_prog(const FoldProg &p, L LD) {
     }
   }
 #pragma unroll
-  for (int s = 0; s < 4; s++) {
+  for (int s = 0; (1 << s) < NM; s++) {
     if (s < p.D) {
       const int h = 1 << s;
       const bool hi_first = (p.pref >> s) & 1;
 #pragma unroll
-      for (int u = 0; u < MAXR; u += 2 << s) {
+      for (int u = 0; u + h < NM; u += 2 << s) {
         if (u < p.n) R[u] = hi_first ? comb<OP>(R[u + h], R[u]) : comb<OP>(R[u], R[u + h]);
       }
     }
   }
   return R[0];
+}
+template <class OP, class V, class L>
+__device__ __forceinline__ V eval_prog(const FoldProg &p, L LD) {
+  return eval_prog_nm<MAXR, OP, V>(p, LD);
+}
+// the same with the bound picked from the program (uniform branch): the
+// latency-bound small-message folds (one-shot, tagged words)
+template <class OP, class V, class L>
+__device__ __forceinline__ V eval_prog_small(const FoldProg &p, L LD) {
+  if (p.n <= 2) return eval_prog_nm<2, OP, V>(p, LD);
+  if (p.n <= 4) return eval_prog_nm<4, OP, V>(p, LD);
+  if (p.n <= 8) return eval_prog_nm<8, OP, V>(p, LD);
+  return eval_prog_nm<MAXR, OP, V>(p, LD);
 }
 
 template <class T, class OP, bool NT>
@@ -266,9 +282,16 @@ template <class T, class OP, bool SYS>
 __device__ bool os_ll(const OneShotArgs &a, uint64_t *tk = nullptr) {
   constexpr int W = (int)(sizeof(T) / 4);
   static_assert(sizeof(T) == 4 || sizeof(T) == 8, "LL carries 4- and 8-byte elements");
-  // lane t's gathered words, [f * kOSB + t]: at most (MAXR - 1) peers x
-  // OS_LL_MAX / 4 / kOSB words = 60 per lane
-  __shared__ uint32_t col[(MAXR - 1) * (OS_LL_MAX / 4 / kOSB) * kOSB];
+  // Roles by wave: waves 0-1 (kG lanes) gather and fold, waves 2-3 push.
+  // gfx950 has one vmcnt for loads and stores, so a wave that has pushed
+  // must wait for its pushes' acknowledgements before it can use any load
+  // issued after them; with the roles split the gathering waves' waits see
+  // only their own loads.
+  constexpr int kG = kOSB / 2, kP = kOSB - kG;
+  constexpr int MW = (int)(OS_LL_MAX / 4 / kP);   // words per pushing lane
+  constexpr int ME = (int)(OS_LL_MAX / 4 / kG);   // words per peer and gathering lane
+  // gathering lane t's words, [f * kG + t]: at most (MAXR - 1) peers x ME
+  __shared__ uint32_t col[(MAXR - 1) * ME * kG];
   __shared__ uint32_t mine[OS_LL_MAX / 4];   // my words, for the fold
   __shared__ int s_bad;
   const int t = threadIdx.x, n = a.n, r = a.rank;
@@ -286,116 +309,130 @@ __device__ bool os_ll(const OneShotArgs &a, uint64_t *tk = nullptr) {
   }
   __syncthreads();
   if (s_bad) return false;
-  // (2) my words (at most MW per lane, all loads in flight at once), tagged,
-  // into every peer's LL area, and into LDS for my own operand of the fold
-  constexpr int MW = (int)(OS_LL_MAX / 4 / kOSB);
-  const size_t nw = a.count * W;
-  const bool al = ((uintptr_t)a.sb & 3) == 0;
-  const uint32_t *sw = reinterpret_cast<const uint32_t *>(a.sb);
-  uint32_t mv[MW];
-#pragma unroll
-  for (int u = 0; u < MW; u++) {
-    const size_t i = (size_t)t + (size_t)u * kOSB;
-    if (i < nw) {
-      if (SYS) mv[u] = __hip_atomic_load(gp(sw + i), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-      else if (al) mv[u] = sw[i];
-      else __builtin_memcpy(&mv[u], a.sb + 4 * i, 4);
-    }
-  }
-#pragma unroll
-  for (int u = 0; u < MW; u++) {
-    const size_t i = (size_t)t + (size_t)u * kOSB;
-    if (i < nw) {
-      mine[i] = mv[u];
-      for (int p = 0; p < n; p++)
-        if (p != r)
-          __hip_atomic_store(gp(reinterpret_cast<uint64_t *>(a.peer_slot[p]) + i), tag | mv[u], __ATOMIC_RELAXED,
-                             __HIP_MEMORY_SCOPE_SYSTEM);
-    }
-  }
-  if (tk && t == 0) tk[1] = wall_clock64();
-  // (3) gather: lane t's words of every peer -- E elements (t, t + kOSB, ...)
-  // of W words each -- flattened as f = (peer * E + i) * W + k and loaded
-  // eight at a time (all eight in flight), into LDS column t
-  const int E = (int)((a.count + kOSB - 1) / kOSB);
-  const int Lw = (n - 1) * E * W;
   bool bad = false;
-  const uint64_t t0 = wall_clock64();
-  for (int f0 = 0; f0 < Lw && !bad; f0 += 8) {
-    uint64_t v[8];
-    const uint64_t *ad[8];
+  const int E = (int)((a.count + kG - 1) / kG);   // elements per gathering lane
+  if (t >= kG) {
+    // (2) my words (MW per lane, all loads in flight at once) into LDS for my
+    // own operand of the fold, then, tagged, into every peer's LL area
+    const int q = t - kG;
+    const size_t nw = a.count * W;
+    const bool al = ((uintptr_t)a.sb & 3) == 0;
+    const uint32_t *sw = reinterpret_cast<const uint32_t *>(a.sb);
+    uint32_t mv[MW];
 #pragma unroll
-    for (int u = 0; u < 8; u++) {
-      const int f = f0 + u;
-      ad[u] = nullptr;
-      if (f < Lw) {
-        const int k = f % W, ii = (f / W) % E, jj = f / (W * E);
-        const size_t e = (size_t)t + (size_t)ii * kOSB;
-        if (e < a.count) {
-          ad[u] = reinterpret_cast<const uint64_t *>(a.src[jj < r ? jj : jj + 1]) + e * W + k;
-          v[u] = ll_ld(ad[u]);
+    for (int u = 0; u < MW; u++) {
+      const size_t i = (size_t)q + (size_t)u * kP;
+      if (i < nw) {
+        if (SYS) mv[u] = __hip_atomic_load(gp(sw + i), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        else if (al) mv[u] = sw[i];
+        else __builtin_memcpy(&mv[u], a.sb + 4 * i, 4);
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < MW; u++) {
+      const size_t i = (size_t)q + (size_t)u * kP;
+      if (i < nw) mine[i] = mv[u];
+    }
+    for (int p = 0; p < n; p++) {
+      if (p == r) continue;
+      uint64_t *d = reinterpret_cast<uint64_t *>(a.peer_slot[p]);
+#pragma unroll
+      for (int u = 0; u < MW; u++) {
+        const size_t i = (size_t)q + (size_t)u * kP;
+        if (i < nw) __hip_atomic_store(gp(d + i), tag | mv[u], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      }
+    }
+    if (tk && t == kG) tk[1] = wall_clock64();
+  } else {
+    // (3) gather: lane t's words of every peer -- E elements (t, t + kG, ...)
+    // of W words each -- flattened as f = (peer * E + i) * W + k and loaded
+    // eight at a time (all eight in flight), into LDS column t
+    const int Lw = (n - 1) * E * W;
+    const uint64_t t0 = wall_clock64();
+    for (int f0 = 0; f0 < Lw && !bad; f0 += 8) {
+      uint64_t v[8];
+      const uint64_t *ad[8];
+#pragma unroll
+      for (int u = 0; u < 8; u++) {
+        const int f = f0 + u;
+        ad[u] = nullptr;
+        if (f < Lw) {
+          const int k = f % W, ii = (f / W) % E, jj = f / (W * E);
+          const size_t e = (size_t)t + (size_t)ii * kG;
+          if (e < a.count) {
+            ad[u] = reinterpret_cast<const uint64_t *>(a.src[jj < r ? jj : jj + 1]) + e * W + k;
+            v[u] = ll_ld(ad[u]);
+          }
         }
       }
-    }
-    // words not yet of this generation are loaded again, all together
-    for (;;) {
-      bool all = true;
+      // words not yet of this generation are loaded again, all together
+      for (;;) {
+        bool all = true;
 #pragma unroll
-      for (int u = 0; u < 8; u++)
-        if (ad[u] && (uint32_t)(v[u] >> 32) != g) all = false;
-      if (all) break;
-      __builtin_amdgcn_s_sleep(1);
-      if (wall_clock64() - t0 > a.timeout_ticks) {
-        raise_timeout(a.err, a.poison);
-        bad = true;
-        break;
+        for (int u = 0; u < 8; u++)
+          if (ad[u] && (uint32_t)(v[u] >> 32) != g) all = false;
+        if (all) break;
+        __builtin_amdgcn_s_sleep(1);
+        if (wall_clock64() - t0 > a.timeout_ticks) {
+          raise_timeout(a.err, a.poison);
+          bad = true;
+          break;
+        }
+#pragma unroll
+        for (int u = 0; u < 8; u++)
+          if (ad[u] && (uint32_t)(v[u] >> 32) != g) v[u] = ll_ld(ad[u]);
       }
 #pragma unroll
       for (int u = 0; u < 8; u++)
-        if (ad[u] && (uint32_t)(v[u] >> 32) != g) v[u] = ll_ld(ad[u]);
+        if (ad[u]) col[(f0 + u) * kG + t] = (uint32_t)v[u];
     }
-#pragma unroll
-    for (int u = 0; u < 8; u++)
-      if (ad[u]) col[(f0 + u) * kOSB + t] = (uint32_t)v[u];
   }
   if (bad) s_bad = 1;
   __syncthreads();
   if (s_bad) return false;   // a peer's words never came: no DONE
   if (tk && t == 0) tk[2] = wall_clock64();
-  // (4) fold lane t's elements from its column
-  int sidx = 0;
-  for (int ii = 0; ii < E; ii++) {
-    const size_t e = (size_t)t + (size_t)ii * kOSB;
-    if (e >= a.count) break;
-    while (sidx + 1 < a.nseg && e >= a.seg[sidx].hi) sidx++;
-    const size_t off = e * sizeof(T);
-    const T v = eval_prog<OP, T>(a.seg[sidx].p, [&](int j) {
-      T x;
-      uint32_t u[W];
-      if (j != r) {
-        const int jj = j < r ? j : j - 1;
+  // (4) every lane folds elements t, t + kOSB, ... from the gathering
+  // lanes' columns (element e was gathered by lane e % kG, as its e / kG-th)
+  {
+    int sidx = 0;
+    for (size_t e = t; e < a.count; e += kOSB) {
+      const int gl = (int)(e % kG), gi = (int)(e / kG);
+      while (sidx + 1 < a.nseg && e >= a.seg[sidx].hi) sidx++;
+      const size_t off = e * sizeof(T);
+      auto LDo = [&](int j) {
+        T x;
+        uint32_t u[W];
+        if (j != r) {
+          const int jj = j < r ? j : j - 1;
 #pragma unroll
-        for (int k = 0; k < W; k++) u[k] = col[((jj * E + ii) * W + k) * kOSB + t];
+          for (int k = 0; k < W; k++) u[k] = col[((jj * E + gi) * W + k) * kG + gl];
+        } else {
+#pragma unroll
+          for (int k = 0; k < W; k++) u[k] = mine[e * W + k];
+        }
+        __builtin_memcpy(&x, u, sizeof(T));
+        return x;
+      };
+      // (the bounded evaluation only where the arguments live in LDS: with
+      // the launch's by-value arguments its copies would spill them)
+      T v;
+      if constexpr (SYS) v = eval_prog_small<OP, T>(a.seg[sidx].p, LDo);
+      else v = eval_prog<OP, T>(a.seg[sidx].p, LDo);
+      if (SYS) {
+        uint32_t u[W];
+        __builtin_memcpy(u, &v, sizeof(T));
+#pragma unroll
+        for (int k = 0; k < W; k++)
+          __hip_atomic_store(gp(reinterpret_cast<uint32_t *>(a.rb) + e * W + k), u[k], __ATOMIC_RELAXED,
+                             __HIP_MEMORY_SCOPE_SYSTEM);
       } else {
-#pragma unroll
-        for (int k = 0; k < W; k++) u[k] = mine[e * W + k];
+        store_fields(reinterpret_cast<T *>(a.rb + off), v);
       }
-      __builtin_memcpy(&x, u, sizeof(T));
-      return x;
-    });
-    if (SYS) {
-      uint32_t u[W];
-      __builtin_memcpy(u, &v, sizeof(T));
-#pragma unroll
-      for (int k = 0; k < W; k++)
-        __hip_atomic_store(gp(reinterpret_cast<uint32_t *>(a.rb) + e * W + k), u[k], __ATOMIC_RELAXED,
-                           __HIP_MEMORY_SCOPE_SYSTEM);
-    } else {
-      store_fields(reinterpret_cast<T *>(a.rb + off), v);
     }
   }
   if (tk && t == 0) tk[3] = wall_clock64();
-  // (5) every lane's gathers returned before the barrier above: DONE(gen) at every peer
+  // (5) every gathering lane's loads returned before the barrier above:
+  // DONE(gen) at every peer
   if (t == 0)
     for (int p = 0; p < n; p++)
       if (p != r) __hip_atomic_store(gp(a.peer_done[p]), a.gen, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
