@@ -1,8 +1,9 @@
 """GPU: the resident small-message allreduce service (csrc/mx_coll_svc.hip;
 VERDICT r5 missing 5).
 
-Blocking allreduces of the tagged-word class (os_ll in csrc/mx_fold.hpp:
-4- and 8-byte elements, up to 4 KiB per rank) are taken by a workgroup kept
+Blocking allreduces of the served tagged-word class (os_ll in
+csrc/mx_fold.hpp: 4- and 8-byte elements, up to 4 KiB per rank; launched
+tagged words go up to 64 KiB over several workgroups) are taken by a workgroup kept
 resident per process, which speaks the launched one-shot kernel's protocol
 exactly.  Checked on 2 processes sharing the GPU:
   * bit-exact against the oracle's coll/tuned order (recursive doubling at
@@ -13,10 +14,11 @@ exactly.  Checked on 2 processes sharing the GPU:
     launched (raw protocol) -- and with the service switched off on ONE rank
     only, the served rank and the launching rank still agree bit for bit
     (the protocol is the launch's);
-  * tagged-word and raw calls alternating on one communicator, int64 data
-    whose upper words are small integers (what a generation tag looks like):
-    the tagged words live in an area of their own, so raw bytes left in a
-    slot are never taken for a peer's words;
+  * tagged-word calls (served, and launched over two workgroups) and raw
+    calls alternating on one communicator, int64 data whose upper words are
+    small integers (what a generation tag looks like): the tagged words live
+    in an area of their own, so raw bytes left in a slot are never taken for
+    a peer's words;
   * at 3 ranks on one device the service stays off (more than two ranks per
     device), and the calls launch;
   * the 8 B latency with and without the service, median of 300 calls, is
@@ -39,11 +41,15 @@ pytestmark = pytest.mark.gpu
 CASES = [("SUM", "FLOAT"), ("MAX", "DOUBLE"), ("MAXLOC", "FLOAT_INT"), ("SUM", "INT64_T")]
 SIZES = [8, 4096, 32768]          # below the autotuned range (64 KiB): always the one-shot path
 SERVED = [8, 4096]                # the tagged-word class (OS_LL_MAX = 4 KiB)
-ALT = [4096, 8192] * 8            # tagged-word / raw alternation, int64 SUM
+# served tagged words (4 KiB), launched tagged words over two workgroups
+# (8 KiB) and the raw protocol (int16: never tagged words), alternating
+ALT = [(4096, "INT64_T"), (8192, "INT64_T"), (4096, "INT16_T")] * 5
 
 
-def _alt_gen(count, seed):
+def _alt_gen(count, seed, t="INT64_T"):
     rng = np.random.default_rng(seed)
+    if t == "INT16_T":
+        return rng.integers(-1000, 1000, count).astype(np.int16).view(np.uint8)
     hi = rng.integers(0, 256, count).astype(np.int64)   # (generations here: ~70-110)
     return ((hi << 32) | rng.integers(0, 1 << 20, count)).astype(np.int64).view(np.uint8)
 
@@ -94,11 +100,12 @@ def _worker(rank, n, port, q, off_rank):
                     outs.append(y.cpu().numpy().tobytes())      # read right after the call
                 res[(op, t, nb)] = outs
         res["served"] = comm.stats()["service_calls"]
-        for k, nb in enumerate(ALT):
-            x = torch.from_numpy(_alt_gen(nb // 8, 5000 + 10 * k + rank)).cuda()
+        for k, (nb, at) in enumerate(ALT):
+            es = mxompi.type_size(at)
+            x = torch.from_numpy(_alt_gen(nb // es, 5000 + 10 * k + rank, at)).cuda()
             y = torch.empty_like(x)
             torch.cuda.synchronize()
-            comm.allreduce(x.data_ptr(), y.data_ptr(), nb // 8, "INT64_T", "SUM", "auto", st)
+            comm.allreduce(x.data_ptr(), y.data_ptr(), nb // es, at, "SUM", "auto", st)
             res[("alt", k)] = y.cpu().numpy().tobytes()
         # 8 B latency, service on / off (this rank), median of 300
         L = mxompi.lib()
@@ -165,8 +172,10 @@ def _check(out, n):
                                        (vp * n)(*[e.ctypes.data for e in exp])) == 0
                 for r in range(n):
                     assert out[r][(op, t, nb)][it] == exp[r].tobytes(), (op, t, nb, it, r)
-    for k, nb in enumerate(ALT):
-        want = sum(_alt_gen(nb // 8, 5000 + 10 * k + r).view(np.int64) for r in range(n))
+    for k, (nb, at) in enumerate(ALT):
+        es = mxompi.type_size(at)
+        dt = np.int16 if at == "INT16_T" else np.int64
+        want = sum(_alt_gen(nb // es, 5000 + 10 * k + r, at).view(dt) for r in range(n)).astype(dt)
         for r in range(n):
             assert out[r][("alt", k)] == want.tobytes(), (k, nb, r)
 

@@ -838,7 +838,9 @@ extern "C" int mx_comm_create_ex(int rank, int size, int device, size_t staging_
       c->os_max = std::min<size_t>(oneshot_max(), c->os_cap);
       // (MX_ONESHOT_LL=0: the raw protocol at every size; same on every rank)
       const char *lle = getenv("MX_ONESHOT_LL");
-      c->os_ll = (lle && *lle == '0') ? 0 : std::min<size_t>(OS_LL_MAX, c->os_cap);
+      // (the LL area, 2 * os_ll, kept within half the raw slot: small
+      // stagings keep their room for the staged paths)
+      c->os_ll = (lle && *lle == '0') ? 0 : std::min<size_t>(OS_LL_CAP, c->os_cap / 4) & ~(size_t)15;
       c->os_slot = c->os_cap ? c->os_cap + 256 + 2 * c->os_ll : 0;
       c->main_bytes = (c->staging_bytes - 2 * (size_t)size * c->os_slot) & ~(size_t)255;
       c->hregion_bytes = heap_bytes ? ((heap_bytes + 4095) & ~(size_t)4095) : 0;
@@ -853,6 +855,12 @@ extern "C" int mx_comm_create_ex(int rank, int size, int device, size_t staging_
            (++stage, ipc_region_alloc(ALL_FLAG_WORDS * sizeof(uint64_t), (char **)&c->flagmem) == MX_SUCCESS) &&
            (++stage, !c->hregion_bytes || ipc_region_alloc(c->hregion_bytes, &c->hregion) == MX_SUCCESS) &&
            (++stage, hipMemsetAsync(c->flagmem, 0, ALL_FLAG_WORDS * sizeof(uint64_t), ls) == hipSuccess) &&
+           // the one-shot slots too: a recycled staging region still holds the
+           // previous communicator's tagged words, whose generations the new
+           // communicator's count restarts through (tag 0 is never current);
+           // no peer writes here before exchange 1, old peers have said BYE
+           (++stage, !c->os_slot || hipMemsetAsync(c->staging + c->main_bytes, 0, 2 * (size_t)size * c->os_slot,
+                                                   ls) == hipSuccess) &&
            (++stage, hipIpcGetMemHandle(&mine.staging, c->staging) == hipSuccess) &&
            (++stage, hipIpcGetMemHandle(&mine.flags, c->flagmem) == hipSuccess) &&
            (++stage, !c->hregion || hipIpcGetMemHandle(&mine.hregion, c->hregion) == hipSuccess) &&
@@ -1681,13 +1689,14 @@ static int allreduce_oneshot(mx_comm *c, oneshot_launch_fn ol, const std::vector
   size_t slice = (count + nwg - 1) / nwg;
   if (16 % es == 0) slice = rup(slice, 16 / es);
   nwg = (count + slice - 1) / slice;
-  if (ll) {   // one workgroup, no completion counter (it is the last one out)
-    nwg = 1;
-    slice = count;
+  if (ll) {   // one workgroup per OS_LL_MAX bytes; a single one needs no completion counter
+    slice = OS_LL_MAX / es;
+    nwg = (count + slice - 1) / slice;
+    if (nwg == 1) slice = count;
   }
   a.slice = slice;
   a.counter_last = c->os_count + nwg - 1;
-  if (!ll) c->os_count += nwg;
+  if (!ll || nwg > 1) c->os_count += nwg;
   a.nseg = (int)segs.size();
   for (size_t i = 0; i < segs.size(); i++) a.seg[i] = OsSeg{segs[i].lo, segs[i].hi, segs[i].p};
   // the resident service takes the call when it can (the same arguments and

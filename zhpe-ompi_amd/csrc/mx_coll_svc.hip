@@ -382,7 +382,8 @@ bool csv_start(Csv &v, csv_launch_fn fn) {
 int csv_allreduce(mx_comm *c, const OneShotArgs &a, int op, int type, hipStream_t s) {
   // the tagged-word calls only (one workgroup's work), operands on 4-byte
   // boundaries (the service moves 4-byte words at system scope)
-  if (!csv_enabled() || !c->csv_ok || c->defer || c->poisoned || !a.ll || (((uintptr_t)a.sb | (uintptr_t)a.rb) & 3) ||
+  if (!csv_enabled() || !c->csv_ok || c->defer || c->poisoned || !a.ll || a.count * a.es > OS_LL_MAX ||
+      (((uintptr_t)a.sb | (uintptr_t)a.rb) & 3) ||
       (((uintptr_t)a.sb | (uintptr_t)a.rb | a.count | a.gen) >> 48))   // (the line's 48-bit fields)
     return 0;
   const auto t_in = std::chrono::steady_clock::now();

@@ -184,7 +184,7 @@ struct mx_comm {
   size_t main_bytes;           // staging for the chunked paths: [0, main_bytes)
   size_t os_max, os_slot;      // one-shot: default max bytes per rank, slot stride
   size_t os_cap;               // one-shot: the most a slot holds (autotuning may pick it up to here)
-  size_t os_ll;                // one-shot: the tagged-word (LL) protocol up to this many bytes per rank
+  size_t os_ll;                // one-shot: the tagged-word (LL) protocol up to this many bytes per rank (<= OS_LL_CAP)
                                // (its area, 2 * os_ll, follows the raw os_cap + 256 in each slot)
   uint64_t os_count;           // one-shot workgroup completions so far
   char *staging;               // mine (uncached, IPC-exported)

@@ -270,7 +270,8 @@ __device__ __forceinline__ void os_spin(const uint64_t *f, uint64_t v, uint64_t 
 // (SYS: its operand and result words too) runs with no cache maintenance at
 // all.  Returns false when the call failed (poisoned, or a peer timed out).
 // ---------------------------------------------------------------------------
-constexpr size_t OS_LL_MAX = 4096;   // bytes per rank (one slice of the raw path)
+constexpr size_t OS_LL_MAX = 4096;         // bytes per rank and workgroup (one slice)
+constexpr size_t OS_LL_CAP = 64 << 10;     // bytes per rank of the launched tagged-word class
 
 __device__ __forceinline__ uint64_t ll_ld(const uint64_t *p) {
   return __hip_atomic_load(gp(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
@@ -310,12 +311,17 @@ __device__ bool os_ll(const OneShotArgs &a, uint64_t *tk = nullptr) {
   __syncthreads();
   if (s_bad) return false;
   bool bad = false;
-  const int E = (int)((a.count + kG - 1) / kG);   // elements per gathering lane
+  // this workgroup's slice of the elements, [lo, hi) (the launch: one per
+  // OS_LL_MAX bytes; the service: one workgroup, the whole call)
+  const size_t lo = (size_t)blockIdx.x * a.slice;
+  const size_t hi = lo + a.slice < a.count ? lo + a.slice : a.count;
+  const size_t cnt = hi > lo ? hi - lo : 0;
+  const int E = (int)((cnt + kG - 1) / kG);   // elements per gathering lane
   if (t >= kG) {
     // (2) my words (MW per lane, all loads in flight at once) into LDS for my
     // own operand of the fold, then, tagged, into every peer's LL area
     const int q = t - kG;
-    const size_t nw = a.count * W;
+    const size_t w0 = lo * W, nw = cnt * W;   // this slice's words: [w0, w0 + nw)
     const bool al = ((uintptr_t)a.sb & 3) == 0;
     const uint32_t *sw = reinterpret_cast<const uint32_t *>(a.sb);
     uint32_t mv[MW];
@@ -323,9 +329,9 @@ __device__ bool os_ll(const OneShotArgs &a, uint64_t *tk = nullptr) {
     for (int u = 0; u < MW; u++) {
       const size_t i = (size_t)q + (size_t)u * kP;
       if (i < nw) {
-        if (SYS) mv[u] = __hip_atomic_load(gp(sw + i), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-        else if (al) mv[u] = sw[i];
-        else __builtin_memcpy(&mv[u], a.sb + 4 * i, 4);
+        if (SYS) mv[u] = __hip_atomic_load(gp(sw + w0 + i), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        else if (al) mv[u] = sw[w0 + i];
+        else __builtin_memcpy(&mv[u], a.sb + 4 * (w0 + i), 4);
       }
     }
 #pragma unroll
@@ -335,7 +341,7 @@ __device__ bool os_ll(const OneShotArgs &a, uint64_t *tk = nullptr) {
     }
     for (int p = 0; p < n; p++) {
       if (p == r) continue;
-      uint64_t *d = reinterpret_cast<uint64_t *>(a.peer_slot[p]);
+      uint64_t *d = reinterpret_cast<uint64_t *>(a.peer_slot[p]) + w0;
 #pragma unroll
       for (int u = 0; u < MW; u++) {
         const size_t i = (size_t)q + (size_t)u * kP;
@@ -358,8 +364,8 @@ __device__ bool os_ll(const OneShotArgs &a, uint64_t *tk = nullptr) {
         ad[u] = nullptr;
         if (f < Lw) {
           const int k = f % W, ii = (f / W) % E, jj = f / (W * E);
-          const size_t e = (size_t)t + (size_t)ii * kG;
-          if (e < a.count) {
+          const size_t e = lo + (size_t)t + (size_t)ii * kG;
+          if (e < hi) {
             ad[u] = reinterpret_cast<const uint64_t *>(a.src[jj < r ? jj : jj + 1]) + e * W + k;
             v[u] = ll_ld(ad[u]);
           }
@@ -395,8 +401,8 @@ __device__ bool os_ll(const OneShotArgs &a, uint64_t *tk = nullptr) {
   // lanes' columns (element e was gathered by lane e % kG, as its e / kG-th)
   {
     int sidx = 0;
-    for (size_t e = t; e < a.count; e += kOSB) {
-      const int gl = (int)(e % kG), gi = (int)(e / kG);
+    for (size_t e = lo + t; e < hi; e += kOSB) {
+      const int gl = (int)((e - lo) % kG), gi = (int)((e - lo) / kG);
       while (sidx + 1 < a.nseg && e >= a.seg[sidx].hi) sidx++;
       const size_t off = e * sizeof(T);
       auto LDo = [&](int j) {
@@ -408,7 +414,7 @@ __device__ bool os_ll(const OneShotArgs &a, uint64_t *tk = nullptr) {
           for (int k = 0; k < W; k++) u[k] = col[((jj * E + gi) * W + k) * kG + gl];
         } else {
 #pragma unroll
-          for (int k = 0; k < W; k++) u[k] = mine[e * W + k];
+          for (int k = 0; k < W; k++) u[k] = mine[(e - lo) * W + k];
         }
         __builtin_memcpy(&x, u, sizeof(T));
         return x;
@@ -432,10 +438,15 @@ __device__ bool os_ll(const OneShotArgs &a, uint64_t *tk = nullptr) {
   }
   if (tk && t == 0) tk[3] = wall_clock64();
   // (5) every gathering lane's loads returned before the barrier above:
-  // DONE(gen) at every peer
-  if (t == 0)
-    for (int p = 0; p < n; p++)
-      if (p != r) __hip_atomic_store(gp(a.peer_done[p]), a.gen, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  // DONE(gen) at every peer -- with several workgroups, by the last one out
+  if (t == 0) {
+    bool last = gridDim.x == 1;
+    if (!last) last = __hip_atomic_fetch_add(gp(a.counter), (uint64_t)1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
+                      a.counter_last;
+    if (last)
+      for (int p = 0; p < n; p++)
+        if (p != r) __hip_atomic_store(gp(a.peer_done[p]), a.gen, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
   return true;
 }
 
