@@ -21,6 +21,9 @@ exactly.  Checked on 2 processes sharing the GPU:
     a peer's words;
   * at 3 ranks on one device the service stays off (more than two ranks per
     device), and the calls launch;
+  * with the limit raised (MX_COLL_SERVICE_PER_DEV=n), 4 and 8 ranks on one
+    device run the served protocol at n = 4 and 8 (what ranks on distinct
+    devices get), bit-exact;
   * the 8 B latency with and without the service, median of 300 calls, is
     printed for the log (tools/coll_lat.py measures it properly).
 """
@@ -68,9 +71,10 @@ def _gen(t, count, seed):
     return p.view(np.uint8)
 
 
-def _worker(rank, n, port, q, off_rank):
+def _worker(rank, n, port, q, off_rank, env):
     import torch.distributed as dist
     os.environ["HSA_ENABLE_IPC_MODE_LEGACY"] = "0"
+    os.environ.update(env)
     if rank == off_rank:
         os.environ["MX_COLL_SERVICE"] = "0"
     try:
@@ -133,12 +137,12 @@ def _worker(rank, n, port, q, off_rank):
         q.put((rank, "err", traceback.format_exc()))
 
 
-def _run(n, off_rank=-1):
+def _run(n, off_rank=-1, env=None):
     import torch.multiprocessing as mp
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, n, port, q, off_rank)) for r in range(n)]
+    procs = [ctx.Process(target=_worker, args=(r, n, port, q, off_rank, dict(env or {}))) for r in range(n)]
     for p in procs:
         p.start()
     out = {}
@@ -200,3 +204,14 @@ def test_three_ranks_on_one_device_launch():
     out = _run(3)
     _check(out, 3)
     assert all(out[r]["served"] == 0 for r in range(3))
+
+
+@pytest.mark.parametrize("n", [4, 8])
+def test_ranks_served_with_the_limit_raised(n):
+    out = _run(n, env={"MX_COLL_SERVICE_PER_DEV": str(n)})
+    _check(out, n)
+    served = [out[r]["served"] for r in range(n)]
+    # a service not running within its start window means launches, never a
+    # disagreement: most calls are served, none has to be
+    assert sum(served) > 0, served
+    print(f"n = {n} served calls per rank:", served, "8 B median us:", [out[r]["lat_us"] for r in range(n)])

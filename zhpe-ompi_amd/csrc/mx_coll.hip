@@ -905,7 +905,10 @@ extern "C" int mx_comm_create_ex(int rank, int size, int device, size_t staging_
         for (int q = 0; q < size; q++) k += !strncmp(all[p].pci, all[q].pci, sizeof mine.pci);
         per_dev = std::max(per_dev, k);
       }
-      c->csv_ok = per_dev <= 2;
+      // MX_COLL_SERVICE_PER_DEV: most ranks per device with the service on
+      // (default 2; more is for tests of the n > 2 served protocol on one GPU)
+      const char *spd = getenv("MX_COLL_SERVICE_PER_DEV");
+      c->csv_ok = per_dev <= ((spd && *spd) ? atoi(spd) : 2);
       c->proto = proto_default(c);   // the same on every rank: xdev is symmetric, the env is job-wide
     }
     for (int p = 0; ok && p < size; p++) {
