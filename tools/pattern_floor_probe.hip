@@ -12,7 +12,8 @@
 //             16-byte loads of the 1 GiB packed stream): reads + writes
 // Types: blacs (ref_blacs_indexed: 6 x 52 B every 88 B, then 48..4 B every
 // 92 B, extent 1548, 624 B of data), struct48 (char @0, 28 B @8, extent 48),
-// u4s32 (vector_f32_b4_s8: 16 B every 32 B).
+// u4s32 (16 B every 32 B: vector_f32_b4_s8's blocks without its instance
+// seam), v97 (vector_f32_b4_s8 exactly: 97 x 16 B every 32 B, extent 3088).
 // Prints the median of 7 timed launches per variant (HIP events).
 #include <hip/hip_runtime.h>
 #include <cstdio>
@@ -96,6 +97,9 @@ int main(int argc, char **argv) {
   } else if (!strcmp(type, "u4s32")) {   // vector_f32_b4_s8: 16 B every 32 B
     blocks.push_back({0, 16});
     ext = 32;
+  } else if (!strcmp(type, "v97")) {     // vector_f32_b4_s8 as committed
+    for (int k = 0; k < 97; k++) blocks.push_back({(uint32_t)(32 * k), 16});
+    ext = 3088;
   } else if (!strcmp(type, "struct48")) {
     blocks.push_back({0, 1});
     blocks.push_back({8, 28});
