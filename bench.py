@@ -684,16 +684,30 @@ def allreduce_sweep(torch, mx, dist, comm, world, x, out, sp, flags, budget_s=45
                     rows.append({"bytes": nbytes, "type": t, "op": op, "alg": alg, "error": "unsupported"})
                     continue
                 dist.barrier()
+                sv0 = comm.stats()["service_calls"]
+                small = nbytes <= (64 << 10)   # blocking calls: each one's own time too (median)
+                ts = []
                 t0 = time.perf_counter()
                 for _ in range(iters):
+                    t1 = time.perf_counter() if small else 0.0
                     comm.allreduce(bx.data_ptr(), bo.data_ptr(), count, t, op, alg, sp)
+                    if small:
+                        ts.append(time.perf_counter() - t1)
                 torch.cuda.synchronize()
                 el = torch.tensor([time.perf_counter() - t0], dtype=torch.float64)
+                served = comm.stats()["service_calls"] - sv0
+                med = None
+                if small:
+                    mt = torch.tensor([sorted(ts)[len(ts) // 2]], dtype=torch.float64)
+                    dist.all_reduce(mt, op=dist.ReduceOp.MAX)
+                    med = round(float(mt[0]) * 1e6, 2)
                 dist.all_reduce(el, op=dist.ReduceOp.MAX)
                 per = float(el[0]) / iters
                 algbw = count * (4 if t == "FLOAT" else 2) / per / 1e9
                 rows.append({"bytes": nbytes, "type": t, "op": op, "alg": alg, "us": round(per * 1e6, 2),
-                             "algbw_gbs": round(algbw, 2), "busbw_gbs": round(algbw * 2 * (world - 1) / world, 2)})
+                             "algbw_gbs": round(algbw, 2), "busbw_gbs": round(algbw * 2 * (world - 1) / world, 2),
+                             **({"us_median": med} if med is not None else {}),
+                             **({"served": served} if served else {})})
         done = torch.tensor([1.0 if time.perf_counter() - t_start > budget_s else 0.0])
         dist.all_reduce(done, op=dist.ReduceOp.MAX)
         if done[0] > 0:

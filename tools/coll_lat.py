@@ -89,6 +89,24 @@ def worker(rank, n, port, q, sizes):
                     row["trace_us"] = {nm: round((tr1[i + 1] * tr1[0] - tr0[i + 1] * tr0[0]) / k, 2)
                                        for i, nm in enumerate(names)}
                     row["full_commands"] = int(tr1[9] - tr0[9])
+        if nb == sizes[0]:
+            # calls after an idle gap (the service leaves after 200 us idle):
+            # each call alone, the ranks aligned by a barrier, then the gap
+            for mode, gap in (("service", 0.0005), ("service", 0.002), ("launch", 0.0005), ("launch", 0.002)):
+                L.mx_coll_service_set(1 if mode == "service" else 0)
+                ts = []
+                for _ in range(60):
+                    dist.barrier()
+                    time.sleep(gap)
+                    t0 = time.perf_counter()
+                    comm.allreduce(x.data_ptr(), y.data_ptr(), cnt, "FLOAT", "SUM", "auto", st)
+                    ts.append(time.perf_counter() - t0)
+                ts = ts[10:]
+                agg = torch.tensor([sorted(ts)[len(ts) // 2] * 1e6, sum(ts) / len(ts) * 1e6])
+                dist.all_reduce(agg, op=dist.ReduceOp.MAX)
+                row[f"{mode}_after_gap_{int(gap * 1e6)}us"] = {"median": round(float(agg[0]), 2),
+                                                                "mean": round(float(agg[1]), 2)}
+            L.mx_coll_service_set(1)
         rows.append(row)
         if rank == 0:
             print(f"n={n}", row, flush=True)

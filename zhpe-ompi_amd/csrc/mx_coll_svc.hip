@@ -53,7 +53,15 @@
 
 namespace mx {
 
-constexpr double kCsvIdleS = 200e-6;        // leave after 200 us without a command
+// leave after 200 us without a command.  A longer idle exit keeps calls
+// after gaps served (8 B n = 2 after a 0.5 ms gap: 9.5 us with 2 ms, 26 us
+// with 200 us -- the restart costs more than the launch path's 20), but a
+// device-wide synchronisation (hipDeviceSynchronize, torch.cuda.synchronize)
+// waits for the resident kernel to leave: with 2 ms the bench sweep's loops
+// of 50 calls + one synchronize took 50 us per call at a 9.5 us median
+// (profiles/r06/coll_lat_r6as_idle_exit.txt).  MX_COLL_SERVICE_IDLE_US
+// raises it for applications that never synchronise the whole device.
+constexpr double kCsvIdleS = 200e-6;
 constexpr double kCsvLifeS = 5e-3;          // and between commands once 5 ms old (then relaunched)
 constexpr double kCsvStartUs = 1000;        // a kernel not running 1 ms after its launch is held
 constexpr double kCsvFirstStartUs = 50000;  // (50 ms for a pair's first launch: its code object loads)
@@ -317,7 +325,10 @@ int csv_setup(Csv &v) {
   if (hipDeviceGetAttribute(&rate_khz, hipDeviceAttributeWallClockRate, v.device) != hipSuccess || rate_khz <= 0)
     rate_khz = 100000;
   v.tick_us = 1e3 / rate_khz;
-  v.idle_ticks = (uint64_t)(kCsvIdleS * rate_khz * 1000.0);
+  // MX_COLL_SERVICE_IDLE_US: the idle exit (default kCsvIdleS), at most the lifetime
+  const char *ie = getenv("MX_COLL_SERVICE_IDLE_US");
+  const double idle_s = (ie && *ie) ? std::min(kCsvLifeS, std::max(1e-6, atof(ie) * 1e-6)) : kCsvIdleS;
+  v.idle_ticks = (uint64_t)(idle_s * rate_khz * 1000.0);
   v.life_ticks = (uint64_t)(kCsvLifeS * rate_khz * 1000.0);
   int least = 0, greatest = 0;
   if (hipDeviceGetStreamPriorityRange(&least, &greatest) != hipSuccess) least = 0;
