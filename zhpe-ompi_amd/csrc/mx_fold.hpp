@@ -401,9 +401,17 @@ __device__ bool os_ll(const OneShotArgs &a, uint64_t *tk = nullptr) {
   // lanes' columns (element e was gathered by lane e % kG, as its e / kG-th)
   {
     int sidx = 0;
+    // (SYS: the segment's program copied out of the LDS argument block once
+    // per segment -- evaluated from LDS, every step re-read its operand
+    // indices, a dependent LDS load per step of every element)
+    FoldProg P;
+    if constexpr (SYS) P = a.seg[0].p;
     for (size_t e = lo + t; e < hi; e += kOSB) {
       const int gl = (int)((e - lo) % kG), gi = (int)((e - lo) / kG);
-      while (sidx + 1 < a.nseg && e >= a.seg[sidx].hi) sidx++;
+      if (sidx + 1 < a.nseg && e >= a.seg[sidx].hi) {
+        while (sidx + 1 < a.nseg && e >= a.seg[sidx].hi) sidx++;
+        if constexpr (SYS) P = a.seg[sidx].p;
+      }
       const size_t off = e * sizeof(T);
       auto LDo = [&](int j) {
         T x;
@@ -422,7 +430,7 @@ __device__ bool os_ll(const OneShotArgs &a, uint64_t *tk = nullptr) {
       // (the bounded evaluation only where the arguments live in LDS: with
       // the launch's by-value arguments its copies would spill them)
       T v;
-      if constexpr (SYS) v = eval_prog_small<OP, T>(a.seg[sidx].p, LDo);
+      if constexpr (SYS) v = eval_prog_small<OP, T>(P, LDo);
       else v = eval_prog<OP, T>(a.seg[sidx].p, LDo);
       if (SYS) {
         uint32_t u[W];
