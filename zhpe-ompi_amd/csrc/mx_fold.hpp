@@ -404,12 +404,18 @@ __device__ bool os_ll(const OneShotArgs &a, uint64_t *tk = nullptr) {
     // (SYS: the segment's program copied out of the LDS argument block once
     // per segment -- evaluated from LDS, every step re-read its operand
     // indices, a dependent LDS load per step of every element)
+    // (the result pointer, the segment count and bound likewise: loop
+    // invariants the compiler would otherwise reload from LDS per element)
     FoldProg P;
     if constexpr (SYS) P = a.seg[0].p;
+    const int nseg = a.nseg;
+    size_t seg_hi = a.seg[0].hi;
+    char *const rbase = a.rb;
     for (size_t e = lo + t; e < hi; e += kOSB) {
       const int gl = (int)((e - lo) % kG), gi = (int)((e - lo) / kG);
-      if (sidx + 1 < a.nseg && e >= a.seg[sidx].hi) {
-        while (sidx + 1 < a.nseg && e >= a.seg[sidx].hi) sidx++;
+      if (sidx + 1 < nseg && e >= seg_hi) {
+        while (sidx + 1 < nseg && e >= a.seg[sidx].hi) sidx++;
+        seg_hi = a.seg[sidx].hi;
         if constexpr (SYS) P = a.seg[sidx].p;
       }
       const size_t off = e * sizeof(T);
@@ -437,10 +443,10 @@ __device__ bool os_ll(const OneShotArgs &a, uint64_t *tk = nullptr) {
         __builtin_memcpy(u, &v, sizeof(T));
 #pragma unroll
         for (int k = 0; k < W; k++)
-          __hip_atomic_store(gp(reinterpret_cast<uint32_t *>(a.rb) + e * W + k), u[k], __ATOMIC_RELAXED,
+          __hip_atomic_store(gp(reinterpret_cast<uint32_t *>(rbase) + e * W + k), u[k], __ATOMIC_RELAXED,
                              __HIP_MEMORY_SCOPE_SYSTEM);
       } else {
-        store_fields(reinterpret_cast<T *>(a.rb + off), v);
+        store_fields(reinterpret_cast<T *>(rbase + off), v);
       }
     }
   }
