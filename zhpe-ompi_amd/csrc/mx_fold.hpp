@@ -301,6 +301,30 @@ __device__ bool os_ll(const OneShotArgs &a, uint64_t *tk = nullptr) {
   if (t == 0) s_bad = poisoned(a.poison);
   __syncthreads();
   if (s_bad) return false;
+  // this workgroup's slice of the elements, [lo, hi) (the launch: one per
+  // OS_LL_MAX bytes; the service: one workgroup, the whole call)
+  const size_t lo = (size_t)blockIdx.x * a.slice;
+  const size_t hi = lo + a.slice < a.count ? lo + a.slice : a.count;
+  const size_t cnt = hi > lo ? hi - lo : 0;
+  const int E = (int)((cnt + kG - 1) / kG);   // elements per gathering lane
+  const size_t w0 = lo * W, nw = cnt * W;     // this slice's words: [w0, w0 + nw)
+  // (2a) the pushing lanes' own words (MW per lane, all loads in flight at
+  // once) are loaded before the gen-2 check below, which they overlap
+  uint32_t mv[MW];
+  if (t >= kG) {
+    const int q = t - kG;
+    const bool al = ((uintptr_t)a.sb & 3) == 0;
+    const uint32_t *sw = reinterpret_cast<const uint32_t *>(a.sb);
+#pragma unroll
+    for (int u = 0; u < MW; u++) {
+      const size_t i = (size_t)q + (size_t)u * kP;
+      if (i < nw) {
+        if (SYS) mv[u] = __hip_atomic_load(gp(sw + w0 + i), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        else if (al) mv[u] = sw[w0 + i];
+        else __builtin_memcpy(&mv[u], a.sb + 4 * (w0 + i), 4);
+      }
+    }
+  }
   // (1) every peer is past gen-2: its reads of this parity's LL area are over
   if (t < n && t != r && a.gen > 2) os_spin(a.my_done + t, a.gen - 2, a.timeout_ticks, a.err, a.poison);
   __syncthreads();
@@ -311,29 +335,10 @@ __device__ bool os_ll(const OneShotArgs &a, uint64_t *tk = nullptr) {
   __syncthreads();
   if (s_bad) return false;
   bool bad = false;
-  // this workgroup's slice of the elements, [lo, hi) (the launch: one per
-  // OS_LL_MAX bytes; the service: one workgroup, the whole call)
-  const size_t lo = (size_t)blockIdx.x * a.slice;
-  const size_t hi = lo + a.slice < a.count ? lo + a.slice : a.count;
-  const size_t cnt = hi > lo ? hi - lo : 0;
-  const int E = (int)((cnt + kG - 1) / kG);   // elements per gathering lane
   if (t >= kG) {
-    // (2) my words (MW per lane, all loads in flight at once) into LDS for my
-    // own operand of the fold, then, tagged, into every peer's LL area
+    // (2b) my words into LDS for my own operand of the fold, then, tagged,
+    // into every peer's LL area
     const int q = t - kG;
-    const size_t w0 = lo * W, nw = cnt * W;   // this slice's words: [w0, w0 + nw)
-    const bool al = ((uintptr_t)a.sb & 3) == 0;
-    const uint32_t *sw = reinterpret_cast<const uint32_t *>(a.sb);
-    uint32_t mv[MW];
-#pragma unroll
-    for (int u = 0; u < MW; u++) {
-      const size_t i = (size_t)q + (size_t)u * kP;
-      if (i < nw) {
-        if (SYS) mv[u] = __hip_atomic_load(gp(sw + w0 + i), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-        else if (al) mv[u] = sw[w0 + i];
-        else __builtin_memcpy(&mv[u], a.sb + 4 * (w0 + i), 4);
-      }
-    }
 #pragma unroll
     for (int u = 0; u < MW; u++) {
       const size_t i = (size_t)q + (size_t)u * kP;
