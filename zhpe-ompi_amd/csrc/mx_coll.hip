@@ -718,15 +718,35 @@ static int ipc_region_alloc(size_t bytes, char **p) {
     if (best != (size_t)-1) {
       *p = g_ipc_pool[best].first;
       g_ipc_pool.erase(g_ipc_pool.begin() + (long)best);
-      return MX_SUCCESS;
+      hipIpcMemHandle_t h;   // (exported before: the same handle again)
+      if (hipIpcGetMemHandle(&h, *p) == hipSuccess) return MX_SUCCESS;
+      (void)hipGetLastError();
+      fprintf(stderr, "mx: a pooled %zu-byte region could not be exported again; allocating another\n", bytes);
+      *p = nullptr;   // (left allocated, out of the pool)
     }
   }
-  if (hipExtMallocWithFlags((void **)p, bytes, hipDeviceMallocUncached) != hipSuccess) {
+  // A fresh allocation may land where an exported allocation of this
+  // process was freed (a torch buffer registered for zero-copy, then
+  // released), and the runtime then refuses to export it: hipIpcGetMemHandle
+  // failed with "invalid argument" on a recycled communicator's heap region
+  // (profiles/r06/gpu_suite_r6az_export_refused.txt).  Such an allocation is
+  // kept aside -- so the next one lands elsewhere -- and another is made.
+  static std::vector<void *> g_unexportable;   // (under g_ipc_pool_mu below)
+  for (int attempt = 0; attempt < 4; attempt++) {
+    if (hipExtMallocWithFlags((void **)p, bytes, hipDeviceMallocUncached) != hipSuccess) {
+      (void)hipGetLastError();
+      *p = nullptr;
+      return MX_ERR_NOMEM;
+    }
+    hipIpcMemHandle_t h;
+    if (hipIpcGetMemHandle(&h, *p) == hipSuccess) return MX_SUCCESS;
     (void)hipGetLastError();
-    *p = nullptr;
-    return MX_ERR_NOMEM;
+    std::lock_guard<std::mutex> lk(g_ipc_pool_mu);
+    g_unexportable.push_back(*p);
+    fprintf(stderr, "mx: a fresh %zu-byte region could not be exported; allocating another\n", bytes);
   }
-  return MX_SUCCESS;
+  *p = nullptr;
+  return MX_ERR_NOMEM;
 }
 
 static size_t ipc_region_size(const char *p) {
