@@ -113,6 +113,7 @@ __global__ void __launch_bounds__(kOSB) k_csv(const CsvCtl *ctl, const uint64_t 
   __shared__ uint64_t tk[TK_N];
   const int t = threadIdx.x;
   uint64_t seen = last;
+  uint64_t gathered = 0;   // the last generation this kernel gathered from every peer
   const uint64_t born = wall_clock64();
   if (t == 0) __hip_atomic_store(&host->running, epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
   for (;;) {
@@ -167,7 +168,10 @@ __global__ void __launch_bounds__(kOSB) k_csv(const CsvCtl *ctl, const uint64_t 
       tk[TK_ARGS] = wall_clock64();
     }
     __syncthreads();
-    const bool ok = os_ll<T, OP, true>(a, &tk[TK_DCHK]);
+    // the gen-2 check is needed only when this kernel did not gather the
+    // previous generation itself (its first call, or gen-1 was launched)
+    const bool ok = os_ll<T, OP, true>(a, &tk[TK_DCHK], gen != gathered + 1);
+    if (ok) gathered = gen;
     // every lane's result words acknowledged before `done`
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();

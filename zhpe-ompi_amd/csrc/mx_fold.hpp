@@ -279,8 +279,11 @@ __device__ __forceinline__ uint64_t ll_ld(const uint64_t *p) {
 
 // tk (the service's phase trace, or null): thread 0 stamps [0] the gen-2
 // check, [1] the push issued, [2] the gather, [3] the fold
+// dchk = false: the caller knows every peer is past gen-2 -- it gathered
+// every peer's gen-1 words, and a peer starts a call only after its previous
+// one (reads of that parity's LL area included) has finished
 template <class T, class OP, bool SYS>
-__device__ bool os_ll(const OneShotArgs &a, uint64_t *tk = nullptr) {
+__device__ bool os_ll(const OneShotArgs &a, uint64_t *tk = nullptr, bool dchk = true) {
   constexpr int W = (int)(sizeof(T) / 4);
   static_assert(sizeof(T) == 4 || sizeof(T) == 8, "LL carries 4- and 8-byte elements");
   // Roles by wave: waves 0-1 (kG lanes) gather and fold, waves 2-3 push.
@@ -326,7 +329,7 @@ __device__ bool os_ll(const OneShotArgs &a, uint64_t *tk = nullptr) {
     }
   }
   // (1) every peer is past gen-2: its reads of this parity's LL area are over
-  if (t < n && t != r && a.gen > 2) os_spin(a.my_done + t, a.gen - 2, a.timeout_ticks, a.err, a.poison);
+  if (dchk && t < n && t != r && a.gen > 2) os_spin(a.my_done + t, a.gen - 2, a.timeout_ticks, a.err, a.poison);
   __syncthreads();
   if (t == 0) {
     s_bad = poisoned(a.poison);
